@@ -1,0 +1,157 @@
+// gwo_device.h -- gfx950 device helpers: Java integer semantics, Flink's hash functions,
+// window arithmetic and the HBM hash-table primitives.  Included only by .hip translation units.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "gwo_internal.h"
+
+namespace gwo {
+
+#define GWO_LONG_MIN ((int64_t)0x8000000000000000LL)
+#define GWO_LONG_MAX ((int64_t)0x7fffffffffffffffLL)
+
+// Java long arithmetic wraps; do it in unsigned to keep the compiler from assuming no overflow.
+__device__ __host__ __forceinline__ int64_t jadd(int64_t a, int64_t b) {
+    return (int64_t)((uint64_t)a + (uint64_t)b);
+}
+__device__ __host__ __forceinline__ int64_t jsub(int64_t a, int64_t b) {
+    return (int64_t)((uint64_t)a - (uint64_t)b);
+}
+// Java '%' on longs (truncating; C++ '%' has the same semantics).  b > 0.
+__device__ __host__ __forceinline__ int64_t jrem(int64_t a, int64_t b) { return a % b; }
+
+// TimeWindow.getWindowStartWithOffset, TimeWindow.java:270-272 (Java '%' quirk included).
+__device__ __host__ __forceinline__ int64_t window_start(int64_t ts, int64_t off, int64_t size) {
+    return jsub(ts, jrem(jadd(jsub(ts, off), size), size));
+}
+
+__device__ __host__ __forceinline__ int64_t floor_div(int64_t a, int64_t b) {
+    int64_t q = a / b;
+    return (a % b != 0 && ((a < 0) != (b < 0))) ? q - 1 : q;
+}
+
+// WindowOperator.cleanupTime (WindowOperator.java:639-646): maxTs + lateness, Long.MAX_VALUE on overflow.
+__device__ __host__ __forceinline__ int64_t cleanup_time(int64_t max_ts, int64_t lateness) {
+    int64_t c = jadd(max_ts, lateness);
+    return c >= max_ts ? c : GWO_LONG_MAX;
+}
+
+// ---- Flink hashing (bit-exact) -----------------------------------------------------------------
+__device__ __host__ __forceinline__ int32_t long_hash_code(int64_t v) {  // JDK Long.hashCode
+    return (int32_t)(uint32_t)((uint64_t)v ^ ((uint64_t)v >> 32));
+}
+__device__ __host__ __forceinline__ int32_t key_hash_code(int64_t v, int kind) {
+    return kind == 1 ? (int32_t)v : long_hash_code(v);
+}
+__device__ __host__ __forceinline__ int32_t bit_mix(int32_t in) {  // MathUtils.java:191-198
+    uint32_t x = (uint32_t)in;
+    x ^= x >> 16;
+    x *= 0x85ebca6bu;
+    x ^= x >> 13;
+    x *= 0xc2b2ae35u;
+    x ^= x >> 16;
+    return (int32_t)x;
+}
+__device__ __host__ __forceinline__ uint32_t rotl32(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }
+__device__ __host__ __forceinline__ int32_t murmur_hash(int32_t code) {  // MathUtils.java:134-154
+    uint32_t c = (uint32_t)code;
+    c *= 0xcc9e2d51u;
+    c = rotl32(c, 15);
+    c *= 0x1b873593u;
+    c = rotl32(c, 13);
+    c = c * 5u + 0xe6546b64u;
+    c ^= 4u;
+    int32_t r = bit_mix((int32_t)c);
+    if (r >= 0) return r;
+    if (r != (int32_t)0x80000000) return -r;
+    return 0;
+}
+// KeyGroupRangeAssignment.java:60-73
+__device__ __host__ __forceinline__ int32_t key_group(int64_t key, int kind, int32_t max_par) {
+    return murmur_hash(key_hash_code(key, kind)) % max_par;
+}
+
+// ---- table hashing -------------------------------------------------------------------------------
+// Slot hash (independent of the key-group hash so that a shard's table is not biased).
+__device__ __forceinline__ uint64_t slot_hash(int64_t key) {
+    uint64_t k = (uint64_t)key ^ 0x9E3779B97F4A7C15ull;
+    k ^= k >> 33;
+    k *= 0xff51afd7ed558ccdull;
+    k ^= k >> 33;
+    k *= 0xc4ceb9fe1a85ec53ull;
+    k ^= k >> 33;
+    return k;
+}
+
+// Double.compareTo total order as a signed int64 key (doubleToLongBits canonicalises NaN).
+__device__ __host__ __forceinline__ int64_t f64_order_key(int64_t bits) {
+    if ((bits & 0x7ff0000000000000LL) == 0x7ff0000000000000LL && (bits & 0x000fffffffffffffLL) != 0)
+        bits = 0x7ff8000000000000LL;
+    return bits >= 0 ? bits : (bits ^ 0x7fffffffffffffffLL);
+}
+__device__ __host__ __forceinline__ int64_t f64_from_order_key(int64_t k) {
+    return k >= 0 ? k : (k ^ 0x7fffffffffffffffLL);
+}
+
+__device__ __forceinline__ int64_t lift_word(const AccPlan &p, int w, int64_t vbits) {
+    switch (p.src[w]) {
+        case SRC_ONE: return 1;
+        case SRC_ORDER: return f64_order_key(vbits);
+        default: return vbits;
+    }
+}
+
+// Atomic combine into a global (HBM) word -- device scope.
+__device__ __forceinline__ void atomic_combine(int64_t *dst, int op, int64_t x) {
+    switch (op) {
+        case ACC_ADD_I64: atomicAdd((unsigned long long *)dst, (unsigned long long)x); break;
+        case ACC_ADD_F64: atomicAdd((double *)dst, __longlong_as_double(x)); break;
+        case ACC_MIN_I64: atomicMin((long long *)dst, (long long)x); break;
+        default: atomicMax((long long *)dst, (long long)x); break;
+    }
+}
+
+// Plain (non-atomic) combine.
+__device__ __forceinline__ int64_t combine(int op, int64_t a, int64_t b) {
+    switch (op) {
+        case ACC_ADD_I64: return jadd(a, b);
+        case ACC_ADD_F64: return __double_as_longlong(__longlong_as_double(a) + __longlong_as_double(b));
+        case ACC_MIN_I64: return a < b ? a : b;
+        default: return a > b ? a : b;
+    }
+}
+
+// Find the entry of `key` in table t, claiming a free slot if absent.  Returns the entry's
+// accumulator words.  Linear probing; the table never fills (host keeps load <= 0.7).
+__device__ __forceinline__ int64_t *find_or_insert(const TableDesc &t, int stride, int64_t key) {
+    if (key == GWO_EMPTY_KEY) {
+        if (__hip_atomic_load(t.side, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
+            if (atomicCAS((unsigned long long *)t.side, 0ull, 1ull) == 0ull) atomicAdd(t.occ, 1ull);
+        }
+        return t.side + 1;
+    }
+    uint64_t slot = slot_hash(key) & t.mask;
+    while (true) {
+        int64_t *e = t.base + slot * (uint64_t)stride;
+        int64_t cur = __hip_atomic_load(e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (cur == key) return e + 1;
+        if (cur == GWO_EMPTY_KEY) {
+            unsigned long long prev =
+                atomicCAS((unsigned long long *)e, (unsigned long long)GWO_EMPTY_KEY, (unsigned long long)key);
+            if ((int64_t)prev == GWO_EMPTY_KEY) {
+                atomicAdd(t.occ, 1ull);
+                return e + 1;
+            }
+            if ((int64_t)prev == key) return e + 1;
+        }
+        slot = (slot + 1) & t.mask;
+    }
+}
+
+// Wave-level sum for counters: one atomic per wave.
+__device__ __forceinline__ void wave_atomic_add(unsigned long long *dst, unsigned long long v) {
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    if ((threadIdx.x & 63) == 0 && v) atomicAdd(dst, v);
+}
+
+}  // namespace gwo

@@ -1,0 +1,264 @@
+// gwo_handle.cpp -- handle lifecycle, batch submit, watermark dispatch and output draining.
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+#include <numeric>
+
+#include "gwo_handle.h"
+
+namespace gwo {
+
+static int64_t floor_mod(int64_t a, int64_t b) {
+    int64_t r = a % b;
+    return r < 0 ? r + b : r;
+}
+
+// WindowOperator ctor + assigner ctors: argument checks mirror the reference exceptions.
+gwo_status Handle::init(const gwo_config &c) {
+    cfg = c;
+    if (c.abi_version != GWO_ABI_VERSION) return fail(GWO_ERR_INVALID_ARGUMENT, "ABI version %d != %d", c.abi_version, GWO_ABI_VERSION);
+    if (c.allowed_lateness < 0) return fail(GWO_ERR_INVALID_ARGUMENT, "The allowed lateness cannot be negative.");
+    switch (c.assigner) {
+        case GWO_ASSIGNER_TUMBLING:
+            // TumblingEventTimeWindows.java:57-60
+            if (c.size <= 0 || (c.offset < 0 ? -c.offset : c.offset) >= c.size)
+                return fail(GWO_ERR_INVALID_ARGUMENT, "TumblingEventTimeWindows parameters must satisfy abs(offset) < size");
+            break;
+        case GWO_ASSIGNER_SLIDING:
+            // SlidingEventTimeWindows.java:56-60
+            if ((c.offset < 0 ? -c.offset : c.offset) >= c.slide || c.size <= 0)
+                return fail(GWO_ERR_INVALID_ARGUMENT,
+                            "SlidingEventTimeWindows parameters must satisfy abs(offset) < slide and size > 0");
+            break;
+        case GWO_ASSIGNER_SESSION:
+            // EventTimeSessionWindows.java:50-55
+            if (c.gap <= 0) return fail(GWO_ERR_INVALID_ARGUMENT, "EventTimeSessionWindows parameters must satisfy 0 < size");
+            break;
+        default: return fail(GWO_ERR_UNSUPPORTED, "unknown assigner %d", c.assigner);
+    }
+    if (c.max_parallelism <= 0 || c.max_parallelism > 32768)
+        return fail(GWO_ERR_INVALID_ARGUMENT, "maxParallelism must be in (0, 32768]");
+    if (c.key_group_start < 0 || c.key_group_end >= c.max_parallelism || c.key_group_start > c.key_group_end)
+        return fail(GWO_ERR_INVALID_ARGUMENT, "invalid KeyGroupRange [%d, %d]", c.key_group_start, c.key_group_end);
+    if (c.key_kind != GWO_KEY_LONG && c.key_kind != GWO_KEY_INT) return fail(GWO_ERR_UNSUPPORTED, "key kind %d", c.key_kind);
+    if (c.value_dtype != GWO_DTYPE_INT64 && c.value_dtype != GWO_DTYPE_FLOAT64)
+        return fail(GWO_ERR_UNSUPPORTED, "value dtype %d", c.value_dtype);
+    if (c.num_aggs < 1 || c.num_aggs > GWO_MAX_AGGS) return fail(GWO_ERR_INVALID_ARGUMENT, "num_aggs must be 1..4");
+
+    // ---- accumulator plan ----
+    const bool f64 = c.value_dtype == GWO_DTYPE_FLOAT64;
+    plan = AccPlan{};
+    plan.value_is_f64 = f64;
+    rplan = ResultPlan{};
+    rplan.naggs = c.num_aggs;
+    rplan.value_is_f64 = f64;
+    needs_value = false;
+    int w = 0;
+    auto add_word = [&](int op, int src, int64_t ident) {
+        plan.op[w] = op;
+        plan.src[w] = src;
+        plan.ident[w] = ident;
+        ++w;
+    };
+    for (int a = 0; a < c.num_aggs; ++a) {
+        rplan.kind[a] = c.aggs[a];
+        rplan.word[a] = w;
+        switch (c.aggs[a]) {
+            case GWO_AGG_COUNT: add_word(ACC_ADD_I64, SRC_ONE, 0); break;
+            case GWO_AGG_SUM:
+                add_word(f64 ? ACC_ADD_F64 : ACC_ADD_I64, SRC_VALUE, 0);
+                needs_value = true;
+                break;
+            case GWO_AGG_MIN:
+                add_word(ACC_MIN_I64, f64 ? SRC_ORDER : SRC_VALUE, (int64_t)0x7fffffffffffffffLL);
+                needs_value = true;
+                break;
+            case GWO_AGG_MAX:
+                add_word(ACC_MAX_I64, f64 ? SRC_ORDER : SRC_VALUE, (int64_t)0x8000000000000000LL);
+                needs_value = true;
+                break;
+            case GWO_AGG_AVG:
+                add_word(f64 ? ACC_ADD_F64 : ACC_ADD_I64, SRC_VALUE, 0);
+                add_word(ACC_ADD_I64, SRC_ONE, 0);
+                needs_value = true;
+                break;
+            default: return fail(GWO_ERR_UNSUPPORTED, "aggregate kind %d", c.aggs[a]);
+        }
+    }
+    plan.nwords = w;
+    plan.stride = ((1 + w) + 1) & ~1;
+
+    // ---- geometry ----
+    geom = WindowGeom{};
+    geom.size = c.size;
+    geom.offset = c.offset;
+    geom.lateness = c.allowed_lateness;
+    geom.key_kind = c.key_kind;
+    geom.max_par = c.max_parallelism;
+    geom.kg_lo = c.key_group_start;
+    geom.kg_hi = c.key_group_end;
+    if (c.assigner == GWO_ASSIGNER_TUMBLING) {
+        geom.sliding = 0;
+        geom.unit = c.size;
+        geom.slide = c.size;
+        geom.unit_off = c.offset % c.size;  // (globalOffset + staggerOffset) % size, ALIGNED stagger
+        geom.offset = geom.unit_off;
+        geom.unit_off_mod = floor_mod(c.offset, c.size);
+    } else if (c.assigner == GWO_ASSIGNER_SLIDING) {
+        geom.sliding = 1;
+        geom.slide = c.slide;
+        geom.unit = std::gcd(c.size, c.slide);
+        geom.unit_off = c.offset;
+        geom.unit_off_mod = floor_mod(c.offset, geom.unit);
+    }
+
+    const char *pa = getenv("GWO_PREAGG");
+    if (pa) cfg_preagg = atoi(pa) ? 1 : 0;
+    if (cfg_preagg >= 0) use_preagg = cfg_preagg;
+
+    // ---- device resources ----
+    if (hipSetDevice(c.device) != hipSuccess) return fail(GWO_ERR_HIP, "hipSetDevice(%d) failed", c.device);
+    if (c.stream) {
+        stream = (hipStream_t)c.stream;
+    } else {
+        GWO_TRY(hipcheck(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking), "stream"));
+        own_stream = true;
+    }
+    GWO_TRY(dalloc((void **)&d_stats, sizeof(BatchStats)));
+    GWO_TRY(hipcheck(hipHostMalloc((void **)&h_stats, sizeof(BatchStats), hipHostMallocDefault), "pinned"));
+    GWO_TRY(hipcheck(hipHostMalloc((void **)&h_stats_init, sizeof(BatchStats), hipHostMallocDefault), "pinned"));
+    const int kCounters = 1 << 14;
+    counter_used.assign(kCounters, 0);
+    GWO_TRY(dalloc((void **)&d_counters, kCounters * 8));
+    GWO_TRY(hipcheck(hipHostMalloc((void **)&h_counters, kCounters * 8, hipHostMallocDefault), "pinned"));
+    GWO_TRY(dalloc((void **)&d_out_count, 8));
+    GWO_TRY(dalloc((void **)&d_scratch_count, 8));
+    GWO_TRY(dalloc((void **)&d_side_count, 8));
+    GWO_TRY(hipcheck(hipMemsetAsync(d_out_count, 0, 8, stream), "memset"));
+    GWO_TRY(hipcheck(hipMemsetAsync(d_side_count, 0, 8, stream), "memset"));
+    GWO_TRY(hipcheck(hipMemsetAsync(d_counters, 0, kCounters * 8, stream), "memset"));
+    if (side_enabled()) GWO_TRY(grow_side(4096));
+    if (c.assigner == GWO_ASSIGNER_SLIDING) GWO_TRY(slide_init());
+    if (c.assigner == GWO_ASSIGNER_SESSION) GWO_TRY(session_init());
+    return hipcheck(hipStreamSynchronize(stream), "init");
+}
+
+Handle::~Handle() {
+    DeviceGuard g(cfg.device);
+    if (stream) (void)hipStreamSynchronize(stream);
+    (void)prof_collect();
+    comm_free();
+    session_free();
+    slide_free();
+    for (auto &kv : tables) (void)hipFree(kv.second.base);
+    for (auto &t : aux_tables) (void)hipFree(t.base);
+    trim_pool();
+    if (d_stats) (void)hipFree(d_stats);
+    if (h_stats) (void)hipHostFree(h_stats);
+    if (h_stats_init) (void)hipHostFree(h_stats_init);
+    if (d_counters) (void)hipFree(d_counters);
+    if (h_counters) (void)hipHostFree(h_counters);
+    dir_buf.release();
+    stage_key.release();
+    stage_ts.release();
+    stage_val.release();
+    side_key.release();
+    side_ts.release();
+    side_val.release();
+    int64_t *cols[7] = {out.key, out.start, out.end, out.res[0], out.res[1], out.res[2], out.res[3]};
+    for (auto *p : cols)
+        if (p) (void)hipFree(p);
+    if (d_out_count) (void)hipFree(d_out_count);
+    if (d_scratch_count) (void)hipFree(d_scratch_count);
+    if (d_side_count) (void)hipFree(d_side_count);
+    if (own_stream && stream) (void)hipStreamDestroy(stream);
+}
+
+gwo_status Handle::submit(const int64_t *key, const int64_t *ts, const void *val, int64_t n) {
+    const int64_t *dk = nullptr, *dt = nullptr, *dv = nullptr;
+    if (!comm && n == 0) return GWO_OK;
+    if (n > 0) GWO_TRY(stage_inputs(key, ts, needs_value ? val : nullptr, n, &dk, &dt, &dv));
+    if (comm) {
+        const int64_t *rk, *rt, *rv;
+        int64_t rn = 0;
+        GWO_TRY(comm_exchange(dk, dt, dv, n, &rk, &rt, &rv, &rn));
+        return submit_local(rk, rt, rv, rn);
+    }
+    return submit_local(dk, dt, dv, n);
+}
+
+gwo_status Handle::submit_local(const int64_t *k, const int64_t *t, const int64_t *v, int64_t n) {
+    if (n == 0) return GWO_OK;
+    if (cfg.assigner == GWO_ASSIGNER_SESSION) return insert_session(k, t, v, n);
+    return insert_windowed(k, t, v, n);
+}
+
+gwo_status Handle::advance_watermark(int64_t new_wm) {
+    if (comm) GWO_TRY(comm_min_watermark(new_wm, &new_wm));
+    gwo_status s = GWO_OK;
+    switch (cfg.assigner) {
+        case GWO_ASSIGNER_TUMBLING: s = fire_tumbling(new_wm); break;
+        case GWO_ASSIGNER_SLIDING: s = fire_sliding(new_wm); break;
+        default: s = fire_session(new_wm); break;
+    }
+    wm = new_wm;
+    return s;
+}
+
+gwo_status Handle::drain(const gwo_out *cols, int64_t cap, int64_t *n_out) {
+    GWO_TRY(hipcheck(hipStreamSynchronize(stream), "drain"));
+    uint64_t take = std::min<uint64_t>((uint64_t)cap, out_rows);
+    *n_out = (int64_t)take;
+    if (take == 0) return GWO_OK;
+    int64_t *src[7] = {out.key, out.start, out.end, out.res[0], out.res[1], out.res[2], out.res[3]};
+    void *dst[7] = {cols->key, cols->start, cols->end, cols->result[0], cols->result[1], cols->result[2], cols->result[3]};
+    int ncols = 3 + rplan.naggs;
+    for (int c = 0; c < ncols; ++c) {
+        if (!dst[c]) continue;
+        GWO_TRY(hipcheck(hipMemcpyAsync(dst[c], src[c], take * 8, hipMemcpyDefault, stream), "drain copy"));
+    }
+    uint64_t rest = out_rows - take;
+    for (uint64_t off = 0; off < rest; off += take) {
+        uint64_t len = std::min<uint64_t>(take, rest - off);
+        for (int c = 0; c < ncols; ++c)
+            GWO_TRY(hipcheck(hipMemcpyAsync(src[c] + off, src[c] + take + off, len * 8, hipMemcpyDeviceToDevice, stream),
+                             "drain shift"));
+    }
+    out_rows = rest;
+    unsigned long long rc = rest;
+    GWO_TRY(hipcheck(hipMemcpyAsync(d_out_count, &rc, 8, hipMemcpyHostToDevice, stream), "drain count"));
+    return hipcheck(hipStreamSynchronize(stream), "drain sync");
+}
+
+gwo_status Handle::drain_side(const gwo_side_out *cols, int64_t cap, int64_t *n_out) {
+    GWO_TRY(hipcheck(hipStreamSynchronize(stream), "drain side"));
+    uint64_t take = std::min<uint64_t>((uint64_t)cap, side_rows_committed);
+    *n_out = (int64_t)take;
+    if (take == 0) return GWO_OK;
+    DevBuf *src[3] = {&side_key, &side_ts, &side_val};
+    void *dst[3] = {cols->key, cols->ts, cols->value};
+    for (int c = 0; c < 3; ++c)
+        if (dst[c]) GWO_TRY(hipcheck(hipMemcpyAsync(dst[c], src[c]->ptr, take * 8, hipMemcpyDefault, stream), "side copy"));
+    uint64_t rest = side_rows_committed - take;
+    for (uint64_t off = 0; off < rest; off += take) {
+        uint64_t len = std::min<uint64_t>(take, rest - off);
+        for (int c = 0; c < 3; ++c)
+            GWO_TRY(hipcheck(hipMemcpyAsync((int64_t *)src[c]->ptr + off, (int64_t *)src[c]->ptr + take + off, len * 8,
+                                            hipMemcpyDeviceToDevice, stream), "side shift"));
+    }
+    side_rows_committed = side_rows = rest;
+    unsigned long long rc = rest;
+    GWO_TRY(hipcheck(hipMemcpyAsync(d_side_count, &rc, 8, hipMemcpyHostToDevice, stream), "side count"));
+    return hipcheck(hipStreamSynchronize(stream), "side sync");
+}
+
+gwo_status Handle::state_size(int64_t *entries) {
+    if (cfg.assigner == GWO_ASSIGNER_SESSION) return session_state_size(entries);
+    GWO_TRY(read_occupancy());
+    int64_t s = 0;
+    for (auto &kv : tables) s += (int64_t)kv.second.occ;
+    *entries = s;
+    return GWO_OK;
+}
+
+}  // namespace gwo

@@ -1,0 +1,192 @@
+// gwo_handle.h -- the host-side state of one GPU window operator subtask.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <map>
+#include <string>
+#include <vector>
+
+#include "../../include/gwo.h"
+#include "gwo_internal.h"
+
+#define GWO_TRY(expr)                        \
+    do {                                     \
+        gwo_status s__ = (expr);             \
+        if (s__ != GWO_OK) return s__;       \
+    } while (0)
+
+namespace gwo {
+
+const char *status_str(gwo_status s);
+
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (prev != dev) (void)hipSetDevice(dev);
+    }
+    ~DeviceGuard() {
+        int cur = -1;
+        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+    }
+};
+
+struct DevBuf {
+    void *ptr = nullptr;
+    size_t bytes = 0;
+    void release() {
+        if (ptr) (void)hipFree(ptr);
+        ptr = nullptr;
+        bytes = 0;
+    }
+};
+
+struct Table {
+    int64_t *base = nullptr;       // cap entries + side slot
+    int64_t *side = nullptr;
+    uint64_t cap = 0;
+    int counter = -1;              // slot in d_counters
+    uint64_t occ = 0;              // occupancy as of the last read_occupancy()
+    bool fired = false;            // emitted at maxTs (allowedLateness > 0 keeps it until cleanup)
+    bool dirty = false;
+};
+
+struct KStat {
+    int64_t launches = 0;
+    double ms = 0;
+    int64_t items = 0;
+};
+
+struct PendingEvent {
+    int kernel;
+    hipEvent_t a, b;
+    int64_t items;
+};
+
+struct SessionState;   // gwo_session.cpp
+struct SlideState;     // gwo_slide.cpp
+struct Comm;           // gwo_comm.cpp
+
+struct Handle {
+    static constexpr double kMaxLoad = 0.7;   // grow above this load factor
+    static constexpr double kInitLoad = 0.45; // target load after (re)allocation
+    static constexpr uint64_t kMinCap = 1024;
+
+    gwo_config cfg{};
+    hipStream_t stream = nullptr;
+    bool own_stream = false;
+    AccPlan plan{};
+    ResultPlan rplan{};
+    WindowGeom geom{};
+    bool needs_value = true;
+    int64_t wm = (int64_t)0x8000000000000000LL;  // Long.MIN_VALUE, InternalTimerServiceImpl.currentWatermark
+
+    std::map<long long, Table> tables;         // window / pane index -> table
+    std::vector<Table> aux_tables;             // engine-private tables (sliding ring totals)
+    std::multimap<uint64_t, int64_t *> pool;   // clean tables by capacity
+
+    // device scratch
+    BatchStats *d_stats = nullptr;
+    BatchStats *h_stats = nullptr;             // pinned
+    BatchStats *h_stats_init = nullptr;        // pinned
+    unsigned long long *d_counters = nullptr;
+    unsigned long long *h_counters = nullptr;  // pinned
+    std::vector<char> counter_used;
+    DevBuf dir_buf, stage_key, stage_ts, stage_val;
+    std::vector<TableDesc> h_dir;
+    long long hist_hint = 0;
+
+    // output
+    OutCols out{};
+    unsigned long long *d_out_count = nullptr;
+    unsigned long long *d_scratch_count = nullptr;
+    uint64_t out_rows = 0;
+    unsigned long long zero_u64 = 0;
+
+    // late data
+    uint64_t late_dropped = 0;
+    DevBuf side_key, side_ts, side_val;
+    unsigned long long *d_side_count = nullptr;
+    long long side_cap = 0;
+    unsigned long long side_rows = 0, side_rows_committed = 0;
+    bool side_enabled() const { return cfg.side_output != 0; }
+
+    // pre-aggregation policy
+    int use_preagg = 1;
+    int cfg_preagg = -1;                       // GWO_PREAGG env override: 0 / 1
+    uint64_t batches = 0;
+
+    // errors
+    std::string err;
+    bool poisoned = false;
+    gwo_status poison_status = GWO_OK;
+
+    // profiling
+    bool profiling = false;
+    std::vector<PendingEvent> pending_events;
+    KStat kstats[GWO_KERNEL_COUNT_];
+
+    SessionState *sess = nullptr;
+    SlideState *slide = nullptr;
+    Comm *comm = nullptr;
+
+    ~Handle();
+    gwo_status init(const gwo_config &c);
+    gwo_status submit(const int64_t *key, const int64_t *ts, const void *val, int64_t n);
+    gwo_status submit_local(const int64_t *k, const int64_t *t, const int64_t *v, int64_t n);
+    gwo_status advance_watermark(int64_t wm);
+    gwo_status drain(const gwo_out *cols, int64_t cap, int64_t *n_out);
+    gwo_status drain_side(const gwo_side_out *cols, int64_t cap, int64_t *n_out);
+    gwo_status state_size(int64_t *entries);
+
+    gwo_status fail(gwo_status s, const char *fmt, ...);
+    gwo_status poison(gwo_status s, const char *what);
+    gwo_status dalloc(void **p, size_t bytes);
+    gwo_status hipcheck(hipError_t e, const char *what);
+    gwo_status ensure_buf(DevBuf &b, size_t bytes);
+    int take_counter();
+    gwo_status alloc_table(uint64_t cap, Table &t);
+    void release_table(Table &t);
+    void trim_pool();
+    TableDesc desc(const Table &t) const;
+    gwo_status ensure_table(long long u, uint64_t incoming);
+    gwo_status read_occupancy();
+    gwo_status ensure_output(uint64_t extra);
+    gwo_status stage_inputs(const int64_t *key, const int64_t *ts, const void *val, int64_t n, const int64_t **dk,
+                            const int64_t **dt, const int64_t **dv);
+    int64_t unit_start(long long u) const;
+    WindowGeom geom_now() const;
+    gwo_status insert_windowed(const int64_t *k, const int64_t *t, const int64_t *v, int64_t n);
+    void adapt_preagg(uint64_t accepted, uint64_t partials);
+    void init_stats(long long hist_base);
+    gwo_status grow_side(long long need);
+    gwo_status fire_tumbling(int64_t new_wm);
+    int64_t cleanup_time_host(int64_t max_ts) const;
+    OutCols out_cols() {
+        OutCols o = out;
+        o.count = d_out_count;
+        return o;
+    }
+
+    // sliding (gwo_slide.cpp)
+    gwo_status slide_init();
+    void slide_free();
+    gwo_status fire_sliding(int64_t new_wm);
+    // sessions (gwo_session.cpp)
+    gwo_status session_init();
+    void session_free();
+    gwo_status insert_session(const int64_t *k, const int64_t *t, const int64_t *v, int64_t n);
+    gwo_status fire_session(int64_t new_wm);
+    gwo_status session_state_size(int64_t *entries);
+    // comm (gwo_comm.cpp)
+    void comm_free();
+    gwo_status comm_exchange(const int64_t *k, const int64_t *t, const int64_t *v, int64_t n, const int64_t **rk,
+                             const int64_t **rt, const int64_t **rv, int64_t *rn);
+    gwo_status comm_min_watermark(int64_t wm, int64_t *out);
+
+    void prof_begin(int k);
+    void prof_end(int k, int64_t items);
+    gwo_status prof_collect();
+};
+
+}  // namespace gwo

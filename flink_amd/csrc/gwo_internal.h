@@ -1,0 +1,134 @@
+// gwo_internal.h -- structures shared by the host runtime and the gfx950 kernels.
+//
+// State layout in HBM: every live (key, window) -- or (key, pane) for sliding
+// windows -- is one entry of an open-addressed hash table.  There is one table per window (per
+// pane), so a window's fire is a coalesced sweep of one contiguous allocation and the window start
+// is implicit in the table, not stored per entry.  An entry is `stride` int64 words:
+//   word 0           the key (EMPTY_KEY = Long.MIN_VALUE marks a free slot; a real key equal to
+//                    Long.MIN_VALUE lives in the table's one-entry side slot, so no key is lost)
+//   words 1..nwords  the accumulator words (sum / count / min / max ...), see AccPlan
+// padded to a multiple of two words (16 B).
+#pragma once
+#include <stdint.h>
+
+#define GWO_EMPTY_KEY ((int64_t)0x8000000000000000LL)
+#define GWO_MAX_WORDS 8
+#define GWO_HIST_BINS 64
+
+// Combine ops per accumulator word.  Every aggregate decomposes into word-wise commutative
+// monoids, so inserting a record, merging two partials (sessions, pre-aggregation) and folding
+// panes all use the same per-word combine.
+enum AccOp : int32_t {
+    ACC_ADD_I64 = 0,   // Java long +, wrap-around (SumFunction.java:63-68)
+    ACC_ADD_F64 = 1,   // double +  (SumFunction.java:72-78)
+    ACC_MIN_I64 = 2,   // signed min (int64 values, or Double.compareTo order keys)
+    ACC_MAX_I64 = 3,
+};
+// How a record's value is lifted into a word.
+enum AccSrc : int32_t {
+    SRC_VALUE = 0,     // the int64 value, or the float64 value's bits for ACC_ADD_F64
+    SRC_ONE = 1,       // constant 1 (count)
+    SRC_ORDER = 2,     // Double.compareTo total-order key of the float64 value
+};
+
+struct AccPlan {
+    int32_t nwords;
+    int32_t stride;                    // words per entry incl. key, even
+    int32_t value_is_f64;
+    int32_t pad;
+    int32_t op[GWO_MAX_WORDS];
+    int32_t src[GWO_MAX_WORDS];
+    int64_t ident[GWO_MAX_WORDS];      // identity of each word's monoid
+};
+
+// One hash table in HBM.
+struct TableDesc {
+    int64_t *base;                     // cap * stride words
+    int64_t *side;                     // side slot for key == EMPTY_KEY: [flag, acc words...]
+    unsigned long long *occ;           // number of occupied slots (incl. side slot)
+    uint64_t mask;                     // cap - 1 (cap is a power of two)
+};
+
+// Result of the per-batch pre-pass (scan kernel), copied back to the host once per batch.
+struct BatchStats {
+    long long min_idx;                 // min/max window (pane) index over accepted records
+    long long max_idx;
+    unsigned long long accepted;       // records that reach at least one window
+    unsigned long long late;           // dropped as late (or routed to the side output)
+    unsigned long long refire;         // accepted into an already-fired window (allowedLateness > 0)
+    unsigned long long bad_ts;         // Long.MIN_VALUE timestamps
+    unsigned long long bad_kg;         // keys outside the KeyGroupRange
+    long long bad_kg_key;
+    unsigned long long bad_range;      // sliding: ts - offset + slide < 0 (Java '%' quirk region)
+    unsigned long long partials;       // pre-aggregated partials flushed by the insert kernel
+    unsigned long long hist_out;       // accepted records outside the histogram range
+    unsigned long long hist[GWO_HIST_BINS];
+};
+
+// Window geometry of the handle, kernel-parameter sized.
+struct WindowGeom {
+    int64_t unit;                      // tumbling: size; sliding: pane = gcd(size, slide)
+    int64_t unit_off;                  // offset passed to getWindowStartWithOffset for the unit
+    int64_t unit_off_mod;              // floorMod(start, unit) of every unit start
+    int64_t size;                      // window size
+    int64_t slide;                     // sliding slide (== size for tumbling)
+    int64_t offset;                    // assigner offset
+    int64_t lateness;
+    int64_t wm;                        // current watermark when the batch is processed
+    int32_t sliding;
+    int32_t key_kind;
+    int32_t max_par;
+    int32_t kg_lo;
+    int32_t kg_hi;
+    int32_t pad;
+};
+
+// Output columns (SoA) in HBM.
+struct OutCols {
+    int64_t *key;
+    int64_t *start;
+    int64_t *end;
+    int64_t *res[4];
+    unsigned long long *count;         // device row counter
+    long long cap;
+};
+
+struct ResultPlan {
+    int32_t naggs;
+    int32_t kind[4];                   // gwo_agg_kind
+    int32_t word[4];                   // first accumulator word of each aggregate
+    int32_t value_is_f64;
+};
+
+// ---- host-side launchers (gwo_kernels.hip) -----------------------------------------------------
+#include <hip/hip_runtime.h>
+
+namespace gwo {
+
+void launch_scan(const int64_t *key, const int64_t *ts, int64_t n, const WindowGeom &g, long long hist_base,
+                 BatchStats *stats, int64_t *side_key, int64_t *side_ts, int64_t *side_val, const int64_t *val,
+                 unsigned long long *side_count, long long side_cap, int side_enabled, hipStream_t s);
+
+void launch_insert(const int64_t *key, const int64_t *ts, const void *val, int64_t n, const WindowGeom &g,
+                   const AccPlan &plan, const TableDesc *dir, long long dir_base, int dir_len, int preagg,
+                   BatchStats *stats, hipStream_t s);
+
+void launch_fire(const TableDesc &t, uint64_t cap, const AccPlan &plan, const ResultPlan &rp, int64_t start,
+                 int64_t end, OutCols out, int reset, hipStream_t s);
+
+void launch_fill(int64_t *base, uint64_t cap, const AccPlan &plan, hipStream_t s);
+
+void launch_rehash(const TableDesc &src, uint64_t src_cap, const TableDesc &dst, const AccPlan &plan,
+                   hipStream_t s);
+
+void launch_key_groups(const int64_t *keys, int64_t n, int key_kind, int max_par, int par, int32_t *kg,
+                       int32_t *op, hipStream_t s);
+
+void launch_window_starts(const int64_t *ts, int64_t n, int64_t offset, int64_t size, int64_t *out,
+                          hipStream_t s);
+
+void launch_generate(uint64_t seed, int64_t first, int64_t total, int64_t nkeys, int64_t span, int64_t disorder,
+                     int64_t t0, int64_t vrange, int vf64, int key_mode, int64_t n, int64_t *key, int64_t *ts,
+                     void *val, hipStream_t s);
+
+}  // namespace gwo

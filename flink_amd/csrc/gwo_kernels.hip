@@ -1,0 +1,511 @@
+// gwo_kernels.hip -- hand-written gfx950 kernels of the keyed event-time window path.
+//
+//   scan      per batch: window/pane range of the accepted records, histogram for table sizing,
+//             late-record accounting (numLateRecordsDropped / side output), Long.MIN_VALUE check
+//   insert    records -> per-window HBM hash tables, keyed (key) within a window's table;
+//             optional per-workgroup LDS pre-aggregation of duplicate (key, window) pairs before
+//             the device-scope atomics (low-cardinality streams, e.g. YSB's 1K campaigns)
+//   fire      watermark-driven onEventTime: sweep a window's table, stream-compact the occupied
+//             entries into the output columns (key, start, end, results) and reset them
+//   rehash    table growth
+//
+// All of these are HBM-bandwidth-bound integer/byte work (no MFMA).  See DESIGN.md for the
+// algorithmic bytes per unit that bench.py prices each kernel with.
+#include "gwo_device.h"
+
+namespace gwo {
+
+enum RecClass : int { REC_ACCEPT = 0, REC_LATE = 1, REC_SKIP = 2, REC_REFIRE = 3, REC_BAD_TS = 4, REC_BAD_SLIDE = 5 };
+
+// Classifies one record against the batch's watermark; returns the unit (window or pane) index.
+// Tumbling: WindowOperator.java:386-427 with TumblingEventTimeWindows.java:68-81.
+// Sliding:  SlidingEventTimeWindows.java:68-82 restated on panes of gcd(size, slide).
+__device__ __forceinline__ int classify(int64_t ts, const WindowGeom &g, long long &unit_idx) {
+    if (ts == GWO_LONG_MIN) return REC_BAD_TS;
+    int64_t last_start, first_start;
+    if (!g.sliding) {
+        last_start = window_start(ts, g.offset, g.size);
+        first_start = last_start;
+    } else {
+        // Java's '%' gives a start > ts for ts - offset + slide < 0; the pane restatement covers
+        // the well-defined range only and rejects the rest loudly (never a silent difference).
+        if (jadd(jsub(ts, g.offset), g.slide) < 0) return REC_BAD_SLIDE;
+        last_start = window_start(ts, g.offset, g.slide);
+        // smallest start s = last_start - k*slide with s > ts - size
+        int64_t k = (jsub(last_start, jsub(ts, g.size)) - 1) / g.slide;
+        first_start = jsub(last_start, k * g.slide);
+    }
+    int64_t last_max_ts = jsub(jadd(last_start, g.size), 1);
+    if (cleanup_time(last_max_ts, g.lateness) <= g.wm) {
+        // every window of the record is late (isWindowLate); isElementLate decides the count
+        return jadd(ts, g.lateness) <= g.wm ? REC_LATE : REC_SKIP;
+    }
+    int64_t first_max_ts = jsub(jadd(first_start, g.size), 1);
+    if (first_max_ts <= g.wm) {
+        if (g.sliding && cleanup_time(first_max_ts, g.lateness) <= g.wm) {
+            // the earliest windows are already cleaned: with lateness 0 the pane only feeds the
+            // unfired windows, which is exactly the reference's per-window accept set
+            if (g.lateness != 0) return REC_REFIRE;
+        } else {
+            return REC_REFIRE;  // EventTimeTrigger.onElement FIRE: window.maxTs <= watermark
+        }
+    }
+    if (!g.sliding) {
+        unit_idx = floor_div(last_start, g.size);
+    } else {
+        int64_t pane_start = jsub(ts, jsub(jsub(ts, g.unit_off), floor_div(jsub(ts, g.unit_off), g.unit) * g.unit));
+        unit_idx = floor_div(pane_start, g.unit);
+    }
+    return REC_ACCEPT;
+}
+
+// ------------------------------------------------------------------------------------------------
+// scan
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void scan_kernel(const int64_t *__restrict__ key, const int64_t *__restrict__ ts,
+                                                   const int64_t *__restrict__ val, int64_t n, WindowGeom g,
+                                                   long long hist_base, BatchStats *st, int64_t *side_key,
+                                                   int64_t *side_ts, int64_t *side_val,
+                                                   unsigned long long *side_count, long long side_cap,
+                                                   int side_enabled) {
+    __shared__ unsigned long long s_hist[GWO_HIST_BINS];
+    __shared__ long long s_min[4], s_max[4];
+    for (int i = threadIdx.x; i < GWO_HIST_BINS; i += blockDim.x) s_hist[i] = 0;
+    __syncthreads();
+    long long mn = 0x7fffffffffffffffLL, mx = (long long)0x8000000000000000LL;
+    unsigned long long acc = 0, late = 0, refire = 0, bad_ts = 0, bad_slide = 0, hout = 0;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        long long u = 0;
+        int c = classify(ts[i], g, u);
+        if (c == REC_ACCEPT) {
+            acc++;
+            mn = u < mn ? u : mn;
+            mx = u > mx ? u : mx;
+            long long b = u - hist_base;
+            if (b >= 0 && b < GWO_HIST_BINS) atomicAdd(&s_hist[b], 1ull);
+            else hout++;
+        } else if (c == REC_LATE) {
+            late++;
+            if (side_enabled) {
+                unsigned long long pos = atomicAdd(side_count, 1ull);
+                if ((long long)pos < side_cap) {
+                    side_key[pos] = key[i];
+                    side_ts[pos] = ts[i];
+                    side_val[pos] = val ? val[i] : 0;
+                }
+            }
+        } else if (c == REC_REFIRE) {
+            refire++;
+        } else if (c == REC_BAD_TS) {
+            bad_ts++;
+        } else if (c == REC_BAD_SLIDE) {
+            bad_slide++;
+        }
+    }
+    // wave reductions
+    for (int o = 32; o > 0; o >>= 1) {
+        long long a = __shfl_xor(mn, o), b = __shfl_xor(mx, o);
+        mn = a < mn ? a : mn;
+        mx = b > mx ? b : mx;
+    }
+    wave_atomic_add(&st->accepted, acc);
+    wave_atomic_add(&st->late, late);
+    wave_atomic_add(&st->refire, refire);
+    wave_atomic_add(&st->bad_ts, bad_ts);
+    wave_atomic_add(&st->bad_range, bad_slide);
+    wave_atomic_add(&st->hist_out, hout);
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    if (lane == 0) {
+        s_min[wid] = mn;
+        s_max[wid] = mx;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        long long a = s_min[0], b = s_max[0];
+        for (int w = 1; w < (int)(blockDim.x >> 6); ++w) {
+            a = s_min[w] < a ? s_min[w] : a;
+            b = s_max[w] > b ? s_max[w] : b;
+        }
+        if (a != 0x7fffffffffffffffLL) {
+            atomicMin(&st->min_idx, a);
+            atomicMax(&st->max_idx, b);
+        }
+    }
+    for (int i = threadIdx.x; i < GWO_HIST_BINS; i += blockDim.x)
+        if (s_hist[i]) atomicAdd(&st->hist[i], s_hist[i]);
+}
+
+// ------------------------------------------------------------------------------------------------
+// insert (direct): one lane per record, device-scope atomics into the window's table
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ void apply_record(const TableDesc &t, const AccPlan &p, int64_t k, int64_t vbits) {
+    int64_t *acc = find_or_insert(t, p.stride, k);
+    for (int w = 0; w < p.nwords; ++w) atomic_combine(acc + w, p.op[w], lift_word(p, w, vbits));
+}
+
+__device__ __forceinline__ void check_key_group(int64_t k, const WindowGeom &g, BatchStats *st) {
+    int32_t kg = key_group(k, g.key_kind, g.max_par);
+    if (kg < g.kg_lo || kg > g.kg_hi) {
+        atomicAdd(&st->bad_kg, 1ull);
+        st->bad_kg_key = k;
+    }
+}
+
+__global__ __launch_bounds__(256) void insert_direct_kernel(const int64_t *__restrict__ key,
+                                                            const int64_t *__restrict__ ts,
+                                                            const int64_t *__restrict__ val, int64_t n,
+                                                            WindowGeom g, AccPlan p,
+                                                            const TableDesc *__restrict__ dir, long long dir_base,
+                                                            int dir_len, BatchStats *st) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        long long u = 0;
+        int64_t t = ts[i];
+        if (classify(t, g, u) != REC_ACCEPT) continue;
+        long long d = u - dir_base;
+        if (d < 0 || d >= dir_len) continue;
+        int64_t k = key[i];
+        check_key_group(k, g, st);
+        int64_t v = val ? val[i] : 0;
+        apply_record(dir[d], p, k, v);
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// insert (pre-aggregated): each workgroup folds a tile of records into an LDS hash table keyed
+// on (key, unit) first, then flushes one device-scope update per distinct pair.
+// Claim protocol: a 64-bit tag = mix(key, unit)|1 is claimed with an LDS CAS; the claimant writes
+// the exact (key, unit) and the identity accumulator; after a barrier every lane verifies the
+// exact pair (a tag collision falls back to the direct global path, so results never depend on it).
+// ------------------------------------------------------------------------------------------------
+#define PREAGG_SLOTS 2048   // LDS: 2048 x (8 + 8 + 4 + 8*8) B = 168 KiB worst case -> words cap below
+#define PREAGG_WORDS 6      // pre-aggregation is used for <= 6 accumulator words
+#define PREAGG_TILE 4096
+
+__device__ __forceinline__ uint64_t pair_tag(int64_t k, long long u) {
+    uint64_t h = slot_hash(k ^ (int64_t)((uint64_t)u * 0xD1B54A32D192ED03ull));
+    return h | 1ull;
+}
+
+__device__ __forceinline__ void lds_combine(int64_t *dst, int op, int64_t x) {
+    switch (op) {
+        case ACC_ADD_I64: atomicAdd((unsigned long long *)dst, (unsigned long long)x); break;
+        case ACC_ADD_F64: atomicAdd((double *)dst, __longlong_as_double(x)); break;
+        case ACC_MIN_I64: atomicMin((long long *)dst, (long long)x); break;
+        default: atomicMax((long long *)dst, (long long)x); break;
+    }
+}
+
+__global__ __launch_bounds__(256) void insert_preagg_kernel(const int64_t *__restrict__ key,
+                                                            const int64_t *__restrict__ ts,
+                                                            const int64_t *__restrict__ val, int64_t n,
+                                                            WindowGeom g, AccPlan p,
+                                                            const TableDesc *__restrict__ dir, long long dir_base,
+                                                            int dir_len, BatchStats *st,
+                                                            unsigned long long *partials) {
+    __shared__ unsigned long long s_tag[PREAGG_SLOTS];
+    __shared__ int64_t s_key[PREAGG_SLOTS];
+    __shared__ int32_t s_unit[PREAGG_SLOTS];
+    __shared__ int64_t s_acc[PREAGG_SLOTS * PREAGG_WORDS];
+    const int NW = p.nwords;
+    constexpr int PER = PREAGG_TILE / 256;
+    unsigned long long flushed = 0;
+    for (int64_t tile = (int64_t)blockIdx.x * PREAGG_TILE; tile < n; tile += (int64_t)gridDim.x * PREAGG_TILE) {
+        for (int i = threadIdx.x; i < PREAGG_SLOTS; i += 256) s_tag[i] = 0;
+        __syncthreads();
+        int slot[PER];
+        int64_t rk[PER], rv[PER];
+        int32_t ru[PER];
+#pragma unroll
+        for (int j = 0; j < PER; ++j) {
+            slot[j] = -2;  // -2: not accepted, -1: go direct
+            int64_t i = tile + j * 256 + threadIdx.x;
+            if (i >= n) continue;
+            long long u = 0;
+            if (classify(ts[i], g, u) != REC_ACCEPT) continue;
+            long long d = u - dir_base;
+            if (d < 0 || d >= dir_len) continue;
+            int64_t k = key[i];
+            check_key_group(k, g, st);
+            rk[j] = k;
+            rv[j] = val ? val[i] : 0;
+            ru[j] = (int32_t)d;
+            uint64_t tag = pair_tag(k, d);
+            int s = (int)(tag >> 40) & (PREAGG_SLOTS - 1);
+            slot[j] = -1;
+            for (int probe = 0; probe < 32; ++probe) {
+                unsigned long long prev = atomicCAS(&s_tag[s], 0ull, tag);
+                if (prev == 0ull) {
+                    s_key[s] = k;
+                    s_unit[s] = (int32_t)d;
+                    for (int w = 0; w < NW; ++w) s_acc[s * NW + w] = p.ident[w];
+                    slot[j] = s;
+                    break;
+                }
+                if (prev == tag) {
+                    slot[j] = s;
+                    break;
+                }
+                s = (s + 1) & (PREAGG_SLOTS - 1);
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < PER; ++j) {
+            if (slot[j] == -2) continue;
+            int s = slot[j];
+            if (s >= 0 && s_key[s] == rk[j] && s_unit[s] == ru[j]) {
+                for (int w = 0; w < NW; ++w) lds_combine(&s_acc[s * NW + w], p.op[w], lift_word(p, w, rv[j]));
+            } else {
+                apply_record(dir[ru[j]], p, rk[j], rv[j]);
+            }
+        }
+        __syncthreads();
+        for (int s = threadIdx.x; s < PREAGG_SLOTS; s += 256) {
+            if (s_tag[s] == 0ull) continue;
+            flushed++;
+            int64_t *a = find_or_insert(dir[s_unit[s]], p.stride, s_key[s]);
+            for (int w = 0; w < NW; ++w) atomic_combine(a + w, p.op[w], s_acc[s * NW + w]);
+        }
+        __syncthreads();
+    }
+    wave_atomic_add(partials, flushed);
+}
+
+// ------------------------------------------------------------------------------------------------
+// fire: EventTimeTrigger.onEventTime FIRE + clearAllState for one window's table
+// (WindowOperator.java:430-473, 528-550).  Occupied entries -> output rows via wave ballot
+// stream compaction (one device atomic per wave); entries are reset to EMPTY/identity in place
+// so the table returns to the pool clean.
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ void write_results(const AccPlan &p, const ResultPlan &rp, const int64_t *acc,
+                                              const OutCols &o, unsigned long long pos) {
+    for (int a = 0; a < rp.naggs; ++a) {
+        int w = rp.word[a];
+        int64_t r;
+        switch (rp.kind[a]) {
+            case 2:  // MIN
+            case 3:  // MAX
+                r = rp.value_is_f64 ? f64_from_order_key(acc[w]) : acc[w];
+                break;
+            case 4: {  // AVG: (double) sum / count
+                double s = rp.value_is_f64 ? __longlong_as_double(acc[w]) : (double)acc[w];
+                r = __double_as_longlong(s / (double)acc[w + 1]);
+                break;
+            }
+            default: r = acc[w]; break;  // COUNT, SUM (int64 or double bits)
+        }
+        o.res[a][pos] = r;
+    }
+}
+
+__global__ __launch_bounds__(256) void fire_kernel(TableDesc t, uint64_t cap, AccPlan p, ResultPlan rp, int64_t start,
+                                                   int64_t end, OutCols o, int reset) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    const int lane = threadIdx.x & 63;
+    // +1 iteration space for the side slot (key == Long.MIN_VALUE)
+    for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x; base < cap + 1; base += stride) {
+        uint64_t i = base + threadIdx.x;
+        bool occ = false;
+        int64_t k = 0;
+        int64_t acc[GWO_MAX_WORDS];
+        const int NW = p.nwords;
+        int64_t *e = nullptr;
+        if (i < cap) {
+            e = t.base + i * (uint64_t)p.stride;
+            k = e[0];
+            occ = k != GWO_EMPTY_KEY;
+            if (occ) {
+#pragma unroll
+                for (int w = 0; w < GWO_MAX_WORDS; ++w)
+                    if (w < NW) acc[w] = e[1 + w];
+            }
+        } else if (i == cap) {
+            occ = t.side[0] != 0;
+            k = GWO_EMPTY_KEY;
+            if (occ) {
+#pragma unroll
+                for (int w = 0; w < GWO_MAX_WORDS; ++w)
+                    if (w < NW) acc[w] = t.side[1 + w];
+            }
+        }
+        unsigned long long m = __ballot(occ);
+        if (m == 0) continue;
+        unsigned long long wbase = 0;
+        if (lane == 0) wbase = atomicAdd(o.count, (unsigned long long)__popcll(m));
+        wbase = __shfl(wbase, 0);
+        if (occ) {
+            unsigned long long pos = wbase + __popcll(m & ((1ull << lane) - 1));
+            if ((long long)pos < o.cap) {
+                o.key[pos] = k;
+                o.start[pos] = start;
+                o.end[pos] = end;
+                write_results(p, rp, acc, o, pos);
+            }
+            if (reset) {
+                if (i < cap) {
+                    e[0] = GWO_EMPTY_KEY;
+                    for (int w = 0; w < NW; ++w) e[1 + w] = p.ident[w];
+                } else {
+                    t.side[0] = 0;
+                    for (int w = 0; w < NW; ++w) t.side[1 + w] = p.ident[w];
+                }
+            }
+        }
+    }
+}
+
+// Fill a fresh table with EMPTY keys and identity accumulators.
+__global__ __launch_bounds__(256) void fill_kernel(int64_t *base, uint64_t words, AccPlan p) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < words; i += stride) {
+        int w = (int)(i % (uint64_t)p.stride);
+        base[i] = w == 0 ? GWO_EMPTY_KEY : (w - 1 < p.nwords ? p.ident[w - 1] : 0);
+    }
+}
+
+__global__ __launch_bounds__(256) void rehash_kernel(TableDesc src, uint64_t cap, TableDesc dst, AccPlan p) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < cap; i += stride) {
+        int64_t *e = src.base + i * (uint64_t)p.stride;
+        int64_t k = e[0];
+        if (k == GWO_EMPTY_KEY) continue;
+        int64_t *a = find_or_insert(dst, p.stride, k);
+        for (int w = 0; w < p.nwords; ++w) {
+            a[w] = e[1 + w];
+            e[1 + w] = p.ident[w];
+        }
+        e[0] = GWO_EMPTY_KEY;
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// utility kernels
+// ------------------------------------------------------------------------------------------------
+__global__ void key_groups_kernel(const int64_t *keys, int64_t n, int kind, int max_par, int par, int32_t *kg,
+                                  int32_t *op) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        int32_t g = key_group(keys[i], kind, max_par);
+        if (kg) kg[i] = g;
+        if (op) op[i] = g * par / max_par;  // KeyGroupRangeAssignment.java:118-119
+    }
+}
+
+__global__ void window_starts_kernel(const int64_t *ts, int64_t n, int64_t off, int64_t size, int64_t *out) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+        out[i] = window_start(ts[i], off, size);
+}
+
+// Counter-based splitmix64 source (identical definition in oracle/gen.py):
+//   u(s, g) = fmix64(seed + s * 0xD1B54A32D192ED03 + (g + 1) * 0x9E3779B97F4A7C15)
+__device__ __forceinline__ uint64_t sm_u(uint64_t seed, uint64_t s, uint64_t g) {
+    uint64_t z = seed + s * 0xD1B54A32D192ED03ull + (g + 1) * 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+__global__ void generate_kernel(uint64_t seed, int64_t first, int64_t total, int64_t nkeys, int64_t span,
+                                int64_t disorder, int64_t t0, int64_t vrange, int vf64, int key_mode, int64_t n,
+                                int64_t *key, int64_t *ts, int64_t *val) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        uint64_t g = (uint64_t)(first + i);
+        int64_t k;
+        if (key_mode == 1) {  // YSB: ad_id uniform over 10*nkeys ads, campaign = ad_id % nkeys
+            k = (int64_t)((sm_u(seed, 0, g) % (uint64_t)(10 * nkeys)) % (uint64_t)nkeys);
+        } else {
+            k = (int64_t)(sm_u(seed, 0, g) % (uint64_t)nkeys);
+        }
+        key[i] = k;
+        int64_t jitter = disorder > 0 ? (int64_t)(sm_u(seed, 2, g) % (uint64_t)disorder) : 0;
+        // (g * span) / total without overflow for g, span < 2^63: split the product
+        int64_t q = (int64_t)g / total, r = (int64_t)g % total;
+        int64_t base_t = q * span + (int64_t)(((__int128)r * span) / total);
+        ts[i] = t0 + base_t + jitter;
+        if (val) {
+            uint64_t u = sm_u(seed, 1, g);
+            if (vf64) {
+                double d = (double)(u % (uint64_t)vrange) + (double)(sm_u(seed, 3, g) >> 11) * (1.0 / 9007199254740992.0);
+                val[i] = __double_as_longlong(d);
+            } else {
+                val[i] = (int64_t)(u % (uint64_t)vrange);
+            }
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// launchers
+// ------------------------------------------------------------------------------------------------
+static inline int grid_for(int64_t n, int per_thread = 1, int cap = 4096) {
+    int64_t g = (n + 256LL * per_thread - 1) / (256LL * per_thread);
+    if (g < 1) g = 1;
+    if (g > cap) g = cap;
+    return (int)g;
+}
+
+void launch_scan(const int64_t *key, const int64_t *ts, int64_t n, const WindowGeom &g, long long hist_base,
+                 BatchStats *stats, int64_t *side_key, int64_t *side_ts, int64_t *side_val, const int64_t *val,
+                 unsigned long long *side_count, long long side_cap, int side_enabled, hipStream_t s) {
+    hipLaunchKernelGGL(scan_kernel, dim3(grid_for(n, 4, 2048)), dim3(256), 0, s, key, ts, val, n, g, hist_base,
+                       stats, side_key, side_ts, side_val, side_count, side_cap, side_enabled);
+}
+
+void launch_insert(const int64_t *key, const int64_t *ts, const void *val, int64_t n, const WindowGeom &g,
+                   const AccPlan &plan, const TableDesc *dir, long long dir_base, int dir_len, int preagg,
+                   BatchStats *st, hipStream_t s) {
+    unsigned long long *partials = &st->partials;
+    const int64_t *v = (const int64_t *)val;
+    if (preagg && plan.nwords <= PREAGG_WORDS) {
+        int grid = (int)((n + PREAGG_TILE - 1) / PREAGG_TILE);
+        if (grid > 2048) grid = 2048;
+        if (grid < 1) grid = 1;
+        hipLaunchKernelGGL(insert_preagg_kernel, dim3(grid), dim3(256), 0, s, key, ts, v, n, g, plan, dir, dir_base,
+                           dir_len, st, partials);
+    } else {
+        int grid = grid_for(n, 1, 8192);
+        hipLaunchKernelGGL(insert_direct_kernel, dim3(grid), dim3(256), 0, s, key, ts, v, n, g, plan, dir, dir_base,
+                           dir_len, st);
+    }
+}
+
+void launch_fire(const TableDesc &t, uint64_t cap, const AccPlan &plan, const ResultPlan &rp, int64_t start,
+                 int64_t end, OutCols out, int reset, hipStream_t s) {
+    int grid = grid_for((int64_t)cap + 1, 1, 8192);
+    hipLaunchKernelGGL(fire_kernel, dim3(grid), dim3(256), 0, s, t, cap, plan, rp, start, end, out, reset);
+}
+
+void launch_fill(int64_t *base, uint64_t cap, const AccPlan &plan, hipStream_t s) {
+    uint64_t words = cap * (uint64_t)plan.stride;
+    hipLaunchKernelGGL(fill_kernel, dim3(grid_for((int64_t)words, 4, 8192)), dim3(256), 0, s, base, words, plan);
+}
+
+void launch_rehash(const TableDesc &src, uint64_t src_cap, const TableDesc &dst, const AccPlan &plan,
+                   hipStream_t s) {
+    int grid = grid_for((int64_t)src_cap, 1, 8192);
+    hipLaunchKernelGGL(rehash_kernel, dim3(grid), dim3(256), 0, s, src, src_cap, dst, plan);
+}
+
+void launch_key_groups(const int64_t *keys, int64_t n, int key_kind, int max_par, int par, int32_t *kg,
+                       int32_t *op, hipStream_t s) {
+    hipLaunchKernelGGL(key_groups_kernel, dim3(grid_for(n, 4)), dim3(256), 0, s, keys, n, key_kind, max_par, par,
+                       kg, op);
+}
+
+void launch_window_starts(const int64_t *ts, int64_t n, int64_t offset, int64_t size, int64_t *out,
+                          hipStream_t s) {
+    hipLaunchKernelGGL(window_starts_kernel, dim3(grid_for(n, 4)), dim3(256), 0, s, ts, n, offset, size, out);
+}
+
+void launch_generate(uint64_t seed, int64_t first, int64_t total, int64_t nkeys, int64_t span, int64_t disorder,
+                     int64_t t0, int64_t vrange, int vf64, int key_mode, int64_t n, int64_t *key, int64_t *ts,
+                     void *val, hipStream_t s) {
+    hipLaunchKernelGGL(generate_kernel, dim3(grid_for(n, 4, 8192)), dim3(256), 0, s, seed, first, total, nkeys,
+                       span, disorder, t0, vrange, vf64, key_mode, n, key, ts, (int64_t *)val);
+}
+
+}  // namespace gwo

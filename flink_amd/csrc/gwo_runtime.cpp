@@ -1,0 +1,765 @@
+// gwo_runtime.cpp -- host side of the C ABI declared in include/gwo.h.
+//
+// One gwo_handle is one WindowOperator subtask (WindowOperator.java:100) whose keyed window state
+// lives in HBM.  Host code here only does bookkeeping that the reference keeps in its timer
+// service and state table directory: which per-window tables exist, their capacities, which fire
+// at a watermark (InternalTimerServiceImpl.advanceWatermark, :268-278).  Every per-record and
+// per-entry operation runs in the gfx950 kernels of gwo_kernels.hip / gwo_slide.hip / gwo_session.hip.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "../../include/gwo.h"
+#include "gwo_handle.h"
+
+using namespace gwo;
+
+namespace gwo {
+
+const char *status_str(gwo_status s) {
+    switch (s) {
+        case GWO_OK: return "GWO_OK";
+        case GWO_ERR_INVALID_ARGUMENT: return "GWO_ERR_INVALID_ARGUMENT";
+        case GWO_ERR_NO_TIMESTAMP: return "GWO_ERR_NO_TIMESTAMP";
+        case GWO_ERR_KEY_GROUP: return "GWO_ERR_KEY_GROUP";
+        case GWO_ERR_OUT_OF_MEMORY: return "GWO_ERR_OUT_OF_MEMORY";
+        case GWO_ERR_HIP: return "GWO_ERR_HIP";
+        case GWO_ERR_UNSUPPORTED: return "GWO_ERR_UNSUPPORTED";
+        case GWO_ERR_MERGE_LATE: return "GWO_ERR_MERGE_LATE";
+        case GWO_ERR_COMM: return "GWO_ERR_COMM";
+        case GWO_ERR_STATE: return "GWO_ERR_STATE";
+        case GWO_ERR_CAPACITY: return "GWO_ERR_CAPACITY";
+    }
+    return "GWO_ERR_UNKNOWN";
+}
+
+gwo_status Handle::fail(gwo_status s, const char *fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    err = std::string(status_str(s)) + ": " + buf;
+    return s;
+}
+
+gwo_status Handle::poison(gwo_status s, const char *what) {
+    poisoned = true;
+    poison_status = s;
+    err = std::string(status_str(s)) + ": " + what;
+    return s;
+}
+
+// ---- device memory -------------------------------------------------------------------------------
+gwo_status Handle::dalloc(void **p, size_t bytes) {
+    if (bytes == 0) bytes = 16;
+    hipError_t e = hipMalloc(p, bytes);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        return fail(GWO_ERR_OUT_OF_MEMORY, "hipMalloc(%zu) failed: %s", bytes, hipGetErrorString(e));
+    }
+    return GWO_OK;
+}
+
+gwo_status Handle::hipcheck(hipError_t e, const char *what) {
+    if (e == hipSuccess) return GWO_OK;
+    (void)hipGetLastError();
+    return poison(GWO_ERR_HIP, (std::string(what) + ": " + hipGetErrorString(e)).c_str());
+}
+
+gwo_status Handle::ensure_buf(DevBuf &b, size_t bytes) {
+    if (b.bytes >= bytes) return GWO_OK;
+    if (b.ptr) {
+        GWO_TRY(hipcheck(hipStreamSynchronize(stream), "sync before realloc"));
+        (void)hipFree(b.ptr);
+        b.ptr = nullptr;
+        b.bytes = 0;
+    }
+    size_t nb = std::max(bytes, b.bytes * 2);
+    GWO_TRY(dalloc(&b.ptr, nb));
+    b.bytes = nb;
+    return GWO_OK;
+}
+
+// Counter slots for table occupancy (one device array, so one D2H copy reads all of them).
+int Handle::take_counter() {
+    for (size_t i = 0; i < counter_used.size(); ++i)
+        if (!counter_used[i]) {
+            counter_used[i] = 1;
+            return (int)i;
+        }
+    return -1;
+}
+
+gwo_status Handle::alloc_table(uint64_t cap, Table &t) {
+    // pool first: released tables are clean (fire/rehash reset every entry they touch)
+    auto it = pool.find(cap);
+    if (it != pool.end()) {
+        t.base = it->second;
+        pool.erase(it);
+    } else {
+        void *p = nullptr;
+        size_t words = (size_t)cap * plan.stride + plan.stride;  // + side slot
+        gwo_status s = dalloc(&p, words * 8);
+        if (s != GWO_OK) {
+            // return pooled memory to the allocator and retry once
+            trim_pool();
+            GWO_TRY(dalloc(&p, words * 8));
+        }
+        t.base = (int64_t *)p;
+        launch_fill(t.base, cap + 1, plan, stream);  // side slot is entry `cap`: flag word 0 = EMPTY
+        // the side slot's flag must read 0 (not EMPTY): reset its first word
+        int64_t zero = 0;
+        GWO_TRY(hipcheck(hipMemcpyAsync(t.base + cap * plan.stride, &zero, 8, hipMemcpyHostToDevice, stream),
+                         "side slot init"));
+        GWO_TRY(hipcheck(hipStreamSynchronize(stream), "table init"));
+    }
+    t.cap = cap;
+    t.side = t.base + cap * plan.stride;
+    t.counter = take_counter();
+    if (t.counter < 0) return fail(GWO_ERR_OUT_OF_MEMORY, "too many live windows/panes (> %zu)", counter_used.size());
+    t.occ = 0;
+    int64_t zero = 0;
+    return hipcheck(hipMemcpyAsync(d_counters + t.counter, &zero, 8, hipMemcpyHostToDevice, stream), "counter");
+}
+
+void Handle::release_table(Table &t) {
+    if (t.counter >= 0) counter_used[t.counter] = 0;
+    pool.emplace(t.cap, t.base);
+    t.base = nullptr;
+    t.counter = -1;
+}
+
+void Handle::trim_pool() {
+    (void)hipStreamSynchronize(stream);
+    for (auto &kv : pool) (void)hipFree(kv.second);
+    pool.clear();
+}
+
+TableDesc Handle::desc(const Table &t) const {
+    TableDesc d;
+    d.base = t.base;
+    d.side = t.side;
+    d.occ = d_counters + t.counter;
+    d.mask = t.cap - 1;
+    return d;
+}
+
+static uint64_t next_pow2(uint64_t x) {
+    uint64_t p = 1;
+    while (p < x) p <<= 1;
+    return p;
+}
+
+// Make sure table `u` can take `incoming` more entries at load <= kMaxLoad; grow by rehash.
+gwo_status Handle::ensure_table(long long u, uint64_t incoming) {
+    auto it = tables.find(u);
+    uint64_t want_min = std::max<uint64_t>(kMinCap, next_pow2((uint64_t)((double)(incoming) / kInitLoad) + 1));
+    if (cfg.expected_keys > 0)
+        want_min = std::max<uint64_t>(want_min, next_pow2((uint64_t)((double)cfg.expected_keys / kInitLoad) + 1));
+    if (it == tables.end()) {
+        Table t;
+        GWO_TRY(alloc_table(want_min, t));
+        tables.emplace(u, t);
+        return GWO_OK;
+    }
+    Table &t = it->second;
+    if ((double)(t.occ + incoming) <= kMaxLoad * (double)t.cap) return GWO_OK;
+    uint64_t ncap = next_pow2((uint64_t)((double)(t.occ + incoming) / kInitLoad) + 1);
+    Table nt;
+    GWO_TRY(alloc_table(ncap, nt));
+    launch_rehash(desc(t), t.cap, desc(nt), plan, stream);
+    // the side slot moves by copy (flag + words)
+    GWO_TRY(hipcheck(hipMemcpyAsync(nt.side, t.side, (size_t)plan.stride * 8, hipMemcpyDeviceToDevice, stream),
+                     "side copy"));
+    std::vector<int64_t> side_reset(plan.stride, 0);
+    for (int w = 0; w < plan.nwords; ++w) side_reset[1 + w] = plan.ident[w];
+    GWO_TRY(hipcheck(hipMemcpyAsync(t.side, side_reset.data(), (size_t)plan.stride * 8, hipMemcpyHostToDevice, stream),
+                     "side reset"));
+    // occupancy moves with the entries
+    GWO_TRY(hipcheck(hipMemcpyAsync(d_counters + nt.counter, d_counters + t.counter, 8, hipMemcpyDeviceToDevice, stream),
+                     "occ copy"));
+    GWO_TRY(hipcheck(hipStreamSynchronize(stream), "rehash"));
+    nt.occ = t.occ;
+    nt.fired = t.fired;
+    release_table(t);
+    it->second = nt;
+    return GWO_OK;
+}
+
+// Reads every live table's occupancy counter (one D2H copy).
+gwo_status Handle::read_occupancy() {
+    int hi = 0;
+    for (auto &kv : tables) hi = std::max(hi, kv.second.counter + 1);
+    for (auto &kv : aux_tables) hi = std::max(hi, kv.counter + 1);
+    if (hi == 0) return GWO_OK;
+    GWO_TRY(hipcheck(hipMemcpyAsync(h_counters, d_counters, (size_t)hi * 8, hipMemcpyDeviceToHost, stream), "occ"));
+    GWO_TRY(hipcheck(hipStreamSynchronize(stream), "occ sync"));
+    for (auto &kv : tables) kv.second.occ = h_counters[kv.second.counter];
+    for (auto &t : aux_tables) t.occ = h_counters[t.counter];
+    return GWO_OK;
+}
+
+gwo_status Handle::ensure_output(uint64_t extra) {
+    uint64_t need = out_rows + extra;
+    if ((long long)need <= out.cap) return GWO_OK;
+    uint64_t ncap = std::max<uint64_t>(need, (uint64_t)out.cap * 2);
+    ncap = std::max<uint64_t>(ncap, 1 << 16);
+    int ncols = 3 + rplan.naggs;
+    int64_t *cols[7] = {};
+    for (int c = 0; c < ncols; ++c) GWO_TRY(dalloc((void **)&cols[c], ncap * 8));
+    int64_t *old[7] = {out.key, out.start, out.end, out.res[0], out.res[1], out.res[2], out.res[3]};
+    for (int c = 0; c < ncols; ++c) {
+        if (old[c] && out_rows)
+            GWO_TRY(hipcheck(hipMemcpyAsync(cols[c], old[c], out_rows * 8, hipMemcpyDeviceToDevice, stream), "out grow"));
+    }
+    GWO_TRY(hipcheck(hipStreamSynchronize(stream), "out grow sync"));
+    for (int c = 0; c < ncols; ++c)
+        if (old[c]) (void)hipFree(old[c]);
+    out.key = cols[0];
+    out.start = cols[1];
+    out.end = cols[2];
+    for (int a = 0; a < 4; ++a) out.res[a] = a < rplan.naggs ? cols[3 + a] : nullptr;
+    out.cap = (long long)ncap;
+    return GWO_OK;
+}
+
+// ---- profiling ---------------------------------------------------------------------------------
+void Handle::prof_begin(int k) {
+    if (!profiling) return;
+    hipEvent_t a, b;
+    (void)hipEventCreate(&a);
+    (void)hipEventCreate(&b);
+    (void)hipEventRecord(a, stream);
+    pending_events.push_back({k, a, b, 0});
+}
+void Handle::prof_end(int k, int64_t items) {
+    if (!profiling || pending_events.empty()) return;
+    auto &pe = pending_events.back();
+    if (pe.kernel != k) return;
+    (void)hipEventRecord(pe.b, stream);
+    pe.items = items;
+}
+gwo_status Handle::prof_collect() {
+    if (pending_events.empty()) return GWO_OK;
+    GWO_TRY(hipcheck(hipStreamSynchronize(stream), "prof sync"));
+    for (auto &pe : pending_events) {
+        float ms = 0.f;
+        (void)hipEventElapsedTime(&ms, pe.a, pe.b);
+        kstats[pe.kernel].launches++;
+        kstats[pe.kernel].ms += ms;
+        kstats[pe.kernel].items += pe.items;
+        (void)hipEventDestroy(pe.a);
+        (void)hipEventDestroy(pe.b);
+    }
+    pending_events.clear();
+    return GWO_OK;
+}
+
+// ---- input staging ----------------------------------------------------------------------------
+static bool is_device_ptr(const void *p) {
+    if (!p) return true;
+    hipPointerAttribute_t attr;
+    if (hipPointerGetAttributes(&attr, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return attr.type == hipMemoryTypeDevice || attr.type == hipMemoryTypeManaged;
+}
+
+gwo_status Handle::stage_inputs(const int64_t *key, const int64_t *ts, const void *val, int64_t n, const int64_t **dk,
+                                const int64_t **dt, const int64_t **dv) {
+    const void *src[3] = {key, ts, val};
+    DevBuf *bufs[3] = {&stage_key, &stage_ts, &stage_val};
+    const int64_t **dst[3] = {dk, dt, dv};
+    for (int c = 0; c < 3; ++c) {
+        if (!src[c]) {
+            *dst[c] = nullptr;
+            continue;
+        }
+        if (is_device_ptr(src[c])) {
+            *dst[c] = (const int64_t *)src[c];
+        } else {
+            GWO_TRY(ensure_buf(*bufs[c], (size_t)n * 8));
+            GWO_TRY(hipcheck(hipMemcpyAsync(bufs[c]->ptr, src[c], (size_t)n * 8, hipMemcpyHostToDevice, stream), "stage"));
+            *dst[c] = (const int64_t *)bufs[c]->ptr;
+        }
+    }
+    return GWO_OK;
+}
+
+// ---- geometry helpers ---------------------------------------------------------------------------
+int64_t Handle::unit_start(long long u) const {  // start of window/pane u
+    return (int64_t)((uint64_t)u * (uint64_t)geom.unit + (uint64_t)geom.unit_off_mod);
+}
+
+WindowGeom Handle::geom_now() const {
+    WindowGeom g = geom;
+    g.wm = wm;
+    return g;
+}
+
+// ---- tumbling / pane insert -------------------------------------------------------------------------
+gwo_status Handle::insert_windowed(const int64_t *k, const int64_t *t, const int64_t *v, int64_t n) {
+    WindowGeom g = geom_now();
+    long long hist_base = hist_hint;
+    bool first_pass = true;
+    BatchStats &hs = *h_stats;
+    // one scan pass per 64-unit chunk of the batch's unit range (normally exactly one)
+    long long lo = 0, hi = -1;
+    while (true) {
+        init_stats(hist_base);
+        prof_begin(GWO_KERNEL_SCAN);
+        launch_scan(k, t, n, g, hist_base, d_stats, (int64_t *)side_key.ptr, (int64_t *)side_ts.ptr,
+                    (int64_t *)side_val.ptr, v, d_side_count, first_pass && side_enabled() ? side_cap : 0,
+                    first_pass && side_enabled(), stream);
+        prof_end(GWO_KERNEL_SCAN, n);
+        GWO_TRY(hipcheck(hipMemcpyAsync(h_stats, d_stats, sizeof(BatchStats), hipMemcpyDeviceToHost, stream), "stats"));
+        GWO_TRY(read_occupancy());  // syncs
+        if (first_pass) {
+            if (hs.bad_ts) return poison(GWO_ERR_NO_TIMESTAMP,
+                                         "Record has Long.MIN_VALUE timestamp (= no timestamp marker). Is the time "
+                                         "characteristic set to 'ProcessingTime', or did you forget to call "
+                                         "'DataStream.assignTimestampsAndWatermarks(...)'?");
+            if (hs.bad_range) return poison(GWO_ERR_UNSUPPORTED,
+                                            "sliding windows: timestamp < offset - slide (Java '%' quirk range) is "
+                                            "outside the pane restatement");
+            if (hs.refire) return poison(GWO_ERR_UNSUPPORTED,
+                                         "allowedLateness > 0 re-firing on sliding windows is not supported");
+            if (side_enabled()) {
+                GWO_TRY(hipcheck(hipMemcpy(&side_rows, d_side_count, 8, hipMemcpyDeviceToHost), "side count"));
+                if ((long long)side_rows > side_cap) {
+                    // grow and re-collect this batch's side output (first pass only)
+                    side_rows = side_rows_committed;
+                    GWO_TRY(grow_side((long long)hs.late + (long long)side_rows_committed));
+                    GWO_TRY(hipcheck(hipMemcpy(d_side_count, &side_rows, 8, hipMemcpyHostToDevice), "side reset"));
+                    continue;
+                }
+                side_rows_committed = side_rows;
+            } else {
+                late_dropped += hs.late;
+            }
+            if (hs.accepted == 0) return GWO_OK;
+            lo = hs.min_idx;
+            hi = hs.max_idx;
+            first_pass = false;
+            if (hist_base > lo || hist_base + GWO_HIST_BINS <= lo) {
+                hist_base = lo;  // histogram missed the range: rescan this chunk
+                continue;
+            }
+        }
+        // process units [hist_base, min(hi, hist_base+63)] with exact per-unit counts
+        long long chunk_hi = std::min<long long>(hi, hist_base + GWO_HIST_BINS - 1);
+        int dir_len = (int)(chunk_hi - hist_base + 1);
+        h_dir.assign(dir_len, TableDesc{});
+        for (int d = 0; d < dir_len; ++d) {
+            uint64_t cnt = hs.hist[d];
+            if (!cnt) continue;
+            GWO_TRY(ensure_table(hist_base + d, cnt));
+        }
+        for (int d = 0; d < dir_len; ++d) {
+            auto it = tables.find(hist_base + d);
+            if (it != tables.end()) h_dir[d] = desc(it->second);
+        }
+        GWO_TRY(ensure_buf(dir_buf, dir_len * sizeof(TableDesc)));
+        GWO_TRY(hipcheck(hipMemcpyAsync(dir_buf.ptr, h_dir.data(), dir_len * sizeof(TableDesc), hipMemcpyHostToDevice,
+                                        stream), "dir"));
+        prof_begin(GWO_KERNEL_INSERT);
+        launch_insert(k, t, v, n, g, plan, (const TableDesc *)dir_buf.ptr, hist_base, dir_len, use_preagg, d_stats,
+                      stream);
+        prof_end(GWO_KERNEL_INSERT, n);
+        // key-group violations surface at the next sync (Flink fails the task at that record)
+        GWO_TRY(hipcheck(hipMemcpyAsync(&h_stats->bad_kg, &d_stats->bad_kg, 16, hipMemcpyDeviceToHost, stream), "kg"));
+        GWO_TRY(hipcheck(hipMemcpyAsync(&h_stats->partials, &d_stats->partials, 8, hipMemcpyDeviceToHost, stream), "p"));
+        GWO_TRY(hipcheck(hipStreamSynchronize(stream), "insert"));
+        if (hs.bad_kg) {
+            long long kg = -1;
+            (void)kg;
+            return poison(GWO_ERR_KEY_GROUP, ("Key group of key " + std::to_string(hs.bad_kg_key) +
+                                              " is not in KeyGroupRange{startKeyGroup=" + std::to_string(cfg.key_group_start) +
+                                              ", endKeyGroup=" + std::to_string(cfg.key_group_end) + "}.").c_str());
+        }
+        adapt_preagg(hs.accepted, hs.partials);
+        if (chunk_hi >= hi) break;
+        hist_base = chunk_hi + 1;
+        // next chunk: skip empty unit ranges by rescanning from the next populated unit
+    }
+    hist_hint = lo;
+    for (auto &kv : tables) kv.second.dirty = true;
+    return GWO_OK;
+}
+
+void Handle::adapt_preagg(uint64_t accepted, uint64_t partials) {
+    // Pre-aggregation pays when a tile folds several records per (key, window); measured by the
+    // partials it flushed.  Off: re-probe every 32 batches.
+    batches++;
+    if (use_preagg) {
+        if (accepted > 0 && (double)partials > 0.5 * (double)accepted) use_preagg = 0;
+    } else if (batches % 32 == 0) {
+        use_preagg = 1;
+    }
+    if (cfg_preagg >= 0) use_preagg = cfg_preagg;
+}
+
+void Handle::init_stats(long long hist_base) {
+    BatchStats s;
+    memset(&s, 0, sizeof s);
+    s.min_idx = 0x7fffffffffffffffLL;
+    s.max_idx = (long long)0x8000000000000000LL;
+    (void)hist_base;
+    *h_stats_init = s;
+    (void)hipMemcpyAsync(d_stats, h_stats_init, sizeof(BatchStats), hipMemcpyHostToDevice, stream);
+}
+
+gwo_status Handle::grow_side(long long need) {
+    long long ncap = std::max<long long>(need, side_cap * 2);
+    ncap = std::max<long long>(ncap, 1024);
+    DevBuf nk, nt, nv;
+    GWO_TRY(ensure_buf(nk, ncap * 8));
+    GWO_TRY(ensure_buf(nt, ncap * 8));
+    GWO_TRY(ensure_buf(nv, ncap * 8));
+    if (side_rows_committed) {
+        GWO_TRY(hipcheck(hipMemcpyAsync(nk.ptr, side_key.ptr, side_rows_committed * 8, hipMemcpyDeviceToDevice, stream), "s"));
+        GWO_TRY(hipcheck(hipMemcpyAsync(nt.ptr, side_ts.ptr, side_rows_committed * 8, hipMemcpyDeviceToDevice, stream), "s"));
+        GWO_TRY(hipcheck(hipMemcpyAsync(nv.ptr, side_val.ptr, side_rows_committed * 8, hipMemcpyDeviceToDevice, stream), "s"));
+    }
+    GWO_TRY(hipcheck(hipStreamSynchronize(stream), "side grow"));
+    side_key.release();
+    side_ts.release();
+    side_val.release();
+    side_key = nk;
+    side_ts = nt;
+    side_val = nv;
+    nk.ptr = nt.ptr = nv.ptr = nullptr;
+    side_cap = ncap;
+    return GWO_OK;
+}
+
+// ---- watermark: tumbling windows ---------------------------------------------------------------
+gwo_status Handle::fire_tumbling(int64_t new_wm) {
+    // timers in timestamp order; each window has its maxTs (fire) and cleanup timers
+    std::vector<long long> emit, clear;
+    for (auto &kv : tables) {
+        int64_t start = unit_start(kv.first);
+        int64_t end = (int64_t)((uint64_t)start + (uint64_t)cfg.size);
+        int64_t max_ts = (int64_t)((uint64_t)end - 1);
+        int64_t cu = cleanup_time_host(max_ts);
+        bool do_emit = !kv.second.fired && max_ts <= new_wm;
+        bool do_clear = cu <= new_wm;
+        if (do_emit) emit.push_back(kv.first);
+        if (do_clear) clear.push_back(kv.first);
+    }
+    if (emit.empty() && clear.empty()) return GWO_OK;
+    GWO_TRY(read_occupancy());
+    uint64_t extra = 0;
+    for (long long u : emit) extra += tables[u].occ;
+    GWO_TRY(ensure_output(extra));
+    OutCols o = out;
+    o.count = d_out_count;
+    for (long long u : emit) {
+        Table &t = tables[u];
+        bool also_clear = std::find(clear.begin(), clear.end(), u) != clear.end();
+        int64_t start = unit_start(u);
+        int64_t end = (int64_t)((uint64_t)start + (uint64_t)cfg.size);
+        prof_begin(GWO_KERNEL_FIRE);
+        launch_fire(desc(t), t.cap, plan, rplan, start, end, o, also_clear ? 1 : 0, stream);
+        prof_end(GWO_KERNEL_FIRE, (int64_t)t.cap);
+        out_rows += t.occ;
+        t.fired = true;
+    }
+    for (long long u : clear) {
+        Table &t = tables[u];
+        if (std::find(emit.begin(), emit.end(), u) == emit.end()) {
+            // state cleared without emission (already fired at maxTs): reset by a no-output sweep
+            OutCols none = o;
+            none.cap = 0;
+            GWO_TRY(hipcheck(hipMemcpyAsync(d_scratch_count, &zero_u64, 8, hipMemcpyHostToDevice, stream), "z"));
+            none.count = d_scratch_count;
+            launch_fire(desc(t), t.cap, plan, rplan, 0, 0, none, 1, stream);
+        }
+        release_table(t);
+        tables.erase(u);
+    }
+    return GWO_OK;
+}
+
+int64_t Handle::cleanup_time_host(int64_t max_ts) const {
+    int64_t c = (int64_t)((uint64_t)max_ts + (uint64_t)cfg.allowed_lateness);
+    return c >= max_ts ? c : (int64_t)0x7fffffffffffffffLL;
+}
+
+}  // namespace gwo
+
+// ================================================================================================
+// C ABI
+// ================================================================================================
+extern "C" {
+
+void gwo_config_init(gwo_config *cfg) {
+    memset(cfg, 0, sizeof *cfg);
+    cfg->abi_version = GWO_ABI_VERSION;
+    cfg->assigner = GWO_ASSIGNER_TUMBLING;
+    cfg->num_aggs = 1;
+    cfg->aggs[0] = GWO_AGG_SUM;
+    cfg->max_parallelism = 128;
+    cfg->key_group_start = 0;
+    cfg->key_group_end = 127;
+}
+
+const char *gwo_status_string(gwo_status s) { return status_str(s); }
+
+gwo_status gwo_create(const gwo_config *cfg, gwo_handle **out) {
+    if (!cfg || !out) return GWO_ERR_INVALID_ARGUMENT;
+    *out = nullptr;
+    Handle *h = new Handle();
+    gwo_status s = h->init(*cfg);
+    if (s != GWO_OK) {
+        // keep the message reachable: hand back the half-built handle only on success
+        fprintf(stderr, "gwo_create: %s\n", h->err.c_str());
+        delete h;
+        return s;
+    }
+    *out = reinterpret_cast<gwo_handle *>(h);
+    return GWO_OK;
+}
+
+gwo_status gwo_destroy(gwo_handle *hh) {
+    if (!hh) return GWO_ERR_INVALID_ARGUMENT;
+    delete reinterpret_cast<Handle *>(hh);
+    return GWO_OK;
+}
+
+#define H_OR_FAIL                                                            \
+    Handle *h = reinterpret_cast<Handle *>(hh);                              \
+    if (!h) return GWO_ERR_INVALID_ARGUMENT;                                 \
+    if (h->poisoned) return h->poison_status;                                \
+    DeviceGuard guard_(h->cfg.device);
+
+gwo_status gwo_submit(gwo_handle *hh, const int64_t *key, const int64_t *ts, const void *value, int64_t n) {
+    H_OR_FAIL;
+    if (n < 0) return h->fail(GWO_ERR_INVALID_ARGUMENT, "negative record count");
+    if (n > 0 && (!key || !ts)) return h->fail(GWO_ERR_INVALID_ARGUMENT, "key/ts columns are required");
+    if (n > 0 && !value && h->needs_value) return h->fail(GWO_ERR_INVALID_ARGUMENT, "value column required");
+    return h->submit(key, ts, value, n);
+}
+
+gwo_status gwo_advance_watermark(gwo_handle *hh, int64_t wm) {
+    H_OR_FAIL;
+    return h->advance_watermark(wm);
+}
+
+gwo_status gwo_end_input(gwo_handle *hh) { return gwo_advance_watermark(hh, (int64_t)0x7fffffffffffffffLL); }
+
+gwo_status gwo_output_count(gwo_handle *hh, int64_t *n) {
+    H_OR_FAIL;
+    if (!n) return GWO_ERR_INVALID_ARGUMENT;
+    *n = (int64_t)h->out_rows;
+    return GWO_OK;
+}
+
+gwo_status gwo_output_view(gwo_handle *hh, gwo_out *cols, int64_t *n) {
+    H_OR_FAIL;
+    if (!cols || !n) return GWO_ERR_INVALID_ARGUMENT;
+    GWO_TRY(h->hipcheck(hipStreamSynchronize(h->stream), "view"));
+    cols->key = h->out.key;
+    cols->start = h->out.start;
+    cols->end = h->out.end;
+    for (int a = 0; a < GWO_MAX_AGGS; ++a) cols->result[a] = h->out.res[a];
+    *n = (int64_t)h->out_rows;
+    return GWO_OK;
+}
+
+gwo_status gwo_discard_output(gwo_handle *hh) {
+    H_OR_FAIL;
+    h->out_rows = 0;
+    return h->hipcheck(hipMemcpyAsync(h->d_out_count, &h->zero_u64, 8, hipMemcpyHostToDevice, h->stream), "discard");
+}
+
+gwo_status gwo_drain(gwo_handle *hh, const gwo_out *cols, int64_t cap, int64_t *n_out) {
+    H_OR_FAIL;
+    if (!cols || !n_out || cap < 0) return GWO_ERR_INVALID_ARGUMENT;
+    return h->drain(cols, cap, n_out);
+}
+
+gwo_status gwo_result_dtype(const gwo_handle *hh, int32_t agg, int32_t *dtype) {
+    const Handle *h = reinterpret_cast<const Handle *>(hh);
+    if (!h || !dtype || agg < 0 || agg >= h->rplan.naggs) return GWO_ERR_INVALID_ARGUMENT;
+    int k = h->rplan.kind[agg];
+    *dtype = (k == GWO_AGG_AVG || (k != GWO_AGG_COUNT && h->rplan.value_is_f64)) ? GWO_DTYPE_FLOAT64 : GWO_DTYPE_INT64;
+    return GWO_OK;
+}
+
+gwo_status gwo_late_dropped(gwo_handle *hh, int64_t *count) {
+    H_OR_FAIL;
+    if (!count) return GWO_ERR_INVALID_ARGUMENT;
+    *count = (int64_t)h->late_dropped;
+    return GWO_OK;
+}
+
+gwo_status gwo_side_output_count(gwo_handle *hh, int64_t *n) {
+    H_OR_FAIL;
+    if (!n) return GWO_ERR_INVALID_ARGUMENT;
+    *n = (int64_t)h->side_rows_committed;
+    return GWO_OK;
+}
+
+gwo_status gwo_drain_side_output(gwo_handle *hh, const gwo_side_out *cols, int64_t cap, int64_t *n_out) {
+    H_OR_FAIL;
+    if (!cols || !n_out || cap < 0) return GWO_ERR_INVALID_ARGUMENT;
+    return h->drain_side(cols, cap, n_out);
+}
+
+gwo_status gwo_current_watermark(gwo_handle *hh, int64_t *wm) {
+    H_OR_FAIL;
+    if (!wm) return GWO_ERR_INVALID_ARGUMENT;
+    *wm = h->wm;
+    return GWO_OK;
+}
+
+gwo_status gwo_state_size(gwo_handle *hh, int64_t *entries) {
+    H_OR_FAIL;
+    if (!entries) return GWO_ERR_INVALID_ARGUMENT;
+    return h->state_size(entries);
+}
+
+gwo_status gwo_sync(gwo_handle *hh) {
+    H_OR_FAIL;
+    return h->hipcheck(hipStreamSynchronize(h->stream), "sync");
+}
+
+gwo_status gwo_get_stream(gwo_handle *hh, void **stream) {
+    Handle *h = reinterpret_cast<Handle *>(hh);
+    if (!h || !stream) return GWO_ERR_INVALID_ARGUMENT;
+    *stream = (void *)h->stream;
+    return GWO_OK;
+}
+
+const char *gwo_last_error(const gwo_handle *hh) {
+    const Handle *h = reinterpret_cast<const Handle *>(hh);
+    return h ? h->err.c_str() : "null handle";
+}
+
+gwo_status gwo_set_profiling(gwo_handle *hh, int32_t enabled) {
+    Handle *h = reinterpret_cast<Handle *>(hh);
+    if (!h) return GWO_ERR_INVALID_ARGUMENT;
+    h->profiling = enabled != 0;
+    return GWO_OK;
+}
+
+gwo_status gwo_kernel_stats(gwo_handle *hh, int32_t kernel, int64_t *launches, double *total_ms, int64_t *items) {
+    Handle *h = reinterpret_cast<Handle *>(hh);
+    if (!h || kernel < 0 || kernel >= GWO_KERNEL_COUNT_) return GWO_ERR_INVALID_ARGUMENT;
+    DeviceGuard guard_(h->cfg.device);
+    GWO_TRY(h->prof_collect());
+    if (launches) *launches = h->kstats[kernel].launches;
+    if (total_ms) *total_ms = h->kstats[kernel].ms;
+    if (items) *items = h->kstats[kernel].items;
+    return GWO_OK;
+}
+
+gwo_status gwo_reset_stats(gwo_handle *hh) {
+    Handle *h = reinterpret_cast<Handle *>(hh);
+    if (!h) return GWO_ERR_INVALID_ARGUMENT;
+    DeviceGuard guard_(h->cfg.device);
+    GWO_TRY(h->prof_collect());
+    for (auto &k : h->kstats) k = KStat{};
+    return GWO_OK;
+}
+
+// ---- stateless helpers --------------------------------------------------------------------------
+static gwo_status stateless_run(int32_t device, size_t n, const void *in, size_t out_words, void **outs, int nouts,
+                                void (*body)(const int64_t *, void **, hipStream_t, void *), void *ctx) {
+    DeviceGuard guard_(device);
+    hipStream_t s;
+    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return GWO_ERR_HIP;
+    gwo_status st = GWO_OK;
+    const int64_t *din = (const int64_t *)in;
+    void *tmp_in = nullptr;
+    void *tmp_out[2] = {nullptr, nullptr};
+    void *douts[2] = {nullptr, nullptr};
+    if (!is_device_ptr(in)) {
+        if (hipMalloc(&tmp_in, n * 8 + 8) != hipSuccess) st = GWO_ERR_OUT_OF_MEMORY;
+        else (void)hipMemcpyAsync(tmp_in, in, n * 8, hipMemcpyHostToDevice, s);
+        din = (const int64_t *)tmp_in;
+    }
+    for (int i = 0; i < nouts && st == GWO_OK; ++i) {
+        if (!outs[i]) continue;
+        if (is_device_ptr(outs[i])) {
+            douts[i] = outs[i];
+        } else {
+            if (hipMalloc(&tmp_out[i], n * out_words + 8) != hipSuccess) st = GWO_ERR_OUT_OF_MEMORY;
+            douts[i] = tmp_out[i];
+        }
+    }
+    if (st == GWO_OK) {
+        body(din, douts, s, ctx);
+        for (int i = 0; i < nouts; ++i)
+            if (tmp_out[i]) (void)hipMemcpyAsync(outs[i], tmp_out[i], n * out_words, hipMemcpyDeviceToHost, s);
+        if (hipStreamSynchronize(s) != hipSuccess) st = GWO_ERR_HIP;
+    }
+    if (tmp_in) (void)hipFree(tmp_in);
+    for (int i = 0; i < 2; ++i)
+        if (tmp_out[i]) (void)hipFree(tmp_out[i]);
+    (void)hipStreamDestroy(s);
+    return st;
+}
+
+struct KgCtx {
+    int64_t n;
+    int32_t kind, maxp, par;
+};
+static void kg_body(const int64_t *in, void **outs, hipStream_t s, void *c) {
+    KgCtx *k = (KgCtx *)c;
+    launch_key_groups(in, k->n, k->kind, k->maxp, k->par, (int32_t *)outs[0], (int32_t *)outs[1], s);
+}
+
+gwo_status gwo_assign_key_groups(const int64_t *keys, int64_t n, int32_t key_kind, int32_t max_parallelism,
+                                 int32_t parallelism, int32_t *kg_out, int32_t *op_out, int32_t device) {
+    if (n < 0 || !keys || max_parallelism <= 0 || max_parallelism > 32768 || parallelism <= 0 ||
+        parallelism > max_parallelism)
+        return GWO_ERR_INVALID_ARGUMENT;
+    if (n == 0) return GWO_OK;
+    KgCtx c{n, key_kind, max_parallelism, parallelism};
+    void *outs[2] = {kg_out, op_out};
+    return stateless_run(device, (size_t)n, keys, 4, outs, 2, kg_body, &c);
+}
+
+struct WsCtx {
+    int64_t n, off, size;
+};
+static void ws_body(const int64_t *in, void **outs, hipStream_t s, void *c) {
+    WsCtx *w = (WsCtx *)c;
+    launch_window_starts(in, w->n, w->off, w->size, (int64_t *)outs[0], s);
+}
+
+gwo_status gwo_window_starts(const int64_t *ts, int64_t n, int64_t offset, int64_t size, int64_t *start_out,
+                             int32_t device) {
+    if (n < 0 || !ts || !start_out || size <= 0) return GWO_ERR_INVALID_ARGUMENT;
+    if (n == 0) return GWO_OK;
+    WsCtx c{n, offset, size};
+    void *outs[2] = {start_out, nullptr};
+    return stateless_run(device, (size_t)n, ts, 8, outs, 1, ws_body, &c);
+}
+
+gwo_status gwo_generate(const gwo_gen_spec *sp, int64_t n, int64_t *key, int64_t *ts, void *value, void *stream,
+                        int32_t device) {
+    if (!sp || n < 0 || !key || !ts || sp->num_keys <= 0 || sp->total_records <= 0 || sp->span_ms < 0 ||
+        sp->disorder_ms < 0 || (value && sp->value_range <= 0))
+        return GWO_ERR_INVALID_ARGUMENT;
+    if (n == 0) return GWO_OK;
+    if (!is_device_ptr(key) || !is_device_ptr(ts) || (value && !is_device_ptr(value))) return GWO_ERR_INVALID_ARGUMENT;
+    DeviceGuard guard_(device);
+    launch_generate(sp->seed, sp->first_index, sp->total_records, sp->num_keys, sp->span_ms, sp->disorder_ms, sp->t0,
+                    sp->value_range, sp->value_dtype == GWO_DTYPE_FLOAT64, sp->key_mode, n, key, ts, value,
+                    (hipStream_t)stream);
+    if (!stream && hipDeviceSynchronize() != hipSuccess) return GWO_ERR_HIP;
+    return hipGetLastError() == hipSuccess ? GWO_OK : GWO_ERR_HIP;
+}
+
+}  // extern "C"

@@ -1,0 +1,209 @@
+"""``GpuWindowOperator`` -- the host-side mirror of the Java drop-in operator.
+
+Mirrors the interface the task runtime drives (``OneInputStreamOperator``, ``BoundedOneInput``;
+SJ/api/operators/OneInputStreamOperator.java:35-51, BoundedOneInput.java:26-31) and the window
+operator's observable behaviour (WindowOperator.java:294-653): ``process_element`` buffers into
+columnar batches (the mailbox batching the Java operator does), and every ``process_watermark``
+first flushes the pending batch, then fires -- results are emitted before the watermark is
+forwarded (AbstractStreamOperator.java:566-571).  All state lives in HBM behind libgwo.so.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _native as N
+from .windowing import AggregateFunction, WindowAssigner
+
+LONG_MIN = -(1 << 63)
+LONG_MAX = (1 << 63) - 1
+
+
+def _ptr(a):
+    return a.ctypes.data_as(C.c_void_p) if a is not None else None
+
+
+class GpuWindowOperator:
+    """One subtask of ``keyBy(...).window(assigner).aggregate(fn)`` on one MI355X."""
+
+    def __init__(self, assigner: WindowAssigner, aggregate: AggregateFunction, allowed_lateness: int = 0,
+                 side_output_late_data: bool = False, max_parallelism: int = 128, key_group_range=None,
+                 key_kind: str = "long", device: int = 0, batch_size: int = 1 << 20, expected_keys: int = 0,
+                 stream=None):
+        if allowed_lateness < 0:
+            raise ValueError("The allowed lateness cannot be negative.")
+        self._lib = N.lib()
+        cfg = N.GwoConfig()
+        self._lib.gwo_config_init(C.byref(cfg))
+        cfg.assigner = assigner.kind
+        cfg.size = getattr(assigner, "size", 0)
+        cfg.slide = getattr(assigner, "slide", 0)
+        cfg.offset = getattr(assigner, "offset", 0)
+        cfg.gap = getattr(assigner, "gap", 0)
+        cfg.allowed_lateness = allowed_lateness
+        kinds, vdt = aggregate.descriptor
+        cfg.num_aggs = len(kinds)
+        for i, k in enumerate(kinds):
+            cfg.aggs[i] = k
+        cfg.value_dtype = vdt
+        cfg.key_kind = N.KEY_INT if key_kind == "int" else N.KEY_LONG
+        cfg.max_parallelism = max_parallelism
+        lo, hi = key_group_range if key_group_range is not None else (0, max_parallelism - 1)
+        cfg.key_group_start, cfg.key_group_end = lo, hi
+        cfg.device = device
+        cfg.side_output = 1 if side_output_late_data else 0
+        cfg.expected_keys = expected_keys
+        cfg.stream = stream
+        h = C.c_void_p()
+        st = self._lib.gwo_create(C.byref(cfg), C.byref(h))
+        N.check(st, None, "gwo_create")
+        self._h = h
+        self.cfg = cfg
+        self.assigner = assigner
+        self.aggregate = aggregate
+        self.value_dtype = np.float64 if vdt == N.DTYPE_FLOAT64 else np.int64
+        self.batch_size = batch_size
+        self._pk, self._pt, self._pv = [], [], []
+        self.output: list[tuple] = []
+        self.side_output: list[tuple] = []
+        self._result_dtypes = []
+        for i in range(len(kinds)):
+            d = C.c_int32()
+            N.check(self._lib.gwo_result_dtype(h, i, C.byref(d)), h)
+            self._result_dtypes.append(np.float64 if d.value == N.DTYPE_FLOAT64 else np.int64)
+
+    # -- lifecycle ---------------------------------------------------------------------------
+    def open(self):
+        return self
+
+    def close(self):
+        if self._h:
+            self._lib.gwo_destroy(self._h)
+            self._h = None
+
+    dispose = close
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # -- OneInputStreamOperator --------------------------------------------------------------
+    def process_element(self, key: int, timestamp: int, value=0):
+        self._pk.append(key)
+        self._pt.append(timestamp)
+        self._pv.append(value)
+        if len(self._pk) >= self.batch_size:
+            self.flush()
+
+    def process_batch(self, keys, timestamps, values=None):
+        """Columnar batch in arrival order (numpy arrays; host memory)."""
+        self.flush()
+        k = np.ascontiguousarray(keys, dtype=np.int64)
+        t = np.ascontiguousarray(timestamps, dtype=np.int64)
+        v = None if values is None else np.ascontiguousarray(values, dtype=self.value_dtype)
+        self._submit(k, t, v)
+
+    def process_device_batch(self, key_ptr: int, ts_ptr: int, val_ptr, n: int):
+        """Columnar batch already resident in HBM (device pointers)."""
+        self.flush()
+        st = self._lib.gwo_submit(self._h, C.c_void_p(key_ptr), C.c_void_p(ts_ptr),
+                                  C.c_void_p(val_ptr) if val_ptr else None, n)
+        N.check(st, self._h, "gwo_submit")
+
+    def _submit(self, k, t, v):
+        if len(k) == 0:
+            return
+        st = self._lib.gwo_submit(self._h, _ptr(k), _ptr(t), _ptr(v), len(k))
+        N.check(st, self._h, "gwo_submit")
+
+    def flush(self):
+        if not self._pk:
+            return
+        k = np.array(self._pk, dtype=np.int64)
+        t = np.array(self._pt, dtype=np.int64)
+        v = np.array(self._pv, dtype=self.value_dtype)
+        self._pk, self._pt, self._pv = [], [], []
+        self._submit(k, t, v)
+
+    def process_watermark(self, watermark: int):
+        self.flush()
+        N.check(self._lib.gwo_advance_watermark(self._h, int(watermark)), self._h, "gwo_advance_watermark")
+        self._collect()
+
+    def prepare_snapshot_pre_barrier(self, checkpoint_id: int = 0):
+        self.flush()
+
+    def end_input(self):
+        """BoundedOneInput.endInput: the source's final Long.MAX_VALUE watermark."""
+        self.process_watermark(LONG_MAX)
+
+    # -- results -----------------------------------------------------------------------------
+    def _collect(self):
+        n = C.c_int64()
+        N.check(self._lib.gwo_output_count(self._h, C.byref(n)), self._h)
+        if n.value:
+            cols = self.drain_arrays()
+            keys, starts, ends, res = cols
+            for i in range(len(keys)):
+                r = tuple(x[i].item() for x in res)
+                self.output.append((int(keys[i]), int(starts[i]), int(ends[i]), r[0] if len(r) == 1 else r))
+        sn = C.c_int64()
+        N.check(self._lib.gwo_side_output_count(self._h, C.byref(sn)), self._h)
+        if sn.value:
+            m = sn.value
+            k = np.empty(m, np.int64)
+            t = np.empty(m, np.int64)
+            v = np.empty(m, self.value_dtype)
+            so = N.GwoSideOut(_ptr(k).value, _ptr(t).value, _ptr(v).value)
+            got = C.c_int64()
+            N.check(self._lib.gwo_drain_side_output(self._h, C.byref(so), m, C.byref(got)), self._h)
+            for i in range(got.value):
+                self.side_output.append((int(k[i]), int(t[i]), v[i].item()))
+
+    def drain_arrays(self):
+        """Drain pending fired rows into numpy columns: (key, start, end, [results...])."""
+        n = C.c_int64()
+        N.check(self._lib.gwo_output_count(self._h, C.byref(n)), self._h)
+        m = n.value
+        key = np.empty(m, np.int64)
+        start = np.empty(m, np.int64)
+        end = np.empty(m, np.int64)
+        res = [np.empty(m, dt) for dt in self._result_dtypes]
+        o = N.GwoOut()
+        o.key, o.start, o.end = _ptr(key).value, _ptr(start).value, _ptr(end).value
+        for i, r in enumerate(res):
+            o.result[i] = _ptr(r).value
+        got = C.c_int64()
+        if m:
+            N.check(self._lib.gwo_drain(self._h, C.byref(o), m, C.byref(got)), self._h, "gwo_drain")
+        return key, start, end, res
+
+    @property
+    def num_late_records_dropped(self) -> int:
+        n = C.c_int64()
+        N.check(self._lib.gwo_late_dropped(self._h, C.byref(n)), self._h)
+        return n.value
+
+    @property
+    def current_watermark(self) -> int:
+        n = C.c_int64()
+        N.check(self._lib.gwo_current_watermark(self._h, C.byref(n)), self._h)
+        return n.value
+
+    def state_size(self) -> int:
+        n = C.c_int64()
+        N.check(self._lib.gwo_state_size(self._h, C.byref(n)), self._h)
+        return n.value
+
+    @property
+    def handle(self):
+        return self._h

@@ -1,0 +1,212 @@
+/*
+ * gwo.h -- C ABI of the MI355X-native keyed event-time window operator ("GPU window operator").
+ *
+ * This is the drop-in boundary for Flink's `keyBy().window(WindowAssigner).aggregate(...)` path.
+ * A Java `GpuWindowOperator` binds these entry points through a thin JNI
+ * shim; the C++ and Python harnesses in this repository bind them directly.  No torch or HIP
+ * types appear in any signature: plain pointers, sizes and integer status codes.
+ *
+ * Reference interfaces each entry point replaces (paths relative to the Flink source tree,
+ * SJ/ = flink-streaming-java/src/main/java/org/apache/flink/streaming/):
+ *
+ *   gwo_create            WindowOperator ctor + open()          SJ/runtime/operators/windowing/WindowOperator.java:182-273
+ *                         (assigner/trigger/lateness/state descriptor built by WindowedStream.aggregate,
+ *                          SJ/api/datastream/WindowedStream.java:792-850)
+ *   gwo_submit            OneInputStreamOperator.processElement, batched
+ *                                                               SJ/api/operators/OneInputStreamOperator.java:35-41,
+ *                                                               WindowOperator.java:294-427 (via OneInputStreamTask.java:158-162)
+ *   gwo_advance_watermark OneInputStreamOperator.processWatermark -> InternalTimerServiceImpl.advanceWatermark
+ *                                                               SJ/api/operators/AbstractStreamOperator.java:566-571,
+ *                                                               InternalTimerServiceImpl.java:268-278, WindowOperator.java:430-473
+ *   gwo_drain             TimestampedCollector.collect of emitted window results
+ *                                                               SJ/api/operators/TimestampedCollector.java:52-64,
+ *                                                               WindowOperator.java:546-550
+ *   gwo_late_dropped      metric numLateRecordsDropped          WindowOperator.java:141,221,424
+ *   gwo_drain_side_output late-data side output (sideOutputLateData)   WindowOperator.java:420-423,560-562
+ *   gwo_destroy           StreamOperator.close/dispose          SJ/api/operators/StreamOperator.java:96-110
+ *   gwo_assign_key_groups KeyGroupRangeAssignment.assignToKeyGroup / computeOperatorIndexForKeyGroup
+ *                                                               flink-runtime/.../state/KeyGroupRangeAssignment.java:48-73,118-119
+ *   gwo_comm_*            keyBy shuffle (KeyGroupStreamPartitioner + network stack) across the GPUs of a node
+ *                                                               SJ/runtime/partitioner/KeyGroupStreamPartitioner.java:51-58
+ *
+ * Error convention: every call returns a gwo_status; nothing is thrown across the ABI.  A failing
+ * gwo_submit rejects the WHOLE batch before any state changes (Flink would have failed the task at
+ * the first offending record).  gwo_last_error() gives a message for the last failure on a handle.
+ *
+ * Threading: one handle = one operator subtask = one thread at a time (Flink's mailbox model,
+ * SJ/runtime/tasks/mailbox/TaskMailboxImpl.java:98-110).  Distinct handles may be driven
+ * concurrently from different threads.
+ *
+ * Buffers: input columns may be host or device pointers (detected per call).  Device input is
+ * borrowed until the next call on the handle returns; host input is copied before gwo_submit
+ * returns.  Output columns given to gwo_drain may be host or device pointers.
+ */
+#ifndef GWO_H
+#define GWO_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GWO_ABI_VERSION 1
+#define GWO_MAX_AGGS 4
+
+typedef enum {
+    GWO_OK = 0,
+    GWO_ERR_INVALID_ARGUMENT = 1, /* bad config (mirrors the assigners' IllegalArgumentException) */
+    GWO_ERR_NO_TIMESTAMP = 2,     /* a record carries Long.MIN_VALUE (TumblingEventTimeWindows.java:76-79) */
+    GWO_ERR_KEY_GROUP = 3,        /* key outside this subtask's KeyGroupRange (HeapKeyedStateBackend) */
+    GWO_ERR_OUT_OF_MEMORY = 4,
+    GWO_ERR_HIP = 5,              /* HIP runtime failure */
+    GWO_ERR_UNSUPPORTED = 6,      /* configuration outside the GPU-describable subset: rejected, never faked */
+    GWO_ERR_MERGE_LATE = 7,       /* UnsupportedOperationException of WindowOperator.java:318-323 */
+    GWO_ERR_COMM = 8,             /* RCCL failure */
+    GWO_ERR_STATE = 9,            /* call out of order (e.g. submit after destroy) */
+    GWO_ERR_CAPACITY = 10         /* caller buffer too small */
+} gwo_status;
+
+typedef enum {
+    GWO_ASSIGNER_TUMBLING = 0,    /* TumblingEventTimeWindows.of(size, offset), stagger ALIGNED */
+    GWO_ASSIGNER_SLIDING = 1,     /* SlidingEventTimeWindows.of(size, slide, offset) */
+    GWO_ASSIGNER_SESSION = 2      /* EventTimeSessionWindows.withGap(gap) */
+} gwo_assigner_kind;
+
+typedef enum {
+    GWO_AGG_COUNT = 0,            /* result int64 */
+    GWO_AGG_SUM = 1,              /* int64 (Java wrap-around) or float64, per value_dtype */
+    GWO_AGG_MIN = 2,              /* Comparable min (Double.compareTo order for float64) */
+    GWO_AGG_MAX = 3,
+    GWO_AGG_AVG = 4               /* (sum, count) accumulator, result float64 = (double)sum / count */
+} gwo_agg_kind;
+
+typedef enum { GWO_DTYPE_INT64 = 0, GWO_DTYPE_FLOAT64 = 1 } gwo_dtype;
+
+typedef enum {
+    GWO_KEY_LONG = 0,             /* key.hashCode() = Long.hashCode: (int)(v ^ (v >>> 32)) */
+    GWO_KEY_INT = 1               /* key.hashCode() = Integer.hashCode: (int)v; key must fit in int32 */
+} gwo_key_kind;
+
+typedef struct {
+    int32_t abi_version;          /* must be GWO_ABI_VERSION */
+    int32_t assigner;             /* gwo_assigner_kind */
+    int64_t size;                 /* tumbling/sliding window size, ms */
+    int64_t slide;                /* sliding slide, ms */
+    int64_t offset;               /* tumbling/sliding offset, ms */
+    int64_t gap;                  /* session gap, ms */
+    int64_t allowed_lateness;     /* WindowedStream.allowedLateness, ms (>= 0) */
+    int32_t num_aggs;             /* 1..GWO_MAX_AGGS aggregates over the same value column */
+    int32_t aggs[GWO_MAX_AGGS];   /* gwo_agg_kind */
+    int32_t value_dtype;          /* gwo_dtype of the value column */
+    int32_t key_kind;             /* gwo_key_kind */
+    int32_t max_parallelism;      /* number of key groups (1 .. 32768) */
+    int32_t key_group_start;      /* inclusive KeyGroupRange owned by this subtask */
+    int32_t key_group_end;
+    int32_t device;               /* HIP device ordinal */
+    int32_t side_output;          /* 1: late records go to the side output instead of being counted */
+    int64_t expected_keys;        /* sizing hint: distinct keys per window (0 = grow on demand) */
+    void *stream;                 /* hipStream_t to run on; NULL: the handle creates its own */
+} gwo_config;
+
+typedef struct gwo_handle gwo_handle;
+
+/* Output rows: one per fired (key, window); result[i] is int64 or float64 per gwo_result_dtype. */
+typedef struct {
+    int64_t *key;
+    int64_t *start;
+    int64_t *end;
+    void *result[GWO_MAX_AGGS];
+} gwo_out;
+
+/* Late records routed to the side output (WindowOperator.sideOutput). */
+typedef struct {
+    int64_t *key;
+    int64_t *ts;
+    void *value;
+} gwo_side_out;
+
+void gwo_config_init(gwo_config *cfg);
+gwo_status gwo_create(const gwo_config *cfg, gwo_handle **out);
+gwo_status gwo_destroy(gwo_handle *h);
+
+/* processElement for n records in arrival order; value may be NULL when every aggregate is COUNT. */
+gwo_status gwo_submit(gwo_handle *h, const int64_t *key, const int64_t *ts, const void *value, int64_t n);
+/* processWatermark: fire every window whose timers are <= wm, then adopt wm as current watermark. */
+gwo_status gwo_advance_watermark(gwo_handle *h, int64_t wm);
+/* processWatermark(Long.MAX_VALUE) -- a bounded source's end (StreamSource.java:122). */
+gwo_status gwo_end_input(gwo_handle *h);
+
+gwo_status gwo_output_count(gwo_handle *h, int64_t *n);
+/* Copies up to cap rows into cols (host or device buffers) and removes them from the handle. */
+gwo_status gwo_drain(gwo_handle *h, const gwo_out *cols, int64_t cap, int64_t *n_out);
+/* Library-owned device columns of the pending output (valid until the next call); n_out rows. */
+gwo_status gwo_output_view(gwo_handle *h, gwo_out *cols, int64_t *n_out);
+gwo_status gwo_discard_output(gwo_handle *h);
+gwo_status gwo_result_dtype(const gwo_handle *h, int32_t agg_index, int32_t *dtype);
+
+gwo_status gwo_late_dropped(gwo_handle *h, int64_t *count);
+gwo_status gwo_side_output_count(gwo_handle *h, int64_t *n);
+gwo_status gwo_drain_side_output(gwo_handle *h, const gwo_side_out *cols, int64_t cap, int64_t *n_out);
+gwo_status gwo_current_watermark(gwo_handle *h, int64_t *wm);
+/* Number of (key, window) entries currently held (device-resident state). */
+gwo_status gwo_state_size(gwo_handle *h, int64_t *entries);
+
+gwo_status gwo_sync(gwo_handle *h);
+gwo_status gwo_get_stream(gwo_handle *h, void **stream);
+const char *gwo_last_error(const gwo_handle *h);
+const char *gwo_status_string(gwo_status s);
+
+/* Per-kernel HIP-event timing, for bench.py's roofline (off by default). */
+typedef enum {
+    GWO_KERNEL_SCAN = 0,          /* batch pre-pass: window range, lateness, key-group checks */
+    GWO_KERNEL_INSERT = 1,        /* insert into the per-window HBM hash tables */
+    GWO_KERNEL_FIRE = 2,          /* watermark fire: compact, emit, reset */
+    GWO_KERNEL_PARTITION = 3,     /* multi-GPU: destination partition */
+    GWO_KERNEL_EXCHANGE = 4,      /* multi-GPU: RCCL all-to-all */
+    GWO_KERNEL_SLIDE = 5,         /* sliding: pane fold/expire */
+    GWO_KERNEL_SESSION = 6,       /* sessions: per-key merge */
+    GWO_KERNEL_COUNT_ = 7
+} gwo_kernel_id;
+gwo_status gwo_set_profiling(gwo_handle *h, int32_t enabled);
+gwo_status gwo_kernel_stats(gwo_handle *h, int32_t kernel, int64_t *launches, double *total_ms,
+                            int64_t *items);
+gwo_status gwo_reset_stats(gwo_handle *h);
+
+/* Bit-exact KeyGroupRangeAssignment over a key column (host or device pointers; outputs may be NULL). */
+gwo_status gwo_assign_key_groups(const int64_t *keys, int64_t n, int32_t key_kind, int32_t max_parallelism,
+                                 int32_t parallelism, int32_t *key_group_out, int32_t *operator_out,
+                                 int32_t device);
+/* TimeWindow.getWindowStartWithOffset over a timestamp column (Java '%' semantics). */
+gwo_status gwo_window_starts(const int64_t *ts, int64_t n, int64_t offset, int64_t size, int64_t *start_out,
+                             int32_t device);
+
+/* ---- multi-GPU keyBy shuffle over RCCL (one process per GPU) ---------------------------------- */
+#define GWO_COMM_ID_BYTES 128
+gwo_status gwo_comm_unique_id(uint8_t id[GWO_COMM_ID_BYTES]);
+/* Collective: every rank calls it with the same id. The handle's key-group range must be
+ * computeKeyGroupRangeForOperatorIndex(max_parallelism, nranks, rank). Afterwards gwo_submit and
+ * gwo_advance_watermark are collective: gwo_submit routes records to their owner GPU
+ * (partition + ncclSend/ncclRecv all-to-all); the watermark becomes the min over ranks. */
+gwo_status gwo_comm_init(gwo_handle *h, const uint8_t id[GWO_COMM_ID_BYTES], int32_t nranks, int32_t rank);
+
+/* ---- synthetic sources (device-resident benchmark/parity inputs; splitmix64) ---- */
+typedef struct {
+    uint64_t seed;
+    int64_t first_index;          /* global record index of row 0 */
+    int64_t total_records;        /* N of the whole stream (time spacing = span_ms / N) */
+    int64_t num_keys;
+    int64_t span_ms;              /* event-time span of the whole stream */
+    int64_t disorder_ms;          /* ts = t0 + i*span/N + U[0, disorder) */
+    int64_t t0;
+    int64_t value_range;          /* value = U[0, value_range) */
+    int32_t value_dtype;
+    int32_t key_mode;             /* 0: uniform keys; 1: YSB ad_id -> campaign (ad % num_keys) */
+} gwo_gen_spec;
+gwo_status gwo_generate(const gwo_gen_spec *spec, int64_t n, int64_t *key, int64_t *ts, void *value,
+                        void *stream, int32_t device);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GWO_H */

@@ -1,0 +1,276 @@
+"""GPU parity: libgwo.so's HIP kernels against the oracle (bit-exact for integers, 1e-6 relative
+for float64 sums/averages -- the tolerance BASELINE.json's north_star states)."""
+import numpy as np
+import pytest
+
+from oracle import flink_oracle as O
+from oracle import gen as G
+from oracle import vectorized as V
+
+pytestmark = pytest.mark.gpu
+
+LONG_MIN, LONG_MAX = -(1 << 63), (1 << 63) - 1
+FLOAT_RTOL = 1e-6
+
+
+@pytest.fixture(scope="module")
+def F():
+    import flink_amd
+    from flink_amd import _native
+    _native.lib()
+    return flink_amd
+
+
+def mk(F, a):
+    if a["kind"] == "tumbling":
+        return F.TumblingEventTimeWindows.of(a["size"], a["offset"])
+    if a["kind"] == "sliding":
+        return F.SlidingEventTimeWindows.of(a["size"], a["slide"], a["offset"])
+    return F.EventTimeSessionWindows.withGap(a["gap"])
+
+
+# ---- stateless kernels ---------------------------------------------------------------------------
+def test_key_group_kernel_bit_exact(F):
+    rng = np.random.default_rng(0)
+    keys = np.concatenate([np.arange(-1000, 1000), rng.integers(LONG_MIN, LONG_MAX, 20000, dtype=np.int64),
+                           np.array([LONG_MIN, LONG_MAX, 0, -1, 1 << 32, (1 << 32) - 1], dtype=np.int64)])
+    for maxp, par in [(128, 1), (32768, 8), (10, 3), (1000, 7)]:
+        kg, op = F.assign_key_groups(keys, maxp, par)
+        want = np.array([O.assign_to_key_group(O.long_hash_code(int(k)), maxp) for k in keys])
+        assert (kg == want).all()
+        assert (op == want * par // maxp).all()
+    kg, _ = F.assign_key_groups(np.arange(10), 128)
+    assert kg.tolist() == [94, 86, 127, 113, 7, 126, 18, 113, 15, 51]
+
+
+def test_key_group_kernel_int_keys(F):
+    keys = np.arange(-5000, 5000)
+    kg, _ = F.assign_key_groups(keys, 128, 1, key_kind="int")
+    want = [O.assign_to_key_group(O.int_hash_code(int(k)), 128) for k in keys]
+    assert kg.tolist() == want
+
+
+def test_window_start_kernel(F, golden):
+    cases = golden["window_start_with_offset"]["cases"]
+    for ts, off, size, start in cases:
+        assert F.window_starts(np.array([ts]), off, size)[0] == start
+    rng = np.random.default_rng(1)
+    ts = np.concatenate([rng.integers(-10**12, 10**12, 5000), np.arange(-50, 50)])
+    for off, size in [(0, 7), (3, 7), (-2, 7), (0, 5000), (-100, 5000)]:
+        got = F.window_starts(ts, off, size)
+        want = [O.get_window_start_with_offset(int(t), off, size) for t in ts]
+        assert got.tolist() == want
+
+
+def test_generator_kernel_matches_numpy(F):
+    import ctypes as C
+    import torch
+    from flink_amd import _native as N
+    spec = G.GenSpec(seed=7, first_index=123, total_records=10**6, num_keys=5000, span_ms=60000,
+                     disorder_ms=1000, value_range=1000)
+    n = 100_000
+    for vdt in ("int64", "float64"):
+        spec.value_dtype = vdt
+        k = torch.empty(n, dtype=torch.int64, device="cuda")
+        t = torch.empty(n, dtype=torch.int64, device="cuda")
+        v = torch.empty(n, dtype=torch.int64, device="cuda")
+        gs = N.GwoGenSpec(spec.seed, spec.first_index, spec.total_records, spec.num_keys, spec.span_ms,
+                          spec.disorder_ms, spec.t0, spec.value_range,
+                          N.DTYPE_FLOAT64 if vdt == "float64" else N.DTYPE_INT64, 0)
+        N.check(N.lib().gwo_generate(C.byref(gs), n, k.data_ptr(), t.data_ptr(), v.data_ptr(), None, 0))
+        wk, wt, wv = G.generate(spec, n)
+        assert (k.cpu().numpy() == wk).all() and (t.cpu().numpy() == wt).all()
+        got_v = v.cpu().numpy().view(np.float64) if vdt == "float64" else v.cpu().numpy()
+        assert (got_v == wv).all()
+
+
+# ---- the reference's operator streams (WindowOperatorTest / examples) ----------------------------
+def _run_stream(F, s, agg=None):
+    op = F.GpuWindowOperator(mk(F, s["assigner"]), agg or F.SumAggregate(), allowed_lateness=s["lateness"],
+                             side_output_late_data=s["side_output"])
+    for ev in s["events"]:
+        if ev[0] == "e":
+            op.process_element(ev[1], ev[2], ev[3])
+        else:
+            op.process_watermark(ev[1])
+    return op
+
+
+def _golden_streams(golden, kinds):
+    return [s for s in golden["operator_streams"] if s["assigner"]["kind"] in kinds]
+
+
+@pytest.mark.parametrize("name", ["sliding_3s_1s", "tumbling_3s", "side_output_lateness_tumbling",
+                                  "side_output_lateness_sliding", "cleanup_time_overflow"])
+def test_reference_operator_streams(F, golden, name):
+    s = next(x for x in golden["operator_streams"] if x["name"] == name)
+    op = _run_stream(F, s)
+    assert sorted(op.output) == sorted(map(tuple, s["expected"]))
+    assert sorted(op.side_output) == sorted(map(tuple, s.get("side", [])))
+    assert op.num_late_records_dropped == s["late"]
+    op.close()
+
+
+# ---- randomized parity against the oracle -------------------------------------------------------
+def _c1(n=1_000_000, nkeys=10_000, every=10_000, lag=1000, vdt="int64", seed=42, disorder=1000):
+    spec = G.GenSpec(seed=seed, total_records=n, num_keys=nkeys, span_ms=60000, disorder_ms=disorder,
+                     value_range=1000, value_dtype=vdt)
+    k, t, v = G.generate(spec, n)
+    return k, t, v, G.punctuated_watermarks(t, every, lag)
+
+
+def _run_batches(op, k, t, v, batches):
+    prev = 0
+    for end, wm in batches:
+        op.process_batch(k[prev:end], t[prev:end], v[prev:end] if v is not None else None)
+        op.process_watermark(wm)
+        prev = end
+    op.end_input()
+
+
+def _rows(op):
+    return sorted(op.output)
+
+
+def _want(k, s, e, res):
+    cols = [x.tolist() for x in res]
+    return sorted(zip(k.tolist(), s.tolist(), e.tolist(), *cols)) if len(cols) > 1 else \
+        sorted(zip(k.tolist(), s.tolist(), e.tolist(), cols[0]))
+
+
+def _final(batches):
+    return batches + [(batches[-1][0], LONG_MAX)]
+
+
+def test_c1_tumbling_sum_bit_exact(F):
+    """Config 1: 1M records, 10K Long keys, 5 s tumbling sum, watermark every 10K records."""
+    k, t, v, b = _c1()
+    op = F.GpuWindowOperator(F.TumblingEventTimeWindows.of(5000), F.SumAggregate())
+    _run_batches(op, k, t, v, b)
+    (wk, ws, we, res), late = V.tumbling_lateness0(k, t, v, _final(b), 5000, 0, [1])
+    got = _rows(op)
+    assert len(got) == len(wk) > 100_000
+    assert got == _want(wk, ws, we, res)
+    assert op.num_late_records_dropped == late
+    op.close()
+
+
+@pytest.mark.parametrize("lag", [0, 200])
+def test_tumbling_multi_agg_with_late_records(F, lag):
+    """sum/min/max/count with disorder larger than the lag: late drops must match exactly."""
+    k, t, v, b = _c1(n=300_000, nkeys=50_000, every=3_000, lag=lag, disorder=1500, seed=3)
+    v = v - 500
+    op = F.GpuWindowOperator(F.TumblingEventTimeWindows.of(2000, 300),
+                             F.MultiAggregate(F.SumAggregate(), F.MinAggregate(), F.MaxAggregate(), F.CountAggregate()))
+    _run_batches(op, k, t, v, b)
+    (wk, ws, we, res), late = V.tumbling_lateness0(k, t, v, _final(b), 2000, 300, [1, 2, 3, 0])
+    assert late > 0
+    assert op.num_late_records_dropped == late
+    got = sorted((a, s, e, *r) for a, s, e, r in op.output)
+    assert got == _want(wk, ws, we, res)
+    op.close()
+
+
+def test_tumbling_avg_int_bit_exact(F):
+    k, t, v, b = _c1(n=200_000, nkeys=3_000, every=5_000)
+    op = F.GpuWindowOperator(F.TumblingEventTimeWindows.of(10000), F.AverageAggregate())
+    _run_batches(op, k, t, v, b)
+    (wk, ws, we, res), _ = V.tumbling_lateness0(k, t, v, _final(b), 10000, 0, [4])
+    assert _rows(op) == _want(wk, ws, we, res)   # (double)sum/count is exactly rounded on both sides
+    op.close()
+
+
+def test_tumbling_float64_sum_avg_min_max(F):
+    k, t, v, b = _c1(n=200_000, nkeys=2_000, every=5_000, vdt="float64")
+    agg = F.MultiAggregate(F.SumAggregate("float64"), F.AverageAggregate("float64"), F.MinAggregate("float64"),
+                           F.MaxAggregate("float64"))
+    op = F.GpuWindowOperator(F.TumblingEventTimeWindows.of(5000), agg)
+    _run_batches(op, k, t, v, b)
+    (wk, ws, we, res), _ = V.tumbling_lateness0(k, t, v, _final(b), 5000, 0, [1, 4, 2, 3], value_is_f64=True)
+    got = sorted((a, s, e, *r) for a, s, e, r in op.output)
+    want = _want(wk, ws, we, res)
+    assert [g[:3] for g in got] == [w[:3] for w in want]
+    gs = np.array([g[3:] for g in got])
+    ws_ = np.array([w[3:] for w in want])
+    np.testing.assert_allclose(gs[:, :2], ws_[:, :2], rtol=FLOAT_RTOL)   # order-dependent float sums
+    assert (gs[:, 2:] == ws_[:, 2:]).all()                                # min/max are exact
+    op.close()
+
+
+def test_high_cardinality_growth_and_rehash(F):
+    """1M distinct keys in few windows: tables start small and must grow (rehash) mid-stream."""
+    k, t, v, b = _c1(n=2_000_000, nkeys=1_000_000, every=400_000)
+    op = F.GpuWindowOperator(F.TumblingEventTimeWindows.of(20000), F.MultiAggregate(F.SumAggregate(), F.MaxAggregate()))
+    _run_batches(op, k, t, v, b)
+    (wk, ws, we, res), late = V.tumbling_lateness0(k, t, v, _final(b), 20000, 0, [1, 3])
+    got = sorted((a, s, e, *r) for a, s, e, r in op.output)
+    assert got == _want(wk, ws, we, res)
+    op.close()
+
+
+def test_count_only_without_value_column(F):
+    k, t, _, b = _c1(n=100_000, nkeys=1000, every=10_000)
+    op = F.GpuWindowOperator(F.TumblingEventTimeWindows.of(10000), F.CountAggregate())
+    prev = 0
+    for end, wm in b:
+        op.process_batch(k[prev:end], t[prev:end], None)
+        op.process_watermark(wm)
+        prev = end
+    op.end_input()
+    (wk, ws, we, res), _ = V.tumbling_lateness0(k, t, None, _final(b), 10000, 0, [0])
+    assert _rows(op) == _want(wk, ws, we, res)
+    op.close()
+
+
+def test_extreme_keys_and_timestamps(F):
+    """Long.MIN_VALUE as a key (the table's EMPTY sentinel) and negative timestamps (Java '%')."""
+    op = F.GpuWindowOperator(F.TumblingEventTimeWindows.of(5), F.SumAggregate())
+    ref = O.WindowOperatorOracle(O.TumblingEventTimeWindows(5), O.SumLongAgg())
+    events = [(LONG_MIN, -7, 1), (LONG_MIN, -6, 2), (LONG_MAX, -7, 3), (0, -12, 4), (-1, 3, 5), (LONG_MIN, 4, 6)]
+    for key, ts, val in events:
+        op.process_element(key, ts, val)
+        ref.process_element(key, ts, val)
+    op.end_input()
+    ref.end_input()
+    assert sorted(op.output) == O.rows_as_tuples(ref.output)
+    op.close()
+
+
+def test_key_group_violation_fails_like_the_task(F):
+    from flink_amd import _native as N
+    op = F.GpuWindowOperator(F.TumblingEventTimeWindows.of(1000), F.SumAggregate(), max_parallelism=128,
+                             key_group_range=(0, 63))
+    keys = np.arange(100)
+    kg = np.array([O.assign_to_key_group(O.long_hash_code(int(x)), 128) for x in keys])
+    with pytest.raises(N.GwoError) as ei:
+        op.process_batch(keys, np.full(100, 5), np.ones(100))
+    assert ei.value.status_name == "GWO_ERR_KEY_GROUP" and (kg > 63).any()
+    op.close()
+
+
+def test_no_timestamp_fails(F):
+    from flink_amd import _native as N
+    op = F.GpuWindowOperator(F.TumblingEventTimeWindows.of(1000), F.SumAggregate())
+    with pytest.raises(N.GwoError) as ei:
+        op.process_batch(np.array([1, 2]), np.array([5, LONG_MIN]), np.array([1, 1]))
+    assert ei.value.status_name == "GWO_ERR_NO_TIMESTAMP"
+    op.close()
+
+
+def test_batch_boundaries_do_not_change_results(F):
+    """Same stream, different batch splits between the same watermarks -> identical output."""
+    k, t, v, b = _c1(n=120_000, nkeys=5_000, every=6_000, lag=300, disorder=900)
+    outs = []
+    for split in (1, 7):
+        op = F.GpuWindowOperator(F.TumblingEventTimeWindows.of(3000), F.SumAggregate())
+        prev = 0
+        for end, wm in b:
+            edges = np.linspace(prev, end, split + 1).astype(int)
+            for a, c in zip(edges[:-1], edges[1:]):
+                op.process_batch(k[a:c], t[a:c], v[a:c])
+            op.process_watermark(wm)
+            prev = end
+        op.end_input()
+        outs.append((_rows(op), op.num_late_records_dropped))
+        op.close()
+    assert outs[0] == outs[1]
