@@ -97,7 +97,18 @@ class NativeLibraryMissing(RuntimeError):
     pass
 
 
+def _share_hip_runtime_with_torch():
+    """PyTorch-ROCm wheels bundle their own libamdhip64/libhsa-runtime64 (same SONAMEs as
+    /opt/rocm's).  Two HSA runtimes in one process break GPU discovery for whichever loads second,
+    so when torch is importable it is loaded first and libgwo.so binds to the runtime it brought."""
+    try:
+        import torch  # noqa: F401
+    except Exception:
+        pass
+
+
 def load(path: str = LIB_PATH):
+    _share_hip_runtime_with_torch()
     if not os.path.exists(path):
         raise NativeLibraryMissing(
             f"{path} is missing: build it with `make` (or __graft_entry__.build()). "

@@ -112,6 +112,7 @@ gwo_status Handle::init(const gwo_config &c) {
         geom.unit_off_mod = floor_mod(c.offset, geom.unit);
     }
 
+    debug = getenv("GWO_DEBUG") != nullptr;
     const char *pa = getenv("GWO_PREAGG");
     if (pa) cfg_preagg = atoi(pa) ? 1 : 0;
     if (cfg_preagg >= 0) use_preagg = cfg_preagg;
@@ -131,6 +132,8 @@ gwo_status Handle::init(const gwo_config &c) {
     counter_used.assign(kCounters, 0);
     GWO_TRY(dalloc((void **)&d_counters, kCounters * 8));
     GWO_TRY(hipcheck(hipHostMalloc((void **)&h_counters, kCounters * 8, hipHostMallocDefault), "pinned"));
+    GWO_TRY(hipcheck(hipHostMalloc((void **)&h_scalar, 64, hipHostMallocDefault), "pinned"));
+    GWO_TRY(hipcheck(hipHostMalloc((void **)&h_ident_side, GWO_MAX_WORDS * 16 + 16, hipHostMallocDefault), "pinned"));
     GWO_TRY(dalloc((void **)&d_out_count, 8));
     GWO_TRY(dalloc((void **)&d_scratch_count, 8));
     GWO_TRY(dalloc((void **)&d_side_count, 8));
@@ -138,8 +141,10 @@ gwo_status Handle::init(const gwo_config &c) {
     GWO_TRY(hipcheck(hipMemsetAsync(d_side_count, 0, 8, stream), "memset"));
     GWO_TRY(hipcheck(hipMemsetAsync(d_counters, 0, kCounters * 8, stream), "memset"));
     if (side_enabled()) GWO_TRY(grow_side(4096));
-    if (c.assigner == GWO_ASSIGNER_SLIDING) GWO_TRY(slide_init());
+    if (c.assigner == GWO_ASSIGNER_SLIDING) GWO_TRY(slide_init());   // may append a hidden count word
     if (c.assigner == GWO_ASSIGNER_SESSION) GWO_TRY(session_init());
+    memset(h_ident_side, 0, GWO_MAX_WORDS * 16 + 16);
+    for (int w = 0; w < plan.nwords; ++w) h_ident_side[1 + w] = plan.ident[w];
     return hipcheck(hipStreamSynchronize(stream), "init");
 }
 
@@ -158,6 +163,8 @@ Handle::~Handle() {
     if (h_stats_init) (void)hipHostFree(h_stats_init);
     if (d_counters) (void)hipFree(d_counters);
     if (h_counters) (void)hipHostFree(h_counters);
+    if (h_scalar) (void)hipHostFree(h_scalar);
+    if (h_ident_side) (void)hipHostFree(h_ident_side);
     dir_buf.release();
     stage_key.release();
     stage_ts.release();
@@ -225,8 +232,8 @@ gwo_status Handle::drain(const gwo_out *cols, int64_t cap, int64_t *n_out) {
                              "drain shift"));
     }
     out_rows = rest;
-    unsigned long long rc = rest;
-    GWO_TRY(hipcheck(hipMemcpyAsync(d_out_count, &rc, 8, hipMemcpyHostToDevice, stream), "drain count"));
+    *h_scalar = rest;
+    GWO_TRY(hipcheck(hipMemcpyAsync(d_out_count, h_scalar, 8, hipMemcpyHostToDevice, stream), "drain count"));
     return hipcheck(hipStreamSynchronize(stream), "drain sync");
 }
 
@@ -247,8 +254,8 @@ gwo_status Handle::drain_side(const gwo_side_out *cols, int64_t cap, int64_t *n_
                                             hipMemcpyDeviceToDevice, stream), "side shift"));
     }
     side_rows_committed = side_rows = rest;
-    unsigned long long rc = rest;
-    GWO_TRY(hipcheck(hipMemcpyAsync(d_side_count, &rc, 8, hipMemcpyHostToDevice, stream), "side count"));
+    *h_scalar = rest;
+    GWO_TRY(hipcheck(hipMemcpyAsync(d_side_count, h_scalar, 8, hipMemcpyHostToDevice, stream), "side count"));
     return hipcheck(hipStreamSynchronize(stream), "side sync");
 }
 

@@ -102,6 +102,8 @@ struct Handle {
     unsigned long long *d_scratch_count = nullptr;
     uint64_t out_rows = 0;
     unsigned long long zero_u64 = 0;
+    unsigned long long *h_scalar = nullptr;    // pinned scalar staging
+    int64_t *h_ident_side = nullptr;           // pinned [0, identity words...] side-slot image
 
     // late data
     uint64_t late_dropped = 0;
@@ -123,6 +125,7 @@ struct Handle {
 
     // profiling
     bool profiling = false;
+    bool debug = false;                        // GWO_DEBUG=1: trace batches to stderr
     std::vector<PendingEvent> pending_events;
     KStat kstats[GWO_KERNEL_COUNT_];
 
@@ -151,6 +154,8 @@ struct Handle {
     TableDesc desc(const Table &t) const;
     gwo_status ensure_table(long long u, uint64_t incoming);
     gwo_status read_occupancy();
+    gwo_status launch_ok(const char *what);
+    gwo_status reset_side(const Table &t);
     gwo_status ensure_output(uint64_t extra);
     gwo_status stage_inputs(const int64_t *key, const int64_t *ts, const void *val, int64_t n, const int64_t **dk,
                             const int64_t **dt, const int64_t **dv);
@@ -169,10 +174,23 @@ struct Handle {
     }
 
     // sliding (gwo_slide.cpp)
+    int64_t win_start(__int128 j) const;
+    long long win_first_pane(__int128 j) const;
+    long long win_last_pane(__int128 j) const;
+    __int128 first_window_of_pane(long long u) const;
+    RingDesc ring_desc();
+    gwo_status ensure_ring(uint64_t incoming);
+    gwo_status slide_prepare_insert(long long base, int len, const unsigned long long *hist);
+    gwo_status ring_rebuild();
+    gwo_status release_panes_before(long long first);
     gwo_status slide_init();
     void slide_free();
     gwo_status fire_sliding(int64_t new_wm);
     // sessions (gwo_session.cpp)
+    gwo_status sess_alloc(uint64_t cap, Table &t);
+    gwo_status sess_read_err();
+    gwo_status sess_ensure(uint64_t incoming);
+    gwo_status read_occupancy_one(Table &t);
     gwo_status session_init();
     void session_free();
     gwo_status insert_session(const int64_t *k, const int64_t *t, const int64_t *v, int64_t n);

@@ -49,6 +49,17 @@ struct TableDesc {
     uint64_t mask;                     // cap - 1 (cap is a power of two)
 };
 
+// Sliding windows, invertible aggregates: the running total of the next window to fire
+// ("ring").  Records whose pane lies in [lo, hi] are also added to it; `live` counts entries whose
+// hidden count word (`count_word`) is > 0, i.e. keys present in that window.
+struct RingDesc {
+    TableDesc t;
+    long long lo, hi;                  // pane index range of the window (lo > hi: disabled)
+    unsigned long long *live;
+    int32_t count_word;
+    int32_t pad;
+};
+
 // Result of the per-batch pre-pass (scan kernel), copied back to the host once per batch.
 struct BatchStats {
     long long min_idx;                 // min/max window (pane) index over accepted records
@@ -100,6 +111,24 @@ struct ResultPlan {
     int32_t value_is_f64;
 };
 
+// Sessions (gwo_session.hip)
+struct SessGeom {
+    int64_t gap;
+    int64_t lateness;
+    int64_t wm;
+    int32_t smax;                      // in-flight sessions per key (entry capacity)
+    int32_t key_kind, max_par, kg_lo, kg_hi;
+    int32_t side_enabled;
+};
+
+struct SessErr {
+    unsigned long long bad_ts, bad_kg, merge_late, capacity;
+    long long bad_kg_key;
+    unsigned long long late;
+    unsigned long long emitted;
+    unsigned long long live_delta;     // sessions created - removed (two's complement)
+};
+
 // ---- host-side launchers (gwo_kernels.hip) -----------------------------------------------------
 #include <hip/hip_runtime.h>
 
@@ -111,10 +140,20 @@ void launch_scan(const int64_t *key, const int64_t *ts, int64_t n, const WindowG
 
 void launch_insert(const int64_t *key, const int64_t *ts, const void *val, int64_t n, const WindowGeom &g,
                    const AccPlan &plan, const TableDesc *dir, long long dir_base, int dir_len, int preagg,
-                   BatchStats *stats, hipStream_t s);
+                   BatchStats *stats, const RingDesc &ring, hipStream_t s);
 
+// Emits every occupied entry (with live_word >= 0: every entry whose word live_word is > 0).
 void launch_fire(const TableDesc &t, uint64_t cap, const AccPlan &plan, const ResultPlan &rp, int64_t start,
-                 int64_t end, OutCols out, int reset, hipStream_t s);
+                 int64_t end, OutCols out, int reset, int live_word, hipStream_t s);
+
+// dst += sign * src for every occupied entry of src (sign -1 only for all-ACC_ADD_I64 plans);
+// live_word/live maintain dst's count of entries with a positive count word.
+void launch_fold(const TableDesc &src, uint64_t src_cap, const TableDesc &dst, const AccPlan &plan, int sign,
+                 int live_word, unsigned long long *live, hipStream_t s);
+
+// rehash keeping only entries whose live_word is > 0 (live_word < 0: every occupied entry)
+void launch_rehash_live(const TableDesc &src, uint64_t src_cap, const TableDesc &dst, const AccPlan &plan,
+                        int live_word, hipStream_t s);
 
 void launch_fill(int64_t *base, uint64_t cap, const AccPlan &plan, hipStream_t s);
 

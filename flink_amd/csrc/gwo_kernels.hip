@@ -144,6 +144,19 @@ __device__ __forceinline__ void apply_record(const TableDesc &t, const AccPlan &
     for (int w = 0; w < p.nwords; ++w) atomic_combine(acc + w, p.op[w], lift_word(p, w, vbits));
 }
 
+// Ring update with live-entry accounting on the hidden count word.
+__device__ __forceinline__ void apply_ring(const RingDesc &r, const AccPlan &p, int64_t k, const int64_t *words) {
+    int64_t *acc = find_or_insert(r.t, p.stride, k);
+    for (int w = 0; w < p.nwords; ++w) {
+        if (w == r.count_word) {
+            unsigned long long old = atomicAdd((unsigned long long *)(acc + w), (unsigned long long)words[w]);
+            if (old == 0 && words[w] != 0) atomicAdd(r.live, 1ull);
+        } else {
+            atomic_combine(acc + w, p.op[w], words[w]);
+        }
+    }
+}
+
 __device__ __forceinline__ void check_key_group(int64_t k, const WindowGeom &g, BatchStats *st) {
     int32_t kg = key_group(k, g.key_kind, g.max_par);
     if (kg < g.kg_lo || kg > g.kg_hi) {
@@ -157,7 +170,7 @@ __global__ __launch_bounds__(256) void insert_direct_kernel(const int64_t *__res
                                                             const int64_t *__restrict__ val, int64_t n,
                                                             WindowGeom g, AccPlan p,
                                                             const TableDesc *__restrict__ dir, long long dir_base,
-                                                            int dir_len, BatchStats *st) {
+                                                            int dir_len, BatchStats *st, RingDesc ring) {
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
         long long u = 0;
@@ -169,6 +182,11 @@ __global__ __launch_bounds__(256) void insert_direct_kernel(const int64_t *__res
         check_key_group(k, g, st);
         int64_t v = val ? val[i] : 0;
         apply_record(dir[d], p, k, v);
+        if (u >= ring.lo && u <= ring.hi) {
+            int64_t words[GWO_MAX_WORDS];
+            for (int w = 0; w < p.nwords; ++w) words[w] = lift_word(p, w, v);
+            apply_ring(ring, p, k, words);
+        }
     }
 }
 
@@ -203,7 +221,7 @@ __global__ __launch_bounds__(256) void insert_preagg_kernel(const int64_t *__res
                                                             WindowGeom g, AccPlan p,
                                                             const TableDesc *__restrict__ dir, long long dir_base,
                                                             int dir_len, BatchStats *st,
-                                                            unsigned long long *partials) {
+                                                            unsigned long long *partials, RingDesc ring) {
     __shared__ unsigned long long s_tag[PREAGG_SLOTS];
     __shared__ int64_t s_key[PREAGG_SLOTS];
     __shared__ int32_t s_unit[PREAGG_SLOTS];
@@ -259,6 +277,12 @@ __global__ __launch_bounds__(256) void insert_preagg_kernel(const int64_t *__res
                 for (int w = 0; w < NW; ++w) lds_combine(&s_acc[s * NW + w], p.op[w], lift_word(p, w, rv[j]));
             } else {
                 apply_record(dir[ru[j]], p, rk[j], rv[j]);
+                long long u = dir_base + ru[j];
+                if (u >= ring.lo && u <= ring.hi) {
+                    int64_t words[GWO_MAX_WORDS];
+                    for (int w = 0; w < p.nwords; ++w) words[w] = lift_word(p, w, rv[j]);
+                    apply_ring(ring, p, rk[j], words);
+                }
             }
         }
         __syncthreads();
@@ -267,6 +291,8 @@ __global__ __launch_bounds__(256) void insert_preagg_kernel(const int64_t *__res
             flushed++;
             int64_t *a = find_or_insert(dir[s_unit[s]], p.stride, s_key[s]);
             for (int w = 0; w < NW; ++w) atomic_combine(a + w, p.op[w], s_acc[s * NW + w]);
+            long long u = dir_base + s_unit[s];
+            if (u >= ring.lo && u <= ring.hi) apply_ring(ring, p, s_key[s], &s_acc[s * NW]);
         }
         __syncthreads();
     }
@@ -301,7 +327,7 @@ __device__ __forceinline__ void write_results(const AccPlan &p, const ResultPlan
 }
 
 __global__ __launch_bounds__(256) void fire_kernel(TableDesc t, uint64_t cap, AccPlan p, ResultPlan rp, int64_t start,
-                                                   int64_t end, OutCols o, int reset) {
+                                                   int64_t end, OutCols o, int reset, int live_word) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     const int lane = threadIdx.x & 63;
     // +1 iteration space for the side slot (key == Long.MIN_VALUE)
@@ -330,6 +356,7 @@ __global__ __launch_bounds__(256) void fire_kernel(TableDesc t, uint64_t cap, Ac
                     if (w < NW) acc[w] = t.side[1 + w];
             }
         }
+        if (live_word >= 0 && occ) occ = acc[live_word] > 0;
         unsigned long long m = __ballot(occ);
         if (m == 0) continue;
         unsigned long long wbase = 0;
@@ -365,18 +392,57 @@ __global__ __launch_bounds__(256) void fill_kernel(int64_t *base, uint64_t words
     }
 }
 
-__global__ __launch_bounds__(256) void rehash_kernel(TableDesc src, uint64_t cap, TableDesc dst, AccPlan p) {
+__global__ __launch_bounds__(256) void rehash_kernel(TableDesc src, uint64_t cap, TableDesc dst, AccPlan p,
+                                                     int live_word) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < cap; i += stride) {
         int64_t *e = src.base + i * (uint64_t)p.stride;
         int64_t k = e[0];
         if (k == GWO_EMPTY_KEY) continue;
+        if (live_word >= 0 && e[1 + live_word] <= 0) {   // dead ring entry: drop it
+            for (int w = 0; w < p.nwords; ++w) e[1 + w] = p.ident[w];
+            e[0] = GWO_EMPTY_KEY;
+            continue;
+        }
         int64_t *a = find_or_insert(dst, p.stride, k);
         for (int w = 0; w < p.nwords; ++w) {
             a[w] = e[1 + w];
             e[1 + w] = p.ident[w];
         }
         e[0] = GWO_EMPTY_KEY;
+    }
+}
+
+// Pane fold: dst (+/-)= src entry-wise.  Sliding windows: add an entering pane to / subtract a
+// leaving pane from the running window total, or combine a window's panes (recompute strategy).
+__global__ __launch_bounds__(256) void fold_kernel(TableDesc src, uint64_t cap, TableDesc dst, AccPlan p, int sign,
+                                                   int live_word, unsigned long long *live) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i <= cap; i += stride) {
+        const int64_t *e;
+        int64_t k;
+        if (i < cap) {
+            e = src.base + i * (uint64_t)p.stride;
+            k = e[0];
+            if (k == GWO_EMPTY_KEY) continue;
+        } else {
+            if (src.side[0] == 0) continue;
+            e = src.side;
+            k = GWO_EMPTY_KEY;
+        }
+        int64_t *a = find_or_insert(dst, p.stride, k);
+        for (int w = 0; w < p.nwords; ++w) {
+            int64_t x = e[1 + w];
+            if (sign < 0) x = (int64_t)(0ull - (uint64_t)x);   // ACC_ADD_I64 only: wrap-around inverse
+            if (w == live_word) {
+                unsigned long long old = atomicAdd((unsigned long long *)(a + w), (unsigned long long)x);
+                long long nw = (long long)(old + (unsigned long long)x);
+                if ((long long)old <= 0 && nw > 0) atomicAdd(live, 1ull);
+                else if ((long long)old > 0 && nw <= 0) atomicAdd(live, ~0ull);  // -1
+            } else {
+                atomic_combine(a + w, p.op[w], x);
+            }
+        }
     }
 }
 
@@ -457,7 +523,7 @@ void launch_scan(const int64_t *key, const int64_t *ts, int64_t n, const WindowG
 
 void launch_insert(const int64_t *key, const int64_t *ts, const void *val, int64_t n, const WindowGeom &g,
                    const AccPlan &plan, const TableDesc *dir, long long dir_base, int dir_len, int preagg,
-                   BatchStats *st, hipStream_t s) {
+                   BatchStats *st, const RingDesc &ring, hipStream_t s) {
     unsigned long long *partials = &st->partials;
     const int64_t *v = (const int64_t *)val;
     if (preagg && plan.nwords <= PREAGG_WORDS) {
@@ -465,18 +531,18 @@ void launch_insert(const int64_t *key, const int64_t *ts, const void *val, int64
         if (grid > 2048) grid = 2048;
         if (grid < 1) grid = 1;
         hipLaunchKernelGGL(insert_preagg_kernel, dim3(grid), dim3(256), 0, s, key, ts, v, n, g, plan, dir, dir_base,
-                           dir_len, st, partials);
+                           dir_len, st, partials, ring);
     } else {
         int grid = grid_for(n, 1, 8192);
         hipLaunchKernelGGL(insert_direct_kernel, dim3(grid), dim3(256), 0, s, key, ts, v, n, g, plan, dir, dir_base,
-                           dir_len, st);
+                           dir_len, st, ring);
     }
 }
 
 void launch_fire(const TableDesc &t, uint64_t cap, const AccPlan &plan, const ResultPlan &rp, int64_t start,
-                 int64_t end, OutCols out, int reset, hipStream_t s) {
+                 int64_t end, OutCols out, int reset, int live_word, hipStream_t s) {
     int grid = grid_for((int64_t)cap + 1, 1, 8192);
-    hipLaunchKernelGGL(fire_kernel, dim3(grid), dim3(256), 0, s, t, cap, plan, rp, start, end, out, reset);
+    hipLaunchKernelGGL(fire_kernel, dim3(grid), dim3(256), 0, s, t, cap, plan, rp, start, end, out, reset, live_word);
 }
 
 void launch_fill(int64_t *base, uint64_t cap, const AccPlan &plan, hipStream_t s) {
@@ -487,7 +553,19 @@ void launch_fill(int64_t *base, uint64_t cap, const AccPlan &plan, hipStream_t s
 void launch_rehash(const TableDesc &src, uint64_t src_cap, const TableDesc &dst, const AccPlan &plan,
                    hipStream_t s) {
     int grid = grid_for((int64_t)src_cap, 1, 8192);
-    hipLaunchKernelGGL(rehash_kernel, dim3(grid), dim3(256), 0, s, src, src_cap, dst, plan);
+    hipLaunchKernelGGL(rehash_kernel, dim3(grid), dim3(256), 0, s, src, src_cap, dst, plan, -1);
+}
+
+void launch_rehash_live(const TableDesc &src, uint64_t src_cap, const TableDesc &dst, const AccPlan &plan,
+                        int live_word, hipStream_t s) {
+    int grid = grid_for((int64_t)src_cap, 1, 8192);
+    hipLaunchKernelGGL(rehash_kernel, dim3(grid), dim3(256), 0, s, src, src_cap, dst, plan, live_word);
+}
+
+void launch_fold(const TableDesc &src, uint64_t src_cap, const TableDesc &dst, const AccPlan &plan, int sign,
+                 int live_word, unsigned long long *live, hipStream_t s) {
+    int grid = grid_for((int64_t)src_cap + 1, 1, 8192);
+    hipLaunchKernelGGL(fold_kernel, dim3(grid), dim3(256), 0, s, src, src_cap, dst, plan, sign, live_word, live);
 }
 
 void launch_key_groups(const int64_t *keys, int64_t n, int key_kind, int max_par, int par, int32_t *kg,

@@ -114,19 +114,16 @@ gwo_status Handle::alloc_table(uint64_t cap, Table &t) {
         }
         t.base = (int64_t *)p;
         launch_fill(t.base, cap + 1, plan, stream);  // side slot is entry `cap`: flag word 0 = EMPTY
+        GWO_TRY(launch_ok("fill"));
         // the side slot's flag must read 0 (not EMPTY): reset its first word
-        int64_t zero = 0;
-        GWO_TRY(hipcheck(hipMemcpyAsync(t.base + cap * plan.stride, &zero, 8, hipMemcpyHostToDevice, stream),
-                         "side slot init"));
-        GWO_TRY(hipcheck(hipStreamSynchronize(stream), "table init"));
+        GWO_TRY(hipcheck(hipMemsetAsync(t.base + cap * plan.stride, 0, 8, stream), "side slot init"));
     }
     t.cap = cap;
     t.side = t.base + cap * plan.stride;
     t.counter = take_counter();
     if (t.counter < 0) return fail(GWO_ERR_OUT_OF_MEMORY, "too many live windows/panes (> %zu)", counter_used.size());
     t.occ = 0;
-    int64_t zero = 0;
-    return hipcheck(hipMemcpyAsync(d_counters + t.counter, &zero, 8, hipMemcpyHostToDevice, stream), "counter");
+    return hipcheck(hipMemsetAsync(d_counters + t.counter, 0, 8, stream), "counter");
 }
 
 void Handle::release_table(Table &t) {
@@ -175,13 +172,11 @@ gwo_status Handle::ensure_table(long long u, uint64_t incoming) {
     Table nt;
     GWO_TRY(alloc_table(ncap, nt));
     launch_rehash(desc(t), t.cap, desc(nt), plan, stream);
+    GWO_TRY(launch_ok("rehash"));
     // the side slot moves by copy (flag + words)
     GWO_TRY(hipcheck(hipMemcpyAsync(nt.side, t.side, (size_t)plan.stride * 8, hipMemcpyDeviceToDevice, stream),
                      "side copy"));
-    std::vector<int64_t> side_reset(plan.stride, 0);
-    for (int w = 0; w < plan.nwords; ++w) side_reset[1 + w] = plan.ident[w];
-    GWO_TRY(hipcheck(hipMemcpyAsync(t.side, side_reset.data(), (size_t)plan.stride * 8, hipMemcpyHostToDevice, stream),
-                     "side reset"));
+    GWO_TRY(reset_side(t));
     // occupancy moves with the entries
     GWO_TRY(hipcheck(hipMemcpyAsync(d_counters + nt.counter, d_counters + t.counter, 8, hipMemcpyDeviceToDevice, stream),
                      "occ copy"));
@@ -193,12 +188,20 @@ gwo_status Handle::ensure_table(long long u, uint64_t incoming) {
     return GWO_OK;
 }
 
+gwo_status Handle::launch_ok(const char *what) { return hipcheck(hipGetLastError(), what); }
+
+// side slot := [flag 0, identity words] (copied from the pinned identity entry built at init)
+gwo_status Handle::reset_side(const Table &t) {
+    return hipcheck(hipMemcpyAsync(t.side, h_ident_side, (size_t)plan.stride * 8, hipMemcpyHostToDevice, stream),
+                    "side reset");
+}
+
 // Reads every live table's occupancy counter (one D2H copy).
 gwo_status Handle::read_occupancy() {
     int hi = 0;
     for (auto &kv : tables) hi = std::max(hi, kv.second.counter + 1);
     for (auto &kv : aux_tables) hi = std::max(hi, kv.counter + 1);
-    if (hi == 0) return GWO_OK;
+    if (hi == 0) return hipcheck(hipStreamSynchronize(stream), "occ sync");   // callers rely on the sync
     GWO_TRY(hipcheck(hipMemcpyAsync(h_counters, d_counters, (size_t)hi * 8, hipMemcpyDeviceToHost, stream), "occ"));
     GWO_TRY(hipcheck(hipStreamSynchronize(stream), "occ sync"));
     for (auto &kv : tables) kv.second.occ = h_counters[kv.second.counter];
@@ -319,9 +322,14 @@ gwo_status Handle::insert_windowed(const int64_t *k, const int64_t *t, const int
         launch_scan(k, t, n, g, hist_base, d_stats, (int64_t *)side_key.ptr, (int64_t *)side_ts.ptr,
                     (int64_t *)side_val.ptr, v, d_side_count, first_pass && side_enabled() ? side_cap : 0,
                     first_pass && side_enabled(), stream);
+        GWO_TRY(launch_ok("scan"));
         prof_end(GWO_KERNEL_SCAN, n);
         GWO_TRY(hipcheck(hipMemcpyAsync(h_stats, d_stats, sizeof(BatchStats), hipMemcpyDeviceToHost, stream), "stats"));
         GWO_TRY(read_occupancy());  // syncs
+        if (debug)
+            fprintf(stderr, "[gwo] scan n=%lld base=%lld acc=%llu late=%llu refire=%llu badts=%llu range=%llu min=%lld max=%lld "
+                    "hout=%llu h0=%llu h1=%llu wm=%lld\n", (long long)n, hist_base, hs.accepted, hs.late, hs.refire, hs.bad_ts,
+                    hs.bad_range, hs.min_idx, hs.max_idx, hs.hist_out, hs.hist[0], hs.hist[1], (long long)g.wm);
         if (first_pass) {
             if (hs.bad_ts) return poison(GWO_ERR_NO_TIMESTAMP,
                                          "Record has Long.MIN_VALUE timestamp (= no timestamp marker). Is the time "
@@ -333,12 +341,16 @@ gwo_status Handle::insert_windowed(const int64_t *k, const int64_t *t, const int
             if (hs.refire) return poison(GWO_ERR_UNSUPPORTED,
                                          "allowedLateness > 0 re-firing on sliding windows is not supported");
             if (side_enabled()) {
-                GWO_TRY(hipcheck(hipMemcpy(&side_rows, d_side_count, 8, hipMemcpyDeviceToHost), "side count"));
+                GWO_TRY(hipcheck(hipMemcpyAsync(h_scalar, d_side_count, 8, hipMemcpyDeviceToHost, stream), "side count"));
+                GWO_TRY(hipcheck(hipStreamSynchronize(stream), "side count sync"));
+                side_rows = *h_scalar;
                 if ((long long)side_rows > side_cap) {
                     // grow and re-collect this batch's side output (first pass only)
                     side_rows = side_rows_committed;
                     GWO_TRY(grow_side((long long)hs.late + (long long)side_rows_committed));
-                    GWO_TRY(hipcheck(hipMemcpy(d_side_count, &side_rows, 8, hipMemcpyHostToDevice), "side reset"));
+                    *h_scalar = side_rows;
+                    GWO_TRY(hipcheck(hipMemcpyAsync(d_side_count, h_scalar, 8, hipMemcpyHostToDevice, stream), "side reset"));
+                    GWO_TRY(hipcheck(hipStreamSynchronize(stream), "side reset sync"));
                     continue;
                 }
                 side_rows_committed = side_rows;
@@ -367,12 +379,14 @@ gwo_status Handle::insert_windowed(const int64_t *k, const int64_t *t, const int
             auto it = tables.find(hist_base + d);
             if (it != tables.end()) h_dir[d] = desc(it->second);
         }
+        if (slide) GWO_TRY(slide_prepare_insert(hist_base, dir_len, hs.hist));
         GWO_TRY(ensure_buf(dir_buf, dir_len * sizeof(TableDesc)));
         GWO_TRY(hipcheck(hipMemcpyAsync(dir_buf.ptr, h_dir.data(), dir_len * sizeof(TableDesc), hipMemcpyHostToDevice,
                                         stream), "dir"));
         prof_begin(GWO_KERNEL_INSERT);
         launch_insert(k, t, v, n, g, plan, (const TableDesc *)dir_buf.ptr, hist_base, dir_len, use_preagg, d_stats,
-                      stream);
+                      ring_desc(), stream);
+        GWO_TRY(launch_ok("insert"));
         prof_end(GWO_KERNEL_INSERT, n);
         // key-group violations surface at the next sync (Flink fails the task at that record)
         GWO_TRY(hipcheck(hipMemcpyAsync(&h_stats->bad_kg, &d_stats->bad_kg, 16, hipMemcpyDeviceToHost, stream), "kg"));
@@ -413,7 +427,7 @@ void Handle::init_stats(long long hist_base) {
     s.min_idx = 0x7fffffffffffffffLL;
     s.max_idx = (long long)0x8000000000000000LL;
     (void)hist_base;
-    *h_stats_init = s;
+    *h_stats_init = s;   // pinned; the previous batch's copy has completed (every batch ends in a sync)
     (void)hipMemcpyAsync(d_stats, h_stats_init, sizeof(BatchStats), hipMemcpyHostToDevice, stream);
 }
 
@@ -468,7 +482,8 @@ gwo_status Handle::fire_tumbling(int64_t new_wm) {
         int64_t start = unit_start(u);
         int64_t end = (int64_t)((uint64_t)start + (uint64_t)cfg.size);
         prof_begin(GWO_KERNEL_FIRE);
-        launch_fire(desc(t), t.cap, plan, rplan, start, end, o, also_clear ? 1 : 0, stream);
+        launch_fire(desc(t), t.cap, plan, rplan, start, end, o, also_clear ? 1 : 0, -1, stream);
+        GWO_TRY(launch_ok("fire"));
         prof_end(GWO_KERNEL_FIRE, (int64_t)t.cap);
         out_rows += t.occ;
         t.fired = true;
@@ -479,9 +494,9 @@ gwo_status Handle::fire_tumbling(int64_t new_wm) {
             // state cleared without emission (already fired at maxTs): reset by a no-output sweep
             OutCols none = o;
             none.cap = 0;
-            GWO_TRY(hipcheck(hipMemcpyAsync(d_scratch_count, &zero_u64, 8, hipMemcpyHostToDevice, stream), "z"));
+            GWO_TRY(hipcheck(hipMemsetAsync(d_scratch_count, 0, 8, stream), "z"));
             none.count = d_scratch_count;
-            launch_fire(desc(t), t.cap, plan, rplan, 0, 0, none, 1, stream);
+            launch_fire(desc(t), t.cap, plan, rplan, 0, 0, none, 1, -1, stream);
         }
         release_table(t);
         tables.erase(u);
@@ -578,7 +593,7 @@ gwo_status gwo_output_view(gwo_handle *hh, gwo_out *cols, int64_t *n) {
 gwo_status gwo_discard_output(gwo_handle *hh) {
     H_OR_FAIL;
     h->out_rows = 0;
-    return h->hipcheck(hipMemcpyAsync(h->d_out_count, &h->zero_u64, 8, hipMemcpyHostToDevice, h->stream), "discard");
+    return h->hipcheck(hipMemsetAsync(h->d_out_count, 0, 8, h->stream), "discard");
 }
 
 gwo_status gwo_drain(gwo_handle *hh, const gwo_out *cols, int64_t cap, int64_t *n_out) {

@@ -1,0 +1,209 @@
+// gwo_session.cpp -- host side of EventTimeSessionWindows (kernels: gwo_session.hip, gwo_sort.hip).
+#include <algorithm>
+#include <cstdlib>
+
+#include "gwo_handle.h"
+
+namespace gwo {
+
+void launch_sess_slot(const int64_t *key, const int64_t *ts, int64_t n, const TableDesc &t, uint64_t cap, int stride,
+                      const SessGeom &g, uint32_t *rec_slot, SessErr *err, hipStream_t s);
+void launch_sess_process(const int64_t *key, const int64_t *ts, const int64_t *val, int64_t n, const uint32_t *sslot,
+                         const uint32_t *sidx, const TableDesc &t, uint64_t cap, int stride, const AccPlan &p,
+                         const ResultPlan &rp, const SessGeom &g, OutCols o, SessErr *err, int64_t *sk, int64_t *st,
+                         int64_t *sv, unsigned long long *sc, long long scap, hipStream_t s);
+void launch_sess_fire(const TableDesc &t, uint64_t cap, int stride, const AccPlan &p, const ResultPlan &rp,
+                      const SessGeom &g, OutCols o, SessErr *err, hipStream_t s);
+void launch_sess_compact(const TableDesc &src, uint64_t cap, const TableDesc &dst, int stride, hipStream_t s);
+int radix_sort_pairs(const uint32_t *keys, const uint32_t *vals, int64_t n, int key_bits, uint32_t *k1, uint32_t *v1,
+                     uint32_t *k2, uint32_t *v2, uint32_t *hist, hipStream_t s);
+
+struct SessionState {
+    int smax = 8;
+    int stride = 0;
+    Table T;
+    uint64_t live = 0;              // in-flight sessions
+    SessErr *d_err = nullptr;
+    SessErr *h_err = nullptr;       // pinned
+    DevBuf rec_slot, k1, v1, k2, v2, hist;
+};
+
+gwo_status Handle::sess_alloc(uint64_t cap, Table &t) {
+    SessionState &S = *sess;
+    void *p = nullptr;
+    GWO_TRY(dalloc(&p, ((size_t)cap + 1) * S.stride * 8));
+    t.base = (int64_t *)p;
+    t.cap = cap;
+    t.side = t.base + cap * S.stride;
+    AccPlan fp{};
+    fp.stride = S.stride;   // word 0 = EMPTY, every other word 0 (no sessions)
+    launch_fill(t.base, cap + 1, fp, stream);
+    GWO_TRY(launch_ok("fill"));
+    GWO_TRY(hipcheck(hipMemsetAsync(t.side, 0, 8, stream), "side"));
+    t.counter = take_counter();
+    if (t.counter < 0) return fail(GWO_ERR_OUT_OF_MEMORY, "counter slots exhausted");
+    t.occ = 0;
+    return hipcheck(hipMemsetAsync(d_counters + t.counter, 0, 8, stream), "counter");
+}
+
+gwo_status Handle::session_init() {
+    sess = new SessionState();
+    SessionState &S = *sess;
+    if (const char *e = getenv("GWO_SESSION_SLOTS")) S.smax = std::max(1, std::min(16, atoi(e)));
+    S.stride = (2 + S.smax * (3 + plan.nwords) + 1) & ~1;
+    GWO_TRY(dalloc((void **)&S.d_err, sizeof(SessErr)));
+    GWO_TRY(hipcheck(hipHostMalloc((void **)&S.h_err, sizeof(SessErr), hipHostMallocDefault), "pinned"));
+    uint64_t cap = kMinCap;
+    if (cfg.expected_keys > 0)
+        while ((double)cfg.expected_keys > kInitLoad * (double)cap) cap <<= 1;
+    return sess_alloc(cap, S.T);
+}
+
+void Handle::session_free() {
+    if (!sess) return;
+    SessionState &S = *sess;
+    if (S.T.base) (void)hipFree(S.T.base);
+    if (S.d_err) (void)hipFree(S.d_err);
+    if (S.h_err) (void)hipHostFree(S.h_err);
+    S.rec_slot.release();
+    S.k1.release();
+    S.v1.release();
+    S.k2.release();
+    S.v2.release();
+    S.hist.release();
+    delete sess;
+    sess = nullptr;
+}
+
+static SessGeom sess_geom(const Handle &h, int smax) {
+    SessGeom g{};
+    g.gap = h.cfg.gap;
+    g.lateness = h.cfg.allowed_lateness;
+    g.wm = h.wm;
+    g.smax = smax;
+    g.key_kind = h.cfg.key_kind;
+    g.max_par = h.cfg.max_parallelism;
+    g.kg_lo = h.cfg.key_group_start;
+    g.kg_hi = h.cfg.key_group_end;
+    g.side_enabled = h.cfg.side_output;
+    return g;
+}
+
+gwo_status Handle::sess_read_err() {
+    SessionState &S = *sess;
+    GWO_TRY(hipcheck(hipMemcpyAsync(S.h_err, S.d_err, sizeof(SessErr), hipMemcpyDeviceToHost, stream), "err"));
+    return hipcheck(hipStreamSynchronize(stream), "err sync");
+}
+
+// Grow the per-key table (dropping keys without sessions) so `incoming` new keys fit.
+gwo_status Handle::sess_ensure(uint64_t incoming) {
+    SessionState &S = *sess;
+    GWO_TRY(read_occupancy_one(S.T));
+    if ((double)(S.T.occ + incoming) <= kMaxLoad * (double)S.T.cap) return GWO_OK;
+    uint64_t need = std::min<uint64_t>(S.T.occ, S.live) + incoming;
+    uint64_t cap = kMinCap;
+    while ((double)need > kInitLoad * (double)cap) cap <<= 1;
+    Table nt;
+    GWO_TRY(sess_alloc(cap, nt));
+    launch_sess_compact(desc(S.T), S.T.cap, desc(nt), S.stride, stream);
+    GWO_TRY(launch_ok("compact"));
+    GWO_TRY(hipcheck(hipMemcpyAsync(nt.side, S.T.side, (size_t)S.stride * 8, hipMemcpyDeviceToDevice, stream), "side"));
+    GWO_TRY(hipcheck(hipStreamSynchronize(stream), "compact sync"));
+    (void)hipFree(S.T.base);
+    counter_used[S.T.counter] = 0;
+    S.T = nt;
+    return read_occupancy_one(S.T);
+}
+
+gwo_status Handle::read_occupancy_one(Table &t) {
+    GWO_TRY(hipcheck(hipMemcpyAsync(h_counters + t.counter, d_counters + t.counter, 8, hipMemcpyDeviceToHost, stream),
+                     "occ"));
+    GWO_TRY(hipcheck(hipStreamSynchronize(stream), "occ sync"));
+    t.occ = h_counters[t.counter];
+    return GWO_OK;
+}
+
+gwo_status Handle::insert_session(const int64_t *k, const int64_t *t, const int64_t *v, int64_t n) {
+    SessionState &S = *sess;
+    if (n > 0xffffffffll) return fail(GWO_ERR_INVALID_ARGUMENT, "session batches are limited to 2^32 records");
+    GWO_TRY(sess_ensure((uint64_t)n));
+    if (cfg.allowed_lateness > 0) GWO_TRY(ensure_output((uint64_t)n));   // re-fires: at most one row per record
+    GWO_TRY(ensure_buf(S.rec_slot, n * 4));
+    GWO_TRY(ensure_buf(S.k1, n * 4));
+    GWO_TRY(ensure_buf(S.v1, n * 4));
+    GWO_TRY(ensure_buf(S.k2, n * 4));
+    GWO_TRY(ensure_buf(S.v2, n * 4));
+    int64_t nblocks = (n + 4095) / 4096;
+    GWO_TRY(ensure_buf(S.hist, (size_t)256 * nblocks * 4 + 16));
+    GWO_TRY(hipcheck(hipMemsetAsync(S.d_err, 0, sizeof(SessErr), stream), "err"));
+    if (side_enabled() && side_cap - (long long)side_rows_committed < n)
+        GWO_TRY(grow_side((long long)side_rows_committed + n));
+    SessGeom g = sess_geom(*this, S.smax);
+    prof_begin(GWO_KERNEL_SESSION);
+    launch_sess_slot(k, t, n, desc(S.T), S.T.cap, S.stride, g, (uint32_t *)S.rec_slot.ptr, S.d_err, stream);
+    GWO_TRY(launch_ok("sess slot"));
+    int bits = 8;
+    while (bits < 32 && (S.T.cap >> bits) > 0) bits += 8;
+    int which = radix_sort_pairs((const uint32_t *)S.rec_slot.ptr, nullptr, n, bits, (uint32_t *)S.k1.ptr,
+                                 (uint32_t *)S.v1.ptr, (uint32_t *)S.k2.ptr, (uint32_t *)S.v2.ptr,
+                                 (uint32_t *)S.hist.ptr, stream);
+    GWO_TRY(launch_ok("radix sort"));
+    const uint32_t *ss = which ? (const uint32_t *)S.k2.ptr : (const uint32_t *)S.k1.ptr;
+    const uint32_t *si = which ? (const uint32_t *)S.v2.ptr : (const uint32_t *)S.v1.ptr;
+    OutCols o = out_cols();
+    launch_sess_process(k, t, v, n, ss, si, desc(S.T), S.T.cap, S.stride, plan, rplan, g, o, S.d_err,
+                        (int64_t *)side_key.ptr, (int64_t *)side_ts.ptr, (int64_t *)side_val.ptr, d_side_count,
+                        side_enabled() ? side_cap : 0, stream);
+    GWO_TRY(launch_ok("sess process"));
+    prof_end(GWO_KERNEL_SESSION, n);
+    GWO_TRY(sess_read_err());
+    SessErr &e = *S.h_err;
+    if (e.bad_ts)
+        return poison(GWO_ERR_NO_TIMESTAMP, "Record has Long.MIN_VALUE timestamp (= no timestamp marker).");
+    if (e.bad_kg)
+        return poison(GWO_ERR_KEY_GROUP, ("Key group of key " + std::to_string(e.bad_kg_key) +
+                                          " is not in KeyGroupRange{startKeyGroup=" + std::to_string(cfg.key_group_start) +
+                                          ", endKeyGroup=" + std::to_string(cfg.key_group_end) + "}.").c_str());
+    if (e.merge_late)
+        return poison(GWO_ERR_MERGE_LATE, "The end timestamp of an event-time window cannot become earlier than the "
+                                          "current watermark by merging.");
+    if (e.capacity)
+        return poison(GWO_ERR_CAPACITY, ("a key exceeded " + std::to_string(S.smax) +
+                                         " in-flight sessions (raise GWO_SESSION_SLOTS, max 16)").c_str());
+    S.live += e.live_delta;
+    out_rows += e.emitted;
+    if (side_enabled()) {
+        GWO_TRY(hipcheck(hipMemcpyAsync(h_scalar, d_side_count, 8, hipMemcpyDeviceToHost, stream), "side"));
+        GWO_TRY(hipcheck(hipStreamSynchronize(stream), "side sync"));
+        if ((long long)*h_scalar > side_cap)
+            return poison(GWO_ERR_CAPACITY, "side output overflow");
+        side_rows = side_rows_committed = *h_scalar;
+    } else {
+        late_dropped += e.late;
+    }
+    return GWO_OK;
+}
+
+gwo_status Handle::fire_session(int64_t new_wm) {
+    SessionState &S = *sess;
+    if (S.live == 0) return GWO_OK;
+    GWO_TRY(ensure_output(S.live));
+    GWO_TRY(hipcheck(hipMemsetAsync(S.d_err, 0, sizeof(SessErr), stream), "err"));
+    SessGeom g = sess_geom(*this, S.smax);
+    g.wm = new_wm;
+    prof_begin(GWO_KERNEL_FIRE);
+    launch_sess_fire(desc(S.T), S.T.cap, S.stride, plan, rplan, g, out_cols(), S.d_err, stream);
+    GWO_TRY(launch_ok("sess fire"));
+    prof_end(GWO_KERNEL_FIRE, (int64_t)S.T.cap);
+    GWO_TRY(sess_read_err());
+    S.live += S.h_err->live_delta;
+    out_rows += S.h_err->emitted;
+    return GWO_OK;
+}
+
+gwo_status Handle::session_state_size(int64_t *entries) {
+    *entries = (int64_t)sess->live;
+    return GWO_OK;
+}
+
+}  // namespace gwo

@@ -75,3 +75,38 @@ def punctuated_watermarks(ts: np.ndarray, every: int, lag: int):
         e = min(end, len(ts))
         out.append((e, int(running[e - 1]) - lag - 1))
     return out
+
+
+def session_stream(num_keys: int, n: int, gap: int = 30_000, lag: int = 5_000, seed: int = 42,
+                   late_fraction: float = 0.0, mean_inner: int = 5_000, events_per_session: int = 10):
+    """Config 5: per key, bursts with exponential inner gaps (mean 5 s, capped below
+    the session gap) separated by >= gap + 1 ms; arrival order sorted by ts + U[0, lag) (so
+    wm = maxTs - lag - 1 never makes an on-time event late); a late variant delays a fraction of
+    events by U[lag, 3*lag) past that order.  Returns (key, ts, value, arrival order applied)."""
+    rng = np.random.default_rng(seed)
+    per = max(1, n // num_keys)
+    keys = np.repeat(np.arange(num_keys, dtype=np.int64), per)
+    m = len(keys)
+    inner = np.minimum(rng.exponential(mean_inner, m), gap - 1).astype(np.int64)
+    new_sess = rng.random(m) < 1.0 / events_per_session
+    between = (gap + 1 + rng.exponential(gap, m)).astype(np.int64)
+    step = np.where(new_sess, between, inner)
+    first = np.arange(m) % per == 0
+    start = rng.integers(0, 60_000, num_keys)
+    step[first] = 0
+    ts = np.cumsum(step)
+    # restart the cumulative sum at each key
+    base = ts[first]
+    ts = ts - np.repeat(base, per) + np.repeat(start, per)
+    vals = rng.integers(0, 1000, m).astype(np.int64)
+    arrival = ts + rng.integers(0, lag, m)
+    if late_fraction > 0:
+        late = rng.random(m) < late_fraction
+        arrival[late] += rng.integers(lag, 3 * lag, int(late.sum()))
+    order = np.argsort(arrival, kind="stable")
+    return keys[order], ts[order], vals[order], arrival[order]
+
+
+def session_watermarks(arrival_ts: np.ndarray, ts: np.ndarray, every: int, lag: int):
+    """Punctuated BoundedOutOfOrderness watermarks over the arrival sequence."""
+    return punctuated_watermarks(ts, every, lag)

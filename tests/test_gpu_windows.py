@@ -274,3 +274,137 @@ def test_batch_boundaries_do_not_change_results(F):
         outs.append((_rows(op), op.num_late_records_dropped))
         op.close()
     assert outs[0] == outs[1]
+
+
+# ---- sliding windows (panes; ring for invertible aggregates, recompute otherwise) ----------------
+@pytest.mark.parametrize("size,slide,offset", [(60000, 1000, 0), (3000, 1000, 0), (3000, 2000, 500), (5000, 5000, 0),
+                                               (7000, 3000, -1000)])
+def test_sliding_avg_ring_bit_exact(F, size, slide, offset):
+    """Config 3 shape (AverageAggregate over int64, exact int64 accumulators, double result)."""
+    k, t, v, b = _c1(n=150_000, nkeys=20_000, every=5_000, lag=500, disorder=900, seed=5)
+    op = F.GpuWindowOperator(F.SlidingEventTimeWindows.of(size, slide, offset), F.AverageAggregate())
+    _run_batches(op, k, t, v, b)
+    (wk, ws, we, res), late = V.sliding_lateness0(k, t, v, _final(b), size, slide, offset, [4])
+    got = _rows(op)
+    assert len(got) == len(wk)
+    assert got == _want(wk, ws, we, res)
+    assert op.num_late_records_dropped == late
+    op.close()
+
+
+def test_sliding_sum_count_ring(F):
+    k, t, v, b = _c1(n=100_000, nkeys=3_000, every=2_000, lag=0, disorder=700, seed=9)
+    agg = F.MultiAggregate(F.SumAggregate(), F.CountAggregate())
+    op = F.GpuWindowOperator(F.SlidingEventTimeWindows.of(4000, 1000), agg)
+    _run_batches(op, k, t, v, b)
+    (wk, ws, we, res), late = V.sliding_lateness0(k, t, v, _final(b), 4000, 1000, 0, [1, 0])
+    got = sorted((a, s, e, *r) for a, s, e, r in op.output)
+    assert got == _want(wk, ws, we, res)
+    assert op.num_late_records_dropped == late > 0
+    op.close()
+
+
+def test_sliding_min_max_recompute(F):
+    k, t, v, b = _c1(n=100_000, nkeys=5_000, every=4_000, lag=200, disorder=800, seed=11)
+    agg = F.MultiAggregate(F.MinAggregate(), F.MaxAggregate(), F.SumAggregate())
+    op = F.GpuWindowOperator(F.SlidingEventTimeWindows.of(6000, 2000, 0), agg)
+    _run_batches(op, k, t, v, b)
+    (wk, ws, we, res), late = V.sliding_lateness0(k, t, v, _final(b), 6000, 2000, 0, [2, 3, 1])
+    got = sorted((a, s, e, *r) for a, s, e, r in op.output)
+    assert got == _want(wk, ws, we, res)
+    assert op.num_late_records_dropped == late
+    op.close()
+
+
+def test_sliding_float64_avg_recompute(F):
+    k, t, v, b = _c1(n=80_000, nkeys=2_000, every=4_000, vdt="float64", seed=13)
+    op = F.GpuWindowOperator(F.SlidingEventTimeWindows.of(10000, 5000), F.AverageAggregate("float64"))
+    _run_batches(op, k, t, v, b)
+    (wk, ws, we, res), _ = V.sliding_lateness0(k, t, v, _final(b), 10000, 5000, 0, [4], value_is_f64=True)
+    got = _rows(op)
+    want = _want(wk, ws, we, res)
+    assert [g[:3] for g in got] == [w[:3] for w in want]
+    np.testing.assert_allclose([g[3] for g in got], [w[3] for w in want], rtol=FLOAT_RTOL)
+    op.close()
+
+
+def test_sliding_gap_in_stream(F):
+    """Event time with a hole of many windows: empty windows are skipped, the ring re-anchors."""
+    k1, t1, v1, _ = _c1(n=20_000, nkeys=500, seed=21)
+    t2 = t1 + 10_000_000
+    k = np.concatenate([k1, k1])
+    t = np.concatenate([t1, t2])
+    v = np.concatenate([v1, v1])
+    b = G.punctuated_watermarks(t, 2_000, 1000)
+    op = F.GpuWindowOperator(F.SlidingEventTimeWindows.of(3000, 1000), F.SumAggregate())
+    _run_batches(op, k, t, v, b)
+    (wk, ws, we, res), late = V.sliding_lateness0(k, t, v, _final(b), 3000, 1000, 0, [1])
+    assert _rows(op) == _want(wk, ws, we, res)
+    op.close()
+
+
+# ---- session windows ----------------------------------------------------------------------------
+@pytest.mark.parametrize("name", ["session_reduce_3s", "session_list_3s", "side_output_lateness_session_zero",
+                                  "session_lateness_10", "session_lateness_10000"])
+def test_reference_session_streams(F, golden, name):
+    s = next(x for x in golden["operator_streams"] if x["name"] == name)
+    op = _run_stream(F, s)
+    assert sorted(op.output) == sorted(map(tuple, s["expected"]))
+    assert sorted(op.side_output) == sorted(map(tuple, s.get("side", [])))
+    op.close()
+
+
+def test_session_windowing_example(F, golden):
+    s = next(x for x in golden["operator_streams"] if x["name"] == "session_windowing_example")
+    op = _run_stream(F, s)
+    assert sorted((k, st, r) for k, st, e, r in op.output) == sorted(map(tuple, s["expected_key_start_sum"]))
+    op.close()
+
+
+def _session_oracle(k, t, v, batches, gap, lateness=0, agg=None):
+    op = O.WindowOperatorOracle(O.EventTimeSessionWindows(gap), agg or O.SumLongAgg(), lateness)
+    prev = 0
+    for end, wm in batches:
+        for i in range(prev, end):
+            op.process_element(int(k[i]), int(t[i]), int(v[i]))
+        op.process_watermark(wm)
+        prev = end
+    op.process_watermark(LONG_MAX)
+    return op
+
+
+@pytest.mark.parametrize("late_fraction", [0.0, 0.01])
+def test_c5_sessions_vs_oracle(F, late_fraction):
+    """Config 5 shape: bursty sessions, 30 s gap, disorder < lag (plus a late variant)."""
+    k, t, v, _ = G.session_stream(2_000, 60_000, late_fraction=late_fraction, seed=17)
+    b = G.punctuated_watermarks(t, 100, 5_000)
+    ref = _session_oracle(k, t, v, b, 30_000, agg=O.MultiAgg([O.SumLongAgg(), O.CountAgg(), O.MaxAgg()]))
+    op = F.GpuWindowOperator(F.EventTimeSessionWindows.withGap(30_000),
+                             F.MultiAggregate(F.SumAggregate(), F.CountAggregate(), F.MaxAggregate()))
+    _run_batches(op, k, t, v, b)
+    got = sorted(op.output)
+    want = sorted((r.key, r.start, r.end, r.result) for r in ref.output)
+    assert len(got) == len(want) > 1000
+    assert got == want
+    assert op.num_late_records_dropped == ref.num_late_records_dropped
+    if late_fraction:
+        assert ref.num_late_records_dropped > 0
+    op.close()
+
+
+@pytest.mark.parametrize("lateness", [0, 3_000])
+def test_sessions_out_of_order_with_lateness(F, lateness):
+    """Heavy disorder relative to the lag, small gap: merges, bridging, late drops and (with
+    allowedLateness) per-element re-fires, all in arrival order per key."""
+    rng = np.random.default_rng(lateness + 3)
+    n = 20_000
+    k = rng.integers(0, 300, n)
+    t = np.sort(rng.integers(0, 400_000, n)) + rng.integers(0, 6_000, n)
+    v = rng.integers(0, 100, n)
+    b = G.punctuated_watermarks(t, 500, 1_000)
+    ref = _session_oracle(k, t, v, b, 2_000, lateness)
+    op = F.GpuWindowOperator(F.EventTimeSessionWindows.withGap(2_000), F.SumAggregate(), allowed_lateness=lateness)
+    _run_batches(op, k, t, v, b)
+    assert sorted(op.output) == sorted((r.key, r.start, r.end, r.result) for r in ref.output)
+    assert op.num_late_records_dropped == ref.num_late_records_dropped > 0
+    op.close()
