@@ -78,11 +78,13 @@ def punctuated_watermarks(ts: np.ndarray, every: int, lag: int):
 
 
 def session_stream(num_keys: int, n: int, gap: int = 30_000, lag: int = 5_000, seed: int = 42,
-                   late_fraction: float = 0.0, mean_inner: int = 5_000, events_per_session: int = 10):
+                   late_fraction: float = 0.0, mean_inner: int = 5_000, events_per_session: int = 10,
+                   late_extra: int = 0):
     """Config 5: per key, bursts with exponential inner gaps (mean 5 s, capped below
     the session gap) separated by >= gap + 1 ms; arrival order sorted by ts + U[0, lag) (so
     wm = maxTs - lag - 1 never makes an on-time event late); a late variant delays a fraction of
-    events by U[lag, 3*lag) past that order.  Returns (key, ts, value, arrival order applied)."""
+    events by U[lag, 3*lag) (+ late_extra) past that order.  Note a delay below gap + lag is absorbed:
+    the late event's own session window [ts, ts + gap) still ends after the watermark.  Returns (key, ts, value, arrival order applied)."""
     rng = np.random.default_rng(seed)
     per = max(1, n // num_keys)
     keys = np.repeat(np.arange(num_keys, dtype=np.int64), per)
@@ -102,7 +104,7 @@ def session_stream(num_keys: int, n: int, gap: int = 30_000, lag: int = 5_000, s
     arrival = ts + rng.integers(0, lag, m)
     if late_fraction > 0:
         late = rng.random(m) < late_fraction
-        arrival[late] += rng.integers(lag, 3 * lag, int(late.sum()))
+        arrival[late] += rng.integers(lag, 3 * lag, int(late.sum())) + late_extra
     order = np.argsort(arrival, kind="stable")
     return keys[order], ts[order], vals[order], arrival[order]
 

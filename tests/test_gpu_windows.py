@@ -293,7 +293,7 @@ def test_sliding_avg_ring_bit_exact(F, size, slide, offset):
 
 
 def test_sliding_sum_count_ring(F):
-    k, t, v, b = _c1(n=100_000, nkeys=3_000, every=2_000, lag=0, disorder=700, seed=9)
+    k, t, v, b = _c1(n=100_000, nkeys=3_000, every=2_000, lag=0, disorder=2500, seed=9)
     agg = F.MultiAggregate(F.SumAggregate(), F.CountAggregate())
     op = F.GpuWindowOperator(F.SlidingEventTimeWindows.of(4000, 1000), agg)
     _run_batches(op, k, t, v, b)
@@ -376,7 +376,7 @@ def _session_oracle(k, t, v, batches, gap, lateness=0, agg=None):
 @pytest.mark.parametrize("late_fraction", [0.0, 0.01])
 def test_c5_sessions_vs_oracle(F, late_fraction):
     """Config 5 shape: bursty sessions, 30 s gap, disorder < lag (plus a late variant)."""
-    k, t, v, _ = G.session_stream(2_000, 60_000, late_fraction=late_fraction, seed=17)
+    k, t, v, _ = G.session_stream(2_000, 60_000, late_fraction=late_fraction, seed=17, late_extra=30_000)
     b = G.punctuated_watermarks(t, 100, 5_000)
     ref = _session_oracle(k, t, v, b, 30_000, agg=O.MultiAgg([O.SumLongAgg(), O.CountAgg(), O.MaxAgg()]))
     op = F.GpuWindowOperator(F.EventTimeSessionWindows.withGap(30_000),
@@ -406,5 +406,7 @@ def test_sessions_out_of_order_with_lateness(F, lateness):
     op = F.GpuWindowOperator(F.EventTimeSessionWindows.withGap(2_000), F.SumAggregate(), allowed_lateness=lateness)
     _run_batches(op, k, t, v, b)
     assert sorted(op.output) == sorted((r.key, r.start, r.end, r.result) for r in ref.output)
-    assert op.num_late_records_dropped == ref.num_late_records_dropped > 0
+    assert op.num_late_records_dropped == ref.num_late_records_dropped
+    if lateness == 0:
+        assert ref.num_late_records_dropped > 0
     op.close()
