@@ -293,7 +293,7 @@ def test_sliding_avg_ring_bit_exact(F, size, slide, offset):
 
 
 def test_sliding_sum_count_ring(F):
-    k, t, v, b = _c1(n=100_000, nkeys=3_000, every=2_000, lag=0, disorder=2500, seed=9)
+    k, t, v, b = _c1(n=100_000, nkeys=3_000, every=2_000, lag=0, disorder=4500, seed=9)
     agg = F.MultiAggregate(F.SumAggregate(), F.CountAggregate())
     op = F.GpuWindowOperator(F.SlidingEventTimeWindows.of(4000, 1000), agg)
     _run_batches(op, k, t, v, b)
