@@ -122,11 +122,14 @@ __device__ __forceinline__ int64_t combine(int op, int64_t a, int64_t b) {
 }
 
 // Find the entry of `key` in table t, claiming a free slot if absent.  Returns the entry's
-// accumulator words.  Linear probing; the table never fills (host keeps load <= 0.7).
-__device__ __forceinline__ int64_t *find_or_insert(const TableDesc &t, int stride, int64_t key) {
+// accumulator words; `claimed` is set when this call took a new slot.  Linear probing; the table
+// never fills (host keeps load <= 0.7).  Occupancy is NOT counted here: callers pass `claimed`
+// to count_claims() at a point where the whole wave has re-converged.
+__device__ __forceinline__ int64_t *find_or_insert(const TableDesc &t, int stride, int64_t key, bool &claimed) {
+    claimed = false;
     if (key == GWO_EMPTY_KEY) {
         if (__hip_atomic_load(t.side, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
-            if (atomicCAS((unsigned long long *)t.side, 0ull, 1ull) == 0ull) atomicAdd(t.occ, 1ull);
+            if (atomicCAS((unsigned long long *)t.side, 0ull, 1ull) == 0ull) claimed = true;
         }
         return t.side + 1;
     }
@@ -139,13 +142,64 @@ __device__ __forceinline__ int64_t *find_or_insert(const TableDesc &t, int strid
             unsigned long long prev =
                 atomicCAS((unsigned long long *)e, (unsigned long long)GWO_EMPTY_KEY, (unsigned long long)key);
             if ((int64_t)prev == GWO_EMPTY_KEY) {
-                atomicAdd(t.occ, 1ull);
+                claimed = true;
                 return e + 1;
             }
             if ((int64_t)prev == key) return e + 1;
         }
         slot = (slot + 1) & t.mask;
     }
+}
+
+// Occupancy counters are GWO_OCC_SHARDS words on separate 64-B lines (host sums them); a workgroup
+// adds to shard blockIdx % GWO_OCC_SHARDS, so one hot word never serialises a whole launch.
+__device__ __forceinline__ void occ_add(unsigned long long *occ, unsigned long long n) {
+    atomicAdd(occ + (blockIdx.x & (GWO_OCC_SHARDS - 1)) * GWO_OCC_SHARD_STRIDE, n);
+}
+
+// Adds the claims of the active lanes to their tables' occupancy: one atomic per (wave, table).
+__device__ __forceinline__ void count_claims(unsigned long long *occ, bool claimed) {
+    unsigned long long m = __ballot(claimed);
+    const int lane = threadIdx.x & 63;
+    while (m) {
+        int leader = __ffsll((long long)m) - 1;
+        unsigned long long *p = (unsigned long long *)__shfl((long long)occ, leader);
+        bool mine = claimed && occ == p;
+        unsigned long long peers = __ballot(mine);
+        if (lane == leader) occ_add(p, (unsigned long long)__popcll(peers));
+        if (mine) claimed = false;
+        m &= ~peers;
+    }
+}
+
+// Workgroup-wide exclusive prefix of v (blockDim.x a multiple of 64, <= 1024) plus ONE atomicAdd of
+// the workgroup total on *ctr: returns this thread's first output position.  Used by every kernel
+// that stream-compacts rows into a shared output, so a launch issues one atomic per workgroup
+// chunk, not one per lane or per wave.  Must be called by all threads of the workgroup.
+__device__ __forceinline__ unsigned long long block_reserve(unsigned v, unsigned long long *ctr) {
+    __shared__ unsigned s_wave[16];
+    __shared__ unsigned long long s_base;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    unsigned incl = v;
+    for (int o = 1; o < 64; o <<= 1) {
+        unsigned y = __shfl_up(incl, o);
+        if (lane >= o) incl += y;
+    }
+    if (lane == 63) s_wave[wid] = incl;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned run = 0;
+        for (int w = 0; w < nw; ++w) {
+            unsigned t = s_wave[w];
+            s_wave[w] = run;
+            run += t;
+        }
+        s_base = run ? atomicAdd(ctr, (unsigned long long)run) : 0ull;
+    }
+    __syncthreads();
+    unsigned long long r = s_base + s_wave[wid] + (incl - v);
+    __syncthreads();   // s_wave / s_base are reused by the next call
+    return r;
 }
 
 // Wave-level sum for counters: one atomic per wave.

@@ -128,10 +128,11 @@ gwo_status Handle::init(const gwo_config &c) {
     GWO_TRY(dalloc((void **)&d_stats, sizeof(BatchStats)));
     GWO_TRY(hipcheck(hipHostMalloc((void **)&h_stats, sizeof(BatchStats), hipHostMallocDefault), "pinned"));
     GWO_TRY(hipcheck(hipHostMalloc((void **)&h_stats_init, sizeof(BatchStats), hipHostMallocDefault), "pinned"));
-    const int kCounters = 1 << 14;
+    const int kCounters = 1 << 12;
     counter_used.assign(kCounters, 0);
-    GWO_TRY(dalloc((void **)&d_counters, kCounters * 8));
-    GWO_TRY(hipcheck(hipHostMalloc((void **)&h_counters, kCounters * 8, hipHostMallocDefault), "pinned"));
+    GWO_TRY(dalloc((void **)&d_counters, (size_t)kCounters * GWO_OCC_WORDS * 8));
+    GWO_TRY(hipcheck(hipHostMalloc((void **)&h_counters, (size_t)kCounters * GWO_OCC_WORDS * 8, hipHostMallocDefault),
+                     "pinned"));
     GWO_TRY(hipcheck(hipHostMalloc((void **)&h_scalar, 64, hipHostMallocDefault), "pinned"));
     GWO_TRY(hipcheck(hipHostMalloc((void **)&h_ident_side, GWO_MAX_WORDS * 16 + 16, hipHostMallocDefault), "pinned"));
     GWO_TRY(dalloc((void **)&d_out_count, 8));
@@ -139,7 +140,7 @@ gwo_status Handle::init(const gwo_config &c) {
     GWO_TRY(dalloc((void **)&d_side_count, 8));
     GWO_TRY(hipcheck(hipMemsetAsync(d_out_count, 0, 8, stream), "memset"));
     GWO_TRY(hipcheck(hipMemsetAsync(d_side_count, 0, 8, stream), "memset"));
-    GWO_TRY(hipcheck(hipMemsetAsync(d_counters, 0, kCounters * 8, stream), "memset"));
+    GWO_TRY(hipcheck(hipMemsetAsync(d_counters, 0, (size_t)kCounters * GWO_OCC_WORDS * 8, stream), "memset"));
     if (side_enabled()) GWO_TRY(grow_side(4096));
     if (c.assigner == GWO_ASSIGNER_SLIDING) GWO_TRY(slide_init());   // may append a hidden count word
     if (c.assigner == GWO_ASSIGNER_SESSION) GWO_TRY(session_init());

@@ -148,6 +148,17 @@ struct Handle {
     gwo_status hipcheck(hipError_t e, const char *what);
     gwo_status ensure_buf(DevBuf &b, size_t bytes);
     int take_counter();
+    // occupancy counter c: GWO_OCC_WORDS device words (sharded, see gwo_device.h occ_add)
+    unsigned long long *ctr(int c) const { return d_counters + (size_t)c * GWO_OCC_WORDS; }
+    uint64_t ctr_host(int c) const {
+        uint64_t s = 0;
+        for (int i = 0; i < GWO_OCC_SHARDS; ++i) s += h_counters[(size_t)c * GWO_OCC_WORDS + i * GWO_OCC_SHARD_STRIDE];
+        return s;
+    }
+    gwo_status ctr_zero(int c) {
+        return hipcheck(hipMemsetAsync(ctr(c), 0, GWO_OCC_WORDS * 8, stream), "counter reset");
+    }
+    gwo_status ctr_read(int c, uint64_t *v);   // D2H + sync
     gwo_status alloc_table(uint64_t cap, Table &t);
     void release_table(Table &t);
     void trim_pool();

@@ -14,6 +14,9 @@
 #define GWO_EMPTY_KEY ((int64_t)0x8000000000000000LL)
 #define GWO_MAX_WORDS 8
 #define GWO_HIST_BINS 64
+#define GWO_OCC_SHARDS 8          // occupancy counter shards (gwo_device.h occ_add)
+#define GWO_OCC_SHARD_STRIDE 8    // words between shards: one 64-B line each
+#define GWO_OCC_WORDS (GWO_OCC_SHARDS * GWO_OCC_SHARD_STRIDE)
 
 // Combine ops per accumulator word.  Every aggregate decomposes into word-wise commutative
 // monoids, so inserting a record, merging two partials (sessions, pre-aggregation) and folding
@@ -45,7 +48,7 @@ struct AccPlan {
 struct TableDesc {
     int64_t *base;                     // cap * stride words
     int64_t *side;                     // side slot for key == EMPTY_KEY: [flag, acc words...]
-    unsigned long long *occ;           // number of occupied slots (incl. side slot)
+    unsigned long long *occ;           // occupied slots (incl. side slot): GWO_OCC_SHARDS sharded words
     uint64_t mask;                     // cap - 1 (cap is a power of two)
 };
 

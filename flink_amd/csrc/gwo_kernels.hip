@@ -140,13 +140,17 @@ __global__ __launch_bounds__(256) void scan_kernel(const int64_t *__restrict__ k
 // insert (direct): one lane per record, device-scope atomics into the window's table
 // ------------------------------------------------------------------------------------------------
 __device__ __forceinline__ void apply_record(const TableDesc &t, const AccPlan &p, int64_t k, int64_t vbits) {
-    int64_t *acc = find_or_insert(t, p.stride, k);
+    bool claimed;
+    int64_t *acc = find_or_insert(t, p.stride, k, claimed);
+    count_claims(t.occ, claimed);
     for (int w = 0; w < p.nwords; ++w) atomic_combine(acc + w, p.op[w], lift_word(p, w, vbits));
 }
 
 // Ring update with live-entry accounting on the hidden count word.
 __device__ __forceinline__ void apply_ring(const RingDesc &r, const AccPlan &p, int64_t k, const int64_t *words) {
-    int64_t *acc = find_or_insert(r.t, p.stride, k);
+    bool claimed;
+    int64_t *acc = find_or_insert(r.t, p.stride, k, claimed);
+    count_claims(r.t.occ, claimed);
     for (int w = 0; w < p.nwords; ++w) {
         if (w == r.count_word) {
             unsigned long long old = atomicAdd((unsigned long long *)(acc + w), (unsigned long long)words[w]);
@@ -289,7 +293,10 @@ __global__ __launch_bounds__(256) void insert_preagg_kernel(const int64_t *__res
         for (int s = threadIdx.x; s < PREAGG_SLOTS; s += 256) {
             if (s_tag[s] == 0ull) continue;
             flushed++;
-            int64_t *a = find_or_insert(dir[s_unit[s]], p.stride, s_key[s]);
+            bool claimed;
+            const TableDesc &ft = dir[s_unit[s]];
+            int64_t *a = find_or_insert(ft, p.stride, s_key[s], claimed);
+            count_claims(ft.occ, claimed);
             for (int w = 0; w < NW; ++w) atomic_combine(a + w, p.op[w], s_acc[s * NW + w]);
             long long u = dir_base + s_unit[s];
             if (u >= ring.lo && u <= ring.hi) apply_ring(ring, p, s_key[s], &s_acc[s * NW]);
@@ -326,58 +333,50 @@ __device__ __forceinline__ void write_results(const AccPlan &p, const ResultPlan
     }
 }
 
+#define FIRE_FPT 8   // slots per thread per chunk: one output reservation per 2048 slots
+
+__device__ __forceinline__ const int64_t *fire_entry(const TableDesc &t, uint64_t cap, int stride, uint64_t i) {
+    return i < cap ? t.base + i * (uint64_t)stride : t.side;   // i == cap: the side slot
+}
+
 __global__ __launch_bounds__(256) void fire_kernel(TableDesc t, uint64_t cap, AccPlan p, ResultPlan rp, int64_t start,
                                                    int64_t end, OutCols o, int reset, int live_word) {
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    const int lane = threadIdx.x & 63;
+    constexpr uint64_t CH = 256 * FIRE_FPT;
+    const int NW = p.nwords;
     // +1 iteration space for the side slot (key == Long.MIN_VALUE)
-    for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x; base < cap + 1; base += stride) {
-        uint64_t i = base + threadIdx.x;
-        bool occ = false;
-        int64_t k = 0;
-        int64_t acc[GWO_MAX_WORDS];
-        const int NW = p.nwords;
-        int64_t *e = nullptr;
-        if (i < cap) {
-            e = t.base + i * (uint64_t)p.stride;
-            k = e[0];
-            occ = k != GWO_EMPTY_KEY;
-            if (occ) {
+    for (uint64_t b0 = (uint64_t)blockIdx.x * CH; b0 < cap + 1; b0 += (uint64_t)gridDim.x * CH) {
+        unsigned flags = 0, cnt = 0;
 #pragma unroll
-                for (int w = 0; w < GWO_MAX_WORDS; ++w)
-                    if (w < NW) acc[w] = e[1 + w];
-            }
-        } else if (i == cap) {
-            occ = t.side[0] != 0;
-            k = GWO_EMPTY_KEY;
+        for (int j = 0; j < FIRE_FPT; ++j) {
+            uint64_t i = b0 + (uint64_t)j * 256 + threadIdx.x;
+            if (i > cap) continue;
+            const int64_t *e = fire_entry(t, cap, p.stride, i);
+            bool occ = i < cap ? e[0] != GWO_EMPTY_KEY : e[0] != 0;
+            if (occ && live_word >= 0) occ = e[1 + live_word] > 0;
             if (occ) {
-#pragma unroll
-                for (int w = 0; w < GWO_MAX_WORDS; ++w)
-                    if (w < NW) acc[w] = t.side[1 + w];
+                flags |= 1u << j;
+                cnt++;
             }
         }
-        if (live_word >= 0 && occ) occ = acc[live_word] > 0;
-        unsigned long long m = __ballot(occ);
-        if (m == 0) continue;
-        unsigned long long wbase = 0;
-        if (lane == 0) wbase = atomicAdd(o.count, (unsigned long long)__popcll(m));
-        wbase = __shfl(wbase, 0);
-        if (occ) {
-            unsigned long long pos = wbase + __popcll(m & ((1ull << lane) - 1));
+        unsigned long long pos = block_reserve(cnt, o.count);
+        for (int j = 0; j < FIRE_FPT; ++j) {
+            if (!(flags >> j & 1u)) continue;
+            uint64_t i = b0 + (uint64_t)j * 256 + threadIdx.x;
+            int64_t *e = (int64_t *)fire_entry(t, cap, p.stride, i);
+            int64_t acc[GWO_MAX_WORDS];
+#pragma unroll
+            for (int w = 0; w < GWO_MAX_WORDS; ++w)
+                if (w < NW) acc[w] = e[1 + w];
             if ((long long)pos < o.cap) {
-                o.key[pos] = k;
+                o.key[pos] = i < cap ? e[0] : GWO_EMPTY_KEY;
                 o.start[pos] = start;
                 o.end[pos] = end;
                 write_results(p, rp, acc, o, pos);
             }
+            pos++;
             if (reset) {
-                if (i < cap) {
-                    e[0] = GWO_EMPTY_KEY;
-                    for (int w = 0; w < NW; ++w) e[1 + w] = p.ident[w];
-                } else {
-                    t.side[0] = 0;
-                    for (int w = 0; w < NW; ++w) t.side[1 + w] = p.ident[w];
-                }
+                e[0] = i < cap ? GWO_EMPTY_KEY : 0;
+                for (int w = 0; w < NW; ++w) e[1 + w] = p.ident[w];
             }
         }
     }
@@ -404,7 +403,9 @@ __global__ __launch_bounds__(256) void rehash_kernel(TableDesc src, uint64_t cap
             e[0] = GWO_EMPTY_KEY;
             continue;
         }
-        int64_t *a = find_or_insert(dst, p.stride, k);
+        bool claimed;
+        int64_t *a = find_or_insert(dst, p.stride, k, claimed);
+        count_claims(dst.occ, claimed);
         for (int w = 0; w < p.nwords; ++w) {
             a[w] = e[1 + w];
             e[1 + w] = p.ident[w];
@@ -430,7 +431,9 @@ __global__ __launch_bounds__(256) void fold_kernel(TableDesc src, uint64_t cap, 
             e = src.side;
             k = GWO_EMPTY_KEY;
         }
-        int64_t *a = find_or_insert(dst, p.stride, k);
+        bool claimed;
+        int64_t *a = find_or_insert(dst, p.stride, k, claimed);
+        count_claims(dst.occ, claimed);
         for (int w = 0; w < p.nwords; ++w) {
             int64_t x = e[1 + w];
             if (sign < 0) x = (int64_t)(0ull - (uint64_t)x);   // ACC_ADD_I64 only: wrap-around inverse
@@ -541,7 +544,7 @@ void launch_insert(const int64_t *key, const int64_t *ts, const void *val, int64
 
 void launch_fire(const TableDesc &t, uint64_t cap, const AccPlan &plan, const ResultPlan &rp, int64_t start,
                  int64_t end, OutCols out, int reset, int live_word, hipStream_t s) {
-    int grid = grid_for((int64_t)cap + 1, 1, 8192);
+    int grid = grid_for((int64_t)cap + 1, FIRE_FPT, 4096);
     hipLaunchKernelGGL(fire_kernel, dim3(grid), dim3(256), 0, s, t, cap, plan, rp, start, end, out, reset, live_word);
 }
 

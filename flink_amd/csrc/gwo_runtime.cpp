@@ -123,7 +123,15 @@ gwo_status Handle::alloc_table(uint64_t cap, Table &t) {
     t.counter = take_counter();
     if (t.counter < 0) return fail(GWO_ERR_OUT_OF_MEMORY, "too many live windows/panes (> %zu)", counter_used.size());
     t.occ = 0;
-    return hipcheck(hipMemsetAsync(d_counters + t.counter, 0, 8, stream), "counter");
+    return ctr_zero(t.counter);
+}
+
+gwo_status Handle::ctr_read(int c, uint64_t *v) {
+    GWO_TRY(hipcheck(hipMemcpyAsync(h_counters + (size_t)c * GWO_OCC_WORDS, ctr(c), GWO_OCC_WORDS * 8,
+                                    hipMemcpyDeviceToHost, stream), "occ"));
+    GWO_TRY(hipcheck(hipStreamSynchronize(stream), "occ sync"));
+    *v = ctr_host(c);
+    return GWO_OK;
 }
 
 void Handle::release_table(Table &t) {
@@ -143,7 +151,7 @@ TableDesc Handle::desc(const Table &t) const {
     TableDesc d;
     d.base = t.base;
     d.side = t.side;
-    d.occ = d_counters + t.counter;
+    d.occ = ctr(t.counter);
     d.mask = t.cap - 1;
     return d;
 }
@@ -178,7 +186,7 @@ gwo_status Handle::ensure_table(long long u, uint64_t incoming) {
                      "side copy"));
     GWO_TRY(reset_side(t));
     // occupancy moves with the entries
-    GWO_TRY(hipcheck(hipMemcpyAsync(d_counters + nt.counter, d_counters + t.counter, 8, hipMemcpyDeviceToDevice, stream),
+    GWO_TRY(hipcheck(hipMemcpyAsync(ctr(nt.counter), ctr(t.counter), GWO_OCC_WORDS * 8, hipMemcpyDeviceToDevice, stream),
                      "occ copy"));
     GWO_TRY(hipcheck(hipStreamSynchronize(stream), "rehash"));
     nt.occ = t.occ;
@@ -202,10 +210,11 @@ gwo_status Handle::read_occupancy() {
     for (auto &kv : tables) hi = std::max(hi, kv.second.counter + 1);
     for (auto &kv : aux_tables) hi = std::max(hi, kv.counter + 1);
     if (hi == 0) return hipcheck(hipStreamSynchronize(stream), "occ sync");   // callers rely on the sync
-    GWO_TRY(hipcheck(hipMemcpyAsync(h_counters, d_counters, (size_t)hi * 8, hipMemcpyDeviceToHost, stream), "occ"));
+    GWO_TRY(hipcheck(hipMemcpyAsync(h_counters, d_counters, (size_t)hi * GWO_OCC_WORDS * 8, hipMemcpyDeviceToHost, stream),
+                     "occ"));
     GWO_TRY(hipcheck(hipStreamSynchronize(stream), "occ sync"));
-    for (auto &kv : tables) kv.second.occ = h_counters[kv.second.counter];
-    for (auto &t : aux_tables) t.occ = h_counters[t.counter];
+    for (auto &kv : tables) kv.second.occ = ctr_host(kv.second.counter);
+    for (auto &t : aux_tables) t.occ = ctr_host(t.counter);
     return GWO_OK;
 }
 

@@ -43,7 +43,7 @@ gwo_status Handle::sess_alloc(uint64_t cap, Table &t) {
     t.counter = take_counter();
     if (t.counter < 0) return fail(GWO_ERR_OUT_OF_MEMORY, "counter slots exhausted");
     t.occ = 0;
-    return hipcheck(hipMemsetAsync(d_counters + t.counter, 0, 8, stream), "counter");
+    return ctr_zero(t.counter);
 }
 
 gwo_status Handle::session_init() {
@@ -116,11 +116,7 @@ gwo_status Handle::sess_ensure(uint64_t incoming) {
 }
 
 gwo_status Handle::read_occupancy_one(Table &t) {
-    GWO_TRY(hipcheck(hipMemcpyAsync(h_counters + t.counter, d_counters + t.counter, 8, hipMemcpyDeviceToHost, stream),
-                     "occ"));
-    GWO_TRY(hipcheck(hipStreamSynchronize(stream), "occ sync"));
-    t.occ = h_counters[t.counter];
-    return GWO_OK;
+    return ctr_read(t.counter, &t.occ);
 }
 
 gwo_status Handle::insert_session(const int64_t *k, const int64_t *t, const int64_t *v, int64_t n) {

@@ -36,7 +36,9 @@ __global__ __launch_bounds__(256) void sess_slot_kernel(const int64_t *__restric
             atomicAdd(&err->bad_kg, 1ull);
             err->bad_kg_key = k;
         }
-        int64_t *a = find_or_insert(t, stride, k);
+        bool claimed;
+        int64_t *a = find_or_insert(t, stride, k, claimed);
+        count_claims(t.occ, claimed);
         rec_slot[i] = k == GWO_EMPTY_KEY ? (uint32_t)cap : (uint32_t)((a - 1 - t.base) / stride);
     }
 }
@@ -239,7 +241,9 @@ __global__ __launch_bounds__(256) void sess_compact_kernel(TableDesc src, uint64
         int64_t *e = src.base + i * (uint64_t)stride;
         int64_t k = e[0];
         if (k == GWO_EMPTY_KEY || e[1] == 0) continue;
-        int64_t *a = find_or_insert(dst, stride, k) - 1;
+        bool claimed;
+        int64_t *a = find_or_insert(dst, stride, k, claimed) - 1;
+        count_claims(dst.occ, claimed);
         for (int w = 1; w < stride; ++w) a[w] = e[w];
     }
 }

@@ -143,7 +143,7 @@ gwo_status Handle::ring_rebuild() {
     launch_fill(T0.base, T0.cap, plan, stream);
     GWO_TRY(launch_ok("fill"));
     GWO_TRY(reset_side(T0));
-    GWO_TRY(hipcheck(hipMemsetAsync(d_counters + T0.counter, 0, 8, stream), "occ reset"));
+    GWO_TRY(ctr_zero(T0.counter));
     GWO_TRY(hipcheck(hipMemsetAsync(S.d_live, 0, 8, stream), "live reset"));
     T0.occ = 0;
     GWO_TRY(read_occupancy());
@@ -218,10 +218,8 @@ gwo_status Handle::fire_sliding(int64_t new_wm) {
             for (auto it = tables.lower_bound(lo); it != tables.end() && it->first <= hi; ++it)
                 launch_fold(desc(it->second), it->second.cap, desc(W), plan, +1, -1, nullptr, stream);
             prof_end(GWO_KERNEL_SLIDE, (int64_t)total);
-            GWO_TRY(hipcheck(hipMemcpyAsync(h_counters + W.counter, d_counters + W.counter, 8, hipMemcpyDeviceToHost,
-                                            stream), "w occ"));
-            GWO_TRY(hipcheck(hipStreamSynchronize(stream), "w occ sync"));
-            uint64_t rows = h_counters[W.counter];
+            uint64_t rows = 0;
+            GWO_TRY(ctr_read(W.counter, &rows));
             GWO_TRY(ensure_output(rows));
             o = out_cols();
             prof_begin(GWO_KERNEL_FIRE);
