@@ -11,7 +11,7 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libgwo.so")
 
-GWO_ABI_VERSION = 1
+GWO_ABI_VERSION = 2
 GWO_MAX_AGGS = 4
 
 # gwo_status
@@ -25,6 +25,7 @@ ASSIGNER_TUMBLING, ASSIGNER_SLIDING, ASSIGNER_SESSION = 0, 1, 2
 AGG_COUNT, AGG_SUM, AGG_MIN, AGG_MAX, AGG_AVG = 0, 1, 2, 3, 4
 DTYPE_INT64, DTYPE_FLOAT64 = 0, 1
 KEY_LONG, KEY_INT = 0, 1
+STATE_AUTO, STATE_TABLE, STATE_LOG = 0, 1, 2
 KERNEL_SCAN, KERNEL_INSERT, KERNEL_FIRE, KERNEL_PARTITION, KERNEL_EXCHANGE, KERNEL_SLIDE, KERNEL_SESSION = range(7)
 COMM_ID_BYTES = 128
 
@@ -37,7 +38,8 @@ class GwoConfig(C.Structure):
         ("num_aggs", C.c_int32), ("aggs", C.c_int32 * GWO_MAX_AGGS),
         ("value_dtype", C.c_int32), ("key_kind", C.c_int32), ("max_parallelism", C.c_int32),
         ("key_group_start", C.c_int32), ("key_group_end", C.c_int32), ("device", C.c_int32),
-        ("side_output", C.c_int32), ("expected_keys", C.c_int64), ("stream", C.c_void_p),
+        ("side_output", C.c_int32), ("state_layout", C.c_int32), ("expected_keys", C.c_int64),
+        ("stream", C.c_void_p),
     ]
 
 

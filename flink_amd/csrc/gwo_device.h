@@ -30,6 +30,36 @@ __device__ __host__ __forceinline__ int64_t floor_div(int64_t a, int64_t b) {
     return (a % b != 0 && ((a < 0) != (b < 0))) ? q - 1 : q;
 }
 
+// floor(a / d) for d > 0, exact for every int64 a, without the ~150-instruction 64-bit integer
+// division: a double-precision reciprocal estimate, one refinement on the (small) remainder, and
+// exact integer corrections.  Products wrap, which is harmless because the true remainder fits.
+__device__ __forceinline__ int64_t fdiv_floor(int64_t a, int64_t d, double inv) {
+    double x = (double)a * inv;
+    x = x > 9.2e18 ? 9.2e18 : (x < -9.2e18 ? -9.2e18 : x);
+    int64_t q = (int64_t)x;
+    int64_t r = jsub(a, (int64_t)((uint64_t)q * (uint64_t)d));
+    q += (int64_t)((double)r * inv);
+    r = jsub(a, (int64_t)((uint64_t)q * (uint64_t)d));
+    while (r < 0) {
+        q -= 1;
+        r = jadd(r, d);
+    }
+    while (r >= d) {
+        q += 1;
+        r = jsub(r, d);
+    }
+    return q;
+}
+// Java '%' (truncating) for d > 0 via fdiv_floor.
+__device__ __forceinline__ int64_t jrem_f(int64_t a, int64_t d, double inv) {
+    int64_t fm = jsub(a, (int64_t)((uint64_t)fdiv_floor(a, d, inv) * (uint64_t)d));   // floorMod in [0, d)
+    return (a < 0 && fm != 0) ? fm - d : fm;
+}
+// TimeWindow.getWindowStartWithOffset with the fast remainder (TimeWindow.java:270-272).
+__device__ __forceinline__ int64_t window_start_f(int64_t ts, int64_t off, int64_t size, double inv) {
+    return jsub(ts, jrem_f(jadd(jsub(ts, off), size), size, inv));
+}
+
 // WindowOperator.cleanupTime (WindowOperator.java:639-646): maxTs + lateness, Long.MAX_VALUE on overflow.
 __device__ __host__ __forceinline__ int64_t cleanup_time(int64_t max_ts, int64_t lateness) {
     int64_t c = jadd(max_ts, lateness);
@@ -81,6 +111,15 @@ __device__ __forceinline__ uint64_t slot_hash(int64_t key) {
     k *= 0xc4ceb9fe1a85ec53ull;
     k ^= k >> 33;
     return k;
+}
+
+// Partition hash of the log-structured state (gwo_log.hip): a bijective 64-bit mix, different from
+// slot_hash.  Top 8 bits = coarse digit, top lp bits = partition, low bits = LDS slot.
+__device__ __forceinline__ uint64_t part_hash(int64_t key) {
+    uint64_t z = (uint64_t)key + 0x632BE59BD9B4E019ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
 }
 
 // Double.compareTo total order as a signed int64 key (doubleToLongBits canonicalises NaN).
@@ -199,6 +238,33 @@ __device__ __forceinline__ unsigned long long block_reserve(unsigned v, unsigned
     __syncthreads();
     unsigned long long r = s_base + s_wave[wid] + (incl - v);
     __syncthreads();   // s_wave / s_base are reused by the next call
+    return r;
+}
+
+// Workgroup-wide exclusive prefix sum of v (all threads call it); *total gets the sum.
+__device__ __forceinline__ unsigned block_exclusive_scan(unsigned v, unsigned *total) {
+    __shared__ unsigned s_w[16];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    unsigned incl = v;
+    for (int o = 1; o < 64; o <<= 1) {
+        unsigned y = __shfl_up(incl, o);
+        if (lane >= o) incl += y;
+    }
+    if (lane == 63) s_w[wid] = incl;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned run = 0;
+        for (int w = 0; w < nw; ++w) {
+            unsigned t = s_w[w];
+            s_w[w] = run;
+            run += t;
+        }
+        s_w[15] = run;   // nw <= 15 for the 512-thread kernels that use this
+    }
+    __syncthreads();
+    unsigned r = s_w[wid] + incl - v;
+    *total = s_w[15];
+    __syncthreads();
     return r;
 }
 

@@ -112,6 +112,9 @@ gwo_status Handle::init(const gwo_config &c) {
         geom.unit_off_mod = floor_mod(c.offset, geom.unit);
     }
 
+    if (geom.size > 0) geom.inv_size = 1.0 / (double)geom.size;
+    if (geom.slide > 0) geom.inv_slide = 1.0 / (double)geom.slide;
+    if (geom.unit > 0) geom.inv_unit = 1.0 / (double)geom.unit;
     debug = getenv("GWO_DEBUG") != nullptr;
     const char *pa = getenv("GWO_PREAGG");
     if (pa) cfg_preagg = atoi(pa) ? 1 : 0;
@@ -144,6 +147,13 @@ gwo_status Handle::init(const gwo_config &c) {
     if (side_enabled()) GWO_TRY(grow_side(4096));
     if (c.assigner == GWO_ASSIGNER_SLIDING) GWO_TRY(slide_init());   // may append a hidden count word
     if (c.assigner == GWO_ASSIGNER_SESSION) GWO_TRY(session_init());
+    if (c.state_layout < GWO_STATE_AUTO || c.state_layout > GWO_STATE_LOG)
+        return fail(GWO_ERR_INVALID_ARGUMENT, "state layout %d", c.state_layout);
+    if (c.state_layout == GWO_STATE_LOG && c.assigner != GWO_ASSIGNER_TUMBLING)
+        return fail(GWO_ERR_UNSUPPORTED, "the log-structured state layout serves tumbling windows only");
+    if (c.assigner == GWO_ASSIGNER_TUMBLING &&
+        (c.state_layout == GWO_STATE_LOG || (c.state_layout == GWO_STATE_AUTO && c.expected_keys >= (1 << 20))))
+        GWO_TRY(log_init());
     memset(h_ident_side, 0, GWO_MAX_WORDS * 16 + 16);
     for (int w = 0; w < plan.nwords; ++w) h_ident_side[1 + w] = plan.ident[w];
     return hipcheck(hipStreamSynchronize(stream), "init");
@@ -154,6 +164,7 @@ Handle::~Handle() {
     if (stream) (void)hipStreamSynchronize(stream);
     (void)prof_collect();
     comm_free();
+    log_free();
     session_free();
     slide_free();
     for (auto &kv : tables) (void)hipFree(kv.second.base);
@@ -198,6 +209,7 @@ gwo_status Handle::submit(const int64_t *key, const int64_t *ts, const void *val
 gwo_status Handle::submit_local(const int64_t *k, const int64_t *t, const int64_t *v, int64_t n) {
     if (n == 0) return GWO_OK;
     if (cfg.assigner == GWO_ASSIGNER_SESSION) return insert_session(k, t, v, n);
+    if (logst) return insert_log(k, t, v, n);
     return insert_windowed(k, t, v, n);
 }
 
@@ -205,7 +217,7 @@ gwo_status Handle::advance_watermark(int64_t new_wm) {
     if (comm) GWO_TRY(comm_min_watermark(new_wm, &new_wm));
     gwo_status s = GWO_OK;
     switch (cfg.assigner) {
-        case GWO_ASSIGNER_TUMBLING: s = fire_tumbling(new_wm); break;
+        case GWO_ASSIGNER_TUMBLING: s = logst ? fire_log(new_wm) : fire_tumbling(new_wm); break;
         case GWO_ASSIGNER_SLIDING: s = fire_sliding(new_wm); break;
         default: s = fire_session(new_wm); break;
     }
@@ -262,6 +274,7 @@ gwo_status Handle::drain_side(const gwo_side_out *cols, int64_t cap, int64_t *n_
 
 gwo_status Handle::state_size(int64_t *entries) {
     if (cfg.assigner == GWO_ASSIGNER_SESSION) return session_state_size(entries);
+    if (logst) return log_state_size(entries);
     GWO_TRY(read_occupancy());
     int64_t s = 0;
     for (auto &kv : tables) s += (int64_t)kv.second.occ;

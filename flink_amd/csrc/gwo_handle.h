@@ -66,6 +66,8 @@ struct PendingEvent {
 struct SessionState;   // gwo_session.cpp
 struct SlideState;     // gwo_slide.cpp
 struct Comm;           // gwo_comm.cpp
+struct LogState;       // gwo_log.cpp
+struct LogWindow;
 
 struct Handle {
     static constexpr double kMaxLoad = 0.7;   // grow above this load factor
@@ -132,6 +134,7 @@ struct Handle {
     SessionState *sess = nullptr;
     SlideState *slide = nullptr;
     Comm *comm = nullptr;
+    LogState *logst = nullptr;                 // non-null: log-structured tumbling state
 
     ~Handle();
     gwo_status init(const gwo_config &c);
@@ -207,6 +210,15 @@ struct Handle {
     gwo_status insert_session(const int64_t *k, const int64_t *t, const int64_t *v, int64_t n);
     gwo_status fire_session(int64_t new_wm);
     gwo_status session_state_size(int64_t *entries);
+    // log-structured tumbling state (gwo_log.cpp)
+    gwo_status log_init();
+    void log_free();
+    gwo_status log_carve(LogWindow &W, size_t bytes, char **out);
+    void log_release(LogWindow &W);
+    int log_choose_lp(uint64_t batch_records) const;
+    gwo_status insert_log(const int64_t *k, const int64_t *t, const int64_t *v, int64_t n);
+    gwo_status fire_log(int64_t new_wm);
+    gwo_status log_state_size(int64_t *entries);
     // comm (gwo_comm.cpp)
     void comm_free();
     gwo_status comm_exchange(const int64_t *k, const int64_t *t, const int64_t *v, int64_t n, const int64_t **rk,

@@ -89,6 +89,9 @@ struct WindowGeom {
     int64_t offset;                    // assigner offset
     int64_t lateness;
     int64_t wm;                        // current watermark when the batch is processed
+    double inv_size;                   // 1.0 / size, 1.0 / slide, 1.0 / unit: fast exact division
+    double inv_slide;                  //   (gwo_device.h fdiv_floor)
+    double inv_unit;
     int32_t sliding;
     int32_t key_kind;
     int32_t max_par;

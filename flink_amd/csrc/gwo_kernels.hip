@@ -24,15 +24,15 @@ __device__ __forceinline__ int classify(int64_t ts, const WindowGeom &g, long lo
     if (ts == GWO_LONG_MIN) return REC_BAD_TS;
     int64_t last_start, first_start;
     if (!g.sliding) {
-        last_start = window_start(ts, g.offset, g.size);
+        last_start = window_start_f(ts, g.offset, g.size, g.inv_size);
         first_start = last_start;
     } else {
         // Java's '%' gives a start > ts for ts - offset + slide < 0; the pane restatement covers
         // the well-defined range only and rejects the rest loudly (never a silent difference).
         if (jadd(jsub(ts, g.offset), g.slide) < 0) return REC_BAD_SLIDE;
-        last_start = window_start(ts, g.offset, g.slide);
+        last_start = window_start_f(ts, g.offset, g.slide, g.inv_slide);
         // smallest start s = last_start - k*slide with s > ts - size
-        int64_t k = (jsub(last_start, jsub(ts, g.size)) - 1) / g.slide;
+        int64_t k = fdiv_floor(jsub(last_start, jsub(ts, g.size)) - 1, g.slide, g.inv_slide);
         first_start = jsub(last_start, k * g.slide);
     }
     int64_t last_max_ts = jsub(jadd(last_start, g.size), 1);
@@ -51,10 +51,11 @@ __device__ __forceinline__ int classify(int64_t ts, const WindowGeom &g, long lo
         }
     }
     if (!g.sliding) {
-        unit_idx = floor_div(last_start, g.size);
+        unit_idx = fdiv_floor(last_start, g.size, g.inv_size);
     } else {
-        int64_t pane_start = jsub(ts, jsub(jsub(ts, g.unit_off), floor_div(jsub(ts, g.unit_off), g.unit) * g.unit));
-        unit_idx = floor_div(pane_start, g.unit);
+        int64_t pane_start =
+            jsub(ts, jsub(jsub(ts, g.unit_off), fdiv_floor(jsub(ts, g.unit_off), g.unit, g.inv_unit) * g.unit));
+        unit_idx = fdiv_floor(pane_start, g.unit, g.inv_unit);
     }
     return REC_ACCEPT;
 }
@@ -462,10 +463,11 @@ __global__ void key_groups_kernel(const int64_t *keys, int64_t n, int kind, int 
     }
 }
 
-__global__ void window_starts_kernel(const int64_t *ts, int64_t n, int64_t off, int64_t size, int64_t *out) {
+__global__ void window_starts_kernel(const int64_t *ts, int64_t n, int64_t off, int64_t size, double inv,
+                                     int64_t *out) {
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
-        out[i] = window_start(ts[i], off, size);
+        out[i] = window_start_f(ts[i], off, size, inv);
 }
 
 // Counter-based splitmix64 source (identical definition in oracle/gen.py):
@@ -579,7 +581,8 @@ void launch_key_groups(const int64_t *keys, int64_t n, int key_kind, int max_par
 
 void launch_window_starts(const int64_t *ts, int64_t n, int64_t offset, int64_t size, int64_t *out,
                           hipStream_t s) {
-    hipLaunchKernelGGL(window_starts_kernel, dim3(grid_for(n, 4)), dim3(256), 0, s, ts, n, offset, size, out);
+    hipLaunchKernelGGL(window_starts_kernel, dim3(grid_for(n, 4)), dim3(256), 0, s, ts, n, offset, size,
+                       1.0 / (double)size, out);
 }
 
 void launch_generate(uint64_t seed, int64_t first, int64_t total, int64_t nkeys, int64_t span, int64_t disorder,

@@ -30,7 +30,7 @@ class GpuWindowOperator:
     def __init__(self, assigner: WindowAssigner, aggregate: AggregateFunction, allowed_lateness: int = 0,
                  side_output_late_data: bool = False, max_parallelism: int = 128, key_group_range=None,
                  key_kind: str = "long", device: int = 0, batch_size: int = 1 << 20, expected_keys: int = 0,
-                 stream=None):
+                 stream=None, state_layout: str = "auto"):
         if allowed_lateness < 0:
             raise ValueError("The allowed lateness cannot be negative.")
         self._lib = N.lib()
@@ -54,6 +54,10 @@ class GpuWindowOperator:
         cfg.device = device
         cfg.side_output = 1 if side_output_late_data else 0
         cfg.expected_keys = expected_keys
+        layouts = {"auto": N.STATE_AUTO, "table": N.STATE_TABLE, "log": N.STATE_LOG}
+        if state_layout not in layouts:
+            raise ValueError(f"state_layout must be one of {sorted(layouts)}")
+        cfg.state_layout = layouts[state_layout]
         cfg.stream = stream
         h = C.c_void_p()
         st = self._lib.gwo_create(C.byref(cfg), C.byref(h))

@@ -50,7 +50,7 @@
 extern "C" {
 #endif
 
-#define GWO_ABI_VERSION 1
+#define GWO_ABI_VERSION 2
 #define GWO_MAX_AGGS 4
 
 typedef enum {
@@ -83,6 +83,13 @@ typedef enum {
 
 typedef enum { GWO_DTYPE_INT64 = 0, GWO_DTYPE_FLOAT64 = 1 } gwo_dtype;
 
+/* Device layout of the keyed window state.  Both give identical results. */
+typedef enum {
+    GWO_STATE_AUTO = 0,           /* tumbling: LOG when expected_keys >= 2^20, else TABLE; others TABLE */
+    GWO_STATE_TABLE = 1,          /* open-addressed HBM hash table per window/pane, updated per batch */
+    GWO_STATE_LOG = 2             /* tumbling only: per-window partitioned record log, folded in LDS at fire */
+} gwo_state_layout;
+
 typedef enum {
     GWO_KEY_LONG = 0,             /* key.hashCode() = Long.hashCode: (int)(v ^ (v >>> 32)) */
     GWO_KEY_INT = 1               /* key.hashCode() = Integer.hashCode: (int)v; key must fit in int32 */
@@ -105,6 +112,7 @@ typedef struct {
     int32_t key_group_end;
     int32_t device;               /* HIP device ordinal */
     int32_t side_output;          /* 1: late records go to the side output instead of being counted */
+    int32_t state_layout;         /* gwo_state_layout */
     int64_t expected_keys;        /* sizing hint: distinct keys per window (0 = grow on demand) */
     void *stream;                 /* hipStream_t to run on; NULL: the handle creates its own */
 } gwo_config;

@@ -11,6 +11,9 @@ pytestmark = pytest.mark.gpu
 
 LONG_MIN, LONG_MAX = -(1 << 63), (1 << 63) - 1
 FLOAT_RTOL = 1e-6
+# tumbling windows run on both device state layouts: per-window hash tables, and the
+# per-window partitioned record log folded in LDS at fire -- results must be identical
+LAYOUTS = pytest.mark.parametrize("layout", ["table", "log"])
 
 
 @pytest.fixture(scope="module")
@@ -85,9 +88,9 @@ def test_generator_kernel_matches_numpy(F):
 
 
 # ---- the reference's operator streams (WindowOperatorTest / examples) ----------------------------
-def _run_stream(F, s, agg=None):
+def _run_stream(F, s, agg=None, layout="auto"):
     op = F.GpuWindowOperator(mk(F, s["assigner"]), agg or F.SumAggregate(), allowed_lateness=s["lateness"],
-                             side_output_late_data=s["side_output"])
+                             side_output_late_data=s["side_output"], state_layout=layout)
     for ev in s["events"]:
         if ev[0] == "e":
             op.process_element(ev[1], ev[2], ev[3])
@@ -109,6 +112,53 @@ def test_reference_operator_streams(F, golden, name):
     assert sorted(op.side_output) == sorted(map(tuple, s.get("side", [])))
     assert op.num_late_records_dropped == s["late"]
     op.close()
+
+
+@pytest.mark.parametrize("name", ["tumbling_3s", "side_output_lateness_tumbling", "cleanup_time_overflow"])
+def test_reference_tumbling_streams_log_layout(F, golden, name):
+    s = next(x for x in golden["operator_streams"] if x["name"] == name)
+    if s["assigner"]["kind"] != "tumbling":
+        pytest.skip("log layout serves tumbling windows")
+    op = _run_stream(F, s, layout="log")
+    assert sorted(op.output) == sorted(map(tuple, s["expected"]))
+    assert sorted(op.side_output) == sorted(map(tuple, s.get("side", [])))
+    assert op.num_late_records_dropped == s["late"]
+    op.close()
+
+
+def test_log_layout_multi_round_partitions(F):
+    """One window fed by many small batches: the window's partitions (sized from its first batch)
+    end up holding ~10x the LDS table, so the fire kernel folds them in hash rounds."""
+    k, t, v, b = _c1(n=1_000_000, nkeys=200_000, every=10_000, lag=100, disorder=50)
+    agg = F.MultiAggregate(F.SumAggregate(), F.MinAggregate(), F.MaxAggregate())
+    op = F.GpuWindowOperator(F.TumblingEventTimeWindows.of(60000), agg, state_layout="log")
+    _run_batches(op, k, t, v, b)
+    (wk, ws, we, res), late = V.tumbling_lateness0(k, t, v, _final(b), 60000, 0, [1, 2, 3])
+    got = sorted((a, s, e, *r) for a, s, e, r in op.output)
+    assert got == _want(wk, ws, we, res)
+    assert op.num_late_records_dropped == late
+    op.close()
+
+
+def test_log_layout_hot_key(F):
+    """Half the records on one key: its partition is huge but holds one distinct key."""
+    k, t, v, b = _c1(n=400_000, nkeys=20_000, every=20_000)
+    k = k.copy()
+    k[::2] = 7
+    op = F.GpuWindowOperator(F.TumblingEventTimeWindows.of(5000), F.MultiAggregate(F.SumAggregate(), F.CountAggregate()),
+                             state_layout="log")
+    _run_batches(op, k, t, v, b)
+    (wk, ws, we, res), _ = V.tumbling_lateness0(k, t, v, _final(b), 5000, 0, [1, 0])
+    got = sorted((a, s, e, *r) for a, s, e, r in op.output)
+    assert got == _want(wk, ws, we, res)
+    op.close()
+
+
+def test_log_layout_rejected_for_sliding(F):
+    from flink_amd import _native as N
+    with pytest.raises(N.GwoError) as ei:
+        F.GpuWindowOperator(F.SlidingEventTimeWindows.of(3000, 1000), F.SumAggregate(), state_layout="log")
+    assert ei.value.status_name == "GWO_ERR_UNSUPPORTED"
 
 
 # ---- randomized parity against the oracle -------------------------------------------------------
@@ -142,10 +192,11 @@ def _final(batches):
     return batches + [(batches[-1][0], LONG_MAX)]
 
 
-def test_c1_tumbling_sum_bit_exact(F):
+@LAYOUTS
+def test_c1_tumbling_sum_bit_exact(F, layout):
     """Config 1: 1M records, 10K Long keys, 5 s tumbling sum, watermark every 10K records."""
     k, t, v, b = _c1()
-    op = F.GpuWindowOperator(F.TumblingEventTimeWindows.of(5000), F.SumAggregate())
+    op = F.GpuWindowOperator(F.TumblingEventTimeWindows.of(5000), F.SumAggregate(), state_layout=layout)
     _run_batches(op, k, t, v, b)
     (wk, ws, we, res), late = V.tumbling_lateness0(k, t, v, _final(b), 5000, 0, [1])
     got = _rows(op)
@@ -156,12 +207,13 @@ def test_c1_tumbling_sum_bit_exact(F):
 
 
 @pytest.mark.parametrize("lag", [0, 200])
-def test_tumbling_multi_agg_with_late_records(F, lag):
+@LAYOUTS
+def test_tumbling_multi_agg_with_late_records(F, lag, layout):
     """sum/min/max/count with disorder larger than the lag: late drops must match exactly."""
     k, t, v, b = _c1(n=300_000, nkeys=50_000, every=3_000, lag=lag, disorder=1500, seed=3)
     v = v - 500
     op = F.GpuWindowOperator(F.TumblingEventTimeWindows.of(2000, 300),
-                             F.MultiAggregate(F.SumAggregate(), F.MinAggregate(), F.MaxAggregate(), F.CountAggregate()))
+                             F.MultiAggregate(F.SumAggregate(), F.MinAggregate(), F.MaxAggregate(), F.CountAggregate()), state_layout=layout)
     _run_batches(op, k, t, v, b)
     (wk, ws, we, res), late = V.tumbling_lateness0(k, t, v, _final(b), 2000, 300, [1, 2, 3, 0])
     assert late > 0
@@ -171,20 +223,22 @@ def test_tumbling_multi_agg_with_late_records(F, lag):
     op.close()
 
 
-def test_tumbling_avg_int_bit_exact(F):
+@LAYOUTS
+def test_tumbling_avg_int_bit_exact(F, layout):
     k, t, v, b = _c1(n=200_000, nkeys=3_000, every=5_000)
-    op = F.GpuWindowOperator(F.TumblingEventTimeWindows.of(10000), F.AverageAggregate())
+    op = F.GpuWindowOperator(F.TumblingEventTimeWindows.of(10000), F.AverageAggregate(), state_layout=layout)
     _run_batches(op, k, t, v, b)
     (wk, ws, we, res), _ = V.tumbling_lateness0(k, t, v, _final(b), 10000, 0, [4])
     assert _rows(op) == _want(wk, ws, we, res)   # (double)sum/count is exactly rounded on both sides
     op.close()
 
 
-def test_tumbling_float64_sum_avg_min_max(F):
+@LAYOUTS
+def test_tumbling_float64_sum_avg_min_max(F, layout):
     k, t, v, b = _c1(n=200_000, nkeys=2_000, every=5_000, vdt="float64")
     agg = F.MultiAggregate(F.SumAggregate("float64"), F.AverageAggregate("float64"), F.MinAggregate("float64"),
                            F.MaxAggregate("float64"))
-    op = F.GpuWindowOperator(F.TumblingEventTimeWindows.of(5000), agg)
+    op = F.GpuWindowOperator(F.TumblingEventTimeWindows.of(5000), agg, state_layout=layout)
     _run_batches(op, k, t, v, b)
     (wk, ws, we, res), _ = V.tumbling_lateness0(k, t, v, _final(b), 5000, 0, [1, 4, 2, 3], value_is_f64=True)
     got = sorted((a, s, e, *r) for a, s, e, r in op.output)
@@ -197,10 +251,11 @@ def test_tumbling_float64_sum_avg_min_max(F):
     op.close()
 
 
-def test_high_cardinality_growth_and_rehash(F):
+@LAYOUTS
+def test_high_cardinality_growth_and_rehash(F, layout):
     """1M distinct keys in few windows: tables start small and must grow (rehash) mid-stream."""
     k, t, v, b = _c1(n=2_000_000, nkeys=1_000_000, every=400_000)
-    op = F.GpuWindowOperator(F.TumblingEventTimeWindows.of(20000), F.MultiAggregate(F.SumAggregate(), F.MaxAggregate()))
+    op = F.GpuWindowOperator(F.TumblingEventTimeWindows.of(20000), F.MultiAggregate(F.SumAggregate(), F.MaxAggregate()), state_layout=layout)
     _run_batches(op, k, t, v, b)
     (wk, ws, we, res), late = V.tumbling_lateness0(k, t, v, _final(b), 20000, 0, [1, 3])
     got = sorted((a, s, e, *r) for a, s, e, r in op.output)
@@ -208,9 +263,10 @@ def test_high_cardinality_growth_and_rehash(F):
     op.close()
 
 
-def test_count_only_without_value_column(F):
+@LAYOUTS
+def test_count_only_without_value_column(F, layout):
     k, t, _, b = _c1(n=100_000, nkeys=1000, every=10_000)
-    op = F.GpuWindowOperator(F.TumblingEventTimeWindows.of(10000), F.CountAggregate())
+    op = F.GpuWindowOperator(F.TumblingEventTimeWindows.of(10000), F.CountAggregate(), state_layout=layout)
     prev = 0
     for end, wm in b:
         op.process_batch(k[prev:end], t[prev:end], None)
@@ -222,9 +278,10 @@ def test_count_only_without_value_column(F):
     op.close()
 
 
-def test_extreme_keys_and_timestamps(F):
+@LAYOUTS
+def test_extreme_keys_and_timestamps(F, layout):
     """Long.MIN_VALUE as a key (the table's EMPTY sentinel) and negative timestamps (Java '%')."""
-    op = F.GpuWindowOperator(F.TumblingEventTimeWindows.of(5), F.SumAggregate())
+    op = F.GpuWindowOperator(F.TumblingEventTimeWindows.of(5), F.SumAggregate(), state_layout=layout)
     ref = O.WindowOperatorOracle(O.TumblingEventTimeWindows(5), O.SumLongAgg())
     events = [(LONG_MIN, -7, 1), (LONG_MIN, -6, 2), (LONG_MAX, -7, 3), (0, -12, 4), (-1, 3, 5), (LONG_MIN, 4, 6)]
     for key, ts, val in events:
@@ -236,10 +293,11 @@ def test_extreme_keys_and_timestamps(F):
     op.close()
 
 
-def test_key_group_violation_fails_like_the_task(F):
+@LAYOUTS
+def test_key_group_violation_fails_like_the_task(F, layout):
     from flink_amd import _native as N
     op = F.GpuWindowOperator(F.TumblingEventTimeWindows.of(1000), F.SumAggregate(), max_parallelism=128,
-                             key_group_range=(0, 63))
+                             key_group_range=(0, 63), state_layout=layout)
     keys = np.arange(100)
     kg = np.array([O.assign_to_key_group(O.long_hash_code(int(x)), 128) for x in keys])
     with pytest.raises(N.GwoError) as ei:
@@ -248,21 +306,23 @@ def test_key_group_violation_fails_like_the_task(F):
     op.close()
 
 
-def test_no_timestamp_fails(F):
+@LAYOUTS
+def test_no_timestamp_fails(F, layout):
     from flink_amd import _native as N
-    op = F.GpuWindowOperator(F.TumblingEventTimeWindows.of(1000), F.SumAggregate())
+    op = F.GpuWindowOperator(F.TumblingEventTimeWindows.of(1000), F.SumAggregate(), state_layout=layout)
     with pytest.raises(N.GwoError) as ei:
         op.process_batch(np.array([1, 2]), np.array([5, LONG_MIN]), np.array([1, 1]))
     assert ei.value.status_name == "GWO_ERR_NO_TIMESTAMP"
     op.close()
 
 
-def test_batch_boundaries_do_not_change_results(F):
+@LAYOUTS
+def test_batch_boundaries_do_not_change_results(F, layout):
     """Same stream, different batch splits between the same watermarks -> identical output."""
     k, t, v, b = _c1(n=120_000, nkeys=5_000, every=6_000, lag=300, disorder=900)
     outs = []
     for split in (1, 7):
-        op = F.GpuWindowOperator(F.TumblingEventTimeWindows.of(3000), F.SumAggregate())
+        op = F.GpuWindowOperator(F.TumblingEventTimeWindows.of(3000), F.SumAggregate(), state_layout=layout)
         prev = 0
         for end, wm in b:
             edges = np.linspace(prev, end, split + 1).astype(int)
@@ -410,3 +470,17 @@ def test_sessions_out_of_order_with_lateness(F, lateness):
     if lateness == 0:
         assert ref.num_late_records_dropped > 0
     op.close()
+
+
+def test_fast_division_full_int64_range(F):
+    """window_start_f/fdiv_floor (double reciprocal + exact corrections) against Java semantics over
+    the whole int64 range, including the extremes and sizes from 1 to Long.MAX_VALUE."""
+    rng = np.random.default_rng(11)
+    ts = np.concatenate([rng.integers(LONG_MIN, LONG_MAX, 20000, dtype=np.int64),
+                         np.array([LONG_MIN + 1, LONG_MAX, LONG_MAX - 1, 0, -1, 1, -(1 << 62), 1 << 62],
+                                  dtype=np.int64)])
+    for size in [1, 2, 3, 7, 1000, 86_400_000, (1 << 40) + 7, (1 << 62) + 3, LONG_MAX]:
+        for off in sorted({0, size // 3, -(size // 5)}):
+            got = F.window_starts(ts, off, size)
+            want = [O.get_window_start_with_offset(int(t), off, size) for t in ts]
+            assert got.tolist() == want, (size, off)
