@@ -6,10 +6,13 @@ windows, sum/min/max over an int64 value, maxParallelism 32768, event time spann
 U[0, 1 s) disorder and punctuated watermarks (lag 1 s) once per second of event time.  Per GPU the
 stream is 1e9 records (16.7M per step); the input is generated into HBM before the timed region.
 
-A "step" = one watermark interval: gwo_submit(batch) (scan + insert into the per-window HBM
-tables) + gwo_advance_watermark (fire kernels emit every window whose end passed).  With --gpus N
-the job runs one process per GPU; every rank generates its own slice of a 100M*N-key stream and
-gwo_submit shuffles records to their key-group owner with an RCCL all-to-all (weak scaling).
+A "step" = one watermark interval: gwo_submit(batch) (classify + partition into the windows'
+record logs) + gwo_advance_watermark (fire: fold every window whose end passed and
+emit its rows).  The default warmup (12 steps) covers one full window lifecycle (first fire at step
+10), so the timed steps are the engine's steady state (device pools warm, output sized); 20 timed
+steps include two fires.  With --gpus N the job runs one process per GPU; every rank generates its
+own slice of a 100M*N-key stream and gwo_submit shuffles records to their key-group owner with an
+RCCL all-to-all (weak scaling).
 
 Prints ONE JSON line (rank 0).
 """
@@ -29,8 +32,8 @@ import numpy as np  # noqa: E402
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=30)
-    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=12)   # one full window lifecycle: pools warm
     p.add_argument("--records-per-gpu", type=int, default=1_000_000_000)
     p.add_argument("--keys-per-gpu", type=int, default=100_000_000)
     p.add_argument("--span-ms", type=int, default=60_000)
@@ -97,7 +100,9 @@ def main():
     else:
         rng = (0, a.max_parallelism - 1)
     agg = F.MultiAggregate(F.SumAggregate(), F.MinAggregate(), F.MaxAggregate())
-    exp_keys = int(a.keys_per_gpu * 0.9)
+    # sizing hint = expected distinct keys per window: uniform keys, records_per_window draws
+    rec_per_window = R * a.window_ms // span
+    exp_keys = int(a.keys_per_gpu * (1.0 - np.exp(-rec_per_window / a.keys_per_gpu)))
     op = F.GpuWindowOperator(F.TumblingEventTimeWindows.of(a.window_ms), agg, max_parallelism=a.max_parallelism,
                              key_group_range=rng, device=local, expected_keys=exp_keys)
     h = op.handle
@@ -110,15 +115,21 @@ def main():
         uid = (C.c_uint8 * N.COMM_ID_BYTES)(*t_uid.cpu().tolist())
         N.check(lib.gwo_comm_init(h, uid, world, rank), h, "gwo_comm_init")
 
+    fired_rows = [0]
+
     def step(i):
         s, e = bounds[i]
         N.check(lib.gwo_submit(h, C.c_void_p(key.data_ptr() + 8 * s), C.c_void_p(ts.data_ptr() + 8 * s),
                                C.c_void_p(val.data_ptr() + 8 * s), e - s), h, "submit")
         N.check(lib.gwo_advance_watermark(h, wms[i]), h, "watermark")
+        nrow = C.c_int64()
+        N.check(lib.gwo_output_count(h, C.byref(nrow)), h)
+        fired_rows[0] += nrow.value
         N.check(lib.gwo_discard_output(h), h)   # rows stay in HBM; the sink is not part of the path
 
     for i in range(a.warmup):
         step(i)
+    fired_rows[0] = 0
     N.check(lib.gwo_sync(h), h)
     lib.gwo_reset_stats(h)
     lib.gwo_set_profiling(h, 1)
@@ -141,9 +152,9 @@ def main():
         lib.gwo_kernel_stats(h, k, C.byref(la), C.byref(ms), C.byref(it))
         return la.value, ms.value, it.value
 
-    ins = kstat(N.KERNEL_INSERT)
-    fire = kstat(N.KERNEL_FIRE)
-    scan = kstat(N.KERNEL_SCAN)
+    stats = {name: kstat(k) for name, k in (("scan", N.KERNEL_SCAN), ("insert", N.KERNEL_INSERT),
+                                             ("fire", N.KERNEL_FIRE), ("partition", N.KERNEL_PARTITION),
+                                             ("exchange", N.KERNEL_EXCHANGE))}
     records = (nsteps - a.warmup) * rec_per_step
     if dist:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
@@ -155,10 +166,14 @@ def main():
     else:
         total_records = records
 
-    # ---- roofline of the dominant kernel (insert): algorithmic bytes per launch ----
-    # B_alg(insert) = n*I + U*2*S per launch; I = 24 B (key, ts, value), S = 32 B (key + sum/min/max;
-    # the window start is implicit in the per-window table), U = distinct (key, window) per batch.
-    I_B, S_B, O_B = 24, 32, 48
+    # ---- algorithmic bytes ----
+    # path:   B_alg = N*I + U*2S + F*(S+O); I = 24 B (key, ts, value), S = 40 B (key, window, sum, min,
+    #         max), O = 48 B (key, start, end, sum, min, max), U = distinct (key, window) per batch,
+    #         F = fired rows.
+    # kernels (log layout, the C4 default): log_part reads I per record and appends 16 B per accepted
+    #         (key, value); log_split moves 16 B in + 16 B out per logged record; log_fire reads the
+    #         window's 16-B records and writes O per row.
+    I_B, S_B, O_B, REC_B = 24, 40, 48, 16
     u_tot = 0
     if rank == 0:
         wnd = a.window_ms
@@ -166,18 +181,35 @@ def main():
             s, e = bounds[i]
             pair = key[s:e] * 64 + torch.div(ts[s:e], wnd, rounding_mode="floor")
             u_tot += int(torch.unique(pair).numel())
-    ins_launches, ins_ms, _ = ins
-    fire_launches, fire_ms, fire_slots = fire
-    alg_insert = (records * I_B + u_tot * 2 * S_B) / max(ins_launches, 1)
-    avg_ins_s = ins_ms / max(ins_launches, 1) / 1e3
-    achieved = alg_insert / avg_ins_s / 1e9 if avg_ins_s > 0 else 0.0
+    rows = fired_rows[0]
+    path_bytes = records * I_B + u_tot * 2 * S_B + rows * (S_B + O_B)
+    kern = {
+        "insert": ("log_part_kernel", records * (I_B + REC_B)),
+        "partition": ("log_split_kernel", records * 2 * REC_B),
+        "fire": ("log_fire_kernel", stats["fire"][2] * REC_B + rows * O_B),
+    }
+    if stats["partition"][0] == 0:   # table layout: scan + insert + fire sweep
+        kern = {"insert": ("insert_direct_kernel", records * I_B + u_tot * 2 * 32),
+                "fire": ("fire_kernel", stats["fire"][2] * 32 + rows * O_B)}
+    dom = max(kern, key=lambda k: stats[k][1])
+    dname, dbytes = kern[dom]
+    dl, dms, _ = stats[dom]
+    avg_ms = dms / max(dl, 1)
+    achieved = dbytes / max(dl, 1) / (avg_ms / 1e3) / 1e9 if avg_ms > 0 else 0.0
     peak = 8000.0
+    traffic = None
+    tfile = os.path.join(ROOT, "profiles", "traffic.json")
+    if os.path.exists(tfile):
+        t = json.load(open(tfile)).get(dname)
+        if t:
+            traffic = t["hbm_bytes_per_launch"]
 
     out = None
     if rank == 0:
         cpu = None
         if not a.no_cpu_baseline:
             cpu = cpu_baseline(a, key, ts, val, bounds, wms)
+        ms_per_step = elapsed / a.steps * 1e3
         out = {
             "metric": "records/sec per node, keyed window agg @1/2/4/8 GPU; % of HBM peak",
             "value": total_records / elapsed,
@@ -185,7 +217,7 @@ def main():
             "n_gpus": world,
             "steps": a.steps,
             "warmup": a.warmup,
-            "ms_per_step": elapsed / a.steps * 1e3,
+            "ms_per_step": ms_per_step,
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
@@ -196,11 +228,14 @@ def main():
                        "window_ms": a.window_ms, "watermark_every_ms": a.wm_interval_ms, "lag_ms": a.lag_ms,
                        "max_parallelism": a.max_parallelism, "parallelism": f"keyBy over {world} GPU(s)"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": peak, "unit": "GB/s",
-                         "frac": achieved / peak, "traffic": None, "kernel": "insert_direct_kernel",
-                         "alg_bytes_per_launch": alg_insert, "avg_launch_ms": avg_ins_s * 1e3,
-                         "distinct_entries_per_launch": u_tot / max(ins_launches, 1)},
-            "kernels_ms": {"scan": scan[1], "insert": ins_ms, "fire": fire_ms,
-                           "fire_launches": fire_launches, "fire_slots": fire_slots},
+                         "frac": achieved / peak, "traffic": traffic, "kernel": dname,
+                         "alg_bytes_per_launch": dbytes / max(dl, 1), "avg_launch_ms": avg_ms,
+                         "launches": dl, "traffic_source": "profiles/traffic.json (rocprofv3 PMC)" if traffic else None},
+            "roofline_path": {"alg_bytes_per_step": path_bytes / a.steps,
+                              "achieved": path_bytes / elapsed / 1e9, "unit": "GB/s",
+                              "frac": path_bytes / elapsed / 1e9 / peak,
+                              "distinct_entries_per_step": u_tot / a.steps, "fired_rows_per_step": rows / a.steps},
+            "kernels_ms": {k: {"launches": v[0], "total_ms": v[1]} for k, v in stats.items() if v[0]},
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)

@@ -9,7 +9,8 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libgwo.so")
+# GWO_LIB_PATH selects an alternative build of the same library (A/B kernel experiments)
+LIB_PATH = os.environ.get("GWO_LIB_PATH") or os.path.join(_HERE, "libgwo.so")
 
 GWO_ABI_VERSION = 2
 GWO_MAX_AGGS = 4

@@ -243,7 +243,7 @@ __device__ __forceinline__ unsigned long long block_reserve(unsigned v, unsigned
 
 // Workgroup-wide exclusive prefix sum of v (all threads call it); *total gets the sum.
 __device__ __forceinline__ unsigned block_exclusive_scan(unsigned v, unsigned *total) {
-    __shared__ unsigned s_w[16];
+    __shared__ unsigned s_w[17];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
     unsigned incl = v;
     for (int o = 1; o < 64; o <<= 1) {
@@ -259,11 +259,11 @@ __device__ __forceinline__ unsigned block_exclusive_scan(unsigned v, unsigned *t
             s_w[w] = run;
             run += t;
         }
-        s_w[15] = run;   // nw <= 15 for the 512-thread kernels that use this
+        s_w[16] = run;
     }
     __syncthreads();
     unsigned r = s_w[wid] + incl - v;
-    *total = s_w[15];
+    *total = s_w[16];
     __syncthreads();
     return r;
 }

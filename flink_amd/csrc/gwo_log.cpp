@@ -1,10 +1,12 @@
 // gwo_log.cpp -- host side of the log-structured tumbling-window state (kernels: gwo_log.hip).
 //
 // Bookkeeping only: which windows are open, the device memory of their segments, the partition
-// count of each window, and the per-batch scan/scatter/fire launch sequence.  The reference's
-// equivalents are the window-contents state table and the timer queue of WindowOperator
-// (WindowOperator.java:218-273 open(), :430-473 onEventTime, InternalTimerServiceImpl.java:268-278).
+// count of each window, bucket/partition capacities, and the per-batch partition/split/fire launch
+// sequence.  The reference's equivalents are the window-contents state table and the timer queue
+// of WindowOperator (WindowOperator.java:218-273 open(), :430-473 onEventTime,
+// InternalTimerServiceImpl.java:268-278).
 #include <algorithm>
+#include <cmath>
 #include <cstring>
 #include <map>
 #include <vector>
@@ -30,30 +32,43 @@ struct LogWindow {
 struct LogState {
     std::map<long long, LogWindow> wins;
     std::multimap<size_t, char *> free_chunks;
-    DevBuf tkey, tval, cbase, segdesc, firedesc;
-    unsigned *d_chist = nullptr;
-    unsigned *h_chist = nullptr;                 // pinned [LOG_UNITS * 256]
-    unsigned long long *h_cbase = nullptr;       // pinned [LOG_UNITS * 256 + 1]
-    LogSegDesc *h_desc = nullptr;                // pinned [LOG_UNITS]
+    DevBuf tmp, buckets, segdesc, firedesc;
+    unsigned long long *d_cursor = nullptr;      // [LOG_NU * 256 * LOG_CUR_STRIDE] bucket cursors of K1
+    unsigned long long *d_counts = nullptr;      // [LOG_NU * 256] gathered cursor values
+    unsigned long long *h_cursor = nullptr;      // pinned copy
+    unsigned *d_split_ovf = nullptr;
+    LogBucket *h_buckets = nullptr;              // pinned [LOG_NU * 256 + 1]
+    LogSegDesc *h_desc = nullptr;                // pinned [LOG_NU]
     std::vector<LogSegDesc> h_fire;
     unsigned long long *d_overflow = nullptr;
-    uint64_t last_window_records = 0;
+    uint64_t last_window_keys = 0;               // distinct keys of the last fired window
+    uint64_t last_window_records = 0;            // records of the last fired window
+    long long span_hint = 1;                     // windows the previous batch spanned
     int cap_log2 = 0;
+    int max_groups = 0;                          // persistent fire workgroups (2 per CU)
 };
 
 static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
+// Capacity of a fixed-size group that receives Binomial(n, 1/k) records: mean + 6 sigma + slack.
+static uint64_t group_capacity(double mean) {
+    return (uint64_t)std::ceil(mean + 6.0 * std::sqrt(mean) + 4.0);
+}
+
 gwo_status Handle::log_init() {
     logst = new LogState();
     LogState &L = *logst;
-    GWO_TRY(dalloc((void **)&L.d_chist, LOG_UNITS * 256 * sizeof(unsigned)));
-    GWO_TRY(dalloc((void **)&L.d_overflow, 8));
-    GWO_TRY(hipcheck(hipMemsetAsync(L.d_overflow, 0, 8, stream), "overflow"));
-    GWO_TRY(hipcheck(hipHostMalloc((void **)&L.h_chist, LOG_UNITS * 256 * sizeof(unsigned), hipHostMallocDefault), "pinned"));
-    GWO_TRY(hipcheck(hipHostMalloc((void **)&L.h_cbase, (LOG_UNITS * 256 + 1) * 8, hipHostMallocDefault), "pinned"));
-    GWO_TRY(hipcheck(hipHostMalloc((void **)&L.h_desc, LOG_UNITS * sizeof(LogSegDesc), hipHostMallocDefault), "pinned"));
-    GWO_TRY(ensure_buf(L.cbase, (LOG_UNITS * 256 + 1) * 8 * 2));
-    GWO_TRY(ensure_buf(L.segdesc, LOG_UNITS * sizeof(LogSegDesc)));
+    GWO_TRY(dalloc((void **)&L.d_cursor, LOG_NU * 256 * LOG_CUR_STRIDE * 8));
+    GWO_TRY(dalloc((void **)&L.d_counts, LOG_NU * 256 * 8));
+    GWO_TRY(dalloc((void **)&L.d_split_ovf, 8));
+    GWO_TRY(dalloc((void **)&L.d_overflow, 16));
+    GWO_TRY(hipcheck(hipMemsetAsync(L.d_overflow, 0, 16, stream), "overflow"));
+    GWO_TRY(hipcheck(hipHostMalloc((void **)&L.h_cursor, LOG_NU * 256 * 8, hipHostMallocDefault), "pinned"));
+    GWO_TRY(hipcheck(hipHostMalloc((void **)&L.h_buckets, (LOG_NU * 256 + 1) * sizeof(LogBucket), hipHostMallocDefault),
+                     "pinned"));
+    GWO_TRY(hipcheck(hipHostMalloc((void **)&L.h_desc, LOG_NU * sizeof(LogSegDesc), hipHostMallocDefault), "pinned"));
+    GWO_TRY(ensure_buf(L.buckets, (LOG_NU * 256 + 1) * sizeof(LogBucket)));
+    GWO_TRY(ensure_buf(L.segdesc, LOG_NU * sizeof(LogSegDesc)));
     L.cap_log2 = log_fire_cap_log2(plan.nwords);
     return GWO_OK;
 }
@@ -64,15 +79,16 @@ void Handle::log_free() {
     for (auto &kv : L.wins)
         for (auto &c : kv.second.chunks) (void)hipFree(c.base);
     for (auto &kv : L.free_chunks) (void)hipFree(kv.second);
-    L.tkey.release();
-    L.tval.release();
-    L.cbase.release();
+    L.tmp.release();
+    L.buckets.release();
     L.segdesc.release();
     L.firedesc.release();
-    if (L.d_chist) (void)hipFree(L.d_chist);
+    if (L.d_cursor) (void)hipFree(L.d_cursor);
+    if (L.d_counts) (void)hipFree(L.d_counts);
+    if (L.d_split_ovf) (void)hipFree(L.d_split_ovf);
     if (L.d_overflow) (void)hipFree(L.d_overflow);
-    if (L.h_chist) (void)hipHostFree(L.h_chist);
-    if (L.h_cbase) (void)hipHostFree(L.h_cbase);
+    if (L.h_cursor) (void)hipHostFree(L.h_cursor);
+    if (L.h_buckets) (void)hipHostFree(L.h_buckets);
     if (L.h_desc) (void)hipHostFree(L.h_desc);
     delete logst;
     logst = nullptr;
@@ -83,7 +99,7 @@ gwo_status Handle::log_carve(LogWindow &W, size_t bytes, char **out) {
     bytes = align256(bytes);
     if (W.chunks.empty() || W.chunks.back().size - W.chunks.back().used < bytes) {
         size_t want = 1 << 20;
-        while (want < bytes * 4 && want < ((size_t)512 << 20)) want <<= 1;
+        while (want < bytes * 4 && want < ((size_t)1 << 30)) want <<= 1;
         want = std::max(want, bytes);
         LogChunk c;
         auto it = logst->free_chunks.lower_bound(want);
@@ -117,39 +133,141 @@ void Handle::log_release(LogWindow &W) {
     W.segs.clear();
 }
 
-// Partitions of a new window: about 5/8 of the fire kernel's LDS table per partition, sized from
-// the previous window's record count, the caller's key hint and what this batch already brings.
+// Partitions of a new window: about 3/4 of the fire kernel's fast-path capacity (FIRE_RCAP records)
+// per partition, from the last fired window's record count, else the caller's distinct-key hint
+// (records >= keys; x2 covers the usual duplication) or this batch's size.  An underestimate only
+// sends partitions to the fire's slow path.
 int Handle::log_choose_lp(uint64_t batch_records) const {
     const LogState &L = *logst;
-    uint64_t est = std::max<uint64_t>(L.last_window_records, (uint64_t)std::max<int64_t>(cfg.expected_keys, 0) * 2);
-    est = std::max<uint64_t>(est, batch_records * 8);
-    uint64_t per = ((uint64_t)1 << L.cap_log2) * 5 / 8;
-    int lp = 0;
+    uint64_t est = L.last_window_records;
+    if (est == 0) est = std::max<uint64_t>((uint64_t)std::max<int64_t>(cfg.expected_keys, 0) * 2, batch_records * 8);
+    const uint64_t per = (uint64_t)FIRE_RCAP * 3 / 4;
+    int lp = LOG_MIN_LP;
     while (lp < LOG_MAX_LP && ((uint64_t)1 << lp) * per < est) lp++;
     return lp;
+}
+
+// Pass 2 for windows [base, base + nunits) of the batch buffer (bucket counts in h_cursor).
+gwo_status Handle::log_split_chunk(long long base, int nunits, uint64_t cap) {
+    LogState &L = *logst;
+    const int W = needs_value ? 2 : 1;
+    const int nb = nunits * 256;
+    std::vector<LogWindow *> wins(nunits, nullptr);
+    std::vector<uint64_t> wcount(nunits, 0);
+    for (int b = 0; b < nb; ++b) wcount[b >> 8] += L.h_cursor[b];
+    std::vector<uint32_t> pcap_exact(nb, 0);   // after an overflow: the measured partition maximum
+    while (true) {
+        uint32_t chunks = 0;
+        for (int w = 0; w < nunits; ++w) {
+            LogSegDesc d{};
+            const int c0 = w * 256;
+            if (wcount[w]) {
+                long long u = base + w;
+                auto it = L.wins.find(u);
+                if (it == L.wins.end()) {
+                    LogWindow Wn;
+                    Wn.lp = log_choose_lp(wcount[w]);
+                    it = L.wins.emplace(u, std::move(Wn)).first;
+                }
+                wins[w] = &it->second;
+                const int lp = it->second.lp, F = 1 << (lp - 8);
+                uint64_t seg = 0;
+                for (int dgt = 0; dgt < 256; ++dgt) {
+                    const uint64_t n_b = L.h_cursor[c0 + dgt];
+                    LogBucket &B = L.h_buckets[c0 + dgt];
+                    B.src = (uint64_t)(c0 + dgt) * cap;
+                    B.n = (uint32_t)n_b;
+                    B.pcap = n_b ? std::max<uint32_t>((uint32_t)group_capacity((double)n_b / F), pcap_exact[c0 + dgt])
+                                 : 0u;
+                    B.seg_base = (uint32_t)seg;
+                    B.chunk0 = chunks;
+                    seg += (uint64_t)F * B.pcap;
+                    chunks += (uint32_t)((n_b + LOG_TILE - 1) / LOG_TILE);
+                }
+                if (seg >= (1ull << 32)) return poison(GWO_ERR_CAPACITY, "log layout: batch segment exceeds 2^32 records");
+                char *p = nullptr;
+                GWO_TRY(log_carve(it->second, seg * W * 8, &p));
+                d.rec = (int64_t *)p;
+                GWO_TRY(log_carve(it->second, ((size_t)1 << lp) * 4, &p));
+                d.off = (uint32_t *)p;
+                GWO_TRY(log_carve(it->second, ((size_t)1 << lp) * 4, &p));
+                d.cnt = (uint32_t *)p;
+                d.lp = lp;
+                GWO_TRY(hipcheck(hipMemsetAsync(d.cnt, 0, ((size_t)1 << lp) * 4, stream), "segment counts"));
+            } else {
+                for (int dgt = 0; dgt < 256; ++dgt) {
+                    LogBucket &B = L.h_buckets[c0 + dgt];
+                    B = LogBucket{};
+                    B.chunk0 = chunks;
+                }
+            }
+            L.h_desc[w] = d;
+        }
+        L.h_buckets[nb] = LogBucket{};
+        L.h_buckets[nb].chunk0 = chunks;
+        GWO_TRY(hipcheck(hipMemcpyAsync(L.buckets.ptr, L.h_buckets, (nb + 1) * sizeof(LogBucket), hipMemcpyHostToDevice,
+                                        stream), "buckets"));
+        GWO_TRY(hipcheck(hipMemcpyAsync(L.segdesc.ptr, L.h_desc, nunits * sizeof(LogSegDesc), hipMemcpyHostToDevice,
+                                        stream), "segdesc"));
+        GWO_TRY(hipcheck(hipMemsetAsync(L.d_split_ovf, 0, 4, stream), "split overflow"));
+        prof_begin(GWO_KERNEL_PARTITION);
+        launch_log_split((const int64_t *)L.tmp.ptr, needs_value, (const LogBucket *)L.buckets.ptr, nb, nunits,
+                         (const LogSegDesc *)L.segdesc.ptr, L.d_split_ovf, chunks, stream);
+        GWO_TRY(launch_ok("log split"));
+        uint64_t total = 0;
+        for (int w = 0; w < nunits; ++w) total += wcount[w];
+        prof_end(GWO_KERNEL_PARTITION, (int64_t)total);
+        GWO_TRY(hipcheck(hipMemcpyAsync(h_scalar, L.d_split_ovf, 4, hipMemcpyDeviceToHost, stream), "split overflow"));
+        GWO_TRY(hipcheck(hipStreamSynchronize(stream), "log split"));
+        if ((uint32_t)h_scalar[0] == 0) break;
+        // a partition received more than its capacity (skewed keys): the cursors hold the exact
+        // counts, so redo with each bucket's partitions sized to its largest one (the segments
+        // carved above stay unused until the window is released)
+        for (int w = 0; w < nunits; ++w) {
+            if (!wins[w]) continue;
+            const int F = 1 << (L.h_desc[w].lp - 8);
+            std::vector<uint32_t> cnt((size_t)256 * F);
+            GWO_TRY(hipcheck(hipMemcpy(cnt.data(), L.h_desc[w].cnt, cnt.size() * 4, hipMemcpyDeviceToHost), "counts"));
+            for (int dgt = 0; dgt < 256; ++dgt)
+                for (int f = 0; f < F; ++f)
+                    pcap_exact[w * 256 + dgt] = std::max(pcap_exact[w * 256 + dgt], cnt[(size_t)dgt * F + f]);
+        }
+    }
+    for (int w = 0; w < nunits; ++w) {
+        if (!wins[w]) continue;
+        wins[w]->segs.push_back(L.h_desc[w]);
+        wins[w]->records += wcount[w];
+    }
+    return GWO_OK;
 }
 
 gwo_status Handle::insert_log(const int64_t *k, const int64_t *t, const int64_t *v, int64_t n) {
     LogState &L = *logst;
     WindowGeom g = geom_now();
     BatchStats &hs = *h_stats;
+    const int W = needs_value ? 2 : 1;
     long long base = hist_hint;
+    int nunits = (int)std::min<long long>(LOG_NU, std::max<long long>(1, L.span_hint));
+    uint64_t cap = group_capacity((double)n / 256.0);
     bool first_pass = true;
     long long lo = 0, hi = -1;
-    const int64_t *val = needs_value ? v : nullptr;
     while (true) {
+        GWO_TRY(ensure_buf(L.tmp, (size_t)nunits * 256 * cap * W * 8));
         init_stats(base);
-        GWO_TRY(hipcheck(hipMemsetAsync(L.d_chist, 0, LOG_UNITS * 256 * sizeof(unsigned), stream), "chist"));
-        prof_begin(GWO_KERNEL_SCAN);
-        launch_log_scan(k, t, v, n, g, base, d_stats, L.d_chist, (int64_t *)side_key.ptr, (int64_t *)side_ts.ptr,
-                        (int64_t *)side_val.ptr, d_side_count, first_pass && side_enabled() ? side_cap : 0,
-                        first_pass && side_enabled(), stream);
-        GWO_TRY(launch_ok("log scan"));
-        prof_end(GWO_KERNEL_SCAN, n);
+        GWO_TRY(hipcheck(hipMemsetAsync(L.d_cursor, 0, (size_t)nunits * 256 * LOG_CUR_STRIDE * 8, stream), "cursor"));
+        prof_begin(GWO_KERNEL_INSERT);
+        launch_log_part(k, t, v, n, g, base, nunits, needs_value, L.d_cursor, cap, (int64_t *)L.tmp.ptr, d_stats,
+                        (int64_t *)side_key.ptr, (int64_t *)side_ts.ptr, (int64_t *)side_val.ptr, d_side_count,
+                        first_pass && side_enabled() ? side_cap : 0, first_pass && side_enabled(), stream);
+        GWO_TRY(launch_ok("log partition"));
+        prof_end(GWO_KERNEL_INSERT, n);
         GWO_TRY(hipcheck(hipMemcpyAsync(h_stats, d_stats, sizeof(BatchStats), hipMemcpyDeviceToHost, stream), "stats"));
-        GWO_TRY(hipcheck(hipMemcpyAsync(L.h_chist, L.d_chist, LOG_UNITS * 256 * sizeof(unsigned), hipMemcpyDeviceToHost,
-                                        stream), "chist"));
-        GWO_TRY(hipcheck(hipStreamSynchronize(stream), "log scan sync"));
+        launch_log_gather(L.d_cursor, L.d_counts, nunits * 256, stream);
+        GWO_TRY(hipcheck(hipMemcpyAsync(L.h_cursor, L.d_counts, (size_t)nunits * 256 * 8, hipMemcpyDeviceToHost, stream),
+                         "cursor"));
+        if (first_pass && side_enabled())
+            GWO_TRY(hipcheck(hipMemcpyAsync(h_scalar, d_side_count, 8, hipMemcpyDeviceToHost, stream), "side count"));
+        GWO_TRY(hipcheck(hipStreamSynchronize(stream), "log partition sync"));
         if (first_pass) {
             if (hs.bad_ts) return poison(GWO_ERR_NO_TIMESTAMP,
                                          "Record has Long.MIN_VALUE timestamp (= no timestamp marker). Is the time "
@@ -163,8 +281,6 @@ gwo_status Handle::insert_log(const int64_t *k, const int64_t *t, const int64_t 
                                                              std::to_string(cfg.key_group_start) + ", endKeyGroup=" +
                                                              std::to_string(cfg.key_group_end) + "}.").c_str());
             if (side_enabled()) {
-                GWO_TRY(hipcheck(hipMemcpyAsync(h_scalar, d_side_count, 8, hipMemcpyDeviceToHost, stream), "side count"));
-                GWO_TRY(hipcheck(hipStreamSynchronize(stream), "side count sync"));
                 side_rows = *h_scalar;
                 if ((long long)side_rows > side_cap) {
                     side_rows = side_rows_committed;
@@ -182,77 +298,26 @@ gwo_status Handle::insert_log(const int64_t *k, const int64_t *t, const int64_t 
             lo = hs.min_idx;
             hi = hs.max_idx;
             first_pass = false;
-            if (base > lo || base + LOG_UNITS <= lo) {
+            if (base > lo || base + nunits <= lo) {   // wrong window range guess: redo from the first window
                 base = lo;
+                nunits = (int)std::min<long long>(LOG_NU, hi - lo + 1);
                 continue;
             }
         }
-        const long long chunk_hi = std::min<long long>(hi, base + LOG_UNITS - 1);
-        const int nunits = (int)(chunk_hi - base + 1);
-        const int nb = nunits * 256;
-        // coarse bucket bases (exclusive scan) and per-window record counts
-        uint64_t run = 0;
-        std::vector<uint64_t> wcount(nunits, 0);
-        for (int b = 0; b < nb; ++b) {
-            L.h_cbase[b] = run;
-            run += L.h_chist[b];
-            wcount[b >> 8] += L.h_chist[b];
+        uint64_t maxc = 0;
+        for (int b = 0; b < nunits * 256; ++b) maxc = std::max<uint64_t>(maxc, L.h_cursor[b]);
+        if (maxc > cap) {   // a bucket overflowed its capacity (skewed keys): redo this range exactly
+            cap = maxc;
+            continue;
         }
-        L.h_cbase[nb] = run;
-        const uint64_t total = run;
-        if (total > 0) {
-            GWO_TRY(ensure_buf(L.tkey, total * 8));
-            if (val) GWO_TRY(ensure_buf(L.tval, total * 8));
-            // cursors (consumed by pass 1) and a pristine copy of the bases (read by pass 2)
-            unsigned long long *d_cursor = (unsigned long long *)L.cbase.ptr;
-            unsigned long long *d_cb = d_cursor + (LOG_UNITS * 256 + 1);
-            GWO_TRY(hipcheck(hipMemcpyAsync(d_cursor, L.h_cbase, (nb + 1) * 8, hipMemcpyHostToDevice, stream), "cursor"));
-            GWO_TRY(hipcheck(hipMemcpyAsync(d_cb, L.h_cbase, (nb + 1) * 8, hipMemcpyHostToDevice, stream), "cbase"));
-            for (int w = 0; w < nunits; ++w) {
-                LogSegDesc d{};
-                if (wcount[w]) {
-                    long long u = base + w;
-                    auto it = L.wins.find(u);
-                    if (it == L.wins.end()) {
-                        LogWindow W;
-                        W.lp = log_choose_lp(wcount[w]);
-                        it = L.wins.emplace(u, std::move(W)).first;
-                    }
-                    LogWindow &W = it->second;
-                    d.lp = W.lp;
-                    char *p = nullptr;
-                    GWO_TRY(log_carve(W, wcount[w] * 8, &p));
-                    d.key = (int64_t *)p;
-                    if (val) {
-                        GWO_TRY(log_carve(W, wcount[w] * 8, &p));
-                        d.val = (int64_t *)p;
-                    }
-                    GWO_TRY(log_carve(W, (((size_t)1 << W.lp) + 1) * 4, &p));
-                    d.off = (uint32_t *)p;
-                    W.segs.push_back(d);
-                    W.records += wcount[w];
-                }
-                L.h_desc[w] = d;
-            }
-            GWO_TRY(hipcheck(hipMemcpyAsync(L.segdesc.ptr, L.h_desc, nunits * sizeof(LogSegDesc), hipMemcpyHostToDevice,
-                                            stream), "segdesc"));
-            prof_begin(GWO_KERNEL_INSERT);
-            launch_log_pass1(k, t, val, n, g, base, nunits, d_cursor, (int64_t *)L.tkey.ptr,
-                             val ? (int64_t *)L.tval.ptr : nullptr, stream);
-            GWO_TRY(launch_ok("log pass1"));
-            prof_end(GWO_KERNEL_INSERT, n);
-            prof_begin(GWO_KERNEL_PARTITION);
-            launch_log_pass2((const int64_t *)L.tkey.ptr, val ? (const int64_t *)L.tval.ptr : nullptr, d_cb, nunits,
-                             (const LogSegDesc *)L.segdesc.ptr, stream);
-            GWO_TRY(launch_ok("log pass2"));
-            prof_end(GWO_KERNEL_PARTITION, (int64_t)total);
-            // the pinned staging above is reused by the next chunk/batch
-            GWO_TRY(hipcheck(hipStreamSynchronize(stream), "log insert"));
-        }
+        GWO_TRY(log_split_chunk(base, nunits, cap));
+        const long long chunk_hi = base + nunits - 1;
         if (chunk_hi >= hi) break;
         base = chunk_hi + 1;
+        nunits = (int)std::min<long long>(LOG_NU, hi - base + 1);
     }
     hist_hint = lo;
+    L.span_hint = hi - lo + 2;
     return GWO_OK;
 }
 
@@ -268,11 +333,16 @@ gwo_status Handle::fire_log(int64_t new_wm) {
         if (max_ts <= new_wm) fire.push_back(kv.first);   // EventTimeTrigger.onEventTime FIRE
     }
     if (fire.empty()) return GWO_OK;
-    uint64_t bound = 0;
-    for (long long u : fire) bound += L.wins[u].records;
-    GWO_TRY(ensure_output(bound));
-    OutCols o = out_cols();
-    // one descriptor array per fired window, uploaded together
+    // Output rows: one per distinct key.  Reserve for the expected count (last window's keys, or the
+    // caller's hint) rather than the record count; if the fire emits more, it is re-run into a
+    // bigger buffer (fire only reads the segments, so a re-run is exact).
+    uint64_t bound = 0, expect = 0;
+    const uint64_t per_window = std::max<uint64_t>(L.last_window_keys, (uint64_t)std::max<int64_t>(cfg.expected_keys, 0));
+    for (long long u : fire) {
+        bound += L.wins[u].records;
+        expect += std::min<uint64_t>(L.wins[u].records, per_window + per_window / 8 + 4096);
+    }
+    GWO_TRY(ensure_output(expect));
     size_t ndesc = 0;
     for (long long u : fire) ndesc += L.wins[u].segs.size();
     L.h_fire.clear();
@@ -281,29 +351,52 @@ gwo_status Handle::fire_log(int64_t new_wm) {
     GWO_TRY(ensure_buf(L.firedesc, ndesc * sizeof(LogSegDesc)));
     GWO_TRY(hipcheck(hipMemcpyAsync(L.firedesc.ptr, L.h_fire.data(), ndesc * sizeof(LogSegDesc), hipMemcpyHostToDevice,
                                     stream), "fire desc"));
-    size_t at = 0;
-    for (long long u : fire) {
-        LogWindow &W = L.wins[u];
-        int64_t start = unit_start(u);
-        int64_t end = (int64_t)((uint64_t)start + (uint64_t)cfg.size);
-        prof_begin(GWO_KERNEL_FIRE);
-        launch_log_fire((const LogSegDesc *)L.firedesc.ptr + at, (int)W.segs.size(), W.lp, plan, rplan, start, end, o,
-                        L.d_overflow, stream);
-        GWO_TRY(launch_ok("log fire"));
-        prof_end(GWO_KERNEL_FIRE, (int64_t)W.records);
-        at += W.segs.size();
+    if (L.max_groups == 0) {
+        int cus = 0;
+        GWO_TRY(hipcheck(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, cfg.device), "CU count"));
+        L.max_groups = 2 * std::max(cus, 1);   // two 64-KiB-LDS workgroups per CU
     }
-    GWO_TRY(hipcheck(hipMemcpyAsync(h_scalar, d_out_count, 8, hipMemcpyDeviceToHost, stream), "out count"));
-    GWO_TRY(hipcheck(hipMemcpyAsync(h_scalar + 1, L.d_overflow, 8, hipMemcpyDeviceToHost, stream), "overflow"));
-    GWO_TRY(hipcheck(hipStreamSynchronize(stream), "log fire"));
+    const uint64_t rows0 = out_rows;
+    for (int attempt = 0; attempt < 2; ++attempt) {
+        OutCols o = out_cols();
+        size_t at = 0;
+        for (long long u : fire) {
+            LogWindow &W = L.wins[u];
+            int64_t start = unit_start(u);
+            int64_t end = (int64_t)((uint64_t)start + (uint64_t)cfg.size);
+            prof_begin(GWO_KERNEL_FIRE);
+            launch_log_fire((const LogSegDesc *)L.firedesc.ptr + at, (int)W.segs.size(), W.lp, needs_value, plan,
+                            rplan, start, end, o, L.d_overflow, L.max_groups, stream);
+            GWO_TRY(launch_ok("log fire"));
+            prof_end(GWO_KERNEL_FIRE, (int64_t)W.records);
+            at += W.segs.size();
+        }
+        GWO_TRY(hipcheck(hipMemcpyAsync(h_scalar, d_out_count, 8, hipMemcpyDeviceToHost, stream), "out count"));
+        GWO_TRY(hipcheck(hipMemcpyAsync(h_scalar + 1, L.d_overflow, 16, hipMemcpyDeviceToHost, stream), "overflow"));
+        GWO_TRY(hipcheck(hipStreamSynchronize(stream), "log fire"));
+        if (h_scalar[1]) return poison(GWO_ERR_CAPACITY, "log fire: a partition overflowed its LDS table");
+        if ((long long)h_scalar[0] <= out.cap) break;
+        // more rows than reserved: rewind the row counter, grow to the exact need, fire again
+        const uint64_t need = h_scalar[0] - rows0;
+        h_scalar[0] = rows0;
+        GWO_TRY(hipcheck(hipMemcpyAsync(d_out_count, h_scalar, 8, hipMemcpyHostToDevice, stream), "out rewind"));
+        GWO_TRY(hipcheck(hipStreamSynchronize(stream), "out rewind"));
+        GWO_TRY(ensure_output(std::min(need, bound)));
+    }
+    const uint64_t emitted = h_scalar[0] - rows0;
+    if (debug)
+        fprintf(stderr, "[gwo] fire %zu window(s): rows=%llu slow_partitions=%llu lp=%d records=%llu\n", fire.size(),
+                (unsigned long long)emitted, (unsigned long long)h_scalar[2], L.wins[fire[0]].lp,
+                (unsigned long long)L.wins[fire[0]].records);
     out_rows = h_scalar[0];
-    if (h_scalar[1]) return poison(GWO_ERR_CAPACITY, "log fire: a partition overflowed its LDS table");
+    L.last_window_keys = emitted / fire.size();
+    L.last_window_records = 0;
+    for (long long u : fire) L.last_window_records = std::max<uint64_t>(L.last_window_records, L.wins[u].records);
     for (long long u : fire) {
         LogWindow &W = L.wins[u];
-        L.last_window_records = std::max<uint64_t>(W.records, L.last_window_records / 2);
         log_release(W);
         // allowedLateness > 0: any later record of this window is a re-fire and is rejected at
-        // scan time, so nothing of the window is kept until its cleanup time
+        // classification, so nothing of the window is kept until its cleanup time
         L.wins.erase(u);
     }
     return GWO_OK;

@@ -4,32 +4,51 @@
 
 #include "gwo_internal.h"
 
-#define LOG_UNITS 16            // windows covered by one scan/scatter chunk
+#define LOG_NU 4                 // windows one partition launch (K1) covers
+#define LOG_TILE_PER 14          // records per thread in a K1 tile / pass-2 chunk
+#define LOG_TILE_THREADS 256
+#define LOG_TILE (LOG_TILE_PER * LOG_TILE_THREADS)   // 3584 records: 56 KiB of 16-B records in LDS
+#define LOG_MIN_LP 8             // a window has at least 256 partitions (one per coarse digit)
+#define LOG_MAX_LP 18            // at most 2^18 partitions per window (<= 1024 per coarse digit)
 #define LOG_FIRE_THREADS 512
-#define LOG_MAX_LP 18           // at most 2^18 partitions per window
-#define LOG_MAX_SEGS 512        // segments (batches) per window that one fire folds (= LOG_FIRE_THREADS)
+#define LOG_CUR_STRIDE 16        // K1 bucket cursors: one per 128-B line (memory-side atomics serialise per line)
+#define FIRE_RPT 7                                   // records per thread in the fire's register prefetch
+#define FIRE_RCAP (FIRE_RPT * LOG_FIRE_THREADS)      // 3584: records per partition of the fire's fast path
+#define FIRE_GROUPS 2048                             // hash groups of the fast path's LDS counting sort
+#define LOG_MAX_SEGS 512         // segments (batches) per window that one fire folds (= LOG_FIRE_THREADS)
 
-// One segment = the records one batch appended to one window, grouped by partition:
-// partition p's records are key[off[p] .. off[p+1]) (and val[...] unless the aggregates need no value).
+// One segment = the records one batch appended to one window.  Partition p's records are
+// rec[off[p] .. off[p] + cnt[p]) ((key, value) pairs, or keys only when no aggregate reads the value).
 struct LogSegDesc {
-    int64_t *key;
-    int64_t *val;
-    uint32_t *off;              // 2^lp + 1 entries
+    int64_t *rec;
+    uint32_t *off;               // 2^lp start offsets (in records)
+    uint32_t *cnt;               // 2^lp record counts (atomic cursors while pass 2 runs)
     int32_t lp;
     int32_t pad;
 };
 
+// Pass-2 work description of one coarse bucket (window w of the launch, coarse digit d).
+struct LogBucket {
+    uint64_t src;                // first record of the bucket in the batch buffer
+    uint32_t n;                  // records in the bucket
+    uint32_t pcap;               // capacity of each of the bucket's 2^(lp-8) partitions in the segment
+    uint32_t seg_base;           // first record of the bucket's partitions in the segment
+    uint32_t chunk0;             // first pass-2 workgroup of the bucket (prefix over buckets)
+};
+
 namespace gwo {
-void launch_log_scan(const int64_t *key, const int64_t *ts, const int64_t *val, int64_t n, const WindowGeom &g,
-                     long long base, BatchStats *st, unsigned *chist, int64_t *side_key, int64_t *side_ts,
-                     int64_t *side_val, unsigned long long *side_count, long long side_cap, int side_enabled,
-                     hipStream_t s);
-void launch_log_pass1(const int64_t *key, const int64_t *ts, const int64_t *val, int64_t n, const WindowGeom &g,
-                      long long base, int nunits, unsigned long long *cursor, int64_t *tkey, int64_t *tval,
-                      hipStream_t s);
-void launch_log_pass2(const int64_t *tkey, const int64_t *tval, const unsigned long long *cbase, int nunits,
-                      const LogSegDesc *segs, hipStream_t s);
+// K1: classify + key-group check + late accounting + (window, coarse digit) grouping of a batch.
+void launch_log_part(const int64_t *key, const int64_t *ts, const int64_t *val, int64_t n, const WindowGeom &g,
+                     long long base, int nunits, int has_val, unsigned long long *cursor, uint64_t cap,
+                     int64_t *tmp, BatchStats *st, int64_t *side_key, int64_t *side_ts, int64_t *side_val,
+                     unsigned long long *side_count, long long side_cap, int side_enabled, hipStream_t s);
+// Pass 2: every coarse bucket -> its window's segment, grouped by partition.
+// cursor[b * LOG_CUR_STRIDE] -> counts[b], b < nb
+void launch_log_gather(const unsigned long long *cursor, unsigned long long *counts, int nb, hipStream_t s);
+void launch_log_split(const int64_t *tmp, int has_val, const LogBucket *buckets, int nb, int nunits,
+                      const LogSegDesc *segs, unsigned *overflow, uint32_t nchunks, hipStream_t s);
 int log_fire_cap_log2(int nwords);
-void launch_log_fire(const LogSegDesc *segs, int nseg, int lp, const AccPlan &plan, const ResultPlan &rp,
-                     int64_t start, int64_t end, OutCols out, unsigned long long *overflow, hipStream_t s);
+void launch_log_fire(const LogSegDesc *segs, int nseg, int lp, int has_val, const AccPlan &plan,
+                     const ResultPlan &rp, int64_t start, int64_t end, OutCols out, unsigned long long *overflow,
+                     int max_groups, hipStream_t s);
 }  // namespace gwo

@@ -4,25 +4,30 @@
 // record (HeapAggregatingState.add, HeapAggregatingState.java:96-109; StateTable.transform,
 // heap/StateTable.java:194-202).  On MI355X a random read-modify-write of a 32-B entry in an
 // 8-GB table costs a 64-128-B line round trip per record, and device-scope atomics execute at the
-// memory side (tools/micro_table.hip: 8 G updates/s for sum/min/max).  For windows that receive
-// about as many distinct keys as records (config C4: 166M records -> 81M (key, window) pairs),
-// this path defers the aggregation to the window's fire instead:
+// memory side (tools/micro_table.hip).  For windows that receive about as many distinct keys as
+// records (config C4: 166M records -> 81M (key, window) pairs) this path defers the aggregation to
+// the window's fire instead:
 //
-//   per batch  log_scan   classify + late accounting + key-group check + a (window, coarse digit)
-//                         histogram (coarse digit = top 8 bits of the partition hash)
-//              log_pass1  scatter accepted (key, value) pairs into a batch buffer grouped by
-//                         (window, coarse digit); one cursor reservation per tile and bucket
-//              log_pass2  one workgroup per coarse bucket splits it by the fine partition bits
-//                         into the window's new segment and writes the segment's offsets
+//   per batch  log_part   (K1) classify every record (WindowOperator.java:386-427), check its key
+//                         group, count late records / route them to the side output, and group the
+//                         accepted (key, value) pairs of a 3584-record tile by (window, coarse digit)
+//                         in LDS; each group is appended with one cursor reservation to its bucket
+//                         of the batch buffer (fixed-capacity buckets, overflow -> exact rerun)
+//              log_split  (pass 2) one workgroup per 3584-record chunk of a bucket groups it by the
+//                         fine partition bits in LDS and appends each group to its partition of the
+//                         window's new segment (fixed-capacity partitions, overflow -> rerun)
 //   at fire    log_fire   one workgroup per partition folds the partition's records from every
 //                         segment of the window into an LDS hash table and emits one row per key
 //                         (WindowOperator.onEventTime + emitWindowContents, WindowOperator.java:430-473,546-550)
 //
-// Every byte moved is a coalesced or run-length-grouped stream; the only random accesses are LDS.
+// Every HBM byte moves as a coalesced stream or as a run of consecutive 16-B records; the only
+// random accesses are LDS.
 #include "gwo_device.h"
 #include "gwo_log.h"
 
 namespace gwo {
+
+typedef long long ll2 __attribute__((ext_vector_type(2)));
 
 enum LogClass : int { L_ACCEPT = 0, L_LATE = 1, L_SKIP = 2, L_REFIRE = 3, L_BAD_TS = 4 };
 
@@ -37,53 +42,142 @@ __device__ __forceinline__ int log_classify(int64_t ts, const WindowGeom &g, lon
     return L_ACCEPT;
 }
 
+// Exclusive prefix over nb (<= 1024) LDS counters s_cnt -> s_off; thread t owns the `per`
+// consecutive counters [t*per, t*per+per).  Returns the total.  All threads call it; ends
+// synchronised, so s_off is complete on return.
+__device__ __forceinline__ uint32_t tile_offsets(const uint32_t *s_cnt, uint32_t *s_off, int nb, uint32_t loc[4],
+                                                 int per) {
+    uint32_t sum = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        int b = threadIdx.x * per + q;
+        loc[q] = (q < per && b < nb) ? s_cnt[b] : 0u;
+        sum += loc[q];
+    }
+    uint32_t total;
+    uint32_t ex = block_exclusive_scan(sum, &total);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        int b = threadIdx.x * per + q;
+        if (q < per && b < nb) s_off[b] = ex;
+        ex += loc[q];
+    }
+    __syncthreads();   // every thread reads other threads' s_off next
+    return total;
+}
+
 // ------------------------------------------------------------------------------------------------
-// log_scan: per-batch statistics + (unit, coarse digit) histogram for units [base, base+LOG_UNITS)
+// K1 log_part: batch -> batch buffer, grouped by bucket b = (window - base) * 256 + coarse digit.
+// Bucket b owns records [b*cap, (b+1)*cap) of the buffer; cursor[b*LOG_CUR_STRIDE] ends as its record
+// count (also when it exceeds cap: those records are not written and the host reruns).
 // ------------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void log_scan_kernel(const int64_t *__restrict__ key, const int64_t *__restrict__ ts,
-                                                       const int64_t *__restrict__ val, int64_t n, WindowGeom g,
-                                                       long long base, BatchStats *st, unsigned *chist,
-                                                       int64_t *side_key, int64_t *side_ts, int64_t *side_val,
-                                                       unsigned long long *side_count, long long side_cap,
-                                                       int side_enabled) {
-    __shared__ unsigned s_c[LOG_UNITS * 256];
-    __shared__ long long s_min[4], s_max[4];
-    for (int i = threadIdx.x; i < LOG_UNITS * 256; i += blockDim.x) s_c[i] = 0;
-    __syncthreads();
+template <bool HASV>
+__global__ __launch_bounds__(LOG_TILE_THREADS) void log_part_kernel(
+    const int64_t *__restrict__ key, const int64_t *__restrict__ ts, const int64_t *__restrict__ val, int64_t n,
+    WindowGeom g, long long base, int nunits, unsigned long long *__restrict__ cursor, uint64_t cap,
+    int64_t *__restrict__ tmp, BatchStats *st, int64_t *side_key, int64_t *side_ts, int64_t *side_val,
+    unsigned long long *side_count, long long side_cap, int side_enabled) {
+    constexpr int W = HASV ? 2 : 1;
+    __shared__ __attribute__((aligned(16))) int64_t s_rec[LOG_TILE * W];
+    __shared__ uint16_t s_bk[LOG_TILE];
+    __shared__ uint32_t s_cnt[LOG_NU * 256];
+    __shared__ uint32_t s_off[LOG_NU * 256];
+    __shared__ long long s_min[LOG_TILE_THREADS / 64], s_max[LOG_TILE_THREADS / 64];
+    const int nb = nunits * 256;
+    const int tid = threadIdx.x;
     long long mn = 0x7fffffffffffffffLL, mx = (long long)0x8000000000000000LL;
     unsigned long long acc = 0, late = 0, refire = 0, bad_ts = 0, out = 0, bad_kg = 0;
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-        long long u = 0;
-        int c = log_classify(ts[i], g, u);
-        if (c == L_ACCEPT) {
-            int64_t k = key[i];
-            int32_t kg = key_group(k, g.key_kind, g.max_par);
-            if (kg < g.kg_lo || kg > g.kg_hi) {
-                bad_kg++;
-                st->bad_kg_key = k;
-            }
-            acc++;
-            mn = u < mn ? u : mn;
-            mx = u > mx ? u : mx;
-            long long b = u - base;
-            if (b >= 0 && b < LOG_UNITS) atomicAdd(&s_c[b * 256 + (int)(part_hash(k) >> 56)], 1u);
-            else out++;
-        } else if (c == L_LATE) {
-            late++;
-            if (side_enabled) {
-                unsigned long long pos = atomicAdd(side_count, 1ull);
-                if ((long long)pos < side_cap) {
-                    side_key[pos] = key[i];
-                    side_ts[pos] = ts[i];
-                    side_val[pos] = val ? val[i] : 0;
-                }
-            }
-        } else if (c == L_REFIRE) {
-            refire++;
-        } else if (c == L_BAD_TS) {
-            bad_ts++;
+    for (int64_t tile = (int64_t)blockIdx.x * LOG_TILE; tile < n; tile += (int64_t)gridDim.x * LOG_TILE) {
+        for (int i = tid; i < nb; i += LOG_TILE_THREADS) s_cnt[i] = 0;
+        __syncthreads();
+        int64_t kk[LOG_TILE_PER], vv[LOG_TILE_PER], tt[LOG_TILE_PER];
+        uint32_t code[LOG_TILE_PER];
+#pragma unroll
+        for (int j = 0; j < LOG_TILE_PER; ++j) {
+            int64_t i = tile + j * LOG_TILE_THREADS + tid;
+            i = i < n ? i : tile;   // unconditional loads; lanes past the end are discarded below
+            tt[j] = __builtin_nontemporal_load(ts + i);
+            kk[j] = __builtin_nontemporal_load(key + i);
+            vv[j] = HASV ? __builtin_nontemporal_load(val + i) : 0;
         }
+#pragma unroll
+        for (int j = 0; j < LOG_TILE_PER; ++j) {
+            int64_t i = tile + j * LOG_TILE_THREADS + tid;
+            code[j] = 0xffffffffu;
+            if (i >= n) continue;
+            long long u = 0;
+            int c = log_classify(tt[j], g, u);
+            if (c == L_ACCEPT) {
+                int64_t k = kk[j];
+                int32_t kg = key_group(k, g.key_kind, g.max_par);
+                if (kg < g.kg_lo || kg > g.kg_hi) {
+                    bad_kg++;
+                    st->bad_kg_key = k;
+                }
+                acc++;
+                mn = u < mn ? u : mn;
+                mx = u > mx ? u : mx;
+                long long w = u - base;
+                if (w >= 0 && w < nunits) {
+                    uint32_t b = (uint32_t)(w * 256 + (int)(part_hash(k) >> 56));
+                    uint32_t r = atomicAdd(&s_cnt[b], 1u);
+                    code[j] = (b << 16) | r;
+                } else {
+                    out++;
+                }
+            } else if (c == L_LATE) {
+                late++;
+                if (side_enabled) {
+                    unsigned long long pos = atomicAdd(side_count, 1ull);
+                    if ((long long)pos < side_cap) {
+                        side_key[pos] = kk[j];
+                        side_ts[pos] = tt[j];
+                        side_val[pos] = val ? val[i] : 0;
+                    }
+                }
+            } else if (c == L_REFIRE) {
+                refire++;
+            } else if (c == L_BAD_TS) {
+                bad_ts++;
+            }
+        }
+        __syncthreads();
+        uint32_t loc[4];
+        const uint32_t total = tile_offsets(s_cnt, s_off, nb, loc, nunits);
+        // reserve each bucket's run; s_cnt[b] becomes the run's first record in the bucket
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            int b = tid * nunits + q;
+            if (q < nunits && loc[q]) {
+                unsigned long long at = atomicAdd(&cursor[(size_t)b * LOG_CUR_STRIDE], (unsigned long long)loc[q]);
+                s_cnt[b] = (uint32_t)(at < cap ? at : cap);
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < LOG_TILE_PER; ++j) {
+            if (code[j] == 0xffffffffu) continue;
+            uint32_t b = code[j] >> 16;
+            uint32_t pos = s_off[b] + (code[j] & 0xffffu);
+            if (HASV) {
+                ll2 r2 = {kk[j], vv[j]};
+                *(ll2 *)&s_rec[2 * pos] = r2;
+            } else {
+                s_rec[pos] = kk[j];
+            }
+            s_bk[pos] = (uint16_t)b;
+        }
+        __syncthreads();
+        for (uint32_t p = tid; p < total; p += LOG_TILE_THREADS) {
+            uint32_t b = s_bk[p];
+            if (b >= (uint32_t)nb) continue;   // defensive: never a write outside the buffer
+            uint64_t q = (uint64_t)s_cnt[b] + (p - s_off[b]);
+            if (q < cap) {
+                int64_t *dst = tmp + ((uint64_t)b * cap + q) * W;
+                if (HASV) *(ll2 *)dst = *(const ll2 *)&s_rec[2 * p];
+                else *dst = s_rec[p];
+            }
+        }
+        __syncthreads();
     }
     for (int o = 32; o > 0; o >>= 1) {
         long long a = __shfl_xor(mn, o), b = __shfl_xor(mx, o);
@@ -96,15 +190,15 @@ __global__ __launch_bounds__(256) void log_scan_kernel(const int64_t *__restrict
     wave_atomic_add(&st->bad_ts, bad_ts);
     wave_atomic_add(&st->hist_out, out);
     wave_atomic_add(&st->bad_kg, bad_kg);
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int lane = tid & 63, wid = tid >> 6;
     if (lane == 0) {
         s_min[wid] = mn;
         s_max[wid] = mx;
     }
     __syncthreads();
-    if (threadIdx.x == 0) {
+    if (tid == 0) {
         long long a = s_min[0], b = s_max[0];
-        for (int w = 1; w < (int)(blockDim.x >> 6); ++w) {
+        for (int w = 1; w < LOG_TILE_THREADS / 64; ++w) {
             a = s_min[w] < a ? s_min[w] : a;
             b = s_max[w] > b ? s_max[w] : b;
         }
@@ -113,156 +207,130 @@ __global__ __launch_bounds__(256) void log_scan_kernel(const int64_t *__restrict
             atomicMax(&st->max_idx, b);
         }
     }
-    for (int i = threadIdx.x; i < LOG_UNITS * 256; i += blockDim.x)
-        if (s_c[i]) atomicAdd(&chist[i], s_c[i]);
 }
 
 // ------------------------------------------------------------------------------------------------
-// log_pass1: records -> batch buffer grouped by coarse bucket b = (unit - base) * 256 + digit.
-// A tile of P1_TILE records counts its buckets in LDS, reserves each bucket's run with one device
-// atomic on the bucket cursor, then writes every record at cursor + rank.
+// Pass 2 log_split: workgroup = one LOG_TILE chunk of one bucket (window w, coarse digit d).
+// Partition p = top lp bits of part_hash = d * F + f, F = 2^(lp-8).  Partition p of the segment owns
+// records [seg_base + f*pcap, + pcap); cnt[p] is its cursor (ends as its count, overflow -> rerun).
 // ------------------------------------------------------------------------------------------------
-#define P1_PER 32
-#define P1_TILE (256 * P1_PER)
-
-__global__ __launch_bounds__(256) void log_pass1_kernel(const int64_t *__restrict__ key, const int64_t *__restrict__ ts,
-                                                        const int64_t *__restrict__ val, int64_t n, WindowGeom g,
-                                                        long long base, int nunits,
-                                                        unsigned long long *__restrict__ cursor,
-                                                        int64_t *__restrict__ tkey, int64_t *__restrict__ tval) {
-    __shared__ unsigned s_cnt[LOG_UNITS * 256];
-    __shared__ unsigned long long s_pos[LOG_UNITS * 256];
-    __shared__ uint16_t s_b[P1_TILE];
-    const int nb = nunits * 256;
-    for (int i = threadIdx.x; i < nb; i += 256) s_cnt[i] = 0;
+template <bool HASV>
+__global__ __launch_bounds__(LOG_TILE_THREADS) void log_split_kernel(const int64_t *__restrict__ tmp,
+                                                                     const LogBucket *__restrict__ bk, int nb,
+                                                                     const LogSegDesc *__restrict__ segs,
+                                                                     unsigned *overflow) {
+    constexpr int W = HASV ? 2 : 1;
+    __shared__ __attribute__((aligned(16))) int64_t s_rec[LOG_TILE * W];
+    __shared__ uint16_t s_bk[LOG_TILE];
+    __shared__ uint32_t s_cnt[1024];
+    __shared__ uint32_t s_off[1024];
+    __shared__ int s_c;
+    const int tid = threadIdx.x;
+    // this chunk's bucket: the largest c with bk[c].chunk0 <= blockIdx.x (one parallel load of the
+    // nb chunk prefixes into LDS, then a binary search there)
+    for (int c = tid; c < nb; c += LOG_TILE_THREADS) s_off[c] = bk[c].chunk0;
     __syncthreads();
-    for (int64_t tile = (int64_t)blockIdx.x * P1_TILE; tile < n; tile += (int64_t)gridDim.x * P1_TILE) {
-#pragma unroll 4
-        for (int j = 0; j < P1_PER; ++j) {
-            int64_t i = tile + j * 256 + threadIdx.x;
-            uint16_t b = 0xffff;
-            if (i < n) {
-                long long u = 0;
-                if (log_classify(ts[i], g, u) == L_ACCEPT) {
-                    long long w = u - base;
-                    if (w >= 0 && w < nunits) {
-                        b = (uint16_t)(w * 256 + (int)(part_hash(key[i]) >> 56));
-                        atomicAdd(&s_cnt[b], 1u);
-                    }
-                }
-            }
-            s_b[j * 256 + threadIdx.x] = b;
+    if (tid == 0) {
+        int lo = 0, hi = nb;
+        while (hi - lo > 1) {
+            int mid = (lo + hi) >> 1;
+            if (s_off[mid] <= blockIdx.x) lo = mid;
+            else hi = mid;
         }
-        __syncthreads();
-        for (int b = threadIdx.x; b < nb; b += 256) {
-            unsigned c = s_cnt[b];
-            if (c) {
-                s_pos[b] = atomicAdd(&cursor[b], (unsigned long long)c);
-                s_cnt[b] = 0;
-            }
-        }
-        __syncthreads();
-#pragma unroll 4
-        for (int j = 0; j < P1_PER; ++j) {
-            uint16_t b = s_b[j * 256 + threadIdx.x];
-            if (b == 0xffff) continue;
-            int64_t i = tile + j * 256 + threadIdx.x;
-            unsigned long long pos = s_pos[b] + atomicAdd(&s_cnt[b], 1u);
-            tkey[pos] = key[i];
-            if (tval) tval[pos] = val[i];
-        }
-        __syncthreads();
-        for (int b = threadIdx.x; b < nb; b += 256) s_cnt[b] = 0;
-        __syncthreads();
+        s_c = lo;
     }
-}
-
-// ------------------------------------------------------------------------------------------------
-// log_pass2: one workgroup per coarse bucket -> the window's segment, ordered by partition.
-// Partition p = top lp bits of the partition hash; coarse digit d = top 8 bits.  lp <= 8: a
-// partition is 2^(8-lp) whole coarse buckets (copy); lp > 8: the bucket splits into 2^(lp-8)
-// partitions by a counting sort.  Also writes the segment's partition offsets.
-// ------------------------------------------------------------------------------------------------
-#define P2_THREADS 512
-#define P2_MAXF 1024   // lp <= 18
-
-__global__ __launch_bounds__(P2_THREADS) void log_pass2_kernel(const int64_t *__restrict__ tkey,
-                                                               const int64_t *__restrict__ tval,
-                                                               const unsigned long long *__restrict__ cbase,
-                                                               const LogSegDesc *__restrict__ segs) {
-    __shared__ unsigned s_hist[P2_MAXF];
-    __shared__ unsigned s_pre[P2_MAXF];
-    const int c = blockIdx.x;
+    __syncthreads();
+    const int c = s_c;
+    const LogBucket B = bk[c];
+    const uint32_t chunk = blockIdx.x - B.chunk0;
     const int w = c >> 8, d = c & 255;
-    const LogSegDesc sd = segs[w];
-    if (!sd.off) return;   // no records of this window in the chunk
-    const int lp = sd.lp;
-    const unsigned long long lo = cbase[c], hi = cbase[c + 1], wbase = cbase[w * 256];
-    const uint32_t rel = (uint32_t)(lo - wbase);
-    if (lp <= 8) {
-        const int sh = 8 - lp;
-        if (threadIdx.x == 0) {
-            if ((d & ((1 << sh) - 1)) == 0) sd.off[d >> sh] = rel;
-            if (d == 255) sd.off[1u << lp] = (uint32_t)(hi - wbase);
-        }
-        for (unsigned long long i = lo + threadIdx.x; i < hi; i += P2_THREADS) {
-            unsigned long long o = i - wbase;
-            sd.key[o] = tkey[i];
-            if (sd.val) sd.val[o] = tval[i];
-        }
-        return;
-    }
-    const int fb = lp - 8, F = 1 << fb;
-    for (int f = threadIdx.x; f < F; f += P2_THREADS) s_hist[f] = 0;
+    const LogSegDesc S = segs[w];
+    const int lp = S.lp, fb = lp - 8, F = 1 << fb;
+    if (chunk == 0)
+        for (int f = tid; f < F; f += LOG_TILE_THREADS) S.off[d * F + f] = B.seg_base + (uint32_t)f * B.pcap;
+    for (int f = tid; f < F; f += LOG_TILE_THREADS) s_cnt[f] = 0;
     __syncthreads();
-    for (unsigned long long i0 = lo + threadIdx.x; i0 < hi; i0 += 4 * P2_THREADS) {
-        int64_t kk[4];
+    const uint32_t begin = chunk * LOG_TILE;
+    const uint32_t m = min((uint32_t)LOG_TILE, B.n - begin);
+    int64_t kk[LOG_TILE_PER], vv[LOG_TILE_PER];
+    uint32_t code[LOG_TILE_PER];
+    // unconditional loads (a lane past the end re-reads the chunk's first record): no branch per load
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            unsigned long long i = i0 + u * P2_THREADS;
-            kk[u] = i < hi ? tkey[i] : 0;
+    for (int j = 0; j < LOG_TILE_PER; ++j) {
+        uint32_t i = j * LOG_TILE_THREADS + tid;
+        const int64_t *src = tmp + (B.src + begin + (i < m ? i : 0u)) * W;
+        if (HASV) {
+            ll2 r2 = __builtin_nontemporal_load((const ll2 *)src);
+            kk[j] = r2.x;
+            vv[j] = r2.y;
+        } else {
+            kk[j] = __builtin_nontemporal_load(src);
+            vv[j] = 0;
         }
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-            if (i0 + u * P2_THREADS < hi) atomicAdd(&s_hist[(int)(part_hash(kk[u]) >> (64 - lp)) & (F - 1)], 1u);
     }
-    __syncthreads();
-    if (threadIdx.x == 0) {   // F <= 1024: serial scan is a few microseconds at most
-        unsigned run = 0;
-        for (int f = 0; f < F; ++f) {
-            s_pre[f] = run;
-            run += s_hist[f];
-            s_hist[f] = 0;
+#pragma unroll
+    for (int j = 0; j < LOG_TILE_PER; ++j) {
+        uint32_t i = j * LOG_TILE_THREADS + tid;
+        code[j] = 0xffffffffu;
+        if (i < m) {
+            uint32_t f = (uint32_t)(part_hash(kk[j]) >> (64 - lp)) & (uint32_t)(F - 1);
+            uint32_t r = atomicAdd(&s_cnt[f], 1u);
+            code[j] = (f << 16) | r;
         }
     }
     __syncthreads();
-    for (int f = threadIdx.x; f < F; f += P2_THREADS) sd.off[(size_t)d * F + f] = rel + s_pre[f];
-    if (d == 255 && threadIdx.x == 0) sd.off[(size_t)256 * F] = (uint32_t)(hi - wbase);
-    for (unsigned long long i0 = lo + threadIdx.x; i0 < hi; i0 += 4 * P2_THREADS) {
-        int64_t kk[4], vv[4];
+    const int per = F <= LOG_TILE_THREADS ? 1 : F / LOG_TILE_THREADS;
+    uint32_t loc[4];
+    const uint32_t total = tile_offsets(s_cnt, s_off, F, loc, per);
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            unsigned long long i = i0 + u * P2_THREADS;
-            kk[u] = i < hi ? tkey[i] : 0;
-            vv[u] = (i < hi && tval) ? tval[i] : 0;
+    for (int q = 0; q < 4; ++q) {
+        int f = tid * per + q;
+        if (q < per && f < F && loc[q]) {
+            uint32_t at = atomicAdd(&S.cnt[d * F + f], loc[q]);
+            if (at + loc[q] > B.pcap) atomicOr(overflow, 1u);
+            s_cnt[f] = at;
         }
+    }
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            if (i0 + u * P2_THREADS >= hi) break;
-            int f = (int)(part_hash(kk[u]) >> (64 - lp)) & (F - 1);
-            unsigned long long o = rel + s_pre[f] + atomicAdd(&s_hist[f], 1u);
-            sd.key[o] = kk[u];
-            if (sd.val) sd.val[o] = vv[u];
+    for (int j = 0; j < LOG_TILE_PER; ++j) {
+        if (code[j] == 0xffffffffu) continue;
+        uint32_t f = code[j] >> 16;
+        uint32_t pos = s_off[f] + (code[j] & 0xffffu);
+        if (HASV) {
+            ll2 r2 = {kk[j], vv[j]};
+            *(ll2 *)&s_rec[2 * pos] = r2;
+        } else {
+            s_rec[pos] = kk[j];
+        }
+        s_bk[pos] = (uint16_t)f;
+    }
+    __syncthreads();
+    for (uint32_t p = tid; p < total; p += LOG_TILE_THREADS) {
+        uint32_t f = s_bk[p];
+        if (f >= (uint32_t)F) continue;   // defensive: never a write outside the segment
+        uint32_t q = s_cnt[f] + (p - s_off[f]);
+        if (q < B.pcap) {
+            int64_t *dst = S.rec + (uint64_t)(B.seg_base + f * B.pcap + q) * W;
+            if (HASV) *(ll2 *)dst = *(const ll2 *)&s_rec[2 * p];
+            else *dst = s_rec[p];
         }
     }
 }
 
 // ------------------------------------------------------------------------------------------------
-// log_fire: one workgroup per partition.  Folds the partition's records from every segment of the
-// window into an LDS hash table (key -> accumulator words), then emits one output row per key.
-// A partition holding more records than 3/4 of the table is folded in rounds over a second set of
-// hash bits, so the table can never overflow for non-adversarial keys; an overflow is reported.
+// log_fire: persistent workgroups, each folding partitions p = blockIdx.x, + gridDim.x, ...
+// (WindowOperator.onEventTime + emitWindowContents, WindowOperator.java:430-473, 546-550).
+// Fast path (a partition of <= FIRE_RCAP records): the records are grouped by FIRE_GROUPS hash bits
+// with an LDS counting sort (one 32-bit LDS atomic per record), then each thread folds its groups
+// sequentially in registers -- the first occurrence of a key aggregates the later ones -- and
+// emits one row per key.  No per-word LDS atomics: those were the fold's bottleneck (a hash-table
+// fold costs ~4.5 64-bit LDS atomics per record).  The next partition's segment offsets and
+// records are loaded while the current one is folded and emitted, so a workgroup exposes about one
+// HBM round trip per partition.  Slow path (more records): an LDS hash table folded in rounds over
+// disjoint ranges of a second group of hash bits (the range halves until it fits).
 // ------------------------------------------------------------------------------------------------
+
+
 __device__ __forceinline__ void lds_combine64(int64_t *dst, int op, int64_t x) {
     switch (op) {
         case ACC_ADD_I64: atomicAdd((unsigned long long *)dst, (unsigned long long)x); break;
@@ -272,8 +340,8 @@ __device__ __forceinline__ void lds_combine64(int64_t *dst, int op, int64_t x) {
     }
 }
 
-__device__ __forceinline__ void emit_results(const AccPlan &p, const ResultPlan &rp, const int64_t *acc, int accs,
-                                             const OutCols &o, unsigned long long pos) {
+__device__ __forceinline__ void emit_results(const ResultPlan &rp, const int64_t *acc, int accs, const OutCols &o,
+                                             unsigned long long pos) {
     for (int a = 0; a < rp.naggs; ++a) {
         int w = rp.word[a];
         int64_t r;
@@ -291,170 +359,436 @@ __device__ __forceinline__ void emit_results(const AccPlan &p, const ResultPlan 
     }
 }
 
+struct FireCtx {
+    int64_t *key;                 // LDS table: [cap] keys, then nwords x [cap] words (SoA)
+    int64_t *acc;
+    int64_t *side;                // key == Long.MIN_VALUE: [flag, words...]
+    unsigned *used, *fail;
+    int cap;
+    unsigned limit;
+};
 
-__device__ __forceinline__ void lds_insert(int64_t *s_key, int64_t *s_acc, int64_t *s_side, int cap, const AccPlan &p,
-                                           int64_t k, uint64_t h, int64_t v, unsigned *fail) {
+// Folds one record into the LDS table; a key that finds no slot (or overfills it) sets *fail.
+__device__ __forceinline__ void fire_insert(const FireCtx &c, const AccPlan &p, int64_t k, uint64_t h, int64_t v) {
     int64_t *acc;
     int accs;
     if (k == GWO_EMPTY_KEY) {
-        s_side[0] = 1;
-        acc = s_side + 1;
+        c.side[0] = 1;
+        acc = c.side + 1;
         accs = 1;
     } else {
-        int slot = (int)(h & (uint64_t)(cap - 1)), probes = 0;
+        int slot = (int)(h & (uint64_t)(c.cap - 1)), probes = 0;
         while (true) {
-            unsigned long long prev = atomicCAS((unsigned long long *)&s_key[slot], (unsigned long long)GWO_EMPTY_KEY,
+            unsigned long long prev = atomicCAS((unsigned long long *)&c.key[slot], (unsigned long long)GWO_EMPTY_KEY,
                                                 (unsigned long long)k);
-            if ((int64_t)prev == GWO_EMPTY_KEY || (int64_t)prev == k) break;
-            slot = (slot + 1) & (cap - 1);
-            if (++probes >= cap) {
-                *fail = 1;
+            if ((int64_t)prev == GWO_EMPTY_KEY) {
+                if (atomicAdd(c.used, 1u) >= c.limit) *c.fail = 1;
+                break;
+            }
+            if ((int64_t)prev == k) break;
+            slot = (slot + 1) & (c.cap - 1);
+            if (++probes >= c.cap) {
+                *c.fail = 1;
                 return;
             }
         }
-        acc = s_acc + slot;
-        accs = cap;
+        acc = c.acc + slot;
+        accs = c.cap;
     }
     for (int w = 0; w < p.nwords; ++w) lds_combine64(acc + w * accs, p.op[w], lift_word(p, w, v));
 }
 
-__global__ __launch_bounds__(LOG_FIRE_THREADS) void log_fire_kernel(const LogSegDesc *__restrict__ segs, int nseg,
-                                                                    int lp, int cap_log2, AccPlan p, ResultPlan rp,
-                                                                    int64_t start, int64_t end, OutCols o,
-                                                                    unsigned long long *overflow) {
-    extern __shared__ int64_t s_tab[];   // [cap] keys, then nwords x [cap] accumulator words (SoA)
-    __shared__ int64_t s_side[GWO_MAX_WORDS + 1];   // key == Long.MIN_VALUE: [flag, words...]
-    __shared__ unsigned s_fail;
-    __shared__ uint32_t s_beg[LOG_MAX_SEGS + 1];      // flattened record space: segment s covers
-    __shared__ uint32_t s_src[LOG_MAX_SEGS];          //   [s_beg[s], s_beg[s+1]) starting at offset s_src[s]
-    const int cap = 1 << cap_log2;
-    const int NW = p.nwords;
-    int64_t *s_key = s_tab;
-    int64_t *s_acc = s_tab + cap;
-    const uint32_t part = blockIdx.x;
-    // prologue: every segment's slice of this partition, loaded in parallel
-    uint32_t cnt_s = 0;
-    if (threadIdx.x < (unsigned)nseg) {
-        const uint32_t *off = segs[threadIdx.x].off;
-        uint32_t a = off[part], b = off[part + 1];
-        s_src[threadIdx.x] = a;
-        cnt_s = b - a;
+// Resets every slot, the side slot and the flags (caller synchronises).
+__device__ __forceinline__ void fire_clear(const FireCtx &c, const AccPlan &p) {
+    for (int i = threadIdx.x; i < c.cap; i += LOG_FIRE_THREADS) {
+        c.key[i] = GWO_EMPTY_KEY;
+        for (int w = 0; w < p.nwords; ++w) c.acc[w * c.cap + i] = p.ident[w];
     }
-    if (threadIdx.x == 0) s_fail = 0;
-    uint32_t seg_total;
-    uint32_t excl = block_exclusive_scan(cnt_s, &seg_total);
-    if (threadIdx.x < (unsigned)nseg) s_beg[threadIdx.x] = excl;
-    if (threadIdx.x == 0) s_beg[nseg] = seg_total;
-    __syncthreads();
-    const uint32_t total = s_beg[nseg];
-    if (total == 0) return;
-    int rbits = 0;
-    while ((total >> rbits) > (uint32_t)(cap * 3 / 4)) rbits++;   // rounds = 2^rbits
-    for (int round = 0; round < (1 << rbits); ++round) {
-        for (int i = threadIdx.x; i < cap; i += LOG_FIRE_THREADS) {
-            s_key[i] = GWO_EMPTY_KEY;
-            for (int w = 0; w < NW; ++w) s_acc[w * cap + i] = p.ident[w];
+    if (threadIdx.x <= GWO_MAX_WORDS) c.side[threadIdx.x] = threadIdx.x == 0 ? 0 : p.ident[threadIdx.x - 1];
+    if (threadIdx.x == 0) {
+        *c.used = 0;
+        *c.fail = 0;
+    }
+}
+
+// Emits every occupied slot (one output reservation per workgroup) and resets the table as it goes.
+// Ends synchronised.
+__device__ __forceinline__ void fire_emit(const FireCtx &c, const AccPlan &p, const ResultPlan &rp, int64_t start,
+                                          int64_t end, const OutCols &o) {
+    unsigned cnt = 0;
+    for (int i = threadIdx.x; i < c.cap; i += LOG_FIRE_THREADS) cnt += c.key[i] != GWO_EMPTY_KEY;
+    const bool side = threadIdx.x == 0 && c.side[0] != 0;
+    cnt += side;
+    unsigned long long pos = block_reserve(cnt, o.count);
+    if (side) {
+        if ((long long)pos < o.cap) {
+            o.key[pos] = GWO_EMPTY_KEY;
+            o.start[pos] = start;
+            o.end[pos] = end;
+            emit_results(rp, c.side + 1, 1, o, pos);
         }
-        if (threadIdx.x <= GWO_MAX_WORDS) s_side[threadIdx.x] = threadIdx.x == 0 ? 0 : p.ident[threadIdx.x - 1];
-        __syncthreads();
-        // records in flattened order, 4 loads in flight per thread
-        int seg = 0;
-        for (uint32_t i0 = threadIdx.x; i0 < total; i0 += 4 * LOG_FIRE_THREADS) {
-            int64_t kk[4], vv[4];
+        pos++;
+    }
+    for (int i = threadIdx.x; i < c.cap; i += LOG_FIRE_THREADS) {
+        int64_t k = c.key[i];
+        if (k == GWO_EMPTY_KEY) continue;
+        if ((long long)pos < o.cap) {
+            o.key[pos] = k;
+            o.start[pos] = start;
+            o.end[pos] = end;
+            emit_results(rp, c.acc + i, c.cap, o, pos);
+        }
+        pos++;
+        c.key[i] = GWO_EMPTY_KEY;
+        for (int w = 0; w < p.nwords; ++w) c.acc[w * c.cap + i] = p.ident[w];
+    }
+    __syncthreads();
+    if (threadIdx.x <= GWO_MAX_WORDS) c.side[threadIdx.x] = threadIdx.x == 0 ? 0 : p.ident[threadIdx.x - 1];
+    if (threadIdx.x == 0) {
+        *c.used = 0;
+        *c.fail = 0;
+    }
+    __syncthreads();
+}
+
+typedef __attribute__((address_space(1))) const ll2 g_ll2;
+typedef __attribute__((address_space(1))) const int64_t g_i64;
+
+// One output row from NW register words.  Every loop has a compile-time trip count (unrolled), so
+// the plan fields and the result-column pointers are read from kernel arguments once, outside the
+// caller's loops, and no register array is indexed at run time.
+template <int NW>
+__device__ __forceinline__ void emit_row(const ResultPlan &rp, const int64_t (&acc)[NW], const OutCols &o,
+                                         unsigned long long pos, int64_t k, int64_t start, int64_t end) {
+    o.key[pos] = k;
+    o.start[pos] = start;
+    o.end[pos] = end;
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                uint32_t i = i0 + u * LOG_FIRE_THREADS;
-                kk[u] = 0;
-                vv[u] = 0;
+    for (int a = 0; a < 4; ++a) {
+        if (a >= rp.naggs) break;
+        const int wi = rp.word[a];
+        int64_t x = acc[0], y = acc[0];
+#pragma unroll
+        for (int w = 1; w < NW; ++w) {
+            if (w == wi) x = acc[w];
+            if (w == wi + 1) y = acc[w];
+        }
+        int64_t r;
+        switch (rp.kind[a]) {
+            case 2:
+            case 3: r = rp.value_is_f64 ? f64_from_order_key(x) : x; break;
+            case 4: {
+                double s = rp.value_is_f64 ? __longlong_as_double(x) : (double)x;
+                r = __double_as_longlong(s / (double)y);
+                break;
+            }
+            default: r = x; break;
+        }
+        o.res[a][pos] = r;
+    }
+}
+
+template <int NW>
+__global__ __launch_bounds__(LOG_FIRE_THREADS) void log_fire_kernel(const LogSegDesc *__restrict__ segs, int nseg,
+                                                                    uint32_t nparts, int cap_log2, int has_val,
+                                                                    AccPlan p, ResultPlan rp, int64_t start,
+                                                                    int64_t end, OutCols o,
+                                                                    unsigned long long *overflow) {
+    extern __shared__ __attribute__((aligned(16))) int64_t s_dyn[];   // FIRE_RCAP sorted (key, value) pairs,
+                                                                       // or the slow path's hash table
+    __shared__ uint32_t s_grp[FIRE_GROUPS + 1];       // group counts, then group offsets (+ total)
+    __shared__ int64_t s_side[GWO_MAX_WORDS + 1];
+    __shared__ unsigned s_used, s_fail;
+    __shared__ uint32_t s_beg[2][LOG_MAX_SEGS + 1];   // flattened record space of a partition: segment s
+    __shared__ uint32_t s_src[2][LOG_MAX_SEGS];       //   covers [s_beg[s], s_beg[s+1]) from record s_src[s]
+    __shared__ const int64_t *s_rp[LOG_MAX_SEGS];
+    __shared__ uint32_t s_wrows[FIRE_RPT][LOG_FIRE_THREADS / 64];   // rows per (round, wave), then prefixes
+    __shared__ unsigned long long s_rbase;
+    const int tid = threadIdx.x;
+    const int cap = 1 << cap_log2;
+    FireCtx c{s_dyn, s_dyn + cap, s_side, &s_used, &s_fail, cap, (unsigned)(cap - (cap >> 3))};
+    uint32_t part = blockIdx.x;
+    if (part >= nparts) return;
+    for (int s = tid; s < nseg; s += LOG_FIRE_THREADS) s_rp[s] = segs[s].rec;
+
+    // segment ranges of a partition -> s_beg[b] / s_src[b] (all threads; ends synchronised)
+    auto publish = [&](int b, uint32_t cnt, uint32_t off) {
+        uint32_t tot;
+        uint32_t ex = block_exclusive_scan(cnt, &tot);
+        if (tid < nseg) {
+            s_beg[b][tid] = ex;
+            s_src[b][tid] = off;
+        }
+        if (tid == 0) s_beg[b][nseg] = tot;
+        __syncthreads();
+    };
+    // register prefetch of a partition's records (only when they all fit); global (not flat) loads,
+    // so LDS waits in between do not wait for them
+    int64_t rk[FIRE_RPT], rv[FIRE_RPT];
+    auto prefetch = [&](int b) {
+        const uint32_t total = s_beg[b][nseg];
+        const bool fits = total <= (uint32_t)FIRE_RCAP;
+        const int64_t *addr[FIRE_RPT];
+        int seg = 0;
+#pragma unroll
+        for (int r = 0; r < FIRE_RPT; ++r) {
+            uint32_t i = tid + r * LOG_FIRE_THREADS;
+            addr[r] = s_rp[0];
+            if (fits && i < total) {
+                while (i >= s_beg[b][seg + 1]) seg++;
+                addr[r] = s_rp[seg] + (uint64_t)(s_src[b][seg] + (i - s_beg[b][seg])) * (has_val ? 2 : 1);
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < FIRE_RPT; ++r) {
+            if (has_val) {
+                ll2 r2 = __builtin_nontemporal_load((g_ll2 *)addr[r]);
+                rk[r] = r2.x;
+                rv[r] = r2.y;
+            } else {
+                rk[r] = __builtin_nontemporal_load((g_i64 *)addr[r]);
+                rv[r] = 0;
+            }
+        }
+    };
+
+    uint32_t a_cnt = 0, a_off = 0;
+    if (tid < nseg) {
+        a_cnt = segs[tid].cnt[part];
+        a_off = segs[tid].off[part];
+    }
+    int buf = 0;
+    publish(buf, a_cnt, a_off);
+    prefetch(buf);
+    while (true) {
+        const uint32_t total = s_beg[buf][nseg];
+        const uint32_t nxt = part + gridDim.x;
+        const bool more = nxt < nparts;
+        // next partition's segment offsets: in flight while this one is folded
+        a_cnt = 0;
+        a_off = 0;
+        if (more && tid < nseg) {
+            a_cnt = segs[tid].cnt[nxt];
+            a_off = segs[tid].off[nxt];
+        }
+        const bool fast = total <= (uint32_t)FIRE_RCAP;
+        if (fast) {
+            // group the partition's records by FIRE_GROUPS hash bits: LDS counting sort
+            for (int g = tid; g < FIRE_GROUPS; g += LOG_FIRE_THREADS) s_grp[g] = 0;
+            __syncthreads();
+            uint32_t code[FIRE_RPT];
+#pragma unroll
+            for (int r = 0; r < FIRE_RPT; ++r) {
+                uint32_t i = tid + r * LOG_FIRE_THREADS;
+                code[r] = 0xffffffffu;
                 if (i < total) {
-                    while (i >= s_beg[seg + 1]) seg++;
-                    const LogSegDesc &sd = segs[seg];
-                    uint32_t o_ = s_src[seg] + (i - s_beg[seg]);
-                    kk[u] = sd.key[o_];
-                    if (sd.val) vv[u] = sd.val[o_];
+                    uint32_t g = (uint32_t)part_hash(rk[r]) & (FIRE_GROUPS - 1);
+                    code[r] = (g << 16) | atomicAdd(&s_grp[g], 1u);
                 }
             }
+            __syncthreads();
+            {
+                constexpr int PER = FIRE_GROUPS / LOG_FIRE_THREADS;
+                uint32_t loc[PER], sum = 0, tot;
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                if (i0 + u * LOG_FIRE_THREADS >= total) break;
-                uint64_t h = part_hash(kk[u]);
-                if (rbits && (int)((h >> 24) & ((1u << rbits) - 1)) != round) continue;
-                lds_insert(s_key, s_acc, s_side, cap, p, kk[u], h, vv[u], &s_fail);
+                for (int q = 0; q < PER; ++q) {
+                    loc[q] = s_grp[tid * PER + q];
+                    sum += loc[q];
+                }
+                uint32_t ex = block_exclusive_scan(sum, &tot);
+#pragma unroll
+                for (int q = 0; q < PER; ++q) {
+                    s_grp[tid * PER + q] = ex;
+                    ex += loc[q];
+                }
+                if (tid == 0) s_grp[FIRE_GROUPS] = tot;
+            }
+            __syncthreads();
+#pragma unroll
+            for (int r = 0; r < FIRE_RPT; ++r) {
+                if (code[r] == 0xffffffffu) continue;
+                uint32_t pos = s_grp[code[r] >> 16] + (code[r] & 0xffffu);
+                ll2 r2 = {rk[r], rv[r]};
+                *(ll2 *)&s_dyn[2 * pos] = r2;
+            }
+            __syncthreads();
+        } else {
+            // slow path: hash-table rounds over disjoint ranges of hash bits 12..43, direct loads
+            if (tid == 0) atomicAdd(overflow + 1, 1ull);   // slow-path partitions (statistics)
+            fire_clear(c, p);
+            __syncthreads();
+            const uint64_t kAll = 1ull << 32;
+            uint64_t lo = 0, width = kAll;
+            while (lo < kAll) {
+                const uint64_t hi = lo + width < kAll ? lo + width : kAll;
+                const bool ranged = width < kAll;
+                int seg = 0;
+                for (uint32_t i = tid; i < total; i += LOG_FIRE_THREADS) {
+                    while (i >= s_beg[buf][seg + 1]) seg++;
+                    const int64_t *q = s_rp[seg] + (uint64_t)(s_src[buf][seg] + (i - s_beg[buf][seg])) * (has_val ? 2 : 1);
+                    const int64_t k = q[0];
+                    const uint64_t h = part_hash(k);
+                    if (ranged) {
+                        uint64_t sub = (uint32_t)(h >> 12);
+                        if (sub < lo || sub >= hi) continue;
+                    }
+                    fire_insert(c, p, k, h, has_val ? q[1] : 0);
+                }
+                __syncthreads();
+                const bool failed = s_fail != 0;
+                __syncthreads();
+                if (failed) {
+                    fire_clear(c, p);
+                    __syncthreads();
+                    width >>= 1;
+                    if (width == 0) {
+                        if (tid == 0) atomicAdd(overflow, 1ull);
+                        break;
+                    }
+                    continue;
+                }
+                fire_emit(c, p, rp, start, end, o);
+                lo = hi;
             }
         }
-        __syncthreads();
-        // emit: occupied slots, one output reservation per workgroup
-        unsigned cnt = 0;
-        for (int i = threadIdx.x; i < cap; i += LOG_FIRE_THREADS) cnt += s_key[i] != GWO_EMPTY_KEY;
-        bool side = threadIdx.x == 0 && s_side[0] != 0;
-        cnt += side;
-        unsigned long long pos = block_reserve(cnt, o.count);
-        if (side) {
-            if ((long long)pos < o.cap) {
-                o.key[pos] = GWO_EMPTY_KEY;
-                o.start[pos] = start;
-                o.end[pos] = end;
-                emit_results(p, rp, s_side + 1, 1, o, pos);
-            }
-            pos++;
+        if (more) {
+            publish(buf ^ 1, a_cnt, a_off);
+            prefetch(buf ^ 1);   // in flight during this partition's fold and emit
         }
-        for (int i = threadIdx.x; i < cap; i += LOG_FIRE_THREADS) {
-            int64_t k = s_key[i];
-            if (k == GWO_EMPTY_KEY) continue;
-            if ((long long)pos < o.cap) {
-                o.key[pos] = k;
-                o.start[pos] = start;
-                o.end[pos] = end;
-                emit_results(p, rp, s_acc + i, cap, o, pos);
+        if (fast) {
+            // fold: thread t takes sorted records i = t + r*512; the first occurrence of a key in
+            // its hash group aggregates the group's later records with that key (groups hold ~1-2
+            // records), so every lane walks about the same, short distance.  Rows are placed in
+            // (r, wave, lane) order: each wave's rows of one round are consecutive, so every store
+            // instruction writes one contiguous run.
+            constexpr int NWAVES = LOG_FIRE_THREADS / 64;
+            const int lane = tid & 63, wave = tid >> 6;
+            unsigned first_mask = 0;
+            for (int r = 0; r < FIRE_RPT; ++r) {
+                const uint32_t i = tid + r * LOG_FIRE_THREADS;
+                bool first = false;
+                if (i < total) {
+                    const int64_t k = s_dyn[2 * i];
+                    const uint32_t b = s_grp[(uint32_t)part_hash(k) & (FIRE_GROUPS - 1)];
+                    first = true;
+                    for (uint32_t j = b; j < i; ++j) first &= s_dyn[2 * j] != k;
+                }
+                first_mask |= (unsigned)first << r;
+                const unsigned long long bal = __ballot(first);
+                if (lane == 0) s_wrows[r][wave] = (uint32_t)__popcll(bal);
             }
-            pos++;
+            __syncthreads();
+            if (tid == 0) {   // exclusive prefix over (round, wave), then one reservation per partition
+                uint32_t run = 0;
+                for (int r = 0; r < FIRE_RPT; ++r)
+                    for (int w = 0; w < NWAVES; ++w) {
+                        uint32_t t = s_wrows[r][w];
+                        s_wrows[r][w] = run;
+                        run += t;
+                    }
+                s_rbase = run ? atomicAdd(o.count, (unsigned long long)run) : 0ull;
+            }
+            __syncthreads();
+            const unsigned long long rbase = s_rbase;
+            for (int r = 0; r < FIRE_RPT; ++r) {
+                const bool first = (first_mask >> r) & 1u;
+                const unsigned long long bal = __ballot(first);
+                if (!first) continue;
+                const uint32_t i = tid + r * LOG_FIRE_THREADS;
+                const int64_t k = s_dyn[2 * i];
+                const uint32_t e = s_grp[((uint32_t)part_hash(k) & (FIRE_GROUPS - 1)) + 1];
+                int64_t acc[NW];
+                const int64_t v0 = s_dyn[2 * i + 1];
+#pragma unroll
+                for (int w = 0; w < NW; ++w) acc[w] = lift_word(p, w, v0);
+                for (uint32_t j = i + 1; j < e; ++j) {
+                    const ll2 rr = *(const ll2 *)&s_dyn[2 * j];
+                    if (rr.x != k) continue;
+#pragma unroll
+                    for (int w = 0; w < NW; ++w) acc[w] = combine(p.op[w], acc[w], lift_word(p, w, rr.y));
+                }
+                const unsigned long long pos =
+                    rbase + s_wrows[r][wave] + (unsigned long long)__popcll(bal & ((1ull << lane) - 1ull));
+                if ((long long)pos < o.cap) emit_row<NW>(rp, acc, o, pos, k, start, end);
+            }
+            __syncthreads();   // s_dyn / s_grp are rewritten by the next partition
         }
-        __syncthreads();
+        if (!more) break;
+        part = nxt;
+        buf ^= 1;
     }
-    if (threadIdx.x == 0 && s_fail) atomicAdd(overflow, 1ull);
 }
 
 // ------------------------------------------------------------------------------------------------
 // launchers
 // ------------------------------------------------------------------------------------------------
-void launch_log_scan(const int64_t *key, const int64_t *ts, const int64_t *val, int64_t n, const WindowGeom &g,
-                     long long base, BatchStats *st, unsigned *chist, int64_t *side_key, int64_t *side_ts,
-                     int64_t *side_val, unsigned long long *side_count, long long side_cap, int side_enabled,
-                     hipStream_t s) {
-    int64_t grid = (n + 256LL * 16 - 1) / (256LL * 16);
-    grid = grid < 1 ? 1 : (grid > 1024 ? 1024 : grid);
-    hipLaunchKernelGGL(log_scan_kernel, dim3((int)grid), dim3(256), 0, s, key, ts, val, n, g, base, st, chist,
-                       side_key, side_ts, side_val, side_count, side_cap, side_enabled);
-}
-
-void launch_log_pass1(const int64_t *key, const int64_t *ts, const int64_t *val, int64_t n, const WindowGeom &g,
-                      long long base, int nunits, unsigned long long *cursor, int64_t *tkey, int64_t *tval,
-                      hipStream_t s) {
-    int64_t grid = (n + P1_TILE - 1) / P1_TILE;
+void launch_log_part(const int64_t *key, const int64_t *ts, const int64_t *val, int64_t n, const WindowGeom &g,
+                     long long base, int nunits, int has_val, unsigned long long *cursor, uint64_t cap,
+                     int64_t *tmp, BatchStats *st, int64_t *side_key, int64_t *side_ts, int64_t *side_val,
+                     unsigned long long *side_count, long long side_cap, int side_enabled, hipStream_t s) {
+    int64_t grid = (n + LOG_TILE - 1) / LOG_TILE;
     grid = grid < 1 ? 1 : (grid > 2048 ? 2048 : grid);
-    hipLaunchKernelGGL(log_pass1_kernel, dim3((int)grid), dim3(256), 0, s, key, ts, val, n, g, base, nunits, cursor,
-                       tkey, tval);
+    if (has_val)
+        hipLaunchKernelGGL(log_part_kernel<true>, dim3((int)grid), dim3(LOG_TILE_THREADS), 0, s, key, ts, val, n, g,
+                           base, nunits, cursor, cap, tmp, st, side_key, side_ts, side_val, side_count, side_cap,
+                           side_enabled);
+    else
+        hipLaunchKernelGGL(log_part_kernel<false>, dim3((int)grid), dim3(LOG_TILE_THREADS), 0, s, key, ts, val, n, g,
+                           base, nunits, cursor, cap, tmp, st, side_key, side_ts, side_val, side_count, side_cap,
+                           side_enabled);
 }
 
-void launch_log_pass2(const int64_t *tkey, const int64_t *tval, const unsigned long long *cbase, int nunits,
-                      const LogSegDesc *segs, hipStream_t s) {
-    hipLaunchKernelGGL(log_pass2_kernel, dim3(nunits * 256), dim3(P2_THREADS), 0, s, tkey, tval, cbase, segs);
+__global__ void log_gather_kernel(const unsigned long long *cursor, unsigned long long *counts, int nb) {
+    for (int b = threadIdx.x; b < nb; b += blockDim.x) counts[b] = cursor[(size_t)b * LOG_CUR_STRIDE];
 }
 
+void launch_log_gather(const unsigned long long *cursor, unsigned long long *counts, int nb, hipStream_t s) {
+    hipLaunchKernelGGL(log_gather_kernel, dim3(1), dim3(1024), 0, s, cursor, counts, nb);
+}
+
+void launch_log_split(const int64_t *tmp, int has_val, const LogBucket *buckets, int nb, int nunits,
+                      const LogSegDesc *segs, unsigned *overflow, uint32_t nchunks, hipStream_t s) {
+    (void)nunits;
+    if (nchunks == 0) return;
+    if (has_val)
+        hipLaunchKernelGGL(log_split_kernel<true>, dim3(nchunks), dim3(LOG_TILE_THREADS), 0, s, tmp, buckets, nb, segs,
+                           overflow);
+    else
+        hipLaunchKernelGGL(log_split_kernel<false>, dim3(nchunks), dim3(LOG_TILE_THREADS), 0, s, tmp, buckets, nb,
+                           segs, overflow);
+}
+
+// Slow-path hash table in the fast path's record area (FIRE_RCAP * 16 B): (1 + nwords) * 8 B per slot.
 int log_fire_cap_log2(int nwords) {
-    // table of 64 KiB: (1 + nwords) * 8 B per slot
     int bytes_per = (1 + nwords) * 8;
     int c = 0;
-    while ((2 << c) * bytes_per <= 64 * 1024) c++;
+    while ((2 << c) * bytes_per <= FIRE_RCAP * 16) c++;
     return c;
 }
 
-void launch_log_fire(const LogSegDesc *segs, int nseg, int lp, const AccPlan &plan, const ResultPlan &rp,
-                     int64_t start, int64_t end, OutCols out, unsigned long long *overflow, hipStream_t s) {
+void launch_log_fire(const LogSegDesc *segs, int nseg, int lp, int has_val, const AccPlan &plan,
+                     const ResultPlan &rp, int64_t start, int64_t end, OutCols out, unsigned long long *overflow,
+                     int max_groups, hipStream_t s) {
     int cl = log_fire_cap_log2(plan.nwords);
-    size_t lds = (size_t)(1 + plan.nwords) * 8 << cl;
-    hipLaunchKernelGGL(log_fire_kernel, dim3(1u << lp), dim3(LOG_FIRE_THREADS), lds, s, segs, nseg, lp, cl, plan, rp,
-                       start, end, out, overflow);
+    size_t lds = (size_t)FIRE_RCAP * 16;
+    uint32_t parts = 1u << lp;
+    uint32_t grid = parts < (uint32_t)max_groups ? parts : (uint32_t)max_groups;
+#define GWO_FIRE_NW(NW)                                                                                          \
+    case NW:                                                                                                     \
+        hipLaunchKernelGGL(log_fire_kernel<NW>, dim3(grid), dim3(LOG_FIRE_THREADS), lds, s, segs, nseg, parts, cl, \
+                           has_val, plan, rp, start, end, out, overflow);                                        \
+        break;
+    switch (plan.nwords) {
+        GWO_FIRE_NW(1)
+        GWO_FIRE_NW(2)
+        GWO_FIRE_NW(3)
+        GWO_FIRE_NW(4)
+        GWO_FIRE_NW(5)
+        GWO_FIRE_NW(6)
+        GWO_FIRE_NW(7)
+        default: GWO_FIRE_NW(8)
+    }
+#undef GWO_FIRE_NW
 }
 
 }  // namespace gwo
