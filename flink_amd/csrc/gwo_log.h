@@ -14,7 +14,6 @@
 #define LOG_CUR_STRIDE 16        // K1 bucket cursors: one per 128-B line (memory-side atomics serialise per line)
 #define FIRE_RPT 7                                   // records per thread in the fire's register prefetch
 #define FIRE_RCAP (FIRE_RPT * LOG_FIRE_THREADS)      // 3584: records per partition of the fire's fast path
-#define FIRE_GROUPS 2048                             // hash groups of the fast path's LDS counting sort
 #define LOG_MAX_SEGS 512         // segments (batches) per window that one fire folds (= LOG_FIRE_THREADS)
 
 // One segment = the records one batch appended to one window.  Partition p's records are

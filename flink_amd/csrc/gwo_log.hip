@@ -319,18 +319,20 @@ __global__ __launch_bounds__(LOG_TILE_THREADS) void log_split_kernel(const int64
 
 // ------------------------------------------------------------------------------------------------
 // log_fire: persistent workgroups, each folding partitions p = blockIdx.x, + gridDim.x, ...
-// (WindowOperator.onEventTime + emitWindowContents, WindowOperator.java:430-473, 546-550).
-// Fast path (a partition of <= FIRE_RCAP records): the records are grouped by FIRE_GROUPS hash bits
-// with an LDS counting sort (one 32-bit LDS atomic per record), then each thread folds its groups
-// sequentially in registers -- the first occurrence of a key aggregates the later ones -- and
-// emits one row per key.  No per-word LDS atomics: those were the fold's bottleneck (a hash-table
-// fold costs ~4.5 64-bit LDS atomics per record).  The next partition's segment offsets and
-// records are loaded while the current one is folded and emitted, so a workgroup exposes about one
-// HBM round trip per partition.  Slow path (more records): an LDS hash table folded in rounds over
-// disjoint ranges of a second group of hash bits (the range halves until it fits).
+// (WindowOperator.onEventTime + emitWindowContents, WindowOperator.java:430-473, 546-550) into an LDS
+// hash table (key -> accumulator words) and emitting one row per key.
+// Fast path (a partition of <= FIRE_RCAP records, held in registers by the prefetch):
+//   1. every record finds or claims its key's slot (LDS CAS per probe);
+//   2. the claiming record initialises the slot's words with plain stores;
+//   3. the key's other records combine atomically -- so a key's first record costs no word atomics
+//      (the per-word 64-bit LDS atomics were the fold's bottleneck);
+//   4. the table is swept, rows placed in (round, wave, lane) order so each store instruction writes
+//      one contiguous run, one row-counter reservation per partition, slots reset as they are read.
+// The next partition's segment offsets and records are loaded while the current one is folded and
+// emitted, so a workgroup exposes about one HBM round trip per partition.  Slow path (more records
+// than the prefetch holds, or more keys than the table): rounds over disjoint ranges of a second
+// group of hash bits with direct loads (the range halves until it fits), so no key is lost.
 // ------------------------------------------------------------------------------------------------
-
-
 __device__ __forceinline__ void lds_combine64(int64_t *dst, int op, int64_t x) {
     switch (op) {
         case ACC_ADD_I64: atomicAdd((unsigned long long *)dst, (unsigned long long)x); break;
@@ -494,22 +496,22 @@ __global__ __launch_bounds__(LOG_FIRE_THREADS) void log_fire_kernel(const LogSeg
                                                                     AccPlan p, ResultPlan rp, int64_t start,
                                                                     int64_t end, OutCols o,
                                                                     unsigned long long *overflow) {
-    extern __shared__ __attribute__((aligned(16))) int64_t s_dyn[];   // FIRE_RCAP sorted (key, value) pairs,
-                                                                       // or the slow path's hash table
-    __shared__ uint32_t s_grp[FIRE_GROUPS + 1];       // group counts, then group offsets (+ total)
+    extern __shared__ __attribute__((aligned(16))) int64_t s_dyn[];   // the LDS hash table (key, words; SoA)
     __shared__ int64_t s_side[GWO_MAX_WORDS + 1];
     __shared__ unsigned s_used, s_fail;
     __shared__ uint32_t s_beg[2][LOG_MAX_SEGS + 1];   // flattened record space of a partition: segment s
     __shared__ uint32_t s_src[2][LOG_MAX_SEGS];       //   covers [s_beg[s], s_beg[s+1]) from record s_src[s]
     __shared__ const int64_t *s_rp[LOG_MAX_SEGS];
-    __shared__ uint32_t s_wrows[FIRE_RPT][LOG_FIRE_THREADS / 64];   // rows per (round, wave), then prefixes
+    __shared__ uint32_t s_wrows[8][LOG_FIRE_THREADS / 64];   // rows per (sweep round, wave), then prefixes
     __shared__ unsigned long long s_rbase;
+    __shared__ uint32_t s_side_pos;
     const int tid = threadIdx.x;
     const int cap = 1 << cap_log2;
     FireCtx c{s_dyn, s_dyn + cap, s_side, &s_used, &s_fail, cap, (unsigned)(cap - (cap >> 3))};
     uint32_t part = blockIdx.x;
     if (part >= nparts) return;
     for (int s = tid; s < nseg; s += LOG_FIRE_THREADS) s_rp[s] = segs[s].rec;
+    fire_clear(c, p);   // the first publish() synchronises
 
     // segment ranges of a partition -> s_beg[b] / s_src[b] (all threads; ends synchronised)
     auto publish = [&](int b, uint32_t cnt, uint32_t off) {
@@ -571,48 +573,75 @@ __global__ __launch_bounds__(LOG_FIRE_THREADS) void log_fire_kernel(const LogSeg
             a_cnt = segs[tid].cnt[nxt];
             a_off = segs[tid].off[nxt];
         }
-        const bool fast = total <= (uint32_t)FIRE_RCAP;
+        bool fast = total <= (uint32_t)FIRE_RCAP;
         if (fast) {
-            // group the partition's records by FIRE_GROUPS hash bits: LDS counting sort
-            for (int g = tid; g < FIRE_GROUPS; g += LOG_FIRE_THREADS) s_grp[g] = 0;
-            __syncthreads();
-            uint32_t code[FIRE_RPT];
+            // phase 1: every record finds (or claims) its key's slot; one LDS CAS per probe
+            int slot[FIRE_RPT];
+            unsigned claimed = 0;
 #pragma unroll
             for (int r = 0; r < FIRE_RPT; ++r) {
-                uint32_t i = tid + r * LOG_FIRE_THREADS;
-                code[r] = 0xffffffffu;
+                const uint32_t i = tid + r * LOG_FIRE_THREADS;
+                slot[r] = -1;
+                bool cl = false;
                 if (i < total) {
-                    uint32_t g = (uint32_t)part_hash(rk[r]) & (FIRE_GROUPS - 1);
-                    code[r] = (g << 16) | atomicAdd(&s_grp[g], 1u);
+                    const int64_t k = rk[r];
+                    if (k == GWO_EMPTY_KEY) {
+                        slot[r] = -2;   // Long.MIN_VALUE key: the side slot
+                    } else {
+                        int sl = (int)(part_hash(k) & (uint64_t)(cap - 1));
+                        for (int probes = 0; probes < cap; ++probes) {
+                            unsigned long long prev = atomicCAS((unsigned long long *)&c.key[sl],
+                                                                (unsigned long long)GWO_EMPTY_KEY, (unsigned long long)k);
+                            if ((int64_t)prev == GWO_EMPTY_KEY || (int64_t)prev == k) {
+                                cl = (int64_t)prev == GWO_EMPTY_KEY;
+                                slot[r] = sl;
+                                break;
+                            }
+                            sl = (sl + 1) & (cap - 1);
+                        }
+                        if (slot[r] == -1) s_fail = 1;   // table full
+                    }
                 }
+                claimed |= (unsigned)cl << r;
+                const unsigned long long bal = __ballot(cl);
+                if ((tid & 63) == 0 && bal) atomicAdd(&s_used, (unsigned)__popcll(bal));
             }
             __syncthreads();
-            {
-                constexpr int PER = FIRE_GROUPS / LOG_FIRE_THREADS;
-                uint32_t loc[PER], sum = 0, tot;
-#pragma unroll
-                for (int q = 0; q < PER; ++q) {
-                    loc[q] = s_grp[tid * PER + q];
-                    sum += loc[q];
-                }
-                uint32_t ex = block_exclusive_scan(sum, &tot);
-#pragma unroll
-                for (int q = 0; q < PER; ++q) {
-                    s_grp[tid * PER + q] = ex;
-                    ex += loc[q];
-                }
-                if (tid == 0) s_grp[FIRE_GROUPS] = tot;
-            }
+            fast = s_fail == 0 && s_used <= c.limit;
             __syncthreads();
+            if (fast) {
+                // phase 2: the claiming record initialises its slot with plain stores
 #pragma unroll
-            for (int r = 0; r < FIRE_RPT; ++r) {
-                if (code[r] == 0xffffffffu) continue;
-                uint32_t pos = s_grp[code[r] >> 16] + (code[r] & 0xffffu);
-                ll2 r2 = {rk[r], rv[r]};
-                *(ll2 *)&s_dyn[2 * pos] = r2;
+                for (int r = 0; r < FIRE_RPT; ++r) {
+                    if (!((claimed >> r) & 1u)) continue;
+#pragma unroll
+                    for (int w = 0; w < NW; ++w) c.acc[w * cap + slot[r]] = lift_word(p, w, rv[r]);
+                }
+                __syncthreads();
+                // phase 3: the other records of a key combine atomically (about half of them in C4)
+#pragma unroll
+                for (int r = 0; r < FIRE_RPT; ++r) {
+                    if (slot[r] == -1 || ((claimed >> r) & 1u)) continue;
+                    int64_t *acc;
+                    int accs;
+                    if (slot[r] == -2) {
+                        s_side[0] = 1;
+                        acc = s_side + 1;
+                        accs = 1;
+                    } else {
+                        acc = c.acc + slot[r];
+                        accs = cap;
+                    }
+#pragma unroll
+                    for (int w = 0; w < NW; ++w) lds_combine64(acc + w * accs, p.op[w], lift_word(p, w, rv[r]));
+                }
+                __syncthreads();
+            } else {
+                fire_clear(c, p);   // back to a clean table for the slow path
+                __syncthreads();
             }
-            __syncthreads();
-        } else {
+        }
+        if (!fast) {
             // slow path: hash-table rounds over disjoint ranges of hash bits 12..43, direct loads
             if (tid == 0) atomicAdd(overflow + 1, 1ull);   // slow-path partitions (statistics)
             fire_clear(c, p);
@@ -656,62 +685,61 @@ __global__ __launch_bounds__(LOG_FIRE_THREADS) void log_fire_kernel(const LogSeg
             prefetch(buf ^ 1);   // in flight during this partition's fold and emit
         }
         if (fast) {
-            // fold: thread t takes sorted records i = t + r*512; the first occurrence of a key in
-            // its hash group aggregates the group's later records with that key (groups hold ~1-2
-            // records), so every lane walks about the same, short distance.  Rows are placed in
-            // (r, wave, lane) order: each wave's rows of one round are consecutive, so every store
-            // instruction writes one contiguous run.
+            // emit: thread t sweeps slots t + m*512; rows are placed in (m, wave, lane) order, so each
+            // store instruction writes one contiguous run; slots are reset as they are read
             constexpr int NWAVES = LOG_FIRE_THREADS / 64;
             const int lane = tid & 63, wave = tid >> 6;
-            unsigned first_mask = 0;
-            for (int r = 0; r < FIRE_RPT; ++r) {
-                const uint32_t i = tid + r * LOG_FIRE_THREADS;
-                bool first = false;
-                if (i < total) {
-                    const int64_t k = s_dyn[2 * i];
-                    const uint32_t b = s_grp[(uint32_t)part_hash(k) & (FIRE_GROUPS - 1)];
-                    first = true;
-                    for (uint32_t j = b; j < i; ++j) first &= s_dyn[2 * j] != k;
-                }
-                first_mask |= (unsigned)first << r;
-                const unsigned long long bal = __ballot(first);
-                if (lane == 0) s_wrows[r][wave] = (uint32_t)__popcll(bal);
+            const int rounds = cap / LOG_FIRE_THREADS;
+            for (int m = 0; m < rounds; ++m) {
+                const unsigned long long bal = __ballot(c.key[m * LOG_FIRE_THREADS + tid] != GWO_EMPTY_KEY);
+                if (lane == 0) s_wrows[m][wave] = (uint32_t)__popcll(bal);
             }
             __syncthreads();
             if (tid == 0) {   // exclusive prefix over (round, wave), then one reservation per partition
                 uint32_t run = 0;
-                for (int r = 0; r < FIRE_RPT; ++r)
+                for (int m = 0; m < rounds; ++m)
                     for (int w = 0; w < NWAVES; ++w) {
-                        uint32_t t = s_wrows[r][w];
-                        s_wrows[r][w] = run;
+                        uint32_t t = s_wrows[m][w];
+                        s_wrows[m][w] = run;
                         run += t;
                     }
+                s_side_pos = run;
+                run += s_side[0] != 0;
                 s_rbase = run ? atomicAdd(o.count, (unsigned long long)run) : 0ull;
             }
             __syncthreads();
             const unsigned long long rbase = s_rbase;
-            for (int r = 0; r < FIRE_RPT; ++r) {
-                const bool first = (first_mask >> r) & 1u;
-                const unsigned long long bal = __ballot(first);
-                if (!first) continue;
-                const uint32_t i = tid + r * LOG_FIRE_THREADS;
-                const int64_t k = s_dyn[2 * i];
-                const uint32_t e = s_grp[((uint32_t)part_hash(k) & (FIRE_GROUPS - 1)) + 1];
+            for (int m = 0; m < rounds; ++m) {
+                const int sl = m * LOG_FIRE_THREADS + tid;
+                const int64_t k = c.key[sl];
+                const bool occ = k != GWO_EMPTY_KEY;
+                const unsigned long long bal = __ballot(occ);
+                if (!occ) continue;
                 int64_t acc[NW];
-                const int64_t v0 = s_dyn[2 * i + 1];
 #pragma unroll
-                for (int w = 0; w < NW; ++w) acc[w] = lift_word(p, w, v0);
-                for (uint32_t j = i + 1; j < e; ++j) {
-                    const ll2 rr = *(const ll2 *)&s_dyn[2 * j];
-                    if (rr.x != k) continue;
-#pragma unroll
-                    for (int w = 0; w < NW; ++w) acc[w] = combine(p.op[w], acc[w], lift_word(p, w, rr.y));
+                for (int w = 0; w < NW; ++w) {
+                    acc[w] = c.acc[w * cap + sl];
+                    c.acc[w * cap + sl] = p.ident[w];
                 }
+                c.key[sl] = GWO_EMPTY_KEY;
                 const unsigned long long pos =
-                    rbase + s_wrows[r][wave] + (unsigned long long)__popcll(bal & ((1ull << lane) - 1ull));
+                    rbase + s_wrows[m][wave] + (unsigned long long)__popcll(bal & ((1ull << lane) - 1ull));
                 if ((long long)pos < o.cap) emit_row<NW>(rp, acc, o, pos, k, start, end);
             }
-            __syncthreads();   // s_dyn / s_grp are rewritten by the next partition
+            if (tid == 0 && s_side[0] != 0) {
+                int64_t acc[NW];
+#pragma unroll
+                for (int w = 0; w < NW; ++w) acc[w] = s_side[1 + w];
+                const unsigned long long pos = rbase + s_side_pos;
+                if ((long long)pos < o.cap) emit_row<NW>(rp, acc, o, pos, GWO_EMPTY_KEY, start, end);
+            }
+            __syncthreads();
+            if (tid <= GWO_MAX_WORDS) s_side[tid] = tid == 0 ? 0 : p.ident[tid - 1];
+            if (tid == 0) {
+                s_used = 0;
+                s_fail = 0;
+            }
+            __syncthreads();
         }
         if (!more) break;
         part = nxt;
@@ -758,11 +786,11 @@ void launch_log_split(const int64_t *tmp, int has_val, const LogBucket *buckets,
                            segs, overflow);
 }
 
-// Slow-path hash table in the fast path's record area (FIRE_RCAP * 16 B): (1 + nwords) * 8 B per slot.
+// The fire's LDS hash table: 64 KiB of (1 + nwords) * 8 B slots (power of two).
 int log_fire_cap_log2(int nwords) {
     int bytes_per = (1 + nwords) * 8;
     int c = 0;
-    while ((2 << c) * bytes_per <= FIRE_RCAP * 16) c++;
+    while ((2 << c) * bytes_per <= 64 * 1024) c++;
     return c;
 }
 
@@ -770,7 +798,7 @@ void launch_log_fire(const LogSegDesc *segs, int nseg, int lp, int has_val, cons
                      const ResultPlan &rp, int64_t start, int64_t end, OutCols out, unsigned long long *overflow,
                      int max_groups, hipStream_t s) {
     int cl = log_fire_cap_log2(plan.nwords);
-    size_t lds = (size_t)FIRE_RCAP * 16;
+    size_t lds = (size_t)(1 + plan.nwords) * 8 << cl;
     uint32_t parts = 1u << lp;
     uint32_t grid = parts < (uint32_t)max_groups ? parts : (uint32_t)max_groups;
 #define GWO_FIRE_NW(NW)                                                                                          \
