@@ -22,6 +22,7 @@ STATUS_NAMES = {
     4: "GWO_ERR_OUT_OF_MEMORY", 5: "GWO_ERR_HIP", 6: "GWO_ERR_UNSUPPORTED", 7: "GWO_ERR_MERGE_LATE",
     8: "GWO_ERR_COMM", 9: "GWO_ERR_STATE", 10: "GWO_ERR_CAPACITY",
 }
+globals().update({name: code for code, name in STATUS_NAMES.items()})
 ASSIGNER_TUMBLING, ASSIGNER_SLIDING, ASSIGNER_SESSION = 0, 1, 2
 AGG_COUNT, AGG_SUM, AGG_MIN, AGG_MAX, AGG_AVG = 0, 1, 2, 3, 4
 DTYPE_INT64, DTYPE_FLOAT64 = 0, 1

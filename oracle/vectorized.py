@@ -124,3 +124,32 @@ def sliding_lateness0(keys, ts, vals, batches, size, slide, offset, kinds, value
     v = np.concatenate(vs) if vals is not None else None
     k, s, res = group_aggregate(k, s, v, kinds, value_is_f64)
     return (k, s, s + size, res), late
+
+
+def key_groups(keys, max_parallelism, parallelism=1):
+    """numpy restatement of ``KeyGroupRangeAssignment.assignToKeyGroup`` for Long keys
+    (``Long.hashCode`` -> ``MathUtils.murmurHash`` -> ``% maxParallelism``,
+    RT/state/KeyGroupRangeAssignment.java:60-73, CO/util/MathUtils.java:134-198) and
+    ``computeOperatorIndexForKeyGroup`` (:118-119).  Returns (key_group, operator_index)."""
+    k = np.asarray(keys, dtype=np.int64).view(np.uint64)
+    h = ((k ^ (k >> np.uint64(32))) & np.uint64(0xFFFFFFFF)).astype(np.uint32)
+
+    def rotl(x, r):
+        return (x << np.uint32(r)) | (x >> np.uint32(32 - r))
+
+    with np.errstate(over="ignore"):
+        c = h * np.uint32(0xCC9E2D51)
+        c = rotl(c, 15)
+        c = c * np.uint32(0x1B873593)
+        c = rotl(c, 13)
+        c = c * np.uint32(5) + np.uint32(0xE6546B64)
+        c = c ^ np.uint32(4)
+        c ^= c >> np.uint32(16)
+        c = c * np.uint32(0x85EBCA6B)
+        c ^= c >> np.uint32(13)
+        c = c * np.uint32(0xC2B2AE35)
+        c ^= c >> np.uint32(16)
+    s = c.view(np.int32).astype(np.int64)
+    s = np.where(s >= 0, s, np.where(s == -(1 << 31), 0, -s))
+    kg = s % max_parallelism
+    return kg, kg * parallelism // max_parallelism

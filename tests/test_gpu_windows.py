@@ -484,3 +484,39 @@ def test_fast_division_full_int64_range(F):
             got = F.window_starts(ts, off, size)
             want = [O.get_window_start_with_offset(int(t), off, size) for t in ts]
             assert got.tolist() == want, (size, off)
+
+
+# ---- multi-GPU path (RCCL keyBy shuffle), one rank on the box's one GPU -----------------------------
+@LAYOUTS
+def test_comm_single_rank_matches_oracle(F, layout):
+    """gwo_comm_init with one rank: every batch goes through the partition kernels, the RCCL count and
+    record exchange (send/recv to self) and the min-watermark all-reduce before the local insert."""
+    import ctypes as C
+    from flink_amd import _native as N
+    lib = N.lib()
+    k, t, v, b = _c1(n=300_000, nkeys=20_000, every=20_000)
+    agg = F.MultiAggregate(F.SumAggregate(), F.MinAggregate(), F.MaxAggregate())
+    op = F.GpuWindowOperator(F.TumblingEventTimeWindows.of(5000), agg, state_layout=layout)
+    uid = (C.c_uint8 * N.COMM_ID_BYTES)()
+    N.check(lib.gwo_comm_unique_id(uid))
+    N.check(lib.gwo_comm_init(op.handle, uid, 1, 0), op.handle, "gwo_comm_init")
+    _run_batches(op, k, t, v, b)
+    (wk, ws, we, res), late = V.tumbling_lateness0(k, t, v, _final(b), 5000, 0, [1, 2, 3])
+    got = sorted((a, s, e, *r) for a, s, e, r in op.output)
+    assert got == _want(wk, ws, we, res)
+    assert op.num_late_records_dropped == late
+    op.close()
+
+
+def test_comm_rejects_wrong_key_group_range(F):
+    """With a communicator the handle's range must be its rank's computeKeyGroupRangeForOperatorIndex."""
+    import ctypes as C
+    from flink_amd import _native as N
+    lib = N.lib()
+    op = F.GpuWindowOperator(F.TumblingEventTimeWindows.of(5000), F.SumAggregate(), max_parallelism=128,
+                             key_group_range=(0, 63))
+    uid = (C.c_uint8 * N.COMM_ID_BYTES)()
+    N.check(lib.gwo_comm_unique_id(uid))
+    st = lib.gwo_comm_init(op.handle, uid, 1, 0)   # rank 0 of 1 owns [0, 127], not [0, 63]
+    assert st == N.GWO_ERR_INVALID_ARGUMENT
+    op.close()
