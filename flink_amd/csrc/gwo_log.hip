@@ -531,14 +531,31 @@ __global__ __launch_bounds__(LOG_FIRE_THREADS) void log_fire_kernel(const LogSeg
         const uint32_t total = s_beg[b][nseg];
         const bool fits = total <= (uint32_t)FIRE_RCAP;
         const int64_t *addr[FIRE_RPT];
-        int seg = 0;
+        int segr[FIRE_RPT];
+        if (nseg <= 32) {   // segment of record i = number of segment starts <= i (broadcast LDS reads)
+#pragma unroll
+            for (int r = 0; r < FIRE_RPT; ++r) segr[r] = 0;
+            for (int sg = 1; sg < nseg; ++sg) {
+                const uint32_t bs = s_beg[b][sg];
+#pragma unroll
+                for (int r = 0; r < FIRE_RPT; ++r) segr[r] += (uint32_t)(tid + r * LOG_FIRE_THREADS) >= bs;
+            }
+        } else {
+            int seg = 0;
+#pragma unroll
+            for (int r = 0; r < FIRE_RPT; ++r) {
+                const uint32_t i = tid + r * LOG_FIRE_THREADS;
+                while (i < total && i >= s_beg[b][seg + 1]) seg++;
+                segr[r] = seg;
+            }
+        }
 #pragma unroll
         for (int r = 0; r < FIRE_RPT; ++r) {
-            uint32_t i = tid + r * LOG_FIRE_THREADS;
+            const uint32_t i = tid + r * LOG_FIRE_THREADS;
             addr[r] = s_rp[0];
             if (fits && i < total) {
-                while (i >= s_beg[b][seg + 1]) seg++;
-                addr[r] = s_rp[seg] + (uint64_t)(s_src[b][seg] + (i - s_beg[b][seg])) * (has_val ? 2 : 1);
+                const int sg = segr[r];
+                addr[r] = s_rp[sg] + (uint64_t)(s_src[b][sg] + (i - s_beg[b][sg])) * (has_val ? 2 : 1);
             }
         }
 #pragma unroll
@@ -577,34 +594,36 @@ __global__ __launch_bounds__(LOG_FIRE_THREADS) void log_fire_kernel(const LogSeg
         if (fast) {
             // phase 1: every record finds (or claims) its key's slot; one LDS CAS per probe
             int slot[FIRE_RPT];
-            unsigned claimed = 0;
+            unsigned claimed = 0, pending = 0;
 #pragma unroll
             for (int r = 0; r < FIRE_RPT; ++r) {
                 const uint32_t i = tid + r * LOG_FIRE_THREADS;
                 slot[r] = -1;
-                bool cl = false;
                 if (i < total) {
                     const int64_t k = rk[r];
                     if (k == GWO_EMPTY_KEY) {
-                        slot[r] = -2;   // Long.MIN_VALUE key: the side slot
+                        slot[r] = -2;
                     } else {
                         int sl = (int)(part_hash(k) & (uint64_t)(cap - 1));
                         for (int probes = 0; probes < cap; ++probes) {
                             unsigned long long prev = atomicCAS((unsigned long long *)&c.key[sl],
                                                                 (unsigned long long)GWO_EMPTY_KEY, (unsigned long long)k);
                             if ((int64_t)prev == GWO_EMPTY_KEY || (int64_t)prev == k) {
-                                cl = (int64_t)prev == GWO_EMPTY_KEY;
+                                claimed |= (unsigned)((int64_t)prev == GWO_EMPTY_KEY) << r;
                                 slot[r] = sl;
                                 break;
                             }
                             sl = (sl + 1) & (cap - 1);
                         }
-                        if (slot[r] == -1) s_fail = 1;   // table full
+                        if (slot[r] == -1) pending = 1;
                     }
                 }
-                claimed |= (unsigned)cl << r;
-                const unsigned long long bal = __ballot(cl);
-                if ((tid & 63) == 0 && bal) atomicAdd(&s_used, (unsigned)__popcll(bal));
+            }
+            if (pending) s_fail = 1;   // table full
+            {
+                unsigned nc = (unsigned)__popc(claimed);
+                for (int o2 = 32; o2 > 0; o2 >>= 1) nc += __shfl_xor(nc, o2);
+                if ((tid & 63) == 0 && nc) atomicAdd(&s_used, nc);
             }
             __syncthreads();
             fast = s_fail == 0 && s_used <= c.limit;
@@ -717,11 +736,8 @@ __global__ __launch_bounds__(LOG_FIRE_THREADS) void log_fire_kernel(const LogSeg
                 if (!occ) continue;
                 int64_t acc[NW];
 #pragma unroll
-                for (int w = 0; w < NW; ++w) {
-                    acc[w] = c.acc[w * cap + sl];
-                    c.acc[w * cap + sl] = p.ident[w];
-                }
-                c.key[sl] = GWO_EMPTY_KEY;
+                for (int w = 0; w < NW; ++w) acc[w] = c.acc[w * cap + sl];
+                c.key[sl] = GWO_EMPTY_KEY;   // words need no reset: the next claimer overwrites them
                 const unsigned long long pos =
                     rbase + s_wrows[m][wave] + (unsigned long long)__popcll(bal & ((1ull << lane) - 1ull));
                 if ((long long)pos < o.cap) emit_row<NW>(rp, acc, o, pos, k, start, end);
