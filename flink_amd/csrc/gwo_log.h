@@ -5,9 +5,12 @@
 #include "gwo_internal.h"
 
 #define LOG_NU 4                 // windows one partition launch (K1) covers
-#define LOG_TILE_PER 14          // records per thread in a K1 tile / pass-2 chunk
-#define LOG_TILE_THREADS 256
+#define LOG_K1_PER 14            // K1 tile: 256 threads x 14 records
+#define LOG_K1_THREADS 256
+#define LOG_TILE_PER 7            // pass-2 chunk: 512 threads x 7 records
+#define LOG_TILE_THREADS 512
 #define LOG_TILE (LOG_TILE_PER * LOG_TILE_THREADS)   // 3584 records: 56 KiB of 16-B records in LDS
+static_assert(LOG_K1_PER * LOG_K1_THREADS == LOG_TILE, "K1 tile and pass-2 chunk hold the same records");
 #define LOG_MIN_LP 8             // a window has at least 256 partitions (one per coarse digit)
 #define LOG_MAX_LP 18            // at most 2^18 partitions per window (<= 1024 per coarse digit)
 #define LOG_FIRE_THREADS 512

@@ -72,7 +72,7 @@ __device__ __forceinline__ uint32_t tile_offsets(const uint32_t *s_cnt, uint32_t
 // count (also when it exceeds cap: those records are not written and the host reruns).
 // ------------------------------------------------------------------------------------------------
 template <bool HASV>
-__global__ __launch_bounds__(LOG_TILE_THREADS) void log_part_kernel(
+__global__ __launch_bounds__(LOG_K1_THREADS) void log_part_kernel(
     const int64_t *__restrict__ key, const int64_t *__restrict__ ts, const int64_t *__restrict__ val, int64_t n,
     WindowGeom g, long long base, int nunits, unsigned long long *__restrict__ cursor, uint64_t cap,
     int64_t *__restrict__ tmp, BatchStats *st, int64_t *side_key, int64_t *side_ts, int64_t *side_val,
@@ -82,27 +82,34 @@ __global__ __launch_bounds__(LOG_TILE_THREADS) void log_part_kernel(
     __shared__ uint16_t s_bk[LOG_TILE];
     __shared__ uint32_t s_cnt[LOG_NU * 256];
     __shared__ uint32_t s_off[LOG_NU * 256];
-    __shared__ long long s_min[LOG_TILE_THREADS / 64], s_max[LOG_TILE_THREADS / 64];
+    __shared__ long long s_min[LOG_K1_THREADS / 64], s_max[LOG_K1_THREADS / 64];
     const int nb = nunits * 256;
+    const int per = (nb + LOG_K1_THREADS - 1) / LOG_K1_THREADS;   // counters owned per thread (<= 4)
     const int tid = threadIdx.x;
     long long mn = 0x7fffffffffffffffLL, mx = (long long)0x8000000000000000LL;
     unsigned long long acc = 0, late = 0, refire = 0, bad_ts = 0, out = 0, bad_kg = 0;
-    for (int64_t tile = (int64_t)blockIdx.x * LOG_TILE; tile < n; tile += (int64_t)gridDim.x * LOG_TILE) {
-        for (int i = tid; i < nb; i += LOG_TILE_THREADS) s_cnt[i] = 0;
-        __syncthreads();
-        int64_t kk[LOG_TILE_PER], vv[LOG_TILE_PER], tt[LOG_TILE_PER];
-        uint32_t code[LOG_TILE_PER];
+    int64_t kk[LOG_K1_PER], vv[LOG_K1_PER], tt[LOG_K1_PER];
+    // unconditional loads of a tile (lanes past the end re-read the tile's first record and are
+    // discarded); the next tile's loads are issued before this tile's write phase
+    auto load_tile = [&](int64_t tile) {
 #pragma unroll
-        for (int j = 0; j < LOG_TILE_PER; ++j) {
-            int64_t i = tile + j * LOG_TILE_THREADS + tid;
-            i = i < n ? i : tile;   // unconditional loads; lanes past the end are discarded below
+        for (int j = 0; j < LOG_K1_PER; ++j) {
+            int64_t i = tile + j * LOG_K1_THREADS + tid;
+            i = i < n ? i : (tile < n ? tile : 0);
             tt[j] = __builtin_nontemporal_load(ts + i);
             kk[j] = __builtin_nontemporal_load(key + i);
             vv[j] = HASV ? __builtin_nontemporal_load(val + i) : 0;
         }
+    };
+    const int64_t tstride = (int64_t)gridDim.x * LOG_TILE;
+    if ((int64_t)blockIdx.x * LOG_TILE < n) load_tile((int64_t)blockIdx.x * LOG_TILE);
+    for (int64_t tile = (int64_t)blockIdx.x * LOG_TILE; tile < n; tile += tstride) {
+        for (int i = tid; i < nb; i += LOG_K1_THREADS) s_cnt[i] = 0;
+        __syncthreads();
+        uint32_t code[LOG_K1_PER];
 #pragma unroll
-        for (int j = 0; j < LOG_TILE_PER; ++j) {
-            int64_t i = tile + j * LOG_TILE_THREADS + tid;
+        for (int j = 0; j < LOG_K1_PER; ++j) {
+            int64_t i = tile + j * LOG_K1_THREADS + tid;
             code[j] = 0xffffffffu;
             if (i >= n) continue;
             long long u = 0;
@@ -143,18 +150,18 @@ __global__ __launch_bounds__(LOG_TILE_THREADS) void log_part_kernel(
         }
         __syncthreads();
         uint32_t loc[4];
-        const uint32_t total = tile_offsets(s_cnt, s_off, nb, loc, nunits);
-        // reserve each bucket's run; s_cnt[b] becomes the run's first record in the bucket
+        const uint32_t total = tile_offsets(s_cnt, s_off, nb, loc, per);
+        // reserve each bucket's run (the atomics' round trip overlaps the LDS scatter below);
+        // s_cnt[b] becomes the run's first record in the bucket
+        unsigned long long at[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-            int b = tid * nunits + q;
-            if (q < nunits && loc[q]) {
-                unsigned long long at = atomicAdd(&cursor[(size_t)b * LOG_CUR_STRIDE], (unsigned long long)loc[q]);
-                s_cnt[b] = (uint32_t)(at < cap ? at : cap);
-            }
+            int b = tid * per + q;
+            at[q] = 0;
+            if (q < per && loc[q]) at[q] = atomicAdd(&cursor[(size_t)b * LOG_CUR_STRIDE], (unsigned long long)loc[q]);
         }
 #pragma unroll
-        for (int j = 0; j < LOG_TILE_PER; ++j) {
+        for (int j = 0; j < LOG_K1_PER; ++j) {
             if (code[j] == 0xffffffffu) continue;
             uint32_t b = code[j] >> 16;
             uint32_t pos = s_off[b] + (code[j] & 0xffffu);
@@ -166,8 +173,14 @@ __global__ __launch_bounds__(LOG_TILE_THREADS) void log_part_kernel(
             }
             s_bk[pos] = (uint16_t)b;
         }
+        if (tile + tstride < n) load_tile(tile + tstride);   // next tile in flight during the writes
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            int b = tid * per + q;
+            if (q < per && loc[q]) s_cnt[b] = (uint32_t)(at[q] < cap ? at[q] : cap);
+        }
         __syncthreads();
-        for (uint32_t p = tid; p < total; p += LOG_TILE_THREADS) {
+        for (uint32_t p = tid; p < total; p += LOG_K1_THREADS) {
             uint32_t b = s_bk[p];
             if (b >= (uint32_t)nb) continue;   // defensive: never a write outside the buffer
             uint64_t q = (uint64_t)s_cnt[b] + (p - s_off[b]);
@@ -198,7 +211,7 @@ __global__ __launch_bounds__(LOG_TILE_THREADS) void log_part_kernel(
     __syncthreads();
     if (tid == 0) {
         long long a = s_min[0], b = s_max[0];
-        for (int w = 1; w < LOG_TILE_THREADS / 64; ++w) {
+        for (int w = 1; w < LOG_K1_THREADS / 64; ++w) {
             a = s_min[w] < a ? s_min[w] : a;
             b = s_max[w] > b ? s_max[w] : b;
         }
@@ -773,11 +786,11 @@ void launch_log_part(const int64_t *key, const int64_t *ts, const int64_t *val, 
     int64_t grid = (n + LOG_TILE - 1) / LOG_TILE;
     grid = grid < 1 ? 1 : (grid > 2048 ? 2048 : grid);
     if (has_val)
-        hipLaunchKernelGGL(log_part_kernel<true>, dim3((int)grid), dim3(LOG_TILE_THREADS), 0, s, key, ts, val, n, g,
+        hipLaunchKernelGGL(log_part_kernel<true>, dim3((int)grid), dim3(LOG_K1_THREADS), 0, s, key, ts, val, n, g,
                            base, nunits, cursor, cap, tmp, st, side_key, side_ts, side_val, side_count, side_cap,
                            side_enabled);
     else
-        hipLaunchKernelGGL(log_part_kernel<false>, dim3((int)grid), dim3(LOG_TILE_THREADS), 0, s, key, ts, val, n, g,
+        hipLaunchKernelGGL(log_part_kernel<false>, dim3((int)grid), dim3(LOG_K1_THREADS), 0, s, key, ts, val, n, g,
                            base, nunits, cursor, cap, tmp, st, side_key, side_ts, side_val, side_count, side_cap,
                            side_enabled);
 }
