@@ -163,6 +163,7 @@ Handle::~Handle() {
     DeviceGuard g(cfg.device);
     if (stream) (void)hipStreamSynchronize(stream);
     (void)prof_collect();
+    for (hipEvent_t e : event_pool) (void)hipEventDestroy(e);
     comm_free();
     log_free();
     session_free();

@@ -103,6 +103,7 @@ struct Handle {
     unsigned long long *d_out_count = nullptr;
     unsigned long long *d_scratch_count = nullptr;
     uint64_t out_rows = 0;
+    bool out_count_dirty = false;              // gwo_discard_output: reset d_out_count before the next fire
     unsigned long long zero_u64 = 0;
     unsigned long long *h_scalar = nullptr;    // pinned scalar staging
     int64_t *h_ident_side = nullptr;           // pinned [0, identity words...] side-slot image
@@ -129,6 +130,7 @@ struct Handle {
     bool profiling = false;
     bool debug = false;                        // GWO_DEBUG=1: trace batches to stderr
     std::vector<PendingEvent> pending_events;
+    std::vector<hipEvent_t> event_pool;        // recycled profiling events
     KStat kstats[GWO_KERNEL_COUNT_];
 
     SessionState *sess = nullptr;

@@ -32,13 +32,17 @@ struct LogWindow {
 struct LogState {
     std::map<long long, LogWindow> wins;
     std::multimap<size_t, char *> free_chunks;
-    DevBuf tmp, buckets, segdesc, firedesc;
+    DevBuf tmp, firedesc;
     unsigned long long *d_cursor = nullptr;      // [LOG_NU * 256 * LOG_CUR_STRIDE] bucket cursors of K1
-    unsigned long long *d_counts = nullptr;      // [LOG_NU * 256] gathered cursor values
-    unsigned long long *h_cursor = nullptr;      // pinned copy
-    unsigned *d_split_ovf = nullptr;
-    LogBucket *h_buckets = nullptr;              // pinned [LOG_NU * 256 + 1]
-    LogSegDesc *h_desc = nullptr;                // pinned [LOG_NU]
+    // K1 readback, one D2H copy: [LOG_NU * 256] bucket counts, then the batch's BatchStats
+    // (log_collect_kernel copies them here and resets the cursors and stats for the next launch)
+    unsigned long long *d_rb = nullptr, *h_rb = nullptr;
+    unsigned long long *h_cursor = nullptr;      // = h_rb (counts)
+    // pass-2 plan, one H2D copy: [LOG_NU] segment descriptors, overflow word, [nb + 1] buckets
+    char *d_plan = nullptr, *h_plan = nullptr;
+    LogSegDesc *h_desc = nullptr;
+    unsigned *h_ovf = nullptr;
+    LogBucket *h_buckets = nullptr;
     std::vector<LogSegDesc> h_fire;
     unsigned long long *d_overflow = nullptr;
     uint64_t last_window_keys = 0;               // distinct keys of the last fired window
@@ -50,6 +54,10 @@ struct LogState {
 
 static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
+static constexpr size_t kRbBytes = LOG_NU * 256 * 8 + sizeof(BatchStats);
+static constexpr size_t kPlanDescBytes = LOG_NU * sizeof(LogSegDesc);
+static constexpr size_t kPlanBytes = kPlanDescBytes + 8 + (LOG_NU * 256 + 1) * sizeof(LogBucket);
+
 // Capacity of a fixed-size group that receives Binomial(n, 1/k) records: mean + 6 sigma + slack.
 static uint64_t group_capacity(double mean) {
     return (uint64_t)std::ceil(mean + 6.0 * std::sqrt(mean) + 4.0);
@@ -59,16 +67,18 @@ gwo_status Handle::log_init() {
     logst = new LogState();
     LogState &L = *logst;
     GWO_TRY(dalloc((void **)&L.d_cursor, LOG_NU * 256 * LOG_CUR_STRIDE * 8));
-    GWO_TRY(dalloc((void **)&L.d_counts, LOG_NU * 256 * 8));
-    GWO_TRY(dalloc((void **)&L.d_split_ovf, 8));
+    GWO_TRY(hipcheck(hipMemsetAsync(L.d_cursor, 0, LOG_NU * 256 * LOG_CUR_STRIDE * 8, stream), "cursor"));
+    GWO_TRY(dalloc((void **)&L.d_rb, kRbBytes));
+    GWO_TRY(dalloc((void **)&L.d_plan, kPlanBytes));
     GWO_TRY(dalloc((void **)&L.d_overflow, 16));
     GWO_TRY(hipcheck(hipMemsetAsync(L.d_overflow, 0, 16, stream), "overflow"));
-    GWO_TRY(hipcheck(hipHostMalloc((void **)&L.h_cursor, LOG_NU * 256 * 8, hipHostMallocDefault), "pinned"));
-    GWO_TRY(hipcheck(hipHostMalloc((void **)&L.h_buckets, (LOG_NU * 256 + 1) * sizeof(LogBucket), hipHostMallocDefault),
-                     "pinned"));
-    GWO_TRY(hipcheck(hipHostMalloc((void **)&L.h_desc, LOG_NU * sizeof(LogSegDesc), hipHostMallocDefault), "pinned"));
-    GWO_TRY(ensure_buf(L.buckets, (LOG_NU * 256 + 1) * sizeof(LogBucket)));
-    GWO_TRY(ensure_buf(L.segdesc, LOG_NU * sizeof(LogSegDesc)));
+    GWO_TRY(hipcheck(hipHostMalloc((void **)&L.h_rb, kRbBytes, hipHostMallocDefault), "pinned"));
+    GWO_TRY(hipcheck(hipHostMalloc((void **)&L.h_plan, kPlanBytes, hipHostMallocDefault), "pinned"));
+    L.h_cursor = L.h_rb;
+    L.h_desc = (LogSegDesc *)L.h_plan;
+    L.h_ovf = (unsigned *)(L.h_plan + kPlanDescBytes);
+    L.h_buckets = (LogBucket *)(L.h_plan + kPlanDescBytes + 8);
+    init_stats(0);   // afterwards log_collect_kernel resets the device stats after every K1
     L.cap_log2 = log_fire_cap_log2(plan.nwords);
     return GWO_OK;
 }
@@ -80,16 +90,13 @@ void Handle::log_free() {
         for (auto &c : kv.second.chunks) (void)hipFree(c.base);
     for (auto &kv : L.free_chunks) (void)hipFree(kv.second);
     L.tmp.release();
-    L.buckets.release();
-    L.segdesc.release();
     L.firedesc.release();
     if (L.d_cursor) (void)hipFree(L.d_cursor);
-    if (L.d_counts) (void)hipFree(L.d_counts);
-    if (L.d_split_ovf) (void)hipFree(L.d_split_ovf);
+    if (L.d_rb) (void)hipFree(L.d_rb);
+    if (L.d_plan) (void)hipFree(L.d_plan);
     if (L.d_overflow) (void)hipFree(L.d_overflow);
-    if (L.h_cursor) (void)hipHostFree(L.h_cursor);
-    if (L.h_buckets) (void)hipHostFree(L.h_buckets);
-    if (L.h_desc) (void)hipHostFree(L.h_desc);
+    if (L.h_rb) (void)hipHostFree(L.h_rb);
+    if (L.h_plan) (void)hipHostFree(L.h_plan);
     delete logst;
     logst = nullptr;
 }
@@ -205,19 +212,18 @@ gwo_status Handle::log_split_chunk(long long base, int nunits, uint64_t cap) {
         }
         L.h_buckets[nb] = LogBucket{};
         L.h_buckets[nb].chunk0 = chunks;
-        GWO_TRY(hipcheck(hipMemcpyAsync(L.buckets.ptr, L.h_buckets, (nb + 1) * sizeof(LogBucket), hipMemcpyHostToDevice,
-                                        stream), "buckets"));
-        GWO_TRY(hipcheck(hipMemcpyAsync(L.segdesc.ptr, L.h_desc, nunits * sizeof(LogSegDesc), hipMemcpyHostToDevice,
-                                        stream), "segdesc"));
-        GWO_TRY(hipcheck(hipMemsetAsync(L.d_split_ovf, 0, 4, stream), "split overflow"));
+        *L.h_ovf = 0;
+        GWO_TRY(hipcheck(hipMemcpyAsync(L.d_plan, L.h_plan, kPlanDescBytes + 8 + (nb + 1) * sizeof(LogBucket),
+                                        hipMemcpyHostToDevice, stream), "split plan"));
+        unsigned *d_ovf = (unsigned *)(L.d_plan + kPlanDescBytes);
         prof_begin(GWO_KERNEL_PARTITION);
-        launch_log_split((const int64_t *)L.tmp.ptr, needs_value, (const LogBucket *)L.buckets.ptr, nb, nunits,
-                         (const LogSegDesc *)L.segdesc.ptr, L.d_split_ovf, chunks, stream);
+        launch_log_split((const int64_t *)L.tmp.ptr, needs_value, (const LogBucket *)(L.d_plan + kPlanDescBytes + 8), nb,
+                         nunits, (const LogSegDesc *)L.d_plan, d_ovf, chunks, stream);
         GWO_TRY(launch_ok("log split"));
         uint64_t total = 0;
         for (int w = 0; w < nunits; ++w) total += wcount[w];
         prof_end(GWO_KERNEL_PARTITION, (int64_t)total);
-        GWO_TRY(hipcheck(hipMemcpyAsync(h_scalar, L.d_split_ovf, 4, hipMemcpyDeviceToHost, stream), "split overflow"));
+        GWO_TRY(hipcheck(hipMemcpyAsync(h_scalar, d_ovf, 4, hipMemcpyDeviceToHost, stream), "split overflow"));
         GWO_TRY(hipcheck(hipStreamSynchronize(stream), "log split"));
         if ((uint32_t)h_scalar[0] == 0) break;
         // a partition received more than its capacity (skewed keys): the cursors hold the exact
@@ -253,21 +259,18 @@ gwo_status Handle::insert_log(const int64_t *k, const int64_t *t, const int64_t 
     long long lo = 0, hi = -1;
     while (true) {
         GWO_TRY(ensure_buf(L.tmp, (size_t)nunits * 256 * cap * W * 8));
-        init_stats(base);
-        GWO_TRY(hipcheck(hipMemsetAsync(L.d_cursor, 0, (size_t)nunits * 256 * LOG_CUR_STRIDE * 8, stream), "cursor"));
         prof_begin(GWO_KERNEL_INSERT);
         launch_log_part(k, t, v, n, g, base, nunits, needs_value, L.d_cursor, cap, (int64_t *)L.tmp.ptr, d_stats,
                         (int64_t *)side_key.ptr, (int64_t *)side_ts.ptr, (int64_t *)side_val.ptr, d_side_count,
                         first_pass && side_enabled() ? side_cap : 0, first_pass && side_enabled(), stream);
         GWO_TRY(launch_ok("log partition"));
         prof_end(GWO_KERNEL_INSERT, n);
-        GWO_TRY(hipcheck(hipMemcpyAsync(h_stats, d_stats, sizeof(BatchStats), hipMemcpyDeviceToHost, stream), "stats"));
-        launch_log_gather(L.d_cursor, L.d_counts, nunits * 256, stream);
-        GWO_TRY(hipcheck(hipMemcpyAsync(L.h_cursor, L.d_counts, (size_t)nunits * 256 * 8, hipMemcpyDeviceToHost, stream),
-                         "cursor"));
+        launch_log_collect(L.d_cursor, nunits * 256, d_stats, L.d_rb, stream);
+        GWO_TRY(hipcheck(hipMemcpyAsync(L.h_rb, L.d_rb, kRbBytes, hipMemcpyDeviceToHost, stream), "readback"));
         if (first_pass && side_enabled())
             GWO_TRY(hipcheck(hipMemcpyAsync(h_scalar, d_side_count, 8, hipMemcpyDeviceToHost, stream), "side count"));
         GWO_TRY(hipcheck(hipStreamSynchronize(stream), "log partition sync"));
+        memcpy(h_stats, L.h_rb + LOG_NU * 256, sizeof(BatchStats));
         if (first_pass) {
             if (hs.bad_ts) return poison(GWO_ERR_NO_TIMESTAMP,
                                          "Record has Long.MIN_VALUE timestamp (= no timestamp marker). Is the time "

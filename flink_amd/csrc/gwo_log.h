@@ -45,8 +45,9 @@ void launch_log_part(const int64_t *key, const int64_t *ts, const int64_t *val, 
                      int64_t *tmp, BatchStats *st, int64_t *side_key, int64_t *side_ts, int64_t *side_val,
                      unsigned long long *side_count, long long side_cap, int side_enabled, hipStream_t s);
 // Pass 2: every coarse bucket -> its window's segment, grouped by partition.
-// cursor[b * LOG_CUR_STRIDE] -> counts[b], b < nb
-void launch_log_gather(const unsigned long long *cursor, unsigned long long *counts, int nb, hipStream_t s);
+// After K1: rb[b] = cursor[b * LOG_CUR_STRIDE] (b < nb) and rb[LOG_NU * 256 ...] = *stats; then resets the
+// cursors and the stats for the next K1 launch.
+void launch_log_collect(unsigned long long *cursor, int nb, BatchStats *stats, unsigned long long *rb, hipStream_t s);
 void launch_log_split(const int64_t *tmp, int has_val, const LogBucket *buckets, int nb, int nunits,
                       const LogSegDesc *segs, unsigned *overflow, uint32_t nchunks, hipStream_t s);
 int log_fire_cap_log2(int nwords);

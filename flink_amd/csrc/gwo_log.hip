@@ -795,12 +795,30 @@ void launch_log_part(const int64_t *key, const int64_t *ts, const int64_t *val, 
                            side_enabled);
 }
 
-__global__ void log_gather_kernel(const unsigned long long *cursor, unsigned long long *counts, int nb) {
-    for (int b = threadIdx.x; b < nb; b += blockDim.x) counts[b] = cursor[(size_t)b * LOG_CUR_STRIDE];
+__global__ __launch_bounds__(1024) void log_collect_kernel(unsigned long long *cursor, int nb, BatchStats *st,
+                                                          unsigned long long *rb) {
+    constexpr int SW = (int)(sizeof(BatchStats) / 8);
+    unsigned long long *sw = (unsigned long long *)st;
+    for (int b = threadIdx.x; b < nb; b += blockDim.x) {
+        rb[b] = cursor[(size_t)b * LOG_CUR_STRIDE];
+        cursor[(size_t)b * LOG_CUR_STRIDE] = 0;
+    }
+    unsigned long long w = 0;
+    if (threadIdx.x < SW) {
+        w = sw[threadIdx.x];
+        rb[LOG_NU * 256 + threadIdx.x] = w;
+    }
+    __syncthreads();
+    if (threadIdx.x < SW) sw[threadIdx.x] = 0;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        st->min_idx = 0x7fffffffffffffffLL;
+        st->max_idx = (long long)0x8000000000000000LL;
+    }
 }
 
-void launch_log_gather(const unsigned long long *cursor, unsigned long long *counts, int nb, hipStream_t s) {
-    hipLaunchKernelGGL(log_gather_kernel, dim3(1), dim3(1024), 0, s, cursor, counts, nb);
+void launch_log_collect(unsigned long long *cursor, int nb, BatchStats *stats, unsigned long long *rb, hipStream_t s) {
+    hipLaunchKernelGGL(log_collect_kernel, dim3(1), dim3(1024), 0, s, cursor, nb, stats, rb);
 }
 
 void launch_log_split(const int64_t *tmp, int has_val, const LogBucket *buckets, int nb, int nunits,

@@ -219,6 +219,10 @@ gwo_status Handle::read_occupancy() {
 }
 
 gwo_status Handle::ensure_output(uint64_t extra) {
+    if (out_count_dirty) {
+        GWO_TRY(hipcheck(hipMemsetAsync(d_out_count, 0, 8, stream), "row counter"));
+        out_count_dirty = false;
+    }
     uint64_t need = out_rows + extra;
     if ((long long)need <= out.cap) return GWO_OK;
     uint64_t ncap = std::max<uint64_t>(need, (uint64_t)out.cap * 2);
@@ -246,8 +250,15 @@ gwo_status Handle::ensure_output(uint64_t extra) {
 void Handle::prof_begin(int k) {
     if (!profiling) return;
     hipEvent_t a, b;
-    (void)hipEventCreate(&a);
-    (void)hipEventCreate(&b);
+    if (event_pool.size() >= 2) {   // events are recycled: hipEventCreate costs microseconds per call
+        a = event_pool.back();
+        event_pool.pop_back();
+        b = event_pool.back();
+        event_pool.pop_back();
+    } else {
+        (void)hipEventCreate(&a);
+        (void)hipEventCreate(&b);
+    }
     (void)hipEventRecord(a, stream);
     pending_events.push_back({k, a, b, 0});
 }
@@ -267,8 +278,8 @@ gwo_status Handle::prof_collect() {
         kstats[pe.kernel].launches++;
         kstats[pe.kernel].ms += ms;
         kstats[pe.kernel].items += pe.items;
-        (void)hipEventDestroy(pe.a);
-        (void)hipEventDestroy(pe.b);
+        event_pool.push_back(pe.a);
+        event_pool.push_back(pe.b);
     }
     pending_events.clear();
     return GWO_OK;
@@ -602,7 +613,8 @@ gwo_status gwo_output_view(gwo_handle *hh, gwo_out *cols, int64_t *n) {
 gwo_status gwo_discard_output(gwo_handle *hh) {
     H_OR_FAIL;
     h->out_rows = 0;
-    return h->hipcheck(hipMemsetAsync(h->d_out_count, 0, 8, h->stream), "discard");
+    h->out_count_dirty = true;   // the device row counter is reset before the next fire (ensure_output)
+    return GWO_OK;
 }
 
 gwo_status gwo_drain(gwo_handle *hh, const gwo_out *cols, int64_t cap, int64_t *n_out) {
