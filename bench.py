@@ -43,6 +43,8 @@ def parse():
     p.add_argument("--max-parallelism", type=int, default=32768)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-sample", type=int, default=2_000_000)
+    p.add_argument("--comm-single", action="store_true",
+                   help="attach a 1-rank RCCL communicator at N=1 (measures the exchange path on one GPU)")
     return p.parse_args()
 
 
@@ -114,6 +116,10 @@ def main():
         dist.broadcast(t_uid, 0)
         uid = (C.c_uint8 * N.COMM_ID_BYTES)(*t_uid.cpu().tolist())
         N.check(lib.gwo_comm_init(h, uid, world, rank), h, "gwo_comm_init")
+    elif a.comm_single:
+        uid = (C.c_uint8 * N.COMM_ID_BYTES)()
+        N.check(lib.gwo_comm_unique_id(uid))
+        N.check(lib.gwo_comm_init(h, uid, 1, 0), h, "gwo_comm_init")
 
     fired_rows = [0]
 

@@ -93,6 +93,8 @@ SIGNATURES = [
     ("gwo_window_starts", C.c_int, [_P, C.c_int64, C.c_int64, C.c_int64, _P, C.c_int32]),
     ("gwo_comm_unique_id", C.c_int, [C.POINTER(C.c_uint8)]),
     ("gwo_comm_init", C.c_int, [_P, C.POINTER(C.c_uint8), C.c_int32, C.c_int32]),
+    ("gwo_partition_by_operator", C.c_int, [_P, _P, _P, C.c_int64, C.c_int32, C.c_int32, C.c_int32, _P, C.c_int64,
+                                            _P, C.c_int32]),
     ("gwo_generate", C.c_int, [C.POINTER(GwoGenSpec), C.c_int64, _P, _P, _P, _P, C.c_int32]),
 ]
 

@@ -9,6 +9,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstring>
 #include <vector>
 
@@ -23,11 +24,15 @@ void launch_pack(const int64_t *key, const int64_t *ts, const int64_t *val, cons
 void launch_unpack(const int64_t *in, int64_t n, int64_t *key, int64_t *ts, int64_t *val, hipStream_t s);
 int radix_sort_pairs(const uint32_t *keys, const uint32_t *vals, int64_t n, int key_bits, uint32_t *k1, uint32_t *v1,
                      uint32_t *k2, uint32_t *v2, uint32_t *hist, hipStream_t s);
+void launch_route(const int64_t *key, const int64_t *ts, const int64_t *val, int64_t n, int kind, int max_par,
+                  int nranks, unsigned long long *cursor, uint64_t cap, int64_t *send, hipStream_t s);
+void launch_route_collect(unsigned long long *cursor, int nranks, unsigned long long *counts, hipStream_t s);
+size_t route_cursor_bytes();
 
 struct Comm {
     ncclComm_t nc = nullptr;
     int nranks = 1, rank = 0;
-    DevBuf dest, k1, v1, hist, sendbuf, recvbuf, rk, rt, rv, counts;
+    DevBuf dest, k1, v1, hist, sendbuf, recvbuf, rk, rt, rv, counts, cursor;
     unsigned long long *h_counts = nullptr;   // pinned: [send counts | recv counts]
     int64_t *h_wm = nullptr;                  // pinned
 };
@@ -36,7 +41,7 @@ void Handle::comm_free() {
     if (!comm) return;
     if (comm->nc) ncclCommDestroy(comm->nc);
     for (DevBuf *b : {&comm->dest, &comm->k1, &comm->v1, &comm->hist, &comm->sendbuf, &comm->recvbuf, &comm->rk,
-                      &comm->rt, &comm->rv, &comm->counts})
+                      &comm->rt, &comm->rv, &comm->counts, &comm->cursor})
         b->release();
     if (comm->h_counts) (void)hipHostFree(comm->h_counts);
     if (comm->h_wm) (void)hipHostFree(comm->h_wm);
@@ -49,71 +54,105 @@ static gwo_status nccl_ok(Handle *h, ncclResult_t r, const char *what) {
     return h->poison(GWO_ERR_COMM, (std::string(what) + ": " + ncclGetErrorString(r)).c_str());
 }
 
-gwo_status Handle::comm_exchange(const int64_t *k, const int64_t *t, const int64_t *v, int64_t n, const int64_t **rk,
-                                 const int64_t **rt, const int64_t **rv, int64_t *rn) {
+// keyBy shuffle of one batch: every record goes to the GPU owning its key group; returns the
+// records this rank receives as 24-B {key, ts, value} records (AoS).  Order-insensitive state
+// (tumbling/sliding) uses the fused route kernel; sessions need each source's arrival order per key,
+// so they group by destination with a stable radix pass instead.
+gwo_status Handle::comm_exchange(const int64_t *k, const int64_t *t, const int64_t *v, int64_t n, const int64_t **aos,
+                                 int64_t *rn) {
     Comm &C = *comm;
     const int P = C.nranks;
+    const bool stable = cfg.assigner == GWO_ASSIGNER_SESSION;
     GWO_TRY(ensure_buf(C.counts, (size_t)2 * P * 8));
     unsigned long long *d_send = (unsigned long long *)C.counts.ptr, *d_recv = d_send + P;
-    GWO_TRY(hipcheck(hipMemsetAsync(d_send, 0, (size_t)2 * P * 8, stream), "counts"));
-    const int64_t *perm_src = nullptr;
+    std::vector<uint64_t> soff(P + 1, 0), roff(P + 1, 0);
     prof_begin(GWO_KERNEL_PARTITION);
-    if (n > 0) {
-        GWO_TRY(ensure_buf(C.dest, n * 4));
-        GWO_TRY(ensure_buf(C.k1, n * 4));
-        GWO_TRY(ensure_buf(C.v1, n * 4));
-        GWO_TRY(ensure_buf(C.hist, (size_t)256 * ((n + 4095) / 4096) * 4 + 16));
-        GWO_TRY(ensure_buf(C.sendbuf, n * 24));
-        launch_dest(k, n, cfg.key_kind, cfg.max_parallelism, P, (uint32_t *)C.dest.ptr, stream);
-        launch_dest_count((const uint32_t *)C.dest.ptr, n, d_send, stream);
-        // one stable 8-bit pass: destinations < 256; payload = record index (arrival order kept)
-        radix_sort_pairs((const uint32_t *)C.dest.ptr, nullptr, n, 8, (uint32_t *)C.k1.ptr, (uint32_t *)C.v1.ptr,
-                         nullptr, nullptr, (uint32_t *)C.hist.ptr, stream);
-        launch_pack(k, t, v, (const uint32_t *)C.v1.ptr, n, (int64_t *)C.sendbuf.ptr, stream);
-        GWO_TRY(launch_ok("partition"));
-        perm_src = (const int64_t *)C.sendbuf.ptr;
+    if (!stable) {
+        if (!C.cursor.ptr) {
+            GWO_TRY(ensure_buf(C.cursor, route_cursor_bytes()));
+            GWO_TRY(hipcheck(hipMemsetAsync(C.cursor.ptr, 0, route_cursor_bytes(), stream), "route cursors"));
+        }
+        const double mean = (double)n / P;
+        uint64_t cap = (uint64_t)(mean + 6.0 * std::sqrt(mean) + 64.0);
+        while (true) {
+            GWO_TRY(ensure_buf(C.sendbuf, (size_t)P * cap * 24 + 24));
+            if (n > 0)
+                launch_route(k, t, v, n, cfg.key_kind, cfg.max_parallelism, P, (unsigned long long *)C.cursor.ptr, cap,
+                             (int64_t *)C.sendbuf.ptr, stream);
+            launch_route_collect((unsigned long long *)C.cursor.ptr, P, d_send, stream);
+            GWO_TRY(launch_ok("route"));
+            GWO_TRY(hipcheck(hipMemcpyAsync(C.h_counts, d_send, (size_t)P * 8, hipMemcpyDeviceToHost, stream), "counts"));
+            GWO_TRY(hipcheck(hipStreamSynchronize(stream), "route sync"));
+            uint64_t mx = 0;
+            for (int p = 0; p < P; ++p) mx = std::max<uint64_t>(mx, C.h_counts[p]);
+            if (mx <= cap) break;
+            cap = mx;   // skewed keys: a destination overflowed its region -- redo with the exact size
+        }
+        for (int p = 0; p < P; ++p) soff[p] = (uint64_t)p * cap;   // region starts (records)
+    } else {
+        GWO_TRY(hipcheck(hipMemsetAsync(d_send, 0, (size_t)2 * P * 8, stream), "counts"));
+        if (n > 0) {
+            GWO_TRY(ensure_buf(C.dest, n * 4));
+            GWO_TRY(ensure_buf(C.k1, n * 4));
+            GWO_TRY(ensure_buf(C.v1, n * 4));
+            GWO_TRY(ensure_buf(C.hist, (size_t)256 * ((n + 4095) / 4096) * 4 + 16));
+            GWO_TRY(ensure_buf(C.sendbuf, n * 24));
+            launch_dest(k, n, cfg.key_kind, cfg.max_parallelism, P, (uint32_t *)C.dest.ptr, stream);
+            launch_dest_count((const uint32_t *)C.dest.ptr, n, d_send, stream);
+            // one stable 8-bit pass: destinations < 256; payload = record index (arrival order kept)
+            radix_sort_pairs((const uint32_t *)C.dest.ptr, nullptr, n, 8, (uint32_t *)C.k1.ptr, (uint32_t *)C.v1.ptr,
+                             nullptr, nullptr, (uint32_t *)C.hist.ptr, stream);
+            launch_pack(k, t, v, (const uint32_t *)C.v1.ptr, n, (int64_t *)C.sendbuf.ptr, stream);
+            GWO_TRY(launch_ok("partition"));
+        }
+        GWO_TRY(hipcheck(hipMemcpyAsync(C.h_counts, d_send, (size_t)P * 8, hipMemcpyDeviceToHost, stream), "counts"));
+        GWO_TRY(hipcheck(hipStreamSynchronize(stream), "counts sync"));
+        for (int p = 0; p < P; ++p) soff[p + 1] = soff[p] + C.h_counts[p];
     }
     prof_end(GWO_KERNEL_PARTITION, n);
-    // exchange counts
+    // exchange counts, then records (xGMI is point-to-point: one send/recv pair per peer)
     GWO_TRY(nccl_ok(this, ncclGroupStart(), "group"));
     for (int p = 0; p < P; ++p) {
         GWO_TRY(nccl_ok(this, ncclSend(d_send + p, 1, ncclUint64, p, C.nc, stream), "send count"));
         GWO_TRY(nccl_ok(this, ncclRecv(d_recv + p, 1, ncclUint64, p, C.nc, stream), "recv count"));
     }
     GWO_TRY(nccl_ok(this, ncclGroupEnd(), "group end"));
-    GWO_TRY(hipcheck(hipMemcpyAsync(C.h_counts, d_send, (size_t)2 * P * 8, hipMemcpyDeviceToHost, stream), "counts"));
+    GWO_TRY(hipcheck(hipMemcpyAsync(C.h_counts + P, d_recv, (size_t)P * 8, hipMemcpyDeviceToHost, stream), "counts"));
     GWO_TRY(hipcheck(hipStreamSynchronize(stream), "counts sync"));
-    std::vector<uint64_t> soff(P + 1, 0), roff(P + 1, 0);
-    for (int p = 0; p < P; ++p) {
-        soff[p + 1] = soff[p] + C.h_counts[p];
-        roff[p + 1] = roff[p] + C.h_counts[P + p];
-    }
+    for (int p = 0; p < P; ++p) roff[p + 1] = roff[p] + C.h_counts[P + p];
     const int64_t R = (int64_t)roff[P];
     GWO_TRY(ensure_buf(C.recvbuf, R * 24 + 24));
+    const int64_t *sb = (const int64_t *)C.sendbuf.ptr;
     prof_begin(GWO_KERNEL_EXCHANGE);
     GWO_TRY(nccl_ok(this, ncclGroupStart(), "group"));
     for (int p = 0; p < P; ++p) {
         uint64_t sc = C.h_counts[p], rc = C.h_counts[P + p];
-        if (sc)
-            GWO_TRY(nccl_ok(this, ncclSend(perm_src + 3 * soff[p], 3 * sc, ncclInt64, p, C.nc, stream), "send"));
+        if (sc) GWO_TRY(nccl_ok(this, ncclSend(sb + 3 * soff[p], 3 * sc, ncclInt64, p, C.nc, stream), "send"));
         if (rc)
             GWO_TRY(nccl_ok(this, ncclRecv((int64_t *)C.recvbuf.ptr + 3 * roff[p], 3 * rc, ncclInt64, p, C.nc, stream),
                             "recv"));
     }
     GWO_TRY(nccl_ok(this, ncclGroupEnd(), "group end"));
     prof_end(GWO_KERNEL_EXCHANGE, R);
-    GWO_TRY(ensure_buf(C.rk, R * 8 + 8));
-    GWO_TRY(ensure_buf(C.rt, R * 8 + 8));
-    GWO_TRY(ensure_buf(C.rv, R * 8 + 8));
-    if (R > 0) {
-        launch_unpack((const int64_t *)C.recvbuf.ptr, R, (int64_t *)C.rk.ptr, (int64_t *)C.rt.ptr, (int64_t *)C.rv.ptr,
-                      stream);
+    *aos = (const int64_t *)C.recvbuf.ptr;
+    *rn = R;
+    return GWO_OK;
+}
+
+// AoS {key, ts, value} records -> the handle's column scratch (table, sliding and session layouts)
+gwo_status Handle::comm_unpack(const int64_t *aos, int64_t n, const int64_t **rk, const int64_t **rt,
+                               const int64_t **rv) {
+    Comm &C = *comm;
+    GWO_TRY(ensure_buf(C.rk, n * 8 + 8));
+    GWO_TRY(ensure_buf(C.rt, n * 8 + 8));
+    GWO_TRY(ensure_buf(C.rv, n * 8 + 8));
+    if (n > 0) {
+        launch_unpack(aos, n, (int64_t *)C.rk.ptr, (int64_t *)C.rt.ptr, (int64_t *)C.rv.ptr, stream);
         GWO_TRY(launch_ok("unpack"));
     }
     *rk = (const int64_t *)C.rk.ptr;
     *rt = (const int64_t *)C.rt.ptr;
     *rv = needs_value ? (const int64_t *)C.rv.ptr : nullptr;
-    *rn = R;
     return GWO_OK;
 }
 
@@ -174,4 +213,44 @@ extern "C" gwo_status gwo_comm_init(gwo_handle *hh, const uint8_t *id, int32_t n
     }
     h->comm = C;
     return GWO_OK;
+}
+
+// Stateless batch form of KeyGroupStreamPartitioner.selectChannel (the route kernel the exchange
+// uses), for hosts that run their own transport and for the tests.  Host or device pointers.
+extern "C" gwo_status gwo_partition_by_operator(const int64_t *key, const int64_t *ts, const int64_t *value, int64_t n,
+                                                int32_t key_kind, int32_t max_parallelism, int32_t parallelism,
+                                                int64_t *out, int64_t cap, int64_t *counts, int32_t device) {
+    if (n < 0 || cap < 0 || !out || !counts || (n > 0 && (!key || !ts))) return GWO_ERR_INVALID_ARGUMENT;
+    if (max_parallelism < 1 || max_parallelism > 32768 || parallelism < 1 || parallelism > 256 ||
+        parallelism > max_parallelism || (key_kind != GWO_KEY_LONG && key_kind != GWO_KEY_INT))
+        return GWO_ERR_INVALID_ARGUMENT;
+    DeviceGuard guard_(device);
+    hipStream_t s;
+    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return GWO_ERR_HIP;
+    const size_t nb = (size_t)n * 8 + 8, ob = (size_t)parallelism * cap * 24 + 24;
+    void *dk = nullptr, *dt = nullptr, *dv = nullptr, *dout = nullptr, *dcur = nullptr, *dcnt = nullptr;
+    gwo_status st = GWO_OK;
+    if (hipMalloc(&dk, nb) != hipSuccess || hipMalloc(&dt, nb) != hipSuccess || hipMalloc(&dv, nb) != hipSuccess ||
+        hipMalloc(&dout, ob) != hipSuccess || hipMalloc(&dcur, route_cursor_bytes()) != hipSuccess ||
+        hipMalloc(&dcnt, 256 * 8) != hipSuccess)
+        st = GWO_ERR_OUT_OF_MEMORY;
+    if (st == GWO_OK) {
+        (void)hipMemsetAsync(dcur, 0, route_cursor_bytes(), s);
+        (void)hipMemsetAsync(dv, 0, nb, s);
+        if (n > 0) {
+            (void)hipMemcpyAsync(dk, key, n * 8, hipMemcpyDefault, s);
+            (void)hipMemcpyAsync(dt, ts, n * 8, hipMemcpyDefault, s);
+            if (value) (void)hipMemcpyAsync(dv, value, n * 8, hipMemcpyDefault, s);
+            launch_route((const int64_t *)dk, (const int64_t *)dt, (const int64_t *)dv, n, key_kind, max_parallelism,
+                         parallelism, (unsigned long long *)dcur, (uint64_t)cap, (int64_t *)dout, s);
+        }
+        launch_route_collect((unsigned long long *)dcur, parallelism, (unsigned long long *)dcnt, s);
+        (void)hipMemcpyAsync(out, dout, (size_t)parallelism * cap * 24, hipMemcpyDefault, s);
+        (void)hipMemcpyAsync(counts, dcnt, (size_t)parallelism * 8, hipMemcpyDefault, s);
+        if (hipStreamSynchronize(s) != hipSuccess) st = GWO_ERR_HIP;
+    }
+    for (void *p : {dk, dt, dv, dout, dcur, dcnt})
+        if (p) (void)hipFree(p);
+    (void)hipStreamDestroy(s);
+    return st;
 }

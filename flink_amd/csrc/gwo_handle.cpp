@@ -199,9 +199,13 @@ gwo_status Handle::submit(const int64_t *key, const int64_t *ts, const void *val
     if (!comm && n == 0) return GWO_OK;
     if (n > 0) GWO_TRY(stage_inputs(key, ts, needs_value ? val : nullptr, n, &dk, &dt, &dv));
     if (comm) {
-        const int64_t *rk, *rt, *rv;
+        const int64_t *aos = nullptr;
         int64_t rn = 0;
-        GWO_TRY(comm_exchange(dk, dt, dv, n, &rk, &rt, &rv, &rn));
+        GWO_TRY(comm_exchange(dk, dt, dv, n, &aos, &rn));
+        if (rn == 0) return GWO_OK;
+        if (logst) return insert_log(aos, aos + 1, aos + 2, rn, 3);   // K1 reads the received records in place
+        const int64_t *rk, *rt, *rv;
+        GWO_TRY(comm_unpack(aos, rn, &rk, &rt, &rv));
         return submit_local(rk, rt, rv, rn);
     }
     return submit_local(dk, dt, dv, n);

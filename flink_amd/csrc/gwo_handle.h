@@ -219,13 +219,14 @@ struct Handle {
     void log_release(LogWindow &W);
     int log_choose_lp(uint64_t batch_records) const;
     gwo_status log_split_chunk(long long base, int nunits, uint64_t cap);
-    gwo_status insert_log(const int64_t *k, const int64_t *t, const int64_t *v, int64_t n);
+    gwo_status insert_log(const int64_t *k, const int64_t *t, const int64_t *v, int64_t n, int64_t stride = 1);
     gwo_status fire_log(int64_t new_wm);
     gwo_status log_state_size(int64_t *entries);
     // comm (gwo_comm.cpp)
     void comm_free();
-    gwo_status comm_exchange(const int64_t *k, const int64_t *t, const int64_t *v, int64_t n, const int64_t **rk,
-                             const int64_t **rt, const int64_t **rv, int64_t *rn);
+    gwo_status comm_exchange(const int64_t *k, const int64_t *t, const int64_t *v, int64_t n, const int64_t **aos,
+                             int64_t *rn);
+    gwo_status comm_unpack(const int64_t *aos, int64_t n, const int64_t **rk, const int64_t **rt, const int64_t **rv);
     gwo_status comm_min_watermark(int64_t wm, int64_t *out);
 
     void prof_begin(int k);

@@ -247,7 +247,7 @@ gwo_status Handle::log_split_chunk(long long base, int nunits, uint64_t cap) {
     return GWO_OK;
 }
 
-gwo_status Handle::insert_log(const int64_t *k, const int64_t *t, const int64_t *v, int64_t n) {
+gwo_status Handle::insert_log(const int64_t *k, const int64_t *t, const int64_t *v, int64_t n, int64_t stride) {
     LogState &L = *logst;
     WindowGeom g = geom_now();
     BatchStats &hs = *h_stats;
@@ -260,7 +260,7 @@ gwo_status Handle::insert_log(const int64_t *k, const int64_t *t, const int64_t 
     while (true) {
         GWO_TRY(ensure_buf(L.tmp, (size_t)nunits * 256 * cap * W * 8));
         prof_begin(GWO_KERNEL_INSERT);
-        launch_log_part(k, t, v, n, g, base, nunits, needs_value, L.d_cursor, cap, (int64_t *)L.tmp.ptr, d_stats,
+        launch_log_part(k, t, v, n, stride, g, base, nunits, needs_value, L.d_cursor, cap, (int64_t *)L.tmp.ptr, d_stats,
                         (int64_t *)side_key.ptr, (int64_t *)side_ts.ptr, (int64_t *)side_val.ptr, d_side_count,
                         first_pass && side_enabled() ? side_cap : 0, first_pass && side_enabled(), stream);
         GWO_TRY(launch_ok("log partition"));

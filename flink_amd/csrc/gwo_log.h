@@ -40,7 +40,9 @@ struct LogBucket {
 
 namespace gwo {
 // K1: classify + key-group check + late accounting + (window, coarse digit) grouping of a batch.
-void launch_log_part(const int64_t *key, const int64_t *ts, const int64_t *val, int64_t n, const WindowGeom &g,
+// key/ts/val columns with `stride` int64 words between records (1: SoA columns; 3: {key, ts, value} records)
+void launch_log_part(const int64_t *key, const int64_t *ts, const int64_t *val, int64_t n, int64_t stride,
+                     const WindowGeom &g,
                      long long base, int nunits, int has_val, unsigned long long *cursor, uint64_t cap,
                      int64_t *tmp, BatchStats *st, int64_t *side_key, int64_t *side_ts, int64_t *side_val,
                      unsigned long long *side_count, long long side_cap, int side_enabled, hipStream_t s);

@@ -74,7 +74,7 @@ __device__ __forceinline__ uint32_t tile_offsets(const uint32_t *s_cnt, uint32_t
 template <bool HASV>
 __global__ __launch_bounds__(LOG_K1_THREADS) void log_part_kernel(
     const int64_t *__restrict__ key, const int64_t *__restrict__ ts, const int64_t *__restrict__ val, int64_t n,
-    WindowGeom g, long long base, int nunits, unsigned long long *__restrict__ cursor, uint64_t cap,
+    int64_t stride, WindowGeom g, long long base, int nunits, unsigned long long *__restrict__ cursor, uint64_t cap,
     int64_t *__restrict__ tmp, BatchStats *st, int64_t *side_key, int64_t *side_ts, int64_t *side_val,
     unsigned long long *side_count, long long side_cap, int side_enabled) {
     constexpr int W = HASV ? 2 : 1;
@@ -96,9 +96,9 @@ __global__ __launch_bounds__(LOG_K1_THREADS) void log_part_kernel(
         for (int j = 0; j < LOG_K1_PER; ++j) {
             int64_t i = tile + j * LOG_K1_THREADS + tid;
             i = i < n ? i : (tile < n ? tile : 0);
-            tt[j] = __builtin_nontemporal_load(ts + i);
-            kk[j] = __builtin_nontemporal_load(key + i);
-            vv[j] = HASV ? __builtin_nontemporal_load(val + i) : 0;
+            tt[j] = __builtin_nontemporal_load(ts + i * stride);
+            kk[j] = __builtin_nontemporal_load(key + i * stride);
+            vv[j] = HASV ? __builtin_nontemporal_load(val + i * stride) : 0;
         }
     };
     const int64_t tstride = (int64_t)gridDim.x * LOG_TILE;
@@ -139,7 +139,7 @@ __global__ __launch_bounds__(LOG_K1_THREADS) void log_part_kernel(
                     if ((long long)pos < side_cap) {
                         side_key[pos] = kk[j];
                         side_ts[pos] = tt[j];
-                        side_val[pos] = val ? val[i] : 0;
+                        side_val[pos] = val ? val[i * stride] : 0;
                     }
                 }
             } else if (c == L_REFIRE) {
@@ -779,18 +779,19 @@ __global__ __launch_bounds__(LOG_FIRE_THREADS) void log_fire_kernel(const LogSeg
 // ------------------------------------------------------------------------------------------------
 // launchers
 // ------------------------------------------------------------------------------------------------
-void launch_log_part(const int64_t *key, const int64_t *ts, const int64_t *val, int64_t n, const WindowGeom &g,
+void launch_log_part(const int64_t *key, const int64_t *ts, const int64_t *val, int64_t n, int64_t stride,
+                     const WindowGeom &g,
                      long long base, int nunits, int has_val, unsigned long long *cursor, uint64_t cap,
                      int64_t *tmp, BatchStats *st, int64_t *side_key, int64_t *side_ts, int64_t *side_val,
                      unsigned long long *side_count, long long side_cap, int side_enabled, hipStream_t s) {
     int64_t grid = (n + LOG_TILE - 1) / LOG_TILE;
     grid = grid < 1 ? 1 : (grid > 2048 ? 2048 : grid);
     if (has_val)
-        hipLaunchKernelGGL(log_part_kernel<true>, dim3((int)grid), dim3(LOG_K1_THREADS), 0, s, key, ts, val, n, g,
+        hipLaunchKernelGGL(log_part_kernel<true>, dim3((int)grid), dim3(LOG_K1_THREADS), 0, s, key, ts, val, n, stride, g,
                            base, nunits, cursor, cap, tmp, st, side_key, side_ts, side_val, side_count, side_cap,
                            side_enabled);
     else
-        hipLaunchKernelGGL(log_part_kernel<false>, dim3((int)grid), dim3(LOG_K1_THREADS), 0, s, key, ts, val, n, g,
+        hipLaunchKernelGGL(log_part_kernel<false>, dim3((int)grid), dim3(LOG_K1_THREADS), 0, s, key, ts, val, n, stride, g,
                            base, nunits, cursor, cap, tmp, st, side_key, side_ts, side_val, side_count, side_cap,
                            side_enabled);
 }

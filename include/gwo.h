@@ -27,6 +27,7 @@
  *   gwo_assign_key_groups KeyGroupRangeAssignment.assignToKeyGroup / computeOperatorIndexForKeyGroup
  *                                                               flink-runtime/.../state/KeyGroupRangeAssignment.java:48-73,118-119
  *   gwo_comm_*            keyBy shuffle (KeyGroupStreamPartitioner + network stack) across the GPUs of a node
+ *   gwo_partition_by_operator  KeyGroupStreamPartitioner.selectChannel over a batch (route step of the shuffle)
  *                                                               SJ/runtime/partitioner/KeyGroupStreamPartitioner.java:51-58
  *
  * Error convention: every call returns a gwo_status; nothing is thrown across the ABI.  A failing
@@ -197,6 +198,16 @@ gwo_status gwo_comm_unique_id(uint8_t id[GWO_COMM_ID_BYTES]);
  * gwo_advance_watermark are collective: gwo_submit routes records to their owner GPU
  * (partition + ncclSend/ncclRecv all-to-all); the watermark becomes the min over ranks. */
 gwo_status gwo_comm_init(gwo_handle *h, const uint8_t id[GWO_COMM_ID_BYTES], int32_t nranks, int32_t rank);
+
+/* Batch form of KeyGroupStreamPartitioner.selectChannel (KeyGroupStreamPartitioner.java:51-58): groups n
+ * records by destination computeOperatorIndexForKeyGroup(assignToKeyGroup(key)) into per-destination runs
+ * of 24-byte {key, ts, value} records -- the route step of the multi-GPU exchange, for hosts with their own
+ * transport.  out holds `parallelism` regions of `cap` records (region p at out + 3 * p * cap int64 words);
+ * counts[p] = records routed to p (a count above cap: region p overflowed and only cap were written).
+ * Order within a region is unspecified.  Host or device pointers; value may be NULL (sent as 0). */
+gwo_status gwo_partition_by_operator(const int64_t *key, const int64_t *ts, const int64_t *value, int64_t n,
+                                     int32_t key_kind, int32_t max_parallelism, int32_t parallelism, int64_t *out,
+                                     int64_t cap, int64_t *counts, int32_t device);
 
 /* ---- synthetic sources (device-resident benchmark/parity inputs; splitmix64) ---- */
 typedef struct {

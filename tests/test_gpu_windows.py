@@ -520,3 +520,33 @@ def test_comm_rejects_wrong_key_group_range(F):
     st = lib.gwo_comm_init(op.handle, uid, 1, 0)   # rank 0 of 1 owns [0, 127], not [0, 63]
     assert st == N.GWO_ERR_INVALID_ARGUMENT
     op.close()
+
+
+@pytest.mark.parametrize("par,maxp", [(8, 32768), (3, 128), (1, 128), (256, 32768)])
+def test_partition_by_operator_routes_like_the_partitioner(F, par, maxp):
+    """The exchange's route kernel: every record lands in the region of
+    computeOperatorIndexForKeyGroup(assignToKeyGroup(key)) with its ts and value, none lost or duplicated."""
+    import ctypes as C
+    from flink_amd import _native as N
+    rng = np.random.default_rng(par)
+    n = 200_003
+    k = rng.integers(-(1 << 63), (1 << 63) - 1, n, dtype=np.int64)
+    k[:1000] = 42   # a hot key: one destination gets far more than its share
+    t = rng.integers(0, 1 << 40, n, dtype=np.int64)
+    v = rng.integers(-1000, 1000, n, dtype=np.int64)
+    _, dest = V.key_groups(k, maxp, par)
+    cap = int(np.bincount(dest, minlength=par).max())
+    out = np.zeros((par, cap, 3), np.int64)
+    counts = np.zeros(par, np.int64)
+    p = lambda a: a.ctypes.data_as(C.c_void_p)
+    N.check(N.lib().gwo_partition_by_operator(p(k), p(t), p(v), n, N.KEY_LONG, maxp, par, p(out), cap, p(counts), 0))
+    assert counts.tolist() == np.bincount(dest, minlength=par).tolist()
+    for d in range(par):
+        got = out[d, :counts[d]]
+        want = np.stack([k[dest == d], t[dest == d], v[dest == d]], 1)
+        assert sorted(map(tuple, got.tolist())) == sorted(map(tuple, want.tolist()))
+    # a too-small region reports the true count and writes only `cap` records
+    small = max(1, cap // 4)
+    out2 = np.zeros((par, small, 3), np.int64)
+    N.check(N.lib().gwo_partition_by_operator(p(k), p(t), p(v), n, N.KEY_LONG, maxp, par, p(out2), small, p(counts), 0))
+    assert counts.tolist() == np.bincount(dest, minlength=par).tolist()
