@@ -1,0 +1,160 @@
+#!/usr/bin/env python3
+"""Throughput of the other BASELINE.json configurations (bench.py is the C4 headline).
+
+  c1  README-style tumbling sum: 1M records, 10K Long keys, 5 s windows, watermark every 10K records
+  c2  YSB-shaped: 10 s tumbling count per campaign (1K campaigns from 10K ad ids), 100M events at
+      1M events/s of event time, watermark every second (the ad-event filter is not modelled)
+  c3  sliding 60 s / 1 s average over 10M keys, 200M records over 120 s (pane design)
+  c5  event-time sessions, 30 s gap: 100K keys, 10M records in bursts, arrival order = ts + U[0, 5 s),
+      watermark maxTs - 5 s - 1 after every 10 s of event time
+
+Inputs are synthetic and resident in HBM before timing (C5's stream is built on the host with numpy
+and uploaded once).  A step = gwo_submit(batch) + gwo_advance_watermark + discarding the rows.
+Prints one JSON line per configuration (same fields as bench.py; `roofline_path` uses SURVEY.md
+§8d's B_alg with the configuration's I/S/O).  Usage: python bench_configs.py [c1 c2 c3 c5]
+"""
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+
+KERNELS = ("scan", "insert", "fire", "partition", "exchange", "slide", "session")
+
+
+def gen_device(N, lib, dev, torch, n, nkeys, span, disorder, key_mode=0, seed=42):
+    key = torch.empty(n, dtype=torch.int64, device=dev)
+    ts = torch.empty(n, dtype=torch.int64, device=dev)
+    val = torch.empty(n, dtype=torch.int64, device=dev)
+    spec = N.GwoGenSpec(seed, 0, n, nkeys, span, disorder, 0, 1000, N.DTYPE_INT64, key_mode)
+    N.check(lib.gwo_generate(C.byref(spec), n, key.data_ptr(), ts.data_ptr(), val.data_ptr(), None, 0), None, "gen")
+    torch.cuda.synchronize()
+    return key, ts, val
+
+
+def session_stream(num_keys, n, gap=30_000, lag=5_000, seed=42, mean_inner=5_000, events_per_session=10):
+    """Bursts per key with exponential inner gaps (< gap), separated by >= gap + 1 ms; arrival order
+    sorted by ts + U[0, lag) (same shape as SURVEY.md §8d's C5 generator)."""
+    rng = np.random.default_rng(seed)
+    per = max(1, n // num_keys)
+    keys = np.repeat(np.arange(num_keys, dtype=np.int64), per)
+    m = len(keys)
+    inner = np.minimum(rng.exponential(mean_inner, m), gap - 1).astype(np.int64)
+    new = rng.random(m) < 1.0 / events_per_session
+    between = (gap + 1 + rng.exponential(gap, m)).astype(np.int64)
+    step = np.where(new, between, inner)
+    first = np.arange(m) % per == 0
+    start = rng.integers(0, 60_000, num_keys)
+    step[first] = 0
+    ts = np.cumsum(step)
+    ts = ts - np.repeat(ts[first], per) + np.repeat(start, per)
+    vals = rng.integers(0, 1000, m).astype(np.int64)
+    order = np.argsort(ts + rng.integers(0, lag, m), kind="stable")
+    return keys[order], ts[order], vals[order]
+
+
+def run(cfg):
+    import torch
+    import flink_amd as F
+    from flink_amd import _native as N
+    lib = N.lib()
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(0)
+    lag = 1000
+    if cfg == "c1":
+        n, nkeys, span, every = 1_000_000, 10_000, 60_000, 10_000
+        key, ts, val = gen_device(N, lib, dev, torch, n, nkeys, span, 1000)
+        assigner, agg, exp = F.TumblingEventTimeWindows.of(5000), F.SumAggregate(), 0
+        I_B, S_B, O_B, workload = 24, 24, 32, "C1 tumbling 5 s sum, 1M records, 10K keys"
+    elif cfg == "c2":
+        n, nkeys, span, every = 100_000_000, 1_000, 100_000, 1_000_000
+        key, ts, val = gen_device(N, lib, dev, torch, n, nkeys, span, 1000, key_mode=1)
+        assigner, agg, exp = F.TumblingEventTimeWindows.of(10_000), F.CountAggregate(), 1000
+        I_B, S_B, O_B, workload = 16, 24, 32, "C2 YSB-shaped 10 s tumbling count per campaign, 1K campaigns"
+    elif cfg == "c3":
+        n, nkeys, span = 200_000_000, 10_000_000, 120_000
+        every = n * 1000 // span
+        key, ts, val = gen_device(N, lib, dev, torch, n, nkeys, span, 1000)
+        assigner, agg, exp = F.SlidingEventTimeWindows.of(60_000, 1000), F.AverageAggregate(), 0
+        I_B, S_B, O_B, workload = 24, 32, 32, "C3 sliding 60 s / 1 s avg, 10M keys, 200M records"
+    elif cfg == "c5":
+        lag = 5000
+        k, t, v = session_stream(100_000, 10_000_000, lag=lag)
+        n, every = len(k), 100_000
+        key, ts, val = (torch.from_numpy(x).to(dev) for x in (k, t, v))
+        assigner, agg, exp = F.EventTimeSessionWindows.withGap(30_000), F.SumAggregate(), 100_000
+        I_B, S_B, O_B, workload = 24, 32, 32, "C5 event-time sessions 30 s gap, 100K keys, 10M records"
+    else:
+        raise SystemExit(f"unknown config {cfg}")
+    if cfg == "c5":
+        # punctuate by event time (every 10 s of the running max timestamp), as a periodic
+        # BoundedOutOfOrderness generator would: the stream's sparse tail would otherwise put many
+        # sessions of one key into a single batch ahead of its watermark
+        rm = np.maximum.accumulate(t)
+        cuts = np.flatnonzero(np.diff(rm // 10_000)) + 1
+        edges = [0] + cuts.tolist() + [n]
+        bounds = [(a, b) for a, b in zip(edges[:-1], edges[1:]) if b > a]
+    else:
+        bounds = [(s, min(s + every, n)) for s in range(0, n, every)]
+    run_max, wms = -(1 << 63), []
+    tsc = ts.cpu().numpy()
+    for s, e in bounds:
+        run_max = max(run_max, int(tsc[s:e].max()))
+        wms.append(run_max - lag - 1)
+    op = F.GpuWindowOperator(assigner, agg, max_parallelism=128, expected_keys=exp)
+    h = op.handle
+    rows = [0]
+
+    def step(i):
+        s, e = bounds[i]
+        N.check(lib.gwo_submit(h, C.c_void_p(key.data_ptr() + 8 * s), C.c_void_p(ts.data_ptr() + 8 * s),
+                               C.c_void_p(val.data_ptr() + 8 * s), e - s), h, "submit")
+        N.check(lib.gwo_advance_watermark(h, wms[i]), h, "watermark")
+        c = C.c_int64()
+        N.check(lib.gwo_output_count(h, C.byref(c)), h)
+        rows[0] += c.value
+        N.check(lib.gwo_discard_output(h), h)
+
+    warm = max(1, len(bounds) // 10)
+    for i in range(warm):
+        step(i)
+    rows[0] = 0
+    N.check(lib.gwo_sync(h), h)
+    lib.gwo_reset_stats(h)
+    lib.gwo_set_profiling(h, 1)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(warm, len(bounds)):
+        step(i)
+    N.check(lib.gwo_sync(h), h)
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    recs = bounds[-1][1] - bounds[warm][0]
+
+    def kstat(k):
+        la, ms, it = C.c_int64(), C.c_double(), C.c_int64()
+        lib.gwo_kernel_stats(h, k, C.byref(la), C.byref(ms), C.byref(it))
+        return la.value, ms.value
+
+    stats = {name: kstat(i) for i, name in enumerate(KERNELS)}
+    op.close()
+    path_bytes = recs * I_B + rows[0] * (S_B + O_B)   # U*2S omitted: not measured here (lower bound)
+    return {"metric": "records/sec per node, keyed window agg @1/2/4/8 GPU; % of HBM peak",
+            "value": recs / elapsed, "unit": "records/s", "n_gpus": 1, "steps": len(bounds) - warm, "warmup": warm,
+            "ms_per_step": elapsed / (len(bounds) - warm) * 1e3, "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "int64", "data": "synthetic, resident in HBM before timing",
+            "config": {"workload": workload, "records": n, "records_per_step": every},
+            "roofline_path": {"alg_bytes_lower_bound": path_bytes, "achieved": path_bytes / elapsed / 1e9,
+                              "unit": "GB/s", "frac": path_bytes / elapsed / 1e9 / 8000.0},
+            "fired_rows": rows[0],
+            "kernels_ms": {k: {"launches": v[0], "total_ms": v[1]} for k, v in stats.items() if v[0]}}
+
+
+if __name__ == "__main__":
+    for c in (sys.argv[1:] or ["c1", "c2", "c3", "c5"]):
+        print(json.dumps(run(c)), flush=True)
