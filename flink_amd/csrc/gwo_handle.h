@@ -218,7 +218,8 @@ struct Handle {
     gwo_status log_carve(LogWindow &W, size_t bytes, char **out);
     void log_release(LogWindow &W);
     int log_choose_lp(uint64_t batch_records) const;
-    gwo_status log_split_chunk(long long base, int nunits, uint64_t cap);
+    gwo_status log_split_chunk(long long base, int nunits, uint64_t cap, const uint64_t *counts, int tmpx, bool deferred);
+    gwo_status log_resolve_split();
     gwo_status insert_log(const int64_t *k, const int64_t *t, const int64_t *v, int64_t n, int64_t stride = 1);
     gwo_status fire_log(int64_t new_wm);
     gwo_status log_state_size(int64_t *entries);

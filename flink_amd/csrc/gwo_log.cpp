@@ -32,7 +32,18 @@ struct LogWindow {
 struct LogState {
     std::map<long long, LogWindow> wins;
     std::multimap<size_t, char *> free_chunks;
-    DevBuf tmp, firedesc;
+    DevBuf tmp[2], firedesc;                     // batch buffers: K1 of batch i+1 writes the one split i is not reading
+    int tmp_cur = 0;
+    // the last pass-2 launch, checked for overflow at the next sync point (deferred so the next batch's
+    // K1 queues right behind it); its segments are already in the windows
+    struct {
+        bool active = false;
+        int tmpx = 0, nunits = 0;
+        long long base = 0;
+        uint64_t cap = 0;
+        std::vector<uint64_t> counts;
+    } pend;
+    unsigned *h_split_flag = nullptr;            // pinned [2]: pass-2 overflow flag per batch buffer
     unsigned long long *d_cursor = nullptr;      // [LOG_NU * 256 * LOG_CUR_STRIDE] bucket cursors of K1
     // K1 readback, one D2H copy: [LOG_NU * 256] bucket counts, then the batch's BatchStats
     // (log_collect_kernel copies them here and resets the cursors and stats for the next launch)
@@ -74,6 +85,7 @@ gwo_status Handle::log_init() {
     GWO_TRY(hipcheck(hipMemsetAsync(L.d_overflow, 0, 16, stream), "overflow"));
     GWO_TRY(hipcheck(hipHostMalloc((void **)&L.h_rb, kRbBytes, hipHostMallocDefault), "pinned"));
     GWO_TRY(hipcheck(hipHostMalloc((void **)&L.h_plan, kPlanBytes, hipHostMallocDefault), "pinned"));
+    GWO_TRY(hipcheck(hipHostMalloc((void **)&L.h_split_flag, 16, hipHostMallocDefault), "pinned"));
     L.h_cursor = L.h_rb;
     L.h_desc = (LogSegDesc *)L.h_plan;
     L.h_ovf = (unsigned *)(L.h_plan + kPlanDescBytes);
@@ -89,8 +101,10 @@ void Handle::log_free() {
     for (auto &kv : L.wins)
         for (auto &c : kv.second.chunks) (void)hipFree(c.base);
     for (auto &kv : L.free_chunks) (void)hipFree(kv.second);
-    L.tmp.release();
+    L.tmp[0].release();
+    L.tmp[1].release();
     L.firedesc.release();
+    if (L.h_split_flag) (void)hipHostFree(L.h_split_flag);
     if (L.d_cursor) (void)hipFree(L.d_cursor);
     if (L.d_rb) (void)hipFree(L.d_rb);
     if (L.d_plan) (void)hipFree(L.d_plan);
@@ -154,14 +168,17 @@ int Handle::log_choose_lp(uint64_t batch_records) const {
     return lp;
 }
 
-// Pass 2 for windows [base, base + nunits) of the batch buffer (bucket counts in h_cursor).
-gwo_status Handle::log_split_chunk(long long base, int nunits, uint64_t cap) {
+// Pass 2 for windows [base, base + nunits) of batch buffer `tmpx` (bucket counts in `counts`).
+// deferred: launch and return; the overflow flag is checked by log_resolve_split at the next sync
+// point.  Otherwise synchronous, re-running with measured capacities until nothing overflows.
+gwo_status Handle::log_split_chunk(long long base, int nunits, uint64_t cap, const uint64_t *counts, int tmpx,
+                                   bool deferred) {
     LogState &L = *logst;
     const int W = needs_value ? 2 : 1;
     const int nb = nunits * 256;
     std::vector<LogWindow *> wins(nunits, nullptr);
     std::vector<uint64_t> wcount(nunits, 0);
-    for (int b = 0; b < nb; ++b) wcount[b >> 8] += L.h_cursor[b];
+    for (int b = 0; b < nb; ++b) wcount[b >> 8] += counts[b];
     std::vector<uint32_t> pcap_exact(nb, 0);   // after an overflow: the measured partition maximum
     while (true) {
         uint32_t chunks = 0;
@@ -180,7 +197,7 @@ gwo_status Handle::log_split_chunk(long long base, int nunits, uint64_t cap) {
                 const int lp = it->second.lp, F = 1 << (lp - 8);
                 uint64_t seg = 0;
                 for (int dgt = 0; dgt < 256; ++dgt) {
-                    const uint64_t n_b = L.h_cursor[c0 + dgt];
+                    const uint64_t n_b = counts[c0 + dgt];
                     LogBucket &B = L.h_buckets[c0 + dgt];
                     B.src = (uint64_t)(c0 + dgt) * cap;
                     B.n = (uint32_t)n_b;
@@ -217,15 +234,25 @@ gwo_status Handle::log_split_chunk(long long base, int nunits, uint64_t cap) {
                                         hipMemcpyHostToDevice, stream), "split plan"));
         unsigned *d_ovf = (unsigned *)(L.d_plan + kPlanDescBytes);
         prof_begin(GWO_KERNEL_PARTITION);
-        launch_log_split((const int64_t *)L.tmp.ptr, needs_value, (const LogBucket *)(L.d_plan + kPlanDescBytes + 8), nb,
-                         nunits, (const LogSegDesc *)L.d_plan, d_ovf, chunks, stream);
+        launch_log_split((const int64_t *)L.tmp[tmpx].ptr, needs_value,
+                         (const LogBucket *)(L.d_plan + kPlanDescBytes + 8), nb, nunits, (const LogSegDesc *)L.d_plan,
+                         d_ovf, chunks, stream);
         GWO_TRY(launch_ok("log split"));
         uint64_t total = 0;
         for (int w = 0; w < nunits; ++w) total += wcount[w];
         prof_end(GWO_KERNEL_PARTITION, (int64_t)total);
-        GWO_TRY(hipcheck(hipMemcpyAsync(h_scalar, d_ovf, 4, hipMemcpyDeviceToHost, stream), "split overflow"));
+        GWO_TRY(hipcheck(hipMemcpyAsync(&L.h_split_flag[tmpx], d_ovf, 4, hipMemcpyDeviceToHost, stream), "split flag"));
+        if (deferred) {
+            L.pend.active = true;
+            L.pend.tmpx = tmpx;
+            L.pend.nunits = nunits;
+            L.pend.base = base;
+            L.pend.cap = cap;
+            L.pend.counts.assign(counts, counts + nb);
+            break;
+        }
         GWO_TRY(hipcheck(hipStreamSynchronize(stream), "log split"));
-        if ((uint32_t)h_scalar[0] == 0) break;
+        if (L.h_split_flag[tmpx] == 0) break;
         // a partition received more than its capacity (skewed keys): the cursors hold the exact
         // counts, so redo with each bucket's partitions sized to its largest one (the segments
         // carved above stay unused until the window is released)
@@ -247,6 +274,26 @@ gwo_status Handle::log_split_chunk(long long base, int nunits, uint64_t cap) {
     return GWO_OK;
 }
 
+// Checks the deferred pass 2: on overflow, its segments come out of their windows and pass 2 re-runs
+// synchronously on the same batch buffer (which the next K1 did not touch).
+gwo_status Handle::log_resolve_split() {
+    LogState &L = *logst;
+    if (!L.pend.active) return GWO_OK;
+    GWO_TRY(hipcheck(hipStreamSynchronize(stream), "pass 2"));
+    L.pend.active = false;
+    if (L.h_split_flag[L.pend.tmpx] == 0) return GWO_OK;
+    for (int w = 0; w < L.pend.nunits; ++w) {
+        uint64_t c = 0;
+        for (int d = 0; d < 256; ++d) c += L.pend.counts[(size_t)w * 256 + d];
+        if (!c) continue;
+        LogWindow &Wn = L.wins[L.pend.base + w];
+        Wn.segs.pop_back();   // the deferred split's segment is the window's last one
+        Wn.records -= c;
+    }
+    std::vector<uint64_t> counts = L.pend.counts;
+    return log_split_chunk(L.pend.base, L.pend.nunits, L.pend.cap, counts.data(), L.pend.tmpx, false);
+}
+
 gwo_status Handle::insert_log(const int64_t *k, const int64_t *t, const int64_t *v, int64_t n, int64_t stride) {
     LogState &L = *logst;
     WindowGeom g = geom_now();
@@ -258,9 +305,13 @@ gwo_status Handle::insert_log(const int64_t *k, const int64_t *t, const int64_t 
     bool first_pass = true;
     long long lo = 0, hi = -1;
     while (true) {
-        GWO_TRY(ensure_buf(L.tmp, (size_t)nunits * 256 * cap * W * 8));
+        DevBuf &tmp = L.tmp[L.tmp_cur];
+        if (tmp.bytes < (size_t)nunits * 256 * cap * W * 8) {
+            GWO_TRY(log_resolve_split());   // ensure_buf may free: nothing may still read it
+            GWO_TRY(ensure_buf(tmp, (size_t)nunits * 256 * cap * W * 8));
+        }
         prof_begin(GWO_KERNEL_INSERT);
-        launch_log_part(k, t, v, n, stride, g, base, nunits, needs_value, L.d_cursor, cap, (int64_t *)L.tmp.ptr, d_stats,
+        launch_log_part(k, t, v, n, stride, g, base, nunits, needs_value, L.d_cursor, cap, (int64_t *)tmp.ptr, d_stats,
                         (int64_t *)side_key.ptr, (int64_t *)side_ts.ptr, (int64_t *)side_val.ptr, d_side_count,
                         first_pass && side_enabled() ? side_cap : 0, first_pass && side_enabled(), stream);
         GWO_TRY(launch_ok("log partition"));
@@ -271,6 +322,7 @@ gwo_status Handle::insert_log(const int64_t *k, const int64_t *t, const int64_t 
             GWO_TRY(hipcheck(hipMemcpyAsync(h_scalar, d_side_count, 8, hipMemcpyDeviceToHost, stream), "side count"));
         GWO_TRY(hipcheck(hipStreamSynchronize(stream), "log partition sync"));
         memcpy(h_stats, L.h_rb + LOG_NU * 256, sizeof(BatchStats));
+        GWO_TRY(log_resolve_split());   // the previous pass 2 has completed (stream order)
         if (first_pass) {
             if (hs.bad_ts) return poison(GWO_ERR_NO_TIMESTAMP,
                                          "Record has Long.MIN_VALUE timestamp (= no timestamp marker). Is the time "
@@ -313,7 +365,8 @@ gwo_status Handle::insert_log(const int64_t *k, const int64_t *t, const int64_t 
             cap = maxc;
             continue;
         }
-        GWO_TRY(log_split_chunk(base, nunits, cap));
+        GWO_TRY(log_split_chunk(base, nunits, cap, (const uint64_t *)L.h_cursor, L.tmp_cur, true));
+        L.tmp_cur ^= 1;
         const long long chunk_hi = base + nunits - 1;
         if (chunk_hi >= hi) break;
         base = chunk_hi + 1;
@@ -327,6 +380,12 @@ gwo_status Handle::insert_log(const int64_t *k, const int64_t *t, const int64_t 
 gwo_status Handle::fire_log(int64_t new_wm) {
     LogState &L = *logst;
     std::vector<long long> fire;
+    if (L.pend.active) {   // a window may fire: its last segment must be complete
+        bool any = false;
+        for (auto &kv : L.wins)
+            any |= (int64_t)((uint64_t)unit_start(kv.first) + (uint64_t)cfg.size - 1) <= new_wm;
+        if (any) GWO_TRY(log_resolve_split());
+    }
     for (auto &kv : L.wins) {
         if (kv.second.segs.size() > LOG_MAX_SEGS)
             return poison(GWO_ERR_CAPACITY, "log layout: a window collected more than 512 batches; use the table layout "

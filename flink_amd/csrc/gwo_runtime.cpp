@@ -666,6 +666,7 @@ gwo_status gwo_state_size(gwo_handle *hh, int64_t *entries) {
 
 gwo_status gwo_sync(gwo_handle *hh) {
     H_OR_FAIL;
+    if (h->logst) GWO_TRY(h->log_resolve_split());
     return h->hipcheck(hipStreamSynchronize(h->stream), "sync");
 }
 
