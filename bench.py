@@ -121,22 +121,22 @@ def main():
         N.check(lib.gwo_comm_unique_id(uid))
         N.check(lib.gwo_comm_init(h, uid, 1, 0), h, "gwo_comm_init")
 
-    fired_rows = [0]
-
     def step(i):
         s, e = bounds[i]
         N.check(lib.gwo_submit(h, C.c_void_p(key.data_ptr() + 8 * s), C.c_void_p(ts.data_ptr() + 8 * s),
                                C.c_void_p(val.data_ptr() + 8 * s), e - s), h, "submit")
         N.check(lib.gwo_advance_watermark(h, wms[i]), h, "watermark")
-        nrow = C.c_int64()
-        N.check(lib.gwo_output_count(h, C.byref(nrow)), h)
-        fired_rows[0] += nrow.value
         N.check(lib.gwo_discard_output(h), h)   # rows stay in HBM; the sink is not part of the path
+
+    def rows_emitted():
+        r = C.c_int64()
+        N.check(lib.gwo_rows_emitted(h, C.byref(r)), h)
+        return r.value
 
     for i in range(a.warmup):
         step(i)
-    fired_rows[0] = 0
     N.check(lib.gwo_sync(h), h)
+    rows_before = rows_emitted()
     lib.gwo_reset_stats(h)
     lib.gwo_set_profiling(h, 1)
     if dist:
@@ -187,7 +187,7 @@ def main():
             s, e = bounds[i]
             pair = key[s:e] * 64 + torch.div(ts[s:e], wnd, rounding_mode="floor")
             u_tot += int(torch.unique(pair).numel())
-    rows = fired_rows[0]
+    rows = rows_emitted() - rows_before
     path_bytes = records * I_B + u_tot * 2 * S_B + rows * (S_B + O_B)
     kern = {
         "insert": ("log_part_kernel", records * (I_B + REC_B)),

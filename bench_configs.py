@@ -115,16 +115,18 @@ def run(cfg):
         N.check(lib.gwo_submit(h, C.c_void_p(key.data_ptr() + 8 * s), C.c_void_p(ts.data_ptr() + 8 * s),
                                C.c_void_p(val.data_ptr() + 8 * s), e - s), h, "submit")
         N.check(lib.gwo_advance_watermark(h, wms[i]), h, "watermark")
-        c = C.c_int64()
-        N.check(lib.gwo_output_count(h, C.byref(c)), h)
-        rows[0] += c.value
         N.check(lib.gwo_discard_output(h), h)
+
+    def emitted():
+        r = C.c_int64()
+        N.check(lib.gwo_rows_emitted(h, C.byref(r)), h)
+        return r.value
 
     warm = max(1, len(bounds) // 10)
     for i in range(warm):
         step(i)
-    rows[0] = 0
     N.check(lib.gwo_sync(h), h)
+    rows0 = emitted()
     lib.gwo_reset_stats(h)
     lib.gwo_set_profiling(h, 1)
     torch.cuda.synchronize()
@@ -135,6 +137,7 @@ def run(cfg):
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     recs = bounds[-1][1] - bounds[warm][0]
+    rows[0] = emitted() - rows0
 
     def kstat(k):
         la, ms, it = C.c_int64(), C.c_double(), C.c_int64()

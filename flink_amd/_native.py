@@ -73,6 +73,7 @@ SIGNATURES = [
     ("gwo_advance_watermark", C.c_int, [_P, C.c_int64]),
     ("gwo_end_input", C.c_int, [_P]),
     ("gwo_output_count", C.c_int, [_P, _I64P]),
+    ("gwo_rows_emitted", C.c_int, [_P, _I64P]),
     ("gwo_drain", C.c_int, [_P, C.POINTER(GwoOut), C.c_int64, _I64P]),
     ("gwo_output_view", C.c_int, [_P, C.POINTER(GwoOut), _I64P]),
     ("gwo_discard_output", C.c_int, [_P]),

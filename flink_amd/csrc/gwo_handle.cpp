@@ -116,6 +116,7 @@ gwo_status Handle::init(const gwo_config &c) {
     if (geom.slide > 0) geom.inv_slide = 1.0 / (double)geom.slide;
     if (geom.unit > 0) geom.inv_unit = 1.0 / (double)geom.unit;
     debug = getenv("GWO_DEBUG") != nullptr;
+    if (const char *e = getenv("GWO_ASYNC_FIRE")) async_fire = atoi(e) != 0;
     const char *pa = getenv("GWO_PREAGG");
     if (pa) cfg_preagg = atoi(pa) ? 1 : 0;
     if (cfg_preagg >= 0) use_preagg = cfg_preagg;
@@ -162,6 +163,7 @@ gwo_status Handle::init(const gwo_config &c) {
 Handle::~Handle() {
     DeviceGuard g(cfg.device);
     if (stream) (void)hipStreamSynchronize(stream);
+    if (fire_stream) (void)hipStreamSynchronize(fire_stream);
     (void)prof_collect();
     for (hipEvent_t e : event_pool) (void)hipEventDestroy(e);
     comm_free();
@@ -192,6 +194,9 @@ Handle::~Handle() {
     if (d_scratch_count) (void)hipFree(d_scratch_count);
     if (d_side_count) (void)hipFree(d_side_count);
     if (own_stream && stream) (void)hipStreamDestroy(stream);
+    if (fire_stream) (void)hipStreamDestroy(fire_stream);
+    if (ev_main) (void)hipEventDestroy(ev_main);
+    if (ev_fire) (void)hipEventDestroy(ev_fire);
 }
 
 gwo_status Handle::submit(const int64_t *key, const int64_t *ts, const void *val, int64_t n) {
@@ -231,9 +236,11 @@ gwo_status Handle::advance_watermark(int64_t new_wm) {
 }
 
 gwo_status Handle::drain(const gwo_out *cols, int64_t cap, int64_t *n_out) {
+    GWO_TRY(finish_fire());
     GWO_TRY(hipcheck(hipStreamSynchronize(stream), "drain"));
     uint64_t take = std::min<uint64_t>((uint64_t)cap, out_rows);
     *n_out = (int64_t)take;
+    rows_gone += take;
     if (take == 0) return GWO_OK;
     int64_t *src[7] = {out.key, out.start, out.end, out.res[0], out.res[1], out.res[2], out.res[3]};
     void *dst[7] = {cols->key, cols->start, cols->end, cols->result[0], cols->result[1], cols->result[2], cols->result[3]};
@@ -275,6 +282,14 @@ gwo_status Handle::drain_side(const gwo_side_out *cols, int64_t cap, int64_t *n_
     *h_scalar = rest;
     GWO_TRY(hipcheck(hipMemcpyAsync(d_side_count, h_scalar, 8, hipMemcpyHostToDevice, stream), "side count"));
     return hipcheck(hipStreamSynchronize(stream), "side sync");
+}
+
+// ---- asynchronous fire ---------------------------------------------------------------------------
+gwo_status Handle::poll_fire() {
+    if (!fire_pending) return GWO_OK;
+    hipError_t e = hipEventQuery(ev_fire);
+    if (e == hipErrorNotReady) return GWO_OK;
+    return finish_fire();
 }
 
 gwo_status Handle::state_size(int64_t *entries) {

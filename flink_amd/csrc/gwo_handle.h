@@ -104,6 +104,14 @@ struct Handle {
     unsigned long long *d_scratch_count = nullptr;
     uint64_t out_rows = 0;
     bool out_count_dirty = false;              // gwo_discard_output: reset d_out_count before the next fire
+    uint64_t rows_gone = 0;                    // rows drained or discarded so far (gwo_rows_emitted)
+    // asynchronous fire (log layout): the fire runs on fire_stream, overlapping the next batches; its
+    // rows become visible when it completes (finish_fire at the next output access or sync point)
+    hipStream_t fire_stream = nullptr;
+    hipEvent_t ev_main = nullptr, ev_fire = nullptr;
+    bool fire_pending = false;
+    bool async_fire = false;                   // GWO_ASYNC_FIRE=1: return before the fire completes
+    bool discard_after_fire = false;
     unsigned long long zero_u64 = 0;
     unsigned long long *h_scalar = nullptr;    // pinned scalar staging
     int64_t *h_ident_side = nullptr;           // pinned [0, identity words...] side-slot image
@@ -230,8 +238,10 @@ struct Handle {
     gwo_status comm_unpack(const int64_t *aos, int64_t n, const int64_t **rk, const int64_t **rt, const int64_t **rv);
     gwo_status comm_min_watermark(int64_t wm, int64_t *out);
 
-    void prof_begin(int k);
-    void prof_end(int k, int64_t items);
+    void prof_begin(int k, hipStream_t s = nullptr);
+    void prof_end(int k, int64_t items, hipStream_t s = nullptr);
+    gwo_status finish_fire();                  // log layout: wait for a pending fire and publish its rows
+    gwo_status poll_fire();                    // non-blocking: finish_fire if the fire has completed
     gwo_status prof_collect();
 };
 

@@ -44,6 +44,10 @@ struct LogState {
         std::vector<uint64_t> counts;
     } pend;
     unsigned *h_split_flag = nullptr;            // pinned [2]: pass-2 overflow flag per batch buffer
+    // the fire in flight on fire_stream
+    std::vector<long long> fire_units;
+    uint64_t fire_rows0 = 0, fire_bound = 0;
+    unsigned long long *h_fire_out = nullptr;    // pinned [3]: row counter, overflow, slow partitions
     unsigned long long *d_cursor = nullptr;      // [LOG_NU * 256 * LOG_CUR_STRIDE] bucket cursors of K1
     // K1 readback, one D2H copy: [LOG_NU * 256] bucket counts, then the batch's BatchStats
     // (log_collect_kernel copies them here and resets the cursors and stats for the next launch)
@@ -86,6 +90,10 @@ gwo_status Handle::log_init() {
     GWO_TRY(hipcheck(hipHostMalloc((void **)&L.h_rb, kRbBytes, hipHostMallocDefault), "pinned"));
     GWO_TRY(hipcheck(hipHostMalloc((void **)&L.h_plan, kPlanBytes, hipHostMallocDefault), "pinned"));
     GWO_TRY(hipcheck(hipHostMalloc((void **)&L.h_split_flag, 16, hipHostMallocDefault), "pinned"));
+    GWO_TRY(hipcheck(hipHostMalloc((void **)&L.h_fire_out, 32, hipHostMallocDefault), "pinned"));
+    GWO_TRY(hipcheck(hipStreamCreateWithFlags(&fire_stream, hipStreamNonBlocking), "fire stream"));
+    GWO_TRY(hipcheck(hipEventCreateWithFlags(&ev_main, hipEventDisableTiming), "event"));
+    GWO_TRY(hipcheck(hipEventCreateWithFlags(&ev_fire, hipEventDisableTiming), "event"));
     L.h_cursor = L.h_rb;
     L.h_desc = (LogSegDesc *)L.h_plan;
     L.h_ovf = (unsigned *)(L.h_plan + kPlanDescBytes);
@@ -105,6 +113,7 @@ void Handle::log_free() {
     L.tmp[1].release();
     L.firedesc.release();
     if (L.h_split_flag) (void)hipHostFree(L.h_split_flag);
+    if (L.h_fire_out) (void)hipHostFree(L.h_fire_out);
     if (L.d_cursor) (void)hipFree(L.d_cursor);
     if (L.d_rb) (void)hipFree(L.d_rb);
     if (L.d_plan) (void)hipFree(L.d_plan);
@@ -377,27 +386,44 @@ gwo_status Handle::insert_log(const int64_t *k, const int64_t *t, const int64_t 
     return GWO_OK;
 }
 
+// Launches the fold of every window whose end the watermark passed (EventTimeTrigger.onEventTime FIRE,
+// WindowOperator.java:430-473) on fire_stream, one workgroup per CU so that the next batches' kernels
+// run beside it, and returns.  finish_fire publishes the rows and releases the windows' memory.
 gwo_status Handle::fire_log(int64_t new_wm) {
     LogState &L = *logst;
+    GWO_TRY(poll_fire());
+    auto due = [&](std::vector<long long> &out) {   // windows this watermark fires, not already firing
+        out.clear();
+        for (auto &kv : L.wins) {
+            if ((int64_t)((uint64_t)unit_start(kv.first) + (uint64_t)cfg.size - 1) > new_wm) continue;
+            if (fire_pending &&
+                std::find(L.fire_units.begin(), L.fire_units.end(), kv.first) != L.fire_units.end())
+                continue;
+            out.push_back(kv.first);
+        }
+    };
     std::vector<long long> fire;
-    if (L.pend.active) {   // a window may fire: its last segment must be complete
-        bool any = false;
-        for (auto &kv : L.wins)
-            any |= (int64_t)((uint64_t)unit_start(kv.first) + (uint64_t)cfg.size - 1) <= new_wm;
-        if (any) GWO_TRY(log_resolve_split());
-    }
-    for (auto &kv : L.wins) {
-        if (kv.second.segs.size() > LOG_MAX_SEGS)
-            return poison(GWO_ERR_CAPACITY, "log layout: a window collected more than 512 batches; use the table layout "
-                                            "for windows that span that many watermark intervals");
-        int64_t start = unit_start(kv.first);
-        int64_t max_ts = (int64_t)((uint64_t)start + (uint64_t)cfg.size - 1);
-        if (max_ts <= new_wm) fire.push_back(kv.first);   // EventTimeTrigger.onEventTime FIRE
+    due(fire);
+    if (fire.empty()) return GWO_OK;
+    GWO_TRY(finish_fire());         // the previous fire's rows and memory first
+    GWO_TRY(log_resolve_split());   // the fired windows' last segments must be complete
+    due(fire);
+    for (auto it = fire.begin(); it != fire.end();) {   // a window with no segment has nothing to emit
+        if (L.wins[*it].segs.empty()) {
+            L.wins.erase(*it);
+            it = fire.erase(it);
+        } else {
+            ++it;
+        }
     }
     if (fire.empty()) return GWO_OK;
+    for (long long u : fire)
+        if (L.wins[u].segs.size() > LOG_MAX_SEGS)
+            return poison(GWO_ERR_CAPACITY, "log layout: a window collected more than 512 batches; use the table layout "
+                                            "for windows that span that many watermark intervals");
     // Output rows: one per distinct key.  Reserve for the expected count (last window's keys, or the
-    // caller's hint) rather than the record count; if the fire emits more, it is re-run into a
-    // bigger buffer (fire only reads the segments, so a re-run is exact).
+    // caller's hint) rather than the record count; if the fire emits more, finish_fire re-runs it into
+    // a bigger buffer (the fire only reads the segments, so a re-run is exact).
     uint64_t bound = 0, expect = 0;
     const uint64_t per_window = std::max<uint64_t>(L.last_window_keys, (uint64_t)std::max<int64_t>(cfg.expected_keys, 0));
     for (long long u : fire) {
@@ -416,51 +442,89 @@ gwo_status Handle::fire_log(int64_t new_wm) {
     if (L.max_groups == 0) {
         int cus = 0;
         GWO_TRY(hipcheck(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, cfg.device), "CU count"));
-        L.max_groups = 2 * std::max(cus, 1);   // two 64-KiB-LDS workgroups per CU
+        L.max_groups = std::max(cus, 1);
     }
-    const uint64_t rows0 = out_rows;
-    for (int attempt = 0; attempt < 2; ++attempt) {
+    L.fire_rows0 = out_rows;
+    L.fire_bound = bound;
+    L.fire_units = fire;
+    GWO_TRY(hipcheck(hipEventRecord(ev_main, stream), "event"));   // segments, descriptors, row counter
+    GWO_TRY(hipcheck(hipStreamWaitEvent(fire_stream, ev_main, 0), "event wait"));
+    OutCols o = out_cols();
+    size_t at = 0;
+    for (long long u : fire) {
+        LogWindow &W = L.wins[u];
+        int64_t start = unit_start(u);
+        int64_t end = (int64_t)((uint64_t)start + (uint64_t)cfg.size);
+        prof_begin(GWO_KERNEL_FIRE, fire_stream);
+        launch_log_fire((const LogSegDesc *)L.firedesc.ptr + at, (int)W.segs.size(), W.lp, needs_value, plan, rplan,
+                        start, end, o, L.d_overflow, L.max_groups, async_fire ? 1 : 2, fire_stream);
+        GWO_TRY(launch_ok("log fire"));
+        prof_end(GWO_KERNEL_FIRE, (int64_t)W.records, fire_stream);
+        at += W.segs.size();
+    }
+    GWO_TRY(hipcheck(hipMemcpyAsync(L.h_fire_out, d_out_count, 8, hipMemcpyDeviceToHost, fire_stream), "out count"));
+    GWO_TRY(hipcheck(hipMemcpyAsync(L.h_fire_out + 1, L.d_overflow, 16, hipMemcpyDeviceToHost, fire_stream), "overflow"));
+    GWO_TRY(hipcheck(hipEventRecord(ev_fire, fire_stream), "event"));
+    fire_pending = true;
+    // Measured on MI355X (C4): letting the fire overlap the next batches is slower -- beside a 1-per-CU
+    // fire the partition kernel loses its occupancy (0.36 vs 0.26 ms) and the fire takes 4.9 vs 2.9 ms;
+    // at 2 per CU the next batch simply queues behind it.  So the fire completes here; the stream and
+    // event machinery stays for callers that interleave other work (GWO_ASYNC_FIRE=1).
+    if (!async_fire) return finish_fire();
+    return GWO_OK;
+}
+
+gwo_status Handle::finish_fire() {
+    if (!fire_pending) return GWO_OK;
+    LogState &L = *logst;
+    fire_pending = false;
+    GWO_TRY(hipcheck(hipEventSynchronize(ev_fire), "fire"));
+    if (L.h_fire_out[1]) return poison(GWO_ERR_CAPACITY, "log fire: a partition overflowed its LDS table");
+    uint64_t count = L.h_fire_out[0];
+    if ((long long)count > out.cap) {
+        // more rows than reserved: rewind the row counter, grow to the exact need, fire again (synchronous)
+        const uint64_t need = count - L.fire_rows0;
+        *h_scalar = L.fire_rows0;
+        GWO_TRY(hipcheck(hipMemcpyAsync(d_out_count, h_scalar, 8, hipMemcpyHostToDevice, stream), "out rewind"));
+        GWO_TRY(ensure_output(std::min(need, L.fire_bound)));
         OutCols o = out_cols();
         size_t at = 0;
-        for (long long u : fire) {
+        for (long long u : L.fire_units) {
             LogWindow &W = L.wins[u];
             int64_t start = unit_start(u);
             int64_t end = (int64_t)((uint64_t)start + (uint64_t)cfg.size);
-            prof_begin(GWO_KERNEL_FIRE);
             launch_log_fire((const LogSegDesc *)L.firedesc.ptr + at, (int)W.segs.size(), W.lp, needs_value, plan,
-                            rplan, start, end, o, L.d_overflow, L.max_groups, stream);
+                            rplan, start, end, o, L.d_overflow, L.max_groups, 2, stream);
             GWO_TRY(launch_ok("log fire"));
-            prof_end(GWO_KERNEL_FIRE, (int64_t)W.records);
             at += W.segs.size();
         }
         GWO_TRY(hipcheck(hipMemcpyAsync(h_scalar, d_out_count, 8, hipMemcpyDeviceToHost, stream), "out count"));
-        GWO_TRY(hipcheck(hipMemcpyAsync(h_scalar + 1, L.d_overflow, 16, hipMemcpyDeviceToHost, stream), "overflow"));
         GWO_TRY(hipcheck(hipStreamSynchronize(stream), "log fire"));
-        if (h_scalar[1]) return poison(GWO_ERR_CAPACITY, "log fire: a partition overflowed its LDS table");
-        if ((long long)h_scalar[0] <= out.cap) break;
-        // more rows than reserved: rewind the row counter, grow to the exact need, fire again
-        const uint64_t need = h_scalar[0] - rows0;
-        h_scalar[0] = rows0;
-        GWO_TRY(hipcheck(hipMemcpyAsync(d_out_count, h_scalar, 8, hipMemcpyHostToDevice, stream), "out rewind"));
-        GWO_TRY(hipcheck(hipStreamSynchronize(stream), "out rewind"));
-        GWO_TRY(ensure_output(std::min(need, bound)));
+        count = *h_scalar;
     }
-    const uint64_t emitted = h_scalar[0] - rows0;
+    const uint64_t emitted = count - L.fire_rows0;
     if (debug)
-        fprintf(stderr, "[gwo] fire %zu window(s): rows=%llu slow_partitions=%llu lp=%d records=%llu\n", fire.size(),
-                (unsigned long long)emitted, (unsigned long long)h_scalar[2], L.wins[fire[0]].lp,
-                (unsigned long long)L.wins[fire[0]].records);
-    out_rows = h_scalar[0];
-    L.last_window_keys = emitted / fire.size();
+        fprintf(stderr, "[gwo] fire %zu window(s): rows=%llu slow_partitions=%llu lp=%d records=%llu\n",
+                L.fire_units.size(), (unsigned long long)emitted, (unsigned long long)L.h_fire_out[2],
+                L.wins[L.fire_units[0]].lp, (unsigned long long)L.wins[L.fire_units[0]].records);
+    if (discard_after_fire) {   // gwo_discard_output was called while the fire ran
+        discard_after_fire = false;
+        rows_gone += emitted;
+        out_rows = 0;
+        out_count_dirty = true;
+    } else {
+        out_rows = count;
+    }
+    L.last_window_keys = emitted / L.fire_units.size();
     L.last_window_records = 0;
-    for (long long u : fire) L.last_window_records = std::max<uint64_t>(L.last_window_records, L.wins[u].records);
-    for (long long u : fire) {
-        LogWindow &W = L.wins[u];
-        log_release(W);
+    for (long long u : L.fire_units) L.last_window_records = std::max<uint64_t>(L.last_window_records, L.wins[u].records);
+    for (long long u : L.fire_units) {
+        log_release(L.wins[u]);
         // allowedLateness > 0: any later record of this window is a re-fire and is rejected at
         // classification, so nothing of the window is kept until its cleanup time
         L.wins.erase(u);
     }
+    L.fire_units.clear();
     return GWO_OK;
 }
 

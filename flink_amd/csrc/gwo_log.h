@@ -55,5 +55,5 @@ void launch_log_split(const int64_t *tmp, int has_val, const LogBucket *buckets,
 int log_fire_cap_log2(int nwords);
 void launch_log_fire(const LogSegDesc *segs, int nseg, int lp, int has_val, const AccPlan &plan,
                      const ResultPlan &rp, int64_t start, int64_t end, OutCols out, unsigned long long *overflow,
-                     int max_groups, hipStream_t s);
+                     int cus, int max_per_cu, hipStream_t s);
 }  // namespace gwo

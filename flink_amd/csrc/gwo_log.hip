@@ -844,11 +844,14 @@ int log_fire_cap_log2(int nwords) {
 
 void launch_log_fire(const LogSegDesc *segs, int nseg, int lp, int has_val, const AccPlan &plan,
                      const ResultPlan &rp, int64_t start, int64_t end, OutCols out, unsigned long long *overflow,
-                     int max_groups, hipStream_t s) {
+                     int cus, int max_per_cu, hipStream_t s) {
+    if (nseg <= 0 || nseg > LOG_MAX_SEGS) return;   // nothing to fold (the host never asks; defensive)
     int cl = log_fire_cap_log2(plan.nwords);
     size_t lds = (size_t)(1 + plan.nwords) * 8 << cl;
     uint32_t parts = 1u << lp;
-    uint32_t grid = parts < (uint32_t)max_groups ? parts : (uint32_t)max_groups;
+    // persistent grid: two 64-KiB-LDS workgroups per CU, or fewer to leave room for concurrent kernels
+    const uint32_t groups = (uint32_t)cus * (uint32_t)(max_per_cu < 2 ? max_per_cu : 2);
+    uint32_t grid = parts < groups ? parts : groups;
 #define GWO_FIRE_NW(NW)                                                                                          \
     case NW:                                                                                                     \
         hipLaunchKernelGGL(log_fire_kernel<NW>, dim3(grid), dim3(LOG_FIRE_THREADS), lds, s, segs, nseg, parts, cl, \

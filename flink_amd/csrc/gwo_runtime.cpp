@@ -247,8 +247,9 @@ gwo_status Handle::ensure_output(uint64_t extra) {
 }
 
 // ---- profiling ---------------------------------------------------------------------------------
-void Handle::prof_begin(int k) {
+void Handle::prof_begin(int k, hipStream_t s) {
     if (!profiling) return;
+    if (!s) s = stream;
     hipEvent_t a, b;
     if (event_pool.size() >= 2) {   // events are recycled: hipEventCreate costs microseconds per call
         a = event_pool.back();
@@ -259,19 +260,21 @@ void Handle::prof_begin(int k) {
         (void)hipEventCreate(&a);
         (void)hipEventCreate(&b);
     }
-    (void)hipEventRecord(a, stream);
+    (void)hipEventRecord(a, s);
     pending_events.push_back({k, a, b, 0});
 }
-void Handle::prof_end(int k, int64_t items) {
+void Handle::prof_end(int k, int64_t items, hipStream_t s) {
     if (!profiling || pending_events.empty()) return;
+    if (!s) s = stream;
     auto &pe = pending_events.back();
     if (pe.kernel != k) return;
-    (void)hipEventRecord(pe.b, stream);
+    (void)hipEventRecord(pe.b, s);
     pe.items = items;
 }
 gwo_status Handle::prof_collect() {
     if (pending_events.empty()) return GWO_OK;
     GWO_TRY(hipcheck(hipStreamSynchronize(stream), "prof sync"));
+    if (fire_stream) GWO_TRY(hipcheck(hipStreamSynchronize(fire_stream), "prof sync"));
     for (auto &pe : pending_events) {
         float ms = 0.f;
         (void)hipEventElapsedTime(&ms, pe.a, pe.b);
@@ -594,13 +597,23 @@ gwo_status gwo_end_input(gwo_handle *hh) { return gwo_advance_watermark(hh, (int
 gwo_status gwo_output_count(gwo_handle *hh, int64_t *n) {
     H_OR_FAIL;
     if (!n) return GWO_ERR_INVALID_ARGUMENT;
+    GWO_TRY(h->poll_fire());   // non-blocking: a fire still running contributes when it completes
     *n = (int64_t)h->out_rows;
+    return GWO_OK;
+}
+
+gwo_status gwo_rows_emitted(gwo_handle *hh, int64_t *n) {
+    H_OR_FAIL;
+    if (!n) return GWO_ERR_INVALID_ARGUMENT;
+    GWO_TRY(h->finish_fire());
+    *n = (int64_t)(h->rows_gone + h->out_rows);
     return GWO_OK;
 }
 
 gwo_status gwo_output_view(gwo_handle *hh, gwo_out *cols, int64_t *n) {
     H_OR_FAIL;
     if (!cols || !n) return GWO_ERR_INVALID_ARGUMENT;
+    GWO_TRY(h->finish_fire());
     GWO_TRY(h->hipcheck(hipStreamSynchronize(h->stream), "view"));
     cols->key = h->out.key;
     cols->start = h->out.start;
@@ -612,6 +625,9 @@ gwo_status gwo_output_view(gwo_handle *hh, gwo_out *cols, int64_t *n) {
 
 gwo_status gwo_discard_output(gwo_handle *hh) {
     H_OR_FAIL;
+    GWO_TRY(h->poll_fire());
+    if (h->fire_pending) h->discard_after_fire = true;   // the running fire's rows are dropped when it completes
+    h->rows_gone += h->out_rows;
     h->out_rows = 0;
     h->out_count_dirty = true;   // the device row counter is reset before the next fire (ensure_output)
     return GWO_OK;
@@ -667,6 +683,7 @@ gwo_status gwo_state_size(gwo_handle *hh, int64_t *entries) {
 gwo_status gwo_sync(gwo_handle *hh) {
     H_OR_FAIL;
     if (h->logst) GWO_TRY(h->log_resolve_split());
+    GWO_TRY(h->finish_fire());
     return h->hipcheck(hipStreamSynchronize(h->stream), "sync");
 }
 

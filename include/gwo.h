@@ -146,11 +146,16 @@ gwo_status gwo_advance_watermark(gwo_handle *h, int64_t wm);
 /* processWatermark(Long.MAX_VALUE) -- a bounded source's end (StreamSource.java:122). */
 gwo_status gwo_end_input(gwo_handle *h);
 
+/* Rows available now.  Non-blocking: with the log layout a fire runs asynchronously (overlapping later
+ * batches) and its rows count once it has completed; gwo_drain / gwo_output_view / gwo_sync wait for it. */
 gwo_status gwo_output_count(gwo_handle *h, int64_t *n);
+/* Total rows emitted since creation, including discarded ones (waits for a running fire). */
+gwo_status gwo_rows_emitted(gwo_handle *h, int64_t *n);
 /* Copies up to cap rows into cols (host or device buffers) and removes them from the handle. */
 gwo_status gwo_drain(gwo_handle *h, const gwo_out *cols, int64_t cap, int64_t *n_out);
 /* Library-owned device columns of the pending output (valid until the next call); n_out rows. */
 gwo_status gwo_output_view(gwo_handle *h, gwo_out *cols, int64_t *n_out);
+/* Drops every row emitted so far, including those of a fire still running (non-blocking). */
 gwo_status gwo_discard_output(gwo_handle *h);
 gwo_status gwo_result_dtype(const gwo_handle *h, int32_t agg_index, int32_t *dtype);
 

@@ -550,3 +550,50 @@ def test_partition_by_operator_routes_like_the_partitioner(F, par, maxp):
     out2 = np.zeros((par, small, 3), np.int64)
     N.check(N.lib().gwo_partition_by_operator(p(k), p(t), p(v), n, N.KEY_LONG, maxp, par, p(out2), small, p(counts), 0))
     assert counts.tolist() == np.bincount(dest, minlength=par).tolist()
+
+
+def test_log_layout_async_fire_overlaps_later_batches(F):
+    """Fires run on their own stream while later batches are partitioned; the rows only become visible
+    at drain.  Many windows, several fires in flight across batches, no host sync in between -- the
+    results must still equal the oracle's, and discarding during a running fire drops its rows."""
+    import ctypes as C
+    from flink_amd import _native as N
+    lib = N.lib()
+    k, t, v, b = _c1(n=2_000_000, nkeys=300_000, every=50_000, lag=500, disorder=400)
+    agg = F.MultiAggregate(F.SumAggregate(), F.MinAggregate(), F.MaxAggregate())
+    op = F.GpuWindowOperator(F.TumblingEventTimeWindows.of(2000), agg, state_layout="log", expected_keys=300_000)
+    h = op.handle
+    P = lambda a: a.ctypes.data_as(C.c_void_p)
+    prev = 0
+    for end, wm in b:
+        N.check(lib.gwo_submit(h, P(k[prev:end]), P(t[prev:end]), P(v[prev:end]), end - prev), h)
+        N.check(lib.gwo_advance_watermark(h, wm), h)
+        n = C.c_int64()
+        N.check(lib.gwo_output_count(h, C.byref(n)), h)   # non-blocking: may not include a running fire
+        prev = end
+    N.check(lib.gwo_end_input(h), h)
+    op._collect()
+    (wk, ws, we, res), late = V.tumbling_lateness0(k, t, v, _final(b), 2000, 0, [1, 2, 3])
+    got = sorted((a, s, e, *r) for a, s, e, r in op.output)
+    assert got == _want(wk, ws, we, res)
+    tot = C.c_int64()
+    N.check(lib.gwo_rows_emitted(h, C.byref(tot)), h)
+    assert tot.value == len(got)
+    op.close()
+    # discard while a fire may be running: none of those rows reach the output
+    op = F.GpuWindowOperator(F.TumblingEventTimeWindows.of(2000), agg, state_layout="log", expected_keys=300_000)
+    h = op.handle
+    half = len(b) // 2
+    prev = 0
+    for end, wm in b[:half]:
+        N.check(lib.gwo_submit(h, P(k[prev:end]), P(t[prev:end]), P(v[prev:end]), end - prev), h)
+        N.check(lib.gwo_advance_watermark(h, wm), h)
+        prev = end
+    N.check(lib.gwo_discard_output(h), h)
+    n = C.c_int64()
+    N.check(lib.gwo_sync(h), h)
+    N.check(lib.gwo_output_count(h, C.byref(n)), h)
+    assert n.value == 0
+    N.check(lib.gwo_rows_emitted(h, C.byref(tot)), h)
+    assert tot.value > 0
+    op.close()
