@@ -18,6 +18,10 @@ CXXFLAGS := -O2 -std=c++17 -fPIC -Wall -Wno-unused-function -D__HIP_PLATFORM_AMD
 
 all: $(LIB)
 
+# gwo_log.hip: no atomic optimizer -- it turns the fire's single-lane row reservation into a
+# wave scan + readfirstlane that waits for the atomic's round trip on the spot.
+$(BUILD)/gwo_log.hip.o: HIPFLAGS += -mllvm -amdgpu-atomic-optimizer-strategy=None
+
 $(BUILD)/%.hip.o: flink_amd/csrc/%.hip $(HDRS)
 	@mkdir -p $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
@@ -33,3 +37,13 @@ clean:
 	rm -rf build $(LIB)
 
 .PHONY: all clean
+
+# Profiling variant of the library (per-phase s_memtime printout of the log fire, GWO_FIRE_XP=16).
+PROF_LIB := flink_amd/libgwo_prof.so
+$(BUILD)/gwo_log_prof.hip.o: flink_amd/csrc/gwo_log.hip $(HDRS)
+	@mkdir -p $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -mllvm -amdgpu-atomic-optimizer-strategy=None -DGWO_FIRE_PROF -c $< -o $@
+$(PROF_LIB): $(filter-out $(BUILD)/gwo_log.hip.o,$(HIP_OBJS)) $(BUILD)/gwo_log_prof.hip.o $(CPP_OBJS)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -L$(ROCM)/lib -lamdhip64 -lrccl -Wl,-rpath,$(ROCM)/lib
+prof: $(PROF_LIB)
+.PHONY: prof

@@ -24,6 +24,7 @@
 // random accesses are LDS.
 #include "gwo_device.h"
 #include "gwo_log.h"
+#include <stdlib.h>
 
 namespace gwo {
 
@@ -468,6 +469,7 @@ __device__ __forceinline__ void fire_emit(const FireCtx &c, const AccPlan &p, co
 
 typedef __attribute__((address_space(1))) const ll2 g_ll2;
 typedef __attribute__((address_space(1))) const int64_t g_i64;
+typedef __attribute__((address_space(1))) const uint32_t g_u32;
 
 // One output row from NW register words.  Every loop has a compile-time trip count (unrolled), so
 // the plan fields and the result-column pointers are read from kernel arguments once, outside the
@@ -503,53 +505,146 @@ __device__ __forceinline__ void emit_row(const ResultPlan &rp, const int64_t (&a
     }
 }
 
+// Result columns of one row from NW accumulator words (ResultPlan: value, f64 order key, avg).
 template <int NW>
-__global__ __launch_bounds__(LOG_FIRE_THREADS) void log_fire_kernel(const LogSegDesc *__restrict__ segs, int nseg,
+__device__ __forceinline__ void row_results(const ResultPlan &rp, const int64_t (&acc)[NW], int64_t (&res)[4]) {
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+        if (a >= rp.naggs) break;
+        const int wi = rp.word[a];
+        int64_t x = acc[0], y = acc[0];
+#pragma unroll
+        for (int w = 1; w < NW; ++w) {
+            if (w == wi) x = acc[w];
+            if (w == wi + 1) y = acc[w];
+        }
+        switch (rp.kind[a]) {
+            case 2:
+            case 3: res[a] = rp.value_is_f64 ? f64_from_order_key(x) : x; break;
+            case 4: {
+                double s = rp.value_is_f64 ? __longlong_as_double(x) : (double)x;
+                res[a] = __double_as_longlong(s / (double)y);
+                break;
+            }
+            default: res[a] = x; break;
+        }
+    }
+}
+
+// Value of the other lane of the pair (2m, 2m+1): DPP quad_perm [1,0,3,2].
+__device__ __forceinline__ int dpp_swap_pair(int x) { return __builtin_amdgcn_mov_dpp(x, 0xb1, 0xf, 0xf, false); }
+__device__ __forceinline__ int64_t dpp_swap_pair64(int64_t x) {
+    const int lo = dpp_swap_pair((int)(uint32_t)x), hi = dpp_swap_pair((int)(uint32_t)((uint64_t)x >> 32));
+    return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+
+// Inclusive prefix sum across a wave64 (DPP row shifts + row broadcasts; VALU only, no LDS).
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false);   // row_shr:1
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false);   // row_shr:2
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false);   // row_shr:4
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false);   // row_shr:8
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);   // row_bcast:15 -> rows 1, 3
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);   // row_bcast:31 -> rows 2, 3
+    return x;
+}
+
+__device__ __forceinline__ int64_t word_combine(int op, int64_t a, int64_t b) {
+    switch (op) {
+        case ACC_ADD_I64: return (int64_t)((uint64_t)a + (uint64_t)b);
+        case ACC_ADD_F64: return __double_as_longlong(__longlong_as_double(a) + __longlong_as_double(b));
+        case ACC_MIN_I64: return b < a ? b : a;
+        default: return b > a ? b : a;
+    }
+}
+
+// Election priority of record i in probe round r: earlier rounds beat later ones (a slot's owner never
+// changes once elected), then the smaller record index wins.  0 = free slot.
+__device__ __forceinline__ uint32_t elect_prio(int round, uint32_t i) {
+    return ((uint32_t)(FIRE_MAXR - round) << 12) | (4095u - i);
+}
+
+template <int NW>
+__global__ __launch_bounds__(LOG_FIRE_THREADS) __attribute__((amdgpu_waves_per_eu(4, 4))) void log_fire_kernel(const LogSegDesc *__restrict__ segs, int nseg,
                                                                     uint32_t nparts, int cap_log2, int has_val,
                                                                     AccPlan p, ResultPlan rp, int64_t start,
                                                                     int64_t end, OutCols o,
-                                                                    unsigned long long *overflow) {
-    extern __shared__ __attribute__((aligned(16))) int64_t s_dyn[];   // the LDS hash table (key, words; SoA)
+                                                                    unsigned long long *overflow, int xp) {
+    // Dynamic LDS (FIRE_LDS bytes).  Fast path:
+    //   s_key [FIRE_RCAP] int64   record keys (record i = r * 512 + tid), then leader keys by row ordinal
+    //   s_val [FIRE_RCAP] int64   values grouped by key (after the election; overlays s_own)
+    //   s_own [FIRE_OWN]  uint32  election table: slot -> priority of its owner record
+    //   s_cnt [FIRE_RCAP] uint32  per-leader record counts -> offsets -> (offset | count << 16) by ordinal
+    // Slow path: the same bytes hold a FireCtx hash table (key + words, SoA, 2^cap_log2 slots).
+    extern __shared__ __attribute__((aligned(16))) int64_t s_dyn[];
+    int64_t *const s_key = s_dyn;
+    int64_t *const s_val = s_dyn + FIRE_RCAP;
+    uint32_t *const s_own = (uint32_t *)(s_dyn + FIRE_RCAP);
+    uint32_t *const s_cnt = (uint32_t *)(s_dyn + 2 * FIRE_RCAP);
     __shared__ int64_t s_side[GWO_MAX_WORDS + 1];
     __shared__ unsigned s_used, s_fail;
-    __shared__ uint32_t s_beg[2][LOG_MAX_SEGS + 1];   // flattened record space of a partition: segment s
-    __shared__ uint32_t s_src[2][LOG_MAX_SEGS];       //   covers [s_beg[s], s_beg[s+1]) from record s_src[s]
+    __shared__ uint32_t s_beg[LOG_MAX_SEGS + 1];   // flattened record space of a partition: segment s
+    __shared__ uint32_t s_src[LOG_MAX_SEGS];       //   covers [s_beg[s], s_beg[s+1]) from record s_src[s]
     __shared__ const int64_t *s_rp[LOG_MAX_SEGS];
-    __shared__ uint32_t s_wrows[8][LOG_FIRE_THREADS / 64];   // rows per (sweep round, wave), then prefixes
+    __shared__ uint32_t s_wsum[FIRE_RPT * (LOG_FIRE_THREADS / 64)];   // per-(r, wave) sums -> prefixes
+    __shared__ uint32_t s_tot;
+    __shared__ int s_any[2];
+    __shared__ uint32_t s_pw[LOG_FIRE_THREADS / 64 + 1];
     __shared__ unsigned long long s_rbase;
-    __shared__ uint32_t s_side_pos;
-    const int tid = threadIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int cap = 1 << cap_log2;
     FireCtx c{s_dyn, s_dyn + cap, s_side, &s_used, &s_fail, cap, (unsigned)(cap - (cap >> 3))};
     uint32_t part = blockIdx.x;
     if (part >= nparts) return;
+    if ((xp >> 8) && blockIdx.x >= gridDim.x / 2) {   // experiment: phase offset of the CU's second workgroup
+        const unsigned long long t0x = clock64();
+        while (clock64() - t0x < (unsigned long long)(xp >> 8) * 1000ull) __builtin_amdgcn_s_sleep(8);
+    }
     for (int s = tid; s < nseg; s += LOG_FIRE_THREADS) s_rp[s] = segs[s].rec;
-    fire_clear(c, p);   // the first publish() synchronises
+    if (tid <= GWO_MAX_WORDS) s_side[tid] = tid == 0 ? 0 : p.ident[tid - 1];
+    if (tid == 0) {
+        s_used = 0;
+        s_fail = 0;
+    }
 
-    // segment ranges of a partition -> s_beg[b] / s_src[b] (all threads; ends synchronised)
-    auto publish = [&](int b, uint32_t cnt, uint32_t off) {
-        uint32_t tot;
-        uint32_t ex = block_exclusive_scan(cnt, &tot);
-        if (tid < nseg) {
-            s_beg[b][tid] = ex;
-            s_src[b][tid] = off;
+    // segment ranges of a partition -> s_beg / s_src (all threads; ends synchronised)
+    // (a DPP scan with the workgroup size fixed at compile time: block_exclusive_scan reads blockDim,
+    // which costs a dispatch-packet load and a vmcnt(0) wait on everything in flight)
+    auto publish = [&](uint32_t cnt, uint32_t off) {
+        const uint32_t incl_c = wave_incl_scan(cnt);
+        if (lane == 63) s_pw[wave] = incl_c;
+        __syncthreads();
+        if (tid == 0) {
+            uint32_t run = 0;
+#pragma unroll
+            for (int w = 0; w < LOG_FIRE_THREADS / 64; ++w) {
+                const uint32_t t = s_pw[w];
+                s_pw[w] = run;
+                run += t;
+            }
+            s_pw[LOG_FIRE_THREADS / 64] = run;
         }
-        if (tid == 0) s_beg[b][nseg] = tot;
+        __syncthreads();
+        if (tid < nseg) {
+            s_beg[tid] = s_pw[wave] + incl_c - cnt;
+            s_src[tid] = off;
+        }
+        if (tid == 0) s_beg[nseg] = s_pw[LOG_FIRE_THREADS / 64];
         __syncthreads();
     };
     // register prefetch of a partition's records (only when they all fit); global (not flat) loads,
     // so LDS waits in between do not wait for them
     int64_t rk[FIRE_RPT], rv[FIRE_RPT];
-    auto prefetch = [&](int b) {
-        const uint32_t total = s_beg[b][nseg];
-        const bool fits = total <= (uint32_t)FIRE_RCAP;
+    auto prefetch = [&](bool on) {
+        const uint32_t total = s_beg[nseg];
+        const bool fits = on && total <= (uint32_t)FIRE_RCAP;
         const int64_t *addr[FIRE_RPT];
         int segr[FIRE_RPT];
         if (nseg <= 32) {   // segment of record i = number of segment starts <= i (broadcast LDS reads)
 #pragma unroll
             for (int r = 0; r < FIRE_RPT; ++r) segr[r] = 0;
             for (int sg = 1; sg < nseg; ++sg) {
-                const uint32_t bs = s_beg[b][sg];
+                const uint32_t bs = s_beg[sg];
 #pragma unroll
                 for (int r = 0; r < FIRE_RPT; ++r) segr[r] += (uint32_t)(tid + r * LOG_FIRE_THREADS) >= bs;
             }
@@ -558,7 +653,7 @@ __global__ __launch_bounds__(LOG_FIRE_THREADS) void log_fire_kernel(const LogSeg
 #pragma unroll
             for (int r = 0; r < FIRE_RPT; ++r) {
                 const uint32_t i = tid + r * LOG_FIRE_THREADS;
-                while (i < total && i >= s_beg[b][seg + 1]) seg++;
+                while (i < total && i >= s_beg[seg + 1]) seg++;
                 segr[r] = seg;
             }
         }
@@ -568,7 +663,7 @@ __global__ __launch_bounds__(LOG_FIRE_THREADS) void log_fire_kernel(const LogSeg
             addr[r] = s_rp[0];
             if (fits && i < total) {
                 const int sg = segr[r];
-                addr[r] = s_rp[sg] + (uint64_t)(s_src[b][sg] + (i - s_beg[b][sg])) * (has_val ? 2 : 1);
+                addr[r] = s_rp[sg] + (uint64_t)(s_src[sg] + (i - s_beg[sg])) * (has_val ? 2 : 1);
             }
         }
 #pragma unroll
@@ -584,98 +679,187 @@ __global__ __launch_bounds__(LOG_FIRE_THREADS) void log_fire_kernel(const LogSeg
         }
     };
 
+    // thread s < nseg keeps segment s's count / offset arrays (loaded once)
+    g_u32 *seg_cnt = nullptr, *seg_off = nullptr;
     uint32_t a_cnt = 0, a_off = 0;
     if (tid < nseg) {
-        a_cnt = segs[tid].cnt[part];
-        a_off = segs[tid].off[part];
+        seg_cnt = (g_u32 *)segs[tid].cnt;
+        seg_off = (g_u32 *)segs[tid].off;
+        a_cnt = seg_cnt[part];
+        a_off = seg_off[part];
     }
-    int buf = 0;
-    publish(buf, a_cnt, a_off);
-    prefetch(buf);
+    publish(a_cnt, a_off);
+    prefetch(true);
+#ifdef GWO_FIRE_PROF   // per-phase s_memtime totals of workgroup 0 (GWO_FIRE_XP & 16), printed at the end
+    unsigned long long T[8] = {0, 0, 0, 0, 0, 0, 0, 0}, t0 = 0, t1 = 0, rounds_total = 0;
+    const bool prof = (xp & 16) && blockIdx.x == 0;
+#define TSTAMP(i)            \
+    if (prof) {              \
+        t1 = clock64();      \
+        T[i] += t1 - t0;     \
+        t0 = t1;             \
+    }
+    if (prof) t0 = clock64();
+#else
+#define TSTAMP(i)
+#endif
     while (true) {
-        const uint32_t total = s_beg[buf][nseg];
+        if (xp & 32) { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+        TSTAMP(0)
+        const uint32_t total = s_beg[nseg];
         const uint32_t nxt = part + gridDim.x;
         const bool more = nxt < nparts;
-        // next partition's segment offsets: in flight while this one is folded
-        a_cnt = 0;
-        a_off = 0;
-        if (more && tid < nseg) {
-            a_cnt = segs[tid].cnt[nxt];
-            a_off = segs[tid].off[nxt];
-        }
+        // next partition's segment offsets: in flight while this one is folded (issued after the fast
+        // path's first use of rk/rv, so waiting for the prefetch does not wait for them too)
+        auto load_next = [&]() {
+            a_cnt = 0;
+            a_off = 0;
+            if (more && tid < nseg) {
+                a_cnt = seg_cnt[nxt];
+                a_off = seg_off[nxt];
+            }
+        };
+        unsigned long long rbase_lane0 = 0;   // wave 0 lane 0: the row reservation, consumed after P4
         bool fast = total <= (uint32_t)FIRE_RCAP;
         if (fast) {
-            // phase 1: every record finds (or claims) its key's slot; one LDS CAS per probe
-            int slot[FIRE_RPT];
-            unsigned claimed = 0, pending = 0;
+            // P0: record keys into LDS; free election table; zero counts
 #pragma unroll
             for (int r = 0; r < FIRE_RPT; ++r) {
-                const uint32_t i = tid + r * LOG_FIRE_THREADS;
-                slot[r] = -1;
-                if (i < total) {
-                    const int64_t k = rk[r];
-                    if (k == GWO_EMPTY_KEY) {
-                        slot[r] = -2;
+                const uint32_t i = r * LOG_FIRE_THREADS + tid;
+                if (i < total) s_key[i] = rk[r];
+            }
+            load_next();
+            for (int q = tid; q < FIRE_OWN / 4; q += LOG_FIRE_THREADS) ((uint4 *)s_own)[q] = make_uint4(0, 0, 0, 0);
+            for (int q = tid; q < FIRE_RCAP / 4; q += LOG_FIRE_THREADS) ((uint4 *)s_cnt)[q] = make_uint4(0, 0, 0, 0);
+            if (tid == 0) {
+                s_any[0] = 0;
+                s_any[1] = 0;
+            }
+            __syncthreads();
+            // P1: election.  Every record of a key probes the same slot sequence (double hashing on
+            // part_hash), so they resolve together; a slot's winner is the key's leader record.
+            // sl[r] is the record's probe slot while it is pending, then its leader record.
+            uint32_t sl[FIRE_RPT];
+            unsigned pend = 0;
+#pragma unroll
+            for (int r = 0; r < FIRE_RPT; ++r) {
+                const uint32_t i = r * LOG_FIRE_THREADS + tid;
+                sl[r] = (uint32_t)part_hash(rk[r]) & (FIRE_OWN - 1);
+                if (i < total) pend |= 1u << r;
+            }
+            int round = 0;
+            while (true) {
+#pragma unroll
+                for (int r = 0; r < FIRE_RPT; ++r)
+                    if ((pend >> r) & 1u) atomicMax(&s_own[sl[r]], elect_prio(round, r * LOG_FIRE_THREADS + tid));
+                __syncthreads();
+                if (tid == 0) s_any[(round + 1) & 1] = 0;   // every read of it (round - 1) is behind the barrier
+#pragma unroll
+                for (int r = 0; r < FIRE_RPT; ++r) {
+                    if (!((pend >> r) & 1u)) continue;
+                    const uint32_t i = r * LOG_FIRE_THREADS + tid;
+                    const uint32_t j = 4095u - (s_own[sl[r]] & 4095u);
+                    if (j == i || s_key[j] == rk[r]) {
+                        sl[r] = j;
+                        pend &= ~(1u << r);
                     } else {
-                        int sl = (int)(part_hash(k) & (uint64_t)(cap - 1));
-                        for (int probes = 0; probes < cap; ++probes) {
-                            unsigned long long prev = atomicCAS((unsigned long long *)&c.key[sl],
-                                                                (unsigned long long)GWO_EMPTY_KEY, (unsigned long long)k);
-                            if ((int64_t)prev == GWO_EMPTY_KEY || (int64_t)prev == k) {
-                                claimed |= (unsigned)((int64_t)prev == GWO_EMPTY_KEY) << r;
-                                slot[r] = sl;
-                                break;
-                            }
-                            sl = (sl + 1) & (cap - 1);
-                        }
-                        if (slot[r] == -1) pending = 1;
+                        const uint32_t step = ((uint32_t)(part_hash(rk[r]) >> 24) & (FIRE_OWN - 1)) | 1u;
+                        sl[r] = (sl[r] + step) & (FIRE_OWN - 1);
                     }
                 }
+                if (pend) s_any[round & 1] = 1;
+                __syncthreads();
+                const bool again = s_any[round & 1] != 0;   // (no __syncthreads_or: it reads the dispatch
+                ++round;                                     //  packet with a vector load and waits vmcnt(0))
+                if (!again) break;
+                if (round >= FIRE_MAXR) {   // uniform: give the partition to the slow path
+                    fast = false;
+                    break;
+                }
             }
-            if (pending) s_fail = 1;   // table full
-            {
-                unsigned nc = (unsigned)__popc(claimed);
-                for (int o2 = 32; o2 > 0; o2 >>= 1) nc += __shfl_xor(nc, o2);
-                if ((tid & 63) == 0 && nc) atomicAdd(&s_used, nc);
-            }
-            __syncthreads();
-            fast = s_fail == 0 && s_used <= c.limit;
-            __syncthreads();
+#ifdef GWO_FIRE_PROF
+            rounds_total += round;
+#endif
+            TSTAMP(1)
             if (fast) {
-                // phase 2: the claiming record initialises its slot with plain stores
+                // P2: rank of each record among its key's records (rk is dead from here on)
+                uint32_t rank[FIRE_RPT];
 #pragma unroll
                 for (int r = 0; r < FIRE_RPT; ++r) {
-                    if (!((claimed >> r) & 1u)) continue;
-#pragma unroll
-                    for (int w = 0; w < NW; ++w) c.acc[w * cap + slot[r]] = lift_word(p, w, rv[r]);
+                    const uint32_t i = r * LOG_FIRE_THREADS + tid;
+                    rank[r] = i < total ? atomicAdd(&s_cnt[sl[r]], 1u) : 0u;
                 }
                 __syncthreads();
-                // phase 3: the other records of a key combine atomically (about half of them in C4)
+                // P3: exclusive scan over record ids of (count | 1 << 16) at leaders -> each leader's
+                // first value offset (low half) and row ordinal (high half)
+                uint32_t x[FIRE_RPT], incl[FIRE_RPT];
 #pragma unroll
                 for (int r = 0; r < FIRE_RPT; ++r) {
-                    if (slot[r] == -1 || ((claimed >> r) & 1u)) continue;
-                    int64_t *acc;
-                    int accs;
-                    if (slot[r] == -2) {
-                        s_side[0] = 1;
-                        acc = s_side + 1;
-                        accs = 1;
-                    } else {
-                        acc = c.acc + slot[r];
-                        accs = cap;
+                    const uint32_t i = r * LOG_FIRE_THREADS + tid;
+                    x[r] = (i < total && sl[r] == i) ? (s_cnt[i] | 0x10000u) : 0u;
+                }
+#pragma unroll
+                for (int r = 0; r < FIRE_RPT; ++r) {
+                    incl[r] = wave_incl_scan(x[r]);
+                    if (lane == 63) s_wsum[r * (LOG_FIRE_THREADS / 64) + wave] = incl[r];
+                }
+                __syncthreads();
+                if (wave == 0) {
+                    constexpr int NS = FIRE_RPT * (LOG_FIRE_THREADS / 64);
+                    const uint32_t w = lane < NS ? s_wsum[lane] : 0u;
+                    const uint32_t wi = wave_incl_scan(w);
+                    if (lane < NS) s_wsum[lane] = wi - w;
+                    const uint32_t tot = __shfl(wi, 63);
+                    if (lane == 0) {
+                        s_tot = tot;
+                        const uint32_t rows = tot >> 16;
+                        rbase_lane0 = rows ? atomicAdd(o.count, (unsigned long long)rows) : 0ull;
                     }
-#pragma unroll
-                    for (int w = 0; w < NW; ++w) lds_combine64(acc + w * accs, p.op[w], lift_word(p, w, rv[r]));
                 }
                 __syncthreads();
-            } else {
-                fire_clear(c, p);   // back to a clean table for the slow path
+                uint32_t lo[FIRE_RPT];   // leaders: value offset | row ordinal << 16
+                unsigned leader = 0;
+#pragma unroll
+                for (int r = 0; r < FIRE_RPT; ++r) {
+                    const uint32_t i = r * LOG_FIRE_THREADS + tid;
+                    const uint32_t pre = s_wsum[r * (LOG_FIRE_THREADS / 64) + wave] + incl[r] - x[r];
+                    lo[r] = pre;
+                    if (x[r]) {
+                        leader |= 1u << r;
+                        s_cnt[i] = pre & 0xffffu;
+                    }
+                }
                 __syncthreads();
+                // P4: values grouped by key, in row order (the election table is dead)
+                if (has_val) {
+#pragma unroll
+                    for (int r = 0; r < FIRE_RPT; ++r) {
+                        const uint32_t i = r * LOG_FIRE_THREADS + tid;
+                        if (i >= total) continue;
+                        const uint32_t off = ((leader >> r) & 1u) ? (lo[r] & 0xffffu) : s_cnt[sl[r]];
+                        const uint32_t at = off + rank[r];
+                        if (at < (uint32_t)FIRE_RCAP) s_val[at] = rv[r];
+                    }
+                }
+                __syncthreads();
+                // P4b: row ordinal -> (value offset | leader record << 16); a row's value count is the
+                // next row's offset minus its own (s_cnt[rows] = total)
+#pragma unroll
+                for (int r = 0; r < FIRE_RPT; ++r)
+                    if ((leader >> r) & 1u)
+                        s_cnt[lo[r] >> 16] = (lo[r] & 0xffffu) | ((uint32_t)(r * LOG_FIRE_THREADS + tid) << 16);
+                if (tid == 0) {
+                    s_cnt[s_tot >> 16] = s_tot & 0xffffu;
+                    s_rbase = rbase_lane0;   // the atomic's round trip overlapped P4
+                }
             }
         }
+        TSTAMP(2)
+        if (total > (uint32_t)FIRE_RCAP) load_next();   // (the fast path loaded them in P0)
         if (!fast) {
             // slow path: hash-table rounds over disjoint ranges of hash bits 12..43, direct loads
             if (tid == 0) atomicAdd(overflow + 1, 1ull);   // slow-path partitions (statistics)
+            __syncthreads();
             fire_clear(c, p);
             __syncthreads();
             const uint64_t kAll = 1ull << 32;
@@ -685,8 +869,8 @@ __global__ __launch_bounds__(LOG_FIRE_THREADS) void log_fire_kernel(const LogSeg
                 const bool ranged = width < kAll;
                 int seg = 0;
                 for (uint32_t i = tid; i < total; i += LOG_FIRE_THREADS) {
-                    while (i >= s_beg[buf][seg + 1]) seg++;
-                    const int64_t *q = s_rp[seg] + (uint64_t)(s_src[buf][seg] + (i - s_beg[buf][seg])) * (has_val ? 2 : 1);
+                    while (i >= s_beg[seg + 1]) seg++;
+                    const int64_t *q = s_rp[seg] + (uint64_t)(s_src[seg] + (i - s_beg[seg])) * (has_val ? 2 : 1);
                     const int64_t k = q[0];
                     const uint64_t h = part_hash(k);
                     if (ranged) {
@@ -712,68 +896,102 @@ __global__ __launch_bounds__(LOG_FIRE_THREADS) void log_fire_kernel(const LogSeg
                 lo = hi;
             }
         }
-        if (more) {
-            publish(buf ^ 1, a_cnt, a_off);
-            prefetch(buf ^ 1);   // in flight during this partition's fold and emit
-        }
+        // (synchronises: the fast path's (offset, count) words and s_rbase are visible)
+        if (more) publish(a_cnt, a_off);
+        else __syncthreads();
+        // unconditional, so the loads land straight in rk/rv (no loop-carried copy that would wait for
+        // them): in flight during this partition's emit and the next one's election
+        prefetch(more);
+        TSTAMP(3)
         if (fast) {
-            // emit: thread t sweeps slots t + m*512; rows are placed in (m, wave, lane) order, so each
-            // store instruction writes one contiguous run; slots are reset as they are read
-            constexpr int NWAVES = LOG_FIRE_THREADS / 64;
-            const int lane = tid & 63, wave = tid >> 6;
-            const int rounds = cap / LOG_FIRE_THREADS;
-            for (int m = 0; m < rounds; ++m) {
-                const unsigned long long bal = __ballot(c.key[m * LOG_FIRE_THREADS + tid] != GWO_EMPTY_KEY);
-                if (lane == 0) s_wrows[m][wave] = (uint32_t)__popcll(bal);
-            }
-            __syncthreads();
-            if (tid == 0) {   // exclusive prefix over (round, wave), then one reservation per partition
-                uint32_t run = 0;
-                for (int m = 0; m < rounds; ++m)
-                    for (int w = 0; w < NWAVES; ++w) {
-                        uint32_t t = s_wrows[m][w];
-                        s_wrows[m][w] = run;
-                        run += t;
-                    }
-                s_side_pos = run;
-                run += s_side[0] != 0;
-                s_rbase = run ? atomicAdd(o.count, (unsigned long long)run) : 0ull;
-            }
-            __syncthreads();
+            // P5: one row per leader, in ordinal order.  Thread t takes ordinal t - sh (sh = rbase & 1),
+            // so lanes 2m and 2m+1 own a 16-B-aligned pair of global rows; after a DPP swap within the
+            // pair the even lane stores the pair's key/start/end and the odd lane its results, one 16-B
+            // store per column (8-B stores are issue-bound at about half the bandwidth).  A row whose
+            // partner is outside the partition's run is stored alone, 8 B per column.
+            const uint32_t rows = s_tot >> 16;
             const unsigned long long rbase = s_rbase;
-            for (int m = 0; m < rounds; ++m) {
-                const int sl = m * LOG_FIRE_THREADS + tid;
-                const int64_t k = c.key[sl];
-                const bool occ = k != GWO_EMPTY_KEY;
-                const unsigned long long bal = __ballot(occ);
-                if (!occ) continue;
-                int64_t acc[NW];
+            const int sh = (int)(rbase & 1ull);
+            const bool odd = (tid & 1) != 0;
+            for (int base = 0; base < (int)rows + sh; base += LOG_FIRE_THREADS) {
+                const int q = base + tid - sh;
+                const bool valid = q >= 0 && q < (int)rows;
+                int64_t k = 0, res[4] = {0, 0, 0, 0};
+                if (valid && !(xp & 128)) {
+                    const uint32_t w0 = s_cnt[q], off = w0 & 0xffffu, n = (xp & 64) ? 1u : (s_cnt[q + 1] & 0xffffu) - off;
+                    k = s_key[w0 >> 16];
+                    // the run's count, sum and min/max (of the values, or of their Double.compareTo order
+                    // keys for float64) in a tight loop; the plan's words are read off them afterwards
+                    int64_t si = 0, mn = 0x7fffffffffffffffLL, mx = (int64_t)0x8000000000000000LL;
+                    double sf = 0.0;
+                    if (has_val) {
+                        if (p.value_is_f64) {
+                            for (uint32_t t = 0; t < n; ++t) {
+                                const int64_t v = s_val[off + t], ok = f64_order_key(v);
+                                sf += __longlong_as_double(v);
+                                mn = ok < mn ? ok : mn;
+                                mx = ok > mx ? ok : mx;
+                            }
+                        } else {
+                            for (uint32_t t = 0; t < n; ++t) {
+                                const int64_t v = s_val[off + t];
+                                si = (int64_t)((uint64_t)si + (uint64_t)v);
+                                mn = v < mn ? v : mn;
+                                mx = v > mx ? v : mx;
+                            }
+                        }
+                    }
+                    int64_t acc[NW];
 #pragma unroll
-                for (int w = 0; w < NW; ++w) acc[w] = c.acc[w * cap + sl];
-                c.key[sl] = GWO_EMPTY_KEY;   // words need no reset: the next claimer overwrites them
-                const unsigned long long pos =
-                    rbase + s_wrows[m][wave] + (unsigned long long)__popcll(bal & ((1ull << lane) - 1ull));
-                if ((long long)pos < o.cap) emit_row<NW>(rp, acc, o, pos, k, start, end);
-            }
-            if (tid == 0 && s_side[0] != 0) {
-                int64_t acc[NW];
+                    for (int w = 0; w < NW; ++w) {
+                        switch (p.op[w]) {
+                            case ACC_ADD_I64: acc[w] = p.src[w] == SRC_ONE ? (int64_t)n : si; break;
+                            case ACC_ADD_F64: acc[w] = __double_as_longlong(sf); break;
+                            case ACC_MIN_I64: acc[w] = p.src[w] == SRC_ONE ? 1 : mn; break;
+                            default: acc[w] = p.src[w] == SRC_ONE ? 1 : mx; break;
+                        }
+                    }
+                    row_results<NW>(rp, acc, res);
+                }
+                const bool pvalid = dpp_swap_pair(valid ? 1 : 0) != 0;
+                const int64_t kp = dpp_swap_pair64(k);
+                int64_t rpv[4];
 #pragma unroll
-                for (int w = 0; w < NW; ++w) acc[w] = s_side[1 + w];
-                const unsigned long long pos = rbase + s_side_pos;
-                if ((long long)pos < o.cap) emit_row<NW>(rp, acc, o, pos, GWO_EMPTY_KEY, start, end);
+                for (int a = 0; a < 4; ++a) rpv[a] = dpp_swap_pair64(res[a]);
+                if (!valid || (xp & 1)) continue;
+                const unsigned long long pos = rbase + (unsigned long long)(long long)q;
+                const unsigned long long pb = pos & ~1ull;   // the pair's first row
+                if (pvalid && (long long)pb + 1 < o.cap) {
+                    if (!odd) {
+                        *(ll2 *)(o.key + pb) = ll2{k, kp};
+                        *(ll2 *)(o.start + pb) = ll2{start, start};
+                        *(ll2 *)(o.end + pb) = ll2{end, end};
+                    } else {
+#pragma unroll
+                        for (int a = 0; a < 4; ++a)
+                            if (a < rp.naggs) *(ll2 *)(o.res[a] + pb) = ll2{rpv[a], res[a]};
+                    }
+                } else if ((long long)pos < o.cap) {
+                    o.key[pos] = k;
+                    o.start[pos] = start;
+                    o.end[pos] = end;
+#pragma unroll
+                    for (int a = 0; a < 4; ++a)
+                        if (a < rp.naggs) o.res[a][pos] = res[a];
+                }
             }
-            __syncthreads();
-            if (tid <= GWO_MAX_WORDS) s_side[tid] = tid == 0 ? 0 : p.ident[tid - 1];
-            if (tid == 0) {
-                s_used = 0;
-                s_fail = 0;
-            }
-            __syncthreads();
+            __syncthreads();   // the next partition overwrites s_key / s_cnt
         }
+        TSTAMP(4)
         if (!more) break;
         part = nxt;
-        buf ^= 1;
     }
+#ifdef GWO_FIRE_PROF
+    if (prof && tid == 0)
+        printf("FIREPROF parts=%u rounds=%llu wait=%llu elect=%llu sortscan=%llu pubpre=%llu emit=%llu\n",
+               nparts / gridDim.x, rounds_total, T[0], T[1], T[2], T[3], T[4]);
+#endif
+#undef TSTAMP
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -846,16 +1064,19 @@ void launch_log_fire(const LogSegDesc *segs, int nseg, int lp, int has_val, cons
                      const ResultPlan &rp, int64_t start, int64_t end, OutCols out, unsigned long long *overflow,
                      int cus, int max_per_cu, hipStream_t s) {
     if (nseg <= 0 || nseg > LOG_MAX_SEGS) return;   // nothing to fold (the host never asks; defensive)
+    static_assert(FIRE_OWN * 4 <= FIRE_RCAP * 8 && FIRE_RCAP <= 4096 && FIRE_MAXR < 16, "fire fast-path layout");
     int cl = log_fire_cap_log2(plan.nwords);
     size_t lds = (size_t)(1 + plan.nwords) * 8 << cl;
+    if (lds < (size_t)FIRE_LDS) lds = FIRE_LDS;
     uint32_t parts = 1u << lp;
     // persistent grid: two 64-KiB-LDS workgroups per CU, or fewer to leave room for concurrent kernels
     const uint32_t groups = (uint32_t)cus * (uint32_t)(max_per_cu < 2 ? max_per_cu : 2);
     uint32_t grid = parts < groups ? parts : groups;
+    static const int xp = getenv("GWO_FIRE_XP") ? atoi(getenv("GWO_FIRE_XP")) : 0;
 #define GWO_FIRE_NW(NW)                                                                                          \
     case NW:                                                                                                     \
         hipLaunchKernelGGL(log_fire_kernel<NW>, dim3(grid), dim3(LOG_FIRE_THREADS), lds, s, segs, nseg, parts, cl, \
-                           has_val, plan, rp, start, end, out, overflow);                                        \
+                           has_val, plan, rp, start, end, out, overflow, xp);                                    \
         break;
     switch (plan.nwords) {
         GWO_FIRE_NW(1)
