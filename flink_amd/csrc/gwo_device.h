@@ -60,6 +60,18 @@ __device__ __forceinline__ int64_t window_start_f(int64_t ts, int64_t off, int64
     return jsub(ts, jrem_f(jadd(jsub(ts, off), size), size, inv));
 }
 
+// floor(a / d) for 0 <= a < 2^52 and d > 0: the double estimate is within 1 of the quotient, so one
+// exact correction step suffices (about 10 instructions instead of fdiv_floor's 40).
+__device__ __forceinline__ int64_t fdiv_small(int64_t a, int64_t d, double inv) {
+    const double two52 = 4503599627370496.0;
+    const double af = __longlong_as_double(a | 0x4330000000000000LL) - two52;   // exact: a < 2^52
+    const double qf = trunc(af * inv);
+    int64_t q = __double_as_longlong(qf + two52) & 0x000FFFFFFFFFFFFFLL;        // exact: 0 <= qf < 2^52
+    const int64_t r = a - q * d;
+    q += (int64_t)(r >= d) - (int64_t)(r < 0);
+    return q;
+}
+
 // WindowOperator.cleanupTime (WindowOperator.java:639-646): maxTs + lateness, Long.MAX_VALUE on overflow.
 __device__ __host__ __forceinline__ int64_t cleanup_time(int64_t max_ts, int64_t lateness) {
     int64_t c = jadd(max_ts, lateness);
@@ -96,9 +108,11 @@ __device__ __host__ __forceinline__ int32_t murmur_hash(int32_t code) {  // Math
     if (r != (int32_t)0x80000000) return -r;
     return 0;
 }
-// KeyGroupRangeAssignment.java:60-73
+// KeyGroupRangeAssignment.java:60-73 (murmur_hash is non-negative, so a power-of-two maxParallelism --
+// the default 128 and every C4 setting -- is a mask, not a 32-bit division)
 __device__ __host__ __forceinline__ int32_t key_group(int64_t key, int kind, int32_t max_par) {
-    return murmur_hash(key_hash_code(key, kind)) % max_par;
+    const int32_t m = murmur_hash(key_hash_code(key, kind));
+    return (max_par & (max_par - 1)) == 0 ? (m & (max_par - 1)) : m % max_par;
 }
 
 // ---- table hashing -------------------------------------------------------------------------------

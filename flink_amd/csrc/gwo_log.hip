@@ -33,13 +33,26 @@ typedef long long ll2 __attribute__((ext_vector_type(2)));
 enum LogClass : int { L_ACCEPT = 0, L_LATE = 1, L_SKIP = 2, L_REFIRE = 3, L_BAD_TS = 4 };
 
 // Tumbling classification, WindowOperator.java:386-427 + TumblingEventTimeWindows.java:68-81.
+// With a = ts - offset + size in [0, 2^52) (every timestamp within 142,000 years of the epoch):
+// getWindowStartWithOffset = ts - a % size = offset + (q - 1) * size for q = floor(a / size), and the
+// window index floor(start / size) = q - 1 - (offset < 0) since |offset| < size (the assigner's
+// constructor check, TumblingEventTimeWindows.java:57-60) -- one small division instead of two full ones.
 __device__ __forceinline__ int log_classify(int64_t ts, const WindowGeom &g, long long &unit) {
     if (ts == GWO_LONG_MIN) return L_BAD_TS;
-    int64_t start = window_start_f(ts, g.offset, g.size, g.inv_size);
+    const int64_t a = jadd(jsub(ts, g.offset), g.size);
+    int64_t start, u;
+    if ((uint64_t)a < (1ull << 52)) {
+        const int64_t q = fdiv_small(a, g.size, g.inv_size);
+        start = g.offset + (q - 1) * g.size;
+        u = q - 1 - (g.offset < 0 ? 1 : 0);
+    } else {
+        start = window_start_f(ts, g.offset, g.size, g.inv_size);
+        u = fdiv_floor(start, g.size, g.inv_size);
+    }
     int64_t max_ts = jsub(jadd(start, g.size), 1);
     if (cleanup_time(max_ts, g.lateness) <= g.wm) return jadd(ts, g.lateness) <= g.wm ? L_LATE : L_SKIP;
     if (max_ts <= g.wm) return L_REFIRE;
-    unit = fdiv_floor(start, g.size, g.inv_size);
+    unit = u;
     return L_ACCEPT;
 }
 
@@ -72,7 +85,7 @@ __device__ __forceinline__ uint32_t tile_offsets(const uint32_t *s_cnt, uint32_t
 // Bucket b owns records [b*cap, (b+1)*cap) of the buffer; cursor[b*LOG_CUR_STRIDE] ends as its record
 // count (also when it exceeds cap: those records are not written and the host reruns).
 // ------------------------------------------------------------------------------------------------
-template <bool HASV>
+template <bool HASV, int S>   // S: record stride in int64 words (1: SoA columns, 3: {key, ts, value}; 0: runtime)
 __global__ __launch_bounds__(LOG_K1_THREADS) void log_part_kernel(
     const int64_t *__restrict__ key, const int64_t *__restrict__ ts, const int64_t *__restrict__ val, int64_t n,
     int64_t stride, WindowGeom g, long long base, int nunits, unsigned long long *__restrict__ cursor, uint64_t cap,
@@ -97,9 +110,10 @@ __global__ __launch_bounds__(LOG_K1_THREADS) void log_part_kernel(
         for (int j = 0; j < LOG_K1_PER; ++j) {
             int64_t i = tile + j * LOG_K1_THREADS + tid;
             i = i < n ? i : (tile < n ? tile : 0);
-            tt[j] = __builtin_nontemporal_load(ts + i * stride);
-            kk[j] = __builtin_nontemporal_load(key + i * stride);
-            vv[j] = HASV ? __builtin_nontemporal_load(val + i * stride) : 0;
+            const int64_t o = S ? i * S : i * stride;
+            tt[j] = __builtin_nontemporal_load(ts + o);
+            kk[j] = __builtin_nontemporal_load(key + o);
+            vv[j] = HASV ? __builtin_nontemporal_load(val + o) : 0;
         }
     };
     const int64_t tstride = (int64_t)gridDim.x * LOG_TILE;
@@ -140,7 +154,7 @@ __global__ __launch_bounds__(LOG_K1_THREADS) void log_part_kernel(
                     if ((long long)pos < side_cap) {
                         side_key[pos] = kk[j];
                         side_ts[pos] = tt[j];
-                        side_val[pos] = val ? val[i * stride] : 0;
+                        side_val[pos] = HASV ? vv[j] : (val ? val[i * stride] : 0);
                     }
                 }
             } else if (c == L_REFIRE) {
@@ -1004,14 +1018,20 @@ void launch_log_part(const int64_t *key, const int64_t *ts, const int64_t *val, 
                      unsigned long long *side_count, long long side_cap, int side_enabled, hipStream_t s) {
     int64_t grid = (n + LOG_TILE - 1) / LOG_TILE;
     grid = grid < 1 ? 1 : (grid > 2048 ? 2048 : grid);
-    if (has_val)
-        hipLaunchKernelGGL(log_part_kernel<true>, dim3((int)grid), dim3(LOG_K1_THREADS), 0, s, key, ts, val, n, stride, g,
-                           base, nunits, cursor, cap, tmp, st, side_key, side_ts, side_val, side_count, side_cap,
-                           side_enabled);
-    else
-        hipLaunchKernelGGL(log_part_kernel<false>, dim3((int)grid), dim3(LOG_K1_THREADS), 0, s, key, ts, val, n, stride, g,
-                           base, nunits, cursor, cap, tmp, st, side_key, side_ts, side_val, side_count, side_cap,
-                           side_enabled);
+#define GWO_K1(HV, S)                                                                                          \
+    hipLaunchKernelGGL((log_part_kernel<HV, S>), dim3((int)grid), dim3(LOG_K1_THREADS), 0, s, key, ts, val, n, \
+                       stride, g, base, nunits, cursor, cap, tmp, st, side_key, side_ts, side_val, side_count,   \
+                       side_cap, side_enabled)
+    if (has_val) {
+        if (stride == 1) GWO_K1(true, 1);
+        else if (stride == 3) GWO_K1(true, 3);
+        else GWO_K1(true, 0);
+    } else {
+        if (stride == 1) GWO_K1(false, 1);
+        else if (stride == 3) GWO_K1(false, 3);
+        else GWO_K1(false, 0);
+    }
+#undef GWO_K1
 }
 
 __global__ __launch_bounds__(1024) void log_collect_kernel(unsigned long long *cursor, int nb, BatchStats *st,
