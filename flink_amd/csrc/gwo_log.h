@@ -17,7 +17,8 @@ static_assert(LOG_K1_PER * LOG_K1_THREADS == LOG_TILE, "K1 tile and pass-2 chunk
 #define LOG_CUR_STRIDE 16        // K1 bucket cursors: one per 128-B line (memory-side atomics serialise per line)
 #define FIRE_RPT 7                                   // records per thread in the fire's register prefetch
 #define FIRE_RCAP (FIRE_RPT * LOG_FIRE_THREADS)      // 3584: records per partition of the fire's fast path
-#define FIRE_OWN 4096                                // election table slots of the fire's fast path
+#define FIRE_OWN_LOG2 13
+#define FIRE_OWN (1 << FIRE_OWN_LOG2)                // election table slots of the fire's fast path
 #define FIRE_MAXR 15                                 // election rounds before a partition takes the slow path
 #define FIRE_LDS (FIRE_RCAP * 8 * 2 + (FIRE_RCAP + 4) * 4)   // fast-path dynamic LDS: keys, values, counts (70 KiB)
 #define LOG_MAX_SEGS 512         // segments (batches) per window that one fire folds (= LOG_FIRE_THREADS)

@@ -572,6 +572,12 @@ __device__ __forceinline__ int64_t word_combine(int op, int64_t a, int64_t b) {
     }
 }
 
+// Slot hash of the fire's election table: two 32-bit multiplies (part_hash, whose top bits picked the
+// partition, costs about 20 instructions); the top bits index the table, lower bits give the probe step.
+__device__ __forceinline__ uint32_t slot_mix(int64_t k) {
+    return (uint32_t)k * 0x9E3779B1u + (uint32_t)((uint64_t)k >> 32) * 0x85EBCA77u;
+}
+
 // Election priority of record i in probe round r: earlier rounds beat later ones (a slot's owner never
 // changes once elected), then the smaller record index wins.  0 = free slot.
 __device__ __forceinline__ uint32_t elect_prio(int round, uint32_t i) {
@@ -587,7 +593,8 @@ __global__ __launch_bounds__(LOG_FIRE_THREADS) __attribute__((amdgpu_waves_per_e
     // Dynamic LDS (FIRE_LDS bytes).  Fast path:
     //   s_key [FIRE_RCAP] int64   record keys (record i = r * 512 + tid), then leader keys by row ordinal
     //   s_val [FIRE_RCAP] int64   values grouped by key (after the election; overlays s_own)
-    //   s_own [FIRE_OWN]  uint32  election table: slot -> priority of its owner record
+    //   s_own [FIRE_OWN]  uint32  election table: slot -> priority of its owner record (overlays s_val
+    //                             and the head of s_cnt; s_cnt is zeroed after the election)
     //   s_cnt [FIRE_RCAP] uint32  per-leader record counts -> offsets -> (offset | count << 16) by ordinal
     // Slow path: the same bytes hold a FireCtx hash table (key + words, SoA, 2^cap_log2 slots).
     extern __shared__ __attribute__((aligned(16))) int64_t s_dyn[];
@@ -744,7 +751,6 @@ __global__ __launch_bounds__(LOG_FIRE_THREADS) __attribute__((amdgpu_waves_per_e
             }
             load_next();
             for (int q = tid; q < FIRE_OWN / 4; q += LOG_FIRE_THREADS) ((uint4 *)s_own)[q] = make_uint4(0, 0, 0, 0);
-            for (int q = tid; q < FIRE_RCAP / 4; q += LOG_FIRE_THREADS) ((uint4 *)s_cnt)[q] = make_uint4(0, 0, 0, 0);
             if (tid == 0) {
                 s_any[0] = 0;
                 s_any[1] = 0;
@@ -758,7 +764,7 @@ __global__ __launch_bounds__(LOG_FIRE_THREADS) __attribute__((amdgpu_waves_per_e
 #pragma unroll
             for (int r = 0; r < FIRE_RPT; ++r) {
                 const uint32_t i = r * LOG_FIRE_THREADS + tid;
-                sl[r] = (uint32_t)part_hash(rk[r]) & (FIRE_OWN - 1);
+                sl[r] = slot_mix(rk[r]) >> (32 - FIRE_OWN_LOG2);
                 if (i < total) pend |= 1u << r;
             }
             int round = 0;
@@ -777,7 +783,7 @@ __global__ __launch_bounds__(LOG_FIRE_THREADS) __attribute__((amdgpu_waves_per_e
                         sl[r] = j;
                         pend &= ~(1u << r);
                     } else {
-                        const uint32_t step = ((uint32_t)(part_hash(rk[r]) >> 24) & (FIRE_OWN - 1)) | 1u;
+                        const uint32_t step = ((slot_mix(rk[r]) >> 4) & (FIRE_OWN - 1)) | 1u;
                         sl[r] = (sl[r] + step) & (FIRE_OWN - 1);
                     }
                 }
@@ -796,6 +802,8 @@ __global__ __launch_bounds__(LOG_FIRE_THREADS) __attribute__((amdgpu_waves_per_e
 #endif
             TSTAMP(1)
             if (fast) {
+                for (int q = tid; q < FIRE_RCAP / 4; q += LOG_FIRE_THREADS) ((uint4 *)s_cnt)[q] = make_uint4(0, 0, 0, 0);
+                __syncthreads();
                 // P2: rank of each record among its key's records (rk is dead from here on)
                 uint32_t rank[FIRE_RPT];
 #pragma unroll
@@ -1084,7 +1092,8 @@ void launch_log_fire(const LogSegDesc *segs, int nseg, int lp, int has_val, cons
                      const ResultPlan &rp, int64_t start, int64_t end, OutCols out, unsigned long long *overflow,
                      int cus, int max_per_cu, hipStream_t s) {
     if (nseg <= 0 || nseg > LOG_MAX_SEGS) return;   // nothing to fold (the host never asks; defensive)
-    static_assert(FIRE_OWN * 4 <= FIRE_RCAP * 8 && FIRE_RCAP <= 4096 && FIRE_MAXR < 16, "fire fast-path layout");
+    static_assert(FIRE_OWN * 4 <= FIRE_RCAP * 12 && FIRE_OWN == (1 << FIRE_OWN_LOG2) && FIRE_RCAP <= 4096 &&
+                      FIRE_MAXR < 16, "fire fast-path layout");
     int cl = log_fire_cap_log2(plan.nwords);
     size_t lds = (size_t)(1 + plan.nwords) * 8 << cl;
     if (lds < (size_t)FIRE_LDS) lds = FIRE_LDS;
