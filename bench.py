@@ -43,6 +43,11 @@ def parse():
     p.add_argument("--max-parallelism", type=int, default=32768)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-sample", type=int, default=2_000_000)
+    p.add_argument("--no-profile", action="store_true",
+                   help="no per-kernel HIP events in the timed region (diagnostic: the events' own cost)")
+    p.add_argument("--pipeline", action="store_true",
+                   help="pipelined submission (gwo_set_pipelined_submit): measured slower on C4, since pass 2 then "
+                        "runs after the next batch's K1 and misses its batch buffer in the MALL")
     p.add_argument("--comm-single", action="store_true",
                    help="attach a 1-rank RCCL communicator at N=1 (measures the exchange path on one GPU)")
     return p.parse_args()
@@ -108,6 +113,8 @@ def main():
     op = F.GpuWindowOperator(F.TumblingEventTimeWindows.of(a.window_ms), agg, max_parallelism=a.max_parallelism,
                              key_group_range=rng, device=local, expected_keys=exp_keys)
     h = op.handle
+    if a.pipeline:   # K1 of batch i queues before batch i-1 resolves (gwo.h gwo_set_pipelined_submit)
+        N.check(lib.gwo_set_pipelined_submit(h, 1), h)
     if world > 1:
         uid = (C.c_uint8 * N.COMM_ID_BYTES)()
         if rank == 0:
@@ -138,7 +145,7 @@ def main():
     N.check(lib.gwo_sync(h), h)
     rows_before = rows_emitted()
     lib.gwo_reset_stats(h)
-    lib.gwo_set_profiling(h, 1)
+    lib.gwo_set_profiling(h, 0 if a.no_profile else 1)
     if dist:
         dist.barrier()
     torch.cuda.synchronize()

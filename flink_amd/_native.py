@@ -88,6 +88,7 @@ SIGNATURES = [
     ("gwo_last_error", C.c_char_p, [_P]),
     ("gwo_status_string", C.c_char_p, [C.c_int]),
     ("gwo_set_profiling", C.c_int, [_P, C.c_int32]),
+    ("gwo_set_pipelined_submit", C.c_int, [_P, C.c_int32]),
     ("gwo_kernel_stats", C.c_int, [_P, C.c_int32, _I64P, C.POINTER(C.c_double), _I64P]),
     ("gwo_reset_stats", C.c_int, [_P]),
     ("gwo_assign_key_groups", C.c_int, [_P, C.c_int64, C.c_int32, C.c_int32, C.c_int32, _P, _P, C.c_int32]),
@@ -122,6 +123,8 @@ def load(path: str = LIB_PATH):
             "flink_amd has no CPU fallback.")
     lib = C.CDLL(path)
     for name, res, args in SIGNATURES:
+        if os.environ.get("GWO_LIB_PATH") and not hasattr(lib, name):
+            continue   # an older build under A/B comparison: entry points it predates stay unbound
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args

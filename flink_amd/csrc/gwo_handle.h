@@ -68,6 +68,7 @@ struct SlideState;     // gwo_slide.cpp
 struct Comm;           // gwo_comm.cpp
 struct LogState;       // gwo_log.cpp
 struct LogWindow;
+struct LogJob;
 
 struct Handle {
     static constexpr double kMaxLoad = 0.7;   // grow above this load factor
@@ -226,9 +227,15 @@ struct Handle {
     gwo_status log_carve(LogWindow &W, size_t bytes, char **out);
     void log_release(LogWindow &W);
     int log_choose_lp(uint64_t batch_records) const;
-    gwo_status log_split_chunk(long long base, int nunits, uint64_t cap, const uint64_t *counts, int tmpx, bool deferred);
+    gwo_status log_split_exact(long long base, int nunits, uint64_t cap, const uint64_t *counts, int tmpx);
+    gwo_status log_split_dev(const LogJob &J, const unsigned long long *rbp);
     gwo_status log_resolve_split();
     gwo_status insert_log(const int64_t *k, const int64_t *t, const int64_t *v, int64_t n, int64_t stride = 1);
+    gwo_status log_k1(LogJob &J, bool first_pass);
+    gwo_status log_resolve_k1(LogJob J);
+    gwo_status log_flush();                    // resolve the pipelined batch (no-op without one)
+    bool log_pending_may_fire(int64_t new_wm) const;
+    gwo_status set_pipelined(bool on);
     gwo_status fire_log(int64_t new_wm);
     gwo_status log_state_size(int64_t *entries);
     // comm (gwo_comm.cpp)

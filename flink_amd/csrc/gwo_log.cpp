@@ -29,11 +29,24 @@ struct LogWindow {
     uint64_t records = 0;
 };
 
+// One K1 launch over a window range of a batch (re-launched with a new range or capacity as needed).
+struct LogJob {
+    bool active = false;
+    const int64_t *k = nullptr, *t = nullptr, *v = nullptr;
+    int64_t n = 0, stride = 1;
+    WindowGeom g{};              // geometry + watermark at gwo_submit time (classification input)
+    long long base = 0;          // first window of the range
+    int nunits = 1;
+    uint64_t cap = 0;            // records per (window, coarse digit) region of the batch buffer
+    int slot = 0;                // batch buffer / readback slot
+    LogSegDesc desc[LOG_NU] = {}; // the range's new segments: counters/offsets carved at launch, records after
+};
+
 struct LogState {
     std::map<long long, LogWindow> wins;
     std::multimap<size_t, char *> free_chunks;
-    DevBuf tmp[2], firedesc;                     // batch buffers: K1 of batch i+1 writes the one split i is not reading
-    int tmp_cur = 0;
+    // batch buffers: one for the K1 in flight, one for the deferred pass 2, one for the next K1
+    DevBuf tmp[LOG_SLOTS], firedesc;
     // the last pass-2 launch, checked for overflow at the next sync point (deferred so the next batch's
     // K1 queues right behind it); its segments are already in the windows
     struct {
@@ -43,21 +56,25 @@ struct LogState {
         uint64_t cap = 0;
         std::vector<uint64_t> counts;
     } pend;
-    unsigned *h_split_flag = nullptr;            // pinned [2]: pass-2 overflow flag per batch buffer
+    hipEvent_t ev_split = nullptr;               // after the deferred pass 2's overflow flag readback
+    unsigned *h_split_flag = nullptr;            // pinned, device-written [LOG_SLOTS]: pass-2 overflow flags
+    unsigned *d_split_flag = nullptr;            // device view of h_split_flag
+    // pipelined submission (gwo_set_pipelined_submit): the batch whose K1 is in flight, resolved by the
+    // next call on the handle
+    bool pipeline = false;
+    LogJob job;
     // the fire in flight on fire_stream
     std::vector<long long> fire_units;
     uint64_t fire_rows0 = 0, fire_bound = 0;
     unsigned long long *h_fire_out = nullptr;    // pinned [3]: row counter, overflow, slow partitions
     unsigned long long *d_cursor = nullptr;      // [LOG_NU * 256 * LOG_CUR_STRIDE] bucket cursors of K1
-    // K1 readback, one D2H copy: [LOG_NU * 256] bucket counts, then the batch's BatchStats
-    // (log_collect_kernel copies them here and resets the cursors and stats for the next launch)
-    unsigned long long *d_rb = nullptr, *h_rb = nullptr;
-    unsigned long long *h_cursor = nullptr;      // = h_rb (counts)
-    // pass-2 plan, one H2D copy: [LOG_NU] segment descriptors, overflow word, [nb + 1] buckets
-    char *d_plan = nullptr, *h_plan = nullptr;
-    LogSegDesc *h_desc = nullptr;
-    unsigned *h_ovf = nullptr;
-    LogBucket *h_buckets = nullptr;
+    // K1 readback per slot (LOG_RB_* layout), written into pinned host memory by log_collect_kernel,
+    // which also leaves the device plan of pass 2 in d_bk (per slot) and resets cursors and stats
+    unsigned long long *h_rb = nullptr, *d_rbh = nullptr;   // host / device views
+    LogBucket *d_bk = nullptr;                   // [LOG_SLOTS][LOG_NU * 256 + 1]
+    hipEvent_t ev_rb[LOG_SLOTS] = {};
+    // host-planned pass 2 (exact re-run after an overflow): [nb + 1] buckets, one H2D copy
+    LogBucket *d_plan = nullptr, *h_buckets = nullptr;
     std::vector<LogSegDesc> h_fire;
     unsigned long long *d_overflow = nullptr;
     uint64_t last_window_keys = 0;               // distinct keys of the last fired window
@@ -65,13 +82,22 @@ struct LogState {
     long long span_hint = 1;                     // windows the previous batch spanned
     int cap_log2 = 0;
     int max_groups = 0;                          // persistent fire workgroups (2 per CU)
+
+    unsigned long long *rb(int slot) const { return h_rb + (size_t)slot * LOG_RB_WORDS; }
+    unsigned long long *rb_dev(int slot) const { return d_rbh + (size_t)slot * LOG_RB_WORDS; }
+    LogBucket *bk(int slot) const { return d_bk + (size_t)slot * (LOG_NU * 256 + 1); }
+    // a batch buffer neither the K1 in flight nor the deferred pass 2 holds
+    int free_slot() const {
+        for (int s = 0; s < LOG_SLOTS; ++s)
+            if (!(job.active && job.slot == s) && !(pend.active && pend.tmpx == s)) return s;
+        return 0;   // unreachable: LOG_SLOTS = 3 > 2 busy slots
+    }
 };
 
 static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
-static constexpr size_t kRbBytes = LOG_NU * 256 * 8 + sizeof(BatchStats);
-static constexpr size_t kPlanDescBytes = LOG_NU * sizeof(LogSegDesc);
-static constexpr size_t kPlanBytes = kPlanDescBytes + 8 + (LOG_NU * 256 + 1) * sizeof(LogBucket);
+static constexpr size_t kRbBytes = (size_t)LOG_RB_WORDS * 8;
+static constexpr size_t kPlanBytes = (LOG_NU * 256 + 1) * sizeof(LogBucket);
 
 // Capacity of a fixed-size group that receives Binomial(n, 1/k) records: mean + 6 sigma + slack.
 static uint64_t group_capacity(double mean) {
@@ -83,21 +109,26 @@ gwo_status Handle::log_init() {
     LogState &L = *logst;
     GWO_TRY(dalloc((void **)&L.d_cursor, LOG_NU * 256 * LOG_CUR_STRIDE * 8));
     GWO_TRY(hipcheck(hipMemsetAsync(L.d_cursor, 0, LOG_NU * 256 * LOG_CUR_STRIDE * 8, stream), "cursor"));
-    GWO_TRY(dalloc((void **)&L.d_rb, kRbBytes));
+    GWO_TRY(dalloc((void **)&L.d_bk, kPlanBytes * LOG_SLOTS));
     GWO_TRY(dalloc((void **)&L.d_plan, kPlanBytes));
     GWO_TRY(dalloc((void **)&L.d_overflow, 16));
     GWO_TRY(hipcheck(hipMemsetAsync(L.d_overflow, 0, 16, stream), "overflow"));
-    GWO_TRY(hipcheck(hipHostMalloc((void **)&L.h_rb, kRbBytes, hipHostMallocDefault), "pinned"));
-    GWO_TRY(hipcheck(hipHostMalloc((void **)&L.h_plan, kPlanBytes, hipHostMallocDefault), "pinned"));
-    GWO_TRY(hipcheck(hipHostMalloc((void **)&L.h_split_flag, 16, hipHostMallocDefault), "pinned"));
+    // written by kernels, read by the host after an event: coherent, mapped
+    GWO_TRY(hipcheck(hipHostMalloc((void **)&L.h_rb, kRbBytes * LOG_SLOTS, hipHostMallocCoherent | hipHostMallocMapped),
+                     "pinned"));
+    GWO_TRY(hipcheck(hipHostGetDevicePointer((void **)&L.d_rbh, L.h_rb, 0), "mapped readback"));
+    for (int i = 0; i < LOG_SLOTS; ++i)
+        GWO_TRY(hipcheck(hipEventCreateWithFlags(&L.ev_rb[i], hipEventDisableTiming), "event"));
+    GWO_TRY(hipcheck(hipEventCreateWithFlags(&L.ev_split, hipEventDisableTiming), "event"));
+    GWO_TRY(hipcheck(hipHostMalloc((void **)&L.h_buckets, kPlanBytes, hipHostMallocDefault), "pinned"));
+    GWO_TRY(hipcheck(hipHostMalloc((void **)&L.h_split_flag, 16, hipHostMallocCoherent | hipHostMallocMapped),
+                     "pinned"));
+    GWO_TRY(hipcheck(hipHostGetDevicePointer((void **)&L.d_split_flag, L.h_split_flag, 0), "mapped flag"));
+    GWO_TRY(ensure_buf(L.firedesc, 4096 * sizeof(LogSegDesc)));   // no reallocation inside a fire
     GWO_TRY(hipcheck(hipHostMalloc((void **)&L.h_fire_out, 32, hipHostMallocDefault), "pinned"));
     GWO_TRY(hipcheck(hipStreamCreateWithFlags(&fire_stream, hipStreamNonBlocking), "fire stream"));
     GWO_TRY(hipcheck(hipEventCreateWithFlags(&ev_main, hipEventDisableTiming), "event"));
     GWO_TRY(hipcheck(hipEventCreateWithFlags(&ev_fire, hipEventDisableTiming), "event"));
-    L.h_cursor = L.h_rb;
-    L.h_desc = (LogSegDesc *)L.h_plan;
-    L.h_ovf = (unsigned *)(L.h_plan + kPlanDescBytes);
-    L.h_buckets = (LogBucket *)(L.h_plan + kPlanDescBytes + 8);
     init_stats(0);   // afterwards log_collect_kernel resets the device stats after every K1
     L.cap_log2 = log_fire_cap_log2(plan.nwords);
     return GWO_OK;
@@ -109,17 +140,20 @@ void Handle::log_free() {
     for (auto &kv : L.wins)
         for (auto &c : kv.second.chunks) (void)hipFree(c.base);
     for (auto &kv : L.free_chunks) (void)hipFree(kv.second);
-    L.tmp[0].release();
-    L.tmp[1].release();
+    for (int i = 0; i < LOG_SLOTS; ++i) {
+        L.tmp[i].release();
+        if (L.ev_rb[i]) (void)hipEventDestroy(L.ev_rb[i]);
+    }
+    if (L.ev_split) (void)hipEventDestroy(L.ev_split);
     L.firedesc.release();
     if (L.h_split_flag) (void)hipHostFree(L.h_split_flag);
     if (L.h_fire_out) (void)hipHostFree(L.h_fire_out);
     if (L.d_cursor) (void)hipFree(L.d_cursor);
-    if (L.d_rb) (void)hipFree(L.d_rb);
+    if (L.d_bk) (void)hipFree(L.d_bk);
     if (L.d_plan) (void)hipFree(L.d_plan);
     if (L.d_overflow) (void)hipFree(L.d_overflow);
     if (L.h_rb) (void)hipHostFree(L.h_rb);
-    if (L.h_plan) (void)hipHostFree(L.h_plan);
+    if (L.h_buckets) (void)hipHostFree(L.h_buckets);
     delete logst;
     logst = nullptr;
 }
@@ -177,11 +211,11 @@ int Handle::log_choose_lp(uint64_t batch_records) const {
     return lp;
 }
 
-// Pass 2 for windows [base, base + nunits) of batch buffer `tmpx` (bucket counts in `counts`).
-// deferred: launch and return; the overflow flag is checked by log_resolve_split at the next sync
-// point.  Otherwise synchronous, re-running with measured capacities until nothing overflows.
-gwo_status Handle::log_split_chunk(long long base, int nunits, uint64_t cap, const uint64_t *counts, int tmpx,
-                                   bool deferred) {
+// Pass 2 planned on the host, synchronous: the exact re-run after a deferred pass 2 overflowed (skewed
+// keys).  Fresh segments for windows [base, base + nunits) of batch buffer `tmpx` (bucket counts in
+// `counts`); re-runs with each bucket's partitions sized to its measured largest one until nothing
+// overflows.
+gwo_status Handle::log_split_exact(long long base, int nunits, uint64_t cap, const uint64_t *counts, int tmpx) {
     LogState &L = *logst;
     const int W = needs_value ? 2 : 1;
     const int nb = nunits * 256;
@@ -189,21 +223,16 @@ gwo_status Handle::log_split_chunk(long long base, int nunits, uint64_t cap, con
     std::vector<uint64_t> wcount(nunits, 0);
     for (int b = 0; b < nb; ++b) wcount[b >> 8] += counts[b];
     std::vector<uint32_t> pcap_exact(nb, 0);   // after an overflow: the measured partition maximum
+    LogSegSet set{};
     while (true) {
         uint32_t chunks = 0;
         for (int w = 0; w < nunits; ++w) {
             LogSegDesc d{};
             const int c0 = w * 256;
             if (wcount[w]) {
-                long long u = base + w;
-                auto it = L.wins.find(u);
-                if (it == L.wins.end()) {
-                    LogWindow Wn;
-                    Wn.lp = log_choose_lp(wcount[w]);
-                    it = L.wins.emplace(u, std::move(Wn)).first;
-                }
-                wins[w] = &it->second;
-                const int lp = it->second.lp, F = 1 << (lp - 8);
+                LogWindow &Wn = L.wins[base + w];   // exists: created when K1 was launched over it
+                wins[w] = &Wn;
+                const int lp = Wn.lp, F = 1 << (lp - 8);
                 uint64_t seg = 0;
                 for (int dgt = 0; dgt < 256; ++dgt) {
                     const uint64_t n_b = counts[c0 + dgt];
@@ -219,11 +248,11 @@ gwo_status Handle::log_split_chunk(long long base, int nunits, uint64_t cap, con
                 }
                 if (seg >= (1ull << 32)) return poison(GWO_ERR_CAPACITY, "log layout: batch segment exceeds 2^32 records");
                 char *p = nullptr;
-                GWO_TRY(log_carve(it->second, seg * W * 8, &p));
+                GWO_TRY(log_carve(Wn, seg * W * 8, &p));
                 d.rec = (int64_t *)p;
-                GWO_TRY(log_carve(it->second, ((size_t)1 << lp) * 4, &p));
+                GWO_TRY(log_carve(Wn, ((size_t)1 << lp) * 4, &p));
                 d.off = (uint32_t *)p;
-                GWO_TRY(log_carve(it->second, ((size_t)1 << lp) * 4, &p));
+                GWO_TRY(log_carve(Wn, ((size_t)1 << lp) * 4, &p));
                 d.cnt = (uint32_t *)p;
                 d.lp = lp;
                 GWO_TRY(hipcheck(hipMemsetAsync(d.cnt, 0, ((size_t)1 << lp) * 4, stream), "segment counts"));
@@ -234,42 +263,25 @@ gwo_status Handle::log_split_chunk(long long base, int nunits, uint64_t cap, con
                     B.chunk0 = chunks;
                 }
             }
-            L.h_desc[w] = d;
+            set.s[w] = d;
         }
         L.h_buckets[nb] = LogBucket{};
         L.h_buckets[nb].chunk0 = chunks;
-        *L.h_ovf = 0;
-        GWO_TRY(hipcheck(hipMemcpyAsync(L.d_plan, L.h_plan, kPlanDescBytes + 8 + (nb + 1) * sizeof(LogBucket),
-                                        hipMemcpyHostToDevice, stream), "split plan"));
-        unsigned *d_ovf = (unsigned *)(L.d_plan + kPlanDescBytes);
-        prof_begin(GWO_KERNEL_PARTITION);
-        launch_log_split((const int64_t *)L.tmp[tmpx].ptr, needs_value,
-                         (const LogBucket *)(L.d_plan + kPlanDescBytes + 8), nb, nunits, (const LogSegDesc *)L.d_plan,
-                         d_ovf, chunks, stream);
+        L.h_split_flag[tmpx] = 0;
+        GWO_TRY(hipcheck(hipMemcpyAsync(L.d_plan, L.h_buckets, (nb + 1) * sizeof(LogBucket), hipMemcpyHostToDevice, stream),
+                         "split plan"));
+        launch_log_split((const int64_t *)L.tmp[tmpx].ptr, needs_value, L.d_plan, nb, set, L.d_split_flag + tmpx, chunks,
+                         stream);
         GWO_TRY(launch_ok("log split"));
-        uint64_t total = 0;
-        for (int w = 0; w < nunits; ++w) total += wcount[w];
-        prof_end(GWO_KERNEL_PARTITION, (int64_t)total);
-        GWO_TRY(hipcheck(hipMemcpyAsync(&L.h_split_flag[tmpx], d_ovf, 4, hipMemcpyDeviceToHost, stream), "split flag"));
-        if (deferred) {
-            L.pend.active = true;
-            L.pend.tmpx = tmpx;
-            L.pend.nunits = nunits;
-            L.pend.base = base;
-            L.pend.cap = cap;
-            L.pend.counts.assign(counts, counts + nb);
-            break;
-        }
         GWO_TRY(hipcheck(hipStreamSynchronize(stream), "log split"));
         if (L.h_split_flag[tmpx] == 0) break;
-        // a partition received more than its capacity (skewed keys): the cursors hold the exact
-        // counts, so redo with each bucket's partitions sized to its largest one (the segments
-        // carved above stay unused until the window is released)
+        // the cursors hold the exact counts: redo with each bucket's partitions sized to its largest one
+        // (the segments carved above stay unused until the window is released)
         for (int w = 0; w < nunits; ++w) {
             if (!wins[w]) continue;
-            const int F = 1 << (L.h_desc[w].lp - 8);
+            const int F = 1 << (set.s[w].lp - 8);
             std::vector<uint32_t> cnt((size_t)256 * F);
-            GWO_TRY(hipcheck(hipMemcpy(cnt.data(), L.h_desc[w].cnt, cnt.size() * 4, hipMemcpyDeviceToHost), "counts"));
+            GWO_TRY(hipcheck(hipMemcpy(cnt.data(), set.s[w].cnt, cnt.size() * 4, hipMemcpyDeviceToHost), "counts"));
             for (int dgt = 0; dgt < 256; ++dgt)
                 for (int f = 0; f < F; ++f)
                     pcap_exact[w * 256 + dgt] = std::max(pcap_exact[w * 256 + dgt], cnt[(size_t)dgt * F + f]);
@@ -277,18 +289,60 @@ gwo_status Handle::log_split_chunk(long long base, int nunits, uint64_t cap, con
     }
     for (int w = 0; w < nunits; ++w) {
         if (!wins[w]) continue;
-        wins[w]->segs.push_back(L.h_desc[w]);
+        wins[w]->segs.push_back(set.s[w]);
         wins[w]->records += wcount[w];
     }
     return GWO_OK;
 }
 
+// Pass 2 of job J from the device plan log_collect_kernel left in bk(J.slot): carve each window's segment
+// records (sizes from the readback), launch, and return; the overflow flag is checked by
+// log_resolve_split at the next sync point.
+gwo_status Handle::log_split_dev(const LogJob &J, const unsigned long long *rbp) {
+    LogState &L = *logst;
+    const int W = needs_value ? 2 : 1;
+    LogSegSet set{};
+    uint64_t wcount[LOG_NU] = {}, total = 0;
+    for (int b = 0; b < J.nunits * 256; ++b) wcount[b >> 8] += rbp[b];
+    for (int w = 0; w < J.nunits; ++w) {
+        set.s[w] = J.desc[w];
+        if (!wcount[w]) continue;
+        const uint64_t seg = rbp[LOG_RB_SEG + w];
+        if (seg >= (1ull << 32)) return poison(GWO_ERR_CAPACITY, "log layout: batch segment exceeds 2^32 records");
+        char *p = nullptr;
+        GWO_TRY(log_carve(L.wins[J.base + w], seg * W * 8, &p));
+        set.s[w].rec = (int64_t *)p;
+        total += wcount[w];
+    }
+    L.h_split_flag[J.slot] = 0;
+    prof_begin(GWO_KERNEL_PARTITION);
+    launch_log_split((const int64_t *)L.tmp[J.slot].ptr, needs_value, L.bk(J.slot), J.nunits * 256, set,
+                     L.d_split_flag + J.slot, (uint32_t)rbp[LOG_RB_CHUNKS], stream);
+    GWO_TRY(launch_ok("log split"));
+    prof_end(GWO_KERNEL_PARTITION, (int64_t)total);
+    GWO_TRY(hipcheck(hipEventRecord(L.ev_split, stream), "event"));
+    L.pend.active = true;
+    L.pend.tmpx = J.slot;
+    L.pend.nunits = J.nunits;
+    L.pend.base = J.base;
+    L.pend.cap = J.cap;
+    L.pend.counts.assign(rbp, rbp + J.nunits * 256);
+    for (int w = 0; w < J.nunits; ++w) {
+        if (!wcount[w]) continue;
+        LogWindow &Wn = L.wins[J.base + w];
+        Wn.segs.push_back(set.s[w]);
+        Wn.records += wcount[w];
+    }
+    return GWO_OK;
+}
+
 // Checks the deferred pass 2: on overflow, its segments come out of their windows and pass 2 re-runs
-// synchronously on the same batch buffer (which the next K1 did not touch).
+// synchronously on the same batch buffer (which no later K1 touched).
 gwo_status Handle::log_resolve_split() {
     LogState &L = *logst;
     if (!L.pend.active) return GWO_OK;
-    GWO_TRY(hipcheck(hipStreamSynchronize(stream), "pass 2"));
+    // the event, not the stream: a pipelined K1 may be queued behind this pass 2
+    GWO_TRY(hipcheck(hipEventSynchronize(L.ev_split), "pass 2"));
     L.pend.active = false;
     if (L.h_split_flag[L.pend.tmpx] == 0) return GWO_OK;
     for (int w = 0; w < L.pend.nunits; ++w) {
@@ -300,38 +354,70 @@ gwo_status Handle::log_resolve_split() {
         Wn.records -= c;
     }
     std::vector<uint64_t> counts = L.pend.counts;
-    return log_split_chunk(L.pend.base, L.pend.nunits, L.pend.cap, counts.data(), L.pend.tmpx, false);
+    return log_split_exact(L.pend.base, L.pend.nunits, L.pend.cap, counts.data(), L.pend.tmpx);
 }
 
-gwo_status Handle::insert_log(const int64_t *k, const int64_t *t, const int64_t *v, int64_t n, int64_t stride) {
+// K1 of job J (one window range of a batch) into batch buffer J.slot, then the collect kernel and one
+// readback of its bucket counts and statistics; ev_rb[J.slot] marks the readback's completion.
+gwo_status Handle::log_k1(LogJob &J, bool first_pass) {
     LogState &L = *logst;
-    WindowGeom g = geom_now();
-    BatchStats &hs = *h_stats;
     const int W = needs_value ? 2 : 1;
-    long long base = hist_hint;
-    int nunits = (int)std::min<long long>(LOG_NU, std::max<long long>(1, L.span_hint));
-    uint64_t cap = group_capacity((double)n / 256.0);
+    // the range's windows and their new segments' offsets/counters (zeroed by the collect kernel)
+    CollectArgs ca{};
+    ca.nunits = J.nunits;
+    ca.cap = J.cap;
+    ca.bk = L.bk(J.slot);
+    ca.rb = L.rb_dev(J.slot);
+    for (int w = 0; w < J.nunits; ++w) {
+        auto it = L.wins.find(J.base + w);
+        if (it == L.wins.end()) {
+            LogWindow Wn;
+            Wn.lp = log_choose_lp((uint64_t)J.n);
+            it = L.wins.emplace(J.base + w, std::move(Wn)).first;
+        }
+        const int lp = it->second.lp;
+        char *p = nullptr;
+        LogSegDesc d{};
+        GWO_TRY(log_carve(it->second, ((size_t)1 << lp) * 4, &p));
+        d.off = (uint32_t *)p;
+        GWO_TRY(log_carve(it->second, ((size_t)1 << lp) * 4, &p));
+        d.cnt = (uint32_t *)p;
+        d.lp = lp;
+        J.desc[w] = d;
+        ca.lp[w] = lp;
+        ca.cnt[w] = d.cnt;
+    }
+    DevBuf &tmp = L.tmp[J.slot];
+    if (tmp.bytes < (size_t)J.nunits * 256 * J.cap * W * 8) {
+        GWO_TRY(log_resolve_split());   // ensure_buf may free: nothing may still read it
+        GWO_TRY(ensure_buf(tmp, (size_t)J.nunits * 256 * J.cap * W * 8));
+    }
+    const bool side = first_pass && side_enabled();
+    prof_begin(GWO_KERNEL_INSERT);
+    launch_log_part(J.k, J.t, J.v, J.n, J.stride, J.g, J.base, J.nunits, needs_value, L.d_cursor, J.cap,
+                    (int64_t *)tmp.ptr, d_stats, (int64_t *)side_key.ptr, (int64_t *)side_ts.ptr,
+                    (int64_t *)side_val.ptr, d_side_count, side ? side_cap : 0, side, stream);
+    GWO_TRY(launch_ok("log partition"));
+    prof_end(GWO_KERNEL_INSERT, J.n);
+    launch_log_collect(L.d_cursor, d_stats, ca, stream);
+    GWO_TRY(launch_ok("log collect"));
+    if (side) GWO_TRY(hipcheck(hipMemcpyAsync(h_scalar, d_side_count, 8, hipMemcpyDeviceToHost, stream), "side count"));
+    return hipcheck(hipEventRecord(L.ev_rb[J.slot], stream), "event");
+}
+
+// Completes a batch whose first K1 is queued: waits for its readback, rejects the batch on a
+// classification error (before any window state changes), re-runs K1 when the window range guess or a
+// region capacity was wrong, and launches pass 2 (deferred) for each window range.
+gwo_status Handle::log_resolve_k1(LogJob J) {
+    LogState &L = *logst;
+    BatchStats &hs = *h_stats;
     bool first_pass = true;
     long long lo = 0, hi = -1;
     while (true) {
-        DevBuf &tmp = L.tmp[L.tmp_cur];
-        if (tmp.bytes < (size_t)nunits * 256 * cap * W * 8) {
-            GWO_TRY(log_resolve_split());   // ensure_buf may free: nothing may still read it
-            GWO_TRY(ensure_buf(tmp, (size_t)nunits * 256 * cap * W * 8));
-        }
-        prof_begin(GWO_KERNEL_INSERT);
-        launch_log_part(k, t, v, n, stride, g, base, nunits, needs_value, L.d_cursor, cap, (int64_t *)tmp.ptr, d_stats,
-                        (int64_t *)side_key.ptr, (int64_t *)side_ts.ptr, (int64_t *)side_val.ptr, d_side_count,
-                        first_pass && side_enabled() ? side_cap : 0, first_pass && side_enabled(), stream);
-        GWO_TRY(launch_ok("log partition"));
-        prof_end(GWO_KERNEL_INSERT, n);
-        launch_log_collect(L.d_cursor, nunits * 256, d_stats, L.d_rb, stream);
-        GWO_TRY(hipcheck(hipMemcpyAsync(L.h_rb, L.d_rb, kRbBytes, hipMemcpyDeviceToHost, stream), "readback"));
-        if (first_pass && side_enabled())
-            GWO_TRY(hipcheck(hipMemcpyAsync(h_scalar, d_side_count, 8, hipMemcpyDeviceToHost, stream), "side count"));
-        GWO_TRY(hipcheck(hipStreamSynchronize(stream), "log partition sync"));
-        memcpy(h_stats, L.h_rb + LOG_NU * 256, sizeof(BatchStats));
-        GWO_TRY(log_resolve_split());   // the previous pass 2 has completed (stream order)
+        GWO_TRY(hipcheck(hipEventSynchronize(L.ev_rb[J.slot]), "log partition sync"));
+        const unsigned long long *rbp = L.rb(J.slot);
+        memcpy(h_stats, rbp + LOG_RB_STATS, sizeof(BatchStats));
+        GWO_TRY(log_resolve_split());   // the previous pass 2 (also frees its plan staging for reuse)
         if (first_pass) {
             if (hs.bad_ts) return poison(GWO_ERR_NO_TIMESTAMP,
                                          "Record has Long.MIN_VALUE timestamp (= no timestamp marker). Is the time "
@@ -352,6 +438,7 @@ gwo_status Handle::insert_log(const int64_t *k, const int64_t *t, const int64_t 
                     *h_scalar = side_rows;
                     GWO_TRY(hipcheck(hipMemcpyAsync(d_side_count, h_scalar, 8, hipMemcpyHostToDevice, stream), "side reset"));
                     GWO_TRY(hipcheck(hipStreamSynchronize(stream), "side reset sync"));
+                    GWO_TRY(log_k1(J, true));
                     continue;
                 }
                 side_rows_committed = side_rows;
@@ -362,28 +449,83 @@ gwo_status Handle::insert_log(const int64_t *k, const int64_t *t, const int64_t 
             lo = hs.min_idx;
             hi = hs.max_idx;
             first_pass = false;
-            if (base > lo || base + nunits <= lo) {   // wrong window range guess: redo from the first window
-                base = lo;
-                nunits = (int)std::min<long long>(LOG_NU, hi - lo + 1);
+            if (J.base > lo || J.base + J.nunits <= lo) {   // wrong window range guess: redo from the first window
+                J.base = lo;
+                J.nunits = (int)std::min<long long>(LOG_NU, hi - lo + 1);
+                GWO_TRY(log_k1(J, false));
                 continue;
             }
         }
         uint64_t maxc = 0;
-        for (int b = 0; b < nunits * 256; ++b) maxc = std::max<uint64_t>(maxc, L.h_cursor[b]);
-        if (maxc > cap) {   // a bucket overflowed its capacity (skewed keys): redo this range exactly
-            cap = maxc;
+        for (int b = 0; b < J.nunits * 256; ++b) maxc = std::max<uint64_t>(maxc, rbp[b]);
+        if (maxc > J.cap) {   // a bucket overflowed its capacity (skewed keys): redo this range exactly
+            J.cap = maxc;
+            GWO_TRY(log_k1(J, false));
             continue;
         }
-        GWO_TRY(log_split_chunk(base, nunits, cap, (const uint64_t *)L.h_cursor, L.tmp_cur, true));
-        L.tmp_cur ^= 1;
-        const long long chunk_hi = base + nunits - 1;
+        GWO_TRY(log_split_dev(J, rbp));
+        const long long chunk_hi = J.base + J.nunits - 1;
         if (chunk_hi >= hi) break;
-        base = chunk_hi + 1;
-        nunits = (int)std::min<long long>(LOG_NU, hi - base + 1);
+        J.base = chunk_hi + 1;
+        J.nunits = (int)std::min<long long>(LOG_NU, hi - J.base + 1);
+        J.slot = L.free_slot();
+        GWO_TRY(log_k1(J, false));
     }
     hist_hint = lo;
     L.span_hint = hi - lo + 2;
     return GWO_OK;
+}
+
+// Resolves the pipelined batch, if any (every call that observes state or fires windows comes here first).
+gwo_status Handle::log_flush() {
+    if (!logst || !logst->job.active) return GWO_OK;
+    LogJob J = logst->job;
+    logst->job.active = false;
+    return log_resolve_k1(J);
+}
+
+gwo_status Handle::insert_log(const int64_t *k, const int64_t *t, const int64_t *v, int64_t n, int64_t stride) {
+    LogState &L = *logst;
+    LogJob J;
+    J.k = k;
+    J.t = t;
+    J.v = v;
+    J.n = n;
+    J.stride = stride;
+    J.g = geom_now();
+    J.base = hist_hint;
+    J.nunits = (int)std::min<long long>(LOG_NU, std::max<long long>(1, L.span_hint));
+    J.cap = group_capacity((double)n / 256.0);
+    // Pipelined: this batch's K1 is queued before the previous batch is resolved, so the host's wait,
+    // checks and pass-2 planning overlap a running K1.  Only for caller-owned device columns (borrowed
+    // until the next call returns, gwo.h) -- staged host input and received exchange buffers are reused
+    // by the next batch -- and without a side output (K1 appends to it on the first pass).
+    const bool pipe = L.pipeline && stride == 1 && !side_enabled() && !comm && (const void *)k != stage_key.ptr &&
+                      (const void *)t != stage_ts.ptr && (!v || (const void *)v != stage_val.ptr);
+    if (L.job.active && !pipe) GWO_TRY(log_flush());
+    J.slot = L.free_slot();
+    GWO_TRY(log_k1(J, true));
+    if (!pipe) return log_resolve_k1(J);
+    LogJob prev = L.job;
+    L.job = J;
+    L.job.active = true;
+    if (!prev.active) return GWO_OK;
+    gwo_status s = log_resolve_k1(prev);
+    // a window range guess taken before the previous batch resolved is refreshed for the next launch
+    return s;
+}
+
+// A pipelined batch may hold records of a window this watermark fires: any accepted record has
+// end - 1 > (watermark at its K1), so that needs a window end in (that watermark, new_wm].
+bool Handle::log_pending_may_fire(int64_t new_wm) const {
+    const LogState &L = *logst;
+    if (!L.job.active) return false;
+    const __int128 w0 = (__int128)L.job.g.wm + 1;
+    const __int128 size = cfg.size, off = geom.unit_off_mod;
+    __int128 q = (w0 - off) / size;
+    if ((w0 - off) % size < 0) q -= 1;                  // floor division
+    const __int128 end_m1 = q * size + off + size - 1;  // max timestamp of the window holding w0
+    return end_m1 <= (__int128)new_wm;
 }
 
 // Launches the fold of every window whose end the watermark passed (EventTimeTrigger.onEventTime FIRE,
@@ -402,6 +544,7 @@ gwo_status Handle::fire_log(int64_t new_wm) {
             out.push_back(kv.first);
         }
     };
+    if (log_pending_may_fire(new_wm)) GWO_TRY(log_flush());
     std::vector<long long> fire;
     due(fire);
     if (fire.empty()) return GWO_OK;
@@ -410,6 +553,7 @@ gwo_status Handle::fire_log(int64_t new_wm) {
     due(fire);
     for (auto it = fire.begin(); it != fire.end();) {   // a window with no segment has nothing to emit
         if (L.wins[*it].segs.empty()) {
+            log_release(L.wins[*it]);   // offsets/counters carved for a K1 range that got no records
             L.wins.erase(*it);
             it = fire.erase(it);
         } else {
@@ -447,24 +591,28 @@ gwo_status Handle::fire_log(int64_t new_wm) {
     L.fire_rows0 = out_rows;
     L.fire_bound = bound;
     L.fire_units = fire;
-    GWO_TRY(hipcheck(hipEventRecord(ev_main, stream), "event"));   // segments, descriptors, row counter
-    GWO_TRY(hipcheck(hipStreamWaitEvent(fire_stream, ev_main, 0), "event wait"));
+    // synchronous fire: on the handle's stream (no cross-stream event); asynchronous: on fire_stream
+    hipStream_t fs = async_fire ? fire_stream : stream;
+    if (async_fire) {
+        GWO_TRY(hipcheck(hipEventRecord(ev_main, stream), "event"));   // segments, descriptors, row counter
+        GWO_TRY(hipcheck(hipStreamWaitEvent(fire_stream, ev_main, 0), "event wait"));
+    }
     OutCols o = out_cols();
     size_t at = 0;
     for (long long u : fire) {
         LogWindow &W = L.wins[u];
         int64_t start = unit_start(u);
         int64_t end = (int64_t)((uint64_t)start + (uint64_t)cfg.size);
-        prof_begin(GWO_KERNEL_FIRE, fire_stream);
+        prof_begin(GWO_KERNEL_FIRE, fs);
         launch_log_fire((const LogSegDesc *)L.firedesc.ptr + at, (int)W.segs.size(), W.lp, needs_value, plan, rplan,
-                        start, end, o, L.d_overflow, L.max_groups, async_fire ? 1 : 2, fire_stream);
+                        start, end, o, L.d_overflow, L.max_groups, async_fire ? 1 : 2, fs);
         GWO_TRY(launch_ok("log fire"));
-        prof_end(GWO_KERNEL_FIRE, (int64_t)W.records, fire_stream);
+        prof_end(GWO_KERNEL_FIRE, (int64_t)W.records, fs);
         at += W.segs.size();
     }
-    GWO_TRY(hipcheck(hipMemcpyAsync(L.h_fire_out, d_out_count, 8, hipMemcpyDeviceToHost, fire_stream), "out count"));
-    GWO_TRY(hipcheck(hipMemcpyAsync(L.h_fire_out + 1, L.d_overflow, 16, hipMemcpyDeviceToHost, fire_stream), "overflow"));
-    GWO_TRY(hipcheck(hipEventRecord(ev_fire, fire_stream), "event"));
+    GWO_TRY(hipcheck(hipMemcpyAsync(L.h_fire_out, d_out_count, 8, hipMemcpyDeviceToHost, fs), "out count"));
+    GWO_TRY(hipcheck(hipMemcpyAsync(L.h_fire_out + 1, L.d_overflow, 16, hipMemcpyDeviceToHost, fs), "overflow"));
+    GWO_TRY(hipcheck(hipEventRecord(ev_fire, fs), "event"));
     fire_pending = true;
     // Measured on MI355X (C4): letting the fire overlap the next batches is slower -- beside a 1-per-CU
     // fire the partition kernel loses its occupancy (0.36 vs 0.26 ms) and the fire takes 4.9 vs 2.9 ms;
@@ -528,7 +676,15 @@ gwo_status Handle::finish_fire() {
     return GWO_OK;
 }
 
+gwo_status Handle::set_pipelined(bool on) {
+    if (!logst) return GWO_OK;   // other layouts resolve every batch inside gwo_submit
+    if (!on) GWO_TRY(log_flush());
+    logst->pipeline = on;
+    return GWO_OK;
+}
+
 gwo_status Handle::log_state_size(int64_t *entries) {
+    GWO_TRY(log_flush());
     uint64_t s = 0;
     for (auto &kv : logst->wins) s += kv.second.records;
     *entries = (int64_t)s;

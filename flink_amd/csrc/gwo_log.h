@@ -5,6 +5,7 @@
 #include "gwo_internal.h"
 
 #define LOG_NU 4                 // windows one partition launch (K1) covers
+#define LOG_SLOTS 3              // batch buffers: K1 in flight (pipelined), deferred pass 2, next K1
 #define LOG_K1_PER 14            // K1 tile: 256 threads x 14 records
 #define LOG_K1_THREADS 256
 #define LOG_TILE_PER 7            // pass-2 chunk: 512 threads x 7 records
@@ -42,6 +43,27 @@ struct LogBucket {
     uint32_t chunk0;             // first pass-2 workgroup of the bucket (prefix over buckets)
 };
 
+// The segment descriptors of one pass-2 launch (kernel argument).
+struct LogSegSet {
+    LogSegDesc s[LOG_NU];
+};
+
+// K1 readback block (host-visible, written by log_collect_kernel): [LOG_NU * 256] bucket counts, the
+// BatchStats words, [LOG_NU] segment sizes (records) of the device plan, and its pass-2 workgroup count.
+static constexpr int LOG_RB_STATS = LOG_NU * 256;
+static constexpr int LOG_RB_SEG = LOG_RB_STATS + (int)((sizeof(BatchStats) + 7) / 8);
+static constexpr int LOG_RB_CHUNKS = LOG_RB_SEG + LOG_NU;
+static constexpr int LOG_RB_WORDS = LOG_RB_CHUNKS + 1;
+
+struct CollectArgs {
+    int nunits;
+    int lp[LOG_NU];              // partition bits of each window of the launch
+    uint32_t *cnt[LOG_NU];       // the windows' new segment counters (zeroed here)
+    uint64_t cap;                // bucket region capacity of the batch buffer
+    LogBucket *bk;               // out: [nunits * 256 + 1] pass-2 plan (device)
+    unsigned long long *rb;      // out: readback block (pinned host memory)
+};
+
 namespace gwo {
 // K1: classify + key-group check + late accounting + (window, coarse digit) grouping of a batch.
 // key/ts/val columns with `stride` int64 words between records (1: SoA columns; 3: {key, ts, value} records)
@@ -50,12 +72,13 @@ void launch_log_part(const int64_t *key, const int64_t *ts, const int64_t *val, 
                      long long base, int nunits, int has_val, unsigned long long *cursor, uint64_t cap,
                      int64_t *tmp, BatchStats *st, int64_t *side_key, int64_t *side_ts, int64_t *side_val,
                      unsigned long long *side_count, long long side_cap, int side_enabled, hipStream_t s);
-// Pass 2: every coarse bucket -> its window's segment, grouped by partition.
-// After K1: rb[b] = cursor[b * LOG_CUR_STRIDE] (b < nb) and rb[LOG_NU * 256 ...] = *stats; then resets the
-// cursors and the stats for the next K1 launch.
-void launch_log_collect(unsigned long long *cursor, int nb, BatchStats *stats, unsigned long long *rb, hipStream_t s);
-void launch_log_split(const int64_t *tmp, int has_val, const LogBucket *buckets, int nb, int nunits,
-                      const LogSegDesc *segs, unsigned *overflow, uint32_t nchunks, hipStream_t s);
+// After K1: readback block + device plan of pass 2 + zeroed segment counters (see CollectArgs); resets
+// the cursors and the stats for the next K1 launch.
+void launch_log_collect(unsigned long long *cursor, BatchStats *stats, const CollectArgs &a, hipStream_t s);
+// Pass 2: every coarse bucket -> its window's segment, grouped by partition.  `overflow` is a
+// host-visible flag (set to 1 when a partition exceeds its capacity).
+void launch_log_split(const int64_t *tmp, int has_val, const LogBucket *buckets, int nb, const LogSegSet &segs,
+                      unsigned *overflow, uint32_t nchunks, hipStream_t s);
 int log_fire_cap_log2(int nwords);
 void launch_log_fire(const LogSegDesc *segs, int nseg, int lp, int has_val, const AccPlan &plan,
                      const ResultPlan &rp, int64_t start, int64_t end, OutCols out, unsigned long long *overflow,

@@ -245,7 +245,7 @@ __global__ __launch_bounds__(LOG_K1_THREADS) void log_part_kernel(
 template <bool HASV>
 __global__ __launch_bounds__(LOG_TILE_THREADS) void log_split_kernel(const int64_t *__restrict__ tmp,
                                                                      const LogBucket *__restrict__ bk, int nb,
-                                                                     const LogSegDesc *__restrict__ segs,
+                                                                     const LogSegSet segs,
                                                                      unsigned *overflow) {
     constexpr int W = HASV ? 2 : 1;
     __shared__ __attribute__((aligned(16))) int64_t s_rec[LOG_TILE * W];
@@ -272,7 +272,7 @@ __global__ __launch_bounds__(LOG_TILE_THREADS) void log_split_kernel(const int64
     const LogBucket B = bk[c];
     const uint32_t chunk = blockIdx.x - B.chunk0;
     const int w = c >> 8, d = c & 255;
-    const LogSegDesc S = segs[w];
+    const LogSegDesc S = segs.s[w];
     const int lp = S.lp, fb = lp - 8, F = 1 << fb;
     if (chunk == 0)
         for (int f = tid; f < F; f += LOG_TILE_THREADS) S.off[d * F + f] = B.seg_base + (uint32_t)f * B.pcap;
@@ -315,7 +315,7 @@ __global__ __launch_bounds__(LOG_TILE_THREADS) void log_split_kernel(const int64
         int f = tid * per + q;
         if (q < per && f < F && loc[q]) {
             uint32_t at = atomicAdd(&S.cnt[d * F + f], loc[q]);
-            if (at + loc[q] > B.pcap) atomicOr(overflow, 1u);
+            if (at + loc[q] > B.pcap) *(volatile unsigned *)overflow = 1u;   // host-visible flag, plain store
             s_cnt[f] = at;
         }
     }
@@ -1042,35 +1042,92 @@ void launch_log_part(const int64_t *key, const int64_t *ts, const int64_t *val, 
 #undef GWO_K1
 }
 
-__global__ __launch_bounds__(1024) void log_collect_kernel(unsigned long long *cursor, int nb, BatchStats *st,
-                                                          unsigned long long *rb) {
+// After K1: block 0 moves the bucket counts and the batch statistics into the host-visible readback
+// block (resetting the cursors and statistics for the next K1) and plans pass 2 on the device -- per
+// bucket the partition capacity (mean + 6 sigma + 4 of a Binomial(n_b, 1/F) partition, the same
+// formula as the host's group_capacity), the bucket's first record in its window's segment and its
+// first pass-2 workgroup -- writing the segment size of each window and the workgroup total into the
+// readback.  Blocks 1.. zero the segments' partition counters (pass 2's cursors).
+__global__ __launch_bounds__(1024) void log_collect_kernel(unsigned long long *cursor, BatchStats *st, CollectArgs a) {
+    if (blockIdx.x > 0) {   // zero the counters of every window of the launch
+        const int zb = blockIdx.x - 1, nzb = gridDim.x - 1;
+        for (int w = 0; w < a.nunits; ++w) {
+            uint4 *c4 = (uint4 *)a.cnt[w];
+            const uint32_t n4 = (1u << a.lp[w]) / 4;
+            for (uint32_t i = zb * blockDim.x + threadIdx.x; i < n4; i += nzb * blockDim.x) c4[i] = make_uint4(0, 0, 0, 0);
+        }
+        return;
+    }
     constexpr int SW = (int)(sizeof(BatchStats) / 8);
+    __shared__ uint64_t s_seg[1024];
+    __shared__ uint32_t s_chk[1024];
     unsigned long long *sw = (unsigned long long *)st;
-    for (int b = threadIdx.x; b < nb; b += blockDim.x) {
-        rb[b] = cursor[(size_t)b * LOG_CUR_STRIDE];
+    const int nb = a.nunits * 256, b = threadIdx.x;
+    unsigned long long n_b = 0;
+    uint32_t pcap = 0, chunks = 0;
+    uint64_t seg = 0;
+    if (b < nb) {
+        n_b = cursor[(size_t)b * LOG_CUR_STRIDE];
         cursor[(size_t)b * LOG_CUR_STRIDE] = 0;
+        a.rb[b] = n_b;
+        if (n_b) {
+            const int F = 1 << (a.lp[b >> 8] - 8);
+            const double mean = (double)n_b / (double)F;
+            pcap = (uint32_t)ceil(__dadd_rn(__dadd_rn(mean, __dmul_rn(6.0, sqrt(mean))), 4.0));
+            seg = (uint64_t)F * pcap;
+            chunks = (uint32_t)((n_b + LOG_TILE - 1) / LOG_TILE);
+        }
     }
+    s_seg[b] = seg;
+    s_chk[b] = chunks;
     unsigned long long w = 0;
-    if (threadIdx.x < SW) {
-        w = sw[threadIdx.x];
-        rb[LOG_NU * 256 + threadIdx.x] = w;
+    if (b < SW) {
+        w = sw[b];
+        a.rb[LOG_NU * 256 + b] = w;
     }
     __syncthreads();
-    if (threadIdx.x < SW) sw[threadIdx.x] = 0;
-    __syncthreads();
-    if (threadIdx.x == 0) {
+    if (b < SW) sw[b] = 0;
+    // inclusive scans (Hillis-Steele): segment records within each window's 256 buckets, chunks overall
+    for (int off = 1; off < 1024; off <<= 1) {
+        uint64_t xs = 0;
+        uint32_t xc = 0;
+        if (b >= off) {
+            xc = s_chk[b - off];
+            if ((b & 255) >= off) xs = s_seg[b - off];
+        }
+        __syncthreads();
+        s_seg[b] += xs;
+        s_chk[b] += xc;
+        __syncthreads();
+    }
+    if (b == 0) {
         st->min_idx = 0x7fffffffffffffffLL;
         st->max_idx = (long long)0x8000000000000000LL;
     }
+    if (b < nb) {
+        LogBucket B;
+        B.src = (uint64_t)b * a.cap;
+        B.n = (uint32_t)n_b;
+        B.pcap = pcap;
+        B.seg_base = (uint32_t)(s_seg[b] - seg);
+        B.chunk0 = s_chk[b] - chunks;
+        a.bk[b] = B;
+        if ((b & 255) == 255) a.rb[LOG_RB_SEG + (b >> 8)] = s_seg[b];
+        if (b == nb - 1) {
+            LogBucket E{};
+            E.chunk0 = s_chk[b];
+            a.bk[nb] = E;
+            a.rb[LOG_RB_CHUNKS] = s_chk[b];
+        }
+    }
 }
 
-void launch_log_collect(unsigned long long *cursor, int nb, BatchStats *stats, unsigned long long *rb, hipStream_t s) {
-    hipLaunchKernelGGL(log_collect_kernel, dim3(1), dim3(1024), 0, s, cursor, nb, stats, rb);
+void launch_log_collect(unsigned long long *cursor, BatchStats *stats, const CollectArgs &a, hipStream_t s) {
+    hipLaunchKernelGGL(log_collect_kernel, dim3(1 + 32), dim3(1024), 0, s, cursor, stats, a);
 }
 
-void launch_log_split(const int64_t *tmp, int has_val, const LogBucket *buckets, int nb, int nunits,
-                      const LogSegDesc *segs, unsigned *overflow, uint32_t nchunks, hipStream_t s) {
-    (void)nunits;
+void launch_log_split(const int64_t *tmp, int has_val, const LogBucket *buckets, int nb, const LogSegSet &segs,
+                      unsigned *overflow, uint32_t nchunks, hipStream_t s) {
     if (nchunks == 0) return;
     if (has_val)
         hipLaunchKernelGGL(log_split_kernel<true>, dim3(nchunks), dim3(LOG_TILE_THREADS), 0, s, tmp, buckets, nb, segs,

@@ -650,6 +650,7 @@ gwo_status gwo_result_dtype(const gwo_handle *hh, int32_t agg, int32_t *dtype) {
 gwo_status gwo_late_dropped(gwo_handle *hh, int64_t *count) {
     H_OR_FAIL;
     if (!count) return GWO_ERR_INVALID_ARGUMENT;
+    GWO_TRY(h->log_flush());
     *count = (int64_t)h->late_dropped;
     return GWO_OK;
 }
@@ -657,6 +658,7 @@ gwo_status gwo_late_dropped(gwo_handle *hh, int64_t *count) {
 gwo_status gwo_side_output_count(gwo_handle *hh, int64_t *n) {
     H_OR_FAIL;
     if (!n) return GWO_ERR_INVALID_ARGUMENT;
+    GWO_TRY(h->log_flush());
     *n = (int64_t)h->side_rows_committed;
     return GWO_OK;
 }
@@ -664,6 +666,7 @@ gwo_status gwo_side_output_count(gwo_handle *hh, int64_t *n) {
 gwo_status gwo_drain_side_output(gwo_handle *hh, const gwo_side_out *cols, int64_t cap, int64_t *n_out) {
     H_OR_FAIL;
     if (!cols || !n_out || cap < 0) return GWO_ERR_INVALID_ARGUMENT;
+    GWO_TRY(h->log_flush());
     return h->drain_side(cols, cap, n_out);
 }
 
@@ -682,6 +685,7 @@ gwo_status gwo_state_size(gwo_handle *hh, int64_t *entries) {
 
 gwo_status gwo_sync(gwo_handle *hh) {
     H_OR_FAIL;
+    if (h->logst) GWO_TRY(h->log_flush());
     if (h->logst) GWO_TRY(h->log_resolve_split());
     GWO_TRY(h->finish_fire());
     return h->hipcheck(hipStreamSynchronize(h->stream), "sync");
@@ -697,6 +701,11 @@ gwo_status gwo_get_stream(gwo_handle *hh, void **stream) {
 const char *gwo_last_error(const gwo_handle *hh) {
     const Handle *h = reinterpret_cast<const Handle *>(hh);
     return h ? h->err.c_str() : "null handle";
+}
+
+gwo_status gwo_set_pipelined_submit(gwo_handle *hh, int32_t enabled) {
+    H_OR_FAIL;
+    return h->set_pipelined(enabled != 0);
 }
 
 gwo_status gwo_set_profiling(gwo_handle *hh, int32_t enabled) {

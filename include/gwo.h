@@ -171,6 +171,16 @@ gwo_status gwo_get_stream(gwo_handle *h, void **stream);
 const char *gwo_last_error(const gwo_handle *h);
 const char *gwo_status_string(gwo_status s);
 
+/* Pipelined submission (off by default; log layout with caller-owned device columns and no side output --
+ * other batches are resolved inside gwo_submit as usual).  gwo_submit queues the batch's partition kernel
+ * and returns after completing the PREVIOUS batch (its classification checks and pass 2), so the host's
+ * wait and planning overlap a running kernel.  Observable results are unchanged: gwo_advance_watermark,
+ * gwo_sync, gwo_late_dropped, gwo_state_size and the side-output calls complete the pending batch first.
+ * What moves is error reporting: a batch's GWO_ERR_NO_TIMESTAMP / GWO_ERR_KEY_GROUP is returned by the
+ * next call on the handle (the batch is still rejected before any window state changes, and the handle
+ * stays failed).  Device columns stay borrowed until that next call returns. */
+gwo_status gwo_set_pipelined_submit(gwo_handle *h, int32_t enabled);
+
 /* Per-kernel HIP-event timing, for bench.py's roofline (off by default). */
 typedef enum {
     GWO_KERNEL_SCAN = 0,          /* batch pre-pass: window range, lateness, key-group checks */

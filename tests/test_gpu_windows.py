@@ -597,3 +597,92 @@ def test_log_layout_async_fire_overlaps_later_batches(F):
     N.check(lib.gwo_rows_emitted(h, C.byref(tot)), h)
     assert tot.value > 0
     op.close()
+
+
+def _pipelined_run(F, k, t, v, b, agg, size, offset=0, split=1, expected_keys=0, layout="log"):
+    """Drives gwo_submit in pipelined mode with caller-owned DEVICE columns (the bench's mode): each
+    watermark interval is cut into `split` batches, so K1 launches queue ahead of the previous batch's
+    resolution; the watermark flushes only when the pending batch may hold a window it fires."""
+    import ctypes as C
+    import torch
+    from flink_amd import _native as N
+    lib = N.lib()
+    dk, dt, dv = (torch.from_numpy(np.ascontiguousarray(x)).cuda() for x in (k, t, v))
+    op = F.GpuWindowOperator(F.TumblingEventTimeWindows.of(size, offset), agg, state_layout=layout,
+                             expected_keys=expected_keys)
+    h = op.handle
+    N.check(lib.gwo_set_pipelined_submit(h, 1), h)
+    prev = 0
+    for end, wm in b:
+        edges = np.linspace(prev, end, split + 1).astype(int)
+        for a, c in zip(edges[:-1].tolist(), edges[1:].tolist()):
+            if c > a:
+                N.check(lib.gwo_submit(h, C.c_void_p(dk.data_ptr() + 8 * a), C.c_void_p(dt.data_ptr() + 8 * a),
+                                       C.c_void_p(dv.data_ptr() + 8 * a), int(c - a)), h)
+        N.check(lib.gwo_advance_watermark(h, wm), h)
+        prev = end
+    N.check(lib.gwo_end_input(h), h)
+    op._collect()
+    got = sorted((a, s, e, *r) for a, s, e, r in op.output)
+    late = op.num_late_records_dropped
+    op.close()
+    return got, late
+
+
+@pytest.mark.parametrize("split", [1, 3])
+def test_log_layout_pipelined_submit_matches_oracle(F, split):
+    """Pipelined submission (K1 of batch i queued before batch i-1 is resolved) gives exactly the
+    oracle's rows and late count, with late records and several batches between watermarks."""
+    k, t, v, b = _c1(n=600_000, nkeys=200_000, every=20_000, lag=200, disorder=1500, seed=11)
+    v = v - 500
+    agg = F.MultiAggregate(F.SumAggregate(), F.MinAggregate(), F.MaxAggregate(), F.CountAggregate())
+    got, late = _pipelined_run(F, k, t, v, b, agg, 2000, 300, split=split, expected_keys=200_000)
+    (wk, ws, we, res), want_late = V.tumbling_lateness0(k, t, v, _final(b), 2000, 300, [1, 2, 3, 0])
+    assert want_late > 0 and late == want_late
+    assert got == _want(wk, ws, we, res)
+
+
+def test_log_layout_pipelined_window_jumps_and_wide_batches(F):
+    """Event time jumps many windows between batches (the pipelined K1's window-range guess is wrong and
+    must be re-run) and batches spanning more windows than one K1 covers (multi-range resolution)."""
+    rng = np.random.default_rng(5)
+    parts = []
+    t0 = 0
+    for i in range(12):
+        n = 20_000
+        width = 50_000 if i % 3 == 0 else 3_000          # every third batch spans ~25 windows
+        ts = t0 + np.sort(rng.integers(0, width, n))
+        parts.append(ts)
+        t0 = int(ts[-1]) + (40_000 if i % 4 == 1 else 500)   # jumps of 20 windows
+    t = np.concatenate(parts).astype(np.int64)
+    n = len(t)
+    k = rng.integers(0, 30_000, n).astype(np.int64)
+    v = rng.integers(-1000, 1000, n).astype(np.int64)
+    ends = np.cumsum([len(p) for p in parts])
+    b = [(int(e), int(t[:e].max()) - 100 - 1) for e in ends]
+    agg = F.MultiAggregate(F.SumAggregate(), F.MaxAggregate())
+    got, late = _pipelined_run(F, k, t, v, b, agg, 2000, expected_keys=30_000)
+    (wk, ws, we, res), want_late = V.tumbling_lateness0(k, t, v, _final(b), 2000, 0, [1, 3])
+    assert late == want_late
+    assert got == _want(wk, ws, we, res)
+
+
+def test_log_layout_pipelined_error_reported_by_next_call(F):
+    """A pipelined batch's Long.MIN_VALUE timestamp is reported by the next call on the handle, and the
+    handle stays failed (gwo.h: gwo_set_pipelined_submit)."""
+    import ctypes as C
+    import torch
+    from flink_amd import _native as N
+    lib = N.lib()
+    op = F.GpuWindowOperator(F.TumblingEventTimeWindows.of(1000), F.SumAggregate(), state_layout="log")
+    h = op.handle
+    N.check(lib.gwo_set_pipelined_submit(h, 1), h)
+    good = [torch.tensor(x, dtype=torch.int64, device="cuda") for x in ([1, 2], [5, 6], [1, 1])]
+    bad = [torch.tensor(x, dtype=torch.int64, device="cuda") for x in ([1, 2], [5, LONG_MIN], [1, 1])]
+    P = lambda x: C.c_void_p(x.data_ptr())
+    assert lib.gwo_submit(h, *map(P, good), 2) == 0
+    assert lib.gwo_submit(h, *map(P, bad), 2) == 0          # queued; resolved by the next call
+    st = lib.gwo_sync(h)
+    assert N.STATUS_NAMES.get(st) == "GWO_ERR_NO_TIMESTAMP"
+    assert lib.gwo_submit(h, *map(P, good), 2) == st         # the handle stays failed
+    op.close()
