@@ -153,7 +153,8 @@ gwo_status Handle::init(const gwo_config &c) {
     if (c.state_layout == GWO_STATE_LOG && c.assigner != GWO_ASSIGNER_TUMBLING)
         return fail(GWO_ERR_UNSUPPORTED, "the log-structured state layout serves tumbling windows only");
     if (c.assigner == GWO_ASSIGNER_TUMBLING &&
-        (c.state_layout == GWO_STATE_LOG || (c.state_layout == GWO_STATE_AUTO && c.expected_keys >= (1 << 20))))
+        (c.state_layout == GWO_STATE_LOG ||
+         (c.state_layout == GWO_STATE_AUTO && c.expected_keys >= (1 << 20) && c.allowed_lateness == 0)))
         GWO_TRY(log_init());
     memset(h_ident_side, 0, GWO_MAX_WORDS * 16 + 16);
     for (int w = 0; w < plan.nwords; ++w) h_ident_side[1 + w] = plan.ident[w];
@@ -181,6 +182,7 @@ Handle::~Handle() {
     if (h_scalar) (void)hipHostFree(h_scalar);
     if (h_ident_side) (void)hipHostFree(h_ident_side);
     dir_buf.release();
+    refire_buf.release();
     stage_key.release();
     stage_ts.release();
     stage_val.release();

@@ -96,6 +96,7 @@ struct Handle {
     unsigned long long *h_counters = nullptr;  // pinned
     std::vector<char> counter_used;
     DevBuf dir_buf, stage_key, stage_ts, stage_val;
+    DevBuf refire_buf;                         // per-element re-fire scratch (refire_rows)
     std::vector<TableDesc> h_dir;
     long long hist_hint = 0;
 
@@ -187,6 +188,8 @@ struct Handle {
     int64_t unit_start(long long u) const;
     WindowGeom geom_now() const;
     gwo_status insert_windowed(const int64_t *k, const int64_t *t, const int64_t *v, int64_t n);
+    gwo_status refire_rows(const int64_t *k, const int64_t *t, const int64_t *v, int64_t n, const WindowGeom &g,
+                           long long dir_base, int dir_len, uint64_t mmax);
     void adapt_preagg(uint64_t accepted, uint64_t partials);
     void init_stats(long long hist_base);
     gwo_status grow_side(long long need);

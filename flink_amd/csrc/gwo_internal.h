@@ -97,7 +97,7 @@ struct WindowGeom {
     int32_t max_par;
     int32_t kg_lo;
     int32_t kg_hi;
-    int32_t pad;
+    int32_t refire_ok;                 // tumbling table layout: re-fire records are emitted + inserted
 };
 
 // Output columns (SoA) in HBM.
@@ -149,6 +149,18 @@ void launch_insert(const int64_t *key, const int64_t *ts, const void *val, int64
                    BatchStats *stats, const RingDesc &ring, hipStream_t s);
 
 // Emits every occupied entry (with live_word >= 0: every entry whose word live_word is > 0).
+void launch_refire_collect(const int64_t *ts, int64_t n, const WindowGeom &g, long long dir_base, int dir_len,
+                           uint32_t *blk, int64_t *r_idx, long long *r_u, hipStream_t s);
+void launch_refire_slots(const int64_t *key, const int64_t *r_idx, const long long *r_u, int64_t m, const AccPlan &p,
+                         const TableDesc *dir, long long dir_base, const uint64_t *slot_off, uint32_t *r_slot,
+                         int64_t *before, hipStream_t s);
+void launch_refire_emit(const int64_t *key, const int64_t *val, const int64_t *r_idx, const long long *r_u, int64_t m,
+                        const uint32_t *skey, const uint32_t *spay, const int64_t *before, const AccPlan &p,
+                        const ResultPlan &rp, int64_t unit, int64_t unit_off_mod, OutCols o, hipStream_t s);
+// gwo_sort.hip: stable LSD radix sort of (uint32 key, uint32 payload; vals NULL = index); returns 0 when the
+// result is in (k1, v1), 1 when in (k2, v2)
+int radix_sort_pairs(const uint32_t *keys, const uint32_t *vals, int64_t n, int key_bits, uint32_t *k1, uint32_t *v1,
+                     uint32_t *k2, uint32_t *v2, uint32_t *hist, hipStream_t s);
 void launch_fire(const TableDesc &t, uint64_t cap, const AccPlan &plan, const ResultPlan &rp, int64_t start,
                  int64_t end, OutCols out, int reset, int live_word, hipStream_t s);
 

@@ -47,7 +47,9 @@ __device__ __forceinline__ int classify(int64_t ts, const WindowGeom &g, long lo
             // unfired windows, which is exactly the reference's per-window accept set
             if (g.lateness != 0) return REC_REFIRE;
         } else {
-            return REC_REFIRE;  // EventTimeTrigger.onElement FIRE: window.maxTs <= watermark
+            // EventTimeTrigger.onElement FIRE: window.maxTs <= watermark (tumbling: the unit is the window)
+            if (!g.sliding) unit_idx = fdiv_floor(last_start, g.size, g.inv_size);
+            return REC_REFIRE;
         }
     }
     if (!g.sliding) {
@@ -79,7 +81,8 @@ __global__ __launch_bounds__(256) void scan_kernel(const int64_t *__restrict__ k
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
         long long u = 0;
         int c = classify(ts[i], g, u);
-        if (c == REC_ACCEPT) {
+        if (c == REC_REFIRE && g.refire_ok) refire++;   // also inserted: counted with the accepted records
+        if (c == REC_ACCEPT || (c == REC_REFIRE && g.refire_ok)) {
             acc++;
             mn = u < mn ? u : mn;
             mx = u > mx ? u : mx;
@@ -180,7 +183,8 @@ __global__ __launch_bounds__(256) void insert_direct_kernel(const int64_t *__res
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
         long long u = 0;
         int64_t t = ts[i];
-        if (classify(t, g, u) != REC_ACCEPT) continue;
+        const int c = classify(t, g, u);
+        if (c != REC_ACCEPT && !(c == REC_REFIRE && g.refire_ok)) continue;
         long long d = u - dir_base;
         if (d < 0 || d >= dir_len) continue;
         int64_t k = key[i];
@@ -246,7 +250,8 @@ __global__ __launch_bounds__(256) void insert_preagg_kernel(const int64_t *__res
             int64_t i = tile + j * 256 + threadIdx.x;
             if (i >= n) continue;
             long long u = 0;
-            if (classify(ts[i], g, u) != REC_ACCEPT) continue;
+            const int c = classify(ts[i], g, u);
+            if (c != REC_ACCEPT && !(c == REC_REFIRE && g.refire_ok)) continue;
             long long d = u - dir_base;
             if (d < 0 || d >= dir_len) continue;
             int64_t k = key[i];
@@ -517,6 +522,190 @@ static inline int grid_for(int64_t n, int per_thread = 1, int cap = 4096) {
     if (g < 1) g = 1;
     if (g > cap) g = cap;
     return (int)g;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Per-element re-fire (allowedLateness > 0, tumbling): a record whose window already fired but is not
+// yet cleaned up is added to the window state and EventTimeTrigger.onElement FIREs at once, emitting
+// the window's contents including it (WindowOperator.java:393-406, EventTimeTrigger.java:37-45).  Every
+// record of such a (key, window) in a batch is a re-fire, so re-fire j's row is
+//   state before the batch  (+)  the batch's re-fire values of that (key, window) up to j, arrival order.
+// Device steps: order-preserving compaction of the re-fire records, find-or-claim of their entries
+// (reading the state before the batch), a stable radix sort by entry, and a segmented scan that emits
+// the rows.  The batch's ordinary insert then adds the same records to the tables.
+// ------------------------------------------------------------------------------------------------
+#define RF_BLOCKS 256
+#define RF_THREADS 256
+
+__device__ __forceinline__ bool refire_in_dir(const int64_t *ts, int64_t i, const WindowGeom &g, long long dir_base,
+                                              int dir_len, long long &u) {
+    u = 0;
+    if (classify(ts[i], g, u) != REC_REFIRE) return false;
+    return u - dir_base >= 0 && u - dir_base < dir_len;
+}
+
+// per block: re-fire records of its contiguous share of the batch
+__global__ __launch_bounds__(RF_THREADS) void refire_count_kernel(const int64_t *__restrict__ ts, int64_t n,
+                                                                  WindowGeom g, long long dir_base, int dir_len,
+                                                                  uint32_t *blk) {
+    const int64_t per = (n + gridDim.x - 1) / gridDim.x;
+    const int64_t b0 = (int64_t)blockIdx.x * per, b1 = min(n, b0 + per);
+    unsigned c = 0;
+    for (int64_t i = b0 + threadIdx.x; i < b1; i += RF_THREADS) {
+        long long u;
+        c += refire_in_dir(ts, i, g, dir_base, dir_len, u);
+    }
+    unsigned total;
+    (void)block_exclusive_scan(c, &total);
+    if (threadIdx.x == 0) blk[blockIdx.x] = total;
+}
+
+// writes the re-fire records of each block's share in arrival order: r_idx (batch index), r_u (window)
+__global__ __launch_bounds__(RF_THREADS) void refire_write_kernel(const int64_t *__restrict__ ts, int64_t n,
+                                                                  WindowGeom g, long long dir_base, int dir_len,
+                                                                  const uint32_t *blk, int64_t *r_idx,
+                                                                  long long *r_u) {
+    __shared__ unsigned s_base;
+    if (threadIdx.x == 0) {
+        unsigned b = 0;
+        for (unsigned x = 0; x < blockIdx.x; ++x) b += blk[x];
+        s_base = b;
+    }
+    __syncthreads();
+    unsigned base = s_base;
+    const int64_t per = (n + gridDim.x - 1) / gridDim.x;
+    const int64_t b0 = (int64_t)blockIdx.x * per, b1 = min(n, b0 + per);
+    for (int64_t i0 = b0; i0 < b1; i0 += RF_THREADS) {
+        const int64_t i = i0 + threadIdx.x;
+        long long u = 0;
+        const bool f = i < b1 && refire_in_dir(ts, i, g, dir_base, dir_len, u);
+        unsigned total;
+        const unsigned at = block_exclusive_scan(f ? 1u : 0u, &total);
+        if (f) {
+            r_idx[base + at] = i;
+            r_u[base + at] = u;
+        }
+        base += total;
+    }
+}
+
+// find-or-claim each re-fire record's entry; sort key = the entry's global slot, before = its words
+__global__ __launch_bounds__(RF_THREADS) void refire_slot_kernel(const int64_t *__restrict__ key, const int64_t *r_idx,
+                                                                 const long long *r_u, int64_t m, AccPlan p,
+                                                                 const TableDesc *__restrict__ dir, long long dir_base,
+                                                                 const uint64_t *slot_off, uint32_t *r_slot,
+                                                                 int64_t *before) {
+    for (int64_t j0 = (int64_t)blockIdx.x * RF_THREADS; j0 < m; j0 += (int64_t)gridDim.x * RF_THREADS) {
+        const int64_t j = j0 + threadIdx.x;
+        bool claimed = false;
+        unsigned long long *occ = nullptr;
+        if (j < m) {
+            const int d = (int)(r_u[j] - dir_base);
+            const TableDesc t = dir[d];
+            const int64_t k = key[r_idx[j]];
+            int64_t *acc = find_or_insert(t, p.stride, k, claimed);
+            occ = t.occ;
+            const uint64_t local = k == GWO_EMPTY_KEY ? t.mask + 1 : (uint64_t)(acc - 1 - t.base) / (uint64_t)p.stride;
+            r_slot[j] = (uint32_t)(slot_off[d] + local);
+            for (int w = 0; w < p.nwords; ++w) before[j * GWO_MAX_WORDS + w] = acc[w];
+        }
+        count_claims(occ, claimed);
+    }
+}
+
+// One workgroup: segmented inclusive scan of the sorted re-fire records (segment = entry) in chunks of
+// 1024, each row = before (+) prefix, written to rows [base, base + m) of the output.
+__global__ __launch_bounds__(1024) void refire_emit_kernel(const int64_t *__restrict__ key,
+                                                           const int64_t *__restrict__ val, const int64_t *r_idx,
+                                                           const long long *r_u, int64_t m, const uint32_t *skey,
+                                                           const uint32_t *spay, const int64_t *before, AccPlan p,
+                                                           ResultPlan rp, int64_t unit, int64_t unit_off_mod,
+                                                           OutCols o) {
+    __shared__ int64_t s_x[1024][GWO_MAX_WORDS];
+    __shared__ uint32_t s_slot[1024];
+    __shared__ uint8_t s_flag[1024];
+    __shared__ unsigned long long s_base;
+    __shared__ uint32_t c_slot;
+    __shared__ int64_t c_x[GWO_MAX_WORDS];
+    const int t = threadIdx.x, NW = p.nwords;
+    if (t == 0) {
+        s_base = atomicAdd(o.count, (unsigned long long)m);
+        c_slot = 0xffffffffu;
+    }
+    __syncthreads();
+    for (int64_t q0 = 0; q0 < m; q0 += 1024) {
+        const int64_t q = q0 + t;
+        const bool live = q < m;
+        const uint32_t j = live ? spay[q] : 0u;
+        const uint32_t sl = live ? skey[q] : 0xfffffffeu;
+        const int64_t vb = live && val ? val[r_idx[j]] : 0;
+        int64_t x[GWO_MAX_WORDS];
+        for (int w = 0; w < NW; ++w) x[w] = lift_word(p, w, vb);
+        s_slot[t] = sl;
+        __syncthreads();
+        // a segment starts where the entry changes (element 0: against the previous chunk's last entry)
+        uint8_t f = t == 0 ? (sl != c_slot) : (sl != s_slot[t - 1]);
+        if (t == 0 && !f)   // continues the previous chunk's segment: fold its running value in first
+            for (int w = 0; w < NW; ++w) x[w] = combine(p.op[w], c_x[w], x[w]);
+        for (int w = 0; w < NW; ++w) s_x[t][w] = x[w];
+        s_flag[t] = f;
+        __syncthreads();
+        for (int off = 1; off < 1024; off <<= 1) {
+            int64_t y[GWO_MAX_WORDS];
+            uint8_t fy = 1;
+            if (t >= off && !s_flag[t]) {
+                fy = s_flag[t - off];
+                for (int w = 0; w < NW; ++w) y[w] = s_x[t - off][w];
+            }
+            __syncthreads();
+            if (t >= off && !s_flag[t]) {
+                for (int w = 0; w < NW; ++w) s_x[t][w] = combine(p.op[w], y[w], s_x[t][w]);
+                s_flag[t] = fy;
+            }
+            __syncthreads();
+        }
+        if (live) {
+            int64_t acc[GWO_MAX_WORDS];
+            for (int w = 0; w < NW; ++w) acc[w] = combine(p.op[w], before[(int64_t)j * GWO_MAX_WORDS + w], s_x[t][w]);
+            const unsigned long long pos = s_base + (unsigned long long)q;
+            if ((long long)pos < o.cap) {
+                const int64_t start = (int64_t)((uint64_t)r_u[j] * (uint64_t)unit + (uint64_t)unit_off_mod);
+                o.key[pos] = key[r_idx[j]];
+                o.start[pos] = start;
+                o.end[pos] = (int64_t)((uint64_t)start + (uint64_t)unit);
+                write_results(p, rp, acc, o, pos);
+            }
+        }
+        __syncthreads();
+        const int last = (int)min((int64_t)1023, m - 1 - q0);
+        if (t == last) {
+            c_slot = s_slot[t];
+            for (int w = 0; w < NW; ++w) c_x[w] = s_x[t][w];
+        }
+        __syncthreads();
+    }
+}
+
+void launch_refire_collect(const int64_t *ts, int64_t n, const WindowGeom &g, long long dir_base, int dir_len,
+                           uint32_t *blk, int64_t *r_idx, long long *r_u, hipStream_t s) {
+    hipLaunchKernelGGL(refire_count_kernel, dim3(RF_BLOCKS), dim3(RF_THREADS), 0, s, ts, n, g, dir_base, dir_len, blk);
+    hipLaunchKernelGGL(refire_write_kernel, dim3(RF_BLOCKS), dim3(RF_THREADS), 0, s, ts, n, g, dir_base, dir_len, blk,
+                       r_idx, r_u);
+}
+
+void launch_refire_slots(const int64_t *key, const int64_t *r_idx, const long long *r_u, int64_t m, const AccPlan &p,
+                         const TableDesc *dir, long long dir_base, const uint64_t *slot_off, uint32_t *r_slot,
+                         int64_t *before, hipStream_t s) {
+    int blocks = (int)std::min<int64_t>(1024, (m + RF_THREADS - 1) / RF_THREADS);
+    hipLaunchKernelGGL(refire_slot_kernel, dim3(std::max(blocks, 1)), dim3(RF_THREADS), 0, s, key, r_idx, r_u, m, p,
+                       dir, dir_base, slot_off, r_slot, before);
+}
+
+void launch_refire_emit(const int64_t *key, const int64_t *val, const int64_t *r_idx, const long long *r_u, int64_t m,
+                        const uint32_t *skey, const uint32_t *spay, const int64_t *before, const AccPlan &p,
+                        const ResultPlan &rp, int64_t unit, int64_t unit_off_mod, OutCols o, hipStream_t s) {
+    hipLaunchKernelGGL(refire_emit_kernel, dim3(1), dim3(1024), 0, s, key, val, r_idx, r_u, m, skey, spay, before, p, rp,
+                       unit, unit_off_mod, o);
 }
 
 void launch_scan(const int64_t *key, const int64_t *ts, int64_t n, const WindowGeom &g, long long hist_base,

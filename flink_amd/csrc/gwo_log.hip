@@ -173,7 +173,11 @@ __global__ __launch_bounds__(LOG_K1_THREADS) void log_part_kernel(
         for (int q = 0; q < 4; ++q) {
             int b = tid * per + q;
             at[q] = 0;
+#ifdef GWO_K1_XP_NOATOMIC   // experiment build only: timing without the reservation atomics
+            if (q < per && loc[q]) at[q] = (blockIdx.x & 7) * 16;
+#else
             if (q < per && loc[q]) at[q] = atomicAdd(&cursor[(size_t)b * LOG_CUR_STRIDE], (unsigned long long)loc[q]);
+#endif
         }
 #pragma unroll
         for (int j = 0; j < LOG_K1_PER; ++j) {
@@ -199,7 +203,11 @@ __global__ __launch_bounds__(LOG_K1_THREADS) void log_part_kernel(
             uint32_t b = s_bk[p];
             if (b >= (uint32_t)nb) continue;   // defensive: never a write outside the buffer
             uint64_t q = (uint64_t)s_cnt[b] + (p - s_off[b]);
+#ifdef GWO_K1_XP_NOWRITE   // experiment build only: timing without the batch-buffer writes
+            if (q == (uint64_t)-1) {
+#else
             if (q < cap) {
+#endif
                 int64_t *dst = tmp + ((uint64_t)b * cap + q) * W;
                 if (HASV) *(ll2 *)dst = *(const ll2 *)&s_rec[2 * p];
                 else *dst = s_rec[p];

@@ -171,6 +171,11 @@ gwo_status Handle::ensure_table(long long u, uint64_t incoming) {
     if (it == tables.end()) {
         Table t;
         GWO_TRY(alloc_table(want_min, t));
+        // tumbling: a window created after the watermark passed its end only receives re-fire records
+        // (EventTimeTrigger.onElement FIREs them; no maxTs timer, WindowOperator.java:393-410)
+        if (cfg.assigner == GWO_ASSIGNER_TUMBLING &&
+            (int64_t)((uint64_t)unit_start(u) + (uint64_t)cfg.size - 1) <= wm)
+            t.fired = true;
         tables.emplace(u, t);
         return GWO_OK;
     }
@@ -332,8 +337,63 @@ WindowGeom Handle::geom_now() const {
 }
 
 // ---- tumbling / pane insert -------------------------------------------------------------------------
+// Rows of the batch's re-fire records in directory units [dir_base, dir_base + dir_len) (see
+// refire_emit_kernel, gwo_kernels.hip): emitted before the batch's insert, which then adds them.
+gwo_status Handle::refire_rows(const int64_t *k, const int64_t *t, const int64_t *v, int64_t n, const WindowGeom &g,
+                               long long dir_base, int dir_len, uint64_t mmax) {
+    std::vector<uint64_t> off(dir_len, 0);
+    uint64_t tot = 0;
+    for (int d = 0; d < dir_len; ++d) {
+        off[d] = tot;
+        if (h_dir[d].base) tot += h_dir[d].mask + 2;   // cap entries + the side slot
+    }
+    if (tot >= (1ull << 32))
+        return poison(GWO_ERR_CAPACITY, "allowedLateness re-fire: the re-fired windows' tables exceed 2^32 entries");
+    const uint64_t m8 = std::max<uint64_t>(mmax, 1);
+    const uint64_t rs_blocks = (m8 + 4095) / 4096;
+    // carve: blk[256] u32 | slot_off[dir_len] u64 | r_idx[m] i64 | r_u[m] i64 | before[m][MAX_WORDS] i64 |
+    //        r_slot, k1, v1, k2, v2 [m] u32 | hist[256 * rs_blocks] u32
+    size_t o_blk = 0, o_off = 1024, o_idx = o_off + (size_t)dir_len * 8;
+    o_idx = (o_idx + 255) & ~(size_t)255;
+    size_t o_u = o_idx + m8 * 8, o_before = o_u + m8 * 8, o_slot = o_before + m8 * GWO_MAX_WORDS * 8;
+    size_t o_k1 = o_slot + m8 * 4, o_v1 = o_k1 + m8 * 4, o_k2 = o_v1 + m8 * 4, o_v2 = o_k2 + m8 * 4;
+    size_t o_hist = (o_v2 + m8 * 4 + 255) & ~(size_t)255, total = o_hist + 256 * 4 * rs_blocks;
+    GWO_TRY(ensure_buf(refire_buf, total));
+    char *b = (char *)refire_buf.ptr;
+    GWO_TRY(hipcheck(hipMemcpyAsync(b + o_off, off.data(), (size_t)dir_len * 8, hipMemcpyHostToDevice, stream), "refire"));
+    launch_refire_collect(t, n, g, dir_base, dir_len, (uint32_t *)(b + o_blk), (int64_t *)(b + o_idx),
+                          (long long *)(b + o_u), stream);
+    GWO_TRY(launch_ok("refire collect"));
+    std::vector<uint32_t> blk(256);
+    GWO_TRY(hipcheck(hipMemcpyAsync(blk.data(), b + o_blk, 256 * 4, hipMemcpyDeviceToHost, stream), "refire count"));
+    GWO_TRY(hipcheck(hipStreamSynchronize(stream), "refire count"));
+    uint64_t m = 0;
+    for (uint32_t c : blk) m += c;
+    if (m == 0) return GWO_OK;
+    if (m > mmax) return poison(GWO_ERR_HIP, "allowedLateness re-fire: more re-fire records than the scan counted");
+    launch_refire_slots(k, (const int64_t *)(b + o_idx), (const long long *)(b + o_u), (int64_t)m, plan,
+                        (const TableDesc *)dir_buf.ptr, dir_base, (const uint64_t *)(b + o_off), (uint32_t *)(b + o_slot),
+                        (int64_t *)(b + o_before), stream);
+    GWO_TRY(launch_ok("refire slots"));
+    const int which = radix_sort_pairs((const uint32_t *)(b + o_slot), nullptr, (int64_t)m, 32, (uint32_t *)(b + o_k1),
+                                       (uint32_t *)(b + o_v1), (uint32_t *)(b + o_k2), (uint32_t *)(b + o_v2),
+                                       (uint32_t *)(b + o_hist), stream);
+    GWO_TRY(launch_ok("refire sort"));
+    GWO_TRY(ensure_output(m));
+    const uint32_t *sk = (const uint32_t *)(b + (which ? o_k2 : o_k1));
+    const uint32_t *sp = (const uint32_t *)(b + (which ? o_v2 : o_v1));
+    launch_refire_emit(k, v, (const int64_t *)(b + o_idx), (const long long *)(b + o_u), (int64_t)m, sk, sp,
+                       (const int64_t *)(b + o_before), plan, rplan, geom.unit, geom.unit_off_mod, out_cols(), stream);
+    GWO_TRY(launch_ok("refire emit"));
+    out_rows += m;
+    return GWO_OK;
+}
+
 gwo_status Handle::insert_windowed(const int64_t *k, const int64_t *t, const int64_t *v, int64_t n) {
     WindowGeom g = geom_now();
+    // tumbling: re-fire records (allowedLateness > 0) are emitted per element and inserted
+    g.refire_ok = cfg.assigner == GWO_ASSIGNER_TUMBLING ? 1 : 0;
+    uint64_t refire_total = 0;
     long long hist_base = hist_hint;
     bool first_pass = true;
     BatchStats &hs = *h_stats;
@@ -361,8 +421,9 @@ gwo_status Handle::insert_windowed(const int64_t *k, const int64_t *t, const int
             if (hs.bad_range) return poison(GWO_ERR_UNSUPPORTED,
                                             "sliding windows: timestamp < offset - slide (Java '%' quirk range) is "
                                             "outside the pane restatement");
-            if (hs.refire) return poison(GWO_ERR_UNSUPPORTED,
-                                         "allowedLateness > 0 re-firing on sliding windows is not supported");
+            if (hs.refire && !g.refire_ok)
+                return poison(GWO_ERR_UNSUPPORTED, "allowedLateness > 0 re-firing on sliding windows is not supported");
+            refire_total = hs.refire;
             if (side_enabled()) {
                 GWO_TRY(hipcheck(hipMemcpyAsync(h_scalar, d_side_count, 8, hipMemcpyDeviceToHost, stream), "side count"));
                 GWO_TRY(hipcheck(hipStreamSynchronize(stream), "side count sync"));
@@ -406,6 +467,7 @@ gwo_status Handle::insert_windowed(const int64_t *k, const int64_t *t, const int
         GWO_TRY(ensure_buf(dir_buf, dir_len * sizeof(TableDesc)));
         GWO_TRY(hipcheck(hipMemcpyAsync(dir_buf.ptr, h_dir.data(), dir_len * sizeof(TableDesc), hipMemcpyHostToDevice,
                                         stream), "dir"));
+        if (refire_total) GWO_TRY(refire_rows(k, t, v, n, g, hist_base, dir_len, refire_total));
         prof_begin(GWO_KERNEL_INSERT);
         launch_insert(k, t, v, n, g, plan, (const TableDesc *)dir_buf.ptr, hist_base, dir_len, use_preagg, d_stats,
                       ring_desc(), stream);

@@ -15,8 +15,6 @@ void launch_sess_process(const int64_t *key, const int64_t *ts, const int64_t *v
 void launch_sess_fire(const TableDesc &t, uint64_t cap, int stride, const AccPlan &p, const ResultPlan &rp,
                       const SessGeom &g, OutCols o, SessErr *err, hipStream_t s);
 void launch_sess_compact(const TableDesc &src, uint64_t cap, const TableDesc &dst, int stride, hipStream_t s);
-int radix_sort_pairs(const uint32_t *keys, const uint32_t *vals, int64_t n, int key_bits, uint32_t *k1, uint32_t *v1,
-                     uint32_t *k2, uint32_t *v2, uint32_t *hist, hipStream_t s);
 
 struct SessionState {
     int smax = 8;

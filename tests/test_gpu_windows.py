@@ -686,3 +686,71 @@ def test_log_layout_pipelined_error_reported_by_next_call(F):
     assert N.STATUS_NAMES.get(st) == "GWO_ERR_NO_TIMESTAMP"
     assert lib.gwo_submit(h, *map(P, good), 2) == st         # the handle stays failed
     op.close()
+
+
+def _tumbling_oracle(k, t, v, batches, size, offset, lateness, agg, side_output=False):
+    op = O.WindowOperatorOracle(O.TumblingEventTimeWindows(size, offset), agg, lateness, side_output=side_output)
+    prev = 0
+    for end, wm in batches:
+        for i in range(prev, end):
+            op.process_element(int(k[i]), int(t[i]), v[i].item())
+        op.process_watermark(wm)
+        prev = end
+    op.process_watermark(LONG_MAX)
+    return op
+
+
+@pytest.mark.parametrize("layout", ["table", "auto"])
+@pytest.mark.parametrize("lateness", [1_500, 7_000])
+def test_tumbling_per_element_refire_with_lateness(F, lateness, layout):
+    """allowedLateness > 0: a record landing in an already-fired window (before its cleanup time) is
+    added and EventTimeTrigger.onElement FIREs at once -- one row per such record with the window's
+    contents including it, in arrival order (WindowOperator.java:393-406).  Heavy disorder relative to
+    the lag, several records per (key, window) per batch, windows first created after the watermark
+    passed their end, and late drops beyond the lateness -- all exactly as the loop restatement."""
+    rng = np.random.default_rng(lateness)
+    n = 12_000
+    k = rng.integers(0, 60, n).astype(np.int64)
+    t = (np.sort(rng.integers(0, 200_000, n)) + rng.integers(0, 9_000, n)).astype(np.int64)
+    v = rng.integers(-50, 100, n).astype(np.int64)
+    b = G.punctuated_watermarks(t, 400, 500)
+    ref = _tumbling_oracle(k, t, v, b, 2_000, 300, lateness,
+                           O.MultiAgg([O.SumLongAgg(), O.CountAgg(), O.MaxAgg(), O.MinAgg()]))
+    op = F.GpuWindowOperator(F.TumblingEventTimeWindows.of(2_000, 300),
+                             F.MultiAggregate(F.SumAggregate(), F.CountAggregate(), F.MaxAggregate(), F.MinAggregate()),
+                             allowed_lateness=lateness, state_layout=layout, expected_keys=2_000_000 if layout == "auto" else 0)
+    _run_batches(op, k, t, v, b)
+    got = sorted(op.output)
+    want = sorted((r.key, r.start, r.end, r.result) for r in ref.output)
+    # re-fires make duplicate (key, window) rows with growing contents: compare multisets
+    assert len(got) == len(want)
+    assert got == want
+    n_windows = len({(r.key, r.start) for r in ref.output})
+    assert len(want) > n_windows + 500          # many per-element re-fire rows
+    assert op.num_late_records_dropped == ref.num_late_records_dropped > 0
+    op.close()
+
+
+def test_tumbling_refire_avg_and_float_sum(F):
+    """Re-fire rows for AVG ((double) sum / count of an exact int64 accumulator: bit-exact) and a float64
+    sum (order-dependent: within FLOAT_RTOL)."""
+    rng = np.random.default_rng(9)
+    n = 8_000
+    k = rng.integers(0, 40, n).astype(np.int64)
+    t = (np.sort(rng.integers(0, 120_000, n)) + rng.integers(0, 6_000, n)).astype(np.int64)
+    vi = rng.integers(0, 1000, n).astype(np.int64)
+    b = G.punctuated_watermarks(t, 300, 300)
+    ref = _tumbling_oracle(k, t, vi, b, 3_000, 0, 4_000, O.AvgAgg())
+    op = F.GpuWindowOperator(F.TumblingEventTimeWindows.of(3_000), F.AverageAggregate(), allowed_lateness=4_000)
+    _run_batches(op, k, t, vi, b)
+    assert sorted(op.output) == sorted((r.key, r.start, r.end, r.result) for r in ref.output)
+    op.close()
+    vf = rng.random(n) * 10.0
+    ref = _tumbling_oracle(k, t, vf, b, 3_000, 0, 4_000, O.SumDoubleAgg())
+    op = F.GpuWindowOperator(F.TumblingEventTimeWindows.of(3_000), F.SumAggregate("float64"), allowed_lateness=4_000)
+    _run_batches(op, k, t, vf, b)
+    got = sorted(op.output, key=lambda r: (r[0], r[1], r[3]))
+    want = sorted(((r.key, r.start, r.end, r.result) for r in ref.output), key=lambda r: (r[0], r[1], r[3]))
+    assert [g[:3] for g in got] == [w[:3] for w in want]
+    np.testing.assert_allclose([g[3] for g in got], [w[3] for w in want], rtol=FLOAT_RTOL)
+    op.close()
