@@ -161,6 +161,7 @@ struct Handle {
     gwo_status poison(gwo_status s, const char *what);
     gwo_status dalloc(void **p, size_t bytes);
     gwo_status hipcheck(hipError_t e, const char *what);
+    gwo_status spin_event(hipEvent_t ev, const char *what);
     gwo_status ensure_buf(DevBuf &b, size_t bytes);
     int take_counter();
     // occupancy counter c: GWO_OCC_WORDS device words (sharded, see gwo_device.h occ_add)
@@ -236,6 +237,7 @@ struct Handle {
     gwo_status insert_log(const int64_t *k, const int64_t *t, const int64_t *v, int64_t n, int64_t stride = 1);
     gwo_status log_k1(LogJob &J, bool first_pass);
     gwo_status log_resolve_k1(LogJob J);
+    gwo_status log_wait_readback(int slot, unsigned long long seq);
     gwo_status log_flush();                    // resolve the pipelined batch (no-op without one)
     bool log_pending_may_fire(int64_t new_wm) const;
     gwo_status set_pipelined(bool on);

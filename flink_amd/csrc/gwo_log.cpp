@@ -39,6 +39,7 @@ struct LogJob {
     int nunits = 1;
     uint64_t cap = 0;            // records per (window, coarse digit) region of the batch buffer
     int slot = 0;                // batch buffer / readback slot
+    unsigned long long seq = 0;  // readback sequence number of the last K1 launch
     LogSegDesc desc[LOG_NU] = {}; // the range's new segments: counters/offsets carved at launch, records after
 };
 
@@ -82,6 +83,7 @@ struct LogState {
     long long span_hint = 1;                     // windows the previous batch spanned
     int cap_log2 = 0;
     int max_groups = 0;                          // persistent fire workgroups (2 per CU)
+    unsigned long long seq = 0;                  // last readback sequence number issued
 
     unsigned long long *rb(int slot) const { return h_rb + (size_t)slot * LOG_RB_WORDS; }
     unsigned long long *rb_dev(int slot) const { return d_rbh + (size_t)slot * LOG_RB_WORDS; }
@@ -368,6 +370,7 @@ gwo_status Handle::log_k1(LogJob &J, bool first_pass) {
     ca.cap = J.cap;
     ca.bk = L.bk(J.slot);
     ca.rb = L.rb_dev(J.slot);
+    ca.seq = J.seq = ++L.seq;
     for (int w = 0; w < J.nunits; ++w) {
         auto it = L.wins.find(J.base + w);
         if (it == L.wins.end()) {
@@ -405,6 +408,26 @@ gwo_status Handle::log_k1(LogJob &J, bool first_pass) {
     return hipcheck(hipEventRecord(L.ev_rb[J.slot], stream), "event");
 }
 
+// Waits for K1's readback by spinning on its sequence word in pinned host memory (the collect kernel
+// writes it last), which wakes the host as soon as the data lands instead of through the runtime's
+// completion wait; the event is polled now and then so a failed launch cannot spin forever.
+gwo_status Handle::log_wait_readback(int slot, unsigned long long seq) {
+    LogState &L = *logst;
+    volatile unsigned long long *w = L.rb(slot) + LOG_RB_SEQ;
+    for (unsigned it = 1;; ++it) {
+        if (*w == seq) break;
+        if ((it & 1023) == 0) {
+            hipError_t e = hipEventQuery(L.ev_rb[slot]);
+            if (e != hipSuccess && e != hipErrorNotReady) return hipcheck(e, "log partition");
+            if (e == hipSuccess && *w != seq)   // completed, yet the word never arrived: fail loudly
+                return poison(GWO_ERR_HIP, "log partition: readback sequence word not visible after completion");
+        }
+        __builtin_ia32_pause();
+    }
+    __atomic_thread_fence(__ATOMIC_ACQUIRE);
+    return GWO_OK;
+}
+
 // Completes a batch whose first K1 is queued: waits for its readback, rejects the batch on a
 // classification error (before any window state changes), re-runs K1 when the window range guess or a
 // region capacity was wrong, and launches pass 2 (deferred) for each window range.
@@ -414,7 +437,9 @@ gwo_status Handle::log_resolve_k1(LogJob J) {
     bool first_pass = true;
     long long lo = 0, hi = -1;
     while (true) {
-        GWO_TRY(hipcheck(hipEventSynchronize(L.ev_rb[J.slot]), "log partition sync"));
+        GWO_TRY(log_wait_readback(J.slot, J.seq));
+        // the side-output row count follows the collect kernel by a copy: wait for that too
+        if (first_pass && side_enabled()) GWO_TRY(spin_event(L.ev_rb[J.slot], "side count"));
         const unsigned long long *rbp = L.rb(J.slot);
         memcpy(h_stats, rbp + LOG_RB_STATS, sizeof(BatchStats));
         GWO_TRY(log_resolve_split());   // the previous pass 2 (also frees its plan staging for reuse)
@@ -626,7 +651,7 @@ gwo_status Handle::finish_fire() {
     if (!fire_pending) return GWO_OK;
     LogState &L = *logst;
     fire_pending = false;
-    GWO_TRY(hipcheck(hipEventSynchronize(ev_fire), "fire"));
+    GWO_TRY(spin_event(ev_fire, "fire"));
     if (L.h_fire_out[1]) return poison(GWO_ERR_CAPACITY, "log fire: a partition overflowed its LDS table");
     uint64_t count = L.h_fire_out[0];
     if ((long long)count > out.cap) {

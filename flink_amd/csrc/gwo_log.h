@@ -6,8 +6,14 @@
 
 #define LOG_NU 4                 // windows one partition launch (K1) covers
 #define LOG_SLOTS 3              // batch buffers: K1 in flight (pipelined), deferred pass 2, next K1
+#ifndef LOG_K1_PER
 #define LOG_K1_PER 14            // K1 tile: 256 threads x 14 records
 #define LOG_K1_THREADS 256
+#endif
+#ifndef LOG_K1_GRID
+#define LOG_K1_GRID 512          // K1 workgroups: 2 per CU on MI355X's 256 CUs, all resident, each looping over
+                                 // tiles with the next tile prefetched (measured: 0.223 ms vs 0.249 at 2048)
+#endif
 #define LOG_TILE_PER 7            // pass-2 chunk: 512 threads x 7 records
 #define LOG_TILE_THREADS 512
 #define LOG_TILE (LOG_TILE_PER * LOG_TILE_THREADS)   // 3584 records: 56 KiB of 16-B records in LDS
@@ -53,7 +59,8 @@ struct LogSegSet {
 static constexpr int LOG_RB_STATS = LOG_NU * 256;
 static constexpr int LOG_RB_SEG = LOG_RB_STATS + (int)((sizeof(BatchStats) + 7) / 8);
 static constexpr int LOG_RB_CHUNKS = LOG_RB_SEG + LOG_NU;
-static constexpr int LOG_RB_WORDS = LOG_RB_CHUNKS + 1;
+static constexpr int LOG_RB_SEQ = LOG_RB_CHUNKS + 1;     // written last: the launch's sequence number
+static constexpr int LOG_RB_WORDS = LOG_RB_SEQ + 1;
 
 struct CollectArgs {
     int nunits;
@@ -62,6 +69,7 @@ struct CollectArgs {
     uint64_t cap;                // bucket region capacity of the batch buffer
     LogBucket *bk;               // out: [nunits * 256 + 1] pass-2 plan (device)
     unsigned long long *rb;      // out: readback block (pinned host memory)
+    unsigned long long seq;      // written to rb[LOG_RB_SEQ] after every other readback word
 };
 
 namespace gwo {

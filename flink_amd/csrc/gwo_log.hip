@@ -1033,7 +1033,7 @@ void launch_log_part(const int64_t *key, const int64_t *ts, const int64_t *val, 
                      int64_t *tmp, BatchStats *st, int64_t *side_key, int64_t *side_ts, int64_t *side_val,
                      unsigned long long *side_count, long long side_cap, int side_enabled, hipStream_t s) {
     int64_t grid = (n + LOG_TILE - 1) / LOG_TILE;
-    grid = grid < 1 ? 1 : (grid > 2048 ? 2048 : grid);
+    grid = grid < 1 ? 1 : (grid > LOG_K1_GRID ? LOG_K1_GRID : grid);
 #define GWO_K1(HV, S)                                                                                          \
     hipLaunchKernelGGL((log_part_kernel<HV, S>), dim3((int)grid), dim3(LOG_K1_THREADS), 0, s, key, ts, val, n, \
                        stride, g, base, nunits, cursor, cap, tmp, st, side_key, side_ts, side_val, side_count,   \
@@ -1127,6 +1127,13 @@ __global__ __launch_bounds__(1024) void log_collect_kernel(unsigned long long *c
             a.bk[nb] = E;
             a.rb[LOG_RB_CHUNKS] = s_chk[b];
         }
+    }
+    // the host spins on the sequence word: every other readback word must be visible first
+    __threadfence_system();
+    __syncthreads();
+    if (b == 0) {
+        __threadfence_system();
+        *(volatile unsigned long long *)&a.rb[LOG_RB_SEQ] = a.seq;
     }
 }
 

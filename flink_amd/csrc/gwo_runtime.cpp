@@ -67,6 +67,17 @@ gwo_status Handle::dalloc(void **p, size_t bytes) {
     return GWO_OK;
 }
 
+// Waits for an event by polling it (no blocking runtime wait: its wake-up latency varies widely
+// between hosts, and the fire's completion is on the watermark's critical path).
+gwo_status Handle::spin_event(hipEvent_t ev, const char *what) {
+    while (true) {
+        hipError_t e = hipEventQuery(ev);
+        if (e == hipSuccess) return GWO_OK;
+        if (e != hipErrorNotReady) return hipcheck(e, what);
+        for (int i = 0; i < 64; ++i) __builtin_ia32_pause();
+    }
+}
+
 gwo_status Handle::hipcheck(hipError_t e, const char *what) {
     if (e == hipSuccess) return GWO_OK;
     (void)hipGetLastError();
