@@ -54,10 +54,13 @@ struct LogState {
         bool active = false;
         int tmpx = 0, nunits = 0;
         long long base = 0;
+        unsigned long long after_seq = 0;   // a K1 readback with a higher sequence number follows it
+        bool has_event = false;
         uint64_t cap = 0;
         std::vector<uint64_t> counts;
     } pend;
-    hipEvent_t ev_split = nullptr;               // after the deferred pass 2's overflow flag readback
+    hipEvent_t ev_split = nullptr;               // after the deferred pass 2 (pipelined mode only)
+    unsigned long long seen_seq = 0;             // highest K1 readback sequence number observed complete
     unsigned *h_split_flag = nullptr;            // pinned, device-written [LOG_SLOTS]: pass-2 overflow flags
     unsigned *d_split_flag = nullptr;            // device view of h_split_flag
     // pipelined submission (gwo_set_pipelined_submit): the batch whose K1 is in flight, resolved by the
@@ -322,7 +325,11 @@ gwo_status Handle::log_split_dev(const LogJob &J, const unsigned long long *rbp)
                      L.d_split_flag + J.slot, (uint32_t)rbp[LOG_RB_CHUNKS], stream);
     GWO_TRY(launch_ok("log split"));
     prof_end(GWO_KERNEL_PARTITION, (int64_t)total);
-    GWO_TRY(hipcheck(hipEventRecord(L.ev_split, stream), "event"));
+    // completion is implied by the next K1's readback (stream order); only a pipelined K1, queued before
+    // this pass 2, needs an event (a marker between the kernels costs several microseconds)
+    L.pend.after_seq = L.seq;
+    L.pend.has_event = L.pipeline;
+    if (L.pipeline) GWO_TRY(hipcheck(hipEventRecord(L.ev_split, stream), "event"));
     L.pend.active = true;
     L.pend.tmpx = J.slot;
     L.pend.nunits = J.nunits;
@@ -344,7 +351,10 @@ gwo_status Handle::log_resolve_split() {
     LogState &L = *logst;
     if (!L.pend.active) return GWO_OK;
     // the event, not the stream: a pipelined K1 may be queued behind this pass 2
-    GWO_TRY(hipcheck(hipEventSynchronize(L.ev_split), "pass 2"));
+    if (L.seen_seq <= L.pend.after_seq) {
+        if (L.pend.has_event) GWO_TRY(spin_event(L.ev_split, "pass 2"));
+        else GWO_TRY(hipcheck(hipStreamSynchronize(stream), "pass 2"));
+    }
     L.pend.active = false;
     if (L.h_split_flag[L.pend.tmpx] == 0) return GWO_OK;
     for (int w = 0; w < L.pend.nunits; ++w) {
@@ -425,6 +435,7 @@ gwo_status Handle::log_wait_readback(int slot, unsigned long long seq) {
         __builtin_ia32_pause();
     }
     __atomic_thread_fence(__ATOMIC_ACQUIRE);
+    L.seen_seq = std::max(L.seen_seq, seq);
     return GWO_OK;
 }
 
