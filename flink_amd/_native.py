@@ -92,6 +92,7 @@ SIGNATURES = [
     ("gwo_kernel_stats", C.c_int, [_P, C.c_int32, _I64P, C.POINTER(C.c_double), _I64P]),
     ("gwo_reset_stats", C.c_int, [_P]),
     ("gwo_assign_key_groups", C.c_int, [_P, C.c_int64, C.c_int32, C.c_int32, C.c_int32, _P, _P, C.c_int32]),
+    ("gwo_assign_key_groups_utf16", C.c_int, [_P, _P, C.c_int64, C.c_int32, C.c_int32, _P, _P, _P, C.c_int32]),
     ("gwo_window_starts", C.c_int, [_P, C.c_int64, C.c_int64, C.c_int64, _P, C.c_int32]),
     ("gwo_comm_unique_id", C.c_int, [C.POINTER(C.c_uint8)]),
     ("gwo_comm_init", C.c_int, [_P, C.POINTER(C.c_uint8), C.c_int32, C.c_int32]),

@@ -161,6 +161,8 @@ void launch_refire_emit(const int64_t *key, const int64_t *val, const int64_t *r
 // result is in (k1, v1), 1 when in (k2, v2)
 int radix_sort_pairs(const uint32_t *keys, const uint32_t *vals, int64_t n, int key_bits, uint32_t *k1, uint32_t *v1,
                      uint32_t *k2, uint32_t *v2, uint32_t *hist, hipStream_t s);
+void launch_key_groups_utf16(const uint16_t *chars, const int64_t *offsets, int64_t n, int max_par, int par,
+                             int32_t *hash, int32_t *kg, int32_t *op, hipStream_t s);
 void launch_fire(const TableDesc &t, uint64_t cap, const AccPlan &plan, const ResultPlan &rp, int64_t start,
                  int64_t end, OutCols out, int reset, int live_word, hipStream_t s);
 

@@ -468,6 +468,22 @@ __global__ void key_groups_kernel(const int64_t *keys, int64_t n, int kind, int 
     }
 }
 
+// String keys: JDK String.hashCode (h = 31 * h + c over UTF-16 code units, wrapping) -> murmur -> key group.
+// One lane per string (keys are short; a long one just loops).
+__global__ void key_groups_utf16_kernel(const uint16_t *chars, const int64_t *offsets, int64_t n, int max_par, int par,
+                                        int32_t *hash, int32_t *kg, int32_t *op) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        uint32_t h = 0;
+        for (int64_t c = offsets[i], e = offsets[i + 1]; c < e; ++c) h = 31u * h + (uint32_t)chars[c];
+        const int32_t m = murmur_hash((int32_t)h);
+        const int32_t g = (max_par & (max_par - 1)) == 0 ? (m & (max_par - 1)) : m % max_par;
+        if (hash) hash[i] = (int32_t)h;
+        if (kg) kg[i] = g;
+        if (op) op[i] = g * par / max_par;  // KeyGroupRangeAssignment.java:118-119
+    }
+}
+
 __global__ void window_starts_kernel(const int64_t *ts, int64_t n, int64_t off, int64_t size, double inv,
                                      int64_t *out) {
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
@@ -766,6 +782,12 @@ void launch_key_groups(const int64_t *keys, int64_t n, int key_kind, int max_par
                        int32_t *op, hipStream_t s) {
     hipLaunchKernelGGL(key_groups_kernel, dim3(grid_for(n, 4)), dim3(256), 0, s, keys, n, key_kind, max_par, par,
                        kg, op);
+}
+
+void launch_key_groups_utf16(const uint16_t *chars, const int64_t *offsets, int64_t n, int max_par, int par,
+                             int32_t *hash, int32_t *kg, int32_t *op, hipStream_t s) {
+    hipLaunchKernelGGL(key_groups_utf16_kernel, dim3(grid_for(n, 1)), dim3(256), 0, s, chars, offsets, n, max_par, par,
+                       hash, kg, op);
 }
 
 void launch_window_starts(const int64_t *ts, int64_t n, int64_t offset, int64_t size, int64_t *out,

@@ -866,6 +866,63 @@ gwo_status gwo_assign_key_groups(const int64_t *keys, int64_t n, int32_t key_kin
     return stateless_run(device, (size_t)n, keys, 4, outs, 2, kg_body, &c);
 }
 
+gwo_status gwo_assign_key_groups_utf16(const uint16_t *chars, const int64_t *offsets, int64_t n,
+                                       int32_t max_parallelism, int32_t parallelism, int32_t *hash_out, int32_t *kg_out,
+                                       int32_t *op_out, int32_t device) {
+    if (n < 0 || !offsets || max_parallelism <= 0 || max_parallelism > 32768 || parallelism <= 0 ||
+        parallelism > max_parallelism)
+        return GWO_ERR_INVALID_ARGUMENT;
+    if (n == 0) return GWO_OK;
+    DeviceGuard guard_(device);
+    hipStream_t s;
+    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return GWO_ERR_HIP;
+    gwo_status st = GWO_OK;
+    std::vector<void *> owned;
+    auto dev_alloc = [&](size_t bytes) -> void * {
+        void *p = nullptr;
+        if (hipMalloc(&p, bytes + 8) != hipSuccess) {
+            st = GWO_ERR_OUT_OF_MEMORY;
+            return nullptr;
+        }
+        owned.push_back(p);
+        return p;
+    };
+    // offsets (n + 1) and the total code-unit count
+    const int64_t *d_off = offsets;
+    int64_t nchars = 0;
+    if (is_device_ptr(offsets)) {
+        if (hipMemcpy(&nchars, offsets + n, 8, hipMemcpyDeviceToHost) != hipSuccess) st = GWO_ERR_HIP;
+    } else {
+        nchars = offsets[n];
+        int64_t *p = (int64_t *)dev_alloc((size_t)(n + 1) * 8);
+        if (p) (void)hipMemcpyAsync(p, offsets, (size_t)(n + 1) * 8, hipMemcpyHostToDevice, s);
+        d_off = p;
+    }
+    if (st == GWO_OK && (nchars < 0 || (nchars > 0 && !chars))) st = GWO_ERR_INVALID_ARGUMENT;
+    const uint16_t *d_chars = chars;
+    if (st == GWO_OK && nchars > 0 && !is_device_ptr(chars)) {
+        uint16_t *p = (uint16_t *)dev_alloc((size_t)nchars * 2);
+        if (p) (void)hipMemcpyAsync(p, chars, (size_t)nchars * 2, hipMemcpyHostToDevice, s);
+        d_chars = p;
+    }
+    int32_t *outs[3] = {hash_out, kg_out, op_out}, *douts[3] = {nullptr, nullptr, nullptr};
+    for (int i = 0; i < 3 && st == GWO_OK; ++i) {
+        if (!outs[i]) continue;
+        douts[i] = is_device_ptr(outs[i]) ? outs[i] : (int32_t *)dev_alloc((size_t)n * 4);
+    }
+    if (st == GWO_OK) {
+        launch_key_groups_utf16(d_chars, d_off, n, max_parallelism, parallelism, douts[0], douts[1], douts[2], s);
+        if (hipGetLastError() != hipSuccess) st = GWO_ERR_HIP;
+        for (int i = 0; i < 3 && st == GWO_OK; ++i)
+            if (outs[i] && douts[i] != outs[i])
+                (void)hipMemcpyAsync(outs[i], douts[i], (size_t)n * 4, hipMemcpyDeviceToHost, s);
+    }
+    if (hipStreamSynchronize(s) != hipSuccess && st == GWO_OK) st = GWO_ERR_HIP;
+    for (void *p : owned) (void)hipFree(p);
+    (void)hipStreamDestroy(s);
+    return st;
+}
+
 struct WsCtx {
     int64_t n, off, size;
 };

@@ -26,6 +26,7 @@
  *   gwo_destroy           StreamOperator.close/dispose          SJ/api/operators/StreamOperator.java:96-110
  *   gwo_assign_key_groups KeyGroupRangeAssignment.assignToKeyGroup / computeOperatorIndexForKeyGroup
  *                                                               flink-runtime/.../state/KeyGroupRangeAssignment.java:48-73,118-119
+ *   gwo_assign_key_groups_utf16  the same for String keys (JDK String.hashCode over UTF-16 code units)
  *   gwo_comm_*            keyBy shuffle (KeyGroupStreamPartitioner + network stack) across the GPUs of a node
  *   gwo_partition_by_operator  KeyGroupStreamPartitioner.selectChannel over a batch (route step of the shuffle)
  *                                                               SJ/runtime/partitioner/KeyGroupStreamPartitioner.java:51-58
@@ -201,6 +202,14 @@ gwo_status gwo_reset_stats(gwo_handle *h);
 gwo_status gwo_assign_key_groups(const int64_t *keys, int64_t n, int32_t key_kind, int32_t max_parallelism,
                                  int32_t parallelism, int32_t *key_group_out, int32_t *operator_out,
                                  int32_t device);
+/* KeyGroupRangeAssignment for java.lang.String keys (the key selector of a String-keyed stream,
+ * KeyGroupRangeAssignment.java:60-73 over String.hashCode): key i is the UTF-16 code units
+ * chars[offsets[i] .. offsets[i + 1]) hashed as h = 31 * h + c (wrapping int32, JDK String.hashCode), then
+ * murmur -> key group -> operator index.  Any output may be NULL; hash_out receives the hashCodes.
+ * Host or device pointers. */
+gwo_status gwo_assign_key_groups_utf16(const uint16_t *chars, const int64_t *offsets, int64_t n,
+                                       int32_t max_parallelism, int32_t parallelism, int32_t *hash_out,
+                                       int32_t *key_group_out, int32_t *operator_out, int32_t device);
 /* TimeWindow.getWindowStartWithOffset over a timestamp column (Java '%' semantics). */
 gwo_status gwo_window_starts(const int64_t *ts, int64_t n, int64_t offset, int64_t size, int64_t *start_out,
                              int32_t device);

@@ -46,6 +46,25 @@ def test_key_group_kernel_bit_exact(F):
     assert kg.tolist() == [94, 86, 127, 113, 7, 126, 18, 113, 15, 51]
 
 
+def test_key_group_kernel_string_keys(F, golden):
+    """String keys: JDK String.hashCode over UTF-16 code units (surrogate pairs count as two units) ->
+    murmur -> key group, pinned by the reference's own String-key vectors
+    (RocksIncrementalCheckpointRescalingTest.java:55-92) and checked against the restatement."""
+    g = golden["key_groups_string"]
+    _, kg, op = F.assign_key_groups_strings(g["keys"], g["max_parallelism"], 1)
+    assert kg.tolist() == g["groups"] and op.tolist() == [0] * len(g["keys"])
+    rng = np.random.default_rng(1)
+    alphabet = list("abcXYZ019 _-") + ["\u00e9", "\u4e2d", "\U0001F600", "\uffff"]
+    keys = ["", "a", "campaign-42", "\U0001F600" * 3] + \
+        ["".join(rng.choice(alphabet, rng.integers(0, 40))) for _ in range(3000)]
+    for maxp, par in [(128, 1), (32768, 8), (10, 3)]:
+        h, kg, op = F.assign_key_groups_strings(keys, maxp, par)
+        want_h = [O.string_hash_code(k) for k in keys]
+        want = np.array([O.assign_to_key_group(x, maxp) for x in want_h])
+        assert h.tolist() == want_h
+        assert (kg == want).all() and (op == want * par // maxp).all()
+
+
 def test_key_group_kernel_int_keys(F):
     keys = np.arange(-5000, 5000)
     kg, _ = F.assign_key_groups(keys, 128, 1, key_kind="int")
