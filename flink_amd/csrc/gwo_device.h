@@ -136,6 +136,14 @@ __device__ __forceinline__ uint64_t part_hash(int64_t key) {
     return z ^ (z >> 31);
 }
 
+// Partition digit hash of the log layout (K1 and pass 2; the fire never recomputes a record's
+// partition): two 32-bit multiplies whose sum's top bits carry every key bit, ~4 instructions instead of
+// part_hash's ~24.  Independent of the fire's election hash (gwo_log.hip slot_mix: other multipliers).
+// A skewed key set only costs capacity re-runs and slow-path partitions, never a wrong result.
+__device__ __forceinline__ uint32_t digit_hash(int64_t key) {
+    return (uint32_t)key * 0xCC9E2D51u + (uint32_t)((uint64_t)key >> 32) * 0x1B873593u;
+}
+
 // Double.compareTo total order as a signed int64 key (doubleToLongBits canonicalises NaN).
 __device__ __host__ __forceinline__ int64_t f64_order_key(int64_t bits) {
     if ((bits & 0x7ff0000000000000LL) == 0x7ff0000000000000LL && (bits & 0x000fffffffffffffLL) != 0)

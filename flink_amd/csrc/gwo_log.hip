@@ -101,7 +101,7 @@ __global__ __launch_bounds__(LOG_K1_THREADS) void log_part_kernel(
     const int per = (nb + LOG_K1_THREADS - 1) / LOG_K1_THREADS;   // counters owned per thread (<= 4)
     const int tid = threadIdx.x;
     long long mn = 0x7fffffffffffffffLL, mx = (long long)0x8000000000000000LL;
-    unsigned long long acc = 0, late = 0, refire = 0, bad_ts = 0, out = 0, bad_kg = 0;
+    unsigned acc = 0, late = 0, refire = 0, bad_ts = 0, out = 0, bad_kg = 0;   // per thread: < 2^32 records
     int64_t kk[LOG_K1_PER], vv[LOG_K1_PER], tt[LOG_K1_PER];
     // unconditional loads of a tile (lanes past the end re-read the tile's first record and are
     // discarded); the next tile's loads are issued before this tile's write phase
@@ -141,7 +141,7 @@ __global__ __launch_bounds__(LOG_K1_THREADS) void log_part_kernel(
                 mx = u > mx ? u : mx;
                 long long w = u - base;
                 if (w >= 0 && w < nunits) {
-                    uint32_t b = (uint32_t)(w * 256 + (int)(part_hash(k) >> 56));
+                    uint32_t b = (uint32_t)(w * 256 + (int)(digit_hash(k) >> 24));
                     uint32_t r = atomicAdd(&s_cnt[b], 1u);
                     code[j] = (b << 16) | r;
                 } else {
@@ -247,7 +247,7 @@ __global__ __launch_bounds__(LOG_K1_THREADS) void log_part_kernel(
 
 // ------------------------------------------------------------------------------------------------
 // Pass 2 log_split: workgroup = one LOG_TILE chunk of one bucket (window w, coarse digit d).
-// Partition p = top lp bits of part_hash = d * F + f, F = 2^(lp-8).  Partition p of the segment owns
+// Partition p = top lp bits of digit_hash = d * F + f, F = 2^(lp-8).  Partition p of the segment owns
 // records [seg_base + f*pcap, + pcap); cnt[p] is its cursor (ends as its count, overflow -> rerun).
 // ------------------------------------------------------------------------------------------------
 template <bool HASV>
@@ -309,7 +309,7 @@ __global__ __launch_bounds__(LOG_TILE_THREADS) void log_split_kernel(const int64
         uint32_t i = j * LOG_TILE_THREADS + tid;
         code[j] = 0xffffffffu;
         if (i < m) {
-            uint32_t f = (uint32_t)(part_hash(kk[j]) >> (64 - lp)) & (uint32_t)(F - 1);
+            uint32_t f = (uint32_t)(digit_hash(kk[j]) >> (32 - lp)) & (uint32_t)(F - 1);
             uint32_t r = atomicAdd(&s_cnt[f], 1u);
             code[j] = (f << 16) | r;
         }
@@ -580,8 +580,8 @@ __device__ __forceinline__ int64_t word_combine(int op, int64_t a, int64_t b) {
     }
 }
 
-// Slot hash of the fire's election table: two 32-bit multiplies (part_hash, whose top bits picked the
-// partition, costs about 20 instructions); the top bits index the table, lower bits give the probe step.
+// Slot hash of the fire's election table: two 32-bit multiplies with other multipliers than digit_hash
+// (whose top bits picked the partition); the top bits index the table, lower bits give the probe step.
 __device__ __forceinline__ uint32_t slot_mix(int64_t k) {
     return (uint32_t)k * 0x9E3779B1u + (uint32_t)((uint64_t)k >> 32) * 0x85EBCA77u;
 }
