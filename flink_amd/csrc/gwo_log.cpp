@@ -210,7 +210,7 @@ int Handle::log_choose_lp(uint64_t batch_records) const {
     const LogState &L = *logst;
     uint64_t est = L.last_window_records;
     if (est == 0) est = std::max<uint64_t>((uint64_t)std::max<int64_t>(cfg.expected_keys, 0) * 2, batch_records * 8);
-    const uint64_t per = (uint64_t)FIRE_RCAP * 3 / 4;
+    const uint64_t per = (uint64_t)FIRE_RCAP * LOG_PART_FILL / 8;
     int lp = LOG_MIN_LP;
     while (lp < LOG_MAX_LP && ((uint64_t)1 << lp) * per < est) lp++;
     return lp;
