@@ -719,9 +719,10 @@ def _tumbling_oracle(k, t, v, batches, size, offset, lateness, agg, side_output=
     return op
 
 
+@pytest.mark.parametrize("side", [False, True])
 @pytest.mark.parametrize("layout", ["table", "auto"])
 @pytest.mark.parametrize("lateness", [1_500, 7_000])
-def test_tumbling_per_element_refire_with_lateness(F, lateness, layout):
+def test_tumbling_per_element_refire_with_lateness(F, lateness, layout, side):
     """allowedLateness > 0: a record landing in an already-fired window (before its cleanup time) is
     added and EventTimeTrigger.onElement FIREs at once -- one row per such record with the window's
     contents including it, in arrival order (WindowOperator.java:393-406).  Heavy disorder relative to
@@ -734,10 +735,11 @@ def test_tumbling_per_element_refire_with_lateness(F, lateness, layout):
     v = rng.integers(-50, 100, n).astype(np.int64)
     b = G.punctuated_watermarks(t, 400, 500)
     ref = _tumbling_oracle(k, t, v, b, 2_000, 300, lateness,
-                           O.MultiAgg([O.SumLongAgg(), O.CountAgg(), O.MaxAgg(), O.MinAgg()]))
+                           O.MultiAgg([O.SumLongAgg(), O.CountAgg(), O.MaxAgg(), O.MinAgg()]), side_output=side)
     op = F.GpuWindowOperator(F.TumblingEventTimeWindows.of(2_000, 300),
                              F.MultiAggregate(F.SumAggregate(), F.CountAggregate(), F.MaxAggregate(), F.MinAggregate()),
-                             allowed_lateness=lateness, state_layout=layout, expected_keys=2_000_000 if layout == "auto" else 0)
+                             allowed_lateness=lateness, state_layout=layout, side_output_late_data=side,
+                             expected_keys=2_000_000 if layout == "auto" else 0)
     _run_batches(op, k, t, v, b)
     got = sorted(op.output)
     want = sorted((r.key, r.start, r.end, r.result) for r in ref.output)
@@ -746,7 +748,11 @@ def test_tumbling_per_element_refire_with_lateness(F, lateness, layout):
     assert got == want
     n_windows = len({(r.key, r.start) for r in ref.output})
     assert len(want) > n_windows + 500          # many per-element re-fire rows
-    assert op.num_late_records_dropped == ref.num_late_records_dropped > 0
+    if side:   # late records beyond the lateness go to the side output instead of being counted
+        assert sorted(op.side_output) == sorted((r[0], r[1], r[2]) for r in ref.side_output) and op.side_output
+        assert op.num_late_records_dropped == ref.num_late_records_dropped == 0
+    else:
+        assert op.num_late_records_dropped == ref.num_late_records_dropped > 0
     op.close()
 
 
