@@ -83,6 +83,9 @@ SIGNATURES = [
     ("gwo_drain_side_output", C.c_int, [_P, C.POINTER(GwoSideOut), C.c_int64, _I64P]),
     ("gwo_current_watermark", C.c_int, [_P, _I64P]),
     ("gwo_state_size", C.c_int, [_P, _I64P]),
+    ("gwo_snapshot_rows", C.c_int, [_P, _I64P, C.POINTER(C.c_int32)]),
+    ("gwo_snapshot", C.c_int, [_P, _P, _P, _P, C.c_int64, _I64P, _I64P]),
+    ("gwo_restore", C.c_int, [_P, _P, _P, _P, C.c_int64, C.c_int64]),
     ("gwo_sync", C.c_int, [_P]),
     ("gwo_get_stream", C.c_int, [_P, C.POINTER(_P)]),
     ("gwo_last_error", C.c_char_p, [_P]),

@@ -156,6 +156,10 @@ struct Handle {
     gwo_status drain(const gwo_out *cols, int64_t cap, int64_t *n_out);
     gwo_status drain_side(const gwo_side_out *cols, int64_t cap, int64_t *n_out);
     gwo_status state_size(int64_t *entries);
+    gwo_status snapshot_supported();
+    gwo_status snapshot_rows(int64_t *n_rows);
+    gwo_status snapshot(int64_t *key, int64_t *wstart, int64_t *words, int64_t cap, int64_t *n_out);
+    gwo_status restore(const int64_t *key, const int64_t *wstart, const int64_t *words, int64_t n, int64_t new_wm);
 
     gwo_status fail(gwo_status s, const char *fmt, ...);
     gwo_status poison(gwo_status s, const char *what);

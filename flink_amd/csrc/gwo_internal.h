@@ -149,6 +149,10 @@ void launch_insert(const int64_t *key, const int64_t *ts, const void *val, int64
                    BatchStats *stats, const RingDesc &ring, hipStream_t s);
 
 // Emits every occupied entry (with live_word >= 0: every entry whose word live_word is > 0).
+void launch_snapshot(const TableDesc &t, uint64_t cap, const AccPlan &p, int64_t start, int64_t *key,
+                     int64_t *wstart, int64_t *words, unsigned long long *count, long long out_cap, hipStream_t s);
+void launch_restore(const int64_t *key, const int64_t *wstart, const int64_t *words, int64_t n, const AccPlan &p,
+                    const WindowGeom &g, const TableDesc *dir, long long dir_base, int dir_len, hipStream_t s);
 void launch_refire_collect(const int64_t *ts, int64_t n, const WindowGeom &g, long long dir_base, int dir_len,
                            uint32_t *blk, int64_t *r_idx, long long *r_u, hipStream_t s);
 void launch_refire_slots(const int64_t *key, const int64_t *r_idx, const long long *r_u, int64_t m, const AccPlan &p,

@@ -702,6 +702,63 @@ __global__ __launch_bounds__(1024) void refire_emit_kernel(const int64_t *__rest
     }
 }
 
+// ------------------------------------------------------------------------------------------------
+// Snapshot / restore of the tumbling table state (the heap backend's per-(key, namespace) entries,
+// CopyOnWriteStateMapSnapshot.java:127-129): raw accumulator words, so a restore continues exactly.
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void snapshot_kernel(TableDesc t, uint64_t cap, AccPlan p, int64_t start,
+                                                       int64_t *key, int64_t *wstart, int64_t *words,
+                                                       unsigned long long *count, long long out_cap) {
+    for (uint64_t b0 = (uint64_t)blockIdx.x * 256; b0 < cap + 1; b0 += (uint64_t)gridDim.x * 256) {
+        const uint64_t i = b0 + threadIdx.x;
+        const int64_t *e = i <= cap ? fire_entry(t, cap, p.stride, i) : nullptr;
+        const bool occ = e && (i < cap ? e[0] != GWO_EMPTY_KEY : e[0] != 0);
+        const unsigned long long pos = block_reserve(occ ? 1u : 0u, count);
+        if (occ && (long long)pos < out_cap) {
+            key[pos] = i < cap ? e[0] : GWO_EMPTY_KEY;
+            wstart[pos] = start;
+            for (int w = 0; w < p.nwords; ++w) words[pos * p.nwords + w] = e[1 + w];
+        }
+    }
+}
+
+// Rows whose key group is outside [kg_lo, kg_hi] belong to another subtask (rescaling) and are skipped.
+__global__ __launch_bounds__(256) void restore_kernel(const int64_t *key, const int64_t *wstart, const int64_t *words,
+                                                      int64_t n, AccPlan p, WindowGeom g,
+                                                      const TableDesc *__restrict__ dir, long long dir_base,
+                                                      int dir_len) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t j0 = (int64_t)blockIdx.x * blockDim.x; j0 < n; j0 += stride) {
+        const int64_t j = j0 + threadIdx.x;
+        bool claimed = false;
+        unsigned long long *occ = nullptr;
+        if (j < n) {
+            const int64_t k = key[j];
+            const int32_t kg = key_group(k, g.key_kind, g.max_par);
+            const long long d = fdiv_floor(jsub(wstart[j], g.unit_off_mod), g.unit, g.inv_unit) - dir_base;
+            if (kg >= g.kg_lo && kg <= g.kg_hi && d >= 0 && d < dir_len) {
+                const TableDesc t = dir[d];
+                int64_t *acc = find_or_insert(t, p.stride, k, claimed);
+                occ = t.occ;
+                for (int w = 0; w < p.nwords; ++w) atomic_combine(acc + w, p.op[w], words[j * p.nwords + w]);
+            }
+        }
+        count_claims(occ, claimed);
+    }
+}
+
+void launch_snapshot(const TableDesc &t, uint64_t cap, const AccPlan &p, int64_t start, int64_t *key,
+                     int64_t *wstart, int64_t *words, unsigned long long *count, long long out_cap, hipStream_t s) {
+    hipLaunchKernelGGL(snapshot_kernel, dim3(grid_for((int64_t)cap + 1, 1, 4096)), dim3(256), 0, s, t, cap, p, start,
+                       key, wstart, words, count, out_cap);
+}
+
+void launch_restore(const int64_t *key, const int64_t *wstart, const int64_t *words, int64_t n, const AccPlan &p,
+                    const WindowGeom &g, const TableDesc *dir, long long dir_base, int dir_len, hipStream_t s) {
+    hipLaunchKernelGGL(restore_kernel, dim3(grid_for(n, 1, 4096)), dim3(256), 0, s, key, wstart, words, n, p, g, dir,
+                       dir_base, dir_len);
+}
+
 void launch_refire_collect(const int64_t *ts, int64_t n, const WindowGeom &g, long long dir_base, int dir_len,
                            uint32_t *blk, int64_t *r_idx, long long *r_u, hipStream_t s) {
     hipLaunchKernelGGL(refire_count_kernel, dim3(RF_BLOCKS), dim3(RF_THREADS), 0, s, ts, n, g, dir_base, dir_len, blk);

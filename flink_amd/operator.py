@@ -206,6 +206,35 @@ class GpuWindowOperator:
         N.check(self._lib.gwo_current_watermark(self._h, C.byref(n)), self._h)
         return n.value
 
+    def snapshot_state(self):
+        """Checkpoint of the keyed window state (tumbling, table layout): dict of numpy columns key,
+        window_start, words[n, n_words] and the watermark (gwo.h gwo_snapshot)."""
+        self.flush()
+        n, nw = C.c_int64(), C.c_int32()
+        N.check(self._lib.gwo_snapshot_rows(self._h, C.byref(n), C.byref(nw)), self._h, "gwo_snapshot_rows")
+        m = n.value
+        key = np.empty(max(m, 1), np.int64)
+        start = np.empty(max(m, 1), np.int64)
+        words = np.empty((max(m, 1), nw.value), np.int64)
+        got, wm = C.c_int64(), C.c_int64()
+        N.check(self._lib.gwo_snapshot(self._h, _ptr(key), _ptr(start), _ptr(words), m, C.byref(got), C.byref(wm)),
+                self._h, "gwo_snapshot")
+        g = got.value
+        return {"key": key[:g], "window_start": start[:g], "words": words[:g], "watermark": wm.value}
+
+    def restore_state(self, snap):
+        """initializeState from one or more snapshots (a list restores a rescaled job: rows outside this
+        subtask's KeyGroupRange are skipped)."""
+        snaps = snap if isinstance(snap, (list, tuple)) else [snap]
+        key = np.ascontiguousarray(np.concatenate([x["key"] for x in snaps]), dtype=np.int64)
+        start = np.ascontiguousarray(np.concatenate([x["window_start"] for x in snaps]), dtype=np.int64)
+        words = np.ascontiguousarray(np.concatenate([x["words"] for x in snaps]), dtype=np.int64)
+        wm = min(x["watermark"] for x in snaps)
+        n = len(key)
+        if n == 0:
+            key, start, words = np.zeros(1, np.int64), np.zeros(1, np.int64), np.zeros((1, 1), np.int64)
+        N.check(self._lib.gwo_restore(self._h, _ptr(key), _ptr(start), _ptr(words), n, wm), self._h, "gwo_restore")
+
     def state_size(self) -> int:
         n = C.c_int64()
         N.check(self._lib.gwo_state_size(self._h, C.byref(n)), self._h)

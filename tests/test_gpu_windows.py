@@ -779,3 +779,84 @@ def test_tumbling_refire_avg_and_float_sum(F):
     assert [g[:3] for g in got] == [w[:3] for w in want]
     np.testing.assert_allclose([g[3] for g in got], [w[3] for w in want], rtol=FLOAT_RTOL)
     op.close()
+
+
+@pytest.mark.parametrize("lateness", [0, 3_000])
+def test_snapshot_restore_continues_exactly(F, lateness):
+    """Checkpoint mid-stream (raw accumulators + watermark), restore into a fresh operator, continue:
+    the rows before the checkpoint plus the restored operator's rows equal the uninterrupted oracle
+    run (no window lost, none emitted twice; with allowedLateness the restored windows still re-fire)."""
+    rng = np.random.default_rng(21 + lateness)
+    n = 40_000
+    k = rng.integers(0, 500, n).astype(np.int64)
+    t = (np.sort(rng.integers(0, 300_000, n)) + rng.integers(0, 4_000, n)).astype(np.int64)
+    v = rng.integers(-100, 100, n).astype(np.int64)
+    b = G.punctuated_watermarks(t, 1_000, 1_000)
+    agg_o = O.MultiAgg([O.SumLongAgg(), O.CountAgg(), O.MaxAgg()])
+    ref = _tumbling_oracle(k, t, v, b, 5_000, 0, lateness, agg_o)
+    mk_op = lambda: F.GpuWindowOperator(F.TumblingEventTimeWindows.of(5_000),
+                                        F.MultiAggregate(F.SumAggregate(), F.CountAggregate(), F.MaxAggregate()),
+                                        allowed_lateness=lateness, state_layout="table")
+    half = len(b) // 2
+    a = mk_op()
+    prev = 0
+    for end, wm in b[:half]:
+        a.process_batch(k[prev:end], t[prev:end], v[prev:end])
+        a.process_watermark(wm)
+        prev = end
+    snap = a.snapshot_state()
+    assert len(snap["key"]) == a.state_size() > 0 and snap["watermark"] == b[half - 1][1]
+    rows, late = list(a.output), a.num_late_records_dropped
+    a.close()
+    c = mk_op()
+    c.restore_state(snap)
+    assert c.state_size() == len(snap["key"]) and c.current_watermark == snap["watermark"]
+    _run_batches(c, k[prev:], t[prev:], v[prev:], [(e - prev, w) for e, w in b[half:]])
+    got = sorted(rows + list(c.output))
+    assert got == sorted((r.key, r.start, r.end, r.result) for r in ref.output)
+    assert late + c.num_late_records_dropped == ref.num_late_records_dropped
+    c.close()
+
+
+def test_snapshot_restore_rescales_by_key_group(F):
+    """Rescale 1 -> 2 subtasks: both new subtasks restore the same snapshot and keep only their
+    KeyGroupRange (computeKeyGroupRangeForOperatorIndex); each then receives its keys' records (as the
+    keyBy partitioner routes them).  The union of outputs equals the single-operator oracle."""
+    rng = np.random.default_rng(4)
+    n = 30_000
+    k = rng.integers(0, 2_000, n).astype(np.int64)
+    t = (np.sort(rng.integers(0, 200_000, n)) + rng.integers(0, 2_000, n)).astype(np.int64)
+    v = rng.integers(0, 50, n).astype(np.int64)
+    b = G.punctuated_watermarks(t, 1_000, 2_000)
+    ref = _tumbling_oracle(k, t, v, b, 4_000, 0, 0, O.SumLongAgg())
+    half = len(b) // 2
+    a = F.GpuWindowOperator(F.TumblingEventTimeWindows.of(4_000), F.SumAggregate(), state_layout="table",
+                            max_parallelism=128)
+    prev = 0
+    for end, wm in b[:half]:
+        a.process_batch(k[prev:end], t[prev:end], v[prev:end])
+        a.process_watermark(wm)
+        prev = end
+    snap = a.snapshot_state()
+    rows = list(a.output)
+    a.close()
+    kg, _ = F.assign_key_groups(k, 128, 1)
+    restored = 0
+    for idx in range(2):
+        r = F.compute_key_group_range_for_operator_index(128, 2, idx)
+        op = F.GpuWindowOperator(F.TumblingEventTimeWindows.of(4_000), F.SumAggregate(), state_layout="table",
+                                 max_parallelism=128, key_group_range=(r.start_key_group, r.end_key_group))
+        op.restore_state([snap])
+        restored += op.state_size()
+        mine = (kg >= r.start_key_group) & (kg <= r.end_key_group)
+        p0 = prev
+        for end, wm in b[half:]:
+            sel = np.nonzero(mine[p0:end])[0] + p0
+            op.process_batch(k[sel], t[sel], v[sel])
+            op.process_watermark(wm)
+            p0 = end
+        op.end_input()
+        rows += list(op.output)
+        op.close()
+    assert restored == len(snap["key"])
+    assert sorted(rows) == sorted((r.key, r.start, r.end, r.result) for r in ref.output)
