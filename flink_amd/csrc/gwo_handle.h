@@ -219,6 +219,7 @@ struct Handle {
     gwo_status slide_init();
     void slide_free();
     gwo_status fire_sliding(int64_t new_wm);
+    gwo_status slide_restore_anchor();
     // sessions (gwo_session.cpp)
     gwo_status sess_alloc(uint64_t cap, Table &t);
     gwo_status sess_read_err();

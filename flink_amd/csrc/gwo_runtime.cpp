@@ -402,8 +402,8 @@ gwo_status Handle::refire_rows(const int64_t *k, const int64_t *t, const int64_t
 
 // ---- snapshot / restore (tumbling, table layout) -------------------------------------------------
 gwo_status Handle::snapshot_supported() {
-    if (cfg.assigner != GWO_ASSIGNER_TUMBLING || logst)
-        return fail(GWO_ERR_UNSUPPORTED, "snapshot/restore: tumbling windows with the table layout only");
+    if (cfg.assigner == GWO_ASSIGNER_SESSION || logst)
+        return fail(GWO_ERR_UNSUPPORTED, "snapshot/restore: tumbling or sliding windows with the table layout only");
     return GWO_OK;
 }
 
@@ -450,9 +450,9 @@ gwo_status Handle::restore(const int64_t *key, const int64_t *wstart, const int6
     if (!tables.empty() || wm != (int64_t)0x8000000000000000LL)
         return fail(GWO_ERR_STATE, "restore: the handle already holds state");
     wm = new_wm;
-    if (n == 0) return GWO_OK;
+    if (n == 0) return slide ? slide_restore_anchor() : GWO_OK;
     const int NW = plan.nwords;
-    // host view of the window starts (to size the tables); the rows themselves go to the device
+    // host view of the window (sliding: pane) starts (to size the tables); the rows themselves go to the device
     std::vector<int64_t> hs((size_t)n);
     GWO_TRY(hipcheck(hipMemcpy(hs.data(), wstart, (size_t)n * 8, hipMemcpyDefault), "restore starts"));
     std::map<long long, uint64_t> per_unit;
@@ -507,6 +507,7 @@ gwo_status Handle::restore(const int64_t *key, const int64_t *wstart, const int6
             ++it;
         }
     }
+    if (st == GWO_OK && slide) st = slide_restore_anchor();
     return st;
 }
 

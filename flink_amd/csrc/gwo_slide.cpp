@@ -157,6 +157,20 @@ gwo_status Handle::ring_rebuild() {
     return GWO_OK;
 }
 
+// After gwo_restore: every window that ends at or before the restored watermark fired before the
+// checkpoint, so the next window to fire is the first one open at it; the ring total is rebuilt from
+// the restored panes.
+gwo_status Handle::slide_restore_anchor() {
+    SlideState &S = *slide;
+    __int128 j = fdiv128((__int128)wm - cfg.size + 1 - S.om, cfg.slide) + 1;
+    const __int128 j_lo = fdiv128((__int128)GWO_LONG_MIN_H + 2 * (__int128)cfg.size + cfg.slide, cfg.slide);
+    const __int128 j_hi = fdiv128((__int128)GWO_LONG_MAX_H - 2 * (__int128)cfg.size - cfg.slide, cfg.slide);
+    S.J = std::max(j_lo, std::min(j_hi, j));
+    S.j_set = true;
+    if (S.ring) GWO_TRY(ring_rebuild());
+    return GWO_OK;
+}
+
 gwo_status Handle::fire_sliding(int64_t new_wm) {
     SlideState &S = *slide;
     // first window that is not fired at new_wm: start_j + size - 1 > wm

@@ -167,7 +167,8 @@ gwo_status gwo_current_watermark(gwo_handle *h, int64_t *wm);
 /* Number of (key, window) entries currently held (device-resident state). */
 gwo_status gwo_state_size(gwo_handle *h, int64_t *entries);
 
-/* Checkpoint / restore of the keyed window state (tumbling windows, table layout -- the heap
+/* Checkpoint / restore of the keyed window state (tumbling and sliding windows, table layout; sliding
+ * rows carry pane starts -- the heap
  * backend's (key, TimeWindow, accumulator) entries, CopyOnWriteStateMapSnapshot.java:127-129, and the
  * watermark that the restored timers imply).  gwo_snapshot_rows gives the row count and the accumulator
  * words per row; gwo_snapshot writes key, window start and the raw words (row-major, n_words per row)
@@ -175,7 +176,7 @@ gwo_status gwo_state_size(gwo_handle *h, int64_t *entries);
  * same configuration re-creates the entries whose key group lies in ITS KeyGroupRange (rows of other
  * key groups are skipped, so the union of old snapshots restores a rescaled job) and adopts the
  * watermark; windows whose end it already passed count as fired (emitted before the checkpoint).
- * Other assigners/layouts: GWO_ERR_UNSUPPORTED. */
+ * Sessions and the log layout: GWO_ERR_UNSUPPORTED. */
 gwo_status gwo_snapshot_rows(gwo_handle *h, int64_t *n_rows, int32_t *n_words);
 gwo_status gwo_snapshot(gwo_handle *h, int64_t *key, int64_t *window_start, int64_t *words, int64_t cap,
                         int64_t *n_out, int64_t *watermark);

@@ -860,3 +860,41 @@ def test_snapshot_restore_rescales_by_key_group(F):
         op.close()
     assert restored == len(snap["key"])
     assert sorted(rows) == sorted((r.key, r.start, r.end, r.result) for r in ref.output)
+
+
+@pytest.mark.parametrize("ring", [True, False])
+def test_snapshot_restore_sliding_panes(F, ring):
+    """Sliding windows checkpoint their panes; the restored operator anchors the next window to fire
+    at the restored watermark and rebuilds the running ring total (invertible aggregates) from the panes."""
+    rng = np.random.default_rng(8)
+    n = 30_000
+    k = rng.integers(0, 300, n).astype(np.int64)
+    t = (np.sort(rng.integers(0, 120_000, n)) + rng.integers(0, 1_500, n)).astype(np.int64)
+    v = rng.integers(0, 1_000, n).astype(np.int64)
+    b = G.punctuated_watermarks(t, 700, 1_500)
+    agg_o = O.AvgAgg() if ring else O.MultiAgg([O.MinAgg(), O.MaxAgg()])
+    mk = lambda: F.GpuWindowOperator(F.SlidingEventTimeWindows.of(6_000, 2_000),
+                                     F.AverageAggregate() if ring else F.MultiAggregate(F.MinAggregate(), F.MaxAggregate()))
+    ref = O.WindowOperatorOracle(O.SlidingEventTimeWindows(6_000, 2_000), agg_o)
+    prev = 0
+    for end, wm in b:
+        for i in range(prev, end):
+            ref.process_element(int(k[i]), int(t[i]), int(v[i]))
+        ref.process_watermark(wm)
+        prev = end
+    ref.process_watermark(LONG_MAX)
+    half = len(b) // 2
+    a = mk()
+    prev = 0
+    for end, wm in b[:half]:
+        a.process_batch(k[prev:end], t[prev:end], v[prev:end])
+        a.process_watermark(wm)
+        prev = end
+    snap = a.snapshot_state()
+    rows = list(a.output)
+    a.close()
+    c = mk()
+    c.restore_state(snap)
+    _run_batches(c, k[prev:], t[prev:], v[prev:], [(e - prev, w) for e, w in b[half:]])
+    assert sorted(rows + list(c.output)) == sorted((r.key, r.start, r.end, r.result) for r in ref.output)
+    c.close()
