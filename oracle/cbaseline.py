@@ -40,11 +40,19 @@ def run_tumbling(keys, ts, vals, batches, size, offset=0, lateness=0, threads=1,
     args = lambda out: (_p(k), _p(t), _p(v), C.c_int64(len(k)), _p(be), _p(bw), C.c_int(len(be)), C.c_int64(size),
                         C.c_int64(offset), C.c_int64(lateness), C.c_int(threads), C.c_int32(max_par), out,
                         C.byref(cs), C.byref(late))
-    n = f(*args(None))
-    out = None
-    if rows:
-        out = np.empty((n, 7), np.int64)
-        f(*args(_p(out)))
+    if not rows:
+        f(*args(None))
+        return None, cs.value, late.value
+    g = lib().wo_tumbling_rows
+    g.restype = C.c_int64
+    buf = C.c_void_p()
+    n = g(_p(k), _p(t), _p(v), C.c_int64(len(k)), _p(be), _p(bw), C.c_int(len(be)), C.c_int64(size),
+          C.c_int64(offset), C.c_int64(lateness), C.c_int(threads), C.c_int32(max_par), C.byref(buf),
+          C.byref(cs), C.byref(late))
+    out = np.empty((n, 7), np.int64)
+    if n:
+        C.memmove(out.ctypes.data, buf, n * 7 * 8)
+    lib().wo_free(buf)
     return out, cs.value, late.value
 
 
@@ -52,3 +60,14 @@ def time_tumbling(keys, ts, vals, batches, size, threads):
     t0 = time.perf_counter()
     run_tumbling(keys, ts, vals, batches, size, threads=threads, rows=False)
     return time.perf_counter() - t0
+
+
+def row_checksum(rows) -> int:
+    """The C twin's order-independent output checksum (window_oracle.c emit()): the wrapping sum over
+    rows of an FNV-1a-style hash of the row's 7 words (key, start, end, sum, min, max, count)."""
+    r = np.ascontiguousarray(rows, np.int64).view(np.uint64)
+    h = np.full(r.shape[0], 1469598103934665603, np.uint64)
+    with np.errstate(over="ignore"):
+        for c in range(r.shape[1]):
+            h = (h ^ r[:, c]) * np.uint64(1099511628211)
+        return int(h.sum(dtype=np.uint64))

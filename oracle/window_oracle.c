@@ -272,9 +272,30 @@ static void *run_job(void *arg) {
  * *checksum = sum of per-row FNV hashes (order independent); *late = numLateRecordsDropped.
  * If rows != NULL it must hold 7 * (returned rows) int64 (call once with NULL to size).
  */
+static int64_t run(const int64_t *key, const int64_t *ts, const int64_t *val, int64_t n, const int64_t *bend,
+                   const int64_t *bwm, int nb, int64_t size, int64_t offset, int64_t lateness, int nthreads,
+                   int32_t max_par, int store, int64_t *rows, int64_t **rows_out, uint64_t *checksum, int64_t *late);
+
 int64_t wo_tumbling(const int64_t *key, const int64_t *ts, const int64_t *val, int64_t n, const int64_t *bend,
                     const int64_t *bwm, int nb, int64_t size, int64_t offset, int64_t lateness, int nthreads,
                     int32_t max_par, int64_t *rows, uint64_t *checksum, int64_t *late) {
+    return run(key, ts, val, n, bend, bwm, nb, size, offset, lateness, nthreads, max_par, rows != NULL, rows, NULL,
+               checksum, late);
+}
+
+/* One pass that also returns the rows: *rows_out = malloc'd [returned rows][7] (free with wo_free). */
+int64_t wo_tumbling_rows(const int64_t *key, const int64_t *ts, const int64_t *val, int64_t n, const int64_t *bend,
+                         const int64_t *bwm, int nb, int64_t size, int64_t offset, int64_t lateness, int nthreads,
+                         int32_t max_par, int64_t **rows_out, uint64_t *checksum, int64_t *late) {
+    return run(key, ts, val, n, bend, bwm, nb, size, offset, lateness, nthreads, max_par, 1, NULL, rows_out,
+               checksum, late);
+}
+
+void wo_free(void *p) { free(p); }
+
+static int64_t run(const int64_t *key, const int64_t *ts, const int64_t *val, int64_t n, const int64_t *bend,
+                   const int64_t *bwm, int nb, int64_t size, int64_t offset, int64_t lateness, int nthreads,
+                   int32_t max_par, int store, int64_t *rows, int64_t **rows_out, uint64_t *checksum, int64_t *late) {
     if (nthreads < 1) nthreads = 1;
     /* keyBy routing: subtask = computeOperatorIndexForKeyGroup(kg) */
     int64_t *cnt = (int64_t *)calloc(nthreads + 1, sizeof(int64_t));
@@ -295,15 +316,21 @@ int64_t wo_tumbling(const int64_t *key, const int64_t *ts, const int64_t *val, i
     for (int t = 0; t < nthreads; ++t) {
         subs[t].mask = 1023;
         subs[t].slot = (int64_t *)calloc(1024, sizeof(int64_t));
-        subs[t].store_rows = rows != NULL;
+        subs[t].store_rows = store;
         jobs[t] = (Job){&subs[t], key, ts, val, idx + cnt[t], cnt[t + 1] - cnt[t], bend, bwm, nb, size, offset, lateness};
         pthread_create(&th[t], NULL, run_job, &jobs[t]);
     }
     int64_t total = 0;
     uint64_t cs = 0;
     int64_t lt = 0;
+    for (int t = 0; t < nthreads; ++t) pthread_join(th[t], NULL);
+    if (rows_out) {
+        int64_t all = 0;
+        for (int t = 0; t < nthreads; ++t) all += subs[t].nout;
+        *rows_out = (int64_t *)malloc((size_t)(all ? all : 1) * 7 * sizeof(int64_t));
+        rows = *rows_out;
+    }
     for (int t = 0; t < nthreads; ++t) {
-        pthread_join(th[t], NULL);
         if (rows) memcpy(rows + total * 7, subs[t].out, subs[t].nout * 7 * sizeof(int64_t));
         total += subs[t].nout;
         cs += subs[t].checksum;
