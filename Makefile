@@ -37,13 +37,3 @@ clean:
 	rm -rf build $(LIB)
 
 .PHONY: all clean
-
-# Profiling variant of the library (per-phase s_memtime printout of the log fire, GWO_FIRE_XP=16).
-PROF_LIB := flink_amd/libgwo_prof.so
-$(BUILD)/gwo_log_prof.hip.o: flink_amd/csrc/gwo_log.hip $(HDRS)
-	@mkdir -p $(BUILD)
-	$(HIPCC) $(HIPFLAGS) -mllvm -amdgpu-atomic-optimizer-strategy=None -DGWO_FIRE_PROF -c $< -o $@
-$(PROF_LIB): $(filter-out $(BUILD)/gwo_log.hip.o,$(HIP_OBJS)) $(BUILD)/gwo_log_prof.hip.o $(CPP_OBJS)
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -L$(ROCM)/lib -lamdhip64 -lrccl -Wl,-rpath,$(ROCM)/lib
-prof: $(PROF_LIB)
-.PHONY: prof

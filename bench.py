@@ -8,11 +8,16 @@ stream is 1e9 records (16.7M per step); the input is generated into HBM before t
 
 A "step" = one watermark interval: gwo_submit(batch) (classify + partition into the windows'
 record logs) + gwo_advance_watermark (fire: fold every window whose end passed and
-emit its rows).  The default warmup (12 steps) covers one full window lifecycle (first fire at step
-10), so the timed steps are the engine's steady state (device pools warm, output sized); 20 timed
-steps include two fires.  With --gpus N the job runs one process per GPU; every rank generates its
-own slice of a 100M*N-key stream and gwo_submit shuffles records to their key-group owner with an
+emit its rows).  The operator reserves its steady-state device memory at creation from the
+distinct-keys hint, so any warmup >= 0 measures the steady state; 20 timed steps include two fires
+(a window fires every 10 steps).  With --gpus N the job runs one process per GPU; every rank generates
+its own slice of a 100M*N-key stream and gwo_submit shuffles records to their key-group owner with an
 RCCL all-to-all (weak scaling).
+
+The roofline kernel is the one with the most time in the timed region (HIP events on the handle's
+stream around K1 and the fire only -- each timed launch adds two stream markers).  host_fed is a
+separate, smaller run: pinned host columns in, fired rows drained to pinned host memory (PCIe-bound,
+never the headline value).
 
 Prints ONE JSON line (rank 0).
 """
@@ -33,7 +38,7 @@ def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
-    p.add_argument("--warmup", type=int, default=12)   # one full window lifecycle: pools warm
+    p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--records-per-gpu", type=int, default=1_000_000_000)
     p.add_argument("--keys-per-gpu", type=int, default=100_000_000)
     p.add_argument("--span-ms", type=int, default=60_000)
@@ -42,7 +47,12 @@ def parse():
     p.add_argument("--lag-ms", type=int, default=1_000)
     p.add_argument("--max-parallelism", type=int, default=32768)
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--cpu-sample", type=int, default=2_000_000)
+    p.add_argument("--cpu-scale", type=int, default=8,
+                   help="CPU baseline sample: the C4 stream with keys and records per step divided by this")
+    p.add_argument("--layout", choices=["auto", "log", "table"], default="auto",
+                   help="device state layout (auto = the log layout at this cardinality)")
+    p.add_argument("--no-host-fed", action="store_true")
+    p.add_argument("--host-fed-steps", type=int, default=12)
     p.add_argument("--no-profile", action="store_true",
                    help="no per-kernel HIP events in the timed region (diagnostic: the events' own cost)")
     p.add_argument("--pipeline", action="store_true",
@@ -111,7 +121,7 @@ def main():
     rec_per_window = R * a.window_ms // span
     exp_keys = int(a.keys_per_gpu * (1.0 - np.exp(-rec_per_window / a.keys_per_gpu)))
     op = F.GpuWindowOperator(F.TumblingEventTimeWindows.of(a.window_ms), agg, max_parallelism=a.max_parallelism,
-                             key_group_range=rng, device=local, expected_keys=exp_keys)
+                             key_group_range=rng, device=local, expected_keys=exp_keys, state_layout=a.layout)
     h = op.handle
     if a.pipeline:   # K1 of batch i queues before batch i-1 resolves (gwo.h gwo_set_pipelined_submit)
         N.check(lib.gwo_set_pipelined_submit(h, 1), h)
@@ -145,7 +155,8 @@ def main():
     N.check(lib.gwo_sync(h), h)
     rows_before = rows_emitted()
     lib.gwo_reset_stats(h)
-    lib.gwo_set_profiling(h, 0 if a.no_profile else 1)
+    # time K1 and the fire (the candidates for the dominant kernel); pass 2 is never dominant here
+    lib.gwo_set_profiling_mask(h, 0 if a.no_profile else (1 << N.KERNEL_INSERT) | (1 << N.KERNEL_FIRE))
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
@@ -198,10 +209,9 @@ def main():
     path_bytes = records * I_B + u_tot * 2 * S_B + rows * (S_B + O_B)
     kern = {
         "insert": ("log_part_kernel", records * (I_B + REC_B)),
-        "partition": ("log_split_kernel", records * 2 * REC_B),
         "fire": ("log_fire_kernel", stats["fire"][2] * REC_B + rows * O_B),
     }
-    if stats["partition"][0] == 0:   # table layout: scan + insert + fire sweep
+    if a.layout == "table":   # scan + insert + fire sweep
         kern = {"insert": ("insert_direct_kernel", records * I_B + u_tot * 2 * 32),
                 "fire": ("fire_kernel", stats["fire"][2] * 32 + rows * O_B)}
     dom = max(kern, key=lambda k: stats[k][1])
@@ -217,11 +227,17 @@ def main():
         if t:
             traffic = t["hbm_bytes_per_launch"]
 
+    op.close()
+    del key, ts, val
+    torch.cuda.empty_cache()
+    host_fed = None
+    if rank == 0 and world == 1 and not a.no_host_fed:
+        host_fed = host_fed_run(a, F, N, lib, local, rec_per_step, exp_keys)
     out = None
     if rank == 0:
         cpu = None
         if not a.no_cpu_baseline:
-            cpu = cpu_baseline(a, key, ts, val, bounds, wms)
+            cpu = cpu_baseline(a, N, lib, local)
         ms_per_step = elapsed / a.steps * 1e3
         out = {
             "metric": "records/sec per node, keyed window agg @1/2/4/8 GPU; % of HBM peak",
@@ -237,7 +253,9 @@ def main():
             "dtype": "int64",
             "data": "synthetic (splitmix64 counter generator, generated in HBM before timing)",
             "config": {"workload": "C4 high-cardinality tumbling sum/min/max",
-                       "keys_per_gpu": a.keys_per_gpu, "records_per_gpu": R, "records_per_step_per_gpu": rec_per_step,
+                       "keys_per_gpu": a.keys_per_gpu, "records_per_gpu": records,
+                       "records_generated_per_gpu": n_gen, "stream_rate": f"{R} records per {span} ms per GPU",
+                       "records_per_step_per_gpu": rec_per_step,
                        "window_ms": a.window_ms, "watermark_every_ms": a.wm_interval_ms, "lag_ms": a.lag_ms,
                        "max_parallelism": a.max_parallelism, "parallelism": f"keyBy over {world} GPU(s)"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": peak, "unit": "GB/s",
@@ -250,37 +268,109 @@ def main():
                               "distinct_entries_per_step": u_tot / a.steps, "fired_rows_per_step": rows / a.steps},
             "kernels_ms": {k: {"launches": v[0], "total_ms": v[1]} for k, v in stats.items() if v[0]},
             "cpu_baseline": cpu,
+            "host_fed": host_fed,
         }
         print(json.dumps(out), flush=True)
-    op.close()
     if dist:
         dist.barrier()
         dist.destroy_process_group()
 
 
-def cpu_baseline(a, key, ts, val, bounds, wms):
-    """Times the oracle's C restatement (oracle/_ref-free; kind 'port') on a bounded sample of the
-    same workload on host cores; falls back to the numpy restatement when the C build is absent."""
-    n = min(a.cpu_sample, bounds[-1][1])
-    k = key[:n].cpu().numpy()
-    t = ts[:n].cpu().numpy()
-    v = val[:n].cpu().numpy()
-    per = bounds[0][1] - bounds[0][0]
-    batches = [(min((i + 1) * per, n), wms[i]) for i in range((n + per - 1) // per)]
-    batches[-1] = (n, batches[-1][1])
-    from oracle import cbaseline
-    if cbaseline.available():
-        threads = min(os.cpu_count() or 1, 16)
-        secs = cbaseline.time_tumbling(k, t, v, batches, a.window_ms, threads)
-        return {"value": n / secs, "unit": "records/s", "cores": threads, "kind": "port",
-                "sample": f"first {n} records of the same C4 stream, same windows/watermarks; C restatement "
-                          f"of WindowOperator (oracle/window_oracle.c), {threads} threads sharded by key group"}
-    from oracle import vectorized as V
+def gen_stream(N, lib, local, seed, total, nkeys, span, n, first=0):
+    import torch
+    dev = torch.device("cuda", local)
+    k = torch.empty(n, dtype=torch.int64, device=dev)
+    t = torch.empty(n, dtype=torch.int64, device=dev)
+    v = torch.empty(n, dtype=torch.int64, device=dev)
+    spec = N.GwoGenSpec(seed, first, total, nkeys, span, 1000, 0, 1000, N.DTYPE_INT64, 0)
+    N.check(lib.gwo_generate(C.byref(spec), n, k.data_ptr(), t.data_ptr(), v.data_ptr(), None, local), None,
+            "gwo_generate")
+    torch.cuda.synchronize()
+    return k, t, v
+
+
+def step_watermarks(ts_host, per, nsteps, lag):
+    wms, run = [], -(1 << 63)
+    for i in range(nsteps):
+        run = max(run, int(ts_host[i * per:(i + 1) * per].max()))
+        wms.append(run - lag - 1)
+    return wms
+
+
+def host_fed_run(a, F, N, lib, local, per, exp_keys):
+    """End-to-end from host memory (SURVEY.md §8d 'host-fed'): the C4 stream's first host_fed_steps steps as
+    pinned host columns; per step gwo_submit(host pointers: one H2D copy per column on the handle's stream)
+    + gwo_advance_watermark + every fired row drained into pinned host columns.  Window [0, 10 s) fires
+    at step 10, so 12 steps include one full fire (~81M rows)."""
+    import torch
+    steps = a.host_fed_steps
+    n = per * steps
+    k, t, v = gen_stream(N, lib, local, 42, a.records_per_gpu, a.keys_per_gpu, a.span_ms, n)
+    hk, ht, hv = (x.cpu().pin_memory() for x in (k, t, v))
+    del k, t, v
+    torch.cuda.empty_cache()
+    wms = step_watermarks(ht.numpy(), per, steps, a.lag_ms)
+    agg = F.MultiAggregate(F.SumAggregate(), F.MinAggregate(), F.MaxAggregate())
+    op = F.GpuWindowOperator(F.TumblingEventTimeWindows.of(a.window_ms), agg, max_parallelism=a.max_parallelism,
+                             device=local, expected_keys=exp_keys)
+    h = op.handle
+    cap = exp_keys + exp_keys // 8 + 4096
+    outs = [torch.empty(cap, dtype=torch.int64).pin_memory() for _ in range(6)]
+    o = N.GwoOut()
+    o.key, o.start, o.end = outs[0].data_ptr(), outs[1].data_ptr(), outs[2].data_ptr()
+    for i in range(3):
+        o.result[i] = outs[3 + i].data_ptr()
+    drained = 0
+    torch.cuda.synchronize()
     t0 = time.perf_counter()
-    V.tumbling_lateness0(k, t, v, batches, a.window_ms, 0, [1, 2, 3])
+    for i in range(steps):
+        s = i * per
+        N.check(lib.gwo_submit(h, C.c_void_p(hk.data_ptr() + 8 * s), C.c_void_p(ht.data_ptr() + 8 * s),
+                               C.c_void_p(hv.data_ptr() + 8 * s), per), h, "submit")
+        N.check(lib.gwo_advance_watermark(h, wms[i]), h, "watermark")
+        while True:
+            got = C.c_int64()
+            N.check(lib.gwo_drain(h, C.byref(o), cap, C.byref(got)), h, "drain")
+            drained += got.value
+            if got.value < cap:
+                break
+    N.check(lib.gwo_sync(h), h)
     secs = time.perf_counter() - t0
-    return {"value": n / secs, "unit": "records/s", "cores": 1, "kind": "port",
-            "sample": f"first {n} records; numpy restatement (oracle/vectorized.py), 1 thread"}
+    op.close()
+    return {"value": n / secs, "unit": "records/s", "steps": steps, "records": n, "rows_drained": drained,
+            "note": "pinned host key/ts/value columns in (H2D inside gwo_submit), fired rows drained to pinned "
+                    "host columns; 1 GPU, same C4 stream and operator config"}
+
+
+def cpu_baseline(a, N, lib, local):
+    """The oracle's C restatement of WindowOperator (oracle/window_oracle.c: per-subtask heap hash map +
+    deduplicated timer heap, 16 threads sharded by key group; kind 'port', not Flink -- no JDK here) on a
+    bounded sample of the same workload: the C4 stream with keys and records per step scaled down by
+    --cpu-scale (keys per record unchanged), 11 one-second steps -- window [0, 10 s) complete -- ending
+    with the final Long.MAX_VALUE watermark, so every window fires and state reaches its steady size."""
+    from oracle import cbaseline
+    if not cbaseline.available():
+        return None
+    sc = max(1, a.cpu_scale)
+    total, nkeys = a.records_per_gpu // sc, a.keys_per_gpu // sc
+    per = total * a.wm_interval_ms // a.span_ms
+    steps = a.window_ms // a.wm_interval_ms + 1
+    k, t, v = gen_stream(N, lib, local, 42, total, nkeys, a.span_ms, per * steps)
+    kh, th, vh = k.cpu().numpy(), t.cpu().numpy(), v.cpu().numpy()
+    del k, t, v
+    wms = step_watermarks(th, per, steps, a.lag_ms)
+    batches = [((i + 1) * per, wms[i]) for i in range(steps)] + [(per * steps, (1 << 63) - 1)]
+    threads = min(os.cpu_count() or 1, 16)
+    t0 = time.perf_counter()
+    _, _, late = cbaseline.run_tumbling(kh, th, vh, batches, a.window_ms, threads=threads,
+                                        max_par=a.max_parallelism, rows=False)
+    secs = time.perf_counter() - t0
+    n = per * steps
+    return {"value": n / secs, "unit": "records/s", "cores": threads, "kind": "port", "seconds": secs,
+            "sample": f"C4 stream scaled 1/{sc}: {nkeys} keys, {per} records per 1-s step, {steps} steps "
+                      f"({n} records: window [0, {a.window_ms} ms) complete) then the final Long.MAX_VALUE "
+                      f"watermark (every window fires); C restatement of WindowOperator (oracle/window_oracle.c), "
+                      f"{threads} threads sharded by key group"}
 
 
 if __name__ == "__main__":

@@ -91,6 +91,7 @@ SIGNATURES = [
     ("gwo_last_error", C.c_char_p, [_P]),
     ("gwo_status_string", C.c_char_p, [C.c_int]),
     ("gwo_set_profiling", C.c_int, [_P, C.c_int32]),
+    ("gwo_set_profiling_mask", C.c_int, [_P, C.c_uint32]),
     ("gwo_set_pipelined_submit", C.c_int, [_P, C.c_int32]),
     ("gwo_kernel_stats", C.c_int, [_P, C.c_int32, _I64P, C.POINTER(C.c_double), _I64P]),
     ("gwo_reset_stats", C.c_int, [_P]),

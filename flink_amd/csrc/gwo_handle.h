@@ -138,6 +138,7 @@ struct Handle {
 
     // profiling
     bool profiling = false;
+    uint32_t prof_mask = ~0u;                  // kernels timed while profiling (bit = gwo_kernel_id)
     bool debug = false;                        // GWO_DEBUG=1: trace batches to stderr
     std::vector<PendingEvent> pending_events;
     std::vector<hipEvent_t> event_pool;        // recycled profiling events
@@ -232,6 +233,7 @@ struct Handle {
     gwo_status session_state_size(int64_t *entries);
     // log-structured tumbling state (gwo_log.cpp)
     gwo_status log_init();
+    gwo_status log_reserve();
     void log_free();
     gwo_status log_carve(LogWindow &W, size_t bytes, char **out);
     void log_release(LogWindow &W);
@@ -241,6 +243,8 @@ struct Handle {
     gwo_status log_resolve_split();
     gwo_status insert_log(const int64_t *k, const int64_t *t, const int64_t *v, int64_t n, int64_t stride = 1);
     gwo_status log_k1(LogJob &J, bool first_pass);
+    void log_uncarve(const LogJob &J, int w, uint64_t keep);
+    gwo_status log_commit_spec(LogJob &J, const unsigned long long *rbp);
     gwo_status log_resolve_k1(LogJob J);
     gwo_status log_wait_readback(int slot, unsigned long long seq);
     gwo_status log_flush();                    // resolve the pipelined batch (no-op without one)

@@ -41,6 +41,13 @@ struct LogJob {
     int slot = 0;                // batch buffer / readback slot
     unsigned long long seq = 0;  // readback sequence number of the last K1 launch
     LogSegDesc desc[LOG_NU] = {}; // the range's new segments: counters/offsets carved at launch, records after
+    // speculative pass 2 (queued right behind K1, no host round trip): each window's segment records were
+    // carved at launch with an upper bound; the readback either commits them (trimmed to the device plan's
+    // size) or the host un-carves them and takes the planned path
+    bool spec = false;
+    uint64_t seg_cap[LOG_NU] = {};
+    char *carve_at[LOG_NU] = {};  // start of the carved segment records
+    char *carve_end[LOG_NU] = {}; // end of the carve (the window's chunk cursor right after it)
 };
 
 struct LogState {
@@ -63,6 +70,8 @@ struct LogState {
     unsigned long long seen_seq = 0;             // highest K1 readback sequence number observed complete
     unsigned *h_split_flag = nullptr;            // pinned, device-written [LOG_SLOTS]: pass-2 overflow flags
     unsigned *d_split_flag = nullptr;            // device view of h_split_flag
+    unsigned *d_go = nullptr;                    // [LOG_SLOTS] K1's verdict on the speculative pass 2
+    unsigned long long *d_done = nullptr;        // K1 workgroups finished (reset by the last one)
     // pipelined submission (gwo_set_pipelined_submit): the batch whose K1 is in flight, resolved by the
     // next call on the handle
     bool pipeline = false;
@@ -118,6 +127,9 @@ gwo_status Handle::log_init() {
     GWO_TRY(dalloc((void **)&L.d_plan, kPlanBytes));
     GWO_TRY(dalloc((void **)&L.d_overflow, 16));
     GWO_TRY(hipcheck(hipMemsetAsync(L.d_overflow, 0, 16, stream), "overflow"));
+    GWO_TRY(dalloc((void **)&L.d_go, LOG_SLOTS * sizeof(unsigned)));
+    GWO_TRY(dalloc((void **)&L.d_done, 8));
+    GWO_TRY(hipcheck(hipMemsetAsync(L.d_done, 0, 8, stream), "done"));
     // written by kernels, read by the host after an event: coherent, mapped
     GWO_TRY(hipcheck(hipHostMalloc((void **)&L.h_rb, kRbBytes * LOG_SLOTS, hipHostMallocCoherent | hipHostMallocMapped),
                      "pinned"));
@@ -134,8 +146,39 @@ gwo_status Handle::log_init() {
     GWO_TRY(hipcheck(hipStreamCreateWithFlags(&fire_stream, hipStreamNonBlocking), "fire stream"));
     GWO_TRY(hipcheck(hipEventCreateWithFlags(&ev_main, hipEventDisableTiming), "event"));
     GWO_TRY(hipcheck(hipEventCreateWithFlags(&ev_fire, hipEventDisableTiming), "event"));
-    init_stats(0);   // afterwards log_collect_kernel resets the device stats after every K1
+    init_stats(0);   // afterwards K1's last workgroup resets the device stats after every launch
     L.cap_log2 = log_fire_cap_log2(plan.nwords);
+    return log_reserve();
+}
+
+// With a distinct-keys hint, the steady state's device memory is reserved (and touched) at creation, so no
+// batch or fire allocates: the output rows of one window, and a chunk pool for the records of three
+// windows in flight (one filling, one fired, the next -- 16-B records, about two records per key, 1.4x for
+// the partitions' capacity slack), capped at a quarter of the free device memory.
+gwo_status Handle::log_reserve() {
+    if (cfg.expected_keys <= 0) return GWO_OK;
+    LogState &L = *logst;
+    const uint64_t keys = (uint64_t)cfg.expected_keys;
+    GWO_TRY(ensure_output(keys + keys / 8 + 4096));
+    for (int64_t *c : {out.key, out.start, out.end, out.res[0], out.res[1], out.res[2], out.res[3]})
+        if (c) GWO_TRY(hipcheck(hipMemsetAsync(c, 0, (size_t)out.cap * 8, stream), "output reserve"));
+    size_t free_b = 0, total_b = 0;
+    GWO_TRY(hipcheck(hipMemGetInfo(&free_b, &total_b), "memory info"));
+    const double per_window = (double)keys * 2.0 * (needs_value ? 16.0 : 8.0) * 1.4;
+    for (int i = 0; i < 8; ++i) {   // a new window's first carves (its partition offsets/counters) take 1-MB chunks
+        void *p = nullptr;
+        GWO_TRY(dalloc(&p, (size_t)1 << 20));
+        GWO_TRY(hipcheck(hipMemsetAsync(p, 0, (size_t)1 << 20, stream), "pool reserve"));
+        L.free_chunks.emplace((size_t)1 << 20, (char *)p);
+    }
+    const size_t chunk = (size_t)1 << 30;
+    size_t want = (size_t)std::min(3.0 * per_window, (double)free_b / 4.0);
+    for (size_t got = 0; got + chunk <= want; got += chunk) {
+        void *p = nullptr;
+        GWO_TRY(dalloc(&p, chunk));
+        GWO_TRY(hipcheck(hipMemsetAsync(p, 0, chunk, stream), "pool reserve"));
+        L.free_chunks.emplace(chunk, (char *)p);
+    }
     return GWO_OK;
 }
 
@@ -157,6 +200,8 @@ void Handle::log_free() {
     if (L.d_bk) (void)hipFree(L.d_bk);
     if (L.d_plan) (void)hipFree(L.d_plan);
     if (L.d_overflow) (void)hipFree(L.d_overflow);
+    if (L.d_go) (void)hipFree(L.d_go);
+    if (L.d_done) (void)hipFree(L.d_done);
     if (L.h_rb) (void)hipHostFree(L.h_rb);
     if (L.h_buckets) (void)hipHostFree(L.h_buckets);
     delete logst;
@@ -276,7 +321,7 @@ gwo_status Handle::log_split_exact(long long base, int nunits, uint64_t cap, con
         GWO_TRY(hipcheck(hipMemcpyAsync(L.d_plan, L.h_buckets, (nb + 1) * sizeof(LogBucket), hipMemcpyHostToDevice, stream),
                          "split plan"));
         launch_log_split((const int64_t *)L.tmp[tmpx].ptr, needs_value, L.d_plan, nb, set, L.d_split_flag + tmpx, chunks,
-                         stream);
+                         nullptr, stream);
         GWO_TRY(launch_ok("log split"));
         GWO_TRY(hipcheck(hipStreamSynchronize(stream), "log split"));
         if (L.h_split_flag[tmpx] == 0) break;
@@ -296,6 +341,31 @@ gwo_status Handle::log_split_exact(long long base, int nunits, uint64_t cap, con
         if (!wins[w]) continue;
         wins[w]->segs.push_back(set.s[w]);
         wins[w]->records += wcount[w];
+    }
+    return GWO_OK;
+}
+
+// Commits a speculative pass 2 that runs the device plan (rb[LOG_RB_GO]): each window's segment records
+// are trimmed to the plan's size and the segments join their windows; the partition-overflow flag is checked
+// at the next sync point as for every pass 2 (log_resolve_split).
+gwo_status Handle::log_commit_spec(LogJob &J, const unsigned long long *rbp) {
+    LogState &L = *logst;
+    uint64_t wcount[LOG_NU] = {};
+    for (int b = 0; b < J.nunits * 256; ++b) wcount[b >> 8] += rbp[b];
+    for (int w = 0; w < J.nunits; ++w) log_uncarve(J, w, wcount[w] ? rbp[LOG_RB_SEG + w] : 0);
+    L.pend.after_seq = J.seq;   // any later readback implies this pass 2 completed (stream order)
+    L.pend.has_event = false;
+    L.pend.active = true;
+    L.pend.tmpx = J.slot;
+    L.pend.nunits = J.nunits;
+    L.pend.base = J.base;
+    L.pend.cap = J.cap;
+    L.pend.counts.assign(rbp, rbp + J.nunits * 256);
+    for (int w = 0; w < J.nunits; ++w) {
+        if (!wcount[w]) continue;
+        LogWindow &Wn = L.wins[J.base + w];
+        Wn.segs.push_back(J.desc[w]);
+        Wn.records += wcount[w];
     }
     return GWO_OK;
 }
@@ -322,7 +392,7 @@ gwo_status Handle::log_split_dev(const LogJob &J, const unsigned long long *rbp)
     L.h_split_flag[J.slot] = 0;
     prof_begin(GWO_KERNEL_PARTITION);
     launch_log_split((const int64_t *)L.tmp[J.slot].ptr, needs_value, L.bk(J.slot), J.nunits * 256, set,
-                     L.d_split_flag + J.slot, (uint32_t)rbp[LOG_RB_CHUNKS], stream);
+                     L.d_split_flag + J.slot, (uint32_t)rbp[LOG_RB_CHUNKS], nullptr, stream);
     GWO_TRY(launch_ok("log split"));
     prof_end(GWO_KERNEL_PARTITION, (int64_t)total);
     // completion is implied by the next K1's readback (stream order); only a pipelined K1, queued before
@@ -369,18 +439,32 @@ gwo_status Handle::log_resolve_split() {
     return log_split_exact(L.pend.base, L.pend.nunits, L.pend.cap, counts.data(), L.pend.tmpx);
 }
 
-// K1 of job J (one window range of a batch) into batch buffer J.slot, then the collect kernel and one
-// readback of its bucket counts and statistics; ev_rb[J.slot] marks the readback's completion.
+// Upper bound of the segment records one window receives from a batch of n records: the device plan
+// gives each of its 256 coarse buckets F * pcap records, pcap = ceil(n_b/F + 6 sqrt(n_b/F) + 4), so the
+// window's segment is at most n + 6 sqrt(F) * sum_b sqrt(n_b) + 5 * 256 * F <= n + 96 sqrt(F n) + 1280 F
+// (Cauchy-Schwarz over the 256 buckets).
+static uint64_t seg_upper_bound(uint64_t n, int lp) {
+    const double F = (double)(1u << (lp - 8));
+    return (uint64_t)std::ceil((double)n + 96.0 * std::sqrt(F * (double)n) + 1280.0 * F) + 64;
+}
+
+// K1 of job J (one window range of a batch) into batch buffer J.slot; its last workgroup writes the readback
+// block (bucket counts, statistics, device plan of pass 2); ev_rb[J.slot] marks the readback's completion.
+// J.spec: each window's segment records are carved now with an upper bound and pass 2 is queued right
+// behind K1 with an upper bound of workgroups; it runs the device plan unless K1's verdict says the batch
+// needs the host (log_resolve_k1 then un-carves and re-plans), so no host round trip sits between them.
 gwo_status Handle::log_k1(LogJob &J, bool first_pass) {
     LogState &L = *logst;
     const int W = needs_value ? 2 : 1;
-    // the range's windows and their new segments' offsets/counters (zeroed by the collect kernel)
     CollectArgs ca{};
     ca.nunits = J.nunits;
     ca.cap = J.cap;
     ca.bk = L.bk(J.slot);
+    ca.go = L.d_go + J.slot;
     ca.rb = L.rb_dev(J.slot);
+    ca.done = L.d_done;
     ca.seq = J.seq = ++L.seq;
+    ca.spec = J.spec ? 1 : 0;
     for (int w = 0; w < J.nunits; ++w) {
         auto it = L.wins.find(J.base + w);
         if (it == L.wins.end()) {
@@ -396,6 +480,14 @@ gwo_status Handle::log_k1(LogJob &J, bool first_pass) {
         GWO_TRY(log_carve(it->second, ((size_t)1 << lp) * 4, &p));
         d.cnt = (uint32_t *)p;
         d.lp = lp;
+        if (J.spec) {
+            J.seg_cap[w] = seg_upper_bound((uint64_t)J.n, lp);
+            GWO_TRY(log_carve(it->second, J.seg_cap[w] * W * 8, &p));
+            d.rec = (int64_t *)p;
+            J.carve_at[w] = p;
+            J.carve_end[w] = it->second.chunks.back().base + it->second.chunks.back().used;
+            ca.seg_cap[w] = J.seg_cap[w];
+        }
         J.desc[w] = d;
         ca.lp[w] = lp;
         ca.cnt[w] = d.cnt;
@@ -409,13 +501,36 @@ gwo_status Handle::log_k1(LogJob &J, bool first_pass) {
     prof_begin(GWO_KERNEL_INSERT);
     launch_log_part(J.k, J.t, J.v, J.n, J.stride, J.g, J.base, J.nunits, needs_value, L.d_cursor, J.cap,
                     (int64_t *)tmp.ptr, d_stats, (int64_t *)side_key.ptr, (int64_t *)side_ts.ptr,
-                    (int64_t *)side_val.ptr, d_side_count, side ? side_cap : 0, side, stream);
+                    (int64_t *)side_val.ptr, d_side_count, side ? side_cap : 0, side, ca, stream);
     GWO_TRY(launch_ok("log partition"));
     prof_end(GWO_KERNEL_INSERT, J.n);
-    launch_log_collect(L.d_cursor, d_stats, ca, stream);
-    GWO_TRY(launch_ok("log collect"));
     if (side) GWO_TRY(hipcheck(hipMemcpyAsync(h_scalar, d_side_count, 8, hipMemcpyDeviceToHost, stream), "side count"));
-    return hipcheck(hipEventRecord(L.ev_rb[J.slot], stream), "event");
+    GWO_TRY(hipcheck(hipEventRecord(L.ev_rb[J.slot], stream), "event"));
+    if (J.spec) {
+        LogSegSet set{};
+        for (int w = 0; w < J.nunits; ++w) set.s[w] = J.desc[w];
+        // chunks = sum over buckets of ceil(n_b / TILE) <= ceil(n / TILE) + buckets
+        const uint64_t grid = ((uint64_t)J.n + LOG_TILE - 1) / LOG_TILE + (uint64_t)J.nunits * 256;
+        L.h_split_flag[J.slot] = 0;
+        prof_begin(GWO_KERNEL_PARTITION);
+        launch_log_split((const int64_t *)tmp.ptr, needs_value, L.bk(J.slot), J.nunits * 256, set,
+                         L.d_split_flag + J.slot, (uint32_t)grid, L.d_go + J.slot, stream);
+        GWO_TRY(launch_ok("log split"));
+        prof_end(GWO_KERNEL_PARTITION, J.n);
+    }
+    return GWO_OK;
+}
+
+// Gives back the speculative segment carve of window w of job J (the device did not run the plan, or the
+// window got no records), or trims it to `keep` records -- only while it is still the last carve of its
+// chunk; otherwise the tail simply stays unused until the window is released.
+void Handle::log_uncarve(const LogJob &J, int w, uint64_t keep) {
+    auto it = logst->wins.find(J.base + w);
+    if (it == logst->wins.end() || it->second.chunks.empty() || !J.carve_at[w]) return;
+    LogChunk &c = it->second.chunks.back();
+    if (c.base + c.used != J.carve_end[w]) return;
+    const size_t bytes = keep ? ((keep * (needs_value ? 2 : 1) * 8 + 255) & ~(size_t)255) : 0;
+    c.used = (size_t)(J.carve_at[w] - c.base) + bytes;
 }
 
 // Waits for K1's readback by spinning on its sequence word in pinned host memory (the collect kernel
@@ -481,10 +596,31 @@ gwo_status Handle::log_resolve_k1(LogJob J) {
             } else {
                 late_dropped += hs.late;
             }
-            if (hs.accepted == 0) return GWO_OK;
+            if (hs.accepted == 0) {
+                if (J.spec)
+                    for (int w = 0; w < J.nunits; ++w) log_uncarve(J, w, 0);
+                return GWO_OK;
+            }
             lo = hs.min_idx;
             hi = hs.max_idx;
             first_pass = false;
+            if (J.spec) {
+                if (rbp[LOG_RB_GO] && J.base <= lo && lo < J.base + J.nunits) {
+                    // the speculative pass 2 is running the device plan: commit its segments
+                    GWO_TRY(log_commit_spec(J, rbp));
+                    const long long chunk_hi = J.base + J.nunits - 1;
+                    if (chunk_hi >= hi) break;
+                    J.spec = false;
+                    J.base = chunk_hi + 1;
+                    J.nunits = (int)std::min<long long>(LOG_NU, hi - J.base + 1);
+                    J.slot = L.free_slot();
+                    GWO_TRY(log_k1(J, false));
+                    continue;
+                }
+                // it exited: give its carves back and plan on the host from this readback
+                for (int w = 0; w < J.nunits; ++w) log_uncarve(J, w, 0);
+                J.spec = false;
+            }
             if (J.base > lo || J.base + J.nunits <= lo) {   // wrong window range guess: redo from the first window
                 J.base = lo;
                 J.nunits = (int)std::min<long long>(LOG_NU, hi - lo + 1);
@@ -532,6 +668,9 @@ gwo_status Handle::insert_log(const int64_t *k, const int64_t *t, const int64_t 
     J.base = hist_hint;
     J.nunits = (int)std::min<long long>(LOG_NU, std::max<long long>(1, L.span_hint));
     J.cap = group_capacity((double)n / 256.0);
+    // speculative pass 2 (no host round trip between K1 and pass 2) unless late records go to the side output
+    // (K1's first pass appends them; a re-run must not repeat that)
+    J.spec = !side_enabled();
     // Pipelined: this batch's K1 is queued before the previous batch is resolved, so the host's wait,
     // checks and pass-2 planning overlap a running K1.  Only for caller-owned device columns (borrowed
     // until the next call returns, gwo.h) -- staged host input and received exchange buffers are reused

@@ -57,39 +57,46 @@ struct LogSegSet {
     LogSegDesc s[LOG_NU];
 };
 
-// K1 readback block (host-visible, written by log_collect_kernel): [LOG_NU * 256] bucket counts, the
-// BatchStats words, [LOG_NU] segment sizes (records) of the device plan, and its pass-2 workgroup count.
+// K1 readback block (host-visible, written by K1's last workgroup): [LOG_NU * 256] bucket counts, the
+// BatchStats words, [LOG_NU] segment sizes (records) of the device plan, its pass-2 workgroup count, the
+// speculation verdict (1: the speculative pass 2 queued behind K1 runs the plan), and the sequence number.
 static constexpr int LOG_RB_STATS = LOG_NU * 256;
 static constexpr int LOG_RB_SEG = LOG_RB_STATS + (int)((sizeof(BatchStats) + 7) / 8);
 static constexpr int LOG_RB_CHUNKS = LOG_RB_SEG + LOG_NU;
-static constexpr int LOG_RB_SEQ = LOG_RB_CHUNKS + 1;     // written last: the launch's sequence number
+static constexpr int LOG_RB_GO = LOG_RB_CHUNKS + 1;
+static constexpr int LOG_RB_SEQ = LOG_RB_GO + 1;         // written last: the launch's sequence number
 static constexpr int LOG_RB_WORDS = LOG_RB_SEQ + 1;
 
+// What K1's last workgroup needs to plan pass 2 (the former collect step, fused into K1's tail).
 struct CollectArgs {
     int nunits;
     int lp[LOG_NU];              // partition bits of each window of the launch
-    uint32_t *cnt[LOG_NU];       // the windows' new segment counters (zeroed here)
+    uint32_t *cnt[LOG_NU];       // the windows' new segment counters (zeroed by every K1 workgroup first)
     uint64_t cap;                // bucket region capacity of the batch buffer
+    uint64_t seg_cap[LOG_NU];    // speculative pass 2: segment records carved per window (spec only)
+    int spec;                    // 1: a pass 2 is queued behind K1 and runs iff the plan fits (rb[LOG_RB_GO])
     LogBucket *bk;               // out: [nunits * 256 + 1] pass-2 plan (device)
+    unsigned *go;                // out: 1 = the queued speculative pass 2 runs the plan, 0 = it exits
     unsigned long long *rb;      // out: readback block (pinned host memory)
     unsigned long long seq;      // written to rb[LOG_RB_SEQ] after every other readback word
+    unsigned long long *done;    // K1 workgroups finished (the last one plans; it resets the counter)
 };
 
 namespace gwo {
-// K1: classify + key-group check + late accounting + (window, coarse digit) grouping of a batch.
+// K1: classify + key-group check + late accounting + (window, coarse digit) grouping of a batch; its last
+// workgroup writes the readback block and the device plan of pass 2, and resets cursors and statistics.
 // key/ts/val columns with `stride` int64 words between records (1: SoA columns; 3: {key, ts, value} records)
 void launch_log_part(const int64_t *key, const int64_t *ts, const int64_t *val, int64_t n, int64_t stride,
                      const WindowGeom &g,
                      long long base, int nunits, int has_val, unsigned long long *cursor, uint64_t cap,
                      int64_t *tmp, BatchStats *st, int64_t *side_key, int64_t *side_ts, int64_t *side_val,
-                     unsigned long long *side_count, long long side_cap, int side_enabled, hipStream_t s);
-// After K1: readback block + device plan of pass 2 + zeroed segment counters (see CollectArgs); resets
-// the cursors and the stats for the next K1 launch.
-void launch_log_collect(unsigned long long *cursor, BatchStats *stats, const CollectArgs &a, hipStream_t s);
+                     unsigned long long *side_count, long long side_cap, int side_enabled, const CollectArgs &ca,
+                     hipStream_t s);
 // Pass 2: every coarse bucket -> its window's segment, grouped by partition.  `overflow` is a
-// host-visible flag (set to 1 when a partition exceeds its capacity).
+// host-visible flag (set to 1 when a partition exceeds its capacity).  go != NULL: a speculative launch
+// of `nchunks` (an upper bound) workgroups that exits unless *go (K1's verdict) is set.
 void launch_log_split(const int64_t *tmp, int has_val, const LogBucket *buckets, int nb, const LogSegSet &segs,
-                      unsigned *overflow, uint32_t nchunks, hipStream_t s);
+                      unsigned *overflow, uint32_t nchunks, const unsigned *go, hipStream_t s);
 int log_fire_cap_log2(int nwords);
 void launch_log_fire(const LogSegDesc *segs, int nseg, int lp, int has_val, const AccPlan &plan,
                      const ResultPlan &rp, int64_t start, int64_t end, OutCols out, unsigned long long *overflow,

@@ -24,7 +24,6 @@
 // random accesses are LDS.
 #include "gwo_device.h"
 #include "gwo_log.h"
-#include <stdlib.h>
 
 namespace gwo {
 
@@ -80,6 +79,104 @@ __device__ __forceinline__ uint32_t tile_offsets(const uint32_t *s_cnt, uint32_t
     return total;
 }
 
+// Inclusive prefix of a 64-bit value over a 256-thread workgroup (wave shuffles + one LDS round);
+// ends synchronised.  *total = the workgroup sum.
+__device__ __forceinline__ unsigned long long block256_incl_scan64(unsigned long long v, unsigned long long *total) {
+    __shared__ unsigned long long s_w[4];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const unsigned long long y = __shfl_up(v, o);
+        if (lane >= o) v += y;
+    }
+    if (lane == 63) s_w[wid] = v;
+    __syncthreads();
+    unsigned long long pre = 0;
+    for (int w = 0; w < wid; ++w) pre += s_w[w];
+    *total = s_w[0] + s_w[1] + s_w[2] + s_w[3];
+    __syncthreads();
+    return v + pre;
+}
+
+// K1's tail, run by its last workgroup (256 threads; formerly a separate collect kernel): moves the bucket
+// counts and batch statistics into the host-visible readback block (resetting cursors and statistics for the
+// next K1), and plans pass 2 on the device -- per bucket the partition capacity (mean + 6 sigma + 4 of a
+// Binomial(n_b, 1/F) partition, the host's group_capacity), the bucket's first record in its window's
+// segment and its first pass-2 workgroup -- with each window's segment size and the workgroup total in the
+// readback.  Speculative launches (ca.spec): the pass 2 already queued behind K1 runs the plan only if it
+// is the batch's final plan -- no error, no bucket over its region capacity, the batch's first window inside
+// the launch's window range, every segment within its carved capacity -- else it exits and the host takes over.
+__device__ __forceinline__ void k1_plan_tail(unsigned long long *cursor, BatchStats *st, const CollectArgs &a,
+                                          long long base) {
+    constexpr int SW = (int)(sizeof(BatchStats) / 8);
+    static_assert(SW <= LOG_K1_THREADS, "statistics words");
+    __shared__ unsigned long long s_sw[SW];
+    __shared__ unsigned s_bad;
+    const int t = threadIdx.x;
+    unsigned long long *sw = (unsigned long long *)st;
+    if (t == 0) s_bad = 0;
+    if (t < SW) {   // read-and-reset through the same device-scope atomics the workgroups used
+        const unsigned long long reset = t == 0 ? 0x7fffffffffffffffull : (t == 1 ? 0x8000000000000000ull : 0ull);
+        const unsigned long long w = atomicExch(&sw[t], reset);
+        s_sw[t] = w;
+        a.rb[LOG_RB_STATS + t] = w;
+    }
+    __syncthreads();
+    const BatchStats &S = *(const BatchStats *)s_sw;
+    unsigned long long chunk_run = 0;
+    unsigned bad = 0;
+    for (int q = 0; q < a.nunits; ++q) {   // window q of the launch: bucket b = q * 256 + t (digit t)
+        const int b = q * 256 + t;
+        const unsigned long long n_b = atomicExch(&cursor[(size_t)b * LOG_CUR_STRIDE], 0ull);
+        a.rb[b] = n_b;
+        if (n_b > a.cap) bad = 1;          // K1 dropped records past the region: the host re-runs K1
+        uint32_t pcap = 0, chunks = 0;
+        unsigned long long seg = 0;
+        if (n_b) {
+            const int F = 1 << (a.lp[q] - 8);
+            const double mean = (double)n_b / (double)F;
+            pcap = (uint32_t)ceil(__dadd_rn(__dadd_rn(mean, __dmul_rn(6.0, sqrt(mean))), 4.0));
+            seg = (unsigned long long)F * pcap;
+            chunks = (uint32_t)((n_b + LOG_TILE - 1) / LOG_TILE);
+        }
+        unsigned long long seg_tot, chk_tot;
+        const unsigned long long seg_incl = block256_incl_scan64(seg, &seg_tot);
+        const unsigned long long chk_incl = block256_incl_scan64(chunks, &chk_tot);
+        LogBucket B;
+        B.src = (uint64_t)b * a.cap;
+        B.n = (uint32_t)n_b;
+        B.pcap = pcap;
+        B.seg_base = (uint32_t)(seg_incl - seg);
+        B.chunk0 = (uint32_t)(chunk_run + chk_incl - chunks);
+        a.bk[b] = B;
+        if (t == 0) {
+            a.rb[LOG_RB_SEG + q] = seg_tot;
+            if (a.spec && seg_tot > a.seg_cap[q]) bad = 1;
+        }
+        chunk_run += chk_tot;
+    }
+    if (bad) atomicOr(&s_bad, 1u);
+    __syncthreads();
+    if (t == 0) {
+        LogBucket E{};
+        E.chunk0 = (uint32_t)chunk_run;
+        a.bk[a.nunits * 256] = E;
+        a.rb[LOG_RB_CHUNKS] = chunk_run;
+        const bool go = a.spec && !s_bad && S.bad_ts == 0 && S.bad_kg == 0 && S.refire == 0 && S.accepted > 0 &&
+                        S.min_idx >= base && S.min_idx < base + a.nunits && chunk_run < (1ull << 32);
+        *a.go = go ? 1u : 0u;
+        a.rb[LOG_RB_GO] = go ? 1ull : 0ull;
+        *a.done = 0;   // the next K1 launch counts from zero (stream order)
+    }
+    // the host spins on the sequence word: every other readback word must be visible first
+    __threadfence_system();
+    __syncthreads();
+    if (t == 0) {
+        __threadfence_system();
+        *(volatile unsigned long long *)&a.rb[LOG_RB_SEQ] = a.seq;
+    }
+}
+
 // ------------------------------------------------------------------------------------------------
 // K1 log_part: batch -> batch buffer, grouped by bucket b = (window - base) * 256 + coarse digit.
 // Bucket b owns records [b*cap, (b+1)*cap) of the buffer; cursor[b*LOG_CUR_STRIDE] ends as its record
@@ -90,8 +187,15 @@ __global__ __launch_bounds__(LOG_K1_THREADS) void log_part_kernel(
     const int64_t *__restrict__ key, const int64_t *__restrict__ ts, const int64_t *__restrict__ val, int64_t n,
     int64_t stride, WindowGeom g, long long base, int nunits, unsigned long long *__restrict__ cursor, uint64_t cap,
     int64_t *__restrict__ tmp, BatchStats *st, int64_t *side_key, int64_t *side_ts, int64_t *side_val,
-    unsigned long long *side_count, long long side_cap, int side_enabled) {
+    unsigned long long *side_count, long long side_cap, int side_enabled, CollectArgs ca) {
     constexpr int W = HASV ? 2 : 1;
+    // the new segments' partition counters (pass 2's cursors) start at zero: pass 2 follows in stream order
+    for (int w = 0; w < ca.nunits; ++w) {
+        uint4 *c4 = (uint4 *)ca.cnt[w];
+        const uint32_t n4 = (1u << ca.lp[w]) / 4;
+        for (uint32_t i = blockIdx.x * LOG_K1_THREADS + threadIdx.x; i < n4; i += gridDim.x * LOG_K1_THREADS)
+            c4[i] = make_uint4(0, 0, 0, 0);
+    }
     __shared__ __attribute__((aligned(16))) int64_t s_rec[LOG_TILE * W];
     __shared__ uint16_t s_bk[LOG_TILE];
     __shared__ uint32_t s_cnt[LOG_NU * 256];
@@ -173,11 +277,7 @@ __global__ __launch_bounds__(LOG_K1_THREADS) void log_part_kernel(
         for (int q = 0; q < 4; ++q) {
             int b = tid * per + q;
             at[q] = 0;
-#ifdef GWO_K1_XP_NOATOMIC   // experiment build only: timing without the reservation atomics
-            if (q < per && loc[q]) at[q] = (blockIdx.x & 7) * 16;
-#else
             if (q < per && loc[q]) at[q] = atomicAdd(&cursor[(size_t)b * LOG_CUR_STRIDE], (unsigned long long)loc[q]);
-#endif
         }
 #pragma unroll
         for (int j = 0; j < LOG_K1_PER; ++j) {
@@ -203,11 +303,7 @@ __global__ __launch_bounds__(LOG_K1_THREADS) void log_part_kernel(
             uint32_t b = s_bk[p];
             if (b >= (uint32_t)nb) continue;   // defensive: never a write outside the buffer
             uint64_t q = (uint64_t)s_cnt[b] + (p - s_off[b]);
-#ifdef GWO_K1_XP_NOWRITE   // experiment build only: timing without the batch-buffer writes
-            if (q == (uint64_t)-1) {
-#else
             if (q < cap) {
-#endif
                 int64_t *dst = tmp + ((uint64_t)b * cap + q) * W;
                 if (HASV) *(ll2 *)dst = *(const ll2 *)&s_rec[2 * p];
                 else *dst = s_rec[p];
@@ -243,6 +339,18 @@ __global__ __launch_bounds__(LOG_K1_THREADS) void log_part_kernel(
             atomicMax(&st->max_idx, b);
         }
     }
+    // the last workgroup to finish plans pass 2: every workgroup's atomics are complete before its arrival
+    // is counted (each wave drains its memory operations, then one lane releases at agent scope)
+    __shared__ int s_last;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        s_last = atomicAdd(ca.done, 1ull) == (unsigned long long)(gridDim.x - 1);
+    }
+    __syncthreads();
+    if (s_last) k1_plan_tail(cursor, st, ca, base);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -254,8 +362,10 @@ template <bool HASV>
 __global__ __launch_bounds__(LOG_TILE_THREADS) void log_split_kernel(const int64_t *__restrict__ tmp,
                                                                      const LogBucket *__restrict__ bk, int nb,
                                                                      const LogSegSet segs,
-                                                                     unsigned *overflow) {
+                                                                     unsigned *overflow, const unsigned *go) {
     constexpr int W = HASV ? 2 : 1;
+    // speculative launch: an upper bound of workgroups, behind K1 in stream order -- run only the plan
+    if (go && (*go == 0u || blockIdx.x >= bk[nb].chunk0)) return;
     __shared__ __attribute__((aligned(16))) int64_t s_rec[LOG_TILE * W];
     __shared__ uint16_t s_bk[LOG_TILE];
     __shared__ uint32_t s_cnt[1024];
@@ -597,7 +707,7 @@ __global__ __launch_bounds__(LOG_FIRE_THREADS) __attribute__((amdgpu_waves_per_e
                                                                     uint32_t nparts, int cap_log2, int has_val,
                                                                     AccPlan p, ResultPlan rp, int64_t start,
                                                                     int64_t end, OutCols o,
-                                                                    unsigned long long *overflow, int xp) {
+                                                                    unsigned long long *overflow) {
     // Dynamic LDS (FIRE_LDS bytes).  Fast path:
     //   s_key [FIRE_RCAP] int64   record keys (record i = r * 512 + tid), then leader keys by row ordinal
     //   s_val [FIRE_RCAP] int64   values grouped by key (after the election; overlays s_own)
@@ -625,10 +735,6 @@ __global__ __launch_bounds__(LOG_FIRE_THREADS) __attribute__((amdgpu_waves_per_e
     FireCtx c{s_dyn, s_dyn + cap, s_side, &s_used, &s_fail, cap, (unsigned)(cap - (cap >> 3))};
     uint32_t part = blockIdx.x;
     if (part >= nparts) return;
-    if ((xp >> 8) && blockIdx.x >= gridDim.x / 2) {   // experiment: phase offset of the CU's second workgroup
-        const unsigned long long t0x = clock64();
-        while (clock64() - t0x < (unsigned long long)(xp >> 8) * 1000ull) __builtin_amdgcn_s_sleep(8);
-    }
     for (int s = tid; s < nseg; s += LOG_FIRE_THREADS) s_rp[s] = segs[s].rec;
     if (tid <= GWO_MAX_WORDS) s_side[tid] = tid == 0 ? 0 : p.ident[tid - 1];
     if (tid == 0) {
@@ -719,22 +825,7 @@ __global__ __launch_bounds__(LOG_FIRE_THREADS) __attribute__((amdgpu_waves_per_e
     }
     publish(a_cnt, a_off);
     prefetch(true);
-#ifdef GWO_FIRE_PROF   // per-phase s_memtime totals of workgroup 0 (GWO_FIRE_XP & 16), printed at the end
-    unsigned long long T[8] = {0, 0, 0, 0, 0, 0, 0, 0}, t0 = 0, t1 = 0, rounds_total = 0;
-    const bool prof = (xp & 16) && blockIdx.x == 0;
-#define TSTAMP(i)            \
-    if (prof) {              \
-        t1 = clock64();      \
-        T[i] += t1 - t0;     \
-        t0 = t1;             \
-    }
-    if (prof) t0 = clock64();
-#else
-#define TSTAMP(i)
-#endif
     while (true) {
-        if (xp & 32) { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
-        TSTAMP(0)
         const uint32_t total = s_beg[nseg];
         const uint32_t nxt = part + gridDim.x;
         const bool more = nxt < nparts;
@@ -805,10 +896,6 @@ __global__ __launch_bounds__(LOG_FIRE_THREADS) __attribute__((amdgpu_waves_per_e
                     break;
                 }
             }
-#ifdef GWO_FIRE_PROF
-            rounds_total += round;
-#endif
-            TSTAMP(1)
             if (fast) {
                 for (int q = tid; q < FIRE_RCAP / 4; q += LOG_FIRE_THREADS) ((uint4 *)s_cnt)[q] = make_uint4(0, 0, 0, 0);
                 __syncthreads();
@@ -884,7 +971,6 @@ __global__ __launch_bounds__(LOG_FIRE_THREADS) __attribute__((amdgpu_waves_per_e
                 }
             }
         }
-        TSTAMP(2)
         if (total > (uint32_t)FIRE_RCAP) load_next();   // (the fast path loaded them in P0)
         if (!fast) {
             // slow path: hash-table rounds over disjoint ranges of hash bits 12..43, direct loads
@@ -932,7 +1018,6 @@ __global__ __launch_bounds__(LOG_FIRE_THREADS) __attribute__((amdgpu_waves_per_e
         // unconditional, so the loads land straight in rk/rv (no loop-carried copy that would wait for
         // them): in flight during this partition's emit and the next one's election
         prefetch(more);
-        TSTAMP(3)
         if (fast) {
             // P5: one row per leader, in ordinal order.  Thread t takes ordinal t - sh (sh = rbase & 1),
             // so lanes 2m and 2m+1 own a 16-B-aligned pair of global rows; after a DPP swap within the
@@ -947,8 +1032,8 @@ __global__ __launch_bounds__(LOG_FIRE_THREADS) __attribute__((amdgpu_waves_per_e
                 const int q = base + tid - sh;
                 const bool valid = q >= 0 && q < (int)rows;
                 int64_t k = 0, res[4] = {0, 0, 0, 0};
-                if (valid && !(xp & 128)) {
-                    const uint32_t w0 = s_cnt[q], off = w0 & 0xffffu, n = (xp & 64) ? 1u : (s_cnt[q + 1] & 0xffffu) - off;
+                if (valid) {
+                    const uint32_t w0 = s_cnt[q], off = w0 & 0xffffu, n = (s_cnt[q + 1] & 0xffffu) - off;
                     k = s_key[w0 >> 16];
                     // the run's count, sum and min/max (of the values, or of their Double.compareTo order
                     // keys for float64) in a tight loop; the plan's words are read off them afterwards
@@ -988,7 +1073,7 @@ __global__ __launch_bounds__(LOG_FIRE_THREADS) __attribute__((amdgpu_waves_per_e
                 int64_t rpv[4];
 #pragma unroll
                 for (int a = 0; a < 4; ++a) rpv[a] = dpp_swap_pair64(res[a]);
-                if (!valid || (xp & 1)) continue;
+                if (!valid) continue;
                 const unsigned long long pos = rbase + (unsigned long long)(long long)q;
                 const unsigned long long pb = pos & ~1ull;   // the pair's first row
                 if (pvalid && (long long)pb + 1 < o.cap) {
@@ -1012,16 +1097,9 @@ __global__ __launch_bounds__(LOG_FIRE_THREADS) __attribute__((amdgpu_waves_per_e
             }
             __syncthreads();   // the next partition overwrites s_key / s_cnt
         }
-        TSTAMP(4)
         if (!more) break;
         part = nxt;
     }
-#ifdef GWO_FIRE_PROF
-    if (prof && tid == 0)
-        printf("FIREPROF parts=%u rounds=%llu wait=%llu elect=%llu sortscan=%llu pubpre=%llu emit=%llu\n",
-               nparts / gridDim.x, rounds_total, T[0], T[1], T[2], T[3], T[4]);
-#endif
-#undef TSTAMP
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1031,13 +1109,14 @@ void launch_log_part(const int64_t *key, const int64_t *ts, const int64_t *val, 
                      const WindowGeom &g,
                      long long base, int nunits, int has_val, unsigned long long *cursor, uint64_t cap,
                      int64_t *tmp, BatchStats *st, int64_t *side_key, int64_t *side_ts, int64_t *side_val,
-                     unsigned long long *side_count, long long side_cap, int side_enabled, hipStream_t s) {
+                     unsigned long long *side_count, long long side_cap, int side_enabled, const CollectArgs &ca,
+                     hipStream_t s) {
     int64_t grid = (n + LOG_TILE - 1) / LOG_TILE;
     grid = grid < 1 ? 1 : (grid > LOG_K1_GRID ? LOG_K1_GRID : grid);
 #define GWO_K1(HV, S)                                                                                          \
     hipLaunchKernelGGL((log_part_kernel<HV, S>), dim3((int)grid), dim3(LOG_K1_THREADS), 0, s, key, ts, val, n, \
                        stride, g, base, nunits, cursor, cap, tmp, st, side_key, side_ts, side_val, side_count,   \
-                       side_cap, side_enabled)
+                       side_cap, side_enabled, ca)
     if (has_val) {
         if (stride == 1) GWO_K1(true, 1);
         else if (stride == 3) GWO_K1(true, 3);
@@ -1050,106 +1129,15 @@ void launch_log_part(const int64_t *key, const int64_t *ts, const int64_t *val, 
 #undef GWO_K1
 }
 
-// After K1: block 0 moves the bucket counts and the batch statistics into the host-visible readback
-// block (resetting the cursors and statistics for the next K1) and plans pass 2 on the device -- per
-// bucket the partition capacity (mean + 6 sigma + 4 of a Binomial(n_b, 1/F) partition, the same
-// formula as the host's group_capacity), the bucket's first record in its window's segment and its
-// first pass-2 workgroup -- writing the segment size of each window and the workgroup total into the
-// readback.  Blocks 1.. zero the segments' partition counters (pass 2's cursors).
-__global__ __launch_bounds__(1024) void log_collect_kernel(unsigned long long *cursor, BatchStats *st, CollectArgs a) {
-    if (blockIdx.x > 0) {   // zero the counters of every window of the launch
-        const int zb = blockIdx.x - 1, nzb = gridDim.x - 1;
-        for (int w = 0; w < a.nunits; ++w) {
-            uint4 *c4 = (uint4 *)a.cnt[w];
-            const uint32_t n4 = (1u << a.lp[w]) / 4;
-            for (uint32_t i = zb * blockDim.x + threadIdx.x; i < n4; i += nzb * blockDim.x) c4[i] = make_uint4(0, 0, 0, 0);
-        }
-        return;
-    }
-    constexpr int SW = (int)(sizeof(BatchStats) / 8);
-    __shared__ uint64_t s_seg[1024];
-    __shared__ uint32_t s_chk[1024];
-    unsigned long long *sw = (unsigned long long *)st;
-    const int nb = a.nunits * 256, b = threadIdx.x;
-    unsigned long long n_b = 0;
-    uint32_t pcap = 0, chunks = 0;
-    uint64_t seg = 0;
-    if (b < nb) {
-        n_b = cursor[(size_t)b * LOG_CUR_STRIDE];
-        cursor[(size_t)b * LOG_CUR_STRIDE] = 0;
-        a.rb[b] = n_b;
-        if (n_b) {
-            const int F = 1 << (a.lp[b >> 8] - 8);
-            const double mean = (double)n_b / (double)F;
-            pcap = (uint32_t)ceil(__dadd_rn(__dadd_rn(mean, __dmul_rn(6.0, sqrt(mean))), 4.0));
-            seg = (uint64_t)F * pcap;
-            chunks = (uint32_t)((n_b + LOG_TILE - 1) / LOG_TILE);
-        }
-    }
-    s_seg[b] = seg;
-    s_chk[b] = chunks;
-    unsigned long long w = 0;
-    if (b < SW) {
-        w = sw[b];
-        a.rb[LOG_NU * 256 + b] = w;
-    }
-    __syncthreads();
-    if (b < SW) sw[b] = 0;
-    // inclusive scans (Hillis-Steele): segment records within each window's 256 buckets, chunks overall
-    for (int off = 1; off < 1024; off <<= 1) {
-        uint64_t xs = 0;
-        uint32_t xc = 0;
-        if (b >= off) {
-            xc = s_chk[b - off];
-            if ((b & 255) >= off) xs = s_seg[b - off];
-        }
-        __syncthreads();
-        s_seg[b] += xs;
-        s_chk[b] += xc;
-        __syncthreads();
-    }
-    if (b == 0) {
-        st->min_idx = 0x7fffffffffffffffLL;
-        st->max_idx = (long long)0x8000000000000000LL;
-    }
-    if (b < nb) {
-        LogBucket B;
-        B.src = (uint64_t)b * a.cap;
-        B.n = (uint32_t)n_b;
-        B.pcap = pcap;
-        B.seg_base = (uint32_t)(s_seg[b] - seg);
-        B.chunk0 = s_chk[b] - chunks;
-        a.bk[b] = B;
-        if ((b & 255) == 255) a.rb[LOG_RB_SEG + (b >> 8)] = s_seg[b];
-        if (b == nb - 1) {
-            LogBucket E{};
-            E.chunk0 = s_chk[b];
-            a.bk[nb] = E;
-            a.rb[LOG_RB_CHUNKS] = s_chk[b];
-        }
-    }
-    // the host spins on the sequence word: every other readback word must be visible first
-    __threadfence_system();
-    __syncthreads();
-    if (b == 0) {
-        __threadfence_system();
-        *(volatile unsigned long long *)&a.rb[LOG_RB_SEQ] = a.seq;
-    }
-}
-
-void launch_log_collect(unsigned long long *cursor, BatchStats *stats, const CollectArgs &a, hipStream_t s) {
-    hipLaunchKernelGGL(log_collect_kernel, dim3(1 + 32), dim3(1024), 0, s, cursor, stats, a);
-}
-
 void launch_log_split(const int64_t *tmp, int has_val, const LogBucket *buckets, int nb, const LogSegSet &segs,
-                      unsigned *overflow, uint32_t nchunks, hipStream_t s) {
+                      unsigned *overflow, uint32_t nchunks, const unsigned *go, hipStream_t s) {
     if (nchunks == 0) return;
     if (has_val)
         hipLaunchKernelGGL(log_split_kernel<true>, dim3(nchunks), dim3(LOG_TILE_THREADS), 0, s, tmp, buckets, nb, segs,
-                           overflow);
+                           overflow, go);
     else
         hipLaunchKernelGGL(log_split_kernel<false>, dim3(nchunks), dim3(LOG_TILE_THREADS), 0, s, tmp, buckets, nb,
-                           segs, overflow);
+                           segs, overflow, go);
 }
 
 // The fire's LDS hash table: 64 KiB of (1 + nwords) * 8 B slots (power of two).
@@ -1173,11 +1161,10 @@ void launch_log_fire(const LogSegDesc *segs, int nseg, int lp, int has_val, cons
     // persistent grid: two 64-KiB-LDS workgroups per CU, or fewer to leave room for concurrent kernels
     const uint32_t groups = (uint32_t)cus * (uint32_t)(max_per_cu < 2 ? max_per_cu : 2);
     uint32_t grid = parts < groups ? parts : groups;
-    static const int xp = getenv("GWO_FIRE_XP") ? atoi(getenv("GWO_FIRE_XP")) : 0;
 #define GWO_FIRE_NW(NW)                                                                                          \
     case NW:                                                                                                     \
         hipLaunchKernelGGL(log_fire_kernel<NW>, dim3(grid), dim3(LOG_FIRE_THREADS), lds, s, segs, nseg, parts, cl, \
-                           has_val, plan, rp, start, end, out, overflow, xp);                                    \
+                           has_val, plan, rp, start, end, out, overflow);                                    \
         break;
     switch (plan.nwords) {
         GWO_FIRE_NW(1)

@@ -264,7 +264,7 @@ gwo_status Handle::ensure_output(uint64_t extra) {
 
 // ---- profiling ---------------------------------------------------------------------------------
 void Handle::prof_begin(int k, hipStream_t s) {
-    if (!profiling) return;
+    if (!profiling || !((prof_mask >> k) & 1u)) return;
     if (!s) s = stream;
     hipEvent_t a, b;
     if (event_pool.size() >= 2) {   // events are recycled: hipEventCreate costs microseconds per call
@@ -918,6 +918,15 @@ gwo_status gwo_set_profiling(gwo_handle *hh, int32_t enabled) {
     Handle *h = reinterpret_cast<Handle *>(hh);
     if (!h) return GWO_ERR_INVALID_ARGUMENT;
     h->profiling = enabled != 0;
+    h->prof_mask = ~0u;
+    return GWO_OK;
+}
+
+gwo_status gwo_set_profiling_mask(gwo_handle *hh, uint32_t mask) {
+    Handle *h = reinterpret_cast<Handle *>(hh);
+    if (!h) return GWO_ERR_INVALID_ARGUMENT;
+    h->profiling = mask != 0;
+    h->prof_mask = mask;
     return GWO_OK;
 }
 

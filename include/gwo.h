@@ -210,6 +210,9 @@ typedef enum {
     GWO_KERNEL_COUNT_ = 7
 } gwo_kernel_id;
 gwo_status gwo_set_profiling(gwo_handle *h, int32_t enabled);
+/* Times only the kernels whose bit (1 << gwo_kernel_id) is set (each timed launch adds two event markers to
+ * the stream; 0 turns profiling off). */
+gwo_status gwo_set_profiling_mask(gwo_handle *h, uint32_t mask);
 gwo_status gwo_kernel_stats(gwo_handle *h, int32_t kernel, int64_t *launches, double *total_ms,
                             int64_t *items);
 gwo_status gwo_reset_stats(gwo_handle *h);
