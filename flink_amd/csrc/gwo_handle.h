@@ -15,6 +15,8 @@
         if (s__ != GWO_OK) return s__;       \
     } while (0)
 
+struct LogThr;   // gwo_log.h
+
 namespace gwo {
 
 const char *status_str(gwo_status s);
@@ -243,6 +245,7 @@ struct Handle {
     gwo_status log_resolve_split();
     gwo_status insert_log(const int64_t *k, const int64_t *t, const int64_t *v, int64_t n, int64_t stride = 1);
     gwo_status log_k1(LogJob &J, bool first_pass);
+    LogThr log_thresholds(const LogJob &J) const;
     void log_uncarve(const LogJob &J, int w, uint64_t keep);
     gwo_status log_commit_spec(LogJob &J, const unsigned long long *rbp);
     gwo_status log_resolve_k1(LogJob J);

@@ -37,7 +37,7 @@ struct LogJob {
     WindowGeom g{};              // geometry + watermark at gwo_submit time (classification input)
     long long base = 0;          // first window of the range
     int nunits = 1;
-    uint64_t cap = 0;            // records per (window, coarse digit) region of the batch buffer
+    uint64_t cap = 0;            // records per (window, coarse digit, region group) region of the batch buffer
     int slot = 0;                // batch buffer / readback slot
     unsigned long long seq = 0;  // readback sequence number of the last K1 launch
     LogSegDesc desc[LOG_NU] = {}; // the range's new segments: counters/offsets carved at launch, records after
@@ -80,7 +80,7 @@ struct LogState {
     std::vector<long long> fire_units;
     uint64_t fire_rows0 = 0, fire_bound = 0;
     unsigned long long *h_fire_out = nullptr;    // pinned [3]: row counter, overflow, slow partitions
-    unsigned long long *d_cursor = nullptr;      // [LOG_NU * 256 * LOG_CUR_STRIDE] bucket cursors of K1
+    unsigned long long *d_cursor = nullptr;      // [LOG_NU * 256 * LOG_XG * LOG_CUR_STRIDE] region cursors of K1
     // K1 readback per slot (LOG_RB_* layout), written into pinned host memory by log_collect_kernel,
     // which also leaves the device plan of pass 2 in d_bk (per slot) and resets cursors and stats
     unsigned long long *h_rb = nullptr, *d_rbh = nullptr;   // host / device views
@@ -121,8 +121,8 @@ static uint64_t group_capacity(double mean) {
 gwo_status Handle::log_init() {
     logst = new LogState();
     LogState &L = *logst;
-    GWO_TRY(dalloc((void **)&L.d_cursor, LOG_NU * 256 * LOG_CUR_STRIDE * 8));
-    GWO_TRY(hipcheck(hipMemsetAsync(L.d_cursor, 0, LOG_NU * 256 * LOG_CUR_STRIDE * 8, stream), "cursor"));
+    GWO_TRY(dalloc((void **)&L.d_cursor, LOG_NU * 256 * LOG_XG * LOG_CUR_STRIDE * 8));
+    GWO_TRY(hipcheck(hipMemsetAsync(L.d_cursor, 0, LOG_NU * 256 * LOG_XG * LOG_CUR_STRIDE * 8, stream), "cursor"));
     GWO_TRY(dalloc((void **)&L.d_bk, kPlanBytes * LOG_SLOTS));
     GWO_TRY(dalloc((void **)&L.d_plan, kPlanBytes));
     GWO_TRY(dalloc((void **)&L.d_overflow, 16));
@@ -148,6 +148,14 @@ gwo_status Handle::log_init() {
     GWO_TRY(hipcheck(hipEventCreateWithFlags(&ev_fire, hipEventDisableTiming), "event"));
     init_stats(0);   // afterwards K1's last workgroup resets the device stats after every launch
     L.cap_log2 = log_fire_cap_log2(plan.nwords);
+    warm_log_kernels(plan.nwords, needs_value, stream);
+    GWO_TRY(launch_ok("warm-up"));
+    {   // pass 2's code object too: a speculative launch whose verdict word is 0 exits at once
+        GWO_TRY(hipcheck(hipMemsetAsync(L.d_go, 0, LOG_SLOTS * sizeof(unsigned), stream), "go"));
+        GWO_TRY(hipcheck(hipMemsetAsync(L.d_bk, 0, kPlanBytes, stream), "plan"));
+        launch_log_split(nullptr, 1, needs_value, L.d_bk, 0, LogSegSet{}, L.d_split_flag, 1, L.d_go, stream);
+        GWO_TRY(launch_ok("warm-up"));
+    }
     return log_reserve();
 }
 
@@ -274,6 +282,10 @@ gwo_status Handle::log_split_exact(long long base, int nunits, uint64_t cap, con
     for (int b = 0; b < nb; ++b) wcount[b >> 8] += counts[b];
     std::vector<uint32_t> pcap_exact(nb, 0);   // after an overflow: the measured partition maximum
     LogSegSet set{};
+    // the device plan of this batch buffer holds each bucket's region-group offsets (xoff)
+    GWO_TRY(hipcheck(hipMemcpyAsync(L.h_buckets, L.bk(tmpx), (nb + 1) * sizeof(LogBucket), hipMemcpyDeviceToHost,
+                                    stream), "plan"));
+    GWO_TRY(hipcheck(hipStreamSynchronize(stream), "plan"));
     while (true) {
         uint32_t chunks = 0;
         for (int w = 0; w < nunits; ++w) {
@@ -287,7 +299,6 @@ gwo_status Handle::log_split_exact(long long base, int nunits, uint64_t cap, con
                 for (int dgt = 0; dgt < 256; ++dgt) {
                     const uint64_t n_b = counts[c0 + dgt];
                     LogBucket &B = L.h_buckets[c0 + dgt];
-                    B.src = (uint64_t)(c0 + dgt) * cap;
                     B.n = (uint32_t)n_b;
                     B.pcap = n_b ? std::max<uint32_t>((uint32_t)group_capacity((double)n_b / F), pcap_exact[c0 + dgt])
                                  : 0u;
@@ -320,8 +331,8 @@ gwo_status Handle::log_split_exact(long long base, int nunits, uint64_t cap, con
         L.h_split_flag[tmpx] = 0;
         GWO_TRY(hipcheck(hipMemcpyAsync(L.d_plan, L.h_buckets, (nb + 1) * sizeof(LogBucket), hipMemcpyHostToDevice, stream),
                          "split plan"));
-        launch_log_split((const int64_t *)L.tmp[tmpx].ptr, needs_value, L.d_plan, nb, set, L.d_split_flag + tmpx, chunks,
-                         nullptr, stream);
+        launch_log_split((const int64_t *)L.tmp[tmpx].ptr, cap, needs_value, L.d_plan, nb, set, L.d_split_flag + tmpx,
+                         chunks, nullptr, stream);
         GWO_TRY(launch_ok("log split"));
         GWO_TRY(hipcheck(hipStreamSynchronize(stream), "log split"));
         if (L.h_split_flag[tmpx] == 0) break;
@@ -391,7 +402,7 @@ gwo_status Handle::log_split_dev(const LogJob &J, const unsigned long long *rbp)
     }
     L.h_split_flag[J.slot] = 0;
     prof_begin(GWO_KERNEL_PARTITION);
-    launch_log_split((const int64_t *)L.tmp[J.slot].ptr, needs_value, L.bk(J.slot), J.nunits * 256, set,
+    launch_log_split((const int64_t *)L.tmp[J.slot].ptr, J.cap, needs_value, L.bk(J.slot), J.nunits * 256, set,
                      L.d_split_flag + J.slot, (uint32_t)rbp[LOG_RB_CHUNKS], nullptr, stream);
     GWO_TRY(launch_ok("log split"));
     prof_end(GWO_KERNEL_PARTITION, (int64_t)total);
@@ -448,6 +459,27 @@ static uint64_t seg_upper_bound(uint64_t n, int lp) {
     return (uint64_t)std::ceil((double)n + 96.0 * std::sqrt(F * (double)n) + 1280.0 * F) + 64;
 }
 
+// Window bounds of K1's launch range [base, base + nunits) and each window's class at the batch's watermark
+// (WindowOperator.java:386-427: isWindowLate via cleanupTime, EventTimeTrigger.onElement FIRE for maxTs <= wm),
+// so K1 classifies a record inside the range by comparing its timestamp with the bounds.  Off when a bound
+// leaves the int64 range or lies where getWindowStartWithOffset is not monotone (ts < offset - size).
+LogThr Handle::log_thresholds(const LogJob &J) const {
+    LogThr t{};
+    for (int j = 0; j <= LOG_NU; ++j) t.bound[j] = (int64_t)0x7fffffffffffffffLL;
+    t.full_range = cfg.key_group_start == 0 && cfg.key_group_end == cfg.max_parallelism - 1;
+    const __int128 size = cfg.size, s0 = (__int128)J.base * size + (__int128)geom.unit_off_mod;
+    const __int128 lo = (__int128)(int64_t)0x8000000000000000LL, hi = (__int128)(int64_t)0x7fffffffffffffffLL;
+    if (s0 <= lo || s0 + (__int128)J.nunits * size > hi || s0 < (__int128)geom.offset - size) return t;
+    for (int j = 0; j <= J.nunits; ++j) t.bound[j] = (int64_t)(s0 + (__int128)j * size);
+    for (int j = 0; j < J.nunits; ++j) {
+        const int64_t max_ts = (int64_t)(s0 + (__int128)(j + 1) * size - 1);
+        const uint32_t c = cleanup_time_host(max_ts) <= J.g.wm ? 1u : (max_ts <= J.g.wm ? 2u : 0u);
+        t.cls |= c << (2 * j);
+    }
+    t.ok = 1;
+    return t;
+}
+
 // K1 of job J (one window range of a batch) into batch buffer J.slot; its last workgroup writes the readback
 // block (bucket counts, statistics, device plan of pass 2); ev_rb[J.slot] marks the readback's completion.
 // J.spec: each window's segment records are carved now with an upper bound and pass 2 is queued right
@@ -493,15 +525,17 @@ gwo_status Handle::log_k1(LogJob &J, bool first_pass) {
         ca.cnt[w] = d.cnt;
     }
     DevBuf &tmp = L.tmp[J.slot];
-    if (tmp.bytes < (size_t)J.nunits * 256 * J.cap * W * 8) {
+    if (tmp.bytes < (size_t)J.nunits * 256 * LOG_XG * J.cap * W * 8) {
         GWO_TRY(log_resolve_split());   // ensure_buf may free: nothing may still read it
-        GWO_TRY(ensure_buf(tmp, (size_t)J.nunits * 256 * J.cap * W * 8));
+        // sized for LOG_NU windows, so a batch spanning more windows than the last one does not reallocate
+        GWO_TRY(ensure_buf(tmp, (size_t)std::max(J.nunits, LOG_NU) * 256 * LOG_XG * J.cap * W * 8));
     }
     const bool side = first_pass && side_enabled();
+    const LogThr thr = log_thresholds(J);
     prof_begin(GWO_KERNEL_INSERT);
     launch_log_part(J.k, J.t, J.v, J.n, J.stride, J.g, J.base, J.nunits, needs_value, L.d_cursor, J.cap,
                     (int64_t *)tmp.ptr, d_stats, (int64_t *)side_key.ptr, (int64_t *)side_ts.ptr,
-                    (int64_t *)side_val.ptr, d_side_count, side ? side_cap : 0, side, ca, stream);
+                    (int64_t *)side_val.ptr, d_side_count, side ? side_cap : 0, side, ca, thr, stream);
     GWO_TRY(launch_ok("log partition"));
     prof_end(GWO_KERNEL_INSERT, J.n);
     if (side) GWO_TRY(hipcheck(hipMemcpyAsync(h_scalar, d_side_count, 8, hipMemcpyDeviceToHost, stream), "side count"));
@@ -513,7 +547,7 @@ gwo_status Handle::log_k1(LogJob &J, bool first_pass) {
         const uint64_t grid = ((uint64_t)J.n + LOG_TILE - 1) / LOG_TILE + (uint64_t)J.nunits * 256;
         L.h_split_flag[J.slot] = 0;
         prof_begin(GWO_KERNEL_PARTITION);
-        launch_log_split((const int64_t *)tmp.ptr, needs_value, L.bk(J.slot), J.nunits * 256, set,
+        launch_log_split((const int64_t *)tmp.ptr, J.cap, needs_value, L.bk(J.slot), J.nunits * 256, set,
                          L.d_split_flag + J.slot, (uint32_t)grid, L.d_go + J.slot, stream);
         GWO_TRY(launch_ok("log split"));
         prof_end(GWO_KERNEL_PARTITION, J.n);
@@ -628,9 +662,8 @@ gwo_status Handle::log_resolve_k1(LogJob J) {
                 continue;
             }
         }
-        uint64_t maxc = 0;
-        for (int b = 0; b < J.nunits * 256; ++b) maxc = std::max<uint64_t>(maxc, rbp[b]);
-        if (maxc > J.cap) {   // a bucket overflowed its capacity (skewed keys): redo this range exactly
+        const uint64_t maxc = rbp[LOG_RB_MAXREG];
+        if (maxc > J.cap) {   // a region overflowed its capacity (skewed keys): redo this range exactly
             J.cap = maxc;
             GWO_TRY(log_k1(J, false));
             continue;
@@ -667,7 +700,7 @@ gwo_status Handle::insert_log(const int64_t *k, const int64_t *t, const int64_t 
     J.g = geom_now();
     J.base = hist_hint;
     J.nunits = (int)std::min<long long>(LOG_NU, std::max<long long>(1, L.span_hint));
-    J.cap = group_capacity((double)n / 256.0);
+    J.cap = group_capacity((double)n / (256.0 * LOG_XG));
     // speculative pass 2 (no host round trip between K1 and pass 2) unless late records go to the side output
     // (K1's first pass appends them; a re-run must not repeat that)
     J.spec = !side_enabled();

@@ -22,6 +22,12 @@ static_assert(LOG_K1_PER * LOG_K1_THREADS == LOG_TILE, "K1 tile and pass-2 chunk
 #define LOG_MAX_LP 18            // at most 2^18 partitions per window (<= 1024 per coarse digit)
 #define LOG_FIRE_THREADS 512
 #define LOG_CUR_STRIDE 16        // K1 bucket cursors: one per 128-B line (memory-side atomics serialise per line)
+#ifndef LOG_XG
+#define LOG_XG 1                 // K1 region groups per bucket: workgroup w appends to group w % LOG_XG.  With 8
+                                 // (workgroups w and w + 8 share an XCD) each group's runs merge in one L2: K1 alone
+                                 // ran 13 % faster in isolation, but end to end K1 + pass 2 measured 221 + 100 us (1
+                                 // group), 224 + 122 (4), 223 + 134 (8) per C4 batch -- so one group
+#endif
 #define FIRE_RPT 7                                   // records per thread in the fire's register prefetch
 #define FIRE_RCAP (FIRE_RPT * LOG_FIRE_THREADS)      // 3584: records per partition of the fire's fast path
 #define FIRE_OWN_LOG2 13
@@ -43,13 +49,26 @@ struct LogSegDesc {
     int32_t pad;
 };
 
-// Pass-2 work description of one coarse bucket (window w of the launch, coarse digit d).
+// Pass-2 work description of one coarse bucket b (window w of the launch, coarse digit d).  The bucket's
+// records sit in LOG_XG regions of the batch buffer: group x holds records [(b * LOG_XG + x) * cap, + count).
 struct LogBucket {
-    uint64_t src;                // first record of the bucket in the batch buffer
     uint32_t n;                  // records in the bucket
     uint32_t pcap;               // capacity of each of the bucket's 2^(lp-8) partitions in the segment
     uint32_t seg_base;           // first record of the bucket's partitions in the segment
     uint32_t chunk0;             // first pass-2 workgroup of the bucket (prefix over buckets)
+    uint32_t xoff[LOG_XG];       // exclusive prefix of the groups' record counts (the bucket read as one array)
+};
+
+// K1's classification by window bounds (tumbling): a record with bound[0] <= ts < bound[nunits] belongs to
+// window base + j for the j with bound[j] <= ts < bound[j + 1] -- a few compares instead of the window
+// arithmetic; valid only where getWindowStartWithOffset is monotone (ts >= offset - size).  Records outside
+// take the full restatement.
+struct LogThr {
+    int64_t bound[LOG_NU + 1];   // window starts base .. base + nunits (unused entries: Long.MAX_VALUE)
+    uint32_t cls;                // 2 bits per window: 0 accept, 1 window late (cleanup time passed), 2 re-fire
+    int32_t ok;                  // 1: the bounds are valid
+    int32_t full_range;          // 1: the subtask owns every key group (no key-group check needed)
+    int32_t pad;
 };
 
 // The segment descriptors of one pass-2 launch (kernel argument).
@@ -64,7 +83,8 @@ static constexpr int LOG_RB_STATS = LOG_NU * 256;
 static constexpr int LOG_RB_SEG = LOG_RB_STATS + (int)((sizeof(BatchStats) + 7) / 8);
 static constexpr int LOG_RB_CHUNKS = LOG_RB_SEG + LOG_NU;
 static constexpr int LOG_RB_GO = LOG_RB_CHUNKS + 1;
-static constexpr int LOG_RB_SEQ = LOG_RB_GO + 1;         // written last: the launch's sequence number
+static constexpr int LOG_RB_MAXREG = LOG_RB_GO + 1;      // largest region count (> cap: K1 dropped records)
+static constexpr int LOG_RB_SEQ = LOG_RB_MAXREG + 1;     // written last: the launch's sequence number
 static constexpr int LOG_RB_WORDS = LOG_RB_SEQ + 1;
 
 // What K1's last workgroup needs to plan pass 2 (the former collect step, fused into K1's tail).
@@ -72,7 +92,7 @@ struct CollectArgs {
     int nunits;
     int lp[LOG_NU];              // partition bits of each window of the launch
     uint32_t *cnt[LOG_NU];       // the windows' new segment counters (zeroed by every K1 workgroup first)
-    uint64_t cap;                // bucket region capacity of the batch buffer
+    uint64_t cap;                // region capacity of the batch buffer (records per bucket and region group)
     uint64_t seg_cap[LOG_NU];    // speculative pass 2: segment records carved per window (spec only)
     int spec;                    // 1: a pass 2 is queued behind K1 and runs iff the plan fits (rb[LOG_RB_GO])
     LogBucket *bk;               // out: [nunits * 256 + 1] pass-2 plan (device)
@@ -91,13 +111,16 @@ void launch_log_part(const int64_t *key, const int64_t *ts, const int64_t *val, 
                      long long base, int nunits, int has_val, unsigned long long *cursor, uint64_t cap,
                      int64_t *tmp, BatchStats *st, int64_t *side_key, int64_t *side_ts, int64_t *side_val,
                      unsigned long long *side_count, long long side_cap, int side_enabled, const CollectArgs &ca,
-                     hipStream_t s);
+                     const LogThr &thr, hipStream_t s);
 // Pass 2: every coarse bucket -> its window's segment, grouped by partition.  `overflow` is a
 // host-visible flag (set to 1 when a partition exceeds its capacity).  go != NULL: a speculative launch
 // of `nchunks` (an upper bound) workgroups that exits unless *go (K1's verdict) is set.
-void launch_log_split(const int64_t *tmp, int has_val, const LogBucket *buckets, int nb, const LogSegSet &segs,
-                      unsigned *overflow, uint32_t nchunks, const unsigned *go, hipStream_t s);
+void launch_log_split(const int64_t *tmp, uint64_t cap, int has_val, const LogBucket *buckets, int nb,
+                      const LogSegSet &segs, unsigned *overflow, uint32_t nchunks, const unsigned *go, hipStream_t s);
 int log_fire_cap_log2(int nwords);
+// Loads the fire and pass-2 code objects with empty launches (HIP loads a kernel's code on its first launch:
+// ~0.25 ms that would otherwise land on the first watermark that fires a window).
+void warm_log_kernels(int nwords, int has_val, hipStream_t s);
 void launch_log_fire(const LogSegDesc *segs, int nseg, int lp, int has_val, const AccPlan &plan,
                      const ResultPlan &rp, int64_t start, int64_t end, OutCols out, unsigned long long *overflow,
                      int cus, int max_per_cu, hipStream_t s);

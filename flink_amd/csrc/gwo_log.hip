@@ -112,9 +112,13 @@ __device__ __forceinline__ void k1_plan_tail(unsigned long long *cursor, BatchSt
     static_assert(SW <= LOG_K1_THREADS, "statistics words");
     __shared__ unsigned long long s_sw[SW];
     __shared__ unsigned s_bad;
+    __shared__ unsigned long long s_maxreg;
     const int t = threadIdx.x;
     unsigned long long *sw = (unsigned long long *)st;
-    if (t == 0) s_bad = 0;
+    if (t == 0) {
+        s_bad = 0;
+        s_maxreg = 0;
+    }
     if (t < SW) {   // read-and-reset through the same device-scope atomics the workgroups used
         const unsigned long long reset = t == 0 ? 0x7fffffffffffffffull : (t == 1 ? 0x8000000000000000ull : 0ull);
         const unsigned long long w = atomicExch(&sw[t], reset);
@@ -125,11 +129,20 @@ __device__ __forceinline__ void k1_plan_tail(unsigned long long *cursor, BatchSt
     const BatchStats &S = *(const BatchStats *)s_sw;
     unsigned long long chunk_run = 0;
     unsigned bad = 0;
+    unsigned long long maxreg = 0;
     for (int q = 0; q < a.nunits; ++q) {   // window q of the launch: bucket b = q * 256 + t (digit t)
         const int b = q * 256 + t;
-        const unsigned long long n_b = atomicExch(&cursor[(size_t)b * LOG_CUR_STRIDE], 0ull);
+        unsigned long long c[LOG_XG], n_b = 0;
+#pragma unroll
+        for (int x = 0; x < LOG_XG; ++x) c[x] = atomicExch(&cursor[((size_t)b * LOG_XG + x) * LOG_CUR_STRIDE], 0ull);
+        uint32_t xoff[LOG_XG];
+#pragma unroll
+        for (int x = 0; x < LOG_XG; ++x) {
+            xoff[x] = (uint32_t)n_b;
+            n_b += c[x];
+            maxreg = c[x] > maxreg ? c[x] : maxreg;
+        }
         a.rb[b] = n_b;
-        if (n_b > a.cap) bad = 1;          // K1 dropped records past the region: the host re-runs K1
         uint32_t pcap = 0, chunks = 0;
         unsigned long long seg = 0;
         if (n_b) {
@@ -143,8 +156,9 @@ __device__ __forceinline__ void k1_plan_tail(unsigned long long *cursor, BatchSt
         const unsigned long long seg_incl = block256_incl_scan64(seg, &seg_tot);
         const unsigned long long chk_incl = block256_incl_scan64(chunks, &chk_tot);
         LogBucket B;
-        B.src = (uint64_t)b * a.cap;
         B.n = (uint32_t)n_b;
+#pragma unroll
+        for (int x = 0; x < LOG_XG; ++x) B.xoff[x] = xoff[x];
         B.pcap = pcap;
         B.seg_base = (uint32_t)(seg_incl - seg);
         B.chunk0 = (uint32_t)(chunk_run + chk_incl - chunks);
@@ -155,7 +169,9 @@ __device__ __forceinline__ void k1_plan_tail(unsigned long long *cursor, BatchSt
         }
         chunk_run += chk_tot;
     }
+    if (maxreg > a.cap) bad = 1;           // K1 dropped records past a region: the host re-runs K1
     if (bad) atomicOr(&s_bad, 1u);
+    if (maxreg) atomicMax(&s_maxreg, maxreg);
     __syncthreads();
     if (t == 0) {
         LogBucket E{};
@@ -166,6 +182,7 @@ __device__ __forceinline__ void k1_plan_tail(unsigned long long *cursor, BatchSt
                         S.min_idx >= base && S.min_idx < base + a.nunits && chunk_run < (1ull << 32);
         *a.go = go ? 1u : 0u;
         a.rb[LOG_RB_GO] = go ? 1ull : 0ull;
+        a.rb[LOG_RB_MAXREG] = s_maxreg;
         *a.done = 0;   // the next K1 launch counts from zero (stream order)
     }
     // the host spins on the sequence word: every other readback word must be visible first
@@ -179,15 +196,16 @@ __device__ __forceinline__ void k1_plan_tail(unsigned long long *cursor, BatchSt
 
 // ------------------------------------------------------------------------------------------------
 // K1 log_part: batch -> batch buffer, grouped by bucket b = (window - base) * 256 + coarse digit.
-// Bucket b owns records [b*cap, (b+1)*cap) of the buffer; cursor[b*LOG_CUR_STRIDE] ends as its record
-// count (also when it exceeds cap: those records are not written and the host reruns).
+// Bucket b owns LOG_XG regions of cap records; workgroup w appends to region group x = w % LOG_XG at
+// records [(b * LOG_XG + x) * cap, ...), whose cursor cursor[(b * LOG_XG + x) * LOG_CUR_STRIDE] ends as its
+// record count (also when it exceeds cap: those records are not written and the host reruns).
 // ------------------------------------------------------------------------------------------------
 template <bool HASV, int S>   // S: record stride in int64 words (1: SoA columns, 3: {key, ts, value}; 0: runtime)
 __global__ __launch_bounds__(LOG_K1_THREADS) void log_part_kernel(
     const int64_t *__restrict__ key, const int64_t *__restrict__ ts, const int64_t *__restrict__ val, int64_t n,
     int64_t stride, WindowGeom g, long long base, int nunits, unsigned long long *__restrict__ cursor, uint64_t cap,
     int64_t *__restrict__ tmp, BatchStats *st, int64_t *side_key, int64_t *side_ts, int64_t *side_val,
-    unsigned long long *side_count, long long side_cap, int side_enabled, CollectArgs ca) {
+    unsigned long long *side_count, long long side_cap, int side_enabled, CollectArgs ca, LogThr th) {
     constexpr int W = HASV ? 2 : 1;
     // the new segments' partition counters (pass 2's cursors) start at zero: pass 2 follows in stream order
     for (int w = 0; w < ca.nunits; ++w) {
@@ -204,6 +222,7 @@ __global__ __launch_bounds__(LOG_K1_THREADS) void log_part_kernel(
     const int nb = nunits * 256;
     const int per = (nb + LOG_K1_THREADS - 1) / LOG_K1_THREADS;   // counters owned per thread (<= 4)
     const int tid = threadIdx.x;
+    const int xg = blockIdx.x % LOG_XG;                           // region group (an XCD under round-robin placement)
     long long mn = 0x7fffffffffffffffLL, mx = (long long)0x8000000000000000LL;
     unsigned acc = 0, late = 0, refire = 0, bad_ts = 0, out = 0, bad_kg = 0;   // per thread: < 2^32 records
     int64_t kk[LOG_K1_PER], vv[LOG_K1_PER], tt[LOG_K1_PER];
@@ -232,13 +251,24 @@ __global__ __launch_bounds__(LOG_K1_THREADS) void log_part_kernel(
             code[j] = 0xffffffffu;
             if (i >= n) continue;
             long long u = 0;
-            int c = log_classify(tt[j], g, u);
+            int c;
+            const int64_t t = tt[j];
+            if (th.ok && t >= th.bound[0] && t < th.bound[nunits]) {   // within the launch's windows
+                const int jj = (t >= th.bound[1]) + (t >= th.bound[2]) + (t >= th.bound[3]);
+                const uint32_t cc = (th.cls >> (2 * jj)) & 3u;
+                c = cc == 0 ? L_ACCEPT : (cc == 2 ? L_REFIRE : (jadd(t, g.lateness) <= g.wm ? L_LATE : L_SKIP));
+                u = base + jj;
+            } else {
+                c = log_classify(t, g, u);
+            }
             if (c == L_ACCEPT) {
                 int64_t k = kk[j];
-                int32_t kg = key_group(k, g.key_kind, g.max_par);
-                if (kg < g.kg_lo || kg > g.kg_hi) {
-                    bad_kg++;
-                    st->bad_kg_key = k;
+                if (!th.full_range) {
+                    int32_t kg = key_group(k, g.key_kind, g.max_par);
+                    if (kg < g.kg_lo || kg > g.kg_hi) {
+                        bad_kg++;
+                        st->bad_kg_key = k;
+                    }
                 }
                 acc++;
                 mn = u < mn ? u : mn;
@@ -268,17 +298,17 @@ __global__ __launch_bounds__(LOG_K1_THREADS) void log_part_kernel(
             }
         }
         __syncthreads();
-        uint32_t loc[4];
-        const uint32_t total = tile_offsets(s_cnt, s_off, nb, loc, per);
-        // reserve each bucket's run (the atomics' round trip overlaps the LDS scatter below);
-        // s_cnt[b] becomes the run's first record in the bucket
+        // reserve each bucket's run in this workgroup's region group, before the offsets scan, so that the
+        // atomics' round trip overlaps the scan and the LDS scatter; s_cnt[b] becomes the run's first record
         unsigned long long at[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-            int b = tid * per + q;
-            at[q] = 0;
-            if (q < per && loc[q]) at[q] = atomicAdd(&cursor[(size_t)b * LOG_CUR_STRIDE], (unsigned long long)loc[q]);
+            const int b = tid * per + q;
+            const uint32_t c = (q < per && b < nb) ? s_cnt[b] : 0u;
+            at[q] = c ? atomicAdd(&cursor[((size_t)b * LOG_XG + xg) * LOG_CUR_STRIDE], (unsigned long long)c) : 0ull;
         }
+        uint32_t loc[4];
+        const uint32_t total = tile_offsets(s_cnt, s_off, nb, loc, per);
 #pragma unroll
         for (int j = 0; j < LOG_K1_PER; ++j) {
             if (code[j] == 0xffffffffu) continue;
@@ -304,7 +334,7 @@ __global__ __launch_bounds__(LOG_K1_THREADS) void log_part_kernel(
             if (b >= (uint32_t)nb) continue;   // defensive: never a write outside the buffer
             uint64_t q = (uint64_t)s_cnt[b] + (p - s_off[b]);
             if (q < cap) {
-                int64_t *dst = tmp + ((uint64_t)b * cap + q) * W;
+                int64_t *dst = tmp + (((uint64_t)b * LOG_XG + xg) * cap + q) * W;
                 if (HASV) *(ll2 *)dst = *(const ll2 *)&s_rec[2 * p];
                 else *dst = s_rec[p];
             }
@@ -359,7 +389,7 @@ __global__ __launch_bounds__(LOG_K1_THREADS) void log_part_kernel(
 // records [seg_base + f*pcap, + pcap); cnt[p] is its cursor (ends as its count, overflow -> rerun).
 // ------------------------------------------------------------------------------------------------
 template <bool HASV>
-__global__ __launch_bounds__(LOG_TILE_THREADS) void log_split_kernel(const int64_t *__restrict__ tmp,
+__global__ __launch_bounds__(LOG_TILE_THREADS) void log_split_kernel(const int64_t *__restrict__ tmp, uint64_t cap,
                                                                      const LogBucket *__restrict__ bk, int nb,
                                                                      const LogSegSet segs,
                                                                      unsigned *overflow, const unsigned *go) {
@@ -400,11 +430,16 @@ __global__ __launch_bounds__(LOG_TILE_THREADS) void log_split_kernel(const int64
     const uint32_t m = min((uint32_t)LOG_TILE, B.n - begin);
     int64_t kk[LOG_TILE_PER], vv[LOG_TILE_PER];
     uint32_t code[LOG_TILE_PER];
-    // unconditional loads (a lane past the end re-reads the chunk's first record): no branch per load
+    // unconditional loads (a lane past the end re-reads the chunk's first record): no branch per load; record v
+    // of the bucket is record v - xoff[x] of region group x, the last group with xoff[x] <= v
 #pragma unroll
     for (int j = 0; j < LOG_TILE_PER; ++j) {
         uint32_t i = j * LOG_TILE_THREADS + tid;
-        const int64_t *src = tmp + (B.src + begin + (i < m ? i : 0u)) * W;
+        const uint32_t v = begin + (i < m ? i : 0u);
+        int x = 0;
+#pragma unroll
+        for (int y = 1; y < LOG_XG; ++y) x += v >= B.xoff[y];
+        const int64_t *src = tmp + (((uint64_t)c * LOG_XG + x) * cap + (v - B.xoff[x])) * W;
         if (HASV) {
             ll2 r2 = __builtin_nontemporal_load((const ll2 *)src);
             kk[j] = r2.x;
@@ -1110,13 +1145,13 @@ void launch_log_part(const int64_t *key, const int64_t *ts, const int64_t *val, 
                      long long base, int nunits, int has_val, unsigned long long *cursor, uint64_t cap,
                      int64_t *tmp, BatchStats *st, int64_t *side_key, int64_t *side_ts, int64_t *side_val,
                      unsigned long long *side_count, long long side_cap, int side_enabled, const CollectArgs &ca,
-                     hipStream_t s) {
+                     const LogThr &thr, hipStream_t s) {
     int64_t grid = (n + LOG_TILE - 1) / LOG_TILE;
     grid = grid < 1 ? 1 : (grid > LOG_K1_GRID ? LOG_K1_GRID : grid);
 #define GWO_K1(HV, S)                                                                                          \
     hipLaunchKernelGGL((log_part_kernel<HV, S>), dim3((int)grid), dim3(LOG_K1_THREADS), 0, s, key, ts, val, n, \
                        stride, g, base, nunits, cursor, cap, tmp, st, side_key, side_ts, side_val, side_count,   \
-                       side_cap, side_enabled, ca)
+                       side_cap, side_enabled, ca, thr)
     if (has_val) {
         if (stride == 1) GWO_K1(true, 1);
         else if (stride == 3) GWO_K1(true, 3);
@@ -1129,15 +1164,40 @@ void launch_log_part(const int64_t *key, const int64_t *ts, const int64_t *val, 
 #undef GWO_K1
 }
 
-void launch_log_split(const int64_t *tmp, int has_val, const LogBucket *buckets, int nb, const LogSegSet &segs,
-                      unsigned *overflow, uint32_t nchunks, const unsigned *go, hipStream_t s) {
+void launch_log_split(const int64_t *tmp, uint64_t cap, int has_val, const LogBucket *buckets, int nb,
+                      const LogSegSet &segs, unsigned *overflow, uint32_t nchunks, const unsigned *go, hipStream_t s) {
     if (nchunks == 0) return;
     if (has_val)
-        hipLaunchKernelGGL(log_split_kernel<true>, dim3(nchunks), dim3(LOG_TILE_THREADS), 0, s, tmp, buckets, nb, segs,
-                           overflow, go);
-    else
-        hipLaunchKernelGGL(log_split_kernel<false>, dim3(nchunks), dim3(LOG_TILE_THREADS), 0, s, tmp, buckets, nb,
+        hipLaunchKernelGGL(log_split_kernel<true>, dim3(nchunks), dim3(LOG_TILE_THREADS), 0, s, tmp, cap, buckets, nb,
                            segs, overflow, go);
+    else
+        hipLaunchKernelGGL(log_split_kernel<false>, dim3(nchunks), dim3(LOG_TILE_THREADS), 0, s, tmp, cap, buckets, nb,
+                           segs, overflow, go);
+}
+
+void warm_log_kernels(int nwords, int has_val, hipStream_t s) {
+    const AccPlan p{};
+    const ResultPlan rp{};
+    const OutCols o{};
+    const int cl = log_fire_cap_log2(nwords);
+    size_t lds = (size_t)(1 + nwords) * 8 << cl;
+    if (lds < (size_t)FIRE_LDS) lds = FIRE_LDS;
+#define GWO_WARM_NW(NW)                                                                                            \
+    case NW:                                                                                                       \
+        hipLaunchKernelGGL(log_fire_kernel<NW>, dim3(1), dim3(LOG_FIRE_THREADS), lds, s, nullptr, 0, 0u, cl, has_val, p, \
+                           rp, 0, 0, o, nullptr);                                                                  \
+        break;
+    switch (nwords) {
+        GWO_WARM_NW(1)
+        GWO_WARM_NW(2)
+        GWO_WARM_NW(3)
+        GWO_WARM_NW(4)
+        GWO_WARM_NW(5)
+        GWO_WARM_NW(6)
+        GWO_WARM_NW(7)
+        default: GWO_WARM_NW(8)
+    }
+#undef GWO_WARM_NW
 }
 
 // The fire's LDS hash table: 64 KiB of (1 + nwords) * 8 B slots (power of two).
