@@ -37,3 +37,9 @@ clean:
 	rm -rf build $(LIB)
 
 .PHONY: all clean
+
+# Access-pattern microbenchmark of the table layout; not part of the library.
+tools/micro_table: tools/micro_table.hip
+	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -o $@ $<
+tools: tools/micro_table
+.PHONY: tools

@@ -12,7 +12,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # GWO_LIB_PATH selects an alternative build of the same library (A/B kernel experiments)
 LIB_PATH = os.environ.get("GWO_LIB_PATH") or os.path.join(_HERE, "libgwo.so")
 
-GWO_ABI_VERSION = 2
+GWO_ABI_VERSION = 3
 GWO_MAX_AGGS = 4
 
 # gwo_status
@@ -54,6 +54,11 @@ class GwoSideOut(C.Structure):
     _fields_ = [("key", C.c_void_p), ("ts", C.c_void_p), ("value", C.c_void_p)]
 
 
+class GwoStateRows(C.Structure):
+    _fields_ = [("key", C.c_void_p), ("window_start", C.c_void_p), ("window_end", C.c_void_p), ("words", C.c_void_p),
+                ("key_group", C.c_void_p), ("timer", C.c_void_p)]
+
+
 class GwoGenSpec(C.Structure):
     _fields_ = [
         ("seed", C.c_uint64), ("first_index", C.c_int64), ("total_records", C.c_int64),
@@ -84,8 +89,8 @@ SIGNATURES = [
     ("gwo_current_watermark", C.c_int, [_P, _I64P]),
     ("gwo_state_size", C.c_int, [_P, _I64P]),
     ("gwo_snapshot_rows", C.c_int, [_P, _I64P, C.POINTER(C.c_int32)]),
-    ("gwo_snapshot", C.c_int, [_P, _P, _P, _P, C.c_int64, _I64P, _I64P]),
-    ("gwo_restore", C.c_int, [_P, _P, _P, _P, C.c_int64, C.c_int64]),
+    ("gwo_snapshot", C.c_int, [_P, C.POINTER(GwoStateRows), C.c_int64, _I64P, _I64P]),
+    ("gwo_restore", C.c_int, [_P, C.POINTER(GwoStateRows), C.c_int32, C.c_int64, C.c_int64]),
     ("gwo_sync", C.c_int, [_P]),
     ("gwo_get_stream", C.c_int, [_P, C.POINTER(_P)]),
     ("gwo_last_error", C.c_char_p, [_P]),

@@ -8,6 +8,7 @@
 
 #include "../../include/gwo.h"
 #include "gwo_internal.h"
+#include "gwo_hash.h"
 
 #define GWO_TRY(expr)                        \
     do {                                     \
@@ -18,6 +19,15 @@
 struct LogThr;   // gwo_log.h
 
 namespace gwo {
+
+// Checkpoint rows being restored, in host memory (gwo_snapshot.cpp).
+struct RestoreRows {
+    int64_t n = 0;
+    int nw = 0;
+    std::vector<int64_t> key, start, end, words;   // words: nw per row, row-major
+    std::vector<int32_t> timer;                    // empty: derive fire timers from the restored watermark
+    std::vector<char> mine;                        // row's key group lies in this subtask's KeyGroupRange
+};
 
 const char *status_str(gwo_status s);
 
@@ -159,10 +169,12 @@ struct Handle {
     gwo_status drain(const gwo_out *cols, int64_t cap, int64_t *n_out);
     gwo_status drain_side(const gwo_side_out *cols, int64_t cap, int64_t *n_out);
     gwo_status state_size(int64_t *entries);
-    gwo_status snapshot_supported();
+    // checkpoint / restore (gwo_snapshot.cpp)
+    gwo_status snapshot_quiesce();
     gwo_status snapshot_rows(int64_t *n_rows);
-    gwo_status snapshot(int64_t *key, int64_t *wstart, int64_t *words, int64_t cap, int64_t *n_out);
-    gwo_status restore(const int64_t *key, const int64_t *wstart, const int64_t *words, int64_t n, int64_t new_wm);
+    gwo_status snapshot(const gwo_state_rows *rows, int64_t cap, int64_t *n_out);
+    gwo_status restore(const gwo_state_rows *rows, int32_t n_words, int64_t n, int64_t new_wm);
+    gwo_status table_restore_rows(const RestoreRows &R, int64_t new_wm);
 
     gwo_status fail(gwo_status s, const char *fmt, ...);
     gwo_status poison(gwo_status s, const char *what);
@@ -233,6 +245,9 @@ struct Handle {
     gwo_status insert_session(const int64_t *k, const int64_t *t, const int64_t *v, int64_t n);
     gwo_status fire_session(int64_t new_wm);
     gwo_status session_state_size(int64_t *entries);
+    gwo_status session_snapshot_collect(const SnapCols &c);
+    gwo_status session_restore_rows(const RestoreRows &R, int64_t new_wm);
+    uint64_t session_live() const;
     // log-structured tumbling state (gwo_log.cpp)
     gwo_status log_init();
     gwo_status log_reserve();
@@ -255,6 +270,9 @@ struct Handle {
     gwo_status set_pipelined(bool on);
     gwo_status fire_log(int64_t new_wm);
     gwo_status log_state_size(int64_t *entries);
+    gwo_status log_snapshot_collect(const SnapCols &c);
+    gwo_status log_restore_rows(const RestoreRows &R, int64_t new_wm);
+    size_t log_window_count() const;
     // comm (gwo_comm.cpp)
     void comm_free();
     gwo_status comm_exchange(const int64_t *k, const int64_t *t, const int64_t *v, int64_t n, const int64_t **aos,

@@ -105,16 +105,26 @@ struct OutCols {
     int64_t *key;
     int64_t *start;
     int64_t *end;
-    int64_t *res[4];
+    int64_t *res[GWO_MAX_WORDS];       // result columns (a checkpoint's raw accumulator words use up to 8)
     unsigned long long *count;         // device row counter
     long long cap;
 };
 
 struct ResultPlan {
-    int32_t naggs;
-    int32_t kind[4];                   // gwo_agg_kind
-    int32_t word[4];                   // first accumulator word of each aggregate
+    int32_t naggs;                     // result columns (<= 4 aggregates; a raw-word plan: nwords <= 8)
+    int32_t kind[GWO_MAX_WORDS];       // gwo_agg_kind (COUNT = the word itself)
+    int32_t word[GWO_MAX_WORDS];       // first accumulator word of each aggregate
     int32_t value_is_f64;
+};
+
+// Checkpoint rows being collected on the device (SoA): one per (key, window) -- per pane for sliding windows,
+// per in-flight session for session windows -- with the raw accumulator words and the fire-timer flag.
+struct SnapCols {
+    int64_t *key, *start, *end;
+    int32_t *timer;                    // 1: the window's event-time fire timer is still pending
+    int64_t *w[GWO_MAX_WORDS];
+    unsigned long long *count;         // rows written (block reservations)
+    long long cap;
 };
 
 // Sessions (gwo_session.hip)

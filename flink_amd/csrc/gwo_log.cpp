@@ -27,6 +27,8 @@ struct LogWindow {
     std::vector<LogSegDesc> segs;
     std::vector<LogChunk> chunks;
     uint64_t records = 0;
+    LogSegDesc partial{};        // restored checkpoint accumulators (rec == nullptr: none), folded at the fire
+    uint64_t partial_rows = 0;
 };
 
 // One K1 launch over a window range of a batch (re-launched with a new range or capacity as needed).
@@ -253,6 +255,8 @@ void Handle::log_release(LogWindow &W) {
     for (auto &c : W.chunks) logst->free_chunks.emplace(c.size, c.base);
     W.chunks.clear();
     W.segs.clear();
+    W.partial = LogSegDesc{};
+    W.partial_rows = 0;
 }
 
 // Partitions of a new window: about 3/4 of the fire kernel's fast-path capacity (FIRE_RCAP records)
@@ -760,7 +764,7 @@ gwo_status Handle::fire_log(int64_t new_wm) {
     GWO_TRY(log_resolve_split());   // the fired windows' last segments must be complete
     due(fire);
     for (auto it = fire.begin(); it != fire.end();) {   // a window with no segment has nothing to emit
-        if (L.wins[*it].segs.empty()) {
+        if (L.wins[*it].segs.empty() && !L.wins[*it].partial.rec) {
             log_release(L.wins[*it]);   // offsets/counters carved for a K1 range that got no records
             L.wins.erase(*it);
             it = fire.erase(it);
@@ -779,8 +783,9 @@ gwo_status Handle::fire_log(int64_t new_wm) {
     uint64_t bound = 0, expect = 0;
     const uint64_t per_window = std::max<uint64_t>(L.last_window_keys, (uint64_t)std::max<int64_t>(cfg.expected_keys, 0));
     for (long long u : fire) {
-        bound += L.wins[u].records;
-        expect += std::min<uint64_t>(L.wins[u].records, per_window + per_window / 8 + 4096);
+        const uint64_t r = L.wins[u].records + L.wins[u].partial_rows;
+        bound += r;
+        expect += std::min<uint64_t>(r, per_window + per_window / 8 + 4096);
     }
     GWO_TRY(ensure_output(expect));
     size_t ndesc = 0;
@@ -813,7 +818,8 @@ gwo_status Handle::fire_log(int64_t new_wm) {
         int64_t end = (int64_t)((uint64_t)start + (uint64_t)cfg.size);
         prof_begin(GWO_KERNEL_FIRE, fs);
         launch_log_fire((const LogSegDesc *)L.firedesc.ptr + at, (int)W.segs.size(), W.lp, needs_value, plan, rplan,
-                        start, end, o, L.d_overflow, L.max_groups, async_fire ? 1 : 2, fs);
+                        start, end, o, L.d_overflow, L.max_groups, async_fire ? 1 : 2, W.partial.rec ? 1 : 0, W.partial,
+                        fs);
         GWO_TRY(launch_ok("log fire"));
         prof_end(GWO_KERNEL_FIRE, (int64_t)W.records, fs);
         at += W.segs.size();
@@ -850,7 +856,8 @@ gwo_status Handle::finish_fire() {
             int64_t start = unit_start(u);
             int64_t end = (int64_t)((uint64_t)start + (uint64_t)cfg.size);
             launch_log_fire((const LogSegDesc *)L.firedesc.ptr + at, (int)W.segs.size(), W.lp, needs_value, plan,
-                            rplan, start, end, o, L.d_overflow, L.max_groups, 2, stream);
+                            rplan, start, end, o, L.d_overflow, L.max_groups, 2, W.partial.rec ? 1 : 0, W.partial,
+                            stream);
             GWO_TRY(launch_ok("log fire"));
             at += W.segs.size();
         }
@@ -894,8 +901,117 @@ gwo_status Handle::set_pipelined(bool on) {
 gwo_status Handle::log_state_size(int64_t *entries) {
     GWO_TRY(log_flush());
     uint64_t s = 0;
-    for (auto &kv : logst->wins) s += kv.second.records;
+    for (auto &kv : logst->wins) s += kv.second.records + kv.second.partial_rows;
     *entries = (int64_t)s;
+    return GWO_OK;
+}
+
+}  // namespace gwo
+
+// ---- checkpoint / restore of the log layout (gwo_snapshot.cpp orchestrates) ---------------------------------
+namespace gwo {
+
+size_t Handle::log_window_count() const { return logst->wins.size(); }
+
+// Folds every open window without releasing it -- the fire kernel, LDS hash-table path only, with a result
+// plan that emits the raw accumulator words -- into checkpoint rows (fire timers pending: a log window is
+// released when it fires).
+gwo_status Handle::log_snapshot_collect(const SnapCols &c) {
+    LogState &L = *logst;
+    ResultPlan raw{};
+    raw.naggs = plan.nwords;
+    for (int w = 0; w < plan.nwords; ++w) {
+        raw.kind[w] = GWO_AGG_COUNT;   // a COUNT result is its accumulator word as it is
+        raw.word[w] = w;
+    }
+    OutCols o{};
+    o.key = c.key;
+    o.start = c.start;
+    o.end = c.end;
+    for (int w = 0; w < plan.nwords; ++w) o.res[w] = c.w[w];
+    o.count = c.count;
+    o.cap = c.cap;
+    if (L.max_groups == 0) {
+        int cus = 0;
+        GWO_TRY(hipcheck(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, cfg.device), "CU count"));
+        L.max_groups = std::max(cus, 1);
+    }
+    L.h_fire.clear();
+    for (auto &kv : L.wins)
+        for (auto &d : kv.second.segs) L.h_fire.push_back(d);
+    if (!L.h_fire.empty()) {
+        GWO_TRY(ensure_buf(L.firedesc, L.h_fire.size() * sizeof(LogSegDesc)));
+        GWO_TRY(hipcheck(hipMemcpy(L.firedesc.ptr, L.h_fire.data(), L.h_fire.size() * sizeof(LogSegDesc),
+                                   hipMemcpyHostToDevice), "snapshot desc"));
+    }
+    GWO_TRY(hipcheck(hipMemsetAsync(L.d_overflow, 0, 16, stream), "overflow"));
+    size_t at = 0;
+    for (auto &kv : L.wins) {
+        LogWindow &W = kv.second;
+        const int64_t start = unit_start(kv.first);
+        const int64_t end = (int64_t)((uint64_t)start + (uint64_t)cfg.size);
+        launch_log_fire((const LogSegDesc *)L.firedesc.ptr + at, (int)W.segs.size(), W.lp, needs_value, plan, raw, start,
+                        end, o, L.d_overflow, L.max_groups, 2, 1, W.partial, stream);
+        GWO_TRY(launch_ok("log snapshot"));
+        at += W.segs.size();
+    }
+    GWO_TRY(hipcheck(hipMemcpyAsync(L.h_fire_out + 1, L.d_overflow, 16, hipMemcpyDeviceToHost, stream), "overflow"));
+    GWO_TRY(hipcheck(hipStreamSynchronize(stream), "log snapshot"));
+    if (L.h_fire_out[1]) return poison(GWO_ERR_CAPACITY, "log snapshot: a partition overflowed its LDS table");
+    return GWO_OK;
+}
+
+// Restored rows of a window become that window's partial-accumulator segment: records of (key, raw words)
+// grouped by partition (top lp bits of digit_hash, as every later batch's segments), folded into the window's
+// rows at its fire.
+gwo_status Handle::log_restore_rows(const RestoreRows &R, int64_t new_wm) {
+    LogState &L = *logst;
+    std::map<long long, std::vector<int64_t>> rows_of;
+    for (int64_t i = 0; i < R.n; ++i) {
+        if (!R.mine[i]) continue;
+        const __int128 a = (__int128)R.start[i] - (__int128)geom.unit_off_mod;
+        __int128 q = a / geom.unit;
+        if (a % geom.unit != 0 && a < 0) q -= 1;
+        const long long u = (long long)q;
+        if (unit_start(u) != R.start[i])
+            return fail(GWO_ERR_INVALID_ARGUMENT, "restore: %lld is not a window start", (long long)R.start[i]);
+        if (!R.timer.empty() && R.timer[i] == 0)
+            return fail(GWO_ERR_UNSUPPORTED, "restore: the log layout holds no already emitted windows "
+                                             "(allowedLateness 0); use the table layout");
+        rows_of[u].push_back(i);
+    }
+    wm = new_wm;
+    const int RW = 1 + plan.nwords;
+    for (auto &kv : rows_of) {
+        const std::vector<int64_t> &ix = kv.second;
+        LogWindow &W = L.wins[kv.first];
+        W.lp = log_choose_lp((uint64_t)ix.size());
+        const uint32_t F = 1u << W.lp;
+        std::vector<uint32_t> cnt(F, 0), off(F, 0);
+        for (int64_t i : ix) cnt[digit_hash(R.key[i]) >> (32 - W.lp)]++;
+        uint32_t run = 0;
+        for (uint32_t p = 0; p < F; ++p) {
+            off[p] = run;
+            run += cnt[p];
+        }
+        std::vector<uint32_t> fill(off);
+        std::vector<int64_t> rec((size_t)ix.size() * RW);
+        for (int64_t i : ix) {
+            const uint32_t p = digit_hash(R.key[i]) >> (32 - W.lp);
+            int64_t *r = rec.data() + (size_t)fill[p]++ * RW;
+            r[0] = R.key[i];
+            for (int w = 0; w < plan.nwords; ++w) r[1 + w] = R.words[(size_t)i * R.nw + w];
+        }
+        char *p_rec = nullptr, *p_off = nullptr, *p_cnt = nullptr;
+        GWO_TRY(log_carve(W, rec.size() * 8, &p_rec));
+        GWO_TRY(log_carve(W, (size_t)F * 4, &p_off));
+        GWO_TRY(log_carve(W, (size_t)F * 4, &p_cnt));
+        GWO_TRY(hipcheck(hipMemcpy(p_rec, rec.data(), rec.size() * 8, hipMemcpyHostToDevice), "restore records"));
+        GWO_TRY(hipcheck(hipMemcpy(p_off, off.data(), (size_t)F * 4, hipMemcpyHostToDevice), "restore offsets"));
+        GWO_TRY(hipcheck(hipMemcpy(p_cnt, cnt.data(), (size_t)F * 4, hipMemcpyHostToDevice), "restore counts"));
+        W.partial = LogSegDesc{(int64_t *)p_rec, (uint32_t *)p_off, (uint32_t *)p_cnt, W.lp, 0};
+        W.partial_rows = ix.size();
+    }
     return GWO_OK;
 }
 

@@ -121,7 +121,10 @@ int log_fire_cap_log2(int nwords);
 // Loads the fire and pass-2 code objects with empty launches (HIP loads a kernel's code on its first launch:
 // ~0.25 ms that would otherwise land on the first watermark that fires a window).
 void warm_log_kernels(int nwords, int has_val, hipStream_t s);
+// Folds a window's segments (plus, when partial.rec is set, the restored accumulators of a checkpoint: records
+// of 1 + nwords words grouped by partition like a segment) and emits one row per key.  slow_only: every
+// partition takes the LDS hash-table path (a checkpoint fold with a raw-word result plan: up to 8 columns).
 void launch_log_fire(const LogSegDesc *segs, int nseg, int lp, int has_val, const AccPlan &plan,
                      const ResultPlan &rp, int64_t start, int64_t end, OutCols out, unsigned long long *overflow,
-                     int cus, int max_per_cu, hipStream_t s);
+                     int cus, int max_per_cu, int slow_only, const LogSegDesc &partial, hipStream_t s);
 }  // namespace gwo

@@ -581,6 +581,37 @@ __device__ __forceinline__ void fire_insert(const FireCtx &c, const AccPlan &p, 
     for (int w = 0; w < p.nwords; ++w) lds_combine64(acc + w * accs, p.op[w], lift_word(p, w, v));
 }
 
+// Folds a partial accumulator (restored from a checkpoint: raw words, already lifted) into the LDS table.
+__device__ __forceinline__ void fire_insert_words(const FireCtx &c, const AccPlan &p, int64_t k, uint64_t h,
+                                                  const int64_t *words) {
+    int64_t *acc;
+    int accs;
+    if (k == GWO_EMPTY_KEY) {
+        c.side[0] = 1;
+        acc = c.side + 1;
+        accs = 1;
+    } else {
+        int slot = (int)(h & (uint64_t)(c.cap - 1)), probes = 0;
+        while (true) {
+            unsigned long long prev = atomicCAS((unsigned long long *)&c.key[slot], (unsigned long long)GWO_EMPTY_KEY,
+                                                (unsigned long long)k);
+            if ((int64_t)prev == GWO_EMPTY_KEY) {
+                if (atomicAdd(c.used, 1u) >= c.limit) *c.fail = 1;
+                break;
+            }
+            if ((int64_t)prev == k) break;
+            slot = (slot + 1) & (c.cap - 1);
+            if (++probes >= c.cap) {
+                *c.fail = 1;
+                return;
+            }
+        }
+        acc = c.acc + slot;
+        accs = c.cap;
+    }
+    for (int w = 0; w < p.nwords; ++w) lds_combine64(acc + w * accs, p.op[w], words[w]);
+}
+
 // Resets every slot, the side slot and the flags (caller synchronises).
 __device__ __forceinline__ void fire_clear(const FireCtx &c, const AccPlan &p) {
     for (int i = threadIdx.x; i < c.cap; i += LOG_FIRE_THREADS) {
@@ -742,7 +773,8 @@ __global__ __launch_bounds__(LOG_FIRE_THREADS) __attribute__((amdgpu_waves_per_e
                                                                     uint32_t nparts, int cap_log2, int has_val,
                                                                     AccPlan p, ResultPlan rp, int64_t start,
                                                                     int64_t end, OutCols o,
-                                                                    unsigned long long *overflow) {
+                                                                    unsigned long long *overflow, int slow_only,
+                                                                    LogSegDesc partial) {
     // Dynamic LDS (FIRE_LDS bytes).  Fast path:
     //   s_key [FIRE_RCAP] int64   record keys (record i = r * 512 + tid), then leader keys by row ordinal
     //   s_val [FIRE_RCAP] int64   values grouped by key (after the election; overlays s_own)
@@ -806,6 +838,11 @@ __global__ __launch_bounds__(LOG_FIRE_THREADS) __attribute__((amdgpu_waves_per_e
     // so LDS waits in between do not wait for them
     int64_t rk[FIRE_RPT], rv[FIRE_RPT];
     auto prefetch = [&](bool on) {
+        if (!on) {   // uniform: nothing to prefetch (no next partition, or a slow-path-only fold)
+#pragma unroll
+            for (int r = 0; r < FIRE_RPT; ++r) rk[r] = rv[r] = 0;
+            return;
+        }
         const uint32_t total = s_beg[nseg];
         const bool fits = on && total <= (uint32_t)FIRE_RCAP;
         const int64_t *addr[FIRE_RPT];
@@ -859,7 +896,7 @@ __global__ __launch_bounds__(LOG_FIRE_THREADS) __attribute__((amdgpu_waves_per_e
         a_off = seg_off[part];
     }
     publish(a_cnt, a_off);
-    prefetch(true);
+    prefetch(!slow_only);
     while (true) {
         const uint32_t total = s_beg[nseg];
         const uint32_t nxt = part + gridDim.x;
@@ -875,7 +912,7 @@ __global__ __launch_bounds__(LOG_FIRE_THREADS) __attribute__((amdgpu_waves_per_e
             }
         };
         unsigned long long rbase_lane0 = 0;   // wave 0 lane 0: the row reservation, consumed after P4
-        bool fast = total <= (uint32_t)FIRE_RCAP;
+        bool fast = !slow_only && total <= (uint32_t)FIRE_RCAP;
         if (fast) {
             // P0: record keys into LDS; free election table; zero counts
 #pragma unroll
@@ -1030,6 +1067,19 @@ __global__ __launch_bounds__(LOG_FIRE_THREADS) __attribute__((amdgpu_waves_per_e
                     }
                     fire_insert(c, p, k, h, has_val ? q[1] : 0);
                 }
+                if (partial.rec) {   // restored accumulators of this partition (raw words, combined as they are)
+                    const uint32_t pc = partial.cnt[part], po = partial.off[part];
+                    for (uint32_t i = tid; i < pc; i += LOG_FIRE_THREADS) {
+                        const int64_t *q = partial.rec + (uint64_t)(po + i) * (1 + p.nwords);
+                        const int64_t k = q[0];
+                        const uint64_t h = part_hash(k);
+                        if (ranged) {
+                            uint64_t sub = (uint32_t)(h >> 12);
+                            if (sub < lo || sub >= hi) continue;
+                        }
+                        fire_insert_words(c, p, k, h, q + 1);
+                    }
+                }
                 __syncthreads();
                 const bool failed = s_fail != 0;
                 __syncthreads();
@@ -1052,7 +1102,7 @@ __global__ __launch_bounds__(LOG_FIRE_THREADS) __attribute__((amdgpu_waves_per_e
         else __syncthreads();
         // unconditional, so the loads land straight in rk/rv (no loop-carried copy that would wait for
         // them): in flight during this partition's emit and the next one's election
-        prefetch(more);
+        prefetch(more && !slow_only);
         if (fast) {
             // P5: one row per leader, in ordinal order.  Thread t takes ordinal t - sh (sh = rbase & 1),
             // so lanes 2m and 2m+1 own a 16-B-aligned pair of global rows; after a DPP swap within the
@@ -1185,7 +1235,7 @@ void warm_log_kernels(int nwords, int has_val, hipStream_t s) {
 #define GWO_WARM_NW(NW)                                                                                            \
     case NW:                                                                                                       \
         hipLaunchKernelGGL(log_fire_kernel<NW>, dim3(1), dim3(LOG_FIRE_THREADS), lds, s, nullptr, 0, 0u, cl, has_val, p, \
-                           rp, 0, 0, o, nullptr);                                                                  \
+                           rp, 0, 0, o, nullptr, 0, LogSegDesc{});                                                 \
         break;
     switch (nwords) {
         GWO_WARM_NW(1)
@@ -1210,8 +1260,8 @@ int log_fire_cap_log2(int nwords) {
 
 void launch_log_fire(const LogSegDesc *segs, int nseg, int lp, int has_val, const AccPlan &plan,
                      const ResultPlan &rp, int64_t start, int64_t end, OutCols out, unsigned long long *overflow,
-                     int cus, int max_per_cu, hipStream_t s) {
-    if (nseg <= 0 || nseg > LOG_MAX_SEGS) return;   // nothing to fold (the host never asks; defensive)
+                     int cus, int max_per_cu, int slow_only, const LogSegDesc &partial, hipStream_t s) {
+    if (nseg < 0 || nseg > LOG_MAX_SEGS || (nseg == 0 && !partial.rec)) return;   // nothing to fold (defensive)
     static_assert(FIRE_OWN * 4 <= FIRE_RCAP * 12 && FIRE_OWN == (1 << FIRE_OWN_LOG2) && FIRE_RCAP <= 4096 &&
                       FIRE_MAXR < 16, "fire fast-path layout");
     int cl = log_fire_cap_log2(plan.nwords);
@@ -1224,7 +1274,7 @@ void launch_log_fire(const LogSegDesc *segs, int nseg, int lp, int has_val, cons
 #define GWO_FIRE_NW(NW)                                                                                          \
     case NW:                                                                                                     \
         hipLaunchKernelGGL(log_fire_kernel<NW>, dim3(grid), dim3(LOG_FIRE_THREADS), lds, s, segs, nseg, parts, cl, \
-                           has_val, plan, rp, start, end, out, overflow);                                    \
+                           has_val, plan, rp, start, end, out, overflow, slow_only, partial);                \
         break;
     switch (plan.nwords) {
         GWO_FIRE_NW(1)

@@ -400,117 +400,6 @@ gwo_status Handle::refire_rows(const int64_t *k, const int64_t *t, const int64_t
     return GWO_OK;
 }
 
-// ---- snapshot / restore (tumbling, table layout) -------------------------------------------------
-gwo_status Handle::snapshot_supported() {
-    if (cfg.assigner == GWO_ASSIGNER_SESSION || logst)
-        return fail(GWO_ERR_UNSUPPORTED, "snapshot/restore: tumbling or sliding windows with the table layout only");
-    return GWO_OK;
-}
-
-gwo_status Handle::snapshot_rows(int64_t *n_rows) {
-    GWO_TRY(snapshot_supported());
-    GWO_TRY(read_occupancy());
-    int64_t r = 0;
-    for (auto &kv : tables) r += (int64_t)kv.second.occ;
-    *n_rows = r;
-    return GWO_OK;
-}
-
-gwo_status Handle::snapshot(int64_t *key, int64_t *wstart, int64_t *words, int64_t cap, int64_t *n_out) {
-    GWO_TRY(snapshot_supported());
-    int64_t rows = 0;
-    GWO_TRY(snapshot_rows(&rows));
-    if (rows > cap) return fail(GWO_ERR_CAPACITY, "snapshot: %lld rows, buffer holds %lld", (long long)rows, (long long)cap);
-    const int NW = plan.nwords;
-    DevBuf bk, bs, bw;
-    GWO_TRY(ensure_buf(bk, (size_t)std::max<int64_t>(rows, 1) * 8));
-    GWO_TRY(ensure_buf(bs, (size_t)std::max<int64_t>(rows, 1) * 8));
-    GWO_TRY(ensure_buf(bw, (size_t)std::max<int64_t>(rows, 1) * NW * 8));
-    GWO_TRY(hipcheck(hipMemsetAsync(d_scratch_count, 0, 8, stream), "snapshot count"));
-    for (auto &kv : tables)
-        launch_snapshot(desc(kv.second), kv.second.cap, plan, unit_start(kv.first), (int64_t *)bk.ptr,
-                        (int64_t *)bs.ptr, (int64_t *)bw.ptr, d_scratch_count, rows, stream);
-    gwo_status st = launch_ok("snapshot");
-    if (st == GWO_OK && rows) {
-        st = hipcheck(hipMemcpyAsync(key, bk.ptr, rows * 8, hipMemcpyDefault, stream), "snapshot copy");
-        if (st == GWO_OK) st = hipcheck(hipMemcpyAsync(wstart, bs.ptr, rows * 8, hipMemcpyDefault, stream), "snapshot copy");
-        if (st == GWO_OK)
-            st = hipcheck(hipMemcpyAsync(words, bw.ptr, (size_t)rows * NW * 8, hipMemcpyDefault, stream), "snapshot copy");
-    }
-    if (st == GWO_OK) st = hipcheck(hipStreamSynchronize(stream), "snapshot sync");
-    bk.release();
-    bs.release();
-    bw.release();
-    *n_out = rows;
-    return st;
-}
-
-gwo_status Handle::restore(const int64_t *key, const int64_t *wstart, const int64_t *words, int64_t n, int64_t new_wm) {
-    GWO_TRY(snapshot_supported());
-    if (!tables.empty() || wm != (int64_t)0x8000000000000000LL)
-        return fail(GWO_ERR_STATE, "restore: the handle already holds state");
-    wm = new_wm;
-    if (n == 0) return slide ? slide_restore_anchor() : GWO_OK;
-    const int NW = plan.nwords;
-    // host view of the window (sliding: pane) starts (to size the tables); the rows themselves go to the device
-    std::vector<int64_t> hs((size_t)n);
-    GWO_TRY(hipcheck(hipMemcpy(hs.data(), wstart, (size_t)n * 8, hipMemcpyDefault), "restore starts"));
-    std::map<long long, uint64_t> per_unit;
-    for (int64_t x : hs) {
-        const __int128 a = (__int128)x - (__int128)geom.unit_off_mod;
-        __int128 q = a / geom.unit;
-        if (a % geom.unit != 0 && a < 0) q -= 1;   // floor (unit > 0)
-        const long long u = (long long)q;
-        if (unit_start(u) != x) return fail(GWO_ERR_INVALID_ARGUMENT, "restore: %lld is not a window start", (long long)x);
-        per_unit[u]++;
-    }
-    const long long lo = per_unit.begin()->first, hi = per_unit.rbegin()->first;
-    if (hi - lo >= (1LL << 20)) return fail(GWO_ERR_UNSUPPORTED, "restore: windows span more than 2^20 units");
-    for (auto &kv : per_unit) GWO_TRY(ensure_table(kv.first, kv.second));   // marks windows the watermark passed fired
-    const int dir_len = (int)(hi - lo + 1);
-    h_dir.assign(dir_len, TableDesc{});
-    for (auto &kv : tables) h_dir[kv.first - lo] = desc(kv.second);
-    GWO_TRY(ensure_buf(dir_buf, dir_len * sizeof(TableDesc)));
-    GWO_TRY(hipcheck(hipMemcpyAsync(dir_buf.ptr, h_dir.data(), dir_len * sizeof(TableDesc), hipMemcpyHostToDevice, stream),
-                     "restore dir"));
-    const int64_t *dk = key, *ds = wstart, *dw = words;
-    DevBuf bk, bs, bw;
-    if (!is_device_ptr(key)) {
-        GWO_TRY(ensure_buf(bk, (size_t)n * 8));
-        GWO_TRY(hipcheck(hipMemcpyAsync(bk.ptr, key, (size_t)n * 8, hipMemcpyHostToDevice, stream), "restore keys"));
-        dk = (const int64_t *)bk.ptr;
-    }
-    if (!is_device_ptr(wstart)) {
-        GWO_TRY(ensure_buf(bs, (size_t)n * 8));
-        GWO_TRY(hipcheck(hipMemcpyAsync(bs.ptr, hs.data(), (size_t)n * 8, hipMemcpyHostToDevice, stream), "restore starts"));
-        ds = (const int64_t *)bs.ptr;
-    }
-    if (!is_device_ptr(words)) {
-        GWO_TRY(ensure_buf(bw, (size_t)n * NW * 8));
-        GWO_TRY(hipcheck(hipMemcpyAsync(bw.ptr, words, (size_t)n * NW * 8, hipMemcpyHostToDevice, stream), "restore words"));
-        dw = (const int64_t *)bw.ptr;
-    }
-    launch_restore(dk, ds, dw, n, plan, geom_now(), (const TableDesc *)dir_buf.ptr, lo, dir_len, stream);
-    gwo_status st = launch_ok("restore");
-    if (st == GWO_OK) st = hipcheck(hipStreamSynchronize(stream), "restore sync");
-    bk.release();
-    bs.release();
-    bw.release();
-    for (auto &kv : tables) kv.second.dirty = true;
-    if (st == GWO_OK) st = read_occupancy();
-    // a table the restore left empty (all its rows belonged to other key groups) goes back to the pool
-    for (auto it = tables.begin(); it != tables.end();) {
-        if (it->second.occ == 0) {
-            release_table(it->second);
-            it = tables.erase(it);
-        } else {
-            ++it;
-        }
-    }
-    if (st == GWO_OK && slide) st = slide_restore_anchor();
-    return st;
-}
-
 gwo_status Handle::insert_windowed(const int64_t *k, const int64_t *t, const int64_t *v, int64_t n) {
     WindowGeom g = geom_now();
     // tumbling: re-fire records (allowedLateness > 0) are emitted per element and inserted
@@ -874,19 +763,20 @@ gwo_status gwo_snapshot_rows(gwo_handle *hh, int64_t *n_rows, int32_t *n_words) 
     return h->snapshot_rows(n_rows);
 }
 
-gwo_status gwo_snapshot(gwo_handle *hh, int64_t *key, int64_t *window_start, int64_t *words, int64_t cap,
-                        int64_t *n_out, int64_t *watermark) {
+gwo_status gwo_snapshot(gwo_handle *hh, const gwo_state_rows *rows, int64_t cap, int64_t *n_out, int64_t *watermark) {
     H_OR_FAIL;
-    if (!n_out || !watermark || cap < 0 || (cap > 0 && (!key || !window_start || !words))) return GWO_ERR_INVALID_ARGUMENT;
+    if (!rows || !n_out || !watermark || cap < 0 ||
+        (cap > 0 && (!rows->key || !rows->window_start || !rows->window_end || !rows->words)))
+        return GWO_ERR_INVALID_ARGUMENT;
     *watermark = h->wm;
-    return h->snapshot(key, window_start, words, cap, n_out);
+    return h->snapshot(rows, cap, n_out);
 }
 
-gwo_status gwo_restore(gwo_handle *hh, const int64_t *key, const int64_t *window_start, const int64_t *words, int64_t n,
-                       int64_t watermark) {
+gwo_status gwo_restore(gwo_handle *hh, const gwo_state_rows *rows, int32_t n_words, int64_t n, int64_t watermark) {
     H_OR_FAIL;
-    if (n < 0 || (n > 0 && (!key || !window_start || !words))) return GWO_ERR_INVALID_ARGUMENT;
-    return h->restore(key, window_start, words, n, watermark);
+    if (n < 0 || (n > 0 && (!rows || !rows->key || !rows->window_start || !rows->window_end || !rows->words)))
+        return GWO_ERR_INVALID_ARGUMENT;
+    return h->restore(rows, n_words, n, watermark);
 }
 
 gwo_status gwo_sync(gwo_handle *hh) {

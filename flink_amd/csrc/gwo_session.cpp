@@ -200,4 +200,63 @@ gwo_status Handle::session_state_size(int64_t *entries) {
     return GWO_OK;
 }
 
+// ---- checkpoint / restore (gwo_snapshot.cpp orchestrates; kernels in gwo_snapshot.hip) ----------------------
+void launch_snap_session(const TableDesc &t, uint64_t cap, int stride, const AccPlan &p, const SnapCols &c,
+                         hipStream_t s);
+void launch_sess_restore(const int64_t *key, const int64_t *start, const int64_t *end, const int32_t *timer,
+                         const int64_t *words, int64_t n, const TableDesc &t, uint64_t cap, int stride,
+                         const AccPlan &p, const SessGeom &g, SessErr *err, hipStream_t s);
+
+gwo_status Handle::session_snapshot_collect(const SnapCols &c) {
+    launch_snap_session(desc(sess->T), sess->T.cap, sess->stride, plan, c, stream);
+    return launch_ok("session snapshot");
+}
+
+uint64_t Handle::session_live() const { return sess->live; }
+
+// Rows of this subtask's key groups become in-flight sessions of their keys, each with its fire-timer flag
+// (a pending timer at maxTimestamp, EventTimeTrigger.java:37-45; without flags: pending iff maxTs > watermark).
+gwo_status Handle::session_restore_rows(const RestoreRows &R, int64_t new_wm) {
+    SessionState &S = *sess;
+    uint64_t mine = 0;
+    for (int64_t i = 0; i < R.n; ++i) {
+        if (!R.mine[i]) continue;
+        if (R.end[i] <= R.start[i]) return fail(GWO_ERR_INVALID_ARGUMENT, "restore: empty session window");
+        mine++;
+    }
+    wm = new_wm;
+    if (mine == 0) return GWO_OK;
+    GWO_TRY(sess_ensure(mine));
+    DevBuf k, st, en, tm, w;
+    GWO_TRY(ensure_buf(k, (size_t)R.n * 8));
+    GWO_TRY(ensure_buf(st, (size_t)R.n * 8));
+    GWO_TRY(ensure_buf(en, (size_t)R.n * 8));
+    GWO_TRY(ensure_buf(w, (size_t)R.n * R.nw * 8));
+    GWO_TRY(hipcheck(hipMemcpyAsync(k.ptr, R.key.data(), (size_t)R.n * 8, hipMemcpyHostToDevice, stream), "restore"));
+    GWO_TRY(hipcheck(hipMemcpyAsync(st.ptr, R.start.data(), (size_t)R.n * 8, hipMemcpyHostToDevice, stream), "restore"));
+    GWO_TRY(hipcheck(hipMemcpyAsync(en.ptr, R.end.data(), (size_t)R.n * 8, hipMemcpyHostToDevice, stream), "restore"));
+    GWO_TRY(hipcheck(hipMemcpyAsync(w.ptr, R.words.data(), (size_t)R.n * R.nw * 8, hipMemcpyHostToDevice, stream),
+                     "restore"));
+    if (!R.timer.empty()) {
+        GWO_TRY(ensure_buf(tm, (size_t)R.n * 4));
+        GWO_TRY(hipcheck(hipMemcpyAsync(tm.ptr, R.timer.data(), (size_t)R.n * 4, hipMemcpyHostToDevice, stream), "restore"));
+    }
+    GWO_TRY(hipcheck(hipMemsetAsync(S.d_err, 0, sizeof(SessErr), stream), "err"));
+    launch_sess_restore((const int64_t *)k.ptr, (const int64_t *)st.ptr, (const int64_t *)en.ptr,
+                        R.timer.empty() ? nullptr : (const int32_t *)tm.ptr, (const int64_t *)w.ptr, R.n, desc(S.T),
+                        S.T.cap, S.stride, plan, sess_geom(*this, S.smax), S.d_err, stream);
+    GWO_TRY(launch_ok("session restore"));
+    GWO_TRY(sess_read_err());
+    k.release();
+    st.release();
+    en.release();
+    tm.release();
+    w.release();
+    if (S.h_err->capacity)
+        return poison(GWO_ERR_CAPACITY, ("restore: a key has more than " + std::to_string(S.smax) +
+                                         " in-flight sessions").c_str());
+    S.live += S.h_err->live_delta;
+    return GWO_OK;
+}
+
 }  // namespace gwo

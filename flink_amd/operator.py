@@ -207,33 +207,56 @@ class GpuWindowOperator:
         return n.value
 
     def snapshot_state(self):
-        """Checkpoint of the keyed window state (tumbling, table layout): dict of numpy columns key,
-        window_start, words[n, n_words] and the watermark (gwo.h gwo_snapshot)."""
+        """Checkpoint of the keyed window state (every assigner and layout; gwo.h gwo_snapshot): numpy columns
+        key, window_start, window_end, words[n, n_words], key_group, timer (rows grouped by key group, the
+        heap backend's per-key-group (namespace, key, state) entries with their window timers) and the
+        watermark."""
         self.flush()
         n, nw = C.c_int64(), C.c_int32()
         N.check(self._lib.gwo_snapshot_rows(self._h, C.byref(n), C.byref(nw)), self._h, "gwo_snapshot_rows")
-        m = n.value
-        key = np.empty(max(m, 1), np.int64)
-        start = np.empty(max(m, 1), np.int64)
-        words = np.empty((max(m, 1), nw.value), np.int64)
+        m = max(n.value, 1)
+        cols = {"key": np.empty(m, np.int64), "window_start": np.empty(m, np.int64), "window_end": np.empty(m, np.int64),
+                "words": np.empty((m, nw.value), np.int64), "key_group": np.empty(m, np.int32),
+                "timer": np.empty(m, np.int32)}
+        rows = N.GwoStateRows(*[_ptr(cols[c]).value for c in ("key", "window_start", "window_end", "words", "key_group",
+                                                              "timer")])
         got, wm = C.c_int64(), C.c_int64()
-        N.check(self._lib.gwo_snapshot(self._h, _ptr(key), _ptr(start), _ptr(words), m, C.byref(got), C.byref(wm)),
-                self._h, "gwo_snapshot")
+        N.check(self._lib.gwo_snapshot(self._h, C.byref(rows), n.value, C.byref(got), C.byref(wm)), self._h,
+                "gwo_snapshot")
         g = got.value
-        return {"key": key[:g], "window_start": start[:g], "words": words[:g], "watermark": wm.value}
+        out = {c: v[:g] for c, v in cols.items()}
+        out["watermark"] = wm.value
+        return out
 
     def restore_state(self, snap):
-        """initializeState from one or more snapshots (a list restores a rescaled job: rows outside this
-        subtask's KeyGroupRange are skipped)."""
+        """initializeState from one or more snapshots.  A list restores a rescaled job: every subtask's rows are
+        offered and only this subtask's KeyGroupRange is kept.  The restored watermark is the minimum of the
+        snapshots'; each row's timer says whether its window was already emitted.  Sliding windows checkpoint
+        panes, whose emitted windows follow from the watermark alone, so snapshots whose watermarks straddle a
+        window end are rejected rather than restored ambiguously."""
         snaps = snap if isinstance(snap, (list, tuple)) else [snap]
-        key = np.ascontiguousarray(np.concatenate([x["key"] for x in snaps]), dtype=np.int64)
-        start = np.ascontiguousarray(np.concatenate([x["window_start"] for x in snaps]), dtype=np.int64)
+        wms = [x["watermark"] for x in snaps]
+        wm = min(wms)
+        if self.cfg.assigner == N.ASSIGNER_SLIDING and max(wms) != wm:
+            size, slide, off = self.cfg.size, self.cfg.slide, self.cfg.offset
+            # the first window end e (e = off + k * slide + size) still pending at the minimum watermark: e - 1 > wm
+            first_end = (wm + 2) + ((off + size - (wm + 2)) % slide)
+            if first_end - 1 <= max(wms):
+                raise N.GwoError(N.GWO_ERR_UNSUPPORTED, "sliding-window snapshots taken at watermarks that straddle a "
+                                 "window end cannot be restored together")
+        cat = lambda c, dt: np.ascontiguousarray(np.concatenate([x[c] for x in snaps]), dtype=dt)
+        key, start, end = cat("key", np.int64), cat("window_start", np.int64), cat("window_end", np.int64)
+        timer = cat("timer", np.int32)
         words = np.ascontiguousarray(np.concatenate([x["words"] for x in snaps]), dtype=np.int64)
-        wm = min(x["watermark"] for x in snaps)
+        nw = words.shape[1] if words.ndim == 2 else 0
         n = len(key)
         if n == 0:
-            key, start, words = np.zeros(1, np.int64), np.zeros(1, np.int64), np.zeros((1, 1), np.int64)
-        N.check(self._lib.gwo_restore(self._h, _ptr(key), _ptr(start), _ptr(words), n, wm), self._h, "gwo_restore")
+            key = start = end = np.zeros(1, np.int64)
+            timer = np.zeros(1, np.int32)
+            words = np.zeros((1, max(nw, 1)), np.int64)
+        rows = N.GwoStateRows(_ptr(key).value, _ptr(start).value, _ptr(end).value, _ptr(words).value, None,
+                              _ptr(timer).value)
+        N.check(self._lib.gwo_restore(self._h, C.byref(rows), nw, n, wm), self._h, "gwo_restore")
 
     def state_size(self) -> int:
         n = C.c_int64()

@@ -52,7 +52,7 @@
 extern "C" {
 #endif
 
-#define GWO_ABI_VERSION 2
+#define GWO_ABI_VERSION 3
 #define GWO_MAX_AGGS 4
 
 typedef enum {
@@ -167,21 +167,32 @@ gwo_status gwo_current_watermark(gwo_handle *h, int64_t *wm);
 /* Number of (key, window) entries currently held (device-resident state). */
 gwo_status gwo_state_size(gwo_handle *h, int64_t *entries);
 
-/* Checkpoint / restore of the keyed window state (tumbling and sliding windows, table layout; sliding
- * rows carry pane starts -- the heap
- * backend's (key, TimeWindow, accumulator) entries, CopyOnWriteStateMapSnapshot.java:127-129, and the
- * watermark that the restored timers imply).  gwo_snapshot_rows gives the row count and the accumulator
- * words per row; gwo_snapshot writes key, window start and the raw words (row-major, n_words per row)
- * into caller buffers (host or device) and the current watermark.  gwo_restore on a fresh handle of the
- * same configuration re-creates the entries whose key group lies in ITS KeyGroupRange (rows of other
- * key groups are skipped, so the union of old snapshots restores a rescaled job) and adopts the
- * watermark; windows whose end it already passed count as fired (emitted before the checkpoint).
- * Sessions and the log layout: GWO_ERR_UNSUPPORTED. */
+/* Checkpoint / restore of the keyed window state, every assigner and state layout.  A row is the heap backend's
+ * (namespace, key, state) entry (CopyOnWriteStateMapSnapshot.java:127-129) plus that entry's window timer
+ * (InternalTimeServiceManager.java:160-198): key, TimeWindow{window_start, window_end}, the raw accumulator words
+ * (n_words per row, row-major) and timer = 1 while the window's event-time fire timer is pending (0: already
+ * emitted, kept for allowedLateness re-fires).  Sliding windows checkpoint their panes ([start, end) = the pane);
+ * session windows one row per in-flight session.  gwo_snapshot writes rows grouped by key group in ascending
+ * order (key_group[i] = KeyGroupRangeAssignment.assignToKeyGroup of key[i]; the per-key-group layout of
+ * HeapSnapshotStrategy.java:97-222) and the current watermark; key_group and timer may be NULL.
+ * gwo_snapshot_rows gives an upper bound of the rows (exact except for the log layout, whose records are folded
+ * only by the snapshot) and the words per row.  gwo_restore on a fresh handle of the same configuration
+ * (n_words must match: GWO_ERR_INVALID_ARGUMENT) re-creates the rows whose key group lies in ITS KeyGroupRange
+ * (rows of other key groups are skipped, so the union of the old subtasks' checkpoints restores a rescaled job)
+ * and adopts `watermark`; with timer == NULL a window counts as emitted iff the watermark passed its end.  A
+ * tumbling window whose rows disagree on their timer (subtasks checkpointed at different watermarks, lateness >
+ * 0) is GWO_ERR_UNSUPPORTED.  Nothing changes on a failed validation.  Buffers may be host or device memory. */
+typedef struct {
+    int64_t *key;
+    int64_t *window_start;
+    int64_t *window_end;
+    int64_t *words;
+    int32_t *key_group;
+    int32_t *timer;
+} gwo_state_rows;
 gwo_status gwo_snapshot_rows(gwo_handle *h, int64_t *n_rows, int32_t *n_words);
-gwo_status gwo_snapshot(gwo_handle *h, int64_t *key, int64_t *window_start, int64_t *words, int64_t cap,
-                        int64_t *n_out, int64_t *watermark);
-gwo_status gwo_restore(gwo_handle *h, const int64_t *key, const int64_t *window_start, const int64_t *words,
-                       int64_t n, int64_t watermark);
+gwo_status gwo_snapshot(gwo_handle *h, const gwo_state_rows *rows, int64_t cap, int64_t *n_out, int64_t *watermark);
+gwo_status gwo_restore(gwo_handle *h, const gwo_state_rows *rows, int32_t n_words, int64_t n, int64_t watermark);
 
 gwo_status gwo_sync(gwo_handle *h);
 gwo_status gwo_get_stream(gwo_handle *h, void **stream);
