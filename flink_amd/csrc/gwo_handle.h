@@ -239,6 +239,7 @@ struct Handle {
     gwo_status sess_alloc(uint64_t cap, Table &t);
     gwo_status sess_read_err();
     gwo_status sess_ensure(uint64_t incoming);
+    gwo_status sess_ensure_pool(uint64_t n);
     gwo_status read_occupancy_one(Table &t);
     gwo_status session_init();
     void session_free();

@@ -128,13 +128,19 @@ struct SnapCols {
 };
 
 // Sessions (gwo_session.hip)
+// A key entry holds up to smax in-flight sessions inline: word 1 = their count.  A key that needs more
+// spills its session list into the pool (word 1 = -1, word 2 = first pool record, word 3 = capacity in
+// sessions, word 4 = count); pool arrays double when full and are bump-allocated from *pool_top.
 struct SessGeom {
     int64_t gap;
     int64_t lateness;
     int64_t wm;
-    int32_t smax;                      // in-flight sessions per key (entry capacity)
+    int32_t smax;                      // in-flight sessions per key held inline in its entry
     int32_t key_kind, max_par, kg_lo, kg_hi;
     int32_t side_enabled;
+    int64_t *pool;                     // spilled session lists: (3 + nwords)-word session records
+    unsigned long long *pool_top;      // next free pool record (device bump counter)
+    uint64_t pool_cap;                 // pool capacity in session records
 };
 
 struct SessErr {
@@ -143,6 +149,7 @@ struct SessErr {
     unsigned long long late;
     unsigned long long emitted;
     unsigned long long live_delta;     // sessions created - removed (two's complement)
+    unsigned long long pool_full;      // a spill found no pool room (the host sizes the pool so it cannot)
 };
 
 // ---- host-side launchers (gwo_kernels.hip) -----------------------------------------------------

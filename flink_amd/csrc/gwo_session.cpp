@@ -1,6 +1,7 @@
 // gwo_session.cpp -- host side of EventTimeSessionWindows (kernels: gwo_session.hip, gwo_sort.hip).
 #include <algorithm>
 #include <cstdlib>
+#include <unordered_map>
 
 #include "gwo_handle.h"
 
@@ -15,6 +16,8 @@ void launch_sess_process(const int64_t *key, const int64_t *ts, const int64_t *v
 void launch_sess_fire(const TableDesc &t, uint64_t cap, int stride, const AccPlan &p, const ResultPlan &rp,
                       const SessGeom &g, OutCols o, SessErr *err, hipStream_t s);
 void launch_sess_compact(const TableDesc &src, uint64_t cap, const TableDesc &dst, int stride, hipStream_t s);
+void launch_sess_pool_compact(const TableDesc &t, uint64_t cap, int stride, int sw, const int64_t *old_pool,
+                              const SessGeom &g, hipStream_t s);
 
 struct SessionState {
     int smax = 8;
@@ -24,6 +27,11 @@ struct SessionState {
     SessErr *d_err = nullptr;
     SessErr *h_err = nullptr;       // pinned
     DevBuf rec_slot, k1, v1, k2, v2, hist;
+    // spill pool of keys with more in-flight sessions than an entry holds (gwo_internal.h SessGeom)
+    int64_t *pool = nullptr;
+    uint64_t pool_cap = 0;          // session records
+    unsigned long long *d_pool_top = nullptr;
+    uint64_t pool_top = 0;          // as of the last read-back
 };
 
 gwo_status Handle::sess_alloc(uint64_t cap, Table &t) {
@@ -50,7 +58,9 @@ gwo_status Handle::session_init() {
     if (const char *e = getenv("GWO_SESSION_SLOTS")) S.smax = std::max(1, std::min(16, atoi(e)));
     S.stride = (2 + S.smax * (3 + plan.nwords) + 1) & ~1;
     GWO_TRY(dalloc((void **)&S.d_err, sizeof(SessErr)));
-    GWO_TRY(hipcheck(hipHostMalloc((void **)&S.h_err, sizeof(SessErr), hipHostMallocDefault), "pinned"));
+    GWO_TRY(hipcheck(hipHostMalloc((void **)&S.h_err, sizeof(SessErr) + 8, hipHostMallocDefault), "pinned"));
+    GWO_TRY(dalloc((void **)&S.d_pool_top, 8));
+    GWO_TRY(hipcheck(hipMemsetAsync(S.d_pool_top, 0, 8, stream), "pool top"));
     uint64_t cap = kMinCap;
     if (cfg.expected_keys > 0)
         while ((double)cfg.expected_keys > kInitLoad * (double)cap) cap <<= 1;
@@ -63,6 +73,8 @@ void Handle::session_free() {
     if (S.T.base) (void)hipFree(S.T.base);
     if (S.d_err) (void)hipFree(S.d_err);
     if (S.h_err) (void)hipHostFree(S.h_err);
+    if (S.pool) (void)hipFree(S.pool);
+    if (S.d_pool_top) (void)hipFree(S.d_pool_top);
     S.rec_slot.release();
     S.k1.release();
     S.v1.release();
@@ -75,6 +87,9 @@ void Handle::session_free() {
 
 static SessGeom sess_geom(const Handle &h, int smax) {
     SessGeom g{};
+    g.pool = h.sess->pool;
+    g.pool_top = h.sess->d_pool_top;
+    g.pool_cap = h.sess->pool_cap;
     g.gap = h.cfg.gap;
     g.lateness = h.cfg.allowed_lateness;
     g.wm = h.wm;
@@ -90,7 +105,38 @@ static SessGeom sess_geom(const Handle &h, int smax) {
 gwo_status Handle::sess_read_err() {
     SessionState &S = *sess;
     GWO_TRY(hipcheck(hipMemcpyAsync(S.h_err, S.d_err, sizeof(SessErr), hipMemcpyDeviceToHost, stream), "err"));
-    return hipcheck(hipStreamSynchronize(stream), "err sync");
+    GWO_TRY(hipcheck(hipMemcpyAsync((char *)S.h_err + sizeof(SessErr), S.d_pool_top, 8, hipMemcpyDeviceToHost, stream),
+                     "pool top"));
+    GWO_TRY(hipcheck(hipStreamSynchronize(stream), "err sync"));
+    S.pool_top = *(const unsigned long long *)((const char *)S.h_err + sizeof(SessErr));
+    return GWO_OK;
+}
+
+// A batch of n records can grow the spilled session lists by at most 4 x (live + n) session records (each key's
+// arrays double, so one batch's allocations for a key stay within 4x its final count): the pool keeps that
+// much room, compacting the spilled lists into a fresh pool (2 x their count each) when it runs short.
+gwo_status Handle::sess_ensure_pool(uint64_t n) {
+    SessionState &S = *sess;
+    const uint64_t need = 4 * (S.live + n);
+    if (S.pool_cap - S.pool_top >= need) return GWO_OK;
+    const uint64_t ncap = std::max<uint64_t>(6 * (S.live + n), 1 << 16);
+    const int sw = 3 + plan.nwords;
+    int64_t *np = nullptr;
+    GWO_TRY(dalloc((void **)&np, ncap * sw * 8));
+    int64_t *old = S.pool;
+    S.pool = np;
+    S.pool_cap = ncap;
+    GWO_TRY(hipcheck(hipMemsetAsync(S.d_pool_top, 0, 8, stream), "pool top"));
+    if (old) {
+        launch_sess_pool_compact(desc(S.T), S.T.cap, S.stride, sw, old, sess_geom(*this, S.smax), stream);
+        GWO_TRY(launch_ok("session pool compaction"));
+    }
+    GWO_TRY(hipcheck(hipMemcpyAsync((char *)S.h_err + sizeof(SessErr), S.d_pool_top, 8, hipMemcpyDeviceToHost, stream),
+                     "pool top"));
+    GWO_TRY(hipcheck(hipStreamSynchronize(stream), "pool compaction"));
+    S.pool_top = *(const unsigned long long *)((const char *)S.h_err + sizeof(SessErr));
+    if (old) (void)hipFree(old);
+    return GWO_OK;
 }
 
 // Grow the per-key table (dropping keys without sessions) so `incoming` new keys fit.
@@ -121,6 +167,7 @@ gwo_status Handle::insert_session(const int64_t *k, const int64_t *t, const int6
     SessionState &S = *sess;
     if (n > 0xffffffffll) return fail(GWO_ERR_INVALID_ARGUMENT, "session batches are limited to 2^32 records");
     GWO_TRY(sess_ensure((uint64_t)n));
+    GWO_TRY(sess_ensure_pool((uint64_t)n));
     if (cfg.allowed_lateness > 0) GWO_TRY(ensure_output((uint64_t)n));   // re-fires: at most one row per record
     GWO_TRY(ensure_buf(S.rec_slot, n * 4));
     GWO_TRY(ensure_buf(S.k1, n * 4));
@@ -161,9 +208,7 @@ gwo_status Handle::insert_session(const int64_t *k, const int64_t *t, const int6
     if (e.merge_late)
         return poison(GWO_ERR_MERGE_LATE, "The end timestamp of an event-time window cannot become earlier than the "
                                           "current watermark by merging.");
-    if (e.capacity)
-        return poison(GWO_ERR_CAPACITY, ("a key exceeded " + std::to_string(S.smax) +
-                                         " in-flight sessions (raise GWO_SESSION_SLOTS, max 16)").c_str());
+    if (e.pool_full) return poison(GWO_ERR_HIP, "session spill pool exhausted despite its reservation");
     S.live += e.live_delta;
     out_rows += e.emitted;
     if (side_enabled()) {
@@ -201,14 +246,16 @@ gwo_status Handle::session_state_size(int64_t *entries) {
 }
 
 // ---- checkpoint / restore (gwo_snapshot.cpp orchestrates; kernels in gwo_snapshot.hip) ----------------------
-void launch_snap_session(const TableDesc &t, uint64_t cap, int stride, const AccPlan &p, const SnapCols &c,
-                         hipStream_t s);
+void launch_snap_session(const TableDesc &t, uint64_t cap, int stride, const AccPlan &p, const int64_t *pool,
+                         const SnapCols &c, hipStream_t s);
+void launch_sess_restore_wide(const int64_t *key, const int64_t *off, const int64_t *lcap, const int64_t *count,
+                              int64_t m, const TableDesc &t, int stride, hipStream_t s);
 void launch_sess_restore(const int64_t *key, const int64_t *start, const int64_t *end, const int32_t *timer,
                          const int64_t *words, int64_t n, const TableDesc &t, uint64_t cap, int stride,
                          const AccPlan &p, const SessGeom &g, SessErr *err, hipStream_t s);
 
 gwo_status Handle::session_snapshot_collect(const SnapCols &c) {
-    launch_snap_session(desc(sess->T), sess->T.cap, sess->stride, plan, c, stream);
+    launch_snap_session(desc(sess->T), sess->T.cap, sess->stride, plan, sess->pool, c, stream);
     return launch_ok("session snapshot");
 }
 
@@ -218,43 +265,96 @@ uint64_t Handle::session_live() const { return sess->live; }
 // (a pending timer at maxTimestamp, EventTimeTrigger.java:37-45; without flags: pending iff maxTs > watermark).
 gwo_status Handle::session_restore_rows(const RestoreRows &R, int64_t new_wm) {
     SessionState &S = *sess;
+    std::unordered_map<int64_t, int64_t> per_key;
     uint64_t mine = 0;
     for (int64_t i = 0; i < R.n; ++i) {
         if (!R.mine[i]) continue;
         if (R.end[i] <= R.start[i]) return fail(GWO_ERR_INVALID_ARGUMENT, "restore: empty session window");
+        per_key[R.key[i]]++;
         mine++;
     }
     wm = new_wm;
     if (mine == 0) return GWO_OK;
-    GWO_TRY(sess_ensure(mine));
-    DevBuf k, st, en, tm, w;
-    GWO_TRY(ensure_buf(k, (size_t)R.n * 8));
-    GWO_TRY(ensure_buf(st, (size_t)R.n * 8));
-    GWO_TRY(ensure_buf(en, (size_t)R.n * 8));
-    GWO_TRY(ensure_buf(w, (size_t)R.n * R.nw * 8));
-    GWO_TRY(hipcheck(hipMemcpyAsync(k.ptr, R.key.data(), (size_t)R.n * 8, hipMemcpyHostToDevice, stream), "restore"));
-    GWO_TRY(hipcheck(hipMemcpyAsync(st.ptr, R.start.data(), (size_t)R.n * 8, hipMemcpyHostToDevice, stream), "restore"));
-    GWO_TRY(hipcheck(hipMemcpyAsync(en.ptr, R.end.data(), (size_t)R.n * 8, hipMemcpyHostToDevice, stream), "restore"));
-    GWO_TRY(hipcheck(hipMemcpyAsync(w.ptr, R.words.data(), (size_t)R.n * R.nw * 8, hipMemcpyHostToDevice, stream),
-                     "restore"));
-    if (!R.timer.empty()) {
-        GWO_TRY(ensure_buf(tm, (size_t)R.n * 4));
-        GWO_TRY(hipcheck(hipMemcpyAsync(tm.ptr, R.timer.data(), (size_t)R.n * 4, hipMemcpyHostToDevice, stream), "restore"));
+    GWO_TRY(sess_ensure(per_key.size()));
+    const int sw = 3 + plan.nwords;
+    // keys with more sessions than an entry holds: lists built here, uploaded into the spill pool
+    std::unordered_map<int64_t, int64_t> wide_at;   // key -> index in the wide lists
+    std::vector<int64_t> wk, woff, wcap, wcnt;
+    uint64_t wide_records = 0;
+    for (auto &kv : per_key)
+        if (kv.second > S.smax) {
+            wide_at[kv.first] = (int64_t)wk.size();
+            wk.push_back(kv.first);
+            woff.push_back((int64_t)wide_records);
+            wcap.push_back(2 * kv.second);
+            wcnt.push_back(0);
+            wide_records += 2 * kv.second;
+        }
+    std::vector<int64_t> pool_img(wide_records * sw, 0);
+    std::vector<int64_t> nk, nst, nen, nw;
+    std::vector<int32_t> ntm;
+    for (int64_t i = 0; i < R.n; ++i) {
+        if (!R.mine[i]) continue;
+        const bool timer = R.timer.empty() ? (int64_t)((uint64_t)R.end[i] - 1) > new_wm : R.timer[i] != 0;
+        auto it = wide_at.find(R.key[i]);
+        if (it == wide_at.end()) {
+            nk.push_back(R.key[i]);
+            nst.push_back(R.start[i]);
+            nen.push_back(R.end[i]);
+            ntm.push_back(timer ? 1 : 0);
+            for (int w = 0; w < R.nw; ++w) nw.push_back(R.words[(size_t)i * R.nw + w]);
+            continue;
+        }
+        const int64_t j = it->second;
+        int64_t *X = pool_img.data() + (size_t)(woff[j] + wcnt[j]++) * sw;
+        X[0] = R.start[i];
+        X[1] = R.end[i];
+        X[2] = timer ? 1 : 0;
+        for (int w = 0; w < R.nw; ++w) X[3 + w] = R.words[(size_t)i * R.nw + w];
     }
+    GWO_TRY(sess_ensure_pool(mine + wide_records));   // a fresh handle: the pool starts empty
+    if (!wk.empty()) {
+        if (S.pool_top + wide_records > S.pool_cap) return poison(GWO_ERR_HIP, "restore: spill pool too small");
+        for (auto &o : woff) o += (int64_t)S.pool_top;
+        GWO_TRY(hipcheck(hipMemcpy(S.pool + S.pool_top * sw, pool_img.data(), pool_img.size() * 8, hipMemcpyHostToDevice),
+                         "restore pool"));
+        const unsigned long long top = S.pool_top + wide_records;
+        GWO_TRY(hipcheck(hipMemcpy(S.d_pool_top, &top, 8, hipMemcpyHostToDevice), "restore pool top"));
+        S.pool_top = top;
+        DevBuf a, b, c, d;
+        for (DevBuf *x : {&a, &b, &c, &d}) GWO_TRY(ensure_buf(*x, wk.size() * 8));
+        GWO_TRY(hipcheck(hipMemcpy(a.ptr, wk.data(), wk.size() * 8, hipMemcpyHostToDevice), "restore"));
+        GWO_TRY(hipcheck(hipMemcpy(b.ptr, woff.data(), wk.size() * 8, hipMemcpyHostToDevice), "restore"));
+        GWO_TRY(hipcheck(hipMemcpy(c.ptr, wcap.data(), wk.size() * 8, hipMemcpyHostToDevice), "restore"));
+        GWO_TRY(hipcheck(hipMemcpy(d.ptr, wcnt.data(), wk.size() * 8, hipMemcpyHostToDevice), "restore"));
+        launch_sess_restore_wide((const int64_t *)a.ptr, (const int64_t *)b.ptr, (const int64_t *)c.ptr,
+                                 (const int64_t *)d.ptr, (int64_t)wk.size(), desc(S.T), S.stride, stream);
+        GWO_TRY(launch_ok("session restore"));
+        GWO_TRY(hipcheck(hipStreamSynchronize(stream), "session restore"));
+        for (DevBuf *x : {&a, &b, &c, &d}) x->release();
+        S.live += mine - nk.size();
+    }
+    const int64_t m = (int64_t)nk.size();
+    if (m == 0) return GWO_OK;
+    DevBuf k, st, en, tm, w;
+    GWO_TRY(ensure_buf(k, (size_t)m * 8));
+    GWO_TRY(ensure_buf(st, (size_t)m * 8));
+    GWO_TRY(ensure_buf(en, (size_t)m * 8));
+    GWO_TRY(ensure_buf(tm, (size_t)m * 4));
+    GWO_TRY(ensure_buf(w, (size_t)m * R.nw * 8));
+    GWO_TRY(hipcheck(hipMemcpyAsync(k.ptr, nk.data(), (size_t)m * 8, hipMemcpyHostToDevice, stream), "restore"));
+    GWO_TRY(hipcheck(hipMemcpyAsync(st.ptr, nst.data(), (size_t)m * 8, hipMemcpyHostToDevice, stream), "restore"));
+    GWO_TRY(hipcheck(hipMemcpyAsync(en.ptr, nen.data(), (size_t)m * 8, hipMemcpyHostToDevice, stream), "restore"));
+    GWO_TRY(hipcheck(hipMemcpyAsync(tm.ptr, ntm.data(), (size_t)m * 4, hipMemcpyHostToDevice, stream), "restore"));
+    GWO_TRY(hipcheck(hipMemcpyAsync(w.ptr, nw.data(), (size_t)m * R.nw * 8, hipMemcpyHostToDevice, stream), "restore"));
     GWO_TRY(hipcheck(hipMemsetAsync(S.d_err, 0, sizeof(SessErr), stream), "err"));
     launch_sess_restore((const int64_t *)k.ptr, (const int64_t *)st.ptr, (const int64_t *)en.ptr,
-                        R.timer.empty() ? nullptr : (const int32_t *)tm.ptr, (const int64_t *)w.ptr, R.n, desc(S.T),
-                        S.T.cap, S.stride, plan, sess_geom(*this, S.smax), S.d_err, stream);
+                        (const int32_t *)tm.ptr, (const int64_t *)w.ptr, m, desc(S.T), S.T.cap, S.stride, plan,
+                        sess_geom(*this, S.smax), S.d_err, stream);
     GWO_TRY(launch_ok("session restore"));
     GWO_TRY(sess_read_err());
-    k.release();
-    st.release();
-    en.release();
-    tm.release();
-    w.release();
-    if (S.h_err->capacity)
-        return poison(GWO_ERR_CAPACITY, ("restore: a key has more than " + std::to_string(S.smax) +
-                                         " in-flight sessions").c_str());
+    for (DevBuf *x : {&k, &st, &en, &tm, &w}) x->release();
+    if (S.h_err->capacity) return poison(GWO_ERR_HIP, "restore: an entry overflowed its inline sessions");
     S.live += S.h_err->live_delta;
     return GWO_OK;
 }

@@ -7,9 +7,11 @@
 //
 // State: one HBM hash-table entry per key holding that key's in-flight sessions inline:
 //   word 0 key | word 1 number of sessions | smax x [start, end, flags, acc words...]
-// (flags bit 0 = an event-time timer at maxTimestamp is pending).  In-flight sessions of a key are
-// pairwise non-intersecting (every addWindow merges all intersecting windows), so merging a new
-// window touches a contiguous run of them.
+// (flags bit 0 = an event-time timer at maxTimestamp is pending).  A key with more in-flight sessions
+// than its entry holds spills them into a pool array (word 1 = -1, words 2..4 = pool record, capacity,
+// count; SessGeom): MergingWindowSet (MergingWindowSet.java:156-225) bounds nothing per key, nor does
+// this.  In-flight sessions of a key are pairwise non-intersecting (every addWindow merges all
+// intersecting windows).
 //
 // A batch is processed key-parallel but arrival-ordered within a key: records are grouped by
 // their key's table slot with a stable radix sort (gwo_sort.hip) and one lane walks each key's
@@ -70,6 +72,19 @@ __device__ __forceinline__ void emit_row(const OutCols &o, const AccPlan &p, con
 #define SESS_MAXS 16
 #define SESS_MAXW (3 + GWO_MAX_WORDS)
 
+// Moves a key's session list into a fresh pool array of at least `want` sessions (doubling); returns the
+// array or nullptr when the pool is exhausted (the host sizes the pool so that cannot happen).
+__device__ __forceinline__ int64_t *sess_grow(const SessGeom &g, const int64_t *S, int ns, int sw, int want,
+                                              int64_t &off, int &scap) {
+    const unsigned long long o = atomicAdd(g.pool_top, (unsigned long long)want);
+    if (o + (unsigned long long)want > g.pool_cap) return nullptr;
+    int64_t *dst = g.pool + o * (unsigned long long)sw;
+    for (int i = 0; i < ns * sw; ++i) dst[i] = S[i];
+    off = (int64_t)o;
+    scap = want;
+    return dst;
+}
+
 // pass 2: one lane per key, records in arrival order
 __global__ __launch_bounds__(64) void sess_process_kernel(const int64_t *__restrict__ key, const int64_t *__restrict__ ts,
                                                           const int64_t *__restrict__ val, int64_t n,
@@ -85,10 +100,21 @@ __global__ __launch_bounds__(64) void sess_process_kernel(const int64_t *__restr
         uint32_t slot = sorted_slot[q];
         if (q > 0 && sorted_slot[q - 1] == slot) continue;  // not the head of this key's run
         int64_t *e = entry_ptr(t, slot, stride, cap);
-        int ns = (int)e[1];
-        int64_t S[SESS_MAXS][SESS_MAXW];  // start, end, flags, acc...
-        for (int s = 0; s < ns; ++s)
-            for (int w = 0; w < sw; ++w) S[s][w] = e[2 + s * sw + w];
+        // the key's session list: the inline sessions copied into L (written back at the end), or its pool array
+        int64_t L[SESS_MAXS * SESS_MAXW];
+        int64_t *S = L;
+        int ns, scap = g.smax;
+        int64_t off = 0;
+        bool spilled = e[1] < 0;
+        if (spilled) {
+            off = e[2];
+            scap = (int)e[3];
+            ns = (int)e[4];
+            S = g.pool + (uint64_t)off * sw;
+        } else {
+            ns = (int)e[1];
+            for (int i = 0; i < ns * sw; ++i) L[i] = e[2 + i];
+        }
         long long created = 0;
         bool dirty = false;
         for (int64_t r = q; r < n && sorted_slot[r] == slot; ++r) {
@@ -101,28 +127,35 @@ __global__ __launch_bounds__(64) void sess_process_kernel(const int64_t *__restr
             int64_t ms = ws, me = we;
             int nm = 0, first = -1;
             for (int s = 0; s < ns; ++s) {
-                if (S[s][0] <= we && S[s][1] >= ws) {
+                const int64_t *X = S + s * sw;
+                if (X[0] <= we && X[1] >= ws) {
                     if (first < 0) first = s;
                     nm++;
-                    ms = S[s][0] < ms ? S[s][0] : ms;
-                    me = S[s][1] > me ? S[s][1] : me;
+                    ms = X[0] < ms ? X[0] : ms;
+                    me = X[1] > me ? X[1] : me;
                 }
             }
             int actual;
             bool fresh = false;
             if (nm == 0) {
-                if (ns >= g.smax) {
-                    atomicAdd(&err->capacity, 1ull);
-                    continue;
+                if (ns >= scap) {   // the list is full: spill (or grow) into a pool array twice its size
+                    int64_t *nS = sess_grow(g, S, ns, sw, 2 * scap, off, scap);
+                    if (!nS) {
+                        atomicAdd(&err->pool_full, 1ull);
+                        continue;
+                    }
+                    S = nS;
+                    spilled = true;
                 }
                 actual = ns++;
-                S[actual][0] = ws;
-                S[actual][1] = we;
-                S[actual][2] = 0;
-                for (int w = 0; w < p.nwords; ++w) S[actual][3 + w] = p.ident[w];
+                int64_t *X = S + actual * sw;
+                X[0] = ws;
+                X[1] = we;
+                X[2] = 0;
+                for (int w = 0; w < p.nwords; ++w) X[3 + w] = p.ident[w];
                 fresh = true;
                 created++;
-            } else if (nm == 1 && S[first][0] == ms && S[first][1] == me) {
+            } else if (nm == 1 && S[first * sw] == ms && S[first * sw + 1] == me) {
                 actual = first;  // new window inside an existing session: no merge callback
             } else {
                 int64_t rmax = jsub(me, 1);
@@ -135,25 +168,28 @@ __global__ __launch_bounds__(64) void sess_process_kernel(const int64_t *__restr
                 for (int w = 0; w < p.nwords; ++w) acc[w] = p.ident[w];
                 int keep = 0;
                 for (int s = 0; s < ns; ++s) {
-                    bool m = S[s][0] <= we && S[s][1] >= ws;
+                    const int64_t *X = S + s * sw;
+                    bool m = X[0] <= we && X[1] >= ws;
                     if (m) {
-                        for (int w = 0; w < p.nwords; ++w) acc[w] = combine(p.op[w], acc[w], S[s][3 + w]);
+                        for (int w = 0; w < p.nwords; ++w) acc[w] = combine(p.op[w], acc[w], X[3 + w]);
                     } else {
                         if (keep != s)
-                            for (int w = 0; w < sw; ++w) S[keep][w] = S[s][w];
+                            for (int w = 0; w < sw; ++w) S[keep * sw + w] = X[w];
                         keep++;
                     }
                 }
                 created -= nm - 1;
                 ns = keep + 1;
                 actual = keep;
-                S[actual][0] = ms;
-                S[actual][1] = me;
-                S[actual][2] = rmax > g.wm ? 1 : 0;  // EventTimeTrigger.onMerge: timer iff maxTs > watermark
-                for (int w = 0; w < p.nwords; ++w) S[actual][3 + w] = acc[w];
+                int64_t *X = S + actual * sw;
+                X[0] = ms;
+                X[1] = me;
+                X[2] = rmax > g.wm ? 1 : 0;  // EventTimeTrigger.onMerge: timer iff maxTs > watermark
+                for (int w = 0; w < p.nwords; ++w) X[3 + w] = acc[w];
             }
             dirty = true;
-            const int64_t amax = jsub(S[actual][1], 1);
+            int64_t *A = S + actual * sw;
+            const int64_t amax = jsub(A[1], 1);
             if (cleanup_time(amax, g.lateness) <= g.wm) {  // isWindowLate -> retireWindow
                 if (fresh) {
                     ns--;
@@ -172,18 +208,24 @@ __global__ __launch_bounds__(64) void sess_process_kernel(const int64_t *__restr
                 }
                 continue;
             }
-            for (int w = 0; w < p.nwords; ++w) S[actual][3 + w] = combine(p.op[w], S[actual][3 + w], lift_word(p, w, v));
+            for (int w = 0; w < p.nwords; ++w) A[3 + w] = combine(p.op[w], A[3 + w], lift_word(p, w, v));
             if (amax <= g.wm) {
-                emit_row(o, p, rp, k, S[actual][0], S[actual][1], &S[actual][3]);  // onElement FIRE
+                emit_row(o, p, rp, k, A[0], A[1], A + 3);  // onElement FIRE
                 atomicAdd(&err->emitted, 1ull);
             } else {
-                S[actual][2] = 1;                                                 // registerEventTimeTimer
+                A[2] = 1;                                  // registerEventTimeTimer
             }
         }
         if (dirty) {
-            e[1] = ns;
-            for (int s = 0; s < ns; ++s)
-                for (int w = 0; w < sw; ++w) e[2 + s * sw + w] = S[s][w];
+            if (spilled) {
+                e[1] = -1;
+                e[2] = off;
+                e[3] = scap;
+                e[4] = ns;
+            } else {
+                e[1] = ns;
+                for (int i = 0; i < ns * sw; ++i) e[2 + i] = L[i];
+            }
             if (created) atomicAdd(&err->live_delta, (unsigned long long)created);
         }
     }
@@ -206,12 +248,14 @@ __global__ __launch_bounds__(256) void sess_fire_kernel(TableDesc t, uint64_t ca
             if (e[0] == 0) continue;
             k = GWO_EMPTY_KEY;
         }
-        int ns = (int)e[1];
+        const bool spilled = e[1] < 0;
+        int ns = spilled ? (int)e[4] : (int)e[1];
         if (ns == 0) continue;
+        int64_t *base = spilled ? g.pool + (uint64_t)e[2] * sw : e + 2;
         int keep = 0;
         long long removed = 0;
         for (int s = 0; s < ns; ++s) {
-            int64_t *S = e + 2 + s * sw;
+            int64_t *S = base + s * sw;
             int64_t mx = jsub(S[1], 1);
             bool changed = false;
             if ((S[2] & 1) && mx <= g.wm) {
@@ -226,10 +270,14 @@ __global__ __launch_bounds__(256) void sess_fire_kernel(TableDesc t, uint64_t ca
                 continue;
             }
             if (keep != s)
-                for (int w = 0; w < sw; ++w) e[2 + keep * sw + w] = S[w];
+                for (int w = 0; w < sw; ++w) base[keep * sw + w] = S[w];
             keep++;
         }
-        if (keep != ns) e[1] = keep;
+        if (keep != ns) {
+            if (!spilled) e[1] = keep;
+            else if (keep == 0) e[1] = 0;   // every spilled session retired: the key is inline (and empty) again
+            else e[4] = keep;
+        }
         if (removed) atomicAdd(&err->live_delta, (unsigned long long)(-removed));
     }
 }
@@ -240,11 +288,30 @@ __global__ __launch_bounds__(256) void sess_compact_kernel(TableDesc src, uint64
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < cap; i += step) {
         int64_t *e = src.base + i * (uint64_t)stride;
         int64_t k = e[0];
-        if (k == GWO_EMPTY_KEY || e[1] == 0) continue;
+        if (k == GWO_EMPTY_KEY || e[1] == 0) continue;   // (e[1] < 0: spilled, kept with its pool reference)
         bool claimed;
         int64_t *a = find_or_insert(dst, stride, k, claimed) - 1;
         count_claims(dst.occ, claimed);
         for (int w = 1; w < stride; ++w) a[w] = e[w];
+    }
+}
+
+// pool compaction: every spilled list moves to a fresh pool (capacity 2 x its count, at least 2 x smax)
+__global__ __launch_bounds__(256) void sess_pool_compact_kernel(TableDesc t, uint64_t cap, int stride, int sw,
+                                                                const int64_t *__restrict__ old_pool, SessGeom g) {
+    const uint64_t step = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i <= cap; i += step) {
+        int64_t *e = i < cap ? t.base + i * (uint64_t)stride : t.side;
+        if (i < cap ? e[0] == GWO_EMPTY_KEY : e[0] == 0) continue;
+        if (e[1] >= 0) continue;
+        const int ns = (int)e[4];
+        const int want = 2 * ns > 2 * g.smax ? 2 * ns : 2 * g.smax;
+        const unsigned long long o = atomicAdd(g.pool_top, (unsigned long long)want);
+        const int64_t *src = old_pool + (uint64_t)e[2] * sw;
+        int64_t *dst = g.pool + o * (uint64_t)sw;
+        for (int k = 0; k < ns * sw; ++k) dst[k] = src[k];
+        e[2] = (int64_t)o;
+        e[3] = want;
     }
 }
 
@@ -272,6 +339,12 @@ void launch_sess_fire(const TableDesc &t, uint64_t cap, int stride, const AccPla
                       const SessGeom &g, OutCols o, SessErr *err, hipStream_t s) {
     hipLaunchKernelGGL(sess_fire_kernel, dim3(sgrid((int64_t)cap + 1, 256, 8192)), dim3(256), 0, s, t, cap, stride,
                        p, rp, g, o, err);
+}
+
+void launch_sess_pool_compact(const TableDesc &t, uint64_t cap, int stride, int sw, const int64_t *old_pool,
+                              const SessGeom &g, hipStream_t s) {
+    hipLaunchKernelGGL(sess_pool_compact_kernel, dim3(sgrid((int64_t)cap + 1, 256, 8192)), dim3(256), 0, s, t, cap,
+                       stride, sw, old_pool, g);
 }
 
 void launch_sess_compact(const TableDesc &src, uint64_t cap, const TableDesc &dst, int stride, hipStream_t s) {

@@ -35,7 +35,7 @@ __global__ __launch_bounds__(256) void snap_table_kernel(TableDesc t, uint64_t c
 // words...] per session): the reference's session state windows (MergingWindowSet.java:81-109 persists the
 // in-flight window -> state window mapping; here the merged window is its own namespace).
 __global__ __launch_bounds__(256) void snap_session_kernel(TableDesc t, uint64_t cap, int stride, AccPlan p,
-                                                           SnapCols c) {
+                                                           const int64_t *pool, SnapCols c) {
     const int sw = 3 + p.nwords;
     for (uint64_t b0 = (uint64_t)blockIdx.x * 256; b0 < cap + 1; b0 += (uint64_t)gridDim.x * 256) {
         const uint64_t i = b0 + threadIdx.x;
@@ -45,16 +45,20 @@ __global__ __launch_bounds__(256) void snap_session_kernel(TableDesc t, uint64_t
         if (i < cap) {
             e = t.base + i * (uint64_t)stride;
             k = e[0];
-            if (k != GWO_EMPTY_KEY) ns = (unsigned)e[1];
+            if (k == GWO_EMPTY_KEY) e = nullptr;
         } else if (i == cap && t.side[0] != 0) {
             e = t.side;
             k = GWO_EMPTY_KEY;
-            ns = (unsigned)e[1];
+        }
+        const int64_t *list = nullptr;
+        if (e) {   // inline sessions, or a spilled list in the pool
+            ns = e[1] < 0 ? (unsigned)e[4] : (unsigned)e[1];
+            list = e[1] < 0 ? pool + (uint64_t)e[2] * sw : e + 2;
         }
         unsigned long long pos = block_reserve(ns, c.count);
         for (unsigned s = 0; s < ns; ++s, ++pos) {
             if ((long long)pos >= c.cap) break;
-            const int64_t *S = e + 2 + (uint64_t)s * sw;
+            const int64_t *S = list + (uint64_t)s * sw;
             c.key[pos] = k;
             c.start[pos] = S[0];
             c.end[pos] = S[1];
@@ -119,6 +123,26 @@ __global__ __launch_bounds__(256) void sess_restore_kernel(const int64_t *key, c
     }
 }
 
+// Keys restored with more sessions than an entry holds: their lists were uploaded into the spill pool by the
+// host; each key's entry points at its list (word 1 = -1, pool record, capacity, count).
+__global__ __launch_bounds__(256) void sess_restore_wide_kernel(const int64_t *key, const int64_t *off,
+                                                                const int64_t *lcap, const int64_t *count, int64_t m,
+                                                                TableDesc t, int stride) {
+    const int64_t step = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t j0 = (int64_t)blockIdx.x * blockDim.x; j0 < m; j0 += step) {
+        const int64_t j = j0 + threadIdx.x;
+        bool claimed = false;
+        if (j < m) {
+            int64_t *e = find_or_insert(t, stride, key[j], claimed) - 1;
+            e[1] = -1;
+            e[2] = off[j];
+            e[3] = lcap[j];
+            e[4] = count[j];
+        }
+        count_claims(t.occ, claimed);
+    }
+}
+
 static inline int snap_grid(int64_t n) {
     int64_t g = (n + 255) / 256;
     return (int)(g < 1 ? 1 : (g > 4096 ? 4096 : g));
@@ -130,9 +154,16 @@ void launch_snap_table(const TableDesc &t, uint64_t cap, const AccPlan &p, int64
                        timer, c);
 }
 
-void launch_snap_session(const TableDesc &t, uint64_t cap, int stride, const AccPlan &p, const SnapCols &c,
-                         hipStream_t s) {
-    hipLaunchKernelGGL(snap_session_kernel, dim3(snap_grid((int64_t)cap + 1)), dim3(256), 0, s, t, cap, stride, p, c);
+void launch_snap_session(const TableDesc &t, uint64_t cap, int stride, const AccPlan &p, const int64_t *pool,
+                         const SnapCols &c, hipStream_t s) {
+    hipLaunchKernelGGL(snap_session_kernel, dim3(snap_grid((int64_t)cap + 1)), dim3(256), 0, s, t, cap, stride, p, pool,
+                       c);
+}
+
+void launch_sess_restore_wide(const int64_t *key, const int64_t *off, const int64_t *lcap, const int64_t *count,
+                              int64_t m, const TableDesc &t, int stride, hipStream_t s) {
+    hipLaunchKernelGGL(sess_restore_wide_kernel, dim3(snap_grid(m)), dim3(256), 0, s, key, off, lcap, count, m, t,
+                       stride);
 }
 
 void launch_snap_gather(const SnapCols &c, const uint32_t *perm, const uint32_t *kg_sorted, int64_t n, int nw,

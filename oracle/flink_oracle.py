@@ -286,6 +286,14 @@ class MergingWindowSet:
     def __init__(self, assigner, mapping: dict):
         self.assigner = assigner
         self.mapping = mapping          # the persisted dict is mutated in place (persist() is implicit)
+        self.initial = dict(mapping)    # MergingWindowSet.java:81-96: the mapping as restored
+
+    def persist(self):
+        """MergingWindowSet.java:102-109: rewrite the list state only if the mapping changed; returns the
+        (window, state window) entries added to the state (None: the state is left untouched)."""
+        if self.mapping == self.initial:
+            return None
+        return list(self.mapping.items())
 
     def get_state_window(self, w):
         return self.mapping.get(w)

@@ -155,3 +155,66 @@ def test_generator_definition():
     # first value pinned (guards the cross-language definition)
     z = (42 + 0 * 0xD1B54A32D192ED03 + 1 * 0x9E3779B97F4A7C15) % (1 << 64)
     assert int(k[0]) == O.splitmix64((z - 0x9E3779B97F4A7C15) % (1 << 64)) % 10
+
+
+class _NonEagerAssigner:
+    """The MergingWindowSetTest's misbehaving assigner (MergingWindowSetTest.java:470-536): the windows that start
+    inside the earliest-starting window merge into [its start, its end + 1)."""
+    merging = True
+
+    def __init__(self, timeout):
+        self.timeout = timeout
+
+    def merge_windows(self, windows, callback):
+        earliest = None
+        for w in windows:
+            if earliest is None or w.start < earliest.start:
+                earliest = w
+        assoc = [w for w in windows if earliest.start <= w.start < earliest.end]
+        if len(assoc) > 1:
+            callback(set(assoc), O.TimeWindow(earliest.start, earliest.end + 1))
+
+
+@pytest.mark.parametrize("case", range(9))
+def test_merging_window_set_known_answers(case):
+    """MergingWindowSetTest.java:71-437 (tests/golden/merging_window_set.json) against the oracle's
+    MergingWindowSet restatement -- the session bookkeeping the GPU's per-key session lists follow."""
+    import json
+    import os
+    with open(os.path.join(os.path.dirname(__file__), "golden", "merging_window_set.json")) as f:
+        c = json.load(f)["cases"][case]
+    W = lambda x: O.TimeWindow(*x)
+    assigner = _NonEagerAssigner(c["timeout"]) if c["assigner"] == "non_eager" else O.EventTimeSessionWindows(c["assigner"])
+    ws = O.MergingWindowSet(assigner, {W(a): W(b) for a, b in c.get("initial", [])})
+    for op in c["ops"]:
+        if op[0] == "add":
+            calls = []
+            res = ws.add_window(W(op[1]), lambda *a: calls.append(a))
+            if op[3] == "any":
+                assert ws.get_state_window(res) is not None
+                continue
+            assert res == W(op[2])
+            if op[3] is None:
+                assert calls == []
+                continue
+            assert len(calls) == 1                      # one merge per added window
+            target, sources, state_window, merged_state = calls[0]
+            m = op[3]
+            if "target" in m:
+                assert target == W(m["target"])
+                assert sorted(sources) == sorted(W(x) for x in m["sources"])
+                assert state_window in [W(x) for x in m["state_window"]]
+            if "merged_state_windows" in m:
+                assert sorted(merged_state) in [sorted(W(x) for x in alt) for alt in m["merged_state_windows"]]
+                assert target not in merged_state
+        elif op[0] == "state":
+            got = ws.get_state_window(W(op[1]))
+            assert got is None if op[2] is None else got in [W(x) for x in op[2]]
+        elif op[0] == "retire":
+            ws.retire_window(W(op[1]))
+        elif op[0] == "persist":
+            adds = ws.persist()
+            if op[1] is None:
+                assert adds is None
+            else:
+                assert sorted(adds) == sorted((W(a), W(b)) for a, b in op[1])
