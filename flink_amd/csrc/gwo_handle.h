@@ -235,6 +235,10 @@ struct Handle {
     void slide_free();
     gwo_status fire_sliding(int64_t new_wm);
     gwo_status slide_restore_anchor();
+    __int128 first_uncleaned_window(int64_t at_wm) const;
+    __int128 first_unfired_window(int64_t at_wm) const;
+    gwo_status slide_refire_rows(const int64_t *k, const int64_t *t, const int64_t *v, int64_t n, const WindowGeom &g,
+                                 uint64_t records);
     // sessions (gwo_session.cpp)
     gwo_status sess_alloc(uint64_t cap, Table &t);
     gwo_status sess_read_err();

@@ -177,7 +177,12 @@ void launch_refire_slots(const int64_t *key, const int64_t *r_idx, const long lo
                          int64_t *before, hipStream_t s);
 void launch_refire_emit(const int64_t *key, const int64_t *val, const int64_t *r_idx, const long long *r_u, int64_t m,
                         const uint32_t *skey, const uint32_t *spay, const int64_t *before, const AccPlan &p,
-                        const ResultPlan &rp, int64_t unit, int64_t unit_off_mod, OutCols o, hipStream_t s);
+                        const ResultPlan &rp, int64_t unit, int64_t unit_off_mod, int64_t span, OutCols o,
+                        hipStream_t s);
+void launch_slide_refire_slots(const int64_t *key, const int64_t *r_idx, const long long *r_u, int64_t m,
+                               const AccPlan &p, const WindowGeom &g, unsigned long long *keytab, uint64_t kmask,
+                               long long j0, uint32_t nj, const TableDesc *pdir, long long pane_base,
+                               long long pane_len, uint32_t *r_slot, int64_t *before, hipStream_t s);
 // gwo_sort.hip: stable LSD radix sort of (uint32 key, uint32 payload; vals NULL = index); returns 0 when the
 // result is in (k1, v1), 1 when in (k2, v2)
 int radix_sort_pairs(const uint32_t *keys, const uint32_t *vals, int64_t n, int key_bits, uint32_t *k1, uint32_t *v1,

@@ -41,25 +41,41 @@ __device__ __forceinline__ int classify(int64_t ts, const WindowGeom &g, long lo
         return jadd(ts, g.lateness) <= g.wm ? REC_LATE : REC_SKIP;
     }
     int64_t first_max_ts = jsub(jadd(first_start, g.size), 1);
-    if (first_max_ts <= g.wm) {
-        if (g.sliding && cleanup_time(first_max_ts, g.lateness) <= g.wm) {
-            // the earliest windows are already cleaned: with lateness 0 the pane only feeds the
-            // unfired windows, which is exactly the reference's per-window accept set
-            if (g.lateness != 0) return REC_REFIRE;
-        } else {
-            // EventTimeTrigger.onElement FIRE: window.maxTs <= watermark (tumbling: the unit is the window)
-            if (!g.sliding) unit_idx = fdiv_floor(last_start, g.size, g.inv_size);
-            return REC_REFIRE;
-        }
-    }
     if (!g.sliding) {
         unit_idx = fdiv_floor(last_start, g.size, g.inv_size);
-    } else {
-        int64_t pane_start =
-            jsub(ts, jsub(jsub(ts, g.unit_off), fdiv_floor(jsub(ts, g.unit_off), g.unit, g.inv_unit) * g.unit));
-        unit_idx = fdiv_floor(pane_start, g.unit, g.inv_unit);
+        // EventTimeTrigger.onElement FIRE: window.maxTs <= watermark (the unit is the window)
+        return first_max_ts <= g.wm ? REC_REFIRE : REC_ACCEPT;
     }
-    return REC_ACCEPT;
+    int64_t pane_start =
+        jsub(ts, jsub(jsub(ts, g.unit_off), fdiv_floor(jsub(ts, g.unit_off), g.unit, g.inv_unit) * g.unit));
+    unit_idx = fdiv_floor(pane_start, g.unit, g.inv_unit);
+    // The pane feeds every window of the record: cleaned ones never emit again, unfired ones fire later,
+    // and fired-but-not-cleaned ones (only with allowedLateness > 0) re-fire now, one row each.
+    if (first_max_ts > g.wm || g.lateness == 0) return REC_ACCEPT;
+    int64_t newest_fired = last_start;   // newest window of the record with maxTs <= watermark
+    if (last_max_ts > g.wm) {
+        const int64_t d = last_max_ts - g.wm;   // in (0, size): no overflow
+        newest_fired = jsub(last_start, (fdiv_floor(d - 1, g.slide, g.inv_slide) + 1) * g.slide);
+    }
+    return cleanup_time(jsub(jadd(newest_fired, g.size), 1), g.lateness) > g.wm ? REC_REFIRE : REC_ACCEPT;
+}
+
+// Sliding re-fire record: its fired-but-not-cleaned windows are j in [ja, jb] (window j starts at
+// j * slide + floorMod(offset, slide)); call only for records classify() calls REC_REFIRE.
+__device__ __forceinline__ void slide_refire_windows(int64_t ts, const WindowGeom &g, long long &ja, long long &jb) {
+    const int64_t last_start = window_start_f(ts, g.offset, g.slide, g.inv_slide);
+    const int64_t k = fdiv_floor(jsub(last_start, jsub(ts, g.size)) - 1, g.slide, g.inv_slide);
+    const int64_t first_start = jsub(last_start, k * g.slide);
+    const int64_t om = jsub(g.offset, fdiv_floor(g.offset, g.slide, g.inv_slide) * g.slide);
+    const long long j_first = fdiv_floor(jsub(first_start, om), g.slide, g.inv_slide);
+    const long long j_last = j_first + k;
+    // cleaned: maxTs + lateness <= wm (never saturated here: the record's last window is not cleaned)
+    const int64_t first_max_ts = jsub(jadd(first_start, g.size), 1);
+    const int64_t first_cleanup = cleanup_time(first_max_ts, g.lateness);
+    ja = first_cleanup > g.wm ? j_first : j_first + fdiv_floor(g.wm - first_cleanup, g.slide, g.inv_slide) + 1;
+    // fired: maxTs <= wm
+    const int64_t last_max_ts = jsub(jadd(last_start, g.size), 1);
+    jb = last_max_ts <= g.wm ? j_last : j_last - (fdiv_floor(last_max_ts - g.wm - 1, g.slide, g.inv_slide) + 1);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -553,14 +569,22 @@ static inline int grid_for(int64_t n, int per_thread = 1, int cap = 4096) {
 #define RF_BLOCKS 256
 #define RF_THREADS 256
 
-__device__ __forceinline__ bool refire_in_dir(const int64_t *ts, int64_t i, const WindowGeom &g, long long dir_base,
-                                              int dir_len, long long &u) {
+// Re-fire (record, window) pairs of record i: tumbling, its window if inside the directory (0 or 1);
+// sliding, every fired-but-not-cleaned window of the record (u = the first, the rest consecutive).
+__device__ __forceinline__ int refire_pairs(const int64_t *ts, int64_t i, const WindowGeom &g, long long dir_base,
+                                           int dir_len, long long &u) {
     u = 0;
-    if (classify(ts[i], g, u) != REC_REFIRE) return false;
+    if (classify(ts[i], g, u) != REC_REFIRE) return 0;
+    if (g.sliding) {
+        long long ja, jb;
+        slide_refire_windows(ts[i], g, ja, jb);
+        u = ja;
+        return (int)(jb - ja + 1);
+    }
     return u - dir_base >= 0 && u - dir_base < dir_len;
 }
 
-// per block: re-fire records of its contiguous share of the batch
+// per block: re-fire pairs of its contiguous share of the batch
 __global__ __launch_bounds__(RF_THREADS) void refire_count_kernel(const int64_t *__restrict__ ts, int64_t n,
                                                                   WindowGeom g, long long dir_base, int dir_len,
                                                                   uint32_t *blk) {
@@ -569,14 +593,15 @@ __global__ __launch_bounds__(RF_THREADS) void refire_count_kernel(const int64_t 
     unsigned c = 0;
     for (int64_t i = b0 + threadIdx.x; i < b1; i += RF_THREADS) {
         long long u;
-        c += refire_in_dir(ts, i, g, dir_base, dir_len, u);
+        c += (unsigned)refire_pairs(ts, i, g, dir_base, dir_len, u);
     }
     unsigned total;
     (void)block_exclusive_scan(c, &total);
     if (threadIdx.x == 0) blk[blockIdx.x] = total;
 }
 
-// writes the re-fire records of each block's share in arrival order: r_idx (batch index), r_u (window)
+// writes the re-fire pairs of each block's share in arrival order (a record's windows ascending):
+// r_idx (batch index), r_u (window)
 __global__ __launch_bounds__(RF_THREADS) void refire_write_kernel(const int64_t *__restrict__ ts, int64_t n,
                                                                   WindowGeom g, long long dir_base, int dir_len,
                                                                   const uint32_t *blk, int64_t *r_idx,
@@ -594,14 +619,65 @@ __global__ __launch_bounds__(RF_THREADS) void refire_write_kernel(const int64_t 
     for (int64_t i0 = b0; i0 < b1; i0 += RF_THREADS) {
         const int64_t i = i0 + threadIdx.x;
         long long u = 0;
-        const bool f = i < b1 && refire_in_dir(ts, i, g, dir_base, dir_len, u);
+        const int c = i < b1 ? refire_pairs(ts, i, g, dir_base, dir_len, u) : 0;
         unsigned total;
-        const unsigned at = block_exclusive_scan(f ? 1u : 0u, &total);
-        if (f) {
-            r_idx[base + at] = i;
-            r_u[base + at] = u;
+        const unsigned at = block_exclusive_scan((unsigned)c, &total);
+        for (int x = 0; x < c; ++x) {
+            r_idx[base + at + x] = i;
+            r_u[base + at + x] = u + x;
         }
         base += total;
+    }
+}
+
+// Sliding: pair q's entry is (key, window); its sort key is key slot * nj + (window - j0), the key slot
+// from a scratch table of the batch's re-fire keys (slot words hold key ^ 2^63, 0 = free; the empty-key
+// marker itself takes slot cap).  `before` = the window's state before the batch: its panes' entries
+// for the key, combined (the panes are the pane directory [pane_base, pane_base + pane_len)).
+__device__ __forceinline__ const int64_t *table_find(const TableDesc &t, int stride, int64_t key) {
+    if (!t.base) return nullptr;
+    if (key == GWO_EMPTY_KEY) return t.side[0] != 0 ? t.side + 1 : nullptr;
+    uint64_t slot = slot_hash(key) & t.mask;
+    while (true) {
+        const int64_t *e = t.base + slot * (uint64_t)stride;
+        if (e[0] == key) return e + 1;
+        if (e[0] == GWO_EMPTY_KEY) return nullptr;
+        slot = (slot + 1) & t.mask;
+    }
+}
+
+__global__ __launch_bounds__(RF_THREADS) void slide_refire_slot_kernel(
+    const int64_t *__restrict__ key, const int64_t *r_idx, const long long *r_u, int64_t m, AccPlan p, WindowGeom g,
+    unsigned long long *keytab, uint64_t kmask, long long j0, uint32_t nj, const TableDesc *__restrict__ pdir,
+    long long pane_base, long long pane_len, uint32_t *r_slot, int64_t *before) {
+    const int64_t om = jsub(g.offset, fdiv_floor(g.offset, g.slide, g.inv_slide) * g.slide);
+    const long long panes = g.size / g.unit;
+    for (int64_t j = (int64_t)blockIdx.x * RF_THREADS + threadIdx.x; j < m; j += (int64_t)gridDim.x * RF_THREADS) {
+        const int64_t k = key[r_idx[j]];
+        uint64_t ks = kmask + 1;
+        if (k != GWO_EMPTY_KEY) {
+            const unsigned long long enc = (unsigned long long)k ^ 0x8000000000000000ull;
+            ks = slot_hash(k) & kmask;
+            while (true) {
+                const unsigned long long prev = atomicCAS(&keytab[ks], 0ull, enc);
+                if (prev == 0ull || prev == enc) break;
+                ks = (ks + 1) & kmask;
+            }
+        }
+        const long long w = r_u[j];
+        r_slot[j] = (uint32_t)(ks * nj + (uint64_t)(w - j0));
+        int64_t acc[GWO_MAX_WORDS];
+        for (int x = 0; x < p.nwords; ++x) acc[x] = p.ident[x];
+        const int64_t start = (int64_t)((uint64_t)w * (uint64_t)g.slide + (uint64_t)om);
+        const long long u0 = fdiv_floor(jsub(start, g.unit_off_mod), g.unit, g.inv_unit);
+        for (long long u = u0; u < u0 + panes; ++u) {
+            const long long d = u - pane_base;
+            if (d < 0 || d >= pane_len) continue;
+            const int64_t *e = table_find(pdir[d], p.stride, k);
+            if (e)
+                for (int x = 0; x < p.nwords; ++x) acc[x] = combine(p.op[x], acc[x], e[x]);
+        }
+        for (int x = 0; x < p.nwords; ++x) before[j * GWO_MAX_WORDS + x] = acc[x];
     }
 }
 
@@ -636,7 +712,7 @@ __global__ __launch_bounds__(1024) void refire_emit_kernel(const int64_t *__rest
                                                            const long long *r_u, int64_t m, const uint32_t *skey,
                                                            const uint32_t *spay, const int64_t *before, AccPlan p,
                                                            ResultPlan rp, int64_t unit, int64_t unit_off_mod,
-                                                           OutCols o) {
+                                                           int64_t span, OutCols o) {
     __shared__ int64_t s_x[1024][GWO_MAX_WORDS];
     __shared__ uint32_t s_slot[1024];
     __shared__ uint8_t s_flag[1024];
@@ -688,7 +764,7 @@ __global__ __launch_bounds__(1024) void refire_emit_kernel(const int64_t *__rest
                 const int64_t start = (int64_t)((uint64_t)r_u[j] * (uint64_t)unit + (uint64_t)unit_off_mod);
                 o.key[pos] = key[r_idx[j]];
                 o.start[pos] = start;
-                o.end[pos] = (int64_t)((uint64_t)start + (uint64_t)unit);
+                o.end[pos] = (int64_t)((uint64_t)start + (uint64_t)span);
                 write_results(p, rp, acc, o, pos);
             }
         }
@@ -776,9 +852,19 @@ void launch_refire_slots(const int64_t *key, const int64_t *r_idx, const long lo
 
 void launch_refire_emit(const int64_t *key, const int64_t *val, const int64_t *r_idx, const long long *r_u, int64_t m,
                         const uint32_t *skey, const uint32_t *spay, const int64_t *before, const AccPlan &p,
-                        const ResultPlan &rp, int64_t unit, int64_t unit_off_mod, OutCols o, hipStream_t s) {
+                        const ResultPlan &rp, int64_t unit, int64_t unit_off_mod, int64_t span, OutCols o,
+                        hipStream_t s) {
     hipLaunchKernelGGL(refire_emit_kernel, dim3(1), dim3(1024), 0, s, key, val, r_idx, r_u, m, skey, spay, before, p, rp,
-                       unit, unit_off_mod, o);
+                       unit, unit_off_mod, span, o);
+}
+
+void launch_slide_refire_slots(const int64_t *key, const int64_t *r_idx, const long long *r_u, int64_t m,
+                               const AccPlan &p, const WindowGeom &g, unsigned long long *keytab, uint64_t kmask,
+                               long long j0, uint32_t nj, const TableDesc *pdir, long long pane_base,
+                               long long pane_len, uint32_t *r_slot, int64_t *before, hipStream_t s) {
+    int blocks = (int)std::min<int64_t>(1024, (m + RF_THREADS - 1) / RF_THREADS);
+    hipLaunchKernelGGL(slide_refire_slot_kernel, dim3(std::max(blocks, 1)), dim3(RF_THREADS), 0, s, key, r_idx, r_u, m,
+                       p, g, keytab, kmask, j0, nj, pdir, pane_base, pane_len, r_slot, before);
 }
 
 void launch_scan(const int64_t *key, const int64_t *ts, int64_t n, const WindowGeom &g, long long hist_base,

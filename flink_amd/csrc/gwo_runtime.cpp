@@ -394,7 +394,8 @@ gwo_status Handle::refire_rows(const int64_t *k, const int64_t *t, const int64_t
     const uint32_t *sk = (const uint32_t *)(b + (which ? o_k2 : o_k1));
     const uint32_t *sp = (const uint32_t *)(b + (which ? o_v2 : o_v1));
     launch_refire_emit(k, v, (const int64_t *)(b + o_idx), (const long long *)(b + o_u), (int64_t)m, sk, sp,
-                       (const int64_t *)(b + o_before), plan, rplan, geom.unit, geom.unit_off_mod, out_cols(), stream);
+                       (const int64_t *)(b + o_before), plan, rplan, geom.unit, geom.unit_off_mod, geom.unit, out_cols(),
+                       stream);
     GWO_TRY(launch_ok("refire emit"));
     out_rows += m;
     return GWO_OK;
@@ -402,9 +403,10 @@ gwo_status Handle::refire_rows(const int64_t *k, const int64_t *t, const int64_t
 
 gwo_status Handle::insert_windowed(const int64_t *k, const int64_t *t, const int64_t *v, int64_t n) {
     WindowGeom g = geom_now();
-    // tumbling: re-fire records (allowedLateness > 0) are emitted per element and inserted
-    g.refire_ok = cfg.assigner == GWO_ASSIGNER_TUMBLING ? 1 : 0;
+    // re-fire records (allowedLateness > 0) are emitted per element and inserted
+    g.refire_ok = 1;
     uint64_t refire_total = 0;
+    bool slide_refired = false;
     long long hist_base = hist_hint;
     bool first_pass = true;
     BatchStats &hs = *h_stats;
@@ -432,8 +434,6 @@ gwo_status Handle::insert_windowed(const int64_t *k, const int64_t *t, const int
             if (hs.bad_range) return poison(GWO_ERR_UNSUPPORTED,
                                             "sliding windows: timestamp < offset - slide (Java '%' quirk range) is "
                                             "outside the pane restatement");
-            if (hs.refire && !g.refire_ok)
-                return poison(GWO_ERR_UNSUPPORTED, "allowedLateness > 0 re-firing on sliding windows is not supported");
             refire_total = hs.refire;
             if (side_enabled()) {
                 GWO_TRY(hipcheck(hipMemcpyAsync(h_scalar, d_side_count, 8, hipMemcpyDeviceToHost, stream), "side count"));
@@ -478,7 +478,11 @@ gwo_status Handle::insert_windowed(const int64_t *k, const int64_t *t, const int
         GWO_TRY(ensure_buf(dir_buf, dir_len * sizeof(TableDesc)));
         GWO_TRY(hipcheck(hipMemcpyAsync(dir_buf.ptr, h_dir.data(), dir_len * sizeof(TableDesc), hipMemcpyHostToDevice,
                                         stream), "dir"));
-        if (refire_total) GWO_TRY(refire_rows(k, t, v, n, g, hist_base, dir_len, refire_total));
+        if (refire_total && !slide) GWO_TRY(refire_rows(k, t, v, n, g, hist_base, dir_len, refire_total));
+        if (refire_total && slide && !slide_refired) {   // whole batch, before its first insert
+            GWO_TRY(slide_refire_rows(k, t, v, n, g, refire_total));
+            slide_refired = true;
+        }
         prof_begin(GWO_KERNEL_INSERT);
         launch_insert(k, t, v, n, g, plan, (const TableDesc *)dir_buf.ptr, hist_base, dir_len, use_preagg, d_stats,
                       ring_desc(), stream);

@@ -43,8 +43,6 @@ static __int128 fdiv128(__int128 a, __int128 b) {
 }
 
 gwo_status Handle::slide_init() {
-    if (cfg.allowed_lateness != 0)
-        return fail(GWO_ERR_UNSUPPORTED, "sliding windows with allowedLateness > 0 are not in the GPU subset");
     slide = new SlideState();
     SlideState &S = *slide;
     S.om = fmod64(cfg.offset, cfg.slide);
@@ -171,14 +169,32 @@ gwo_status Handle::slide_restore_anchor() {
     return GWO_OK;
 }
 
+// Window indices are kept where start_j + size cannot overflow a long.
+static __int128 clamp_window(__int128 j, int64_t size, int64_t slide) {
+    const __int128 j_lo = fdiv128((__int128)GWO_LONG_MIN_H + 2 * (__int128)size + slide, slide);
+    const __int128 j_hi = fdiv128((__int128)GWO_LONG_MAX_H - 2 * (__int128)size - slide, slide);
+    return std::max(j_lo, std::min(j_hi, j));
+}
+
+// first window not fired at watermark w: start_j + size - 1 > w
+__int128 Handle::first_unfired_window(int64_t w) const {
+    return clamp_window(fdiv128((__int128)w - cfg.size + 1 - slide->om, cfg.slide) + 1, cfg.size, cfg.slide);
+}
+
+// first window not cleaned up at watermark w: start_j + size - 1 + allowedLateness > w (WindowOperator.java:
+// 639-646 saturates the cleanup time at Long.MAX_VALUE; keeping such windows' panes a little longer is harmless)
+__int128 Handle::first_uncleaned_window(int64_t w) const {
+    const __int128 j =
+        fdiv128((__int128)w - cfg.size + 1 - (__int128)cfg.allowed_lateness - slide->om, cfg.slide) + 1;
+    return std::min(first_unfired_window(w), clamp_window(j, cfg.size, cfg.slide));
+}
+
 gwo_status Handle::fire_sliding(int64_t new_wm) {
     SlideState &S = *slide;
-    // first window that is not fired at new_wm: start_j + size - 1 > wm
-    __int128 j_new = fdiv128((__int128)new_wm - cfg.size + 1 - S.om, cfg.slide) + 1;
-    // keep window starts representable: start_j + size must not overflow a long
-    const __int128 j_lo = fdiv128((__int128)GWO_LONG_MIN_H + 2 * (__int128)cfg.size + cfg.slide, cfg.slide);
-    const __int128 j_hi = fdiv128((__int128)GWO_LONG_MAX_H - 2 * (__int128)cfg.size - cfg.slide, cfg.slide);
-    j_new = std::max(j_lo, std::min(j_hi, j_new));
+    const __int128 j_new = first_unfired_window(new_wm);
+    // panes stay while a window holding them is not cleaned up: with allowedLateness > 0 fired windows
+    // still take (and re-fire for) late records until their cleanup time
+    const long long keep_from = win_first_pane(first_uncleaned_window(new_wm));
     if (!S.j_set) {
         // anchor: windows before j_new have fired (were empty); the first window with data may be earlier
         S.J = j_new;
@@ -203,8 +219,8 @@ gwo_status Handle::fire_sliding(int64_t new_wm) {
             __int128 target = j_new;
             auto it = tables.lower_bound(lo);
             if (it != tables.end()) target = std::min(j_new, std::max(S.J + 1, first_window_of_pane(it->first)));
-            // panes before the target window are in no unfired window any more
-            GWO_TRY(release_panes_before(win_first_pane(target)));
+            // panes before the target window are in no unfired (or uncleaned) window any more
+            GWO_TRY(release_panes_before(std::min(win_first_pane(target), keep_from)));
             S.J = target;
             if (S.ring) GWO_TRY(ring_rebuild());
             continue;
@@ -260,10 +276,11 @@ gwo_status Handle::fire_sliding(int64_t new_wm) {
                             S.d_live, stream);
             prof_end(GWO_KERNEL_SLIDE, 0);
         }
-        GWO_TRY(release_panes_before(nlo));
+        GWO_TRY(release_panes_before(std::min(nlo, keep_from)));
         S.J += 1;
     }
-    return GWO_OK;
+    // windows whose cleanup time this watermark passed (no fire needed) free their panes too
+    return release_panes_before(std::min(win_first_pane(S.J), keep_from));
 }
 
 // Reset and return to the pool every pane table with index < first.
@@ -278,6 +295,80 @@ gwo_status Handle::release_panes_before(long long first) {
         release_table(t);
         it = tables.erase(it);
     }
+    return GWO_OK;
+}
+
+// Per-element re-fire on sliding windows (allowedLateness > 0).  The reference adds a record to each of its
+// windows that is not late (WindowOperator.java:386-427) and EventTimeTrigger.onElement FIREs the ones whose
+// maxTimestamp the watermark passed (EventTimeTrigger.java:37-45): one row per (record, fired-but-not-cleaned
+// window) with that window's contents including the record.  Every record of the batch that reaches such a
+// window re-fires it, so pair q's row is
+//     window state before the batch  (+)  the batch's values for that (key, window) up to q, arrival order,
+// where the state before the batch is the combine of the window's panes for the key.  The pairs are written in
+// arrival order, sorted stably by (key, window) and scanned (refire_emit_kernel); then the batch's insert adds
+// the records to their panes.
+gwo_status Handle::slide_refire_rows(const int64_t *k, const int64_t *t, const int64_t *v, int64_t n,
+                                     const WindowGeom &g, uint64_t records) {
+    SlideState &S = *slide;
+    const __int128 j_fire = first_unfired_window(g.wm), j_clean = first_uncleaned_window(g.wm);
+    if (j_fire <= j_clean) return poison(GWO_ERR_HIP, "sliding re-fire records but no fired, uncleaned window");
+    if (j_fire - j_clean >= ((__int128)1 << 24))
+        return fail(GWO_ERR_UNSUPPORTED, "allowedLateness re-fire: more than 2^24 fired, uncleaned windows");
+    const uint32_t nj = (uint32_t)(j_fire - j_clean);
+    const uint64_t per = std::min<uint64_t>((uint64_t)((cfg.size + cfg.slide - 1) / cfg.slide), nj);
+    const uint64_t mmax = std::max<uint64_t>(records * per, 1);
+    uint64_t kcap = 64;
+    while (kcap < 2 * records) kcap <<= 1;
+    const unsigned __int128 groups = (unsigned __int128)(kcap + 1) * nj;
+    if (groups >= ((unsigned __int128)1 << 32))
+        return poison(GWO_ERR_CAPACITY, "allowedLateness re-fire: (re-fire keys x fired windows) exceeds 2^32");
+    int bits = 8;
+    while (bits < 32 && ((unsigned __int128)1 << bits) < groups) bits += 8;
+    const long long pane_base = win_first_pane(j_clean), pane_hi = win_last_pane(j_fire - 1);
+    const long long pane_len = pane_hi - pane_base + 1;
+    if (pane_len <= 0 || pane_len > (1LL << 24))
+        return fail(GWO_ERR_UNSUPPORTED, "allowedLateness re-fire: fired windows span more than 2^24 panes");
+    std::vector<TableDesc> pdir((size_t)pane_len, TableDesc{});
+    for (auto it = tables.lower_bound(pane_base); it != tables.end() && it->first <= pane_hi; ++it)
+        pdir[(size_t)(it->first - pane_base)] = desc(it->second);
+    const uint64_t rs_blocks = (mmax + 4095) / 4096;
+    auto up = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    // carve: blk[256] u32 | pdir | r_idx[m] | r_u[m] | before[m][MAX_WORDS] | r_slot, k1, v1, k2, v2 [m] u32 |
+    //        hist | keytab[kcap] u64
+    const size_t o_blk = 0, o_pdir = 1024, o_idx = up(o_pdir + (size_t)pane_len * sizeof(TableDesc));
+    const size_t o_u = o_idx + mmax * 8, o_before = o_u + mmax * 8, o_slot = o_before + mmax * GWO_MAX_WORDS * 8;
+    const size_t o_k1 = o_slot + mmax * 4, o_v1 = o_k1 + mmax * 4, o_k2 = o_v1 + mmax * 4, o_v2 = o_k2 + mmax * 4;
+    const size_t o_hist = up(o_v2 + mmax * 4), o_keys = up(o_hist + 256 * 4 * rs_blocks), total = o_keys + kcap * 8;
+    GWO_TRY(ensure_buf(refire_buf, total));
+    char *b = (char *)refire_buf.ptr;
+    GWO_TRY(hipcheck(hipMemcpyAsync(b + o_pdir, pdir.data(), (size_t)pane_len * sizeof(TableDesc),
+                                    hipMemcpyHostToDevice, stream), "refire panes"));
+    GWO_TRY(hipcheck(hipMemsetAsync(b + o_keys, 0, kcap * 8, stream), "refire keys"));
+    launch_refire_collect(t, n, g, 0, 0, (uint32_t *)(b + o_blk), (int64_t *)(b + o_idx), (long long *)(b + o_u),
+                          stream);
+    GWO_TRY(launch_ok("refire collect"));
+    std::vector<uint32_t> blk(256);
+    GWO_TRY(hipcheck(hipMemcpyAsync(blk.data(), b + o_blk, 256 * 4, hipMemcpyDeviceToHost, stream), "refire count"));
+    GWO_TRY(hipcheck(hipStreamSynchronize(stream), "refire count"));
+    uint64_t m = 0;
+    for (uint32_t c : blk) m += c;
+    if (m == 0 || m > mmax) return poison(GWO_ERR_HIP, "allowedLateness re-fire: pair count disagrees with the scan");
+    launch_slide_refire_slots(k, (const int64_t *)(b + o_idx), (const long long *)(b + o_u), (int64_t)m, plan, g,
+                              (unsigned long long *)(b + o_keys), kcap - 1, (long long)j_clean, nj,
+                              (const TableDesc *)(b + o_pdir), pane_base, pane_len, (uint32_t *)(b + o_slot),
+                              (int64_t *)(b + o_before), stream);
+    GWO_TRY(launch_ok("refire slots"));
+    const int which = radix_sort_pairs((const uint32_t *)(b + o_slot), nullptr, (int64_t)m, bits,
+                                       (uint32_t *)(b + o_k1), (uint32_t *)(b + o_v1), (uint32_t *)(b + o_k2),
+                                       (uint32_t *)(b + o_v2), (uint32_t *)(b + o_hist), stream);
+    GWO_TRY(launch_ok("refire sort"));
+    GWO_TRY(ensure_output(m));
+    const uint32_t *sk = (const uint32_t *)(b + (which ? o_k2 : o_k1));
+    const uint32_t *sp = (const uint32_t *)(b + (which ? o_v2 : o_v1));
+    launch_refire_emit(k, v, (const int64_t *)(b + o_idx), (const long long *)(b + o_u), (int64_t)m, sk, sp,
+                       (const int64_t *)(b + o_before), plan, rplan, cfg.slide, S.om, cfg.size, out_cols(), stream);
+    GWO_TRY(launch_ok("refire emit"));
+    out_rows += m;
     return GWO_OK;
 }
 
