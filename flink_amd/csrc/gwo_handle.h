@@ -207,7 +207,8 @@ struct Handle {
                             const int64_t **dt, const int64_t **dv);
     int64_t unit_start(long long u) const;
     WindowGeom geom_now() const;
-    gwo_status insert_windowed(const int64_t *k, const int64_t *t, const int64_t *v, int64_t n);
+    gwo_status insert_windowed(const int64_t *k, const int64_t *t, const int64_t *v, int64_t n,
+                               const WindowGeom *at = nullptr);
     gwo_status refire_rows(const int64_t *k, const int64_t *t, const int64_t *v, int64_t n, const WindowGeom &g,
                            long long dir_base, int dir_len, uint64_t mmax);
     void adapt_preagg(uint64_t accepted, uint64_t partials);
@@ -269,6 +270,9 @@ struct Handle {
     void log_uncarve(const LogJob &J, int w, uint64_t keep);
     gwo_status log_commit_spec(LogJob &J, const unsigned long long *rbp);
     gwo_status log_resolve_k1(LogJob J);
+    gwo_status log_resolve_batch(LogJob &J, bool &refire);
+    gwo_status log_fold_raw(const std::vector<long long> &units, const SnapCols &c);
+    gwo_status log_migrate(long long u);
     gwo_status log_wait_readback(int slot, unsigned long long seq);
     gwo_status log_flush();                    // resolve the pipelined batch (no-op without one)
     bool log_pending_may_fire(int64_t new_wm) const;

@@ -97,7 +97,8 @@ struct WindowGeom {
     int32_t max_par;
     int32_t kg_lo;
     int32_t kg_hi;
-    int32_t refire_ok;                 // tumbling table layout: re-fire records are emitted + inserted
+    int32_t refire_ok;                 // table passes: re-fire records are emitted + inserted
+    int32_t refire_only;               // table pass over the log layout's fired windows: re-fire records only
 };
 
 // Output columns (SoA) in HBM.
@@ -165,9 +166,6 @@ void launch_insert(const int64_t *key, const int64_t *ts, const void *val, int64
                    const AccPlan &plan, const TableDesc *dir, long long dir_base, int dir_len, int preagg,
                    BatchStats *stats, const RingDesc &ring, hipStream_t s);
 
-// Emits every occupied entry (with live_word >= 0: every entry whose word live_word is > 0).
-void launch_snapshot(const TableDesc &t, uint64_t cap, const AccPlan &p, int64_t start, int64_t *key,
-                     int64_t *wstart, int64_t *words, unsigned long long *count, long long out_cap, hipStream_t s);
 void launch_restore(const int64_t *key, const int64_t *wstart, const int64_t *words, int64_t n, const AccPlan &p,
                     const WindowGeom &g, const TableDesc *dir, long long dir_base, int dir_len, hipStream_t s);
 void launch_refire_collect(const int64_t *ts, int64_t n, const WindowGeom &g, long long dir_base, int dir_len,
@@ -189,6 +187,8 @@ int radix_sort_pairs(const uint32_t *keys, const uint32_t *vals, int64_t n, int 
                      uint32_t *k2, uint32_t *v2, uint32_t *hist, hipStream_t s);
 void launch_key_groups_utf16(const uint16_t *chars, const int64_t *offsets, int64_t n, int max_par, int par,
                              int32_t *hash, int32_t *kg, int32_t *op, hipStream_t s);
+void launch_table_load(const SnapCols &c, int64_t n, const TableDesc &t, const AccPlan &p, hipStream_t s);
+// Emits every occupied entry (with live_word >= 0: every entry whose word live_word is > 0).
 void launch_fire(const TableDesc &t, uint64_t cap, const AccPlan &plan, const ResultPlan &rp, int64_t start,
                  int64_t end, OutCols out, int reset, int live_word, hipStream_t s);
 

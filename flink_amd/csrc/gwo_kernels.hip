@@ -78,6 +78,12 @@ __device__ __forceinline__ void slide_refire_windows(int64_t ts, const WindowGeo
     jb = last_max_ts <= g.wm ? j_last : j_last - (fdiv_floor(last_max_ts - g.wm - 1, g.slide, g.inv_slide) + 1);
 }
 
+// Records a table pass inserts: accepted ones and (re-fire enabled) re-fire ones; a refire_only pass (the
+// log layout's fired windows, gwo_log.cpp) leaves accepted records and late accounting to the log's K1.
+__device__ __forceinline__ bool takes(int c, const WindowGeom &g) {
+    return (c == REC_ACCEPT && !g.refire_only) || (c == REC_REFIRE && g.refire_ok);
+}
+
 // ------------------------------------------------------------------------------------------------
 // scan
 // ------------------------------------------------------------------------------------------------
@@ -98,14 +104,14 @@ __global__ __launch_bounds__(256) void scan_kernel(const int64_t *__restrict__ k
         long long u = 0;
         int c = classify(ts[i], g, u);
         if (c == REC_REFIRE && g.refire_ok) refire++;   // also inserted: counted with the accepted records
-        if (c == REC_ACCEPT || (c == REC_REFIRE && g.refire_ok)) {
+        if (takes(c, g)) {
             acc++;
             mn = u < mn ? u : mn;
             mx = u > mx ? u : mx;
             long long b = u - hist_base;
             if (b >= 0 && b < GWO_HIST_BINS) atomicAdd(&s_hist[b], 1ull);
             else hout++;
-        } else if (c == REC_LATE) {
+        } else if (c == REC_LATE && !g.refire_only) {
             late++;
             if (side_enabled) {
                 unsigned long long pos = atomicAdd(side_count, 1ull);
@@ -200,7 +206,7 @@ __global__ __launch_bounds__(256) void insert_direct_kernel(const int64_t *__res
         long long u = 0;
         int64_t t = ts[i];
         const int c = classify(t, g, u);
-        if (c != REC_ACCEPT && !(c == REC_REFIRE && g.refire_ok)) continue;
+        if (!takes(c, g)) continue;
         long long d = u - dir_base;
         if (d < 0 || d >= dir_len) continue;
         int64_t k = key[i];
@@ -267,7 +273,7 @@ __global__ __launch_bounds__(256) void insert_preagg_kernel(const int64_t *__res
             if (i >= n) continue;
             long long u = 0;
             const int c = classify(ts[i], g, u);
-            if (c != REC_ACCEPT && !(c == REC_REFIRE && g.refire_ok)) continue;
+            if (!takes(c, g)) continue;
             long long d = u - dir_base;
             if (d < 0 || d >= dir_len) continue;
             int64_t k = key[i];
@@ -779,25 +785,9 @@ __global__ __launch_bounds__(1024) void refire_emit_kernel(const int64_t *__rest
 }
 
 // ------------------------------------------------------------------------------------------------
-// Snapshot / restore of the tumbling table state (the heap backend's per-(key, namespace) entries,
-// CopyOnWriteStateMapSnapshot.java:127-129): raw accumulator words, so a restore continues exactly.
+// Restore of table state (the heap backend's per-(key, namespace) entries, CopyOnWriteStateMapSnapshot.java:
+// 127-129): raw accumulator words, so a restore continues exactly (collection: gwo_snapshot.hip).
 // ------------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void snapshot_kernel(TableDesc t, uint64_t cap, AccPlan p, int64_t start,
-                                                       int64_t *key, int64_t *wstart, int64_t *words,
-                                                       unsigned long long *count, long long out_cap) {
-    for (uint64_t b0 = (uint64_t)blockIdx.x * 256; b0 < cap + 1; b0 += (uint64_t)gridDim.x * 256) {
-        const uint64_t i = b0 + threadIdx.x;
-        const int64_t *e = i <= cap ? fire_entry(t, cap, p.stride, i) : nullptr;
-        const bool occ = e && (i < cap ? e[0] != GWO_EMPTY_KEY : e[0] != 0);
-        const unsigned long long pos = block_reserve(occ ? 1u : 0u, count);
-        if (occ && (long long)pos < out_cap) {
-            key[pos] = i < cap ? e[0] : GWO_EMPTY_KEY;
-            wstart[pos] = start;
-            for (int w = 0; w < p.nwords; ++w) words[pos * p.nwords + w] = e[1 + w];
-        }
-    }
-}
-
 // Rows whose key group is outside [kg_lo, kg_hi] belong to another subtask (rescaling) and are skipped.
 __global__ __launch_bounds__(256) void restore_kernel(const int64_t *key, const int64_t *wstart, const int64_t *words,
                                                       int64_t n, AccPlan p, WindowGeom g,
@@ -821,12 +811,6 @@ __global__ __launch_bounds__(256) void restore_kernel(const int64_t *key, const 
         }
         count_claims(occ, claimed);
     }
-}
-
-void launch_snapshot(const TableDesc &t, uint64_t cap, const AccPlan &p, int64_t start, int64_t *key,
-                     int64_t *wstart, int64_t *words, unsigned long long *count, long long out_cap, hipStream_t s) {
-    hipLaunchKernelGGL(snapshot_kernel, dim3(grid_for((int64_t)cap + 1, 1, 4096)), dim3(256), 0, s, t, cap, p, start,
-                       key, wstart, words, count, out_cap);
 }
 
 void launch_restore(const int64_t *key, const int64_t *wstart, const int64_t *words, int64_t n, const AccPlan &p,

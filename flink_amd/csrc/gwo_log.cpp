@@ -596,6 +596,23 @@ gwo_status Handle::log_wait_readback(int slot, unsigned long long seq) {
 // classification error (before any window state changes), re-runs K1 when the window range guess or a
 // region capacity was wrong, and launches pass 2 (deferred) for each window range.
 gwo_status Handle::log_resolve_k1(LogJob J) {
+    const LogJob J0 = J;
+    bool refire = false;
+    GWO_TRY(log_resolve_batch(J, refire));
+    if (!refire) return GWO_OK;
+    // allowedLateness > 0: records of fired, not yet cleaned windows re-fire them (EventTimeTrigger.onElement
+    // FIRE, WindowOperator.java:393-406).  Those windows live in hash tables (log_migrate); a table pass over
+    // the batch takes the re-fire records only -- the log took the accepted ones, K1 counted the late ones.
+    WindowGeom g = J0.g;
+    g.refire_ok = 1;
+    g.refire_only = 1;
+    const long long hint = hist_hint;   // the log's window-range guess, not the fired windows'
+    const gwo_status s = insert_windowed(J0.k, J0.t, J0.v, J0.n, &g);
+    hist_hint = hint;
+    return s;
+}
+
+gwo_status Handle::log_resolve_batch(LogJob &J, bool &refire) {
     LogState &L = *logst;
     BatchStats &hs = *h_stats;
     bool first_pass = true;
@@ -612,9 +629,12 @@ gwo_status Handle::log_resolve_k1(LogJob J) {
                                          "Record has Long.MIN_VALUE timestamp (= no timestamp marker). Is the time "
                                          "characteristic set to 'ProcessingTime', or did you forget to call "
                                          "'DataStream.assignTimestampsAndWatermarks(...)'?");
-            if (hs.refire) return poison(GWO_ERR_UNSUPPORTED,
-                                         "allowedLateness > 0: a record re-fires an already emitted window "
-                                         "(EventTimeTrigger.onElement FIRE) -- not supported by the GPU operator");
+            if (hs.refire) {
+                if (J.stride != 1)
+                    return poison(GWO_ERR_UNSUPPORTED, "allowedLateness > 0 re-fire on records received by the "
+                                                       "multi-GPU exchange: use the table layout");
+                refire = true;
+            }
             if (hs.bad_kg) return poison(GWO_ERR_KEY_GROUP, ("Key group of key " + std::to_string(hs.bad_kg_key) +
                                                              " is not in KeyGroupRange{startKeyGroup=" +
                                                              std::to_string(cfg.key_group_start) + ", endKeyGroup=" +
@@ -712,7 +732,10 @@ gwo_status Handle::insert_log(const int64_t *k, const int64_t *t, const int64_t 
     // checks and pass-2 planning overlap a running K1.  Only for caller-owned device columns (borrowed
     // until the next call returns, gwo.h) -- staged host input and received exchange buffers are reused
     // by the next batch -- and without a side output (K1 appends to it on the first pass).
-    const bool pipe = L.pipeline && stride == 1 && !side_enabled() && !comm && (const void *)k != stage_key.ptr &&
+    // With allowedLateness > 0 a batch resolves before the next watermark: its re-fire records must reach the
+    // fired windows' tables before a watermark cleans them up.
+    const bool pipe = L.pipeline && cfg.allowed_lateness == 0 && stride == 1 && !side_enabled() && !comm &&
+                      (const void *)k != stage_key.ptr &&
                       (const void *)t != stage_ts.ptr && (!v || (const void *)v != stage_val.ptr);
     if (L.job.active && !pipe) GWO_TRY(log_flush());
     J.slot = L.free_slot();
@@ -759,6 +782,18 @@ gwo_status Handle::fire_log(int64_t new_wm) {
     if (log_pending_may_fire(new_wm)) GWO_TRY(log_flush());
     std::vector<long long> fire;
     due(fire);
+    if (cfg.allowed_lateness == 0 && !tables.empty()) GWO_TRY(fire_tumbling(new_wm));   // restored fired windows
+    if (cfg.allowed_lateness > 0) {
+        // a fired window stays until its cleanup time and takes late records: it moves to a hash table,
+        // which the table path fires, re-fires and cleans up (fire_tumbling, refire_rows)
+        if (!fire.empty()) {
+            GWO_TRY(finish_fire());
+            GWO_TRY(log_resolve_split());
+            due(fire);
+            for (long long u : fire) GWO_TRY(log_migrate(u));
+        }
+        return fire_tumbling(new_wm);
+    }
     if (fire.empty()) return GWO_OK;
     GWO_TRY(finish_fire());         // the previous fire's rows and memory first
     GWO_TRY(log_resolve_split());   // the fired windows' last segments must be complete
@@ -882,9 +917,7 @@ gwo_status Handle::finish_fire() {
     L.last_window_records = 0;
     for (long long u : L.fire_units) L.last_window_records = std::max<uint64_t>(L.last_window_records, L.wins[u].records);
     for (long long u : L.fire_units) {
-        log_release(L.wins[u]);
-        // allowedLateness > 0: any later record of this window is a re-fire and is rejected at
-        // classification, so nothing of the window is kept until its cleanup time
+        log_release(L.wins[u]);   // allowedLateness 0: the window's cleanup time is its fire
         L.wins.erase(u);
     }
     L.fire_units.clear();
@@ -902,6 +935,10 @@ gwo_status Handle::log_state_size(int64_t *entries) {
     GWO_TRY(log_flush());
     uint64_t s = 0;
     for (auto &kv : logst->wins) s += kv.second.records + kv.second.partial_rows;
+    if (!tables.empty()) {   // fired windows kept for allowedLateness
+        GWO_TRY(read_occupancy());
+        for (auto &kv : tables) s += kv.second.occ;
+    }
     *entries = (int64_t)s;
     return GWO_OK;
 }
@@ -913,10 +950,9 @@ namespace gwo {
 
 size_t Handle::log_window_count() const { return logst->wins.size(); }
 
-// Folds every open window without releasing it -- the fire kernel, LDS hash-table path only, with a result
-// plan that emits the raw accumulator words -- into checkpoint rows (fire timers pending: a log window is
-// released when it fires).
-gwo_status Handle::log_snapshot_collect(const SnapCols &c) {
+// Folds windows without releasing them -- the fire kernel, LDS hash-table path only, with a result plan that
+// emits the raw accumulator words -- into rows (key, window, words) of `c`.
+gwo_status Handle::log_fold_raw(const std::vector<long long> &units, const SnapCols &c) {
     LogState &L = *logst;
     ResultPlan raw{};
     raw.naggs = plan.nwords;
@@ -937,36 +973,84 @@ gwo_status Handle::log_snapshot_collect(const SnapCols &c) {
         L.max_groups = std::max(cus, 1);
     }
     L.h_fire.clear();
-    for (auto &kv : L.wins)
-        for (auto &d : kv.second.segs) L.h_fire.push_back(d);
+    for (long long u : units)
+        for (auto &d : L.wins[u].segs) L.h_fire.push_back(d);
     if (!L.h_fire.empty()) {
         GWO_TRY(ensure_buf(L.firedesc, L.h_fire.size() * sizeof(LogSegDesc)));
-        GWO_TRY(hipcheck(hipMemcpy(L.firedesc.ptr, L.h_fire.data(), L.h_fire.size() * sizeof(LogSegDesc),
-                                   hipMemcpyHostToDevice), "snapshot desc"));
+        GWO_TRY(hipcheck(hipMemcpyAsync(L.firedesc.ptr, L.h_fire.data(), L.h_fire.size() * sizeof(LogSegDesc),
+                                        hipMemcpyHostToDevice, stream), "fold desc"));
     }
     GWO_TRY(hipcheck(hipMemsetAsync(L.d_overflow, 0, 16, stream), "overflow"));
     size_t at = 0;
-    for (auto &kv : L.wins) {
-        LogWindow &W = kv.second;
-        const int64_t start = unit_start(kv.first);
+    for (long long u : units) {
+        LogWindow &W = L.wins[u];
+        const int64_t start = unit_start(u);
         const int64_t end = (int64_t)((uint64_t)start + (uint64_t)cfg.size);
         launch_log_fire((const LogSegDesc *)L.firedesc.ptr + at, (int)W.segs.size(), W.lp, needs_value, plan, raw, start,
                         end, o, L.d_overflow, L.max_groups, 2, 1, W.partial, stream);
-        GWO_TRY(launch_ok("log snapshot"));
+        GWO_TRY(launch_ok("log fold"));
         at += W.segs.size();
     }
     GWO_TRY(hipcheck(hipMemcpyAsync(L.h_fire_out + 1, L.d_overflow, 16, hipMemcpyDeviceToHost, stream), "overflow"));
-    GWO_TRY(hipcheck(hipStreamSynchronize(stream), "log snapshot"));
-    if (L.h_fire_out[1]) return poison(GWO_ERR_CAPACITY, "log snapshot: a partition overflowed its LDS table");
+    GWO_TRY(hipcheck(hipStreamSynchronize(stream), "log fold"));
+    if (L.h_fire_out[1]) return poison(GWO_ERR_CAPACITY, "log fold: a partition overflowed its LDS table");
     return GWO_OK;
+}
+
+// Checkpoint rows of every collecting window (fire timers pending: a log window leaves the log at its fire).
+gwo_status Handle::log_snapshot_collect(const SnapCols &c) {
+    std::vector<long long> units;
+    for (auto &kv : logst->wins) units.push_back(kv.first);
+    return log_fold_raw(units, c);
+}
+
+// allowedLateness > 0: window u, due to fire, leaves the log for a hash table (its state, one entry per key),
+// where the table path emits it, re-fires it for late records and clears it at its cleanup time.
+gwo_status Handle::log_migrate(long long u) {
+    LogState &L = *logst;
+    LogWindow &W = L.wins[u];
+    const uint64_t bound = W.records + W.partial_rows;
+    if (bound > 0 && (!W.segs.empty() || W.partial.rec)) {
+        const int NW = plan.nwords;
+        DevBuf b[3 + GWO_MAX_WORDS];
+        for (int i = 0; i < 3 + NW; ++i) GWO_TRY(ensure_buf(b[i], (size_t)bound * 8));
+        SnapCols c{};
+        c.key = (int64_t *)b[0].ptr;
+        c.start = (int64_t *)b[1].ptr;
+        c.end = (int64_t *)b[2].ptr;
+        for (int w = 0; w < NW; ++w) c.w[w] = (int64_t *)b[3 + w].ptr;
+        c.count = d_scratch_count;
+        c.cap = (long long)bound;
+        GWO_TRY(hipcheck(hipMemsetAsync(d_scratch_count, 0, 8, stream), "migrate count"));
+        GWO_TRY(log_fold_raw({u}, c));
+        GWO_TRY(hipcheck(hipMemcpyAsync(h_scalar, d_scratch_count, 8, hipMemcpyDeviceToHost, stream), "migrate count"));
+        GWO_TRY(hipcheck(hipStreamSynchronize(stream), "migrate count"));
+        const int64_t n = (int64_t)*h_scalar;
+        if (n > (int64_t)bound) return poison(GWO_ERR_HIP, "log migrate: more keys than records");
+        if (n > 0) {
+            GWO_TRY(ensure_table(u, (uint64_t)n));
+            launch_table_load(c, n, desc(tables[u]), plan, stream);
+            GWO_TRY(launch_ok("log migrate"));
+            tables[u].dirty = true;
+        }
+        GWO_TRY(hipcheck(hipStreamSynchronize(stream), "log migrate"));
+        for (auto &x : b) x.release();
+    }
+    log_release(L.wins[u]);
+    L.wins.erase(u);
+    return read_occupancy();
 }
 
 // Restored rows of a window become that window's partial-accumulator segment: records of (key, raw words)
 // grouped by partition (top lp bits of digit_hash, as every later batch's segments), folded into the window's
 // rows at its fire.
+// Rows of windows that already fired (timer flag 0: kept for allowedLateness) go to hash tables, as
+// log_migrate leaves them.
 gwo_status Handle::log_restore_rows(const RestoreRows &R, int64_t new_wm) {
     LogState &L = *logst;
     std::map<long long, std::vector<int64_t>> rows_of;
+    std::map<long long, int> kinds;   // bit 0: rows with a pending fire timer, bit 1: rows already emitted
+    std::vector<int64_t> fired;
     for (int64_t i = 0; i < R.n; ++i) {
         if (!R.mine[i]) continue;
         const __int128 a = (__int128)R.start[i] - (__int128)geom.unit_off_mod;
@@ -975,10 +1059,32 @@ gwo_status Handle::log_restore_rows(const RestoreRows &R, int64_t new_wm) {
         const long long u = (long long)q;
         if (unit_start(u) != R.start[i])
             return fail(GWO_ERR_INVALID_ARGUMENT, "restore: %lld is not a window start", (long long)R.start[i]);
-        if (!R.timer.empty() && R.timer[i] == 0)
-            return fail(GWO_ERR_UNSUPPORTED, "restore: the log layout holds no already emitted windows "
-                                             "(allowedLateness 0); use the table layout");
-        rows_of[u].push_back(i);
+        if (!R.timer.empty() && R.timer[i] == 0) {
+            fired.push_back(i);
+            kinds[u] |= 2;
+        } else {
+            rows_of[u].push_back(i);
+            kinds[u] |= 1;
+        }
+    }
+    for (auto &kv : kinds)
+        if (kv.second == 3)
+            return fail(GWO_ERR_UNSUPPORTED, "restore: window %lld has rows already emitted and rows still pending "
+                                             "(checkpoints taken at different watermarks)",
+                        (long long)unit_start(kv.first));
+    if (!fired.empty()) {
+        RestoreRows T;
+        T.n = (int64_t)fired.size();
+        T.nw = R.nw;
+        for (int64_t i : fired) {
+            T.key.push_back(R.key[i]);
+            T.start.push_back(R.start[i]);
+            T.end.push_back(R.end[i]);
+            T.timer.push_back(0);
+            T.words.insert(T.words.end(), R.words.begin() + (size_t)i * R.nw, R.words.begin() + (size_t)(i + 1) * R.nw);
+        }
+        T.mine.assign(T.n, 1);
+        GWO_TRY(table_restore_rows(T, new_wm));
     }
     wm = new_wm;
     const int RW = 1 + plan.nwords;

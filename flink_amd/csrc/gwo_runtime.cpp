@@ -401,8 +401,10 @@ gwo_status Handle::refire_rows(const int64_t *k, const int64_t *t, const int64_t
     return GWO_OK;
 }
 
-gwo_status Handle::insert_windowed(const int64_t *k, const int64_t *t, const int64_t *v, int64_t n) {
-    WindowGeom g = geom_now();
+gwo_status Handle::insert_windowed(const int64_t *k, const int64_t *t, const int64_t *v, int64_t n,
+                                   const WindowGeom *at) {
+    WindowGeom g = at ? *at : geom_now();
+    const bool count_late = !g.refire_only;   // a refire_only pass: the log's K1 did the late accounting
     // re-fire records (allowedLateness > 0) are emitted per element and inserted
     g.refire_ok = 1;
     uint64_t refire_total = 0;
@@ -416,8 +418,8 @@ gwo_status Handle::insert_windowed(const int64_t *k, const int64_t *t, const int
         init_stats(hist_base);
         prof_begin(GWO_KERNEL_SCAN);
         launch_scan(k, t, n, g, hist_base, d_stats, (int64_t *)side_key.ptr, (int64_t *)side_ts.ptr,
-                    (int64_t *)side_val.ptr, v, d_side_count, first_pass && side_enabled() ? side_cap : 0,
-                    first_pass && side_enabled(), stream);
+                    (int64_t *)side_val.ptr, v, d_side_count, first_pass && count_late && side_enabled() ? side_cap : 0,
+                    first_pass && count_late && side_enabled(), stream);
         GWO_TRY(launch_ok("scan"));
         prof_end(GWO_KERNEL_SCAN, n);
         GWO_TRY(hipcheck(hipMemcpyAsync(h_stats, d_stats, sizeof(BatchStats), hipMemcpyDeviceToHost, stream), "stats"));
@@ -435,7 +437,9 @@ gwo_status Handle::insert_windowed(const int64_t *k, const int64_t *t, const int
                                             "sliding windows: timestamp < offset - slide (Java '%' quirk range) is "
                                             "outside the pane restatement");
             refire_total = hs.refire;
-            if (side_enabled()) {
+            if (!count_late) {
+                // late records were counted (or side-output) by the log's K1
+            } else if (side_enabled()) {
                 GWO_TRY(hipcheck(hipMemcpyAsync(h_scalar, d_side_count, 8, hipMemcpyDeviceToHost, stream), "side count"));
                 GWO_TRY(hipcheck(hipStreamSynchronize(stream), "side count sync"));
                 side_rows = *h_scalar;

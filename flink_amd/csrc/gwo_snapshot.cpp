@@ -74,9 +74,14 @@ gwo_status Handle::snapshot(const gwo_state_rows *rows, int64_t cap, int64_t *n_
     GWO_TRY(hipcheck(hipMemsetAsync(d_scratch_count, 0, 8, stream), "snapshot count"));
     if (sess) {
         GWO_TRY(session_snapshot_collect(c));
-    } else if (logst) {
-        GWO_TRY(log_snapshot_collect(c));
     } else {
+        if (logst) {   // collecting windows: fire timers pending; then any fired windows kept in tables
+            GWO_TRY(log_snapshot_collect(c));
+            GWO_TRY(hipcheck(hipMemcpyAsync(h_scalar, d_scratch_count, 8, hipMemcpyDeviceToHost, stream), "snapshot count"));
+            GWO_TRY(hipcheck(hipStreamSynchronize(stream), "snapshot count"));
+            const int64_t n_log = std::min<int64_t>((int64_t)*h_scalar, (int64_t)m);
+            if (n_log > 0) launch_snap_fill_i32(c.timer, n_log, 1, stream);
+        }
         for (auto &kv : tables) {
             const int64_t start = unit_start(kv.first);
             const int64_t span = slide ? geom.unit : cfg.size;   // sliding rows carry their pane
@@ -93,7 +98,6 @@ gwo_status Handle::snapshot(const gwo_state_rows *rows, int64_t cap, int64_t *n_
     if (n > (int64_t)m) return poison(GWO_ERR_HIP, "snapshot: more rows than the state holds");
     if (n > cap) return fail(GWO_ERR_CAPACITY, "snapshot: %lld rows, buffer holds %lld", (long long)n, (long long)cap);
     if (n == 0) return GWO_OK;
-    if (logst) launch_snap_fill_i32(c.timer, n, 1, stream);   // log windows are never fired (released at the fire)
     // key groups, then a stable radix sort by key group (KeyGroupRangeAssignment.java:60-73)
     DevBuf kg, k1, v1, k2, v2, hist, ok, os, oe, ow, okg, ot;
     GWO_TRY(ensure_buf(kg, (size_t)n * 4));

@@ -143,6 +143,21 @@ __global__ __launch_bounds__(256) void sess_restore_wide_kernel(const int64_t *k
     }
 }
 
+// Rows (SoA, one per key) folded into a window's hash table: the log layout hands a fired window that must
+// stay until its cleanup time (allowedLateness > 0) to the table path this way.
+__global__ __launch_bounds__(256) void table_load_kernel(SnapCols c, int64_t n, TableDesc t, AccPlan p) {
+    const int64_t step = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t j0 = (int64_t)blockIdx.x * blockDim.x; j0 < n; j0 += step) {
+        const int64_t j = j0 + threadIdx.x;
+        bool claimed = false;
+        if (j < n) {
+            int64_t *acc = find_or_insert(t, p.stride, c.key[j], claimed);
+            for (int w = 0; w < p.nwords; ++w) atomic_combine(acc + w, p.op[w], c.w[w][j]);
+        }
+        count_claims(t.occ, claimed);
+    }
+}
+
 static inline int snap_grid(int64_t n) {
     int64_t g = (n + 255) / 256;
     return (int)(g < 1 ? 1 : (g > 4096 ? 4096 : g));
@@ -171,6 +186,10 @@ void launch_snap_gather(const SnapCols &c, const uint32_t *perm, const uint32_t 
                         hipStream_t s) {
     hipLaunchKernelGGL(snap_gather_kernel, dim3(snap_grid(n)), dim3(256), 0, s, c, perm, kg_sorted, n, nw, key, start,
                        end, words, kg, timer);
+}
+
+void launch_table_load(const SnapCols &c, int64_t n, const TableDesc &t, const AccPlan &p, hipStream_t s) {
+    hipLaunchKernelGGL(table_load_kernel, dim3(snap_grid(n)), dim3(256), 0, s, c, n, t, p);
 }
 
 void launch_snap_fill_i32(int32_t *p, int64_t n, int32_t v, hipStream_t s) {
