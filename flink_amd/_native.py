@@ -12,7 +12,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # GWO_LIB_PATH selects an alternative build of the same library (A/B kernel experiments)
 LIB_PATH = os.environ.get("GWO_LIB_PATH") or os.path.join(_HERE, "libgwo.so")
 
-GWO_ABI_VERSION = 3
+GWO_ABI_VERSION = 4
 GWO_MAX_AGGS = 4
 
 # gwo_status
@@ -26,7 +26,7 @@ globals().update({name: code for code, name in STATUS_NAMES.items()})
 ASSIGNER_TUMBLING, ASSIGNER_SLIDING, ASSIGNER_SESSION = 0, 1, 2
 AGG_COUNT, AGG_SUM, AGG_MIN, AGG_MAX, AGG_AVG = 0, 1, 2, 3, 4
 DTYPE_INT64, DTYPE_FLOAT64 = 0, 1
-KEY_LONG, KEY_INT = 0, 1
+KEY_LONG, KEY_INT, KEY_STRING = 0, 1, 2
 STATE_AUTO, STATE_TABLE, STATE_LOG = 0, 1, 2
 KERNEL_SCAN, KERNEL_INSERT, KERNEL_FIRE, KERNEL_PARTITION, KERNEL_EXCHANGE, KERNEL_SLIDE, KERNEL_SESSION = range(7)
 COMM_ID_BYTES = 128
@@ -75,6 +75,9 @@ SIGNATURES = [
     ("gwo_create", C.c_int, [C.POINTER(GwoConfig), C.POINTER(_P)]),
     ("gwo_destroy", C.c_int, [_P]),
     ("gwo_submit", C.c_int, [_P, _P, _P, _P, C.c_int64]),
+    ("gwo_submit_utf16", C.c_int, [_P, _P, _P, _P, _P, C.c_int64]),
+    ("gwo_intern_utf16", C.c_int, [_P, _P, _P, C.c_int64, _P]),
+    ("gwo_key_strings", C.c_int, [_P, _P, C.c_int64, _P, _P, C.c_int64, _I64P]),
     ("gwo_advance_watermark", C.c_int, [_P, C.c_int64]),
     ("gwo_end_input", C.c_int, [_P]),
     ("gwo_output_count", C.c_int, [_P, _I64P]),

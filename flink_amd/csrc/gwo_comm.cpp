@@ -187,6 +187,9 @@ extern "C" gwo_status gwo_comm_init(gwo_handle *hh, const uint8_t *id, int32_t n
     if (!h || !id || nranks < 1 || nranks > 256 || rank < 0 || rank >= nranks) return GWO_ERR_INVALID_ARGUMENT;
     if (h->poisoned) return h->poison_status;
     if (h->comm) return h->fail(GWO_ERR_STATE, "communicator already initialised");
+    if (h->cfg.key_kind == GWO_KEY_STRING)   // ids are per handle: the exchange would have to ship the Strings
+        return h->fail(GWO_ERR_UNSUPPORTED, "the multi-GPU exchange carries int64 keys; route String keys on the host "
+                                            "(gwo_assign_key_groups_utf16) and submit per GPU");
     DeviceGuard guard_(h->cfg.device);
     const int maxp = h->cfg.max_parallelism;
     if (nranks > maxp) return h->fail(GWO_ERR_INVALID_ARGUMENT, "Maximum parallelism must not be smaller than parallelism.");

@@ -40,7 +40,8 @@ gwo_status Handle::init(const gwo_config &c) {
         return fail(GWO_ERR_INVALID_ARGUMENT, "maxParallelism must be in (0, 32768]");
     if (c.key_group_start < 0 || c.key_group_end >= c.max_parallelism || c.key_group_start > c.key_group_end)
         return fail(GWO_ERR_INVALID_ARGUMENT, "invalid KeyGroupRange [%d, %d]", c.key_group_start, c.key_group_end);
-    if (c.key_kind != GWO_KEY_LONG && c.key_kind != GWO_KEY_INT) return fail(GWO_ERR_UNSUPPORTED, "key kind %d", c.key_kind);
+    if (c.key_kind != GWO_KEY_LONG && c.key_kind != GWO_KEY_INT && c.key_kind != GWO_KEY_STRING)
+        return fail(GWO_ERR_UNSUPPORTED, "key kind %d", c.key_kind);
     if (c.value_dtype != GWO_DTYPE_INT64 && c.value_dtype != GWO_DTYPE_FLOAT64)
         return fail(GWO_ERR_UNSUPPORTED, "value dtype %d", c.value_dtype);
     if (c.num_aggs < 1 || c.num_aggs > GWO_MAX_AGGS) return fail(GWO_ERR_INVALID_ARGUMENT, "num_aggs must be 1..4");
@@ -171,6 +172,7 @@ Handle::~Handle() {
     log_free();
     session_free();
     slide_free();
+    dict_free();
     for (auto &kv : tables) (void)hipFree(kv.second.base);
     for (auto &t : aux_tables) (void)hipFree(t.base);
     trim_pool();

@@ -30,6 +30,7 @@ struct RestoreRows {
 };
 
 const char *status_str(gwo_status s);
+bool is_device_ptr(const void *p);   // NULL counts as device (nothing to stage)
 
 struct DeviceGuard {
     int prev = -1;
@@ -81,6 +82,7 @@ struct Comm;           // gwo_comm.cpp
 struct LogState;       // gwo_log.cpp
 struct LogWindow;
 struct LogJob;
+struct StrDict;        // gwo_strings.cpp
 
 struct Handle {
     static constexpr double kMaxLoad = 0.7;   // grow above this load factor
@@ -160,6 +162,7 @@ struct Handle {
     SlideState *slide = nullptr;
     Comm *comm = nullptr;
     LogState *logst = nullptr;                 // non-null: log-structured tumbling state
+    StrDict *dict = nullptr;                   // String keys: the key dictionary (gwo_strings.cpp)
 
     ~Handle();
     gwo_status init(const gwo_config &c);
@@ -175,6 +178,12 @@ struct Handle {
     gwo_status snapshot(const gwo_state_rows *rows, int64_t cap, int64_t *n_out);
     gwo_status restore(const gwo_state_rows *rows, int32_t n_words, int64_t n, int64_t new_wm);
     gwo_status table_restore_rows(const RestoreRows &R, int64_t new_wm);
+
+    // String keys (gwo_strings.cpp)
+    gwo_status intern_utf16(const uint16_t *chars, const int64_t *offsets, int64_t n, const int64_t **ids);
+    gwo_status key_strings(const int64_t *ids, int64_t n, int64_t *offsets_out, uint16_t *chars_out,
+                           int64_t chars_cap, int64_t *chars_needed);
+    void dict_free();
 
     gwo_status fail(gwo_status s, const char *fmt, ...);
     gwo_status poison(gwo_status s, const char *what);

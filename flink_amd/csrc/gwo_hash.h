@@ -10,8 +10,10 @@ namespace gwo {
 __device__ __host__ inline int32_t long_hash_code(int64_t v) {  // JDK Long.hashCode
     return (int32_t)(uint32_t)((uint64_t)v ^ ((uint64_t)v >> 32));
 }
+// kind 0 Long, 1 Integer, 2 String: a String key travels as its dictionary id, whose high 32 bits are the
+// String.hashCode (gwo_strings.hip)
 __device__ __host__ inline int32_t key_hash_code(int64_t v, int kind) {
-    return kind == 1 ? (int32_t)v : long_hash_code(v);
+    return kind == 1 ? (int32_t)v : kind == 2 ? (int32_t)(uint32_t)((uint64_t)v >> 32) : long_hash_code(v);
 }
 __device__ __host__ inline int32_t bit_mix(int32_t in) {  // MathUtils.java:191-198
     uint32_t x = (uint32_t)in;

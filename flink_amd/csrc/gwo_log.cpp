@@ -734,7 +734,7 @@ gwo_status Handle::insert_log(const int64_t *k, const int64_t *t, const int64_t 
     // by the next batch -- and without a side output (K1 appends to it on the first pass).
     // With allowedLateness > 0 a batch resolves before the next watermark: its re-fire records must reach the
     // fired windows' tables before a watermark cleans them up.
-    const bool pipe = L.pipeline && cfg.allowed_lateness == 0 && stride == 1 && !side_enabled() && !comm &&
+    const bool pipe = L.pipeline && cfg.allowed_lateness == 0 && stride == 1 && !side_enabled() && !comm && !dict &&
                       (const void *)k != stage_key.ptr &&
                       (const void *)t != stage_ts.ptr && (!v || (const void *)v != stage_val.ptr);
     if (L.job.active && !pipe) GWO_TRY(log_flush());

@@ -305,7 +305,7 @@ gwo_status Handle::prof_collect() {
 }
 
 // ---- input staging ----------------------------------------------------------------------------
-static bool is_device_ptr(const void *p) {
+bool is_device_ptr(const void *p) {
     if (!p) return true;
     hipPointerAttribute_t attr;
     if (hipPointerGetAttributes(&attr, p) != hipSuccess) {
@@ -666,6 +666,35 @@ gwo_status gwo_submit(gwo_handle *hh, const int64_t *key, const int64_t *ts, con
     if (n > 0 && (!key || !ts)) return h->fail(GWO_ERR_INVALID_ARGUMENT, "key/ts columns are required");
     if (n > 0 && !value && h->needs_value) return h->fail(GWO_ERR_INVALID_ARGUMENT, "value column required");
     return h->submit(key, ts, value, n);
+}
+
+gwo_status gwo_submit_utf16(gwo_handle *hh, const uint16_t *chars, const int64_t *offsets, const int64_t *ts,
+                            const void *value, int64_t n) {
+    H_OR_FAIL;
+    if (n < 0) return h->fail(GWO_ERR_INVALID_ARGUMENT, "negative record count");
+    if (n == 0) return GWO_OK;
+    if (!offsets || !ts) return h->fail(GWO_ERR_INVALID_ARGUMENT, "offsets/ts columns are required");
+    if (!value && h->needs_value) return h->fail(GWO_ERR_INVALID_ARGUMENT, "value column required");
+    const int64_t *ids = nullptr;
+    GWO_TRY(h->intern_utf16(chars, offsets, n, &ids));
+    return h->submit(ids, ts, value, n);
+}
+
+gwo_status gwo_intern_utf16(gwo_handle *hh, const uint16_t *chars, const int64_t *offsets, int64_t n,
+                            int64_t *ids_out) {
+    H_OR_FAIL;
+    if (n < 0 || (n > 0 && (!offsets || !ids_out))) return h->fail(GWO_ERR_INVALID_ARGUMENT, "intern arguments");
+    if (n == 0) return GWO_OK;
+    const int64_t *ids = nullptr;
+    GWO_TRY(h->intern_utf16(chars, offsets, n, &ids));
+    return h->hipcheck(hipMemcpy(ids_out, ids, (size_t)n * 8, hipMemcpyDefault), "intern ids");
+}
+
+gwo_status gwo_key_strings(gwo_handle *hh, const int64_t *ids, int64_t n, int64_t *offsets_out, uint16_t *chars_out,
+                           int64_t chars_cap, int64_t *chars_needed) {
+    H_OR_FAIL;
+    if (n < 0 || !offsets_out || (n > 0 && !ids)) return h->fail(GWO_ERR_INVALID_ARGUMENT, "key_strings arguments");
+    return h->key_strings(ids, n, offsets_out, chars_out, chars_cap, chars_needed);
 }
 
 gwo_status gwo_advance_watermark(gwo_handle *hh, int64_t wm) {

@@ -68,19 +68,33 @@ def assign_key_groups(keys, max_parallelism: int, parallelism: int = 1, key_kind
     return kg, op
 
 
+def encode_utf16(keys):
+    """Strings -> (UTF-16 code units, int64 offsets): the columnar form a host hands over (a Java String's
+    chars; lone surrogates pass through as code units, as in Java)."""
+    enc = [k.encode("utf-16-le", "surrogatepass") for k in keys]
+    offsets = np.zeros(len(enc) + 1, np.int64)
+    if enc:
+        offsets[1:] = np.cumsum([len(b) // 2 for b in enc])
+    chars = np.frombuffer(b"".join(enc), dtype=np.uint16).copy() if offsets[-1] else np.zeros(1, np.uint16)
+    return chars, offsets
+
+
+def decode_utf16(chars, offsets):
+    b = np.ascontiguousarray(chars, np.uint16).tobytes()
+    return [b[2 * offsets[i]:2 * offsets[i + 1]].decode("utf-16-le", "surrogatepass") for i in range(len(offsets) - 1)]
+
+
 def assign_key_groups_strings(keys, max_parallelism: int, parallelism: int = 1, device: int = 0):
     """GPU kernel: String.hashCode (UTF-16 code units), key groups and operator indices of String keys.
     The strings are packed as one UTF-16 code-unit array plus int64 offsets (the columnar form a host
     would hand over)."""
-    units = [np.frombuffer(k.encode("utf-16-le"), dtype=np.uint16) for k in keys]
-    offsets = np.zeros(len(units) + 1, np.int64)
-    offsets[1:] = np.cumsum([len(u) for u in units])
-    chars = np.concatenate(units) if offsets[-1] else np.zeros(1, np.uint16)
-    h = np.empty(len(units), np.int32)
-    kg = np.empty(len(units), np.int32)
-    op = np.empty(len(units), np.int32)
+    chars, offsets = encode_utf16(keys)
+    n = len(offsets) - 1
+    h = np.empty(n, np.int32)
+    kg = np.empty(n, np.int32)
+    op = np.empty(n, np.int32)
     P = lambda a: a.ctypes.data_as(C.c_void_p)
-    st = N.lib().gwo_assign_key_groups_utf16(P(chars), P(offsets), len(units), max_parallelism, parallelism, P(h),
+    st = N.lib().gwo_assign_key_groups_utf16(P(chars), P(offsets), n, max_parallelism, parallelism, P(h),
                                              P(kg), P(op), device)
     N.check(st, None, "gwo_assign_key_groups_utf16")
     return h, kg, op

@@ -14,6 +14,7 @@ import ctypes as C
 import numpy as np
 
 from . import _native as N
+from .keygroups import decode_utf16, encode_utf16
 from .windowing import AggregateFunction, WindowAssigner
 
 LONG_MIN = -(1 << 63)
@@ -47,7 +48,13 @@ class GpuWindowOperator:
         for i, k in enumerate(kinds):
             cfg.aggs[i] = k
         cfg.value_dtype = vdt
-        cfg.key_kind = N.KEY_INT if key_kind == "int" else N.KEY_LONG
+        kinds_ = {"long": N.KEY_LONG, "int": N.KEY_INT, "string": N.KEY_STRING}
+        if key_kind not in kinds_:
+            raise ValueError(f"key_kind must be one of {sorted(kinds_)}")
+        cfg.key_kind = kinds_[key_kind]
+        # String keys (KeyGroupRangeAssignment over String.hashCode): the handle interns them into its device
+        # dictionary; rows come back keyed by the Strings (gwo.h gwo_submit_utf16 / gwo_key_strings)
+        self._strings = key_kind == "string"
         cfg.max_parallelism = max_parallelism
         lo, hi = key_group_range if key_group_range is not None else (0, max_parallelism - 1)
         cfg.key_group_start, cfg.key_group_end = lo, hi
@@ -109,9 +116,9 @@ class GpuWindowOperator:
             self.flush()
 
     def process_batch(self, keys, timestamps, values=None):
-        """Columnar batch in arrival order (numpy arrays; host memory)."""
+        """Columnar batch in arrival order (numpy arrays; host memory; String keys: a sequence of str)."""
         self.flush()
-        k = np.ascontiguousarray(keys, dtype=np.int64)
+        k = list(keys) if self._strings else np.ascontiguousarray(keys, dtype=np.int64)
         t = np.ascontiguousarray(timestamps, dtype=np.int64)
         v = None if values is None else np.ascontiguousarray(values, dtype=self.value_dtype)
         self._submit(k, t, v)
@@ -126,13 +133,38 @@ class GpuWindowOperator:
     def _submit(self, k, t, v):
         if len(k) == 0:
             return
+        if self._strings:
+            chars, offsets = encode_utf16(k)
+            st = self._lib.gwo_submit_utf16(self._h, _ptr(chars), _ptr(offsets), _ptr(t), _ptr(v), len(k))
+            N.check(st, self._h, "gwo_submit_utf16")
+            return
         st = self._lib.gwo_submit(self._h, _ptr(k), _ptr(t), _ptr(v), len(k))
         N.check(st, self._h, "gwo_submit")
+
+    def key_strings(self, ids):
+        """Dictionary ids (output / side-output / checkpoint key column of a String-keyed handle) -> Strings."""
+        ids = np.ascontiguousarray(ids, dtype=np.int64)
+        n = len(ids)
+        off = np.empty(n + 1, np.int64)
+        need = C.c_int64()
+        N.check(self._lib.gwo_key_strings(self._h, _ptr(ids), n, _ptr(off), None, 0, C.byref(need)), self._h)
+        chars = np.empty(max(need.value, 1), np.uint16)
+        N.check(self._lib.gwo_key_strings(self._h, _ptr(ids), n, _ptr(off), _ptr(chars), need.value, C.byref(need)),
+                self._h)
+        return decode_utf16(chars, off)
+
+    def intern_strings(self, keys):
+        """Strings -> this handle's dictionary ids."""
+        chars, offsets = encode_utf16(keys)
+        ids = np.empty(max(len(keys), 1), np.int64)
+        N.check(self._lib.gwo_intern_utf16(self._h, _ptr(chars), _ptr(offsets), len(keys), _ptr(ids)), self._h,
+                "gwo_intern_utf16")
+        return ids[:len(keys)]
 
     def flush(self):
         if not self._pk:
             return
-        k = np.array(self._pk, dtype=np.int64)
+        k = list(self._pk) if self._strings else np.array(self._pk, dtype=np.int64)
         t = np.array(self._pt, dtype=np.int64)
         v = np.array(self._pv, dtype=self.value_dtype)
         self._pk, self._pt, self._pv = [], [], []
@@ -160,9 +192,10 @@ class GpuWindowOperator:
         if n.value:
             cols = self.drain_arrays()
             keys, starts, ends, res = cols
+            ks = self.key_strings(keys) if self._strings else [int(x) for x in keys]
             for i in range(len(keys)):
                 r = tuple(x[i].item() for x in res)
-                self.output.append((int(keys[i]), int(starts[i]), int(ends[i]), r[0] if len(r) == 1 else r))
+                self.output.append((ks[i], int(starts[i]), int(ends[i]), r[0] if len(r) == 1 else r))
         sn = C.c_int64()
         N.check(self._lib.gwo_side_output_count(self._h, C.byref(sn)), self._h)
         if sn.value:
@@ -173,8 +206,9 @@ class GpuWindowOperator:
             so = N.GwoSideOut(_ptr(k).value, _ptr(t).value, _ptr(v).value)
             got = C.c_int64()
             N.check(self._lib.gwo_drain_side_output(self._h, C.byref(so), m, C.byref(got)), self._h)
+            ks = self.key_strings(k[:got.value]) if self._strings else [int(x) for x in k[:got.value]]
             for i in range(got.value):
-                self.side_output.append((int(k[i]), int(t[i]), v[i].item()))
+                self.side_output.append((ks[i], int(t[i]), v[i].item()))
 
     def drain_arrays(self):
         """Drain pending fired rows into numpy columns: (key, start, end, [results...])."""
@@ -225,6 +259,8 @@ class GpuWindowOperator:
                 "gwo_snapshot")
         g = got.value
         out = {c: v[:g] for c, v in cols.items()}
+        if self._strings:   # checkpoints carry the Strings: dictionary ids are private to a handle
+            out["key"] = np.array(self.key_strings(out["key"]), dtype=object)
         out["watermark"] = wm.value
         return out
 
@@ -245,7 +281,11 @@ class GpuWindowOperator:
                 raise N.GwoError(N.GWO_ERR_UNSUPPORTED, "sliding-window snapshots taken at watermarks that straddle a "
                                  "window end cannot be restored together")
         cat = lambda c, dt: np.ascontiguousarray(np.concatenate([x[c] for x in snaps]), dtype=dt)
-        key, start, end = cat("key", np.int64), cat("window_start", np.int64), cat("window_end", np.int64)
+        if self._strings:
+            key = self.intern_strings([k for x in snaps for k in x["key"]])
+        else:
+            key = cat("key", np.int64)
+        start, end = cat("window_start", np.int64), cat("window_end", np.int64)
         timer = cat("timer", np.int32)
         words = np.ascontiguousarray(np.concatenate([x["words"] for x in snaps]), dtype=np.int64)
         nw = words.shape[1] if words.ndim == 2 else 0

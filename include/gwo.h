@@ -52,7 +52,7 @@
 extern "C" {
 #endif
 
-#define GWO_ABI_VERSION 3
+#define GWO_ABI_VERSION 4
 #define GWO_MAX_AGGS 4
 
 typedef enum {
@@ -94,7 +94,9 @@ typedef enum {
 
 typedef enum {
     GWO_KEY_LONG = 0,             /* key.hashCode() = Long.hashCode: (int)(v ^ (v >>> 32)) */
-    GWO_KEY_INT = 1               /* key.hashCode() = Integer.hashCode: (int)v; key must fit in int32 */
+    GWO_KEY_INT = 1,              /* key.hashCode() = Integer.hashCode: (int)v; key must fit in int32 */
+    GWO_KEY_STRING = 2            /* java.lang.String keys: gwo_submit_utf16; inside the handle a key is its
+                                     dictionary id, (int64)String.hashCode << 32 | sequence number */
 } gwo_key_kind;
 
 typedef struct {
@@ -198,6 +200,25 @@ gwo_status gwo_sync(gwo_handle *h);
 gwo_status gwo_get_stream(gwo_handle *h, void **stream);
 const char *gwo_last_error(const gwo_handle *h);
 const char *gwo_status_string(gwo_status s);
+
+/* ---- String keys (key_kind GWO_KEY_STRING) -------------------------------------------------------------------
+ * The reference keys a String-keyed stream by the String itself: its key group is murmur(String.hashCode)
+ * (KeyGroupRangeAssignment.java:60-73) and the window state is keyed by the String.  Here every distinct String
+ * a handle sees is interned into a device-resident dictionary and the state is keyed by its id, whose high 32 bits
+ * are the JDK String.hashCode (so every key-group computation is the reference's) and whose low 32 bits number the
+ * handle's distinct keys.  Key i of a batch is the UTF-16 code units chars[offsets[i] .. offsets[i + 1]).
+ * Output rows, side-output rows and checkpoint rows carry ids; gwo_key_strings turns ids back into Strings (a
+ * checkpoint restored into another handle is re-keyed by interning its Strings there).  Host or device pointers.
+ * Interning is exact: two distinct Strings never share an id (a 64-bit fingerprint match is verified code unit by
+ * code unit; a true fingerprint collision rejects the batch with GWO_ERR_UNSUPPORTED). */
+gwo_status gwo_submit_utf16(gwo_handle *h, const uint16_t *chars, const int64_t *offsets, const int64_t *ts,
+                            const void *value, int64_t n);
+gwo_status gwo_intern_utf16(gwo_handle *h, const uint16_t *chars, const int64_t *offsets, int64_t n,
+                            int64_t *ids_out);
+/* offsets_out: n + 1 entries (host memory); chars_out may be NULL to query chars_needed (GWO_ERR_CAPACITY when
+ * chars_cap is too small).  An id the handle never issued: GWO_ERR_INVALID_ARGUMENT. */
+gwo_status gwo_key_strings(gwo_handle *h, const int64_t *ids, int64_t n, int64_t *offsets_out, uint16_t *chars_out,
+                           int64_t chars_cap, int64_t *chars_needed);
 
 /* Pipelined submission (off by default; log layout with caller-owned device columns and no side output --
  * other batches are resolved inside gwo_submit as usual).  gwo_submit queues the batch's partition kernel

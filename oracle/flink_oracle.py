@@ -81,7 +81,7 @@ def int_hash_code(v: int) -> int:
 def string_hash_code(s: str) -> int:
     """JDK ``String.hashCode``: ``h = 31*h + c`` over UTF-16 code units."""
     h = 0
-    data = s.encode("utf-16-le")
+    data = s.encode("utf-16-le", "surrogatepass")   # Java Strings may hold lone surrogates
     for i in range(0, len(data), 2):
         c = data[i] | (data[i + 1] << 8)
         h = i32(31 * h + c)
