@@ -121,6 +121,7 @@ gwo_status Handle::init(const gwo_config &c) {
     const char *pa = getenv("GWO_PREAGG");
     if (pa) cfg_preagg = atoi(pa) ? 1 : 0;
     if (cfg_preagg >= 0) use_preagg = cfg_preagg;
+    if (const char *cb = getenv("GWO_COMBINE")) use_combine = atoi(cb) ? 1 : 0;
 
     // ---- device resources ----
     if (hipSetDevice(c.device) != hipSuccess) return fail(GWO_ERR_HIP, "hipSetDevice(%d) failed", c.device);
@@ -185,6 +186,7 @@ Handle::~Handle() {
     if (h_ident_side) (void)hipHostFree(h_ident_side);
     dir_buf.release();
     refire_buf.release();
+    for (DevBuf *b : {&cb_dump_key, &cb_dump_acc, &cb_ovf, &cb_blk, &cb_ctr}) b->release();
     stage_key.release();
     stage_ts.release();
     stage_val.release();

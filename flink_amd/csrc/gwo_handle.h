@@ -142,6 +142,9 @@ struct Handle {
 
     // pre-aggregation policy
     int use_preagg = 1;
+    int use_combine = 1;                       // GWO_COMBINE=0: the two-pass scan + insert path only
+    int cb_cus = 0;
+    DevBuf cb_dump_key, cb_dump_acc, cb_ovf, cb_blk, cb_ctr;   // combine path scratch (insert_combined)
     int cfg_preagg = -1;                       // GWO_PREAGG env override: 0 / 1
     uint64_t batches = 0;
 
@@ -218,6 +221,7 @@ struct Handle {
     WindowGeom geom_now() const;
     gwo_status insert_windowed(const int64_t *k, const int64_t *t, const int64_t *v, int64_t n,
                                const WindowGeom *at = nullptr);
+    gwo_status insert_combined(const int64_t *k, const int64_t *t, const int64_t *v, int64_t n, bool *done);
     gwo_status refire_rows(const int64_t *k, const int64_t *t, const int64_t *v, int64_t n, const WindowGeom &g,
                            long long dir_base, int dir_len, uint64_t mmax);
     void adapt_preagg(uint64_t accepted, uint64_t partials);

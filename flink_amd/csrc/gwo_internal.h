@@ -77,6 +77,9 @@ struct BatchStats {
     unsigned long long partials;       // pre-aggregated partials flushed by the insert kernel
     unsigned long long hist_out;       // accepted records outside the histogram range
     unsigned long long hist[GWO_HIST_BINS];
+    unsigned long long distinct[2];    // combine path: (key, unit) entries of units hint, hint + 1 summed over
+                                       // workgroups (an upper bound of the keys the batch adds to each)
+    unsigned long long overflow;       // combine path: records left to the merge one by one
 };
 
 // Window geometry of the handle, kernel-parameter sized.
@@ -99,6 +102,28 @@ struct WindowGeom {
     int32_t kg_hi;
     int32_t refire_ok;                 // table passes: re-fire records are emitted + inserted
     int32_t refire_only;               // table pass over the log layout's fired windows: re-fire records only
+};
+
+// Combine path buffers (gwo_kernels.hip gather / merge): per-workgroup LDS table dumps, the records left to
+// the merge, per-workgroup statistics slots.
+struct CombineArgs {
+    int64_t *dump_key;                 // [G][2 * S]
+    int64_t *dump_acc;                 // [G][2 * S][nwords]
+    uint32_t *ovf;                     // record indices left to the merge
+    unsigned long long *ovf_count;     // reset by the gather's last workgroup
+    unsigned long long ovf_cap;
+    unsigned long long *blk;           // statistics shards (gather_stat_words(); min/max words preset)
+    unsigned long long *done;          // workgroups finished (reset by the last one)
+    int32_t S;                         // LDS slots per unit (power of two)
+    int32_t sbits;                     // log2(S)
+    long long hint;                    // units hint, hint + 1 fold in LDS; the histogram starts at hint
+    // tumbling: windows hint .. hint + 3 by comparisons -- starts bound[0..4], 2-bit class per window
+    // (0 accept, 1 every window late, 2 re-fire); thr_ok = 0: classify every record
+    int64_t bound[5];
+    uint32_t cls;
+    int32_t thr_ok;
+    int32_t full_range;                // the handle owns every key group: no per-record key-group check
+    int32_t pad;
 };
 
 // Output columns (SoA) in HBM.
@@ -177,6 +202,16 @@ void launch_refire_emit(const int64_t *key, const int64_t *val, const int64_t *r
                         const uint32_t *skey, const uint32_t *spay, const int64_t *before, const AccPlan &p,
                         const ResultPlan &rp, int64_t unit, int64_t unit_off_mod, int64_t span, OutCols o,
                         hipStream_t s);
+size_t gather_lds_bytes(int S, int nwords);
+int gather_tile();         // records per gather workgroup tile
+int gather_stat_words();   // statistics shard words (zeroed once; the gather leaves them reset)
+void launch_gather(const int64_t *key, const int64_t *ts, const int64_t *val, int64_t n, const WindowGeom &g,
+                   const AccPlan &p, const CombineArgs &a, int grid, BatchStats *st, int64_t *side_key, int64_t *side_ts,
+                   int64_t *side_val, unsigned long long *side_count, long long side_cap, int side_enabled,
+                   hipStream_t s);
+void launch_merge(const int64_t *key, const int64_t *ts, const int64_t *val, const WindowGeom &g, const AccPlan &p,
+                  const CombineArgs &a, int G, uint64_t novf, const TableDesc *dir, long long dir_base, int dir_len,
+                  const RingDesc &ring, hipStream_t s);
 void launch_slide_refire_slots(const int64_t *key, const int64_t *r_idx, const long long *r_u, int64_t m,
                                const AccPlan &p, const WindowGeom &g, unsigned long long *keytab, uint64_t kmask,
                                long long j0, uint32_t nj, const TableDesc *pdir, long long pane_base,

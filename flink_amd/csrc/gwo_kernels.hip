@@ -335,6 +335,325 @@ __global__ __launch_bounds__(256) void insert_preagg_kernel(const int64_t *__res
 }
 
 // ------------------------------------------------------------------------------------------------
+// Combine path (table layout, low-cardinality batches such as YSB's 1K campaigns): the scan and the
+// pre-aggregated insert as ONE pass over the records plus a merge, with the host's checks in between.
+//   gather  persistent workgroups: every record is classified (the scan's statistics, histogram, side
+//           output, key-group check) and folded into the workgroup's LDS table of units hint and hint + 1
+//           (key-indexed, accumulators preset to the identity, so a claim is one CAS of the key word); the
+//           table is then dumped densely per workgroup.  Records of other units, of a full table or with
+//           the empty-key marker are listed for the merge.  Statistics go to a per-workgroup slot and the
+//           last workgroup reduces them into BatchStats: device-scope atomics on one address serialise at
+//           ~12 ns each on MI355X (measured), so per-wave counter atomics cost more than the pass itself.
+//   merge   after the host accepted the batch (nothing changed before -- the reject-before-any-change rule
+//           holds): per dump slot and run of workgroups, entries of one key fold in registers into one
+//           find-or-insert + combine; then the listed records one by one.
+// ------------------------------------------------------------------------------------------------
+#define CB_NU 2
+#ifndef CB_THREADS
+#define CB_THREADS 1024
+#endif
+#ifndef CB_PER
+#define CB_PER 4
+#endif
+#define CB_TILE (CB_THREADS * CB_PER)
+#define CB_MERGE_RUN 8
+#define CB_SHARDS 16      // statistics shards (gather)
+#ifndef CB_XP
+#define CB_XP 0   // experiment ablations (exp/cbbench): 1 no LDS fold, 2 no tail, 4 no dump, 8 no key group
+#endif
+
+enum : int { CS_ACC = 0, CS_LATE, CS_REFIRE, CS_BADTS, CS_BADRANGE, CS_BADKG, CS_HOUT, CS_MIN, CS_MAX, CS_D0, CS_D1,
+             CS_HIST = 16, CS_WORDS = CS_HIST + GWO_HIST_BINS };
+
+__global__ __launch_bounds__(CB_THREADS) void gather_kernel(const int64_t *__restrict__ key,
+                                                            const int64_t *__restrict__ ts,
+                                                            const int64_t *__restrict__ val, int64_t n, WindowGeom g,
+                                                            AccPlan p, CombineArgs a, BatchStats *st, int64_t *side_key,
+                                                            int64_t *side_ts, int64_t *side_val,
+                                                            unsigned long long *side_count, long long side_cap,
+                                                            int side_enabled) {
+    extern __shared__ int64_t s_dyn[];
+    const int S = a.S, NW = p.nwords, tid = threadIdx.x;
+    int64_t *s_key = s_dyn;                     // [CB_NU * S]
+    int64_t *s_acc = s_dyn + CB_NU * S;         // [CB_NU * S * NW]
+    __shared__ unsigned s_hist[GWO_HIST_BINS];
+    __shared__ unsigned long long s_red[CB_THREADS / 64][CS_HIST];
+    for (int i = tid; i < CB_NU * S; i += CB_THREADS) s_key[i] = GWO_EMPTY_KEY;
+    for (int i = tid; i < CB_NU * S * NW; i += CB_THREADS) s_acc[i] = p.ident[i % NW];
+    if (tid < GWO_HIST_BINS) s_hist[tid] = 0;
+    __syncthreads();
+    unsigned acc = 0, late = 0, refire = 0, bad_ts = 0, bad_range = 0, bad_kg = 0, hout = 0;
+    long long mn = 0x7fffffffffffffffLL, mx = (long long)0x8000000000000000LL;
+    int run_b = -1;
+    unsigned run_n = 0;
+    for (int64_t tile = (int64_t)blockIdx.x * CB_TILE; tile < n; tile += (int64_t)gridDim.x * CB_TILE) {
+        unsigned ovm = 0;   // records of this tile left to the merge (bit j: record tile + j * CB_THREADS + tid)
+        int64_t tt[CB_PER], kk[CB_PER];   // the tile's loads all in flight before any record is processed
+#pragma unroll
+        for (int j = 0; j < CB_PER; ++j) {
+            int64_t i = tile + j * CB_THREADS + tid;
+            i = i < n ? i : tile;
+            tt[j] = __builtin_nontemporal_load(ts + i);
+            kk[j] = __builtin_nontemporal_load(key + i);
+        }
+#pragma unroll
+        for (int j = 0; j < CB_PER; ++j) {
+            const int64_t i = tile + j * CB_THREADS + tid;
+            if (i >= n) continue;
+            long long u = 0;
+            int c;
+            const int64_t tv = tt[j];
+            if (a.thr_ok && tv >= a.bound[0] && tv < a.bound[4]) {   // a window of the batch's range: compares
+                const int jj = (tv >= a.bound[1]) + (tv >= a.bound[2]) + (tv >= a.bound[3]);
+                const uint32_t cc = (a.cls >> (2 * jj)) & 3u;
+                c = cc == 0 ? REC_ACCEPT : (cc == 2 ? REC_REFIRE : (jadd(tv, g.lateness) <= g.wm ? REC_LATE : REC_SKIP));
+                u = a.hint + jj;
+            } else {
+                c = classify(tv, g, u);
+            }
+            if (c == REC_BAD_TS) {
+                bad_ts++;
+            } else if (c == REC_BAD_SLIDE) {
+                bad_range++;
+            } else if (c == REC_LATE) {
+                if (g.refire_only) continue;
+                late++;
+                if (side_enabled) {
+                    const unsigned long long pos = atomicAdd(side_count, 1ull);
+                    if ((long long)pos < side_cap) {
+                        side_key[pos] = key[i];
+                        side_ts[pos] = ts[i];
+                        side_val[pos] = val ? val[i] : 0;
+                    }
+                }
+            } else if (takes(c, g)) {
+                acc++;
+                refire += c == REC_REFIRE;
+                const int64_t k = kk[j];
+                const int32_t kg = ((CB_XP & 8) || a.full_range) ? g.kg_lo : key_group(k, g.key_kind, g.max_par);
+                if (kg < g.kg_lo || kg > g.kg_hi) {
+                    bad_kg++;
+                    atomicExch((unsigned long long *)&st->bad_kg_key, (unsigned long long)k);
+                }
+                mn = u < mn ? u : mn;
+                mx = u > mx ? u : mx;
+                const long long b = u - a.hint;
+                if (b >= 0 && b < GWO_HIST_BINS) {   // run-length histogram: a batch's records share few units
+                    if ((int)b != run_b) {
+                        if (run_n) atomicAdd(&s_hist[run_b], run_n);
+                        run_b = (int)b;
+                        run_n = 0;
+                    }
+                    run_n++;
+                } else {
+                    hout++;
+                }
+                bool placed = (CB_XP & 1) != 0;
+                if (!placed && b >= 0 && b < CB_NU && k != GWO_EMPTY_KEY) {
+                    int64_t *kb = s_key + b * S;
+                    // LDS slot: two 32-bit multiplies (the table is private to this pass; any spread will do)
+                    uint32_t sl = ((uint32_t)k * 0x9E3779B1u ^ (uint32_t)((uint64_t)k >> 32) * 0x85EBCA77u) >>
+                                  (32 - a.sbits);
+                    for (int probe = 0; probe < 32; ++probe) {
+                        int64_t cur = kb[sl];
+                        if (cur == GWO_EMPTY_KEY) {
+                            cur = (int64_t)atomicCAS((unsigned long long *)&kb[sl], (unsigned long long)GWO_EMPTY_KEY,
+                                                     (unsigned long long)k);
+                            if (cur == GWO_EMPTY_KEY) cur = k;
+                        }
+                        if (cur == k) {
+                            const int64_t v = val ? val[i] : 0;
+                            int64_t *dst = s_acc + ((size_t)b * S + sl) * NW;
+                            for (int w = 0; w < NW; ++w) lds_combine(dst + w, p.op[w], lift_word(p, w, v));
+                            placed = true;
+                            break;
+                        }
+                        sl = (sl + 1) & (uint32_t)(S - 1);
+                    }
+                }
+                if (!placed) ovm |= 1u << j;
+            }
+        }
+        // the tile's listed records: one reservation per workgroup
+        unsigned long long at = block_reserve((unsigned)__popc(ovm), a.ovf_count);
+        for (int j = 0; j < CB_PER; ++j)
+            if ((ovm >> j) & 1u) {
+                if (at < a.ovf_cap) a.ovf[at] = (uint32_t)(tile + j * CB_THREADS + tid);
+                at++;
+            }
+    }
+    if (run_n) atomicAdd(&s_hist[run_b], run_n);
+    // per-workgroup statistics slot
+    unsigned long long v[CS_HIST] = {acc, late, refire, bad_ts, bad_range, bad_kg, hout, 0, 0, 0, 0};
+    for (int o = 32; o > 0; o >>= 1) {
+        for (int f = 0; f < CS_MIN; ++f) v[f] += __shfl_xor(v[f], o);
+        const long long x = __shfl_xor(mn, o), y = __shfl_xor(mx, o);
+        mn = x < mn ? x : mn;
+        mx = y > mx ? y : mx;
+    }
+    __syncthreads();   // every LDS table update and histogram run is in
+    unsigned d0 = 0, d1 = 0;
+    int64_t *dk = a.dump_key + (size_t)blockIdx.x * CB_NU * S;
+    int64_t *da = a.dump_acc + (size_t)blockIdx.x * CB_NU * S * NW;
+    for (int i = tid; i < CB_NU * S; i += CB_THREADS) {
+        const int64_t k = s_key[i];
+        if (!(CB_XP & 4)) dk[i] = k;
+        if (k != GWO_EMPTY_KEY) (i < S ? d0 : d1)++;
+    }
+    if (!(CB_XP & 4))
+        for (int i = tid; i < CB_NU * S * NW; i += CB_THREADS) da[i] = s_acc[i];
+    unsigned long long e0 = d0, e1 = d1;
+    for (int o = 32; o > 0; o >>= 1) {
+        e0 += __shfl_xor(e0, o);
+        e1 += __shfl_xor(e1, o);
+    }
+    const int lane = tid & 63, wid = tid >> 6;
+    if (lane == 0) {
+        for (int f = 0; f < CS_HIST; ++f) s_red[wid][f] = 0;
+        for (int f = 0; f < CS_MIN; ++f) s_red[wid][f] = v[f];
+        s_red[wid][CS_MIN] = (unsigned long long)mn;
+        s_red[wid][CS_MAX] = (unsigned long long)mx;
+        s_red[wid][CS_D0] = e0;
+        s_red[wid][CS_D1] = e1;
+    }
+    __syncthreads();
+    // this workgroup's statistics go into shard blockIdx % CB_SHARDS of the statistics words (device-scope
+    // atomics, zero words skipped: ~G / CB_SHARDS operations per address)
+    unsigned long long *shard = a.blk + (size_t)(blockIdx.x % CB_SHARDS) * CS_WORDS;
+    if (tid < CS_HIST) {
+        unsigned long long r = tid == CS_MIN ? 0x7fffffffffffffffull : 0ull;
+        for (int w = 0; w < CB_THREADS / 64; ++w) {
+            const unsigned long long x = s_red[w][tid];
+            if (tid == CS_MIN) r = (long long)x < (long long)r ? x : r;
+            else if (tid == CS_MAX) r = (w == 0 || (long long)x > (long long)r) ? x : r;
+            else r += x;
+        }
+        if (tid == CS_MIN) atomicMin((long long *)&shard[tid], (long long)r);
+        else if (tid == CS_MAX) atomicMax((long long *)&shard[tid], (long long)r);
+        else if (r) atomicAdd(&shard[tid], r);
+    } else if (tid < CS_WORDS) {
+        if (s_hist[tid - CS_HIST]) atomicAdd(&shard[tid], (unsigned long long)s_hist[tid - CS_HIST]);
+    }
+    // the last workgroup reduces the shards into BatchStats (and resets them).  Shards are updated and read with
+    // device-scope read-modify-write atomics, coherent across XCDs without an L2 write-back; each workgroup's
+    // have completed (vmcnt) before its arrival is counted.  No release fence: on gfx950 one writes back the
+    // XCD's whole L2, per workgroup costlier than the pass (the dumps reach the merge through the kernel boundary).
+    __shared__ int s_last;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) s_last = atomicAdd(a.done, 1ull) == (unsigned long long)(gridDim.x - 1);
+    __syncthreads();
+    if (!s_last) return;
+    if (CB_XP & 2) {
+        if (tid == 0) *a.done = 0;
+        return;
+    }
+    __shared__ unsigned long long s_tot[CS_WORDS];
+    if (tid < CS_WORDS) {
+        const unsigned long long init =
+            tid == CS_MIN ? 0x7fffffffffffffffull : (tid == CS_MAX ? 0x8000000000000000ull : 0ull);
+        unsigned long long r = init;
+        for (int q = 0; q < CB_SHARDS; ++q) {   // read and reset for the next batch
+            const unsigned long long x = atomicExch(&a.blk[(size_t)q * CS_WORDS + tid], init);
+            if (tid == CS_MIN) r = (long long)x < (long long)r ? x : r;
+            else if (tid == CS_MAX) r = (long long)x > (long long)r ? x : r;
+            else r += x;
+        }
+        s_tot[tid] = r;
+    }
+    if (tid < CS_WORDS && (tid < CS_HIST ? tid <= CS_D1 : true)) {
+        const unsigned long long r = s_tot[tid];
+        switch (tid) {
+            case CS_ACC: st->accepted = r; break;
+            case CS_LATE: st->late = r; break;
+            case CS_REFIRE: st->refire = r; break;
+            case CS_BADTS: st->bad_ts = r; break;
+            case CS_BADRANGE: st->bad_range = r; break;
+            case CS_BADKG: st->bad_kg = r; break;
+            case CS_HOUT: st->hist_out = r; break;
+            case CS_MIN: st->min_idx = (long long)r; break;
+            case CS_MAX: st->max_idx = (long long)r; break;
+            case CS_D0: st->distinct[0] = r; break;
+            case CS_D1: st->distinct[1] = r; break;
+            default: st->hist[tid - CS_HIST] = r; break;
+        }
+    }
+    if (tid == 0) {
+        st->overflow = __hip_atomic_load(a.ovf_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        *a.done = 0;          // the next batch counts from zero (stream order)
+        *a.ovf_count = 0;
+    }
+}
+
+// merge: threads [0, dump_threads) take (slot, run of CB_MERGE_RUN workgroups) of the dumps; the rest take the
+// listed records.  dir covers units [dir_base, dir_base + dir_len) (the host includes hint, hint + 1 whenever
+// their dumps hold entries).
+__global__ __launch_bounds__(256) void merge_kernel(const int64_t *__restrict__ key, const int64_t *__restrict__ ts,
+                                                    const int64_t *__restrict__ val, WindowGeom g, AccPlan p,
+                                                    CombineArgs a, int G, int64_t dump_threads, uint64_t novf,
+                                                    const TableDesc *__restrict__ dir, long long dir_base,
+                                                    int dir_len, RingDesc ring) {
+    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int S = a.S, NW = p.nwords, slots = CB_NU * S;
+    if ((int64_t)blockIdx.x * 256 < dump_threads) {   // whole workgroups: count_claims needs the full wave
+        const int slot = (int)(t % slots);
+        const int w0 = (int)(t / slots) * CB_MERGE_RUN;
+        const bool live = t < dump_threads && w0 < G;
+        const long long d = a.hint + slot / S - dir_base;
+        int64_t k[CB_MERGE_RUN];
+#pragma unroll
+        for (int j = 0; j < CB_MERGE_RUN; ++j)
+            k[j] = live && w0 + j < G ? a.dump_key[(size_t)(w0 + j) * slots + slot] : GWO_EMPTY_KEY;
+        int64_t run_k = GWO_EMPTY_KEY;
+        int64_t run[GWO_MAX_WORDS];
+        auto flush = [&]() {   // entries exist only for units of accepted records: inside the directory
+            if (run_k == GWO_EMPTY_KEY || d < 0 || d >= dir_len) return;
+            const TableDesc &tb = dir[d];
+            bool cl;
+            int64_t *e = find_or_insert(tb, p.stride, run_k, cl);
+            if (cl) occ_add(tb.occ, 1ull);
+            for (int w = 0; w < NW; ++w) atomic_combine(e + w, p.op[w], run[w]);
+            const long long u = a.hint + slot / S;
+            if (u >= ring.lo && u <= ring.hi) apply_ring(ring, p, run_k, run);
+        };
+#pragma unroll
+        for (int j = 0; j < CB_MERGE_RUN; ++j) {
+            if (k[j] == GWO_EMPTY_KEY) continue;
+            const int64_t *src = a.dump_acc + ((size_t)(w0 + j) * slots + slot) * NW;
+            if (k[j] == run_k) {
+                for (int w = 0; w < NW; ++w) run[w] = combine(p.op[w], run[w], src[w]);
+            } else {
+                flush();
+                run_k = k[j];
+                for (int w = 0; w < NW; ++w) run[w] = src[w];
+            }
+        }
+        flush();
+        return;
+    }
+    // listed records: insert_direct's per-record path
+    const int64_t q = t - dump_threads;
+    if (q >= (int64_t)novf) return;
+    const int64_t i = a.ovf[q];
+    long long u = 0;
+    const int c = classify(ts[i], g, u);
+    if (!takes(c, g)) return;
+    const long long d = u - dir_base;
+    if (d < 0 || d >= dir_len) return;
+    const int64_t k = key[i];
+    const int64_t v = val ? val[i] : 0;
+    bool cl;
+    int64_t *e = find_or_insert(dir[d], p.stride, k, cl);
+    if (cl) occ_add(dir[d].occ, 1ull);
+    for (int w = 0; w < p.nwords; ++w) atomic_combine(e + w, p.op[w], lift_word(p, w, v));
+    if (u >= ring.lo && u <= ring.hi) {
+        int64_t words[GWO_MAX_WORDS];
+        for (int w = 0; w < p.nwords; ++w) words[w] = lift_word(p, w, v);
+        apply_ring(ring, p, k, words);
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
 // fire: EventTimeTrigger.onEventTime FIRE + clearAllState for one window's table
 // (WindowOperator.java:430-473, 528-550).  Occupied entries -> output rows via wave ballot
 // stream compaction (one device atomic per wave); entries are reset to EMPTY/identity in place
@@ -928,6 +1247,29 @@ void launch_generate(uint64_t seed, int64_t first, int64_t total, int64_t nkeys,
                      void *val, hipStream_t s) {
     hipLaunchKernelGGL(generate_kernel, dim3(grid_for(n, 4, 8192)), dim3(256), 0, s, seed, first, total, nkeys,
                        span, disorder, t0, vrange, vf64, key_mode, n, key, ts, (int64_t *)val);
+}
+
+size_t gather_lds_bytes(int S, int nwords) { return (size_t)CB_NU * S * (1 + nwords) * 8; }
+int gather_tile() { return CB_TILE; }
+int gather_stat_words() { return CB_SHARDS * CS_WORDS; }
+
+void launch_gather(const int64_t *key, const int64_t *ts, const int64_t *val, int64_t n, const WindowGeom &g,
+                   const AccPlan &p, const CombineArgs &a, int grid, BatchStats *st, int64_t *side_key, int64_t *side_ts,
+                   int64_t *side_val, unsigned long long *side_count, long long side_cap, int side_enabled,
+                   hipStream_t s) {
+    hipLaunchKernelGGL(gather_kernel, dim3(grid), dim3(CB_THREADS), gather_lds_bytes(a.S, p.nwords), s, key, ts, val,
+                       n, g, p, a, st, side_key, side_ts, side_val, side_count, side_cap, side_enabled);
+}
+
+void launch_merge(const int64_t *key, const int64_t *ts, const int64_t *val, const WindowGeom &g, const AccPlan &p,
+                  const CombineArgs &a, int G, uint64_t novf, const TableDesc *dir, long long dir_base, int dir_len,
+                  const RingDesc &ring, hipStream_t s) {
+    const int64_t runs = (G + CB_MERGE_RUN - 1) / CB_MERGE_RUN;
+    int64_t dump_threads = (int64_t)CB_NU * a.S * runs;
+    dump_threads = (dump_threads + 255) / 256 * 256;
+    const int64_t total = dump_threads + (int64_t)novf;
+    hipLaunchKernelGGL(merge_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, key, ts, val, g, p, a, G,
+                       dump_threads, novf, dir, dir_base, dir_len, ring);
 }
 
 }  // namespace gwo

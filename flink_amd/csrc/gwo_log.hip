@@ -267,7 +267,7 @@ __global__ __launch_bounds__(LOG_K1_THREADS) void log_part_kernel(
                     int32_t kg = key_group(k, g.key_kind, g.max_par);
                     if (kg < g.kg_lo || kg > g.kg_hi) {
                         bad_kg++;
-                        st->bad_kg_key = k;
+                        atomicExch((unsigned long long *)&st->bad_kg_key, (unsigned long long)k);
                     }
                 }
                 acc++;
@@ -370,15 +370,13 @@ __global__ __launch_bounds__(LOG_K1_THREADS) void log_part_kernel(
         }
     }
     // the last workgroup to finish plans pass 2: every workgroup's atomics are complete before its arrival
-    // is counted (each wave drains its memory operations, then one lane releases at agent scope)
+    // is counted (each wave drains its memory operations).  Everything the tail reads was written by
+    // device-scope read-modify-write atomics, coherent across XCDs; the records reach pass 2 through the kernel
+    // boundary -- so no release fence, which on gfx950 writes back the XCD's whole L2 once per workgroup.
     __shared__ int s_last;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (tid == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        s_last = atomicAdd(ca.done, 1ull) == (unsigned long long)(gridDim.x - 1);
-    }
+    if (tid == 0) s_last = atomicAdd(ca.done, 1ull) == (unsigned long long)(gridDim.x - 1);
     __syncthreads();
     if (s_last) k1_plan_tail(cursor, st, ca, base);
 }

@@ -401,8 +401,135 @@ gwo_status Handle::refire_rows(const int64_t *k, const int64_t *t, const int64_t
     return GWO_OK;
 }
 
+// Combine path (gather + merge, gwo_kernels.hip): one pass over the batch classifies and pre-aggregates in
+// LDS; after the host's checks the merge folds the workgroups' tables into the window tables.  *done = false
+// leaves the batch untouched for the two-pass path (window range outside the histogram, side-output growth).
+gwo_status Handle::insert_combined(const int64_t *k, const int64_t *t, const int64_t *v, int64_t n, bool *done) {
+    *done = false;
+    WindowGeom g = geom_now();
+    g.refire_ok = 1;
+    if (!cb_cus) GWO_TRY(hipcheck(hipDeviceGetAttribute(&cb_cus, hipDeviceAttributeMultiprocessorCount, cfg.device), "CUs"));
+    const int NW = plan.nwords;
+    int S = 2048;
+    while (S > 256 && gather_lds_bytes(S, NW) > 65536) S >>= 1;
+    const int64_t tile = gather_tile();
+    const int G = (int)std::max<int64_t>(1, std::min<int64_t>((n + tile - 1) / tile, 4 * (int64_t)cb_cus));
+    GWO_TRY(ensure_buf(cb_dump_key, (size_t)G * 2 * S * 8));
+    GWO_TRY(ensure_buf(cb_dump_acc, (size_t)G * 2 * S * NW * 8));
+    GWO_TRY(ensure_buf(cb_ovf, (size_t)n * 4));
+    if (!cb_ctr.ptr) {   // counters and statistics shards start reset; every gather leaves them reset
+        GWO_TRY(ensure_buf(cb_ctr, 16));
+        GWO_TRY(hipcheck(hipMemsetAsync(cb_ctr.ptr, 0, 16, stream), "combine counters"));
+        const int words = gather_stat_words();
+        std::vector<unsigned long long> init((size_t)words, 0ull);
+        for (int q = 0; q < words / 80; ++q) {
+            init[(size_t)q * 80 + 7] = 0x7fffffffffffffffull;   // min / max words of each shard
+            init[(size_t)q * 80 + 8] = 0x8000000000000000ull;
+        }
+        GWO_TRY(ensure_buf(cb_blk, (size_t)words * 8));
+        GWO_TRY(hipcheck(hipMemcpy(cb_blk.ptr, init.data(), (size_t)words * 8, hipMemcpyHostToDevice), "shards"));
+    }
+    CombineArgs a{};
+    a.dump_key = (int64_t *)cb_dump_key.ptr;
+    a.dump_acc = (int64_t *)cb_dump_acc.ptr;
+    a.ovf = (uint32_t *)cb_ovf.ptr;
+    a.ovf_count = (unsigned long long *)cb_ctr.ptr;
+    a.ovf_cap = (unsigned long long)n;
+    a.blk = (unsigned long long *)cb_blk.ptr;
+    a.done = (unsigned long long *)cb_ctr.ptr + 1;
+    a.S = S;
+    a.sbits = __builtin_ctz((unsigned)S);
+    a.hint = hist_hint;
+    a.full_range = cfg.key_group_start == 0 && cfg.key_group_end == cfg.max_parallelism - 1;
+    if (cfg.assigner == GWO_ASSIGNER_TUMBLING) {   // windows hint .. hint + 3 (gwo_log.cpp log_thresholds)
+        const __int128 size = cfg.size, s0 = (__int128)hist_hint * size + (__int128)geom.unit_off_mod;
+        const __int128 lo = (__int128)(int64_t)0x8000000000000000LL, hi = (__int128)(int64_t)0x7fffffffffffffffLL;
+        if (s0 > lo && s0 + 4 * size <= hi && s0 >= (__int128)geom.offset - size) {
+            for (int j = 0; j <= 4; ++j) a.bound[j] = (int64_t)(s0 + (__int128)j * size);
+            for (int j = 0; j < 4; ++j) {
+                const int64_t max_ts = (int64_t)(s0 + (__int128)(j + 1) * size - 1);
+                const uint32_t c = cleanup_time_host(max_ts) <= g.wm ? 1u : (max_ts <= g.wm ? 2u : 0u);
+                a.cls |= c << (2 * j);
+            }
+            a.thr_ok = 1;
+        }
+    }
+    init_stats(hist_hint);
+    prof_begin(GWO_KERNEL_SCAN);
+    launch_gather(k, t, v, n, g, plan, a, G, d_stats, (int64_t *)side_key.ptr, (int64_t *)side_ts.ptr,
+                  (int64_t *)side_val.ptr, d_side_count, side_enabled() ? side_cap : 0, side_enabled(), stream);
+    GWO_TRY(launch_ok("gather"));
+    prof_end(GWO_KERNEL_SCAN, n);
+    BatchStats &hs = *h_stats;
+    GWO_TRY(hipcheck(hipMemcpyAsync(h_stats, d_stats, sizeof(BatchStats), hipMemcpyDeviceToHost, stream), "stats"));
+    if (side_enabled())
+        GWO_TRY(hipcheck(hipMemcpyAsync(h_scalar, d_side_count, 8, hipMemcpyDeviceToHost, stream), "side count"));
+    GWO_TRY(read_occupancy());   // syncs
+    if (hs.bad_ts) return poison(GWO_ERR_NO_TIMESTAMP,
+                                 "Record has Long.MIN_VALUE timestamp (= no timestamp marker). Is the time "
+                                 "characteristic set to 'ProcessingTime', or did you forget to call "
+                                 "'DataStream.assignTimestampsAndWatermarks(...)'?");
+    if (hs.bad_range) return poison(GWO_ERR_UNSUPPORTED, "sliding windows: timestamp < offset - slide (Java '%' quirk "
+                                                         "range) is outside the pane restatement");
+    if (hs.bad_kg)
+        return poison(GWO_ERR_KEY_GROUP, ("Key group of key " + std::to_string(hs.bad_kg_key) +
+                                          " is not in KeyGroupRange{startKeyGroup=" + std::to_string(cfg.key_group_start) +
+                                          ", endKeyGroup=" + std::to_string(cfg.key_group_end) + "}.").c_str());
+    auto give_back = [&]() -> gwo_status {   // nothing of the batch stays: the two-pass path takes it
+        if (!side_enabled()) return GWO_OK;
+        *h_scalar = side_rows_committed;
+        GWO_TRY(hipcheck(hipMemcpyAsync(d_side_count, h_scalar, 8, hipMemcpyHostToDevice, stream), "side reset"));
+        return hipcheck(hipStreamSynchronize(stream), "side reset");
+    };
+    const uint64_t side_now = side_enabled() ? *h_scalar : 0;
+    if (side_enabled() && (long long)side_now > side_cap) return give_back();
+    const long long lo = hs.min_idx, hi = hs.max_idx;
+    if (hs.accepted > 0 && (lo < hist_hint || hi >= hist_hint + GWO_HIST_BINS || hs.hist_out)) {
+        hist_hint = lo;
+        return give_back();
+    }
+    if (side_enabled()) side_rows = side_rows_committed = side_now;
+    else late_dropped += hs.late;
+    *done = true;
+    if (hs.accepted == 0) return GWO_OK;
+    const int dir_len = (int)(hi - lo + 1);
+    h_dir.assign(dir_len, TableDesc{});
+    for (int d = 0; d < dir_len; ++d) {
+        const long long r = lo + d - hist_hint;
+        uint64_t cnt = hs.hist[r];
+        if (!cnt) continue;
+        if (r < 2) cnt = std::min<uint64_t>(cnt, hs.distinct[r] + hs.overflow);   // keys, not records
+        GWO_TRY(ensure_table(lo + d, cnt));
+    }
+    for (int d = 0; d < dir_len; ++d) {
+        auto it = tables.find(lo + d);
+        if (it != tables.end()) h_dir[d] = desc(it->second);
+    }
+    if (slide) GWO_TRY(slide_prepare_insert(lo, dir_len, hs.hist + (lo - hist_hint)));
+    GWO_TRY(ensure_buf(dir_buf, dir_len * sizeof(TableDesc)));
+    GWO_TRY(hipcheck(hipMemcpyAsync(dir_buf.ptr, h_dir.data(), dir_len * sizeof(TableDesc), hipMemcpyHostToDevice, stream),
+                     "dir"));
+    if (hs.refire) {   // rows read the windows' state before the batch: before the merge
+        if (slide) GWO_TRY(slide_refire_rows(k, t, v, n, g, hs.refire));
+        else GWO_TRY(refire_rows(k, t, v, n, g, lo, dir_len, hs.refire));
+    }
+    prof_begin(GWO_KERNEL_INSERT);
+    launch_merge(k, t, v, g, plan, a, G, hs.overflow, (const TableDesc *)dir_buf.ptr, lo, dir_len, ring_desc(), stream);
+    GWO_TRY(launch_ok("merge"));
+    prof_end(GWO_KERNEL_INSERT, n);
+    adapt_preagg(hs.accepted, hs.distinct[0] + hs.distinct[1] + hs.overflow);
+    hist_hint = lo;
+    for (auto &kv : tables) kv.second.dirty = true;
+    return GWO_OK;
+}
+
 gwo_status Handle::insert_windowed(const int64_t *k, const int64_t *t, const int64_t *v, int64_t n,
                                    const WindowGeom *at) {
+    if (!at && use_preagg && use_combine && n < (1LL << 31)) {
+        bool done = false;
+        GWO_TRY(insert_combined(k, t, v, n, &done));
+        if (done) return GWO_OK;
+    }
     WindowGeom g = at ? *at : geom_now();
     const bool count_late = !g.refire_only;   // a refire_only pass: the log's K1 did the late accounting
     // re-fire records (allowedLateness > 0) are emitted per element and inserted
