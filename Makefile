@@ -38,6 +38,22 @@ clean:
 
 .PHONY: all clean
 
+# JNI shim for the Java GpuWindowOperator (java/): built only where a JDK provides jni.h (none in this image).
+JAVA_HOME ?= /usr/lib/jvm/default-java
+JNI_LIB := flink_amd/libgwo_jni.so
+jni: $(LIB)
+	@if [ -f "$(JAVA_HOME)/include/jni.h" ]; then \
+	  $(CXX_HOST:g++=gcc) -O2 -fPIC -shared -Wall -I$(JAVA_HOME)/include -I$(JAVA_HOME)/include/linux -Iinclude \
+	    jni/gwo_jni.c -o $(JNI_LIB) -Lflink_amd -lgwo -Wl,-rpath,'$$ORIGIN'; \
+	  echo "built $(JNI_LIB)"; \
+	else echo "jni: no $(JAVA_HOME)/include/jni.h -- skipped (set JAVA_HOME to a JDK)"; fi
+# Java classes (needs javac and the Flink jars on FLINK_CLASSPATH)
+java-classes:
+	@if command -v javac >/dev/null 2>&1 && [ -n "$(FLINK_CLASSPATH)" ]; then \
+	  mkdir -p build/java && javac -d build/java -cp "$(FLINK_CLASSPATH)" $$(find java -name '*.java'); \
+	else echo "java-classes: javac or FLINK_CLASSPATH missing -- skipped"; fi
+.PHONY: jni java-classes
+
 # Access-pattern microbenchmark of the table layout; not part of the library.
 tools/micro_table: tools/micro_table.hip
 	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -o $@ $<

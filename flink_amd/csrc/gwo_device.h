@@ -153,7 +153,10 @@ __device__ __forceinline__ int64_t *find_or_insert(const TableDesc &t, int strid
     uint64_t slot = slot_hash(key) & t.mask;
     while (true) {
         int64_t *e = t.base + slot * (uint64_t)stride;
-        int64_t cur = __hip_atomic_load(e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // Within a kernel a slot's key only goes EMPTY -> key, so a possibly stale read is safe: a stale EMPTY
+        // is settled by the CAS (which returns the current key), any other key is final.  Workgroup scope keeps
+        // the probe in the caches instead of bypassing them to the coherence point.
+        int64_t cur = __hip_atomic_load(e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         if (cur == key) return e + 1;
         if (cur == GWO_EMPTY_KEY) {
             unsigned long long prev =

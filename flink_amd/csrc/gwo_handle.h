@@ -144,7 +144,12 @@ struct Handle {
     int use_preagg = 1;
     int use_combine = 1;                       // GWO_COMBINE=0: the two-pass scan + insert path only
     int cb_cus = 0;
-    DevBuf cb_dump_key, cb_dump_acc, cb_ovf, cb_blk, cb_ctr;   // combine path scratch (insert_combined)
+    DevBuf cb_dump_key, cb_dump_acc, cb_ovf, cb_blk, cb_ctr, cb_dir;   // combine path scratch (insert_combined)
+    unsigned long long *cb_rb = nullptr, *cb_rb_dev = nullptr;        // host-mapped readback block
+    unsigned long long cb_seq = 0;
+    hipEvent_t cb_ev = nullptr;
+    std::vector<TableDesc> cb_dir_host;                                // what cb_dir holds
+    long long cb_dir_base = 0;
     int cfg_preagg = -1;                       // GWO_PREAGG env override: 0 / 1
     uint64_t batches = 0;
 

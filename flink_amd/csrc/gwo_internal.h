@@ -123,8 +123,18 @@ struct CombineArgs {
     uint32_t cls;
     int32_t thr_ok;
     int32_t full_range;                // the handle owns every key group: no per-record key-group check
-    int32_t pad;
+    int32_t side_enabled;
+    // readback (host-mapped): BatchStats words, side-output count, occupancy of the tables of units hint and
+    // hint + 1 (occ[i] NULL: no table), then the sequence word, written last
+    unsigned long long *rb;
+    unsigned long long seq;
+    unsigned long long *occ[2];
 };
+#define CB_RB_STATS_WORDS ((int)((sizeof(BatchStats) + 7) / 8))
+#define CB_RB_SIDE (CB_RB_STATS_WORDS)
+#define CB_RB_OCC (CB_RB_STATS_WORDS + 1)
+#define CB_RB_SEQ (CB_RB_STATS_WORDS + 3)
+#define CB_RB_WORDS (CB_RB_STATS_WORDS + 4)
 
 // Output columns (SoA) in HBM.
 struct OutCols {

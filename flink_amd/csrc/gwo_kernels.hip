@@ -561,27 +561,47 @@ __global__ __launch_bounds__(CB_THREADS) void gather_kernel(const int64_t *__res
         }
         s_tot[tid] = r;
     }
+    // the readback block: BatchStats image, side-output count, occupancy of the hint tables, sequence word last
+    BatchStats *rs = (BatchStats *)a.rb;
     if (tid < CS_WORDS && (tid < CS_HIST ? tid <= CS_D1 : true)) {
         const unsigned long long r = s_tot[tid];
         switch (tid) {
-            case CS_ACC: st->accepted = r; break;
-            case CS_LATE: st->late = r; break;
-            case CS_REFIRE: st->refire = r; break;
-            case CS_BADTS: st->bad_ts = r; break;
-            case CS_BADRANGE: st->bad_range = r; break;
-            case CS_BADKG: st->bad_kg = r; break;
-            case CS_HOUT: st->hist_out = r; break;
-            case CS_MIN: st->min_idx = (long long)r; break;
-            case CS_MAX: st->max_idx = (long long)r; break;
-            case CS_D0: st->distinct[0] = r; break;
-            case CS_D1: st->distinct[1] = r; break;
-            default: st->hist[tid - CS_HIST] = r; break;
+            case CS_ACC: rs->accepted = r; break;
+            case CS_LATE: rs->late = r; break;
+            case CS_REFIRE: rs->refire = r; break;
+            case CS_BADTS: rs->bad_ts = r; break;
+            case CS_BADRANGE: rs->bad_range = r; break;
+            case CS_BADKG:
+                rs->bad_kg = r;
+                rs->bad_kg_key = r ? (long long)atomicAdd((unsigned long long *)&st->bad_kg_key, 0ull) : 0;
+                break;
+            case CS_HOUT: rs->hist_out = r; break;
+            case CS_MIN: rs->min_idx = (long long)r; break;
+            case CS_MAX: rs->max_idx = (long long)r; break;
+            case CS_D0: rs->distinct[0] = r; break;
+            case CS_D1: rs->distinct[1] = r; break;
+            default: rs->hist[tid - CS_HIST] = r; break;
+        }
+    } else if (tid >= CB_THREADS - 4) {
+        const int q = tid - (CB_THREADS - 4);   // 0: overflow, 1: side count, 2-3: occupancy
+        if (q == 0) {
+            rs->overflow = atomicExch(a.ovf_count, 0ull);   // read and reset for the next batch
+            *a.done = 0;
+        } else if (q == 1) {
+            a.rb[CB_RB_SIDE] = a.side_enabled ? atomicAdd(side_count, 0ull) : 0ull;
+        } else {
+            unsigned long long *o = a.occ[q - 2];
+            unsigned long long tot = 0;
+            if (o)
+                for (int sh = 0; sh < GWO_OCC_SHARDS; ++sh) tot += atomicAdd(o + sh * GWO_OCC_SHARD_STRIDE, 0ull);
+            a.rb[CB_RB_OCC + q - 2] = tot;
         }
     }
+    __threadfence_system();
+    __syncthreads();
     if (tid == 0) {
-        st->overflow = __hip_atomic_load(a.ovf_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        *a.done = 0;          // the next batch counts from zero (stream order)
-        *a.ovf_count = 0;
+        __threadfence_system();
+        *(volatile unsigned long long *)&a.rb[CB_RB_SEQ] = a.seq;
     }
 }
 

@@ -437,6 +437,24 @@ gwo_status Handle::insert_combined(const int64_t *k, const int64_t *t, const int
     a.ovf_cap = (unsigned long long)n;
     a.blk = (unsigned long long *)cb_blk.ptr;
     a.done = (unsigned long long *)cb_ctr.ptr + 1;
+    if (!cb_rb) {
+        GWO_TRY(hipcheck(hipHostMalloc((void **)&cb_rb, CB_RB_WORDS * 8, hipHostMallocCoherent | hipHostMallocMapped),
+                         "combine readback"));
+        memset(cb_rb, 0, CB_RB_WORDS * 8);
+        GWO_TRY(hipcheck(hipHostGetDevicePointer((void **)&cb_rb_dev, cb_rb, 0), "combine readback"));
+        GWO_TRY(hipcheck(hipEventCreateWithFlags(&cb_ev, hipEventDisableTiming), "event"));
+    }
+    a.rb = cb_rb_dev;
+    a.seq = ++cb_seq;
+    a.side_enabled = side_enabled();
+    Table *hint_tab[2] = {nullptr, nullptr};
+    for (int j = 0; j < 2; ++j) {
+        auto it = tables.find(hist_hint + j);
+        if (it != tables.end()) {
+            hint_tab[j] = &it->second;
+            a.occ[j] = ctr(it->second.counter);
+        }
+    }
     a.S = S;
     a.sbits = __builtin_ctz((unsigned)S);
     a.hint = hist_hint;
@@ -454,17 +472,30 @@ gwo_status Handle::insert_combined(const int64_t *k, const int64_t *t, const int
             a.thr_ok = 1;
         }
     }
-    init_stats(hist_hint);
     prof_begin(GWO_KERNEL_SCAN);
     launch_gather(k, t, v, n, g, plan, a, G, d_stats, (int64_t *)side_key.ptr, (int64_t *)side_ts.ptr,
                   (int64_t *)side_val.ptr, d_side_count, side_enabled() ? side_cap : 0, side_enabled(), stream);
     GWO_TRY(launch_ok("gather"));
     prof_end(GWO_KERNEL_SCAN, n);
+    GWO_TRY(hipcheck(hipEventRecord(cb_ev, stream), "event"));
+    // the gather's last workgroup writes the readback block, sequence word last: spin on it (the event is polled
+    // now and then so that a failed launch cannot spin forever)
+    volatile unsigned long long *seqw = cb_rb + CB_RB_SEQ;
+    for (unsigned it = 1; *seqw != a.seq; ++it) {
+        if ((it & 1023) == 0) {
+            hipError_t e = hipEventQuery(cb_ev);
+            if (e != hipSuccess && e != hipErrorNotReady) return hipcheck(e, "gather");
+            if (e == hipSuccess && *seqw != a.seq)
+                return poison(GWO_ERR_HIP, "gather: readback sequence word not visible after completion");
+        }
+        __builtin_ia32_pause();
+    }
+    __atomic_thread_fence(__ATOMIC_ACQUIRE);
     BatchStats &hs = *h_stats;
-    GWO_TRY(hipcheck(hipMemcpyAsync(h_stats, d_stats, sizeof(BatchStats), hipMemcpyDeviceToHost, stream), "stats"));
-    if (side_enabled())
-        GWO_TRY(hipcheck(hipMemcpyAsync(h_scalar, d_side_count, 8, hipMemcpyDeviceToHost, stream), "side count"));
-    GWO_TRY(read_occupancy());   // syncs
+    memcpy(h_stats, cb_rb, sizeof(BatchStats));
+    *h_scalar = cb_rb[CB_RB_SIDE];
+    for (int j = 0; j < 2; ++j)
+        if (hint_tab[j]) hint_tab[j]->occ = cb_rb[CB_RB_OCC + j];   // exact: the previous merges are done
     if (hs.bad_ts) return poison(GWO_ERR_NO_TIMESTAMP,
                                  "Record has Long.MIN_VALUE timestamp (= no timestamp marker). Is the time "
                                  "characteristic set to 'ProcessingTime', or did you forget to call "
@@ -493,6 +524,13 @@ gwo_status Handle::insert_combined(const int64_t *k, const int64_t *t, const int
     *done = true;
     if (hs.accepted == 0) return GWO_OK;
     const int dir_len = (int)(hi - lo + 1);
+    for (int d = 0; d < dir_len; ++d) {   // a table outside the readback's two: refresh every occupancy
+        auto it = tables.find(lo + d);
+        if (it != tables.end() && &it->second != hint_tab[0] && &it->second != hint_tab[1]) {
+            GWO_TRY(read_occupancy());
+            break;
+        }
+    }
     h_dir.assign(dir_len, TableDesc{});
     for (int d = 0; d < dir_len; ++d) {
         const long long r = lo + d - hist_hint;
@@ -506,15 +544,25 @@ gwo_status Handle::insert_combined(const int64_t *k, const int64_t *t, const int
         if (it != tables.end()) h_dir[d] = desc(it->second);
     }
     if (slide) GWO_TRY(slide_prepare_insert(lo, dir_len, hs.hist + (lo - hist_hint)));
-    GWO_TRY(ensure_buf(dir_buf, dir_len * sizeof(TableDesc)));
-    GWO_TRY(hipcheck(hipMemcpyAsync(dir_buf.ptr, h_dir.data(), dir_len * sizeof(TableDesc), hipMemcpyHostToDevice, stream),
-                     "dir"));
+    // the directory lives in its own buffer and is uploaded only when it changed (usually once per window)
+    if (cb_dir_base != lo || cb_dir_host.size() != (size_t)dir_len ||
+        memcmp(cb_dir_host.data(), h_dir.data(), dir_len * sizeof(TableDesc)) != 0) {
+        GWO_TRY(ensure_buf(cb_dir, dir_len * sizeof(TableDesc)));
+        GWO_TRY(hipcheck(hipMemcpyAsync(cb_dir.ptr, h_dir.data(), dir_len * sizeof(TableDesc), hipMemcpyHostToDevice,
+                                        stream), "dir"));
+        GWO_TRY(hipcheck(hipStreamSynchronize(stream), "dir"));   // h_dir is reused
+        cb_dir_host = h_dir;
+        cb_dir_base = lo;
+    }
     if (hs.refire) {   // rows read the windows' state before the batch: before the merge
+        GWO_TRY(ensure_buf(dir_buf, dir_len * sizeof(TableDesc)));
+        GWO_TRY(hipcheck(hipMemcpyAsync(dir_buf.ptr, h_dir.data(), dir_len * sizeof(TableDesc), hipMemcpyHostToDevice,
+                                        stream), "dir"));
         if (slide) GWO_TRY(slide_refire_rows(k, t, v, n, g, hs.refire));
         else GWO_TRY(refire_rows(k, t, v, n, g, lo, dir_len, hs.refire));
     }
     prof_begin(GWO_KERNEL_INSERT);
-    launch_merge(k, t, v, g, plan, a, G, hs.overflow, (const TableDesc *)dir_buf.ptr, lo, dir_len, ring_desc(), stream);
+    launch_merge(k, t, v, g, plan, a, G, hs.overflow, (const TableDesc *)cb_dir.ptr, lo, dir_len, ring_desc(), stream);
     GWO_TRY(launch_ok("merge"));
     prof_end(GWO_KERNEL_INSERT, n);
     adapt_preagg(hs.accepted, hs.distinct[0] + hs.distinct[1] + hs.overflow);
