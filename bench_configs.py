@@ -128,7 +128,8 @@ def run(cfg):
     N.check(lib.gwo_sync(h), h)
     rows0 = emitted()
     lib.gwo_reset_stats(h)
-    lib.gwo_set_profiling(h, 1)
+    prof = os.environ.get("BENCH_PROF", "1") != "0"   # per-kernel HIP events (two markers per launch)
+    lib.gwo_set_profiling(h, 1 if prof else 0)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(warm, len(bounds)):

@@ -150,6 +150,10 @@ struct Handle {
     hipEvent_t cb_ev = nullptr;
     std::vector<TableDesc> cb_dir_host;                                // what cb_dir holds
     long long cb_dir_base = 0;
+    int use_combine_spec = 1;                                          // GWO_COMBINE_SPEC=0: no speculative merge
+    DevBuf cb_spec_dir;                                                // the speculative merge's directory
+    std::vector<TableDesc> cb_spec_host;
+    long long cb_spec_base = 0;
     int cfg_preagg = -1;                       // GWO_PREAGG env override: 0 / 1
     uint64_t batches = 0;
 

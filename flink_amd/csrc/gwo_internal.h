@@ -129,12 +129,18 @@ struct CombineArgs {
     unsigned long long *rb;
     unsigned long long seq;
     unsigned long long *occ[2];
+    // speculation: the merge queued right behind the gather runs iff the gather's verdict *go is 1 -- no error,
+    // no re-fire, no listed record, every record in units hint / hint + 1 whose tables exist with room
+    uint32_t *go;                      // NULL: no speculative merge
+    uint64_t cap[2];                   // capacities of the hint tables
+    long long side_cap;
 };
 #define CB_RB_STATS_WORDS ((int)((sizeof(BatchStats) + 7) / 8))
 #define CB_RB_SIDE (CB_RB_STATS_WORDS)
 #define CB_RB_OCC (CB_RB_STATS_WORDS + 1)
-#define CB_RB_SEQ (CB_RB_STATS_WORDS + 3)
-#define CB_RB_WORDS (CB_RB_STATS_WORDS + 4)
+#define CB_RB_GO (CB_RB_STATS_WORDS + 3)
+#define CB_RB_SEQ (CB_RB_STATS_WORDS + 4)
+#define CB_RB_WORDS (CB_RB_STATS_WORDS + 5)
 
 // Output columns (SoA) in HBM.
 struct OutCols {
@@ -221,7 +227,7 @@ void launch_gather(const int64_t *key, const int64_t *ts, const int64_t *val, in
                    hipStream_t s);
 void launch_merge(const int64_t *key, const int64_t *ts, const int64_t *val, const WindowGeom &g, const AccPlan &p,
                   const CombineArgs &a, int G, uint64_t novf, const TableDesc *dir, long long dir_base, int dir_len,
-                  const RingDesc &ring, hipStream_t s);
+                  const RingDesc &ring, const uint32_t *go, hipStream_t s);
 void launch_slide_refire_slots(const int64_t *key, const int64_t *r_idx, const long long *r_u, int64_t m,
                                const AccPlan &p, const WindowGeom &g, unsigned long long *keytab, uint64_t kmask,
                                long long j0, uint32_t nj, const TableDesc *pdir, long long pane_base,

@@ -563,6 +563,7 @@ __global__ __launch_bounds__(CB_THREADS) void gather_kernel(const int64_t *__res
     }
     // the readback block: BatchStats image, side-output count, occupancy of the hint tables, sequence word last
     BatchStats *rs = (BatchStats *)a.rb;
+    __shared__ unsigned long long s_spec[4];   // listed records, side-output count, occupancy of the hint tables
     if (tid < CS_WORDS && (tid < CS_HIST ? tid <= CS_D1 : true)) {
         const unsigned long long r = s_tot[tid];
         switch (tid) {
@@ -587,15 +588,34 @@ __global__ __launch_bounds__(CB_THREADS) void gather_kernel(const int64_t *__res
         if (q == 0) {
             rs->overflow = atomicExch(a.ovf_count, 0ull);   // read and reset for the next batch
             *a.done = 0;
+            s_spec[0] = rs->overflow;
         } else if (q == 1) {
-            a.rb[CB_RB_SIDE] = a.side_enabled ? atomicAdd(side_count, 0ull) : 0ull;
+            const unsigned long long sc = a.side_enabled ? atomicAdd(side_count, 0ull) : 0ull;
+            a.rb[CB_RB_SIDE] = sc;
+            s_spec[1] = sc;
         } else {
             unsigned long long *o = a.occ[q - 2];
             unsigned long long tot = 0;
             if (o)
                 for (int sh = 0; sh < GWO_OCC_SHARDS; ++sh) tot += atomicAdd(o + sh * GWO_OCC_SHARD_STRIDE, 0ull);
             a.rb[CB_RB_OCC + q - 2] = tot;
+            s_spec[q] = tot;
         }
+    }
+    __syncthreads();
+    if (tid == 0) {   // the speculative merge's verdict
+        bool go = a.go != nullptr && s_tot[CS_ACC] > 0 && s_tot[CS_BADTS] == 0 && s_tot[CS_BADRANGE] == 0 &&
+                  s_tot[CS_BADKG] == 0 && s_tot[CS_REFIRE] == 0 && s_tot[CS_HOUT] == 0 && s_spec[0] == 0 &&
+                  (!a.side_enabled || (long long)s_spec[1] <= a.side_cap) &&
+                  (long long)s_tot[CS_MIN] >= a.hint && (long long)s_tot[CS_MAX] <= a.hint + 1;
+        for (int r = 0; r < 2 && go; ++r) {
+            const unsigned long long recs = s_tot[CS_HIST + r];
+            if (!recs) continue;
+            const unsigned long long inc = min(recs, s_tot[CS_D0 + r]);
+            go = a.occ[r] != nullptr && 10 * (s_spec[2 + r] + inc) <= 7 * a.cap[r];   // the host's kMaxLoad 0.7
+        }
+        if (a.go) *a.go = go ? 1u : 0u;
+        a.rb[CB_RB_GO] = go ? 1ull : 0ull;
     }
     __threadfence_system();
     __syncthreads();
@@ -612,7 +632,8 @@ __global__ __launch_bounds__(256) void merge_kernel(const int64_t *__restrict__ 
                                                     const int64_t *__restrict__ val, WindowGeom g, AccPlan p,
                                                     CombineArgs a, int G, int64_t dump_threads, uint64_t novf,
                                                     const TableDesc *__restrict__ dir, long long dir_base,
-                                                    int dir_len, RingDesc ring) {
+                                                    int dir_len, RingDesc ring, const uint32_t *go) {
+    if (go && *go == 0) return;   // speculative launch the gather's verdict turned down: the host takes over
     const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
     const int S = a.S, NW = p.nwords, slots = CB_NU * S;
     if ((int64_t)blockIdx.x * 256 < dump_threads) {   // whole workgroups: count_claims needs the full wave
@@ -1283,13 +1304,13 @@ void launch_gather(const int64_t *key, const int64_t *ts, const int64_t *val, in
 
 void launch_merge(const int64_t *key, const int64_t *ts, const int64_t *val, const WindowGeom &g, const AccPlan &p,
                   const CombineArgs &a, int G, uint64_t novf, const TableDesc *dir, long long dir_base, int dir_len,
-                  const RingDesc &ring, hipStream_t s) {
+                  const RingDesc &ring, const uint32_t *go, hipStream_t s) {
     const int64_t runs = (G + CB_MERGE_RUN - 1) / CB_MERGE_RUN;
     int64_t dump_threads = (int64_t)CB_NU * a.S * runs;
     dump_threads = (dump_threads + 255) / 256 * 256;
     const int64_t total = dump_threads + (int64_t)novf;
     hipLaunchKernelGGL(merge_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, key, ts, val, g, p, a, G,
-                       dump_threads, novf, dir, dir_base, dir_len, ring);
+                       dump_threads, novf, dir, dir_base, dir_len, ring, go);
 }
 
 }  // namespace gwo

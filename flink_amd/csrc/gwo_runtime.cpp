@@ -418,8 +418,8 @@ gwo_status Handle::insert_combined(const int64_t *k, const int64_t *t, const int
     GWO_TRY(ensure_buf(cb_dump_acc, (size_t)G * 2 * S * NW * 8));
     GWO_TRY(ensure_buf(cb_ovf, (size_t)n * 4));
     if (!cb_ctr.ptr) {   // counters and statistics shards start reset; every gather leaves them reset
-        GWO_TRY(ensure_buf(cb_ctr, 16));
-        GWO_TRY(hipcheck(hipMemsetAsync(cb_ctr.ptr, 0, 16, stream), "combine counters"));
+        GWO_TRY(ensure_buf(cb_ctr, 32));   // listed-record count, finished workgroups, speculation verdict
+        GWO_TRY(hipcheck(hipMemsetAsync(cb_ctr.ptr, 0, 32, stream), "combine counters"));
         const int words = gather_stat_words();
         std::vector<unsigned long long> init((size_t)words, 0ull);
         for (int q = 0; q < words / 80; ++q) {
@@ -472,11 +472,42 @@ gwo_status Handle::insert_combined(const int64_t *k, const int64_t *t, const int
             a.thr_ok = 1;
         }
     }
+    a.side_cap = side_cap;
+    // speculation (tumbling): the merge is queued behind the gather with the hint tables as its directory and
+    // runs iff the gather's verdict says the batch needs nothing from the host
+    const bool spec = use_combine_spec && cfg.assigner == GWO_ASSIGNER_TUMBLING;
+    if (spec) {
+        std::vector<TableDesc> sd(2, TableDesc{});
+        for (int j = 0; j < 2; ++j)
+            if (hint_tab[j]) {
+                sd[j] = desc(*hint_tab[j]);
+                a.cap[j] = hint_tab[j]->cap;
+            }
+        if (cb_spec_base != hist_hint || cb_spec_host.size() != 2 ||
+            memcmp(cb_spec_host.data(), sd.data(), 2 * sizeof(TableDesc)) != 0) {
+            GWO_TRY(ensure_buf(cb_spec_dir, 2 * sizeof(TableDesc)));
+            GWO_TRY(hipcheck(hipMemcpyAsync(cb_spec_dir.ptr, sd.data(), 2 * sizeof(TableDesc), hipMemcpyHostToDevice,
+                                            stream), "spec dir"));
+            GWO_TRY(hipcheck(hipStreamSynchronize(stream), "spec dir"));
+            cb_spec_host = sd;
+            cb_spec_base = hist_hint;
+        }
+        a.go = (uint32_t *)((unsigned long long *)cb_ctr.ptr + 2);
+    }
     prof_begin(GWO_KERNEL_SCAN);
     launch_gather(k, t, v, n, g, plan, a, G, d_stats, (int64_t *)side_key.ptr, (int64_t *)side_ts.ptr,
                   (int64_t *)side_val.ptr, d_side_count, side_enabled() ? side_cap : 0, side_enabled(), stream);
     GWO_TRY(launch_ok("gather"));
     prof_end(GWO_KERNEL_SCAN, n);
+    if (spec) {
+        RingDesc none{};
+        none.lo = 1;
+        none.hi = 0;
+        prof_begin(GWO_KERNEL_INSERT);
+        launch_merge(k, t, v, g, plan, a, G, 0, (const TableDesc *)cb_spec_dir.ptr, hist_hint, 2, none, a.go, stream);
+        GWO_TRY(launch_ok("merge"));
+        prof_end(GWO_KERNEL_INSERT, n);
+    }
     GWO_TRY(hipcheck(hipEventRecord(cb_ev, stream), "event"));
     // the gather's last workgroup writes the readback block, sequence word last: spin on it (the event is polled
     // now and then so that a failed launch cannot spin forever)
@@ -496,6 +527,17 @@ gwo_status Handle::insert_combined(const int64_t *k, const int64_t *t, const int
     *h_scalar = cb_rb[CB_RB_SIDE];
     for (int j = 0; j < 2; ++j)
         if (hint_tab[j]) hint_tab[j]->occ = cb_rb[CB_RB_OCC + j];   // exact: the previous merges are done
+    if (spec && cb_rb[CB_RB_GO]) {   // the speculative merge ran: only the bookkeeping is left
+        if (side_enabled()) side_rows = side_rows_committed = *h_scalar;
+        else late_dropped += hs.late;
+        for (int j = 0; j < 2; ++j)   // upper bound until the next readback
+            if (hint_tab[j] && hs.hist[j]) hint_tab[j]->occ += std::min<uint64_t>(hs.hist[j], hs.distinct[j]);
+        adapt_preagg(hs.accepted, hs.distinct[0] + hs.distinct[1] + hs.overflow);
+        hist_hint = hs.min_idx;
+        for (auto &kv : tables) kv.second.dirty = true;
+        *done = true;
+        return GWO_OK;
+    }
     if (hs.bad_ts) return poison(GWO_ERR_NO_TIMESTAMP,
                                  "Record has Long.MIN_VALUE timestamp (= no timestamp marker). Is the time "
                                  "characteristic set to 'ProcessingTime', or did you forget to call "
@@ -562,7 +604,8 @@ gwo_status Handle::insert_combined(const int64_t *k, const int64_t *t, const int
         else GWO_TRY(refire_rows(k, t, v, n, g, lo, dir_len, hs.refire));
     }
     prof_begin(GWO_KERNEL_INSERT);
-    launch_merge(k, t, v, g, plan, a, G, hs.overflow, (const TableDesc *)cb_dir.ptr, lo, dir_len, ring_desc(), stream);
+    launch_merge(k, t, v, g, plan, a, G, hs.overflow, (const TableDesc *)cb_dir.ptr, lo, dir_len, ring_desc(), nullptr,
+                 stream);
     GWO_TRY(launch_ok("merge"));
     prof_end(GWO_KERNEL_INSERT, n);
     adapt_preagg(hs.accepted, hs.distinct[0] + hs.distinct[1] + hs.overflow);
