@@ -82,11 +82,11 @@ struct LogState {
     std::vector<long long> fire_units;
     uint64_t fire_rows0 = 0, fire_bound = 0;
     unsigned long long *h_fire_out = nullptr;    // pinned [3]: row counter, overflow, slow partitions
-    unsigned long long *d_cursor = nullptr;      // [LOG_NU * 256 * LOG_XG * LOG_CUR_STRIDE] region cursors of K1
+    unsigned long long *d_cursor = nullptr;      // [LOG_NU * LOG_ND * LOG_XG * LOG_CUR_STRIDE] region cursors of K1
     // K1 readback per slot (LOG_RB_* layout), written into pinned host memory by log_collect_kernel,
     // which also leaves the device plan of pass 2 in d_bk (per slot) and resets cursors and stats
     unsigned long long *h_rb = nullptr, *d_rbh = nullptr;   // host / device views
-    LogBucket *d_bk = nullptr;                   // [LOG_SLOTS][LOG_NU * 256 + 1]
+    LogBucket *d_bk = nullptr;                   // [LOG_SLOTS][LOG_NU * LOG_ND + 1]
     hipEvent_t ev_rb[LOG_SLOTS] = {};
     // host-planned pass 2 (exact re-run after an overflow): [nb + 1] buckets, one H2D copy
     LogBucket *d_plan = nullptr, *h_buckets = nullptr;
@@ -101,7 +101,7 @@ struct LogState {
 
     unsigned long long *rb(int slot) const { return h_rb + (size_t)slot * LOG_RB_WORDS; }
     unsigned long long *rb_dev(int slot) const { return d_rbh + (size_t)slot * LOG_RB_WORDS; }
-    LogBucket *bk(int slot) const { return d_bk + (size_t)slot * (LOG_NU * 256 + 1); }
+    LogBucket *bk(int slot) const { return d_bk + (size_t)slot * (LOG_NU * LOG_ND + 1); }
     // a batch buffer neither the K1 in flight nor the deferred pass 2 holds
     int free_slot() const {
         for (int s = 0; s < LOG_SLOTS; ++s)
@@ -113,7 +113,7 @@ struct LogState {
 static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 static constexpr size_t kRbBytes = (size_t)LOG_RB_WORDS * 8;
-static constexpr size_t kPlanBytes = (LOG_NU * 256 + 1) * sizeof(LogBucket);
+static constexpr size_t kPlanBytes = (LOG_NU * LOG_ND + 1) * sizeof(LogBucket);
 
 // Capacity of a fixed-size group that receives Binomial(n, 1/k) records: mean + 6 sigma + slack.
 static uint64_t group_capacity(double mean) {
@@ -123,8 +123,8 @@ static uint64_t group_capacity(double mean) {
 gwo_status Handle::log_init() {
     logst = new LogState();
     LogState &L = *logst;
-    GWO_TRY(dalloc((void **)&L.d_cursor, LOG_NU * 256 * LOG_XG * LOG_CUR_STRIDE * 8));
-    GWO_TRY(hipcheck(hipMemsetAsync(L.d_cursor, 0, LOG_NU * 256 * LOG_XG * LOG_CUR_STRIDE * 8, stream), "cursor"));
+    GWO_TRY(dalloc((void **)&L.d_cursor, LOG_NU * LOG_ND * LOG_XG * LOG_CUR_STRIDE * 8));
+    GWO_TRY(hipcheck(hipMemsetAsync(L.d_cursor, 0, LOG_NU * LOG_ND * LOG_XG * LOG_CUR_STRIDE * 8, stream), "cursor"));
     GWO_TRY(dalloc((void **)&L.d_bk, kPlanBytes * LOG_SLOTS));
     GWO_TRY(dalloc((void **)&L.d_plan, kPlanBytes));
     GWO_TRY(dalloc((void **)&L.d_overflow, 16));
@@ -280,10 +280,10 @@ int Handle::log_choose_lp(uint64_t batch_records) const {
 gwo_status Handle::log_split_exact(long long base, int nunits, uint64_t cap, const uint64_t *counts, int tmpx) {
     LogState &L = *logst;
     const int W = needs_value ? 2 : 1;
-    const int nb = nunits * 256;
+    const int nb = nunits * LOG_ND;
     std::vector<LogWindow *> wins(nunits, nullptr);
     std::vector<uint64_t> wcount(nunits, 0);
-    for (int b = 0; b < nb; ++b) wcount[b >> 8] += counts[b];
+    for (int b = 0; b < nb; ++b) wcount[b >> LOG_DB] += counts[b];
     std::vector<uint32_t> pcap_exact(nb, 0);   // after an overflow: the measured partition maximum
     LogSegSet set{};
     // the device plan of this batch buffer holds each bucket's region-group offsets (xoff)
@@ -294,13 +294,13 @@ gwo_status Handle::log_split_exact(long long base, int nunits, uint64_t cap, con
         uint32_t chunks = 0;
         for (int w = 0; w < nunits; ++w) {
             LogSegDesc d{};
-            const int c0 = w * 256;
+            const int c0 = w * LOG_ND;
             if (wcount[w]) {
                 LogWindow &Wn = L.wins[base + w];   // exists: created when K1 was launched over it
                 wins[w] = &Wn;
-                const int lp = Wn.lp, F = 1 << (lp - 8);
+                const int lp = Wn.lp, F = 1 << (lp - LOG_DB);
                 uint64_t seg = 0;
-                for (int dgt = 0; dgt < 256; ++dgt) {
+                for (int dgt = 0; dgt < LOG_ND; ++dgt) {
                     const uint64_t n_b = counts[c0 + dgt];
                     LogBucket &B = L.h_buckets[c0 + dgt];
                     B.n = (uint32_t)n_b;
@@ -322,7 +322,7 @@ gwo_status Handle::log_split_exact(long long base, int nunits, uint64_t cap, con
                 d.lp = lp;
                 GWO_TRY(hipcheck(hipMemsetAsync(d.cnt, 0, ((size_t)1 << lp) * 4, stream), "segment counts"));
             } else {
-                for (int dgt = 0; dgt < 256; ++dgt) {
+                for (int dgt = 0; dgt < LOG_ND; ++dgt) {
                     LogBucket &B = L.h_buckets[c0 + dgt];
                     B = LogBucket{};
                     B.chunk0 = chunks;
@@ -344,12 +344,12 @@ gwo_status Handle::log_split_exact(long long base, int nunits, uint64_t cap, con
         // (the segments carved above stay unused until the window is released)
         for (int w = 0; w < nunits; ++w) {
             if (!wins[w]) continue;
-            const int F = 1 << (set.s[w].lp - 8);
-            std::vector<uint32_t> cnt((size_t)256 * F);
+            const int F = 1 << (set.s[w].lp - LOG_DB);
+            std::vector<uint32_t> cnt((size_t)LOG_ND * F);
             GWO_TRY(hipcheck(hipMemcpy(cnt.data(), set.s[w].cnt, cnt.size() * 4, hipMemcpyDeviceToHost), "counts"));
-            for (int dgt = 0; dgt < 256; ++dgt)
+            for (int dgt = 0; dgt < LOG_ND; ++dgt)
                 for (int f = 0; f < F; ++f)
-                    pcap_exact[w * 256 + dgt] = std::max(pcap_exact[w * 256 + dgt], cnt[(size_t)dgt * F + f]);
+                    pcap_exact[w * LOG_ND + dgt] = std::max(pcap_exact[w * LOG_ND + dgt], cnt[(size_t)dgt * F + f]);
         }
     }
     for (int w = 0; w < nunits; ++w) {
@@ -366,7 +366,7 @@ gwo_status Handle::log_split_exact(long long base, int nunits, uint64_t cap, con
 gwo_status Handle::log_commit_spec(LogJob &J, const unsigned long long *rbp) {
     LogState &L = *logst;
     uint64_t wcount[LOG_NU] = {};
-    for (int b = 0; b < J.nunits * 256; ++b) wcount[b >> 8] += rbp[b];
+    for (int b = 0; b < J.nunits * LOG_ND; ++b) wcount[b >> LOG_DB] += rbp[b];
     for (int w = 0; w < J.nunits; ++w) log_uncarve(J, w, wcount[w] ? rbp[LOG_RB_SEG + w] : 0);
     L.pend.after_seq = J.seq;   // any later readback implies this pass 2 completed (stream order)
     L.pend.has_event = false;
@@ -375,7 +375,7 @@ gwo_status Handle::log_commit_spec(LogJob &J, const unsigned long long *rbp) {
     L.pend.nunits = J.nunits;
     L.pend.base = J.base;
     L.pend.cap = J.cap;
-    L.pend.counts.assign(rbp, rbp + J.nunits * 256);
+    L.pend.counts.assign(rbp, rbp + J.nunits * LOG_ND);
     for (int w = 0; w < J.nunits; ++w) {
         if (!wcount[w]) continue;
         LogWindow &Wn = L.wins[J.base + w];
@@ -393,7 +393,7 @@ gwo_status Handle::log_split_dev(const LogJob &J, const unsigned long long *rbp)
     const int W = needs_value ? 2 : 1;
     LogSegSet set{};
     uint64_t wcount[LOG_NU] = {}, total = 0;
-    for (int b = 0; b < J.nunits * 256; ++b) wcount[b >> 8] += rbp[b];
+    for (int b = 0; b < J.nunits * LOG_ND; ++b) wcount[b >> LOG_DB] += rbp[b];
     for (int w = 0; w < J.nunits; ++w) {
         set.s[w] = J.desc[w];
         if (!wcount[w]) continue;
@@ -406,7 +406,7 @@ gwo_status Handle::log_split_dev(const LogJob &J, const unsigned long long *rbp)
     }
     L.h_split_flag[J.slot] = 0;
     prof_begin(GWO_KERNEL_PARTITION);
-    launch_log_split((const int64_t *)L.tmp[J.slot].ptr, J.cap, needs_value, L.bk(J.slot), J.nunits * 256, set,
+    launch_log_split((const int64_t *)L.tmp[J.slot].ptr, J.cap, needs_value, L.bk(J.slot), J.nunits * LOG_ND, set,
                      L.d_split_flag + J.slot, (uint32_t)rbp[LOG_RB_CHUNKS], nullptr, stream);
     GWO_TRY(launch_ok("log split"));
     prof_end(GWO_KERNEL_PARTITION, (int64_t)total);
@@ -420,7 +420,7 @@ gwo_status Handle::log_split_dev(const LogJob &J, const unsigned long long *rbp)
     L.pend.nunits = J.nunits;
     L.pend.base = J.base;
     L.pend.cap = J.cap;
-    L.pend.counts.assign(rbp, rbp + J.nunits * 256);
+    L.pend.counts.assign(rbp, rbp + J.nunits * LOG_ND);
     for (int w = 0; w < J.nunits; ++w) {
         if (!wcount[w]) continue;
         LogWindow &Wn = L.wins[J.base + w];
@@ -444,7 +444,7 @@ gwo_status Handle::log_resolve_split() {
     if (L.h_split_flag[L.pend.tmpx] == 0) return GWO_OK;
     for (int w = 0; w < L.pend.nunits; ++w) {
         uint64_t c = 0;
-        for (int d = 0; d < 256; ++d) c += L.pend.counts[(size_t)w * 256 + d];
+        for (int d = 0; d < LOG_ND; ++d) c += L.pend.counts[(size_t)w * LOG_ND + d];
         if (!c) continue;
         LogWindow &Wn = L.wins[L.pend.base + w];
         Wn.segs.pop_back();   // the deferred split's segment is the window's last one
@@ -455,12 +455,12 @@ gwo_status Handle::log_resolve_split() {
 }
 
 // Upper bound of the segment records one window receives from a batch of n records: the device plan
-// gives each of its 256 coarse buckets F * pcap records, pcap = ceil(n_b/F + 6 sqrt(n_b/F) + 4), so the
-// window's segment is at most n + 6 sqrt(F) * sum_b sqrt(n_b) + 5 * 256 * F <= n + 96 sqrt(F n) + 1280 F
-// (Cauchy-Schwarz over the 256 buckets).
+// gives each of its LOG_ND coarse buckets F * pcap records (F = 2^lp / LOG_ND partitions each), pcap =
+// ceil(n_b/F + 6 sqrt(n_b/F) + 4), so the window's segment is at most
+//   n + 6 sqrt(F) * sum_b sqrt(n_b) + 5 * 2^lp <= n + 6 sqrt(2^lp n) + 5 * 2^lp   (Cauchy-Schwarz over the buckets).
 static uint64_t seg_upper_bound(uint64_t n, int lp) {
-    const double F = (double)(1u << (lp - 8));
-    return (uint64_t)std::ceil((double)n + 96.0 * std::sqrt(F * (double)n) + 1280.0 * F) + 64;
+    const double P = (double)(1u << lp);
+    return (uint64_t)std::ceil((double)n + 6.0 * std::sqrt(P * (double)n) + 5.0 * P) + 64;
 }
 
 // Window bounds of K1's launch range [base, base + nunits) and each window's class at the batch's watermark
@@ -529,10 +529,10 @@ gwo_status Handle::log_k1(LogJob &J, bool first_pass) {
         ca.cnt[w] = d.cnt;
     }
     DevBuf &tmp = L.tmp[J.slot];
-    if (tmp.bytes < (size_t)J.nunits * 256 * LOG_XG * J.cap * W * 8) {
+    if (tmp.bytes < (size_t)J.nunits * LOG_ND * LOG_XG * J.cap * W * 8) {
         GWO_TRY(log_resolve_split());   // ensure_buf may free: nothing may still read it
         // sized for LOG_NU windows, so a batch spanning more windows than the last one does not reallocate
-        GWO_TRY(ensure_buf(tmp, (size_t)std::max(J.nunits, LOG_NU) * 256 * LOG_XG * J.cap * W * 8));
+        GWO_TRY(ensure_buf(tmp, (size_t)std::max(J.nunits, LOG_NU) * LOG_ND * LOG_XG * J.cap * W * 8));
     }
     const bool side = first_pass && side_enabled();
     const LogThr thr = log_thresholds(J);
@@ -548,10 +548,10 @@ gwo_status Handle::log_k1(LogJob &J, bool first_pass) {
         LogSegSet set{};
         for (int w = 0; w < J.nunits; ++w) set.s[w] = J.desc[w];
         // chunks = sum over buckets of ceil(n_b / TILE) <= ceil(n / TILE) + buckets
-        const uint64_t grid = ((uint64_t)J.n + LOG_TILE - 1) / LOG_TILE + (uint64_t)J.nunits * 256;
+        const uint64_t grid = ((uint64_t)J.n + LOG_TILE - 1) / LOG_TILE + (uint64_t)J.nunits * LOG_ND;
         L.h_split_flag[J.slot] = 0;
         prof_begin(GWO_KERNEL_PARTITION);
-        launch_log_split((const int64_t *)tmp.ptr, J.cap, needs_value, L.bk(J.slot), J.nunits * 256, set,
+        launch_log_split((const int64_t *)tmp.ptr, J.cap, needs_value, L.bk(J.slot), J.nunits * LOG_ND, set,
                          L.d_split_flag + J.slot, (uint32_t)grid, L.d_go + J.slot, stream);
         GWO_TRY(launch_ok("log split"));
         prof_end(GWO_KERNEL_PARTITION, J.n);
@@ -724,7 +724,7 @@ gwo_status Handle::insert_log(const int64_t *k, const int64_t *t, const int64_t 
     J.g = geom_now();
     J.base = hist_hint;
     J.nunits = (int)std::min<long long>(LOG_NU, std::max<long long>(1, L.span_hint));
-    J.cap = group_capacity((double)n / (256.0 * LOG_XG));
+    J.cap = group_capacity((double)n / ((double)LOG_ND * LOG_XG));
     // speculative pass 2 (no host round trip between K1 and pass 2) unless late records go to the side output
     // (K1's first pass appends them; a re-run must not repeat that)
     J.spec = !side_enabled();

@@ -18,8 +18,12 @@
 #define LOG_TILE_THREADS 512
 #define LOG_TILE (LOG_TILE_PER * LOG_TILE_THREADS)   // 3584 records: 56 KiB of 16-B records in LDS
 static_assert(LOG_K1_PER * LOG_K1_THREADS == LOG_TILE, "K1 tile and pass-2 chunk hold the same records");
-#define LOG_MIN_LP 8             // a window has at least 256 partitions (one per coarse digit)
-#define LOG_MAX_LP 18            // at most 2^18 partitions per window (<= 1024 per coarse digit)
+#ifndef LOG_DB
+#define LOG_DB 8                 // coarse digit bits: K1 groups a window's records by the top LOG_DB bits
+#endif
+#define LOG_ND (1 << LOG_DB)     // coarse digits (K1 buckets) per window
+#define LOG_MIN_LP 8             // a window has at least 256 partitions
+#define LOG_MAX_LP (LOG_DB + 10 < 18 ? LOG_DB + 10 : 18)   // <= 1024 partitions per coarse digit (pass-2 LDS)
 #define LOG_FIRE_THREADS 512
 #define LOG_CUR_STRIDE 16        // K1 bucket cursors: one per 128-B line (memory-side atomics serialise per line)
 #ifndef LOG_XG
@@ -76,10 +80,10 @@ struct LogSegSet {
     LogSegDesc s[LOG_NU];
 };
 
-// K1 readback block (host-visible, written by K1's last workgroup): [LOG_NU * 256] bucket counts, the
+// K1 readback block (host-visible, written by K1's last workgroup): [LOG_NU * LOG_ND] bucket counts, the
 // BatchStats words, [LOG_NU] segment sizes (records) of the device plan, its pass-2 workgroup count, the
 // speculation verdict (1: the speculative pass 2 queued behind K1 runs the plan), and the sequence number.
-static constexpr int LOG_RB_STATS = LOG_NU * 256;
+static constexpr int LOG_RB_STATS = LOG_NU * LOG_ND;
 static constexpr int LOG_RB_SEG = LOG_RB_STATS + (int)((sizeof(BatchStats) + 7) / 8);
 static constexpr int LOG_RB_CHUNKS = LOG_RB_SEG + LOG_NU;
 static constexpr int LOG_RB_GO = LOG_RB_CHUNKS + 1;
@@ -95,7 +99,7 @@ struct CollectArgs {
     uint64_t cap;                // region capacity of the batch buffer (records per bucket and region group)
     uint64_t seg_cap[LOG_NU];    // speculative pass 2: segment records carved per window (spec only)
     int spec;                    // 1: a pass 2 is queued behind K1 and runs iff the plan fits (rb[LOG_RB_GO])
-    LogBucket *bk;               // out: [nunits * 256 + 1] pass-2 plan (device)
+    LogBucket *bk;               // out: [nunits * LOG_ND + 1] pass-2 plan (device)
     unsigned *go;                // out: 1 = the queued speculative pass 2 runs the plan, 0 = it exits
     unsigned long long *rb;      // out: readback block (pinned host memory)
     unsigned long long seq;      // written to rb[LOG_RB_SEQ] after every other readback word

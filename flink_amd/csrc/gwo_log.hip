@@ -130,11 +130,13 @@ __device__ __forceinline__ void k1_plan_tail(unsigned long long *cursor, BatchSt
     unsigned long long chunk_run = 0;
     unsigned bad = 0;
     unsigned long long maxreg = 0;
-    for (int q = 0; q < a.nunits; ++q) {   // window q of the launch: bucket b = q * 256 + t (digit t)
-        const int b = q * 256 + t;
+    for (int q = 0; q < a.nunits; ++q) {   // window q of the launch: bucket b = q * LOG_ND + t (digit t)
+        const bool dig = t < LOG_ND;
+        const int b = q * LOG_ND + t;
         unsigned long long c[LOG_XG], n_b = 0;
 #pragma unroll
-        for (int x = 0; x < LOG_XG; ++x) c[x] = atomicExch(&cursor[((size_t)b * LOG_XG + x) * LOG_CUR_STRIDE], 0ull);
+        for (int x = 0; x < LOG_XG; ++x)
+            c[x] = dig ? atomicExch(&cursor[((size_t)b * LOG_XG + x) * LOG_CUR_STRIDE], 0ull) : 0ull;
         uint32_t xoff[LOG_XG];
 #pragma unroll
         for (int x = 0; x < LOG_XG; ++x) {
@@ -142,11 +144,11 @@ __device__ __forceinline__ void k1_plan_tail(unsigned long long *cursor, BatchSt
             n_b += c[x];
             maxreg = c[x] > maxreg ? c[x] : maxreg;
         }
-        a.rb[b] = n_b;
+        if (dig) a.rb[b] = n_b;
         uint32_t pcap = 0, chunks = 0;
         unsigned long long seg = 0;
         if (n_b) {
-            const int F = 1 << (a.lp[q] - 8);
+            const int F = 1 << (a.lp[q] - LOG_DB);
             const double mean = (double)n_b / (double)F;
             pcap = (uint32_t)ceil(__dadd_rn(__dadd_rn(mean, __dmul_rn(6.0, sqrt(mean))), 4.0));
             seg = (unsigned long long)F * pcap;
@@ -162,7 +164,7 @@ __device__ __forceinline__ void k1_plan_tail(unsigned long long *cursor, BatchSt
         B.pcap = pcap;
         B.seg_base = (uint32_t)(seg_incl - seg);
         B.chunk0 = (uint32_t)(chunk_run + chk_incl - chunks);
-        a.bk[b] = B;
+        if (dig) a.bk[b] = B;
         if (t == 0) {
             a.rb[LOG_RB_SEG + q] = seg_tot;
             if (a.spec && seg_tot > a.seg_cap[q]) bad = 1;
@@ -176,7 +178,7 @@ __device__ __forceinline__ void k1_plan_tail(unsigned long long *cursor, BatchSt
     if (t == 0) {
         LogBucket E{};
         E.chunk0 = (uint32_t)chunk_run;
-        a.bk[a.nunits * 256] = E;
+        a.bk[a.nunits * LOG_ND] = E;
         a.rb[LOG_RB_CHUNKS] = chunk_run;
         const bool go = a.spec && !s_bad && S.bad_ts == 0 && S.bad_kg == 0 && S.refire == 0 && S.accepted > 0 &&
                         S.min_idx >= base && S.min_idx < base + a.nunits && chunk_run < (1ull << 32);
@@ -195,7 +197,7 @@ __device__ __forceinline__ void k1_plan_tail(unsigned long long *cursor, BatchSt
 }
 
 // ------------------------------------------------------------------------------------------------
-// K1 log_part: batch -> batch buffer, grouped by bucket b = (window - base) * 256 + coarse digit.
+// K1 log_part: batch -> batch buffer, grouped by bucket b = (window - base) * LOG_ND + coarse digit.
 // Bucket b owns LOG_XG regions of cap records; workgroup w appends to region group x = w % LOG_XG at
 // records [(b * LOG_XG + x) * cap, ...), whose cursor cursor[(b * LOG_XG + x) * LOG_CUR_STRIDE] ends as its
 // record count (also when it exceeds cap: those records are not written and the host reruns).
@@ -216,10 +218,10 @@ __global__ __launch_bounds__(LOG_K1_THREADS) void log_part_kernel(
     }
     __shared__ __attribute__((aligned(16))) int64_t s_rec[LOG_TILE * W];
     __shared__ uint16_t s_bk[LOG_TILE];
-    __shared__ uint32_t s_cnt[LOG_NU * 256];
-    __shared__ uint32_t s_off[LOG_NU * 256];
+    __shared__ uint32_t s_cnt[LOG_NU * LOG_ND];
+    __shared__ uint32_t s_off[LOG_NU * LOG_ND];
     __shared__ long long s_min[LOG_K1_THREADS / 64], s_max[LOG_K1_THREADS / 64];
-    const int nb = nunits * 256;
+    const int nb = nunits * LOG_ND;
     const int per = (nb + LOG_K1_THREADS - 1) / LOG_K1_THREADS;   // counters owned per thread (<= 4)
     const int tid = threadIdx.x;
     const int xg = blockIdx.x % LOG_XG;                           // region group (an XCD under round-robin placement)
@@ -275,7 +277,7 @@ __global__ __launch_bounds__(LOG_K1_THREADS) void log_part_kernel(
                 mx = u > mx ? u : mx;
                 long long w = u - base;
                 if (w >= 0 && w < nunits) {
-                    uint32_t b = (uint32_t)(w * 256 + (int)(digit_hash(k) >> 24));
+                    uint32_t b = (uint32_t)(w * LOG_ND + (int)(digit_hash(k) >> (32 - LOG_DB)));
                     uint32_t r = atomicAdd(&s_cnt[b], 1u);
                     code[j] = (b << 16) | r;
                 } else {
@@ -417,9 +419,9 @@ __global__ __launch_bounds__(LOG_TILE_THREADS) void log_split_kernel(const int64
     const int c = s_c;
     const LogBucket B = bk[c];
     const uint32_t chunk = blockIdx.x - B.chunk0;
-    const int w = c >> 8, d = c & 255;
+    const int w = c >> LOG_DB, d = c & (LOG_ND - 1);
     const LogSegDesc S = segs.s[w];
-    const int lp = S.lp, fb = lp - 8, F = 1 << fb;
+    const int lp = S.lp, fb = lp - LOG_DB, F = 1 << fb;
     if (chunk == 0)
         for (int f = tid; f < F; f += LOG_TILE_THREADS) S.off[d * F + f] = B.seg_base + (uint32_t)f * B.pcap;
     for (int f = tid; f < F; f += LOG_TILE_THREADS) s_cnt[f] = 0;
