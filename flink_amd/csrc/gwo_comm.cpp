@@ -54,18 +54,30 @@ static gwo_status nccl_ok(Handle *h, ncclResult_t r, const char *what) {
     return h->poison(GWO_ERR_COMM, (std::string(what) + ": " + ncclGetErrorString(r)).c_str());
 }
 
-// keyBy shuffle of one batch: every record goes to the GPU owning its key group; returns the
-// records this rank receives as 24-B {key, ts, value} records (AoS).  Order-insensitive state
-// (tumbling/sliding) uses the fused route kernel; sessions need each source's arrival order per key,
-// so they group by destination with a stable radix pass instead.
+// keyBy shuffle of one batch: every record goes to the GPU owning its key group.  Returns the records this
+// rank keeps (its own region of the send buffer: they never touch the wire) and the records it receives from
+// the other ranks, both as 24-B {key, ts, value} records (AoS).  Order-insensitive state (tumbling/sliding)
+// uses the fused route kernel; sessions need each source's arrival order per key, so they group by
+// destination with a stable radix pass instead.  One host round trip per batch: the per-destination counts
+// are exchanged on the device right behind the route, and one copy brings both directions' counts back (a
+// region overflow re-routes locally -- the exchanged counts are exact either way).
 gwo_status Handle::comm_exchange(const int64_t *k, const int64_t *t, const int64_t *v, int64_t n, const int64_t **aos,
-                                 int64_t *rn) {
+                                 int64_t *rn, const int64_t **local, int64_t *ln) {
     Comm &C = *comm;
-    const int P = C.nranks;
+    const int P = C.nranks, me = C.rank;
     const bool stable = cfg.assigner == GWO_ASSIGNER_SESSION;
     GWO_TRY(ensure_buf(C.counts, (size_t)2 * P * 8));
     unsigned long long *d_send = (unsigned long long *)C.counts.ptr, *d_recv = d_send + P;
     std::vector<uint64_t> soff(P + 1, 0), roff(P + 1, 0);
+    uint64_t cap = 0;
+    auto route = [&]() -> gwo_status {
+        GWO_TRY(ensure_buf(C.sendbuf, (size_t)P * cap * 24 + 24));
+        if (n > 0)
+            launch_route(k, t, v, n, cfg.key_kind, cfg.max_parallelism, P, (unsigned long long *)C.cursor.ptr, cap,
+                         (int64_t *)C.sendbuf.ptr, stream);
+        launch_route_collect((unsigned long long *)C.cursor.ptr, P, d_send, stream);
+        return launch_ok("route");
+    };
     prof_begin(GWO_KERNEL_PARTITION);
     if (!stable) {
         if (!C.cursor.ptr) {
@@ -73,22 +85,8 @@ gwo_status Handle::comm_exchange(const int64_t *k, const int64_t *t, const int64
             GWO_TRY(hipcheck(hipMemsetAsync(C.cursor.ptr, 0, route_cursor_bytes(), stream), "route cursors"));
         }
         const double mean = (double)n / P;
-        uint64_t cap = (uint64_t)(mean + 6.0 * std::sqrt(mean) + 64.0);
-        while (true) {
-            GWO_TRY(ensure_buf(C.sendbuf, (size_t)P * cap * 24 + 24));
-            if (n > 0)
-                launch_route(k, t, v, n, cfg.key_kind, cfg.max_parallelism, P, (unsigned long long *)C.cursor.ptr, cap,
-                             (int64_t *)C.sendbuf.ptr, stream);
-            launch_route_collect((unsigned long long *)C.cursor.ptr, P, d_send, stream);
-            GWO_TRY(launch_ok("route"));
-            GWO_TRY(hipcheck(hipMemcpyAsync(C.h_counts, d_send, (size_t)P * 8, hipMemcpyDeviceToHost, stream), "counts"));
-            GWO_TRY(hipcheck(hipStreamSynchronize(stream), "route sync"));
-            uint64_t mx = 0;
-            for (int p = 0; p < P; ++p) mx = std::max<uint64_t>(mx, C.h_counts[p]);
-            if (mx <= cap) break;
-            cap = mx;   // skewed keys: a destination overflowed its region -- redo with the exact size
-        }
-        for (int p = 0; p < P; ++p) soff[p] = (uint64_t)p * cap;   // region starts (records)
+        cap = (uint64_t)(mean + 6.0 * std::sqrt(mean) + 64.0);
+        GWO_TRY(route());
     } else {
         GWO_TRY(hipcheck(hipMemsetAsync(d_send, 0, (size_t)2 * P * 8, stream), "counts"));
         if (n > 0) {
@@ -105,35 +103,52 @@ gwo_status Handle::comm_exchange(const int64_t *k, const int64_t *t, const int64
             launch_pack(k, t, v, (const uint32_t *)C.v1.ptr, n, (int64_t *)C.sendbuf.ptr, stream);
             GWO_TRY(launch_ok("partition"));
         }
-        GWO_TRY(hipcheck(hipMemcpyAsync(C.h_counts, d_send, (size_t)P * 8, hipMemcpyDeviceToHost, stream), "counts"));
-        GWO_TRY(hipcheck(hipStreamSynchronize(stream), "counts sync"));
-        for (int p = 0; p < P; ++p) soff[p + 1] = soff[p] + C.h_counts[p];
     }
     prof_end(GWO_KERNEL_PARTITION, n);
-    // exchange counts, then records (xGMI is point-to-point: one send/recv pair per peer)
-    GWO_TRY(nccl_ok(this, ncclGroupStart(), "group"));
-    for (int p = 0; p < P; ++p) {
-        GWO_TRY(nccl_ok(this, ncclSend(d_send + p, 1, ncclUint64, p, C.nc, stream), "send count"));
-        GWO_TRY(nccl_ok(this, ncclRecv(d_recv + p, 1, ncclUint64, p, C.nc, stream), "recv count"));
+    // counts, on the device right behind the route (xGMI is point-to-point: one send/recv pair per peer)
+    if (P > 1) {
+        GWO_TRY(nccl_ok(this, ncclGroupStart(), "group"));
+        for (int p = 0; p < P; ++p) {
+            if (p == me) continue;
+            GWO_TRY(nccl_ok(this, ncclSend(d_send + p, 1, ncclUint64, p, C.nc, stream), "send count"));
+            GWO_TRY(nccl_ok(this, ncclRecv(d_recv + p, 1, ncclUint64, p, C.nc, stream), "recv count"));
+        }
+        GWO_TRY(nccl_ok(this, ncclGroupEnd(), "group end"));
     }
-    GWO_TRY(nccl_ok(this, ncclGroupEnd(), "group end"));
-    GWO_TRY(hipcheck(hipMemcpyAsync(C.h_counts + P, d_recv, (size_t)P * 8, hipMemcpyDeviceToHost, stream), "counts"));
+    GWO_TRY(hipcheck(hipMemcpyAsync(C.h_counts, d_send, (size_t)2 * P * 8, hipMemcpyDeviceToHost, stream), "counts"));
     GWO_TRY(hipcheck(hipStreamSynchronize(stream), "counts sync"));
+    C.h_counts[P + me] = 0;   // our own records stay here
+    if (!stable) {
+        uint64_t mx = 0;
+        for (int p = 0; p < P; ++p) mx = std::max<uint64_t>(mx, C.h_counts[p]);
+        if (mx > cap) {   // skewed keys: a destination overflowed its region -- re-route with the exact size
+            cap = mx;
+            GWO_TRY(route());
+        }
+        for (int p = 0; p < P; ++p) soff[p] = (uint64_t)p * cap;   // region starts (records)
+    } else {
+        for (int p = 0; p < P; ++p) soff[p + 1] = soff[p] + C.h_counts[p];
+    }
     for (int p = 0; p < P; ++p) roff[p + 1] = roff[p] + C.h_counts[P + p];
     const int64_t R = (int64_t)roff[P];
     GWO_TRY(ensure_buf(C.recvbuf, R * 24 + 24));
     const int64_t *sb = (const int64_t *)C.sendbuf.ptr;
-    prof_begin(GWO_KERNEL_EXCHANGE);
-    GWO_TRY(nccl_ok(this, ncclGroupStart(), "group"));
-    for (int p = 0; p < P; ++p) {
-        uint64_t sc = C.h_counts[p], rc = C.h_counts[P + p];
-        if (sc) GWO_TRY(nccl_ok(this, ncclSend(sb + 3 * soff[p], 3 * sc, ncclInt64, p, C.nc, stream), "send"));
-        if (rc)
-            GWO_TRY(nccl_ok(this, ncclRecv((int64_t *)C.recvbuf.ptr + 3 * roff[p], 3 * rc, ncclInt64, p, C.nc, stream),
-                            "recv"));
+    if (P > 1) {
+        prof_begin(GWO_KERNEL_EXCHANGE);
+        GWO_TRY(nccl_ok(this, ncclGroupStart(), "group"));
+        for (int p = 0; p < P; ++p) {
+            if (p == me) continue;
+            const uint64_t sc = C.h_counts[p], rc = C.h_counts[P + p];
+            if (sc) GWO_TRY(nccl_ok(this, ncclSend(sb + 3 * soff[p], 3 * sc, ncclInt64, p, C.nc, stream), "send"));
+            if (rc)
+                GWO_TRY(nccl_ok(this, ncclRecv((int64_t *)C.recvbuf.ptr + 3 * roff[p], 3 * rc, ncclInt64, p, C.nc,
+                                               stream), "recv"));
+        }
+        GWO_TRY(nccl_ok(this, ncclGroupEnd(), "group end"));
+        prof_end(GWO_KERNEL_EXCHANGE, R);
     }
-    GWO_TRY(nccl_ok(this, ncclGroupEnd(), "group end"));
-    prof_end(GWO_KERNEL_EXCHANGE, R);
+    *local = sb + 3 * soff[me];
+    *ln = (int64_t)C.h_counts[me];
     *aos = (const int64_t *)C.recvbuf.ptr;
     *rn = R;
     return GWO_OK;
@@ -158,6 +173,10 @@ gwo_status Handle::comm_unpack(const int64_t *aos, int64_t n, const int64_t **rk
 
 gwo_status Handle::comm_min_watermark(int64_t wm_in, int64_t *out) {
     Comm &C = *comm;
+    if (C.nranks == 1) {   // nothing to agree on
+        *out = wm_in;
+        return GWO_OK;
+    }
     GWO_TRY(ensure_buf(C.counts, (size_t)2 * C.nranks * 8 + 16));
     int64_t *d = (int64_t *)C.counts.ptr;
     *C.h_wm = wm_in;

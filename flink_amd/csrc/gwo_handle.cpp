@@ -213,14 +213,24 @@ gwo_status Handle::submit(const int64_t *key, const int64_t *ts, const void *val
     if (!comm && n == 0) return GWO_OK;
     if (n > 0) GWO_TRY(stage_inputs(key, ts, needs_value ? val : nullptr, n, &dk, &dt, &dv));
     if (comm) {
-        const int64_t *aos = nullptr;
-        int64_t rn = 0;
-        GWO_TRY(comm_exchange(dk, dt, dv, n, &aos, &rn));
-        if (rn == 0) return GWO_OK;
-        if (logst) return insert_log(aos, aos + 1, aos + 2, rn, 3);   // K1 reads the received records in place
-        const int64_t *rk, *rt, *rv;
-        GWO_TRY(comm_unpack(aos, rn, &rk, &rt, &rv));
-        return submit_local(rk, rt, rv, rn);
+        const int64_t *aos = nullptr, *loc = nullptr;
+        int64_t rn = 0, ln = 0;
+        GWO_TRY(comm_exchange(dk, dt, dv, n, &aos, &rn, &loc, &ln));
+        // the records this rank keeps (never on the wire), then the ones it received; the log layout's K1 reads
+        // both in place (24-B records), the other layouts unpack them to columns
+        const int64_t *parts[2] = {loc, aos};
+        const int64_t counts[2] = {ln, rn};
+        for (int q = 0; q < 2; ++q) {
+            if (counts[q] == 0) continue;
+            if (logst) {
+                GWO_TRY(insert_log(parts[q], parts[q] + 1, parts[q] + 2, counts[q], 3));
+                continue;
+            }
+            const int64_t *rk, *rt, *rv;
+            GWO_TRY(comm_unpack(parts[q], counts[q], &rk, &rt, &rv));
+            GWO_TRY(submit_local(rk, rt, rv, counts[q]));
+        }
+        return GWO_OK;
     }
     return submit_local(dk, dt, dv, n);
 }

@@ -307,7 +307,7 @@ struct Handle {
     // comm (gwo_comm.cpp)
     void comm_free();
     gwo_status comm_exchange(const int64_t *k, const int64_t *t, const int64_t *v, int64_t n, const int64_t **aos,
-                             int64_t *rn);
+                             int64_t *rn, const int64_t **local, int64_t *ln);
     gwo_status comm_unpack(const int64_t *aos, int64_t n, const int64_t **rk, const int64_t **rt, const int64_t **rv);
     gwo_status comm_min_watermark(int64_t wm, int64_t *out);
 
