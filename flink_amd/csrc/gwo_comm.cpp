@@ -35,6 +35,9 @@ struct Comm {
     DevBuf dest, k1, v1, hist, sendbuf, recvbuf, rk, rt, rv, counts, cursor;
     unsigned long long *h_counts = nullptr;   // pinned: [send counts | recv counts]
     int64_t *h_wm = nullptr;                  // pinned
+    // the records' exchange runs on its own stream, so the K1 of the records a rank keeps overlaps it
+    hipStream_t cs = nullptr;
+    hipEvent_t ev_routed = nullptr, ev_recv = nullptr;
 };
 
 void Handle::comm_free() {
@@ -43,6 +46,10 @@ void Handle::comm_free() {
     for (DevBuf *b : {&comm->dest, &comm->k1, &comm->v1, &comm->hist, &comm->sendbuf, &comm->recvbuf, &comm->rk,
                       &comm->rt, &comm->rv, &comm->counts, &comm->cursor})
         b->release();
+    if (comm->cs) (void)hipStreamSynchronize(comm->cs);
+    if (comm->cs) (void)hipStreamDestroy(comm->cs);
+    if (comm->ev_routed) (void)hipEventDestroy(comm->ev_routed);
+    if (comm->ev_recv) (void)hipEventDestroy(comm->ev_recv);
     if (comm->h_counts) (void)hipHostFree(comm->h_counts);
     if (comm->h_wm) (void)hipHostFree(comm->h_wm);
     delete comm;
@@ -134,24 +141,35 @@ gwo_status Handle::comm_exchange(const int64_t *k, const int64_t *t, const int64
     GWO_TRY(ensure_buf(C.recvbuf, R * 24 + 24));
     const int64_t *sb = (const int64_t *)C.sendbuf.ptr;
     if (P > 1) {
-        prof_begin(GWO_KERNEL_EXCHANGE);
+        // on the comm stream, behind the route (and so behind everything earlier batches did with the buffers);
+        // comm_wait_received puts the main stream behind it before the received records are read
+        GWO_TRY(hipcheck(hipEventRecord(C.ev_routed, stream), "event"));
+        GWO_TRY(hipcheck(hipStreamWaitEvent(C.cs, C.ev_routed, 0), "event wait"));
+        prof_begin(GWO_KERNEL_EXCHANGE, C.cs);
         GWO_TRY(nccl_ok(this, ncclGroupStart(), "group"));
         for (int p = 0; p < P; ++p) {
             if (p == me) continue;
             const uint64_t sc = C.h_counts[p], rc = C.h_counts[P + p];
-            if (sc) GWO_TRY(nccl_ok(this, ncclSend(sb + 3 * soff[p], 3 * sc, ncclInt64, p, C.nc, stream), "send"));
+            if (sc) GWO_TRY(nccl_ok(this, ncclSend(sb + 3 * soff[p], 3 * sc, ncclInt64, p, C.nc, C.cs), "send"));
             if (rc)
                 GWO_TRY(nccl_ok(this, ncclRecv((int64_t *)C.recvbuf.ptr + 3 * roff[p], 3 * rc, ncclInt64, p, C.nc,
-                                               stream), "recv"));
+                                               C.cs), "recv"));
         }
         GWO_TRY(nccl_ok(this, ncclGroupEnd(), "group end"));
-        prof_end(GWO_KERNEL_EXCHANGE, R);
+        prof_end(GWO_KERNEL_EXCHANGE, R, C.cs);
+        GWO_TRY(hipcheck(hipEventRecord(C.ev_recv, C.cs), "event"));
     }
     *local = sb + 3 * soff[me];
     *ln = (int64_t)C.h_counts[me];
     *aos = (const int64_t *)C.recvbuf.ptr;
     *rn = R;
     return GWO_OK;
+}
+
+// The main stream waits for the exchange's receives (comm stream) before reading the received records.
+gwo_status Handle::comm_wait_received() {
+    if (comm->nranks == 1) return GWO_OK;
+    return hipcheck(hipStreamWaitEvent(stream, comm->ev_recv, 0), "exchange wait");
 }
 
 // AoS {key, ts, value} records -> the handle's column scratch (table, sliding and session layouts)
@@ -224,10 +242,21 @@ extern "C" gwo_status gwo_comm_init(gwo_handle *hh, const uint8_t *id, int32_t n
         delete C;
         return GWO_ERR_OUT_OF_MEMORY;
     }
+    if (hipStreamCreateWithFlags(&C->cs, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&C->ev_routed, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&C->ev_recv, hipEventDisableTiming) != hipSuccess) {
+        (void)hipHostFree(C->h_counts);
+        (void)hipHostFree(C->h_wm);
+        delete C;
+        return GWO_ERR_HIP;
+    }
     ncclUniqueId u;
     memcpy(&u, id, GWO_COMM_ID_BYTES);
     ncclResult_t r = ncclCommInitRank(&C->nc, nranks, u, rank);
     if (r != ncclSuccess) {
+        (void)hipStreamDestroy(C->cs);
+        (void)hipEventDestroy(C->ev_routed);
+        (void)hipEventDestroy(C->ev_recv);
         (void)hipHostFree(C->h_counts);
         (void)hipHostFree(C->h_wm);
         delete C;

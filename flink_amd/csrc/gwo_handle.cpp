@@ -221,6 +221,7 @@ gwo_status Handle::submit(const int64_t *key, const int64_t *ts, const void *val
         const int64_t *parts[2] = {loc, aos};
         const int64_t counts[2] = {ln, rn};
         for (int q = 0; q < 2; ++q) {
+            if (q == 1) GWO_TRY(comm_wait_received());   // the kept records' pass overlapped the exchange
             if (counts[q] == 0) continue;
             if (logst) {
                 GWO_TRY(insert_log(parts[q], parts[q] + 1, parts[q] + 2, counts[q], 3));

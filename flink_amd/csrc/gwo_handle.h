@@ -310,6 +310,7 @@ struct Handle {
                              int64_t *rn, const int64_t **local, int64_t *ln);
     gwo_status comm_unpack(const int64_t *aos, int64_t n, const int64_t **rk, const int64_t **rt, const int64_t **rv);
     gwo_status comm_min_watermark(int64_t wm, int64_t *out);
+    gwo_status comm_wait_received();
 
     void prof_begin(int k, hipStream_t s = nullptr);
     void prof_end(int k, int64_t items, hipStream_t s = nullptr);
