@@ -88,6 +88,7 @@ struct LogState {
     unsigned long long *h_rb = nullptr, *d_rbh = nullptr;   // host / device views
     LogBucket *d_bk = nullptr;                   // [LOG_SLOTS][LOG_NU * LOG_ND + 1]
     hipEvent_t ev_rb[LOG_SLOTS] = {};
+    bool rb_event[LOG_SLOTS] = {};   // ev_rb[slot] was recorded behind the slot's last K1 (side output only)
     // host-planned pass 2 (exact re-run after an overflow): [nb + 1] buckets, one H2D copy
     LogBucket *d_plan = nullptr, *h_buckets = nullptr;
     std::vector<LogSegDesc> h_fire;
@@ -542,8 +543,13 @@ gwo_status Handle::log_k1(LogJob &J, bool first_pass) {
                     (int64_t *)side_val.ptr, d_side_count, side ? side_cap : 0, side, ca, thr, stream);
     GWO_TRY(launch_ok("log partition"));
     prof_end(GWO_KERNEL_INSERT, J.n);
-    if (side) GWO_TRY(hipcheck(hipMemcpyAsync(h_scalar, d_side_count, 8, hipMemcpyDeviceToHost, stream), "side count"));
-    GWO_TRY(hipcheck(hipEventRecord(L.ev_rb[J.slot], stream), "event"));
+    // The readback's own sequence word tells the host K1 is done; an event is recorded only behind the side-output
+    // count copy (each event marker between K1 and pass 2 costs the stream ~5 us on MI355X, measured in the trace).
+    L.rb_event[J.slot] = side;
+    if (side) {
+        GWO_TRY(hipcheck(hipMemcpyAsync(h_scalar, d_side_count, 8, hipMemcpyDeviceToHost, stream), "side count"));
+        GWO_TRY(hipcheck(hipEventRecord(L.ev_rb[J.slot], stream), "event"));
+    }
     if (J.spec) {
         LogSegSet set{};
         for (int w = 0; w < J.nunits; ++w) set.s[w] = J.desc[w];
@@ -573,14 +579,15 @@ void Handle::log_uncarve(const LogJob &J, int w, uint64_t keep) {
 
 // Waits for K1's readback by spinning on its sequence word in pinned host memory (the collect kernel
 // writes it last), which wakes the host as soon as the data lands instead of through the runtime's
-// completion wait; the event is polled now and then so a failed launch cannot spin forever.
+// completion wait; the stream (or the slot's event, when one was recorded) is polled now and then so a failed
+// launch cannot spin forever.
 gwo_status Handle::log_wait_readback(int slot, unsigned long long seq) {
     LogState &L = *logst;
     volatile unsigned long long *w = L.rb(slot) + LOG_RB_SEQ;
     for (unsigned it = 1;; ++it) {
         if (*w == seq) break;
         if ((it & 1023) == 0) {
-            hipError_t e = hipEventQuery(L.ev_rb[slot]);
+            hipError_t e = L.rb_event[slot] ? hipEventQuery(L.ev_rb[slot]) : hipStreamQuery(stream);
             if (e != hipSuccess && e != hipErrorNotReady) return hipcheck(e, "log partition");
             if (e == hipSuccess && *w != seq)   // completed, yet the word never arrived: fail loudly
                 return poison(GWO_ERR_HIP, "log partition: readback sequence word not visible after completion");

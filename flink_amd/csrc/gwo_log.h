@@ -39,7 +39,7 @@ static_assert(LOG_K1_PER * LOG_K1_THREADS == LOG_TILE, "K1 tile and pass-2 chunk
 #define FIRE_MAXR 15                                 // election rounds before a partition takes the slow path
 #define FIRE_LDS (FIRE_RCAP * 8 * 2 + (FIRE_RCAP + 4) * 4)   // fast-path dynamic LDS: keys, values, counts (70 KiB)
 #ifndef LOG_PART_FILL
-#define LOG_PART_FILL 6          // a new window's partitions are sized for LOG_PART_FILL/8 of FIRE_RCAP records
+#define LOG_PART_FILL 7          // a new window's partitions are sized for LOG_PART_FILL/8 of FIRE_RCAP records
 #endif
 #define LOG_MAX_SEGS 512         // segments (batches) per window that one fire folds (= LOG_FIRE_THREADS)
 

@@ -768,7 +768,9 @@ __device__ __forceinline__ uint32_t elect_prio(int round, uint32_t i) {
     return ((uint32_t)(FIRE_MAXR - round) << 12) | (4095u - i);
 }
 
-template <int NW>
+// PART: the window holds restored partial accumulators (after gwo_restore) -- a separate instance, so the
+// common one carries none of their code or registers.
+template <int NW, bool PART>
 __global__ __launch_bounds__(LOG_FIRE_THREADS) __attribute__((amdgpu_waves_per_eu(4, 4))) void log_fire_kernel(const LogSegDesc *__restrict__ segs, int nseg,
                                                                     uint32_t nparts, int cap_log2, int has_val,
                                                                     AccPlan p, ResultPlan rp, int64_t start,
@@ -837,12 +839,10 @@ __global__ __launch_bounds__(LOG_FIRE_THREADS) __attribute__((amdgpu_waves_per_e
     // register prefetch of a partition's records (only when they all fit); global (not flat) loads,
     // so LDS waits in between do not wait for them
     int64_t rk[FIRE_RPT], rv[FIRE_RPT];
-    auto prefetch = [&](bool on) {
-        if (!on) {   // uniform: nothing to prefetch (no next partition, or a slow-path-only fold)
-#pragma unroll
-            for (int r = 0; r < FIRE_RPT; ++r) rk[r] = rv[r] = 0;
-            return;
-        }
+    // Always issued (a lane with nothing to fetch re-reads a valid record): a branch around the loads would merge
+    // them with a second definition of rk/rv, and that copy waits for the loads (measured: fire 1.71 -> 1.95 ms).
+    auto prefetch = [&](bool on) {   // (called after publish: s_rp is complete)
+        const int64_t *const dflt = (PART && nseg == 0) ? partial.rec : s_rp[0];
         const uint32_t total = s_beg[nseg];
         const bool fits = on && total <= (uint32_t)FIRE_RCAP;
         const int64_t *addr[FIRE_RPT];
@@ -867,7 +867,7 @@ __global__ __launch_bounds__(LOG_FIRE_THREADS) __attribute__((amdgpu_waves_per_e
 #pragma unroll
         for (int r = 0; r < FIRE_RPT; ++r) {
             const uint32_t i = tid + r * LOG_FIRE_THREADS;
-            addr[r] = s_rp[0];
+            addr[r] = dflt;
             if (fits && i < total) {
                 const int sg = segr[r];
                 addr[r] = s_rp[sg] + (uint64_t)(s_src[sg] + (i - s_beg[sg])) * (has_val ? 2 : 1);
@@ -896,7 +896,7 @@ __global__ __launch_bounds__(LOG_FIRE_THREADS) __attribute__((amdgpu_waves_per_e
         a_off = seg_off[part];
     }
     publish(a_cnt, a_off);
-    prefetch(!slow_only);
+    prefetch(!(PART && slow_only));
     while (true) {
         const uint32_t total = s_beg[nseg];
         const uint32_t nxt = part + gridDim.x;
@@ -912,7 +912,7 @@ __global__ __launch_bounds__(LOG_FIRE_THREADS) __attribute__((amdgpu_waves_per_e
             }
         };
         unsigned long long rbase_lane0 = 0;   // wave 0 lane 0: the row reservation, consumed after P4
-        bool fast = !slow_only && total <= (uint32_t)FIRE_RCAP;
+        bool fast = !(PART && slow_only) && total <= (uint32_t)FIRE_RCAP;
         if (fast) {
             // P0: record keys into LDS; free election table; zero counts
 #pragma unroll
@@ -1067,7 +1067,7 @@ __global__ __launch_bounds__(LOG_FIRE_THREADS) __attribute__((amdgpu_waves_per_e
                     }
                     fire_insert(c, p, k, h, has_val ? q[1] : 0);
                 }
-                if (partial.rec) {   // restored accumulators of this partition (raw words, combined as they are)
+                if (PART && partial.rec) {   // restored accumulators of this partition (raw words, combined as they are)
                     const uint32_t pc = partial.cnt[part], po = partial.off[part];
                     for (uint32_t i = tid; i < pc; i += LOG_FIRE_THREADS) {
                         const int64_t *q = partial.rec + (uint64_t)(po + i) * (1 + p.nwords);
@@ -1102,7 +1102,7 @@ __global__ __launch_bounds__(LOG_FIRE_THREADS) __attribute__((amdgpu_waves_per_e
         else __syncthreads();
         // unconditional, so the loads land straight in rk/rv (no loop-carried copy that would wait for
         // them): in flight during this partition's emit and the next one's election
-        prefetch(more && !slow_only);
+        prefetch(more && !(PART && slow_only));
         if (fast) {
             // P5: one row per leader, in ordinal order.  Thread t takes ordinal t - sh (sh = rbase & 1),
             // so lanes 2m and 2m+1 own a 16-B-aligned pair of global rows; after a DPP swap within the
@@ -1234,7 +1234,7 @@ void warm_log_kernels(int nwords, int has_val, hipStream_t s) {
     if (lds < (size_t)FIRE_LDS) lds = FIRE_LDS;
 #define GWO_WARM_NW(NW)                                                                                            \
     case NW:                                                                                                       \
-        hipLaunchKernelGGL(log_fire_kernel<NW>, dim3(1), dim3(LOG_FIRE_THREADS), lds, s, nullptr, 0, 0u, cl, has_val, p, \
+        hipLaunchKernelGGL((log_fire_kernel<NW, false>), dim3(1), dim3(LOG_FIRE_THREADS), lds, s, nullptr, 0, 0u, cl, has_val, p, \
                            rp, 0, 0, o, nullptr, 0, LogSegDesc{});                                                 \
         break;
     switch (nwords) {
@@ -1273,8 +1273,12 @@ void launch_log_fire(const LogSegDesc *segs, int nseg, int lp, int has_val, cons
     uint32_t grid = parts < groups ? parts : groups;
 #define GWO_FIRE_NW(NW)                                                                                          \
     case NW:                                                                                                     \
-        hipLaunchKernelGGL(log_fire_kernel<NW>, dim3(grid), dim3(LOG_FIRE_THREADS), lds, s, segs, nseg, parts, cl, \
-                           has_val, plan, rp, start, end, out, overflow, slow_only, partial);                \
+        if (partial.rec)                                                                                         \
+            hipLaunchKernelGGL((log_fire_kernel<NW, true>), dim3(grid), dim3(LOG_FIRE_THREADS), lds, s, segs, nseg,  \
+                               parts, cl, has_val, plan, rp, start, end, out, overflow, slow_only, partial);     \
+        else                                                                                                     \
+            hipLaunchKernelGGL((log_fire_kernel<NW, false>), dim3(grid), dim3(LOG_FIRE_THREADS), lds, s, segs, nseg, \
+                               parts, cl, has_val, plan, rp, start, end, out, overflow, slow_only, partial);     \
         break;
     switch (plan.nwords) {
         GWO_FIRE_NW(1)
