@@ -768,8 +768,8 @@ __device__ __forceinline__ uint32_t elect_prio(int round, uint32_t i) {
     return ((uint32_t)(FIRE_MAXR - round) << 12) | (4095u - i);
 }
 
-// PART: the window holds restored partial accumulators (after gwo_restore) -- a separate instance, so the
-// common one carries none of their code or registers.
+// PART: the checkpoint instance -- restored partial accumulators (after gwo_restore) and slow-path-only folds
+// (gwo_snapshot's raw-word rows); a separate instance, so the watermark fire carries none of their code or registers.
 template <int NW, bool PART>
 __global__ __launch_bounds__(LOG_FIRE_THREADS) __attribute__((amdgpu_waves_per_eu(4, 4))) void log_fire_kernel(const LogSegDesc *__restrict__ segs, int nseg,
                                                                     uint32_t nparts, int cap_log2, int has_val,
@@ -1273,7 +1273,7 @@ void launch_log_fire(const LogSegDesc *segs, int nseg, int lp, int has_val, cons
     uint32_t grid = parts < groups ? parts : groups;
 #define GWO_FIRE_NW(NW)                                                                                          \
     case NW:                                                                                                     \
-        if (partial.rec)                                                                                         \
+        if (partial.rec || slow_only)                                                                            \
             hipLaunchKernelGGL((log_fire_kernel<NW, true>), dim3(grid), dim3(LOG_FIRE_THREADS), lds, s, segs, nseg,  \
                                parts, cl, has_val, plan, rp, start, end, out, overflow, slow_only, partial);     \
         else                                                                                                     \

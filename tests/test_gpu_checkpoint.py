@@ -92,18 +92,24 @@ def _run(op, k, t, v, batches, start=0):
     return prev
 
 
-def test_log_layout_checkpoint_continues_exactly(F):
+@pytest.mark.parametrize("aggs", ["sum_min_max", "avg_count"])
+def test_log_layout_checkpoint_continues_exactly(F, aggs):
     """The C4 layout: windows still collecting records are folded (not released) into rows; the restored
-    operator folds them back in at the windows' fire together with the records that arrive later."""
+    operator folds them back in at the windows' fire together with the records that arrive later.  avg_count:
+    raw accumulator words differ from the results (avg keeps (sum, count)), so the fold must emit raw words."""
     rng = np.random.default_rng(5)
     n = 60_000
     k = rng.integers(0, 20_000, n).astype(np.int64)
     t = (np.sort(rng.integers(0, 120_000, n)) + rng.integers(0, 3_000, n)).astype(np.int64)
     v = rng.integers(-500, 500, n).astype(np.int64)
     b = G.punctuated_watermarks(t, 1_500, 1_000)
-    want, late = _oracle_rows(O.TumblingEventTimeWindows(10_000), O.MultiAgg([O.SumLongAgg(), O.MinAgg(), O.MaxAgg()]),
-                              k, t, v, b)
-    agg = F.MultiAggregate(F.SumAggregate(), F.MinAggregate(), F.MaxAggregate())
+    if aggs == "sum_min_max":
+        oagg = O.MultiAgg([O.SumLongAgg(), O.MinAgg(), O.MaxAgg()])
+        agg = F.MultiAggregate(F.SumAggregate(), F.MinAggregate(), F.MaxAggregate())
+    else:
+        oagg = O.MultiAgg([O.AvgAgg(), O.CountAgg()])
+        agg = F.MultiAggregate(F.AverageAggregate(), F.CountAggregate())
+    want, late = _oracle_rows(O.TumblingEventTimeWindows(10_000), oagg, k, t, v, b)
     mk = lambda layout: F.GpuWindowOperator(F.TumblingEventTimeWindows.of(10_000), agg, state_layout=layout,
                                             max_parallelism=32768)
     for cut in (len(b) // 3, len(b) // 2 + 3):
