@@ -59,7 +59,10 @@ def parse():
                    help="pipelined submission (gwo_set_pipelined_submit): measured slower on C4, since pass 2 then "
                         "runs after the next batch's K1 and misses its batch buffer in the MALL")
     p.add_argument("--comm-single", action="store_true",
-                   help="attach a 1-rank RCCL communicator at N=1 (measures the exchange path on one GPU)")
+                   help="attach a 1-rank RCCL communicator at N=1 (one rank: no record leaves the GPU)")
+    p.add_argument("--comm-virtual", type=int, default=0,
+                   help="with --comm-single: route as GPU 0 of P GPUs (GWO_COMM_VIRTUAL=P), the other GPUs' records "
+                        "through RCCL to this rank itself -- a rank's multi-GPU data path at P, measured on one GPU")
     return p.parse_args()
 
 
@@ -136,7 +139,10 @@ def main():
     elif a.comm_single:
         uid = (C.c_uint8 * N.COMM_ID_BYTES)()
         N.check(lib.gwo_comm_unique_id(uid))
+        if a.comm_virtual > 1:
+            os.environ["GWO_COMM_VIRTUAL"] = str(a.comm_virtual)
         N.check(lib.gwo_comm_init(h, uid, 1, 0), h, "gwo_comm_init")
+        os.environ.pop("GWO_COMM_VIRTUAL", None)
 
     def step(i):
         s, e = bounds[i]

@@ -10,10 +10,12 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
 #include "gwo_handle.h"
+#include "gwo_log.h"
 
 namespace gwo {
 
@@ -38,7 +40,15 @@ struct Comm {
     // the records' exchange runs on its own stream, so the K1 of the records a rank keeps overlaps it
     hipStream_t cs = nullptr;
     hipEvent_t ev_routed = nullptr, ev_recv = nullptr;
+    // Virtual ranks (GWO_COMM_VIRTUAL=P on a 1-rank communicator, log layout): K1 routes as if P GPUs shared the
+    // key groups and this were GPU 0; the other "GPUs'" records go through RCCL to this rank itself and come back
+    // as received records -- a rank's whole data path at P GPUs on one GPU (outputs unchanged: it owns every key).
+    int vranks = 0;
+    uint64_t rcap = 0;            // send region capacity of the routed K1 (records)
+    int64_t recv_n = 0;           // records received by the last exchange
 };
+
+static int route_ranks(const Comm &C) { return C.vranks > 1 ? C.vranks : C.nranks; }
 
 void Handle::comm_free() {
     if (!comm) return;
@@ -166,9 +176,111 @@ gwo_status Handle::comm_exchange(const int64_t *k, const int64_t *t, const int64
     return GWO_OK;
 }
 
+// Routing fused into the log layout's first K1 of a batch (gwo_log.hip log_part_kernel<.., true>): K1 appends
+// the records of other GPUs to per-destination regions of the send buffer while it partitions its own, so a
+// batch is read once -- the route kernel of comm_exchange (24 B read + 24 B written per record, then K1 reads
+// the kept records again) is gone from the log path.  Regions hold mean + 6 sigma + 64 records; a skewed batch
+// that overflows one is re-routed with exact capacities by the route kernel (the counts are exact either way).
+gwo_status Handle::comm_route_args(int64_t n, LogRoute *rt, bool *on) {
+    Comm &C = *comm;
+    const int P = route_ranks(C);
+    *on = P > 1;
+    if (!*on) return GWO_OK;
+    GWO_TRY(ensure_buf(C.counts, (size_t)2 * P * 8 + 16));
+    if (!C.cursor.ptr) {
+        GWO_TRY(ensure_buf(C.cursor, std::max(route_cursor_bytes(), (size_t)LOG_RT_MAX * LOG_CUR_STRIDE * 8)));
+        GWO_TRY(hipcheck(hipMemsetAsync(C.cursor.ptr, 0, C.cursor.bytes, stream), "route cursors"));
+    }
+    const double mean = (double)n / P;
+    C.rcap = (uint64_t)(mean + 6.0 * std::sqrt(mean) + 64.0);
+    GWO_TRY(ensure_buf(C.sendbuf, (size_t)P * C.rcap * 24 + 24));
+    *rt = LogRoute{};
+    rt->mode = 1;
+    rt->nranks = P;
+    rt->me = C.rank;
+    rt->send = (int64_t *)C.sendbuf.ptr;
+    rt->rcap = C.rcap;
+    rt->cursor = (unsigned long long *)C.cursor.ptr;
+    rt->count = (unsigned long long *)C.counts.ptr;
+    if (n == 0) GWO_TRY(hipcheck(hipMemsetAsync(C.counts.ptr, 0, (size_t)2 * P * 8, stream), "counts"));
+    return GWO_OK;
+}
+
+// Right behind the routed K1 (main stream): the comm stream may start once K1 has finished.
+gwo_status Handle::comm_mark_routed() {
+    return hipcheck(hipEventRecord(comm->ev_routed, stream), "event");
+}
+
+// After the routed K1 is queued: exchange the per-destination counts (RCCL, comm stream), bring them to the host
+// (the batch's one host round trip for the exchange), re-route on a region overflow, and queue the records'
+// exchange on the comm stream -- it runs while the main stream finishes this batch's own records.
+gwo_status Handle::comm_after_route(const int64_t *k, const int64_t *t, const int64_t *v, int64_t n) {
+    Comm &C = *comm;
+    const int P = route_ranks(C), me = C.rank;
+    const bool virt = C.vranks > 1;
+    unsigned long long *d_send = (unsigned long long *)C.counts.ptr, *d_recv = d_send + P;
+    if (n == 0) GWO_TRY(comm_mark_routed());   // (no K1 ran: the counts were zeroed on the main stream)
+    GWO_TRY(hipcheck(hipStreamWaitEvent(C.cs, C.ev_routed, 0), "event wait"));
+    if (!virt) {
+        GWO_TRY(nccl_ok(this, ncclGroupStart(), "group"));
+        for (int p = 0; p < P; ++p) {
+            if (p == me) continue;
+            GWO_TRY(nccl_ok(this, ncclSend(d_send + p, 1, ncclUint64, p, C.nc, C.cs), "send count"));
+            GWO_TRY(nccl_ok(this, ncclRecv(d_recv + p, 1, ncclUint64, p, C.nc, C.cs), "recv count"));
+        }
+        GWO_TRY(nccl_ok(this, ncclGroupEnd(), "group end"));
+    }
+    GWO_TRY(hipcheck(hipMemcpyAsync(C.h_counts, d_send, (size_t)(virt ? 1 : 2) * P * 8, hipMemcpyDeviceToHost, C.cs),
+                     "counts"));
+    GWO_TRY(hipcheck(hipStreamSynchronize(C.cs), "counts sync"));
+    if (virt)   // what this rank routes to virtual GPU p comes back to it "from p"
+        for (int p = 0; p < P; ++p) C.h_counts[P + p] = C.h_counts[p];
+    C.h_counts[me] = 0;       // (K1 never routes a record to its own GPU)
+    C.h_counts[P + me] = 0;
+    uint64_t cap = C.rcap, mx = 0;
+    for (int p = 0; p < P; ++p) mx = std::max<uint64_t>(mx, C.h_counts[p]);
+    if (mx > cap) {   // skewed keys: a region overflowed -- route the batch again with exact regions
+        cap = mx;
+        GWO_TRY(ensure_buf(C.sendbuf, (size_t)P * cap * 24 + 24));
+        launch_route(k, t, v, n, cfg.key_kind, cfg.max_parallelism, P, (unsigned long long *)C.cursor.ptr, cap,
+                     (int64_t *)C.sendbuf.ptr, stream);
+        launch_route_collect((unsigned long long *)C.cursor.ptr, P, d_recv, stream);   // (resets its cursors; the
+                                                                                        //  counts are known)
+        GWO_TRY(launch_ok("route"));
+        GWO_TRY(comm_mark_routed());
+        GWO_TRY(hipcheck(hipStreamWaitEvent(C.cs, C.ev_routed, 0), "event wait"));
+    }
+    std::vector<uint64_t> roff(P + 1, 0);
+    for (int p = 0; p < P; ++p) roff[p + 1] = roff[p] + C.h_counts[P + p];
+    const int64_t R = (int64_t)roff[P];
+    GWO_TRY(ensure_buf(C.recvbuf, R * 24 + 24));
+    const int64_t *sb = (const int64_t *)C.sendbuf.ptr;
+    prof_begin(GWO_KERNEL_EXCHANGE, C.cs);
+    GWO_TRY(nccl_ok(this, ncclGroupStart(), "group"));
+    for (int p = 0; p < P; ++p) {
+        if (p == me) continue;
+        const int peer = virt ? me : p;
+        const uint64_t sc = C.h_counts[p], rc = C.h_counts[P + p];
+        if (sc) GWO_TRY(nccl_ok(this, ncclSend(sb + 3 * (uint64_t)p * cap, 3 * sc, ncclInt64, peer, C.nc, C.cs), "send"));
+        if (rc)
+            GWO_TRY(nccl_ok(this, ncclRecv((int64_t *)C.recvbuf.ptr + 3 * roff[p], 3 * rc, ncclInt64, peer, C.nc, C.cs),
+                            "recv"));
+    }
+    GWO_TRY(nccl_ok(this, ncclGroupEnd(), "group end"));
+    prof_end(GWO_KERNEL_EXCHANGE, R, C.cs);
+    GWO_TRY(hipcheck(hipEventRecord(C.ev_recv, C.cs), "event"));
+    C.recv_n = R;
+    return GWO_OK;
+}
+
+void Handle::comm_received(const int64_t **aos, int64_t *rn) const {
+    *aos = (const int64_t *)comm->recvbuf.ptr;
+    *rn = comm->recv_n;
+}
+
 // The main stream waits for the exchange's receives (comm stream) before reading the received records.
 gwo_status Handle::comm_wait_received() {
-    if (comm->nranks == 1) return GWO_OK;
+    if (route_ranks(*comm) == 1) return GWO_OK;
     return hipcheck(hipStreamWaitEvent(stream, comm->ev_recv, 0), "exchange wait");
 }
 
@@ -237,7 +349,13 @@ extern "C" gwo_status gwo_comm_init(gwo_handle *hh, const uint8_t *id, int32_t n
     Comm *C = new Comm();
     C->nranks = nranks;
     C->rank = rank;
-    if (hipHostMalloc((void **)&C->h_counts, (size_t)2 * nranks * 8 + 16, hipHostMallocDefault) != hipSuccess ||
+    if (nranks == 1)
+        if (const char *e = getenv("GWO_COMM_VIRTUAL")) {   // bench/test rehearsal of a rank's data path at P GPUs
+            const int v = atoi(e);
+            C->vranks = v > 1 && v <= LOG_RT_MAX ? v : 0;
+        }
+    const int cranks = std::max(nranks, C->vranks);
+    if (hipHostMalloc((void **)&C->h_counts, (size_t)2 * cranks * 8 + 16, hipHostMallocDefault) != hipSuccess ||
         hipHostMalloc((void **)&C->h_wm, 16, hipHostMallocDefault) != hipSuccess) {
         delete C;
         return GWO_ERR_OUT_OF_MEMORY;

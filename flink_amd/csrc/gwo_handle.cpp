@@ -5,6 +5,7 @@
 #include <numeric>
 
 #include "gwo_handle.h"
+#include "gwo_log.h"
 
 namespace gwo {
 
@@ -212,6 +213,20 @@ gwo_status Handle::submit(const int64_t *key, const int64_t *ts, const void *val
     const int64_t *dk = nullptr, *dt = nullptr, *dv = nullptr;
     if (!comm && n == 0) return GWO_OK;
     if (n > 0) GWO_TRY(stage_inputs(key, ts, needs_value ? val : nullptr, n, &dk, &dt, &dv));
+    if (comm && logst) {
+        // log layout: K1 routes other GPUs' records while it partitions this one's (comm_route_args)
+        LogRoute rt{};
+        bool routed = false;
+        GWO_TRY(comm_route_args(n, &rt, &routed));
+        if (!routed) return n ? insert_log(dk, dt, dv, n) : GWO_OK;   // one rank: nothing leaves this GPU
+        if (n > 0) GWO_TRY(insert_log(dk, dt, dv, n, 1, &rt));
+        else GWO_TRY(comm_after_route(dk, dt, dv, 0));
+        const int64_t *aos = nullptr;
+        int64_t rn = 0;
+        comm_received(&aos, &rn);
+        GWO_TRY(comm_wait_received());
+        return rn ? insert_log(aos, aos + 1, aos + 2, rn, 3) : GWO_OK;
+    }
     if (comm) {
         const int64_t *aos = nullptr, *loc = nullptr;
         int64_t rn = 0, ln = 0;

@@ -18,6 +18,8 @@
 
 struct LogThr;   // gwo_log.h
 
+struct LogRoute;       // gwo_log.h
+
 namespace gwo {
 
 // Checkpoint rows being restored, in host memory (gwo_snapshot.cpp).
@@ -286,7 +288,8 @@ struct Handle {
     gwo_status log_split_exact(long long base, int nunits, uint64_t cap, const uint64_t *counts, int tmpx);
     gwo_status log_split_dev(const LogJob &J, const unsigned long long *rbp);
     gwo_status log_resolve_split();
-    gwo_status insert_log(const int64_t *k, const int64_t *t, const int64_t *v, int64_t n, int64_t stride = 1);
+    gwo_status insert_log(const int64_t *k, const int64_t *t, const int64_t *v, int64_t n, int64_t stride = 1,
+                          const LogRoute *route = nullptr);
     gwo_status log_k1(LogJob &J, bool first_pass);
     LogThr log_thresholds(const LogJob &J) const;
     void log_uncarve(const LogJob &J, int w, uint64_t keep);
@@ -311,6 +314,12 @@ struct Handle {
     gwo_status comm_unpack(const int64_t *aos, int64_t n, const int64_t **rk, const int64_t **rt, const int64_t **rv);
     gwo_status comm_min_watermark(int64_t wm, int64_t *out);
     gwo_status comm_wait_received();
+    // keyBy routing fused into the log layout's K1 (gwo_comm.cpp): arguments of the batch's routed K1 (*on false:
+    // nothing to route -- one rank), the exchange after it, and the records received
+    gwo_status comm_route_args(int64_t n, LogRoute *rt, bool *on);
+    gwo_status comm_mark_routed();
+    gwo_status comm_after_route(const int64_t *k, const int64_t *t, const int64_t *v, int64_t n);
+    void comm_received(const int64_t **aos, int64_t *rn) const;
 
     void prof_begin(int k, hipStream_t s = nullptr);
     void prof_end(int k, int64_t items, hipStream_t s = nullptr);

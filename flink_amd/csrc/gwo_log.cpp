@@ -50,6 +50,7 @@ struct LogJob {
     uint64_t seg_cap[LOG_NU] = {};
     char *carve_at[LOG_NU] = {};  // start of the carved segment records
     char *carve_end[LOG_NU] = {}; // end of the carve (the window's chunk cursor right after it)
+    LogRoute rt{};               // multi-GPU: the first K1 routes other GPUs' records (mode 1), re-runs skip them (2)
 };
 
 struct LogState {
@@ -540,9 +541,13 @@ gwo_status Handle::log_k1(LogJob &J, bool first_pass) {
     prof_begin(GWO_KERNEL_INSERT);
     launch_log_part(J.k, J.t, J.v, J.n, J.stride, J.g, J.base, J.nunits, needs_value, L.d_cursor, J.cap,
                     (int64_t *)tmp.ptr, d_stats, (int64_t *)side_key.ptr, (int64_t *)side_ts.ptr,
-                    (int64_t *)side_val.ptr, d_side_count, side ? side_cap : 0, side, ca, thr, stream);
+                    (int64_t *)side_val.ptr, d_side_count, side ? side_cap : 0, side, ca, thr, J.rt, stream);
     GWO_TRY(launch_ok("log partition"));
     prof_end(GWO_KERNEL_INSERT, J.n);
+    if (J.rt.mode == 1) {   // routed once: the exchange may start behind this K1; re-runs skip other GPUs' records
+        GWO_TRY(comm_mark_routed());
+        J.rt.mode = 2;
+    }
     // The readback's own sequence word tells the host K1 is done; an event is recorded only behind the side-output
     // count copy (each event marker between K1 and pass 2 costs the stream ~5 us on MI355X, measured in the trace).
     L.rb_event[J.slot] = side;
@@ -720,9 +725,11 @@ gwo_status Handle::log_flush() {
     return log_resolve_k1(J);
 }
 
-gwo_status Handle::insert_log(const int64_t *k, const int64_t *t, const int64_t *v, int64_t n, int64_t stride) {
+gwo_status Handle::insert_log(const int64_t *k, const int64_t *t, const int64_t *v, int64_t n, int64_t stride,
+                              const LogRoute *route) {
     LogState &L = *logst;
     LogJob J;
+    if (route) J.rt = *route;
     J.k = k;
     J.t = t;
     J.v = v;
@@ -747,6 +754,8 @@ gwo_status Handle::insert_log(const int64_t *k, const int64_t *t, const int64_t 
     if (L.job.active && !pipe) GWO_TRY(log_flush());
     J.slot = L.free_slot();
     GWO_TRY(log_k1(J, true));
+    // multi-GPU: the exchange of the routed records is queued now, so it overlaps this batch's own records' work
+    if (route) GWO_TRY(comm_after_route(k, t, v, n));
     if (!pipe) return log_resolve_k1(J);
     LogJob prev = L.job;
     L.job = J;

@@ -106,6 +106,23 @@ struct CollectArgs {
     unsigned long long *done;    // K1 workgroups finished (the last one plans; it resets the counter)
 };
 
+// Multi-GPU keyBy routing fused into K1 (the log layout's first K1 over a batch): a record whose key group
+// belongs to another GPU -- computeOperatorIndexForKeyGroup(assignToKeyGroup(key)) != me,
+// KeyGroupRangeAssignment.java:118-119 -- is not classified here (its owner does that) but appended as a 24-B
+// {key, ts, value} record to that destination's send region; one reservation per (tile, destination).
+#define LOG_RT_MAX 256           // destinations (ranks) K1 routes to
+#define LOG_RT_B 1024            // K1 code of a routed record: bucket field LOG_RT_B + destination
+struct LogRoute {
+    int32_t mode;                // 0: no routing; 1: route remote records; 2: skip them (a re-run of a routed batch)
+    int32_t nranks;              // destinations
+    int32_t me;                  // this GPU's index: its records stay
+    int32_t pad;
+    int64_t *send;               // nranks regions of rcap {key, ts, value} records (region p at send + 3 * p * rcap)
+    uint64_t rcap;
+    unsigned long long *cursor;  // [nranks * LOG_CUR_STRIDE] region cursors (the tail moves them to count, zeroed)
+    unsigned long long *count;   // out: records routed per destination (above rcap: the region overflowed)
+};
+
 namespace gwo {
 // K1: classify + key-group check + late accounting + (window, coarse digit) grouping of a batch; its last
 // workgroup writes the readback block and the device plan of pass 2, and resets cursors and statistics.
@@ -115,7 +132,7 @@ void launch_log_part(const int64_t *key, const int64_t *ts, const int64_t *val, 
                      long long base, int nunits, int has_val, unsigned long long *cursor, uint64_t cap,
                      int64_t *tmp, BatchStats *st, int64_t *side_key, int64_t *side_ts, int64_t *side_val,
                      unsigned long long *side_count, long long side_cap, int side_enabled, const CollectArgs &ca,
-                     const LogThr &thr, hipStream_t s);
+                     const LogThr &thr, const LogRoute &rt, hipStream_t s);
 // Pass 2: every coarse bucket -> its window's segment, grouped by partition.  `overflow` is a
 // host-visible flag (set to 1 when a partition exceeds its capacity).  go != NULL: a speculative launch
 // of `nchunks` (an upper bound) workgroups that exits unless *go (K1's verdict) is set.

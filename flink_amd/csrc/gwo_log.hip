@@ -107,7 +107,7 @@ __device__ __forceinline__ unsigned long long block256_incl_scan64(unsigned long
 // is the batch's final plan -- no error, no bucket over its region capacity, the batch's first window inside
 // the launch's window range, every segment within its carved capacity -- else it exits and the host takes over.
 __device__ __forceinline__ void k1_plan_tail(unsigned long long *cursor, BatchStats *st, const CollectArgs &a,
-                                          long long base) {
+                                          long long base, const LogRoute &rt) {
     constexpr int SW = (int)(sizeof(BatchStats) / 8);
     static_assert(SW <= LOG_K1_THREADS, "statistics words");
     __shared__ unsigned long long s_sw[SW];
@@ -119,6 +119,9 @@ __device__ __forceinline__ void k1_plan_tail(unsigned long long *cursor, BatchSt
         s_bad = 0;
         s_maxreg = 0;
     }
+    if (rt.mode == 1)   // routed records per destination; the cursors start the next routed K1 at zero
+        for (int p = t; p < rt.nranks; p += LOG_K1_THREADS)
+            rt.count[p] = atomicExch(&rt.cursor[(size_t)p * LOG_CUR_STRIDE], 0ull);
     if (t < SW) {   // read-and-reset through the same device-scope atomics the workgroups used
         const unsigned long long reset = t == 0 ? 0x7fffffffffffffffull : (t == 1 ? 0x8000000000000000ull : 0ull);
         const unsigned long long w = atomicExch(&sw[t], reset);
@@ -202,12 +205,13 @@ __device__ __forceinline__ void k1_plan_tail(unsigned long long *cursor, BatchSt
 // records [(b * LOG_XG + x) * cap, ...), whose cursor cursor[(b * LOG_XG + x) * LOG_CUR_STRIDE] ends as its
 // record count (also when it exceeds cap: those records are not written and the host reruns).
 // ------------------------------------------------------------------------------------------------
-template <bool HASV, int S>   // S: record stride in int64 words (1: SoA columns, 3: {key, ts, value}; 0: runtime)
+// ROUTE: the multi-GPU instance (LogRoute): records of other GPUs are routed (rt.mode 1) or skipped (2).
+template <bool HASV, int S, bool ROUTE>   // S: record stride in int64 words (1: SoA columns, 3: {key, ts, value}; 0: runtime)
 __global__ __launch_bounds__(LOG_K1_THREADS) void log_part_kernel(
     const int64_t *__restrict__ key, const int64_t *__restrict__ ts, const int64_t *__restrict__ val, int64_t n,
     int64_t stride, WindowGeom g, long long base, int nunits, unsigned long long *__restrict__ cursor, uint64_t cap,
     int64_t *__restrict__ tmp, BatchStats *st, int64_t *side_key, int64_t *side_ts, int64_t *side_val,
-    unsigned long long *side_count, long long side_cap, int side_enabled, CollectArgs ca, LogThr th) {
+    unsigned long long *side_count, long long side_cap, int side_enabled, CollectArgs ca, LogThr th, LogRoute rt) {
     constexpr int W = HASV ? 2 : 1;
     // the new segments' partition counters (pass 2's cursors) start at zero: pass 2 follows in stream order
     for (int w = 0; w < ca.nunits; ++w) {
@@ -221,7 +225,10 @@ __global__ __launch_bounds__(LOG_K1_THREADS) void log_part_kernel(
     __shared__ uint32_t s_cnt[LOG_NU * LOG_ND];
     __shared__ uint32_t s_off[LOG_NU * LOG_ND];
     __shared__ long long s_min[LOG_K1_THREADS / 64], s_max[LOG_K1_THREADS / 64];
+    __shared__ uint32_t s_rcnt[ROUTE ? LOG_RT_MAX : 1];             // routed records per destination (tile)
+    __shared__ unsigned long long s_rbase[ROUTE ? LOG_RT_MAX : 1];  // their run's first record in the region
     const int nb = nunits * LOG_ND;
+    const int nr = ROUTE ? rt.nranks : 0;
     const int per = (nb + LOG_K1_THREADS - 1) / LOG_K1_THREADS;   // counters owned per thread (<= 4)
     const int tid = threadIdx.x;
     const int xg = blockIdx.x % LOG_XG;                           // region group (an XCD under round-robin placement)
@@ -245,6 +252,8 @@ __global__ __launch_bounds__(LOG_K1_THREADS) void log_part_kernel(
     if ((int64_t)blockIdx.x * LOG_TILE < n) load_tile((int64_t)blockIdx.x * LOG_TILE);
     for (int64_t tile = (int64_t)blockIdx.x * LOG_TILE; tile < n; tile += tstride) {
         for (int i = tid; i < nb; i += LOG_K1_THREADS) s_cnt[i] = 0;
+        if (ROUTE)
+            for (int i = tid; i < nr; i += LOG_K1_THREADS) s_rcnt[i] = 0;
         __syncthreads();
         uint32_t code[LOG_K1_PER];
 #pragma unroll
@@ -252,6 +261,13 @@ __global__ __launch_bounds__(LOG_K1_THREADS) void log_part_kernel(
             int64_t i = tile + j * LOG_K1_THREADS + tid;
             code[j] = 0xffffffffu;
             if (i >= n) continue;
+            if (ROUTE) {   // KeyGroupStreamPartitioner.selectChannel: another GPU's record is its owner's to classify
+                const int dest = (int)(key_group(kk[j], g.key_kind, g.max_par) * rt.nranks / g.max_par);
+                if (dest != rt.me) {
+                    if (rt.mode == 1) code[j] = ((uint32_t)(LOG_RT_B + dest) << 16) | atomicAdd(&s_rcnt[dest], 1u);
+                    continue;
+                }
+            }
             long long u = 0;
             int c;
             const int64_t t = tt[j];
@@ -265,7 +281,7 @@ __global__ __launch_bounds__(LOG_K1_THREADS) void log_part_kernel(
             }
             if (c == L_ACCEPT) {
                 int64_t k = kk[j];
-                if (!th.full_range) {
+                if (!ROUTE && !th.full_range) {   // (routed: a record kept here is in range by construction)
                     int32_t kg = key_group(k, g.key_kind, g.max_par);
                     if (kg < g.kg_lo || kg > g.kg_hi) {
                         bad_kg++;
@@ -309,12 +325,32 @@ __global__ __launch_bounds__(LOG_K1_THREADS) void log_part_kernel(
             const uint32_t c = (q < per && b < nb) ? s_cnt[b] : 0u;
             at[q] = c ? atomicAdd(&cursor[((size_t)b * LOG_XG + xg) * LOG_CUR_STRIDE], (unsigned long long)c) : 0ull;
         }
+        unsigned long long rat = 0;
+        if (ROUTE && rt.mode == 1 && tid < nr) {
+            const uint32_t c = s_rcnt[tid];
+            rat = c ? atomicAdd(&rt.cursor[(size_t)tid * LOG_CUR_STRIDE], (unsigned long long)c) : 0ull;
+        }
         uint32_t loc[4];
         const uint32_t total = tile_offsets(s_cnt, s_off, nb, loc, per);
+        if (ROUTE && rt.mode == 1) {
+            if (tid < nr) s_rbase[tid] = rat;
+            __syncthreads();
+        }
 #pragma unroll
         for (int j = 0; j < LOG_K1_PER; ++j) {
             if (code[j] == 0xffffffffu) continue;
             uint32_t b = code[j] >> 16;
+            if (ROUTE && b >= LOG_RT_B) {   // routed: straight from registers into the destination's run
+                const uint32_t d = b - LOG_RT_B;
+                const unsigned long long q = s_rbase[d] + (code[j] & 0xffffu);
+                if (q < rt.rcap) {
+                    int64_t *dst = rt.send + ((uint64_t)d * rt.rcap + q) * 3;
+                    dst[0] = kk[j];
+                    dst[1] = tt[j];
+                    dst[2] = HASV ? vv[j] : 0;
+                }
+                continue;
+            }
             uint32_t pos = s_off[b] + (code[j] & 0xffffu);
             if (HASV) {
                 ll2 r2 = {kk[j], vv[j]};
@@ -380,7 +416,11 @@ __global__ __launch_bounds__(LOG_K1_THREADS) void log_part_kernel(
     __syncthreads();
     if (tid == 0) s_last = atomicAdd(ca.done, 1ull) == (unsigned long long)(gridDim.x - 1);
     __syncthreads();
-    if (s_last) k1_plan_tail(cursor, st, ca, base);
+    if (s_last) {
+        LogRoute r = rt;
+        if (!ROUTE) r.mode = 0;
+        k1_plan_tail(cursor, st, ca, base, r);
+    }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1195,21 +1235,24 @@ void launch_log_part(const int64_t *key, const int64_t *ts, const int64_t *val, 
                      long long base, int nunits, int has_val, unsigned long long *cursor, uint64_t cap,
                      int64_t *tmp, BatchStats *st, int64_t *side_key, int64_t *side_ts, int64_t *side_val,
                      unsigned long long *side_count, long long side_cap, int side_enabled, const CollectArgs &ca,
-                     const LogThr &thr, hipStream_t s) {
+                     const LogThr &thr, const LogRoute &rt, hipStream_t s) {
     int64_t grid = (n + LOG_TILE - 1) / LOG_TILE;
     grid = grid < 1 ? 1 : (grid > LOG_K1_GRID ? LOG_K1_GRID : grid);
-#define GWO_K1(HV, S)                                                                                          \
-    hipLaunchKernelGGL((log_part_kernel<HV, S>), dim3((int)grid), dim3(LOG_K1_THREADS), 0, s, key, ts, val, n, \
-                       stride, g, base, nunits, cursor, cap, tmp, st, side_key, side_ts, side_val, side_count,   \
-                       side_cap, side_enabled, ca, thr)
-    if (has_val) {
-        if (stride == 1) GWO_K1(true, 1);
-        else if (stride == 3) GWO_K1(true, 3);
-        else GWO_K1(true, 0);
+#define GWO_K1(HV, S, R)                                                                                       \
+    hipLaunchKernelGGL((log_part_kernel<HV, S, R>), dim3((int)grid), dim3(LOG_K1_THREADS), 0, s, key, ts, val, \
+                       n, stride, g, base, nunits, cursor, cap, tmp, st, side_key, side_ts, side_val, side_count, \
+                       side_cap, side_enabled, ca, thr, rt)
+    if (rt.mode != 0 && stride == 1) {   // routing: the first K1 over a batch's own columns
+        if (has_val) GWO_K1(true, 1, true);
+        else GWO_K1(false, 1, true);
+    } else if (has_val) {
+        if (stride == 1) GWO_K1(true, 1, false);
+        else if (stride == 3) GWO_K1(true, 3, false);
+        else GWO_K1(true, 0, false);
     } else {
-        if (stride == 1) GWO_K1(false, 1);
-        else if (stride == 3) GWO_K1(false, 3);
-        else GWO_K1(false, 0);
+        if (stride == 1) GWO_K1(false, 1, false);
+        else if (stride == 3) GWO_K1(false, 3, false);
+        else GWO_K1(false, 0, false);
     }
 #undef GWO_K1
 }

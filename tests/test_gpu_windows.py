@@ -527,6 +527,34 @@ def test_comm_single_rank_matches_oracle(F, layout):
     op.close()
 
 
+@pytest.mark.parametrize("vranks,maxp,hot", [(2, 128, False), (3, 32768, False), (8, 32768, False), (8, 128, True)])
+def test_comm_virtual_ranks_log_route_matches_oracle(F, monkeypatch, vranks, maxp, hot):
+    """The log layout's routed K1 (keyBy routing fused into the partition kernel): GWO_COMM_VIRTUAL=P makes a
+    1-rank communicator route as GPU 0 of P -- the other GPUs' records leave through RCCL (to this rank itself)
+    and come back as received records, so every record takes a rank's real multi-GPU data path once.  hot: one
+    key carries half the records, overflowing its destination's send region (exact re-route)."""
+    import ctypes as C
+    from flink_amd import _native as N
+    lib = N.lib()
+    k, t, v, b = _c1(n=300_000, nkeys=20_000, every=20_000)
+    if hot:
+        k = k.copy()
+        k[::2] = 12345
+    agg = F.MultiAggregate(F.SumAggregate(), F.MinAggregate(), F.MaxAggregate())
+    op = F.GpuWindowOperator(F.TumblingEventTimeWindows.of(5000), agg, state_layout="log", max_parallelism=maxp)
+    uid = (C.c_uint8 * N.COMM_ID_BYTES)()
+    N.check(lib.gwo_comm_unique_id(uid))
+    monkeypatch.setenv("GWO_COMM_VIRTUAL", str(vranks))
+    N.check(lib.gwo_comm_init(op.handle, uid, 1, 0), op.handle, "gwo_comm_init")
+    monkeypatch.delenv("GWO_COMM_VIRTUAL")
+    _run_batches(op, k, t, v, b)
+    (wk, ws, we, res), late = V.tumbling_lateness0(k, t, v, _final(b), 5000, 0, [1, 2, 3])
+    got = sorted((a, s, e, *r) for a, s, e, r in op.output)
+    assert got == _want(wk, ws, we, res)
+    assert op.num_late_records_dropped == late
+    op.close()
+
+
 def test_comm_rejects_wrong_key_group_range(F):
     """With a communicator the handle's range must be its rank's computeKeyGroupRangeForOperatorIndex."""
     import ctypes as C
