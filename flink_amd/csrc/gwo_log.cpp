@@ -74,7 +74,8 @@ struct LogState {
     unsigned *h_split_flag = nullptr;            // pinned, device-written [LOG_SLOTS]: pass-2 overflow flags
     unsigned *d_split_flag = nullptr;            // device view of h_split_flag
     unsigned *d_go = nullptr;                    // [LOG_SLOTS] K1's verdict on the speculative pass 2
-    unsigned long long *d_done = nullptr;        // K1 workgroups finished (reset by the last one)
+    unsigned long long *d_done = nullptr;        // K1 arrival counters (LOG_DONE_WORDS; reset by the last one)
+    unsigned long long *d_k1sh = nullptr;        // K1 statistics shards (reset by the last one)
     // pipelined submission (gwo_set_pipelined_submit): the batch whose K1 is in flight, resolved by the
     // next call on the handle
     bool pipeline = false;
@@ -132,8 +133,17 @@ gwo_status Handle::log_init() {
     GWO_TRY(dalloc((void **)&L.d_overflow, 16));
     GWO_TRY(hipcheck(hipMemsetAsync(L.d_overflow, 0, 16, stream), "overflow"));
     GWO_TRY(dalloc((void **)&L.d_go, LOG_SLOTS * sizeof(unsigned)));
-    GWO_TRY(dalloc((void **)&L.d_done, 8));
-    GWO_TRY(hipcheck(hipMemsetAsync(L.d_done, 0, 8, stream), "done"));
+    GWO_TRY(dalloc((void **)&L.d_done, LOG_DONE_WORDS * 8));
+    GWO_TRY(hipcheck(hipMemsetAsync(L.d_done, 0, LOG_DONE_WORDS * 8, stream), "done"));
+    {
+        std::vector<unsigned long long> sh((size_t)LOG_SHARDS * LOG_CUR_STRIDE, 0ull);
+        for (int q = 0; q < LOG_SHARDS; ++q) {
+            sh[(size_t)q * LOG_CUR_STRIDE + K1S_MIN] = 0x7fffffffffffffffull;
+            sh[(size_t)q * LOG_CUR_STRIDE + K1S_MAX] = 0x8000000000000000ull;
+        }
+        GWO_TRY(dalloc((void **)&L.d_k1sh, sh.size() * 8));
+        GWO_TRY(hipcheck(hipMemcpy(L.d_k1sh, sh.data(), sh.size() * 8, hipMemcpyHostToDevice), "K1 shards"));
+    }
     // written by kernels, read by the host after an event: coherent, mapped
     GWO_TRY(hipcheck(hipHostMalloc((void **)&L.h_rb, kRbBytes * LOG_SLOTS, hipHostMallocCoherent | hipHostMallocMapped),
                      "pinned"));
@@ -214,6 +224,7 @@ void Handle::log_free() {
     if (L.d_overflow) (void)hipFree(L.d_overflow);
     if (L.d_go) (void)hipFree(L.d_go);
     if (L.d_done) (void)hipFree(L.d_done);
+    if (L.d_k1sh) (void)hipFree(L.d_k1sh);
     if (L.h_rb) (void)hipHostFree(L.h_rb);
     if (L.h_buckets) (void)hipHostFree(L.h_buckets);
     delete logst;
@@ -501,6 +512,7 @@ gwo_status Handle::log_k1(LogJob &J, bool first_pass) {
     ca.go = L.d_go + J.slot;
     ca.rb = L.rb_dev(J.slot);
     ca.done = L.d_done;
+    ca.shard = L.d_k1sh;
     ca.seq = J.seq = ++L.seq;
     ca.spec = J.spec ? 1 : 0;
     for (int w = 0; w < J.nunits; ++w) {

@@ -103,8 +103,17 @@ struct CollectArgs {
     unsigned *go;                // out: 1 = the queued speculative pass 2 runs the plan, 0 = it exits
     unsigned long long *rb;      // out: readback block (pinned host memory)
     unsigned long long seq;      // written to rb[LOG_RB_SEQ] after every other readback word
-    unsigned long long *done;    // K1 workgroups finished (the last one plans; it resets the counter)
+    unsigned long long *done;    // K1 workgroups finished: shard counters [LOG_SHARDS * LOG_CUR_STRIDE], then the
+                                 // count of finished shards at done[LOG_SHARDS * LOG_CUR_STRIDE] (the last plans)
+    unsigned long long *shard;   // [LOG_SHARDS * LOG_CUR_STRIDE] K1 statistics shards (K1_SW words each, one line)
 };
+
+// K1's statistics: every workgroup reduces its counters in LDS and folds them into shard blockIdx % LOG_SHARDS
+// (device-scope atomics on the same address serialise at ~12 ns each on MI355X: 4 per-wave atomics per
+// workgroup on one word cost ~25 us at the end of a 512-workgroup launch); the tail folds the shards.
+#define LOG_SHARDS 16
+enum : int { K1S_MIN = 0, K1S_MAX, K1S_ACC, K1S_LATE, K1S_REFIRE, K1S_BADTS, K1S_BADKG, K1S_HOUT, K1_SW };
+static constexpr size_t LOG_DONE_WORDS = (LOG_SHARDS + 1) * LOG_CUR_STRIDE;
 
 // Multi-GPU keyBy routing fused into K1 (the log layout's first K1 over a batch): a record whose key group
 // belongs to another GPU -- computeOperatorIndexForKeyGroup(assignToKeyGroup(key)) != me,

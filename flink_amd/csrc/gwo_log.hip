@@ -109,7 +109,8 @@ __device__ __forceinline__ unsigned long long block256_incl_scan64(unsigned long
 __device__ __forceinline__ void k1_plan_tail(unsigned long long *cursor, BatchStats *st, const CollectArgs &a,
                                           long long base, const LogRoute &rt) {
     constexpr int SW = (int)(sizeof(BatchStats) / 8);
-    static_assert(SW <= LOG_K1_THREADS, "statistics words");
+    constexpr int K1_T0 = LOG_K1_THREADS - 32, K1_T1 = K1_T0 + K1_SW;   // threads past the statistics words
+    static_assert(SW <= K1_T0 && K1_T1 + LOG_SHARDS + 1 <= LOG_K1_THREADS, "statistics words");
     __shared__ unsigned long long s_sw[SW];
     __shared__ unsigned s_bad;
     __shared__ unsigned long long s_maxreg;
@@ -122,13 +123,39 @@ __device__ __forceinline__ void k1_plan_tail(unsigned long long *cursor, BatchSt
     if (rt.mode == 1)   // routed records per destination; the cursors start the next routed K1 at zero
         for (int p = t; p < rt.nranks; p += LOG_K1_THREADS)
             rt.count[p] = atomicExch(&rt.cursor[(size_t)p * LOG_CUR_STRIDE], 0ull);
+    __shared__ unsigned long long s_k1[K1_SW];
     if (t < SW) {   // read-and-reset through the same device-scope atomics the workgroups used
         const unsigned long long reset = t == 0 ? 0x7fffffffffffffffull : (t == 1 ? 0x8000000000000000ull : 0ull);
-        const unsigned long long w = atomicExch(&sw[t], reset);
-        s_sw[t] = w;
-        a.rb[LOG_RB_STATS + t] = w;
+        s_sw[t] = atomicExch(&sw[t], reset);
+    } else if (t >= K1_T0 && t < K1_T0 + K1_SW) {   // fold (and reset) the statistics shards
+        const int f = t - K1_T0;
+        const unsigned long long init =
+            f == K1S_MIN ? 0x7fffffffffffffffull : (f == K1S_MAX ? 0x8000000000000000ull : 0ull);
+        unsigned long long r = init;
+        for (int q = 0; q < LOG_SHARDS; ++q) {
+            const unsigned long long x = atomicExch(&a.shard[q * LOG_CUR_STRIDE + f], init);
+            if (f == K1S_MIN) r = (long long)x < (long long)r ? x : r;
+            else if (f == K1S_MAX) r = (long long)x > (long long)r ? x : r;
+            else r += x;
+        }
+        s_k1[f] = r;
+    } else if (t >= K1_T1 && t < K1_T1 + LOG_SHARDS + 1) {   // arrival counters start the next K1 at zero
+        atomicExch(&a.done[(t - K1_T1) * LOG_CUR_STRIDE], 0ull);
     }
     __syncthreads();
+    if (t == 0) {
+        BatchStats &W = *(BatchStats *)s_sw;
+        W.min_idx = (long long)s_k1[K1S_MIN];
+        W.max_idx = (long long)s_k1[K1S_MAX];
+        W.accepted = s_k1[K1S_ACC];
+        W.late = s_k1[K1S_LATE];
+        W.refire = s_k1[K1S_REFIRE];
+        W.bad_ts = s_k1[K1S_BADTS];
+        W.bad_kg = s_k1[K1S_BADKG];
+        W.hist_out = s_k1[K1S_HOUT];
+    }
+    __syncthreads();
+    if (t < SW) a.rb[LOG_RB_STATS + t] = s_sw[t];
     const BatchStats &S = *(const BatchStats *)s_sw;
     unsigned long long chunk_run = 0;
     unsigned bad = 0;
@@ -188,7 +215,6 @@ __device__ __forceinline__ void k1_plan_tail(unsigned long long *cursor, BatchSt
         *a.go = go ? 1u : 0u;
         a.rb[LOG_RB_GO] = go ? 1ull : 0ull;
         a.rb[LOG_RB_MAXREG] = s_maxreg;
-        *a.done = 0;   // the next K1 launch counts from zero (stream order)
     }
     // the host spins on the sequence word: every other readback word must be visible first
     __threadfence_system();
@@ -224,7 +250,6 @@ __global__ __launch_bounds__(LOG_K1_THREADS) void log_part_kernel(
     __shared__ uint16_t s_bk[LOG_TILE];
     __shared__ uint32_t s_cnt[LOG_NU * LOG_ND];
     __shared__ uint32_t s_off[LOG_NU * LOG_ND];
-    __shared__ long long s_min[LOG_K1_THREADS / 64], s_max[LOG_K1_THREADS / 64];
     __shared__ uint32_t s_rcnt[ROUTE ? LOG_RT_MAX : 1];             // routed records per destination (tile)
     __shared__ unsigned long long s_rbase[ROUTE ? LOG_RT_MAX : 1];  // their run's first record in the region
     const int nb = nunits * LOG_ND;
@@ -232,7 +257,8 @@ __global__ __launch_bounds__(LOG_K1_THREADS) void log_part_kernel(
     const int per = (nb + LOG_K1_THREADS - 1) / LOG_K1_THREADS;   // counters owned per thread (<= 4)
     const int tid = threadIdx.x;
     const int xg = blockIdx.x % LOG_XG;                           // region group (an XCD under round-robin placement)
-    long long mn = 0x7fffffffffffffffLL, mx = (long long)0x8000000000000000LL;
+    long long mn = 0x7fffffffffffffffLL, mx = (long long)0x8000000000000000LL;   // accepted windows (slow path)
+    uint32_t wmask = 0;   // launch windows (bit jj) the inline path accepted records into
     unsigned acc = 0, late = 0, refire = 0, bad_ts = 0, out = 0, bad_kg = 0;   // per thread: < 2^32 records
     int64_t kk[LOG_K1_PER], vv[LOG_K1_PER], tt[LOG_K1_PER];
     // unconditional loads of a tile (lanes past the end re-read the tile's first record and are
@@ -256,9 +282,10 @@ __global__ __launch_bounds__(LOG_K1_THREADS) void log_part_kernel(
             for (int i = tid; i < nr; i += LOG_K1_THREADS) s_rcnt[i] = 0;
         __syncthreads();
         uint32_t code[LOG_K1_PER];
+        uint32_t slow = 0;   // bit j: record j is classified out of line (below)
 #pragma unroll
         for (int j = 0; j < LOG_K1_PER; ++j) {
-            int64_t i = tile + j * LOG_K1_THREADS + tid;
+            const int64_t i = tile + j * LOG_K1_THREADS + tid;
             code[j] = 0xffffffffu;
             if (i >= n) continue;
             if (ROUTE) {   // KeyGroupStreamPartitioner.selectChannel: another GPU's record is its owner's to classify
@@ -268,21 +295,41 @@ __global__ __launch_bounds__(LOG_K1_THREADS) void log_part_kernel(
                     continue;
                 }
             }
-            long long u = 0;
-            int c;
+            // the common case, inline: a timestamp inside one of the launch's windows and that window open --
+            // WindowOperator.java:386-427 decided once per window (LogThr), a few compares per record
             const int64_t t = tt[j];
-            if (th.ok && t >= th.bound[0] && t < th.bound[nunits]) {   // within the launch's windows
-                const int jj = (t >= th.bound[1]) + (t >= th.bound[2]) + (t >= th.bound[3]);
-                const uint32_t cc = (th.cls >> (2 * jj)) & 3u;
-                c = cc == 0 ? L_ACCEPT : (cc == 2 ? L_REFIRE : (jadd(t, g.lateness) <= g.wm ? L_LATE : L_SKIP));
-                u = base + jj;
-            } else {
-                c = log_classify(t, g, u);
+            const int jj = (t >= th.bound[1]) + (t >= th.bound[2]) + (t >= th.bound[3]);
+            if (!(th.ok && t >= th.bound[0] && t < th.bound[nunits] && ((th.cls >> (2 * jj)) & 3u) == 0)) {
+                slow |= 1u << j;
+                continue;
             }
+            const int64_t k = kk[j];
+            if (!ROUTE && !th.full_range) {   // (routed: a record kept here is in range by construction)
+                const int32_t kg = key_group(k, g.key_kind, g.max_par);
+                if (kg < g.kg_lo || kg > g.kg_hi) {
+                    bad_kg++;
+                    atomicExch((unsigned long long *)&st->bad_kg_key, (unsigned long long)k);
+                }
+            }
+            acc++;
+            wmask |= 1u << jj;
+            const uint32_t b = (uint32_t)(jj * LOG_ND + (int)(digit_hash(k) >> (32 - LOG_DB)));
+            code[j] = (b << 16) | atomicAdd(&s_cnt[b], 1u);
+        }
+        // everything else (late, re-fire and out-of-range records, Long.MIN_VALUE timestamps, extreme windows):
+        // reloaded and classified in full by log_classify, one record at a time, outside the unrolled loop
+#pragma unroll 1
+        while (slow) {
+            const int j = __builtin_ctz(slow);
+            slow &= slow - 1;
+            const int64_t i = tile + j * LOG_K1_THREADS + tid;
+            const int64_t o = S ? i * S : i * stride;
+            const int64_t t = ts[o], k = key[o];
+            long long u = 0;
+            const int c = log_classify(t, g, u);
             if (c == L_ACCEPT) {
-                int64_t k = kk[j];
-                if (!ROUTE && !th.full_range) {   // (routed: a record kept here is in range by construction)
-                    int32_t kg = key_group(k, g.key_kind, g.max_par);
+                if (!ROUTE && !th.full_range) {
+                    const int32_t kg = key_group(k, g.key_kind, g.max_par);
                     if (kg < g.kg_lo || kg > g.kg_hi) {
                         bad_kg++;
                         atomicExch((unsigned long long *)&st->bad_kg_key, (unsigned long long)k);
@@ -291,22 +338,24 @@ __global__ __launch_bounds__(LOG_K1_THREADS) void log_part_kernel(
                 acc++;
                 mn = u < mn ? u : mn;
                 mx = u > mx ? u : mx;
-                long long w = u - base;
-                if (w >= 0 && w < nunits) {
-                    uint32_t b = (uint32_t)(w * LOG_ND + (int)(digit_hash(k) >> (32 - LOG_DB)));
-                    uint32_t r = atomicAdd(&s_cnt[b], 1u);
-                    code[j] = (b << 16) | r;
+                const long long w = u - base;
+                if (w >= 0 && w < nunits) {   // only without valid window bounds (th.ok == 0)
+                    const uint32_t b = (uint32_t)(w * LOG_ND + (int)(digit_hash(k) >> (32 - LOG_DB)));
+                    const uint32_t cd = (b << 16) | atomicAdd(&s_cnt[b], 1u);
+#pragma unroll
+                    for (int q = 0; q < LOG_K1_PER; ++q)   // code[j] without a run-time register index
+                        if (q == j) code[q] = cd;
                 } else {
                     out++;
                 }
             } else if (c == L_LATE) {
                 late++;
                 if (side_enabled) {
-                    unsigned long long pos = atomicAdd(side_count, 1ull);
+                    const unsigned long long pos = atomicAdd(side_count, 1ull);
                     if ((long long)pos < side_cap) {
-                        side_key[pos] = kk[j];
-                        side_ts[pos] = tt[j];
-                        side_val[pos] = HASV ? vv[j] : (val ? val[i * stride] : 0);
+                        side_key[pos] = k;
+                        side_ts[pos] = t;
+                        side_val[pos] = val ? val[o] : 0;
                     }
                 }
             } else if (c == L_REFIRE) {
@@ -379,42 +428,62 @@ __global__ __launch_bounds__(LOG_K1_THREADS) void log_part_kernel(
         }
         __syncthreads();
     }
+    if (wmask) {
+        const long long lo = base + __builtin_ctz(wmask), hi = base + 31 - __builtin_clz(wmask);
+        mn = lo < mn ? lo : mn;
+        mx = hi > mx ? hi : mx;
+    }
+    // workgroup statistics -> shard blockIdx % LOG_SHARDS (zero words skipped)
+    unsigned long long v[K1_SW] = {(unsigned long long)mn, (unsigned long long)mx, acc, late, refire, bad_ts, bad_kg,
+                                   out};
+#pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
-        long long a = __shfl_xor(mn, o), b = __shfl_xor(mx, o);
-        mn = a < mn ? a : mn;
-        mx = b > mx ? b : mx;
+        const long long a = __shfl_xor((long long)v[K1S_MIN], o), b = __shfl_xor((long long)v[K1S_MAX], o);
+        v[K1S_MIN] = a < (long long)v[K1S_MIN] ? (unsigned long long)a : v[K1S_MIN];
+        v[K1S_MAX] = b > (long long)v[K1S_MAX] ? (unsigned long long)b : v[K1S_MAX];
+#pragma unroll
+        for (int f = K1S_ACC; f < K1_SW; ++f) v[f] += __shfl_xor(v[f], o);
     }
-    wave_atomic_add(&st->accepted, acc);
-    wave_atomic_add(&st->late, late);
-    wave_atomic_add(&st->refire, refire);
-    wave_atomic_add(&st->bad_ts, bad_ts);
-    wave_atomic_add(&st->hist_out, out);
-    wave_atomic_add(&st->bad_kg, bad_kg);
+    __shared__ unsigned long long s_st[LOG_K1_THREADS / 64][K1_SW];
     const int lane = tid & 63, wid = tid >> 6;
-    if (lane == 0) {
-        s_min[wid] = mn;
-        s_max[wid] = mx;
-    }
+    if (lane == 0)
+#pragma unroll
+        for (int f = 0; f < K1_SW; ++f) s_st[wid][f] = v[f];
     __syncthreads();
-    if (tid == 0) {
-        long long a = s_min[0], b = s_max[0];
+    if (tid < K1_SW) {
+        unsigned long long r = s_st[0][tid];
         for (int w = 1; w < LOG_K1_THREADS / 64; ++w) {
-            a = s_min[w] < a ? s_min[w] : a;
-            b = s_max[w] > b ? s_max[w] : b;
+            const unsigned long long x = s_st[w][tid];
+            if (tid == K1S_MIN) r = (long long)x < (long long)r ? x : r;
+            else if (tid == K1S_MAX) r = (long long)x > (long long)r ? x : r;
+            else r += x;
         }
-        if (a != 0x7fffffffffffffffLL) {
-            atomicMin(&st->min_idx, a);
-            atomicMax(&st->max_idx, b);
+        unsigned long long *sh = ca.shard + (blockIdx.x % LOG_SHARDS) * LOG_CUR_STRIDE + tid;
+        if (tid == K1S_MIN) {
+            if ((long long)r != 0x7fffffffffffffffLL) atomicMin((long long *)sh, (long long)r);
+        } else if (tid == K1S_MAX) {
+            if ((long long)r != (long long)0x8000000000000000LL) atomicMax((long long *)sh, (long long)r);
+        } else if (r) {
+            atomicAdd(sh, r);
         }
     }
     // the last workgroup to finish plans pass 2: every workgroup's atomics are complete before its arrival
-    // is counted (each wave drains its memory operations).  Everything the tail reads was written by
-    // device-scope read-modify-write atomics, coherent across XCDs; the records reach pass 2 through the kernel
-    // boundary -- so no release fence, which on gfx950 writes back the XCD's whole L2 once per workgroup.
+    // is counted (each wave drains its memory operations).  Arrivals are counted per shard; the last arrival of
+    // a shard counts the shard.  Everything the tail reads was written by device-scope read-modify-write
+    // atomics, coherent across XCDs; the records reach pass 2 through the kernel boundary -- so no release
+    // fence, which on gfx950 writes back the XCD's whole L2 once per workgroup.
     __shared__ int s_last;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (tid == 0) s_last = atomicAdd(ca.done, 1ull) == (unsigned long long)(gridDim.x - 1);
+    if (tid == 0) {
+        const unsigned sh = blockIdx.x % LOG_SHARDS;
+        const unsigned members = (gridDim.x - sh + LOG_SHARDS - 1) / LOG_SHARDS;
+        const unsigned nsh = gridDim.x < LOG_SHARDS ? gridDim.x : LOG_SHARDS;
+        bool last = false;
+        if (atomicAdd(&ca.done[sh * LOG_CUR_STRIDE], 1ull) == members - 1)
+            last = atomicAdd(&ca.done[LOG_SHARDS * LOG_CUR_STRIDE], 1ull) == nsh - 1;
+        s_last = last;
+    }
     __syncthreads();
     if (s_last) {
         LogRoute r = rt;
