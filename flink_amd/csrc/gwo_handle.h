@@ -146,6 +146,7 @@ struct Handle {
     int use_preagg = 1;
     int use_combine = 1;                       // GWO_COMBINE=0: the two-pass scan + insert path only
     int cb_cus = 0;
+    int cb_max_wg = 0;                                 // gather workgroups at most (GWO_CB_WG; default 4 per CU)
     DevBuf cb_dump_key, cb_dump_acc, cb_ovf, cb_blk, cb_ctr, cb_dir;   // combine path scratch (insert_combined)
     unsigned long long *cb_rb = nullptr, *cb_rb_dev = nullptr;        // host-mapped readback block
     unsigned long long cb_seq = 0;

@@ -338,7 +338,9 @@ __global__ __launch_bounds__(256) void insert_preagg_kernel(const int64_t *__res
 // Combine path (table layout, low-cardinality batches such as YSB's 1K campaigns): the scan and the
 // pre-aggregated insert as ONE pass over the records plus a merge, with the host's checks in between.
 //   gather  persistent workgroups: every record is classified (the scan's statistics, histogram, side
-//           output, key-group check) and folded into the workgroup's LDS table of units hint and hint + 1
+//           output, key-group check); a wave first folds runs of lanes holding one (unit, key) into one lane
+//           (ballot + masked wave reduction: hot keys), then every record is folded into the workgroup's LDS
+//           table of units hint and hint + 1
 //           (key-indexed, accumulators preset to the identity, so a claim is one CAS of the key word); the
 //           table is then dumped densely per workgroup.  Records of other units, of a full table or with
 //           the empty-key marker are listed for the merge.  Statistics go to a per-workgroup slot and the
@@ -358,9 +360,33 @@ __global__ __launch_bounds__(256) void insert_preagg_kernel(const int64_t *__res
 #define CB_TILE (CB_THREADS * CB_PER)
 #define CB_MERGE_RUN 8
 #define CB_SHARDS 16      // statistics shards (gather)
-#ifndef CB_XP
-#define CB_XP 0   // experiment ablations (exp/cbbench): 1 no LDS fold, 2 no tail, 4 no dump, 8 no key group
-#endif
+#define CB_HOT 8          // lanes of one (unit, key) in a wave that take the wave pre-reduction
+
+// The workgroup's LDS table of one unit (S slots, key-indexed): the slot holding k, claimed if absent; -1 when
+// 32 probes found no room (the record is listed for the merge).  Two 32-bit multiplies place a key: the table
+// is private to the pass, any spread will do.
+__device__ __forceinline__ int lds_slot(int64_t *kb, int S, int sbits, int64_t k) {
+    uint32_t sl = ((uint32_t)k * 0x9E3779B1u ^ (uint32_t)((uint64_t)k >> 32) * 0x85EBCA77u) >> (32 - sbits);
+    for (int probe = 0; probe < 32; ++probe) {
+        int64_t cur = kb[sl];
+        if (cur == GWO_EMPTY_KEY) {
+            cur = (int64_t)atomicCAS((unsigned long long *)&kb[sl], (unsigned long long)GWO_EMPTY_KEY,
+                                     (unsigned long long)k);
+            if (cur == GWO_EMPTY_KEY) return (int)sl;
+        }
+        if (cur == k) return (int)sl;
+        sl = (sl + 1) & (uint32_t)(S - 1);
+    }
+    return -1;
+}
+
+// x folded over the 64 lanes of the wave with the word's monoid (every lane gets the result; lanes that do
+// not take part pass the identity).  Float sums are re-associated: within the 1e-6 relative bound.
+__device__ __forceinline__ int64_t wave_fold(int op, int64_t x) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) x = combine(op, x, __shfl_xor(x, o));
+    return x;
+}
 
 enum : int { CS_ACC = 0, CS_LATE, CS_REFIRE, CS_BADTS, CS_BADRANGE, CS_BADKG, CS_HOUT, CS_MIN, CS_MAX, CS_D0, CS_D1,
              CS_HIST = 16, CS_WORDS = CS_HIST + GWO_HIST_BINS };
@@ -386,16 +412,25 @@ __global__ __launch_bounds__(CB_THREADS) void gather_kernel(const int64_t *__res
     long long mn = 0x7fffffffffffffffLL, mx = (long long)0x8000000000000000LL;
     int run_b = -1;
     unsigned run_n = 0;
-    for (int64_t tile = (int64_t)blockIdx.x * CB_TILE; tile < n; tile += (int64_t)gridDim.x * CB_TILE) {
-        unsigned ovm = 0;   // records of this tile left to the merge (bit j: record tile + j * CB_THREADS + tid)
-        int64_t tt[CB_PER], kk[CB_PER];   // the tile's loads all in flight before any record is processed
+    // a tile's loads all in flight before any record is processed; the next tile's are issued once this tile's
+    // records are in LDS (workgroups loop over tiles when the launch has fewer workgroups than tiles)
+    int64_t tt[CB_PER], kk[CB_PER], vv[CB_PER];
+    auto load_tile = [&](int64_t tile) {
 #pragma unroll
         for (int j = 0; j < CB_PER; ++j) {
             int64_t i = tile + j * CB_THREADS + tid;
             i = i < n ? i : tile;
             tt[j] = __builtin_nontemporal_load(ts + i);
             kk[j] = __builtin_nontemporal_load(key + i);
+            vv[j] = val ? __builtin_nontemporal_load(val + i) : 0;
         }
+    };
+    const int64_t tstride = (int64_t)gridDim.x * CB_TILE;
+    if ((int64_t)blockIdx.x * CB_TILE < n) load_tile((int64_t)blockIdx.x * CB_TILE);
+    for (int64_t tile = (int64_t)blockIdx.x * CB_TILE; tile < n; tile += tstride) {
+        unsigned ovm = 0;   // records of this tile left to the merge (bit j: record tile + j * CB_THREADS + tid)
+        unsigned candm = 0;   // bit j: record j goes into the LDS table of unit cbu[j]
+        int cbu[CB_PER];
 #pragma unroll
         for (int j = 0; j < CB_PER; ++j) {
             const int64_t i = tile + j * CB_THREADS + tid;
@@ -430,7 +465,7 @@ __global__ __launch_bounds__(CB_THREADS) void gather_kernel(const int64_t *__res
                 acc++;
                 refire += c == REC_REFIRE;
                 const int64_t k = kk[j];
-                const int32_t kg = ((CB_XP & 8) || a.full_range) ? g.kg_lo : key_group(k, g.key_kind, g.max_par);
+                const int32_t kg = a.full_range ? g.kg_lo : key_group(k, g.key_kind, g.max_par);
                 if (kg < g.kg_lo || kg > g.kg_hi) {
                     bad_kg++;
                     atomicExch((unsigned long long *)&st->bad_kg_key, (unsigned long long)k);
@@ -448,32 +483,51 @@ __global__ __launch_bounds__(CB_THREADS) void gather_kernel(const int64_t *__res
                 } else {
                     hout++;
                 }
-                bool placed = (CB_XP & 1) != 0;
-                if (!placed && b >= 0 && b < CB_NU && k != GWO_EMPTY_KEY) {
-                    int64_t *kb = s_key + b * S;
-                    // LDS slot: two 32-bit multiplies (the table is private to this pass; any spread will do)
-                    uint32_t sl = ((uint32_t)k * 0x9E3779B1u ^ (uint32_t)((uint64_t)k >> 32) * 0x85EBCA77u) >>
-                                  (32 - a.sbits);
-                    for (int probe = 0; probe < 32; ++probe) {
-                        int64_t cur = kb[sl];
-                        if (cur == GWO_EMPTY_KEY) {
-                            cur = (int64_t)atomicCAS((unsigned long long *)&kb[sl], (unsigned long long)GWO_EMPTY_KEY,
-                                                     (unsigned long long)k);
-                            if (cur == GWO_EMPTY_KEY) cur = k;
-                        }
-                        if (cur == k) {
-                            const int64_t v = val ? val[i] : 0;
-                            int64_t *dst = s_acc + ((size_t)b * S + sl) * NW;
-                            for (int w = 0; w < NW; ++w) lds_combine(dst + w, p.op[w], lift_word(p, w, v));
-                            placed = true;
-                            break;
-                        }
-                        sl = (sl + 1) & (uint32_t)(S - 1);
-                    }
-                }
-                if (!placed) ovm |= 1u << j;
+                cbu[j] = (int)b;
+                if (b >= 0 && b < CB_NU && k != GWO_EMPTY_KEY) candm |= 1u << j;
+                else ovm |= 1u << j;
             }
         }
+        // wave pre-reduction of duplicate keys, then the LDS tables (every lane of the wave is here)
+        const int lane = tid & 63;
+#pragma unroll
+        for (int j = 0; j < CB_PER; ++j) {
+            bool cand = (candm >> j) & 1u;
+            const int64_t k = kk[j];
+            const int b = cand ? cbu[j] : 0;
+            // rounds over the wave's first remaining (unit, key): while it is a hot key (>= CB_HOT lanes), its
+            // lanes' words fold into one lane with a masked wave reduction and that lane updates LDS once
+            unsigned long long m = __ballot(cand);
+            for (int r = 0; r < 8 && m; ++r) {
+                const int leader = __ffsll((long long)m) - 1;
+                const int64_t lk = __shfl(k, leader);
+                const int lb = __shfl(b, leader);
+                const bool mine = cand && k == lk && b == lb;
+                const unsigned long long peers = __ballot(mine);
+                if (__popcll(peers) < CB_HOT) break;
+                int slot = -1;
+                if (lane == leader) slot = lds_slot(s_key + lb * S, S, a.sbits, lk);
+                slot = __shfl(slot, leader);
+                if (slot >= 0) {
+                    int64_t *dst = s_acc + ((size_t)lb * S + slot) * NW;
+                    for (int w = 0; w < NW; ++w) {
+                        const int64_t x = wave_fold(p.op[w], mine ? lift_word(p, w, vv[j]) : p.ident[w]);
+                        if (lane == leader) lds_combine(dst + w, p.op[w], x);
+                    }
+                    if (mine) cand = false;
+                }
+                m &= ~peers;
+            }
+            if (!cand) continue;
+            const int slot = lds_slot(s_key + b * S, S, a.sbits, k);
+            if (slot < 0) {
+                ovm |= 1u << j;
+                continue;
+            }
+            int64_t *dst = s_acc + ((size_t)b * S + slot) * NW;
+            for (int w = 0; w < NW; ++w) lds_combine(dst + w, p.op[w], lift_word(p, w, vv[j]));
+        }
+        if (tile + tstride < n) load_tile(tile + tstride);
         // the tile's listed records: one reservation per workgroup
         unsigned long long at = block_reserve((unsigned)__popc(ovm), a.ovf_count);
         for (int j = 0; j < CB_PER; ++j)
@@ -497,11 +551,10 @@ __global__ __launch_bounds__(CB_THREADS) void gather_kernel(const int64_t *__res
     int64_t *da = a.dump_acc + (size_t)blockIdx.x * CB_NU * S * NW;
     for (int i = tid; i < CB_NU * S; i += CB_THREADS) {
         const int64_t k = s_key[i];
-        if (!(CB_XP & 4)) dk[i] = k;
+        dk[i] = k;
         if (k != GWO_EMPTY_KEY) (i < S ? d0 : d1)++;
     }
-    if (!(CB_XP & 4))
-        for (int i = tid; i < CB_NU * S * NW; i += CB_THREADS) da[i] = s_acc[i];
+    for (int i = tid; i < CB_NU * S * NW; i += CB_THREADS) da[i] = s_acc[i];
     unsigned long long e0 = d0, e1 = d1;
     for (int o = 32; o > 0; o >>= 1) {
         e0 += __shfl_xor(e0, o);
@@ -544,10 +597,6 @@ __global__ __launch_bounds__(CB_THREADS) void gather_kernel(const int64_t *__res
     if (tid == 0) s_last = atomicAdd(a.done, 1ull) == (unsigned long long)(gridDim.x - 1);
     __syncthreads();
     if (!s_last) return;
-    if (CB_XP & 2) {
-        if (tid == 0) *a.done = 0;
-        return;
-    }
     __shared__ unsigned long long s_tot[CS_WORDS];
     if (tid < CS_WORDS) {
         const unsigned long long init =

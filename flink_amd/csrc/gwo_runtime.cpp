@@ -413,7 +413,11 @@ gwo_status Handle::insert_combined(const int64_t *k, const int64_t *t, const int
     int S = 2048;
     while (S > 256 && gather_lds_bytes(S, NW) > 65536) S >>= 1;
     const int64_t tile = gather_tile();
-    const int G = (int)std::max<int64_t>(1, std::min<int64_t>((n + tile - 1) / tile, 4 * (int64_t)cb_cus));
+    if (!cb_max_wg) {
+        cb_max_wg = 4 * cb_cus;
+        if (const char *e = getenv("GWO_CB_WG")) cb_max_wg = std::max(1, atoi(e));
+    }
+    const int G = (int)std::max<int64_t>(1, std::min<int64_t>((n + tile - 1) / tile, (int64_t)cb_max_wg));
     GWO_TRY(ensure_buf(cb_dump_key, (size_t)G * 2 * S * 8));
     GWO_TRY(ensure_buf(cb_dump_acc, (size_t)G * 2 * S * NW * 8));
     GWO_TRY(ensure_buf(cb_ovf, (size_t)n * 4));

@@ -173,6 +173,36 @@ def test_log_layout_hot_key(F):
     op.close()
 
 
+@pytest.mark.parametrize("vdt", ["int64", "float64"])
+def test_table_layout_hot_keys_wave_prereduction(F, vdt):
+    """Combine path (low cardinality): 3/4 of the records on two hot keys, so most waves fold runs of lanes of
+    one key into one lane (ballot + masked wave reduction) before the LDS table; the workgroups' tables then
+    fold into the batch's delta tables and the merge.  int64 bit-exact, float64 sums/avg within 1e-6."""
+    k, t, v, b = _c1(n=600_000, nkeys=800, every=50_000, vdt=vdt, seed=7)
+    k = k.copy()
+    k[0::4] = 7
+    k[1::4] = -3
+    k[2::4] = 7
+    agg = F.MultiAggregate(F.SumAggregate(vdt), F.AverageAggregate(vdt), F.MinAggregate(vdt), F.MaxAggregate(vdt))
+    op = F.GpuWindowOperator(F.TumblingEventTimeWindows.of(5000), agg, state_layout="table", expected_keys=1000)
+    _run_batches(op, k, t, v, b)
+    (wk, ws, we, res), late = V.tumbling_lateness0(k, t, v, _final(b), 5000, 0, [1, 4, 2, 3],
+                                                   value_is_f64=vdt == "float64")
+    got = sorted((a, s, e, *r) for a, s, e, r in op.output)
+    want = _want(wk, ws, we, res)
+    assert [g[:3] for g in got] == [w[:3] for w in want]
+    gs = np.array([g[3:] for g in got])
+    ws_ = np.array([w[3:] for w in want])
+    if vdt == "int64":
+        assert (gs[:, [0, 2, 3]] == ws_[:, [0, 2, 3]]).all()   # sum, min, max bit-exact
+    else:
+        np.testing.assert_allclose(gs[:, 0], ws_[:, 0], rtol=FLOAT_RTOL)
+        assert (gs[:, 2:] == ws_[:, 2:]).all()
+    np.testing.assert_allclose(gs[:, 1], ws_[:, 1], rtol=FLOAT_RTOL)   # avg
+    assert op.num_late_records_dropped == late
+    op.close()
+
+
 def test_log_layout_rejected_for_sliding(F):
     from flink_amd import _native as N
     with pytest.raises(N.GwoError) as ei:
