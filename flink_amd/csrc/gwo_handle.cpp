@@ -134,6 +134,15 @@ gwo_status Handle::init(const gwo_config &c) {
         own_stream = true;
     }
     GWO_TRY(dalloc((void **)&d_stats, sizeof(BatchStats)));
+    {
+        std::vector<unsigned long long> sh(SCAN_SHARD_WORDS, 0ull);
+        for (int q = 0; q < SCAN_SHARDS; ++q) {
+            sh[(size_t)q * SCAN_SW] = 0x7fffffffffffffffull;
+            sh[(size_t)q * SCAN_SW + 1] = 0x8000000000000000ull;
+        }
+        GWO_TRY(dalloc((void **)&d_scan_sh, sh.size() * 8));
+        GWO_TRY(hipcheck(hipMemcpy(d_scan_sh, sh.data(), sh.size() * 8, hipMemcpyHostToDevice), "scan shards"));
+    }
     GWO_TRY(hipcheck(hipHostMalloc((void **)&h_stats, sizeof(BatchStats), hipHostMallocDefault), "pinned"));
     GWO_TRY(hipcheck(hipHostMalloc((void **)&h_stats_init, sizeof(BatchStats), hipHostMallocDefault), "pinned"));
     const int kCounters = 1 << 12;
@@ -180,6 +189,7 @@ Handle::~Handle() {
     for (auto &t : aux_tables) (void)hipFree(t.base);
     trim_pool();
     if (d_stats) (void)hipFree(d_stats);
+    if (d_scan_sh) (void)hipFree(d_scan_sh);
     if (h_stats) (void)hipHostFree(h_stats);
     if (h_stats_init) (void)hipHostFree(h_stats_init);
     if (d_counters) (void)hipFree(d_counters);

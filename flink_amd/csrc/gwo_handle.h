@@ -106,6 +106,7 @@ struct Handle {
 
     // device scratch
     BatchStats *d_stats = nullptr;
+    unsigned long long *d_scan_sh = nullptr;   // scan_kernel statistics shards (SCAN_SHARD_WORDS)
     BatchStats *h_stats = nullptr;             // pinned
     BatchStats *h_stats_init = nullptr;        // pinned
     unsigned long long *d_counters = nullptr;
@@ -146,6 +147,7 @@ struct Handle {
     int use_preagg = 1;
     int use_combine = 1;                       // GWO_COMBINE=0: the two-pass scan + insert path only
     int cb_cus = 0;
+    uint64_t recent_cap = 0;                           // capacity of the last retired window/pane table
     int cb_max_wg = 0;                                 // gather workgroups at most (GWO_CB_WG; default 4 per CU)
     DevBuf cb_dump_key, cb_dump_acc, cb_ovf, cb_blk, cb_ctr, cb_dir;   // combine path scratch (insert_combined)
     unsigned long long *cb_rb = nullptr, *cb_rb_dev = nullptr;        // host-mapped readback block
@@ -266,7 +268,8 @@ struct Handle {
     gwo_status slide_refire_rows(const int64_t *k, const int64_t *t, const int64_t *v, int64_t n, const WindowGeom &g,
                                  uint64_t records);
     // sessions (gwo_session.cpp)
-    gwo_status sess_alloc(uint64_t cap, Table &t);
+    gwo_status sess_alloc(uint64_t cap, Table &t, int64_t **due);
+    gwo_status sess_rebuild_due();
     gwo_status sess_read_err();
     gwo_status sess_ensure(uint64_t incoming);
     gwo_status sess_ensure_pool(uint64_t n);

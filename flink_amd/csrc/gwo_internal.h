@@ -17,6 +17,12 @@
 #define GWO_OCC_SHARDS 8          // occupancy counter shards (gwo_device.h occ_add)
 #define GWO_OCC_SHARD_STRIDE 8    // words between shards: one 64-B line each
 #define GWO_OCC_WORDS (GWO_OCC_SHARDS * GWO_OCC_SHARD_STRIDE)
+// scan_kernel statistics shards: SCAN_SHARDS x SCAN_SW words (min, max, 6 counters, the histogram), then
+// SCAN_SHARDS + 1 arrival counters 16 words apart; min/max preset, every scan leaves them reset
+#define SCAN_SHARDS 16
+#define SCAN_CNT 8
+#define SCAN_SW 80
+#define SCAN_SHARD_WORDS (SCAN_SHARDS * SCAN_SW + (SCAN_SHARDS + 1) * 16)
 
 // Combine ops per accumulator word.  Every aggregate decomposes into word-wise commutative
 // monoids, so inserting a record, merging two partials (sessions, pre-aggregation) and folding
@@ -183,7 +189,10 @@ struct SessGeom {
     int64_t *pool;                     // spilled session lists: (3 + nwords)-word session records
     unsigned long long *pool_top;      // next free pool record (device bump counter)
     uint64_t pool_cap;                 // pool capacity in session records
+    int64_t *due;                      // [cap + 1] per slot (side slot = cap): the earliest watermark at which its
+                                       // sessions fire or retire (SESS_NONE: none) -- the fire sweep skips the rest
 };
+#define SESS_NONE 0x7f7f7f7f7f7f7f7fLL   // a slot without sessions (a byte pattern: set with one memset)
 
 struct SessErr {
     unsigned long long bad_ts, bad_kg, merge_late, capacity;
@@ -201,7 +210,8 @@ namespace gwo {
 
 void launch_scan(const int64_t *key, const int64_t *ts, int64_t n, const WindowGeom &g, long long hist_base,
                  BatchStats *stats, int64_t *side_key, int64_t *side_ts, int64_t *side_val, const int64_t *val,
-                 unsigned long long *side_count, long long side_cap, int side_enabled, hipStream_t s);
+                 unsigned long long *side_count, long long side_cap, int side_enabled, unsigned long long *shards,
+                 hipStream_t s);
 
 void launch_insert(const int64_t *key, const int64_t *ts, const void *val, int64_t n, const WindowGeom &g,
                    const AccPlan &plan, const TableDesc *dir, long long dir_base, int dir_len, int preagg,

@@ -87,14 +87,16 @@ __device__ __forceinline__ bool takes(int c, const WindowGeom &g) {
 // ------------------------------------------------------------------------------------------------
 // scan
 // ------------------------------------------------------------------------------------------------
+// Statistics: every workgroup reduces its counters and histogram in LDS and adds them to shard blockIdx %
+// SCAN_SHARDS (same-address device atomics serialise at ~12 ns each on MI355X: per-wave atomics of a 1.6K-
+// workgroup scan on one word cost ~80 us); the last workgroup folds the shards into *st (and resets them).
 __global__ __launch_bounds__(256) void scan_kernel(const int64_t *__restrict__ key, const int64_t *__restrict__ ts,
                                                    const int64_t *__restrict__ val, int64_t n, WindowGeom g,
                                                    long long hist_base, BatchStats *st, int64_t *side_key,
                                                    int64_t *side_ts, int64_t *side_val,
                                                    unsigned long long *side_count, long long side_cap,
-                                                   int side_enabled) {
+                                                   int side_enabled, unsigned long long *sh) {
     __shared__ unsigned long long s_hist[GWO_HIST_BINS];
-    __shared__ long long s_min[4], s_max[4];
     for (int i = threadIdx.x; i < GWO_HIST_BINS; i += blockDim.x) s_hist[i] = 0;
     __syncthreads();
     long long mn = 0x7fffffffffffffffLL, mx = (long long)0x8000000000000000LL;
@@ -129,37 +131,82 @@ __global__ __launch_bounds__(256) void scan_kernel(const int64_t *__restrict__ k
             bad_slide++;
         }
     }
-    // wave reductions
+    // workgroup reduction -> shard blockIdx % SCAN_SHARDS (zero words skipped)
+    unsigned long long v[SCAN_CNT] = {(unsigned long long)mn, (unsigned long long)mx, acc, late, refire, bad_ts,
+                                      bad_slide, hout};
+#pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
-        long long a = __shfl_xor(mn, o), b = __shfl_xor(mx, o);
-        mn = a < mn ? a : mn;
-        mx = b > mx ? b : mx;
+        const long long a = __shfl_xor((long long)v[0], o), b = __shfl_xor((long long)v[1], o);
+        v[0] = a < (long long)v[0] ? (unsigned long long)a : v[0];
+        v[1] = b > (long long)v[1] ? (unsigned long long)b : v[1];
+#pragma unroll
+        for (int f = 2; f < SCAN_CNT; ++f) v[f] += __shfl_xor(v[f], o);
     }
-    wave_atomic_add(&st->accepted, acc);
-    wave_atomic_add(&st->late, late);
-    wave_atomic_add(&st->refire, refire);
-    wave_atomic_add(&st->bad_ts, bad_ts);
-    wave_atomic_add(&st->bad_range, bad_slide);
-    wave_atomic_add(&st->hist_out, hout);
+    __shared__ unsigned long long s_red[4][SCAN_CNT];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    if (lane == 0) {
-        s_min[wid] = mn;
-        s_max[wid] = mx;
+    if (lane == 0)
+#pragma unroll
+        for (int f = 0; f < SCAN_CNT; ++f) s_red[wid][f] = v[f];
+    __syncthreads();
+    unsigned long long *my = sh + (size_t)(blockIdx.x % SCAN_SHARDS) * SCAN_SW;
+    const int t = threadIdx.x;
+    if (t < SCAN_CNT) {
+        unsigned long long r = s_red[0][t];
+        for (int w = 1; w < (int)(blockDim.x >> 6); ++w) {
+            const unsigned long long x = s_red[w][t];
+            if (t == 0) r = (long long)x < (long long)r ? x : r;
+            else if (t == 1) r = (long long)x > (long long)r ? x : r;
+            else r += x;
+        }
+        if (t == 0) {
+            if ((long long)r != 0x7fffffffffffffffLL) atomicMin((long long *)&my[0], (long long)r);
+        } else if (t == 1) {
+            if ((long long)r != (long long)0x8000000000000000LL) atomicMax((long long *)&my[1], (long long)r);
+        } else if (r) {
+            atomicAdd(&my[t], r);
+        }
+    } else if (t >= 64 && t < 64 + GWO_HIST_BINS) {
+        if (s_hist[t - 64]) atomicAdd(&my[SCAN_CNT + t - 64], s_hist[t - 64]);
+    }
+    // the last workgroup folds the shards (arrivals counted per shard, the last of a shard counts the shard;
+    // every workgroup's atomics have completed before its arrival)
+    __shared__ int s_last;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    unsigned long long *done = sh + (size_t)SCAN_SHARDS * SCAN_SW;
+    if (t == 0) {
+        const unsigned q = blockIdx.x % SCAN_SHARDS;
+        const unsigned members = (gridDim.x - q + SCAN_SHARDS - 1) / SCAN_SHARDS;
+        const unsigned nsh = gridDim.x < SCAN_SHARDS ? gridDim.x : SCAN_SHARDS;
+        bool last = false;
+        if (atomicAdd(&done[q * 16], 1ull) == members - 1) last = atomicAdd(&done[SCAN_SHARDS * 16], 1ull) == nsh - 1;
+        s_last = last;
     }
     __syncthreads();
-    if (threadIdx.x == 0) {
-        long long a = s_min[0], b = s_max[0];
-        for (int w = 1; w < (int)(blockDim.x >> 6); ++w) {
-            a = s_min[w] < a ? s_min[w] : a;
-            b = s_max[w] > b ? s_max[w] : b;
+    if (!s_last) return;
+    if (t < SCAN_CNT + GWO_HIST_BINS) {
+        const unsigned long long init = t == 0 ? 0x7fffffffffffffffull : (t == 1 ? 0x8000000000000000ull : 0ull);
+        unsigned long long r = init;
+        for (int q = 0; q < SCAN_SHARDS; ++q) {
+            const unsigned long long x = atomicExch(&sh[(size_t)q * SCAN_SW + t], init);
+            if (t == 0) r = (long long)x < (long long)r ? x : r;
+            else if (t == 1) r = (long long)x > (long long)r ? x : r;
+            else r += x;
         }
-        if (a != 0x7fffffffffffffffLL) {
-            atomicMin(&st->min_idx, a);
-            atomicMax(&st->max_idx, b);
+        switch (t) {
+            case 0: st->min_idx = (long long)r; break;
+            case 1: st->max_idx = (long long)r; break;
+            case 2: st->accepted = r; break;
+            case 3: st->late = r; break;
+            case 4: st->refire = r; break;
+            case 5: st->bad_ts = r; break;
+            case 6: st->bad_range = r; break;
+            case 7: st->hist_out = r; break;
+            default: st->hist[t - SCAN_CNT] = r; break;
         }
+    } else if (t >= 128 && t < 128 + SCAN_SHARDS + 1) {
+        atomicExch(&done[(t - 128) * 16], 0ull);   // the next scan counts from zero
     }
-    for (int i = threadIdx.x; i < GWO_HIST_BINS; i += blockDim.x)
-        if (s_hist[i]) atomicAdd(&st->hist[i], s_hist[i]);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1262,9 +1309,10 @@ void launch_slide_refire_slots(const int64_t *key, const int64_t *r_idx, const l
 
 void launch_scan(const int64_t *key, const int64_t *ts, int64_t n, const WindowGeom &g, long long hist_base,
                  BatchStats *stats, int64_t *side_key, int64_t *side_ts, int64_t *side_val, const int64_t *val,
-                 unsigned long long *side_count, long long side_cap, int side_enabled, hipStream_t s) {
+                 unsigned long long *side_count, long long side_cap, int side_enabled, unsigned long long *shards,
+                 hipStream_t s) {
     hipLaunchKernelGGL(scan_kernel, dim3(grid_for(n, 4, 2048)), dim3(256), 0, s, key, ts, val, n, g, hist_base,
-                       stats, side_key, side_ts, side_val, side_count, side_cap, side_enabled);
+                       stats, side_key, side_ts, side_val, side_count, side_cap, side_enabled, shards);
 }
 
 void launch_insert(const int64_t *key, const int64_t *ts, const void *val, int64_t n, const WindowGeom &g,

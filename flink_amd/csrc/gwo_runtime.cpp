@@ -180,6 +180,9 @@ gwo_status Handle::ensure_table(long long u, uint64_t incoming) {
     if (cfg.expected_keys > 0)
         want_min = std::max<uint64_t>(want_min, next_pow2((uint64_t)((double)cfg.expected_keys / kInitLoad) + 1));
     if (it == tables.end()) {
+        // a new window / pane starts at the size the last retired one grew to: a unit's records arrive over
+        // several batches (disorder), and sizing by the first batch's share alone rehashes every unit once
+        want_min = std::max<uint64_t>(want_min, recent_cap);
         Table t;
         GWO_TRY(alloc_table(want_min, t));
         // tumbling: a window created after the watermark passed its end only receives re-fire records
@@ -641,7 +644,7 @@ gwo_status Handle::insert_windowed(const int64_t *k, const int64_t *t, const int
         prof_begin(GWO_KERNEL_SCAN);
         launch_scan(k, t, n, g, hist_base, d_stats, (int64_t *)side_key.ptr, (int64_t *)side_ts.ptr,
                     (int64_t *)side_val.ptr, v, d_side_count, first_pass && count_late && side_enabled() ? side_cap : 0,
-                    first_pass && count_late && side_enabled(), stream);
+                    first_pass && count_late && side_enabled(), d_scan_sh, stream);
         GWO_TRY(launch_ok("scan"));
         prof_end(GWO_KERNEL_SCAN, n);
         GWO_TRY(hipcheck(hipMemcpyAsync(h_stats, d_stats, sizeof(BatchStats), hipMemcpyDeviceToHost, stream), "stats"));
@@ -824,6 +827,7 @@ gwo_status Handle::fire_tumbling(int64_t new_wm) {
             none.count = d_scratch_count;
             launch_fire(desc(t), t.cap, plan, rplan, 0, 0, none, 1, -1, stream);
         }
+        recent_cap = t.cap;
         release_table(t);
         tables.erase(u);
     }

@@ -18,11 +18,14 @@ void launch_sess_fire(const TableDesc &t, uint64_t cap, int stride, const AccPla
 void launch_sess_compact(const TableDesc &src, uint64_t cap, const TableDesc &dst, int stride, hipStream_t s);
 void launch_sess_pool_compact(const TableDesc &t, uint64_t cap, int stride, int sw, const int64_t *old_pool,
                               const SessGeom &g, hipStream_t s);
+void launch_sess_due(const TableDesc &t, uint64_t cap, int stride, int sw, const SessGeom &g, hipStream_t s);
 
 struct SessionState {
     int smax = 8;
     int stride = 0;
     Table T;
+    int64_t *due = nullptr;         // [T.cap + 1] due watermark per slot (SessGeom::due)
+    uint64_t occ_pending = 0;       // entries claimed since T.occ was read, at most (one per record)
     uint64_t live = 0;              // in-flight sessions
     SessErr *d_err = nullptr;
     SessErr *h_err = nullptr;       // pinned
@@ -34,11 +37,13 @@ struct SessionState {
     uint64_t pool_top = 0;          // as of the last read-back
 };
 
-gwo_status Handle::sess_alloc(uint64_t cap, Table &t) {
+gwo_status Handle::sess_alloc(uint64_t cap, Table &t, int64_t **due) {
     SessionState &S = *sess;
     void *p = nullptr;
-    GWO_TRY(dalloc(&p, ((size_t)cap + 1) * S.stride * 8));
+    GWO_TRY(dalloc(&p, ((size_t)cap + 1) * S.stride * 8 + ((size_t)cap + 1) * 8));
     t.base = (int64_t *)p;
+    *due = t.base + (cap + 1) * S.stride;   // no sessions anywhere yet
+    GWO_TRY(hipcheck(hipMemsetAsync(*due, 0x7f, ((size_t)cap + 1) * 8, stream), "due"));
     t.cap = cap;
     t.side = t.base + cap * S.stride;
     AccPlan fp{};
@@ -64,7 +69,7 @@ gwo_status Handle::session_init() {
     uint64_t cap = kMinCap;
     if (cfg.expected_keys > 0)
         while ((double)cfg.expected_keys > kInitLoad * (double)cap) cap <<= 1;
-    return sess_alloc(cap, S.T);
+    return sess_alloc(cap, S.T, &S.due);
 }
 
 void Handle::session_free() {
@@ -90,6 +95,7 @@ static SessGeom sess_geom(const Handle &h, int smax) {
     g.pool = h.sess->pool;
     g.pool_top = h.sess->d_pool_top;
     g.pool_cap = h.sess->pool_cap;
+    g.due = h.sess->due;
     g.gap = h.cfg.gap;
     g.lateness = h.cfg.allowed_lateness;
     g.wm = h.wm;
@@ -142,13 +148,20 @@ gwo_status Handle::sess_ensure_pool(uint64_t n) {
 // Grow the per-key table (dropping keys without sessions) so `incoming` new keys fit.
 gwo_status Handle::sess_ensure(uint64_t incoming) {
     SessionState &S = *sess;
+    // upper bound without a device read: the last exact occupancy plus one claim per record since
+    if ((double)(S.T.occ + S.occ_pending + incoming) <= kMaxLoad * (double)S.T.cap) {
+        S.occ_pending += incoming;
+        return GWO_OK;
+    }
     GWO_TRY(read_occupancy_one(S.T));
+    S.occ_pending = incoming;
     if ((double)(S.T.occ + incoming) <= kMaxLoad * (double)S.T.cap) return GWO_OK;
     uint64_t need = std::min<uint64_t>(S.T.occ, S.live) + incoming;
     uint64_t cap = kMinCap;
     while ((double)need > kInitLoad * (double)cap) cap <<= 1;
     Table nt;
-    GWO_TRY(sess_alloc(cap, nt));
+    int64_t *ndue = nullptr;
+    GWO_TRY(sess_alloc(cap, nt, &ndue));
     launch_sess_compact(desc(S.T), S.T.cap, desc(nt), S.stride, stream);
     GWO_TRY(launch_ok("compact"));
     GWO_TRY(hipcheck(hipMemcpyAsync(nt.side, S.T.side, (size_t)S.stride * 8, hipMemcpyDeviceToDevice, stream), "side"));
@@ -156,7 +169,16 @@ gwo_status Handle::sess_ensure(uint64_t incoming) {
     (void)hipFree(S.T.base);
     counter_used[S.T.counter] = 0;
     S.T = nt;
+    S.due = ndue;
+    GWO_TRY(sess_rebuild_due());
     return read_occupancy_one(S.T);
+}
+
+// Every slot's due watermark recomputed from the entries (after entries were written outside the hot path).
+gwo_status Handle::sess_rebuild_due() {
+    SessionState &S = *sess;
+    launch_sess_due(desc(S.T), S.T.cap, S.stride, 3 + plan.nwords, sess_geom(*this, S.smax), stream);
+    return launch_ok("session due");
 }
 
 gwo_status Handle::read_occupancy_one(Table &t) {
@@ -335,7 +357,7 @@ gwo_status Handle::session_restore_rows(const RestoreRows &R, int64_t new_wm) {
         S.live += mine - nk.size();
     }
     const int64_t m = (int64_t)nk.size();
-    if (m == 0) return GWO_OK;
+    if (m == 0) return sess_rebuild_due();
     DevBuf k, st, en, tm, w;
     GWO_TRY(ensure_buf(k, (size_t)m * 8));
     GWO_TRY(ensure_buf(st, (size_t)m * 8));
@@ -356,7 +378,7 @@ gwo_status Handle::session_restore_rows(const RestoreRows &R, int64_t new_wm) {
     for (DevBuf *x : {&k, &st, &en, &tm, &w}) x->release();
     if (S.h_err->capacity) return poison(GWO_ERR_HIP, "restore: an entry overflowed its inline sessions");
     S.live += S.h_err->live_delta;
-    return GWO_OK;
+    return sess_rebuild_due();
 }
 
 }  // namespace gwo

@@ -45,9 +45,10 @@ __global__ __launch_bounds__(256) void sess_slot_kernel(const int64_t *__restric
     }
 }
 
-__device__ __forceinline__ void emit_row(const OutCols &o, const AccPlan &p, const ResultPlan &rp, int64_t key,
-                                         int64_t start, int64_t end, const int64_t *acc) {
-    unsigned long long pos = atomicAdd(o.count, 1ull);
+// One output row at a reserved position (rows past the output capacity are counted, not written).
+__device__ __forceinline__ void emit_row_at(const OutCols &o, const AccPlan &p, const ResultPlan &rp,
+                                            unsigned long long pos, int64_t key, int64_t start, int64_t end,
+                                            const int64_t *acc) {
     if ((long long)pos >= o.cap) return;
     o.key[pos] = key;
     o.start[pos] = start;
@@ -69,8 +70,26 @@ __device__ __forceinline__ void emit_row(const OutCols &o, const AccPlan &p, con
     }
 }
 
+__device__ __forceinline__ void emit_row(const OutCols &o, const AccPlan &p, const ResultPlan &rp, int64_t key,
+                                         int64_t start, int64_t end, const int64_t *acc) {
+    emit_row_at(o, p, rp, atomicAdd(o.count, 1ull), key, start, end, acc);
+}
+
 #define SESS_MAXS 16
 #define SESS_MAXW (3 + GWO_MAX_WORDS)
+
+// The earliest watermark at which an entry's sessions need the fire sweep: a pending event-time timer fires at
+// maxTimestamp = end - 1 (EventTimeTrigger.onEventTime), a session retires at cleanupTime(maxTimestamp)
+// (WindowOperator.java:528-540).  The sweep only visits slots whose value the watermark reached.
+__device__ __forceinline__ int64_t sess_due(const int64_t *S, int ns, int sw, int64_t lateness) {
+    int64_t d = SESS_NONE;
+    for (int s = 0; s < ns; ++s) {
+        const int64_t mx = jsub(S[s * sw + 1], 1);
+        const int64_t t = (S[s * sw + 2] & 1) ? mx : cleanup_time(mx, lateness);
+        d = t < d ? t : d;
+    }
+    return d;
+}
 
 // Moves a key's session list into a fresh pool array of at least `want` sessions (doubling); returns the
 // array or nullptr when the pool is exhausted (the host sizes the pool so that cannot happen).
@@ -226,45 +245,74 @@ __global__ __launch_bounds__(64) void sess_process_kernel(const int64_t *__restr
                 e[1] = ns;
                 for (int i = 0; i < ns * sw; ++i) e[2 + i] = L[i];
             }
+            g.due[slot < cap ? slot : cap] = sess_due(S, ns, sw, g.lateness);
             if (created) atomicAdd(&err->live_delta, (unsigned long long)created);
         }
     }
 }
 
 // watermark: fire pending timers <= wm, clear sessions whose cleanup time <= wm
+// Rows go out with one output reservation per wave (a wave-wide prefix over the lanes' row counts): a per-row
+// atomic on the shared row counter serialises at ~12 ns per row on MI355X (same-address device atomics), which
+// cost ~100 us per watermark at C5's ~5K fired sessions.  Statistics are wave-reduced the same way.
 __global__ __launch_bounds__(256) void sess_fire_kernel(TableDesc t, uint64_t cap, int stride, AccPlan p, ResultPlan rp,
                                                         SessGeom g, OutCols o, SessErr *err) {
     const uint64_t step = (uint64_t)gridDim.x * blockDim.x;
     const int sw = 3 + p.nwords;
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i <= cap; i += step) {
-        int64_t *e;
-        int64_t k;
-        if (i < cap) {
-            e = t.base + i * (uint64_t)stride;
-            k = e[0];
-            if (k == GWO_EMPTY_KEY) continue;
-        } else {
-            e = t.side;
-            if (e[0] == 0) continue;
-            k = GWO_EMPTY_KEY;
+    const int lane = threadIdx.x & 63;
+    unsigned long long emitted = 0;
+    long long removed_all = 0;
+    // every lane runs the same number of iterations (the bound is rounded up to whole waves), so the wave-wide
+    // reservation below always sees the full wave
+    const uint64_t lim = (cap + 1 + 63) & ~63ull;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i - lane < lim; i += step) {
+        int64_t *e = nullptr, *base = nullptr;
+        int64_t k = 0;
+        int ns = 0;
+        bool spilled = false;
+        if (i <= cap && g.due[i] <= g.wm) {   // (a slot whose due watermark is ahead: nothing fires or retires)
+            if (i < cap) {
+                e = t.base + i * (uint64_t)stride;
+                k = e[0];
+                if (k == GWO_EMPTY_KEY) e = nullptr;
+            } else {
+                e = t.side;
+                k = GWO_EMPTY_KEY;
+                if (e[0] == 0) e = nullptr;
+            }
+            if (e) {
+                spilled = e[1] < 0;
+                ns = spilled ? (int)e[4] : (int)e[1];
+                base = spilled ? g.pool + (uint64_t)e[2] * sw : e + 2;
+            }
         }
-        const bool spilled = e[1] < 0;
-        int ns = spilled ? (int)e[4] : (int)e[1];
+        // rows of this lane: sessions with a pending timer at maxTs <= wm (EventTimeTrigger.onEventTime FIRE)
+        unsigned nrow = 0;
+        for (int s = 0; s < ns; ++s) {
+            const int64_t *S = base + s * sw;
+            nrow += (S[2] & 1) && jsub(S[1], 1) <= g.wm;
+        }
+        unsigned incl = nrow;
+#pragma unroll
+        for (int o2 = 1; o2 < 64; o2 <<= 1) {
+            const unsigned y = __shfl_up(incl, o2);
+            if (lane >= o2) incl += y;
+        }
+        const unsigned wtot = __shfl(incl, 63);
+        unsigned long long pos = 0;
+        if (lane == 63 && wtot) pos = atomicAdd(o.count, (unsigned long long)wtot);
+        pos = (unsigned long long)__shfl((long long)pos, 63) + (incl - nrow);
+        emitted += nrow;
         if (ns == 0) continue;
-        int64_t *base = spilled ? g.pool + (uint64_t)e[2] * sw : e + 2;
         int keep = 0;
         long long removed = 0;
         for (int s = 0; s < ns; ++s) {
             int64_t *S = base + s * sw;
-            int64_t mx = jsub(S[1], 1);
-            bool changed = false;
+            const int64_t mx = jsub(S[1], 1);
             if ((S[2] & 1) && mx <= g.wm) {
-                emit_row(o, p, rp, k, S[0], S[1], S + 3);
-                atomicAdd(&err->emitted, 1ull);
+                emit_row_at(o, p, rp, pos++, k, S[0], S[1], S + 3);
                 S[2] &= ~1ll;
-                changed = true;
             }
-            (void)changed;
             if (cleanup_time(mx, g.lateness) <= g.wm) {
                 removed++;
                 continue;
@@ -278,7 +326,32 @@ __global__ __launch_bounds__(256) void sess_fire_kernel(TableDesc t, uint64_t ca
             else if (keep == 0) e[1] = 0;   // every spilled session retired: the key is inline (and empty) again
             else e[4] = keep;
         }
-        if (removed) atomicAdd(&err->live_delta, (unsigned long long)(-removed));
+        g.due[i] = sess_due(base, keep, sw, g.lateness);
+        removed_all += removed;
+    }
+#pragma unroll
+    for (int o2 = 32; o2 > 0; o2 >>= 1) {
+        emitted += __shfl_xor(emitted, o2);
+        removed_all += __shfl_xor(removed_all, o2);
+    }
+    if (lane == 0) {
+        if (emitted) atomicAdd(&err->emitted, emitted);
+        if (removed_all) atomicAdd(&err->live_delta, (unsigned long long)(-removed_all));
+    }
+}
+
+// Every slot's due watermark from its entry (after a compaction or a restore wrote entries directly).
+__global__ __launch_bounds__(256) void sess_due_kernel(TableDesc t, uint64_t cap, int stride, int sw, SessGeom g) {
+    const uint64_t step = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i <= cap; i += step) {
+        const int64_t *e = i < cap ? t.base + i * (uint64_t)stride : t.side;
+        int64_t d = SESS_NONE;
+        if (i < cap ? e[0] != GWO_EMPTY_KEY : e[0] != 0) {
+            const bool spilled = e[1] < 0;
+            const int ns = spilled ? (int)e[4] : (int)e[1];
+            d = sess_due(spilled ? g.pool + (uint64_t)e[2] * sw : e + 2, ns, sw, g.lateness);
+        }
+        g.due[i] = d;
     }
 }
 
@@ -345,6 +418,11 @@ void launch_sess_pool_compact(const TableDesc &t, uint64_t cap, int stride, int 
                               const SessGeom &g, hipStream_t s) {
     hipLaunchKernelGGL(sess_pool_compact_kernel, dim3(sgrid((int64_t)cap + 1, 256, 8192)), dim3(256), 0, s, t, cap,
                        stride, sw, old_pool, g);
+}
+
+void launch_sess_due(const TableDesc &t, uint64_t cap, int stride, int sw, const SessGeom &g, hipStream_t s) {
+    hipLaunchKernelGGL(sess_due_kernel, dim3(sgrid((int64_t)cap + 1, 256, 4096)), dim3(256), 0, s, t, cap, stride, sw,
+                       g);
 }
 
 void launch_sess_compact(const TableDesc &src, uint64_t cap, const TableDesc &dst, int stride, hipStream_t s) {

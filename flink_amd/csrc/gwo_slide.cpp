@@ -292,6 +292,7 @@ gwo_status Handle::release_panes_before(long long first) {
         GWO_TRY(hipcheck(hipMemsetAsync(d_scratch_count, 0, 8, stream), "z"));
         none.count = d_scratch_count;
         launch_fire(desc(t), t.cap, plan, rplan, 0, 0, none, 1, -1, stream);
+        recent_cap = t.cap;
         release_table(t);
         it = tables.erase(it);
     }
