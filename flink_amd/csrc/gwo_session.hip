@@ -252,91 +252,99 @@ __global__ __launch_bounds__(64) void sess_process_kernel(const int64_t *__restr
 }
 
 // watermark: fire pending timers <= wm, clear sessions whose cleanup time <= wm
-// Rows go out with one output reservation per wave (a wave-wide prefix over the lanes' row counts): a per-row
-// atomic on the shared row counter serialises at ~12 ns per row on MI355X (same-address device atomics), which
-// cost ~100 us per watermark at C5's ~5K fired sessions.  Statistics are wave-reduced the same way.
+// Persistent workgroups (about one per CU) sweep the slots in rounds of SF_SPT slots per thread; a round counts
+// its rows first and reserves them with ONE returning atomic per workgroup (block_reserve), then emits.  A
+// reservation per wave or per row serialised on the shared row counter: ~180 us per watermark at C5's ~5K
+// fired sessions, for a kernel that does a few microseconds of work.  Statistics: one add per workgroup.
+#define SF_SPT 8
+__device__ __forceinline__ int64_t *sess_slot_entry(const TableDesc &t, uint64_t cap, int stride, uint64_t i,
+                                                    int64_t &k) {
+    if (i < cap) {
+        int64_t *e = t.base + i * (uint64_t)stride;
+        k = e[0];
+        return k == GWO_EMPTY_KEY ? nullptr : e;
+    }
+    k = GWO_EMPTY_KEY;
+    return t.side[0] == 0 ? nullptr : t.side;
+}
+
 __global__ __launch_bounds__(256) void sess_fire_kernel(TableDesc t, uint64_t cap, int stride, AccPlan p, ResultPlan rp,
                                                         SessGeom g, OutCols o, SessErr *err) {
-    const uint64_t step = (uint64_t)gridDim.x * blockDim.x;
     const int sw = 3 + p.nwords;
-    const int lane = threadIdx.x & 63;
+    const uint64_t span = (uint64_t)gridDim.x * 256;   // slots one pass of the grid covers
     unsigned long long emitted = 0;
     long long removed_all = 0;
-    // every lane runs the same number of iterations (the bound is rounded up to whole waves), so the wave-wide
-    // reservation below always sees the full wave
-    const uint64_t lim = (cap + 1 + 63) & ~63ull;
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i - lane < lim; i += step) {
-        int64_t *e = nullptr, *base = nullptr;
-        int64_t k = 0;
-        int ns = 0;
-        bool spilled = false;
-        if (i <= cap && g.due[i] <= g.wm) {   // (a slot whose due watermark is ahead: nothing fires or retires)
-            if (i < cap) {
-                e = t.base + i * (uint64_t)stride;
-                k = e[0];
-                if (k == GWO_EMPTY_KEY) e = nullptr;
-            } else {
-                e = t.side;
-                k = GWO_EMPTY_KEY;
-                if (e[0] == 0) e = nullptr;
-            }
-            if (e) {
-                spilled = e[1] < 0;
-                ns = spilled ? (int)e[4] : (int)e[1];
-                base = spilled ? g.pool + (uint64_t)e[2] * sw : e + 2;
-            }
-        }
-        // rows of this lane: sessions with a pending timer at maxTs <= wm (EventTimeTrigger.onEventTime FIRE)
-        unsigned nrow = 0;
-        for (int s = 0; s < ns; ++s) {
-            const int64_t *S = base + s * sw;
-            nrow += (S[2] & 1) && jsub(S[1], 1) <= g.wm;
-        }
-        unsigned incl = nrow;
+    // rounds are workgroup-uniform (block_reserve synchronises the workgroup)
+    for (uint64_t r0 = 0; r0 <= cap; r0 += span * SF_SPT) {
+        unsigned due_m = 0, nrow = 0;
 #pragma unroll
-        for (int o2 = 1; o2 < 64; o2 <<= 1) {
-            const unsigned y = __shfl_up(incl, o2);
-            if (lane >= o2) incl += y;
+        for (int j = 0; j < SF_SPT; ++j) {
+            const uint64_t i = r0 + (uint64_t)j * span + (uint64_t)blockIdx.x * 256 + threadIdx.x;
+            if (i > cap || g.due[i] > g.wm) continue;   // a slot whose due watermark is ahead: nothing to do
+            int64_t k;
+            const int64_t *e = sess_slot_entry(t, cap, stride, i, k);
+            if (!e) continue;
+            const bool spilled = e[1] < 0;
+            const int ns = spilled ? (int)e[4] : (int)e[1];
+            const int64_t *base = spilled ? g.pool + (uint64_t)e[2] * sw : e + 2;
+            for (int s = 0; s < ns; ++s)   // rows: pending timers at maxTs <= wm (EventTimeTrigger.onEventTime)
+                nrow += (base[s * sw + 2] & 1) && jsub(base[s * sw + 1], 1) <= g.wm;
+            if (ns) due_m |= 1u << j;
         }
-        const unsigned wtot = __shfl(incl, 63);
-        unsigned long long pos = 0;
-        if (lane == 63 && wtot) pos = atomicAdd(o.count, (unsigned long long)wtot);
-        pos = (unsigned long long)__shfl((long long)pos, 63) + (incl - nrow);
+        unsigned long long pos = block_reserve(nrow, o.count);
         emitted += nrow;
-        if (ns == 0) continue;
-        int keep = 0;
-        long long removed = 0;
-        for (int s = 0; s < ns; ++s) {
-            int64_t *S = base + s * sw;
-            const int64_t mx = jsub(S[1], 1);
-            if ((S[2] & 1) && mx <= g.wm) {
-                emit_row_at(o, p, rp, pos++, k, S[0], S[1], S + 3);
-                S[2] &= ~1ll;
+#pragma unroll
+        for (int j = 0; j < SF_SPT; ++j) {
+            if (!((due_m >> j) & 1u)) continue;
+            const uint64_t i = r0 + (uint64_t)j * span + (uint64_t)blockIdx.x * 256 + threadIdx.x;
+            int64_t k;
+            int64_t *e = sess_slot_entry(t, cap, stride, i, k);
+            const bool spilled = e[1] < 0;
+            const int ns = spilled ? (int)e[4] : (int)e[1];
+            int64_t *base = spilled ? g.pool + (uint64_t)e[2] * sw : e + 2;
+            int keep = 0;
+            for (int s = 0; s < ns; ++s) {
+                int64_t *S = base + s * sw;
+                const int64_t mx = jsub(S[1], 1);
+                if ((S[2] & 1) && mx <= g.wm) {
+                    emit_row_at(o, p, rp, pos++, k, S[0], S[1], S + 3);
+                    S[2] &= ~1ll;
+                }
+                if (cleanup_time(mx, g.lateness) <= g.wm) {
+                    removed_all++;
+                    continue;
+                }
+                if (keep != s)
+                    for (int w = 0; w < sw; ++w) base[keep * sw + w] = S[w];
+                keep++;
             }
-            if (cleanup_time(mx, g.lateness) <= g.wm) {
-                removed++;
-                continue;
+            if (keep != ns) {
+                if (!spilled) e[1] = keep;
+                else if (keep == 0) e[1] = 0;   // every spilled session retired: the key is inline (and empty) again
+                else e[4] = keep;
             }
-            if (keep != s)
-                for (int w = 0; w < sw; ++w) base[keep * sw + w] = S[w];
-            keep++;
+            g.due[i] = sess_due(base, keep, sw, g.lateness);
         }
-        if (keep != ns) {
-            if (!spilled) e[1] = keep;
-            else if (keep == 0) e[1] = 0;   // every spilled session retired: the key is inline (and empty) again
-            else e[4] = keep;
-        }
-        g.due[i] = sess_due(base, keep, sw, g.lateness);
-        removed_all += removed;
     }
+    // workgroup totals: one add each
+    __shared__ unsigned long long s_e[4];
+    __shared__ long long s_r[4];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
 #pragma unroll
     for (int o2 = 32; o2 > 0; o2 >>= 1) {
         emitted += __shfl_xor(emitted, o2);
         removed_all += __shfl_xor(removed_all, o2);
     }
     if (lane == 0) {
-        if (emitted) atomicAdd(&err->emitted, emitted);
-        if (removed_all) atomicAdd(&err->live_delta, (unsigned long long)(-removed_all));
+        s_e[wid] = emitted;
+        s_r[wid] = removed_all;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned long long e = s_e[0] + s_e[1] + s_e[2] + s_e[3];
+        const long long r = s_r[0] + s_r[1] + s_r[2] + s_r[3];
+        if (e) atomicAdd(&err->emitted, e);
+        if (r) atomicAdd(&err->live_delta, (unsigned long long)(-r));
     }
 }
 
@@ -410,8 +418,9 @@ void launch_sess_process(const int64_t *key, const int64_t *ts, const int64_t *v
 
 void launch_sess_fire(const TableDesc &t, uint64_t cap, int stride, const AccPlan &p, const ResultPlan &rp,
                       const SessGeom &g, OutCols o, SessErr *err, hipStream_t s) {
-    hipLaunchKernelGGL(sess_fire_kernel, dim3(sgrid((int64_t)cap + 1, 256, 8192)), dim3(256), 0, s, t, cap, stride,
-                       p, rp, g, o, err);
+    // about one workgroup per CU (MI355X: 256), fewer for small tables
+    hipLaunchKernelGGL(sess_fire_kernel, dim3(sgrid((int64_t)cap + 1, 256 * SF_SPT, 256)), dim3(256), 0, s, t, cap,
+                       stride, p, rp, g, o, err);
 }
 
 void launch_sess_pool_compact(const TableDesc &t, uint64_t cap, int stride, int sw, const int64_t *old_pool,
