@@ -817,35 +817,60 @@ __device__ __forceinline__ void write_results(const AccPlan &p, const ResultPlan
     }
 }
 
+#ifndef FIRE_FPT
 #define FIRE_FPT 8   // slots per thread per chunk: one output reservation per 2048 slots
+#endif
 
 __device__ __forceinline__ const int64_t *fire_entry(const TableDesc &t, uint64_t cap, int stride, uint64_t i) {
     return i < cap ? t.base + i * (uint64_t)stride : t.side;   // i == cap: the side slot
 }
 
+// Rows of a chunk are ordered (slot round j, thread): the 256 lanes that emit in round j write one contiguous run
+// of every output column (coalesced stores); one row reservation per chunk.  (Ordering rows by thread instead --
+// each thread's rows adjacent -- makes a store instruction touch up to 64 scattered 8-B words per column.)
 __global__ __launch_bounds__(256) void fire_kernel(TableDesc t, uint64_t cap, AccPlan p, ResultPlan rp, int64_t start,
                                                    int64_t end, OutCols o, int reset, int live_word) {
     constexpr uint64_t CH = 256 * FIRE_FPT;
     const int NW = p.nwords;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    __shared__ unsigned s_off[FIRE_FPT][4];
+    __shared__ unsigned long long s_base;
+    const unsigned long long below = (1ull << lane) - 1ull;
     // +1 iteration space for the side slot (key == Long.MIN_VALUE)
     for (uint64_t b0 = (uint64_t)blockIdx.x * CH; b0 < cap + 1; b0 += (uint64_t)gridDim.x * CH) {
-        unsigned flags = 0, cnt = 0;
+        unsigned flags = 0;
+        unsigned pre[FIRE_FPT];
 #pragma unroll
         for (int j = 0; j < FIRE_FPT; ++j) {
             uint64_t i = b0 + (uint64_t)j * 256 + threadIdx.x;
-            if (i > cap) continue;
-            const int64_t *e = fire_entry(t, cap, p.stride, i);
-            bool occ = i < cap ? e[0] != GWO_EMPTY_KEY : e[0] != 0;
-            if (occ && live_word >= 0) occ = e[1 + live_word] > 0;
-            if (occ) {
-                flags |= 1u << j;
-                cnt++;
+            bool occ = false;
+            if (i <= cap) {
+                const int64_t *e = fire_entry(t, cap, p.stride, i);
+                occ = i < cap ? e[0] != GWO_EMPTY_KEY : e[0] != 0;
+                if (occ && live_word >= 0) occ = e[1 + live_word] > 0;
             }
+            if (occ) flags |= 1u << j;
+            const unsigned long long m = __ballot(occ);
+            pre[j] = (unsigned)__popcll(m & below);
+            if (lane == 0) s_off[j][wid] = (unsigned)__popcll(m);
         }
-        unsigned long long pos = block_reserve(cnt, o.count);
+        __syncthreads();
+        if (threadIdx.x == 0) {   // (round, wave)-major exclusive offsets, one reservation for the chunk
+            unsigned run = 0;
+            for (int j = 0; j < FIRE_FPT; ++j)
+                for (int w = 0; w < 4; ++w) {
+                    const unsigned c = s_off[j][w];
+                    s_off[j][w] = run;
+                    run += c;
+                }
+            s_base = run ? atomicAdd(o.count, (unsigned long long)run) : 0ull;
+        }
+        __syncthreads();
+        const unsigned long long base = s_base;
         for (int j = 0; j < FIRE_FPT; ++j) {
             if (!(flags >> j & 1u)) continue;
             uint64_t i = b0 + (uint64_t)j * 256 + threadIdx.x;
+            const unsigned long long pos = base + s_off[j][wid] + pre[j];
             int64_t *e = (int64_t *)fire_entry(t, cap, p.stride, i);
             int64_t acc[GWO_MAX_WORDS];
 #pragma unroll
@@ -857,12 +882,12 @@ __global__ __launch_bounds__(256) void fire_kernel(TableDesc t, uint64_t cap, Ac
                 o.end[pos] = end;
                 write_results(p, rp, acc, o, pos);
             }
-            pos++;
             if (reset) {
                 e[0] = i < cap ? GWO_EMPTY_KEY : 0;
                 for (int w = 0; w < NW; ++w) e[1 + w] = p.ident[w];
             }
         }
+        __syncthreads();   // s_off / s_base are rewritten by the next chunk
     }
 }
 
