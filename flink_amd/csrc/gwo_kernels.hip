@@ -219,19 +219,33 @@ __device__ __forceinline__ void apply_record(const TableDesc &t, const AccPlan &
     for (int w = 0; w < p.nwords; ++w) atomic_combine(acc + w, p.op[w], lift_word(p, w, vbits));
 }
 
-// Ring update with live-entry accounting on the hidden count word.
-__device__ __forceinline__ void apply_ring(const RingDesc &r, const AccPlan &p, int64_t k, const int64_t *words) {
+// Ring update with live-entry accounting on the hidden count word; returns the entries it made live (0 or 1)
+// for the caller to add up -- one add per wave on r.live, not one per key.
+__device__ __forceinline__ unsigned ring_update(const RingDesc &r, const AccPlan &p, int64_t k, const int64_t *words) {
     bool claimed;
     int64_t *acc = find_or_insert(r.t, p.stride, k, claimed);
     count_claims(r.t.occ, claimed);
+    unsigned became = 0;
     for (int w = 0; w < p.nwords; ++w) {
         if (w == r.count_word) {
             unsigned long long old = atomicAdd((unsigned long long *)(acc + w), (unsigned long long)words[w]);
-            if (old == 0 && words[w] != 0) atomicAdd(r.live, 1ull);
+            became = old == 0 && words[w] != 0;
         } else {
             atomic_combine(acc + w, p.op[w], words[w]);
         }
     }
+    return became;
+}
+
+// Wave sum of per-lane counts added to *dst by one lane (every lane of the wave calls it).
+__device__ __forceinline__ void wave_add_signed(unsigned long long *dst, long long v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    if ((threadIdx.x & 63) == 0 && v) atomicAdd(dst, (unsigned long long)v);
+}
+
+__device__ __forceinline__ void apply_ring(const RingDesc &r, const AccPlan &p, int64_t k, const int64_t *words) {
+    if (ring_update(r, p, k, words)) atomicAdd(r.live, 1ull);
 }
 
 __device__ __forceinline__ void check_key_group(int64_t k, const WindowGeom &g, BatchStats *st) {
@@ -249,7 +263,12 @@ __global__ __launch_bounds__(256) void insert_direct_kernel(const int64_t *__res
                                                             const TableDesc *__restrict__ dir, long long dir_base,
                                                             int dir_len, BatchStats *st, RingDesc ring) {
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    long long became = 0;   // ring entries made live by this lane
+    // whole waves iterate together (the bound is rounded up to whole waves) so the live count is wave-reduced
+    const int64_t lane = threadIdx.x & 63;
+    const int64_t nw = (n + 63) & ~(int64_t)63;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i - lane < nw; i += stride) {
+        if (i >= n) continue;
         long long u = 0;
         int64_t t = ts[i];
         const int c = classify(t, g, u);
@@ -263,9 +282,10 @@ __global__ __launch_bounds__(256) void insert_direct_kernel(const int64_t *__res
         if (u >= ring.lo && u <= ring.hi) {
             int64_t words[GWO_MAX_WORDS];
             for (int w = 0; w < p.nwords; ++w) words[w] = lift_word(p, w, v);
-            apply_ring(ring, p, k, words);
+            became += ring_update(ring, p, k, words);
         }
     }
+    if (ring.lo <= ring.hi) wave_add_signed(ring.live, became);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -928,7 +948,10 @@ __global__ __launch_bounds__(256) void rehash_kernel(TableDesc src, uint64_t cap
 __global__ __launch_bounds__(256) void fold_kernel(TableDesc src, uint64_t cap, TableDesc dst, AccPlan p, int sign,
                                                    int live_word, unsigned long long *live) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i <= cap; i += stride) {
+    long long dlive = 0;   // live entries this lane added (+) or retired (-): one add per wave at the end
+    const uint64_t lane = threadIdx.x & 63, lim = (cap + 1 + 63) & ~63ull;   // whole waves iterate together
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i - lane < lim; i += stride) {
+        if (i > cap) continue;
         const int64_t *e;
         int64_t k;
         if (i < cap) {
@@ -949,13 +972,14 @@ __global__ __launch_bounds__(256) void fold_kernel(TableDesc src, uint64_t cap, 
             if (w == live_word) {
                 unsigned long long old = atomicAdd((unsigned long long *)(a + w), (unsigned long long)x);
                 long long nw = (long long)(old + (unsigned long long)x);
-                if ((long long)old <= 0 && nw > 0) atomicAdd(live, 1ull);
-                else if ((long long)old > 0 && nw <= 0) atomicAdd(live, ~0ull);  // -1
+                if ((long long)old <= 0 && nw > 0) dlive++;
+                else if ((long long)old > 0 && nw <= 0) dlive--;
             } else {
                 atomic_combine(a + w, p.op[w], x);
             }
         }
     }
+    if (live) wave_add_signed(live, dlive);
 }
 
 // ------------------------------------------------------------------------------------------------
