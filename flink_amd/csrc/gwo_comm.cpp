@@ -24,8 +24,6 @@ void launch_dest_count(const uint32_t *dest, int64_t n, unsigned long long *coun
 void launch_pack(const int64_t *key, const int64_t *ts, const int64_t *val, const uint32_t *perm, int64_t n,
                  int64_t *out, hipStream_t s);
 void launch_unpack(const int64_t *in, int64_t n, int64_t *key, int64_t *ts, int64_t *val, hipStream_t s);
-int radix_sort_pairs(const uint32_t *keys, const uint32_t *vals, int64_t n, int key_bits, uint32_t *k1, uint32_t *v1,
-                     uint32_t *k2, uint32_t *v2, uint32_t *hist, hipStream_t s);
 void launch_route(const int64_t *key, const int64_t *ts, const int64_t *val, int64_t n, int kind, int max_par,
                   int nranks, unsigned long long *cursor, uint64_t cap, int64_t *send, hipStream_t s);
 void launch_route_collect(unsigned long long *cursor, int nranks, unsigned long long *counts, hipStream_t s);

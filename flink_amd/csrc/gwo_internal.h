@@ -245,7 +245,7 @@ void launch_slide_refire_slots(const int64_t *key, const int64_t *r_idx, const l
 // gwo_sort.hip: stable LSD radix sort of (uint32 key, uint32 payload; vals NULL = index); returns 0 when the
 // result is in (k1, v1), 1 when in (k2, v2)
 int radix_sort_pairs(const uint32_t *keys, const uint32_t *vals, int64_t n, int key_bits, uint32_t *k1, uint32_t *v1,
-                     uint32_t *k2, uint32_t *v2, uint32_t *hist, hipStream_t s);
+                     uint32_t *k2, uint32_t *v2, uint32_t *hist, hipStream_t s, int digit_bits = 8);
 void launch_key_groups_utf16(const uint16_t *chars, const int64_t *offsets, int64_t n, int max_par, int par,
                              int32_t *hash, int32_t *kg, int32_t *op, hipStream_t s);
 void launch_table_load(const SnapCols &c, int64_t n, const TableDesc &t, const AccPlan &p, hipStream_t s);

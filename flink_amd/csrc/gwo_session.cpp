@@ -197,7 +197,7 @@ gwo_status Handle::insert_session(const int64_t *k, const int64_t *t, const int6
     GWO_TRY(ensure_buf(S.k2, n * 4));
     GWO_TRY(ensure_buf(S.v2, n * 4));
     int64_t nblocks = (n + 4095) / 4096;
-    GWO_TRY(ensure_buf(S.hist, (size_t)256 * nblocks * 4 + 16));
+    GWO_TRY(ensure_buf(S.hist, (size_t)1024 * nblocks * 4 + 16));
     GWO_TRY(hipcheck(hipMemsetAsync(S.d_err, 0, sizeof(SessErr), stream), "err"));
     if (side_enabled() && side_cap - (long long)side_rows_committed < n)
         GWO_TRY(grow_side((long long)side_rows_committed + n));
@@ -205,8 +205,8 @@ gwo_status Handle::insert_session(const int64_t *k, const int64_t *t, const int6
     prof_begin(GWO_KERNEL_SESSION);
     launch_sess_slot(k, t, n, desc(S.T), S.T.cap, S.stride, g, (uint32_t *)S.rec_slot.ptr, S.d_err, stream);
     GWO_TRY(launch_ok("sess slot"));
-    int bits = 8;
-    while (bits < 32 && (S.T.cap >> bits) > 0) bits += 8;
+    int bits = 1;   // slots are 0..cap (cap: the side slot)
+    while (bits < 32 && (S.T.cap >> bits) > 0) bits++;
     int which = radix_sort_pairs((const uint32_t *)S.rec_slot.ptr, nullptr, n, bits, (uint32_t *)S.k1.ptr,
                                  (uint32_t *)S.v1.ptr, (uint32_t *)S.k2.ptr, (uint32_t *)S.v2.ptr,
                                  (uint32_t *)S.hist.ptr, stream);
