@@ -42,8 +42,10 @@ struct Comm {
     // key groups and this were GPU 0; the other "GPUs'" records go through RCCL to this rank itself and come back
     // as received records -- a rank's whole data path at P GPUs on one GPU (outputs unchanged: it owns every key).
     int vranks = 0;
-    uint64_t rcap = 0;            // send region capacity of the routed K1 (records)
-    int64_t recv_n = 0;           // records received by the last exchange
+    uint64_t rcap = 0, wcap = 0;  // narrow / wide send region capacities of the routed K1 (records)
+    int64_t tbase = 0;            // the routed batch's timestamp base (20-B wire records carry int32 ts - tbase)
+    int64_t recv_n = 0, recv_w = 0;   // narrow / wide records received by the last routed exchange
+    int64_t recv_off_w = 0;       // word offset of the wide records in recvbuf
 };
 
 static int route_ranks(const Comm &C) { return C.vranks > 1 ? C.vranks : C.nranks; }
@@ -184,23 +186,27 @@ gwo_status Handle::comm_route_args(int64_t n, LogRoute *rt, bool *on) {
     const int P = route_ranks(C);
     *on = P > 1;
     if (!*on) return GWO_OK;
-    GWO_TRY(ensure_buf(C.counts, (size_t)2 * P * 8 + 16));
+    GWO_TRY(ensure_buf(C.counts, (size_t)4 * P * 8 + 16));
     if (!C.cursor.ptr) {
-        GWO_TRY(ensure_buf(C.cursor, std::max(route_cursor_bytes(), (size_t)LOG_RT_MAX * LOG_CUR_STRIDE * 8)));
+        GWO_TRY(ensure_buf(C.cursor, std::max(route_cursor_bytes(), (size_t)2 * LOG_RT_MAX * LOG_CUR_STRIDE * 8)));
         GWO_TRY(hipcheck(hipMemsetAsync(C.cursor.ptr, 0, C.cursor.bytes, stream), "route cursors"));
     }
     const double mean = (double)n / P;
-    C.rcap = (uint64_t)(mean + 6.0 * std::sqrt(mean) + 64.0);
-    GWO_TRY(ensure_buf(C.sendbuf, (size_t)P * C.rcap * 24 + 24));
+    C.rcap = ((uint64_t)(mean + 6.0 * std::sqrt(mean) + 64.0) + 1) & ~1ull;   // even: regions stay 8-B aligned
+    C.wcap = 256 + (uint64_t)n / 1024;
+    C.tbase = log_rt_tbase(wm);   // the watermark every rank shares (min over ranks)
+    GWO_TRY(ensure_buf(C.sendbuf, (size_t)P * (C.rcap * 20 + C.wcap * 24) + 24));
     *rt = LogRoute{};
     rt->mode = 1;
     rt->nranks = P;
     rt->me = C.rank;
     rt->send = (int64_t *)C.sendbuf.ptr;
     rt->rcap = C.rcap;
+    rt->wcap = C.wcap;
+    rt->tbase = C.tbase;
     rt->cursor = (unsigned long long *)C.cursor.ptr;
     rt->count = (unsigned long long *)C.counts.ptr;
-    if (n == 0) GWO_TRY(hipcheck(hipMemsetAsync(C.counts.ptr, 0, (size_t)2 * P * 8, stream), "counts"));
+    if (n == 0) GWO_TRY(hipcheck(hipMemsetAsync(C.counts.ptr, 0, (size_t)4 * P * 8, stream), "counts"));
     return GWO_OK;
 }
 
@@ -209,71 +215,114 @@ gwo_status Handle::comm_mark_routed() {
     return hipcheck(hipEventRecord(comm->ev_routed, stream), "event");
 }
 
-// After the routed K1 is queued: exchange the per-destination counts (RCCL, comm stream), bring them to the host
-// (the batch's one host round trip for the exchange), re-route on a region overflow, and queue the records'
-// exchange on the comm stream -- it runs while the main stream finishes this batch's own records.
+// After the routed K1 is queued: exchange the per-destination (narrow, wide) counts (RCCL, comm stream), bring
+// them to the host (the batch's one host round trip for the exchange), re-route on a region overflow, and queue
+// the records' exchange on the comm stream -- it runs while the main stream finishes this batch's own records.
+// Per peer: the narrow records as three arrays (keys, values, int32 timestamps: 20 B a record), then the wide ones.
 gwo_status Handle::comm_after_route(const int64_t *k, const int64_t *t, const int64_t *v, int64_t n) {
     Comm &C = *comm;
     const int P = route_ranks(C), me = C.rank;
     const bool virt = C.vranks > 1;
-    unsigned long long *d_send = (unsigned long long *)C.counts.ptr, *d_recv = d_send + P;
+    unsigned long long *d_send = (unsigned long long *)C.counts.ptr, *d_recv = d_send + 2 * P;
     if (n == 0) GWO_TRY(comm_mark_routed());   // (no K1 ran: the counts were zeroed on the main stream)
     GWO_TRY(hipcheck(hipStreamWaitEvent(C.cs, C.ev_routed, 0), "event wait"));
     if (!virt) {
         GWO_TRY(nccl_ok(this, ncclGroupStart(), "group"));
         for (int p = 0; p < P; ++p) {
             if (p == me) continue;
-            GWO_TRY(nccl_ok(this, ncclSend(d_send + p, 1, ncclUint64, p, C.nc, C.cs), "send count"));
-            GWO_TRY(nccl_ok(this, ncclRecv(d_recv + p, 1, ncclUint64, p, C.nc, C.cs), "recv count"));
+            GWO_TRY(nccl_ok(this, ncclSend(d_send + 2 * p, 2, ncclUint64, p, C.nc, C.cs), "send count"));
+            GWO_TRY(nccl_ok(this, ncclRecv(d_recv + 2 * p, 2, ncclUint64, p, C.nc, C.cs), "recv count"));
         }
         GWO_TRY(nccl_ok(this, ncclGroupEnd(), "group end"));
     }
-    GWO_TRY(hipcheck(hipMemcpyAsync(C.h_counts, d_send, (size_t)(virt ? 1 : 2) * P * 8, hipMemcpyDeviceToHost, C.cs),
-                     "counts"));
+    unsigned long long *hs = C.h_counts, *hr = C.h_counts + 2 * P;
+    GWO_TRY(hipcheck(hipMemcpyAsync(hs, d_send, (size_t)(virt ? 2 : 4) * P * 8, hipMemcpyDeviceToHost, C.cs), "counts"));
     GWO_TRY(hipcheck(hipStreamSynchronize(C.cs), "counts sync"));
     if (virt)   // what this rank routes to virtual GPU p comes back to it "from p"
-        for (int p = 0; p < P; ++p) C.h_counts[P + p] = C.h_counts[p];
-    C.h_counts[me] = 0;       // (K1 never routes a record to its own GPU)
-    C.h_counts[P + me] = 0;
-    uint64_t cap = C.rcap, mx = 0;
-    for (int p = 0; p < P; ++p) mx = std::max<uint64_t>(mx, C.h_counts[p]);
-    if (mx > cap) {   // skewed keys: a region overflowed -- route the batch again with exact regions
-        cap = mx;
-        GWO_TRY(ensure_buf(C.sendbuf, (size_t)P * cap * 24 + 24));
-        launch_route(k, t, v, n, cfg.key_kind, cfg.max_parallelism, P, (unsigned long long *)C.cursor.ptr, cap,
-                     (int64_t *)C.sendbuf.ptr, stream);
-        launch_route_collect((unsigned long long *)C.cursor.ptr, P, d_recv, stream);   // (resets its cursors; the
-                                                                                        //  counts are known)
-        GWO_TRY(launch_ok("route"));
+        for (int q = 0; q < 2 * P; ++q) hr[q] = hs[q];
+    hs[2 * me] = hs[2 * me + 1] = 0;   // (K1 never routes a record to its own GPU)
+    hr[2 * me] = hr[2 * me + 1] = 0;
+    uint64_t rcap = C.rcap, wcap = C.wcap, mx = 0, mw = 0;
+    for (int p = 0; p < P; ++p) {
+        mx = std::max<uint64_t>(mx, hs[2 * p]);
+        mw = std::max<uint64_t>(mw, hs[2 * p + 1]);
+    }
+    if (mx > rcap || mw > wcap) {   // skewed keys: a region overflowed -- route the batch again with exact regions
+        rcap = (std::max<uint64_t>(rcap, mx) + 1) & ~1ull;
+        wcap = std::max<uint64_t>(wcap, mw);
+        GWO_TRY(hipcheck(hipStreamSynchronize(stream), "re-route"));   // the send buffer may move
+        GWO_TRY(ensure_buf(C.sendbuf, (size_t)P * (rcap * 20 + wcap * 24) + 24));
+        LogRoute rt{};
+        rt.mode = 3;   // route only: this GPU's records were partitioned by the first K1
+        rt.nranks = P;
+        rt.me = me;
+        rt.send = (int64_t *)C.sendbuf.ptr;
+        rt.rcap = rcap;
+        rt.wcap = wcap;
+        rt.tbase = C.tbase;
+        rt.cursor = (unsigned long long *)C.cursor.ptr;
+        GWO_TRY(ensure_buf(C.counts, (size_t)6 * P * 8 + 16));
+        rt.count = (unsigned long long *)C.counts.ptr + 4 * P;   // (scratch: the counts are known)
+        GWO_TRY(log_route_only(k, t, v, n, rt));
         GWO_TRY(comm_mark_routed());
         GWO_TRY(hipcheck(hipStreamWaitEvent(C.cs, C.ev_routed, 0), "event wait"));
     }
-    std::vector<uint64_t> roff(P + 1, 0);
-    for (int p = 0; p < P; ++p) roff[p + 1] = roff[p] + C.h_counts[P + p];
-    const int64_t R = (int64_t)roff[P];
-    GWO_TRY(ensure_buf(C.recvbuf, R * 24 + 24));
-    const int64_t *sb = (const int64_t *)C.sendbuf.ptr;
+    std::vector<uint64_t> rn(P + 1, 0), rw(P + 1, 0);
+    for (int p = 0; p < P; ++p) {
+        rn[p + 1] = rn[p] + hr[2 * p];
+        rw[p + 1] = rw[p] + hr[2 * p + 1];
+    }
+    const int64_t RN = (int64_t)rn[P], RW = (int64_t)rw[P];
+    // receive buffer: keys[RN], values[RN], int32 ts[RN] (padded to a word), then the wide records
+    const int64_t ts_words = (RN + 1) / 2;
+    C.recv_off_w = 2 * RN + ts_words;
+    GWO_TRY(ensure_buf(C.recvbuf, (size_t)(C.recv_off_w + 3 * RW) * 8 + 24));
+    int64_t *rb = (int64_t *)C.recvbuf.ptr;
+    int64_t *sb = (int64_t *)C.sendbuf.ptr;
     prof_begin(GWO_KERNEL_EXCHANGE, C.cs);
     GWO_TRY(nccl_ok(this, ncclGroupStart(), "group"));
     for (int p = 0; p < P; ++p) {
         if (p == me) continue;
         const int peer = virt ? me : p;
-        const uint64_t sc = C.h_counts[p], rc = C.h_counts[P + p];
-        if (sc) GWO_TRY(nccl_ok(this, ncclSend(sb + 3 * (uint64_t)p * cap, 3 * sc, ncclInt64, peer, C.nc, C.cs), "send"));
-        if (rc)
-            GWO_TRY(nccl_ok(this, ncclRecv((int64_t *)C.recvbuf.ptr + 3 * roff[p], 3 * rc, ncclInt64, peer, C.nc, C.cs),
-                            "recv"));
+        const uint64_t sn = hs[2 * p], sw = hs[2 * p + 1], qn = hr[2 * p], qw = hr[2 * p + 1];
+        if (sn) {
+            GWO_TRY(nccl_ok(this, ncclSend(log_rt_keys(sb, rcap, p), sn, ncclInt64, peer, C.nc, C.cs), "send keys"));
+            GWO_TRY(nccl_ok(this, ncclSend(log_rt_vals(sb, rcap, p), sn, ncclInt64, peer, C.nc, C.cs), "send values"));
+            GWO_TRY(nccl_ok(this, ncclSend(log_rt_ts32(sb, rcap, p), sn, ncclInt32, peer, C.nc, C.cs), "send ts"));
+        }
+        if (sw)
+            GWO_TRY(nccl_ok(this, ncclSend(log_rt_wide(sb, rcap, P, wcap, p), 3 * sw, ncclInt64, peer, C.nc, C.cs),
+                            "send wide"));
+        if (qn) {
+            GWO_TRY(nccl_ok(this, ncclRecv(rb + rn[p], qn, ncclInt64, peer, C.nc, C.cs), "recv keys"));
+            GWO_TRY(nccl_ok(this, ncclRecv(rb + RN + rn[p], qn, ncclInt64, peer, C.nc, C.cs), "recv values"));
+            GWO_TRY(nccl_ok(this, ncclRecv((int32_t *)(rb + 2 * RN) + rn[p], qn, ncclInt32, peer, C.nc, C.cs),
+                            "recv ts"));
+        }
+        if (qw)
+            GWO_TRY(nccl_ok(this, ncclRecv(rb + C.recv_off_w + 3 * rw[p], 3 * qw, ncclInt64, peer, C.nc, C.cs),
+                            "recv wide"));
     }
     GWO_TRY(nccl_ok(this, ncclGroupEnd(), "group end"));
-    prof_end(GWO_KERNEL_EXCHANGE, R, C.cs);
+    prof_end(GWO_KERNEL_EXCHANGE, RN + RW, C.cs);
     GWO_TRY(hipcheck(hipEventRecord(C.ev_recv, C.cs), "event"));
-    C.recv_n = R;
+    C.recv_n = RN;
+    C.recv_w = RW;
     return GWO_OK;
 }
 
-void Handle::comm_received(const int64_t **aos, int64_t *rn) const {
-    *aos = (const int64_t *)comm->recvbuf.ptr;
-    *rn = comm->recv_n;
+Handle::Received Handle::comm_received() const {
+    const Comm &C = *comm;
+    Received R;
+    const int64_t *rb = (const int64_t *)C.recvbuf.ptr;
+    R.n = C.recv_n;
+    R.key = rb;
+    R.val = rb + C.recv_n;
+    R.ts32 = (const int32_t *)(rb + 2 * C.recv_n);
+    R.tbase = C.tbase;
+    R.wide = rb + C.recv_off_w;
+    R.wide_n = C.recv_w;
+    return R;
 }
 
 // The main stream waits for the exchange's receives (comm stream) before reading the received records.
@@ -353,7 +402,7 @@ extern "C" gwo_status gwo_comm_init(gwo_handle *hh, const uint8_t *id, int32_t n
             C->vranks = v > 1 && v <= LOG_RT_MAX ? v : 0;
         }
     const int cranks = std::max(nranks, C->vranks);
-    if (hipHostMalloc((void **)&C->h_counts, (size_t)2 * cranks * 8 + 16, hipHostMallocDefault) != hipSuccess ||
+    if (hipHostMalloc((void **)&C->h_counts, (size_t)4 * cranks * 8 + 16, hipHostMallocDefault) != hipSuccess ||
         hipHostMalloc((void **)&C->h_wm, 16, hipHostMallocDefault) != hipSuccess) {
         delete C;
         return GWO_ERR_OUT_OF_MEMORY;

@@ -231,11 +231,10 @@ gwo_status Handle::submit(const int64_t *key, const int64_t *ts, const void *val
         if (!routed) return n ? insert_log(dk, dt, dv, n) : GWO_OK;   // one rank: nothing leaves this GPU
         if (n > 0) GWO_TRY(insert_log(dk, dt, dv, n, 1, &rt));
         else GWO_TRY(comm_after_route(dk, dt, dv, 0));
-        const int64_t *aos = nullptr;
-        int64_t rn = 0;
-        comm_received(&aos, &rn);
+        const Received R = comm_received();
         GWO_TRY(comm_wait_received());
-        return rn ? insert_log(aos, aos + 1, aos + 2, rn, 3) : GWO_OK;
+        if (R.n) GWO_TRY(insert_log(R.key, (const int64_t *)R.ts32, R.val, R.n, 1, nullptr, true, R.tbase));
+        return R.wide_n ? insert_log(R.wide, R.wide + 1, R.wide + 2, R.wide_n, 3) : GWO_OK;
     }
     if (comm) {
         const int64_t *aos = nullptr, *loc = nullptr;

@@ -292,8 +292,9 @@ struct Handle {
     gwo_status log_split_exact(long long base, int nunits, uint64_t cap, const uint64_t *counts, int tmpx);
     gwo_status log_split_dev(const LogJob &J, const unsigned long long *rbp);
     gwo_status log_resolve_split();
+    // ts32: `t` points at int32 timestamps - tbase (records received in the 20-B wire format)
     gwo_status insert_log(const int64_t *k, const int64_t *t, const int64_t *v, int64_t n, int64_t stride = 1,
-                          const LogRoute *route = nullptr);
+                          const LogRoute *route = nullptr, bool ts32 = false, int64_t tbase = 0);
     gwo_status log_k1(LogJob &J, bool first_pass);
     LogThr log_thresholds(const LogJob &J) const;
     void log_uncarve(const LogJob &J, int w, uint64_t keep);
@@ -321,9 +322,19 @@ struct Handle {
     // keyBy routing fused into the log layout's K1 (gwo_comm.cpp): arguments of the batch's routed K1 (*on false:
     // nothing to route -- one rank), the exchange after it, and the records received
     gwo_status comm_route_args(int64_t n, LogRoute *rt, bool *on);
+    // K1 in route-only mode (rt.mode 3) over a batch's columns: the exact-capacity re-route after a region overflow
+    gwo_status log_route_only(const int64_t *k, const int64_t *t, const int64_t *v, int64_t n, const LogRoute &rt);
     gwo_status comm_mark_routed();
     gwo_status comm_after_route(const int64_t *k, const int64_t *t, const int64_t *v, int64_t n);
-    void comm_received(const int64_t **aos, int64_t *rn) const;
+    // records received by the last exchange: 20-B ones as columns (keys, values, int32 ts - tbase) and 24-B ones
+    struct Received {
+        const int64_t *key = nullptr, *val = nullptr;
+        const int32_t *ts32 = nullptr;
+        int64_t n = 0, tbase = 0;
+        const int64_t *wide = nullptr;   // {key, ts, value} records
+        int64_t wide_n = 0;
+    };
+    Received comm_received() const;
 
     void prof_begin(int k, hipStream_t s = nullptr);
     void prof_end(int k, int64_t items, hipStream_t s = nullptr);

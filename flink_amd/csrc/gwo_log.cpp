@@ -51,6 +51,8 @@ struct LogJob {
     char *carve_at[LOG_NU] = {};  // start of the carved segment records
     char *carve_end[LOG_NU] = {}; // end of the carve (the window's chunk cursor right after it)
     LogRoute rt{};               // multi-GPU: the first K1 routes other GPUs' records (mode 1), re-runs skip them (2)
+    bool ts32 = false;           // t holds int32 timestamps - tbase (records received in the 20-B wire format)
+    int64_t tbase = 0;
 };
 
 struct LogState {
@@ -140,6 +142,7 @@ gwo_status Handle::log_init() {
         for (int q = 0; q < LOG_SHARDS; ++q) {
             sh[(size_t)q * LOG_CUR_STRIDE + K1S_MIN] = 0x7fffffffffffffffull;
             sh[(size_t)q * LOG_CUR_STRIDE + K1S_MAX] = 0x8000000000000000ull;
+            sh[(size_t)q * LOG_CUR_STRIDE + K1S_NEXT] = 0x7fffffffffffffffull;
         }
         GWO_TRY(dalloc((void **)&L.d_k1sh, sh.size() * 8));
         GWO_TRY(hipcheck(hipMemcpy(L.d_k1sh, sh.data(), sh.size() * 8, hipMemcpyHostToDevice), "K1 shards"));
@@ -549,7 +552,9 @@ gwo_status Handle::log_k1(LogJob &J, bool first_pass) {
         GWO_TRY(ensure_buf(tmp, (size_t)std::max(J.nunits, LOG_NU) * LOG_ND * LOG_XG * J.cap * W * 8));
     }
     const bool side = first_pass && side_enabled();
-    const LogThr thr = log_thresholds(J);
+    LogThr thr = log_thresholds(J);
+    thr.ts32 = J.ts32 ? 1 : 0;
+    thr.tbase = J.tbase;
     prof_begin(GWO_KERNEL_INSERT);
     launch_log_part(J.k, J.t, J.v, J.n, J.stride, J.g, J.base, J.nunits, needs_value, L.d_cursor, J.cap,
                     (int64_t *)tmp.ptr, d_stats, (int64_t *)side_key.ptr, (int64_t *)side_ts.ptr,
@@ -690,10 +695,10 @@ gwo_status Handle::log_resolve_batch(LogJob &J, bool &refire) {
                 if (rbp[LOG_RB_GO] && J.base <= lo && lo < J.base + J.nunits) {
                     // the speculative pass 2 is running the device plan: commit its segments
                     GWO_TRY(log_commit_spec(J, rbp));
-                    const long long chunk_hi = J.base + J.nunits - 1;
-                    if (chunk_hi >= hi) break;
+                    const long long chunk_hi = J.base + J.nunits - 1, nx = (long long)rbp[LOG_RB_NEXT];
+                    if (chunk_hi >= hi || nx > hi) break;
                     J.spec = false;
-                    J.base = chunk_hi + 1;
+                    J.base = std::max(chunk_hi + 1, nx);   // the next window holding records (not every empty one between)
                     J.nunits = (int)std::min<long long>(LOG_NU, hi - J.base + 1);
                     J.slot = L.free_slot();
                     GWO_TRY(log_k1(J, false));
@@ -717,9 +722,9 @@ gwo_status Handle::log_resolve_batch(LogJob &J, bool &refire) {
             continue;
         }
         GWO_TRY(log_split_dev(J, rbp));
-        const long long chunk_hi = J.base + J.nunits - 1;
-        if (chunk_hi >= hi) break;
-        J.base = chunk_hi + 1;
+        const long long chunk_hi = J.base + J.nunits - 1, nx = (long long)rbp[LOG_RB_NEXT];
+        if (chunk_hi >= hi || nx > hi) break;
+        J.base = std::max(chunk_hi + 1, nx);   // the next window holding records (not every empty one between)
         J.nunits = (int)std::min<long long>(LOG_NU, hi - J.base + 1);
         J.slot = L.free_slot();
         GWO_TRY(log_k1(J, false));
@@ -727,6 +732,24 @@ gwo_status Handle::log_resolve_batch(LogJob &J, bool &refire) {
     hist_hint = lo;
     L.span_hint = hi - lo + 2;
     return GWO_OK;
+}
+
+// Route-only K1 (rt.mode 3): every other GPU's record of the batch goes to the send regions again (exact
+// capacities after an overflow); this GPU's records -- partitioned by the batch's first K1 -- are skipped, and the
+// tail moves only the route counts (no plan, no readback: the first K1's are in use).
+gwo_status Handle::log_route_only(const int64_t *k, const int64_t *t, const int64_t *v, int64_t n, const LogRoute &rt) {
+    LogState &L = *logst;
+    if (n == 0) return GWO_OK;
+    CollectArgs ca{};
+    ca.done = L.d_done;
+    ca.shard = L.d_k1sh;
+    LogThr thr{};
+    for (int j = 0; j <= LOG_NU; ++j) thr.bound[j] = (int64_t)0x7fffffffffffffffLL;
+    thr.full_range = 1;
+    const DevBuf &tmp = L.tmp[0];
+    launch_log_part(k, t, v, n, 1, geom_now(), 0, 1, needs_value, L.d_cursor, 0, (int64_t *)tmp.ptr, d_stats,
+                    nullptr, nullptr, nullptr, d_side_count, 0, 0, ca, thr, rt, stream);
+    return launch_ok("route-only partition");
 }
 
 // Resolves the pipelined batch, if any (every call that observes state or fires windows comes here first).
@@ -738,10 +761,12 @@ gwo_status Handle::log_flush() {
 }
 
 gwo_status Handle::insert_log(const int64_t *k, const int64_t *t, const int64_t *v, int64_t n, int64_t stride,
-                              const LogRoute *route) {
+                              const LogRoute *route, bool ts32, int64_t tbase) {
     LogState &L = *logst;
     LogJob J;
     if (route) J.rt = *route;
+    J.ts32 = ts32;
+    J.tbase = tbase;
     J.k = k;
     J.t = t;
     J.v = v;

@@ -72,7 +72,8 @@ struct LogThr {
     uint32_t cls;                // 2 bits per window: 0 accept, 1 window late (cleanup time passed), 2 re-fire
     int32_t ok;                  // 1: the bounds are valid
     int32_t full_range;          // 1: the subtask owns every key group (no key-group check needed)
-    int32_t pad;
+    int32_t ts32;                // 1: `ts` holds int32 timestamps - tbase (records received in the 20-B wire format)
+    int64_t tbase;
 };
 
 // The segment descriptors of one pass-2 launch (kernel argument).
@@ -88,7 +89,9 @@ static constexpr int LOG_RB_SEG = LOG_RB_STATS + (int)((sizeof(BatchStats) + 7) 
 static constexpr int LOG_RB_CHUNKS = LOG_RB_SEG + LOG_NU;
 static constexpr int LOG_RB_GO = LOG_RB_CHUNKS + 1;
 static constexpr int LOG_RB_MAXREG = LOG_RB_GO + 1;      // largest region count (> cap: K1 dropped records)
-static constexpr int LOG_RB_SEQ = LOG_RB_MAXREG + 1;     // written last: the launch's sequence number
+static constexpr int LOG_RB_NEXT = LOG_RB_MAXREG + 1;    // the first window after the launch's range holding accepted
+                                                         // records (Long.MAX_VALUE: none) -- the next K1 range starts there
+static constexpr int LOG_RB_SEQ = LOG_RB_NEXT + 1;       // written last: the launch's sequence number
 static constexpr int LOG_RB_WORDS = LOG_RB_SEQ + 1;
 
 // What K1's last workgroup needs to plan pass 2 (the former collect step, fused into K1's tail).
@@ -112,30 +115,55 @@ struct CollectArgs {
 // (device-scope atomics on the same address serialise at ~12 ns each on MI355X: 4 per-wave atomics per
 // workgroup on one word cost ~25 us at the end of a 512-workgroup launch); the tail folds the shards.
 #define LOG_SHARDS 16
-enum : int { K1S_MIN = 0, K1S_MAX, K1S_ACC, K1S_LATE, K1S_REFIRE, K1S_BADTS, K1S_BADKG, K1S_HOUT, K1_SW };
+enum : int { K1S_MIN = 0, K1S_MAX, K1S_ACC, K1S_LATE, K1S_REFIRE, K1S_BADTS, K1S_BADKG, K1S_HOUT, K1S_NEXT, K1_SW };
 static constexpr size_t LOG_DONE_WORDS = (LOG_SHARDS + 1) * LOG_CUR_STRIDE;
 
 // Multi-GPU keyBy routing fused into K1 (the log layout's first K1 over a batch): a record whose key group
 // belongs to another GPU -- computeOperatorIndexForKeyGroup(assignToKeyGroup(key)) != me,
-// KeyGroupRangeAssignment.java:118-119 -- is not classified here (its owner does that) but appended as a 24-B
-// {key, ts, value} record to that destination's send region; one reservation per (tile, destination).
+// KeyGroupRangeAssignment.java:118-119 -- is not classified here (its owner does that) but appended to that
+// destination's send region; one reservation per (tile, destination).  Wire format: 20-B records, SoA per
+// destination region (keys, values, int32 timestamp - tbase); tbase = the watermark every rank shares (the
+// watermark is the min over ranks), so a timestamp within +-24.8 days of it travels as 4 bytes.  A record outside
+// that goes as a 24-B {key, ts, value} record to the destination's small "wide" region (one atomic each: rare).
 #define LOG_RT_MAX 256           // destinations (ranks) K1 routes to
 #define LOG_RT_B 1024            // K1 code of a routed record: bucket field LOG_RT_B + destination
 struct LogRoute {
-    int32_t mode;                // 0: no routing; 1: route remote records; 2: skip them (a re-run of a routed batch)
+    int32_t mode;                // 0: no routing; 1: route remote records; 2: skip them (a re-run of a routed batch);
+                                 // 3: route only, this GPU's records skipped (exact-capacity re-route after an overflow)
     int32_t nranks;              // destinations
     int32_t me;                  // this GPU's index: its records stay
     int32_t pad;
-    int64_t *send;               // nranks regions of rcap {key, ts, value} records (region p at send + 3 * p * rcap)
-    uint64_t rcap;
-    unsigned long long *cursor;  // [nranks * LOG_CUR_STRIDE] region cursors (the tail moves them to count, zeroed)
-    unsigned long long *count;   // out: records routed per destination (above rcap: the region overflowed)
+    int64_t *send;               // nranks narrow regions (log_rt_keys/vals/ts32), then nranks wide regions (log_rt_wide)
+    uint64_t rcap;               // narrow region capacity (records, even: regions stay 8-B aligned)
+    uint64_t wcap;               // wide region capacity (records)
+    int64_t tbase;               // timestamps travel as int32 ts - tbase
+    unsigned long long *cursor;  // [2 * LOG_RT_MAX * LOG_CUR_STRIDE]: narrow cursors, then wide cursors (the tail moves
+                                 // them to count and zeroes them)
+    unsigned long long *count;   // out: [2 * nranks] (narrow, wide) records per destination (above capacity: overflow)
 };
+// narrow region d: keys[rcap] (int64), values[rcap] (int64), ts[rcap] (int32); 20 B per record = 2.5 words
+static inline __host__ __device__ int64_t *log_rt_keys(int64_t *send, uint64_t rcap, int d) {
+    return send + (uint64_t)d * rcap * 5 / 2;
+}
+static inline __host__ __device__ int64_t *log_rt_vals(int64_t *send, uint64_t rcap, int d) {
+    return log_rt_keys(send, rcap, d) + rcap;
+}
+static inline __host__ __device__ int32_t *log_rt_ts32(int64_t *send, uint64_t rcap, int d) {
+    return (int32_t *)(log_rt_keys(send, rcap, d) + 2 * rcap);
+}
+static inline __host__ __device__ int64_t *log_rt_wide(int64_t *send, uint64_t rcap, int nranks, uint64_t wcap, int d) {
+    return send + (uint64_t)nranks * rcap * 5 / 2 + (uint64_t)d * wcap * 3;
+}
+static inline __host__ __device__ bool log_rt_fits(int64_t t, int64_t tbase) {
+    return t >= tbase ? (uint64_t)t - (uint64_t)tbase <= 0x7fffffffull : (uint64_t)tbase - (uint64_t)t <= 0x80000000ull;
+}
+static inline int64_t log_rt_tbase(int64_t wm) { return wm == (int64_t)0x8000000000000000LL ? 0 : wm; }
 
 namespace gwo {
 // K1: classify + key-group check + late accounting + (window, coarse digit) grouping of a batch; its last
 // workgroup writes the readback block and the device plan of pass 2, and resets cursors and statistics.
 // key/ts/val columns with `stride` int64 words between records (1: SoA columns; 3: {key, ts, value} records)
+// (thr.ts32: `ts` points at int32 timestamps - thr.tbase, columns only)
 void launch_log_part(const int64_t *key, const int64_t *ts, const int64_t *val, int64_t n, int64_t stride,
                      const WindowGeom &g,
                      long long base, int nunits, int has_val, unsigned long long *cursor, uint64_t cap,

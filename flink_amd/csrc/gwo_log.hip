@@ -121,20 +121,22 @@ __device__ __forceinline__ void k1_plan_tail(unsigned long long *cursor, BatchSt
         s_maxreg = 0;
     }
     if (rt.mode == 1)   // routed records per destination; the cursors start the next routed K1 at zero
-        for (int p = t; p < rt.nranks; p += LOG_K1_THREADS)
-            rt.count[p] = atomicExch(&rt.cursor[(size_t)p * LOG_CUR_STRIDE], 0ull);
+        for (int p = t; p < rt.nranks; p += LOG_K1_THREADS) {
+            rt.count[2 * p] = atomicExch(&rt.cursor[(size_t)p * LOG_CUR_STRIDE], 0ull);
+            rt.count[2 * p + 1] = atomicExch(&rt.cursor[(size_t)(LOG_RT_MAX + p) * LOG_CUR_STRIDE], 0ull);
+        }
     __shared__ unsigned long long s_k1[K1_SW];
     if (t < SW) {   // read-and-reset through the same device-scope atomics the workgroups used
         const unsigned long long reset = t == 0 ? 0x7fffffffffffffffull : (t == 1 ? 0x8000000000000000ull : 0ull);
         s_sw[t] = atomicExch(&sw[t], reset);
     } else if (t >= K1_T0 && t < K1_T0 + K1_SW) {   // fold (and reset) the statistics shards
         const int f = t - K1_T0;
-        const unsigned long long init =
-            f == K1S_MIN ? 0x7fffffffffffffffull : (f == K1S_MAX ? 0x8000000000000000ull : 0ull);
+        const unsigned long long init = (f == K1S_MIN || f == K1S_NEXT) ? 0x7fffffffffffffffull
+                                                                        : (f == K1S_MAX ? 0x8000000000000000ull : 0ull);
         unsigned long long r = init;
         for (int q = 0; q < LOG_SHARDS; ++q) {
             const unsigned long long x = atomicExch(&a.shard[q * LOG_CUR_STRIDE + f], init);
-            if (f == K1S_MIN) r = (long long)x < (long long)r ? x : r;
+            if (f == K1S_MIN || f == K1S_NEXT) r = (long long)x < (long long)r ? x : r;
             else if (f == K1S_MAX) r = (long long)x > (long long)r ? x : r;
             else r += x;
         }
@@ -153,6 +155,7 @@ __device__ __forceinline__ void k1_plan_tail(unsigned long long *cursor, BatchSt
         W.bad_ts = s_k1[K1S_BADTS];
         W.bad_kg = s_k1[K1S_BADKG];
         W.hist_out = s_k1[K1S_HOUT];
+        a.rb[LOG_RB_NEXT] = s_k1[K1S_NEXT];
     }
     __syncthreads();
     if (t < SW) a.rb[LOG_RB_STATS + t] = s_sw[t];
@@ -232,7 +235,8 @@ __device__ __forceinline__ void k1_plan_tail(unsigned long long *cursor, BatchSt
 // record count (also when it exceeds cap: those records are not written and the host reruns).
 // ------------------------------------------------------------------------------------------------
 // ROUTE: the multi-GPU instance (LogRoute): records of other GPUs are routed (rt.mode 1) or skipped (2).
-template <bool HASV, int S, bool ROUTE>   // S: record stride in int64 words (1: SoA columns, 3: {key, ts, value}; 0: runtime)
+// TS32: `ts` holds int32 timestamps - th.tbase (records received in the 20-B wire format; S == 1).
+template <bool HASV, int S, bool ROUTE, bool TS32>   // S: record stride in int64 words (1: SoA columns, 3: {key, ts, value}; 0: runtime)
 __global__ __launch_bounds__(LOG_K1_THREADS) void log_part_kernel(
     const int64_t *__restrict__ key, const int64_t *__restrict__ ts, const int64_t *__restrict__ val, int64_t n,
     int64_t stride, WindowGeom g, long long base, int nunits, unsigned long long *__restrict__ cursor, uint64_t cap,
@@ -240,7 +244,8 @@ __global__ __launch_bounds__(LOG_K1_THREADS) void log_part_kernel(
     unsigned long long *side_count, long long side_cap, int side_enabled, CollectArgs ca, LogThr th, LogRoute rt) {
     constexpr int W = HASV ? 2 : 1;
     // the new segments' partition counters (pass 2's cursors) start at zero: pass 2 follows in stream order
-    for (int w = 0; w < ca.nunits; ++w) {
+    // (a route-only re-run follows a pass 2 that already used them)
+    for (int w = 0; w < ((ROUTE && rt.mode == 3) ? 0 : ca.nunits); ++w) {
         uint4 *c4 = (uint4 *)ca.cnt[w];
         const uint32_t n4 = (1u << ca.lp[w]) / 4;
         for (uint32_t i = blockIdx.x * LOG_K1_THREADS + threadIdx.x; i < n4; i += gridDim.x * LOG_K1_THREADS)
@@ -258,6 +263,7 @@ __global__ __launch_bounds__(LOG_K1_THREADS) void log_part_kernel(
     const int tid = threadIdx.x;
     const int xg = blockIdx.x % LOG_XG;                           // region group (an XCD under round-robin placement)
     long long mn = 0x7fffffffffffffffLL, mx = (long long)0x8000000000000000LL;   // accepted windows (slow path)
+    long long nx = 0x7fffffffffffffffLL;   // first accepted window after the launch's range (slow path)
     uint32_t wmask = 0;   // launch windows (bit jj) the inline path accepted records into
     unsigned acc = 0, late = 0, refire = 0, bad_ts = 0, out = 0, bad_kg = 0;   // per thread: < 2^32 records
     int64_t kk[LOG_K1_PER], vv[LOG_K1_PER], tt[LOG_K1_PER];
@@ -269,7 +275,8 @@ __global__ __launch_bounds__(LOG_K1_THREADS) void log_part_kernel(
             int64_t i = tile + j * LOG_K1_THREADS + tid;
             i = i < n ? i : (tile < n ? tile : 0);
             const int64_t o = S ? i * S : i * stride;
-            tt[j] = __builtin_nontemporal_load(ts + o);
+            tt[j] = TS32 ? th.tbase + (int64_t)__builtin_nontemporal_load((const int32_t *)ts + o)
+                         : __builtin_nontemporal_load(ts + o);
             kk[j] = __builtin_nontemporal_load(key + o);
             vv[j] = HASV ? __builtin_nontemporal_load(val + o) : 0;
         }
@@ -291,9 +298,23 @@ __global__ __launch_bounds__(LOG_K1_THREADS) void log_part_kernel(
             if (ROUTE) {   // KeyGroupStreamPartitioner.selectChannel: another GPU's record is its owner's to classify
                 const int dest = (int)(key_group(kk[j], g.key_kind, g.max_par) * rt.nranks / g.max_par);
                 if (dest != rt.me) {
-                    if (rt.mode == 1) code[j] = ((uint32_t)(LOG_RT_B + dest) << 16) | atomicAdd(&s_rcnt[dest], 1u);
+                    if (rt.mode == 1 || rt.mode == 3) {
+                        if (log_rt_fits(tt[j], rt.tbase)) {
+                            code[j] = ((uint32_t)(LOG_RT_B + dest) << 16) | atomicAdd(&s_rcnt[dest], 1u);
+                        } else {   // beyond the int32 timestamp range: a 24-B record in the wide region (rare)
+                            const unsigned long long q =
+                                atomicAdd(&rt.cursor[(size_t)(LOG_RT_MAX + dest) * LOG_CUR_STRIDE], 1ull);
+                            if (q < rt.wcap) {
+                                int64_t *w = log_rt_wide(rt.send, rt.rcap, rt.nranks, rt.wcap, dest) + q * 3;
+                                w[0] = kk[j];
+                                w[1] = tt[j];
+                                w[2] = HASV ? vv[j] : 0;
+                            }
+                        }
+                    }
                     continue;
                 }
+                if (rt.mode == 3) continue;   // route-only re-run: the first K1 partitioned this GPU's records
             }
             // the common case, inline: a timestamp inside one of the launch's windows and that window open --
             // WindowOperator.java:386-427 decided once per window (LogThr), a few compares per record
@@ -324,7 +345,7 @@ __global__ __launch_bounds__(LOG_K1_THREADS) void log_part_kernel(
             slow &= slow - 1;
             const int64_t i = tile + j * LOG_K1_THREADS + tid;
             const int64_t o = S ? i * S : i * stride;
-            const int64_t t = ts[o], k = key[o];
+            const int64_t t = TS32 ? th.tbase + (int64_t)((const int32_t *)ts)[o] : ts[o], k = key[o];
             long long u = 0;
             const int c = log_classify(t, g, u);
             if (c == L_ACCEPT) {
@@ -347,6 +368,7 @@ __global__ __launch_bounds__(LOG_K1_THREADS) void log_part_kernel(
                         if (q == j) code[q] = cd;
                 } else {
                     out++;
+                    if (w >= nunits) nx = u < nx ? u : nx;
                 }
             } else if (c == L_LATE) {
                 late++;
@@ -375,13 +397,13 @@ __global__ __launch_bounds__(LOG_K1_THREADS) void log_part_kernel(
             at[q] = c ? atomicAdd(&cursor[((size_t)b * LOG_XG + xg) * LOG_CUR_STRIDE], (unsigned long long)c) : 0ull;
         }
         unsigned long long rat = 0;
-        if (ROUTE && rt.mode == 1 && tid < nr) {
+        if (ROUTE && (rt.mode == 1 || rt.mode == 3) && tid < nr) {
             const uint32_t c = s_rcnt[tid];
             rat = c ? atomicAdd(&rt.cursor[(size_t)tid * LOG_CUR_STRIDE], (unsigned long long)c) : 0ull;
         }
         uint32_t loc[4];
         const uint32_t total = tile_offsets(s_cnt, s_off, nb, loc, per);
-        if (ROUTE && rt.mode == 1) {
+        if (ROUTE && (rt.mode == 1 || rt.mode == 3)) {
             if (tid < nr) s_rbase[tid] = rat;
             __syncthreads();
         }
@@ -392,11 +414,10 @@ __global__ __launch_bounds__(LOG_K1_THREADS) void log_part_kernel(
             if (ROUTE && b >= LOG_RT_B) {   // routed: straight from registers into the destination's run
                 const uint32_t d = b - LOG_RT_B;
                 const unsigned long long q = s_rbase[d] + (code[j] & 0xffffu);
-                if (q < rt.rcap) {
-                    int64_t *dst = rt.send + ((uint64_t)d * rt.rcap + q) * 3;
-                    dst[0] = kk[j];
-                    dst[1] = tt[j];
-                    dst[2] = HASV ? vv[j] : 0;
+                if (q < rt.rcap) {   // 20-B wire record: key, value, int32 ts - tbase (SoA per destination)
+                    log_rt_keys(rt.send, rt.rcap, (int)d)[q] = kk[j];
+                    log_rt_vals(rt.send, rt.rcap, (int)d)[q] = HASV ? vv[j] : 0;
+                    log_rt_ts32(rt.send, rt.rcap, (int)d)[q] = (int32_t)(uint32_t)((uint64_t)tt[j] - (uint64_t)rt.tbase);
                 }
                 continue;
             }
@@ -435,14 +456,16 @@ __global__ __launch_bounds__(LOG_K1_THREADS) void log_part_kernel(
     }
     // workgroup statistics -> shard blockIdx % LOG_SHARDS (zero words skipped)
     unsigned long long v[K1_SW] = {(unsigned long long)mn, (unsigned long long)mx, acc, late, refire, bad_ts, bad_kg,
-                                   out};
+                                   out, (unsigned long long)nx};
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
         const long long a = __shfl_xor((long long)v[K1S_MIN], o), b = __shfl_xor((long long)v[K1S_MAX], o);
+        const long long c = __shfl_xor((long long)v[K1S_NEXT], o);
         v[K1S_MIN] = a < (long long)v[K1S_MIN] ? (unsigned long long)a : v[K1S_MIN];
         v[K1S_MAX] = b > (long long)v[K1S_MAX] ? (unsigned long long)b : v[K1S_MAX];
+        v[K1S_NEXT] = c < (long long)v[K1S_NEXT] ? (unsigned long long)c : v[K1S_NEXT];
 #pragma unroll
-        for (int f = K1S_ACC; f < K1_SW; ++f) v[f] += __shfl_xor(v[f], o);
+        for (int f = K1S_ACC; f < K1S_NEXT; ++f) v[f] += __shfl_xor(v[f], o);
     }
     __shared__ unsigned long long s_st[LOG_K1_THREADS / 64][K1_SW];
     const int lane = tid & 63, wid = tid >> 6;
@@ -454,12 +477,12 @@ __global__ __launch_bounds__(LOG_K1_THREADS) void log_part_kernel(
         unsigned long long r = s_st[0][tid];
         for (int w = 1; w < LOG_K1_THREADS / 64; ++w) {
             const unsigned long long x = s_st[w][tid];
-            if (tid == K1S_MIN) r = (long long)x < (long long)r ? x : r;
+            if (tid == K1S_MIN || tid == K1S_NEXT) r = (long long)x < (long long)r ? x : r;
             else if (tid == K1S_MAX) r = (long long)x > (long long)r ? x : r;
             else r += x;
         }
         unsigned long long *sh = ca.shard + (blockIdx.x % LOG_SHARDS) * LOG_CUR_STRIDE + tid;
-        if (tid == K1S_MIN) {
+        if (tid == K1S_MIN || tid == K1S_NEXT) {
             if ((long long)r != 0x7fffffffffffffffLL) atomicMin((long long *)sh, (long long)r);
         } else if (tid == K1S_MAX) {
             if ((long long)r != (long long)0x8000000000000000LL) atomicMax((long long *)sh, (long long)r);
@@ -486,6 +509,14 @@ __global__ __launch_bounds__(LOG_K1_THREADS) void log_part_kernel(
     }
     __syncthreads();
     if (s_last) {
+        if (ROUTE && rt.mode == 3) {   // route-only re-run: counts out, cursors and arrival counters reset; no plan
+            for (int p = tid; p < rt.nranks; p += LOG_K1_THREADS) {
+                rt.count[2 * p] = atomicExch(&rt.cursor[(size_t)p * LOG_CUR_STRIDE], 0ull);
+                rt.count[2 * p + 1] = atomicExch(&rt.cursor[(size_t)(LOG_RT_MAX + p) * LOG_CUR_STRIDE], 0ull);
+            }
+            if (tid < LOG_SHARDS + 1) atomicExch(&ca.done[tid * LOG_CUR_STRIDE], 0ull);
+            return;
+        }
         LogRoute r = rt;
         if (!ROUTE) r.mode = 0;
         k1_plan_tail(cursor, st, ca, base, r);
@@ -1307,21 +1338,24 @@ void launch_log_part(const int64_t *key, const int64_t *ts, const int64_t *val, 
                      const LogThr &thr, const LogRoute &rt, hipStream_t s) {
     int64_t grid = (n + LOG_TILE - 1) / LOG_TILE;
     grid = grid < 1 ? 1 : (grid > LOG_K1_GRID ? LOG_K1_GRID : grid);
-#define GWO_K1(HV, S, R)                                                                                       \
-    hipLaunchKernelGGL((log_part_kernel<HV, S, R>), dim3((int)grid), dim3(LOG_K1_THREADS), 0, s, key, ts, val, \
+#define GWO_K1(HV, S, R, T32)                                                                                  \
+    hipLaunchKernelGGL((log_part_kernel<HV, S, R, T32>), dim3((int)grid), dim3(LOG_K1_THREADS), 0, s, key, ts, val, \
                        n, stride, g, base, nunits, cursor, cap, tmp, st, side_key, side_ts, side_val, side_count, \
                        side_cap, side_enabled, ca, thr, rt)
-    if (rt.mode != 0 && stride == 1) {   // routing: the first K1 over a batch's own columns
-        if (has_val) GWO_K1(true, 1, true);
-        else GWO_K1(false, 1, true);
+    if (rt.mode != 0 && stride == 1) {   // routing: the first K1 over a batch's own columns (and its route-only re-run)
+        if (has_val) GWO_K1(true, 1, true, false);
+        else GWO_K1(false, 1, true, false);
+    } else if (thr.ts32) {               // received 20-B wire records (SoA columns, int32 timestamps)
+        if (has_val) GWO_K1(true, 1, false, true);
+        else GWO_K1(false, 1, false, true);
     } else if (has_val) {
-        if (stride == 1) GWO_K1(true, 1, false);
-        else if (stride == 3) GWO_K1(true, 3, false);
-        else GWO_K1(true, 0, false);
+        if (stride == 1) GWO_K1(true, 1, false, false);
+        else if (stride == 3) GWO_K1(true, 3, false, false);
+        else GWO_K1(true, 0, false, false);
     } else {
-        if (stride == 1) GWO_K1(false, 1, false);
-        else if (stride == 3) GWO_K1(false, 3, false);
-        else GWO_K1(false, 0, false);
+        if (stride == 1) GWO_K1(false, 1, false, false);
+        else if (stride == 3) GWO_K1(false, 3, false, false);
+        else GWO_K1(false, 0, false, false);
     }
 #undef GWO_K1
 }

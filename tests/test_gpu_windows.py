@@ -557,19 +557,28 @@ def test_comm_single_rank_matches_oracle(F, layout):
     op.close()
 
 
-@pytest.mark.parametrize("vranks,maxp,hot", [(2, 128, False), (3, 32768, False), (8, 32768, False), (8, 128, True)])
+@pytest.mark.parametrize("vranks,maxp,hot", [(2, 128, False), (3, 32768, False), (8, 32768, False), (8, 128, True),
+                                              (8, 32768, "wide")])
 def test_comm_virtual_ranks_log_route_matches_oracle(F, monkeypatch, vranks, maxp, hot):
     """The log layout's routed K1 (keyBy routing fused into the partition kernel): GWO_COMM_VIRTUAL=P makes a
     1-rank communicator route as GPU 0 of P -- the other GPUs' records leave through RCCL (to this rank itself)
     and come back as received records, so every record takes a rank's real multi-GPU data path once.  hot: one
-    key carries half the records, overflowing its destination's send region (exact re-route)."""
+    key carries half the records, overflowing its destination's send region (exact re-route).  wide: timestamps
+    near 2^40 ms, so before the first watermark (timestamp base 0) every record exceeds the 20-B wire format's
+    int32 range and travels as a 24-B wide record (its regions overflow: route-only re-run), and 1 % of the
+    records sit 2^33 ms before the stream (wide records next to narrow ones, late drops)."""
     import ctypes as C
     from flink_amd import _native as N
     lib = N.lib()
     k, t, v, b = _c1(n=300_000, nkeys=20_000, every=20_000)
-    if hot:
+    if hot is True:
         k = k.copy()
         k[::2] = 12345
+    if hot == "wide":   # watermarks from the in-range stream; then the far-past outliers (wide and late)
+        t = t + (1 << 40)
+        b = G.punctuated_watermarks(t, 20_000, 1000)
+        t = t.copy()
+        t[20_000::100] -= 1 << 33   # (after the first watermark: late)
     agg = F.MultiAggregate(F.SumAggregate(), F.MinAggregate(), F.MaxAggregate())
     op = F.GpuWindowOperator(F.TumblingEventTimeWindows.of(5000), agg, state_layout="log", max_parallelism=maxp)
     uid = (C.c_uint8 * N.COMM_ID_BYTES)()
@@ -579,6 +588,22 @@ def test_comm_virtual_ranks_log_route_matches_oracle(F, monkeypatch, vranks, max
     monkeypatch.delenv("GWO_COMM_VIRTUAL")
     _run_batches(op, k, t, v, b)
     (wk, ws, we, res), late = V.tumbling_lateness0(k, t, v, _final(b), 5000, 0, [1, 2, 3])
+    got = sorted((a, s, e, *r) for a, s, e, r in op.output)
+    assert got == _want(wk, ws, we, res)
+    assert op.num_late_records_dropped == late
+    op.close()
+
+
+def test_log_layout_far_future_records(F):
+    """1 % of the records 2^33 ms (~100 days) after the stream: windows far beyond the batch's range fire at the
+    final watermark; the log layout must not walk the empty windows in between."""
+    k, t, v, b = _c1(n=200_000, nkeys=20_000, every=20_000)
+    t = t.copy()
+    t[50::100] += 1 << 33
+    agg = F.MultiAggregate(F.SumAggregate(), F.MaxAggregate())
+    op = F.GpuWindowOperator(F.TumblingEventTimeWindows.of(5000), agg, state_layout="log")
+    _run_batches(op, k, t, v, b)
+    (wk, ws, we, res), late = V.tumbling_lateness0(k, t, v, _final(b), 5000, 0, [1, 3])
     got = sorted((a, s, e, *r) for a, s, e, r in op.output)
     assert got == _want(wk, ws, we, res)
     assert op.num_late_records_dropped == late
