@@ -338,7 +338,8 @@ struct Handle {
 
     void prof_begin(int k, hipStream_t s = nullptr);
     void prof_end(int k, int64_t items, hipStream_t s = nullptr);
-    gwo_status finish_fire();                  // log layout: wait for a pending fire and publish its rows
+    gwo_status finish_fire();                  // wait for a pending fire (log layout, sessions) and publish its rows
+    gwo_status session_finish_fire();
     gwo_status poll_fire();                    // non-blocking: finish_fire if the fire has completed
     gwo_status prof_collect();
 };

@@ -926,6 +926,7 @@ gwo_status Handle::fire_log(int64_t new_wm) {
 
 gwo_status Handle::finish_fire() {
     if (!fire_pending) return GWO_OK;
+    if (sess) return session_finish_fire();
     LogState &L = *logst;
     fire_pending = false;
     GWO_TRY(spin_event(ev_fire, "fire"));

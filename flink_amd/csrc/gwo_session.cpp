@@ -29,6 +29,8 @@ struct SessionState {
     uint64_t live = 0;              // in-flight sessions
     SessErr *d_err = nullptr;
     SessErr *h_err = nullptr;       // pinned
+    SessErr *d_err_fire = nullptr;  // the watermark sweep's own block: its readback completes lazily (finish_fire)
+    SessErr *h_err_fire = nullptr;  // pinned
     DevBuf rec_slot, k1, v1, k2, v2, hist;
     // spill pool of keys with more in-flight sessions than an entry holds (gwo_internal.h SessGeom)
     int64_t *pool = nullptr;
@@ -64,6 +66,9 @@ gwo_status Handle::session_init() {
     S.stride = (2 + S.smax * (3 + plan.nwords) + 1) & ~1;
     GWO_TRY(dalloc((void **)&S.d_err, sizeof(SessErr)));
     GWO_TRY(hipcheck(hipHostMalloc((void **)&S.h_err, sizeof(SessErr) + 8, hipHostMallocDefault), "pinned"));
+    GWO_TRY(dalloc((void **)&S.d_err_fire, sizeof(SessErr)));
+    GWO_TRY(hipcheck(hipHostMalloc((void **)&S.h_err_fire, sizeof(SessErr), hipHostMallocDefault), "pinned"));
+    GWO_TRY(hipcheck(hipEventCreateWithFlags(&ev_fire, hipEventDisableTiming), "event"));
     GWO_TRY(dalloc((void **)&S.d_pool_top, 8));
     GWO_TRY(hipcheck(hipMemsetAsync(S.d_pool_top, 0, 8, stream), "pool top"));
     uint64_t cap = kMinCap;
@@ -78,6 +83,8 @@ void Handle::session_free() {
     if (S.T.base) (void)hipFree(S.T.base);
     if (S.d_err) (void)hipFree(S.d_err);
     if (S.h_err) (void)hipHostFree(S.h_err);
+    if (S.d_err_fire) (void)hipFree(S.d_err_fire);
+    if (S.h_err_fire) (void)hipHostFree(S.h_err_fire);
     if (S.pool) (void)hipFree(S.pool);
     if (S.d_pool_top) (void)hipFree(S.d_pool_top);
     S.rec_slot.release();
@@ -187,6 +194,7 @@ gwo_status Handle::read_occupancy_one(Table &t) {
 
 gwo_status Handle::insert_session(const int64_t *k, const int64_t *t, const int64_t *v, int64_t n) {
     SessionState &S = *sess;
+    GWO_TRY(finish_fire());   // the last watermark's sweep (usually complete by now: no wait)
     if (n > 0xffffffffll) return fail(GWO_ERR_INVALID_ARGUMENT, "session batches are limited to 2^32 records");
     GWO_TRY(sess_ensure((uint64_t)n));
     GWO_TRY(sess_ensure_pool((uint64_t)n));
@@ -245,24 +253,44 @@ gwo_status Handle::insert_session(const int64_t *k, const int64_t *t, const int6
     return GWO_OK;
 }
 
+// The watermark sweep is queued with its statistics copy behind it and not waited for: its rows and live-session
+// change are applied by finish_fire, at the next batch or output access (by then it has usually completed).
 gwo_status Handle::fire_session(int64_t new_wm) {
     SessionState &S = *sess;
+    GWO_TRY(finish_fire());
     if (S.live == 0) return GWO_OK;
     GWO_TRY(ensure_output(S.live));
-    GWO_TRY(hipcheck(hipMemsetAsync(S.d_err, 0, sizeof(SessErr), stream), "err"));
+    GWO_TRY(hipcheck(hipMemsetAsync(S.d_err_fire, 0, sizeof(SessErr), stream), "err"));
     SessGeom g = sess_geom(*this, S.smax);
     g.wm = new_wm;
     prof_begin(GWO_KERNEL_FIRE);
-    launch_sess_fire(desc(S.T), S.T.cap, S.stride, plan, rplan, g, out_cols(), S.d_err, stream);
+    launch_sess_fire(desc(S.T), S.T.cap, S.stride, plan, rplan, g, out_cols(), S.d_err_fire, stream);
     GWO_TRY(launch_ok("sess fire"));
     prof_end(GWO_KERNEL_FIRE, (int64_t)S.T.cap);
-    GWO_TRY(sess_read_err());
-    S.live += S.h_err->live_delta;
-    out_rows += S.h_err->emitted;
+    GWO_TRY(hipcheck(hipMemcpyAsync(S.h_err_fire, S.d_err_fire, sizeof(SessErr), hipMemcpyDeviceToHost, stream),
+                     "fire err"));
+    GWO_TRY(hipcheck(hipEventRecord(ev_fire, stream), "event"));
+    fire_pending = true;
+    return GWO_OK;
+}
+
+gwo_status Handle::session_finish_fire() {
+    SessionState &S = *sess;
+    fire_pending = false;
+    GWO_TRY(spin_event(ev_fire, "session fire"));
+    S.live += S.h_err_fire->live_delta;
+    if (discard_after_fire) {   // gwo_discard_output was called while the sweep ran: its rows go too
+        discard_after_fire = false;
+        rows_gone += S.h_err_fire->emitted;
+        out_count_dirty = true;
+    } else {
+        out_rows += S.h_err_fire->emitted;
+    }
     return GWO_OK;
 }
 
 gwo_status Handle::session_state_size(int64_t *entries) {
+    GWO_TRY(finish_fire());
     *entries = (int64_t)sess->live;
     return GWO_OK;
 }
