@@ -425,7 +425,9 @@ __global__ __launch_bounds__(256) void insert_preagg_kernel(const int64_t *__res
 #define CB_PER 4
 #endif
 #define CB_TILE (CB_THREADS * CB_PER)
+#ifndef CB_MERGE_RUN
 #define CB_MERGE_RUN 8
+#endif
 #define CB_SHARDS 16      // statistics shards (gather)
 #define CB_HOT 8          // lanes of one (unit, key) in a wave that take the wave pre-reduction
 

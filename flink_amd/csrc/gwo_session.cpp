@@ -64,12 +64,13 @@ gwo_status Handle::session_init() {
     SessionState &S = *sess;
     if (const char *e = getenv("GWO_SESSION_SLOTS")) S.smax = std::max(1, std::min(16, atoi(e)));
     S.stride = (2 + S.smax * (3 + plan.nwords) + 1) & ~1;
-    GWO_TRY(dalloc((void **)&S.d_err, sizeof(SessErr)));
+    // the pool's bump counter sits right behind the batch's SessErr block: one copy reads both back
+    GWO_TRY(dalloc((void **)&S.d_err, sizeof(SessErr) + 8));
     GWO_TRY(hipcheck(hipHostMalloc((void **)&S.h_err, sizeof(SessErr) + 8, hipHostMallocDefault), "pinned"));
     GWO_TRY(dalloc((void **)&S.d_err_fire, sizeof(SessErr)));
     GWO_TRY(hipcheck(hipHostMalloc((void **)&S.h_err_fire, sizeof(SessErr), hipHostMallocDefault), "pinned"));
     GWO_TRY(hipcheck(hipEventCreateWithFlags(&ev_fire, hipEventDisableTiming), "event"));
-    GWO_TRY(dalloc((void **)&S.d_pool_top, 8));
+    S.d_pool_top = (unsigned long long *)((char *)S.d_err + sizeof(SessErr));
     GWO_TRY(hipcheck(hipMemsetAsync(S.d_pool_top, 0, 8, stream), "pool top"));
     uint64_t cap = kMinCap;
     if (cfg.expected_keys > 0)
@@ -86,7 +87,6 @@ void Handle::session_free() {
     if (S.d_err_fire) (void)hipFree(S.d_err_fire);
     if (S.h_err_fire) (void)hipHostFree(S.h_err_fire);
     if (S.pool) (void)hipFree(S.pool);
-    if (S.d_pool_top) (void)hipFree(S.d_pool_top);
     S.rec_slot.release();
     S.k1.release();
     S.v1.release();
@@ -117,9 +117,8 @@ static SessGeom sess_geom(const Handle &h, int smax) {
 
 gwo_status Handle::sess_read_err() {
     SessionState &S = *sess;
-    GWO_TRY(hipcheck(hipMemcpyAsync(S.h_err, S.d_err, sizeof(SessErr), hipMemcpyDeviceToHost, stream), "err"));
-    GWO_TRY(hipcheck(hipMemcpyAsync((char *)S.h_err + sizeof(SessErr), S.d_pool_top, 8, hipMemcpyDeviceToHost, stream),
-                     "pool top"));
+    // the statistics and, right behind them, the pool's bump counter
+    GWO_TRY(hipcheck(hipMemcpyAsync(S.h_err, S.d_err, sizeof(SessErr) + 8, hipMemcpyDeviceToHost, stream), "err"));
     GWO_TRY(hipcheck(hipStreamSynchronize(stream), "err sync"));
     S.pool_top = *(const unsigned long long *)((const char *)S.h_err + sizeof(SessErr));
     return GWO_OK;
