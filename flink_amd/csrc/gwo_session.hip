@@ -113,6 +113,7 @@ __global__ __launch_bounds__(64) void sess_process_kernel(const int64_t *__restr
                                                           OutCols o, SessErr *err, int64_t *side_key, int64_t *side_ts,
                                                           int64_t *side_val, unsigned long long *side_count,
                                                           long long side_cap) {
+    extern __shared__ int64_t s_L[];   // [64][smax * sw]: each lane's copy of its key's inline sessions
     const int64_t step = (int64_t)gridDim.x * blockDim.x;
     const int sw = 3 + p.nwords;
     for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n; q += step) {
@@ -120,7 +121,8 @@ __global__ __launch_bounds__(64) void sess_process_kernel(const int64_t *__restr
         if (q > 0 && sorted_slot[q - 1] == slot) continue;  // not the head of this key's run
         int64_t *e = entry_ptr(t, slot, stride, cap);
         // the key's session list: the inline sessions copied into L (written back at the end), or its pool array
-        int64_t L[SESS_MAXS * SESS_MAXW];
+        // in this lane's LDS slice (a private array indexed at run time would live in scratch memory)
+        int64_t *L = s_L + (size_t)threadIdx.x * g.smax * sw;
         int64_t *S = L;
         int ns, scap = g.smax;
         int64_t off = 0;
@@ -412,7 +414,8 @@ void launch_sess_process(const int64_t *key, const int64_t *ts, const int64_t *v
                          const uint32_t *sidx, const TableDesc &t, uint64_t cap, int stride, const AccPlan &p,
                          const ResultPlan &rp, const SessGeom &g, OutCols o, SessErr *err, int64_t *sk, int64_t *st,
                          int64_t *sv, unsigned long long *sc, long long scap, hipStream_t s) {
-    hipLaunchKernelGGL(sess_process_kernel, dim3(sgrid(n, 64, 65536)), dim3(64), 0, s, key, ts, val, n, sslot, sidx,
+    const size_t lds = (size_t)64 * g.smax * (3 + p.nwords) * 8;
+    hipLaunchKernelGGL(sess_process_kernel, dim3(sgrid(n, 64, 65536)), dim3(64), lds, s, key, ts, val, n, sslot, sidx,
                        t, cap, stride, p, rp, g, o, err, sk, st, sv, sc, scap);
 }
 
