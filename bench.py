@@ -14,8 +14,10 @@ distinct-keys hint, so any warmup >= 0 measures the steady state; 20 timed steps
 its own slice of a 100M*N-key stream and gwo_submit shuffles records to their key-group owner with an
 RCCL all-to-all (weak scaling).
 
-The roofline kernel is the one with the most time in the timed region (HIP events on the handle's
-stream around K1 and the fire only -- each timed launch adds two stream markers).  host_fed is a
+The roofline kernel is the one with the most time in the timed region.  K1 (log_part_kernel) times itself on
+the device wall clock -- workgroup 0's start and its last workgroup's end, read back with its plan -- so the
+timed region carries no stream markers between K1 and pass 2 (each costs the stream ~5 us: 1.3 % of a step);
+the fire is bracketed by HIP events on the handle's stream (one window per 10 steps).  host_fed is a
 separate, smaller run: pinned host columns in, fired rows drained to pinned host memory (PCIe-bound,
 never the headline value).
 

@@ -53,6 +53,7 @@ struct LogJob {
     LogRoute rt{};               // multi-GPU: the first K1 routes other GPUs' records (mode 1), re-runs skip them (2)
     bool ts32 = false;           // t holds int32 timestamps - tbase (records received in the 20-B wire format)
     int64_t tbase = 0;
+    bool timed = false;          // the last K1 launch carries its own device timestamps (profiling)
 };
 
 struct LogState {
@@ -103,6 +104,8 @@ struct LogState {
     int cap_log2 = 0;
     int max_groups = 0;                          // persistent fire workgroups (2 per CU)
     unsigned long long seq = 0;                  // last readback sequence number issued
+    unsigned long long *d_t0 = nullptr;          // K1's start timestamp (profiling)
+    int clock_khz = 0;                           // device wall-clock rate
 
     unsigned long long *rb(int slot) const { return h_rb + (size_t)slot * LOG_RB_WORDS; }
     unsigned long long *rb_dev(int slot) const { return d_rbh + (size_t)slot * LOG_RB_WORDS; }
@@ -135,6 +138,8 @@ gwo_status Handle::log_init() {
     GWO_TRY(dalloc((void **)&L.d_overflow, 16));
     GWO_TRY(hipcheck(hipMemsetAsync(L.d_overflow, 0, 16, stream), "overflow"));
     GWO_TRY(dalloc((void **)&L.d_go, LOG_SLOTS * sizeof(unsigned)));
+    GWO_TRY(dalloc((void **)&L.d_t0, 8));
+    if (hipDeviceGetAttribute(&L.clock_khz, hipDeviceAttributeWallClockRate, cfg.device) != hipSuccess) L.clock_khz = 0;
     GWO_TRY(dalloc((void **)&L.d_done, LOG_DONE_WORDS * 8));
     GWO_TRY(hipcheck(hipMemsetAsync(L.d_done, 0, LOG_DONE_WORDS * 8, stream), "done"));
     {
@@ -227,6 +232,7 @@ void Handle::log_free() {
     if (L.d_overflow) (void)hipFree(L.d_overflow);
     if (L.d_go) (void)hipFree(L.d_go);
     if (L.d_done) (void)hipFree(L.d_done);
+    if (L.d_t0) (void)hipFree(L.d_t0);
     if (L.d_k1sh) (void)hipFree(L.d_k1sh);
     if (L.h_rb) (void)hipHostFree(L.h_rb);
     if (L.h_buckets) (void)hipHostFree(L.h_buckets);
@@ -555,12 +561,14 @@ gwo_status Handle::log_k1(LogJob &J, bool first_pass) {
     LogThr thr = log_thresholds(J);
     thr.ts32 = J.ts32 ? 1 : 0;
     thr.tbase = J.tbase;
-    prof_begin(GWO_KERNEL_INSERT);
+    // profiling: K1 times itself on the device wall clock (workgroup 0's start, the tail's end; read back with the
+    // plan) -- no stream markers around it
+    J.timed = profiling && ((prof_mask >> GWO_KERNEL_INSERT) & 1u) && L.clock_khz > 0;
+    ca.t0 = J.timed ? L.d_t0 : nullptr;
     launch_log_part(J.k, J.t, J.v, J.n, J.stride, J.g, J.base, J.nunits, needs_value, L.d_cursor, J.cap,
                     (int64_t *)tmp.ptr, d_stats, (int64_t *)side_key.ptr, (int64_t *)side_ts.ptr,
                     (int64_t *)side_val.ptr, d_side_count, side ? side_cap : 0, side, ca, thr, J.rt, stream);
     GWO_TRY(launch_ok("log partition"));
-    prof_end(GWO_KERNEL_INSERT, J.n);
     if (J.rt.mode == 1) {   // routed once: the exchange may start behind this K1; re-runs skip other GPUs' records
         GWO_TRY(comm_mark_routed());
         J.rt.mode = 2;
@@ -648,6 +656,14 @@ gwo_status Handle::log_resolve_batch(LogJob &J, bool &refire) {
     long long lo = 0, hi = -1;
     while (true) {
         GWO_TRY(log_wait_readback(J.slot, J.seq));
+        if (J.timed) {   // the launch's own device timestamps
+            const unsigned long long *rb = L.rb(J.slot);
+            KStat &ks = kstats[GWO_KERNEL_INSERT];
+            ks.launches++;
+            ks.ms += (double)(rb[LOG_RB_T1] - rb[LOG_RB_T0]) / (double)L.clock_khz;
+            ks.items += J.n;
+            J.timed = false;
+        }
         // the side-output row count follows the collect kernel by a copy: wait for that too
         if (first_pass && side_enabled()) GWO_TRY(spin_event(L.ev_rb[J.slot], "side count"));
         const unsigned long long *rbp = L.rb(J.slot);

@@ -91,7 +91,9 @@ static constexpr int LOG_RB_GO = LOG_RB_CHUNKS + 1;
 static constexpr int LOG_RB_MAXREG = LOG_RB_GO + 1;      // largest region count (> cap: K1 dropped records)
 static constexpr int LOG_RB_NEXT = LOG_RB_MAXREG + 1;    // the first window after the launch's range holding accepted
                                                          // records (Long.MAX_VALUE: none) -- the next K1 range starts there
-static constexpr int LOG_RB_SEQ = LOG_RB_NEXT + 1;       // written last: the launch's sequence number
+static constexpr int LOG_RB_T0 = LOG_RB_NEXT + 1;        // device wall clock when workgroup 0 started (profiling)
+static constexpr int LOG_RB_T1 = LOG_RB_T0 + 1;          // device wall clock when the tail finished its work
+static constexpr int LOG_RB_SEQ = LOG_RB_T1 + 1;         // written last: the launch's sequence number
 static constexpr int LOG_RB_WORDS = LOG_RB_SEQ + 1;
 
 // What K1's last workgroup needs to plan pass 2 (the former collect step, fused into K1's tail).
@@ -109,6 +111,7 @@ struct CollectArgs {
     unsigned long long *done;    // K1 workgroups finished: shard counters [LOG_SHARDS * LOG_CUR_STRIDE], then the
                                  // count of finished shards at done[LOG_SHARDS * LOG_CUR_STRIDE] (the last plans)
     unsigned long long *shard;   // [LOG_SHARDS * LOG_CUR_STRIDE] K1 statistics shards (K1_SW words each, one line)
+    unsigned long long *t0;      // device wall clock at workgroup 0's start (K1 timing without stream markers)
 };
 
 // K1's statistics: every workgroup reduces its counters in LDS and folds them into shard blockIdx % LOG_SHARDS

@@ -219,6 +219,10 @@ __device__ __forceinline__ void k1_plan_tail(unsigned long long *cursor, BatchSt
         a.rb[LOG_RB_GO] = go ? 1ull : 0ull;
         a.rb[LOG_RB_MAXREG] = s_maxreg;
     }
+    if (t == 0 && a.t0) {
+        a.rb[LOG_RB_T0] = atomicAdd(a.t0, 0ull);
+        a.rb[LOG_RB_T1] = (unsigned long long)wall_clock64();
+    }
     // the host spins on the sequence word: every other readback word must be visible first
     __threadfence_system();
     __syncthreads();
@@ -243,6 +247,9 @@ __global__ __launch_bounds__(LOG_K1_THREADS) void log_part_kernel(
     int64_t *__restrict__ tmp, BatchStats *st, int64_t *side_key, int64_t *side_ts, int64_t *side_val,
     unsigned long long *side_count, long long side_cap, int side_enabled, CollectArgs ca, LogThr th, LogRoute rt) {
     constexpr int W = HASV ? 2 : 1;
+    // K1 times itself: workgroup 0's start and the tail's end on the device wall clock (read back with the plan),
+    // so profiling puts no event markers between K1 and pass 2 (each costs the stream ~5 us)
+    if (blockIdx.x == 0 && threadIdx.x == 0 && ca.t0) atomicExch(ca.t0, (unsigned long long)wall_clock64());
     // the new segments' partition counters (pass 2's cursors) start at zero: pass 2 follows in stream order
     // (a route-only re-run follows a pass 2 that already used them)
     for (int w = 0; w < ((ROUTE && rt.mode == 3) ? 0 : ca.nunits); ++w) {
