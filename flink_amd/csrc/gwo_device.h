@@ -255,4 +255,24 @@ __device__ __forceinline__ void wave_atomic_add(unsigned long long *dst, unsigne
     if ((threadIdx.x & 63) == 0 && v) atomicAdd(dst, v);
 }
 
+// Read-and-reset of N statistics shards (word p[q * stride], q < N) folded with kind 0 sum, 1 signed min,
+// 2 signed max.  Every exchange is issued before the first result is used: a device-scope atomic is a
+// round trip of ~1 us, and a fold between them (branches on the kind) serialised N of them per call.
+template <int N>
+__device__ __forceinline__ unsigned long long xchg_fold(unsigned long long *p, size_t stride, unsigned long long init,
+                                                        int kind) {
+    unsigned long long x[N];
+#pragma unroll
+    for (int q = 0; q < N; ++q) x[q] = atomicExch(p + q * stride, init);
+    long long r = (long long)init;
+#pragma unroll
+    for (int q = 0; q < N; ++q) {
+        const long long v = (long long)x[q];
+        const long long s = (long long)((unsigned long long)r + (unsigned long long)v);
+        const long long lo = v < r ? v : r, hi = v > r ? v : r;
+        r = kind == 0 ? s : (kind == 1 ? lo : hi);
+    }
+    return (unsigned long long)r;
+}
+
 }  // namespace gwo

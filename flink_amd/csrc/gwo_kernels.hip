@@ -186,13 +186,7 @@ __global__ __launch_bounds__(256) void scan_kernel(const int64_t *__restrict__ k
     if (!s_last) return;
     if (t < SCAN_CNT + GWO_HIST_BINS) {
         const unsigned long long init = t == 0 ? 0x7fffffffffffffffull : (t == 1 ? 0x8000000000000000ull : 0ull);
-        unsigned long long r = init;
-        for (int q = 0; q < SCAN_SHARDS; ++q) {
-            const unsigned long long x = atomicExch(&sh[(size_t)q * SCAN_SW + t], init);
-            if (t == 0) r = (long long)x < (long long)r ? x : r;
-            else if (t == 1) r = (long long)x > (long long)r ? x : r;
-            else r += x;
-        }
+        const unsigned long long r = xchg_fold<SCAN_SHARDS>(&sh[t], SCAN_SW, init, t == 0 ? 1 : (t == 1 ? 2 : 0));
         switch (t) {
             case 0: st->min_idx = (long long)r; break;
             case 1: st->max_idx = (long long)r; break;
@@ -670,14 +664,8 @@ __global__ __launch_bounds__(CB_THREADS) void gather_kernel(const int64_t *__res
     if (tid < CS_WORDS) {
         const unsigned long long init =
             tid == CS_MIN ? 0x7fffffffffffffffull : (tid == CS_MAX ? 0x8000000000000000ull : 0ull);
-        unsigned long long r = init;
-        for (int q = 0; q < CB_SHARDS; ++q) {   // read and reset for the next batch
-            const unsigned long long x = atomicExch(&a.blk[(size_t)q * CS_WORDS + tid], init);
-            if (tid == CS_MIN) r = (long long)x < (long long)r ? x : r;
-            else if (tid == CS_MAX) r = (long long)x > (long long)r ? x : r;
-            else r += x;
-        }
-        s_tot[tid] = r;
+        // read and reset for the next batch
+        s_tot[tid] = xchg_fold<CB_SHARDS>(&a.blk[tid], CS_WORDS, init, tid == CS_MIN ? 1 : (tid == CS_MAX ? 2 : 0));
     }
     // the readback block: BatchStats image, side-output count, occupancy of the hint tables, sequence word last
     BatchStats *rs = (BatchStats *)a.rb;

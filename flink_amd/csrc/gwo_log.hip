@@ -120,6 +120,15 @@ __device__ __forceinline__ void k1_plan_tail(unsigned long long *cursor, BatchSt
         s_bad = 0;
         s_maxreg = 0;
     }
+    // the launch's bucket counts (cursors reset for the next K1): every exchange in flight before any is used
+    unsigned long long cq[LOG_NU][LOG_XG];
+#pragma unroll
+    for (int q = 0; q < LOG_NU; ++q)
+#pragma unroll
+        for (int x = 0; x < LOG_XG; ++x)
+            cq[q][x] = t < LOG_ND && q < a.nunits
+                           ? atomicExch(&cursor[((size_t)(q * LOG_ND + t) * LOG_XG + x) * LOG_CUR_STRIDE], 0ull)
+                           : 0ull;
     if (rt.mode == 1)   // routed records per destination; the cursors start the next routed K1 at zero
         for (int p = t; p < rt.nranks; p += LOG_K1_THREADS) {
             rt.count[2 * p] = atomicExch(&rt.cursor[(size_t)p * LOG_CUR_STRIDE], 0ull);
@@ -133,14 +142,8 @@ __device__ __forceinline__ void k1_plan_tail(unsigned long long *cursor, BatchSt
         const int f = t - K1_T0;
         const unsigned long long init = (f == K1S_MIN || f == K1S_NEXT) ? 0x7fffffffffffffffull
                                                                         : (f == K1S_MAX ? 0x8000000000000000ull : 0ull);
-        unsigned long long r = init;
-        for (int q = 0; q < LOG_SHARDS; ++q) {
-            const unsigned long long x = atomicExch(&a.shard[q * LOG_CUR_STRIDE + f], init);
-            if (f == K1S_MIN || f == K1S_NEXT) r = (long long)x < (long long)r ? x : r;
-            else if (f == K1S_MAX) r = (long long)x > (long long)r ? x : r;
-            else r += x;
-        }
-        s_k1[f] = r;
+        const int kind = (f == K1S_MIN || f == K1S_NEXT) ? 1 : (f == K1S_MAX ? 2 : 0);
+        s_k1[f] = xchg_fold<LOG_SHARDS>(&a.shard[f], LOG_CUR_STRIDE, init, kind);
     } else if (t >= K1_T1 && t < K1_T1 + LOG_SHARDS + 1) {   // arrival counters start the next K1 at zero
         atomicExch(&a.done[(t - K1_T1) * LOG_CUR_STRIDE], 0ull);
     }
@@ -163,13 +166,14 @@ __device__ __forceinline__ void k1_plan_tail(unsigned long long *cursor, BatchSt
     unsigned long long chunk_run = 0;
     unsigned bad = 0;
     unsigned long long maxreg = 0;
-    for (int q = 0; q < a.nunits; ++q) {   // window q of the launch: bucket b = q * LOG_ND + t (digit t)
+#pragma unroll
+    for (int q = 0; q < LOG_NU; ++q) {   // window q of the launch: bucket b = q * LOG_ND + t (digit t)
+        if (q >= a.nunits) break;
         const bool dig = t < LOG_ND;
         const int b = q * LOG_ND + t;
         unsigned long long c[LOG_XG], n_b = 0;
 #pragma unroll
-        for (int x = 0; x < LOG_XG; ++x)
-            c[x] = dig ? atomicExch(&cursor[((size_t)b * LOG_XG + x) * LOG_CUR_STRIDE], 0ull) : 0ull;
+        for (int x = 0; x < LOG_XG; ++x) c[x] = cq[q][x];
         uint32_t xoff[LOG_XG];
 #pragma unroll
         for (int x = 0; x < LOG_XG; ++x) {
