@@ -255,6 +255,21 @@ __device__ __forceinline__ void wave_atomic_add(unsigned long long *dst, unsigne
     if ((threadIdx.x & 63) == 0 && v) atomicAdd(dst, v);
 }
 
+// Host-mapped readback blocks (coherent host memory the host spins on).  Every word goes out as a system-scope
+// store, written through the L2 (sc0 sc1), so that the waves' own store counters order the words before the
+// sequence word: a system-scope release fence instead writes back the XCD's whole L2 (measured 4.6 us in the
+// combine gather's tail, ~3 us at K1's end).
+__device__ __forceinline__ void rb_put(unsigned long long *p, unsigned long long v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+// The workgroup's readback words are complete (each wave waits for its stores) before thread 0 writes the
+// sequence word.  Called by every thread of the workgroup.
+__device__ __forceinline__ void rb_publish(unsigned long long *seq_word, unsigned long long seq) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) rb_put(seq_word, seq);
+}
+
 // Read-and-reset of N statistics shards (word p[q * stride], q < N) folded with kind 0 sum, 1 signed min,
 // 2 signed max.  Every exchange is issued before the first result is used: a device-scope atomic is a
 // round trip of ~1 us, and a fold between them (branches on the kind) serialised N of them per call.

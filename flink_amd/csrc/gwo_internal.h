@@ -114,7 +114,8 @@ struct WindowGeom {
 // the merge, per-workgroup statistics slots.
 struct CombineArgs {
     int64_t *dump_key;                 // [G][2 * S]
-    int64_t *dump_acc;                 // [G][2 * S][nwords]
+    int64_t *dump_acc;                 // [G][2 * S][nwords] (occupied slots only)
+    uint32_t *dump_used;               // [G]: bit u set when workgroup g dumped the table of unit hint + u
     uint32_t *ovf;                     // record indices left to the merge
     unsigned long long *ovf_count;     // reset by the gather's last workgroup
     unsigned long long ovf_cap;

@@ -609,15 +609,21 @@ __global__ __launch_bounds__(CB_THREADS) void gather_kernel(const int64_t *__res
         mx = y > mx ? y : mx;
     }
     __syncthreads();   // every LDS table update and histogram run is in
+    // the dump: only the tables of units that took records of this workgroup (a batch usually spans one
+    // window: half the dump), accumulators only of occupied slots; dump_used tells the merge which tables
     unsigned d0 = 0, d1 = 0;
+    const unsigned used = (s_hist[0] ? 1u : 0u) | (s_hist[1] ? 2u : 0u);
+    if (tid == 0) a.dump_used[blockIdx.x] = used;
     int64_t *dk = a.dump_key + (size_t)blockIdx.x * CB_NU * S;
     int64_t *da = a.dump_acc + (size_t)blockIdx.x * CB_NU * S * NW;
     for (int i = tid; i < CB_NU * S; i += CB_THREADS) {
+        if (!((used >> (i >= S ? 1 : 0)) & 1u)) continue;
         const int64_t k = s_key[i];
-        dk[i] = k;
-        if (k != GWO_EMPTY_KEY) (i < S ? d0 : d1)++;
+        __builtin_nontemporal_store(k, &dk[i]);   // streamed out: no dirty dump lines left for the kernel's end
+        if (k == GWO_EMPTY_KEY) continue;
+        (i < S ? d0 : d1)++;
+        for (int w = 0; w < NW; ++w) __builtin_nontemporal_store(s_acc[i * NW + w], &da[(size_t)i * NW + w]);
     }
-    for (int i = tid; i < CB_NU * S * NW; i += CB_THREADS) da[i] = s_acc[i];
     unsigned long long e0 = d0, e1 = d1;
     for (int o = 32; o > 0; o >>= 1) {
         e0 += __shfl_xor(e0, o);
@@ -668,43 +674,34 @@ __global__ __launch_bounds__(CB_THREADS) void gather_kernel(const int64_t *__res
         s_tot[tid] = xchg_fold<CB_SHARDS>(&a.blk[tid], CS_WORDS, init, tid == CS_MIN ? 1 : (tid == CS_MAX ? 2 : 0));
     }
     // the readback block: BatchStats image, side-output count, occupancy of the hint tables, sequence word last
-    BatchStats *rs = (BatchStats *)a.rb;
     __shared__ unsigned long long s_spec[4];   // listed records, side-output count, occupancy of the hint tables
     if (tid < CS_WORDS && (tid < CS_HIST ? tid <= CS_D1 : true)) {
+#define RBW(f) (int)(offsetof(BatchStats, f) / 8)
+        constexpr int word[CS_HIST] = {RBW(accepted), RBW(late),    RBW(refire),      RBW(bad_ts),
+                                       RBW(bad_range), RBW(bad_kg), RBW(hist_out),    RBW(min_idx),
+                                       RBW(max_idx),  RBW(distinct), RBW(distinct) + 1, 0};
         const unsigned long long r = s_tot[tid];
-        switch (tid) {
-            case CS_ACC: rs->accepted = r; break;
-            case CS_LATE: rs->late = r; break;
-            case CS_REFIRE: rs->refire = r; break;
-            case CS_BADTS: rs->bad_ts = r; break;
-            case CS_BADRANGE: rs->bad_range = r; break;
-            case CS_BADKG:
-                rs->bad_kg = r;
-                rs->bad_kg_key = r ? (long long)atomicAdd((unsigned long long *)&st->bad_kg_key, 0ull) : 0;
-                break;
-            case CS_HOUT: rs->hist_out = r; break;
-            case CS_MIN: rs->min_idx = (long long)r; break;
-            case CS_MAX: rs->max_idx = (long long)r; break;
-            case CS_D0: rs->distinct[0] = r; break;
-            case CS_D1: rs->distinct[1] = r; break;
-            default: rs->hist[tid - CS_HIST] = r; break;
-        }
+        rb_put(&a.rb[tid < CS_HIST ? word[tid] : RBW(hist) + tid - CS_HIST], r);
+        if (tid == CS_BADKG)
+            rb_put(&a.rb[RBW(bad_kg_key)], r ? atomicAdd((unsigned long long *)&st->bad_kg_key, 0ull) : 0ull);
     } else if (tid >= CB_THREADS - 4) {
         const int q = tid - (CB_THREADS - 4);   // 0: overflow, 1: side count, 2-3: occupancy
         if (q == 0) {
-            rs->overflow = atomicExch(a.ovf_count, 0ull);   // read and reset for the next batch
+            const unsigned long long ov = atomicExch(a.ovf_count, 0ull);   // read and reset for the next batch
+            rb_put(&a.rb[RBW(overflow)], ov);
+#undef RBW
             *a.done = 0;
-            s_spec[0] = rs->overflow;
+            s_spec[0] = ov;
         } else if (q == 1) {
             const unsigned long long sc = a.side_enabled ? atomicAdd(side_count, 0ull) : 0ull;
-            a.rb[CB_RB_SIDE] = sc;
+            rb_put(&a.rb[CB_RB_SIDE], sc);
             s_spec[1] = sc;
         } else {
             unsigned long long *o = a.occ[q - 2];
             unsigned long long tot = 0;
             if (o)
                 for (int sh = 0; sh < GWO_OCC_SHARDS; ++sh) tot += atomicAdd(o + sh * GWO_OCC_SHARD_STRIDE, 0ull);
-            a.rb[CB_RB_OCC + q - 2] = tot;
+            rb_put(&a.rb[CB_RB_OCC + q - 2], tot);
             s_spec[q] = tot;
         }
     }
@@ -721,14 +718,9 @@ __global__ __launch_bounds__(CB_THREADS) void gather_kernel(const int64_t *__res
             go = a.occ[r] != nullptr && 10 * (s_spec[2 + r] + inc) <= 7 * a.cap[r];   // the host's kMaxLoad 0.7
         }
         if (a.go) *a.go = go ? 1u : 0u;
-        a.rb[CB_RB_GO] = go ? 1ull : 0ull;
+        rb_put(&a.rb[CB_RB_GO], go ? 1ull : 0ull);
     }
-    __threadfence_system();
-    __syncthreads();
-    if (tid == 0) {
-        __threadfence_system();
-        *(volatile unsigned long long *)&a.rb[CB_RB_SEQ] = a.seq;
-    }
+    rb_publish(&a.rb[CB_RB_SEQ], a.seq);
 }
 
 // merge: threads [0, dump_threads) take (slot, run of CB_MERGE_RUN workgroups) of the dumps; the rest take the
@@ -747,10 +739,18 @@ __global__ __launch_bounds__(256) void merge_kernel(const int64_t *__restrict__ 
         const int w0 = (int)(t / slots) * CB_MERGE_RUN;
         const bool live = t < dump_threads && w0 < G;
         const long long d = a.hint + slot / S - dir_base;
+        // keys and table flags load together (a table not dumped holds a stale key: masked by its flag)
         int64_t k[CB_MERGE_RUN];
+        uint32_t used[CB_MERGE_RUN];
+#pragma unroll
+        for (int j = 0; j < CB_MERGE_RUN; ++j) {
+            const bool in = live && w0 + j < G;
+            k[j] = in ? a.dump_key[(size_t)(w0 + j) * slots + slot] : GWO_EMPTY_KEY;
+            used[j] = in ? a.dump_used[w0 + j] : 0u;
+        }
 #pragma unroll
         for (int j = 0; j < CB_MERGE_RUN; ++j)
-            k[j] = live && w0 + j < G ? a.dump_key[(size_t)(w0 + j) * slots + slot] : GWO_EMPTY_KEY;
+            if (!((used[j] >> (slot >= S ? 1 : 0)) & 1u)) k[j] = GWO_EMPTY_KEY;
         int64_t run_k = GWO_EMPTY_KEY;
         int64_t run[GWO_MAX_WORDS];
         auto flush = [&]() {   // entries exist only for units of accepted records: inside the directory
@@ -763,16 +763,27 @@ __global__ __launch_bounds__(256) void merge_kernel(const int64_t *__restrict__ 
             const long long u = a.hint + slot / S;
             if (u >= ring.lo && u <= ring.hi) apply_ring(ring, p, run_k, run);
         };
+        // the first CB_MW accumulator words of every entry load before any is folded (one round trip, not one
+        // per entry); further words, if any, load in the fold
+        constexpr int CB_MW = 2;
+        int64_t av[CB_MERGE_RUN][CB_MW];
+#pragma unroll
+        for (int j = 0; j < CB_MERGE_RUN; ++j)
+#pragma unroll
+            for (int w = 0; w < CB_MW; ++w)
+                av[j][w] = k[j] != GWO_EMPTY_KEY && w < NW ? a.dump_acc[((size_t)(w0 + j) * slots + slot) * NW + w] : 0;
 #pragma unroll
         for (int j = 0; j < CB_MERGE_RUN; ++j) {
             if (k[j] == GWO_EMPTY_KEY) continue;
             const int64_t *src = a.dump_acc + ((size_t)(w0 + j) * slots + slot) * NW;
-            if (k[j] == run_k) {
-                for (int w = 0; w < NW; ++w) run[w] = combine(p.op[w], run[w], src[w]);
-            } else {
+            const bool same = k[j] == run_k;
+            if (!same) {
                 flush();
                 run_k = k[j];
-                for (int w = 0; w < NW; ++w) run[w] = src[w];
+            }
+            for (int w = 0; w < NW; ++w) {
+                const int64_t x = w < CB_MW ? av[j][w < CB_MW ? w : 0] : src[w];
+                run[w] = same ? combine(p.op[w], run[w], x) : x;
             }
         }
         flush();

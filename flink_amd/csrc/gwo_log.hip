@@ -158,10 +158,10 @@ __device__ __forceinline__ void k1_plan_tail(unsigned long long *cursor, BatchSt
         W.bad_ts = s_k1[K1S_BADTS];
         W.bad_kg = s_k1[K1S_BADKG];
         W.hist_out = s_k1[K1S_HOUT];
-        a.rb[LOG_RB_NEXT] = s_k1[K1S_NEXT];
+        rb_put(&a.rb[LOG_RB_NEXT], s_k1[K1S_NEXT]);
     }
     __syncthreads();
-    if (t < SW) a.rb[LOG_RB_STATS + t] = s_sw[t];
+    if (t < SW) rb_put(&a.rb[LOG_RB_STATS + t], s_sw[t]);
     const BatchStats &S = *(const BatchStats *)s_sw;
     unsigned long long chunk_run = 0;
     unsigned bad = 0;
@@ -181,7 +181,7 @@ __device__ __forceinline__ void k1_plan_tail(unsigned long long *cursor, BatchSt
             n_b += c[x];
             maxreg = c[x] > maxreg ? c[x] : maxreg;
         }
-        if (dig) a.rb[b] = n_b;
+        if (dig) rb_put(&a.rb[b], n_b);
         uint32_t pcap = 0, chunks = 0;
         unsigned long long seg = 0;
         if (n_b) {
@@ -203,7 +203,7 @@ __device__ __forceinline__ void k1_plan_tail(unsigned long long *cursor, BatchSt
         B.chunk0 = (uint32_t)(chunk_run + chk_incl - chunks);
         if (dig) a.bk[b] = B;
         if (t == 0) {
-            a.rb[LOG_RB_SEG + q] = seg_tot;
+            rb_put(&a.rb[LOG_RB_SEG + q], seg_tot);
             if (a.spec && seg_tot > a.seg_cap[q]) bad = 1;
         }
         chunk_run += chk_tot;
@@ -216,24 +216,19 @@ __device__ __forceinline__ void k1_plan_tail(unsigned long long *cursor, BatchSt
         LogBucket E{};
         E.chunk0 = (uint32_t)chunk_run;
         a.bk[a.nunits * LOG_ND] = E;
-        a.rb[LOG_RB_CHUNKS] = chunk_run;
+        rb_put(&a.rb[LOG_RB_CHUNKS], chunk_run);
         const bool go = a.spec && !s_bad && S.bad_ts == 0 && S.bad_kg == 0 && S.refire == 0 && S.accepted > 0 &&
                         S.min_idx >= base && S.min_idx < base + a.nunits && chunk_run < (1ull << 32);
         *a.go = go ? 1u : 0u;
-        a.rb[LOG_RB_GO] = go ? 1ull : 0ull;
-        a.rb[LOG_RB_MAXREG] = s_maxreg;
+        rb_put(&a.rb[LOG_RB_GO], go ? 1ull : 0ull);
+        rb_put(&a.rb[LOG_RB_MAXREG], s_maxreg);
     }
     if (t == 0 && a.t0) {
-        a.rb[LOG_RB_T0] = atomicAdd(a.t0, 0ull);
-        a.rb[LOG_RB_T1] = (unsigned long long)wall_clock64();
+        rb_put(&a.rb[LOG_RB_T0], atomicAdd(a.t0, 0ull));
+        rb_put(&a.rb[LOG_RB_T1], (unsigned long long)wall_clock64());
     }
     // the host spins on the sequence word: every other readback word must be visible first
-    __threadfence_system();
-    __syncthreads();
-    if (t == 0) {
-        __threadfence_system();
-        *(volatile unsigned long long *)&a.rb[LOG_RB_SEQ] = a.seq;
-    }
+    rb_publish(&a.rb[LOG_RB_SEQ], a.seq);
 }
 
 // ------------------------------------------------------------------------------------------------

@@ -421,7 +421,7 @@ gwo_status Handle::insert_combined(const int64_t *k, const int64_t *t, const int
         if (const char *e = getenv("GWO_CB_WG")) cb_max_wg = std::max(1, atoi(e));
     }
     const int G = (int)std::max<int64_t>(1, std::min<int64_t>((n + tile - 1) / tile, (int64_t)cb_max_wg));
-    GWO_TRY(ensure_buf(cb_dump_key, (size_t)G * 2 * S * 8));
+    GWO_TRY(ensure_buf(cb_dump_key, (size_t)G * 2 * S * 8 + (size_t)G * 4));
     GWO_TRY(ensure_buf(cb_dump_acc, (size_t)G * 2 * S * NW * 8));
     GWO_TRY(ensure_buf(cb_ovf, (size_t)n * 4));
     if (!cb_ctr.ptr) {   // counters and statistics shards start reset; every gather leaves them reset
@@ -439,6 +439,7 @@ gwo_status Handle::insert_combined(const int64_t *k, const int64_t *t, const int
     CombineArgs a{};
     a.dump_key = (int64_t *)cb_dump_key.ptr;
     a.dump_acc = (int64_t *)cb_dump_acc.ptr;
+    a.dump_used = (uint32_t *)(a.dump_key + (size_t)G * 2 * S);
     a.ovf = (uint32_t *)cb_ovf.ptr;
     a.ovf_count = (unsigned long long *)cb_ctr.ptr;
     a.ovf_cap = (unsigned long long)n;
