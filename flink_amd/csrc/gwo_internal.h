@@ -244,9 +244,11 @@ void launch_slide_refire_slots(const int64_t *key, const int64_t *r_idx, const l
                                long long j0, uint32_t nj, const TableDesc *pdir, long long pane_base,
                                long long pane_len, uint32_t *r_slot, int64_t *before, hipStream_t s);
 // gwo_sort.hip: stable LSD radix sort of (uint32 key, uint32 payload; vals NULL = index); returns 0 when the
-// result is in (k1, v1), 1 when in (k2, v2)
+// result is in (k1, v1), 1 when in (k2, v2).  hist holds hist_cap words (at least 256 * ceil(n / 4096); more lets a
+// small sort use smaller tiles)
 int radix_sort_pairs(const uint32_t *keys, const uint32_t *vals, int64_t n, int key_bits, uint32_t *k1, uint32_t *v1,
-                     uint32_t *k2, uint32_t *v2, uint32_t *hist, hipStream_t s, int digit_bits = 8);
+                     uint32_t *k2, uint32_t *v2, uint32_t *hist, hipStream_t s, int digit_bits = 8,
+                     int64_t hist_cap = 0);
 void launch_key_groups_utf16(const uint16_t *chars, const int64_t *offsets, int64_t n, int max_par, int par,
                              int32_t *hash, int32_t *kg, int32_t *op, hipStream_t s);
 void launch_table_load(const SnapCols &c, int64_t n, const TableDesc &t, const AccPlan &p, hipStream_t s);

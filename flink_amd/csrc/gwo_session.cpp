@@ -27,10 +27,15 @@ struct SessionState {
     int64_t *due = nullptr;         // [T.cap + 1] due watermark per slot (SessGeom::due)
     uint64_t occ_pending = 0;       // entries claimed since T.occ was read, at most (one per record)
     uint64_t live = 0;              // in-flight sessions
+    // the batches' statistics block accumulates (no per-batch reset): each read-back's change since the last is
+    // the batch's (sess_read_err)
     SessErr *d_err = nullptr;
     SessErr *h_err = nullptr;       // pinned
+    SessErr err_prev{};             // d_err as of the last read-back
+    SessErr e{};                    // the last read-back's change (bad_kg_key: the value itself)
     SessErr *d_err_fire = nullptr;  // the watermark sweep's own block: its readback completes lazily (finish_fire)
     SessErr *h_err_fire = nullptr;  // pinned
+    SessErr fire_prev{};            // d_err_fire (also cumulative) as of the last read-back
     DevBuf rec_slot, k1, v1, k2, v2, hist;
     // spill pool of keys with more in-flight sessions than an entry holds (gwo_internal.h SessGeom)
     int64_t *pool = nullptr;
@@ -71,7 +76,8 @@ gwo_status Handle::session_init() {
     GWO_TRY(hipcheck(hipHostMalloc((void **)&S.h_err_fire, sizeof(SessErr), hipHostMallocDefault), "pinned"));
     GWO_TRY(hipcheck(hipEventCreateWithFlags(&ev_fire, hipEventDisableTiming), "event"));
     S.d_pool_top = (unsigned long long *)((char *)S.d_err + sizeof(SessErr));
-    GWO_TRY(hipcheck(hipMemsetAsync(S.d_pool_top, 0, 8, stream), "pool top"));
+    GWO_TRY(hipcheck(hipMemsetAsync(S.d_err, 0, sizeof(SessErr) + 8, stream), "err"));
+    GWO_TRY(hipcheck(hipMemsetAsync(S.d_err_fire, 0, sizeof(SessErr), stream), "fire err"));
     uint64_t cap = kMinCap;
     if (cfg.expected_keys > 0)
         while ((double)cfg.expected_keys > kInitLoad * (double)cap) cap <<= 1;
@@ -121,6 +127,12 @@ gwo_status Handle::sess_read_err() {
     GWO_TRY(hipcheck(hipMemcpyAsync(S.h_err, S.d_err, sizeof(SessErr) + 8, hipMemcpyDeviceToHost, stream), "err"));
     GWO_TRY(hipcheck(hipStreamSynchronize(stream), "err sync"));
     S.pool_top = *(const unsigned long long *)((const char *)S.h_err + sizeof(SessErr));
+    constexpr int W = (int)(sizeof(SessErr) / 8);
+    const unsigned long long *now = (const unsigned long long *)S.h_err, *was = (const unsigned long long *)&S.err_prev;
+    unsigned long long *d = (unsigned long long *)&S.e;
+    for (int i = 0; i < W; ++i) d[i] = now[i] - was[i];
+    S.e.bad_kg_key = S.h_err->bad_kg_key;
+    S.err_prev = *S.h_err;
     return GWO_OK;
 }
 
@@ -205,7 +217,6 @@ gwo_status Handle::insert_session(const int64_t *k, const int64_t *t, const int6
     GWO_TRY(ensure_buf(S.v2, n * 4));
     int64_t nblocks = (n + 4095) / 4096;
     GWO_TRY(ensure_buf(S.hist, (size_t)1024 * nblocks * 4 + 16));
-    GWO_TRY(hipcheck(hipMemsetAsync(S.d_err, 0, sizeof(SessErr), stream), "err"));
     if (side_enabled() && side_cap - (long long)side_rows_committed < n)
         GWO_TRY(grow_side((long long)side_rows_committed + n));
     SessGeom g = sess_geom(*this, S.smax);
@@ -216,7 +227,7 @@ gwo_status Handle::insert_session(const int64_t *k, const int64_t *t, const int6
     while (bits < 32 && (S.T.cap >> bits) > 0) bits++;
     int which = radix_sort_pairs((const uint32_t *)S.rec_slot.ptr, nullptr, n, bits, (uint32_t *)S.k1.ptr,
                                  (uint32_t *)S.v1.ptr, (uint32_t *)S.k2.ptr, (uint32_t *)S.v2.ptr,
-                                 (uint32_t *)S.hist.ptr, stream);
+                                 (uint32_t *)S.hist.ptr, stream, 8, (int64_t)1024 * nblocks);
     GWO_TRY(launch_ok("radix sort"));
     const uint32_t *ss = which ? (const uint32_t *)S.k2.ptr : (const uint32_t *)S.k1.ptr;
     const uint32_t *si = which ? (const uint32_t *)S.v2.ptr : (const uint32_t *)S.v1.ptr;
@@ -227,7 +238,7 @@ gwo_status Handle::insert_session(const int64_t *k, const int64_t *t, const int6
     GWO_TRY(launch_ok("sess process"));
     prof_end(GWO_KERNEL_SESSION, n);
     GWO_TRY(sess_read_err());
-    SessErr &e = *S.h_err;
+    const SessErr &e = S.e;
     if (e.bad_ts)
         return poison(GWO_ERR_NO_TIMESTAMP, "Record has Long.MIN_VALUE timestamp (= no timestamp marker).");
     if (e.bad_kg)
@@ -259,7 +270,6 @@ gwo_status Handle::fire_session(int64_t new_wm) {
     GWO_TRY(finish_fire());
     if (S.live == 0) return GWO_OK;
     GWO_TRY(ensure_output(S.live));
-    GWO_TRY(hipcheck(hipMemsetAsync(S.d_err_fire, 0, sizeof(SessErr), stream), "err"));
     SessGeom g = sess_geom(*this, S.smax);
     g.wm = new_wm;
     prof_begin(GWO_KERNEL_FIRE);
@@ -277,13 +287,15 @@ gwo_status Handle::session_finish_fire() {
     SessionState &S = *sess;
     fire_pending = false;
     GWO_TRY(spin_event(ev_fire, "session fire"));
-    S.live += S.h_err_fire->live_delta;
+    const unsigned long long emitted = S.h_err_fire->emitted - S.fire_prev.emitted;
+    S.live += S.h_err_fire->live_delta - S.fire_prev.live_delta;
+    S.fire_prev = *S.h_err_fire;
     if (discard_after_fire) {   // gwo_discard_output was called while the sweep ran: its rows go too
         discard_after_fire = false;
-        rows_gone += S.h_err_fire->emitted;
+        rows_gone += emitted;
         out_count_dirty = true;
     } else {
-        out_rows += S.h_err_fire->emitted;
+        out_rows += emitted;
     }
     return GWO_OK;
 }
@@ -396,15 +408,14 @@ gwo_status Handle::session_restore_rows(const RestoreRows &R, int64_t new_wm) {
     GWO_TRY(hipcheck(hipMemcpyAsync(en.ptr, nen.data(), (size_t)m * 8, hipMemcpyHostToDevice, stream), "restore"));
     GWO_TRY(hipcheck(hipMemcpyAsync(tm.ptr, ntm.data(), (size_t)m * 4, hipMemcpyHostToDevice, stream), "restore"));
     GWO_TRY(hipcheck(hipMemcpyAsync(w.ptr, nw.data(), (size_t)m * R.nw * 8, hipMemcpyHostToDevice, stream), "restore"));
-    GWO_TRY(hipcheck(hipMemsetAsync(S.d_err, 0, sizeof(SessErr), stream), "err"));
     launch_sess_restore((const int64_t *)k.ptr, (const int64_t *)st.ptr, (const int64_t *)en.ptr,
                         (const int32_t *)tm.ptr, (const int64_t *)w.ptr, m, desc(S.T), S.T.cap, S.stride, plan,
                         sess_geom(*this, S.smax), S.d_err, stream);
     GWO_TRY(launch_ok("session restore"));
     GWO_TRY(sess_read_err());
     for (DevBuf *x : {&k, &st, &en, &tm, &w}) x->release();
-    if (S.h_err->capacity) return poison(GWO_ERR_HIP, "restore: an entry overflowed its inline sessions");
-    S.live += S.h_err->live_delta;
+    if (S.e.capacity) return poison(GWO_ERR_HIP, "restore: an entry overflowed its inline sessions");
+    S.live += S.e.live_delta;
     return sess_rebuild_due();
 }
 

@@ -18,13 +18,13 @@ namespace gwo {
 
 template <int DB>
 __global__ __launch_bounds__(RS_THREADS) void rs_hist_kernel(const uint32_t *__restrict__ keys, int64_t n, int shift,
-                                                             uint32_t *__restrict__ block_hist, int nblocks) {
+                                                             uint32_t *__restrict__ block_hist, int nblocks, int tile) {
     constexpr int BINS = 1 << DB;
     __shared__ uint32_t h[BINS];
     for (int b = threadIdx.x; b < BINS; b += RS_THREADS) h[b] = 0;
     __syncthreads();
-    int64_t base = (int64_t)blockIdx.x * RS_TILE;
-    for (int j = threadIdx.x; j < RS_TILE; j += RS_THREADS) {
+    int64_t base = (int64_t)blockIdx.x * tile;
+    for (int j = threadIdx.x; j < tile; j += RS_THREADS) {
         int64_t i = base + j;
         if (i < n) atomicAdd(&h[(keys[i] >> shift) & (BINS - 1)], 1u);
     }
@@ -57,7 +57,7 @@ __global__ __launch_bounds__(RS_THREADS) void rs_scatter_kernel(const uint32_t *
                                                                 const uint32_t *__restrict__ vals, int64_t n,
                                                                 int shift, const uint32_t *__restrict__ offsets,
                                                                 int nblocks, uint32_t *__restrict__ okeys,
-                                                                uint32_t *__restrict__ ovals) {
+                                                                uint32_t *__restrict__ ovals, int tile) {
     constexpr int BINS = 1 << DB;
     __shared__ uint32_t run[BINS];              // running position per digit for this block
     __shared__ uint32_t wcnt[RS_THREADS / 64][BINS];
@@ -77,14 +77,26 @@ __global__ __launch_bounds__(RS_THREADS) void rs_scatter_kernel(const uint32_t *
     }
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const uint64_t lt = (1ull << lane) - 1;
-    int64_t base = (int64_t)blockIdx.x * RS_TILE;
-    for (int sub = 0; sub < RS_TILE; sub += RS_THREADS) {
+    const int64_t base = (int64_t)blockIdx.x * tile;
+    // the block's keys and payloads load before the first sub-tile is ranked (one round trip, not one per sub-tile)
+    constexpr int SUBS = RS_TILE / RS_THREADS;
+    uint32_t kq[SUBS], vq[SUBS];
+#pragma unroll
+    for (int q = 0; q < SUBS; ++q) {
+        const int64_t i = base + q * RS_THREADS + threadIdx.x;
+        const bool ok = q * RS_THREADS < tile && i < n;
+        kq[q] = ok ? keys[i] : 0u;
+        vq[q] = ok ? (vals ? vals[i] : (uint32_t)i) : 0u;
+    }
+#pragma unroll
+    for (int q = 0; q < SUBS; ++q) {
+        if (q * RS_THREADS >= tile) break;
         for (int b = threadIdx.x; b < BINS; b += RS_THREADS)
             for (int w = 0; w < RS_THREADS / 64; ++w) wcnt[w][b] = 0;
         __syncthreads();
-        int64_t i = base + sub + threadIdx.x;
+        const int64_t i = base + q * RS_THREADS + threadIdx.x;
         bool valid = i < n;
-        uint32_t k = valid ? keys[i] : 0;
+        uint32_t k = kq[q];
         uint32_t d = (k >> shift) & (BINS - 1);
         // lanes of this wave holding the same digit
         uint64_t same = __ballot(valid);
@@ -99,7 +111,7 @@ __global__ __launch_bounds__(RS_THREADS) void rs_scatter_kernel(const uint32_t *
             uint32_t pos = run[d] + rank;
             for (int w = 0; w < wid; ++w) pos += wcnt[w][d];
             okeys[pos] = k;
-            ovals[pos] = vals ? vals[i] : (uint32_t)i;
+            ovals[pos] = vq[q];
         }
         __syncthreads();
         // advance running positions by this sub-tile's digit totals
@@ -116,9 +128,20 @@ __global__ __launch_bounds__(RS_THREADS) void rs_scatter_kernel(const uint32_t *
 // tmp buffers: k1/v1/k2/v2 of n entries each, hist of 256*ceil(n/4096) entries (1024*.. with digit_bits 10).
 // The result lands in (k1, v1) or (k2, v2): returns 0 for (k1, v1), 1 for (k2, v2).
 int radix_sort_pairs(const uint32_t *keys, const uint32_t *vals, int64_t n, int key_bits, uint32_t *k1,
-                     uint32_t *v1, uint32_t *k2, uint32_t *v2, uint32_t *hist, hipStream_t s, int digit_bits) {
+                     uint32_t *v1, uint32_t *k2, uint32_t *v2, uint32_t *hist, hipStream_t s, int digit_bits,
+                     int64_t hist_cap) {
     int nblocks = (int)((n + RS_TILE - 1) / RS_TILE);
     if (nblocks < 1) nblocks = 1;
+    // small batches (the fused two-launch pass): tiles shrink while the block count stays <= 64 and the caller's
+    // histogram holds 256 words per block -- a block's scatter is a chain of tile / 256 ranked sub-tiles
+    int tile = RS_TILE;
+    const bool small = !(digit_bits == 10 && key_bits > 8 && key_bits <= 20) && nblocks <= 64;
+    while (small && tile > RS_THREADS) {
+        const int64_t nb = (n + tile / 2 - 1) / (tile / 2);
+        if (nb > 64 || 256 * nb > hist_cap) break;
+        tile /= 2;
+        nblocks = (int)(nb < 1 ? 1 : nb);
+    }
     const uint32_t *ik = keys;
     const uint32_t *iv = vals;
     uint32_t *ok = k1, *ov = v1;
@@ -126,19 +149,22 @@ int radix_sort_pairs(const uint32_t *keys, const uint32_t *vals, int64_t n, int 
     const int db = digit_bits == 10 && key_bits > 8 && key_bits <= 20 ? 10 : 8;
     for (int shift = 0; shift < key_bits; shift += db) {
         if (db == 10) {
-            hipLaunchKernelGGL(rs_hist_kernel<10>, dim3(nblocks), dim3(RS_THREADS), 0, s, ik, n, shift, hist, nblocks);
+            hipLaunchKernelGGL(rs_hist_kernel<10>, dim3(nblocks), dim3(RS_THREADS), 0, s, ik, n, shift, hist, nblocks,
+                               tile);
             hipLaunchKernelGGL(rs_scan_kernel, dim3(1), dim3(1024), 0, s, hist, (int64_t)1024 * nblocks);
             hipLaunchKernelGGL((rs_scatter_kernel<10, false>), dim3(nblocks), dim3(RS_THREADS), 0, s, ik, iv, n, shift,
-                               hist, nblocks, ok, ov);
+                               hist, nblocks, ok, ov, tile);
         } else if (nblocks <= 64) {   // small batches: two launches per pass
-            hipLaunchKernelGGL(rs_hist_kernel<8>, dim3(nblocks), dim3(RS_THREADS), 0, s, ik, n, shift, hist, nblocks);
+            hipLaunchKernelGGL(rs_hist_kernel<8>, dim3(nblocks), dim3(RS_THREADS), 0, s, ik, n, shift, hist, nblocks,
+                               tile);
             hipLaunchKernelGGL((rs_scatter_kernel<8, true>), dim3(nblocks), dim3(RS_THREADS), 0, s, ik, iv, n, shift,
-                               hist, nblocks, ok, ov);
+                               hist, nblocks, ok, ov, tile);
         } else {
-            hipLaunchKernelGGL(rs_hist_kernel<8>, dim3(nblocks), dim3(RS_THREADS), 0, s, ik, n, shift, hist, nblocks);
+            hipLaunchKernelGGL(rs_hist_kernel<8>, dim3(nblocks), dim3(RS_THREADS), 0, s, ik, n, shift, hist, nblocks,
+                               tile);
             hipLaunchKernelGGL(rs_scan_kernel, dim3(1), dim3(1024), 0, s, hist, (int64_t)256 * nblocks);
             hipLaunchKernelGGL((rs_scatter_kernel<8, false>), dim3(nblocks), dim3(RS_THREADS), 0, s, ik, iv, n, shift,
-                               hist, nblocks, ok, ov);
+                               hist, nblocks, ok, ov, tile);
         }
         ik = ok;
         iv = ov;
