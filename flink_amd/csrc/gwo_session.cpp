@@ -35,7 +35,8 @@ struct SessionState {
     SessErr e{};                    // the last read-back's change (bad_kg_key: the value itself)
     SessErr *d_err_fire = nullptr;  // the watermark sweep's own block: its readback completes lazily (finish_fire)
     SessErr *h_err_fire = nullptr;  // pinned
-    SessErr fire_prev{};            // d_err_fire (also cumulative) as of the last read-back
+    SessErr fire_prev{};
+    int sort_digits = 8;            // radix digit bits of the slot sort (GWO_SESS_DIGITS: 8 or 10)            // d_err_fire (also cumulative) as of the last read-back
     DevBuf rec_slot, k1, v1, k2, v2, hist;
     // spill pool of keys with more in-flight sessions than an entry holds (gwo_internal.h SessGeom)
     int64_t *pool = nullptr;
@@ -68,6 +69,7 @@ gwo_status Handle::session_init() {
     sess = new SessionState();
     SessionState &S = *sess;
     if (const char *e = getenv("GWO_SESSION_SLOTS")) S.smax = std::max(1, std::min(16, atoi(e)));
+    if (const char *e = getenv("GWO_SESS_DIGITS")) S.sort_digits = atoi(e) == 10 ? 10 : 8;
     S.stride = (2 + S.smax * (3 + plan.nwords) + 1) & ~1;
     // the pool's bump counter sits right behind the batch's SessErr block: one copy reads both back
     GWO_TRY(dalloc((void **)&S.d_err, sizeof(SessErr) + 8));
@@ -216,7 +218,8 @@ gwo_status Handle::insert_session(const int64_t *k, const int64_t *t, const int6
     GWO_TRY(ensure_buf(S.k2, n * 4));
     GWO_TRY(ensure_buf(S.v2, n * 4));
     int64_t nblocks = (n + 4095) / 4096;
-    GWO_TRY(ensure_buf(S.hist, (size_t)1024 * nblocks * 4 + 16));
+    const int64_t hist_words = (int64_t)1024 * std::max<int64_t>(nblocks, 64);   // room for the small-sort tiles
+    GWO_TRY(ensure_buf(S.hist, (size_t)hist_words * 4 + 16));
     if (side_enabled() && side_cap - (long long)side_rows_committed < n)
         GWO_TRY(grow_side((long long)side_rows_committed + n));
     SessGeom g = sess_geom(*this, S.smax);
@@ -227,7 +230,7 @@ gwo_status Handle::insert_session(const int64_t *k, const int64_t *t, const int6
     while (bits < 32 && (S.T.cap >> bits) > 0) bits++;
     int which = radix_sort_pairs((const uint32_t *)S.rec_slot.ptr, nullptr, n, bits, (uint32_t *)S.k1.ptr,
                                  (uint32_t *)S.v1.ptr, (uint32_t *)S.k2.ptr, (uint32_t *)S.v2.ptr,
-                                 (uint32_t *)S.hist.ptr, stream, 8, (int64_t)1024 * nblocks);
+                                 (uint32_t *)S.hist.ptr, stream, S.sort_digits, hist_words);
     GWO_TRY(launch_ok("radix sort"));
     const uint32_t *ss = which ? (const uint32_t *)S.k2.ptr : (const uint32_t *)S.k1.ptr;
     const uint32_t *si = which ? (const uint32_t *)S.v2.ptr : (const uint32_t *)S.v1.ptr;

@@ -61,17 +61,30 @@ __global__ __launch_bounds__(RS_THREADS) void rs_scatter_kernel(const uint32_t *
     constexpr int BINS = 1 << DB;
     __shared__ uint32_t run[BINS];              // running position per digit for this block
     __shared__ uint32_t wcnt[RS_THREADS / 64][BINS];
-    if constexpr (FUSED) {
-        static_assert(BINS == RS_THREADS, "one digit per thread");
-        const uint32_t *h = offsets + (int64_t)threadIdx.x * nblocks;
-        uint32_t tot = 0, pre = 0;
-        for (int j = 0; j < nblocks; ++j) {
-            const uint32_t c = h[j];
-            tot += c;
-            pre += j < (int)blockIdx.x ? c : 0u;
+    if constexpr (FUSED) {   // thread t owns digits [t * DPT, (t + 1) * DPT)
+        constexpr int DPT = BINS / RS_THREADS;
+        static_assert(DPT * RS_THREADS == BINS, "whole digits per thread");
+        uint32_t tot[DPT], pre[DPT], sum = 0;
+#pragma unroll
+        for (int c = 0; c < DPT; ++c) {
+            const uint32_t *h = offsets + (int64_t)(threadIdx.x * DPT + c) * nblocks;
+            tot[c] = 0;
+            pre[c] = 0;
+#pragma unroll 16
+            for (int j = 0; j < nblocks; ++j) {   // unrolled: 16 loads in flight, not one round trip per block
+                const uint32_t x = h[j];
+                tot[c] += x;
+                pre[c] += j < (int)blockIdx.x ? x : 0u;
+            }
+            sum += tot[c];
         }
         uint32_t all;
-        run[threadIdx.x] = block_exclusive_scan(tot, &all) + pre;
+        uint32_t at = block_exclusive_scan(sum, &all);
+#pragma unroll
+        for (int c = 0; c < DPT; ++c) {
+            run[threadIdx.x * DPT + c] = at + pre[c];
+            at += tot[c];
+        }
     } else {
         for (int b = threadIdx.x; b < BINS; b += RS_THREADS) run[b] = offsets[(int64_t)b * nblocks + blockIdx.x];
     }
@@ -132,13 +145,17 @@ int radix_sort_pairs(const uint32_t *keys, const uint32_t *vals, int64_t n, int 
                      int64_t hist_cap) {
     int nblocks = (int)((n + RS_TILE - 1) / RS_TILE);
     if (nblocks < 1) nblocks = 1;
-    // small batches (the fused two-launch pass): tiles shrink while the block count stays <= 64 and the caller's
-    // histogram holds 256 words per block -- a block's scatter is a chain of tile / 256 ranked sub-tiles
+    const int db = digit_bits == 10 && key_bits > 8 && key_bits <= 20 ? 10 : 8;
+    const int64_t bins = (int64_t)1 << db;
+    if (hist_cap <= 0) hist_cap = bins * nblocks;   // the documented minimum
+    // small sorts (at most 64 blocks, the histogram in room): two launches per pass, each block deriving its
+    // offsets from the raw histograms; tiles shrink while that holds -- a block's scatter is a chain of
+    // tile / 256 ranked sub-tiles
     int tile = RS_TILE;
-    const bool small = !(digit_bits == 10 && key_bits > 8 && key_bits <= 20) && nblocks <= 64;
-    while (small && tile > RS_THREADS) {
+    const bool fused = nblocks <= 64 && bins * nblocks <= hist_cap;
+    while (fused && tile > RS_THREADS) {
         const int64_t nb = (n + tile / 2 - 1) / (tile / 2);
-        if (nb > 64 || 256 * nb > hist_cap) break;
+        if (nb > 64 || bins * nb > hist_cap) break;
         tile /= 2;
         nblocks = (int)(nb < 1 ? 1 : nb);
     }
@@ -146,25 +163,29 @@ int radix_sort_pairs(const uint32_t *keys, const uint32_t *vals, int64_t n, int 
     const uint32_t *iv = vals;
     uint32_t *ok = k1, *ov = v1;
     int which = 0;
-    const int db = digit_bits == 10 && key_bits > 8 && key_bits <= 20 ? 10 : 8;
     for (int shift = 0; shift < key_bits; shift += db) {
         if (db == 10) {
             hipLaunchKernelGGL(rs_hist_kernel<10>, dim3(nblocks), dim3(RS_THREADS), 0, s, ik, n, shift, hist, nblocks,
                                tile);
-            hipLaunchKernelGGL(rs_scan_kernel, dim3(1), dim3(1024), 0, s, hist, (int64_t)1024 * nblocks);
-            hipLaunchKernelGGL((rs_scatter_kernel<10, false>), dim3(nblocks), dim3(RS_THREADS), 0, s, ik, iv, n, shift,
-                               hist, nblocks, ok, ov, tile);
-        } else if (nblocks <= 64) {   // small batches: two launches per pass
-            hipLaunchKernelGGL(rs_hist_kernel<8>, dim3(nblocks), dim3(RS_THREADS), 0, s, ik, n, shift, hist, nblocks,
-                               tile);
-            hipLaunchKernelGGL((rs_scatter_kernel<8, true>), dim3(nblocks), dim3(RS_THREADS), 0, s, ik, iv, n, shift,
-                               hist, nblocks, ok, ov, tile);
+            if (fused) {
+                hipLaunchKernelGGL((rs_scatter_kernel<10, true>), dim3(nblocks), dim3(RS_THREADS), 0, s, ik, iv, n,
+                                   shift, hist, nblocks, ok, ov, tile);
+            } else {
+                hipLaunchKernelGGL(rs_scan_kernel, dim3(1), dim3(1024), 0, s, hist, (int64_t)1024 * nblocks);
+                hipLaunchKernelGGL((rs_scatter_kernel<10, false>), dim3(nblocks), dim3(RS_THREADS), 0, s, ik, iv, n,
+                                   shift, hist, nblocks, ok, ov, tile);
+            }
         } else {
             hipLaunchKernelGGL(rs_hist_kernel<8>, dim3(nblocks), dim3(RS_THREADS), 0, s, ik, n, shift, hist, nblocks,
                                tile);
-            hipLaunchKernelGGL(rs_scan_kernel, dim3(1), dim3(1024), 0, s, hist, (int64_t)256 * nblocks);
-            hipLaunchKernelGGL((rs_scatter_kernel<8, false>), dim3(nblocks), dim3(RS_THREADS), 0, s, ik, iv, n, shift,
-                               hist, nblocks, ok, ov, tile);
+            if (fused) {
+                hipLaunchKernelGGL((rs_scatter_kernel<8, true>), dim3(nblocks), dim3(RS_THREADS), 0, s, ik, iv, n,
+                                   shift, hist, nblocks, ok, ov, tile);
+            } else {
+                hipLaunchKernelGGL(rs_scan_kernel, dim3(1), dim3(1024), 0, s, hist, (int64_t)256 * nblocks);
+                hipLaunchKernelGGL((rs_scatter_kernel<8, false>), dim3(nblocks), dim3(RS_THREADS), 0, s, ik, iv, n,
+                                   shift, hist, nblocks, ok, ov, tile);
+            }
         }
         ik = ok;
         iv = ov;
