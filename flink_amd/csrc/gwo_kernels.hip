@@ -861,14 +861,29 @@ __global__ __launch_bounds__(256) void fire_kernel(TableDesc t, uint64_t cap, Ac
     for (uint64_t b0 = (uint64_t)blockIdx.x * CH; b0 < cap + 1; b0 += (uint64_t)gridDim.x * CH) {
         unsigned flags = 0;
         unsigned pre[FIRE_FPT];
+        // every slot's key and first two accumulator words load before any is tested (one round trip per chunk,
+        // not two per slot); indices past the table read the side slot, words past the entry its last word
+        int64_t kw[FIRE_FPT], aw[FIRE_FPT][2];
+        const int w2 = NW >= 2 ? 2 : 1;
+#pragma unroll
+        for (int j = 0; j < FIRE_FPT; ++j) {
+            const uint64_t i = b0 + (uint64_t)j * 256 + threadIdx.x;
+            const int64_t *e = fire_entry(t, cap, p.stride, i <= cap ? i : cap);
+            kw[j] = e[0];
+            aw[j][0] = e[1];
+            aw[j][1] = e[w2];
+        }
 #pragma unroll
         for (int j = 0; j < FIRE_FPT; ++j) {
             uint64_t i = b0 + (uint64_t)j * 256 + threadIdx.x;
             bool occ = false;
             if (i <= cap) {
-                const int64_t *e = fire_entry(t, cap, p.stride, i);
-                occ = i < cap ? e[0] != GWO_EMPTY_KEY : e[0] != 0;
-                if (occ && live_word >= 0) occ = e[1 + live_word] > 0;
+                occ = i < cap ? kw[j] != GWO_EMPTY_KEY : kw[j] != 0;
+                if (occ && live_word >= 0) {
+                    const int64_t lv = live_word == 0 ? aw[j][0] : (live_word == 1 && NW >= 2 ? aw[j][1]
+                                                                     : fire_entry(t, cap, p.stride, i)[1 + live_word]);
+                    occ = lv > 0;
+                }
             }
             if (occ) flags |= 1u << j;
             const unsigned long long m = __ballot(occ);
@@ -896,9 +911,9 @@ __global__ __launch_bounds__(256) void fire_kernel(TableDesc t, uint64_t cap, Ac
             int64_t acc[GWO_MAX_WORDS];
 #pragma unroll
             for (int w = 0; w < GWO_MAX_WORDS; ++w)
-                if (w < NW) acc[w] = e[1 + w];
+                if (w < NW) acc[w] = w < 2 ? aw[j][w] : e[1 + w];
             if ((long long)pos < o.cap) {
-                o.key[pos] = i < cap ? e[0] : GWO_EMPTY_KEY;
+                o.key[pos] = i < cap ? kw[j] : GWO_EMPTY_KEY;
                 o.start[pos] = start;
                 o.end[pos] = end;
                 write_results(p, rp, acc, o, pos);

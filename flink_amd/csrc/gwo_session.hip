@@ -279,10 +279,18 @@ __global__ __launch_bounds__(256) void sess_fire_kernel(TableDesc t, uint64_t ca
     // rounds are workgroup-uniform (block_reserve synchronises the workgroup)
     for (uint64_t r0 = 0; r0 <= cap; r0 += span * SF_SPT) {
         unsigned due_m = 0, nrow = 0;
+        // the round's due words load together (most slots are not due: one round trip for all of them)
+        bool due[SF_SPT];
 #pragma unroll
         for (int j = 0; j < SF_SPT; ++j) {
             const uint64_t i = r0 + (uint64_t)j * span + (uint64_t)blockIdx.x * 256 + threadIdx.x;
-            if (i > cap || g.due[i] > g.wm) continue;   // a slot whose due watermark is ahead: nothing to do
+            const int64_t dv = g.due[i <= cap ? i : cap];   // unconditional (clamped): no branch between the loads
+            due[j] = i <= cap && dv <= g.wm;
+        }
+#pragma unroll
+        for (int j = 0; j < SF_SPT; ++j) {
+            const uint64_t i = r0 + (uint64_t)j * span + (uint64_t)blockIdx.x * 256 + threadIdx.x;
+            if (!due[j]) continue;   // a slot whose due watermark is ahead: nothing to do
             int64_t k;
             const int64_t *e = sess_slot_entry(t, cap, stride, i, k);
             if (!e) continue;
