@@ -10,7 +10,8 @@ A "step" = one watermark interval: gwo_submit(batch) (classify + partition into 
 record logs) + gwo_advance_watermark (fire: fold every window whose end passed and
 emit its rows).  The operator reserves its steady-state device memory at creation from the
 distinct-keys hint, so any warmup >= 0 measures the steady state; 20 timed steps include two fires
-(a window fires every 10 steps).  With --gpus N the job runs one process per GPU; every rank generates
+(a window fires every 10 steps).  With --gpus N the job runs one process per GPU (under torch.distributed.run,
+or spawned here when WORLD_SIZE is unset; fewer GPUs than N is an error); every rank generates
 its own slice of a 100M*N-key stream and gwo_submit shuffles records to their key-group owner with an
 RCCL all-to-all (weak scaling).
 
@@ -68,8 +69,59 @@ def parse():
     return p.parse_args()
 
 
+def host_cores():
+    """Host cores this process may use: the CPU affinity mask, capped by a cgroup CPU quota (cpu.max) when one is
+    set.  Returns (cores, detail)."""
+    cpus = os.cpu_count() or 1
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = cpus
+    quota = None
+    for f in ("/sys/fs/cgroup/cpu.max", "/sys/fs/cgroup/cpu/cpu.cfs_quota_us"):
+        try:
+            txt = open(f).read().split()
+        except OSError:
+            continue
+        if f.endswith("cpu.max") and txt and txt[0] != "max":
+            quota = int(txt[0]) / int(txt[1])
+        elif f.endswith("cfs_quota_us") and txt and int(txt[0]) > 0:
+            quota = int(txt[0]) / int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+        break
+    cores = aff if quota is None else max(1, min(aff, int(quota)))
+    return cores, {"os_cpu_count": cpus, "affinity": aff, "cgroup_cpu_quota": quota}
+
+
+def spawn_ranks(a):
+    """--gpus N without a launcher: one child process per GPU (RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* set), as
+    torch.distributed.run would start them.  This parent makes no GPU call: it counts devices (no HIP context on
+    this image) and waits for the children; rank 0 prints the line."""
+    import socket
+    import subprocess
+    import torch
+    have = torch.cuda.device_count()
+    if have < a.gpus:
+        sys.exit(f"bench.py: --gpus {a.gpus} needs {a.gpus} GPUs, this host has {have}")
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(a.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(a.gpus), LOCAL_WORLD_SIZE=str(a.gpus),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    for p in procs:
+        rc = p.wait() or rc
+    sys.exit(rc)
+
+
 def main():
     a = parse()
+    if "WORLD_SIZE" not in os.environ and a.gpus > 1:
+        spawn_ranks(a)
+    if "WORLD_SIZE" in os.environ and int(os.environ["WORLD_SIZE"]) != a.gpus:
+        sys.exit(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={os.environ['WORLD_SIZE']}")
     import torch
     import flink_amd as F
     from flink_amd import _native as N
@@ -244,7 +296,7 @@ def main():
     out = None
     if rank == 0:
         cpu = None
-        if not a.no_cpu_baseline:
+        if not a.no_cpu_baseline and world == 1:   # rank 0 at N=1 only
             cpu = cpu_baseline(a, N, lib, local)
         ms_per_step = elapsed / a.steps * 1e3
         out = {
@@ -352,7 +404,8 @@ def host_fed_run(a, F, N, lib, local, per, exp_keys):
 
 def cpu_baseline(a, N, lib, local):
     """The oracle's C restatement of WindowOperator (oracle/window_oracle.c: per-subtask heap hash map +
-    deduplicated timer heap, 16 threads sharded by key group; kind 'port', not Flink -- no JDK here) on a
+    deduplicated timer heap, one thread per usable host core (host_cores()) sharded by key group; kind 'port', not
+    Flink -- no JDK here) on a
     bounded sample of the same workload: the C4 stream with keys and records per step scaled down by
     --cpu-scale (keys per record unchanged), 11 one-second steps -- window [0, 10 s) complete -- ending
     with the final Long.MAX_VALUE watermark, so every window fires and state reaches its steady size."""
@@ -368,13 +421,14 @@ def cpu_baseline(a, N, lib, local):
     del k, t, v
     wms = step_watermarks(th, per, steps, a.lag_ms)
     batches = [((i + 1) * per, wms[i]) for i in range(steps)] + [(per * steps, (1 << 63) - 1)]
-    threads = min(os.cpu_count() or 1, 16)
+    threads, detail = host_cores()
     t0 = time.perf_counter()
     _, _, late = cbaseline.run_tumbling(kh, th, vh, batches, a.window_ms, threads=threads,
                                         max_par=a.max_parallelism, rows=False)
     secs = time.perf_counter() - t0
     n = per * steps
     return {"value": n / secs, "unit": "records/s", "cores": threads, "kind": "port", "seconds": secs,
+            "cores_detail": dict(detail, rule="threads = the CPU affinity mask, capped by the cgroup CPU quota"),
             "sample": f"C4 stream scaled 1/{sc}: {nkeys} keys, {per} records per 1-s step, {steps} steps "
                       f"({n} records: window [0, {a.window_ms} ms) complete) then the final Long.MAX_VALUE "
                       f"watermark (every window fires); C restatement of WindowOperator (oracle/window_oracle.c), "

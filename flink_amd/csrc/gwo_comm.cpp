@@ -44,6 +44,10 @@ struct Comm {
     int vranks = 0;
     uint64_t rcap = 0, wcap = 0;  // narrow / wide send region capacities of the routed K1 (records)
     int64_t tbase = 0;            // the routed batch's timestamp base (20-B wire records carry int32 ts - tbase)
+    // the min over ranks of their watermarks, as of comm_init or the last gwo_advance_watermark (collective calls):
+    // every rank holds the same value, so sender and receiver derive the same tbase from it even when restored
+    // subtasks hold different watermarks
+    int64_t agreed_wm = (int64_t)0x8000000000000000LL;
     int64_t recv_n = 0, recv_w = 0;   // narrow / wide records received by the last routed exchange
     int64_t recv_off_w = 0;       // word offset of the wide records in recvbuf
 };
@@ -194,7 +198,7 @@ gwo_status Handle::comm_route_args(int64_t n, LogRoute *rt, bool *on) {
     const double mean = (double)n / P;
     C.rcap = ((uint64_t)(mean + 6.0 * std::sqrt(mean) + 64.0) + 1) & ~1ull;   // even: regions stay 8-B aligned
     C.wcap = 256 + (uint64_t)n / 1024;
-    C.tbase = log_rt_tbase(wm);   // the watermark every rank shares (min over ranks)
+    C.tbase = log_rt_tbase(C.agreed_wm);   // the same on every rank (min over ranks)
     GWO_TRY(ensure_buf(C.sendbuf, (size_t)P * (C.rcap * 20 + C.wcap * 24) + 24));
     *rt = LogRoute{};
     rt->mode = 1;
@@ -226,20 +230,19 @@ gwo_status Handle::comm_after_route(const int64_t *k, const int64_t *t, const in
     unsigned long long *d_send = (unsigned long long *)C.counts.ptr, *d_recv = d_send + 2 * P;
     if (n == 0) GWO_TRY(comm_mark_routed());   // (no K1 ran: the counts were zeroed on the main stream)
     GWO_TRY(hipcheck(hipStreamWaitEvent(C.cs, C.ev_routed, 0), "event wait"));
-    if (!virt) {
-        GWO_TRY(nccl_ok(this, ncclGroupStart(), "group"));
-        for (int p = 0; p < P; ++p) {
-            if (p == me) continue;
-            GWO_TRY(nccl_ok(this, ncclSend(d_send + 2 * p, 2, ncclUint64, p, C.nc, C.cs), "send count"));
-            GWO_TRY(nccl_ok(this, ncclRecv(d_recv + 2 * p, 2, ncclUint64, p, C.nc, C.cs), "recv count"));
-        }
-        GWO_TRY(nccl_ok(this, ncclGroupEnd(), "group end"));
+    // one send/recv pair per peer; virtual ranks send to this rank itself, so what it routes to virtual GPU p
+    // comes back "from p" through the same RCCL calls a real rank makes
+    GWO_TRY(nccl_ok(this, ncclGroupStart(), "group"));
+    for (int p = 0; p < P; ++p) {
+        if (p == me) continue;
+        const int peer = virt ? me : p;
+        GWO_TRY(nccl_ok(this, ncclSend(d_send + 2 * p, 2, ncclUint64, peer, C.nc, C.cs), "send count"));
+        GWO_TRY(nccl_ok(this, ncclRecv(d_recv + 2 * p, 2, ncclUint64, peer, C.nc, C.cs), "recv count"));
     }
+    GWO_TRY(nccl_ok(this, ncclGroupEnd(), "group end"));
     unsigned long long *hs = C.h_counts, *hr = C.h_counts + 2 * P;
-    GWO_TRY(hipcheck(hipMemcpyAsync(hs, d_send, (size_t)(virt ? 2 : 4) * P * 8, hipMemcpyDeviceToHost, C.cs), "counts"));
+    GWO_TRY(hipcheck(hipMemcpyAsync(hs, d_send, (size_t)4 * P * 8, hipMemcpyDeviceToHost, C.cs), "counts"));
     GWO_TRY(hipcheck(hipStreamSynchronize(C.cs), "counts sync"));
-    if (virt)   // what this rank routes to virtual GPU p comes back to it "from p"
-        for (int q = 0; q < 2 * P; ++q) hr[q] = hs[q];
     hs[2 * me] = hs[2 * me + 1] = 0;   // (K1 never routes a record to its own GPU)
     hr[2 * me] = hr[2 * me + 1] = 0;
     uint64_t rcap = C.rcap, wcap = C.wcap, mx = 0, mw = 0;
@@ -348,20 +351,28 @@ gwo_status Handle::comm_unpack(const int64_t *aos, int64_t n, const int64_t **rk
     return GWO_OK;
 }
 
+// The min over ranks of the channel watermarks (StatusWatermarkValve.java:163-181): an RCCL all-reduce on the main
+// stream.  It also runs on a 1-rank communicator that rehearses P virtual ranks, so that call executes on one GPU too.
+static gwo_status allreduce_min(Handle *h, int64_t v, int64_t *out) {
+    Comm &C = *h->comm;
+    int64_t *d = (int64_t *)C.counts.ptr + 6 * std::max(C.nranks, C.vranks);   // past the count words and scratch
+    *C.h_wm = v;
+    GWO_TRY(h->hipcheck(hipMemcpyAsync(d, C.h_wm, 8, hipMemcpyHostToDevice, h->stream), "wm"));
+    GWO_TRY(nccl_ok(h, ncclAllReduce(d, d, 1, ncclInt64, ncclMin, C.nc, h->stream), "allreduce wm"));
+    GWO_TRY(h->hipcheck(hipMemcpyAsync(C.h_wm, d, 8, hipMemcpyDeviceToHost, h->stream), "wm"));
+    GWO_TRY(h->hipcheck(hipStreamSynchronize(h->stream), "wm sync"));
+    *out = *C.h_wm;
+    return GWO_OK;
+}
+
 gwo_status Handle::comm_min_watermark(int64_t wm_in, int64_t *out) {
     Comm &C = *comm;
-    if (C.nranks == 1) {   // nothing to agree on
-        *out = wm_in;
+    if (C.nranks == 1 && C.vranks <= 1) {   // nothing to agree on
+        *out = C.agreed_wm = wm_in;
         return GWO_OK;
     }
-    GWO_TRY(ensure_buf(C.counts, (size_t)2 * C.nranks * 8 + 16));
-    int64_t *d = (int64_t *)C.counts.ptr;
-    *C.h_wm = wm_in;
-    GWO_TRY(hipcheck(hipMemcpyAsync(d, C.h_wm, 8, hipMemcpyHostToDevice, stream), "wm"));
-    GWO_TRY(nccl_ok(this, ncclAllReduce(d, d, 1, ncclInt64, ncclMin, C.nc, stream), "allreduce wm"));
-    GWO_TRY(hipcheck(hipMemcpyAsync(C.h_wm, d, 8, hipMemcpyDeviceToHost, stream), "wm"));
-    GWO_TRY(hipcheck(hipStreamSynchronize(stream), "wm sync"));
-    *out = *C.h_wm;
+    GWO_TRY(allreduce_min(this, wm_in, out));
+    C.agreed_wm = *out;
     return GWO_OK;
 }
 
@@ -428,7 +439,11 @@ extern "C" gwo_status gwo_comm_init(gwo_handle *hh, const uint8_t *id, int32_t n
         return h->fail(GWO_ERR_COMM, "ncclCommInitRank: %s", ncclGetErrorString(r));
     }
     h->comm = C;
-    return GWO_OK;
+    // the ranks' watermarks may differ (subtasks restored from different checkpoints): agree on their min now, so
+    // every rank's first routed batch encodes and decodes wire timestamps against the same base
+    gwo_status st = h->ensure_buf(C->counts, (size_t)6 * cranks * 8 + 16);   // (never reallocated later)
+    if (st == GWO_OK) st = allreduce_min(h, h->wm, &C->agreed_wm);
+    return st;
 }
 
 // Stateless batch form of KeyGroupStreamPartitioner.selectChannel (the route kernel the exchange

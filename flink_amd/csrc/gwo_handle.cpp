@@ -267,8 +267,15 @@ gwo_status Handle::submit_local(const int64_t *k, const int64_t *t, const int64_
     return insert_windowed(k, t, v, n);
 }
 
+// StatusWatermarkValve.inputWatermark (SJ/runtime/streamstatus/StatusWatermarkValve.java:86-101,163-181): a
+// channel's watermark that does not increase is ignored, the operator watermark is the min over channels (ranks)
+// and it is forwarded -- here: windows fire -- only when that min grows.  With a communicator every rank must call
+// this (the min is a collective), including the calls that turn out to be no-ops.
 gwo_status Handle::advance_watermark(int64_t new_wm) {
-    if (comm) GWO_TRY(comm_min_watermark(new_wm, &new_wm));
+    if (new_wm > in_wm) in_wm = new_wm;
+    new_wm = in_wm;
+    if (comm) GWO_TRY(comm_min_watermark(in_wm, &new_wm));
+    if (new_wm <= wm) return GWO_OK;
     gwo_status s = GWO_OK;
     switch (cfg.assigner) {
         case GWO_ASSIGNER_TUMBLING: s = logst ? fire_log(new_wm) : fire_tumbling(new_wm); break;

@@ -99,6 +99,9 @@ struct Handle {
     WindowGeom geom{};
     bool needs_value = true;
     int64_t wm = (int64_t)0x8000000000000000LL;  // Long.MIN_VALUE, InternalTimerServiceImpl.currentWatermark
+    // this subtask's input channel watermark (StatusWatermarkValve.InputChannelStatus.watermark): the largest
+    // watermark the caller has passed; the operator watermark is the min of it over ranks
+    int64_t in_wm = (int64_t)0x8000000000000000LL;
 
     std::map<long long, Table> tables;         // window / pane index -> table
     std::vector<Table> aux_tables;             // engine-private tables (sliding ring totals)

@@ -1156,7 +1156,7 @@ gwo_status Handle::log_restore_rows(const RestoreRows &R, int64_t new_wm) {
         T.mine.assign(T.n, 1);
         GWO_TRY(table_restore_rows(T, new_wm));
     }
-    wm = new_wm;
+    wm = in_wm = new_wm;
     const int RW = 1 + plan.nwords;
     for (auto &kv : rows_of) {
         const std::vector<int64_t> &ix = kv.second;

@@ -337,7 +337,7 @@ gwo_status Handle::session_restore_rows(const RestoreRows &R, int64_t new_wm) {
         per_key[R.key[i]]++;
         mine++;
     }
-    wm = new_wm;
+    wm = in_wm = new_wm;
     if (mine == 0) return GWO_OK;
     GWO_TRY(sess_ensure(per_key.size()));
     const int sw = 3 + plan.nwords;

@@ -203,7 +203,7 @@ gwo_status Handle::table_restore_rows(const RestoreRows &R, int64_t new_wm) {
                 return fail(GWO_ERR_UNSUPPORTED, "restore: window %lld has rows already emitted and rows still pending "
                                                  "(checkpoints taken at different watermarks)",
                             (long long)unit_start(kv.first));
-    wm = new_wm;   // validated: from here on the handle holds the restored state
+    wm = in_wm = new_wm;   // validated: from here on the handle holds the restored state
     if (per_unit.empty()) return slide ? slide_restore_anchor() : GWO_OK;
     for (auto &kv : per_unit) {
         GWO_TRY(ensure_table(kv.first, kv.second));   // marks windows whose end the watermark passed as fired

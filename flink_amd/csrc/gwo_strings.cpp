@@ -60,23 +60,32 @@ gwo_status Handle::intern_utf16(const uint16_t *chars, const int64_t *offsets, i
     if (cfg.key_kind != GWO_KEY_STRING) return fail(GWO_ERR_INVALID_ARGUMENT, "String keys need key_kind GWO_KEY_STRING");
     if (!dict) dict = new StrDict();
     StrDict &D = *dict;
-    // offsets on the device; the batch's code-unit range [0, offsets[n]) from wherever it is
+    // offsets on the device; every offset is validated on the host first (the claim, publish and resolve kernels
+    // read chars[offsets[i] .. offsets[i + 1]) unchecked: an interior offset past offsets[n] would read beyond the
+    // staged code units)
     int64_t first_last[2];
     const int64_t *d_off = offsets;
+    const int64_t *h_off = offsets;
+    std::vector<int64_t> off_copy;
+    if (is_device_ptr(offsets)) {
+        off_copy.resize((size_t)n + 1);
+        GWO_TRY(hipcheck(hipMemcpyAsync(off_copy.data(), offsets, (size_t)(n + 1) * 8, hipMemcpyDeviceToHost, stream),
+                         "offsets"));
+        GWO_TRY(hipcheck(hipStreamSynchronize(stream), "offsets"));
+        h_off = off_copy.data();
+    }
+    if (h_off[0] < 0) return fail(GWO_ERR_INVALID_ARGUMENT, "String key offsets must be non-negative and non-decreasing");
+    for (int64_t i = 0; i < n; ++i)
+        if (h_off[i + 1] < h_off[i])
+            return fail(GWO_ERR_INVALID_ARGUMENT, "String key offsets must be non-negative and non-decreasing");
+    first_last[0] = h_off[0];
+    first_last[1] = h_off[n];
     if (!is_device_ptr(offsets)) {
         GWO_TRY(ensure_buf(D.offsets, (size_t)(n + 1) * 8));
         GWO_TRY(hipcheck(hipMemcpyAsync(D.offsets.ptr, offsets, (size_t)(n + 1) * 8, hipMemcpyHostToDevice, stream),
                          "stage offsets"));
         d_off = (const int64_t *)D.offsets.ptr;
-        first_last[0] = offsets[0];
-        first_last[1] = offsets[n];
-    } else {
-        GWO_TRY(hipcheck(hipMemcpyAsync(&first_last[0], offsets, 8, hipMemcpyDeviceToHost, stream), "offsets"));
-        GWO_TRY(hipcheck(hipMemcpyAsync(&first_last[1], offsets + n, 8, hipMemcpyDeviceToHost, stream), "offsets"));
-        GWO_TRY(hipcheck(hipStreamSynchronize(stream), "offsets"));
     }
-    if (first_last[0] < 0 || first_last[1] < first_last[0])
-        return fail(GWO_ERR_INVALID_ARGUMENT, "String key offsets must be non-negative and non-decreasing");
     const uint64_t units = (uint64_t)first_last[1];
     const uint16_t *d_chars = chars;
     if (units > 0 && !is_device_ptr(chars)) {

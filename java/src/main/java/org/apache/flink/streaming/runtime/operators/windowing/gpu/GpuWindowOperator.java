@@ -54,6 +54,10 @@ public class GpuWindowOperator<IN, K> extends AbstractStreamOperator<GpuWindowRe
 
     private transient long handle;
     private transient ByteBuffer keys, timestamps, values, chars, offsets;
+    // drain buffers, allocated once at open() (batch rows; the side output's grow on demand)
+    private transient ByteBuffer outKeys, outStarts, outEnds, sideKeys, sideTs, sideValues;
+    private transient ByteBuffer[] outResults;
+    private transient long[] idScratch;
     private transient List<String> pendingStrings;
     private transient int n;
     private transient long lateReported;
@@ -76,8 +80,12 @@ public class GpuWindowOperator<IN, K> extends AbstractStreamOperator<GpuWindowRe
         super.initializeState(context);
         GwoNative.load();
         KeyGroupRange range = getKeyedStateBackend().getKeyGroupRange();
+        // the number of key groups of this operator: the keyed backend is created with the task's max parallelism
+        // (StreamTaskStateInitializerImpl.java:290-306), which is what getMaxNumberOfParallelSubtasks returns --
+        // per-operator setMaxParallelism and KeyGroupRangeAssignment.computeDefaultMaxParallelism included
+        final int maxParallelism = getRuntimeContext().getMaxNumberOfParallelSubtasks();
         handle = GwoNative.create(spec.assigner, spec.size, spec.slide, spec.offset, spec.gap, spec.allowedLateness,
-                spec.aggs, spec.valueDtype, spec.keyKind, spec.maxParallelism, range.getStartKeyGroup(),
+                spec.aggs, spec.valueDtype, spec.keyKind, maxParallelism, range.getStartKeyGroup(),
                 range.getEndKeyGroup(), spec.device, lateTag != null, spec.stateLayout, spec.expectedKeys);
         if (context.isRestored()) {
             restoreRows(context);
@@ -94,6 +102,14 @@ public class GpuWindowOperator<IN, K> extends AbstractStreamOperator<GpuWindowRe
             pendingStrings = new ArrayList<>(batch);
             offsets = direct((batch + 1) * 8L);
         }
+        outKeys = direct(batch * 8L);
+        outStarts = direct(batch * 8L);
+        outEnds = direct(batch * 8L);
+        outResults = new ByteBuffer[spec.aggs.length];
+        for (int a = 0; a < outResults.length; a++) {
+            outResults[a] = direct(batch * 8L);
+        }
+        idScratch = new long[batch];
         numLateRecordsDropped = metrics.counter("numLateRecordsDropped");
         resultDtypes = new int[spec.aggs.length];
         for (int a = 0; a < spec.aggs.length; a++) {
@@ -153,7 +169,7 @@ public class GpuWindowOperator<IN, K> extends AbstractStreamOperator<GpuWindowRe
             return;
         }
         if (spec.keyKind == GwoNative.KEY_STRING) {
-            int units = 0;
+            long units = 0;
             for (String s : pendingStrings) {
                 units += s.length();
             }
@@ -179,46 +195,63 @@ public class GpuWindowOperator<IN, K> extends AbstractStreamOperator<GpuWindowRe
     }
 
     // ---- results (TimestampedCollector.collect, WindowOperator.java:546-550) --------------------------------
+    // Called after advanceWatermark and before the watermark is forwarded (AbstractStreamOperator.java:566-571):
+    // gwo_sync first completes a fire that runs asynchronously (sessions, log layout), then the rows are drained
+    // in chunks of `batch` rows through the buffers allocated at open() until none is left.
     @SuppressWarnings("unchecked")
     private void emitFired() {
-        long rows = GwoNative.outputCount(handle);
-        while (rows > 0) {
+        GwoNative.sync(handle);
+        long rows;
+        while ((rows = GwoNative.outputCount(handle)) > 0) {
             final int cap = (int) Math.min(rows, batch);
-            ByteBuffer k = direct(cap * 8L), s = direct(cap * 8L), e = direct(cap * 8L);
-            ByteBuffer[] r = new ByteBuffer[spec.aggs.length];
-            for (int a = 0; a < r.length; a++) {
-                r[a] = direct(cap * 8L);
-            }
-            final int got = (int) GwoNative.drain(handle, k, s, e, r, cap);
-            final String[] names = spec.keyKind == GwoNative.KEY_STRING ? GwoNative.keyStrings(handle, k, got) : null;
+            final int got = (int) GwoNative.drain(handle, outKeys, outStarts, outEnds, outResults, cap);
+            final String[] names = spec.keyKind == GwoNative.KEY_STRING ? keyStrings(outKeys, got) : null;
             for (int i = 0; i < got; i++) {
-                Object[] res = new Object[r.length];
-                for (int a = 0; a < r.length; a++) {
-                    res[a] = resultDtypes[a] == GwoNative.DTYPE_FLOAT64 ? (Object) r[a].getDouble(i * 8)
-                            : (Object) r[a].getLong(i * 8);
+                Object[] res = new Object[outResults.length];
+                for (int a = 0; a < outResults.length; a++) {
+                    res[a] = resultDtypes[a] == GwoNative.DTYPE_FLOAT64 ? (Object) outResults[a].getDouble(i * 8)
+                            : (Object) outResults[a].getLong(i * 8);
                 }
-                K key = (K) (names != null ? names[i] : boxKey(k.getLong(i * 8)));
-                long end = e.getLong(i * 8);
-                output.collect(new StreamRecord<>(new GpuWindowResult<>(key, s.getLong(i * 8), end, res), end - 1));
+                K key = (K) (names != null ? names[i] : boxKey(outKeys.getLong(i * 8)));
+                long end = outEnds.getLong(i * 8);
+                output.collect(new StreamRecord<>(new GpuWindowResult<>(key, outStarts.getLong(i * 8), end, res),
+                        end - 1));
             }
-            rows -= got;
+            if (got == 0) {
+                throw new IllegalStateException("gwo_drain returned no rows while " + rows + " are pending");
+            }
         }
-        long side = GwoNative.sideOutputCount(handle);
-        if (side > 0 && lateTag != null) {
-            ByteBuffer k = direct(side * 8), t = direct(side * 8), v = direct(side * 8);
-            final int got = (int) GwoNative.drainSideOutput(handle, k, t, v, side);
-            final String[] names = spec.keyKind == GwoNative.KEY_STRING ? GwoNative.keyStrings(handle, k, got) : null;
+        long side;
+        while (lateTag != null && (side = GwoNative.sideOutputCount(handle)) > 0) {
+            final int cap = (int) Math.min(side, batch);
+            if (sideKeys == null) {
+                sideKeys = direct(batch * 8L);
+                sideTs = direct(batch * 8L);
+                sideValues = direct(batch * 8L);
+            }
+            final int got = (int) GwoNative.drainSideOutput(handle, sideKeys, sideTs, sideValues, cap);
+            final String[] names = spec.keyKind == GwoNative.KEY_STRING ? keyStrings(sideKeys, got) : null;
             for (int i = 0; i < got; i++) {
-                K key = (K) (names != null ? names[i] : boxKey(k.getLong(i * 8)));
-                Object value = spec.valueDtype == GwoNative.DTYPE_FLOAT64 ? (Object) v.getDouble(i * 8)
-                        : (Object) v.getLong(i * 8);
-                output.collect(lateTag, new StreamRecord<>(new GpuLateRecord<>(key, t.getLong(i * 8), value),
-                        t.getLong(i * 8)));
+                K key = (K) (names != null ? names[i] : boxKey(sideKeys.getLong(i * 8)));
+                Object value = spec.valueDtype == GwoNative.DTYPE_FLOAT64 ? (Object) sideValues.getDouble(i * 8)
+                        : (Object) sideValues.getLong(i * 8);
+                output.collect(lateTag, new StreamRecord<>(new GpuLateRecord<>(key, sideTs.getLong(i * 8), value),
+                        sideTs.getLong(i * 8)));
+            }
+            if (got == 0) {
+                throw new IllegalStateException("side output drain returned no rows while " + side + " are pending");
             }
         }
         final long late = GwoNative.lateDropped(handle);
         numLateRecordsDropped.inc(late - lateReported);
         lateReported = late;
+    }
+
+    private String[] keyStrings(ByteBuffer ids, int n) {
+        for (int i = 0; i < n; i++) {
+            idScratch[i] = ids.getLong(i * 8);
+        }
+        return GwoNative.keyStrings(handle, idScratch, n);
     }
 
     private Object boxKey(long k) {
@@ -231,11 +264,16 @@ public class GpuWindowOperator<IN, K> extends AbstractStreamOperator<GpuWindowRe
         super.snapshotState(context);
         flush();   // prepareSnapshotPreBarrier semantics: the batch is part of the state
         final long[] bound = GwoNative.snapshotRows(handle);
-        final long cap = Math.max(bound[0], 1);
         final int words = (int) bound[1];
-        ByteBuffer k = direct(cap * 8), s = direct(cap * 8), e = direct(cap * 8), w = direct(cap * 8 * words),
-                kg = direct(cap * 4), tm = direct(cap * 4);
-        final long[] got = GwoNative.snapshot(handle, k, s, e, w, kg, tm, cap);
+        final long capL = Math.max(bound[0], 1);
+        if (capL * Math.max(words, 1) > Integer.MAX_VALUE - 8) {
+            throw new IllegalStateException("GPU window state of " + bound[0] + " rows x " + words
+                    + " words exceeds one Java array; checkpoint it with more subtasks");
+        }
+        final int cap = (int) capL;
+        final long[] k = new long[cap], s = new long[cap], e = new long[cap], w = new long[cap * Math.max(words, 1)];
+        final int[] kg = new int[cap], tm = new int[cap];
+        final long[] got = GwoNative.snapshot(handle, k, s, e, w, kg, tm, words, cap);
         final int rows = (int) got[0];
         final String[] names = spec.keyKind == GwoNative.KEY_STRING ? GwoNative.keyStrings(handle, k, rows) : null;
         KeyedStateCheckpointOutputStream out = context.getRawKeyedOperatorStateOutput();
@@ -244,7 +282,7 @@ public class GpuWindowOperator<IN, K> extends AbstractStreamOperator<GpuWindowRe
         for (int group : out.getKeyGroupList()) {   // the rows arrive grouped by ascending key group
             out.startNewKeyGroup(group);
             int j = i;
-            while (j < rows && kg.getInt(j * 4) == group) {
+            while (j < rows && kg[j] == group) {
                 j++;
             }
             view.writeLong(got[1]);   // watermark
@@ -256,13 +294,13 @@ public class GpuWindowOperator<IN, K> extends AbstractStreamOperator<GpuWindowRe
                     view.writeInt(utf.length);
                     view.write(utf);
                 } else {
-                    view.writeLong(k.getLong(r * 8));
+                    view.writeLong(k[r]);
                 }
-                view.writeLong(s.getLong(r * 8));
-                view.writeLong(e.getLong(r * 8));
-                view.writeInt(tm.getInt(r * 4));
+                view.writeLong(s[r]);
+                view.writeLong(e[r]);
+                view.writeInt(tm[r]);
                 for (int x = 0; x < words; x++) {
-                    view.writeLong(w.getLong((r * words + x) * 8));
+                    view.writeLong(w[r * words + x]);
                 }
             }
             i = j;
@@ -303,10 +341,14 @@ public class GpuWindowOperator<IN, K> extends AbstractStreamOperator<GpuWindowRe
             return;   // no key group of this subtask held state
         }
         final int m = rows.size();
-        ByteBuffer k = direct(Math.max(m, 1) * 8L), s = direct(Math.max(m, 1) * 8L), e = direct(Math.max(m, 1) * 8L),
-                w = direct(Math.max(m, 1) * 8L * Math.max(words, 1)), tm = direct(Math.max(m, 1) * 4L);
+        if ((long) m * Math.max(words, 1) > Integer.MAX_VALUE - 8) {
+            throw new IllegalStateException("restored GPU window state exceeds one Java array");
+        }
+        final long[] k = new long[Math.max(m, 1)], s = new long[Math.max(m, 1)], e = new long[Math.max(m, 1)],
+                w = new long[Math.max(m, 1) * Math.max(words, 1)];
+        final int[] tm = new int[Math.max(m, 1)];
         if (spec.keyKind == GwoNative.KEY_STRING) {   // re-key by this handle's dictionary
-            int units = 0;
+            long units = 0;
             for (Object o : key) {
                 units += ((String) o).length();
             }
@@ -324,22 +366,23 @@ public class GpuWindowOperator<IN, K> extends AbstractStreamOperator<GpuWindowRe
             GwoNative.internUtf16(handle, c, off, m, k);
         } else {
             for (int r = 0; r < m; r++) {
-                k.putLong(r * 8, (Long) key.get(r));
+                k[r] = (Long) key.get(r);
             }
         }
         for (int r = 0; r < m; r++) {
             long[] row = rows.get(r);
-            s.putLong(r * 8, row[0]);
-            e.putLong(r * 8, row[1]);
-            tm.putInt(r * 4, (int) row[2]);
-            for (int x = 0; x < words; x++) {
-                w.putLong((r * words + x) * 8, row[3 + x]);
-            }
+            s[r] = row[0];
+            e[r] = row[1];
+            tm[r] = (int) row[2];
+            System.arraycopy(row, 3, w, r * words, words);
         }
         GwoNative.restore(handle, k, s, e, w, tm, words, m, watermark);
     }
 
     private static ByteBuffer direct(long bytes) {
+        if (bytes > Integer.MAX_VALUE) {   // a direct ByteBuffer holds at most 2^31 - 1 bytes
+            throw new IllegalArgumentException("direct buffer of " + bytes + " bytes");
+        }
         return ByteBuffer.allocateDirect((int) Math.max(bytes, 8)).order(ByteOrder.nativeOrder());
     }
 }

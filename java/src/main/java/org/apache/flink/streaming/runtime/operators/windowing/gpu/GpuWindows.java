@@ -41,15 +41,16 @@ public final class GpuWindows {
         }
         spec.allowedLateness = allowedLateness;
         spec.aggs = fn.aggs;
-        spec.valueDtype = GwoNative.DTYPE_INT64;
+        spec.valueDtype = fn.valueDtype;
         Class<?> keyClass = keyed.getKeyType().getTypeClass();
         spec.keyKind = keyClass == String.class ? GwoNative.KEY_STRING
                 : keyClass == Integer.class ? GwoNative.KEY_INT : GwoNative.KEY_LONG;
         if (keyClass != String.class && keyClass != Integer.class && keyClass != Long.class) {
             throw new UnsupportedOperationException("GPU keys are Long, Integer or String, not " + keyClass);
         }
-        spec.maxParallelism = keyed.getExecutionConfig().getMaxParallelism() > 0
-                ? keyed.getExecutionConfig().getMaxParallelism() : 128;
+        // the number of key groups is the subtask's: GpuWindowOperator reads it from its runtime context at
+        // initializeState (a per-operator setMaxParallelism or computeDefaultMaxParallelism included)
+        spec.maxParallelism = 0;
         spec.device = gpuIndex;
         KeySelector<IN, K> selector = keyed.getKeySelector();
         @SuppressWarnings({"unchecked", "rawtypes"})

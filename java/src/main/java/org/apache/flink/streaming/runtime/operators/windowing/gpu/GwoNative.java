@@ -59,6 +59,9 @@ final class GwoNative {
 
     static native void advanceWatermark(long handle, long watermark);
 
+    /** gwo_sync: completes a fire still running (sessions, log layout) so outputCount sees all of its rows. */
+    static native void sync(long handle);
+
     static native long outputCount(long handle);
 
     /** gwo_drain into key/start/end columns and one column per aggregate; returns the rows copied. */
@@ -81,16 +84,19 @@ final class GwoNative {
     /** gwo_snapshot_rows: {row bound, accumulator words per row}. */
     static native long[] snapshotRows(long handle);
 
-    /** gwo_snapshot; returns {rows, watermark}. */
-    static native long[] snapshot(long handle, ByteBuffer keys, ByteBuffer starts, ByteBuffer ends, ByteBuffer words,
-                                  ByteBuffer keyGroups, ByteBuffer timers, long capacity);
+    /**
+     * gwo_snapshot into heap arrays of capacity `capacity` rows (words: capacity * nWords); returns {rows,
+     * watermark}.  The shim checks every array's length.
+     */
+    static native long[] snapshot(long handle, long[] keys, long[] starts, long[] ends, long[] words, int[] keyGroups,
+                                  int[] timers, int nWords, long capacity);
 
-    static native void restore(long handle, ByteBuffer keys, ByteBuffer starts, ByteBuffer ends, ByteBuffer words,
-                               ByteBuffer timers, int nWords, long n, long watermark);
+    static native void restore(long handle, long[] keys, long[] starts, long[] ends, long[] words, int[] timers,
+                               int nWords, long n, long watermark);
 
     /** gwo_key_strings: dictionary ids of a String-keyed handle back to Strings. */
-    static native String[] keyStrings(long handle, ByteBuffer ids, long n);
+    static native String[] keyStrings(long handle, long[] ids, int n);
 
     /** gwo_intern_utf16: Strings (UTF-16 code units + offsets) to this handle's ids. */
-    static native void internUtf16(long handle, ByteBuffer chars, ByteBuffer offsets, int n, ByteBuffer idsOut);
+    static native void internUtf16(long handle, ByteBuffer chars, ByteBuffer offsets, int n, long[] idsOut);
 }

@@ -8,6 +8,7 @@
  */
 #include <jni.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include "gwo.h"
@@ -21,11 +22,41 @@ static int fail(JNIEnv *env, gwo_handle *h, gwo_status s) {
                       : (s == GWO_ERR_UNSUPPORTED || s == GWO_ERR_MERGE_LATE) ? "java/lang/UnsupportedOperationException"
                                                                                : "java/lang/RuntimeException";
     const char *msg = h ? gwo_last_error(h) : NULL;
-    (*env)->ThrowNew(env, (*env)->FindClass(env, cls), msg && *msg ? msg : gwo_status_string(s));
+    jclass c = (*env)->FindClass(env, cls);
+    if (c) (*env)->ThrowNew(env, c, msg && *msg ? msg : gwo_status_string(s));
     return 1;
 }
 
 static void *addr(JNIEnv *env, jobject buf) { return buf ? (*env)->GetDirectBufferAddress(env, buf) : NULL; }
+
+static void throw_arg(JNIEnv *env, const char *msg) {
+    jclass c = (*env)->FindClass(env, "java/lang/IllegalArgumentException");
+    if (c) (*env)->ThrowNew(env, c, msg);
+}
+
+/* A direct buffer that must hold `need` bytes: its address, or NULL with an IllegalArgumentException pending. */
+static void *sized(JNIEnv *env, jobject buf, int64_t need, const char *what) {
+    if (!buf) {
+        if (need > 0) throw_arg(env, what);
+        return NULL;
+    }
+    void *p = (*env)->GetDirectBufferAddress(env, buf);
+    jlong cap = (*env)->GetDirectBufferCapacity(env, buf);
+    if (!p || cap < 0 || (int64_t)cap < need) {
+        throw_arg(env, what);
+        return NULL;
+    }
+    return p;
+}
+
+/* A Java primitive array that must hold `need` elements. */
+static int array_ok(JNIEnv *env, jarray a, int64_t need, const char *what) {
+    if (!a || (int64_t)(*env)->GetArrayLength(env, a) < need) {
+        throw_arg(env, what);
+        return 0;
+    }
+    return 1;
+}
 
 JNIEXPORT jint JNICALL JFN(abiVersion)(JNIEnv *env, jclass c) {
     (void)env;
@@ -76,13 +107,39 @@ JNIEXPORT void JNICALL JFN(destroy)(JNIEnv *env, jclass c, jlong h) {
 
 JNIEXPORT void JNICALL JFN(submit)(JNIEnv *env, jclass c, jlong h, jobject k, jobject t, jobject v, jint n) {
     (void)c;
-    fail(env, H(h), gwo_submit(H(h), addr(env, k), addr(env, t), addr(env, v), n));
+    if (n < 0) { throw_arg(env, "negative record count"); return; }
+    void *pk = sized(env, k, 8LL * n, "keys buffer smaller than n records");
+    if ((*env)->ExceptionCheck(env)) return;
+    void *pt = sized(env, t, 8LL * n, "timestamps buffer smaller than n records");
+    if ((*env)->ExceptionCheck(env)) return;
+    void *pv = v ? sized(env, v, 8LL * n, "values buffer smaller than n records") : NULL;
+    if ((*env)->ExceptionCheck(env)) return;
+    fail(env, H(h), gwo_submit(H(h), pk, pt, pv, n));
 }
 
 JNIEXPORT void JNICALL JFN(submitUtf16)(JNIEnv *env, jclass c, jlong h, jobject chars, jobject offsets, jobject t,
                                         jobject v, jint n) {
     (void)c;
-    fail(env, H(h), gwo_submit_utf16(H(h), addr(env, chars), addr(env, offsets), addr(env, t), addr(env, v), n));
+    if (n < 0) { throw_arg(env, "negative record count"); return; }
+    const int64_t *off = sized(env, offsets, 8LL * (n + 1), "offsets buffer smaller than n + 1 entries");
+    if ((*env)->ExceptionCheck(env)) return;
+    if (off[0] != 0) { throw_arg(env, "offsets[0] must be 0"); return; }
+    for (jint i = 0; i < n; ++i)
+        if (off[i + 1] < off[i]) { throw_arg(env, "decreasing offsets"); return; }
+    void *pc = sized(env, chars, 2 * off[n], "chars buffer smaller than offsets[n] code units");
+    if ((*env)->ExceptionCheck(env)) return;
+    void *pt = sized(env, t, 8LL * n, "timestamps buffer smaller than n records");
+    if ((*env)->ExceptionCheck(env)) return;
+    void *pv = v ? sized(env, v, 8LL * n, "values buffer smaller than n records") : NULL;
+    if ((*env)->ExceptionCheck(env)) return;
+    fail(env, H(h), gwo_submit_utf16(H(h), pc, off, pt, pv, n));
+}
+
+/* gwo_sync: waits for a fire still running (sessions and the log layout fire asynchronously), so that
+ * outputCount afterwards counts every row of the watermark just applied. */
+JNIEXPORT void JNICALL JFN(sync)(JNIEnv *env, jclass c, jlong h) {
+    (void)c;
+    fail(env, H(h), gwo_sync(H(h)));
 }
 
 JNIEXPORT void JNICALL JFN(advanceWatermark)(JNIEnv *env, jclass c, jlong h, jlong wm) {
@@ -100,13 +157,22 @@ JNIEXPORT jlong JNICALL JFN(outputCount)(JNIEnv *env, jclass c, jlong h) {
 JNIEXPORT jlong JNICALL JFN(drain)(JNIEnv *env, jclass c, jlong h, jobject k, jobject s, jobject e,
                                    jobjectArray results, jlong cap) {
     (void)c;
+    if (cap < 0) {
+        throw_arg(env, "negative capacity");
+        return 0;
+    }
     gwo_out o;
     memset(&o, 0, sizeof o);
-    o.key = addr(env, k);
-    o.start = addr(env, s);
-    o.end = addr(env, e);
+    o.key = sized(env, k, 8 * cap, "keys buffer smaller than capacity");
+    if (!(*env)->ExceptionCheck(env)) o.start = sized(env, s, 8 * cap, "starts buffer smaller than capacity");
+    if (!(*env)->ExceptionCheck(env)) o.end = sized(env, e, 8 * cap, "ends buffer smaller than capacity");
     jsize nr = results ? (*env)->GetArrayLength(env, results) : 0;
-    for (jsize i = 0; i < nr && i < GWO_MAX_AGGS; ++i) o.result[i] = addr(env, (*env)->GetObjectArrayElement(env, results, i));
+    for (jsize i = 0; i < nr && i < GWO_MAX_AGGS && !(*env)->ExceptionCheck(env); ++i) {
+        jobject b = (*env)->GetObjectArrayElement(env, results, i);
+        o.result[i] = sized(env, b, 8 * cap, "result buffer smaller than capacity");
+        (*env)->DeleteLocalRef(env, b);
+    }
+    if ((*env)->ExceptionCheck(env)) return 0;
     int64_t got = 0;
     fail(env, H(h), gwo_drain(H(h), &o, cap, &got));
     return got;
@@ -136,10 +202,15 @@ JNIEXPORT jlong JNICALL JFN(sideOutputCount)(JNIEnv *env, jclass c, jlong h) {
 JNIEXPORT jlong JNICALL JFN(drainSideOutput)(JNIEnv *env, jclass c, jlong h, jobject k, jobject t, jobject v,
                                              jlong cap) {
     (void)c;
+    if (cap < 0) {
+        throw_arg(env, "negative capacity");
+        return 0;
+    }
     gwo_side_out o;
-    o.key = addr(env, k);
-    o.ts = addr(env, t);
-    o.value = addr(env, v);
+    o.key = sized(env, k, 8 * cap, "keys buffer smaller than capacity");
+    o.ts = (*env)->ExceptionCheck(env) ? NULL : sized(env, t, 8 * cap, "timestamps buffer smaller than capacity");
+    o.value = (*env)->ExceptionCheck(env) ? NULL : sized(env, v, 8 * cap, "values buffer smaller than capacity");
+    if ((*env)->ExceptionCheck(env)) return 0;
     int64_t got = 0;
     fail(env, H(h), gwo_drain_side_output(H(h), &o, cap, &got));
     return got;
@@ -170,51 +241,124 @@ JNIEXPORT jlongArray JNICALL JFN(snapshotRows)(JNIEnv *env, jclass c, jlong h) {
     return r;
 }
 
-JNIEXPORT jlongArray JNICALL JFN(snapshot)(JNIEnv *env, jclass c, jlong h, jobject k, jobject s, jobject e,
-                                           jobject w, jobject kg, jobject tm, jlong cap) {
+/* gwo_snapshot into Java arrays (heap memory, as the heap backend's own snapshot is): capacity `cap` rows; words
+ * holds cap * n_words longs.  Returns {rows, watermark}. */
+JNIEXPORT jlongArray JNICALL JFN(snapshot)(JNIEnv *env, jclass c, jlong h, jlongArray k, jlongArray s, jlongArray e,
+                                           jlongArray w, jintArray kg, jintArray tm, jint nw, jlong cap) {
     (void)c;
-    gwo_state_rows rows = {addr(env, k), addr(env, s), addr(env, e), addr(env, w), addr(env, kg), addr(env, tm)};
-    int64_t n = 0, wm = 0;
-    if (fail(env, H(h), gwo_snapshot(H(h), &rows, cap, &n, &wm))) return NULL;
-    jlongArray r = (*env)->NewLongArray(env, 2);
-    jlong v[2] = {n, wm};
-    (*env)->SetLongArrayRegion(env, r, 0, 2, v);
+    if (cap < 0 || nw < 0) {
+        throw_arg(env, "negative capacity");
+        return NULL;
+    }
+    if (!array_ok(env, k, cap, "keys array smaller than capacity") || !array_ok(env, s, cap, "starts array") ||
+        !array_ok(env, e, cap, "ends array") || !array_ok(env, w, cap * nw, "words array smaller than cap * n_words") ||
+        !array_ok(env, kg, cap, "key groups array") || !array_ok(env, tm, cap, "timers array"))
+        return NULL;
+    jlong *pk = (*env)->GetLongArrayElements(env, k, NULL), *ps = (*env)->GetLongArrayElements(env, s, NULL),
+          *pe = (*env)->GetLongArrayElements(env, e, NULL), *pw = (*env)->GetLongArrayElements(env, w, NULL);
+    jint *pg = (*env)->GetIntArrayElements(env, kg, NULL), *pt = (*env)->GetIntArrayElements(env, tm, NULL);
+    jlongArray r = NULL;
+    if (pk && ps && pe && pw && pg && pt) {
+        gwo_state_rows rows = {(int64_t *)pk, (int64_t *)ps, (int64_t *)pe, (int64_t *)pw, (int32_t *)pg, (int32_t *)pt};
+        int64_t n = 0, wm = 0;
+        if (!fail(env, H(h), gwo_snapshot(H(h), &rows, cap, &n, &wm))) {
+            r = (*env)->NewLongArray(env, 2);
+            jlong v[2] = {n, wm};
+            if (r) (*env)->SetLongArrayRegion(env, r, 0, 2, v);
+        }
+    }
+    const jint mode = r ? 0 : JNI_ABORT;
+    if (pk) (*env)->ReleaseLongArrayElements(env, k, pk, mode);
+    if (ps) (*env)->ReleaseLongArrayElements(env, s, ps, mode);
+    if (pe) (*env)->ReleaseLongArrayElements(env, e, pe, mode);
+    if (pw) (*env)->ReleaseLongArrayElements(env, w, pw, mode);
+    if (pg) (*env)->ReleaseIntArrayElements(env, kg, pg, mode);
+    if (pt) (*env)->ReleaseIntArrayElements(env, tm, pt, mode);
     return r;
 }
 
-JNIEXPORT void JNICALL JFN(restore)(JNIEnv *env, jclass c, jlong h, jobject k, jobject s, jobject e, jobject w,
-                                    jobject tm, jint nw, jlong n, jlong wm) {
+JNIEXPORT void JNICALL JFN(restore)(JNIEnv *env, jclass c, jlong h, jlongArray k, jlongArray s, jlongArray e,
+                                    jlongArray w, jintArray tm, jint nw, jlong n, jlong wm) {
     (void)c;
-    gwo_state_rows rows = {addr(env, k), addr(env, s), addr(env, e), addr(env, w), NULL, addr(env, tm)};
-    fail(env, H(h), gwo_restore(H(h), &rows, nw, n, wm));
+    if (n < 0 || nw < 0) { throw_arg(env, "negative row count"); return; }
+    if (!array_ok(env, k, n, "keys array smaller than n") || !array_ok(env, s, n, "starts array") ||
+        !array_ok(env, e, n, "ends array") || !array_ok(env, w, n * nw, "words array smaller than n * n_words") ||
+        !array_ok(env, tm, n, "timers array"))
+        return;
+    jlong *pk = (*env)->GetLongArrayElements(env, k, NULL), *ps = (*env)->GetLongArrayElements(env, s, NULL),
+          *pe = (*env)->GetLongArrayElements(env, e, NULL), *pw = (*env)->GetLongArrayElements(env, w, NULL);
+    jint *pt = (*env)->GetIntArrayElements(env, tm, NULL);
+    if (pk && ps && pe && pw && pt) {
+        gwo_state_rows rows = {(int64_t *)pk, (int64_t *)ps, (int64_t *)pe, (int64_t *)pw, NULL, (int32_t *)pt};
+        fail(env, H(h), gwo_restore(H(h), &rows, nw, n, wm));
+    }
+    if (pk) (*env)->ReleaseLongArrayElements(env, k, pk, JNI_ABORT);
+    if (ps) (*env)->ReleaseLongArrayElements(env, s, ps, JNI_ABORT);
+    if (pe) (*env)->ReleaseLongArrayElements(env, e, pe, JNI_ABORT);
+    if (pw) (*env)->ReleaseLongArrayElements(env, w, pw, JNI_ABORT);
+    if (pt) (*env)->ReleaseIntArrayElements(env, tm, pt, JNI_ABORT);
 }
 
-JNIEXPORT jobjectArray JNICALL JFN(keyStrings)(JNIEnv *env, jclass c, jlong h, jobject ids, jlong n) {
+/* Ids of a String-keyed handle (a Java long[]) back to Strings. */
+JNIEXPORT jobjectArray JNICALL JFN(keyStrings)(JNIEnv *env, jclass c, jlong h, jlongArray ids, jint n) {
     (void)c;
-    int64_t need = 0;
-    int64_t *off = (int64_t *)(*env)->GetDirectBufferAddress(env, ids);   /* reused below only for the ids */
-    jlongArray offs = (*env)->NewLongArray(env, (jsize)(n + 1));
-    jlong *o = (*env)->GetLongArrayElements(env, offs, NULL);
-    if (fail(env, H(h), gwo_key_strings(H(h), off, n, (int64_t *)o, NULL, 0, &need))) {
-        (*env)->ReleaseLongArrayElements(env, offs, o, JNI_ABORT);
-        return NULL;
-    }
-    jcharArray chars = (*env)->NewCharArray(env, (jsize)(need > 0 ? need : 1));
-    jchar *u = (*env)->GetCharArrayElements(env, chars, NULL);
-    gwo_status st = gwo_key_strings(H(h), off, n, (int64_t *)o, (uint16_t *)u, need, &need);
+    if (n < 0 || !array_ok(env, ids, n, "ids array smaller than n")) return NULL;
+    jclass str = (*env)->FindClass(env, "java/lang/String");
+    if (!str) return NULL;
+    jlong *id = (*env)->GetLongArrayElements(env, ids, NULL);
+    int64_t *off = (int64_t *)malloc(((size_t)n + 1) * sizeof(int64_t));
     jobjectArray out = NULL;
-    if (!fail(env, H(h), st)) {
-        out = (*env)->NewObjectArray(env, (jsize)n, (*env)->FindClass(env, "java/lang/String"), NULL);
-        for (jsize i = 0; i < (jsize)n; ++i)
-            (*env)->SetObjectArrayElement(env, out, i, (*env)->NewString(env, u + o[i], (jsize)(o[i + 1] - o[i])));
+    uint16_t *u = NULL;
+    int64_t need = 0;
+    if (!id || !off) {
+        throw_arg(env, "out of memory");
+        goto done;
     }
-    (*env)->ReleaseCharArrayElements(env, chars, u, JNI_ABORT);
-    (*env)->ReleaseLongArrayElements(env, offs, o, JNI_ABORT);
+    if (fail(env, H(h), gwo_key_strings(H(h), (const int64_t *)id, n, off, NULL, 0, &need))) goto done;
+    u = (uint16_t *)malloc((size_t)(need > 0 ? need : 1) * 2);
+    if (!u) {
+        throw_arg(env, "out of memory");
+        goto done;
+    }
+    if (fail(env, H(h), gwo_key_strings(H(h), (const int64_t *)id, n, off, u, need, &need))) goto done;
+    out = (*env)->NewObjectArray(env, n, str, NULL);
+    for (jint i = 0; out && i < n; ++i) {
+        const int64_t len = off[i + 1] - off[i];
+        if (len > INT32_MAX) {
+            throw_arg(env, "String longer than 2^31 code units");
+            out = NULL;
+            break;
+        }
+        jstring js = (*env)->NewString(env, (const jchar *)(u + off[i]), (jsize)len);
+        if (!js) {
+            out = NULL;
+            break;
+        }
+        (*env)->SetObjectArrayElement(env, out, i, js);
+        (*env)->DeleteLocalRef(env, js);   /* n may exceed the 16 local references JNI guarantees */
+    }
+done:
+    free(u);
+    free(off);
+    if (id) (*env)->ReleaseLongArrayElements(env, ids, id, JNI_ABORT);
+    (*env)->DeleteLocalRef(env, str);
     return out;
 }
 
 JNIEXPORT void JNICALL JFN(internUtf16)(JNIEnv *env, jclass c, jlong h, jobject chars, jobject offsets, jint n,
-                                        jobject ids) {
+                                        jlongArray ids) {
     (void)c;
-    fail(env, H(h), gwo_intern_utf16(H(h), addr(env, chars), addr(env, offsets), n, addr(env, ids)));
+    if (n < 0) { throw_arg(env, "negative count"); return; }
+    const int64_t *off = sized(env, offsets, 8LL * (n + 1), "offsets buffer smaller than n + 1 entries");
+    if ((*env)->ExceptionCheck(env)) return;
+    if (off[0] != 0) { throw_arg(env, "offsets[0] must be 0"); return; }
+    for (jint i = 0; i < n; ++i)
+        if (off[i + 1] < off[i]) { throw_arg(env, "decreasing offsets"); return; }
+    void *pc = sized(env, chars, 2 * off[n], "chars buffer smaller than offsets[n] code units");
+    if ((*env)->ExceptionCheck(env)) return;
+    if (!array_ok(env, ids, n, "ids array smaller than n")) return;
+    jlong *pi = (*env)->GetLongArrayElements(env, ids, NULL);
+    if (!pi) return;
+    const int bad = fail(env, H(h), gwo_intern_utf16(H(h), pc, off, n, (int64_t *)pi));
+    (*env)->ReleaseLongArrayElements(env, ids, pi, bad ? JNI_ABORT : 0);
 }

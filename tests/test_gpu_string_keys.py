@@ -177,3 +177,23 @@ def test_string_dictionary_growth(F):
     h, _, _ = F.assign_key_groups_strings(keys[:1000], 128)
     assert ((ids >> 32).astype(np.int32) == h).all()   # the id's high half is String.hashCode
     op.close()
+
+
+def test_string_offsets_validated_before_any_kernel(F):
+    """Interior offsets are checked on the host: one past offsets[n] or a decreasing pair is
+    GWO_ERR_INVALID_ARGUMENT (no kernel reads beyond the staged code units), and the handle stays usable."""
+    import ctypes as C
+    from flink_amd import _native as N
+    lib = N.lib()
+    op = F.GpuWindowOperator(F.TumblingEventTimeWindows.of(1000), F.CountAggregate(), key_kind="string")
+    chars = np.frombuffer("abcdef".encode("utf-16-le"), np.uint16).copy()
+    ts = np.array([1, 2, 3], np.int64)
+    p = lambda a: a.ctypes.data_as(C.c_void_p)
+    for bad in ([0, 5, 2, 6], [0, 9, 9, 6], [0, 3, 1, 6]):
+        off = np.array(bad, np.int64)
+        st = lib.gwo_submit_utf16(op.handle, p(chars), p(off), p(ts), None, 3)
+        assert N.STATUS_NAMES[st] == "GWO_ERR_INVALID_ARGUMENT", bad
+    op.process_batch(["ab", "cd", "ab"], [1, 2, 3])
+    op.end_input()
+    assert sorted(op.output) == [("ab", 0, 1000, 2), ("cd", 0, 1000, 1)]
+    op.close()

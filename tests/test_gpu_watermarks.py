@@ -1,0 +1,179 @@
+"""Watermark agreement on the GPU: the operator watermark follows StatusWatermarkValve
+(flink-streaming-java/.../runtime/streamstatus/StatusWatermarkValve.java:86-101,163-181) -- a channel
+watermark that does not increase is ignored and windows fire only when the min over channels grows --
+and the multi-GPU min over ranks runs through RCCL even on one GPU (1-rank communicator rehearsing
+P virtual ranks: the count exchange and the ncclMin all-reduce a real rank issues).
+
+Expected outputs come from the oracle run on the same stream with the watermarks made monotone
+(running max), which is what the valve forwards.  Integer aggregates: bit-exact.
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+from oracle import flink_oracle as O
+from oracle import gen as G
+from oracle import vectorized as V
+
+pytestmark = pytest.mark.gpu
+
+LONG_MAX = (1 << 63) - 1
+
+
+@pytest.fixture(scope="module")
+def F():
+    import flink_amd
+    from flink_amd import _native
+    _native.lib()
+    return flink_amd
+
+
+def _stream(n=120_000, nkeys=5_000, every=4_000, lag=500, seed=3, disorder=900):
+    spec = G.GenSpec(seed=seed, total_records=n, num_keys=nkeys, span_ms=60_000, disorder_ms=disorder,
+                     value_range=1000)
+    k, t, v = G.generate(spec, n)
+    return k, t, v, G.punctuated_watermarks(t, every, lag)
+
+
+def _regress(batches, rng):
+    """Every third watermark moves back by up to 3 s (a channel reporting an older watermark)."""
+    out = []
+    for i, (end, wm) in enumerate(batches):
+        out.append((end, wm - int(rng.integers(1, 3_000)) if i % 3 == 2 else wm))
+    return out
+
+
+def _monotone(batches):
+    out, run = [], -(1 << 63)
+    for end, wm in batches:
+        run = max(run, wm)
+        out.append((end, run))
+    return out
+
+
+def _drive(op, k, t, v, batches):
+    prev, seen = 0, []
+    for end, wm in batches:
+        op.process_batch(k[prev:end], t[prev:end], v[prev:end])
+        op.process_watermark(wm)
+        seen.append(op.current_watermark)
+        prev = end
+    op.end_input()
+    return seen
+
+
+@pytest.mark.parametrize("layout", ["table", "log"])
+def test_regressing_watermark_ignored_tumbling(F, layout):
+    rng = np.random.default_rng(1)
+    k, t, v, b = _stream()
+    bad = _regress(b, rng)
+    good = _monotone(bad)
+    op = F.GpuWindowOperator(F.TumblingEventTimeWindows.of(5000),
+                             F.MultiAggregate(F.SumAggregate(), F.MinAggregate(), F.MaxAggregate()), state_layout=layout)
+    seen = _drive(op, k, t, v, bad)
+    assert seen == [w for _, w in good]          # the operator watermark never moves back
+    (wk, ws, we, res), late = V.tumbling_lateness0(k, t, v, good + [(len(k), LONG_MAX)], 5000, 0, [1, 2, 3])
+    want = sorted(zip(wk.tolist(), ws.tolist(), we.tolist(), *[r.tolist() for r in res]))
+    assert sorted((a, s, e, *r) for a, s, e, r in op.output) == want
+    assert op.num_late_records_dropped == late
+    op.close()
+
+
+def test_regressing_watermark_ignored_sliding(F):
+    rng = np.random.default_rng(2)
+    k, t, v, b = _stream(seed=5)
+    bad = _regress(b, rng)
+    good = _monotone(bad)
+    op = F.GpuWindowOperator(F.SlidingEventTimeWindows.of(3000, 1000), F.AverageAggregate())
+    _drive(op, k, t, v, bad)
+    (wk, ws, we, res), late = V.sliding_lateness0(k, t, v, good + [(len(k), LONG_MAX)], 3000, 1000, 0, [4])
+    assert sorted(op.output) == sorted(zip(wk.tolist(), ws.tolist(), we.tolist(), res[0].tolist()))
+    assert op.num_late_records_dropped == late
+    op.close()
+
+
+@pytest.mark.parametrize("lateness", [0, 2_000])
+def test_regressing_watermark_ignored_sessions(F, lateness):
+    rng = np.random.default_rng(3 + lateness)
+    n = 15_000
+    k = rng.integers(0, 200, n)
+    t = np.sort(rng.integers(0, 300_000, n)) + rng.integers(0, 5_000, n)
+    v = rng.integers(0, 100, n)
+    bad = _regress(G.punctuated_watermarks(t, 500, 1_000), rng)
+    good = _monotone(bad)
+    ref = O.WindowOperatorOracle(O.EventTimeSessionWindows(2_000), O.SumLongAgg(), lateness)
+    prev = 0
+    for end, wm in good:
+        for i in range(prev, end):
+            ref.process_element(int(k[i]), int(t[i]), int(v[i]))
+        ref.process_watermark(wm)
+        prev = end
+    ref.process_watermark(LONG_MAX)
+    op = F.GpuWindowOperator(F.EventTimeSessionWindows.withGap(2_000), F.SumAggregate(), allowed_lateness=lateness)
+    _drive(op, k, t, v, bad)
+    assert sorted(op.output) == sorted((r.key, r.start, r.end, r.result) for r in ref.output)
+    assert op.num_late_records_dropped == ref.num_late_records_dropped
+    op.close()
+
+
+def _virtual(F, op, monkeypatch, P):
+    from flink_amd import _native as N
+    lib = N.lib()
+    uid = (C.c_uint8 * N.COMM_ID_BYTES)()
+    N.check(lib.gwo_comm_unique_id(uid))
+    monkeypatch.setenv("GWO_COMM_VIRTUAL", str(P))
+    N.check(lib.gwo_comm_init(op.handle, uid, 1, 0), op.handle, "gwo_comm_init")
+    monkeypatch.delenv("GWO_COMM_VIRTUAL")
+
+
+def test_virtual_ranks_regressing_watermark(F, monkeypatch):
+    """8 virtual ranks: every watermark goes through the ncclMin all-reduce, every batch through the RCCL count
+    exchange; regressions are still ignored."""
+    rng = np.random.default_rng(9)
+    k, t, v, b = _stream(n=200_000, nkeys=20_000, every=20_000, lag=1000)
+    bad = _regress(b, rng)
+    good = _monotone(bad)
+    op = F.GpuWindowOperator(F.TumblingEventTimeWindows.of(5000),
+                             F.MultiAggregate(F.SumAggregate(), F.MinAggregate(), F.MaxAggregate()), state_layout="log",
+                             max_parallelism=32768)
+    _virtual(F, op, monkeypatch, 8)
+    seen = _drive(op, k, t, v, bad)
+    assert seen == [w for _, w in good]
+    (wk, ws, we, res), late = V.tumbling_lateness0(k, t, v, good + [(len(k), LONG_MAX)], 5000, 0, [1, 2, 3])
+    want = sorted(zip(wk.tolist(), ws.tolist(), we.tolist(), *[r.tolist() for r in res]))
+    assert sorted((a, s, e, *r) for a, s, e, r in op.output) == want
+    assert op.num_late_records_dropped == late
+    op.close()
+
+
+def test_virtual_ranks_after_restore(F, monkeypatch):
+    """A subtask restored at watermark W (far from 0) attaches a communicator of 8 virtual ranks: the ranks agree
+    on the wire records' timestamp base at gwo_comm_init (all-reduce of the restored watermarks), so the routed
+    batches after the restore travel as 20-B records relative to W and decode to the same windows."""
+    k, t, v, b = _stream(n=200_000, nkeys=20_000, every=10_000, lag=1000, seed=11)
+    t = t + (1 << 40)
+    b = G.punctuated_watermarks(t, 10_000, 1000)
+    mk = lambda: F.GpuWindowOperator(F.TumblingEventTimeWindows.of(5000),
+                                     F.MultiAggregate(F.SumAggregate(), F.CountAggregate()), state_layout="log",
+                                     max_parallelism=32768)
+    half = len(b) // 2
+    a = mk()
+    prev = 0
+    for end, wm in b[:half]:
+        a.process_batch(k[prev:end], t[prev:end], v[prev:end])
+        a.process_watermark(wm)
+        prev = end
+    snap = a.snapshot_state()
+    rows, late = list(a.output), a.num_late_records_dropped
+    a.close()
+    c = mk()
+    c.restore_state(snap)
+    assert c.current_watermark == b[half - 1][1] > (1 << 40)
+    _virtual(F, c, monkeypatch, 8)
+    _drive(c, k[prev:], t[prev:], v[prev:], [(e - prev, w) for e, w in b[half:]])
+    (wk, ws, we, res), want_late = V.tumbling_lateness0(k, t, v, b + [(len(k), LONG_MAX)], 5000, 0, [1, 0])
+    want = sorted(zip(wk.tolist(), ws.tolist(), we.tolist(), *[r.tolist() for r in res]))
+    assert sorted((a_, s, e, *r) for a_, s, e, r in rows + list(c.output)) == want
+    assert late + c.num_late_records_dropped == want_late
+    c.close()

@@ -61,3 +61,32 @@ def test_jni_mangled_class_matches_package():
     src = _read("jni", "gwo_jni.c")
     pkg = re.search(r"^package ([\w.]+);", open(os.path.join(PKG, "GwoNative.java")).read(), re.M).group(1)
     assert "Java_" + pkg.replace(".", "_") + "_GwoNative_##name" in src
+
+
+def test_jni_shim_compiles_against_the_jni_calls_it_makes():
+    """gcc -fsyntax-only over jni/gwo_jni.c with tests/jni_stub/jni.h (the JNIEnv functions the shim uses, JDK
+    signatures): catches type and arity errors in code that cannot be built here."""
+    import shutil
+    import subprocess
+    import pytest
+    if not shutil.which("gcc"):
+        pytest.skip("no gcc")
+    r = subprocess.run(["gcc", "-fsyntax-only", "-Wall", "-Wextra", "-Werror", "-std=c11",
+                        "-I" + os.path.join(ROOT, "tests", "jni_stub"), "-I" + os.path.join(ROOT, "include"),
+                        os.path.join(ROOT, "jni", "gwo_jni.c")], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+
+
+def test_operator_emits_after_sync_and_reads_max_parallelism_from_the_task():
+    """GpuWindowOperator: emitFired completes a running fire (gwo_sync) before counting rows and drains into buffers
+    allocated once; the number of key groups is the task's (getMaxNumberOfParallelSubtasks), not ExecutionConfig's;
+    the value dtype comes from the aggregate descriptor."""
+    op = open(os.path.join(PKG, "GpuWindowOperator.java")).read()
+    body = op[op.index("private void emitFired()"):op.index("private String[] keyStrings(")]
+    assert body.index("GwoNative.sync(handle)") < body.index("GwoNative.outputCount(handle)")
+    assert "direct(" not in body.replace("sideKeys = direct(", "").replace("sideTs = direct(", "") \
+        .replace("sideValues = direct(", "")
+    assert "getRuntimeContext().getMaxNumberOfParallelSubtasks()" in op
+    assert "spec.maxParallelism" not in op
+    win = open(os.path.join(PKG, "GpuWindows.java")).read()
+    assert "spec.valueDtype = fn.valueDtype" in win and "getExecutionConfig().getMaxParallelism" not in win
