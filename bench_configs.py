@@ -80,7 +80,7 @@ def run(cfg):
         n, nkeys, span = 200_000_000, 10_000_000, 120_000
         every = n * 1000 // span
         key, ts, val = gen_device(N, lib, dev, torch, n, nkeys, span, 1000)
-        assigner, agg, exp = F.SlidingEventTimeWindows.of(60_000, 1000), F.AverageAggregate(), 0
+        assigner, agg, exp = F.SlidingEventTimeWindows.of(60_000, 1000), F.AverageAggregate(), nkeys
         I_B, S_B, O_B, workload = 24, 32, 32, "C3 sliding 60 s / 1 s avg, 10M keys, 200M records"
     elif cfg == "c5":
         lag = 5000

@@ -5,6 +5,7 @@
 #include <numeric>
 
 #include "gwo_handle.h"
+#include "gwo_slide.h"
 #include "gwo_log.h"
 
 namespace gwo {
@@ -163,12 +164,22 @@ gwo_status Handle::init(const gwo_config &c) {
     if (c.assigner == GWO_ASSIGNER_SESSION) GWO_TRY(session_init());
     if (c.state_layout < GWO_STATE_AUTO || c.state_layout > GWO_STATE_LOG)
         return fail(GWO_ERR_INVALID_ARGUMENT, "state layout %d", c.state_layout);
-    if (c.state_layout == GWO_STATE_LOG && c.assigner != GWO_ASSIGNER_TUMBLING)
-        return fail(GWO_ERR_UNSUPPORTED, "the log-structured state layout serves tumbling windows only");
-    if (c.assigner == GWO_ASSIGNER_TUMBLING &&
-        (c.state_layout == GWO_STATE_LOG ||
-         (c.state_layout == GWO_STATE_AUTO && c.expected_keys >= (1 << 20) && c.allowed_lateness == 0)))
+    // sliding windows over logged panes: every aggregate word an int64 sum (the ring), allowedLateness 0, and
+    // the slide divides the size (a pane is one slide)
+    const bool slog_ok = c.assigner == GWO_ASSIGNER_SLIDING && slide && slide->ring && c.allowed_lateness == 0 &&
+                         c.size % c.slide == 0 && getenv("GWO_SLIDE_TABLE") == nullptr;
+    if (c.state_layout == GWO_STATE_LOG && c.assigner == GWO_ASSIGNER_SESSION)
+        return fail(GWO_ERR_UNSUPPORTED, "the log-structured state layout serves tumbling and sliding windows only");
+    if (c.state_layout == GWO_STATE_LOG && c.assigner == GWO_ASSIGNER_SLIDING && !slog_ok)
+        return fail(GWO_ERR_UNSUPPORTED, "the log-structured sliding layout needs int64 count/sum/avg aggregates, "
+                                         "allowedLateness 0 and a size that is a multiple of the slide");
+    const bool big = c.state_layout == GWO_STATE_LOG ||
+                     (c.state_layout == GWO_STATE_AUTO && c.expected_keys >= (1 << 20) && c.allowed_lateness == 0);
+    if (c.assigner == GWO_ASSIGNER_TUMBLING && big) GWO_TRY(log_init());
+    if (c.assigner == GWO_ASSIGNER_SLIDING && big && slog_ok) {
+        GWO_TRY(slog_init());   // (before log_init: the log's lp choice and warm-up see the sliding log)
         GWO_TRY(log_init());
+    }
     memset(h_ident_side, 0, GWO_MAX_WORDS * 16 + 16);
     for (int w = 0; w < plan.nwords; ++w) h_ident_side[1 + w] = plan.ident[w];
     return hipcheck(hipStreamSynchronize(stream), "init");
@@ -182,6 +193,7 @@ Handle::~Handle() {
     for (hipEvent_t e : event_pool) (void)hipEventDestroy(e);
     comm_free();
     log_free();
+    slog_free();
     session_free();
     slide_free();
     dict_free();
@@ -279,7 +291,7 @@ gwo_status Handle::advance_watermark(int64_t new_wm) {
     gwo_status s = GWO_OK;
     switch (cfg.assigner) {
         case GWO_ASSIGNER_TUMBLING: s = logst ? fire_log(new_wm) : fire_tumbling(new_wm); break;
-        case GWO_ASSIGNER_SLIDING: s = fire_sliding(new_wm); break;
+        case GWO_ASSIGNER_SLIDING: s = slog ? fire_slog(new_wm) : fire_sliding(new_wm); break;
         default: s = fire_session(new_wm); break;
     }
     wm = new_wm;

@@ -85,6 +85,7 @@ struct LogState;       // gwo_log.cpp
 struct LogWindow;
 struct LogJob;
 struct StrDict;        // gwo_strings.cpp
+struct SlogState;      // gwo_slog.cpp
 
 struct Handle {
     static constexpr double kMaxLoad = 0.7;   // grow above this load factor
@@ -183,6 +184,8 @@ struct Handle {
     Comm *comm = nullptr;
     LogState *logst = nullptr;                 // non-null: log-structured tumbling state
     StrDict *dict = nullptr;                   // String keys: the key dictionary (gwo_strings.cpp)
+    SlogState *slog = nullptr;                 // non-null (with logst): sliding windows over logged panes
+    size_t log_chunk_min = 0;                  // sliding log: every pane chunk has this size (pool reuse)
 
     ~Handle();
     gwo_status init(const gwo_config &c);
@@ -315,6 +318,18 @@ struct Handle {
     gwo_status log_snapshot_collect(const SnapCols &c);
     gwo_status log_restore_rows(const RestoreRows &R, int64_t new_wm);
     size_t log_window_count() const;
+    int64_t log_usize() const;                 // the log's unit: the tumbling window, or the sliding pane
+    int64_t log_lateness() const;              // cleanup distance past a unit's end: allowedLateness, or size - slide
+    WindowGeom log_geom_now() const;           // K1's geometry (sliding panes: tumbling windows of `slide`)
+    // sliding windows over logged panes (gwo_slog.cpp)
+    gwo_status slog_init();
+    int slog_lp() const;
+    void slog_free();
+    gwo_status slog_reserve(int64_t n);
+    gwo_status slog_anchor();
+    gwo_status slog_late_pass(const LogJob &J0);
+    void slog_release_before(long long first_pane);
+    gwo_status fire_slog(int64_t new_wm);
     // comm (gwo_comm.cpp)
     void comm_free();
     gwo_status comm_exchange(const int64_t *k, const int64_t *t, const int64_t *v, int64_t n, const int64_t **aos,

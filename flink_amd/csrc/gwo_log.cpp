@@ -13,110 +13,9 @@
 
 #include "gwo_handle.h"
 #include "gwo_log.h"
+#include "gwo_log_state.h"
 
 namespace gwo {
-
-struct LogChunk {
-    char *base = nullptr;
-    size_t size = 0;
-    size_t used = 0;
-};
-
-struct LogWindow {
-    int lp = 0;
-    std::vector<LogSegDesc> segs;
-    std::vector<LogChunk> chunks;
-    uint64_t records = 0;
-    LogSegDesc partial{};        // restored checkpoint accumulators (rec == nullptr: none), folded at the fire
-    uint64_t partial_rows = 0;
-};
-
-// One K1 launch over a window range of a batch (re-launched with a new range or capacity as needed).
-struct LogJob {
-    bool active = false;
-    const int64_t *k = nullptr, *t = nullptr, *v = nullptr;
-    int64_t n = 0, stride = 1;
-    WindowGeom g{};              // geometry + watermark at gwo_submit time (classification input)
-    long long base = 0;          // first window of the range
-    int nunits = 1;
-    uint64_t cap = 0;            // records per (window, coarse digit, region group) region of the batch buffer
-    int slot = 0;                // batch buffer / readback slot
-    unsigned long long seq = 0;  // readback sequence number of the last K1 launch
-    LogSegDesc desc[LOG_NU] = {}; // the range's new segments: counters/offsets carved at launch, records after
-    // speculative pass 2 (queued right behind K1, no host round trip): each window's segment records were
-    // carved at launch with an upper bound; the readback either commits them (trimmed to the device plan's
-    // size) or the host un-carves them and takes the planned path
-    bool spec = false;
-    uint64_t seg_cap[LOG_NU] = {};
-    char *carve_at[LOG_NU] = {};  // start of the carved segment records
-    char *carve_end[LOG_NU] = {}; // end of the carve (the window's chunk cursor right after it)
-    LogRoute rt{};               // multi-GPU: the first K1 routes other GPUs' records (mode 1), re-runs skip them (2)
-    bool ts32 = false;           // t holds int32 timestamps - tbase (records received in the 20-B wire format)
-    int64_t tbase = 0;
-    bool timed = false;          // the last K1 launch carries its own device timestamps (profiling)
-};
-
-struct LogState {
-    std::map<long long, LogWindow> wins;
-    std::multimap<size_t, char *> free_chunks;
-    // batch buffers: one for the K1 in flight, one for the deferred pass 2, one for the next K1
-    DevBuf tmp[LOG_SLOTS], firedesc;
-    // the last pass-2 launch, checked for overflow at the next sync point (deferred so the next batch's
-    // K1 queues right behind it); its segments are already in the windows
-    struct {
-        bool active = false;
-        int tmpx = 0, nunits = 0;
-        long long base = 0;
-        unsigned long long after_seq = 0;   // a K1 readback with a higher sequence number follows it
-        bool has_event = false;
-        uint64_t cap = 0;
-        std::vector<uint64_t> counts;
-    } pend;
-    hipEvent_t ev_split = nullptr;               // after the deferred pass 2 (pipelined mode only)
-    unsigned long long seen_seq = 0;             // highest K1 readback sequence number observed complete
-    unsigned *h_split_flag = nullptr;            // pinned, device-written [LOG_SLOTS]: pass-2 overflow flags
-    unsigned *d_split_flag = nullptr;            // device view of h_split_flag
-    unsigned *d_go = nullptr;                    // [LOG_SLOTS] K1's verdict on the speculative pass 2
-    unsigned long long *d_done = nullptr;        // K1 arrival counters (LOG_DONE_WORDS; reset by the last one)
-    unsigned long long *d_k1sh = nullptr;        // K1 statistics shards (reset by the last one)
-    // pipelined submission (gwo_set_pipelined_submit): the batch whose K1 is in flight, resolved by the
-    // next call on the handle
-    bool pipeline = false;
-    LogJob job;
-    // the fire in flight on fire_stream
-    std::vector<long long> fire_units;
-    uint64_t fire_rows0 = 0, fire_bound = 0;
-    unsigned long long *h_fire_out = nullptr;    // pinned [3]: row counter, overflow, slow partitions
-    unsigned long long *d_cursor = nullptr;      // [LOG_NU * LOG_ND * LOG_XG * LOG_CUR_STRIDE] region cursors of K1
-    // K1 readback per slot (LOG_RB_* layout), written into pinned host memory by log_collect_kernel,
-    // which also leaves the device plan of pass 2 in d_bk (per slot) and resets cursors and stats
-    unsigned long long *h_rb = nullptr, *d_rbh = nullptr;   // host / device views
-    LogBucket *d_bk = nullptr;                   // [LOG_SLOTS][LOG_NU * LOG_ND + 1]
-    hipEvent_t ev_rb[LOG_SLOTS] = {};
-    bool rb_event[LOG_SLOTS] = {};   // ev_rb[slot] was recorded behind the slot's last K1 (side output only)
-    // host-planned pass 2 (exact re-run after an overflow): [nb + 1] buckets, one H2D copy
-    LogBucket *d_plan = nullptr, *h_buckets = nullptr;
-    std::vector<LogSegDesc> h_fire;
-    unsigned long long *d_overflow = nullptr;
-    uint64_t last_window_keys = 0;               // distinct keys of the last fired window
-    uint64_t last_window_records = 0;            // records of the last fired window
-    long long span_hint = 1;                     // windows the previous batch spanned
-    int cap_log2 = 0;
-    int max_groups = 0;                          // persistent fire workgroups (2 per CU)
-    unsigned long long seq = 0;                  // last readback sequence number issued
-    unsigned long long *d_t0 = nullptr;          // K1's start timestamp (profiling)
-    int clock_khz = 0;                           // device wall-clock rate
-
-    unsigned long long *rb(int slot) const { return h_rb + (size_t)slot * LOG_RB_WORDS; }
-    unsigned long long *rb_dev(int slot) const { return d_rbh + (size_t)slot * LOG_RB_WORDS; }
-    LogBucket *bk(int slot) const { return d_bk + (size_t)slot * (LOG_NU * LOG_ND + 1); }
-    // a batch buffer neither the K1 in flight nor the deferred pass 2 holds
-    int free_slot() const {
-        for (int s = 0; s < LOG_SLOTS; ++s)
-            if (!(job.active && job.slot == s) && !(pend.active && pend.tmpx == s)) return s;
-        return 0;   // unreachable: LOG_SLOTS = 3 > 2 busy slots
-    }
-};
 
 static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
@@ -186,7 +85,7 @@ gwo_status Handle::log_init() {
 // windows in flight (one filling, one fired, the next -- 16-B records, about two records per key, 1.4x for
 // the partitions' capacity slack), capped at a quarter of the free device memory.
 gwo_status Handle::log_reserve() {
-    if (cfg.expected_keys <= 0) return GWO_OK;
+    if (cfg.expected_keys <= 0 || slog) return GWO_OK;   // (the sliding log reserves at its first batch)
     LogState &L = *logst;
     const uint64_t keys = (uint64_t)cfg.expected_keys;
     GWO_TRY(ensure_output(keys + keys / 8 + 4096));
@@ -247,6 +146,7 @@ gwo_status Handle::log_carve(LogWindow &W, size_t bytes, char **out) {
         size_t want = 1 << 20;
         while (want < bytes * 4 && want < ((size_t)1 << 30)) want <<= 1;
         want = std::max(want, bytes);
+        if (log_chunk_min && bytes <= log_chunk_min) want = log_chunk_min;   // sliding log: one pane size
         LogChunk c;
         auto it = logst->free_chunks.lower_bound(want);
         if (it != logst->free_chunks.end() && it->first <= want * 2) {
@@ -286,6 +186,7 @@ void Handle::log_release(LogWindow &W) {
 // (records >= keys; x2 covers the usual duplication) or this batch's size.  An underestimate only
 // sends partitions to the fire's slow path.
 int Handle::log_choose_lp(uint64_t batch_records) const {
+    if (slog) return slog_lp();   // sliding log: panes are partitioned like the running total
     const LogState &L = *logst;
     uint64_t est = L.last_window_records;
     if (est == 0) est = std::max<uint64_t>((uint64_t)std::max<int64_t>(cfg.expected_keys, 0) * 2, batch_records * 8);
@@ -493,15 +394,19 @@ LogThr Handle::log_thresholds(const LogJob &J) const {
     LogThr t{};
     for (int j = 0; j <= LOG_NU; ++j) t.bound[j] = (int64_t)0x7fffffffffffffffLL;
     t.full_range = cfg.key_group_start == 0 && cfg.key_group_end == cfg.max_parallelism - 1;
-    const __int128 size = cfg.size, s0 = (__int128)J.base * size + (__int128)geom.unit_off_mod;
+    const __int128 size = log_usize(), s0 = (__int128)J.base * size + (__int128)geom.unit_off_mod;
     const __int128 lo = (__int128)(int64_t)0x8000000000000000LL, hi = (__int128)(int64_t)0x7fffffffffffffffLL;
     if (s0 <= lo || s0 + (__int128)J.nunits * size > hi || s0 < (__int128)geom.offset - size) return t;
     for (int j = 0; j <= J.nunits; ++j) t.bound[j] = (int64_t)(s0 + (__int128)j * size);
     for (int j = 0; j < J.nunits; ++j) {
         const int64_t max_ts = (int64_t)(s0 + (__int128)(j + 1) * size - 1);
-        const uint32_t c = cleanup_time_host(max_ts) <= J.g.wm ? 1u : (max_ts <= J.g.wm ? 2u : 0u);
+        const int64_t c_late = (int64_t)((uint64_t)max_ts + (uint64_t)log_lateness());
+        const int64_t cleanup = c_late >= max_ts ? c_late : (int64_t)0x7fffffffffffffffLL;
+        uint32_t c = cleanup <= J.g.wm ? 1u : (max_ts <= J.g.wm ? 2u : 0u);
+        if (J.only_refire) c = c == 2u ? 0u : 1u;   // the late pass takes class-2 units inline, the rest out of line
         t.cls |= c << (2 * j);
     }
+    t.only_refire = J.only_refire ? 1 : 0;
     t.ok = 1;
     return t;
 }
@@ -637,6 +542,7 @@ gwo_status Handle::log_resolve_k1(LogJob J) {
     bool refire = false;
     GWO_TRY(log_resolve_batch(J, refire));
     if (!refire) return GWO_OK;
+    if (slog) return slog_late_pass(J0);
     // allowedLateness > 0: records of fired, not yet cleaned windows re-fire them (EventTimeTrigger.onElement
     // FIRE, WindowOperator.java:393-406).  Those windows live in hash tables (log_migrate); a table pass over
     // the batch takes the re-fire records only -- the log took the accepted ones, K1 counted the late ones.
@@ -665,7 +571,7 @@ gwo_status Handle::log_resolve_batch(LogJob &J, bool &refire) {
             J.timed = false;
         }
         // the side-output row count follows the collect kernel by a copy: wait for that too
-        if (first_pass && side_enabled()) GWO_TRY(spin_event(L.ev_rb[J.slot], "side count"));
+        if (first_pass && side_enabled() && !J.only_refire) GWO_TRY(spin_event(L.ev_rb[J.slot], "side count"));
         const unsigned long long *rbp = L.rb(J.slot);
         memcpy(h_stats, rbp + LOG_RB_STATS, sizeof(BatchStats));
         GWO_TRY(log_resolve_split());   // the previous pass 2 (also frees its plan staging for reuse)
@@ -674,8 +580,10 @@ gwo_status Handle::log_resolve_batch(LogJob &J, bool &refire) {
                                          "Record has Long.MIN_VALUE timestamp (= no timestamp marker). Is the time "
                                          "characteristic set to 'ProcessingTime', or did you forget to call "
                                          "'DataStream.assignTimestampsAndWatermarks(...)'?");
+            if (hs.bad_range) return poison(GWO_ERR_UNSUPPORTED, "sliding windows: timestamp < offset - slide (Java '%' "
+                                                                 "quirk range) is outside the pane restatement");
             if (hs.refire) {
-                if (J.stride != 1)
+                if (J.stride != 1 && !slog)
                     return poison(GWO_ERR_UNSUPPORTED, "allowedLateness > 0 re-fire on records received by the "
                                                        "multi-GPU exchange: use the table layout");
                 refire = true;
@@ -684,7 +592,7 @@ gwo_status Handle::log_resolve_batch(LogJob &J, bool &refire) {
                                                              " is not in KeyGroupRange{startKeyGroup=" +
                                                              std::to_string(cfg.key_group_start) + ", endKeyGroup=" +
                                                              std::to_string(cfg.key_group_end) + "}.").c_str());
-            if (side_enabled()) {
+            if (side_enabled() && !J.only_refire) {
                 side_rows = *h_scalar;
                 if ((long long)side_rows > side_cap) {
                     side_rows = side_rows_committed;
@@ -763,7 +671,7 @@ gwo_status Handle::log_route_only(const int64_t *k, const int64_t *t, const int6
     for (int j = 0; j <= LOG_NU; ++j) thr.bound[j] = (int64_t)0x7fffffffffffffffLL;
     thr.full_range = 1;
     const DevBuf &tmp = L.tmp[0];
-    launch_log_part(k, t, v, n, 1, geom_now(), 0, 1, needs_value, L.d_cursor, 0, (int64_t *)tmp.ptr, d_stats,
+    launch_log_part(k, t, v, n, 1, log_geom_now(), 0, 1, needs_value, L.d_cursor, 0, (int64_t *)tmp.ptr, d_stats,
                     nullptr, nullptr, nullptr, d_side_count, 0, 0, ca, thr, rt, stream);
     return launch_ok("route-only partition");
 }
@@ -788,7 +696,8 @@ gwo_status Handle::insert_log(const int64_t *k, const int64_t *t, const int64_t 
     J.v = v;
     J.n = n;
     J.stride = stride;
-    J.g = geom_now();
+    J.g = log_geom_now();
+    if (slog) GWO_TRY(slog_reserve(n));
     J.base = hist_hint;
     J.nunits = (int)std::min<long long>(LOG_NU, std::max<long long>(1, L.span_hint));
     J.cap = group_capacity((double)n / ((double)LOG_ND * LOG_XG));
@@ -801,7 +710,7 @@ gwo_status Handle::insert_log(const int64_t *k, const int64_t *t, const int64_t 
     // by the next batch -- and without a side output (K1 appends to it on the first pass).
     // With allowedLateness > 0 a batch resolves before the next watermark: its re-fire records must reach the
     // fired windows' tables before a watermark cleans them up.
-    const bool pipe = L.pipeline && cfg.allowed_lateness == 0 && stride == 1 && !side_enabled() && !comm && !dict &&
+    const bool pipe = L.pipeline && !slog && cfg.allowed_lateness == 0 && stride == 1 && !side_enabled() && !comm && !dict &&
                       (const void *)k != stage_key.ptr &&
                       (const void *)t != stage_ts.ptr && (!v || (const void *)v != stage_val.ptr);
     if (L.job.active && !pipe) GWO_TRY(log_flush());
@@ -1055,7 +964,7 @@ gwo_status Handle::log_fold_raw(const std::vector<long long> &units, const SnapC
     for (long long u : units) {
         LogWindow &W = L.wins[u];
         const int64_t start = unit_start(u);
-        const int64_t end = (int64_t)((uint64_t)start + (uint64_t)cfg.size);
+        const int64_t end = (int64_t)((uint64_t)start + (uint64_t)log_usize());   // sliding: the pane
         launch_log_fire((const LogSegDesc *)L.firedesc.ptr + at, (int)W.segs.size(), W.lp, needs_value, plan, raw, start,
                         end, o, L.d_overflow, L.max_groups, 2, 1, W.partial, stream);
         GWO_TRY(launch_ok("log fold"));
@@ -1188,7 +1097,7 @@ gwo_status Handle::log_restore_rows(const RestoreRows &R, int64_t new_wm) {
         W.partial = LogSegDesc{(int64_t *)p_rec, (uint32_t *)p_off, (uint32_t *)p_cnt, W.lp, 0};
         W.partial_rows = ix.size();
     }
-    return GWO_OK;
+    return slog ? slog_anchor() : GWO_OK;
 }
 
 }  // namespace gwo

@@ -73,6 +73,8 @@ struct LogThr {
     int32_t ok;                  // 1: the bounds are valid
     int32_t full_range;          // 1: the subtask owns every key group (no key-group check needed)
     int32_t ts32;                // 1: `ts` holds int32 timestamps - tbase (records received in the 20-B wire format)
+    int32_t only_refire;         // 1: the sliding-log late pass -- accept only records whose pane is already in the
+                                 //    running total (class 2), skip every other record without counting it
     int64_t tbase;
 };
 
@@ -118,7 +120,7 @@ struct CollectArgs {
 // (device-scope atomics on the same address serialise at ~12 ns each on MI355X: 4 per-wave atomics per
 // workgroup on one word cost ~25 us at the end of a 512-workgroup launch); the tail folds the shards.
 #define LOG_SHARDS 16
-enum : int { K1S_MIN = 0, K1S_MAX, K1S_ACC, K1S_LATE, K1S_REFIRE, K1S_BADTS, K1S_BADKG, K1S_HOUT, K1S_NEXT, K1_SW };
+enum : int { K1S_MIN = 0, K1S_MAX, K1S_ACC, K1S_LATE, K1S_REFIRE, K1S_BADTS, K1S_BADKG, K1S_HOUT, K1S_BADR, K1S_NEXT, K1_SW };
 static constexpr size_t LOG_DONE_WORDS = (LOG_SHARDS + 1) * LOG_CUR_STRIDE;
 
 // Multi-GPU keyBy routing fused into K1 (the log layout's first K1 over a batch): a record whose key group

@@ -29,7 +29,7 @@ namespace gwo {
 
 typedef long long ll2 __attribute__((ext_vector_type(2)));
 
-enum LogClass : int { L_ACCEPT = 0, L_LATE = 1, L_SKIP = 2, L_REFIRE = 3, L_BAD_TS = 4 };
+enum LogClass : int { L_ACCEPT = 0, L_LATE = 1, L_SKIP = 2, L_REFIRE = 3, L_BAD_TS = 4, L_BAD_RANGE = 5 };
 
 // Tumbling classification, WindowOperator.java:386-427 + TumblingEventTimeWindows.java:68-81.
 // With a = ts - offset + size in [0, 2^52) (every timestamp within 142,000 years of the epoch):
@@ -39,6 +39,9 @@ enum LogClass : int { L_ACCEPT = 0, L_LATE = 1, L_SKIP = 2, L_REFIRE = 3, L_BAD_
 __device__ __forceinline__ int log_classify(int64_t ts, const WindowGeom &g, long long &unit) {
     if (ts == GWO_LONG_MIN) return L_BAD_TS;
     const int64_t a = jadd(jsub(ts, g.offset), g.size);
+    // sliding panes (g.size = slide): Java's '%' gives a start > ts for ts - offset + slide < 0, outside the
+    // pane restatement -- rejected loudly, as the table path does (gwo_kernels.hip classify)
+    if (g.sliding && a < 0) return L_BAD_RANGE;
     int64_t start, u;
     if ((uint64_t)a < (1ull << 52)) {
         const int64_t q = fdiv_small(a, g.size, g.inv_size);
@@ -50,8 +53,8 @@ __device__ __forceinline__ int log_classify(int64_t ts, const WindowGeom &g, lon
     }
     int64_t max_ts = jsub(jadd(start, g.size), 1);
     if (cleanup_time(max_ts, g.lateness) <= g.wm) return jadd(ts, g.lateness) <= g.wm ? L_LATE : L_SKIP;
-    if (max_ts <= g.wm) return L_REFIRE;
     unit = u;
+    if (max_ts <= g.wm) return L_REFIRE;
     return L_ACCEPT;
 }
 
@@ -158,6 +161,7 @@ __device__ __forceinline__ void k1_plan_tail(unsigned long long *cursor, BatchSt
         W.bad_ts = s_k1[K1S_BADTS];
         W.bad_kg = s_k1[K1S_BADKG];
         W.hist_out = s_k1[K1S_HOUT];
+        W.bad_range = s_k1[K1S_BADR];
         rb_put(&a.rb[LOG_RB_NEXT], s_k1[K1S_NEXT]);
     }
     __syncthreads();
@@ -217,7 +221,7 @@ __device__ __forceinline__ void k1_plan_tail(unsigned long long *cursor, BatchSt
         E.chunk0 = (uint32_t)chunk_run;
         a.bk[a.nunits * LOG_ND] = E;
         rb_put(&a.rb[LOG_RB_CHUNKS], chunk_run);
-        const bool go = a.spec && !s_bad && S.bad_ts == 0 && S.bad_kg == 0 && S.refire == 0 && S.accepted > 0 &&
+        const bool go = a.spec && !s_bad && S.bad_ts == 0 && S.bad_kg == 0 && S.refire == 0 && S.bad_range == 0 && S.accepted > 0 &&
                         S.min_idx >= base && S.min_idx < base + a.nunits && chunk_run < (1ull << 32);
         *a.go = go ? 1u : 0u;
         rb_put(&a.rb[LOG_RB_GO], go ? 1ull : 0ull);
@@ -271,7 +275,7 @@ __global__ __launch_bounds__(LOG_K1_THREADS) void log_part_kernel(
     long long mn = 0x7fffffffffffffffLL, mx = (long long)0x8000000000000000LL;   // accepted windows (slow path)
     long long nx = 0x7fffffffffffffffLL;   // first accepted window after the launch's range (slow path)
     uint32_t wmask = 0;   // launch windows (bit jj) the inline path accepted records into
-    unsigned acc = 0, late = 0, refire = 0, bad_ts = 0, out = 0, bad_kg = 0;   // per thread: < 2^32 records
+    unsigned acc = 0, late = 0, refire = 0, bad_ts = 0, out = 0, bad_kg = 0, bad_range = 0;   // per thread: < 2^32
     int64_t kk[LOG_K1_PER], vv[LOG_K1_PER], tt[LOG_K1_PER];
     // unconditional loads of a tile (lanes past the end re-read the tile's first record and are
     // discarded); the next tile's loads are issued before this tile's write phase
@@ -353,7 +357,9 @@ __global__ __launch_bounds__(LOG_K1_THREADS) void log_part_kernel(
             const int64_t o = S ? i * S : i * stride;
             const int64_t t = TS32 ? th.tbase + (int64_t)((const int32_t *)ts)[o] : ts[o], k = key[o];
             long long u = 0;
-            const int c = log_classify(t, g, u);
+            int c = log_classify(t, g, u);
+            // the sliding-log late pass: only records of panes already in the running total are taken
+            if (th.only_refire) c = c == L_REFIRE ? L_ACCEPT : L_SKIP;
             if (c == L_ACCEPT) {
                 if (!ROUTE && !th.full_range) {
                     const int32_t kg = key_group(k, g.key_kind, g.max_par);
@@ -390,6 +396,8 @@ __global__ __launch_bounds__(LOG_K1_THREADS) void log_part_kernel(
                 refire++;
             } else if (c == L_BAD_TS) {
                 bad_ts++;
+            } else if (c == L_BAD_RANGE) {
+                bad_range++;
             }
         }
         __syncthreads();
@@ -462,7 +470,7 @@ __global__ __launch_bounds__(LOG_K1_THREADS) void log_part_kernel(
     }
     // workgroup statistics -> shard blockIdx % LOG_SHARDS (zero words skipped)
     unsigned long long v[K1_SW] = {(unsigned long long)mn, (unsigned long long)mx, acc, late, refire, bad_ts, bad_kg,
-                                   out, (unsigned long long)nx};
+                                   out, bad_range, (unsigned long long)nx};
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
         const long long a = __shfl_xor((long long)v[K1S_MIN], o), b = __shfl_xor((long long)v[K1S_MAX], o);

@@ -16,19 +16,9 @@
 #include <algorithm>
 
 #include "gwo_handle.h"
+#include "gwo_slide.h"
 
 namespace gwo {
-
-struct SlideState {
-    bool ring = false;
-    int count_word = -1;          // hidden per-entry count (ring): presence of a key in window J
-    int t_idx = -1;               // aux_tables index of T
-    bool j_set = false;
-    __int128 J = 0;               // next window to fire
-    unsigned long long *d_live = nullptr;
-    unsigned long long h_live = 0;
-    int64_t om = 0;               // floorMod(offset, slide): window j starts at j*slide + om
-};
 
 #define GWO_LONG_MIN_H ((int64_t)0x8000000000000000LL)
 #define GWO_LONG_MAX_H ((int64_t)0x7fffffffffffffffLL)
@@ -50,13 +40,18 @@ gwo_status Handle::slide_init() {
     for (int w = 0; w < plan.nwords; ++w) all_add &= plan.op[w] == ACC_ADD_I64;
     S.ring = all_add && getenv("GWO_SLIDE_RECOMPUTE") == nullptr;
     if (S.ring) {
-        if (plan.nwords >= GWO_MAX_WORDS) return fail(GWO_ERR_UNSUPPORTED, "too many accumulator words");
-        S.count_word = plan.nwords;
-        plan.op[plan.nwords] = ACC_ADD_I64;
-        plan.src[plan.nwords] = SRC_ONE;
-        plan.ident[plan.nwords] = 0;
-        plan.nwords++;
-        plan.stride = ((1 + plan.nwords) + 1) & ~1;
+        // presence of a key in the window: an existing record count word (COUNT, AVG) serves, else a hidden one
+        for (int w = 0; w < plan.nwords && S.count_word < 0; ++w)
+            if (plan.op[w] == ACC_ADD_I64 && plan.src[w] == SRC_ONE) S.count_word = w;
+        if (S.count_word < 0) {
+            if (plan.nwords >= GWO_MAX_WORDS) return fail(GWO_ERR_UNSUPPORTED, "too many accumulator words");
+            S.count_word = plan.nwords;
+            plan.op[plan.nwords] = ACC_ADD_I64;
+            plan.src[plan.nwords] = SRC_ONE;
+            plan.ident[plan.nwords] = 0;
+            plan.nwords++;
+            plan.stride = ((1 + plan.nwords) + 1) & ~1;
+        }
         GWO_TRY(dalloc((void **)&S.d_live, 8));
         GWO_TRY(hipcheck(hipMemsetAsync(S.d_live, 0, 8, stream), "live"));
         Table t;

@@ -1,0 +1,367 @@
+// gwo_slog.cpp -- host side of sliding windows over logged panes (kernel: gwo_slog.hip).
+//
+// SlidingEventTimeWindows (SlidingEventTimeWindows.java:68-82) with every aggregate word an int64 sum and
+// allowedLateness 0, at high key cardinality.  A record is logged once, into its pane (a tumbling window
+// of `slide`), by the log layout's K1 + pass 2 (gwo_log.cpp), classified against the pane's windows:
+//   * the pane's last window already fired (cleanupTime of that window <= watermark): late, dropped or
+//     side output -- WindowOperator.java:386-427 skips every window of the record;
+//   * the pane's first window already fired (the pane is in the running total R): the record still
+//     belongs to the pane's unfired windows; a second K1 pass over the batch (the "late pass") logs those
+//     records into their panes and queues the new segments to be added to R at the next window step;
+//   * otherwise it waits in its pane until the pane enters a window.
+// The window step of window J (one kernel, gwo_slog.hip): R' = R + entering pane - leaving pane, and every
+// key of R' with a positive count emits J's row (WindowOperator.onEventTime / emitWindowContents,
+// WindowOperator.java:430-473, 546-550; EventTimeTrigger.onEventTime FIRE at maxTimestamp).  A pane's
+// memory is released when it leaves the window.  R is rebuilt from the panes of J (no leaving pane)
+// when it became empty, after a restore, and at the first fire.
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+
+#include "gwo_handle.h"
+#include "gwo_log.h"
+#include "gwo_log_state.h"
+#include "gwo_slide.h"
+#include "gwo_slog.h"
+
+namespace gwo {
+
+struct SlogState {
+    int lp = 0;                    // partition bits of R and of new pane segments
+    int cap_log2 = 11;             // LDS table slots of the window step
+    bool split_next = false;       // the next window step writes R' at lp + 1
+    DevBuf ring[2];                // R (in) and R' (out) alternate
+    uint32_t *cnt[2] = {nullptr, nullptr};   // [2^LOG_MAX_LP] entries per partition
+    uint64_t rcap[2] = {0, 0};
+    int rlp[2] = {0, 0};
+    int cur = 0;                   // ring[cur] holds R
+    uint64_t live = 0;             // keys in R (the last fired window)
+    uint64_t maxp = 0;             // largest partition of R
+    bool rebuild = true;           // R is not the last fired window's total: rebuild from the panes of J
+    std::vector<std::pair<long long, size_t>> pending;   // (pane, segment) added at the next window step
+    uint64_t pending_records = 0;
+    unsigned long long *d_stat = nullptr, *h_stat = nullptr;
+    DevBuf segdesc;
+    std::vector<SlogSeg> h_segs;
+    int groups = 0;
+    bool reserved = false;
+};
+
+static uint64_t slog_capacity(double mean) { return (uint64_t)std::ceil(mean + 6.0 * std::sqrt(mean) + 16.0); }
+
+int Handle::slog_lp() const { return slog->lp; }
+
+int64_t Handle::log_usize() const { return slog ? cfg.slide : cfg.size; }
+int64_t Handle::log_lateness() const { return slog ? cfg.size - cfg.slide : cfg.allowed_lateness; }
+
+// K1's geometry for the log: sliding panes are tumbling windows of `slide` at the assigner's offset (the
+// pane start is getWindowStartWithOffset(ts, offset, slide), SlidingEventTimeWindows.java:72), and a pane is
+// late when its last window is (cleanup distance size - slide past the pane's end, allowedLateness 0).
+WindowGeom Handle::log_geom_now() const {
+    WindowGeom g = geom_now();
+    if (slog) {
+        g.size = cfg.slide;
+        g.inv_size = 1.0 / (double)cfg.slide;
+        g.offset = cfg.offset;
+        g.lateness = cfg.size - cfg.slide;
+    }
+    return g;
+}
+
+gwo_status Handle::slog_init() {
+    slog = new SlogState();
+    SlogState &G = *slog;
+    int c = 12;
+    while (c > 8 && slog_lds_bytes(c, plan.nwords) > 64 * 1024) c--;
+    G.cap_log2 = c;
+    // R partitions: ~0.6 of the LDS table per partition at the caller's distinct-key hint (or the first batch)
+    const double per = 0.6 * (double)(1 << c);
+    G.lp = LOG_MIN_LP;
+    if (cfg.expected_keys > 0)
+        while (G.lp < LOG_MAX_LP && (double)cfg.expected_keys / (double)(1u << G.lp) > per) G.lp++;
+    for (int i = 0; i < 2; ++i) {
+        GWO_TRY(dalloc((void **)&G.cnt[i], ((size_t)1 << LOG_MAX_LP) * 4));
+        GWO_TRY(hipcheck(hipMemsetAsync(G.cnt[i], 0, ((size_t)1 << LOG_MAX_LP) * 4, stream), "ring counts"));
+        G.rlp[i] = G.lp;
+    }
+    GWO_TRY(dalloc((void **)&G.d_stat, SLOG_SHARDS * SLOG_STAT_STRIDE * 8));
+    GWO_TRY(hipcheck(hipMemsetAsync(G.d_stat, 0, SLOG_SHARDS * SLOG_STAT_STRIDE * 8, stream), "ring stats"));
+    GWO_TRY(hipcheck(hipHostMalloc((void **)&G.h_stat, SLOG_SHARDS * SLOG_STAT_STRIDE * 8, hipHostMallocDefault),
+                     "pinned"));
+    GWO_TRY(ensure_buf(G.segdesc, SLOG_MAX_SEGS * sizeof(SlogSeg)));
+    int cus = 0;
+    GWO_TRY(hipcheck(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, cfg.device), "CU count"));
+    G.groups = std::max(cus, 1) * 2;
+    if (cfg.expected_keys > 0) {   // R and R' for the hinted key count, so the steady state allocates nothing
+        const uint64_t P = 1ull << G.lp;
+        const uint64_t rcap = slog_capacity(1.25 * (double)cfg.expected_keys / (double)P);
+        for (int i = 0; i < 2; ++i) {
+            GWO_TRY(ensure_buf(G.ring[i], P * rcap * (1 + plan.nwords) * 8));
+            G.rcap[i] = rcap;
+        }
+        GWO_TRY(ensure_output((uint64_t)cfg.expected_keys + (uint64_t)cfg.expected_keys / 4 + 4096));
+    }
+    // the window step's code object: one partition, no entries, no segments (HIP loads a kernel on its first launch)
+    SlogArgs a{};
+    a.in = SlogRing{nullptr, G.cnt[0], 0, 0, 0};
+    a.out = SlogRing{nullptr, G.cnt[1], 0, 0, 0};
+    a.p = plan;
+    a.rp = rplan;
+    a.count_word = slide->count_word;
+    a.cap_log2 = G.cap_log2;
+    a.stat = G.d_stat;
+    a.o.count = d_scratch_count;
+    launch_slog_fire(a, 1, stream);
+    GWO_TRY(launch_ok("slog warm-up"));
+    return hipcheck(hipMemsetAsync(G.d_stat, 0, SLOG_SHARDS * SLOG_STAT_STRIDE * 8, stream), "ring stats");
+}
+
+void Handle::slog_free() {
+    if (!slog) return;
+    SlogState &G = *slog;
+    for (int i = 0; i < 2; ++i) {
+        G.ring[i].release();
+        if (G.cnt[i]) (void)hipFree(G.cnt[i]);
+    }
+    G.segdesc.release();
+    if (G.d_stat) (void)hipFree(G.d_stat);
+    if (G.h_stat) (void)hipHostFree(G.h_stat);
+    delete slog;
+    slog = nullptr;
+}
+
+// The pane chunk pool, sized from the first batch: every pane of a window plus a few in flight, each
+// chunk holding a pane's segments (speculative carves included), touched now so no step allocates.
+gwo_status Handle::slog_reserve(int64_t n) {
+    SlogState &G = *slog;
+    if (G.reserved) return GWO_OK;
+    G.reserved = true;
+    const double P = (double)(1u << G.lp);
+    const double seg = (double)n + 6.0 * std::sqrt(P * (double)n) + 5.0 * P + 64.0;
+    size_t chunk = (size_t)1 << 20;
+    while ((double)chunk < 2.2 * seg * (needs_value ? 16.0 : 8.0) + 16.0 * P) chunk <<= 1;
+    log_chunk_min = chunk;
+    size_t free_b = 0, total_b = 0;
+    GWO_TRY(hipcheck(hipMemGetInfo(&free_b, &total_b), "memory info"));
+    const size_t panes = (size_t)(cfg.size / cfg.slide) + 8;
+    const size_t want = std::min(panes * chunk, free_b / 4);
+    for (size_t got = 0; got + chunk <= want; got += chunk) {
+        void *p = nullptr;
+        GWO_TRY(dalloc(&p, chunk));
+        GWO_TRY(hipcheck(hipMemsetAsync(p, 0, chunk, stream), "pane pool"));
+        logst->free_chunks.emplace(chunk, (char *)p);
+    }
+    return GWO_OK;
+}
+
+// After a restore: windows ending at or before the watermark fired before the checkpoint; R is rebuilt
+// from the restored panes at the next window step.
+gwo_status Handle::slog_anchor() {
+    SlideState &S = *slide;
+    S.J = first_unfired_window(wm);
+    S.j_set = true;
+    slog->rebuild = true;
+    slog->pending.clear();
+    slog->pending_records = 0;
+    return GWO_OK;
+}
+
+// The late pass (see the file comment): K1 over the batch again, accepting only the records whose pane is
+// already in R; their new segments are added to R at the next window step (and leave with their pane).
+gwo_status Handle::slog_late_pass(const LogJob &J0) {
+    LogState &L = *logst;
+    SlogState &G = *slog;
+    std::map<long long, std::pair<size_t, uint64_t>> before;
+    for (auto &kv : L.wins) before[kv.first] = {kv.second.segs.size(), kv.second.records};
+    LogJob J = J0;
+    J.only_refire = true;
+    J.spec = false;
+    if (J.rt.mode != 0) J.rt.mode = 2;   // other GPUs' records were routed by the first K1
+    J.nunits = LOG_NU;
+    J.slot = L.free_slot();
+    const long long hint = hist_hint, span = L.span_hint;
+    GWO_TRY(log_k1(J, false));
+    bool refire = false;
+    gwo_status s = log_resolve_batch(J, refire);
+    hist_hint = hint;   // the next batch's window-range guess stays the stream's, not the late panes'
+    L.span_hint = span;
+    GWO_TRY(s);
+    GWO_TRY(log_resolve_split());
+    for (auto &kv : L.wins) {
+        auto it = before.find(kv.first);
+        const size_t s0 = it == before.end() ? 0 : it->second.first;
+        const uint64_t r0 = it == before.end() ? 0 : it->second.second;
+        for (size_t i = s0; i < kv.second.segs.size(); ++i) G.pending.push_back({kv.first, i});
+        G.pending_records += kv.second.records - r0;
+    }
+    return GWO_OK;
+}
+
+void Handle::slog_release_before(long long first_pane) {
+    LogState &L = *logst;
+    for (auto it = L.wins.begin(); it != L.wins.end() && it->first < first_pane;) {
+        log_release(it->second);
+        it = L.wins.erase(it);
+    }
+}
+
+// Window steps for every window whose maxTimestamp the watermark passed (EventTimeTrigger.onEventTime FIRE,
+// InternalTimerServiceImpl.advanceWatermark fires timers in timestamp order: window J before J + 1).
+gwo_status Handle::fire_slog(int64_t new_wm) {
+    SlideState &S = *slide;
+    SlogState &G = *slog;
+    LogState &L = *logst;
+    GWO_TRY(log_flush());
+    GWO_TRY(log_resolve_split());   // every pane's last segment is complete
+    const __int128 j_new = first_unfired_window(new_wm);
+    if (!S.j_set) {
+        S.J = j_new;
+        if (!L.wins.empty()) S.J = std::min(first_window_of_pane(L.wins.begin()->first), j_new);
+        S.j_set = true;
+        G.rebuild = true;
+    }
+    const int NW = plan.nwords, RW = 1 + NW;
+    while (S.J < j_new) {
+        long long lo = win_first_pane(S.J), hi = win_last_pane(S.J);
+        G.h_segs.clear();
+        uint64_t plus_records = 0;
+        std::vector<long long> leaving;
+        auto add_pane = [&](LogWindow &W, int sign) {
+            for (auto &d : W.segs) G.h_segs.push_back(SlogSeg{d.rec, d.off, d.cnt, d.lp, sign, 0, 0});
+            if (W.partial.rec)
+                G.h_segs.push_back(SlogSeg{W.partial.rec, W.partial.off, W.partial.cnt, W.partial.lp, sign, 1, 0});
+            if (sign > 0) plus_records += W.records + W.partial_rows;
+        };
+        if (G.rebuild) {
+            // R holds nothing of window J - 1: skip to the first window holding a pane with records and sum its panes
+            slog_release_before(lo);
+            auto it = L.wins.begin();
+            while (it != L.wins.end() && it->second.segs.empty() && !it->second.partial.rec) {
+                log_release(it->second);   // offsets carved for a K1 range that got no records
+                it = L.wins.erase(it);
+            }
+            if (it == L.wins.end()) {
+                S.J = j_new;
+                break;
+            }
+            const __int128 ja = std::max(S.J, first_window_of_pane(it->first));
+            if (ja >= j_new) break;
+            S.J = ja;
+            lo = win_first_pane(S.J);
+            hi = win_last_pane(S.J);
+            slog_release_before(lo);
+            for (auto jt = L.wins.lower_bound(lo); jt != L.wins.end() && jt->first <= hi; ++jt) add_pane(jt->second, +1);
+            G.live = 0;
+        } else {
+            const long long plo = win_first_pane(S.J - 1), phi = win_last_pane(S.J - 1);
+            for (auto jt = L.wins.upper_bound(phi); jt != L.wins.end() && jt->first <= hi; ++jt) add_pane(jt->second, +1);
+            for (auto &pe : G.pending) {
+                auto jt = L.wins.find(pe.first);
+                if (jt == L.wins.end() || pe.second >= jt->second.segs.size()) continue;
+                const LogSegDesc &d = jt->second.segs[pe.second];
+                G.h_segs.push_back(SlogSeg{d.rec, d.off, d.cnt, d.lp, +1, 0, 0});
+            }
+            plus_records += G.pending_records;
+            for (auto jt = L.wins.lower_bound(plo); jt != L.wins.end() && jt->first < lo; ++jt) {
+                add_pane(jt->second, -1);
+                leaving.push_back(jt->first);
+            }
+        }
+        G.pending.clear();
+        G.pending_records = 0;
+        if (G.h_segs.size() > SLOG_MAX_SEGS)
+            return poison(GWO_ERR_CAPACITY, "sliding log: a window step has more than 64 pane segments; use the "
+                                            "table layout for batches that span that many panes");
+        const int64_t start = win_start(S.J);
+        const int64_t end = (int64_t)((uint64_t)start + (uint64_t)cfg.size);
+        const uint64_t bound = G.live + plus_records;
+        if (G.live == 0 && G.h_segs.empty()) {   // nothing in R and nothing enters: the window is empty
+            for (long long u : leaving) {
+                log_release(L.wins[u]);
+                L.wins.erase(u);
+            }
+            G.rebuild = true;
+            S.J += 1;
+            continue;
+        }
+        // R' geometry: the partitions split when the largest one nears the LDS table
+        const int in = G.cur, outb = 1 - G.cur;
+        const int lp_in = G.rebuild ? G.lp : G.rlp[in];
+        const int lp_out = (G.split_next && lp_in < LOG_MAX_LP) ? lp_in + 1 : lp_in;
+        const uint64_t Pout = 1ull << lp_out;
+        uint64_t rcap = slog_capacity((double)bound / (double)Pout);
+        if (G.ring[outb].bytes < Pout * rcap * RW * 8)
+            GWO_TRY(ensure_buf(G.ring[outb], (size_t)((double)(Pout * rcap * RW * 8) * 1.5)));
+        rcap = G.ring[outb].bytes / (Pout * RW * 8);   // use all of it
+        GWO_TRY(ensure_output(bound));
+        GWO_TRY(hipcheck(hipMemcpyAsync(G.segdesc.ptr, G.h_segs.data(), G.h_segs.size() * sizeof(SlogSeg),
+                                        hipMemcpyHostToDevice, stream), "slog segments"));
+        if (G.rebuild)   // R is empty: every partition of the input reads zero entries
+            GWO_TRY(hipcheck(hipMemsetAsync(G.cnt[in], 0, ((size_t)1 << lp_in) * 4, stream), "ring reset"));
+        SlogArgs a{};
+        a.in = SlogRing{(int64_t *)G.ring[in].ptr, G.cnt[in], G.rcap[in], lp_in, 0};
+        a.out = SlogRing{(int64_t *)G.ring[outb].ptr, G.cnt[outb], rcap, lp_out, 0};
+        a.segs = (const SlogSeg *)G.segdesc.ptr;
+        a.nseg = (int)G.h_segs.size();
+        a.has_val = needs_value ? 1 : 0;
+        a.count_word = S.count_word;
+        a.cap_log2 = G.cap_log2;
+        a.start = start;
+        a.end = end;
+        a.p = plan;
+        a.rp = rplan;
+        a.stat = G.d_stat;
+        const uint64_t rows0 = out_rows;
+        for (int attempt = 0;; ++attempt) {
+            a.o = out_cols();
+            GWO_TRY(hipcheck(hipMemsetAsync(G.d_stat, 0, SLOG_SHARDS * SLOG_STAT_STRIDE * 8, stream), "ring stats"));
+            prof_begin(GWO_KERNEL_FIRE);
+            launch_slog_fire(a, G.groups, stream);
+            GWO_TRY(launch_ok("slog window step"));
+            prof_end(GWO_KERNEL_FIRE, (int64_t)bound);
+            GWO_TRY(hipcheck(hipMemcpyAsync(G.h_stat, G.d_stat, SLOG_SHARDS * SLOG_STAT_STRIDE * 8,
+                                            hipMemcpyDeviceToHost, stream), "ring stats"));
+            GWO_TRY(hipcheck(hipStreamSynchronize(stream), "slog window step"));
+            uint64_t st[SLS_WORDS] = {};
+            for (int q = 0; q < SLOG_SHARDS; ++q)
+                for (int w = 0; w < SLS_WORDS; ++w) {
+                    const uint64_t x = G.h_stat[q * SLOG_STAT_STRIDE + w];
+                    st[w] = w == SLS_MAXP ? std::max(st[w], x) : st[w] + x;
+                }
+            if (st[SLS_NEG]) return poison(GWO_ERR_HIP, "sliding log: a key's window count became negative");
+            if (st[SLS_LDS]) return poison(GWO_ERR_CAPACITY, "sliding log: a partition overflowed its LDS table");
+            if (st[SLS_ROVF]) {   // a partition of R' outgrew its region: larger regions, same step again
+                if (attempt >= 4) return poison(GWO_ERR_CAPACITY, "sliding log: running-total partition overflow");
+                rcap = std::max<uint64_t>(rcap * 2, st[SLS_MAXP] + st[SLS_MAXP] / 4 + 64);
+                GWO_TRY(ensure_buf(G.ring[outb], Pout * rcap * RW * 8));
+                a.out.rec = (int64_t *)G.ring[outb].ptr;
+                a.out.rcap = rcap;
+                *h_scalar = rows0;
+                GWO_TRY(hipcheck(hipMemcpyAsync(d_out_count, h_scalar, 8, hipMemcpyHostToDevice, stream), "row rewind"));
+                continue;
+            }
+            if (debug)
+                fprintf(stderr, "[gwo] slog window %lld: segs=%zu live=%llu maxp=%llu slow=%llu lp %d->%d\n",
+                        (long long)start, G.h_segs.size(), (unsigned long long)st[SLS_LIVE],
+                        (unsigned long long)st[SLS_MAXP], (unsigned long long)st[SLS_SLOW], lp_in, lp_out);
+            G.live = st[SLS_LIVE];
+            G.maxp = st[SLS_MAXP];
+            break;
+        }
+        out_rows = rows0 + G.live;
+        G.cur = outb;
+        G.rcap[outb] = rcap;
+        G.rlp[outb] = lp_out;
+        G.lp = lp_out;   // new panes are logged at R's partitioning
+        G.split_next = (double)G.maxp > 0.75 * (double)(1 << G.cap_log2);
+        G.rebuild = G.live == 0;
+        for (long long u : leaving) {
+            log_release(L.wins[u]);
+            L.wins.erase(u);
+        }
+        S.J += 1;
+    }
+    return GWO_OK;
+}
+
+}  // namespace gwo

@@ -1,0 +1,66 @@
+// gwo_slog.h -- sliding windows over logged panes with a partitioned running total.
+//
+// The reference adds every record to ceil(size/slide) windows (SlidingEventTimeWindows.java:68-82) and
+// keeps one heap entry plus one timer per (key, window) (WindowOperator.java:294-427).  Here a record is
+// logged once into its pane (a tumbling window of `slide`, through the log layout's K1 + pass 2), and
+// the running total R of the last fired window is kept partitioned exactly like the pane logs (top lp
+// bits of digit_hash).  Firing window J is one pass over the partitions: R_p (from HBM) + the entering
+// pane's records of partition p - the leaving pane's records of partition p, folded in an LDS hash
+// table; every key whose window count is positive emits its row and goes back to HBM as R'_p.  Every
+// aggregate word is a wrap-around int64 sum (COUNT, SUM/AVG over int64): subtraction is exact.
+#pragma once
+#include <stdint.h>
+
+#include "gwo_internal.h"
+
+#define SLOG_THREADS 512
+#define SLOG_MAX_SEGS 64          // signed inputs of one window step (pane segments, restored partials)
+#define SLOG_SHARDS 16            // statistics shards (one 128-B line each)
+#define SLOG_STAT_STRIDE 16
+
+// One signed input of a window step: a pane segment (records (key, value), or keys only) or a restored
+// pane's partial accumulators (key + nwords raw words), grouped by the top `lp` bits of digit_hash.
+struct SlogSeg {
+    const int64_t *rec;
+    const uint32_t *off;          // [2^lp] first record of each partition
+    const uint32_t *cnt;          // [2^lp] records of each partition
+    int32_t lp;
+    int32_t sign;                 // +1: the pane enters the window, -1: it leaves
+    int32_t fmt;                  // 0: value records (has_val: key, value; else key), 1: key + nwords raw words
+    int32_t pad;
+};
+
+// The running total: partition q holds cnt[q] entries of (1 + nwords) words (key, words...) at
+// rec[q * rcap * (1 + nwords)].
+struct SlogRing {
+    int64_t *rec;
+    uint32_t *cnt;
+    uint64_t rcap;
+    int32_t lp;
+    int32_t pad;
+};
+
+// Statistics words per shard: live entries written, largest partition, R' capacity overflow, a negative
+// count (an inconsistent leave), LDS table overflow, partitions that took the range rounds.
+enum : int { SLS_LIVE = 0, SLS_MAXP, SLS_ROVF, SLS_NEG, SLS_LDS, SLS_SLOW, SLS_WORDS };
+
+struct SlogArgs {
+    SlogRing in, out;             // out.lp == in.lp (same partitions) or in.lp + 1 (each partition splits in two)
+    const SlogSeg *segs;
+    int32_t nseg;
+    int32_t has_val;
+    int32_t count_word;           // the word whose value > 0 marks a key present in the window
+    int32_t cap_log2;             // LDS table slots
+    int64_t start, end;           // the window being emitted
+    AccPlan p;
+    ResultPlan rp;
+    OutCols o;
+    unsigned long long *stat;     // [SLOG_SHARDS * SLOG_STAT_STRIDE]
+};
+
+namespace gwo {
+// Dynamic LDS bytes of the fire kernel for a table of 2^cap_log2 slots.
+size_t slog_lds_bytes(int cap_log2, int nwords);
+// One window step over every partition of a.in (persistent grid of `groups` workgroups).
+void launch_slog_fire(const SlogArgs &a, int groups, hipStream_t s);
+}  // namespace gwo

@@ -1,0 +1,384 @@
+// gwo_slog.hip -- the window step of sliding windows over logged panes (gwo_slog.h).
+//
+// WindowOperator.onEventTime + emitWindowContents (WindowOperator.java:430-473, 546-550) for every key of
+// sliding window J at once: the running total of window J-1 (R, partitioned by the top lp bits of
+// digit_hash, one HBM region per partition), the records of the pane that enters J and -- negated --
+// of the pane that leaves it, folded per partition in an LDS hash table; then every key whose count is
+// positive emits J's row and is written back as R' (keys whose count fell to zero leave the state:
+// the reference's window for that key holds no element, so it emits nothing).  All words are int64
+// sums (AggregateFunction add of SumFunction/CountAggregate/AverageAggregate; wrap-around as Java long),
+// an abelian group, so the result is bit-identical to summing the window's panes.
+//
+// One persistent workgroup of 512 threads takes partitions p = blockIdx.x, + gridDim.x, ...; every HBM
+// access is a run of consecutive records (R_p, the segments' partition slices, R'_p, the rows); the
+// only random accesses are LDS.  A partition with more keys than the LDS table holds is folded in
+// rounds over disjoint ranges of a second hash (each round re-reads the partition's inputs), so no key
+// is ever lost.
+#include "../../include/gwo.h"
+#include "gwo_device.h"
+#include "gwo_slog.h"
+
+namespace gwo {
+
+constexpr int SLOG_J = 4;   // records per thread per pass (loads of a pass are all in flight together)
+
+typedef __attribute__((address_space(1))) const int64_t g_i64;
+typedef __attribute__((address_space(1))) const uint32_t g_u32;
+
+size_t slog_lds_bytes(int cap_log2, int nwords) { return ((size_t)1 << cap_log2) * (size_t)(1 + nwords) * 8; }
+
+__device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+
+// Find or claim key k's slot (linear probing from h).  -1: the side slot (k == Long.MIN_VALUE, the
+// table's free marker); -2: no free slot.  A slot only goes EMPTY -> key inside a fold, so a plain read
+// that sees another key is final and a stale EMPTY is settled by the CAS.
+__device__ __forceinline__ int slog_find(int64_t *s_key, int T, int64_t k, uint32_t h, unsigned &claims) {
+    if (k == GWO_EMPTY_KEY) return -1;
+    int slot = (int)(h & (uint32_t)(T - 1));
+    for (int probes = 0; probes < T; ++probes) {
+        const int64_t cur = ((volatile int64_t *)s_key)[slot];
+        if (cur == k) return slot;
+        if (cur == GWO_EMPTY_KEY) {
+            const unsigned long long prev = atomicCAS((unsigned long long *)&s_key[slot],
+                                                      (unsigned long long)GWO_EMPTY_KEY, (unsigned long long)k);
+            if ((int64_t)prev == GWO_EMPTY_KEY) {
+                claims++;
+                return slot;
+            }
+            if ((int64_t)prev == k) return slot;
+        }
+        slot = (slot + 1) & (T - 1);
+    }
+    return -2;
+}
+
+template <int NW>
+__global__ __launch_bounds__(SLOG_THREADS) void slog_fire_kernel(SlogArgs a) {
+    extern __shared__ __attribute__((aligned(16))) int64_t s_dyn[];
+    const int T = 1 << a.cap_log2;
+    int64_t *const s_key = s_dyn;       // [T]
+    int64_t *const s_w = s_dyn + T;     // [NW][T]
+    __shared__ int64_t s_side[1 + GWO_MAX_WORDS];   // key == Long.MIN_VALUE: [present, words]
+    __shared__ unsigned s_used, s_fail;
+    // the partition's inputs as one flattened record space: range r covers [s_beg[r], s_beg[r + 1]) from
+    // record s_src[r] of s_ptr[r] (s_stride[r] words per record)
+    __shared__ const int64_t *s_ptr[SLOG_MAX_SEGS + 1];
+    __shared__ uint32_t s_beg[SLOG_MAX_SEGS + 2], s_src[SLOG_MAX_SEGS + 1];
+    __shared__ int32_t s_meta[SLOG_MAX_SEGS + 1];   // stride | words-to-load << 8 | raw << 12 | filter << 13 | neg << 14
+    __shared__ unsigned s_wsum[SLOG_THREADS / 64][2];
+    __shared__ unsigned s_qn[2];          // R' entries written so far for the partition's (one or two) outputs
+    __shared__ unsigned long long s_rowbase;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int lp_in = a.in.lp, split = a.out.lp - a.in.lp;   // 0 or 1
+    const uint32_t P = 1u << lp_in;
+    const int RW = 1 + NW;
+    const unsigned limit = (unsigned)(T - (T >> 3));
+    unsigned long long st_live = 0, st_maxp = 0, st_rovf = 0, st_neg = 0, st_lds = 0, st_slow = 0;
+
+    for (int i = tid; i < T; i += SLOG_THREADS) s_key[i] = GWO_EMPTY_KEY;
+    for (int i = tid; i < T * NW; i += SLOG_THREADS) s_w[i] = 0;
+    if (tid <= GWO_MAX_WORDS) s_side[tid] = 0;
+    if (tid == 0) {
+        s_used = 0;
+        s_fail = 0;
+    }
+    __syncthreads();
+
+    for (uint32_t p = blockIdx.x; p < P; p += gridDim.x) {
+        // ---- the partition's ranges: R_p, then each segment's slice (its partition p >> (lp_in - lp_s),
+        // filtered by the top lp_in bits when the segment is coarser) ----
+        if (wave == 0) {
+            uint32_t c = 0, src = 0;
+            const int r = lane;
+            if (r == 0) {
+                c = ((g_u32 *)a.in.cnt)[p];
+                s_ptr[0] = a.in.rec + (uint64_t)p * a.in.rcap * RW;
+                s_meta[0] = RW | (NW << 8) | (1 << 12);
+            } else if (r <= a.nseg) {
+                const SlogSeg sg = a.segs[r - 1];
+                const int d = lp_in - sg.lp;   // >= 0 (the host never gives a finer segment)
+                const uint32_t q = p >> d;
+                c = ((g_u32 *)sg.cnt)[q];
+                src = ((g_u32 *)sg.off)[q];
+                s_ptr[r] = sg.rec;
+                const int stride = sg.fmt ? RW : (a.has_val ? 2 : 1);
+                const int nl = sg.fmt ? NW : (a.has_val ? 1 : 0);
+                s_meta[r] = stride | (nl << 8) | (sg.fmt << 12) | ((d > 0) << 13) | ((sg.sign < 0) << 14);
+            }
+            uint32_t incl = c;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t y = __shfl_up(incl, o);
+                if (lane >= o) incl += y;
+            }
+            if (r <= a.nseg) {
+                s_beg[r] = incl - c;
+                s_src[r] = src;
+            }
+            if (r == a.nseg) s_beg[r + 1] = incl;
+            if (r == 0) {
+                s_qn[0] = 0;
+                s_qn[1] = 0;
+            }
+        }
+        __syncthreads();
+        const int nr = a.nseg + 1;
+        const uint32_t total = s_beg[nr];
+        uint64_t lo = 0, width = 1ull << 32;
+        bool slow = false;
+        while (lo < (1ull << 32)) {
+            const uint64_t hi = lo + width < (1ull << 32) ? lo + width : (1ull << 32);
+            const bool ranged = width < (1ull << 32);
+            unsigned claims = 0;
+            // ---- fold: every record of every range, SLOG_J per thread with all loads in flight ----
+            for (uint32_t base = 0; base < total; base += SLOG_THREADS * SLOG_J) {
+                int64_t rk[SLOG_J], rw[SLOG_J][NW];
+                int rr[SLOG_J];
+                // every record's range and address first (LDS only), then every load: global (not flat) loads,
+                // so the LDS waits in between do not wait for them
+                const int64_t *ea[SLOG_J];
+                int nlj[SLOG_J];
+#pragma unroll
+                for (int j = 0; j < SLOG_J; ++j) {
+                    const uint32_t i = base + j * SLOG_THREADS + tid;
+                    rr[j] = -1;
+                    ea[j] = s_ptr[0];
+                    nlj[j] = 0;
+                    if (i >= total) continue;
+                    int r = 0;
+                    for (int q = 1; q < nr; ++q) r += i >= s_beg[q];
+                    const int m = s_meta[r];
+                    ea[j] = s_ptr[r] + (uint64_t)(s_src[r] + (i - s_beg[r])) * (uint32_t)(m & 0xff);
+                    nlj[j] = (m >> 8) & 0xf;
+                    rr[j] = r;
+                }
+#pragma unroll
+                for (int j = 0; j < SLOG_J; ++j) {
+                    rk[j] = 0;
+#pragma unroll
+                    for (int w = 0; w < NW; ++w) rw[j][w] = 0;
+                    if (rr[j] < 0) continue;
+                    rk[j] = __builtin_nontemporal_load((g_i64 *)ea[j]);
+#pragma unroll
+                    for (int w = 0; w < NW; ++w)
+                        if (w < nlj[j]) rw[j][w] = __builtin_nontemporal_load((g_i64 *)ea[j] + 1 + w);
+                }
+#pragma unroll
+                for (int j = 0; j < SLOG_J; ++j) {
+                    if (rr[j] < 0) continue;
+                    const int m = s_meta[rr[j]];
+                    const int64_t k = rk[j];
+                    if (((m >> 13) & 1) && (digit_hash(k) >> (32 - lp_in)) != p) continue;
+                    const uint64_t ph = part_hash(k);
+                    if (ranged) {
+                        const uint64_t sub = (uint32_t)ph;
+                        if (sub < lo || sub >= hi) continue;
+                    }
+                    const int slot = slog_find(s_key, T, k, (uint32_t)(ph >> 32), claims);
+                    if (slot == -2) {
+                        s_fail = 1;
+                        continue;
+                    }
+                    int64_t *dst = slot >= 0 ? s_w + slot : s_side + 1;
+                    const int ds = slot >= 0 ? T : 1;
+                    if (slot < 0) s_side[0] = 1;
+                    const bool raw = (m >> 12) & 1, neg = (m >> 14) & 1;
+#pragma unroll
+                    for (int w = 0; w < NW; ++w) {
+                        int64_t x = raw ? rw[j][w] : lift_word(a.p, w, rw[j][0]);
+                        x = neg ? (int64_t)(0ull - (uint64_t)x) : x;
+                        atomicAdd((unsigned long long *)(dst + w * ds), (unsigned long long)x);
+                    }
+                }
+            }
+            const unsigned long long cw = wave_sum_u64(claims);
+            if (lane == 0 && cw) atomicAdd(&s_used, (unsigned)cw);
+            __syncthreads();
+            const bool failed = s_fail != 0 || s_used > limit;
+            __syncthreads();
+            if (failed) {   // more keys in range than the table holds: reset, halve the range
+                for (int i = tid; i < T; i += SLOG_THREADS) s_key[i] = GWO_EMPTY_KEY;
+                for (int i = tid; i < T * NW; i += SLOG_THREADS) s_w[i] = 0;
+                if (tid <= GWO_MAX_WORDS) s_side[tid] = 0;
+                if (tid == 0) {
+                    s_used = 0;
+                    s_fail = 0;
+                }
+                __syncthreads();
+                slow = true;
+                width >>= 1;
+                if (width == 0) {
+                    st_lds++;
+                    break;
+                }
+                continue;
+            }
+            // ---- sweep: live keys -> rows of window J and R'; every slot reset for the next fold ----
+            constexpr int SPT = 8;   // slots per thread per sweep round (T <= 4096)
+            int slotv[SPT];
+            uint32_t cnt0 = 0, cnt1 = 0, code = 0;   // code bit 2i: slot i live, bit 2i+1: its output half
+#pragma unroll
+            for (int i = 0; i < SPT; ++i) {
+                const int s = tid + i * SLOG_THREADS;
+                slotv[i] = s;
+                if (s >= T) continue;
+                const int64_t k = s_key[s];
+                if (k == GWO_EMPTY_KEY) continue;
+                const int64_t c = s_w[a.count_word * T + s];
+                if (c < 0) st_neg++;
+                if (c <= 0) {   // the key left the window: its slot is simply reset
+                    s_key[s] = GWO_EMPTY_KEY;
+#pragma unroll
+                    for (int w = 0; w < NW; ++w) s_w[w * T + s] = 0;
+                    continue;
+                }
+                const uint32_t half = split ? (digit_hash(k) >> (31 - lp_in)) & 1u : 0u;
+                code |= (1u | (half << 1)) << (2 * i);
+                if (half) cnt1++;
+                else cnt0++;
+            }
+            bool side_live = false;
+            uint32_t side_half = 0;
+            if (tid == 0 && s_side[0]) {
+                const int64_t c = s_side[1 + a.count_word];
+                if (c < 0) st_neg++;
+                if (c > 0) {
+                    side_live = true;
+                    side_half = split ? (digit_hash(GWO_EMPTY_KEY) >> (31 - lp_in)) & 1u : 0u;
+                    if (side_half) cnt1++;
+                    else cnt0++;
+                }
+            }
+            // workgroup scan of (cnt0, cnt1) packed in one word (each < 2^16)
+            const uint32_t v = cnt0 | (cnt1 << 16);
+            uint32_t incl = v;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t y = __shfl_up(incl, o);
+                if (lane >= o) incl += y;
+            }
+            if (lane == 63) s_wsum[wave][0] = incl;
+            __syncthreads();
+            uint32_t pre = 0, tot = 0;
+#pragma unroll
+            for (int w = 0; w < SLOG_THREADS / 64; ++w) {
+                const uint32_t x = s_wsum[w][0];
+                pre += w < wave ? x : 0u;
+                tot += x;
+            }
+            const uint32_t ex = pre + incl - v;   // this thread's first positions (low: half 0, high: half 1)
+            const uint32_t tot0 = tot & 0xffffu, tot1 = tot >> 16;
+            if (tid == 0) s_rowbase = (tot0 + tot1) ? atomicAdd(a.o.count, (unsigned long long)(tot0 + tot1)) : 0ull;
+            __syncthreads();
+            const unsigned long long rowbase = s_rowbase;
+            const uint32_t qb0 = s_qn[0], qb1 = s_qn[1];
+            uint32_t at0 = ex & 0xffffu, at1 = ex >> 16;
+            const uint32_t qout0 = split ? 2 * p : p;
+            auto emit = [&](int64_t k, const int64_t *wp, int ws, uint32_t half) {
+                const uint32_t local = half ? at1++ : at0++;
+                const uint32_t qpos = (half ? qb1 : qb0) + local;
+                const uint32_t q = qout0 + half;
+                // rows: half-0 keys first, then half-1 keys, in the partition's reserved run
+                const unsigned long long r = rowbase + (half ? tot0 + local : local);
+                int64_t acc[NW];
+#pragma unroll
+                for (int w = 0; w < NW; ++w) acc[w] = wp[w * ws];
+                if (qpos < a.out.rcap) {
+                    int64_t *e = a.out.rec + ((uint64_t)q * a.out.rcap + qpos) * RW;
+                    e[0] = k;
+#pragma unroll
+                    for (int w = 0; w < NW; ++w) e[1 + w] = acc[w];
+                }
+                if ((long long)r < a.o.cap) {
+                    a.o.key[r] = k;
+                    a.o.start[r] = a.start;
+                    a.o.end[r] = a.end;
+#pragma unroll
+                    for (int g = 0; g < 4; ++g) {
+                        if (g >= a.rp.naggs) break;
+                        const int wi = a.rp.word[g];
+                        int64_t x = acc[0], y = acc[0];
+#pragma unroll
+                        for (int w = 1; w < NW; ++w) {
+                            if (w == wi) x = acc[w];
+                            if (w == wi + 1) y = acc[w];
+                        }
+                        a.o.res[g][r] = a.rp.kind[g] == GWO_AGG_AVG
+                                            ? __double_as_longlong((double)x / (double)y)
+                                            : x;
+                    }
+                }
+            };
+            if (side_live) emit(GWO_EMPTY_KEY, s_side + 1, 1, side_half);
+#pragma unroll
+            for (int i = 0; i < SPT; ++i) {
+                if (!((code >> (2 * i)) & 1u)) continue;
+                const int s = slotv[i];
+                emit(s_key[s], s_w + s, T, (code >> (2 * i + 1)) & 1u);
+                s_key[s] = GWO_EMPTY_KEY;
+#pragma unroll
+                for (int w = 0; w < NW; ++w) s_w[w * T + s] = 0;
+            }
+            __syncthreads();   // every read of s_qn, s_side and s_used is done
+            if (tid == 0) {
+                s_qn[0] = qb0 + tot0;
+                s_qn[1] = qb1 + tot1;
+                s_used = 0;
+            }
+            if (tid <= GWO_MAX_WORDS) s_side[tid] = 0;
+            __syncthreads();
+            lo = hi;
+        }
+        if (slow) st_slow++;
+        if (tid == 0) {
+            const uint32_t n0 = s_qn[0], n1 = s_qn[1];
+            const uint32_t q0 = split ? 2 * p : p;
+            a.out.cnt[q0] = n0 < a.out.rcap ? n0 : (uint32_t)a.out.rcap;
+            if (split) a.out.cnt[q0 + 1] = n1 < a.out.rcap ? n1 : (uint32_t)a.out.rcap;
+            if (n0 > a.out.rcap || n1 > a.out.rcap) st_rovf++;
+            st_live += n0 + n1;
+            const unsigned long long mq = n0 > n1 ? n0 : n1;
+            st_maxp = mq > st_maxp ? mq : st_maxp;
+        }
+        __syncthreads();   // s_beg / s_qn are rewritten for the next partition
+    }
+    // statistics -> shard blockIdx % SLOG_SHARDS
+    const unsigned long long nl = wave_sum_u64(st_neg);
+    if (lane == 0 && nl) atomicAdd(&a.stat[(blockIdx.x % SLOG_SHARDS) * SLOG_STAT_STRIDE + SLS_NEG], nl);
+    if (tid == 0) {
+        unsigned long long *sh = a.stat + (blockIdx.x % SLOG_SHARDS) * SLOG_STAT_STRIDE;
+        if (st_live) atomicAdd(sh + SLS_LIVE, st_live);
+        if (st_maxp) atomicMax(sh + SLS_MAXP, st_maxp);
+        if (st_rovf) atomicAdd(sh + SLS_ROVF, st_rovf);
+        if (st_lds) atomicAdd(sh + SLS_LDS, st_lds);
+        if (st_slow) atomicAdd(sh + SLS_SLOW, st_slow);
+    }
+}
+
+void launch_slog_fire(const SlogArgs &a, int groups, hipStream_t s) {
+    const size_t lds = slog_lds_bytes(a.cap_log2, a.p.nwords);
+    const uint32_t P = 1u << a.in.lp;
+    const int grid = (int)(P < (uint32_t)groups ? P : (uint32_t)groups);
+#define GWO_SLOG(NW)                                                                                    \
+    case NW:                                                                                            \
+        hipLaunchKernelGGL(slog_fire_kernel<NW>, dim3(grid), dim3(SLOG_THREADS), lds, s, a);             \
+        break;
+    switch (a.p.nwords) {
+        GWO_SLOG(1)
+        GWO_SLOG(2)
+        GWO_SLOG(3)
+        GWO_SLOG(4)
+        GWO_SLOG(5)
+        GWO_SLOG(6)
+        GWO_SLOG(7)
+        GWO_SLOG(8)
+        default: break;
+    }
+#undef GWO_SLOG
+}
+
+}  // namespace gwo

@@ -135,7 +135,8 @@ def _compare(counts, sums, kept, want_rows, want_cs, rows, naggs):
             assert torch.equal(got[c], want[c]), f"step {b} column {c}"
 
 
-def test_c3_sliding_10m_keys_full_scale(F):
+@pytest.mark.parametrize("layout", ["table", "log"])
+def test_c3_sliding_10m_keys_full_scale(F, layout):
     import torch
     from flink_amd import _native as N
     R, span, nkeys = 200_000_000, 120_000, 10_000_000
@@ -149,7 +150,8 @@ def test_c3_sliding_10m_keys_full_scale(F):
         mx = max(mx, int(th[s * per:(s + 1) * per].max()))
         wms.append(mx - 1000 - 1)
     batches = [((s + 1) * per, wms[s]) for s in range(steps)] + [(n, LONG_MAX)]
-    op = F.GpuWindowOperator(F.SlidingEventTimeWindows.of(60_000, 1000), F.AverageAggregate(), max_parallelism=128)
+    op = F.GpuWindowOperator(F.SlidingEventTimeWindows.of(60_000, 1000), F.AverageAggregate(), max_parallelism=128,
+                             state_layout=layout, expected_keys=nkeys if layout == "log" else 0)
     keep = {59, 60, 61}   # the watermark steps that fire windows [-1 s, 59 s), [0, 60 s), [1 s, 61 s) ...
     counts, sums, kept = _run_steps(N, op.handle, key, ts, val, batches, 1, keep)
     late_gpu = op.num_late_records_dropped

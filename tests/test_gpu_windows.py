@@ -203,10 +203,15 @@ def test_table_layout_hot_keys_wave_prereduction(F, vdt):
     op.close()
 
 
-def test_log_layout_rejected_for_sliding(F):
+def test_log_layout_rejected_for_sliding_min_and_sessions(F):
+    """Sliding windows take the log layout only with invertible (int64 sum) aggregates (tests/test_gpu_sliding_log.py);
+    sessions never."""
     from flink_amd import _native as N
     with pytest.raises(N.GwoError) as ei:
-        F.GpuWindowOperator(F.SlidingEventTimeWindows.of(3000, 1000), F.SumAggregate(), state_layout="log")
+        F.GpuWindowOperator(F.SlidingEventTimeWindows.of(3000, 1000), F.MinAggregate(), state_layout="log")
+    assert ei.value.status_name == "GWO_ERR_UNSUPPORTED"
+    with pytest.raises(N.GwoError) as ei:
+        F.GpuWindowOperator(F.EventTimeSessionWindows.withGap(3000), F.SumAggregate(), state_layout="log")
     assert ei.value.status_name == "GWO_ERR_UNSUPPORTED"
 
 
