@@ -205,6 +205,103 @@ void Handle::slog_release_before(long long first_pane) {
     }
 }
 
+// One launch of a window step over segments h_segs[s0, s1): R' = R + those segments (rows only when `emit`).
+gwo_status Handle::slog_step(int64_t start, int64_t end, uint64_t bound, size_t s0, size_t s1, bool emit, bool fresh) {
+    SlideState &S = *slide;
+    SlogState &G = *slog;
+    const int NW = plan.nwords, RW = 1 + NW;
+        // R' geometry: the partitions split when the largest one nears the LDS table
+        const int in = G.cur, outb = 1 - G.cur;
+        const int lp_in = fresh ? G.lp : G.rlp[in];
+        const int lp_out = (G.split_next && lp_in < LOG_MAX_LP) ? lp_in + 1 : lp_in;
+        const uint64_t Pout = 1ull << lp_out;
+        uint64_t rcap = slog_capacity((double)bound / (double)Pout);
+        if (G.ring[outb].bytes < Pout * rcap * RW * 8)
+            GWO_TRY(ensure_buf(G.ring[outb], (size_t)((double)(Pout * rcap * RW * 8) * 1.5)));
+        rcap = G.ring[outb].bytes / (Pout * RW * 8);   // use all of it
+        if (emit) GWO_TRY(ensure_output(bound));
+        GWO_TRY(hipcheck(hipMemcpyAsync(G.segdesc.ptr, G.h_segs.data() + s0, (s1 - s0) * sizeof(SlogSeg),
+                                        hipMemcpyHostToDevice, stream), "slog segments"));
+        if (fresh)   // R is empty: every partition of the input reads zero entries
+            GWO_TRY(hipcheck(hipMemsetAsync(G.cnt[in], 0, ((size_t)1 << lp_in) * 4, stream), "ring reset"));
+        SlogArgs a{};
+        a.in = SlogRing{(int64_t *)G.ring[in].ptr, G.cnt[in], G.rcap[in], lp_in, 0};
+        a.out = SlogRing{(int64_t *)G.ring[outb].ptr, G.cnt[outb], rcap, lp_out, 0};
+        a.segs = (const SlogSeg *)G.segdesc.ptr;
+        a.nseg = (int)(s1 - s0);
+        a.emit = emit ? 1 : 0;
+        a.has_val = needs_value ? 1 : 0;
+        a.count_word = S.count_word;
+        a.cap_log2 = G.cap_log2;
+        a.start = start;
+        a.end = end;
+        a.p = plan;
+        a.rp = rplan;
+        a.stat = G.d_stat;
+        static int trace = getenv("GWO_SLOG_TRACE") ? atoi(getenv("GWO_SLOG_TRACE")) : 0;
+        static unsigned long long *d_dbg = nullptr;
+        if (trace && !d_dbg) (void)hipMalloc((void **)&d_dbg, 32 * 8 * 8);
+        a.dbg = trace ? d_dbg : nullptr;
+        static int mode = getenv("GWO_SLOG_MODE") ? atoi(getenv("GWO_SLOG_MODE")) : 0;
+        a.mode = mode;
+        const uint64_t rows0 = out_rows;
+        for (int attempt = 0;; ++attempt) {
+            a.o = out_cols();
+            GWO_TRY(hipcheck(hipMemsetAsync(G.d_stat, 0, SLOG_SHARDS * SLOG_STAT_STRIDE * 8, stream), "ring stats"));
+            prof_begin(GWO_KERNEL_FIRE);
+            launch_slog_fire(a, G.groups, stream);
+            GWO_TRY(launch_ok("slog window step"));
+            prof_end(GWO_KERNEL_FIRE, (int64_t)bound);
+            GWO_TRY(hipcheck(hipMemcpyAsync(G.h_stat, G.d_stat, SLOG_SHARDS * SLOG_STAT_STRIDE * 8,
+                                            hipMemcpyDeviceToHost, stream), "ring stats"));
+            GWO_TRY(hipcheck(hipStreamSynchronize(stream), "slog window step"));
+            uint64_t st[SLS_WORDS] = {};
+            for (int q = 0; q < SLOG_SHARDS; ++q)
+                for (int w = 0; w < SLS_WORDS; ++w) {
+                    const uint64_t x = G.h_stat[q * SLOG_STAT_STRIDE + w];
+                    st[w] = w == SLS_MAXP ? std::max(st[w], x) : st[w] + x;
+                }
+            if (st[SLS_NEG] && !mode) return poison(GWO_ERR_HIP, "sliding log: a key's window count became negative");
+            if (st[SLS_LDS]) return poison(GWO_ERR_CAPACITY, "sliding log: a partition overflowed its LDS table");
+            if (st[SLS_ROVF]) {   // a partition of R' outgrew its region: larger regions, same step again
+                if (attempt >= 4) return poison(GWO_ERR_CAPACITY, "sliding log: running-total partition overflow");
+                rcap = std::max<uint64_t>(rcap * 2, st[SLS_MAXP] + st[SLS_MAXP] / 4 + 64);
+                GWO_TRY(ensure_buf(G.ring[outb], Pout * rcap * RW * 8));
+                a.out.rec = (int64_t *)G.ring[outb].ptr;
+                a.out.rcap = rcap;
+                *h_scalar = rows0;
+                GWO_TRY(hipcheck(hipMemcpyAsync(d_out_count, h_scalar, 8, hipMemcpyHostToDevice, stream), "row rewind"));
+                continue;
+            }
+            if (debug)
+                fprintf(stderr, "[gwo] slog window %lld: segs=%zu live=%llu maxp=%llu slow=%llu lp %d->%d\n",
+                        (long long)start, G.h_segs.size(), (unsigned long long)st[SLS_LIVE],
+                        (unsigned long long)st[SLS_MAXP], (unsigned long long)st[SLS_SLOW], lp_in, lp_out);
+            G.live = st[SLS_LIVE];
+            G.maxp = st[SLS_MAXP];
+            if (trace && (S.J % 16) == 0) {   // phase times of workgroup 0 (device wall clock, 100 MHz)
+                unsigned long long h[32 * 8];
+                (void)hipMemcpy(h, d_dbg, sizeof h, hipMemcpyDeviceToHost);
+                fprintf(stderr, "[slog] window %lld slow=%llu maxp=%llu:", (long long)start, (unsigned long long)st[SLS_SLOW],
+                        (unsigned long long)st[SLS_MAXP]);
+                for (int q = 0; q < 16; ++q)
+                    fprintf(stderr, " [%lld %lld+%lld %lld %lld %lld %lld]", (long long)(h[q * 8 + 1] - h[q * 8]),
+                            (long long)(h[q * 8 + 7] - h[q * 8 + 1]), (long long)(h[q * 8 + 2] - h[q * 8 + 7]), (long long)(h[q * 8 + 3] - h[q * 8 + 2]),
+                            (long long)(h[q * 8 + 4] - h[q * 8 + 3]), (long long)(h[q * 8 + 5] - h[q * 8 + 4]),
+                            (long long)(h[q * 8 + 6] - h[q * 8 + 5]));
+                fprintf(stderr, "\n");
+            }
+            break;
+        }
+        if (emit) out_rows = rows0 + G.live;
+        G.cur = outb;
+        G.rcap[outb] = rcap;
+        G.rlp[outb] = lp_out;
+        G.lp = lp_out;   // new panes are logged at R's partitioning
+        G.split_next = (double)G.maxp > 0.75 * (double)(1 << G.cap_log2);
+    return GWO_OK;
+}
+
 // Window steps for every window whose maxTimestamp the watermark passed (EventTimeTrigger.onEventTime FIRE,
 // InternalTimerServiceImpl.advanceWatermark fires timers in timestamp order: window J before J + 1).
 gwo_status Handle::fire_slog(int64_t new_wm) {
@@ -220,7 +317,6 @@ gwo_status Handle::fire_slog(int64_t new_wm) {
         S.j_set = true;
         G.rebuild = true;
     }
-    const int NW = plan.nwords, RW = 1 + NW;
     while (S.J < j_new) {
         long long lo = win_first_pane(S.J), hi = win_last_pane(S.J);
         G.h_segs.clear();
@@ -269,9 +365,10 @@ gwo_status Handle::fire_slog(int64_t new_wm) {
         }
         G.pending.clear();
         G.pending_records = 0;
-        if (G.h_segs.size() > SLOG_MAX_SEGS)
-            return poison(GWO_ERR_CAPACITY, "sliding log: a window step has more than 64 pane segments; use the "
-                                            "table layout for batches that span that many panes");
+        // more segments than one step takes (a rebuild over a whole window, many small batches per pane): chunks
+        // of SLOG_MAX_SEGS, entering segments first, so a key's count only falls towards its final value; only the
+        // last chunk emits rows
+        std::stable_sort(G.h_segs.begin(), G.h_segs.end(), [](const SlogSeg &x, const SlogSeg &y) { return x.sign > y.sign; });
         const int64_t start = win_start(S.J);
         const int64_t end = (int64_t)((uint64_t)start + (uint64_t)cfg.size);
         const uint64_t bound = G.live + plus_records;
@@ -284,76 +381,12 @@ gwo_status Handle::fire_slog(int64_t new_wm) {
             S.J += 1;
             continue;
         }
-        // R' geometry: the partitions split when the largest one nears the LDS table
-        const int in = G.cur, outb = 1 - G.cur;
-        const int lp_in = G.rebuild ? G.lp : G.rlp[in];
-        const int lp_out = (G.split_next && lp_in < LOG_MAX_LP) ? lp_in + 1 : lp_in;
-        const uint64_t Pout = 1ull << lp_out;
-        uint64_t rcap = slog_capacity((double)bound / (double)Pout);
-        if (G.ring[outb].bytes < Pout * rcap * RW * 8)
-            GWO_TRY(ensure_buf(G.ring[outb], (size_t)((double)(Pout * rcap * RW * 8) * 1.5)));
-        rcap = G.ring[outb].bytes / (Pout * RW * 8);   // use all of it
-        GWO_TRY(ensure_output(bound));
-        GWO_TRY(hipcheck(hipMemcpyAsync(G.segdesc.ptr, G.h_segs.data(), G.h_segs.size() * sizeof(SlogSeg),
-                                        hipMemcpyHostToDevice, stream), "slog segments"));
-        if (G.rebuild)   // R is empty: every partition of the input reads zero entries
-            GWO_TRY(hipcheck(hipMemsetAsync(G.cnt[in], 0, ((size_t)1 << lp_in) * 4, stream), "ring reset"));
-        SlogArgs a{};
-        a.in = SlogRing{(int64_t *)G.ring[in].ptr, G.cnt[in], G.rcap[in], lp_in, 0};
-        a.out = SlogRing{(int64_t *)G.ring[outb].ptr, G.cnt[outb], rcap, lp_out, 0};
-        a.segs = (const SlogSeg *)G.segdesc.ptr;
-        a.nseg = (int)G.h_segs.size();
-        a.has_val = needs_value ? 1 : 0;
-        a.count_word = S.count_word;
-        a.cap_log2 = G.cap_log2;
-        a.start = start;
-        a.end = end;
-        a.p = plan;
-        a.rp = rplan;
-        a.stat = G.d_stat;
-        const uint64_t rows0 = out_rows;
-        for (int attempt = 0;; ++attempt) {
-            a.o = out_cols();
-            GWO_TRY(hipcheck(hipMemsetAsync(G.d_stat, 0, SLOG_SHARDS * SLOG_STAT_STRIDE * 8, stream), "ring stats"));
-            prof_begin(GWO_KERNEL_FIRE);
-            launch_slog_fire(a, G.groups, stream);
-            GWO_TRY(launch_ok("slog window step"));
-            prof_end(GWO_KERNEL_FIRE, (int64_t)bound);
-            GWO_TRY(hipcheck(hipMemcpyAsync(G.h_stat, G.d_stat, SLOG_SHARDS * SLOG_STAT_STRIDE * 8,
-                                            hipMemcpyDeviceToHost, stream), "ring stats"));
-            GWO_TRY(hipcheck(hipStreamSynchronize(stream), "slog window step"));
-            uint64_t st[SLS_WORDS] = {};
-            for (int q = 0; q < SLOG_SHARDS; ++q)
-                for (int w = 0; w < SLS_WORDS; ++w) {
-                    const uint64_t x = G.h_stat[q * SLOG_STAT_STRIDE + w];
-                    st[w] = w == SLS_MAXP ? std::max(st[w], x) : st[w] + x;
-                }
-            if (st[SLS_NEG]) return poison(GWO_ERR_HIP, "sliding log: a key's window count became negative");
-            if (st[SLS_LDS]) return poison(GWO_ERR_CAPACITY, "sliding log: a partition overflowed its LDS table");
-            if (st[SLS_ROVF]) {   // a partition of R' outgrew its region: larger regions, same step again
-                if (attempt >= 4) return poison(GWO_ERR_CAPACITY, "sliding log: running-total partition overflow");
-                rcap = std::max<uint64_t>(rcap * 2, st[SLS_MAXP] + st[SLS_MAXP] / 4 + 64);
-                GWO_TRY(ensure_buf(G.ring[outb], Pout * rcap * RW * 8));
-                a.out.rec = (int64_t *)G.ring[outb].ptr;
-                a.out.rcap = rcap;
-                *h_scalar = rows0;
-                GWO_TRY(hipcheck(hipMemcpyAsync(d_out_count, h_scalar, 8, hipMemcpyHostToDevice, stream), "row rewind"));
-                continue;
-            }
-            if (debug)
-                fprintf(stderr, "[gwo] slog window %lld: segs=%zu live=%llu maxp=%llu slow=%llu lp %d->%d\n",
-                        (long long)start, G.h_segs.size(), (unsigned long long)st[SLS_LIVE],
-                        (unsigned long long)st[SLS_MAXP], (unsigned long long)st[SLS_SLOW], lp_in, lp_out);
-            G.live = st[SLS_LIVE];
-            G.maxp = st[SLS_MAXP];
-            break;
+        const size_t nchunks = std::max<size_t>(1, (G.h_segs.size() + SLOG_MAX_SEGS - 1) / SLOG_MAX_SEGS);
+        for (size_t ch = 0; ch < nchunks; ++ch) {
+            const bool last = ch + 1 == nchunks;
+            const size_t s0 = ch * SLOG_MAX_SEGS, s1 = std::min(G.h_segs.size(), s0 + SLOG_MAX_SEGS);
+            GWO_TRY(slog_step(start, end, bound, s0, s1, last, ch == 0 && G.rebuild));
         }
-        out_rows = rows0 + G.live;
-        G.cur = outb;
-        G.rcap[outb] = rcap;
-        G.rlp[outb] = lp_out;
-        G.lp = lp_out;   // new panes are logged at R's partitioning
-        G.split_next = (double)G.maxp > 0.75 * (double)(1 << G.cap_log2);
         G.rebuild = G.live == 0;
         for (long long u : leaving) {
             log_release(L.wins[u]);

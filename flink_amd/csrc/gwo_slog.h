@@ -56,6 +56,9 @@ struct SlogArgs {
     ResultPlan rp;
     OutCols o;
     unsigned long long *stat;     // [SLOG_SHARDS * SLOG_STAT_STRIDE]
+    unsigned long long *dbg;      // optional phase timestamps of workgroup 0 (GWO_SLOG_TRACE)
+    int32_t mode;                 // diagnostics only (GWO_SLOG_MODE): 1 no probe, 2 no word atomics
+    int32_t emit;                 // 0: an intermediate step of a chunked window step (R' only, no rows)
 };
 
 namespace gwo {

@@ -33,25 +33,41 @@ __device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v)
     return v;
 }
 
-// Find or claim key k's slot (linear probing from h).  -1: the side slot (k == Long.MIN_VALUE, the
-// table's free marker); -2: no free slot.  A slot only goes EMPTY -> key inside a fold, so a plain read
-// that sees another key is final and a stale EMPTY is settled by the CAS.
+// Find or claim key k's slot in a table of 8-slot buckets (home bucket from h, then the next buckets).  -1: the side
+// slot (k == Long.MIN_VALUE, the table's free marker); -2: no free slot.  A probe reads a bucket's 8 keys with
+// workgroup-scope atomic loads (LDS reads, issued together: one round trip) and claims the first free slot with one
+// CAS; a slot only goes EMPTY -> key inside a fold, so a key read is final and a stale EMPTY is settled by the CAS.
+// (Linear probing one slot per round trip at load 0.6: a wave waited for its slowest lane's cluster -- ~12 us per
+// partition in the C3 window step.)
 __device__ __forceinline__ int slog_find(int64_t *s_key, int T, int64_t k, uint32_t h, unsigned &claims) {
     if (k == GWO_EMPTY_KEY) return -1;
-    int slot = (int)(h & (uint32_t)(T - 1));
-    for (int probes = 0; probes < T; ++probes) {
-        const int64_t cur = ((volatile int64_t *)s_key)[slot];
-        if (cur == k) return slot;
-        if (cur == GWO_EMPTY_KEY) {
-            const unsigned long long prev = atomicCAS((unsigned long long *)&s_key[slot],
-                                                      (unsigned long long)GWO_EMPTY_KEY, (unsigned long long)k);
-            if ((int64_t)prev == GWO_EMPTY_KEY) {
-                claims++;
-                return slot;
-            }
-            if ((int64_t)prev == k) return slot;
+    const int nb = T >> 3;
+    int b = (int)(h & (uint32_t)(nb - 1));
+    for (int probes = 0; probes < 2 * nb;) {
+        int64_t kb[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+            kb[i] = __hip_atomic_load(&s_key[b * 8 + i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        int hit = -1, fr = -1;
+#pragma unroll
+        for (int i = 7; i >= 0; --i) {
+            if (kb[i] == k) hit = i;
+            if (kb[i] == GWO_EMPTY_KEY) fr = i;
         }
-        slot = (slot + 1) & (T - 1);
+        if (hit >= 0) return b * 8 + hit;
+        if (fr < 0) {   // bucket full: the next one
+            b = (b + 1) & (nb - 1);
+            ++probes;
+            continue;
+        }
+        const unsigned long long prev = atomicCAS((unsigned long long *)&s_key[b * 8 + fr],
+                                                  (unsigned long long)GWO_EMPTY_KEY, (unsigned long long)k);
+        if ((int64_t)prev == GWO_EMPTY_KEY) {
+            claims++;
+            return b * 8 + fr;
+        }
+        if ((int64_t)prev == k) return b * 8 + fr;
+        ++probes;   // another key took that slot: read the bucket again
     }
     return -2;
 }
@@ -88,7 +104,12 @@ __global__ __launch_bounds__(SLOG_THREADS) void slog_fire_kernel(SlogArgs a) {
     }
     __syncthreads();
 
-    for (uint32_t p = blockIdx.x; p < P; p += gridDim.x) {
+    int pn = 0;
+    auto stamp = [&](int ph) {
+        if (a.dbg && blockIdx.x == 0 && tid == 0 && pn < 32) a.dbg[pn * 8 + ph] = wall_clock64();
+    };
+    for (uint32_t p = blockIdx.x; p < P; p += gridDim.x, ++pn) {
+        stamp(0);
         // ---- the partition's ranges: R_p, then each segment's slice (its partition p >> (lp_in - lp_s),
         // filtered by the top lp_in bits when the segment is coarser) ----
         if (wave == 0) {
@@ -126,6 +147,7 @@ __global__ __launch_bounds__(SLOG_THREADS) void slog_fire_kernel(SlogArgs a) {
             }
         }
         __syncthreads();
+        stamp(1);
         const int nr = a.nseg + 1;
         const uint32_t total = s_beg[nr];
         uint64_t lo = 0, width = 1ull << 32;
@@ -167,6 +189,10 @@ __global__ __launch_bounds__(SLOG_THREADS) void slog_fire_kernel(SlogArgs a) {
                     for (int w = 0; w < NW; ++w)
                         if (w < nlj[j]) rw[j][w] = __builtin_nontemporal_load((g_i64 *)ea[j] + 1 + w);
                 }
+                if (a.dbg && blockIdx.x == 0 && pn < 32 && base == 0) {   // trace: the loads of the first pass landed
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    if (tid == 0) a.dbg[pn * 8 + 7] = wall_clock64();
+                }
 #pragma unroll
                 for (int j = 0; j < SLOG_J; ++j) {
                     if (rr[j] < 0) continue;
@@ -178,7 +204,8 @@ __global__ __launch_bounds__(SLOG_THREADS) void slog_fire_kernel(SlogArgs a) {
                         const uint64_t sub = (uint32_t)ph;
                         if (sub < lo || sub >= hi) continue;
                     }
-                    const int slot = slog_find(s_key, T, k, (uint32_t)(ph >> 32), claims);
+                    const int slot = (a.mode & 1) ? (int)((uint32_t)(ph >> 32) & (uint32_t)(T - 1))
+                                                  : slog_find(s_key, T, k, (uint32_t)(ph >> 32), claims);
                     if (slot == -2) {
                         s_fail = 1;
                         continue;
@@ -187,6 +214,7 @@ __global__ __launch_bounds__(SLOG_THREADS) void slog_fire_kernel(SlogArgs a) {
                     const int ds = slot >= 0 ? T : 1;
                     if (slot < 0) s_side[0] = 1;
                     const bool raw = (m >> 12) & 1, neg = (m >> 14) & 1;
+                    if (a.mode & 2) continue;
 #pragma unroll
                     for (int w = 0; w < NW; ++w) {
                         int64_t x = raw ? rw[j][w] : lift_word(a.p, w, rw[j][0]);
@@ -195,6 +223,7 @@ __global__ __launch_bounds__(SLOG_THREADS) void slog_fire_kernel(SlogArgs a) {
                     }
                 }
             }
+            stamp(2);
             const unsigned long long cw = wave_sum_u64(claims);
             if (lane == 0 && cw) atomicAdd(&s_used, (unsigned)cw);
             __syncthreads();
@@ -217,6 +246,7 @@ __global__ __launch_bounds__(SLOG_THREADS) void slog_fire_kernel(SlogArgs a) {
                 }
                 continue;
             }
+            stamp(3);
             // ---- sweep: live keys -> rows of window J and R'; every slot reset for the next fold ----
             constexpr int SPT = 8;   // slots per thread per sweep round (T <= 4096)
             int slotv[SPT];
@@ -272,8 +302,9 @@ __global__ __launch_bounds__(SLOG_THREADS) void slog_fire_kernel(SlogArgs a) {
             }
             const uint32_t ex = pre + incl - v;   // this thread's first positions (low: half 0, high: half 1)
             const uint32_t tot0 = tot & 0xffffu, tot1 = tot >> 16;
-            if (tid == 0) s_rowbase = (tot0 + tot1) ? atomicAdd(a.o.count, (unsigned long long)(tot0 + tot1)) : 0ull;
+            if (tid == 0) s_rowbase = (a.emit && tot0 + tot1) ? atomicAdd(a.o.count, (unsigned long long)(tot0 + tot1)) : 0ull;
             __syncthreads();
+            stamp(4);
             const unsigned long long rowbase = s_rowbase;
             const uint32_t qb0 = s_qn[0], qb1 = s_qn[1];
             uint32_t at0 = ex & 0xffffu, at1 = ex >> 16;
@@ -293,7 +324,7 @@ __global__ __launch_bounds__(SLOG_THREADS) void slog_fire_kernel(SlogArgs a) {
 #pragma unroll
                     for (int w = 0; w < NW; ++w) e[1 + w] = acc[w];
                 }
-                if ((long long)r < a.o.cap) {
+                if (a.emit && (long long)r < a.o.cap) {
                     a.o.key[r] = k;
                     a.o.start[r] = a.start;
                     a.o.end[r] = a.end;
@@ -323,6 +354,7 @@ __global__ __launch_bounds__(SLOG_THREADS) void slog_fire_kernel(SlogArgs a) {
 #pragma unroll
                 for (int w = 0; w < NW; ++w) s_w[w * T + s] = 0;
             }
+            stamp(5);
             __syncthreads();   // every read of s_qn, s_side and s_used is done
             if (tid == 0) {
                 s_qn[0] = qb0 + tot0;
@@ -345,6 +377,7 @@ __global__ __launch_bounds__(SLOG_THREADS) void slog_fire_kernel(SlogArgs a) {
             st_maxp = mq > st_maxp ? mq : st_maxp;
         }
         __syncthreads();   // s_beg / s_qn are rewritten for the next partition
+        stamp(6);
     }
     // statistics -> shard blockIdx % SLOG_SHARDS
     const unsigned long long nl = wave_sum_u64(st_neg);

@@ -230,3 +230,31 @@ def test_sliding_log_sharded_union(F):
         op.close()
     (wk, ws, we, res), _ = V.sliding_lateness0(k, t, v, _final(b), 10_000, 1_000, 0, [1])
     assert sorted(rows) == _want(wk, ws, we, res)
+
+
+def test_sliding_log_many_small_batches_and_restore_rebuild(F):
+    """Batches of 150 records: ~20 segments per pane, so a window step (entering + leaving pane) and the rebuild
+    after a restore (every pane of a 20-pane window) take more segments than one launch holds -- chunked steps,
+    entering segments first, rows from the last chunk only."""
+    k, t, v, _ = _stream(60_000, 2_000, 150, 300, 300, 51, span=20_000)
+    b = G.punctuated_watermarks(t, 150, 300)
+    agg = F.MultiAggregate(F.SumAggregate(), F.CountAggregate())
+    (wk, ws, we, res), late = V.sliding_lateness0(k, t, v, _final(b), 20_000, 1_000, 0, [1, 0])
+    want = _want(wk, ws, we, res)
+    mk = lambda: F.GpuWindowOperator(F.SlidingEventTimeWindows.of(20_000, 1_000), agg, state_layout="log")
+    op = mk()
+    _run(op, k, t, v, b)
+    assert _got(op) == want and op.num_late_records_dropped == late
+    op.close()
+    cut = len(b) // 2
+    a = mk()
+    prev = _run(a, k, t, v, b[:cut], end_input=False)
+    snap = a.snapshot_state()
+    rows, late_a = list(a.output), a.num_late_records_dropped
+    a.close()
+    c = mk()
+    c.restore_state(snap)
+    _run(c, k, t, v, b[cut:], start=prev)
+    assert sorted((x, s, e, *r) for x, s, e, r in rows + list(c.output)) == want
+    assert late_a + c.num_late_records_dropped == late
+    c.close()
