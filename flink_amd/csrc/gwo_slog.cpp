@@ -31,6 +31,7 @@ struct SlogState {
     int cap_log2 = 11;             // LDS table slots of the window step
     bool split_next = false;       // the next window step writes R' at lp + 1
     DevBuf ring[2];                // R (in) and R' (out) alternate
+    DevBuf bkt[2];                 // their bucket bytes ([2^lp][nb])
     uint32_t *cnt[2] = {nullptr, nullptr};   // [2^LOG_MAX_LP] entries per partition
     uint64_t rcap[2] = {0, 0};
     int rlp[2] = {0, 0};
@@ -43,7 +44,7 @@ struct SlogState {
     unsigned long long *d_stat = nullptr, *h_stat = nullptr;
     DevBuf segdesc;
     std::vector<SlogSeg> h_segs;
-    int groups = 0;
+    int groups = 0;                // CUs
     bool reserved = false;
 };
 
@@ -71,8 +72,10 @@ WindowGeom Handle::log_geom_now() const {
 gwo_status Handle::slog_init() {
     slog = new SlogState();
     SlogState &G = *slog;
-    int c = 12;
-    while (c > 8 && slog_lds_bytes(c, plan.nwords) > 64 * 1024) c--;
+    // a table of <= 32 KiB (1024 slots for avg's two words; the sweep's slots per thread: 2..8) so about five
+    // workgroups share a CU and overlap their partitions' HBM round trips
+    int c = 11;
+    while (c > 9 && slog_lds_bytes(c, plan.nwords) > 32 * 1024) c--;
     G.cap_log2 = c;
     // R partitions: ~0.6 of the LDS table per partition at the caller's distinct-key hint (or the first batch)
     const double per = 0.6 * (double)(1 << c);
@@ -91,7 +94,7 @@ gwo_status Handle::slog_init() {
     GWO_TRY(ensure_buf(G.segdesc, SLOG_MAX_SEGS * sizeof(SlogSeg)));
     int cus = 0;
     GWO_TRY(hipcheck(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, cfg.device), "CU count"));
-    G.groups = std::max(cus, 1) * 2;
+    G.groups = std::max(cus, 1);   // CUs (the launcher multiplies by the kernel's occupancy)
     if (cfg.expected_keys > 0) {   // R and R' for the hinted key count, so the steady state allocates nothing
         const uint64_t P = 1ull << G.lp;
         const uint64_t rcap = slog_capacity(1.25 * (double)cfg.expected_keys / (double)P);
@@ -101,10 +104,12 @@ gwo_status Handle::slog_init() {
         }
         GWO_TRY(ensure_output((uint64_t)cfg.expected_keys + (uint64_t)cfg.expected_keys / 4 + 4096));
     }
+    const size_t nb = ((size_t)1 << G.cap_log2) / 8;
+    for (int i = 0; i < 2; ++i) GWO_TRY(ensure_buf(G.bkt[i], ((size_t)1 << G.lp) * nb));
     // the window step's code object: one partition, no entries, no segments (HIP loads a kernel on its first launch)
     SlogArgs a{};
-    a.in = SlogRing{nullptr, G.cnt[0], 0, 0, 0};
-    a.out = SlogRing{nullptr, G.cnt[1], 0, 0, 0};
+    a.in = SlogRing{nullptr, G.cnt[0], (uint8_t *)G.bkt[0].ptr, 0, 0, 0};
+    a.out = SlogRing{nullptr, G.cnt[1], (uint8_t *)G.bkt[1].ptr, 0, 0, 0};
     a.p = plan;
     a.rp = rplan;
     a.count_word = slide->count_word;
@@ -121,6 +126,7 @@ void Handle::slog_free() {
     SlogState &G = *slog;
     for (int i = 0; i < 2; ++i) {
         G.ring[i].release();
+        G.bkt[i].release();
         if (G.cnt[i]) (void)hipFree(G.cnt[i]);
     }
     G.segdesc.release();
@@ -219,14 +225,15 @@ gwo_status Handle::slog_step(int64_t start, int64_t end, uint64_t bound, size_t 
         if (G.ring[outb].bytes < Pout * rcap * RW * 8)
             GWO_TRY(ensure_buf(G.ring[outb], (size_t)((double)(Pout * rcap * RW * 8) * 1.5)));
         rcap = G.ring[outb].bytes / (Pout * RW * 8);   // use all of it
+        GWO_TRY(ensure_buf(G.bkt[outb], (size_t)Pout * (((size_t)1 << G.cap_log2) / 8)));
         if (emit) GWO_TRY(ensure_output(bound));
         GWO_TRY(hipcheck(hipMemcpyAsync(G.segdesc.ptr, G.h_segs.data() + s0, (s1 - s0) * sizeof(SlogSeg),
                                         hipMemcpyHostToDevice, stream), "slog segments"));
         if (fresh)   // R is empty: every partition of the input reads zero entries
             GWO_TRY(hipcheck(hipMemsetAsync(G.cnt[in], 0, ((size_t)1 << lp_in) * 4, stream), "ring reset"));
         SlogArgs a{};
-        a.in = SlogRing{(int64_t *)G.ring[in].ptr, G.cnt[in], G.rcap[in], lp_in, 0};
-        a.out = SlogRing{(int64_t *)G.ring[outb].ptr, G.cnt[outb], rcap, lp_out, 0};
+        a.in = SlogRing{(int64_t *)G.ring[in].ptr, G.cnt[in], (uint8_t *)G.bkt[in].ptr, G.rcap[in], lp_in, 0};
+        a.out = SlogRing{(int64_t *)G.ring[outb].ptr, G.cnt[outb], (uint8_t *)G.bkt[outb].ptr, rcap, lp_out, 0};
         a.segs = (const SlogSeg *)G.segdesc.ptr;
         a.nseg = (int)(s1 - s0);
         a.emit = emit ? 1 : 0;
@@ -285,10 +292,9 @@ gwo_status Handle::slog_step(int64_t start, int64_t end, uint64_t bound, size_t 
                 fprintf(stderr, "[slog] window %lld slow=%llu maxp=%llu:", (long long)start, (unsigned long long)st[SLS_SLOW],
                         (unsigned long long)st[SLS_MAXP]);
                 for (int q = 0; q < 16; ++q)
-                    fprintf(stderr, " [%lld %lld+%lld %lld %lld %lld %lld]", (long long)(h[q * 8 + 1] - h[q * 8]),
-                            (long long)(h[q * 8 + 7] - h[q * 8 + 1]), (long long)(h[q * 8 + 2] - h[q * 8 + 7]), (long long)(h[q * 8 + 3] - h[q * 8 + 2]),
-                            (long long)(h[q * 8 + 4] - h[q * 8 + 3]), (long long)(h[q * 8 + 5] - h[q * 8 + 4]),
-                            (long long)(h[q * 8 + 6] - h[q * 8 + 5]));
+                    fprintf(stderr, " [%lld %lld %lld %lld %lld]", (long long)(h[q * 8 + 1] - h[q * 8]),
+                            (long long)(h[q * 8 + 2] - h[q * 8 + 1]), (long long)(h[q * 8 + 3] - h[q * 8 + 2]),
+                            (long long)(h[q * 8 + 4] - h[q * 8 + 3]), (long long)(h[q * 8 + 5] - h[q * 8 + 4]));
                 fprintf(stderr, "\n");
             }
             break;

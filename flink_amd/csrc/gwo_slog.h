@@ -13,7 +13,7 @@
 
 #include "gwo_internal.h"
 
-#define SLOG_THREADS 512
+#define SLOG_THREADS 256         // a small workgroup: ~5 per CU keep that many partitions' HBM round trips in flight
 #define SLOG_MAX_SEGS 64          // signed inputs of one window step (pane segments, restored partials)
 #define SLOG_SHARDS 16            // statistics shards (one 128-B line each)
 #define SLOG_STAT_STRIDE 16
@@ -30,15 +30,22 @@ struct SlogSeg {
     int32_t pad;
 };
 
-// The running total: partition q holds cnt[q] entries of (1 + nwords) words (key, words...) at
-// rec[q * rcap * (1 + nwords)].
+// The running total: partition q holds cnt[q] entries in the region rec[q * rcap * (1 + nwords)] as SoA columns
+// (keys[rcap], then each word's [rcap]), in the order of the window step's LDS table buckets (8 slots each, bucket of a
+// key = slog_bucket_hash); bkt[q * nb + b] = the entries of bucket b (bits 0-3) | bucket b overflowed (bit 4: a
+// key was displaced past it, so a search may not stop there).  The next window step places every entry straight
+// into its bucket -- no hashing, probing or atomics for the running total, only for the panes' records.  cnt[q]
+// bit 31: the partition is unstructured (written by the range rounds): its entries are probed like records.
 struct SlogRing {
     int64_t *rec;
     uint32_t *cnt;
+    uint8_t *bkt;
     uint64_t rcap;
     int32_t lp;
     int32_t pad;
 };
+#define SLOG_UNSTRUCT 0x80000000u
+#define SLOG_MAX_NB 256           // buckets of the LDS table at most (2048 slots)
 
 // Statistics words per shard: live entries written, largest partition, R' capacity overflow, a negative
 // count (an inconsistent leave), LDS table overflow, partitions that took the range rounds.
@@ -64,6 +71,6 @@ struct SlogArgs {
 namespace gwo {
 // Dynamic LDS bytes of the fire kernel for a table of 2^cap_log2 slots.
 size_t slog_lds_bytes(int cap_log2, int nwords);
-// One window step over every partition of a.in (persistent grid of `groups` workgroups).
-void launch_slog_fire(const SlogArgs &a, int groups, hipStream_t s);
+// One window step over every partition of a.in (persistent grid: every workgroup resident on the `cus` CUs).
+void launch_slog_fire(const SlogArgs &a, int cus, hipStream_t s);
 }  // namespace gwo

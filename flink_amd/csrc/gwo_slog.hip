@@ -9,23 +9,35 @@
 // sums (AggregateFunction add of SumFunction/CountAggregate/AverageAggregate; wrap-around as Java long),
 // an abelian group, so the result is bit-identical to summing the window's panes.
 //
-// One persistent workgroup of 512 threads takes partitions p = blockIdx.x, + gridDim.x, ...; every HBM
-// access is a run of consecutive records (R_p, the segments' partition slices, R'_p, the rows); the
-// only random accesses are LDS.  A partition with more keys than the LDS table holds is folded in
-// rounds over disjoint ranges of a second hash (each round re-reads the partition's inputs), so no key
-// is ever lost.
+// The LDS table is made of 8-slot buckets.  R' is written bucket by bucket with a byte per bucket (entries,
+// overflow flag), so the next step puts each entry of R straight into its bucket: the running total -- about
+// three quarters of a step's records at C3 -- costs no hash, probe or atomic; only the panes' records search
+// the table (bucket reads, one CAS to claim a new key, word atomics).  (Hashing and probing every entry made
+// the step VALU-issue bound: ~33K VALU instructions per wave, LDS bank conflicts 54 % of the LDS cycles.)
+//
+// One persistent workgroup of 256 threads takes partitions p = blockIdx.x, + gridDim.x, ...; every HBM
+// access is a run of consecutive records (R_p, the segments' partition slices, R'_p, the rows).  A partition
+// with more keys than the table holds is folded in rounds over disjoint ranges of a second hash (each round
+// re-reads the partition's inputs; its R' is then written unstructured), so no key is ever lost.
 #include "../../include/gwo.h"
 #include "gwo_device.h"
 #include "gwo_slog.h"
 
 namespace gwo {
 
-constexpr int SLOG_J = 4;   // records per thread per pass (loads of a pass are all in flight together)
+constexpr int SLOG_J = 4;     // records per thread per pass (the loads of a pass are all in flight together)
 
 typedef __attribute__((address_space(1))) const int64_t g_i64;
 typedef __attribute__((address_space(1))) const uint32_t g_u32;
+typedef __attribute__((address_space(1))) const uint8_t g_u8;
 
 size_t slog_lds_bytes(int cap_log2, int nwords) { return ((size_t)1 << cap_log2) * (size_t)(1 + nwords) * 8; }
+
+// Bucket of a key: a multiplicative hash of both halves, independent of the partition bits (digit_hash) and of lp,
+// so a partition split keeps every key's bucket.
+__device__ __forceinline__ uint32_t slog_bucket(int64_t k, int nbits) {
+    return ((uint32_t)k * 0x9E3779B1u + (uint32_t)((uint64_t)k >> 32) * 0x85EBCA77u) >> (32 - nbits);
+}
 
 __device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v) {
 #pragma unroll
@@ -33,59 +45,67 @@ __device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v)
     return v;
 }
 
-// Find or claim key k's slot in a table of 8-slot buckets (home bucket from h, then the next buckets).  -1: the side
-// slot (k == Long.MIN_VALUE, the table's free marker); -2: no free slot.  A probe reads a bucket's 8 keys with
-// workgroup-scope atomic loads (LDS reads, issued together: one round trip) and claims the first free slot with one
-// CAS; a slot only goes EMPTY -> key inside a fold, so a key read is final and a stale EMPTY is settled by the CAS.
-// (Linear probing one slot per round trip at load 0.6: a wave waited for its slowest lane's cluster -- ~12 us per
-// partition in the C3 window step.)
-__device__ __forceinline__ int slog_find(int64_t *s_key, int T, int64_t k, uint32_t h, unsigned &claims) {
+__device__ __forceinline__ int64_t lds_key(const int64_t *s_key, int slot) {
+    return __hip_atomic_load(&s_key[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// Find or claim key k's slot.  The search reads whole buckets (8 LDS reads, one round trip) from the key's home
+// bucket on, and ends at the first bucket that has a free slot and no overflow flag (a key displaced past a
+// bucket set that bucket's flag when it found the bucket full); a new key is claimed, with one CAS, in the first
+// free slot the search met -- every lane claiming k targets the same slot, so a key is never claimed twice (a
+// failed CAS restarts the search).  -1: the side slot (k == Long.MIN_VALUE, the free marker); -2: table full.
+__device__ __forceinline__ int slog_find(int64_t *s_key, uint8_t *s_ovf, int NB, int nbits, int64_t k,
+                                         unsigned &claims) {
     if (k == GWO_EMPTY_KEY) return -1;
-    const int nb = T >> 3;
-    int b = (int)(h & (uint32_t)(nb - 1));
-    for (int probes = 0; probes < 2 * nb;) {
-        int64_t kb[8];
+    const int home = (int)slog_bucket(k, nbits);
+    for (int attempt = 0; attempt < 64; ++attempt) {
+        int b = home, ff = -1;
+        for (int steps = 0; steps < NB; ++steps) {
+            int64_t kb[8];
 #pragma unroll
-        for (int i = 0; i < 8; ++i)
-            kb[i] = __hip_atomic_load(&s_key[b * 8 + i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        int hit = -1, fr = -1;
+            for (int i = 0; i < 8; ++i) kb[i] = lds_key(s_key, b * 8 + i);
+            int hit = -1, fr = -1;
 #pragma unroll
-        for (int i = 7; i >= 0; --i) {
-            if (kb[i] == k) hit = i;
-            if (kb[i] == GWO_EMPTY_KEY) fr = i;
+            for (int i = 7; i >= 0; --i) {
+                if (kb[i] == k) hit = i;
+                if (kb[i] == GWO_EMPTY_KEY) fr = i;
+            }
+            if (hit >= 0) return b * 8 + hit;
+            if (fr >= 0 && ff < 0) ff = b * 8 + fr;
+            if (fr >= 0 && !s_ovf[b]) break;
+            if (fr < 0) s_ovf[b] = 1;   // full: a key placed beyond it is displaced past it
+            b = (b + 1) & (NB - 1);
         }
-        if (hit >= 0) return b * 8 + hit;
-        if (fr < 0) {   // bucket full: the next one
-            b = (b + 1) & (nb - 1);
-            ++probes;
-            continue;
-        }
-        const unsigned long long prev = atomicCAS((unsigned long long *)&s_key[b * 8 + fr],
-                                                  (unsigned long long)GWO_EMPTY_KEY, (unsigned long long)k);
+        if (ff < 0) return -2;
+        const unsigned long long prev = atomicCAS((unsigned long long *)&s_key[ff], (unsigned long long)GWO_EMPTY_KEY,
+                                                  (unsigned long long)k);
         if ((int64_t)prev == GWO_EMPTY_KEY) {
             claims++;
-            return b * 8 + fr;
+            return ff;
         }
-        if ((int64_t)prev == k) return b * 8 + fr;
-        ++probes;   // another key took that slot: read the bucket again
+        if ((int64_t)prev == k) return ff;
     }
     return -2;
 }
 
 template <int NW>
-__global__ __launch_bounds__(SLOG_THREADS) void slog_fire_kernel(SlogArgs a) {
+__global__ __launch_bounds__(SLOG_THREADS) __attribute__((amdgpu_waves_per_eu(4, 4))) void slog_fire_kernel(SlogArgs a) {
     extern __shared__ __attribute__((aligned(16))) int64_t s_dyn[];
-    const int T = 1 << a.cap_log2;
+    const int T = 1 << a.cap_log2, NB = T >> 3, nbits = a.cap_log2 - 3, SPT = T / SLOG_THREADS;
     int64_t *const s_key = s_dyn;       // [T]
     int64_t *const s_w = s_dyn + T;     // [NW][T]
     __shared__ int64_t s_side[1 + GWO_MAX_WORDS];   // key == Long.MIN_VALUE: [present, words]
-    __shared__ unsigned s_used, s_fail;
-    // the partition's inputs as one flattened record space: range r covers [s_beg[r], s_beg[r + 1]) from
-    // record s_src[r] of s_ptr[r] (s_stride[r] words per record)
+    __shared__ unsigned s_used, s_fail, s_rn;
+    // the partition's record inputs as one flattened record space: range r covers [s_beg[r], s_beg[r + 1]) from
+    // record s_src[r] of s_ptr[r]; range 0 is R_p when it is unstructured (else empty: its entries are placed)
     __shared__ const int64_t *s_ptr[SLOG_MAX_SEGS + 1];
     __shared__ uint32_t s_beg[SLOG_MAX_SEGS + 2], s_src[SLOG_MAX_SEGS + 1];
     __shared__ int32_t s_meta[SLOG_MAX_SEGS + 1];   // stride | words-to-load << 8 | raw << 12 | filter << 13 | neg << 14
-    __shared__ unsigned s_wsum[SLOG_THREADS / 64][2];
+    __shared__ uint8_t s_ovf[SLOG_MAX_NB];          // the fold's overflow flags (R's, and those its inserts set)
+    __shared__ uint8_t s_map[SLOG_MAX_NB * 9];      // R_p entry -> its bucket (a bucket holds <= 8 + the side entry)
+    __shared__ uint16_t s_pre[SLOG_MAX_NB];         // first R_p entry of each bucket
+    __shared__ uint8_t s_ovo[2][SLOG_MAX_NB];       // R''s, recomputed from the keys' displacement by the sweep
+    __shared__ unsigned s_wsum[SLOG_THREADS / 64];
     __shared__ unsigned s_qn[2];          // R' entries written so far for the partition's (one or two) outputs
     __shared__ unsigned long long s_rowbase;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -93,11 +113,16 @@ __global__ __launch_bounds__(SLOG_THREADS) void slog_fire_kernel(SlogArgs a) {
     const uint32_t P = 1u << lp_in;
     const int RW = 1 + NW;
     const unsigned limit = (unsigned)(T - (T >> 3));
+    const int side_bucket = (int)slog_bucket(GWO_EMPTY_KEY, nbits);
     unsigned long long st_live = 0, st_maxp = 0, st_rovf = 0, st_neg = 0, st_lds = 0, st_slow = 0;
 
     for (int i = tid; i < T; i += SLOG_THREADS) s_key[i] = GWO_EMPTY_KEY;
     for (int i = tid; i < T * NW; i += SLOG_THREADS) s_w[i] = 0;
     if (tid <= GWO_MAX_WORDS) s_side[tid] = 0;
+    if (tid < SLOG_MAX_NB) {
+        s_ovo[0][tid] = 0;
+        s_ovo[1][tid] = 0;
+    }
     if (tid == 0) {
         s_used = 0;
         s_fail = 0;
@@ -110,15 +135,17 @@ __global__ __launch_bounds__(SLOG_THREADS) void slog_fire_kernel(SlogArgs a) {
     };
     for (uint32_t p = blockIdx.x; p < P; p += gridDim.x, ++pn) {
         stamp(0);
-        // ---- the partition's ranges: R_p, then each segment's slice (its partition p >> (lp_in - lp_s),
-        // filtered by the top lp_in bits when the segment is coarser) ----
+        // ---- the partition's ranges: each segment's slice (its partition p >> (lp_in - lp_s), filtered by the top
+        // lp_in bits when the segment is coarser), and R_p's entry count ----
         if (wave == 0) {
             uint32_t c = 0, src = 0;
             const int r = lane;
             if (r == 0) {
-                c = ((g_u32 *)a.in.cnt)[p];
+                const uint32_t rn = ((g_u32 *)a.in.cnt)[p];
+                s_rn = rn;
+                c = (rn & SLOG_UNSTRUCT) ? (rn & ~SLOG_UNSTRUCT) : 0u;
                 s_ptr[0] = a.in.rec + (uint64_t)p * a.in.rcap * RW;
-                s_meta[0] = RW | (NW << 8) | (1 << 12);
+                s_meta[0] = 1 | (NW << 8) | (1 << 12) | (1 << 15);   // SoA columns of rcap words
             } else if (r <= a.nseg) {
                 const SlogSeg sg = a.segs[r - 1];
                 const int d = lp_in - sg.lp;   // >= 0 (the host never gives a finer segment)
@@ -148,6 +175,7 @@ __global__ __launch_bounds__(SLOG_THREADS) void slog_fire_kernel(SlogArgs a) {
         }
         __syncthreads();
         stamp(1);
+        const bool structured = !(s_rn & SLOG_UNSTRUCT);
         const int nr = a.nseg + 1;
         const uint32_t total = s_beg[nr];
         uint64_t lo = 0, width = 1ull << 32;
@@ -155,8 +183,75 @@ __global__ __launch_bounds__(SLOG_THREADS) void slog_fire_kernel(SlogArgs a) {
         while (lo < (1ull << 32)) {
             const uint64_t hi = lo + width < (1ull << 32) ? lo + width : (1ull << 32);
             const bool ranged = width < (1ull << 32);
+            auto in_range = [&](int64_t k) {
+                const uint64_t sub = (uint32_t)part_hash(k);
+                return !ranged || (sub >= lo && sub < hi);
+            };
             unsigned claims = 0;
-            // ---- fold: every record of every range, SLOG_J per thread with all loads in flight ----
+            // ---- R_p placed into its buckets (structured): the bucket bytes give each entry's bucket (an LDS map
+            // entry -> bucket), then thread t loads entries t, t + 256, ... -- coalesced SoA columns ----
+            {
+                uint32_t c = 0;
+                const uint32_t rcount = structured ? (s_rn & ~SLOG_UNSTRUCT) : 0u;
+                if (tid < NB) {
+                    const uint32_t byte = rcount ? ((g_u8 *)a.in.bkt)[(size_t)p * NB + tid] : 0u;
+                    c = byte & 15u;
+                    s_ovf[tid] = (uint8_t)((byte >> 4) & 1u);
+                }
+                uint32_t incl = c;
+#pragma unroll
+                for (int o = 1; o < 64; o <<= 1) {
+                    const uint32_t y = __shfl_up(incl, o);
+                    if (lane >= o) incl += y;
+                }
+                if (lane == 63) s_wsum[wave] = incl;
+                __syncthreads();
+                uint32_t pre = incl - c;
+                for (int w = 0; w < wave; ++w) pre += s_wsum[w];
+                if (tid < NB) {
+                    s_pre[tid] = (uint16_t)pre;
+                    for (uint32_t j = 0; j < c; ++j) s_map[pre + j] = (uint8_t)tid;
+                }
+                __syncthreads();
+                const int64_t *col = a.in.rec + (uint64_t)p * a.in.rcap * RW;   // keys[rcap], then each word's column
+                unsigned placed = 0;
+                for (uint32_t base = 0; base < rcount; base += SLOG_THREADS * 4) {
+                    int64_t ek[4], ew[4][NW];
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const uint32_t i = base + j * SLOG_THREADS + tid;
+                        ek[j] = 0;
+#pragma unroll
+                        for (int w = 0; w < NW; ++w) ew[j][w] = 0;
+                        if (i >= rcount) continue;
+                        ek[j] = __builtin_nontemporal_load((g_i64 *)col + i);
+#pragma unroll
+                        for (int w = 0; w < NW; ++w)
+                            ew[j][w] = __builtin_nontemporal_load((g_i64 *)col + (uint64_t)(1 + w) * a.in.rcap + i);
+                    }
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const uint32_t i = base + j * SLOG_THREADS + tid;
+                        if (i >= rcount || !in_range(ek[j])) continue;
+                        if (ek[j] == GWO_EMPTY_KEY) {   // Long.MIN_VALUE: the side slot
+                            s_side[0] = 1;
+#pragma unroll
+                            for (int w = 0; w < NW; ++w) s_side[1 + w] = ew[j][w];
+                            continue;
+                        }
+                        const uint32_t b = s_map[i];
+                        const int slot = (int)(b * 8 + (i - s_pre[b]));
+                        s_key[slot] = ek[j];
+#pragma unroll
+                        for (int w = 0; w < NW; ++w) s_w[w * T + slot] = ew[j][w];
+                        placed++;
+                    }
+                }
+                claims += placed;
+            }
+            __syncthreads();
+            stamp(2);
+            // ---- fold: the segments' records (and R_p when unstructured), SLOG_J per thread, loads in flight ----
             for (uint32_t base = 0; base < total; base += SLOG_THREADS * SLOG_J) {
                 int64_t rk[SLOG_J], rw[SLOG_J][NW];
                 int rr[SLOG_J];
@@ -175,7 +270,7 @@ __global__ __launch_bounds__(SLOG_THREADS) void slog_fire_kernel(SlogArgs a) {
                     for (int q = 1; q < nr; ++q) r += i >= s_beg[q];
                     const int m = s_meta[r];
                     ea[j] = s_ptr[r] + (uint64_t)(s_src[r] + (i - s_beg[r])) * (uint32_t)(m & 0xff);
-                    nlj[j] = (m >> 8) & 0xf;
+                    nlj[j] = ((m >> 8) & 0xf) | (((m >> 15) & 1) << 4);
                     rr[j] = r;
                 }
 #pragma unroll
@@ -185,13 +280,11 @@ __global__ __launch_bounds__(SLOG_THREADS) void slog_fire_kernel(SlogArgs a) {
                     for (int w = 0; w < NW; ++w) rw[j][w] = 0;
                     if (rr[j] < 0) continue;
                     rk[j] = __builtin_nontemporal_load((g_i64 *)ea[j]);
+                    const uint64_t wstride = (nlj[j] >> 4) ? a.in.rcap : 1u;   // R's SoA columns, or record words
 #pragma unroll
                     for (int w = 0; w < NW; ++w)
-                        if (w < nlj[j]) rw[j][w] = __builtin_nontemporal_load((g_i64 *)ea[j] + 1 + w);
-                }
-                if (a.dbg && blockIdx.x == 0 && pn < 32 && base == 0) {   // trace: the loads of the first pass landed
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                    if (tid == 0) a.dbg[pn * 8 + 7] = wall_clock64();
+                        if (w < (nlj[j] & 0xf))
+                            rw[j][w] = __builtin_nontemporal_load((g_i64 *)ea[j] + (uint64_t)(1 + w) * wstride);
                 }
 #pragma unroll
                 for (int j = 0; j < SLOG_J; ++j) {
@@ -199,13 +292,8 @@ __global__ __launch_bounds__(SLOG_THREADS) void slog_fire_kernel(SlogArgs a) {
                     const int m = s_meta[rr[j]];
                     const int64_t k = rk[j];
                     if (((m >> 13) & 1) && (digit_hash(k) >> (32 - lp_in)) != p) continue;
-                    const uint64_t ph = part_hash(k);
-                    if (ranged) {
-                        const uint64_t sub = (uint32_t)ph;
-                        if (sub < lo || sub >= hi) continue;
-                    }
-                    const int slot = (a.mode & 1) ? (int)((uint32_t)(ph >> 32) & (uint32_t)(T - 1))
-                                                  : slog_find(s_key, T, k, (uint32_t)(ph >> 32), claims);
+                    if (!in_range(k)) continue;
+                    const int slot = slog_find(s_key, s_ovf, NB, nbits, k, claims);
                     if (slot == -2) {
                         s_fail = 1;
                         continue;
@@ -214,7 +302,6 @@ __global__ __launch_bounds__(SLOG_THREADS) void slog_fire_kernel(SlogArgs a) {
                     const int ds = slot >= 0 ? T : 1;
                     if (slot < 0) s_side[0] = 1;
                     const bool raw = (m >> 12) & 1, neg = (m >> 14) & 1;
-                    if (a.mode & 2) continue;
 #pragma unroll
                     for (int w = 0; w < NW; ++w) {
                         int64_t x = raw ? rw[j][w] : lift_word(a.p, w, rw[j][0]);
@@ -223,7 +310,7 @@ __global__ __launch_bounds__(SLOG_THREADS) void slog_fire_kernel(SlogArgs a) {
                     }
                 }
             }
-            stamp(2);
+            stamp(3);
             const unsigned long long cw = wave_sum_u64(claims);
             if (lane == 0 && cw) atomicAdd(&s_used, (unsigned)cw);
             __syncthreads();
@@ -246,16 +333,13 @@ __global__ __launch_bounds__(SLOG_THREADS) void slog_fire_kernel(SlogArgs a) {
                 }
                 continue;
             }
-            stamp(3);
-            // ---- sweep: live keys -> rows of window J and R'; every slot reset for the next fold ----
-            constexpr int SPT = 8;   // slots per thread per sweep round (T <= 4096)
-            int slotv[SPT];
+            // ---- sweep: thread t takes slots [t * SPT, (t + 1) * SPT) (one bucket part), so R' comes out bucket by
+            // bucket; live keys -> rows of window J and R'; every slot reset for the next fold ----
+            const bool out_struct = !slow;   // range rounds write R' unstructured
+            const int b_t = (tid * SPT) >> 3;   // this thread's bucket
             uint32_t cnt0 = 0, cnt1 = 0, code = 0;   // code bit 2i: slot i live, bit 2i+1: its output half
-#pragma unroll
             for (int i = 0; i < SPT; ++i) {
-                const int s = tid + i * SLOG_THREADS;
-                slotv[i] = s;
-                if (s >= T) continue;
+                const int s = tid * SPT + i;
                 const int64_t k = s_key[s];
                 if (k == GWO_EMPTY_KEY) continue;
                 const int64_t c = s_w[a.count_word * T + s];
@@ -270,10 +354,14 @@ __global__ __launch_bounds__(SLOG_THREADS) void slog_fire_kernel(SlogArgs a) {
                 code |= (1u | (half << 1)) << (2 * i);
                 if (half) cnt1++;
                 else cnt0++;
+                // a key displaced from its home bucket: every bucket it passed is flagged in its output table
+                const int home = (int)slog_bucket(k, nbits);
+                for (int bb = home; bb != b_t; bb = (bb + 1) & (NB - 1)) s_ovo[half][bb] = 1;
             }
+            // the side entry (Long.MIN_VALUE) goes out with its bucket, before that bucket's slots
             bool side_live = false;
             uint32_t side_half = 0;
-            if (tid == 0 && s_side[0]) {
+            if (tid == (side_bucket * 8) / SPT && s_side[0]) {
                 const int64_t c = s_side[1 + a.count_word];
                 if (c < 0) st_neg++;
                 if (c > 0) {
@@ -291,40 +379,60 @@ __global__ __launch_bounds__(SLOG_THREADS) void slog_fire_kernel(SlogArgs a) {
                 const uint32_t y = __shfl_up(incl, o);
                 if (lane >= o) incl += y;
             }
-            if (lane == 63) s_wsum[wave][0] = incl;
-            __syncthreads();
+            if (lane == 63) s_wsum[wave] = incl;
+            __syncthreads();   // (also: every s_ovo flag is set)
             uint32_t pre = 0, tot = 0;
 #pragma unroll
             for (int w = 0; w < SLOG_THREADS / 64; ++w) {
-                const uint32_t x = s_wsum[w][0];
+                const uint32_t x = s_wsum[w];
                 pre += w < wave ? x : 0u;
                 tot += x;
             }
             const uint32_t ex = pre + incl - v;   // this thread's first positions (low: half 0, high: half 1)
             const uint32_t tot0 = tot & 0xffffu, tot1 = tot >> 16;
             if (tid == 0) s_rowbase = (a.emit && tot0 + tot1) ? atomicAdd(a.o.count, (unsigned long long)(tot0 + tot1)) : 0ull;
-            __syncthreads();
-            stamp(4);
-            const unsigned long long rowbase = s_rowbase;
             const uint32_t qb0 = s_qn[0], qb1 = s_qn[1];
-            uint32_t at0 = ex & 0xffffu, at1 = ex >> 16;
             const uint32_t qout0 = split ? 2 * p : p;
-            auto emit = [&](int64_t k, const int64_t *wp, int ws, uint32_t half) {
-                const uint32_t local = half ? at1++ : at0++;
-                const uint32_t qpos = (half ? qb1 : qb0) + local;
-                const uint32_t q = qout0 + half;
-                // rows: half-0 keys first, then half-1 keys, in the partition's reserved run
-                const unsigned long long r = rowbase + (half ? tot0 + local : local);
-                int64_t acc[NW];
-#pragma unroll
-                for (int w = 0; w < NW; ++w) acc[w] = wp[w * ws];
-                if (qpos < a.out.rcap) {
-                    int64_t *e = a.out.rec + ((uint64_t)q * a.out.rcap + qpos) * RW;
-                    e[0] = k;
-#pragma unroll
-                    for (int w = 0; w < NW; ++w) e[1 + w] = acc[w];
+            // R''s bucket bytes: the first thread of each bucket sums the bucket's threads (consecutive lanes)
+            if (out_struct) {
+                uint32_t bc = v;
+                for (int o = 1; o < 8 / SPT; o <<= 1) bc += __shfl_xor(bc, o);
+                if (((tid * SPT) & 7) == 0) {
+                    uint8_t *ob = a.out.bkt + (size_t)qout0 * NB + b_t;
+                    ob[0] = (uint8_t)((bc & 0xffffu) | ((uint32_t)s_ovo[0][b_t] << 4));
+                    if (split) ob[NB] = (uint8_t)((bc >> 16) | ((uint32_t)s_ovo[1][b_t] << 4));
                 }
-                if (a.emit && (long long)r < a.o.cap) {
+            }
+            // pass A: R' (needs no row base), while thread 0's row reservation is in flight
+            {
+                uint32_t at0 = ex & 0xffffu, at1 = ex >> 16;
+                auto put = [&](int64_t k, const int64_t *wp, int ws, uint32_t half) {
+                    const uint32_t qpos = (half ? qb1 + at1++ : qb0 + at0++);
+                    if (qpos >= a.out.rcap) return;
+                    int64_t *col = a.out.rec + (uint64_t)(qout0 + half) * a.out.rcap * RW;   // SoA columns
+                    col[qpos] = k;
+#pragma unroll
+                    for (int w = 0; w < NW; ++w) col[(uint64_t)(1 + w) * a.out.rcap + qpos] = wp[w * ws];
+                };
+                if (side_live) put(GWO_EMPTY_KEY, s_side + 1, 1, side_half);
+                for (int i = 0; i < SPT; ++i) {
+                    if (!((code >> (2 * i)) & 1u)) continue;
+                    const int sl = tid * SPT + i;
+                    put(s_key[sl], s_w + sl, T, (code >> (2 * i + 1)) & 1u);
+                }
+            }
+            __syncthreads();   // s_rowbase is published; every read of s_qn and s_ovo is done
+            // pass B: rows (the partition's run: half-0 keys first), slots reset for the next fold
+            {
+                const unsigned long long rowbase = s_rowbase;
+                uint32_t at0 = ex & 0xffffu, at1 = ex >> 16;
+                auto row = [&](int64_t k, const int64_t *wp, int ws, uint32_t half) {
+                    const uint32_t ord = half ? tot0 + at1++ : at0++;
+                    const unsigned long long r = rowbase + ord;
+                    if (!a.emit || (long long)r >= a.o.cap) return;
+                    int64_t acc[NW];
+#pragma unroll
+                    for (int w = 0; w < NW; ++w) acc[w] = wp[w * ws];
                     a.o.key[r] = k;
                     a.o.start[r] = a.start;
                     a.o.end[r] = a.end;
@@ -338,30 +446,31 @@ __global__ __launch_bounds__(SLOG_THREADS) void slog_fire_kernel(SlogArgs a) {
                             if (w == wi) x = acc[w];
                             if (w == wi + 1) y = acc[w];
                         }
-                        a.o.res[g][r] = a.rp.kind[g] == GWO_AGG_AVG
-                                            ? __double_as_longlong((double)x / (double)y)
-                                            : x;
+                        a.o.res[g][r] = a.rp.kind[g] == GWO_AGG_AVG ? __double_as_longlong((double)x / (double)y) : x;
                     }
+                };
+                if (side_live) row(GWO_EMPTY_KEY, s_side + 1, 1, side_half);
+                for (int i = 0; i < SPT; ++i) {
+                    if (!((code >> (2 * i)) & 1u)) continue;
+                    const int sl = tid * SPT + i;
+                    row(s_key[sl], s_w + sl, T, (code >> (2 * i + 1)) & 1u);
+                    s_key[sl] = GWO_EMPTY_KEY;
+#pragma unroll
+                    for (int w = 0; w < NW; ++w) s_w[w * T + sl] = 0;
                 }
-            };
-            if (side_live) emit(GWO_EMPTY_KEY, s_side + 1, 1, side_half);
-#pragma unroll
-            for (int i = 0; i < SPT; ++i) {
-                if (!((code >> (2 * i)) & 1u)) continue;
-                const int s = slotv[i];
-                emit(s_key[s], s_w + s, T, (code >> (2 * i + 1)) & 1u);
-                s_key[s] = GWO_EMPTY_KEY;
-#pragma unroll
-                for (int w = 0; w < NW; ++w) s_w[w * T + s] = 0;
             }
-            stamp(5);
-            __syncthreads();   // every read of s_qn, s_side and s_used is done
+            __syncthreads();   // every read of s_side is done
             if (tid == 0) {
                 s_qn[0] = qb0 + tot0;
                 s_qn[1] = qb1 + tot1;
                 s_used = 0;
             }
             if (tid <= GWO_MAX_WORDS) s_side[tid] = 0;
+            if (tid < NB) {
+                s_ovo[0][tid] = 0;
+                s_ovo[1][tid] = 0;
+            }
+            stamp(4);
             __syncthreads();
             lo = hi;
         }
@@ -369,15 +478,16 @@ __global__ __launch_bounds__(SLOG_THREADS) void slog_fire_kernel(SlogArgs a) {
         if (tid == 0) {
             const uint32_t n0 = s_qn[0], n1 = s_qn[1];
             const uint32_t q0 = split ? 2 * p : p;
-            a.out.cnt[q0] = n0 < a.out.rcap ? n0 : (uint32_t)a.out.rcap;
-            if (split) a.out.cnt[q0 + 1] = n1 < a.out.rcap ? n1 : (uint32_t)a.out.rcap;
+            const uint32_t flag = slow ? SLOG_UNSTRUCT : 0u;
+            a.out.cnt[q0] = (n0 < a.out.rcap ? n0 : (uint32_t)a.out.rcap) | flag;
+            if (split) a.out.cnt[q0 + 1] = (n1 < a.out.rcap ? n1 : (uint32_t)a.out.rcap) | flag;
             if (n0 > a.out.rcap || n1 > a.out.rcap) st_rovf++;
             st_live += n0 + n1;
             const unsigned long long mq = n0 > n1 ? n0 : n1;
             st_maxp = mq > st_maxp ? mq : st_maxp;
         }
-        __syncthreads();   // s_beg / s_qn are rewritten for the next partition
-        stamp(6);
+        __syncthreads();   // s_beg / s_qn / s_rn are rewritten for the next partition
+        stamp(5);
     }
     // statistics -> shard blockIdx % SLOG_SHARDS
     const unsigned long long nl = wave_sum_u64(st_neg);
@@ -392,14 +502,24 @@ __global__ __launch_bounds__(SLOG_THREADS) void slog_fire_kernel(SlogArgs a) {
     }
 }
 
-void launch_slog_fire(const SlogArgs &a, int groups, hipStream_t s) {
+// Persistent grid: every workgroup resident at once (the occupancy of the instance at this LDS size, per CU, times
+// the CUs given as `groups`), so no workgroup waits for another to finish before it starts its partitions.
+void launch_slog_fire(const SlogArgs &a, int cus, hipStream_t s) {
     const size_t lds = slog_lds_bytes(a.cap_log2, a.p.nwords);
     const uint32_t P = 1u << a.in.lp;
-    const int grid = (int)(P < (uint32_t)groups ? P : (uint32_t)groups);
 #define GWO_SLOG(NW)                                                                                    \
-    case NW:                                                                                            \
+    case NW: {                                                                                          \
+        static int occ[16] = {};                                                                        \
+        int &per_cu = occ[a.cap_log2 & 15];                                                             \
+        if (!per_cu && hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, slog_fire_kernel<NW>, SLOG_THREADS, \
+                                                                    lds) != hipSuccess)                \
+            per_cu = 1;                                                                                 \
+        if (per_cu < 1) per_cu = 1;                                                                     \
+        const uint32_t groups = (uint32_t)cus * (uint32_t)per_cu;                                       \
+        const int grid = (int)(P < groups ? P : groups);                                                \
         hipLaunchKernelGGL(slog_fire_kernel<NW>, dim3(grid), dim3(SLOG_THREADS), lds, s, a);             \
-        break;
+        break;                                                                                          \
+    }
     switch (a.p.nwords) {
         GWO_SLOG(1)
         GWO_SLOG(2)
