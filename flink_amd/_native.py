@@ -59,6 +59,11 @@ class GwoStateRows(C.Structure):
                 ("key_group", C.c_void_p), ("timer", C.c_void_p)]
 
 
+class GwoHeapStateIds(C.Structure):
+    _fields_ = [("window_contents", C.c_int16), ("merging_window_set", C.c_int16), ("event_timers", C.c_int16),
+                ("processing_timers", C.c_int16)]
+
+
 class GwoGenSpec(C.Structure):
     _fields_ = [
         ("seed", C.c_uint64), ("first_index", C.c_int64), ("total_records", C.c_int64),
@@ -94,6 +99,8 @@ SIGNATURES = [
     ("gwo_snapshot_rows", C.c_int, [_P, _I64P, C.POINTER(C.c_int32)]),
     ("gwo_snapshot", C.c_int, [_P, C.POINTER(GwoStateRows), C.c_int64, _I64P, _I64P]),
     ("gwo_restore", C.c_int, [_P, C.POINTER(GwoStateRows), C.c_int32, C.c_int64, C.c_int64]),
+    ("gwo_export_heap_state", C.c_int, [_P, C.POINTER(GwoHeapStateIds), _P, C.c_int64, _I64P, _P, _I64P]),
+    ("gwo_import_heap_state", C.c_int, [_P, C.POINTER(GwoHeapStateIds), _P, C.c_int64, C.c_int64]),
     ("gwo_sync", C.c_int, [_P]),
     ("gwo_get_stream", C.c_int, [_P, C.POINTER(_P)]),
     ("gwo_last_error", C.c_char_p, [_P]),

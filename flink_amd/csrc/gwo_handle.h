@@ -201,6 +201,10 @@ struct Handle {
     gwo_status snapshot(const gwo_state_rows *rows, int64_t cap, int64_t *n_out);
     gwo_status restore(const gwo_state_rows *rows, int32_t n_words, int64_t n, int64_t new_wm);
     gwo_status table_restore_rows(const RestoreRows &R, int64_t new_wm);
+    // the heap state backend's per-key-group savepoint layout (gwo_heapstate.cpp)
+    gwo_status export_heap_state(const gwo_heap_state_ids *ids, uint8_t *buf, int64_t cap, int64_t *len,
+                                 int64_t *kg_offsets, int64_t *wm_out);
+    gwo_status import_heap_state(const gwo_heap_state_ids *ids, const uint8_t *buf, int64_t len, int64_t new_wm);
 
     // String keys (gwo_strings.cpp)
     gwo_status intern_utf16(const uint16_t *chars, const int64_t *offsets, int64_t n, const int64_t **ids);

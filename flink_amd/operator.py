@@ -298,6 +298,33 @@ class GpuWindowOperator:
                               _ptr(timer).value)
         N.check(self._lib.gwo_restore(self._h, C.byref(rows), nw, n, wm), self._h, "gwo_restore")
 
+    HEAP_STATE_IDS = (0, 1, 2, 3)   # window-contents, merging-window-set, event timers, processing timers
+
+    def export_heap_state(self, ids=HEAP_STATE_IDS):
+        """The keyed state in the heap state backend's per-key-group savepoint layout (gwo.h gwo_export_heap_state;
+        HeapSnapshotStrategy.java:175-193): (bytes, key-group offsets into them, watermark)."""
+        self.flush()
+        sid = N.GwoHeapStateIds(*ids)
+        need = C.c_int64()
+        N.check(self._lib.gwo_export_heap_state(self._h, C.byref(sid), None, 0, C.byref(need), None, None), self._h,
+                "gwo_export_heap_state")
+        buf = np.zeros(max(need.value, 1), np.uint8)
+        nkg = self.cfg.key_group_end - self.cfg.key_group_start + 1
+        offs = np.zeros(nkg, np.int64)
+        got, wm = C.c_int64(), C.c_int64()
+        N.check(self._lib.gwo_export_heap_state(self._h, C.byref(sid), _ptr(buf), buf.size, C.byref(got), _ptr(offs),
+                                                C.byref(wm)), self._h, "gwo_export_heap_state")
+        return buf[:got.value].tobytes(), offs, wm.value
+
+    def import_heap_state(self, data: bytes, watermark: int, ids=HEAP_STATE_IDS):
+        """initializeState from heap-layout key groups (gwo.h gwo_import_heap_state): only this subtask's
+        KeyGroupRange is kept; the watermark is the restored operator watermark."""
+        sid = N.GwoHeapStateIds(*ids)
+        buf = np.frombuffer(data, np.uint8) if len(data) else np.zeros(1, np.uint8)
+        buf = np.ascontiguousarray(buf)
+        N.check(self._lib.gwo_import_heap_state(self._h, C.byref(sid), _ptr(buf), len(data), watermark), self._h,
+                "gwo_import_heap_state")
+
     def state_size(self) -> int:
         n = C.c_int64()
         N.check(self._lib.gwo_state_size(self._h, C.byref(n)), self._h)

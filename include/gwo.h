@@ -196,6 +196,40 @@ gwo_status gwo_snapshot_rows(gwo_handle *h, int64_t *n_rows, int32_t *n_words);
 gwo_status gwo_snapshot(gwo_handle *h, const gwo_state_rows *rows, int64_t cap, int64_t *n_out, int64_t *watermark);
 gwo_status gwo_restore(gwo_handle *h, const gwo_state_rows *rows, int32_t n_words, int64_t n, int64_t watermark);
 
+/* ---- The keyed window state in the heap state backend's savepoint layout ------------------------------------
+ * The data part of a HeapKeyedStateBackend snapshot as WindowOperator's state leaves it (HeapSnapshotStrategy.java:
+ * 172-193): for every key group of the handle's KeyGroupRange, in ascending order, int32 key group, then for every
+ * state int16 state id (the caller's KeyedBackendSerializationProxy numbering) and the state's entries of that key
+ * group, all big-endian:
+ *   window-contents      int32 n, n x {TimeWindow namespace: int64 start, int64 end; key; accumulator}
+ *                        (CopyOnWriteStateMapSnapshot.java:113-131, TimeWindow.java:167-170)
+ *   merging-window-set   sessions only: int32 n, n x {VoidNamespace: one byte 0; key; int32 m, m x {window,
+ *                        state window}} (WindowOperator.java:265-271, MergingWindowSet.java:102-108)
+ *   event timers         "_timer_state/event_window-timers": int32 n, n x {int64 timestamp with its sign bit flipped;
+ *                        key; window} (KeyGroupPartitioner.java:251-264, TimerSerializer.java:158-162) -- a window's
+ *                        fire timer at maxTimestamp and, with allowedLateness > 0, its cleanup timer
+ *                        (WindowOperator.java:598-610)
+ *   processing timers    "_timer_state/processing_window-timers": int32 0
+ * Keys: Long (int64), Integer (int32) or String (StringValue.writeString: length + 1 and UTF-16 units, 7-bit varints).
+ * The accumulator is GpuAggregates.Descriptor's long[] (LongPrimitiveArraySerializer: int32 length, int64 words; two
+ * words per aggregate: COUNT {n, 0}, SUM {sum, 0}, MIN/MAX {value, 0} -- float64 {double bits, 1} --, AVG {sum, count}),
+ * so a savepoint of the reference WindowOperator running that same AggregateFunction restores here and vice versa.
+ * Sliding windows export one entry per (key, window) from their panes; their import is GWO_ERR_UNSUPPORTED.
+ * gwo_export_heap_state with buf == NULL sets *len to the bytes needed; kg_offsets (may be NULL) receives each key
+ * group's offset in buf (KeyGroupRangeOffsets).  gwo_import_heap_state reads a concatenation of key-group sections
+ * (several old subtasks' for a rescale), keeps ITS key groups and restores them as gwo_restore does (fresh handle;
+ * every state id in the data must be one of `ids`). */
+typedef struct {
+    int16_t window_contents;
+    int16_t merging_window_set;   /* -1: not written (non-merging assigners) */
+    int16_t event_timers;
+    int16_t processing_timers;
+} gwo_heap_state_ids;
+gwo_status gwo_export_heap_state(gwo_handle *h, const gwo_heap_state_ids *ids, uint8_t *buf, int64_t cap, int64_t *len,
+                                 int64_t *kg_offsets, int64_t *watermark);
+gwo_status gwo_import_heap_state(gwo_handle *h, const gwo_heap_state_ids *ids, const uint8_t *buf, int64_t len,
+                                 int64_t watermark);
+
 gwo_status gwo_sync(gwo_handle *h);
 gwo_status gwo_get_stream(gwo_handle *h, void **stream);
 const char *gwo_last_error(const gwo_handle *h);

@@ -94,6 +94,17 @@ final class GwoNative {
     static native void restore(long handle, long[] keys, long[] starts, long[] ends, long[] words, int[] timers,
                                int nWords, long n, long watermark);
 
+    /**
+     * gwo_export_heap_state: the keyed state as the heap state backend writes WindowOperator's state, one section
+     * per key group of the handle (HeapSnapshotStrategy.java:175-193).  ids: state ids of {window-contents,
+     * merging-window-set (-1: none), event timers, processing timers}; keyGroupOffsets receives each key group's
+     * byte offset, watermarkOut[0] the watermark.
+     */
+    static native byte[] exportHeapState(long handle, int[] ids, long[] keyGroupOffsets, long[] watermarkOut);
+
+    /** gwo_import_heap_state: key-group sections of that layout; only the handle's KeyGroupRange is kept. */
+    static native void importHeapState(long handle, int[] ids, byte[] data, long watermark);
+
     /** gwo_key_strings: dictionary ids of a String-keyed handle back to Strings. */
     static native String[] keyStrings(long handle, long[] ids, int n);
 

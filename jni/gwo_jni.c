@@ -299,6 +299,57 @@ JNIEXPORT void JNICALL JFN(restore)(JNIEnv *env, jclass c, jlong h, jlongArray k
     if (pt) (*env)->ReleaseIntArrayElements(env, tm, pt, JNI_ABORT);
 }
 
+static int heap_ids(JNIEnv *env, jintArray ids, gwo_heap_state_ids *out) {
+    if (!array_ok(env, ids, 4, "ids: {window-contents, merging-window-set, event timers, processing timers}")) return 0;
+    jint v[4];
+    (*env)->GetIntArrayRegion(env, ids, 0, 4, v);
+    out->window_contents = (int16_t)v[0];
+    out->merging_window_set = (int16_t)v[1];
+    out->event_timers = (int16_t)v[2];
+    out->processing_timers = (int16_t)v[3];
+    return 1;
+}
+
+/* gwo_export_heap_state into a Java byte[] (sized by a first, counting call). */
+JNIEXPORT jbyteArray JNICALL JFN(exportHeapState)(JNIEnv *env, jclass c, jlong h, jintArray ids, jlongArray kgOffsets,
+                                                  jlongArray watermarkOut) {
+    (void)c;
+    gwo_heap_state_ids sid;
+    if (!heap_ids(env, ids, &sid) || !array_ok(env, watermarkOut, 1, "watermark array")) return NULL;
+    int64_t need = 0, len = 0, wm = 0;
+    if (fail(env, H(h), gwo_export_heap_state(H(h), &sid, NULL, 0, &need, NULL, NULL))) return NULL;
+    if (need > 0x7fffffff - 8) {
+        throw_arg(env, "heap-layout state exceeds one Java byte[]; checkpoint it with more subtasks");
+        return NULL;
+    }
+    uint8_t *buf = (uint8_t *)malloc((size_t)(need > 0 ? need : 1));
+    jlong *po = (*env)->GetLongArrayElements(env, kgOffsets, NULL);
+    jbyteArray r = NULL;
+    if (buf && po && !fail(env, H(h), gwo_export_heap_state(H(h), &sid, buf, need, &len, (int64_t *)po, &wm))) {
+        r = (*env)->NewByteArray(env, (jsize)len);
+        if (r) (*env)->SetByteArrayRegion(env, r, 0, (jsize)len, (const jbyte *)buf);
+        jlong w = wm;
+        (*env)->SetLongArrayRegion(env, watermarkOut, 0, 1, &w);
+    } else if (!buf) {
+        throw_arg(env, "out of host memory for the heap-layout state");
+    }
+    if (po) (*env)->ReleaseLongArrayElements(env, kgOffsets, po, r ? 0 : JNI_ABORT);
+    free(buf);
+    return r;
+}
+
+JNIEXPORT void JNICALL JFN(importHeapState)(JNIEnv *env, jclass c, jlong h, jintArray ids, jbyteArray data,
+                                            jlong watermark) {
+    (void)c;
+    gwo_heap_state_ids sid;
+    if (!heap_ids(env, ids, &sid)) return;
+    const jsize n = (*env)->GetArrayLength(env, data);
+    jbyte *p = (*env)->GetByteArrayElements(env, data, NULL);
+    if (!p) return;
+    fail(env, H(h), gwo_import_heap_state(H(h), &sid, (const uint8_t *)p, n, watermark));
+    (*env)->ReleaseByteArrayElements(env, data, p, JNI_ABORT);
+}
+
 /* Ids of a String-keyed handle (a Java long[]) back to Strings. */
 JNIEXPORT jobjectArray JNICALL JFN(keyStrings)(JNIEnv *env, jclass c, jlong h, jlongArray ids, jint n) {
     (void)c;

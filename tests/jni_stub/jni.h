@@ -3,7 +3,7 @@
  * build the shim (`make jni` requires a real JAVA_HOME). */
 #include <stdint.h>
 typedef int32_t jint; typedef int64_t jlong; typedef int8_t jbyte; typedef uint8_t jboolean; typedef uint16_t jchar;
-typedef jint jsize; typedef void *jobject; typedef jobject jclass, jstring, jarray, jobjectArray, jlongArray, jintArray, jcharArray;
+typedef jint jsize; typedef void *jobject; typedef jobject jclass, jstring, jarray, jobjectArray, jlongArray, jintArray, jcharArray, jbyteArray;
 #define JNI_ABORT 2
 #define JNIEXPORT
 #define JNICALL
@@ -28,4 +28,8 @@ struct JNINativeInterface_ {
   jobjectArray (*NewObjectArray)(JNIEnv*, jsize, jclass, jobject);
   jstring (*NewString)(JNIEnv*, const jchar*, jsize);
   void (*SetObjectArrayElement)(JNIEnv*, jobjectArray, jsize, jobject);
+  jbyteArray (*NewByteArray)(JNIEnv*, jsize);
+  void (*SetByteArrayRegion)(JNIEnv*, jbyteArray, jsize, jsize, const jbyte*);
+  jbyte *(*GetByteArrayElements)(JNIEnv*, jbyteArray, jboolean*);
+  void (*ReleaseByteArrayElements)(JNIEnv*, jbyteArray, jbyte*, jint);
 };
