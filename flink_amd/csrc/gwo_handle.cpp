@@ -125,6 +125,7 @@ gwo_status Handle::init(const gwo_config &c) {
     if (cfg_preagg >= 0) use_preagg = cfg_preagg;
     if (const char *cb = getenv("GWO_COMBINE")) use_combine = atoi(cb) ? 1 : 0;
     if (const char *cs = getenv("GWO_COMBINE_SPEC")) use_combine_spec = atoi(cs) ? 1 : 0;
+    if (const char *ss = getenv("GWO_SCAN_SPEC")) use_scan_spec = atoi(ss) ? 1 : 0;
 
     // ---- device resources ----
     if (hipSetDevice(c.device) != hipSuccess) return fail(GWO_ERR_HIP, "hipSetDevice(%d) failed", c.device);
@@ -210,9 +211,12 @@ Handle::~Handle() {
     if (h_ident_side) (void)hipHostFree(h_ident_side);
     dir_buf.release();
     refire_buf.release();
-    for (DevBuf *b : {&cb_dump_key, &cb_dump_acc, &cb_ovf, &cb_blk, &cb_ctr, &cb_dir, &cb_spec_dir}) b->release();
+    for (DevBuf *b : {&cb_dump_key, &cb_dump_acc, &cb_ovf, &cb_blk, &cb_ctr, &cb_dir, &cb_spec_dir, &sp_dir, &sp_go})
+        b->release();
     if (cb_rb) (void)hipHostFree(cb_rb);
     if (cb_ev) (void)hipEventDestroy(cb_ev);
+    if (sp_rb) (void)hipHostFree(sp_rb);
+    if (sp_ev) (void)hipEventDestroy(sp_ev);
     stage_key.release();
     stage_ts.release();
     stage_val.release();

@@ -163,6 +163,14 @@ struct Handle {
     DevBuf cb_spec_dir;                                                // the speculative merge's directory
     std::vector<TableDesc> cb_spec_host;
     long long cb_spec_base = 0;
+    // speculative two-pass insert (insert_speculative): the scan's verdict gates the insert queued behind it
+    int use_scan_spec = 1;                                             // GWO_SCAN_SPEC=0: off
+    DevBuf sp_dir, sp_go;                                              // directory: tables of hint, hint + 1
+    std::vector<TableDesc> sp_dir_host;
+    long long sp_dir_base = 0;
+    unsigned long long *sp_rb = nullptr, *sp_rb_dev = nullptr;        // host-mapped readback block
+    unsigned long long sp_seq = 0;
+    hipEvent_t sp_ev = nullptr;
     int cfg_preagg = -1;                       // GWO_PREAGG env override: 0 / 1
     uint64_t batches = 0;
 
@@ -246,6 +254,7 @@ struct Handle {
     gwo_status insert_windowed(const int64_t *k, const int64_t *t, const int64_t *v, int64_t n,
                                const WindowGeom *at = nullptr);
     gwo_status insert_combined(const int64_t *k, const int64_t *t, const int64_t *v, int64_t n, bool *done);
+    gwo_status insert_speculative(const int64_t *k, const int64_t *t, const int64_t *v, int64_t n, bool *done);
     gwo_status refire_rows(const int64_t *k, const int64_t *t, const int64_t *v, int64_t n, const WindowGeom &g,
                            long long dir_base, int dir_len, uint64_t mmax);
     void adapt_preagg(uint64_t accepted, uint64_t partials);

@@ -20,7 +20,7 @@
 // scan_kernel statistics shards: SCAN_SHARDS x SCAN_SW words (min, max, 6 counters, the histogram), then
 // SCAN_SHARDS + 1 arrival counters 16 words apart; min/max preset, every scan leaves them reset
 #define SCAN_SHARDS 16
-#define SCAN_CNT 8
+#define SCAN_CNT 9        // min, max, accepted, late, refire, bad_ts, bad_range, hist_out, bad_kg (speculative scan)
 #define SCAN_SW 80
 #define SCAN_SHARD_WORDS (SCAN_SHARDS * SCAN_SW + (SCAN_SHARDS + 1) * 16)
 
@@ -149,6 +149,20 @@ struct CombineArgs {
 #define CB_RB_SEQ (CB_RB_STATS_WORDS + 4)
 #define CB_RB_WORDS (CB_RB_STATS_WORDS + 5)
 
+// Speculative two-pass insert (table layout, tumbling; gwo_runtime.cpp insert_speculative): the scan's last
+// workgroup writes the batch statistics into the host-mapped readback block (CB_RB_* layout) and decides whether
+// the insert queued behind it may run with the tables of units hint and hint + 1 as its directory -- no error,
+// no re-fire, every accepted record in those units, whose tables exist with room.  rb == NULL: a plain scan.
+struct ScanSpec {
+    unsigned long long *rb;            // host-mapped readback block (device address), CB_RB_WORDS words
+    unsigned long long seq;
+    uint32_t *go;                      // the insert's verdict word
+    unsigned long long *occ[2];        // occupancy counters of the hint tables (NULL: no table)
+    uint64_t cap[2];                   // their capacities
+    long long hint;                    // == the scan's hist_base
+    int32_t check_kg;                  // the handle does not own every key group: check each accepted key
+};
+
 // Output columns (SoA) in HBM.
 struct OutCols {
     int64_t *key;
@@ -212,11 +226,11 @@ namespace gwo {
 void launch_scan(const int64_t *key, const int64_t *ts, int64_t n, const WindowGeom &g, long long hist_base,
                  BatchStats *stats, int64_t *side_key, int64_t *side_ts, int64_t *side_val, const int64_t *val,
                  unsigned long long *side_count, long long side_cap, int side_enabled, unsigned long long *shards,
-                 hipStream_t s);
+                 hipStream_t s, const ScanSpec *spec = nullptr);
 
 void launch_insert(const int64_t *key, const int64_t *ts, const void *val, int64_t n, const WindowGeom &g,
                    const AccPlan &plan, const TableDesc *dir, long long dir_base, int dir_len, int preagg,
-                   BatchStats *stats, const RingDesc &ring, hipStream_t s);
+                   BatchStats *stats, const RingDesc &ring, hipStream_t s, const uint32_t *go = nullptr);
 
 void launch_restore(const int64_t *key, const int64_t *wstart, const int64_t *words, int64_t n, const AccPlan &p,
                     const WindowGeom &g, const TableDesc *dir, long long dir_base, int dir_len, hipStream_t s);

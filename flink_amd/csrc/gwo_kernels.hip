@@ -95,18 +95,26 @@ __global__ __launch_bounds__(256) void scan_kernel(const int64_t *__restrict__ k
                                                    long long hist_base, BatchStats *st, int64_t *side_key,
                                                    int64_t *side_ts, int64_t *side_val,
                                                    unsigned long long *side_count, long long side_cap,
-                                                   int side_enabled, unsigned long long *sh) {
+                                                   int side_enabled, unsigned long long *sh, ScanSpec sp) {
     __shared__ unsigned long long s_hist[GWO_HIST_BINS];
     for (int i = threadIdx.x; i < GWO_HIST_BINS; i += blockDim.x) s_hist[i] = 0;
     __syncthreads();
     long long mn = 0x7fffffffffffffffLL, mx = (long long)0x8000000000000000LL;
-    unsigned long long acc = 0, late = 0, refire = 0, bad_ts = 0, bad_slide = 0, hout = 0;
+    unsigned long long acc = 0, late = 0, refire = 0, bad_ts = 0, bad_slide = 0, hout = 0, bad_kg = 0;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
         long long u = 0;
         int c = classify(ts[i], g, u);
         if (c == REC_REFIRE && g.refire_ok) refire++;   // also inserted: counted with the accepted records
         if (takes(c, g)) {
+            if (sp.check_kg) {   // the speculative insert runs only if no key is outside the KeyGroupRange
+                const int64_t k = key[i];
+                const int32_t kg = key_group(k, g.key_kind, g.max_par);
+                if (kg < g.kg_lo || kg > g.kg_hi) {
+                    bad_kg++;
+                    atomicExch((unsigned long long *)&st->bad_kg_key, (unsigned long long)k);
+                }
+            }
             acc++;
             mn = u < mn ? u : mn;
             mx = u > mx ? u : mx;
@@ -133,7 +141,7 @@ __global__ __launch_bounds__(256) void scan_kernel(const int64_t *__restrict__ k
     }
     // workgroup reduction -> shard blockIdx % SCAN_SHARDS (zero words skipped)
     unsigned long long v[SCAN_CNT] = {(unsigned long long)mn, (unsigned long long)mx, acc, late, refire, bad_ts,
-                                      bad_slide, hout};
+                                      bad_slide, hout, bad_kg};
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
         const long long a = __shfl_xor((long long)v[0], o), b = __shfl_xor((long long)v[1], o);
@@ -184,23 +192,59 @@ __global__ __launch_bounds__(256) void scan_kernel(const int64_t *__restrict__ k
     }
     __syncthreads();
     if (!s_last) return;
+    __shared__ unsigned long long s_tot[SCAN_CNT + GWO_HIST_BINS];
+    __shared__ unsigned long long s_spec[3];   // occupancy of the hint tables, side-output count
+#define RBW(f) (int)(offsetof(BatchStats, f) / 8)
     if (t < SCAN_CNT + GWO_HIST_BINS) {
         const unsigned long long init = t == 0 ? 0x7fffffffffffffffull : (t == 1 ? 0x8000000000000000ull : 0ull);
         const unsigned long long r = xchg_fold<SCAN_SHARDS>(&sh[t], SCAN_SW, init, t == 0 ? 1 : (t == 1 ? 2 : 0));
+        s_tot[t] = r;
+        int w = RBW(hist) + t - SCAN_CNT;
         switch (t) {
-            case 0: st->min_idx = (long long)r; break;
-            case 1: st->max_idx = (long long)r; break;
-            case 2: st->accepted = r; break;
-            case 3: st->late = r; break;
-            case 4: st->refire = r; break;
-            case 5: st->bad_ts = r; break;
-            case 6: st->bad_range = r; break;
-            case 7: st->hist_out = r; break;
+            case 0: st->min_idx = (long long)r; w = RBW(min_idx); break;
+            case 1: st->max_idx = (long long)r; w = RBW(max_idx); break;
+            case 2: st->accepted = r; w = RBW(accepted); break;
+            case 3: st->late = r; w = RBW(late); break;
+            case 4: st->refire = r; w = RBW(refire); break;
+            case 5: st->bad_ts = r; w = RBW(bad_ts); break;
+            case 6: st->bad_range = r; w = RBW(bad_range); break;
+            case 7: st->hist_out = r; w = RBW(hist_out); break;
+            case 8: w = RBW(bad_kg); break;   // (a plain scan: the insert counts key-group violations)
             default: st->hist[t - SCAN_CNT] = r; break;
         }
+        if (sp.rb) rb_put(&sp.rb[w], r);
     } else if (t >= 128 && t < 128 + SCAN_SHARDS + 1) {
         atomicExch(&done[(t - 128) * 16], 0ull);   // the next scan counts from zero
+    } else if (sp.rb && t >= 192 && t < 195) {
+        const int q = t - 192;   // 0-1: occupancy of the hint tables, 2: side-output count
+        unsigned long long tot = 0;
+        if (q < 2) {
+            unsigned long long *o = sp.occ[q];
+            if (o)
+                for (int s = 0; s < GWO_OCC_SHARDS; ++s) tot += atomicAdd(o + s * GWO_OCC_SHARD_STRIDE, 0ull);
+            rb_put(&sp.rb[CB_RB_OCC + q], tot);
+        } else {
+            tot = side_enabled ? atomicAdd(side_count, 0ull) : 0ull;
+            rb_put(&sp.rb[CB_RB_SIDE], tot);
+        }
+        s_spec[q] = tot;
     }
+    if (!sp.rb) return;
+    __syncthreads();
+    if (t == 0) {   // the speculative insert's verdict (the host's checks and ensure_table's load factor)
+        bool go = s_tot[2] > 0 && s_tot[5] == 0 && s_tot[6] == 0 && s_tot[8] == 0 && s_tot[4] == 0 && s_tot[7] == 0 &&
+                  (long long)s_tot[0] >= sp.hint && (long long)s_tot[1] <= sp.hint + 1 &&
+                  (!side_enabled || (long long)s_spec[2] <= side_cap);
+        for (int r = 0; r < 2 && go; ++r) {
+            const unsigned long long recs = s_tot[SCAN_CNT + r];
+            if (recs) go = sp.occ[r] != nullptr && 10 * (s_spec[r] + recs) <= 7 * sp.cap[r];
+        }
+        *sp.go = go ? 1u : 0u;
+        rb_put(&sp.rb[CB_RB_GO], go ? 1ull : 0ull);
+        rb_put(&sp.rb[RBW(bad_kg_key)], s_tot[8] ? atomicAdd((unsigned long long *)&st->bad_kg_key, 0ull) : 0ull);
+    }
+#undef RBW
+    rb_publish(&sp.rb[CB_RB_SEQ], sp.seq);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -255,7 +299,9 @@ __global__ __launch_bounds__(256) void insert_direct_kernel(const int64_t *__res
                                                             const int64_t *__restrict__ val, int64_t n,
                                                             WindowGeom g, AccPlan p,
                                                             const TableDesc *__restrict__ dir, long long dir_base,
-                                                            int dir_len, BatchStats *st, RingDesc ring) {
+                                                            int dir_len, BatchStats *st, RingDesc ring,
+                                                            const uint32_t *go) {
+    if (go && *go == 0) return;   // speculative launch the scan's verdict turned down: the host takes over
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     long long became = 0;   // ring entries made live by this lane
     // whole waves iterate together (the bound is rounded up to whole waves) so the live count is wave-reduced
@@ -1375,14 +1421,16 @@ void launch_slide_refire_slots(const int64_t *key, const int64_t *r_idx, const l
 void launch_scan(const int64_t *key, const int64_t *ts, int64_t n, const WindowGeom &g, long long hist_base,
                  BatchStats *stats, int64_t *side_key, int64_t *side_ts, int64_t *side_val, const int64_t *val,
                  unsigned long long *side_count, long long side_cap, int side_enabled, unsigned long long *shards,
-                 hipStream_t s) {
+                 hipStream_t s, const ScanSpec *spec) {
+    ScanSpec sp{};
+    if (spec) sp = *spec;
     hipLaunchKernelGGL(scan_kernel, dim3(grid_for(n, 4, 2048)), dim3(256), 0, s, key, ts, val, n, g, hist_base,
-                       stats, side_key, side_ts, side_val, side_count, side_cap, side_enabled, shards);
+                       stats, side_key, side_ts, side_val, side_count, side_cap, side_enabled, shards, sp);
 }
 
 void launch_insert(const int64_t *key, const int64_t *ts, const void *val, int64_t n, const WindowGeom &g,
                    const AccPlan &plan, const TableDesc *dir, long long dir_base, int dir_len, int preagg,
-                   BatchStats *st, const RingDesc &ring, hipStream_t s) {
+                   BatchStats *st, const RingDesc &ring, hipStream_t s, const uint32_t *go) {
     unsigned long long *partials = &st->partials;
     const int64_t *v = (const int64_t *)val;
     if (preagg && plan.nwords <= PREAGG_WORDS) {
@@ -1394,7 +1442,7 @@ void launch_insert(const int64_t *key, const int64_t *ts, const void *val, int64
     } else {
         int grid = grid_for(n, 1, 8192);
         hipLaunchKernelGGL(insert_direct_kernel, dim3(grid), dim3(256), 0, s, key, ts, v, n, g, plan, dir, dir_base,
-                           dir_len, st, ring);
+                           dir_len, st, ring, go);
     }
 }
 

@@ -622,11 +622,108 @@ gwo_status Handle::insert_combined(const int64_t *k, const int64_t *t, const int
     return GWO_OK;
 }
 
+// Speculative two-pass insert (tumbling tables without pre-aggregation, e.g. C1's 10K-record batches over 10K
+// keys): the scan and the direct insert are queued together; the scan's last workgroup checks what the host
+// would check after reading the statistics (errors, re-fires, units outside the hint tables, table load) and
+// the insert runs only on its verdict.  The host spins on the scan's host-mapped readback block -- no stream
+// synchronisation, no statistics copies, no directory upload while the hint tables stay the same.  *done =
+// false: the verdict was no and nothing changed (the side-output count is restored); the caller's path runs.
+gwo_status Handle::insert_speculative(const int64_t *k, const int64_t *t, const int64_t *v, int64_t n, bool *done) {
+    *done = false;
+    WindowGeom g = geom_now();
+    g.refire_ok = 1;
+    Table *hint_tab[2] = {nullptr, nullptr};
+    std::vector<TableDesc> sd(2, TableDesc{});
+    ScanSpec sp{};
+    for (int j = 0; j < 2; ++j) {
+        auto it = tables.find(hist_hint + j);
+        if (it == tables.end()) continue;
+        hint_tab[j] = &it->second;
+        sd[j] = desc(it->second);
+        sp.occ[j] = ctr(it->second.counter);
+        sp.cap[j] = it->second.cap;
+    }
+    if (!hint_tab[0] && !hint_tab[1]) return GWO_OK;   // nothing to speculate into: the host sizes the tables
+    if (!sp_rb) {
+        GWO_TRY(hipcheck(hipHostMalloc((void **)&sp_rb, CB_RB_WORDS * 8, hipHostMallocCoherent | hipHostMallocMapped),
+                         "scan readback"));
+        memset(sp_rb, 0, CB_RB_WORDS * 8);
+        GWO_TRY(hipcheck(hipHostGetDevicePointer((void **)&sp_rb_dev, sp_rb, 0), "scan readback"));
+        GWO_TRY(hipcheck(hipEventCreateWithFlags(&sp_ev, hipEventDisableTiming), "event"));
+        GWO_TRY(ensure_buf(sp_go, 16));
+    }
+    if (sp_dir_base != hist_hint || sp_dir_host.size() != 2 ||
+        memcmp(sp_dir_host.data(), sd.data(), 2 * sizeof(TableDesc)) != 0) {
+        GWO_TRY(ensure_buf(sp_dir, 2 * sizeof(TableDesc)));
+        GWO_TRY(hipcheck(hipMemcpyAsync(sp_dir.ptr, sd.data(), 2 * sizeof(TableDesc), hipMemcpyHostToDevice, stream),
+                         "spec dir"));
+        GWO_TRY(hipcheck(hipStreamSynchronize(stream), "spec dir"));   // sd is a local
+        sp_dir_host = sd;
+        sp_dir_base = hist_hint;
+    }
+    sp.rb = sp_rb_dev;
+    sp.seq = ++sp_seq;
+    sp.go = (uint32_t *)sp_go.ptr;
+    sp.hint = hist_hint;
+    sp.check_kg = !(cfg.key_group_start == 0 && cfg.key_group_end == cfg.max_parallelism - 1);
+    // (no init_stats: the scan's last workgroup writes every statistic the verdict reads; the regular path resets
+    // the rest before it runs)
+    prof_begin(GWO_KERNEL_SCAN);
+    launch_scan(k, t, n, g, hist_hint, d_stats, (int64_t *)side_key.ptr, (int64_t *)side_ts.ptr, (int64_t *)side_val.ptr,
+                v, d_side_count, side_enabled() ? side_cap : 0, side_enabled(), d_scan_sh, stream, &sp);
+    GWO_TRY(launch_ok("scan"));
+    prof_end(GWO_KERNEL_SCAN, n);
+    prof_begin(GWO_KERNEL_INSERT);
+    launch_insert(k, t, v, n, g, plan, (const TableDesc *)sp_dir.ptr, hist_hint, 2, 0, d_stats, ring_desc(), stream,
+                  sp.go);
+    GWO_TRY(launch_ok("insert"));
+    prof_end(GWO_KERNEL_INSERT, n);
+    GWO_TRY(hipcheck(hipEventRecord(sp_ev, stream), "event"));
+    volatile unsigned long long *seqw = sp_rb + CB_RB_SEQ;
+    for (unsigned it = 1; *seqw != sp.seq; ++it) {
+        if ((it & 1023) == 0) {
+            hipError_t e = hipEventQuery(sp_ev);
+            if (e != hipSuccess && e != hipErrorNotReady) return hipcheck(e, "scan");
+            if (e == hipSuccess && *seqw != sp.seq)
+                return poison(GWO_ERR_HIP, "scan: readback sequence word not visible after completion");
+        }
+        __builtin_ia32_pause();
+    }
+    __atomic_thread_fence(__ATOMIC_ACQUIRE);
+#define RBW(f) (int)(offsetof(BatchStats, f) / 8)
+    const unsigned long long accepted = sp_rb[RBW(accepted)], late = sp_rb[RBW(late)];
+    const long long lo = (long long)sp_rb[RBW(min_idx)];
+    unsigned long long hist[2] = {sp_rb[RBW(hist)], sp_rb[RBW(hist) + 1]};
+#undef RBW
+    if (!sp_rb[CB_RB_GO]) {   // the insert exited: the caller's path takes the batch from the start
+        if (side_enabled()) {
+            *h_scalar = side_rows_committed;
+            GWO_TRY(hipcheck(hipMemcpyAsync(d_side_count, h_scalar, 8, hipMemcpyHostToDevice, stream), "side reset"));
+            GWO_TRY(hipcheck(hipStreamSynchronize(stream), "side reset"));
+        }
+        return GWO_OK;
+    }
+    if (side_enabled()) side_rows = side_rows_committed = sp_rb[CB_RB_SIDE];
+    else late_dropped += late;
+    for (int j = 0; j < 2; ++j)   // exact before the insert, plus an upper bound of the keys it added
+        if (hint_tab[j]) hint_tab[j]->occ = sp_rb[CB_RB_OCC + j] + hist[j];
+    adapt_preagg(accepted, 0);
+    hist_hint = lo;
+    for (auto &kv : tables) kv.second.dirty = true;
+    *done = true;
+    return GWO_OK;
+}
+
 gwo_status Handle::insert_windowed(const int64_t *k, const int64_t *t, const int64_t *v, int64_t n,
                                    const WindowGeom *at) {
     if (!at && use_preagg && use_combine && n < (1LL << 31)) {
         bool done = false;
         GWO_TRY(insert_combined(k, t, v, n, &done));
+        if (done) return GWO_OK;
+    }
+    if (!at && !use_preagg && use_scan_spec && cfg.assigner == GWO_ASSIGNER_TUMBLING && !slide && !sess) {
+        bool done = false;
+        GWO_TRY(insert_speculative(k, t, v, n, &done));
         if (done) return GWO_OK;
     }
     WindowGeom g = at ? *at : geom_now();

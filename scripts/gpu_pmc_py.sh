@@ -8,7 +8,7 @@ IFS=';' read -ra GROUPS_ <<< "$PASSES"
 i=0
 for C in "${GROUPS_[@]}"; do
   i=$((i+1))
-  mkdir -p $R/gpurun_out/ppmc_$i
-  timeout -s KILL 240 rocprofv3 --pmc $C --kernel-include-regex "${KREGEX:-gwo}" --output-format csv -d $R/gpurun_out/ppmc_$i -o run -- python3 $R/$PYCMD > $R/gpurun_out/ppmc_$i.log 2>&1 || { echo PMC_FAIL $C; tail -20 $R/gpurun_out/ppmc_$i.log; exit 1; }
+  mkdir -p $R/gpurun_out/${TAG:-ppmc}_$i
+  timeout -s KILL 240 rocprofv3 --pmc $C --kernel-include-regex "${KREGEX:-gwo}" --output-format csv -d $R/gpurun_out/${TAG:-ppmc}_$i -o run -- python3 $R/$PYCMD > $R/gpurun_out/${TAG:-ppmc}_$i.log 2>&1 || { echo PMC_FAIL $C; tail -20 $R/gpurun_out/${TAG:-ppmc}_$i.log; exit 1; }
   echo "pass $i done: $C"
 done
