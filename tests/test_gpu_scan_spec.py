@@ -44,7 +44,7 @@ def test_small_batches_match_oracle(F, monkeypatch, spec):
     """C1's shape (10K-record batches over 10K keys, 5 s windows) with growth: 50K keys, tables start small."""
     monkeypatch.setenv("GWO_PREAGG", "0")
     monkeypatch.setenv("GWO_SCAN_SPEC", spec)
-    k, t, v, b = _stream(300_000, 50_000, 10_000, 1000, 1000)
+    k, t, v, b = _stream(300_000, 50_000, 3_000, 200, 1500)
     op = F.GpuWindowOperator(F.TumblingEventTimeWindows.of(5000), F.MultiAggregate(F.SumAggregate(), F.MaxAggregate()))
     prev = 0
     for end, wm in b:
@@ -61,13 +61,13 @@ def test_small_batches_match_oracle(F, monkeypatch, spec):
 
 @pytest.mark.parametrize("side", [False, True])
 def test_late_records_and_refires(F, monkeypatch, side):
-    """allowedLateness 2 s: re-fire batches turn the verdict down (the host path emits them per element); late
+    """allowedLateness 1 s: re-fire batches turn the verdict down (the host path emits them per element); late
     records go to the side output or are counted, never twice across a turned-down speculation."""
     monkeypatch.setenv("GWO_PREAGG", "0")
-    k, t, v, b = _stream(120_000, 3_000, 4_000, 300, 2500, seed=11)
-    op = F.GpuWindowOperator(F.TumblingEventTimeWindows.of(3000), F.SumAggregate(), allowed_lateness=2000,
+    k, t, v, b = _stream(120_000, 3_000, 4_000, 300, 3000, seed=11)
+    op = F.GpuWindowOperator(F.TumblingEventTimeWindows.of(3000), F.SumAggregate(), allowed_lateness=1000,
                              side_output_late_data=side)
-    ref = O.WindowOperatorOracle(O.TumblingEventTimeWindows(3000), O.SumLongAgg(), 2000, side_output=side)
+    ref = O.WindowOperatorOracle(O.TumblingEventTimeWindows(3000), O.SumLongAgg(), 1000, side_output=side)
     prev = 0
     for end, wm in b:
         op.process_batch(k[prev:end], t[prev:end], v[prev:end])
