@@ -233,6 +233,8 @@ Handle::~Handle() {
     if (fire_stream) (void)hipStreamDestroy(fire_stream);
     if (ev_main) (void)hipEventDestroy(ev_main);
     if (ev_fire) (void)hipEventDestroy(ev_fire);
+    if (ev_out) (void)hipEventDestroy(ev_out);
+    if (h_out_cnt) (void)hipHostFree(h_out_cnt);
 }
 
 gwo_status Handle::submit(const int64_t *key, const int64_t *ts, const void *val, int64_t n) {
@@ -353,6 +355,7 @@ gwo_status Handle::drain_side(const gwo_side_out *cols, int64_t cap, int64_t *n_
 
 // ---- asynchronous fire ---------------------------------------------------------------------------
 gwo_status Handle::poll_fire() {
+    GWO_TRY(settle_out());
     if (!fire_pending) return GWO_OK;
     hipError_t e = hipEventQuery(ev_fire);
     if (e == hipErrorNotReady) return GWO_OK;

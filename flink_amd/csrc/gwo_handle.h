@@ -135,6 +135,11 @@ struct Handle {
     bool fire_pending = false;
     bool async_fire = false;                   // GWO_ASYNC_FIRE=1: return before the fire completes
     bool discard_after_fire = false;
+    // table-layout tumbling fire without a host round trip: the row counter is copied to h_out_cnt behind the
+    // fire kernels and out_rows holds an upper bound (the emitted tables' capacities) until settle_out() reads it
+    bool out_stale = false, discard_stale = false;
+    unsigned long long *h_out_cnt = nullptr;   // pinned
+    hipEvent_t ev_out = nullptr;
     unsigned long long zero_u64 = 0;
     unsigned long long *h_scalar = nullptr;    // pinned scalar staging
     int64_t *h_ident_side = nullptr;           // pinned [0, identity words...] side-slot image
@@ -261,6 +266,7 @@ struct Handle {
     void init_stats(long long hist_base);
     gwo_status grow_side(long long need);
     gwo_status fire_tumbling(int64_t new_wm);
+    gwo_status settle_out();
     int64_t cleanup_time_host(int64_t max_ts) const;
     OutCols out_cols() {
         OutCols o = out;

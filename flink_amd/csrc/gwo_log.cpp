@@ -850,6 +850,7 @@ gwo_status Handle::fire_log(int64_t new_wm) {
 }
 
 gwo_status Handle::finish_fire() {
+    GWO_TRY(settle_out());
     if (!fire_pending) return GWO_OK;
     if (sess) return session_finish_fire();
     LogState &L = *logst;

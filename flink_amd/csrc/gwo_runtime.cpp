@@ -355,6 +355,7 @@ WindowGeom Handle::geom_now() const {
 // refire_emit_kernel, gwo_kernels.hip): emitted before the batch's insert, which then adds them.
 gwo_status Handle::refire_rows(const int64_t *k, const int64_t *t, const int64_t *v, int64_t n, const WindowGeom &g,
                                long long dir_base, int dir_len, uint64_t mmax) {
+    GWO_TRY(settle_out());   // out_rows is added to below
     std::vector<uint64_t> off(dir_len, 0);
     uint64_t tot = 0;
     for (int d = 0; d < dir_len; ++d) {
@@ -632,6 +633,14 @@ gwo_status Handle::insert_speculative(const int64_t *k, const int64_t *t, const 
     *done = false;
     WindowGeom g = geom_now();
     g.refire_ok = 1;
+    // the next window's table exists before its first records arrive (sized like the last retired one), so the
+    // batch that crosses into it stays on this path; an empty table fires no rows
+    if (tables.count(hist_hint) && !tables.count(hist_hint + 1)) {
+        const __int128 end1 = (__int128)(hist_hint + 2) * cfg.size + geom.unit_off_mod;   // window hint + 1's end
+        if (end1 - 1 > (__int128)wm && end1 <= (__int128)(int64_t)0x7fffffffffffffffLL &&
+            end1 - cfg.size >= (__int128)(int64_t)0x8000000000000000LL)
+            GWO_TRY(ensure_table(hist_hint + 1, 0));
+    }
     Table *hint_tab[2] = {nullptr, nullptr};
     std::vector<TableDesc> sd(2, TableDesc{});
     ScanSpec sp{};
@@ -883,6 +892,22 @@ gwo_status Handle::grow_side(long long need) {
 }
 
 // ---- watermark: tumbling windows ---------------------------------------------------------------
+// The exact row count of the last table-layout fire (fire_tumbling): waits for the copy queued behind it.
+gwo_status Handle::settle_out() {
+    if (!out_stale) return GWO_OK;
+    out_stale = false;
+    GWO_TRY(spin_event(ev_out, "row count"));
+    const uint64_t v = *h_out_cnt;
+    if (v > (uint64_t)out.cap) return poison(GWO_ERR_CAPACITY, "fire: more rows than output slots");
+    if (discard_stale) {   // discarded while the count was in flight: the rows are gone
+        rows_gone += v;
+        discard_stale = false;
+    } else {
+        out_rows = v;
+    }
+    return GWO_OK;
+}
+
 gwo_status Handle::fire_tumbling(int64_t new_wm) {
     // timers in timestamp order; each window has its maxTs (fire) and cleanup timers
     std::vector<long long> emit, clear;
@@ -897,9 +922,14 @@ gwo_status Handle::fire_tumbling(int64_t new_wm) {
         if (do_clear) clear.push_back(kv.first);
     }
     if (emit.empty() && clear.empty()) return GWO_OK;
-    GWO_TRY(read_occupancy());
+    // the table layout alone (not the log layout's fired-window tables, whose fire counts rows right after):
+    // no occupancy read -- output room for every slot of the emitted tables, the row count read back behind the
+    // fire kernels (settle_out)
+    const bool lazy = !logst;
+    GWO_TRY(settle_out());
+    if (!lazy) GWO_TRY(read_occupancy());
     uint64_t extra = 0;
-    for (long long u : emit) extra += tables[u].occ;
+    for (long long u : emit) extra += lazy ? tables[u].cap : tables[u].occ;
     GWO_TRY(ensure_output(extra));
     OutCols o = out;
     o.count = d_out_count;
@@ -912,8 +942,18 @@ gwo_status Handle::fire_tumbling(int64_t new_wm) {
         launch_fire(desc(t), t.cap, plan, rplan, start, end, o, also_clear ? 1 : 0, -1, stream);
         GWO_TRY(launch_ok("fire"));
         prof_end(GWO_KERNEL_FIRE, (int64_t)t.cap);
-        out_rows += t.occ;
+        if (!lazy) out_rows += t.occ;
         t.fired = true;
+    }
+    if (lazy && !emit.empty()) {
+        if (!h_out_cnt) {
+            GWO_TRY(hipcheck(hipHostMalloc((void **)&h_out_cnt, 8, hipHostMallocDefault), "row count"));
+            GWO_TRY(hipcheck(hipEventCreateWithFlags(&ev_out, hipEventDisableTiming), "event"));
+        }
+        GWO_TRY(hipcheck(hipMemcpyAsync(h_out_cnt, d_out_count, 8, hipMemcpyDeviceToHost, stream), "row count"));
+        GWO_TRY(hipcheck(hipEventRecord(ev_out, stream), "row count"));
+        out_rows += extra;   // an upper bound until settled
+        out_stale = true;
     }
     for (long long u : clear) {
         Table &t = tables[u];
@@ -1059,6 +1099,12 @@ gwo_status gwo_output_view(gwo_handle *hh, gwo_out *cols, int64_t *n) {
 
 gwo_status gwo_discard_output(gwo_handle *hh) {
     H_OR_FAIL;
+    if (h->out_stale) {   // the rows of a fire still being counted: accounted when the count arrives
+        h->discard_stale = true;
+        h->out_rows = 0;
+        h->out_count_dirty = true;
+        return GWO_OK;
+    }
     GWO_TRY(h->poll_fire());
     if (h->fire_pending) h->discard_after_fire = true;   // the running fire's rows are dropped when it completes
     h->rows_gone += h->out_rows;
