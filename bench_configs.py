@@ -110,12 +110,17 @@ def run(cfg):
     h = op.handle
     rows = [0]
 
+    # the per-step arguments are built before timing: the loop is the operator's three calls per step
+    kp, tp, vp = key.data_ptr(), ts.data_ptr(), val.data_ptr()
+    args = [(C.c_void_p(kp + 8 * s), C.c_void_p(tp + 8 * s), C.c_void_p(vp + 8 * s), e - s, wms[i])
+            for i, (s, e) in enumerate(bounds)]
+    submit, advance, discard = lib.gwo_submit, lib.gwo_advance_watermark, lib.gwo_discard_output
+
     def step(i):
-        s, e = bounds[i]
-        N.check(lib.gwo_submit(h, C.c_void_p(key.data_ptr() + 8 * s), C.c_void_p(ts.data_ptr() + 8 * s),
-                               C.c_void_p(val.data_ptr() + 8 * s), e - s), h, "submit")
-        N.check(lib.gwo_advance_watermark(h, wms[i]), h, "watermark")
-        N.check(lib.gwo_discard_output(h), h)
+        a = args[i]
+        if submit(h, a[0], a[1], a[2], a[3]) or advance(h, a[4]) or discard(h):
+            N.check(lib.gwo_sync(h), h, "step")            # surfaces the handle's error message
+            raise RuntimeError(f"step {i} failed")
 
     def emitted():
         r = C.c_int64()

@@ -166,6 +166,7 @@ struct Handle {
     long long cb_dir_base = 0;
     int use_combine_spec = 1;                                          // GWO_COMBINE_SPEC=0: no speculative merge
     DevBuf cb_spec_dir;                                                // the speculative merge's directory
+    DevBuf cb_dbg;                                                     // GWO_CB_TRACE phase times
     std::vector<TableDesc> cb_spec_host;
     long long cb_spec_base = 0;
     // speculative two-pass insert (insert_speculative): the scan's verdict gates the insert queued behind it
@@ -230,6 +231,9 @@ struct Handle {
     gwo_status dalloc(void **p, size_t bytes);
     gwo_status hipcheck(hipError_t e, const char *what);
     gwo_status spin_event(hipEvent_t ev, const char *what);
+    gwo_status spin_seq(const unsigned long long *word, unsigned long long seq, const char *what);
+    bool known_device(const void *p, size_t bytes);
+    std::vector<std::pair<uintptr_t, uintptr_t>> dev_ranges;   // device allocations seen by stage_inputs
     gwo_status ensure_buf(DevBuf &b, size_t bytes);
     int take_counter();
     // occupancy counter c: GWO_OCC_WORDS device words (sharded, see gwo_device.h occ_add)

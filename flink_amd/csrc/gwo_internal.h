@@ -141,6 +141,7 @@ struct CombineArgs {
     uint32_t *go;                      // NULL: no speculative merge
     uint64_t cap[2];                   // capacities of the hint tables
     long long side_cap;
+    unsigned long long *dbg;           // GWO_CB_TRACE: phase times on the device wall clock (NULL: off)
 };
 #define CB_RB_STATS_WORDS ((int)((sizeof(BatchStats) + 7) / 8))
 #define CB_RB_SIDE (CB_RB_STATS_WORDS)

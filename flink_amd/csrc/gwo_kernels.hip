@@ -509,6 +509,12 @@ __global__ __launch_bounds__(CB_THREADS) void gather_kernel(const int64_t *__res
                                                             int side_enabled) {
     extern __shared__ int64_t s_dyn[];
     const int S = a.S, NW = p.nwords, tid = threadIdx.x;
+    // trace: per-workgroup slot of 8 words, plain stores (start, then phase ends), reduced on the host
+#define CB_STAMP(k)                                                        \
+    do {                                                                   \
+        if (a.dbg && tid == 0) a.dbg[blockIdx.x * 8 + (k)] = wall_clock64(); \
+    } while (0)
+    CB_STAMP(0);
     int64_t *s_key = s_dyn;                     // [CB_NU * S]
     int64_t *s_acc = s_dyn + CB_NU * S;         // [CB_NU * S * NW]
     __shared__ unsigned s_hist[GWO_HIST_BINS];
@@ -536,25 +542,59 @@ __global__ __launch_bounds__(CB_THREADS) void gather_kernel(const int64_t *__res
     };
     const int64_t tstride = (int64_t)gridDim.x * CB_TILE;
     if ((int64_t)blockIdx.x * CB_TILE < n) load_tile((int64_t)blockIdx.x * CB_TILE);
+    if (a.dbg) {   // trace: when the first tile's loads have all arrived
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        CB_STAMP(6);
+    }
     for (int64_t tile = (int64_t)blockIdx.x * CB_TILE; tile < n; tile += tstride) {
         unsigned ovm = 0;   // records of this tile left to the merge (bit j: record tile + j * CB_THREADS + tid)
         unsigned candm = 0;   // bit j: record j goes into the LDS table of unit cbu[j]
         int cbu[CB_PER];
+        // the common case inline: an accepted record of one of the batch's windows (a few compares); everything
+        // else -- late, re-fire, bad timestamps, windows outside the range -- is reloaded and classified in full
+        // out of line below (the full classification inside the unrolled loop bloats the code every record runs)
+        unsigned slow = 0;
 #pragma unroll
         for (int j = 0; j < CB_PER; ++j) {
             const int64_t i = tile + j * CB_THREADS + tid;
             if (i >= n) continue;
-            long long u = 0;
-            int c;
             const int64_t tv = tt[j];
-            if (a.thr_ok && tv >= a.bound[0] && tv < a.bound[4]) {   // a window of the batch's range: compares
-                const int jj = (tv >= a.bound[1]) + (tv >= a.bound[2]) + (tv >= a.bound[3]);
-                const uint32_t cc = (a.cls >> (2 * jj)) & 3u;
-                c = cc == 0 ? REC_ACCEPT : (cc == 2 ? REC_REFIRE : (jadd(tv, g.lateness) <= g.wm ? REC_LATE : REC_SKIP));
-                u = a.hint + jj;
-            } else {
-                c = classify(tv, g, u);
+            const int jj = (tv >= a.bound[1]) + (tv >= a.bound[2]) + (tv >= a.bound[3]);
+            if (!(a.thr_ok && tv >= a.bound[0] && tv < a.bound[4] && ((a.cls >> (2 * jj)) & 3u) == 0 &&
+                  !g.refire_only)) {
+                slow |= 1u << j;
+                continue;
             }
+            acc++;
+            const int64_t k = kk[j];
+            if (!a.full_range) {
+                const int32_t kg = key_group(k, g.key_kind, g.max_par);
+                if (kg < g.kg_lo || kg > g.kg_hi) {
+                    bad_kg++;
+                    atomicExch((unsigned long long *)&st->bad_kg_key, (unsigned long long)k);
+                }
+            }
+            const long long u = a.hint + jj;
+            mn = u < mn ? u : mn;
+            mx = u > mx ? u : mx;
+            if (jj != run_b) {   // run-length histogram: a batch's records share few units
+                if (run_n) atomicAdd(&s_hist[run_b], run_n);
+                run_b = jj;
+                run_n = 0;
+            }
+            run_n++;
+            cbu[j] = jj;
+            if (jj < CB_NU && k != GWO_EMPTY_KEY) candm |= 1u << j;
+            else ovm |= 1u << j;
+        }
+#pragma unroll 1
+        while (slow) {
+            const int j = __builtin_ctz(slow);
+            slow &= slow - 1;
+            const int64_t i = tile + j * CB_THREADS + tid;
+            long long u = 0;
+            const int64_t tv = ts[i];
+            const int c = classify(tv, g, u);
             if (c == REC_BAD_TS) {
                 bad_ts++;
             } else if (c == REC_BAD_SLIDE) {
@@ -566,14 +606,14 @@ __global__ __launch_bounds__(CB_THREADS) void gather_kernel(const int64_t *__res
                     const unsigned long long pos = atomicAdd(side_count, 1ull);
                     if ((long long)pos < side_cap) {
                         side_key[pos] = key[i];
-                        side_ts[pos] = ts[i];
+                        side_ts[pos] = tv;
                         side_val[pos] = val ? val[i] : 0;
                     }
                 }
             } else if (takes(c, g)) {
                 acc++;
                 refire += c == REC_REFIRE;
-                const int64_t k = kk[j];
+                const int64_t k = key[i];
                 const int32_t kg = a.full_range ? g.kg_lo : key_group(k, g.key_kind, g.max_par);
                 if (kg < g.kg_lo || kg > g.kg_hi) {
                     bad_kg++;
@@ -582,7 +622,7 @@ __global__ __launch_bounds__(CB_THREADS) void gather_kernel(const int64_t *__res
                 mn = u < mn ? u : mn;
                 mx = u > mx ? u : mx;
                 const long long b = u - a.hint;
-                if (b >= 0 && b < GWO_HIST_BINS) {   // run-length histogram: a batch's records share few units
+                if (b >= 0 && b < GWO_HIST_BINS) {
                     if ((int)b != run_b) {
                         if (run_n) atomicAdd(&s_hist[run_b], run_n);
                         run_b = (int)b;
@@ -592,14 +632,18 @@ __global__ __launch_bounds__(CB_THREADS) void gather_kernel(const int64_t *__res
                 } else {
                     hout++;
                 }
-                cbu[j] = (int)b;
-                if (b >= 0 && b < CB_NU && k != GWO_EMPTY_KEY) candm |= 1u << j;
+                const bool cand = b >= 0 && b < CB_NU && k != GWO_EMPTY_KEY;
+#pragma unroll
+                for (int q = 0; q < CB_PER; ++q)   // cbu[j] without a run-time register index
+                    if (q == j) cbu[q] = (int)b;
+                if (cand) candm |= 1u << j;
                 else ovm |= 1u << j;
             }
         }
+        CB_STAMP(1);
         // wave pre-reduction of duplicate keys, then the LDS tables (every lane of the wave is here)
         const int lane = tid & 63;
-#pragma unroll
+#pragma unroll 1   // one copy of the insert code (the register arrays are indexed by selects)
         for (int j = 0; j < CB_PER; ++j) {
             bool cand = (candm >> j) & 1u;
             const int64_t k = kk[j];
@@ -645,6 +689,7 @@ __global__ __launch_bounds__(CB_THREADS) void gather_kernel(const int64_t *__res
                 at++;
             }
     }
+    CB_STAMP(2);
     if (run_n) atomicAdd(&s_hist[run_b], run_n);
     // per-workgroup statistics slot
     unsigned long long v[CS_HIST] = {acc, late, refire, bad_ts, bad_range, bad_kg, hout, 0, 0, 0, 0};
@@ -655,21 +700,16 @@ __global__ __launch_bounds__(CB_THREADS) void gather_kernel(const int64_t *__res
         mx = y > mx ? y : mx;
     }
     __syncthreads();   // every LDS table update and histogram run is in
-    // the dump: only the tables of units that took records of this workgroup (a batch usually spans one
-    // window: half the dump), accumulators only of occupied slots; dump_used tells the merge which tables
+    // the occupied slots of the tables of units that took records of this workgroup (a batch usually spans one
+    // window: half the tables) -- counted here, dumped after the arrival below, so that the statistics' round
+    // trips do not wait for the dump's stores
     unsigned d0 = 0, d1 = 0;
     const unsigned used = (s_hist[0] ? 1u : 0u) | (s_hist[1] ? 2u : 0u);
-    if (tid == 0) a.dump_used[blockIdx.x] = used;
-    int64_t *dk = a.dump_key + (size_t)blockIdx.x * CB_NU * S;
-    int64_t *da = a.dump_acc + (size_t)blockIdx.x * CB_NU * S * NW;
     for (int i = tid; i < CB_NU * S; i += CB_THREADS) {
         if (!((used >> (i >= S ? 1 : 0)) & 1u)) continue;
-        const int64_t k = s_key[i];
-        __builtin_nontemporal_store(k, &dk[i]);   // streamed out: no dirty dump lines left for the kernel's end
-        if (k == GWO_EMPTY_KEY) continue;
-        (i < S ? d0 : d1)++;
-        for (int w = 0; w < NW; ++w) __builtin_nontemporal_store(s_acc[i * NW + w], &da[(size_t)i * NW + w]);
+        if (s_key[i] != GWO_EMPTY_KEY) (i < S ? d0 : d1)++;
     }
+    CB_STAMP(3);
     unsigned long long e0 = d0, e1 = d1;
     for (int o = 32; o > 0; o >>= 1) {
         e0 += __shfl_xor(e0, o);
@@ -711,7 +751,25 @@ __global__ __launch_bounds__(CB_THREADS) void gather_kernel(const int64_t *__res
     __syncthreads();
     if (tid == 0) s_last = atomicAdd(a.done, 1ull) == (unsigned long long)(gridDim.x - 1);
     __syncthreads();
-    if (!s_last) return;
+    CB_STAMP(4);
+    // the dump (accumulators only of occupied slots; dump_used tells the merge which tables) reaches the merge
+    // through the kernel boundary; the last workgroup's tail below overlaps its stores
+    auto dump = [&]() {
+        if (tid == 0) a.dump_used[blockIdx.x] = used;
+        int64_t *dk = a.dump_key + (size_t)blockIdx.x * CB_NU * S;
+        int64_t *da = a.dump_acc + (size_t)blockIdx.x * CB_NU * S * NW;
+        for (int i = tid; i < CB_NU * S; i += CB_THREADS) {
+            if (!((used >> (i >= S ? 1 : 0)) & 1u)) continue;
+            const int64_t k = s_key[i];
+            __builtin_nontemporal_store(k, &dk[i]);   // streamed out: no dirty dump lines left for the kernel's end
+            if (k == GWO_EMPTY_KEY) continue;
+            for (int w = 0; w < NW; ++w) __builtin_nontemporal_store(s_acc[i * NW + w], &da[(size_t)i * NW + w]);
+        }
+    };
+    if (!s_last) {
+        dump();
+        return;
+    }
     __shared__ unsigned long long s_tot[CS_WORDS];
     if (tid < CS_WORDS) {
         const unsigned long long init =
@@ -752,6 +810,7 @@ __global__ __launch_bounds__(CB_THREADS) void gather_kernel(const int64_t *__res
         }
     }
     __syncthreads();
+    CB_STAMP(5);
     if (tid == 0) {   // the speculative merge's verdict
         bool go = a.go != nullptr && s_tot[CS_ACC] > 0 && s_tot[CS_BADTS] == 0 && s_tot[CS_BADRANGE] == 0 &&
                   s_tot[CS_BADKG] == 0 && s_tot[CS_REFIRE] == 0 && s_tot[CS_HOUT] == 0 && s_spec[0] == 0 &&
@@ -766,7 +825,9 @@ __global__ __launch_bounds__(CB_THREADS) void gather_kernel(const int64_t *__res
         if (a.go) *a.go = go ? 1u : 0u;
         rb_put(&a.rb[CB_RB_GO], go ? 1ull : 0ull);
     }
+#undef CB_STAMP
     rb_publish(&a.rb[CB_RB_SEQ], a.seq);
+    dump();   // the last workgroup's own dump: after the readback, which waits for every store issued before it
 }
 
 // merge: threads [0, dump_threads) take (slot, run of CB_MERGE_RUN workgroups) of the dumps; the rest take the

@@ -318,6 +318,25 @@ bool is_device_ptr(const void *p) {
     return attr.type == hipMemoryTypeDevice || attr.type == hipMemoryTypeManaged;
 }
 
+// Columns inside a device allocation seen before need no pointer query: a batch's columns are usually slices of
+// the same few buffers (hipPointerGetAttributes is a runtime call per column per batch).  A freed range can only be
+// reused by another device or pinned allocation, both of which the kernels read directly.
+bool Handle::known_device(const void *p, size_t bytes) {
+    const uintptr_t a = (uintptr_t)p;
+    for (const auto &r : dev_ranges)
+        if (a >= r.first && a + bytes <= r.second) return true;
+    if (!is_device_ptr(p)) return false;
+    hipDeviceptr_t base = nullptr;
+    size_t size = 0;
+    if (hipMemGetAddressRange(&base, &size, (hipDeviceptr_t)p) == hipSuccess && size > 0) {
+        if (dev_ranges.size() >= 8) dev_ranges.erase(dev_ranges.begin());
+        dev_ranges.push_back({(uintptr_t)base, (uintptr_t)base + size});
+    } else {
+        (void)hipGetLastError();
+    }
+    return true;
+}
+
 gwo_status Handle::stage_inputs(const int64_t *key, const int64_t *ts, const void *val, int64_t n, const int64_t **dk,
                                 const int64_t **dt, const int64_t **dv) {
     const void *src[3] = {key, ts, val};
@@ -328,7 +347,7 @@ gwo_status Handle::stage_inputs(const int64_t *key, const int64_t *ts, const voi
             *dst[c] = nullptr;
             continue;
         }
-        if (is_device_ptr(src[c])) {
+        if (known_device(src[c], (size_t)n * 8)) {
             *dst[c] = (const int64_t *)src[c];
         } else {
             GWO_TRY(ensure_buf(*bufs[c], (size_t)n * 8));
@@ -503,6 +522,13 @@ gwo_status Handle::insert_combined(const int64_t *k, const int64_t *t, const int
         }
         a.go = (uint32_t *)((unsigned long long *)cb_ctr.ptr + 2);
     }
+    static const int cb_trace = getenv("GWO_CB_TRACE") ? atoi(getenv("GWO_CB_TRACE")) : 0;
+    std::vector<unsigned long long> h_dbg;
+    if (cb_trace) {   // phase times of this gather on the device wall clock (debugging aid)
+        GWO_TRY(ensure_buf(cb_dbg, (size_t)G * 64));
+        GWO_TRY(hipcheck(hipMemset(cb_dbg.ptr, 0, (size_t)G * 64), "trace"));
+        a.dbg = (unsigned long long *)cb_dbg.ptr;
+    }
     prof_begin(GWO_KERNEL_SCAN);
     launch_gather(k, t, v, n, g, plan, a, G, d_stats, (int64_t *)side_key.ptr, (int64_t *)side_ts.ptr,
                   (int64_t *)side_val.ptr, d_side_count, side_enabled() ? side_cap : 0, side_enabled(), stream);
@@ -517,18 +543,31 @@ gwo_status Handle::insert_combined(const int64_t *k, const int64_t *t, const int
         GWO_TRY(launch_ok("merge"));
         prof_end(GWO_KERNEL_INSERT, n);
     }
-    GWO_TRY(hipcheck(hipEventRecord(cb_ev, stream), "event"));
-    // the gather's last workgroup writes the readback block, sequence word last: spin on it (the event is polled
+    // the gather's last workgroup writes the readback block, sequence word last: spin on it (the stream is polled
     // now and then so that a failed launch cannot spin forever)
-    volatile unsigned long long *seqw = cb_rb + CB_RB_SEQ;
-    for (unsigned it = 1; *seqw != a.seq; ++it) {
-        if ((it & 1023) == 0) {
-            hipError_t e = hipEventQuery(cb_ev);
-            if (e != hipSuccess && e != hipErrorNotReady) return hipcheck(e, "gather");
-            if (e == hipSuccess && *seqw != a.seq)
-                return poison(GWO_ERR_HIP, "gather: readback sequence word not visible after completion");
+    GWO_TRY(spin_seq(cb_rb + CB_RB_SEQ, a.seq, "gather"));
+    if (cb_trace) {   // per phase: the latest workgroup end (from the first start) and the longest in-workgroup time
+        h_dbg.resize((size_t)G * 8);
+        GWO_TRY(hipcheck(hipMemcpy(h_dbg.data(), cb_dbg.ptr, (size_t)G * 64, hipMemcpyDeviceToHost), "trace"));
+        unsigned long long t0 = ~0ull, last_start = 0, abs_[8] = {}, rel[8] = {};
+        for (int w = 0; w < G; ++w) {
+            const unsigned long long *d = &h_dbg[(size_t)w * 8];
+            t0 = std::min(t0, d[0]);
+            last_start = std::max(last_start, d[0]);
         }
-        __builtin_ia32_pause();
+        for (int w = 0; w < G; ++w) {
+            const unsigned long long *d = &h_dbg[(size_t)w * 8];
+            for (int q = 1; q < 8; ++q)
+                if (d[q]) {
+                    abs_[q] = std::max(abs_[q], d[q] - t0);
+                    rel[q] = std::max(rel[q], d[q] - d[0]);
+                }
+        }
+        fprintf(stderr, "[cb] G=%d: loads %.2f/%.2f classified %.2f/%.2f lds %.2f/%.2f counted %.2f/%.2f arrived "
+                "%.2f/%.2f tail %.2f (us from the first start / within a workgroup); last start %.2f\n", G,
+                abs_[6] / 100.0, rel[6] / 100.0, abs_[1] / 100.0, rel[1] / 100.0, abs_[2] / 100.0, rel[2] / 100.0,
+                abs_[3] / 100.0, rel[3] / 100.0, abs_[4] / 100.0, rel[4] / 100.0, abs_[5] / 100.0,
+                (last_start - t0) / 100.0);
     }
     __atomic_thread_fence(__ATOMIC_ACQUIRE);
     BatchStats &hs = *h_stats;
@@ -623,6 +662,23 @@ gwo_status Handle::insert_combined(const int64_t *k, const int64_t *t, const int
     return GWO_OK;
 }
 
+// Spins on a host-mapped readback block's sequence word (written last by a kernel's final workgroup).  Now and
+// then the stream is queried, so that a failed launch cannot spin forever: an idle stream whose word never
+// arrived is an error.  Ends with an acquire fence: the block's other words are visible.
+gwo_status Handle::spin_seq(const unsigned long long *word, unsigned long long seq, const char *what) {
+    volatile const unsigned long long *w = word;
+    for (unsigned it = 1; *w != seq; ++it) {
+        if ((it & 1023) == 0) {
+            hipError_t e = hipStreamQuery(stream);
+            if (e != hipSuccess && e != hipErrorNotReady) return hipcheck(e, what);
+            if (e == hipSuccess && *w != seq) return poison(GWO_ERR_HIP, "readback sequence word not visible after completion");
+        }
+        __builtin_ia32_pause();
+    }
+    __atomic_thread_fence(__ATOMIC_ACQUIRE);
+    return GWO_OK;
+}
+
 // Speculative two-pass insert (tumbling tables without pre-aggregation, e.g. C1's 10K-record batches over 10K
 // keys): the scan and the direct insert are queued together; the scan's last workgroup checks what the host
 // would check after reading the statistics (errors, re-fires, units outside the hint tables, table load) and
@@ -687,18 +743,7 @@ gwo_status Handle::insert_speculative(const int64_t *k, const int64_t *t, const 
                   sp.go);
     GWO_TRY(launch_ok("insert"));
     prof_end(GWO_KERNEL_INSERT, n);
-    GWO_TRY(hipcheck(hipEventRecord(sp_ev, stream), "event"));
-    volatile unsigned long long *seqw = sp_rb + CB_RB_SEQ;
-    for (unsigned it = 1; *seqw != sp.seq; ++it) {
-        if ((it & 1023) == 0) {
-            hipError_t e = hipEventQuery(sp_ev);
-            if (e != hipSuccess && e != hipErrorNotReady) return hipcheck(e, "scan");
-            if (e == hipSuccess && *seqw != sp.seq)
-                return poison(GWO_ERR_HIP, "scan: readback sequence word not visible after completion");
-        }
-        __builtin_ia32_pause();
-    }
-    __atomic_thread_fence(__ATOMIC_ACQUIRE);
+    GWO_TRY(spin_seq(sp_rb + CB_RB_SEQ, sp.seq, "scan"));
 #define RBW(f) (int)(offsetof(BatchStats, f) / 8)
     const unsigned long long accepted = sp_rb[RBW(accepted)], late = sp_rb[RBW(late)];
     const long long lo = (long long)sp_rb[RBW(min_idx)];
