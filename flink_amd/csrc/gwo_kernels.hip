@@ -473,7 +473,8 @@ __global__ __launch_bounds__(256) void insert_preagg_kernel(const int64_t *__res
 
 // The workgroup's LDS table of one unit (S slots, key-indexed): the slot holding k, claimed if absent; -1 when
 // 32 probes found no room (the record is listed for the merge).  Two 32-bit multiplies place a key: the table
-// is private to the pass, any spread will do.
+// is private to the pass, any spread will do.  (Linear probing keeps a key at the same slot in most workgroups'
+// tables, which the merge's runs fold in registers; 4-slot buckets measured no faster here and scattered them.)
 __device__ __forceinline__ int lds_slot(int64_t *kb, int S, int sbits, int64_t k) {
     uint32_t sl = ((uint32_t)k * 0x9E3779B1u ^ (uint32_t)((uint64_t)k >> 32) * 0x85EBCA77u) >> (32 - sbits);
     for (int probe = 0; probe < 32; ++probe) {
@@ -489,6 +490,13 @@ __device__ __forceinline__ int lds_slot(int64_t *kb, int S, int sbits, int64_t k
     return -1;
 }
 
+// Lane `src` (wave-uniform) of x: a scalar read (v_readlane), no LDS permute.
+__device__ __forceinline__ int64_t lane64(int64_t x, int src) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, src);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)x >> 32), src);
+    return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+
 // x folded over the 64 lanes of the wave with the word's monoid (every lane gets the result; lanes that do
 // not take part pass the identity).  Float sums are re-associated: within the 1e-6 relative bound.
 __device__ __forceinline__ int64_t wave_fold(int op, int64_t x) {
@@ -500,6 +508,9 @@ __device__ __forceinline__ int64_t wave_fold(int op, int64_t x) {
 enum : int { CS_ACC = 0, CS_LATE, CS_REFIRE, CS_BADTS, CS_BADRANGE, CS_BADKG, CS_HOUT, CS_MIN, CS_MAX, CS_D0, CS_D1,
              CS_HIST = 16, CS_WORDS = CS_HIST + GWO_HIST_BINS };
 
+// NWT: the accumulator words at compile time (1-4; 0: p.nwords at run time) -- loops over words unroll and the plan's
+// per-word fields become scalar constants instead of run-time indexed arrays (the kernel was VALU-bound on them)
+template <int NWT>
 __global__ __launch_bounds__(CB_THREADS) void gather_kernel(const int64_t *__restrict__ key,
                                                             const int64_t *__restrict__ ts,
                                                             const int64_t *__restrict__ val, int64_t n, WindowGeom g,
@@ -507,8 +518,8 @@ __global__ __launch_bounds__(CB_THREADS) void gather_kernel(const int64_t *__res
                                                             int64_t *side_ts, int64_t *side_val,
                                                             unsigned long long *side_count, long long side_cap,
                                                             int side_enabled) {
-    extern __shared__ int64_t s_dyn[];
-    const int S = a.S, NW = p.nwords, tid = threadIdx.x;
+    extern __shared__ __attribute__((aligned(16))) int64_t s_dyn[];
+    const int S = a.S, NW = NWT > 0 ? NWT : p.nwords, tid = threadIdx.x;
     // trace: per-workgroup slot of 8 words, plain stores (start, then phase ends), reduced on the host
 #define CB_STAMP(k)                                                        \
     do {                                                                   \
@@ -520,7 +531,8 @@ __global__ __launch_bounds__(CB_THREADS) void gather_kernel(const int64_t *__res
     __shared__ unsigned s_hist[GWO_HIST_BINS];
     __shared__ unsigned long long s_red[CB_THREADS / 64][CS_HIST];
     for (int i = tid; i < CB_NU * S; i += CB_THREADS) s_key[i] = GWO_EMPTY_KEY;
-    for (int i = tid; i < CB_NU * S * NW; i += CB_THREADS) s_acc[i] = p.ident[i % NW];
+    for (int i = tid; i < CB_NU * S; i += CB_THREADS)
+        for (int w = 0; w < NW; ++w) s_acc[i * NW + w] = p.ident[w];
     if (tid < GWO_HIST_BINS) s_hist[tid] = 0;
     __syncthreads();
     unsigned acc = 0, late = 0, refire = 0, bad_ts = 0, bad_range = 0, bad_kg = 0, hout = 0;
@@ -643,7 +655,7 @@ __global__ __launch_bounds__(CB_THREADS) void gather_kernel(const int64_t *__res
         CB_STAMP(1);
         // wave pre-reduction of duplicate keys, then the LDS tables (every lane of the wave is here)
         const int lane = tid & 63;
-#pragma unroll 1   // one copy of the insert code (the register arrays are indexed by selects)
+#pragma unroll
         for (int j = 0; j < CB_PER; ++j) {
             bool cand = (candm >> j) & 1u;
             const int64_t k = kk[j];
@@ -652,15 +664,15 @@ __global__ __launch_bounds__(CB_THREADS) void gather_kernel(const int64_t *__res
             // lanes' words fold into one lane with a masked wave reduction and that lane updates LDS once
             unsigned long long m = __ballot(cand);
             for (int r = 0; r < 8 && m; ++r) {
-                const int leader = __ffsll((long long)m) - 1;
-                const int64_t lk = __shfl(k, leader);
-                const int lb = __shfl(b, leader);
+                const int leader = __ffsll((long long)m) - 1;   // wave-uniform: scalar lane reads
+                const int64_t lk = lane64(k, leader);
+                const int lb = __builtin_amdgcn_readlane(b, leader);
                 const bool mine = cand && k == lk && b == lb;
                 const unsigned long long peers = __ballot(mine);
                 if (__popcll(peers) < CB_HOT) break;
                 int slot = -1;
                 if (lane == leader) slot = lds_slot(s_key + lb * S, S, a.sbits, lk);
-                slot = __shfl(slot, leader);
+                slot = __builtin_amdgcn_readlane(slot, leader);
                 if (slot >= 0) {
                     int64_t *dst = s_acc + ((size_t)lb * S + slot) * NW;
                     for (int w = 0; w < NW; ++w) {
@@ -1569,8 +1581,17 @@ void launch_gather(const int64_t *key, const int64_t *ts, const int64_t *val, in
                    const AccPlan &p, const CombineArgs &a, int grid, BatchStats *st, int64_t *side_key, int64_t *side_ts,
                    int64_t *side_val, unsigned long long *side_count, long long side_cap, int side_enabled,
                    hipStream_t s) {
-    hipLaunchKernelGGL(gather_kernel, dim3(grid), dim3(CB_THREADS), gather_lds_bytes(a.S, p.nwords), s, key, ts, val,
-                       n, g, p, a, st, side_key, side_ts, side_val, side_count, side_cap, side_enabled);
+#define GATHER(NWT)                                                                                            \
+    hipLaunchKernelGGL(gather_kernel<NWT>, dim3(grid), dim3(CB_THREADS), gather_lds_bytes(a.S, p.nwords), s, key, ts, \
+                       val, n, g, p, a, st, side_key, side_ts, side_val, side_count, side_cap, side_enabled)
+    switch (p.nwords) {
+        case 1: GATHER(1); break;
+        case 2: GATHER(2); break;
+        case 3: GATHER(3); break;
+        case 4: GATHER(4); break;
+        default: GATHER(0); break;
+    }
+#undef GATHER
 }
 
 void launch_merge(const int64_t *key, const int64_t *ts, const int64_t *val, const WindowGeom &g, const AccPlan &p,
