@@ -198,12 +198,18 @@ def main():
         N.check(lib.gwo_comm_init(h, uid, 1, 0), h, "gwo_comm_init")
         os.environ.pop("GWO_COMM_VIRTUAL", None)
 
+    # the per-step arguments are built before timing: a step is the operator's three calls
+    kp, tp, vp = key.data_ptr(), ts.data_ptr(), val.data_ptr()
+    args = [(C.c_void_p(kp + 8 * s), C.c_void_p(tp + 8 * s), C.c_void_p(vp + 8 * s), e - s, wms[i])
+            for i, (s, e) in enumerate(bounds)]
+    submit, advance, discard = lib.gwo_submit, lib.gwo_advance_watermark, lib.gwo_discard_output
+
     def step(i):
-        s, e = bounds[i]
-        N.check(lib.gwo_submit(h, C.c_void_p(key.data_ptr() + 8 * s), C.c_void_p(ts.data_ptr() + 8 * s),
-                               C.c_void_p(val.data_ptr() + 8 * s), e - s), h, "submit")
-        N.check(lib.gwo_advance_watermark(h, wms[i]), h, "watermark")
-        N.check(lib.gwo_discard_output(h), h)   # rows stay in HBM; the sink is not part of the path
+        a_ = args[i]
+        # rows stay in HBM (discarded): the sink is not part of the path
+        if submit(h, a_[0], a_[1], a_[2], a_[3]) or advance(h, a_[4]) or discard(h):
+            N.check(lib.gwo_sync(h), h, "step")   # surfaces the handle's error message
+            raise RuntimeError(f"step {i} failed")
 
     def rows_emitted():
         r = C.c_int64()
