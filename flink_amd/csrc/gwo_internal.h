@@ -229,6 +229,9 @@ void launch_scan(const int64_t *key, const int64_t *ts, int64_t n, const WindowG
                  unsigned long long *side_count, long long side_cap, int side_enabled, unsigned long long *shards,
                  hipStream_t s, const ScanSpec *spec = nullptr);
 
+void launch_publish_words(const unsigned long long *src, int nw, unsigned long long *rb, unsigned long long seq,
+                          hipStream_t s);
+
 void launch_insert(const int64_t *key, const int64_t *ts, const void *val, int64_t n, const WindowGeom &g,
                    const AccPlan &plan, const TableDesc *dir, long long dir_base, int dir_len, int preagg,
                    BatchStats *stats, const RingDesc &ring, hipStream_t s, const uint32_t *go = nullptr);

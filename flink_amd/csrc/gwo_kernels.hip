@@ -1491,6 +1491,20 @@ void launch_slide_refire_slots(const int64_t *key, const int64_t *r_idx, const l
                        p, g, keytab, kmask, j0, nj, pdir, pane_base, pane_len, r_slot, before);
 }
 
+// Copies nw device words into a host-mapped readback block, sequence word last (the host spins on it instead of a
+// copy and a stream synchronisation).  Agent-scope loads: the words were written by earlier kernels' atomics.
+__global__ __launch_bounds__(64) void publish_words_kernel(const unsigned long long *src, int nw,
+                                                           unsigned long long *rb, unsigned long long seq) {
+    for (int t = threadIdx.x; t < nw; t += 64)
+        rb_put(&rb[t], __hip_atomic_load(&src[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    rb_publish(&rb[nw], seq);
+}
+
+void launch_publish_words(const unsigned long long *src, int nw, unsigned long long *rb, unsigned long long seq,
+                          hipStream_t s) {
+    hipLaunchKernelGGL(publish_words_kernel, dim3(1), dim3(64), 0, s, src, nw, rb, seq);
+}
+
 void launch_scan(const int64_t *key, const int64_t *ts, int64_t n, const WindowGeom &g, long long hist_base,
                  BatchStats *stats, int64_t *side_key, int64_t *side_ts, int64_t *side_val, const int64_t *val,
                  unsigned long long *side_count, long long side_cap, int side_enabled, unsigned long long *shards,

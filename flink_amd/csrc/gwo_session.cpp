@@ -3,6 +3,8 @@
 #include <cstdlib>
 #include <unordered_map>
 
+#include <cstring>
+
 #include "gwo_handle.h"
 
 namespace gwo {
@@ -43,6 +45,9 @@ struct SessionState {
     uint64_t pool_cap = 0;          // session records
     unsigned long long *d_pool_top = nullptr;
     uint64_t pool_top = 0;          // as of the last read-back
+    // host-mapped readback of the statistics block (publish_words_kernel): the batch's read-back is a spin
+    unsigned long long *rb = nullptr, *rb_dev = nullptr;
+    unsigned long long rb_seq = 0;
 };
 
 gwo_status Handle::sess_alloc(uint64_t cap, Table &t, int64_t **due) {
@@ -77,6 +82,10 @@ gwo_status Handle::session_init() {
     GWO_TRY(dalloc((void **)&S.d_err_fire, sizeof(SessErr)));
     GWO_TRY(hipcheck(hipHostMalloc((void **)&S.h_err_fire, sizeof(SessErr), hipHostMallocDefault), "pinned"));
     GWO_TRY(hipcheck(hipEventCreateWithFlags(&ev_fire, hipEventDisableTiming), "event"));
+    GWO_TRY(hipcheck(hipHostMalloc((void **)&S.rb, sizeof(SessErr) + 16, hipHostMallocCoherent | hipHostMallocMapped),
+                     "session readback"));
+    memset(S.rb, 0, sizeof(SessErr) + 16);
+    GWO_TRY(hipcheck(hipHostGetDevicePointer((void **)&S.rb_dev, S.rb, 0), "session readback"));
     S.d_pool_top = (unsigned long long *)((char *)S.d_err + sizeof(SessErr));
     GWO_TRY(hipcheck(hipMemsetAsync(S.d_err, 0, sizeof(SessErr) + 8, stream), "err"));
     GWO_TRY(hipcheck(hipMemsetAsync(S.d_err_fire, 0, sizeof(SessErr), stream), "fire err"));
@@ -92,6 +101,7 @@ void Handle::session_free() {
     if (S.T.base) (void)hipFree(S.T.base);
     if (S.d_err) (void)hipFree(S.d_err);
     if (S.h_err) (void)hipHostFree(S.h_err);
+    if (S.rb) (void)hipHostFree(S.rb);
     if (S.d_err_fire) (void)hipFree(S.d_err_fire);
     if (S.h_err_fire) (void)hipHostFree(S.h_err_fire);
     if (S.pool) (void)hipFree(S.pool);
@@ -125,9 +135,13 @@ static SessGeom sess_geom(const Handle &h, int smax) {
 
 gwo_status Handle::sess_read_err() {
     SessionState &S = *sess;
-    // the statistics and, right behind them, the pool's bump counter
-    GWO_TRY(hipcheck(hipMemcpyAsync(S.h_err, S.d_err, sizeof(SessErr) + 8, hipMemcpyDeviceToHost, stream), "err"));
-    GWO_TRY(hipcheck(hipStreamSynchronize(stream), "err sync"));
+    // the statistics and, right behind them, the pool's bump counter: published into host-mapped memory by a
+    // one-wave kernel behind the batch's kernels, spun on (no copy, no stream synchronisation)
+    constexpr int NWD = (int)(sizeof(SessErr) / 8) + 1;
+    launch_publish_words((const unsigned long long *)S.d_err, NWD, S.rb_dev, ++S.rb_seq, stream);
+    GWO_TRY(launch_ok("session readback"));
+    GWO_TRY(spin_seq(S.rb + NWD, S.rb_seq, "session readback"));
+    memcpy(S.h_err, S.rb, sizeof(SessErr) + 8);
     S.pool_top = *(const unsigned long long *)((const char *)S.h_err + sizeof(SessErr));
     constexpr int W = (int)(sizeof(SessErr) / 8);
     const unsigned long long *now = (const unsigned long long *)S.h_err, *was = (const unsigned long long *)&S.err_prev;
