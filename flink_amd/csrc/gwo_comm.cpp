@@ -48,20 +48,46 @@ struct Comm {
     // every rank holds the same value, so sender and receiver derive the same tbase from it even when restored
     // subtasks hold different watermarks
     int64_t agreed_wm = (int64_t)0x8000000000000000LL;
-    int64_t recv_n = 0, recv_w = 0;   // narrow / wide records received by the last routed exchange
-    int64_t recv_off_w = 0;       // word offset of the wide records in recvbuf
+    // Routed exchanges of the log layout alternate between two send/receive buffer slots: batch i+1's routed K1 fills
+    // one send slot while batch i's records are still on the wire from the other, and batch i+1's receives land in
+    // the slot batch i-1's received records were read from (its K1 was resolved before batch i+1 was queued).
+    DevBuf rsend[2], rrecv[2];
+    hipEvent_t ev_rrecv[2] = {nullptr, nullptr};
+    int rslot = 0;
+    // Counts and watermark agreement run on a second communicator (ncclCommSplit of nc) and stream: RCCL orders the
+    // operations of one communicator, so on nc they would queue behind the previous batch's record exchange and the
+    // host's wait for them would end the overlap.
+    ncclComm_t nc2 = nullptr;
+    hipStream_t cs2 = nullptr;
+    struct Recv {
+        bool active = false;
+        int slot = 0;
+        int64_t n = 0, w = 0;      // narrow / wide records received
+        int64_t off_w = 0;         // word offset of the wide records in the slot's receive buffer
+        int64_t tbase = 0;
+        WindowGeom g{};            // the geometry (watermark) of the batch they belong to
+    };
+    Recv last;                     // the last routed exchange queued
+    Recv pend;                     // deferred: received records not yet inserted (comm_flush_received)
+    bool defer = true;             // GWO_COMM_DEFER=0: insert every batch's received records inside its gwo_submit
 };
 
 static int route_ranks(const Comm &C) { return C.vranks > 1 ? C.vranks : C.nranks; }
 
 void Handle::comm_free() {
     if (!comm) return;
+    if (comm->cs) (void)hipStreamSynchronize(comm->cs);
+    if (comm->cs2) (void)hipStreamSynchronize(comm->cs2);
+    if (comm->nc2) ncclCommDestroy(comm->nc2);
     if (comm->nc) ncclCommDestroy(comm->nc);
     for (DevBuf *b : {&comm->dest, &comm->k1, &comm->v1, &comm->hist, &comm->sendbuf, &comm->recvbuf, &comm->rk,
-                      &comm->rt, &comm->rv, &comm->counts, &comm->cursor})
+                      &comm->rt, &comm->rv, &comm->counts, &comm->cursor, &comm->rsend[0], &comm->rsend[1],
+                      &comm->rrecv[0], &comm->rrecv[1]})
         b->release();
-    if (comm->cs) (void)hipStreamSynchronize(comm->cs);
     if (comm->cs) (void)hipStreamDestroy(comm->cs);
+    if (comm->cs2) (void)hipStreamDestroy(comm->cs2);
+    for (hipEvent_t e : comm->ev_rrecv)
+        if (e) (void)hipEventDestroy(e);
     if (comm->ev_routed) (void)hipEventDestroy(comm->ev_routed);
     if (comm->ev_recv) (void)hipEventDestroy(comm->ev_recv);
     if (comm->h_counts) (void)hipHostFree(comm->h_counts);
@@ -199,12 +225,13 @@ gwo_status Handle::comm_route_args(int64_t n, LogRoute *rt, bool *on) {
     C.rcap = ((uint64_t)(mean + 6.0 * std::sqrt(mean) + 64.0) + 1) & ~1ull;   // even: regions stay 8-B aligned
     C.wcap = 256 + (uint64_t)n / 1024;
     C.tbase = log_rt_tbase(C.agreed_wm);   // the same on every rank (min over ranks)
-    GWO_TRY(ensure_buf(C.sendbuf, (size_t)P * (C.rcap * 20 + C.wcap * 24) + 24));
+    DevBuf &sb = C.rsend[C.rslot];
+    GWO_TRY(ensure_buf(sb, (size_t)P * (C.rcap * 20 + C.wcap * 24) + 24));
     *rt = LogRoute{};
     rt->mode = 1;
     rt->nranks = P;
     rt->me = C.rank;
-    rt->send = (int64_t *)C.sendbuf.ptr;
+    rt->send = (int64_t *)sb.ptr;
     rt->rcap = C.rcap;
     rt->wcap = C.wcap;
     rt->tbase = C.tbase;
@@ -219,30 +246,33 @@ gwo_status Handle::comm_mark_routed() {
     return hipcheck(hipEventRecord(comm->ev_routed, stream), "event");
 }
 
-// After the routed K1 is queued: exchange the per-destination (narrow, wide) counts (RCCL, comm stream), bring
-// them to the host (the batch's one host round trip for the exchange), re-route on a region overflow, and queue
-// the records' exchange on the comm stream -- it runs while the main stream finishes this batch's own records.
-// Per peer: the narrow records as three arrays (keys, values, int32 timestamps: 20 B a record), then the wide ones.
+// After the routed K1 is queued: exchange the per-destination (narrow, wide) counts (RCCL on the count communicator
+// and its stream, so they never queue behind the previous batch's records on the wire), bring them to the host (the
+// batch's one host round trip for the exchange), re-route on a region overflow, and queue the records' exchange on
+// the comm stream -- it runs while the main stream finishes this batch's own records (and, deferred, the next
+// batch's routed K1).  Per peer: the narrow records as three arrays (keys, values, int32 timestamps: 20 B a record),
+// then the wide ones.
 gwo_status Handle::comm_after_route(const int64_t *k, const int64_t *t, const int64_t *v, int64_t n) {
     Comm &C = *comm;
     const int P = route_ranks(C), me = C.rank;
     const bool virt = C.vranks > 1;
+    const int slot = C.rslot;
     unsigned long long *d_send = (unsigned long long *)C.counts.ptr, *d_recv = d_send + 2 * P;
     if (n == 0) GWO_TRY(comm_mark_routed());   // (no K1 ran: the counts were zeroed on the main stream)
-    GWO_TRY(hipcheck(hipStreamWaitEvent(C.cs, C.ev_routed, 0), "event wait"));
+    GWO_TRY(hipcheck(hipStreamWaitEvent(C.cs2, C.ev_routed, 0), "event wait"));
     // one send/recv pair per peer; virtual ranks send to this rank itself, so what it routes to virtual GPU p
     // comes back "from p" through the same RCCL calls a real rank makes
     GWO_TRY(nccl_ok(this, ncclGroupStart(), "group"));
     for (int p = 0; p < P; ++p) {
         if (p == me) continue;
         const int peer = virt ? me : p;
-        GWO_TRY(nccl_ok(this, ncclSend(d_send + 2 * p, 2, ncclUint64, peer, C.nc, C.cs), "send count"));
-        GWO_TRY(nccl_ok(this, ncclRecv(d_recv + 2 * p, 2, ncclUint64, peer, C.nc, C.cs), "recv count"));
+        GWO_TRY(nccl_ok(this, ncclSend(d_send + 2 * p, 2, ncclUint64, peer, C.nc2, C.cs2), "send count"));
+        GWO_TRY(nccl_ok(this, ncclRecv(d_recv + 2 * p, 2, ncclUint64, peer, C.nc2, C.cs2), "recv count"));
     }
     GWO_TRY(nccl_ok(this, ncclGroupEnd(), "group end"));
     unsigned long long *hs = C.h_counts, *hr = C.h_counts + 2 * P;
-    GWO_TRY(hipcheck(hipMemcpyAsync(hs, d_send, (size_t)4 * P * 8, hipMemcpyDeviceToHost, C.cs), "counts"));
-    GWO_TRY(hipcheck(hipStreamSynchronize(C.cs), "counts sync"));
+    GWO_TRY(hipcheck(hipMemcpyAsync(hs, d_send, (size_t)4 * P * 8, hipMemcpyDeviceToHost, C.cs2), "counts"));
+    GWO_TRY(hipcheck(hipStreamSynchronize(C.cs2), "counts sync"));
     hs[2 * me] = hs[2 * me + 1] = 0;   // (K1 never routes a record to its own GPU)
     hr[2 * me] = hr[2 * me + 1] = 0;
     uint64_t rcap = C.rcap, wcap = C.wcap, mx = 0, mw = 0;
@@ -250,16 +280,17 @@ gwo_status Handle::comm_after_route(const int64_t *k, const int64_t *t, const in
         mx = std::max<uint64_t>(mx, hs[2 * p]);
         mw = std::max<uint64_t>(mw, hs[2 * p + 1]);
     }
+    DevBuf &sbuf = C.rsend[slot];
     if (mx > rcap || mw > wcap) {   // skewed keys: a region overflowed -- route the batch again with exact regions
         rcap = (std::max<uint64_t>(rcap, mx) + 1) & ~1ull;
         wcap = std::max<uint64_t>(wcap, mw);
         GWO_TRY(hipcheck(hipStreamSynchronize(stream), "re-route"));   // the send buffer may move
-        GWO_TRY(ensure_buf(C.sendbuf, (size_t)P * (rcap * 20 + wcap * 24) + 24));
+        GWO_TRY(ensure_buf(sbuf, (size_t)P * (rcap * 20 + wcap * 24) + 24));
         LogRoute rt{};
         rt.mode = 3;   // route only: this GPU's records were partitioned by the first K1
         rt.nranks = P;
         rt.me = me;
-        rt.send = (int64_t *)C.sendbuf.ptr;
+        rt.send = (int64_t *)sbuf.ptr;
         rt.rcap = rcap;
         rt.wcap = wcap;
         rt.tbase = C.tbase;
@@ -268,20 +299,28 @@ gwo_status Handle::comm_after_route(const int64_t *k, const int64_t *t, const in
         rt.count = (unsigned long long *)C.counts.ptr + 4 * P;   // (scratch: the counts are known)
         GWO_TRY(log_route_only(k, t, v, n, rt));
         GWO_TRY(comm_mark_routed());
-        GWO_TRY(hipcheck(hipStreamWaitEvent(C.cs, C.ev_routed, 0), "event wait"));
     }
+    // the records may leave once the (last) routed K1 has written them
+    GWO_TRY(hipcheck(hipStreamWaitEvent(C.cs, C.ev_routed, 0), "event wait"));
     std::vector<uint64_t> rn(P + 1, 0), rw(P + 1, 0);
     for (int p = 0; p < P; ++p) {
         rn[p + 1] = rn[p] + hr[2 * p];
         rw[p + 1] = rw[p] + hr[2 * p + 1];
     }
     const int64_t RN = (int64_t)rn[P], RW = (int64_t)rw[P];
-    // receive buffer: keys[RN], values[RN], int32 ts[RN] (padded to a word), then the wide records
+    // receive buffer: keys[RN], values[RN], int32 ts[RN] (padded to a word), then the wide records.  The slot's
+    // previous records (two batches ago) were read by a K1 the host has seen complete.
     const int64_t ts_words = (RN + 1) / 2;
-    C.recv_off_w = 2 * RN + ts_words;
-    GWO_TRY(ensure_buf(C.recvbuf, (size_t)(C.recv_off_w + 3 * RW) * 8 + 24));
-    int64_t *rb = (int64_t *)C.recvbuf.ptr;
-    int64_t *sb = (int64_t *)C.sendbuf.ptr;
+    Comm::Recv R;
+    R.slot = slot;
+    R.n = RN;
+    R.w = RW;
+    R.off_w = 2 * RN + ts_words;
+    R.tbase = C.tbase;
+    R.g = log_geom_now();
+    GWO_TRY(ensure_buf(C.rrecv[slot], (size_t)(R.off_w + 3 * RW) * 8 + 24));
+    int64_t *rb = (int64_t *)C.rrecv[slot].ptr;
+    int64_t *sb = (int64_t *)sbuf.ptr;
     prof_begin(GWO_KERNEL_EXCHANGE, C.cs);
     GWO_TRY(nccl_ok(this, ncclGroupStart(), "group"));
     for (int p = 0; p < P; ++p) {
@@ -303,35 +342,70 @@ gwo_status Handle::comm_after_route(const int64_t *k, const int64_t *t, const in
                             "recv ts"));
         }
         if (qw)
-            GWO_TRY(nccl_ok(this, ncclRecv(rb + C.recv_off_w + 3 * rw[p], 3 * qw, ncclInt64, peer, C.nc, C.cs),
+            GWO_TRY(nccl_ok(this, ncclRecv(rb + R.off_w + 3 * rw[p], 3 * qw, ncclInt64, peer, C.nc, C.cs),
                             "recv wide"));
     }
     GWO_TRY(nccl_ok(this, ncclGroupEnd(), "group end"));
     prof_end(GWO_KERNEL_EXCHANGE, RN + RW, C.cs);
-    GWO_TRY(hipcheck(hipEventRecord(C.ev_recv, C.cs), "event"));
-    C.recv_n = RN;
-    C.recv_w = RW;
+    GWO_TRY(hipcheck(hipEventRecord(C.ev_rrecv[slot], C.cs), "event"));
+    R.active = true;
+    C.last = R;
+    C.rslot ^= 1;
     return GWO_OK;
 }
 
 Handle::Received Handle::comm_received() const {
-    const Comm &C = *comm;
+    const Comm::Recv &L = comm->last;
     Received R;
-    const int64_t *rb = (const int64_t *)C.recvbuf.ptr;
-    R.n = C.recv_n;
+    const int64_t *rb = (const int64_t *)comm->rrecv[L.slot].ptr;
+    R.n = L.n;
     R.key = rb;
-    R.val = rb + C.recv_n;
-    R.ts32 = (const int32_t *)(rb + 2 * C.recv_n);
-    R.tbase = C.tbase;
-    R.wide = rb + C.recv_off_w;
-    R.wide_n = C.recv_w;
+    R.val = rb + L.n;
+    R.ts32 = (const int32_t *)(rb + 2 * L.n);
+    R.tbase = L.tbase;
+    R.wide = rb + L.off_w;
+    R.wide_n = L.w;
     return R;
 }
 
 // The main stream waits for the exchange's receives (comm stream) before reading the received records.
 gwo_status Handle::comm_wait_received() {
     if (route_ranks(*comm) == 1) return GWO_OK;
+    if (comm->last.active) return hipcheck(hipStreamWaitEvent(stream, comm->ev_rrecv[comm->last.slot], 0), "exchange wait");
     return hipcheck(hipStreamWaitEvent(stream, comm->ev_recv, 0), "exchange wait");
+}
+
+// Deferred receives (tumbling log layout, allowedLateness 0, no side output): a routed batch's received records are
+// inserted at the next routed batch -- after that batch's K1 and exchange are queued, so batch i's records on the wire
+// overlap batch i+1's K1 and pass 2 -- or at any earlier point that observes state or fires a window they may fall
+// into (log_flush).  They are classified at their own batch's watermark (the geometry kept with them), exactly as if
+// inserted at once: a fire that could take them flushes them first (log_pending_may_fire).
+bool Handle::comm_defers() const {
+    return comm && logst && !slog && cfg.allowed_lateness == 0 && !side_enabled() && route_ranks(*comm) > 1 &&
+           comm->defer;
+}
+
+gwo_status Handle::comm_flush_received() {
+    if (!comm || !comm->pend.active) return GWO_OK;
+    const Comm::Recv R = comm->pend;
+    comm->pend.active = false;
+    GWO_TRY(hipcheck(hipStreamWaitEvent(stream, comm->ev_rrecv[R.slot], 0), "exchange wait"));
+    const int64_t *rb = (const int64_t *)comm->rrecv[R.slot].ptr;
+    if (R.n) GWO_TRY(insert_log(rb, (const int64_t *)(rb + 2 * R.n), rb + R.n, R.n, 1, nullptr, true, R.tbase, &R.g));
+    if (R.w) GWO_TRY(insert_log(rb + R.off_w, rb + R.off_w + 1, rb + R.off_w + 2, R.w, 3, nullptr, false, 0, &R.g));
+    return GWO_OK;
+}
+
+// Keeps the last routed exchange's receives for the next routed batch (comm_defers).
+void Handle::comm_defer_received() {
+    comm->pend = comm->last;
+    comm->last.active = false;
+}
+
+bool Handle::comm_pending_wm(int64_t *wm) const {
+    if (!comm || !comm->pend.active) return false;
+    *wm = comm->pend.g.wm;
+    return true;
 }
 
 // AoS {key, ts, value} records -> the handle's column scratch (table, sliding and session layouts)
@@ -357,10 +431,11 @@ static gwo_status allreduce_min(Handle *h, int64_t v, int64_t *out) {
     Comm &C = *h->comm;
     int64_t *d = (int64_t *)C.counts.ptr + 6 * std::max(C.nranks, C.vranks);   // past the count words and scratch
     *C.h_wm = v;
-    GWO_TRY(h->hipcheck(hipMemcpyAsync(d, C.h_wm, 8, hipMemcpyHostToDevice, h->stream), "wm"));
-    GWO_TRY(nccl_ok(h, ncclAllReduce(d, d, 1, ncclInt64, ncclMin, C.nc, h->stream), "allreduce wm"));
-    GWO_TRY(h->hipcheck(hipMemcpyAsync(C.h_wm, d, 8, hipMemcpyDeviceToHost, h->stream), "wm"));
-    GWO_TRY(h->hipcheck(hipStreamSynchronize(h->stream), "wm sync"));
+    // on the count communicator's stream: it does not wait for a record exchange still on the wire
+    GWO_TRY(h->hipcheck(hipMemcpyAsync(d, C.h_wm, 8, hipMemcpyHostToDevice, C.cs2), "wm"));
+    GWO_TRY(nccl_ok(h, ncclAllReduce(d, d, 1, ncclInt64, ncclMin, C.nc2, C.cs2), "allreduce wm"));
+    GWO_TRY(h->hipcheck(hipMemcpyAsync(C.h_wm, d, 8, hipMemcpyDeviceToHost, C.cs2), "wm"));
+    GWO_TRY(h->hipcheck(hipStreamSynchronize(C.cs2), "wm sync"));
     *out = *C.h_wm;
     return GWO_OK;
 }
@@ -418,27 +493,27 @@ extern "C" gwo_status gwo_comm_init(gwo_handle *hh, const uint8_t *id, int32_t n
         delete C;
         return GWO_ERR_OUT_OF_MEMORY;
     }
+    if (const char *e = getenv("GWO_COMM_DEFER")) C->defer = atoi(e) != 0;
     if (hipStreamCreateWithFlags(&C->cs, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&C->cs2, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&C->ev_routed, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&C->ev_recv, hipEventDisableTiming) != hipSuccess) {
-        (void)hipHostFree(C->h_counts);
-        (void)hipHostFree(C->h_wm);
-        delete C;
+        hipEventCreateWithFlags(&C->ev_recv, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&C->ev_rrecv[0], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&C->ev_rrecv[1], hipEventDisableTiming) != hipSuccess) {
+        h->comm = C;   // comm_free releases what was created
+        h->comm_free();
         return GWO_ERR_HIP;
     }
     ncclUniqueId u;
     memcpy(&u, id, GWO_COMM_ID_BYTES);
     ncclResult_t r = ncclCommInitRank(&C->nc, nranks, u, rank);
+    // the count communicator: same ranks, its own RCCL ordering (a collective: every rank splits here)
+    if (r == ncclSuccess) r = ncclCommSplit(C->nc, 0, rank, &C->nc2, nullptr);
+    h->comm = C;
     if (r != ncclSuccess) {
-        (void)hipStreamDestroy(C->cs);
-        (void)hipEventDestroy(C->ev_routed);
-        (void)hipEventDestroy(C->ev_recv);
-        (void)hipHostFree(C->h_counts);
-        (void)hipHostFree(C->h_wm);
-        delete C;
+        h->comm_free();
         return h->fail(GWO_ERR_COMM, "ncclCommInitRank: %s", ncclGetErrorString(r));
     }
-    h->comm = C;
     // the ranks' watermarks may differ (subtasks restored from different checkpoints): agree on their min now, so
     // every rank's first routed batch encodes and decodes wire timestamps against the same base
     gwo_status st = h->ensure_buf(C->counts, (size_t)6 * cranks * 8 + 16);   // (never reallocated later)

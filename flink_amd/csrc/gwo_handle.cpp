@@ -249,6 +249,13 @@ gwo_status Handle::submit(const int64_t *key, const int64_t *ts, const void *val
         if (!routed) return n ? insert_log(dk, dt, dv, n) : GWO_OK;   // one rank: nothing leaves this GPU
         if (n > 0) GWO_TRY(insert_log(dk, dt, dv, n, 1, &rt));
         else GWO_TRY(comm_after_route(dk, dt, dv, 0));
+        if (comm_defers()) {
+            // this batch's records are on the wire now; the previous batch's arrived while its K1 ran
+            GWO_TRY(comm_flush_received());
+            comm_defer_received();
+            return GWO_OK;
+        }
+        GWO_TRY(comm_flush_received());   // (deferral switched off by a configuration change: none pending)
         const Received R = comm_received();
         GWO_TRY(comm_wait_received());
         if (R.n) GWO_TRY(insert_log(R.key, (const int64_t *)R.ts32, R.val, R.n, 1, nullptr, true, R.tbase));

@@ -323,7 +323,8 @@ struct Handle {
     gwo_status log_resolve_split();
     // ts32: `t` points at int32 timestamps - tbase (records received in the 20-B wire format)
     gwo_status insert_log(const int64_t *k, const int64_t *t, const int64_t *v, int64_t n, int64_t stride = 1,
-                          const LogRoute *route = nullptr, bool ts32 = false, int64_t tbase = 0);
+                          const LogRoute *route = nullptr, bool ts32 = false, int64_t tbase = 0,
+                          const WindowGeom *geom_at = nullptr);
     gwo_status log_k1(LogJob &J, bool first_pass);
     LogThr log_thresholds(const LogJob &J) const;
     void log_uncarve(const LogJob &J, int w, uint64_t keep);
@@ -335,6 +336,7 @@ struct Handle {
     gwo_status log_wait_readback(int slot, unsigned long long seq);
     gwo_status log_flush();                    // resolve the pipelined batch (no-op without one)
     bool log_pending_may_fire(int64_t new_wm) const;
+    bool log_may_fire_since(int64_t batch_wm, int64_t new_wm) const;   // a window of records accepted at batch_wm fires by new_wm
     gwo_status set_pipelined(bool on);
     gwo_status fire_log(int64_t new_wm);
     gwo_status log_state_size(int64_t *entries);
@@ -368,6 +370,11 @@ struct Handle {
     gwo_status log_route_only(const int64_t *k, const int64_t *t, const int64_t *v, int64_t n, const LogRoute &rt);
     gwo_status comm_mark_routed();
     gwo_status comm_after_route(const int64_t *k, const int64_t *t, const int64_t *v, int64_t n);
+    // deferred receives of the routed log path: inserted at the next routed batch or at log_flush
+    bool comm_defers() const;
+    void comm_defer_received();
+    gwo_status comm_flush_received();
+    bool comm_pending_wm(int64_t *wm) const;   // the watermark the deferred records are classified at
     // records received by the last exchange: 20-B ones as columns (keys, values, int32 ts - tbase) and 24-B ones
     struct Received {
         const int64_t *key = nullptr, *val = nullptr;

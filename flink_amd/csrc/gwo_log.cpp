@@ -678,14 +678,16 @@ gwo_status Handle::log_route_only(const int64_t *k, const int64_t *t, const int6
 
 // Resolves the pipelined batch, if any (every call that observes state or fires windows comes here first).
 gwo_status Handle::log_flush() {
-    if (!logst || !logst->job.active) return GWO_OK;
-    LogJob J = logst->job;
-    logst->job.active = false;
-    return log_resolve_k1(J);
+    if (logst && logst->job.active) {
+        LogJob J = logst->job;
+        logst->job.active = false;
+        GWO_TRY(log_resolve_k1(J));
+    }
+    return comm_flush_received();   // records received by the multi-GPU exchange and not yet inserted
 }
 
 gwo_status Handle::insert_log(const int64_t *k, const int64_t *t, const int64_t *v, int64_t n, int64_t stride,
-                              const LogRoute *route, bool ts32, int64_t tbase) {
+                              const LogRoute *route, bool ts32, int64_t tbase, const WindowGeom *geom_at) {
     LogState &L = *logst;
     LogJob J;
     if (route) J.rt = *route;
@@ -696,7 +698,7 @@ gwo_status Handle::insert_log(const int64_t *k, const int64_t *t, const int64_t 
     J.v = v;
     J.n = n;
     J.stride = stride;
-    J.g = log_geom_now();
+    J.g = geom_at ? *geom_at : log_geom_now();
     if (slog) GWO_TRY(slog_reserve(n));
     J.base = hist_hint;
     J.nunits = (int)std::min<long long>(LOG_NU, std::max<long long>(1, L.span_hint));
@@ -732,8 +734,14 @@ gwo_status Handle::insert_log(const int64_t *k, const int64_t *t, const int64_t 
 // end - 1 > (watermark at its K1), so that needs a window end in (that watermark, new_wm].
 bool Handle::log_pending_may_fire(int64_t new_wm) const {
     const LogState &L = *logst;
+    int64_t rwm;
+    if (comm_pending_wm(&rwm) && log_may_fire_since(rwm, new_wm)) return true;   // deferred received records
     if (!L.job.active) return false;
-    const __int128 w0 = (__int128)L.job.g.wm + 1;
+    return log_may_fire_since(L.job.g.wm, new_wm);
+}
+
+bool Handle::log_may_fire_since(int64_t batch_wm, int64_t new_wm) const {
+    const __int128 w0 = (__int128)batch_wm + 1;
     const __int128 size = cfg.size, off = geom.unit_off_mod;
     __int128 q = (w0 - off) / size;
     if ((w0 - off) % size < 0) q -= 1;                  // floor division
