@@ -301,6 +301,8 @@ gwo_status Handle::advance_watermark(int64_t new_wm) {
     new_wm = in_wm;
     if (comm) GWO_TRY(comm_min_watermark(in_wm, &new_wm));
     if (new_wm <= wm) return GWO_OK;
+    // a pipelined combine batch whose windows this watermark may fire is resolved first
+    if (cb_pend.active && log_may_fire_since(cb_pend.wm, new_wm)) GWO_TRY(combine_flush());
     gwo_status s = GWO_OK;
     switch (cfg.assigner) {
         case GWO_ASSIGNER_TUMBLING: s = logst ? fire_log(new_wm) : fire_tumbling(new_wm); break;
@@ -370,6 +372,7 @@ gwo_status Handle::poll_fire() {
 }
 
 gwo_status Handle::state_size(int64_t *entries) {
+    GWO_TRY(combine_flush());
     if (cfg.assigner == GWO_ASSIGNER_SESSION) return session_state_size(entries);
     if (logst) return log_state_size(entries);
     GWO_TRY(read_occupancy());

@@ -159,7 +159,7 @@ struct Handle {
     uint64_t recent_cap = 0;                           // capacity of the last retired window/pane table
     int cb_max_wg = 0;                                 // gather workgroups at most (GWO_CB_WG; default 4 per CU)
     DevBuf cb_dump_key, cb_dump_acc, cb_ovf, cb_blk, cb_ctr, cb_dir;   // combine path scratch (insert_combined)
-    unsigned long long *cb_rb = nullptr, *cb_rb_dev = nullptr;        // host-mapped readback block
+    unsigned long long *cb_rb = nullptr, *cb_rb_dev = nullptr;        // host-mapped readback blocks (2 slots)
     unsigned long long cb_seq = 0;
     hipEvent_t cb_ev = nullptr;
     std::vector<TableDesc> cb_dir_host;                                // what cb_dir holds
@@ -263,6 +263,25 @@ struct Handle {
     gwo_status insert_windowed(const int64_t *k, const int64_t *t, const int64_t *v, int64_t n,
                                const WindowGeom *at = nullptr);
     gwo_status insert_combined(const int64_t *k, const int64_t *t, const int64_t *v, int64_t n, bool *done);
+    // Pipelined submission of the combine path (gwo_set_pipelined_submit, tumbling, caller-owned device columns):
+    // gwo_submit queues the batch's gather and speculative merge and returns after reading the PREVIOUS batch's
+    // readback, so the host's turnaround overlaps the GPU's work.  The gather chains its verdict on the previous
+    // one (CombineArgs::chain): a batch the host must take over keeps its successor's merge off, and both are redone
+    // in order.
+    struct CbPend {
+        bool active = false;
+        const int64_t *k = nullptr, *t = nullptr, *v = nullptr;
+        int64_t n = 0;
+        int slot = 0;
+        unsigned long long seq = 0;
+        long long hint = 0;   // units hint, hint + 1: the speculative merge's tables
+        int64_t wm = 0;       // the watermark the batch was classified at
+    } cb_pend;
+    bool pipe_submit = false;   // gwo_set_pipelined_submit
+    bool cb_redo = false;       // redoing a batch the pipelined verdict turned down: no pipelining
+    bool combine_pipe_ok(const int64_t *k, const int64_t *t, const int64_t *v) const;
+    gwo_status combine_resolve_pending(bool *go);
+    gwo_status combine_flush();   // resolve the pending pipelined batch (no-op without one)
     gwo_status insert_speculative(const int64_t *k, const int64_t *t, const int64_t *v, int64_t n, bool *done);
     gwo_status refire_rows(const int64_t *k, const int64_t *t, const int64_t *v, int64_t n, const WindowGeom &g,
                            long long dir_base, int dir_len, uint64_t mmax);

@@ -139,6 +139,9 @@ struct CombineArgs {
     // speculation: the merge queued right behind the gather runs iff the gather's verdict *go is 1 -- no error,
     // no re-fire, no listed record, every record in units hint / hint + 1 whose tables exist with room
     uint32_t *go;                      // NULL: no speculative merge
+    // pipelined submission: *go still holds the previous batch's verdict, which the host has not read yet; a no
+    // there is a no here too (the host redoes both batches in order)
+    int32_t chain;
     uint64_t cap[2];                   // capacities of the hint tables
     long long side_cap;
     unsigned long long *dbg;           // GWO_CB_TRACE: phase times on the device wall clock (NULL: off)

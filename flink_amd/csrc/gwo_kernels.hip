@@ -824,7 +824,7 @@ __global__ __launch_bounds__(CB_THREADS) void gather_kernel(const int64_t *__res
     __syncthreads();
     CB_STAMP(5);
     if (tid == 0) {   // the speculative merge's verdict
-        bool go = a.go != nullptr && s_tot[CS_ACC] > 0 && s_tot[CS_BADTS] == 0 && s_tot[CS_BADRANGE] == 0 &&
+        bool go = a.go != nullptr && (!a.chain || *(volatile const uint32_t *)a.go != 0u) && s_tot[CS_ACC] > 0 && s_tot[CS_BADTS] == 0 && s_tot[CS_BADRANGE] == 0 &&
                   s_tot[CS_BADKG] == 0 && s_tot[CS_REFIRE] == 0 && s_tot[CS_HOUT] == 0 && s_spec[0] == 0 &&
                   (!a.side_enabled || (long long)s_spec[1] <= a.side_cap) &&
                   (long long)s_tot[CS_MIN] >= a.hint && (long long)s_tot[CS_MAX] <= a.hint + 1;

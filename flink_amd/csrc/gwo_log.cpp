@@ -913,7 +913,9 @@ gwo_status Handle::finish_fire() {
 }
 
 gwo_status Handle::set_pipelined(bool on) {
-    if (!logst) return GWO_OK;   // other layouts resolve every batch inside gwo_submit
+    if (!on) GWO_TRY(combine_flush());
+    pipe_submit = on;             // the combine path (tumbling tables; combine_pipe_ok)
+    if (!logst) return GWO_OK;    // other layouts resolve every batch inside gwo_submit
     if (!on) GWO_TRY(log_flush());
     logst->pipeline = on;
     return GWO_OK;

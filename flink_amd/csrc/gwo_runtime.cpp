@@ -466,15 +466,29 @@ gwo_status Handle::insert_combined(const int64_t *k, const int64_t *t, const int
     a.blk = (unsigned long long *)cb_blk.ptr;
     a.done = (unsigned long long *)cb_ctr.ptr + 1;
     if (!cb_rb) {
-        GWO_TRY(hipcheck(hipHostMalloc((void **)&cb_rb, CB_RB_WORDS * 8, hipHostMallocCoherent | hipHostMallocMapped),
+        GWO_TRY(hipcheck(hipHostMalloc((void **)&cb_rb, 2 * CB_RB_WORDS * 8, hipHostMallocCoherent | hipHostMallocMapped),
                          "combine readback"));
-        memset(cb_rb, 0, CB_RB_WORDS * 8);
+        memset(cb_rb, 0, 2 * CB_RB_WORDS * 8);
         GWO_TRY(hipcheck(hipHostGetDevicePointer((void **)&cb_rb_dev, cb_rb, 0), "combine readback"));
         GWO_TRY(hipcheck(hipEventCreateWithFlags(&cb_ev, hipEventDisableTiming), "event"));
     }
-    a.rb = cb_rb_dev;
+    // pipelined: the previous batch's readback slot is still unread, so this batch takes the other one
+    const bool pipe = combine_pipe_ok(k, t, v);
+    const int slot = cb_pend.active ? (cb_pend.slot ^ 1) : 0;
+    unsigned long long *const rb = cb_rb + (size_t)slot * CB_RB_WORDS;
+    a.rb = cb_rb_dev + (size_t)slot * CB_RB_WORDS;
     a.seq = ++cb_seq;
+    a.chain = cb_pend.active ? 1 : 0;
     a.side_enabled = side_enabled();
+    // tumbling: the next window's table exists before its first records arrive (sized like the last retired one),
+    // so the batch that crosses into it keeps the speculative merge (and a pipelined batch needs no redo)
+    if (cfg.assigner == GWO_ASSIGNER_TUMBLING && use_combine_spec && !slide && tables.count(hist_hint) &&
+        !tables.count(hist_hint + 1)) {
+        const __int128 end1 = (__int128)(hist_hint + 2) * cfg.size + geom.unit_off_mod;   // window hint + 1's end
+        if (end1 - 1 > (__int128)wm && end1 <= (__int128)(int64_t)0x7fffffffffffffffLL &&
+            end1 - cfg.size >= (__int128)(int64_t)0x8000000000000000LL)
+            GWO_TRY(ensure_table(hist_hint + 1, 0));
+    }
     Table *hint_tab[2] = {nullptr, nullptr};
     for (int j = 0; j < 2; ++j) {
         auto it = tables.find(hist_hint + j);
@@ -524,7 +538,7 @@ gwo_status Handle::insert_combined(const int64_t *k, const int64_t *t, const int
     }
     static const int cb_trace = getenv("GWO_CB_TRACE") ? atoi(getenv("GWO_CB_TRACE")) : 0;
     std::vector<unsigned long long> h_dbg;
-    if (cb_trace) {   // phase times of this gather on the device wall clock (debugging aid)
+    if (cb_trace && !pipe) {   // phase times of this gather on the device wall clock (debugging aid)
         GWO_TRY(ensure_buf(cb_dbg, (size_t)G * 64));
         GWO_TRY(hipcheck(hipMemset(cb_dbg.ptr, 0, (size_t)G * 64), "trace"));
         a.dbg = (unsigned long long *)cb_dbg.ptr;
@@ -543,9 +557,42 @@ gwo_status Handle::insert_combined(const int64_t *k, const int64_t *t, const int
         GWO_TRY(launch_ok("merge"));
         prof_end(GWO_KERNEL_INSERT, n);
     }
+    if (pipe) {
+        CbPend Q;
+        Q.active = true;
+        Q.k = k;
+        Q.t = t;
+        Q.v = v;
+        Q.n = n;
+        Q.slot = slot;
+        Q.seq = a.seq;
+        Q.hint = hist_hint;
+        Q.wm = g.wm;
+        *done = true;
+        if (!cb_pend.active) {   // nothing to complete: return with this batch in flight
+            cb_pend = Q;
+            return GWO_OK;
+        }
+        bool go = false;
+        GWO_TRY(combine_resolve_pending(&go));   // the previous batch (usually finished by now)
+        if (go) {
+            cb_pend = Q;
+            return GWO_OK;
+        }
+        // the previous batch's verdict was no, so this one's is too (chained) and neither merge ran: once this
+        // gather is done, both go through the regular path, in order
+        GWO_TRY(spin_seq(rb + CB_RB_SEQ, Q.seq, "gather"));
+        const CbPend P = cb_pend;   // (a turned-down batch stays in cb_pend)
+        cb_pend.active = false;
+        cb_redo = true;
+        gwo_status s = insert_windowed(P.k, P.t, P.v, P.n);
+        if (s == GWO_OK) s = insert_windowed(k, t, v, n);
+        cb_redo = false;
+        return s;
+    }
     // the gather's last workgroup writes the readback block, sequence word last: spin on it (the stream is polled
     // now and then so that a failed launch cannot spin forever)
-    GWO_TRY(spin_seq(cb_rb + CB_RB_SEQ, a.seq, "gather"));
+    GWO_TRY(spin_seq(rb + CB_RB_SEQ, a.seq, "gather"));
     if (cb_trace) {   // per phase: the latest workgroup end (from the first start) and the longest in-workgroup time
         h_dbg.resize((size_t)G * 8);
         GWO_TRY(hipcheck(hipMemcpy(h_dbg.data(), cb_dbg.ptr, (size_t)G * 64, hipMemcpyDeviceToHost), "trace"));
@@ -571,11 +618,11 @@ gwo_status Handle::insert_combined(const int64_t *k, const int64_t *t, const int
     }
     __atomic_thread_fence(__ATOMIC_ACQUIRE);
     BatchStats &hs = *h_stats;
-    memcpy(h_stats, cb_rb, sizeof(BatchStats));
-    *h_scalar = cb_rb[CB_RB_SIDE];
+    memcpy(h_stats, rb, sizeof(BatchStats));
+    *h_scalar = rb[CB_RB_SIDE];
     for (int j = 0; j < 2; ++j)
-        if (hint_tab[j]) hint_tab[j]->occ = cb_rb[CB_RB_OCC + j];   // exact: the previous merges are done
-    if (spec && cb_rb[CB_RB_GO]) {   // the speculative merge ran: only the bookkeeping is left
+        if (hint_tab[j]) hint_tab[j]->occ = rb[CB_RB_OCC + j];   // exact: the previous merges are done
+    if (spec && rb[CB_RB_GO]) {   // the speculative merge ran: only the bookkeeping is left
         if (side_enabled()) side_rows = side_rows_committed = *h_scalar;
         else late_dropped += hs.late;
         for (int j = 0; j < 2; ++j)   // upper bound until the next readback
@@ -660,6 +707,53 @@ gwo_status Handle::insert_combined(const int64_t *k, const int64_t *t, const int
     hist_hint = lo;
     for (auto &kv : tables) kv.second.dirty = true;
     return GWO_OK;
+}
+
+
+// The combine path may pipeline a batch (gwo_set_pipelined_submit): tumbling windows with the speculative merge,
+// allowedLateness 0, no side output, one GPU, caller-owned device columns (staged host input is reused by the next
+// batch), and not while a turned-down batch is being redone.
+bool Handle::combine_pipe_ok(const int64_t *k, const int64_t *t, const int64_t *v) const {
+    return pipe_submit && !cb_redo && use_combine_spec && cfg.assigner == GWO_ASSIGNER_TUMBLING && !slide && !sess &&
+           !logst && cfg.allowed_lateness == 0 && !side_enabled() && !comm && !dict &&
+           (const void *)k != stage_key.ptr && (const void *)t != stage_ts.ptr && (!v || (const void *)v != stage_val.ptr);
+}
+
+// Reads the pending batch's readback.  Yes: its speculative merge ran -- the bookkeeping insert_combined does after
+// its own wait.  No: nothing of the batch was applied (cb_pend keeps it for the caller to redo).
+gwo_status Handle::combine_resolve_pending(bool *go) {
+    const CbPend &P = cb_pend;
+    const unsigned long long *rb = cb_rb + (size_t)P.slot * CB_RB_WORDS;
+    GWO_TRY(spin_seq(rb + CB_RB_SEQ, P.seq, "gather"));
+    *go = rb[CB_RB_GO] != 0;
+    if (!*go) return GWO_OK;
+    memcpy(h_stats, rb, sizeof(BatchStats));
+    const BatchStats &hs = *h_stats;
+    for (int j = 0; j < 2; ++j) {
+        auto it = tables.find(P.hint + j);
+        if (it == tables.end()) continue;
+        it->second.occ = rb[CB_RB_OCC + j];   // exact before the batch's merge, plus an upper bound of its keys
+        if (hs.hist[j]) it->second.occ += std::min<uint64_t>(hs.hist[j], hs.distinct[j]);
+    }
+    late_dropped += hs.late;
+    adapt_preagg(hs.accepted, hs.distinct[0] + hs.distinct[1] + hs.overflow);
+    hist_hint = hs.min_idx;
+    for (auto &kv : tables) kv.second.dirty = true;
+    cb_pend.active = false;
+    return GWO_OK;
+}
+
+gwo_status Handle::combine_flush() {
+    if (!cb_pend.active) return GWO_OK;
+    bool go = false;
+    GWO_TRY(combine_resolve_pending(&go));
+    if (go) return GWO_OK;
+    const CbPend P = cb_pend;
+    cb_pend.active = false;
+    cb_redo = true;
+    const gwo_status s = insert_windowed(P.k, P.t, P.v, P.n);
+    cb_redo = false;
+    return s;
 }
 
 // Spins on a host-mapped readback block's sequence word (written last by a kernel's final workgroup).  Now and
@@ -770,6 +864,8 @@ gwo_status Handle::insert_speculative(const int64_t *k, const int64_t *t, const 
 
 gwo_status Handle::insert_windowed(const int64_t *k, const int64_t *t, const int64_t *v, int64_t n,
                                    const WindowGeom *at) {
+    if (cb_pend.active && (at || !use_preagg || !use_combine || n >= (1LL << 31) || !combine_pipe_ok(k, t, v)))
+        GWO_TRY(combine_flush());   // a pipelined batch completes before a batch that takes another path
     if (!at && use_preagg && use_combine && n < (1LL << 31)) {
         bool done = false;
         GWO_TRY(insert_combined(k, t, v, n, &done));
@@ -1175,6 +1271,7 @@ gwo_status gwo_result_dtype(const gwo_handle *hh, int32_t agg, int32_t *dtype) {
 gwo_status gwo_late_dropped(gwo_handle *hh, int64_t *count) {
     H_OR_FAIL;
     if (!count) return GWO_ERR_INVALID_ARGUMENT;
+    GWO_TRY(h->combine_flush());
     GWO_TRY(h->log_flush());
     *count = (int64_t)h->late_dropped;
     return GWO_OK;
@@ -1233,6 +1330,7 @@ gwo_status gwo_restore(gwo_handle *hh, const gwo_state_rows *rows, int32_t n_wor
 
 gwo_status gwo_sync(gwo_handle *hh) {
     H_OR_FAIL;
+    GWO_TRY(h->combine_flush());
     if (h->logst) GWO_TRY(h->log_flush());
     if (h->logst) GWO_TRY(h->log_resolve_split());
     GWO_TRY(h->finish_fire());

@@ -193,7 +193,11 @@ def test_c5_sessions_100k_keys_10m_records(F, variant):
     _compare(counts, sums, kept, srows, scs, rows, 4)
 
 
-def test_c2_ysb_campaign_count_1m_batches(F):
+@pytest.mark.parametrize("pipelined", [False, True])
+def test_c2_ysb_campaign_count_1m_batches(F, pipelined):
+    """pipelined: gwo_set_pipelined_submit -- each batch's gather and speculative merge queue before the previous
+    batch's readback is read (the bench's mode for C2); window crossings turn the chained verdicts down and both
+    batches are redone in order."""
     import torch
     from flink_amd import _native as N
     n, every, span = 100_000_000, 1_000_000, 100_000
@@ -206,6 +210,8 @@ def test_c2_ysb_campaign_count_1m_batches(F):
     batches.append((n, LONG_MAX))
     op = F.GpuWindowOperator(F.TumblingEventTimeWindows.of(10_000), F.CountAggregate(), max_parallelism=128,
                              expected_keys=1000)
+    if pipelined:
+        N.check(N.lib().gwo_set_pipelined_submit(op.handle, 1), op.handle)
     nb = len(batches)
     counts, sums, kept = _run_steps(N, op.handle, key, ts, val, batches, 1, set(range(nb)))
     late_gpu = op.num_late_records_dropped

@@ -177,3 +177,38 @@ def test_virtual_ranks_after_restore(F, monkeypatch):
     assert sorted((a_, s, e, *r) for a_, s, e, r in rows + list(c.output)) == want
     assert late + c.num_late_records_dropped == want_late
     c.close()
+
+
+@pytest.mark.parametrize("defer", [1, 0])
+def test_virtual_ranks_deferred_receives_snapshot(F, monkeypatch, defer):
+    """Deferred receives (GWO_COMM_DEFER=1, the default): a routed batch's received records are inserted at the next
+    routed batch, or earlier when a watermark may fire their windows or state is observed.  Watermarks every 2,500
+    records against 5-s windows, so most watermarks leave the receives pending; a snapshot taken in the middle (with a
+    receive pending) must hold them, and the restored subtask (no communicator) continues to the oracle's output.
+    defer=0 runs the same stream with every batch's receives inserted inside its gwo_submit."""
+    monkeypatch.setenv("GWO_COMM_DEFER", str(defer))
+    k, t, v, b = _stream(n=150_000, nkeys=20_000, every=2_500, lag=700, seed=21)
+    mk = lambda: F.GpuWindowOperator(F.TumblingEventTimeWindows.of(5000),
+                                     F.MultiAggregate(F.SumAggregate(), F.MinAggregate(), F.CountAggregate()),
+                                     state_layout="log", max_parallelism=32768)
+    a = mk()
+    _virtual(F, a, monkeypatch, 4)
+    half = len(b) // 2
+    prev = 0
+    for end, wm in b[:half]:
+        a.process_batch(k[prev:end], t[prev:end], v[prev:end])
+        a.process_watermark(wm)
+        prev = end
+    a.process_batch(k[prev:b[half][0]], t[prev:b[half][0]], v[prev:b[half][0]])   # pending, no watermark after it
+    prev = b[half][0]
+    snap = a.snapshot_state()
+    rows, late = list(a.output), a.num_late_records_dropped
+    a.close()
+    c = mk()
+    c.restore_state(snap)
+    _drive(c, k[prev:], t[prev:], v[prev:], [(e - prev, w) for e, w in b[half:]])
+    (wk, ws, we, res), want_late = V.tumbling_lateness0(k, t, v, b + [(len(k), LONG_MAX)], 5000, 0, [1, 2, 0])
+    want = sorted(zip(wk.tolist(), ws.tolist(), we.tolist(), *[r.tolist() for r in res]))
+    assert sorted((a_, s, e, *r) for a_, s, e, r in rows + list(c.output)) == want
+    assert late + c.num_late_records_dropped == want_late
+    c.close()

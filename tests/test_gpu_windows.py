@@ -749,6 +749,20 @@ def test_log_layout_pipelined_submit_matches_oracle(F, split):
     assert got == _want(wk, ws, we, res)
 
 
+@pytest.mark.parametrize("split", [1, 3])
+def test_combine_pipelined_submit_matches_oracle(F, split):
+    """Pipelined submission on the combine path (table layout, few keys: gather + speculative merge): batch i's
+    kernels queue before batch i-1's readback is read.  2-s windows with 20K-record watermark intervals cross a
+    window every few batches, so chained verdicts are turned down and redone in order; late records are counted."""
+    k, t, v, b = _c1(n=600_000, nkeys=1_000, every=20_000, lag=200, disorder=1500, seed=13)
+    v = v - 500
+    agg = F.MultiAggregate(F.SumAggregate(), F.MinAggregate(), F.MaxAggregate(), F.CountAggregate())
+    got, late = _pipelined_run(F, k, t, v, b, agg, 2000, 300, split=split, expected_keys=1_000, layout="table")
+    (wk, ws, we, res), want_late = V.tumbling_lateness0(k, t, v, _final(b), 2000, 300, [1, 2, 3, 0])
+    assert want_late > 0 and late == want_late
+    assert got == _want(wk, ws, we, res)
+
+
 def test_log_layout_pipelined_window_jumps_and_wide_batches(F):
     """Event time jumps many windows between batches (the pipelined K1's window-range guess is wrong and
     must be re-run) and batches spanning more windows than one K1 covers (multi-range resolution)."""
