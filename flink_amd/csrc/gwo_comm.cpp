@@ -494,8 +494,13 @@ extern "C" gwo_status gwo_comm_init(gwo_handle *hh, const uint8_t *id, int32_t n
         return GWO_ERR_OUT_OF_MEMORY;
     }
     if (const char *e = getenv("GWO_COMM_DEFER")) C->defer = atoi(e) != 0;
+    // The count stream gets the greatest priority: HIP multiplexes streams onto a few hardware queues (4 per process
+    // on this pool), and a default-priority count stream shared the record stream's queue (measured in the kernel
+    // trace), so the watermark all-reduce waited behind the previous batch's records on the wire.
+    int prio_least = 0, prio_greatest = 0;
+    (void)hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest);
     if (hipStreamCreateWithFlags(&C->cs, hipStreamNonBlocking) != hipSuccess ||
-        hipStreamCreateWithFlags(&C->cs2, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithPriority(&C->cs2, hipStreamNonBlocking, prio_greatest) != hipSuccess ||
         hipEventCreateWithFlags(&C->ev_routed, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&C->ev_recv, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&C->ev_rrecv[0], hipEventDisableTiming) != hipSuccess ||
