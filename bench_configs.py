@@ -112,9 +112,9 @@ def run(cfg):
             for i, (s, e) in enumerate(bounds)]
     submit, advance, discard = lib.gwo_submit, lib.gwo_advance_watermark, lib.gwo_discard_output
     warm = max(1, len(bounds) // 10)
-    # pipelined submission where the combine path runs (C2); C1's 10K-record batches measured slower with it
+    # pipelined submission on the combine path (C2) and sessions (C5); C1's 10K-record batches measured slower with it
     # (36.4 vs 33.7 us/step: the adaptive pre-aggregation probe batches get redone)
-    pipe = os.environ.get("BENCH_PIPE", "1" if cfg == "c2" else "0") != "0"
+    pipe = os.environ.get("BENCH_PIPE", "1" if cfg in ("c2", "c5") else "0") != "0"
 
     def drive(prof):
         """One operator over the whole stream: `warm` untimed steps, then the rest timed.  prof: per-kernel HIP

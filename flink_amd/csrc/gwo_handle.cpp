@@ -372,7 +372,7 @@ gwo_status Handle::poll_fire() {
 }
 
 gwo_status Handle::state_size(int64_t *entries) {
-    GWO_TRY(combine_flush());
+    GWO_TRY(flush_pending());
     if (cfg.assigner == GWO_ASSIGNER_SESSION) return session_state_size(entries);
     if (logst) return log_state_size(entries);
     GWO_TRY(read_occupancy());

@@ -282,6 +282,11 @@ struct Handle {
     bool combine_pipe_ok(const int64_t *k, const int64_t *t, const int64_t *v) const;
     gwo_status combine_resolve_pending(bool *go);
     gwo_status combine_flush();   // resolve the pending pipelined batch (no-op without one)
+    gwo_status flush_pending();   // every pipelined batch (combine path, sessions) resolved
+    gwo_status sess_publish_err();
+    gwo_status sess_collect_err();
+    gwo_status sess_apply_err();
+    gwo_status sess_resolve();
     gwo_status insert_speculative(const int64_t *k, const int64_t *t, const int64_t *v, int64_t n, bool *done);
     gwo_status refire_rows(const int64_t *k, const int64_t *t, const int64_t *v, int64_t n, const WindowGeom &g,
                            long long dir_base, int dir_len, uint64_t mmax);

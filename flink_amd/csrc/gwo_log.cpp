@@ -913,8 +913,8 @@ gwo_status Handle::finish_fire() {
 }
 
 gwo_status Handle::set_pipelined(bool on) {
-    if (!on) GWO_TRY(combine_flush());
-    pipe_submit = on;             // the combine path (tumbling tables; combine_pipe_ok)
+    if (!on) GWO_TRY(flush_pending());
+    pipe_submit = on;             // the combine path (tumbling tables; combine_pipe_ok) and sessions
     if (!logst) return GWO_OK;    // other layouts resolve every batch inside gwo_submit
     if (!on) GWO_TRY(log_flush());
     logst->pipeline = on;

@@ -743,6 +743,11 @@ gwo_status Handle::combine_resolve_pending(bool *go) {
     return GWO_OK;
 }
 
+gwo_status Handle::flush_pending() {
+    GWO_TRY(combine_flush());
+    return sess_resolve();
+}
+
 gwo_status Handle::combine_flush() {
     if (!cb_pend.active) return GWO_OK;
     bool go = false;
@@ -1271,7 +1276,7 @@ gwo_status gwo_result_dtype(const gwo_handle *hh, int32_t agg, int32_t *dtype) {
 gwo_status gwo_late_dropped(gwo_handle *hh, int64_t *count) {
     H_OR_FAIL;
     if (!count) return GWO_ERR_INVALID_ARGUMENT;
-    GWO_TRY(h->combine_flush());
+    GWO_TRY(h->flush_pending());
     GWO_TRY(h->log_flush());
     *count = (int64_t)h->late_dropped;
     return GWO_OK;
@@ -1330,7 +1335,7 @@ gwo_status gwo_restore(gwo_handle *hh, const gwo_state_rows *rows, int32_t n_wor
 
 gwo_status gwo_sync(gwo_handle *hh) {
     H_OR_FAIL;
-    GWO_TRY(h->combine_flush());
+    GWO_TRY(h->flush_pending());
     if (h->logst) GWO_TRY(h->log_flush());
     if (h->logst) GWO_TRY(h->log_resolve_split());
     GWO_TRY(h->finish_fire());

@@ -48,6 +48,10 @@ struct SessionState {
     // host-mapped readback of the statistics block (publish_words_kernel): the batch's read-back is a spin
     unsigned long long *rb = nullptr, *rb_dev = nullptr;
     unsigned long long rb_seq = 0;
+    // pipelined submission (gwo_set_pipelined_submit, allowedLateness 0, no side output): the batch's readback is
+    // published but not read yet -- read at the watermark right after its sweep is queued, or at any other call
+    bool rb_pending = false;
+    uint64_t pend_n = 0;
 };
 
 gwo_status Handle::sess_alloc(uint64_t cap, Table &t, int64_t **due) {
@@ -133,13 +137,23 @@ static SessGeom sess_geom(const Handle &h, int smax) {
     return g;
 }
 
-gwo_status Handle::sess_read_err() {
+gwo_status Handle::sess_publish_err() {
     SessionState &S = *sess;
     // the statistics and, right behind them, the pool's bump counter: published into host-mapped memory by a
     // one-wave kernel behind the batch's kernels, spun on (no copy, no stream synchronisation)
     constexpr int NWD = (int)(sizeof(SessErr) / 8) + 1;
     launch_publish_words((const unsigned long long *)S.d_err, NWD, S.rb_dev, ++S.rb_seq, stream);
-    GWO_TRY(launch_ok("session readback"));
+    return launch_ok("session readback");
+}
+
+gwo_status Handle::sess_read_err() {
+    GWO_TRY(sess_publish_err());
+    return sess_collect_err();
+}
+
+gwo_status Handle::sess_collect_err() {
+    SessionState &S = *sess;
+    constexpr int NWD = (int)(sizeof(SessErr) / 8) + 1;
     GWO_TRY(spin_seq(S.rb + NWD, S.rb_seq, "session readback"));
     memcpy(S.h_err, S.rb, sizeof(SessErr) + 8);
     S.pool_top = *(const unsigned long long *)((const char *)S.h_err + sizeof(SessErr));
@@ -221,7 +235,12 @@ gwo_status Handle::read_occupancy_one(Table &t) {
 
 gwo_status Handle::insert_session(const int64_t *k, const int64_t *t, const int64_t *v, int64_t n) {
     SessionState &S = *sess;
-    GWO_TRY(finish_fire());   // the last watermark's sweep (usually complete by now: no wait)
+    // The last watermark's sweep is left running: the batch's kernels queue right behind it (no idle gap while the
+    // host waits for it), and its rows and live-session change are applied at the next output access or watermark
+    // (sizing below only needs upper bounds, which the unretired sessions give).  With allowedLateness > 0 the batch
+    // emits re-fire rows behind the sweep's, so the sweep's rows are published first.
+    if (cfg.allowed_lateness > 0) GWO_TRY(finish_fire());
+    GWO_TRY(sess_resolve());   // a pipelined batch's readback (sizing below reads the live-session count)
     if (n > 0xffffffffll) return fail(GWO_ERR_INVALID_ARGUMENT, "session batches are limited to 2^32 records");
     GWO_TRY(sess_ensure((uint64_t)n));
     GWO_TRY(sess_ensure_pool((uint64_t)n));
@@ -254,7 +273,26 @@ gwo_status Handle::insert_session(const int64_t *k, const int64_t *t, const int6
                         side_enabled() ? side_cap : 0, stream);
     GWO_TRY(launch_ok("sess process"));
     prof_end(GWO_KERNEL_SESSION, n);
-    GWO_TRY(sess_read_err());
+    GWO_TRY(sess_publish_err());
+    if (pipe_submit && cfg.allowed_lateness == 0 && !side_enabled()) {   // read at the watermark (sess_resolve)
+        S.rb_pending = true;
+        S.pend_n = (uint64_t)n;
+        return GWO_OK;
+    }
+    GWO_TRY(sess_collect_err());
+    return sess_apply_err();
+}
+
+// Reads and applies a pipelined batch's readback (no-op without one).
+gwo_status Handle::sess_resolve() {
+    if (!sess || !sess->rb_pending) return GWO_OK;
+    sess->rb_pending = false;
+    GWO_TRY(sess_collect_err());
+    return sess_apply_err();
+}
+
+gwo_status Handle::sess_apply_err() {
+    SessionState &S = *sess;
     const SessErr &e = S.e;
     if (e.bad_ts)
         return poison(GWO_ERR_NO_TIMESTAMP, "Record has Long.MIN_VALUE timestamp (= no timestamp marker).");
@@ -285,8 +323,11 @@ gwo_status Handle::insert_session(const int64_t *k, const int64_t *t, const int6
 gwo_status Handle::fire_session(int64_t new_wm) {
     SessionState &S = *sess;
     GWO_TRY(finish_fire());
-    if (S.live == 0) return GWO_OK;
-    GWO_TRY(ensure_output(S.live));
+    // a pipelined batch still unread adds at most one live session per record: the sweep is sized for that and
+    // queued right behind the batch, then the batch's readback is read
+    const uint64_t live_bound = S.live + (S.rb_pending ? S.pend_n : 0);
+    if (live_bound == 0) return sess_resolve();
+    GWO_TRY(ensure_output(live_bound));
     SessGeom g = sess_geom(*this, S.smax);
     g.wm = new_wm;
     prof_begin(GWO_KERNEL_FIRE);
@@ -297,7 +338,7 @@ gwo_status Handle::fire_session(int64_t new_wm) {
                      "fire err"));
     GWO_TRY(hipcheck(hipEventRecord(ev_fire, stream), "event"));
     fire_pending = true;
-    return GWO_OK;
+    return sess_resolve();
 }
 
 gwo_status Handle::session_finish_fire() {
@@ -318,6 +359,7 @@ gwo_status Handle::session_finish_fire() {
 }
 
 gwo_status Handle::session_state_size(int64_t *entries) {
+    GWO_TRY(sess_resolve());
     GWO_TRY(finish_fire());
     *entries = (int64_t)sess->live;
     return GWO_OK;

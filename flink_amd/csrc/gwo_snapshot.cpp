@@ -34,7 +34,7 @@ struct Scratch {
 // Completes everything queued (a pipelined batch, a deferred pass 2, a running fire): a checkpoint is taken
 // between records (prepareSnapshotPreBarrier flushes the operator's batch first, AbstractStreamOperator.java:303).
 gwo_status Handle::snapshot_quiesce() {
-    GWO_TRY(combine_flush());
+    GWO_TRY(flush_pending());
     if (logst) {
         GWO_TRY(log_flush());
         GWO_TRY(log_resolve_split());

@@ -526,6 +526,44 @@ def test_sessions_out_of_order_with_lateness(F, lateness):
     op.close()
 
 
+@pytest.mark.parametrize("split", [1, 3])
+def test_sessions_pipelined_submit_matches_oracle(F, split):
+    """Pipelined submission on sessions: a batch's readback is read at the next watermark, right after that
+    watermark's sweep is queued (sized for every unread record opening a session), or at the next call; the sweep
+    of the previous watermark stays running while the next batch queues.  Several batches between watermarks, merges,
+    bridging and late drops, as the oracle sees them."""
+    import ctypes as C
+    import torch
+    from flink_amd import _native as N
+    lib = N.lib()
+    rng = np.random.default_rng(17)
+    n = 30_000
+    k = rng.integers(0, 400, n)
+    t = np.sort(rng.integers(0, 400_000, n)) + rng.integers(0, 6_000, n)
+    v = rng.integers(0, 100, n)
+    b = G.punctuated_watermarks(t, 600, 1_000)
+    ref = _session_oracle(k, t, v, b, 2_000, 0)
+    dk, dt, dv = (torch.from_numpy(np.ascontiguousarray(x, dtype=np.int64)).cuda() for x in (k, t, v))
+    op = F.GpuWindowOperator(F.EventTimeSessionWindows.withGap(2_000), F.SumAggregate())
+    h = op.handle
+    N.check(lib.gwo_set_pipelined_submit(h, 1), h)
+    prev = 0
+    for end, wm in b:
+        edges = np.linspace(prev, end, split + 1).astype(int)
+        for a, c in zip(edges[:-1].tolist(), edges[1:].tolist()):
+            if c > a:
+                N.check(lib.gwo_submit(h, C.c_void_p(dk.data_ptr() + 8 * a), C.c_void_p(dt.data_ptr() + 8 * a),
+                                       C.c_void_p(dv.data_ptr() + 8 * a), int(c - a)), h)
+        N.check(lib.gwo_advance_watermark(h, wm), h)
+        prev = end
+    assert prev == n
+    N.check(lib.gwo_end_input(h), h)
+    op._collect()
+    assert sorted(op.output) == sorted((r.key, r.start, r.end, r.result) for r in ref.output)
+    assert op.num_late_records_dropped == ref.num_late_records_dropped > 0
+    op.close()
+
+
 def test_fast_division_full_int64_range(F):
     """window_start_f/fdiv_floor (double reciprocal + exact corrections) against Java semantics over
     the whole int64 range, including the extremes and sizes from 1 to Long.MAX_VALUE."""
