@@ -179,6 +179,8 @@ struct Handle {
     hipEvent_t sp_ev = nullptr;
     int cfg_preagg = -1;                       // GWO_PREAGG env override: 0 / 1
     uint64_t batches = 0;
+    uint64_t preagg_probe_every = 32, preagg_probe_at = 32;   // adapt_preagg's re-probe schedule (backs off)
+    bool preagg_probing = false;
 
     // errors
     std::string err;

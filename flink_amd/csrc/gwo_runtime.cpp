@@ -993,12 +993,21 @@ gwo_status Handle::insert_windowed(const int64_t *k, const int64_t *t, const int
 
 void Handle::adapt_preagg(uint64_t accepted, uint64_t partials) {
     // Pre-aggregation pays when a tile folds several records per (key, window); measured by the
-    // partials it flushed.  Off: re-probe every 32 batches.
+    // partials it flushed.  Off: re-probe after 32 batches, backing off (x2 up to 1024 batches) while the probes
+    // keep finding no duplicates, so a stream without them stops paying for the probe.
     batches++;
     if (use_preagg) {
-        if (accepted > 0 && (double)partials > 0.5 * (double)accepted) use_preagg = 0;
-    } else if (batches % 32 == 0) {
+        if (accepted > 0 && (double)partials > 0.5 * (double)accepted) {
+            use_preagg = 0;
+            if (preagg_probing) preagg_probe_every = std::min<uint64_t>(2 * preagg_probe_every, 1024);
+            preagg_probe_at = batches + preagg_probe_every;
+        } else if (preagg_probing) {
+            preagg_probe_every = 32;   // the probe paid: back to the short schedule when it stops paying
+        }
+        preagg_probing = false;
+    } else if (batches >= preagg_probe_at) {
         use_preagg = 1;
+        preagg_probing = true;
     }
     if (cfg_preagg >= 0) use_preagg = cfg_preagg;
 }
