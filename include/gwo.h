@@ -254,11 +254,13 @@ gwo_status gwo_intern_utf16(gwo_handle *h, const uint16_t *chars, const int64_t 
 gwo_status gwo_key_strings(gwo_handle *h, const int64_t *ids, int64_t n, int64_t *offsets_out, uint16_t *chars_out,
                            int64_t chars_cap, int64_t *chars_needed);
 
-/* Pipelined submission (off by default; caller-owned device columns, no side output: the log layout, and the
- * table layout's combine path for tumbling windows with allowedLateness 0 on one GPU -- other batches are resolved
- * inside gwo_submit as usual).  gwo_submit queues the batch's partition kernel (log: K1; combine: the gather and its
- * speculative merge) and returns after completing the PREVIOUS batch (its classification checks and pass 2, or its
- * readback), so the host's wait and planning overlap a running kernel.  Observable results are unchanged: gwo_advance_watermark,
+/* Pipelined submission (off by default; caller-owned device columns, no side output: the log layout, the table
+ * layout's combine path for tumbling windows with allowedLateness 0 on one GPU, and session windows with
+ * allowedLateness 0 -- other batches are resolved inside gwo_submit as usual).  gwo_submit queues the batch's
+ * kernels (log: K1; combine: the gather and its speculative merge; sessions: sort and merge) and returns after
+ * completing the PREVIOUS batch (its classification checks and pass 2, or its readback; sessions: the batch's
+ * readback is read at the next watermark, after that watermark's sweep is queued), so the host's wait and planning
+ * overlap running kernels.  Observable results are unchanged: gwo_advance_watermark,
  * gwo_sync, gwo_late_dropped, gwo_state_size and the side-output calls complete the pending batch first.
  * What moves is error reporting: a batch's GWO_ERR_NO_TIMESTAMP / GWO_ERR_KEY_GROUP is returned by the
  * next call on the handle (the batch is still rejected before any window state changes, and the handle
