@@ -42,6 +42,7 @@ struct SlogState {
     std::vector<std::pair<long long, size_t>> pending;   // (pane, segment) added at the next window step
     uint64_t pending_records = 0;
     unsigned long long *d_stat = nullptr, *h_stat = nullptr;
+    unsigned long long *rb = nullptr, *rb_dev = nullptr, rb_seq = 0;   // host-mapped: the step's folded statistics
     DevBuf segdesc;
     std::vector<SlogSeg> h_segs;
     int groups = 0;                // CUs
@@ -91,6 +92,10 @@ gwo_status Handle::slog_init() {
     GWO_TRY(hipcheck(hipMemsetAsync(G.d_stat, 0, SLOG_SHARDS * SLOG_STAT_STRIDE * 8, stream), "ring stats"));
     GWO_TRY(hipcheck(hipHostMalloc((void **)&G.h_stat, SLOG_SHARDS * SLOG_STAT_STRIDE * 8, hipHostMallocDefault),
                      "pinned"));
+    GWO_TRY(hipcheck(hipHostMalloc((void **)&G.rb, (SLS_WORDS + 1) * 8, hipHostMallocCoherent | hipHostMallocMapped),
+                     "slog readback"));
+    memset(G.rb, 0, (SLS_WORDS + 1) * 8);
+    GWO_TRY(hipcheck(hipHostGetDevicePointer((void **)&G.rb_dev, G.rb, 0), "slog readback"));
     GWO_TRY(ensure_buf(G.segdesc, SLOG_MAX_SEGS * sizeof(SlogSeg)));
     int cus = 0;
     GWO_TRY(hipcheck(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, cfg.device), "CU count"));
@@ -132,6 +137,7 @@ void Handle::slog_free() {
     G.segdesc.release();
     if (G.d_stat) (void)hipFree(G.d_stat);
     if (G.h_stat) (void)hipHostFree(G.h_stat);
+    if (G.rb) (void)hipHostFree(G.rb);
     delete slog;
     slog = nullptr;
 }
@@ -254,20 +260,16 @@ gwo_status Handle::slog_step(int64_t start, int64_t end, uint64_t bound, size_t 
         const uint64_t rows0 = out_rows;
         for (int attempt = 0;; ++attempt) {
             a.o = out_cols();
-            GWO_TRY(hipcheck(hipMemsetAsync(G.d_stat, 0, SLOG_SHARDS * SLOG_STAT_STRIDE * 8, stream), "ring stats"));
+            // (the statistics shards are zero: reset at creation and by every step's publish)
             prof_begin(GWO_KERNEL_FIRE);
             launch_slog_fire(a, G.groups, stream);
             GWO_TRY(launch_ok("slog window step"));
             prof_end(GWO_KERNEL_FIRE, (int64_t)bound);
-            GWO_TRY(hipcheck(hipMemcpyAsync(G.h_stat, G.d_stat, SLOG_SHARDS * SLOG_STAT_STRIDE * 8,
-                                            hipMemcpyDeviceToHost, stream), "ring stats"));
-            GWO_TRY(hipcheck(hipStreamSynchronize(stream), "slog window step"));
+            launch_slog_stat_publish(G.d_stat, G.rb_dev, ++G.rb_seq, stream);
+            GWO_TRY(launch_ok("slog statistics"));
+            GWO_TRY(spin_seq(G.rb + SLS_WORDS, G.rb_seq, "slog window step"));
             uint64_t st[SLS_WORDS] = {};
-            for (int q = 0; q < SLOG_SHARDS; ++q)
-                for (int w = 0; w < SLS_WORDS; ++w) {
-                    const uint64_t x = G.h_stat[q * SLOG_STAT_STRIDE + w];
-                    st[w] = w == SLS_MAXP ? std::max(st[w], x) : st[w] + x;
-                }
+            for (int w = 0; w < SLS_WORDS; ++w) st[w] = G.rb[w];
             if (st[SLS_NEG] && !mode) return poison(GWO_ERR_HIP, "sliding log: a key's window count became negative");
             if (st[SLS_LDS]) return poison(GWO_ERR_CAPACITY, "sliding log: a partition overflowed its LDS table");
             if (st[SLS_ROVF]) {   // a partition of R' outgrew its region: larger regions, same step again

@@ -73,4 +73,5 @@ namespace gwo {
 size_t slog_lds_bytes(int cap_log2, int nwords);
 // One window step over every partition of a.in (persistent grid: every workgroup resident on the `cus` CUs).
 void launch_slog_fire(const SlogArgs &a, int cus, hipStream_t s);
+void launch_slog_stat_publish(unsigned long long *stat, unsigned long long *rb, unsigned long long seq, hipStream_t s);
 }  // namespace gwo

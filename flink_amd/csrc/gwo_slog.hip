@@ -502,6 +502,28 @@ __global__ __launch_bounds__(SLOG_THREADS) __attribute__((amdgpu_waves_per_eu(4,
     }
 }
 
+// The window step's statistics: the shards folded (sums; SLS_MAXP a max) into a host-mapped block, sequence word
+// last, and reset for the next step -- one wave behind the step instead of a memset, a copy and a stream
+// synchronisation (the host spins on the block).
+__global__ __launch_bounds__(64) void slog_stat_publish_kernel(unsigned long long *stat, unsigned long long *rb,
+                                                               unsigned long long seq) {
+    const int t = threadIdx.x;
+    if (t < SLS_WORDS) {
+        unsigned long long x[SLOG_SHARDS];
+#pragma unroll
+        for (int q = 0; q < SLOG_SHARDS; ++q) x[q] = atomicExch(&stat[q * SLOG_STAT_STRIDE + t], 0ull);
+        unsigned long long acc = 0;
+#pragma unroll
+        for (int q = 0; q < SLOG_SHARDS; ++q) acc = t == SLS_MAXP ? (x[q] > acc ? x[q] : acc) : acc + x[q];
+        rb_put(&rb[t], acc);
+    }
+    rb_publish(&rb[SLS_WORDS], seq);
+}
+
+void launch_slog_stat_publish(unsigned long long *stat, unsigned long long *rb, unsigned long long seq, hipStream_t s) {
+    hipLaunchKernelGGL(slog_stat_publish_kernel, dim3(1), dim3(64), 0, s, stat, rb, seq);
+}
+
 // Persistent grid: every workgroup resident at once (the occupancy of the instance at this LDS size, per CU, times
 // the CUs given as `groups`), so no workgroup waits for another to finish before it starts its partitions.
 void launch_slog_fire(const SlogArgs &a, int cus, hipStream_t s) {

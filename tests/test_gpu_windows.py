@@ -801,6 +801,67 @@ def test_combine_pipelined_submit_matches_oracle(F, split):
     assert got == _want(wk, ws, we, res)
 
 
+def test_combine_pipelined_snapshot_and_error(F):
+    """Pipelined combine path: a snapshot taken while a batch is still queued holds that batch (restored into a fresh
+    operator, the rest of the stream gives the oracle's rows); a batch carrying a Long.MIN_VALUE timestamp is reported
+    by the next call as GWO_ERR_NO_TIMESTAMP and fails the handle."""
+    import ctypes as C
+    import torch
+    from flink_amd import _native as N
+    lib = N.lib()
+    k, t, v, b = _c1(n=200_000, nkeys=500, every=20_000, lag=200, disorder=1500, seed=23)
+    dk, dt, dv = (torch.from_numpy(np.ascontiguousarray(x)).cuda() for x in (k, t, v))
+    agg = lambda: F.MultiAggregate(F.SumAggregate(), F.CountAggregate())
+    mk = lambda: F.GpuWindowOperator(F.TumblingEventTimeWindows.of(2000), agg(), state_layout="table",
+                                     expected_keys=500)
+    sub = lambda h, a, c: N.check(lib.gwo_submit(h, C.c_void_p(dk.data_ptr() + 8 * a), C.c_void_p(dt.data_ptr() + 8 * a),
+                                                 C.c_void_p(dv.data_ptr() + 8 * a), int(c - a)), h)
+    op = mk()
+    N.check(lib.gwo_set_pipelined_submit(op.handle, 1), op.handle)
+    half = len(b) // 2
+    prev = 0
+    for end, wm in b[:half]:
+        sub(op.handle, prev, end)
+        N.check(lib.gwo_advance_watermark(op.handle, wm), op.handle)
+        prev = end
+    sub(op.handle, prev, b[half][0])   # queued, its readback unread: the snapshot completes it
+    prev = b[half][0]
+    snap = op.snapshot_state()
+    op._collect()
+    rows, late = list(op.output), op.num_late_records_dropped
+    op.close()
+    c = mk()
+    c.restore_state(snap)
+    h = c.handle
+    N.check(lib.gwo_set_pipelined_submit(h, 1), h)
+    for end, wm in [(b[half][0], b[half][1])] + b[half + 1:]:
+        if end > prev:
+            sub(h, prev, end)
+        N.check(lib.gwo_advance_watermark(h, wm), h)
+        prev = end
+    N.check(lib.gwo_end_input(h), h)
+    c._collect()
+    (wk, ws, we, res), want_late = V.tumbling_lateness0(k, t, v, _final(b), 2000, 0, [1, 0])
+    got = sorted((a_, s_, e_, *r) for a_, s_, e_, r in rows + list(c.output))
+    assert got == _want(wk, ws, we, res)
+    assert late + c.num_late_records_dropped == want_late
+    c.close()
+    # a bad timestamp in a pipelined batch: the next call reports it
+    bad = t[:20_000].copy()
+    bad[777] = LONG_MIN
+    tb = torch.from_numpy(bad).cuda()
+    e = mk()
+    h = e.handle
+    N.check(lib.gwo_set_pipelined_submit(h, 1), h)
+    sub(h, 0, 20_000)
+    st = lib.gwo_submit(h, C.c_void_p(dk.data_ptr()), C.c_void_p(tb.data_ptr()), C.c_void_p(dv.data_ptr()), 20_000)
+    if st == 0:
+        st = lib.gwo_sync(h)
+    assert st == 2   # GWO_ERR_NO_TIMESTAMP
+    assert lib.gwo_advance_watermark(h, 10_000) == 2   # the handle stays failed
+    e.close()
+
+
 def test_log_layout_pipelined_window_jumps_and_wide_batches(F):
     """Event time jumps many windows between batches (the pipelined K1's window-range guess is wrong and
     must be re-run) and batches spanning more windows than one K1 covers (multi-range resolution)."""
