@@ -92,14 +92,38 @@ def host_cores():
     return cores, {"os_cpu_count": cpus, "affinity": aff, "cgroup_cpu_quota": quota}
 
 
+def kfd_gpu_count(topology="/sys/class/kfd/kfd/topology/nodes"):
+    """GPUs this process may use, from the KFD topology in sysfs (nodes with SIMDs are GPUs; the logic of
+    tools/amd-gpu-discovery.sh), restricted by HIP_VISIBLE_DEVICES / ROCR_VISIBLE_DEVICES / CUDA_VISIBLE_DEVICES
+    when set.  No HIP call: the spawning parent must not initialise the GPU before its children start."""
+    n = 0
+    try:
+        nodes = sorted((d for d in os.listdir(topology) if d.isdigit()), key=int)
+    except OSError:
+        nodes = []
+    for d in nodes:
+        try:
+            for line in open(os.path.join(topology, d, "properties")):
+                f = line.split()
+                if len(f) == 2 and f[0] == "simd_count" and int(f[1]) > 0:
+                    n += 1
+                    break
+        except (OSError, ValueError):
+            continue
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None:
+            n = min(n, len([x for x in v.split(",") if x.strip() != ""]))
+    return n
+
+
 def spawn_ranks(a):
     """--gpus N without a launcher: one child process per GPU (RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* set), as
-    torch.distributed.run would start them.  This parent makes no GPU call: it counts devices (no HIP context on
-    this image) and waits for the children; rank 0 prints the line."""
+    torch.distributed.run would start them.  This parent makes no GPU call (it counts devices in the KFD sysfs
+    topology, not through HIP) and waits for the children; rank 0 prints the line."""
     import socket
     import subprocess
-    import torch
-    have = torch.cuda.device_count()
+    have = kfd_gpu_count()
     if have < a.gpus:
         sys.exit(f"bench.py: --gpus {a.gpus} needs {a.gpus} GPUs, this host has {have}")
     with socket.socket() as s:

@@ -95,6 +95,7 @@ SIGNATURES = [
     ("gwo_side_output_count", C.c_int, [_P, _I64P]),
     ("gwo_drain_side_output", C.c_int, [_P, C.POINTER(GwoSideOut), C.c_int64, _I64P]),
     ("gwo_current_watermark", C.c_int, [_P, _I64P]),
+    ("gwo_get_config", C.c_int, [_P, C.POINTER(GwoConfig)]),
     ("gwo_state_size", C.c_int, [_P, _I64P]),
     ("gwo_snapshot_rows", C.c_int, [_P, _I64P, C.POINTER(C.c_int32)]),
     ("gwo_snapshot", C.c_int, [_P, C.POINTER(GwoStateRows), C.c_int64, _I64P, _I64P]),

@@ -119,6 +119,8 @@ gwo_status Handle::init(const gwo_config &c) {
     if (geom.slide > 0) geom.inv_slide = 1.0 / (double)geom.slide;
     if (geom.unit > 0) geom.inv_unit = 1.0 / (double)geom.unit;
     debug = getenv("GWO_DEBUG") != nullptr;
+    ktrace = getenv("GWO_KTRACE") != nullptr;
+    if (ktrace) ktrace_enable(1);
     if (const char *e = getenv("GWO_ASYNC_FIRE")) async_fire = atoi(e) != 0;
     const char *pa = getenv("GWO_PREAGG");
     if (pa) cfg_preagg = atoi(pa) ? 1 : 0;
@@ -190,6 +192,7 @@ Handle::~Handle() {
     DeviceGuard g(cfg.device);
     if (stream) (void)hipStreamSynchronize(stream);
     if (fire_stream) (void)hipStreamSynchronize(fire_stream);
+    if (ktrace) ktrace_report();
     (void)prof_collect();
     for (hipEvent_t e : event_pool) (void)hipEventDestroy(e);
     comm_free();

@@ -191,6 +191,7 @@ struct Handle {
     bool profiling = false;
     uint32_t prof_mask = ~0u;                  // kernels timed while profiling (bit = gwo_kernel_id)
     bool debug = false;                        // GWO_DEBUG=1: trace batches to stderr
+    bool ktrace = false;                       // GWO_KTRACE: per-phase K1 / fire cycle sums at destruction
     std::vector<PendingEvent> pending_events;
     std::vector<hipEvent_t> event_pool;        // recycled profiling events
     KStat kstats[GWO_KERNEL_COUNT_];

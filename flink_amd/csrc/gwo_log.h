@@ -7,9 +7,10 @@
 #define LOG_NU 4                 // windows one partition launch (K1) covers
 #define LOG_SLOTS 3              // batch buffers: K1 in flight (pipelined), deferred pass 2, next K1
 #ifndef LOG_K1_PER
-#define LOG_K1_PER 14            // K1 tile: 256 threads x 14 records
-#define LOG_K1_THREADS 256
-#endif
+#define LOG_K1_PER 16            // K1 tile: up to 256 threads x 16 records (64 KiB of 16-B records in LDS, two
+#define LOG_K1_THREADS 256       // workgroups per CU); a launch's tiles are sized so every workgroup loops over
+#endif                           // the same number of them (log_k1_tile)
+#define LOG_K1_TILE (LOG_K1_PER * LOG_K1_THREADS)
 #ifndef LOG_K1_GRID
 #define LOG_K1_GRID 512          // K1 workgroups: 2 per CU on MI355X's 256 CUs, all resident, each looping over
                                  // tiles with the next tile prefetched (measured: 0.223 ms vs 0.249 at 2048)
@@ -17,7 +18,7 @@
 #define LOG_TILE_PER 7            // pass-2 chunk: 512 threads x 7 records
 #define LOG_TILE_THREADS 512
 #define LOG_TILE (LOG_TILE_PER * LOG_TILE_THREADS)   // 3584 records: 56 KiB of 16-B records in LDS
-static_assert(LOG_K1_PER * LOG_K1_THREADS == LOG_TILE, "K1 tile and pass-2 chunk hold the same records");
+static_assert(LOG_K1_TILE <= 65536, "K1 ranks within a tile are 16-bit");
 #ifndef LOG_DB
 #define LOG_DB 8                 // coarse digit bits: K1 groups a window's records by the top LOG_DB bits
 #endif
@@ -36,7 +37,6 @@ static_assert(LOG_K1_PER * LOG_K1_THREADS == LOG_TILE, "K1 tile and pass-2 chunk
 #define FIRE_RCAP (FIRE_RPT * LOG_FIRE_THREADS)      // 3584: records per partition of the fire's fast path
 #define FIRE_OWN_LOG2 13
 #define FIRE_OWN (1 << FIRE_OWN_LOG2)                // election table slots of the fire's fast path
-#define FIRE_MAXR 15                                 // election rounds before a partition takes the slow path
 #define FIRE_LDS (FIRE_RCAP * 8 * 2 + (FIRE_RCAP + 4) * 4)   // fast-path dynamic LDS: keys, values, counts (70 KiB)
 #ifndef LOG_PART_FILL
 #define LOG_PART_FILL 7          // a new window's partitions are sized for LOG_PART_FILL/8 of FIRE_RCAP records
@@ -184,6 +184,9 @@ int log_fire_cap_log2(int nwords);
 // Loads the fire and pass-2 code objects with empty launches (HIP loads a kernel's code on its first launch:
 // ~0.25 ms that would otherwise land on the first watermark that fires a window).
 void warm_log_kernels(int nwords, int has_val, hipStream_t s);
+// GWO_KTRACE=1: per-phase shader-clock sums of K1 and the fire, printed at handle destruction (diagnostics).
+void ktrace_enable(int on);
+void ktrace_report();
 // Folds a window's segments (plus, when partial.rec is set, the restored accumulators of a checkpoint: records
 // of 1 + nwords words grouped by partition like a segment) and emits one row per key.  slow_only: every
 // partition takes the LDS hash-table path (a checkpoint fold with a raw-word result plan: up to 8 columns).

@@ -29,6 +29,40 @@ namespace gwo {
 
 typedef long long ll2 __attribute__((ext_vector_type(2)));
 
+// Phase trace (GWO_KTRACE=1, diagnostics only): workgroup 0-lane of every K1 / fire workgroup accumulates shader-clock
+// cycles per phase (s_memtime deltas between the phase's closing barriers) and adds them here at its end; the host
+// prints the sums when the handle is destroyed.  Off: one scalar load per launch.
+__device__ int g_kt_on;
+__device__ unsigned long long g_kt[64];   // [0, 16): K1 phases, [16, 32): fire phases, [32]: K1 launches, [33]: fires
+#define KT_K1 0
+#define KT_FIRE 16
+struct KTrace {
+    bool on;
+    uint64_t t;
+    uint64_t acc[8];
+    __device__ __forceinline__ void start(bool en) {
+        on = en;
+        t = on ? __builtin_amdgcn_s_memtime() : 0;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) acc[i] = 0;
+    }
+    __device__ __forceinline__ void stamp(int ph) {
+        if (on) {
+            const uint64_t n = __builtin_amdgcn_s_memtime();
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+                if (i == ph) acc[i] += n - t;
+            t = n;
+        }
+    }
+    __device__ __forceinline__ void flush(int base) {
+        if (on)
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+                if (acc[i]) atomicAdd(&g_kt[base + i], acc[i]);
+    }
+};
+
 enum LogClass : int { L_ACCEPT = 0, L_LATE = 1, L_SKIP = 2, L_REFIRE = 3, L_BAD_TS = 4, L_BAD_RANGE = 5 };
 
 // Tumbling classification, WindowOperator.java:386-427 + TumblingEventTimeWindows.java:68-81.
@@ -248,8 +282,11 @@ __global__ __launch_bounds__(LOG_K1_THREADS) void log_part_kernel(
     const int64_t *__restrict__ key, const int64_t *__restrict__ ts, const int64_t *__restrict__ val, int64_t n,
     int64_t stride, WindowGeom g, long long base, int nunits, unsigned long long *__restrict__ cursor, uint64_t cap,
     int64_t *__restrict__ tmp, BatchStats *st, int64_t *side_key, int64_t *side_ts, int64_t *side_val,
-    unsigned long long *side_count, long long side_cap, int side_enabled, CollectArgs ca, LogThr th, LogRoute rt) {
+    unsigned long long *side_count, long long side_cap, int side_enabled, CollectArgs ca, LogThr th, LogRoute rt,
+    int tlen) {
     constexpr int W = HASV ? 2 : 1;
+    KTrace kt;
+    kt.start(threadIdx.x == 0 && g_kt_on);
     // K1 times itself: workgroup 0's start and the tail's end on the device wall clock (read back with the plan),
     // so profiling puts no event markers between K1 and pass 2 (each costs the stream ~5 us)
     if (blockIdx.x == 0 && threadIdx.x == 0 && ca.t0) atomicExch(ca.t0, (unsigned long long)wall_clock64());
@@ -261,13 +298,16 @@ __global__ __launch_bounds__(LOG_K1_THREADS) void log_part_kernel(
         for (uint32_t i = blockIdx.x * LOG_K1_THREADS + threadIdx.x; i < n4; i += gridDim.x * LOG_K1_THREADS)
             c4[i] = make_uint4(0, 0, 0, 0);
     }
-    __shared__ __attribute__((aligned(16))) int64_t s_rec[LOG_TILE * W];
-    __shared__ uint16_t s_bk[LOG_TILE];
-    __shared__ uint32_t s_cnt[LOG_NU * LOG_ND];
-    __shared__ uint32_t s_off[LOG_NU * LOG_ND];
+    // tlen (<= LOG_K1_TILE) records per tile: the launcher sizes tiles so that every workgroup loops over the same
+    // number of them (a last round of a few workgroups would cost a whole tile's latency)
+    __shared__ __attribute__((aligned(16))) int64_t s_rec[LOG_K1_TILE * W];
+    __shared__ uint16_t s_bk[LOG_K1_TILE];
     __shared__ uint32_t s_rcnt[ROUTE ? LOG_RT_MAX : 1];             // routed records per destination (tile)
-    __shared__ unsigned long long s_rbase[ROUTE ? LOG_RT_MAX : 1];  // their run's first record in the region
+    __shared__ uint32_t s_rbase[ROUTE ? LOG_RT_MAX : 1];            // their run's first record in the region
     const int nb = nunits * LOG_ND;
+    // bucket counters and offsets: dynamic LDS sized for the launch's windows (2 workgroups per CU up to 2 windows)
+    extern __shared__ uint32_t s_kdyn[];
+    uint32_t *const s_cnt = s_kdyn, *const s_off = s_kdyn + nb;
     const int nr = ROUTE ? rt.nranks : 0;
     const int per = (nb + LOG_K1_THREADS - 1) / LOG_K1_THREADS;   // counters owned per thread (<= 4)
     const int tid = threadIdx.x;
@@ -283,7 +323,7 @@ __global__ __launch_bounds__(LOG_K1_THREADS) void log_part_kernel(
 #pragma unroll
         for (int j = 0; j < LOG_K1_PER; ++j) {
             int64_t i = tile + j * LOG_K1_THREADS + tid;
-            i = i < n ? i : (tile < n ? tile : 0);
+            i = (i < n && j * LOG_K1_THREADS + tid < tlen) ? i : (tile < n ? tile : 0);
             const int64_t o = S ? i * S : i * stride;
             tt[j] = TS32 ? th.tbase + (int64_t)__builtin_nontemporal_load((const int32_t *)ts + o)
                          : __builtin_nontemporal_load(ts + o);
@@ -291,20 +331,21 @@ __global__ __launch_bounds__(LOG_K1_THREADS) void log_part_kernel(
             vv[j] = HASV ? __builtin_nontemporal_load(val + o) : 0;
         }
     };
-    const int64_t tstride = (int64_t)gridDim.x * LOG_TILE;
-    if ((int64_t)blockIdx.x * LOG_TILE < n) load_tile((int64_t)blockIdx.x * LOG_TILE);
-    for (int64_t tile = (int64_t)blockIdx.x * LOG_TILE; tile < n; tile += tstride) {
+    const int64_t tstride = (int64_t)gridDim.x * tlen;
+    if ((int64_t)blockIdx.x * tlen < n) load_tile((int64_t)blockIdx.x * tlen);
+    for (int64_t tile = (int64_t)blockIdx.x * tlen; tile < n; tile += tstride) {
         for (int i = tid; i < nb; i += LOG_K1_THREADS) s_cnt[i] = 0;
         if (ROUTE)
             for (int i = tid; i < nr; i += LOG_K1_THREADS) s_rcnt[i] = 0;
         __syncthreads();
+        kt.stamp(0);
         uint32_t code[LOG_K1_PER];
         uint32_t slow = 0;   // bit j: record j is classified out of line (below)
 #pragma unroll
         for (int j = 0; j < LOG_K1_PER; ++j) {
             const int64_t i = tile + j * LOG_K1_THREADS + tid;
             code[j] = 0xffffffffu;
-            if (i >= n) continue;
+            if (i >= n || j * LOG_K1_THREADS + tid >= tlen) continue;
             if (ROUTE) {   // KeyGroupStreamPartitioner.selectChannel: another GPU's record is its owner's to classify
                 const int dest = (int)(key_group(kk[j], g.key_kind, g.max_par) * rt.nranks / g.max_par);
                 if (dest != rt.me) {
@@ -400,7 +441,9 @@ __global__ __launch_bounds__(LOG_K1_THREADS) void log_part_kernel(
                 bad_range++;
             }
         }
+        kt.stamp(1);
         __syncthreads();
+        kt.stamp(2);
         // reserve each bucket's run in this workgroup's region group, before the offsets scan, so that the
         // atomics' round trip overlaps the scan and the LDS scatter; s_cnt[b] becomes the run's first record
         unsigned long long at[4];
@@ -418,16 +461,17 @@ __global__ __launch_bounds__(LOG_K1_THREADS) void log_part_kernel(
         uint32_t loc[4];
         const uint32_t total = tile_offsets(s_cnt, s_off, nb, loc, per);
         if (ROUTE && (rt.mode == 1 || rt.mode == 3)) {
-            if (tid < nr) s_rbase[tid] = rat;
+            if (tid < nr) s_rbase[tid] = rat < 0xffffffffull ? (uint32_t)rat : 0xffffffffu;   // (>= rcap: not written)
             __syncthreads();
         }
+        kt.stamp(3);
 #pragma unroll
         for (int j = 0; j < LOG_K1_PER; ++j) {
             if (code[j] == 0xffffffffu) continue;
             uint32_t b = code[j] >> 16;
             if (ROUTE && b >= LOG_RT_B) {   // routed: straight from registers into the destination's run
                 const uint32_t d = b - LOG_RT_B;
-                const unsigned long long q = s_rbase[d] + (code[j] & 0xffffu);
+                const unsigned long long q = (unsigned long long)s_rbase[d] + (code[j] & 0xffffu);
                 if (q < rt.rcap) {   // 20-B wire record: key, value, int32 ts - tbase (SoA per destination)
                     log_rt_keys(rt.send, rt.rcap, (int)d)[q] = kk[j];
                     log_rt_vals(rt.send, rt.rcap, (int)d)[q] = HASV ? vv[j] : 0;
@@ -451,6 +495,7 @@ __global__ __launch_bounds__(LOG_K1_THREADS) void log_part_kernel(
             if (q < per && loc[q]) s_cnt[b] = (uint32_t)(at[q] < cap ? at[q] : cap);
         }
         __syncthreads();
+        kt.stamp(4);
         for (uint32_t p = tid; p < total; p += LOG_K1_THREADS) {
             uint32_t b = s_bk[p];
             if (b >= (uint32_t)nb) continue;   // defensive: never a write outside the buffer
@@ -462,6 +507,7 @@ __global__ __launch_bounds__(LOG_K1_THREADS) void log_part_kernel(
             }
         }
         __syncthreads();
+        kt.stamp(5);
     }
     if (wmask) {
         const long long lo = base + __builtin_ctz(wmask), hi = base + 31 - __builtin_clz(wmask);
@@ -512,6 +558,9 @@ __global__ __launch_bounds__(LOG_K1_THREADS) void log_part_kernel(
     __shared__ int s_last;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    kt.stamp(6);
+    if (kt.on && blockIdx.x == 0) atomicAdd(&g_kt[32], 1ull);
+    kt.flush(KT_K1);
     if (tid == 0) {
         const unsigned sh = blockIdx.x % LOG_SHARDS;
         const unsigned members = (gridDim.x - sh + LOG_SHARDS - 1) / LOG_SHARDS;
@@ -916,11 +965,9 @@ __device__ __forceinline__ uint32_t slot_mix(int64_t k) {
     return (uint32_t)k * 0x9E3779B1u + (uint32_t)((uint64_t)k >> 32) * 0x85EBCA77u;
 }
 
-// Election priority of record i in probe round r: earlier rounds beat later ones (a slot's owner never
-// changes once elected), then the smaller record index wins.  0 = free slot.
-__device__ __forceinline__ uint32_t elect_prio(int round, uint32_t i) {
-    return ((uint32_t)(FIRE_MAXR - round) << 12) | (4095u - i);
-}
+// Election table word: leader record index (low 12 bits) | records of its key so far << 12.  Free: all ones.
+#define FIRE_FREE 0xffffffffu
+#define FIRE_ONE (1u << 12)
 
 // PART: the checkpoint instance -- restored partial accumulators (after gwo_restore) and slow-path-only folds
 // (gwo_snapshot's raw-word rows); a separate instance, so the watermark fire carries none of their code or registers.
@@ -934,8 +981,8 @@ __global__ __launch_bounds__(LOG_FIRE_THREADS) __attribute__((amdgpu_waves_per_e
     // Dynamic LDS (FIRE_LDS bytes).  Fast path:
     //   s_key [FIRE_RCAP] int64   record keys (record i = r * 512 + tid), then leader keys by row ordinal
     //   s_val [FIRE_RCAP] int64   values grouped by key (after the election; overlays s_own)
-    //   s_own [FIRE_OWN]  uint32  election table: slot -> priority of its owner record (overlays s_val
-    //                             and the head of s_cnt; s_cnt is zeroed after the election)
+    //   s_own [FIRE_OWN]  uint32  election table: slot -> leader record | key's record count << 12 (overlays
+    //                             s_val and the head of s_cnt; dead once the leaders have read their counts)
     //   s_cnt [FIRE_RCAP] uint32  per-leader record counts -> offsets -> (offset | count << 16) by ordinal
     // Slow path: the same bytes hold a FireCtx hash table (key + words, SoA, 2^cap_log2 slots).
     extern __shared__ __attribute__((aligned(16))) int64_t s_dyn[];
@@ -950,7 +997,6 @@ __global__ __launch_bounds__(LOG_FIRE_THREADS) __attribute__((amdgpu_waves_per_e
     __shared__ const int64_t *s_rp[LOG_MAX_SEGS];
     __shared__ uint32_t s_wsum[FIRE_RPT * (LOG_FIRE_THREADS / 64)];   // per-(r, wave) sums -> prefixes
     __shared__ uint32_t s_tot;
-    __shared__ int s_any[2];
     __shared__ uint32_t s_pw[LOG_FIRE_THREADS / 64 + 1];
     __shared__ unsigned long long s_rbase;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -958,6 +1004,8 @@ __global__ __launch_bounds__(LOG_FIRE_THREADS) __attribute__((amdgpu_waves_per_e
     FireCtx c{s_dyn, s_dyn + cap, s_side, &s_used, &s_fail, cap, (unsigned)(cap - (cap >> 3))};
     uint32_t part = blockIdx.x;
     if (part >= nparts) return;
+    KTrace kt;
+    kt.start(tid == 0 && g_kt_on);
     for (int s = tid; s < nseg; s += LOG_FIRE_THREADS) s_rp[s] = segs[s].rec;
     if (tid <= GWO_MAX_WORDS) s_side[tid] = tid == 0 ? 0 : p.ident[tid - 1];
     if (tid == 0) {
@@ -1075,72 +1123,66 @@ __global__ __launch_bounds__(LOG_FIRE_THREADS) __attribute__((amdgpu_waves_per_e
                 if (i < total) s_key[i] = rk[r];
             }
             load_next();
-            for (int q = tid; q < FIRE_OWN / 4; q += LOG_FIRE_THREADS) ((uint4 *)s_own)[q] = make_uint4(0, 0, 0, 0);
-            if (tid == 0) {
-                s_any[0] = 0;
-                s_any[1] = 0;
-            }
+            for (int q = tid; q < FIRE_OWN / 4; q += LOG_FIRE_THREADS)
+                ((uint4 *)s_own)[q] = make_uint4(FIRE_FREE, FIRE_FREE, FIRE_FREE, FIRE_FREE);
             __syncthreads();
-            // P1: election.  Every record of a key probes the same slot sequence (double hashing on
-            // part_hash), so they resolve together; a slot's winner is the key's leader record.
-            // sl[r] is the record's probe slot while it is pending, then its leader record.
-            uint32_t sl[FIRE_RPT];
-            unsigned pend = 0;
+            kt.stamp(0);
+            // P1: claim or join, no barrier per probe round.  Every record of a key walks the same slot
+            // sequence (double hashing on slot_mix).  A compare-and-swap of a free slot makes the record its
+            // key's leader (count 1, rank 0); a slot whose leader holds the same key is joined by one add of
+            // FIRE_ONE, whose return value is the record's rank among its key's records; a slot of another key
+            // sends the record on.  The table never fills (8192 slots, <= 3584 keys), so every record ends.
+            // sl[r]: probe slot while pending, then the leader record; own[r]: a leader's slot.
+            uint32_t sl[FIRE_RPT], own[FIRE_RPT], rank[FIRE_RPT];
+            unsigned pend = 0, leader = 0;
 #pragma unroll
             for (int r = 0; r < FIRE_RPT; ++r) {
                 const uint32_t i = r * LOG_FIRE_THREADS + tid;
                 sl[r] = slot_mix(rk[r]) >> (32 - FIRE_OWN_LOG2);
+                own[r] = 0;
+                rank[r] = 0;
                 if (i < total) pend |= 1u << r;
             }
-            int round = 0;
-            while (true) {
+            while (pend) {   // per wave: ends when its lanes' records are all placed
+                uint32_t prev[FIRE_RPT];
 #pragma unroll
                 for (int r = 0; r < FIRE_RPT; ++r)
-                    if ((pend >> r) & 1u) atomicMax(&s_own[sl[r]], elect_prio(round, r * LOG_FIRE_THREADS + tid));
-                __syncthreads();
-                if (tid == 0) s_any[(round + 1) & 1] = 0;   // every read of it (round - 1) is behind the barrier
+                    prev[r] = ((pend >> r) & 1u)
+                                  ? atomicCAS(&s_own[sl[r]], FIRE_FREE, (r * LOG_FIRE_THREADS + tid) | FIRE_ONE)
+                                  : FIRE_FREE;
+                unsigned join = 0;
 #pragma unroll
                 for (int r = 0; r < FIRE_RPT; ++r) {
                     if (!((pend >> r) & 1u)) continue;
-                    const uint32_t i = r * LOG_FIRE_THREADS + tid;
-                    const uint32_t j = 4095u - (s_own[sl[r]] & 4095u);
-                    if (j == i || s_key[j] == rk[r]) {
-                        sl[r] = j;
+                    if (prev[r] == FIRE_FREE) {   // claimed: this record leads its key
+                        own[r] = sl[r];
+                        sl[r] = r * LOG_FIRE_THREADS + tid;
+                        leader |= 1u << r;
                         pend &= ~(1u << r);
+                    } else if (s_key[prev[r] & (FIRE_ONE - 1)] == rk[r]) {
+                        join |= 1u << r;
                     } else {
                         const uint32_t step = ((slot_mix(rk[r]) >> 4) & (FIRE_OWN - 1)) | 1u;
                         sl[r] = (sl[r] + step) & (FIRE_OWN - 1);
                     }
                 }
-                if (pend) s_any[round & 1] = 1;
-                __syncthreads();
-                const bool again = s_any[round & 1] != 0;   // (no __syncthreads_or: it reads the dispatch
-                ++round;                                     //  packet with a vector load and waits vmcnt(0))
-                if (!again) break;
-                if (round >= FIRE_MAXR) {   // uniform: give the partition to the slow path
-                    fast = false;
-                    break;
-                }
-            }
-            if (fast) {
-                for (int q = tid; q < FIRE_RCAP / 4; q += LOG_FIRE_THREADS) ((uint4 *)s_cnt)[q] = make_uint4(0, 0, 0, 0);
-                __syncthreads();
-                // P2: rank of each record among its key's records (rk is dead from here on)
-                uint32_t rank[FIRE_RPT];
 #pragma unroll
-                for (int r = 0; r < FIRE_RPT; ++r) {
-                    const uint32_t i = r * LOG_FIRE_THREADS + tid;
-                    rank[r] = i < total ? atomicAdd(&s_cnt[sl[r]], 1u) : 0u;
-                }
-                __syncthreads();
+                for (int r = 0; r < FIRE_RPT; ++r)
+                    if ((join >> r) & 1u) rank[r] = atomicAdd(&s_own[sl[r]], FIRE_ONE) >> 12;
+#pragma unroll
+                for (int r = 0; r < FIRE_RPT; ++r)
+                    if ((join >> r) & 1u) sl[r] = prev[r] & (FIRE_ONE - 1);
+                pend &= ~join;
+            }
+            kt.stamp(1);
+            __syncthreads();
+            kt.stamp(2);
+            {
                 // P3: exclusive scan over record ids of (count | 1 << 16) at leaders -> each leader's
-                // first value offset (low half) and row ordinal (high half)
+                // first value offset (low half) and row ordinal (high half).  (rk is dead from here on.)
                 uint32_t x[FIRE_RPT], incl[FIRE_RPT];
 #pragma unroll
-                for (int r = 0; r < FIRE_RPT; ++r) {
-                    const uint32_t i = r * LOG_FIRE_THREADS + tid;
-                    x[r] = (i < total && sl[r] == i) ? (s_cnt[i] | 0x10000u) : 0u;
-                }
+                for (int r = 0; r < FIRE_RPT; ++r) x[r] = ((leader >> r) & 1u) ? ((s_own[own[r]] >> 12) | 0x10000u) : 0u;
 #pragma unroll
                 for (int r = 0; r < FIRE_RPT; ++r) {
                     incl[r] = wave_incl_scan(x[r]);
@@ -1161,16 +1203,12 @@ __global__ __launch_bounds__(LOG_FIRE_THREADS) __attribute__((amdgpu_waves_per_e
                 }
                 __syncthreads();
                 uint32_t lo[FIRE_RPT];   // leaders: value offset | row ordinal << 16
-                unsigned leader = 0;
 #pragma unroll
                 for (int r = 0; r < FIRE_RPT; ++r) {
                     const uint32_t i = r * LOG_FIRE_THREADS + tid;
                     const uint32_t pre = s_wsum[r * (LOG_FIRE_THREADS / 64) + wave] + incl[r] - x[r];
                     lo[r] = pre;
-                    if (x[r]) {
-                        leader |= 1u << r;
-                        s_cnt[i] = pre & 0xffffu;
-                    }
+                    if (x[r]) s_cnt[i] = pre & 0xffffu;
                 }
                 __syncthreads();
                 // P4: values grouped by key, in row order (the election table is dead)
@@ -1195,6 +1233,7 @@ __global__ __launch_bounds__(LOG_FIRE_THREADS) __attribute__((amdgpu_waves_per_e
                     s_cnt[s_tot >> 16] = s_tot & 0xffffu;
                     s_rbase = rbase_lane0;   // the atomic's round trip overlapped P4
                 }
+                kt.stamp(3);
             }
         }
         if (total > (uint32_t)FIRE_RCAP) load_next();   // (the fast path loaded them in P0)
@@ -1257,6 +1296,7 @@ __global__ __launch_bounds__(LOG_FIRE_THREADS) __attribute__((amdgpu_waves_per_e
         // unconditional, so the loads land straight in rk/rv (no loop-carried copy that would wait for
         // them): in flight during this partition's emit and the next one's election
         prefetch(more && !(PART && slow_only));
+        kt.stamp(4);
         if (fast) {
             // P5: one row per leader, in ordinal order.  Thread t takes ordinal t - sh (sh = rbase & 1),
             // so lanes 2m and 2m+1 own a 16-B-aligned pair of global rows; after a DPP swap within the
@@ -1335,10 +1375,13 @@ __global__ __launch_bounds__(LOG_FIRE_THREADS) __attribute__((amdgpu_waves_per_e
                 }
             }
             __syncthreads();   // the next partition overwrites s_key / s_cnt
+            kt.stamp(5);
         }
         if (!more) break;
         part = nxt;
     }
+    if (kt.on && blockIdx.x == 0) atomicAdd(&g_kt[33], 1ull);
+    kt.flush(KT_FIRE);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1350,12 +1393,18 @@ void launch_log_part(const int64_t *key, const int64_t *ts, const int64_t *val, 
                      int64_t *tmp, BatchStats *st, int64_t *side_key, int64_t *side_ts, int64_t *side_val,
                      unsigned long long *side_count, long long side_cap, int side_enabled, const CollectArgs &ca,
                      const LogThr &thr, const LogRoute &rt, hipStream_t s) {
-    int64_t grid = (n + LOG_TILE - 1) / LOG_TILE;
+    // rounds = tiles per workgroup at full tiles; then the tile length that gives every workgroup that many
+    // (16.67M records: 8 rounds of 4070 records instead of 9 rounds for most workgroups and a 10th for 42)
+    int64_t grid = (n + LOG_K1_TILE - 1) / LOG_K1_TILE;
     grid = grid < 1 ? 1 : (grid > LOG_K1_GRID ? LOG_K1_GRID : grid);
+    const int64_t rounds = (n + grid * LOG_K1_TILE - 1) / (grid * LOG_K1_TILE);
+    int64_t tl = rounds > 0 ? (n + grid * rounds - 1) / (grid * rounds) : LOG_K1_TILE;
+    tl = tl < 1 ? 1 : (tl > LOG_K1_TILE ? LOG_K1_TILE : tl);
+    const size_t dyn = (size_t)2 * nunits * LOG_ND * sizeof(uint32_t);
 #define GWO_K1(HV, S, R, T32)                                                                                  \
-    hipLaunchKernelGGL((log_part_kernel<HV, S, R, T32>), dim3((int)grid), dim3(LOG_K1_THREADS), 0, s, key, ts, val, \
+    hipLaunchKernelGGL((log_part_kernel<HV, S, R, T32>), dim3((int)grid), dim3(LOG_K1_THREADS), dyn, s, key, ts, val, \
                        n, stride, g, base, nunits, cursor, cap, tmp, st, side_key, side_ts, side_val, side_count, \
-                       side_cap, side_enabled, ca, thr, rt)
+                       side_cap, side_enabled, ca, thr, rt, (int)tl)
     if (rt.mode != 0 && stride == 1) {   // routing: the first K1 over a batch's own columns (and its route-only re-run)
         if (has_val) GWO_K1(true, 1, true, false);
         else GWO_K1(false, 1, true, false);
@@ -1423,7 +1472,7 @@ void launch_log_fire(const LogSegDesc *segs, int nseg, int lp, int has_val, cons
                      int cus, int max_per_cu, int slow_only, const LogSegDesc &partial, hipStream_t s) {
     if (nseg < 0 || nseg > LOG_MAX_SEGS || (nseg == 0 && !partial.rec)) return;   // nothing to fold (defensive)
     static_assert(FIRE_OWN * 4 <= FIRE_RCAP * 12 && FIRE_OWN == (1 << FIRE_OWN_LOG2) && FIRE_RCAP <= 4096 &&
-                      FIRE_MAXR < 16, "fire fast-path layout");
+                      FIRE_OWN > FIRE_RCAP, "fire fast-path layout");
     int cl = log_fire_cap_log2(plan.nwords);
     size_t lds = (size_t)(1 + plan.nwords) * 8 << cl;
     if (lds < (size_t)FIRE_LDS) lds = FIRE_LDS;
@@ -1451,6 +1500,25 @@ void launch_log_fire(const LogSegDesc *segs, int nseg, int lp, int has_val, cons
         default: GWO_FIRE_NW(8)
     }
 #undef GWO_FIRE_NW
+}
+
+// Phase trace switch and report (GWO_KTRACE=1; diagnostics only).
+void ktrace_enable(int on) {
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_kt_on), &on, sizeof(int));
+}
+
+void ktrace_report() {
+    unsigned long long v[64];
+    if (hipMemcpyFromSymbol(v, HIP_SYMBOL(g_kt), sizeof(v)) != hipSuccess) return;
+    const double k1 = v[32] ? (double)v[32] : 1.0, fi = v[33] ? (double)v[33] : 1.0;
+    fprintf(stderr, "[ktrace] K1 launches %llu, per launch per workgroup (Mcycles, summed over workgroups):\n", v[32]);
+    const char *kn[7] = {"zero+loop", "classify", "slow+barrier", "reserve+offsets", "scatter+prefetch", "write", "stats"};
+    for (int i = 0; i < 7; ++i) fprintf(stderr, "  K1 %-18s %10.3f\n", kn[i], v[i] / k1 / 1e6);
+    const char *fn[6] = {"P0 keys/table", "P1 claim", "P1 barrier", "P3-P4b", "publish+prefetch", "P5 emit"};
+    fprintf(stderr, "[ktrace] fires %llu, per fire (Mcycles, summed over workgroups):\n", v[33]);
+    for (int i = 0; i < 6; ++i) fprintf(stderr, "  fire %-18s %10.3f\n", fn[i], v[16 + i] / fi / 1e6);
+    for (int i = 0; i < 64; ++i) v[i] = 0;
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_kt), v, sizeof(v));
 }
 
 }  // namespace gwo

@@ -1313,6 +1313,13 @@ gwo_status gwo_current_watermark(gwo_handle *hh, int64_t *wm) {
     return GWO_OK;
 }
 
+gwo_status gwo_get_config(const gwo_handle *hh, gwo_config *out) {
+    const Handle *h = reinterpret_cast<const Handle *>(hh);
+    if (!h || !out) return GWO_ERR_INVALID_ARGUMENT;
+    *out = h->cfg;
+    return GWO_OK;
+}
+
 gwo_status gwo_state_size(gwo_handle *hh, int64_t *entries) {
     H_OR_FAIL;
     if (!entries) return GWO_ERR_INVALID_ARGUMENT;

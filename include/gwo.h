@@ -166,6 +166,8 @@ gwo_status gwo_late_dropped(gwo_handle *h, int64_t *count);
 gwo_status gwo_side_output_count(gwo_handle *h, int64_t *n);
 gwo_status gwo_drain_side_output(gwo_handle *h, const gwo_side_out *cols, int64_t cap, int64_t *n_out);
 gwo_status gwo_current_watermark(gwo_handle *h, int64_t *wm);
+/* The configuration the handle runs with (gwo_create's, defaults applied), e.g. its KeyGroupRange. */
+gwo_status gwo_get_config(const gwo_handle *h, gwo_config *out);
 /* Number of (key, window) entries currently held (device-resident state). */
 gwo_status gwo_state_size(gwo_handle *h, int64_t *entries);
 

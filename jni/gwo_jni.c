@@ -315,7 +315,13 @@ JNIEXPORT jbyteArray JNICALL JFN(exportHeapState)(JNIEnv *env, jclass c, jlong h
                                                   jlongArray watermarkOut) {
     (void)c;
     gwo_heap_state_ids sid;
+    gwo_config cfg;
     if (!heap_ids(env, ids, &sid) || !array_ok(env, watermarkOut, 1, "watermark array")) return NULL;
+    if (fail(env, H(h), gwo_get_config(H(h), &cfg))) return NULL;
+    /* one offset per key group of the subtask's KeyGroupRange (gwo_export_heap_state writes all of them) */
+    if (!array_ok(env, kgOffsets, (jlong)cfg.key_group_end - cfg.key_group_start + 1,
+                  "keyGroupOffsets smaller than the subtask's key-group count"))
+        return NULL;
     int64_t need = 0, len = 0, wm = 0;
     if (fail(env, H(h), gwo_export_heap_state(H(h), &sid, NULL, 0, &need, NULL, NULL))) return NULL;
     if (need > 0x7fffffff - 8) {
@@ -342,7 +348,7 @@ JNIEXPORT void JNICALL JFN(importHeapState)(JNIEnv *env, jclass c, jlong h, jint
                                             jlong watermark) {
     (void)c;
     gwo_heap_state_ids sid;
-    if (!heap_ids(env, ids, &sid)) return;
+    if (!heap_ids(env, ids, &sid) || !array_ok(env, data, 0, "state bytes")) return;
     const jsize n = (*env)->GetArrayLength(env, data);
     jbyte *p = (*env)->GetByteArrayElements(env, data, NULL);
     if (!p) return;

@@ -48,3 +48,17 @@ def test_coordination_mode(topo):
     # an entry whose owner has exited is reclaimed
     f.write_text("0 999999999\n1 %d\n" % os.getpid())
     assert run(topo, 2, "--enable-coordination-mode", "--coordination-file", f) == (0, "0,2")
+
+
+def test_bench_counts_gpus_without_hip(topo, monkeypatch):
+    """bench.py's spawning parent counts GPUs from the same KFD topology (no HIP call before the ranks start)."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    for v in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        monkeypatch.delenv(v, raising=False)
+    assert bench.kfd_gpu_count(str(topo / "nodes")) == 3
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "1,2")
+    assert bench.kfd_gpu_count(str(topo / "nodes")) == 2
+    assert bench.kfd_gpu_count(str(topo / "missing")) == 0
