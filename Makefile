@@ -14,6 +14,9 @@ CPP_OBJS := $(patsubst flink_amd/csrc/%.cpp,$(BUILD)/%.cpp.o,$(CPP_SRCS))
 HDRS := $(wildcard flink_amd/csrc/*.h) include/gwo.h
 
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Wall -Wno-unused-function
+ifeq ($(KTRACE),1)   # per-phase shader-clock trace of K1 and the log fire (GWO_KTRACE=1 at run time; diagnostics)
+HIPFLAGS += -DGWO_KTRACE
+endif
 CXXFLAGS := -O2 -std=c++17 -fPIC -Wall -Wno-unused-function -D__HIP_PLATFORM_AMD__ -I$(ROCM)/include
 
 all: $(LIB)

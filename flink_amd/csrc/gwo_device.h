@@ -223,6 +223,12 @@ __device__ __forceinline__ unsigned long long block_reserve(unsigned v, unsigned
 }
 
 // Workgroup-wide exclusive prefix sum of v (all threads call it); *total gets the sum.
+// Workgroup barrier for LDS hand-offs only: this wave's LDS operations complete, then s_barrier -- no memory fence.
+// __syncthreads() lowers to a workgroup release + acquire fence, which on gfx950 waits vmcnt(0) whenever a global
+// store or atomic may be pending: every load, store and atomic in flight (a prefetch, a row reservation, a tile's
+// output) drained at each barrier.  Use only where the barrier orders LDS accesses, never global memory.
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 __device__ __forceinline__ unsigned block_exclusive_scan(unsigned v, unsigned *total) {
     __shared__ unsigned s_w[17];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;

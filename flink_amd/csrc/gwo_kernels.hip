@@ -528,9 +528,11 @@ __global__ __launch_bounds__(CB_THREADS) void gather_kernel(const int64_t *__res
     CB_STAMP(0);
     int64_t *s_key = s_dyn;                     // [CB_NU * S]
     int64_t *s_acc = s_dyn + CB_NU * S;         // [CB_NU * S * NW]
+    int64_t *s_spare = s_acc + CB_NU * S * NW;  // [64]: each lane's spare word for the find-or-claim rounds
     __shared__ unsigned s_hist[GWO_HIST_BINS];
     __shared__ unsigned long long s_red[CB_THREADS / 64][CS_HIST];
     for (int i = tid; i < CB_NU * S; i += CB_THREADS) s_key[i] = GWO_EMPTY_KEY;
+    if (tid < 64) s_spare[tid] = GWO_EMPTY_KEY;
     for (int i = tid; i < CB_NU * S; i += CB_THREADS)
         for (int w = 0; w < NW; ++w) s_acc[i * NW + w] = p.ident[w];
     if (tid < GWO_HIST_BINS) s_hist[tid] = 0;
@@ -655,6 +657,7 @@ __global__ __launch_bounds__(CB_THREADS) void gather_kernel(const int64_t *__res
         CB_STAMP(1);
         // wave pre-reduction of duplicate keys, then the LDS tables (every lane of the wave is here)
         const int lane = tid & 63;
+        unsigned rem = 0;   // bit j: record j still goes into an LDS table after the hot-key rounds
 #pragma unroll
         for (int j = 0; j < CB_PER; ++j) {
             bool cand = (candm >> j) & 1u;
@@ -683,14 +686,47 @@ __global__ __launch_bounds__(CB_THREADS) void gather_kernel(const int64_t *__res
                 }
                 m &= ~peers;
             }
-            if (!cand) continue;
-            const int slot = lds_slot(s_key + b * S, S, a.sbits, k);
-            if (slot < 0) {
-                ovm |= 1u << j;
-                continue;
+            if (cand) rem |= 1u << j;
+        }
+        // find-or-claim of every remaining record at once: per probe round ONE compare-and-swap per record, all
+        // CB_PER in flight together (a record already placed swaps this lane's spare word, so no swap is
+        // conditional: a swap under a branch is waited for at the branch's join -- r03's gather waited for every
+        // record's read and swap in turn).  Linear probing from the key's home slot, as lds_slot.
+        uint32_t sl[CB_PER];
+        int slot[CB_PER];
+#pragma unroll
+        for (int j = 0; j < CB_PER; ++j) {
+            const int64_t k = kk[j];
+            sl[j] = ((uint32_t)k * 0x9E3779B1u ^ (uint32_t)((uint64_t)k >> 32) * 0x85EBCA77u) >> (32 - a.sbits);
+            slot[j] = -1;
+        }
+        unsigned pend = rem;
+        for (int probe = 0; probe < 32 && pend; ++probe) {
+            int64_t prev[CB_PER];
+#pragma unroll
+            for (int j = 0; j < CB_PER; ++j) {
+                const bool pj = (pend >> j) & 1u;
+                int64_t *at = pj ? &s_key[cbu[j] * S + (int)sl[j]] : &s_spare[lane];
+                prev[j] = (int64_t)atomicCAS((unsigned long long *)at, (unsigned long long)GWO_EMPTY_KEY,
+                                             (unsigned long long)(pj ? kk[j] : GWO_EMPTY_KEY));
             }
-            int64_t *dst = s_acc + ((size_t)b * S + slot) * NW;
-            for (int w = 0; w < NW; ++w) lds_combine(dst + w, p.op[w], lift_word(p, w, vv[j]));
+#pragma unroll
+            for (int j = 0; j < CB_PER; ++j) {
+                if (!((pend >> j) & 1u)) continue;
+                if (prev[j] == GWO_EMPTY_KEY || prev[j] == kk[j]) {
+                    slot[j] = (int)sl[j];
+                    pend &= ~(1u << j);
+                } else {
+                    sl[j] = (sl[j] + 1) & (uint32_t)(S - 1);
+                }
+            }
+        }
+        ovm |= pend;   // no room within 32 probes: listed for the merge
+#pragma unroll
+        for (int j = 0; j < CB_PER; ++j) {
+            if (!((rem >> j) & 1u) || slot[j] < 0) continue;
+            int64_t *dst = s_acc + ((size_t)cbu[j] * S + slot[j]) * NW;
+            for (int w = 0; w < NW; ++w) lds_combine(dst + w, p.op[w], lift_word(p, w, vv[j]));   // (no return value)
         }
         if (tile + tstride < n) load_tile(tile + tstride);
         // the tile's listed records: one reservation per workgroup
@@ -1587,7 +1623,7 @@ void launch_generate(uint64_t seed, int64_t first, int64_t total, int64_t nkeys,
                        span, disorder, t0, vrange, vf64, key_mode, n, key, ts, (int64_t *)val);
 }
 
-size_t gather_lds_bytes(int S, int nwords) { return (size_t)CB_NU * S * (1 + nwords) * 8; }
+size_t gather_lds_bytes(int S, int nwords) { return (size_t)CB_NU * S * (1 + nwords) * 8 + 64 * 8; }
 int gather_tile() { return CB_TILE; }
 int gather_stat_words() { return CB_SHARDS * CS_WORDS; }
 

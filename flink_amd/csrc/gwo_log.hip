@@ -29,13 +29,15 @@ namespace gwo {
 
 typedef long long ll2 __attribute__((ext_vector_type(2)));
 
-// Phase trace (GWO_KTRACE=1, diagnostics only): workgroup 0-lane of every K1 / fire workgroup accumulates shader-clock
+// Phase trace (built with -DGWO_KTRACE, run with GWO_KTRACE=1; diagnostics only): lane 0 of every K1 / fire
+// workgroup accumulates shader-clock
 // cycles per phase (s_memtime deltas between the phase's closing barriers) and adds them here at its end; the host
 // prints the sums when the handle is destroyed.  Off: one scalar load per launch.
 __device__ int g_kt_on;
 __device__ unsigned long long g_kt[64];   // [0, 16): K1 phases, [16, 32): fire phases, [32]: K1 launches, [33]: fires
 #define KT_K1 0
 #define KT_FIRE 16
+#ifdef GWO_KTRACE
 struct KTrace {
     bool on;
     uint64_t t;
@@ -56,12 +58,20 @@ struct KTrace {
         }
     }
     __device__ __forceinline__ void flush(int base) {
-        if (on)
+        if (on && (threadIdx.x & 63) == 0)
 #pragma unroll
             for (int i = 0; i < 8; ++i)
                 if (acc[i]) atomicAdd(&g_kt[base + i], acc[i]);
     }
 };
+#else   // the product build: no trace code or registers in the kernels (`make KTRACE=1` builds the traced library)
+struct KTrace {
+    static constexpr bool on = false;
+    __device__ __forceinline__ void start(bool) {}
+    __device__ __forceinline__ void stamp(int) {}
+    __device__ __forceinline__ void flush(int) {}
+};
+#endif
 
 enum LogClass : int { L_ACCEPT = 0, L_LATE = 1, L_SKIP = 2, L_REFIRE = 3, L_BAD_TS = 4, L_BAD_RANGE = 5 };
 
@@ -92,11 +102,43 @@ __device__ __forceinline__ int log_classify(int64_t ts, const WindowGeom &g, lon
     return L_ACCEPT;
 }
 
-// Exclusive prefix over nb (<= 1024) LDS counters s_cnt -> s_off; thread t owns the `per`
-// consecutive counters [t*per, t*per+per).  Returns the total.  All threads call it; ends
+// Inclusive prefix sum across a wave64 (DPP row shifts + row broadcasts; VALU only, no LDS).
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false);   // row_shr:1
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false);   // row_shr:2
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false);   // row_shr:4
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false);   // row_shr:8
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);   // row_bcast:15 -> rows 1, 3
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);   // row_bcast:31 -> rows 2, 3
+    return x;
+}
+
+// Exclusive prefix of v over a workgroup of T threads (DPP wave scans + one LDS round; VALU, no bpermute).
+// *total = the workgroup sum.  The caller synchronises before the next call (s_w is reused).
+template <int T>
+__device__ __forceinline__ uint32_t block_excl_scan_dpp(uint32_t v, uint32_t *total) {
+    __shared__ uint32_t s_w[T / 64];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const uint32_t incl = wave_incl_scan(v);
+    if (lane == 63) s_w[wid] = incl;
+    lds_barrier();
+    uint32_t pre = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < T / 64; ++w) {
+        const uint32_t x = s_w[w];
+        pre += w < wid ? x : 0u;
+        tot += x;
+    }
+    *total = tot;
+    return pre + incl - v;
+}
+
+// Exclusive prefix over nb (<= 4 * T) LDS counters s_cnt -> s_off; thread t owns the `per` consecutive counters
+// [t*per, t*per+per) (their counts in loc, their offsets in lof).  Returns the total.  All T threads call it; ends
 // synchronised, so s_off is complete on return.
+template <int T>
 __device__ __forceinline__ uint32_t tile_offsets(const uint32_t *s_cnt, uint32_t *s_off, int nb, uint32_t loc[4],
-                                                 int per) {
+                                                 uint32_t lof[4], int per) {
     uint32_t sum = 0;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
@@ -105,14 +147,15 @@ __device__ __forceinline__ uint32_t tile_offsets(const uint32_t *s_cnt, uint32_t
         sum += loc[q];
     }
     uint32_t total;
-    uint32_t ex = block_exclusive_scan(sum, &total);
+    uint32_t ex = block_excl_scan_dpp<T>(sum, &total);
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
         int b = threadIdx.x * per + q;
+        lof[q] = ex;
         if (q < per && b < nb) s_off[b] = ex;
         ex += loc[q];
     }
-    __syncthreads();   // every thread reads other threads' s_off next
+    lds_barrier();   // every thread reads other threads' s_off next
     return total;
 }
 
@@ -286,7 +329,7 @@ __global__ __launch_bounds__(LOG_K1_THREADS) void log_part_kernel(
     int tlen) {
     constexpr int W = HASV ? 2 : 1;
     KTrace kt;
-    kt.start(threadIdx.x == 0 && g_kt_on);
+    kt.start(__builtin_amdgcn_readfirstlane(threadIdx.x) < 64 && g_kt_on);   // wave 0, uniform (scalar registers)
     // K1 times itself: workgroup 0's start and the tail's end on the device wall clock (read back with the plan),
     // so profiling puts no event markers between K1 and pass 2 (each costs the stream ~5 us)
     if (blockIdx.x == 0 && threadIdx.x == 0 && ca.t0) atomicExch(ca.t0, (unsigned long long)wall_clock64());
@@ -299,19 +342,23 @@ __global__ __launch_bounds__(LOG_K1_THREADS) void log_part_kernel(
             c4[i] = make_uint4(0, 0, 0, 0);
     }
     // tlen (<= LOG_K1_TILE) records per tile: the launcher sizes tiles so that every workgroup loops over the same
-    // number of them (a last round of a few workgroups would cost a whole tile's latency)
-    __shared__ __attribute__((aligned(16))) int64_t s_rec[LOG_K1_TILE * W];
-    __shared__ uint16_t s_bk[LOG_K1_TILE];
-    __shared__ uint32_t s_rcnt[ROUTE ? LOG_RT_MAX : 1];             // routed records per destination (tile)
-    __shared__ uint32_t s_rbase[ROUTE ? LOG_RT_MAX : 1];            // their run's first record in the region
+    // number of them (a last round of a few workgroups would cost a whole tile's latency).  One spare record slot
+    // (index LOG_K1_TILE) takes the LDS writes of records that go nowhere, so the scatter needs no branch.
+    __shared__ __attribute__((aligned(16))) int64_t s_rec[(LOG_K1_TILE + 1) * W];
+    __shared__ uint16_t s_bk[LOG_K1_TILE + 1];
+    __shared__ uint32_t s_rbase[ROUTE ? LOG_RT_MAX : 1];            // routed runs' first record in the region
     const int nb = nunits * LOG_ND;
-    // bucket counters and offsets: dynamic LDS sized for the launch's windows (2 workgroups per CU up to 2 windows)
+    // dynamic LDS, sized for the launch's windows (2 workgroups per CU up to 2 windows): counters [0, nb), a spare
+    // counter (nb) for records counted nowhere, routed counters per destination (ROUTE), then the offsets [nb]
     extern __shared__ uint32_t s_kdyn[];
-    uint32_t *const s_cnt = s_kdyn, *const s_off = s_kdyn + nb;
+    uint32_t *const s_cnt = s_kdyn;
+    const int rc0 = nb + 1;                                          // first routed counter
+    uint32_t *const s_off = s_kdyn + nb + 1 + (ROUTE ? LOG_RT_MAX : 0);
     const int nr = ROUTE ? rt.nranks : 0;
     const int per = (nb + LOG_K1_THREADS - 1) / LOG_K1_THREADS;   // counters owned per thread (<= 4)
     const int tid = threadIdx.x;
     const int xg = blockIdx.x % LOG_XG;                           // region group (an XCD under round-robin placement)
+    const uint32_t cap32 = cap < 0xffffffffull ? (uint32_t)cap : 0xffffffffu;
     long long mn = 0x7fffffffffffffffLL, mx = (long long)0x8000000000000000LL;   // accepted windows (slow path)
     long long nx = 0x7fffffffffffffffLL;   // first accepted window after the launch's range (slow path)
     uint32_t wmask = 0;   // launch windows (bit jj) the inline path accepted records into
@@ -333,61 +380,75 @@ __global__ __launch_bounds__(LOG_K1_THREADS) void log_part_kernel(
     };
     const int64_t tstride = (int64_t)gridDim.x * tlen;
     if ((int64_t)blockIdx.x * tlen < n) load_tile((int64_t)blockIdx.x * tlen);
+    // the launch's window bounds as scalars (a run-time index into the argument, th.bound[nunits], is a scalar load
+    // per record, and its lgkmcnt wait also waited for the record's LDS atomic)
+    const int64_t tb0 = th.bound[0], tb1 = th.bound[1], tb2 = th.bound[2], tb3 = th.bound[3];
+    const int64_t tbh = nunits <= 1 ? tb1 : (nunits == 2 ? tb2 : (nunits == 3 ? tb3 : th.bound[4]));
+    const bool tok = th.ok != 0;
+    const uint32_t tcls = th.cls;
+    // Every per-record step below is branch-free where it touches LDS: a record's LDS atomic or read inside an
+    // `if` is waited for before the branch joins (its register is merged with the other path's value), which
+    // serialised one LDS round trip per record (ISA of r03: 16 waits per tile in each of classify, scatter, write).
     for (int64_t tile = (int64_t)blockIdx.x * tlen; tile < n; tile += tstride) {
-        for (int i = tid; i < nb; i += LOG_K1_THREADS) s_cnt[i] = 0;
-        if (ROUTE)
-            for (int i = tid; i < nr; i += LOG_K1_THREADS) s_rcnt[i] = 0;
-        __syncthreads();
+        for (int i = tid; i < rc0 + nr; i += LOG_K1_THREADS) s_kdyn[i] = 0;
+        lds_barrier();
         kt.stamp(0);
-        uint32_t code[LOG_K1_PER];
+        uint32_t code[LOG_K1_PER];   // (bucket or LOG_RT_B + destination) << 16 | rank; 0xffffffff: none
+        uint32_t rank[LOG_K1_PER];
         uint32_t slow = 0;   // bit j: record j is classified out of line (below)
 #pragma unroll
         for (int j = 0; j < LOG_K1_PER; ++j) {
             const int64_t i = tile + j * LOG_K1_THREADS + tid;
-            code[j] = 0xffffffffu;
-            if (i >= n || j * LOG_K1_THREADS + tid >= tlen) continue;
+            const bool in = i < n && j * LOG_K1_THREADS + tid < tlen;
+            uint32_t ci = (uint32_t)nb;   // counter this record increments (nb: the spare)
+            uint32_t cb = 0xffffu;        // its code's upper half (0xffff: none)
+            bool local = in;
             if (ROUTE) {   // KeyGroupStreamPartitioner.selectChannel: another GPU's record is its owner's to classify
                 const int dest = (int)(key_group(kk[j], g.key_kind, g.max_par) * rt.nranks / g.max_par);
-                if (dest != rt.me) {
-                    if (rt.mode == 1 || rt.mode == 3) {
-                        if (log_rt_fits(tt[j], rt.tbase)) {
-                            code[j] = ((uint32_t)(LOG_RT_B + dest) << 16) | atomicAdd(&s_rcnt[dest], 1u);
-                        } else {   // beyond the int32 timestamp range: a 24-B record in the wide region (rare)
-                            const unsigned long long q =
-                                atomicAdd(&rt.cursor[(size_t)(LOG_RT_MAX + dest) * LOG_CUR_STRIDE], 1ull);
-                            if (q < rt.wcap) {
-                                int64_t *w = log_rt_wide(rt.send, rt.rcap, rt.nranks, rt.wcap, dest) + q * 3;
-                                w[0] = kk[j];
-                                w[1] = tt[j];
-                                w[2] = HASV ? vv[j] : 0;
-                            }
+                const bool remote = in && dest != rt.me;
+                const bool fits = log_rt_fits(tt[j], rt.tbase);
+                if (remote && (rt.mode == 1 || rt.mode == 3)) {
+                    if (fits) {
+                        ci = (uint32_t)(rc0 + dest);
+                        cb = (uint32_t)(LOG_RT_B + dest);
+                    } else {   // beyond the int32 timestamp range: a 24-B record in the wide region (rare)
+                        const unsigned long long q =
+                            atomicAdd(&rt.cursor[(size_t)(LOG_RT_MAX + dest) * LOG_CUR_STRIDE], 1ull);
+                        if (q < rt.wcap) {
+                            int64_t *w = log_rt_wide(rt.send, rt.rcap, rt.nranks, rt.wcap, dest) + q * 3;
+                            w[0] = kk[j];
+                            w[1] = tt[j];
+                            w[2] = HASV ? vv[j] : 0;
                         }
                     }
-                    continue;
                 }
-                if (rt.mode == 3) continue;   // route-only re-run: the first K1 partitioned this GPU's records
+                local = in && !remote && rt.mode != 3;   // route-only re-run: the first K1 partitioned this GPU's records
             }
             // the common case, inline: a timestamp inside one of the launch's windows and that window open --
             // WindowOperator.java:386-427 decided once per window (LogThr), a few compares per record
             const int64_t t = tt[j];
-            const int jj = (t >= th.bound[1]) + (t >= th.bound[2]) + (t >= th.bound[3]);
-            if (!(th.ok && t >= th.bound[0] && t < th.bound[nunits] && ((th.cls >> (2 * jj)) & 3u) == 0)) {
-                slow |= 1u << j;
-                continue;
-            }
+            const int jj = (t >= tb1) + (t >= tb2) + (t >= tb3);
+            const bool inl = tok & (t >= tb0) & (t < tbh) & (((tcls >> (2 * jj)) & 3u) == 0);   // (no short circuit)
+            const bool take = local & inl;
+            slow |= ((local & !inl) ? 1u : 0u) << j;
             const int64_t k = kk[j];
-            if (!ROUTE && !th.full_range) {   // (routed: a record kept here is in range by construction)
+            if (!ROUTE && !th.full_range && take) {   // (routed: a record kept here is in range by construction)
                 const int32_t kg = key_group(k, g.key_kind, g.max_par);
                 if (kg < g.kg_lo || kg > g.kg_hi) {
                     bad_kg++;
                     atomicExch((unsigned long long *)&st->bad_kg_key, (unsigned long long)k);
                 }
             }
-            acc++;
-            wmask |= 1u << jj;
+            acc += take ? 1u : 0u;
+            wmask |= (take ? 1u : 0u) << jj;
             const uint32_t b = (uint32_t)(jj * LOG_ND + (int)(digit_hash(k) >> (32 - LOG_DB)));
-            code[j] = (b << 16) | atomicAdd(&s_cnt[b], 1u);
+            ci = take ? b : ci;
+            cb = take ? b : cb;
+            rank[j] = atomicAdd(&s_kdyn[ci], 1u);   // every record: the 16 atomics in flight together
+            code[j] = cb;
         }
+#pragma unroll
+        for (int j = 0; j < LOG_K1_PER; ++j) code[j] = code[j] == 0xffffu ? 0xffffffffu : (code[j] << 16) | rank[j];
         // everything else (late, re-fire and out-of-range records, Long.MIN_VALUE timestamps, extreme windows):
         // reloaded and classified in full by log_classify, one record at a time, outside the unrolled loop
 #pragma unroll 1
@@ -440,36 +501,62 @@ __global__ __launch_bounds__(LOG_K1_THREADS) void log_part_kernel(
             } else if (c == L_BAD_RANGE) {
                 bad_range++;
             }
+            // (rare path) its loads complete here, so the compiler's wait tracking carries no pending load of this
+            // path's registers into the common path (it had put an s_waitcnt vmcnt(0) into every tile's offsets scan)
+            __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
         }
         kt.stamp(1);
-        __syncthreads();
+        lds_barrier();
         kt.stamp(2);
         // reserve each bucket's run in this workgroup's region group, before the offsets scan, so that the
-        // atomics' round trip overlaps the scan and the LDS scatter; s_cnt[b] becomes the run's first record
-        unsigned long long at[4];
+        // atomics' round trip overlaps the scan and the LDS scatter (q < per is uniform: no per-lane branch, so the
+        // results are waited for only where they are used, after the scatter)
+        unsigned long long at[4];   // (no initial value: a merge with one would wait for the atomic at the branch)
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const int b = tid * per + q;
-            const uint32_t c = (q < per && b < nb) ? s_cnt[b] : 0u;
-            at[q] = c ? atomicAdd(&cursor[((size_t)b * LOG_XG + xg) * LOG_CUR_STRIDE], (unsigned long long)c) : 0ull;
+            if (q < per) at[q] = atomicAdd(&cursor[((size_t)b * LOG_XG + xg) * LOG_CUR_STRIDE],
+                                           (unsigned long long)(b < nb ? s_cnt[b] : 0u));
         }
         unsigned long long rat = 0;
         if (ROUTE && (rt.mode == 1 || rt.mode == 3) && tid < nr) {
-            const uint32_t c = s_rcnt[tid];
+            const uint32_t c = s_kdyn[rc0 + tid];
             rat = c ? atomicAdd(&rt.cursor[(size_t)tid * LOG_CUR_STRIDE], (unsigned long long)c) : 0ull;
         }
-        uint32_t loc[4];
-        const uint32_t total = tile_offsets(s_cnt, s_off, nb, loc, per);
+        uint32_t loc[4], lof[4];
+        const uint32_t total = tile_offsets<LOG_K1_THREADS>(s_cnt, s_off, nb, loc, lof, per);
         if (ROUTE && (rt.mode == 1 || rt.mode == 3)) {
             if (tid < nr) s_rbase[tid] = rat < 0xffffffffull ? (uint32_t)rat : 0xffffffffu;   // (>= rcap: not written)
-            __syncthreads();
+            lds_barrier();
         }
         kt.stamp(3);
+        // scatter into LDS by bucket: every offset read in flight together, then the writes (records of no local
+        // bucket write the spare slot)
+        uint32_t pos[LOG_K1_PER];
 #pragma unroll
         for (int j = 0; j < LOG_K1_PER; ++j) {
-            if (code[j] == 0xffffffffu) continue;
-            uint32_t b = code[j] >> 16;
-            if (ROUTE && b >= LOG_RT_B) {   // routed: straight from registers into the destination's run
+            const uint32_t b = code[j] >> 16;
+            const bool lc = code[j] != 0xffffffffu && (!ROUTE || b < LOG_RT_B);
+            pos[j] = s_off[lc ? b : 0u];
+        }
+#pragma unroll
+        for (int j = 0; j < LOG_K1_PER; ++j) {
+            const uint32_t b = code[j] >> 16;
+            const bool lc = code[j] != 0xffffffffu && (!ROUTE || b < LOG_RT_B);
+            const uint32_t ps = lc ? pos[j] + (code[j] & 0xffffu) : (uint32_t)LOG_K1_TILE;
+            if (HASV) {
+                ll2 r2 = {kk[j], vv[j]};
+                *(ll2 *)&s_rec[2 * ps] = r2;
+            } else {
+                s_rec[ps] = kk[j];
+            }
+            s_bk[ps] = (uint16_t)b;
+        }
+        if (ROUTE && (rt.mode == 1 || rt.mode == 3)) {
+#pragma unroll
+            for (int j = 0; j < LOG_K1_PER; ++j) {   // routed: straight from registers into the destination's run
+                const uint32_t b = code[j] >> 16;
+                if (code[j] == 0xffffffffu || b < LOG_RT_B) continue;
                 const uint32_t d = b - LOG_RT_B;
                 const unsigned long long q = (unsigned long long)s_rbase[d] + (code[j] & 0xffffu);
                 if (q < rt.rcap) {   // 20-B wire record: key, value, int32 ts - tbase (SoA per destination)
@@ -477,36 +564,55 @@ __global__ __launch_bounds__(LOG_K1_THREADS) void log_part_kernel(
                     log_rt_vals(rt.send, rt.rcap, (int)d)[q] = HASV ? vv[j] : 0;
                     log_rt_ts32(rt.send, rt.rcap, (int)d)[q] = (int32_t)(uint32_t)((uint64_t)tt[j] - (uint64_t)rt.tbase);
                 }
-                continue;
             }
-            uint32_t pos = s_off[b] + (code[j] & 0xffffu);
-            if (HASV) {
-                ll2 r2 = {kk[j], vv[j]};
-                *(ll2 *)&s_rec[2 * pos] = r2;
-            } else {
-                s_rec[pos] = kk[j];
-            }
-            s_bk[pos] = (uint16_t)b;
         }
-        if (tile + tstride < n) load_tile(tile + tstride);   // next tile in flight during the writes
+        // s_cnt[b] := the run's first region record - the bucket's tile offset, so the write phase finds a record's
+        // destination with one read (mod 2^32: q = s_cnt[b] + p; at >= cap -> q >= cap, the run is dropped).  Written
+        // before the next tile's loads are issued: a wait for the atomics after them would wait for those loads too.
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             int b = tid * per + q;
-            if (q < per && loc[q]) s_cnt[b] = (uint32_t)(at[q] < cap ? at[q] : cap);
+            if (q < per && loc[q]) s_cnt[b] = (at[q] < cap32 ? (uint32_t)at[q] : cap32) - lof[q];
         }
-        __syncthreads();
+        // next tile in flight during the writes: unconditional (past the end every lane re-reads record 0, one line),
+        // so the write phase's waits count exactly these loads instead of waiting for all of them
+        load_tile(tile + tstride);
+        lds_barrier();
         kt.stamp(4);
-        for (uint32_t p = tid; p < total; p += LOG_K1_THREADS) {
-            uint32_t b = s_bk[p];
-            if (b >= (uint32_t)nb) continue;   // defensive: never a write outside the buffer
-            uint64_t q = (uint64_t)s_cnt[b] + (p - s_off[b]);
-            if (q < cap) {
-                int64_t *dst = tmp + (((uint64_t)b * LOG_XG + xg) * cap + q) * W;
-                if (HASV) *(ll2 *)dst = *(const ll2 *)&s_rec[2 * p];
-                else *dst = s_rec[p];
+        // write phase: straight-line code (a loop here made the compiler wait for every prefetched load first),
+        // 4 records per thread per group with their LDS reads in flight together
+#pragma unroll
+        for (int p0 = 0; p0 < LOG_K1_TILE; p0 += 4 * LOG_K1_THREADS) {
+            uint32_t bb[4], pp[4];
+            ll2 rr[4];
+            int64_t r1[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                pp[u] = (uint32_t)p0 + u * LOG_K1_THREADS + tid;
+                const uint32_t pe = pp[u] < total ? pp[u] : (uint32_t)LOG_K1_TILE;
+                bb[u] = s_bk[pe];
+                if (HASV) rr[u] = *(const ll2 *)&s_rec[2 * pe];
+                else r1[u] = s_rec[pe];
+            }
+            uint32_t dl[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) dl[u] = s_cnt[bb[u] < (uint32_t)nb ? bb[u] : 0u];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const uint32_t q = dl[u] + pp[u];
+                // (bb >= nb: defensive, never a write outside the buffer)
+#ifdef GWO_ABL_K1_NOSTORE   // ablation (timing experiments only): the write phase without its global stores
+                if (pp[u] > 0xffffffffu - 1) {
+#else
+                if (pp[u] < total && bb[u] < (uint32_t)nb && q < cap32) {
+#endif
+                    int64_t *dst = tmp + (((uint64_t)bb[u] * LOG_XG + xg) * cap + q) * W;
+                    if (HASV) *(ll2 *)dst = rr[u];
+                    else *dst = r1[u];
+                }
             }
         }
-        __syncthreads();
+        lds_barrier();
         kt.stamp(5);
     }
     if (wmask) {
@@ -559,7 +665,7 @@ __global__ __launch_bounds__(LOG_K1_THREADS) void log_part_kernel(
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     kt.stamp(6);
-    if (kt.on && blockIdx.x == 0) atomicAdd(&g_kt[32], 1ull);
+    if (kt.on && blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&g_kt[32], 1ull);
     kt.flush(KT_K1);
     if (tid == 0) {
         const unsigned sh = blockIdx.x % LOG_SHARDS;
@@ -664,8 +770,8 @@ __global__ __launch_bounds__(LOG_TILE_THREADS) void log_split_kernel(const int64
     }
     __syncthreads();
     const int per = F <= LOG_TILE_THREADS ? 1 : F / LOG_TILE_THREADS;
-    uint32_t loc[4];
-    const uint32_t total = tile_offsets(s_cnt, s_off, F, loc, per);
+    uint32_t loc[4], lof[4];
+    const uint32_t total = tile_offsets<LOG_TILE_THREADS>(s_cnt, s_off, F, loc, lof, per);
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
         int f = tid * per + q;
@@ -939,17 +1045,6 @@ __device__ __forceinline__ int64_t dpp_swap_pair64(int64_t x) {
     return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
 }
 
-// Inclusive prefix sum across a wave64 (DPP row shifts + row broadcasts; VALU only, no LDS).
-__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
-    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false);   // row_shr:1
-    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false);   // row_shr:2
-    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false);   // row_shr:4
-    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false);   // row_shr:8
-    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);   // row_bcast:15 -> rows 1, 3
-    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);   // row_bcast:31 -> rows 2, 3
-    return x;
-}
-
 __device__ __forceinline__ int64_t word_combine(int op, int64_t a, int64_t b) {
     switch (op) {
         case ACC_ADD_I64: return (int64_t)((uint64_t)a + (uint64_t)b);
@@ -971,9 +1066,12 @@ __device__ __forceinline__ uint32_t slot_mix(int64_t k) {
 
 // PART: the checkpoint instance -- restored partial accumulators (after gwo_restore) and slow-path-only folds
 // (gwo_snapshot's raw-word rows); a separate instance, so the watermark fire carries none of their code or registers.
-template <int NW, bool PART>
+// HV: the records carry values (16-B records; keys only: 8 B) -- a compile-time choice, since a load into registers
+// chosen at run time between two widths merges the two definitions and waits for the load on the spot (the register
+// prefetch of the next partition had waited for each of its 7 loads in turn).
+template <int NW, bool PART, bool HV>
 __global__ __launch_bounds__(LOG_FIRE_THREADS) __attribute__((amdgpu_waves_per_eu(4, 4))) void log_fire_kernel(const LogSegDesc *__restrict__ segs, int nseg,
-                                                                    uint32_t nparts, int cap_log2, int has_val,
+                                                                    uint32_t nparts, int cap_log2, int has_val_arg,
                                                                     AccPlan p, ResultPlan rp, int64_t start,
                                                                     int64_t end, OutCols o,
                                                                     unsigned long long *overflow, int slow_only,
@@ -985,6 +1083,8 @@ __global__ __launch_bounds__(LOG_FIRE_THREADS) __attribute__((amdgpu_waves_per_e
     //                             s_val and the head of s_cnt; dead once the leaders have read their counts)
     //   s_cnt [FIRE_RCAP] uint32  per-leader record counts -> offsets -> (offset | count << 16) by ordinal
     // Slow path: the same bytes hold a FireCtx hash table (key + words, SoA, 2^cap_log2 slots).
+    (void)has_val_arg;
+    constexpr int has_val = HV ? 1 : 0;
     extern __shared__ __attribute__((aligned(16))) int64_t s_dyn[];
     int64_t *const s_key = s_dyn;
     int64_t *const s_val = s_dyn + FIRE_RCAP;
@@ -996,7 +1096,7 @@ __global__ __launch_bounds__(LOG_FIRE_THREADS) __attribute__((amdgpu_waves_per_e
     __shared__ uint32_t s_src[LOG_MAX_SEGS];       //   covers [s_beg[s], s_beg[s+1]) from record s_src[s]
     __shared__ const int64_t *s_rp[LOG_MAX_SEGS];
     __shared__ uint32_t s_wsum[FIRE_RPT * (LOG_FIRE_THREADS / 64)];   // per-(r, wave) sums -> prefixes
-    __shared__ uint32_t s_tot;
+    __shared__ uint32_t s_tot, s_rows;
     __shared__ uint32_t s_pw[LOG_FIRE_THREADS / 64 + 1];
     __shared__ unsigned long long s_rbase;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -1005,7 +1105,7 @@ __global__ __launch_bounds__(LOG_FIRE_THREADS) __attribute__((amdgpu_waves_per_e
     uint32_t part = blockIdx.x;
     if (part >= nparts) return;
     KTrace kt;
-    kt.start(tid == 0 && g_kt_on);
+    kt.start(__builtin_amdgcn_readfirstlane(threadIdx.x) < 64 && g_kt_on);   // wave 0, uniform (scalar registers)
     for (int s = tid; s < nseg; s += LOG_FIRE_THREADS) s_rp[s] = segs[s].rec;
     if (tid <= GWO_MAX_WORDS) s_side[tid] = tid == 0 ? 0 : p.ident[tid - 1];
     if (tid == 0) {
@@ -1013,13 +1113,15 @@ __global__ __launch_bounds__(LOG_FIRE_THREADS) __attribute__((amdgpu_waves_per_e
         s_fail = 0;
     }
 
+    // Barriers in the fast path are LDS-only (lds_barrier): the next partition's records, the row reservation and
+    // the emitted rows stay in flight across them (__syncthreads() drained every load, store and atomic each time).
     // segment ranges of a partition -> s_beg / s_src (all threads; ends synchronised)
     // (a DPP scan with the workgroup size fixed at compile time: block_exclusive_scan reads blockDim,
     // which costs a dispatch-packet load and a vmcnt(0) wait on everything in flight)
     auto publish = [&](uint32_t cnt, uint32_t off) {
         const uint32_t incl_c = wave_incl_scan(cnt);
         if (lane == 63) s_pw[wave] = incl_c;
-        __syncthreads();
+        lds_barrier();
         if (tid == 0) {
             uint32_t run = 0;
 #pragma unroll
@@ -1030,13 +1132,13 @@ __global__ __launch_bounds__(LOG_FIRE_THREADS) __attribute__((amdgpu_waves_per_e
             }
             s_pw[LOG_FIRE_THREADS / 64] = run;
         }
-        __syncthreads();
+        lds_barrier();
         if (tid < nseg) {
             s_beg[tid] = s_pw[wave] + incl_c - cnt;
             s_src[tid] = off;
         }
         if (tid == 0) s_beg[nseg] = s_pw[LOG_FIRE_THREADS / 64];
-        __syncthreads();
+        lds_barrier();
     };
     // register prefetch of a partition's records (only when they all fit); global (not flat) loads,
     // so LDS waits in between do not wait for them
@@ -1125,21 +1227,21 @@ __global__ __launch_bounds__(LOG_FIRE_THREADS) __attribute__((amdgpu_waves_per_e
             load_next();
             for (int q = tid; q < FIRE_OWN / 4; q += LOG_FIRE_THREADS)
                 ((uint4 *)s_own)[q] = make_uint4(FIRE_FREE, FIRE_FREE, FIRE_FREE, FIRE_FREE);
-            __syncthreads();
+            if (tid == 0) s_rows = 0;
+            lds_barrier();
             kt.stamp(0);
             // P1: claim or join, no barrier per probe round.  Every record of a key walks the same slot
             // sequence (double hashing on slot_mix).  A compare-and-swap of a free slot makes the record its
             // key's leader (count 1, rank 0); a slot whose leader holds the same key is joined by one add of
             // FIRE_ONE, whose return value is the record's rank among its key's records; a slot of another key
             // sends the record on.  The table never fills (8192 slots, <= 3584 keys), so every record ends.
-            // sl[r]: probe slot while pending, then the leader record; own[r]: a leader's slot.
-            uint32_t sl[FIRE_RPT], own[FIRE_RPT], rank[FIRE_RPT];
+            // sl[r]: probe slot while pending; then a leader's own slot, or a follower's leader record.
+            uint32_t sl[FIRE_RPT], rank[FIRE_RPT];
             unsigned pend = 0, leader = 0;
 #pragma unroll
             for (int r = 0; r < FIRE_RPT; ++r) {
                 const uint32_t i = r * LOG_FIRE_THREADS + tid;
                 sl[r] = slot_mix(rk[r]) >> (32 - FIRE_OWN_LOG2);
-                own[r] = 0;
                 rank[r] = 0;
                 if (i < total) pend |= 1u << r;
             }
@@ -1155,9 +1257,7 @@ __global__ __launch_bounds__(LOG_FIRE_THREADS) __attribute__((amdgpu_waves_per_e
                 for (int r = 0; r < FIRE_RPT; ++r) {
                     if (!((pend >> r) & 1u)) continue;
                     if (prev[r] == FIRE_FREE) {   // claimed: this record leads its key
-                        own[r] = sl[r];
-                        sl[r] = r * LOG_FIRE_THREADS + tid;
-                        leader |= 1u << r;
+                        leader |= 1u << r;   // (sl[r] stays its slot)
                         pend &= ~(1u << r);
                     } else if (s_key[prev[r] & (FIRE_ONE - 1)] == rk[r]) {
                         join |= 1u << r;
@@ -1174,61 +1274,71 @@ __global__ __launch_bounds__(LOG_FIRE_THREADS) __attribute__((amdgpu_waves_per_e
                     if ((join >> r) & 1u) sl[r] = prev[r] & (FIRE_ONE - 1);
                 pend &= ~join;
             }
+            {   // the partition's rows = its leaders: counted per wave now, so the row reservation is issued before P3
+                uint32_t nl = 0;
+#pragma unroll
+                for (int r = 0; r < FIRE_RPT; ++r) nl += (uint32_t)__popcll(__ballot((leader >> r) & 1u));
+                if (lane == 0 && nl) atomicAdd(&s_rows, nl);
+            }
             kt.stamp(1);
-            __syncthreads();
+            lds_barrier();
+            // the row reservation's round trip overlaps P3-P4 (consumed at P4b)
+            if (tid == 0) rbase_lane0 = atomicAdd(o.count, (unsigned long long)s_rows);
             kt.stamp(2);
             {
                 // P3: exclusive scan over record ids of (count | 1 << 16) at leaders -> each leader's
-                // first value offset (low half) and row ordinal (high half).  (rk is dead from here on.)
-                uint32_t x[FIRE_RPT], incl[FIRE_RPT];
+                // first value offset (low half) and row ordinal (high half).
+                uint32_t xl[FIRE_RPT];   // exclusive prefix within the wave (one array live across the barriers)
 #pragma unroll
-                for (int r = 0; r < FIRE_RPT; ++r) x[r] = ((leader >> r) & 1u) ? ((s_own[own[r]] >> 12) | 0x10000u) : 0u;
-#pragma unroll
-                for (int r = 0; r < FIRE_RPT; ++r) {
-                    incl[r] = wave_incl_scan(x[r]);
-                    if (lane == 63) s_wsum[r * (LOG_FIRE_THREADS / 64) + wave] = incl[r];
+                for (int r = 0; r < FIRE_RPT; ++r) {   // (an unconditional read: a read under a branch is waited at the join)
+                    const uint32_t ow = s_own[sl[r]];   // followers: sl = a record index, a valid slot too
+                    const uint32_t x = ((leader >> r) & 1u) ? ((ow >> 12) | 0x10000u) : 0u;
+                    const uint32_t incl = wave_incl_scan(x);
+                    xl[r] = incl - x;
+                    if (lane == 63) s_wsum[r * (LOG_FIRE_THREADS / 64) + wave] = incl;
                 }
-                __syncthreads();
+                lds_barrier();
                 if (wave == 0) {
                     constexpr int NS = FIRE_RPT * (LOG_FIRE_THREADS / 64);
                     const uint32_t w = lane < NS ? s_wsum[lane] : 0u;
                     const uint32_t wi = wave_incl_scan(w);
                     if (lane < NS) s_wsum[lane] = wi - w;
                     const uint32_t tot = __shfl(wi, 63);
-                    if (lane == 0) {
-                        s_tot = tot;
-                        const uint32_t rows = tot >> 16;
-                        rbase_lane0 = rows ? atomicAdd(o.count, (unsigned long long)rows) : 0ull;
-                    }
+                    if (lane == 0) s_tot = tot;
                 }
-                __syncthreads();
+                lds_barrier();
                 uint32_t lo[FIRE_RPT];   // leaders: value offset | row ordinal << 16
 #pragma unroll
                 for (int r = 0; r < FIRE_RPT; ++r) {
                     const uint32_t i = r * LOG_FIRE_THREADS + tid;
-                    const uint32_t pre = s_wsum[r * (LOG_FIRE_THREADS / 64) + wave] + incl[r] - x[r];
+                    const uint32_t pre = s_wsum[r * (LOG_FIRE_THREADS / 64) + wave] + xl[r];
                     lo[r] = pre;
-                    if (x[r]) s_cnt[i] = pre & 0xffffu;
+                    if ((leader >> r) & 1u) s_cnt[i] = pre & 0xffffu;
                 }
-                __syncthreads();
-                // P4: values grouped by key, in row order (the election table is dead)
+                lds_barrier();
+                // P4: values grouped by key, in row order (the election table is dead).  Every follower's read of its
+                // leader's offset is issued before any write (reads unconditional: leaders read entry 0).
                 if (has_val) {
+                    uint32_t lof[FIRE_RPT];
+#pragma unroll
+                    for (int r = 0; r < FIRE_RPT; ++r) lof[r] = s_cnt[((leader >> r) & 1u) ? 0u : sl[r]];
 #pragma unroll
                     for (int r = 0; r < FIRE_RPT; ++r) {
                         const uint32_t i = r * LOG_FIRE_THREADS + tid;
-                        if (i >= total) continue;
-                        const uint32_t off = ((leader >> r) & 1u) ? (lo[r] & 0xffffu) : s_cnt[sl[r]];
+                        const uint32_t off = ((leader >> r) & 1u) ? (lo[r] & 0xffffu) : lof[r];
                         const uint32_t at = off + rank[r];
-                        if (at < (uint32_t)FIRE_RCAP) s_val[at] = rv[r];
+                        if (i < total && at < (uint32_t)FIRE_RCAP) s_val[at] = rv[r];
                     }
                 }
-                __syncthreads();
-                // P4b: row ordinal -> (value offset | leader record << 16); a row's value count is the
-                // next row's offset minus its own (s_cnt[rows] = total)
+                lds_barrier();
+                // P4b: by row ordinal, the row's first value offset (a row's value count is the next row's offset
+                // minus its own; s_cnt[rows] = total) and its key (every read of s_key by record is done)
 #pragma unroll
                 for (int r = 0; r < FIRE_RPT; ++r)
-                    if ((leader >> r) & 1u)
-                        s_cnt[lo[r] >> 16] = (lo[r] & 0xffffu) | ((uint32_t)(r * LOG_FIRE_THREADS + tid) << 16);
+                    if ((leader >> r) & 1u) {
+                        s_cnt[lo[r] >> 16] = lo[r] & 0xffffu;
+                        s_key[lo[r] >> 16] = rk[r];
+                    }
                 if (tid == 0) {
                     s_cnt[s_tot >> 16] = s_tot & 0xffffu;
                     s_rbase = rbase_lane0;   // the atomic's round trip overlapped P4
@@ -1292,7 +1402,7 @@ __global__ __launch_bounds__(LOG_FIRE_THREADS) __attribute__((amdgpu_waves_per_e
         }
         // (synchronises: the fast path's (offset, count) words and s_rbase are visible)
         if (more) publish(a_cnt, a_off);
-        else __syncthreads();
+        else lds_barrier();
         // unconditional, so the loads land straight in rk/rv (no loop-carried copy that would wait for
         // them): in flight during this partition's emit and the next one's election
         prefetch(more && !(PART && slow_only));
@@ -1311,23 +1421,48 @@ __global__ __launch_bounds__(LOG_FIRE_THREADS) __attribute__((amdgpu_waves_per_e
                 const int q = base + tid - sh;
                 const bool valid = q >= 0 && q < (int)rows;
                 int64_t k = 0, res[4] = {0, 0, 0, 0};
-                if (valid) {
-                    const uint32_t w0 = s_cnt[q], off = w0 & 0xffffu, n = (s_cnt[q + 1] & 0xffffu) - off;
-                    k = s_key[w0 >> 16];
+                {   // (reads unconditional, from row 0 for lanes without a row: no LDS read waits at a branch join)
+                    const uint32_t qc = valid ? (uint32_t)q : 0u;
+                    const uint32_t off = s_cnt[qc], nxt = s_cnt[qc + 1];
+                    k = s_key[qc];
+                    const uint32_t n = valid ? nxt - off : 0u;
                     // the run's count, sum and min/max (of the values, or of their Double.compareTo order
-                    // keys for float64) in a tight loop; the plan's words are read off them afterwards
+                    // keys for float64): its first 4 values read together, the rest (rare) in a loop; the plan's
+                    // words are read off them afterwards
                     int64_t si = 0, mn = 0x7fffffffffffffffLL, mx = (int64_t)0x8000000000000000LL;
                     double sf = 0.0;
                     if (has_val) {
+                        int64_t v4[4];
+#pragma unroll
+                        for (int t = 0; t < 4; ++t) {
+                            const uint32_t ix = off + t < (uint32_t)FIRE_RCAP ? off + t : 0u;
+                            v4[t] = s_val[ix];
+                        }
                         if (p.value_is_f64) {
-                            for (uint32_t t = 0; t < n; ++t) {
+#pragma unroll
+                            for (int t = 0; t < 4; ++t) {
+                                const bool in = (uint32_t)t < n;
+                                const int64_t v = v4[t], ok = f64_order_key(v);
+                                sf += in ? __longlong_as_double(v) : 0.0;
+                                mn = (in && ok < mn) ? ok : mn;
+                                mx = (in && ok > mx) ? ok : mx;
+                            }
+                            for (uint32_t t = 4; t < n; ++t) {
                                 const int64_t v = s_val[off + t], ok = f64_order_key(v);
                                 sf += __longlong_as_double(v);
                                 mn = ok < mn ? ok : mn;
                                 mx = ok > mx ? ok : mx;
                             }
                         } else {
-                            for (uint32_t t = 0; t < n; ++t) {
+#pragma unroll
+                            for (int t = 0; t < 4; ++t) {
+                                const bool in = (uint32_t)t < n;
+                                const int64_t v = v4[t];
+                                si = (int64_t)((uint64_t)si + (uint64_t)(in ? v : 0));
+                                mn = (in && v < mn) ? v : mn;
+                                mx = (in && v > mx) ? v : mx;
+                            }
+                            for (uint32_t t = 4; t < n; ++t) {
                                 const int64_t v = s_val[off + t];
                                 si = (int64_t)((uint64_t)si + (uint64_t)v);
                                 mn = v < mn ? v : mn;
@@ -1355,6 +1490,9 @@ __global__ __launch_bounds__(LOG_FIRE_THREADS) __attribute__((amdgpu_waves_per_e
                 if (!valid) continue;
                 const unsigned long long pos = rbase + (unsigned long long)(long long)q;
                 const unsigned long long pb = pos & ~1ull;   // the pair's first row
+#ifdef GWO_ABL_FIRE_NOSTORE   // ablation (timing experiments only): the emit without its global stores
+                if (pb != ~0ull) continue;
+#endif
                 if (pvalid && (long long)pb + 1 < o.cap) {
                     if (!odd) {
                         *(ll2 *)(o.key + pb) = ll2{k, kp};
@@ -1374,13 +1512,13 @@ __global__ __launch_bounds__(LOG_FIRE_THREADS) __attribute__((amdgpu_waves_per_e
                         if (a < rp.naggs) o.res[a][pos] = res[a];
                 }
             }
-            __syncthreads();   // the next partition overwrites s_key / s_cnt
+            lds_barrier();   // the next partition overwrites s_key / s_cnt
             kt.stamp(5);
         }
         if (!more) break;
         part = nxt;
     }
-    if (kt.on && blockIdx.x == 0) atomicAdd(&g_kt[33], 1ull);
+    if (kt.on && blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&g_kt[33], 1ull);
     kt.flush(KT_FIRE);
 }
 
@@ -1400,12 +1538,13 @@ void launch_log_part(const int64_t *key, const int64_t *ts, const int64_t *val, 
     const int64_t rounds = (n + grid * LOG_K1_TILE - 1) / (grid * LOG_K1_TILE);
     int64_t tl = rounds > 0 ? (n + grid * rounds - 1) / (grid * rounds) : LOG_K1_TILE;
     tl = tl < 1 ? 1 : (tl > LOG_K1_TILE ? LOG_K1_TILE : tl);
-    const size_t dyn = (size_t)2 * nunits * LOG_ND * sizeof(uint32_t);
+    const bool route = rt.mode != 0 && stride == 1;
+    const size_t dyn = ((size_t)2 * nunits * LOG_ND + 1 + (route ? LOG_RT_MAX : 0)) * sizeof(uint32_t);
 #define GWO_K1(HV, S, R, T32)                                                                                  \
     hipLaunchKernelGGL((log_part_kernel<HV, S, R, T32>), dim3((int)grid), dim3(LOG_K1_THREADS), dyn, s, key, ts, val, \
                        n, stride, g, base, nunits, cursor, cap, tmp, st, side_key, side_ts, side_val, side_count, \
                        side_cap, side_enabled, ca, thr, rt, (int)tl)
-    if (rt.mode != 0 && stride == 1) {   // routing: the first K1 over a batch's own columns (and its route-only re-run)
+    if (route) {   // routing: the first K1 over a batch's own columns (and its route-only re-run)
         if (has_val) GWO_K1(true, 1, true, false);
         else GWO_K1(false, 1, true, false);
     } else if (thr.ts32) {               // received 20-B wire records (SoA columns, int32 timestamps)
@@ -1443,8 +1582,12 @@ void warm_log_kernels(int nwords, int has_val, hipStream_t s) {
     if (lds < (size_t)FIRE_LDS) lds = FIRE_LDS;
 #define GWO_WARM_NW(NW)                                                                                            \
     case NW:                                                                                                       \
-        hipLaunchKernelGGL((log_fire_kernel<NW, false>), dim3(1), dim3(LOG_FIRE_THREADS), lds, s, nullptr, 0, 0u, cl, has_val, p, \
-                           rp, 0, 0, o, nullptr, 0, LogSegDesc{});                                                 \
+        if (has_val)                                                                                               \
+            hipLaunchKernelGGL((log_fire_kernel<NW, false, true>), dim3(1), dim3(LOG_FIRE_THREADS), lds, s, nullptr, 0, 0u, cl, \
+                               has_val, p, rp, 0, 0, o, nullptr, 0, LogSegDesc{});                                 \
+        else                                                                                                       \
+            hipLaunchKernelGGL((log_fire_kernel<NW, false, false>), dim3(1), dim3(LOG_FIRE_THREADS), lds, s, nullptr, 0, 0u, cl, \
+                               has_val, p, rp, 0, 0, o, nullptr, 0, LogSegDesc{});                                 \
         break;
     switch (nwords) {
         GWO_WARM_NW(1)
@@ -1482,12 +1625,20 @@ void launch_log_fire(const LogSegDesc *segs, int nseg, int lp, int has_val, cons
     uint32_t grid = parts < groups ? parts : groups;
 #define GWO_FIRE_NW(NW)                                                                                          \
     case NW:                                                                                                     \
-        if (partial.rec || slow_only)                                                                            \
-            hipLaunchKernelGGL((log_fire_kernel<NW, true>), dim3(grid), dim3(LOG_FIRE_THREADS), lds, s, segs, nseg,  \
+        if (partial.rec || slow_only) {                                                                          \
+            if (has_val)                                                                                         \
+                hipLaunchKernelGGL((log_fire_kernel<NW, true, true>), dim3(grid), dim3(LOG_FIRE_THREADS), lds, s, segs, nseg, \
+                                   parts, cl, has_val, plan, rp, start, end, out, overflow, slow_only, partial); \
+            else                                                                                                 \
+                hipLaunchKernelGGL((log_fire_kernel<NW, true, false>), dim3(grid), dim3(LOG_FIRE_THREADS), lds, s, segs, nseg, \
+                                   parts, cl, has_val, plan, rp, start, end, out, overflow, slow_only, partial); \
+        } else if (has_val) {                                                                                    \
+            hipLaunchKernelGGL((log_fire_kernel<NW, false, true>), dim3(grid), dim3(LOG_FIRE_THREADS), lds, s, segs, nseg, \
                                parts, cl, has_val, plan, rp, start, end, out, overflow, slow_only, partial);     \
-        else                                                                                                     \
-            hipLaunchKernelGGL((log_fire_kernel<NW, false>), dim3(grid), dim3(LOG_FIRE_THREADS), lds, s, segs, nseg, \
+        } else {                                                                                                 \
+            hipLaunchKernelGGL((log_fire_kernel<NW, false, false>), dim3(grid), dim3(LOG_FIRE_THREADS), lds, s, segs, nseg, \
                                parts, cl, has_val, plan, rp, start, end, out, overflow, slow_only, partial);     \
+        }                                                                                                        \
         break;
     switch (plan.nwords) {
         GWO_FIRE_NW(1)

@@ -440,7 +440,7 @@ gwo_status Handle::insert_combined(const int64_t *k, const int64_t *t, const int
     }
     const int G = (int)std::max<int64_t>(1, std::min<int64_t>((n + tile - 1) / tile, (int64_t)cb_max_wg));
     int S = 2048;   // (4096-slot tables where one workgroup per CU leaves the LDS: no faster, the merge slower)
-    while (S > 256 && gather_lds_bytes(S, NW) > 65536) S >>= 1;
+    while (S > 256 && gather_lds_bytes(S, NW) > 65536 + 512) S >>= 1;   // (tables + 64 spare words)
     GWO_TRY(ensure_buf(cb_dump_key, (size_t)G * 2 * S * 8 + (size_t)G * 4));
     GWO_TRY(ensure_buf(cb_dump_acc, (size_t)G * 2 * S * NW * 8));
     GWO_TRY(ensure_buf(cb_ovf, (size_t)n * 4));

@@ -1,0 +1,17 @@
+# Builds an experimental variant of libgwo.so (extra HIP flags, e.g. -DGWO_KTRACE) into exp/NAME/libgwo.so, for
+# A/B runs with GWO_LIB_PATH (exp/ is git-ignored; the .so travels to the GPU box with the tree).
+set -e
+NAME=$1; shift
+FLAGS="$*"
+R=$(cd "$(dirname "$0")/.." && pwd)
+OUT=$R/exp/$NAME
+mkdir -p $OUT/obj
+for f in $R/flink_amd/csrc/*.hip; do
+  b=$(basename $f .hip)
+  EXTRA=""
+  [ "$b" = gwo_log ] && EXTRA="-mllvm -amdgpu-atomic-optimizer-strategy=None"
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unused-function $EXTRA $FLAGS -c $f -o $OUT/obj/$b.hip.o &
+done
+wait
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $OUT/libgwo.so $OUT/obj/*.hip.o $R/build/obj/*.cpp.o -L/opt/rocm/lib -lamdhip64 -lrccl -Wl,-rpath,/opt/rocm/lib
+echo built $OUT/libgwo.so
