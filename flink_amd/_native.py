@@ -80,6 +80,8 @@ SIGNATURES = [
     ("gwo_create", C.c_int, [C.POINTER(GwoConfig), C.POINTER(_P)]),
     ("gwo_destroy", C.c_int, [_P]),
     ("gwo_submit", C.c_int, [_P, _P, _P, _P, C.c_int64]),
+    ("gwo_host_register", C.c_int, [_P, C.c_int64]),
+    ("gwo_host_unregister", C.c_int, [_P]),
     ("gwo_submit_utf16", C.c_int, [_P, _P, _P, _P, _P, C.c_int64]),
     ("gwo_intern_utf16", C.c_int, [_P, _P, _P, C.c_int64, _P]),
     ("gwo_key_strings", C.c_int, [_P, _P, C.c_int64, _P, _P, C.c_int64, _I64P]),
@@ -116,6 +118,8 @@ SIGNATURES = [
     ("gwo_window_starts", C.c_int, [_P, C.c_int64, C.c_int64, C.c_int64, _P, C.c_int32]),
     ("gwo_comm_unique_id", C.c_int, [C.POINTER(C.c_uint8)]),
     ("gwo_comm_init", C.c_int, [_P, C.POINTER(C.c_uint8), C.c_int32, C.c_int32]),
+    ("gwo_comm_set_async_watermark", C.c_int, [_P, C.c_int32]),
+    ("gwo_comm_stats", C.c_int, [_P, _I64P, _I64P, _I64P]),
     ("gwo_partition_by_operator", C.c_int, [_P, _P, _P, C.c_int64, C.c_int32, C.c_int32, C.c_int32, _P, C.c_int64,
                                             _P, C.c_int32]),
     ("gwo_generate", C.c_int, [C.POINTER(GwoGenSpec), C.c_int64, _P, _P, _P, _P, C.c_int32]),

@@ -12,6 +12,7 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
 #include <vector>
 
 #include "gwo_handle.h"
@@ -48,31 +49,61 @@ struct Comm {
     // every rank holds the same value, so sender and receiver derive the same tbase from it even when restored
     // subtasks hold different watermarks
     int64_t agreed_wm = (int64_t)0x8000000000000000LL;
-    // Routed exchanges of the log layout alternate between two send/receive buffer slots: batch i+1's routed K1 fills
-    // one send slot while batch i's records are still on the wire from the other, and batch i+1's receives land in
-    // the slot batch i-1's received records were read from (its K1 was resolved before batch i+1 was queued).
-    DevBuf rsend[2], rrecv[2];
-    hipEvent_t ev_rrecv[2] = {nullptr, nullptr};
+    // Routed exchanges of the log layout rotate over NS send/receive buffer slots.  Batch i's routed K1
+    // fills send slot i % NS and its per-destination counts; the counts are exchanged on the count communicator right
+    // behind K1 and published to host-mapped memory, and batch i's record exchange is posted one batch later -- at
+    // batch i+1's gwo_submit, when the counts have long arrived -- so no routed batch waits on the host for them.
+    // Its received records are inserted at batch i+2 (or at any earlier flush: a fire they may fall into, a snapshot,
+    // gwo_sync, a state query).  Slot reuse is ordered on the device: a routed K1 waits for the exchange that last
+    // sent from its slot, an exchange waits for the K1 that last read its receive slot.
+    static constexpr int NS = 3;
+    DevBuf rsend[NS], rrecv[NS], rcnt[NS];         // send regions; receive buffer; (narrow, wide) counts, 4P words
+    hipEvent_t ev_rrecv[NS] = {};                  // the slot's record exchange finished (cs)
+    hipEvent_t ev_rout[NS] = {};                   // the slot's routed K1 (and re-route) finished (main stream)
+    hipEvent_t ev_read[NS] = {};                   // the slot's received records were read (main stream)
+    bool used_send[NS] = {}, used_read[NS] = {};
+    unsigned long long *hcnt[NS] = {}, *hcnt_dev[NS] = {};   // host-mapped: 4P count words + sequence word
+    unsigned long long cnt_seq = 0;
     int rslot = 0;
     // Counts and watermark agreement run on a second communicator (ncclCommSplit of nc) and stream: RCCL orders the
-    // operations of one communicator, so on nc they would queue behind the previous batch's record exchange and the
-    // host's wait for them would end the overlap.
+    // operations of one communicator, so on nc they would queue behind the previous batch's record exchange.
     ncclComm_t nc2 = nullptr;
     hipStream_t cs2 = nullptr;
-    struct Recv {
+    struct Post {                  // a routed batch whose record exchange is not posted yet
         bool active = false;
+        int slot = 0;
+        unsigned long long seq = 0;
+        uint64_t rcap = 0, wcap = 0;
+        int64_t tbase = 0;
+        WindowGeom g{};
+    };
+    Post post;
+    struct Recv {
         int slot = 0;
         int64_t n = 0, w = 0;      // narrow / wide records received
         int64_t off_w = 0;         // word offset of the wide records in the slot's receive buffer
         int64_t tbase = 0;
         WindowGeom g{};            // the geometry (watermark) of the batch they belong to
     };
-    Recv last;                     // the last routed exchange queued
-    Recv pend;                     // deferred: received records not yet inserted (comm_flush_received)
+    std::deque<Recv> recvq;        // posted exchanges whose records are not inserted yet (oldest first)
+    // host round trips of the routed exchange: batches routed, waits for a batch's counts (only a flush waits: a fire
+    // its records may fall into, a snapshot, gwo_sync), synchronous watermark agreements
+    int64_t routed = 0, count_waits = 0, wm_waits = 0;
+    // asynchronous watermark agreement (gwo_comm_set_async_watermark): two host-mapped result blocks, alternating
+    bool async_wm = false, wm_pending = false;
+    unsigned long long *hwm[2] = {}, *hwm_dev[2] = {};
+    unsigned long long wm_seq = 0;
     bool defer = true;             // GWO_COMM_DEFER=0: insert every batch's received records inside its gwo_submit
 };
 
 static int route_ranks(const Comm &C) { return C.vranks > 1 ? C.vranks : C.nranks; }
+
+static bool comm_events(Comm *C) {
+    for (int q = 0; q < Comm::NS; ++q)
+        for (hipEvent_t *e : {&C->ev_rrecv[q], &C->ev_rout[q], &C->ev_read[q]})
+            if (hipEventCreateWithFlags(e, hipEventDisableTiming) != hipSuccess) return false;
+    return true;
+}
 
 void Handle::comm_free() {
     if (!comm) return;
@@ -81,13 +112,20 @@ void Handle::comm_free() {
     if (comm->nc2) ncclCommDestroy(comm->nc2);
     if (comm->nc) ncclCommDestroy(comm->nc);
     for (DevBuf *b : {&comm->dest, &comm->k1, &comm->v1, &comm->hist, &comm->sendbuf, &comm->recvbuf, &comm->rk,
-                      &comm->rt, &comm->rv, &comm->counts, &comm->cursor, &comm->rsend[0], &comm->rsend[1],
-                      &comm->rrecv[0], &comm->rrecv[1]})
+                      &comm->rt, &comm->rv, &comm->counts, &comm->cursor})
         b->release();
+    for (int q = 0; q < Comm::NS; ++q) {
+        comm->rsend[q].release();
+        comm->rrecv[q].release();
+        comm->rcnt[q].release();
+        for (hipEvent_t e : {comm->ev_rrecv[q], comm->ev_rout[q], comm->ev_read[q]})
+            if (e) (void)hipEventDestroy(e);
+        if (comm->hcnt[q]) (void)hipHostFree(comm->hcnt[q]);
+    }
+    for (unsigned long long *p : comm->hwm)
+        if (p) (void)hipHostFree(p);
     if (comm->cs) (void)hipStreamDestroy(comm->cs);
     if (comm->cs2) (void)hipStreamDestroy(comm->cs2);
-    for (hipEvent_t e : comm->ev_rrecv)
-        if (e) (void)hipEventDestroy(e);
     if (comm->ev_routed) (void)hipEventDestroy(comm->ev_routed);
     if (comm->ev_recv) (void)hipEventDestroy(comm->ev_recv);
     if (comm->h_counts) (void)hipHostFree(comm->h_counts);
@@ -210,23 +248,35 @@ gwo_status Handle::comm_exchange(const int64_t *k, const int64_t *t, const int64
 // the records of other GPUs to per-destination regions of the send buffer while it partitions its own, so a
 // batch is read once -- the route kernel of comm_exchange (24 B read + 24 B written per record, then K1 reads
 // the kept records again) is gone from the log path.  Regions hold mean + 6 sigma + 64 records; a skewed batch
-// that overflows one is re-routed with exact capacities by the route kernel (the counts are exact either way).
+// that overflows one is re-routed with exact capacities (comm_check_route, from K1's readback).
 gwo_status Handle::comm_route_args(int64_t n, LogRoute *rt, bool *on) {
     Comm &C = *comm;
     const int P = route_ranks(C);
     *on = P > 1;
     if (!*on) return GWO_OK;
-    GWO_TRY(ensure_buf(C.counts, (size_t)4 * P * 8 + 16));
+    const int slot = C.rslot;
+    GWO_TRY(ensure_buf(C.rcnt[slot], (size_t)4 * P * 8 + 16));
     if (!C.cursor.ptr) {
         GWO_TRY(ensure_buf(C.cursor, std::max(route_cursor_bytes(), (size_t)2 * LOG_RT_MAX * LOG_CUR_STRIDE * 8)));
         GWO_TRY(hipcheck(hipMemsetAsync(C.cursor.ptr, 0, C.cursor.bytes, stream), "route cursors"));
+    }
+    if (!C.hcnt[slot]) {
+        GWO_TRY(hipcheck(hipHostMalloc((void **)&C.hcnt[slot], (size_t)4 * P * 8 + 16,
+                                       hipHostMallocCoherent | hipHostMallocMapped), "count readback"));
+        GWO_TRY(hipcheck(hipHostGetDevicePointer((void **)&C.hcnt_dev[slot], C.hcnt[slot], 0), "count readback"));
     }
     const double mean = (double)n / P;
     C.rcap = ((uint64_t)(mean + 6.0 * std::sqrt(mean) + 64.0) + 1) & ~1ull;   // even: regions stay 8-B aligned
     C.wcap = 256 + (uint64_t)n / 1024;
     C.tbase = log_rt_tbase(C.agreed_wm);   // the same on every rank (min over ranks)
-    DevBuf &sb = C.rsend[C.rslot];
-    GWO_TRY(ensure_buf(sb, (size_t)P * (C.rcap * 20 + C.wcap * 24) + 24));
+    DevBuf &sb = C.rsend[slot];
+    // the slot's last exchange (NS batches ago) sent from this buffer: K1 overwrites it only behind that (device-side)
+    if (C.used_send[slot]) GWO_TRY(hipcheck(hipStreamWaitEvent(stream, C.ev_rrecv[slot], 0), "send slot"));
+    const size_t need = (size_t)P * (C.rcap * 20 + C.wcap * 24) + 24;
+    if (sb.bytes < need) {
+        if (C.used_send[slot]) GWO_TRY(hipcheck(hipEventSynchronize(C.ev_rrecv[slot]), "send slot"));   // (growth only)
+        GWO_TRY(ensure_buf(sb, need));
+    }
     *rt = LogRoute{};
     rt->mode = 1;
     rt->nranks = P;
@@ -236,30 +286,31 @@ gwo_status Handle::comm_route_args(int64_t n, LogRoute *rt, bool *on) {
     rt->wcap = C.wcap;
     rt->tbase = C.tbase;
     rt->cursor = (unsigned long long *)C.cursor.ptr;
-    rt->count = (unsigned long long *)C.counts.ptr;
-    if (n == 0) GWO_TRY(hipcheck(hipMemsetAsync(C.counts.ptr, 0, (size_t)4 * P * 8, stream), "counts"));
+    rt->count = (unsigned long long *)C.rcnt[slot].ptr;
+    if (n == 0) GWO_TRY(hipcheck(hipMemsetAsync(C.rcnt[slot].ptr, 0, (size_t)2 * P * 8, stream), "counts"));
     return GWO_OK;
 }
 
-// Right behind the routed K1 (main stream): the comm stream may start once K1 has finished.
+// Right behind the routed K1 (main stream): the slot's exchange may start once K1 has finished.
 gwo_status Handle::comm_mark_routed() {
-    return hipcheck(hipEventRecord(comm->ev_routed, stream), "event");
+    return hipcheck(hipEventRecord(comm->ev_rout[comm->rslot], stream), "event");
 }
 
-// After the routed K1 is queued: exchange the per-destination (narrow, wide) counts (RCCL on the count communicator
-// and its stream, so they never queue behind the previous batch's records on the wire), bring them to the host (the
-// batch's one host round trip for the exchange), re-route on a region overflow, and queue the records' exchange on
-// the comm stream -- it runs while the main stream finishes this batch's own records (and, deferred, the next
-// batch's routed K1).  Per peer: the narrow records as three arrays (keys, values, int32 timestamps: 20 B a record),
-// then the wide ones.
+// After the routed K1 of batch i is queued: its per-destination (narrow, wide) counts are exchanged on the count
+// communicator and stream right behind K1 (the counts never queue behind records on the wire) and published, with
+// the counts received, to host-mapped memory by a one-wave kernel (sequence word last).  Then batch i-1's record
+// exchange is posted: its counts arrived while batch i's K1 ran, so the host reads them without waiting.
 gwo_status Handle::comm_after_route(const int64_t *k, const int64_t *t, const int64_t *v, int64_t n) {
+    (void)k;
+    (void)t;
+    (void)v;
     Comm &C = *comm;
     const int P = route_ranks(C), me = C.rank;
     const bool virt = C.vranks > 1;
     const int slot = C.rslot;
-    unsigned long long *d_send = (unsigned long long *)C.counts.ptr, *d_recv = d_send + 2 * P;
+    unsigned long long *d_send = (unsigned long long *)C.rcnt[slot].ptr, *d_recv = d_send + 2 * P;
     if (n == 0) GWO_TRY(comm_mark_routed());   // (no K1 ran: the counts were zeroed on the main stream)
-    GWO_TRY(hipcheck(hipStreamWaitEvent(C.cs2, C.ev_routed, 0), "event wait"));
+    GWO_TRY(hipcheck(hipStreamWaitEvent(C.cs2, C.ev_rout[slot], 0), "event wait"));
     // one send/recv pair per peer; virtual ranks send to this rank itself, so what it routes to virtual GPU p
     // comes back "from p" through the same RCCL calls a real rank makes
     GWO_TRY(nccl_ok(this, ncclGroupStart(), "group"));
@@ -270,57 +321,100 @@ gwo_status Handle::comm_after_route(const int64_t *k, const int64_t *t, const in
         GWO_TRY(nccl_ok(this, ncclRecv(d_recv + 2 * p, 2, ncclUint64, peer, C.nc2, C.cs2), "recv count"));
     }
     GWO_TRY(nccl_ok(this, ncclGroupEnd(), "group end"));
-    unsigned long long *hs = C.h_counts, *hr = C.h_counts + 2 * P;
-    GWO_TRY(hipcheck(hipMemcpyAsync(hs, d_send, (size_t)4 * P * 8, hipMemcpyDeviceToHost, C.cs2), "counts"));
-    GWO_TRY(hipcheck(hipStreamSynchronize(C.cs2), "counts sync"));
+    launch_publish_words(d_send, 4 * P, C.hcnt_dev[slot], ++C.cnt_seq, C.cs2);
+    GWO_TRY(launch_ok("count readback"));
+    C.routed++;
+    if (C.post.active) GWO_TRY(comm_post());   // batch i-1
+    Comm::Post &Q = C.post;
+    Q.active = true;
+    Q.slot = slot;
+    Q.seq = C.cnt_seq;
+    Q.rcap = C.rcap;
+    Q.wcap = C.wcap;
+    Q.tbase = C.tbase;
+    Q.g = log_geom_now();
+    C.used_send[slot] = true;
+    C.rslot = (slot + 1) % Comm::NS;
+    return GWO_OK;
+}
+
+// K1's readback of a routed batch (its largest destination counts): a region that overflowed its capacity (skewed
+// keys) is routed again with exact capacities, inside the batch's gwo_submit -- the batch's columns are still the
+// caller's.  This GPU's records were partitioned by the first K1 (route-only mode skips them); the counts already
+// exchanged are exact either way.
+gwo_status Handle::comm_check_route(const int64_t *k, const int64_t *t, const int64_t *v, int64_t n, uint64_t maxn,
+                                    uint64_t maxw) {
+    Comm &C = *comm;
+    Comm::Post &Q = C.post;
+    if (!Q.active || (maxn <= Q.rcap && maxw <= Q.wcap)) return GWO_OK;
+    const int P = route_ranks(C);
+    const uint64_t rcap = (std::max<uint64_t>(Q.rcap, maxn) + 1) & ~1ull, wcap = std::max<uint64_t>(Q.wcap, maxw);
+    DevBuf &sbuf = C.rsend[Q.slot];
+    GWO_TRY(hipcheck(hipStreamSynchronize(stream), "re-route"));   // the send buffer may move (rare: skewed keys)
+    GWO_TRY(ensure_buf(sbuf, (size_t)P * (rcap * 20 + wcap * 24) + 24));
+    LogRoute rt{};
+    rt.mode = 3;   // route only: this GPU's records were partitioned by the first K1
+    rt.nranks = P;
+    rt.me = C.rank;
+    rt.send = (int64_t *)sbuf.ptr;
+    rt.rcap = rcap;
+    rt.wcap = wcap;
+    rt.tbase = Q.tbase;
+    rt.cursor = (unsigned long long *)C.cursor.ptr;
+    GWO_TRY(ensure_buf(C.counts, (size_t)6 * P * 8 + 16));
+    rt.count = (unsigned long long *)C.counts.ptr + 4 * P;   // (scratch: the counts are known)
+    GWO_TRY(log_route_only(k, t, v, n, rt));
+    GWO_TRY(hipcheck(hipEventRecord(C.ev_rout[Q.slot], stream), "event"));
+    Q.rcap = rcap;
+    Q.wcap = wcap;
+    return GWO_OK;
+}
+
+// Posts the record exchange of the routed batch waiting in C.post: its counts from the host-mapped block (already
+// there unless a flush forces the current batch's exchange), then per peer the narrow records as three arrays (keys,
+// values, int32 timestamps: 20 B a record) and the wide ones, on the record stream behind the batch's routed K1.
+gwo_status Handle::comm_post() {
+    Comm &C = *comm;
+    Comm::Post Q = C.post;
+    C.post.active = false;
+    const int P = route_ranks(C), me = C.rank;
+    const bool virt = C.vranks > 1;
+    constexpr int NSLOT = Comm::NS;
+    (void)NSLOT;
+    volatile const unsigned long long *seqw = C.hcnt[Q.slot] + 4 * P;
+    if (*seqw != Q.seq) C.count_waits++;   // the counts are not there yet: this post waits for them
+    GWO_TRY(spin_seq((const unsigned long long *)seqw, Q.seq, "count exchange"));
+    unsigned long long hs[2 * LOG_RT_MAX], hr[2 * LOG_RT_MAX];
+    memcpy(hs, C.hcnt[Q.slot], (size_t)2 * P * 8);
+    memcpy(hr, C.hcnt[Q.slot] + 2 * P, (size_t)2 * P * 8);
     hs[2 * me] = hs[2 * me + 1] = 0;   // (K1 never routes a record to its own GPU)
     hr[2 * me] = hr[2 * me + 1] = 0;
-    uint64_t rcap = C.rcap, wcap = C.wcap, mx = 0, mw = 0;
-    for (int p = 0; p < P; ++p) {
-        mx = std::max<uint64_t>(mx, hs[2 * p]);
-        mw = std::max<uint64_t>(mw, hs[2 * p + 1]);
-    }
-    DevBuf &sbuf = C.rsend[slot];
-    if (mx > rcap || mw > wcap) {   // skewed keys: a region overflowed -- route the batch again with exact regions
-        rcap = (std::max<uint64_t>(rcap, mx) + 1) & ~1ull;
-        wcap = std::max<uint64_t>(wcap, mw);
-        GWO_TRY(hipcheck(hipStreamSynchronize(stream), "re-route"));   // the send buffer may move
-        GWO_TRY(ensure_buf(sbuf, (size_t)P * (rcap * 20 + wcap * 24) + 24));
-        LogRoute rt{};
-        rt.mode = 3;   // route only: this GPU's records were partitioned by the first K1
-        rt.nranks = P;
-        rt.me = me;
-        rt.send = (int64_t *)sbuf.ptr;
-        rt.rcap = rcap;
-        rt.wcap = wcap;
-        rt.tbase = C.tbase;
-        rt.cursor = (unsigned long long *)C.cursor.ptr;
-        GWO_TRY(ensure_buf(C.counts, (size_t)6 * P * 8 + 16));
-        rt.count = (unsigned long long *)C.counts.ptr + 4 * P;   // (scratch: the counts are known)
-        GWO_TRY(log_route_only(k, t, v, n, rt));
-        GWO_TRY(comm_mark_routed());
-    }
-    // the records may leave once the (last) routed K1 has written them
-    GWO_TRY(hipcheck(hipStreamWaitEvent(C.cs, C.ev_routed, 0), "event wait"));
     std::vector<uint64_t> rn(P + 1, 0), rw(P + 1, 0);
     for (int p = 0; p < P; ++p) {
         rn[p + 1] = rn[p] + hr[2 * p];
         rw[p + 1] = rw[p] + hr[2 * p + 1];
     }
     const int64_t RN = (int64_t)rn[P], RW = (int64_t)rw[P];
-    // receive buffer: keys[RN], values[RN], int32 ts[RN] (padded to a word), then the wide records.  The slot's
-    // previous records (two batches ago) were read by a K1 the host has seen complete.
+    // receive buffer: keys[RN], values[RN], int32 ts[RN] (padded to a word), then the wide records
     const int64_t ts_words = (RN + 1) / 2;
     Comm::Recv R;
-    R.slot = slot;
+    R.slot = Q.slot;
     R.n = RN;
     R.w = RW;
     R.off_w = 2 * RN + ts_words;
-    R.tbase = C.tbase;
-    R.g = log_geom_now();
-    GWO_TRY(ensure_buf(C.rrecv[slot], (size_t)(R.off_w + 3 * RW) * 8 + 24));
-    int64_t *rb = (int64_t *)C.rrecv[slot].ptr;
-    int64_t *sb = (int64_t *)sbuf.ptr;
+    R.tbase = Q.tbase;
+    R.g = Q.g;
+    // the exchange follows the batch's routed K1 and the K1 that last read this receive slot (device-side order)
+    GWO_TRY(hipcheck(hipStreamWaitEvent(C.cs, C.ev_rout[Q.slot], 0), "event wait"));
+    if (C.used_read[Q.slot]) GWO_TRY(hipcheck(hipStreamWaitEvent(C.cs, C.ev_read[Q.slot], 0), "event wait"));
+    DevBuf &rbuf = C.rrecv[Q.slot];
+    const size_t need = (size_t)(R.off_w + 3 * RW) * 8 + 24;
+    if (rbuf.bytes < need) {
+        if (C.used_read[Q.slot]) GWO_TRY(hipcheck(hipEventSynchronize(C.ev_read[Q.slot]), "receive slot"));   // (growth)
+        GWO_TRY(ensure_buf(rbuf, need));
+    }
+    int64_t *rb = (int64_t *)rbuf.ptr;
+    int64_t *sb = (int64_t *)C.rsend[Q.slot].ptr;
     prof_begin(GWO_KERNEL_EXCHANGE, C.cs);
     GWO_TRY(nccl_ok(this, ncclGroupStart(), "group"));
     for (int p = 0; p < P; ++p) {
@@ -328,12 +422,12 @@ gwo_status Handle::comm_after_route(const int64_t *k, const int64_t *t, const in
         const int peer = virt ? me : p;
         const uint64_t sn = hs[2 * p], sw = hs[2 * p + 1], qn = hr[2 * p], qw = hr[2 * p + 1];
         if (sn) {
-            GWO_TRY(nccl_ok(this, ncclSend(log_rt_keys(sb, rcap, p), sn, ncclInt64, peer, C.nc, C.cs), "send keys"));
-            GWO_TRY(nccl_ok(this, ncclSend(log_rt_vals(sb, rcap, p), sn, ncclInt64, peer, C.nc, C.cs), "send values"));
-            GWO_TRY(nccl_ok(this, ncclSend(log_rt_ts32(sb, rcap, p), sn, ncclInt32, peer, C.nc, C.cs), "send ts"));
+            GWO_TRY(nccl_ok(this, ncclSend(log_rt_keys(sb, Q.rcap, p), sn, ncclInt64, peer, C.nc, C.cs), "send keys"));
+            GWO_TRY(nccl_ok(this, ncclSend(log_rt_vals(sb, Q.rcap, p), sn, ncclInt64, peer, C.nc, C.cs), "send values"));
+            GWO_TRY(nccl_ok(this, ncclSend(log_rt_ts32(sb, Q.rcap, p), sn, ncclInt32, peer, C.nc, C.cs), "send ts"));
         }
         if (sw)
-            GWO_TRY(nccl_ok(this, ncclSend(log_rt_wide(sb, rcap, P, wcap, p), 3 * sw, ncclInt64, peer, C.nc, C.cs),
+            GWO_TRY(nccl_ok(this, ncclSend(log_rt_wide(sb, Q.rcap, P, Q.wcap, p), 3 * sw, ncclInt64, peer, C.nc, C.cs),
                             "send wide"));
         if (qn) {
             GWO_TRY(nccl_ok(this, ncclRecv(rb + rn[p], qn, ncclInt64, peer, C.nc, C.cs), "recv keys"));
@@ -347,65 +441,65 @@ gwo_status Handle::comm_after_route(const int64_t *k, const int64_t *t, const in
     }
     GWO_TRY(nccl_ok(this, ncclGroupEnd(), "group end"));
     prof_end(GWO_KERNEL_EXCHANGE, RN + RW, C.cs);
-    GWO_TRY(hipcheck(hipEventRecord(C.ev_rrecv[slot], C.cs), "event"));
-    R.active = true;
-    C.last = R;
-    C.rslot ^= 1;
+    GWO_TRY(hipcheck(hipEventRecord(C.ev_rrecv[Q.slot], C.cs), "event"));
+    C.recvq.push_back(R);
     return GWO_OK;
 }
 
-Handle::Received Handle::comm_received() const {
-    const Comm::Recv &L = comm->last;
-    Received R;
-    const int64_t *rb = (const int64_t *)comm->rrecv[L.slot].ptr;
-    R.n = L.n;
-    R.key = rb;
-    R.val = rb + L.n;
-    R.ts32 = (const int32_t *)(rb + 2 * L.n);
-    R.tbase = L.tbase;
-    R.wide = rb + L.off_w;
-    R.wide_n = L.w;
-    return R;
-}
-
-// The main stream waits for the exchange's receives (comm stream) before reading the received records.
+// The main stream waits for the non-log exchange's receives (comm_exchange, comm stream) before reading them.
 gwo_status Handle::comm_wait_received() {
     if (route_ranks(*comm) == 1) return GWO_OK;
-    if (comm->last.active) return hipcheck(hipStreamWaitEvent(stream, comm->ev_rrecv[comm->last.slot], 0), "exchange wait");
     return hipcheck(hipStreamWaitEvent(stream, comm->ev_recv, 0), "exchange wait");
 }
 
-// Deferred receives (tumbling log layout, allowedLateness 0, no side output): a routed batch's received records are
-// inserted at the next routed batch -- after that batch's K1 and exchange are queued, so batch i's records on the wire
-// overlap batch i+1's K1 and pass 2 -- or at any earlier point that observes state or fires a window they may fall
-// into (log_flush).  They are classified at their own batch's watermark (the geometry kept with them), exactly as if
-// inserted at once: a fire that could take them flushes them first (log_pending_may_fire).
+// Deferred receives (tumbling log layout, allowedLateness 0, no side output): a routed batch's exchange is posted at
+// the next routed batch and its received records are inserted at the one after -- or at any earlier point that
+// observes state or fires a window they may fall into (log_flush).  They are classified at their own batch's
+// watermark (the geometry kept with them), exactly as if inserted at once: a fire that could take them flushes them
+// first (log_pending_may_fire).
 bool Handle::comm_defers() const {
     return comm && logst && !slog && cfg.allowed_lateness == 0 && !side_enabled() && route_ranks(*comm) > 1 &&
            comm->defer;
 }
 
-gwo_status Handle::comm_flush_received() {
-    if (!comm || !comm->pend.active) return GWO_OK;
-    const Comm::Recv R = comm->pend;
-    comm->pend.active = false;
-    GWO_TRY(hipcheck(hipStreamWaitEvent(stream, comm->ev_rrecv[R.slot], 0), "exchange wait"));
-    const int64_t *rb = (const int64_t *)comm->rrecv[R.slot].ptr;
-    if (R.n) GWO_TRY(insert_log(rb, (const int64_t *)(rb + 2 * R.n), rb + R.n, R.n, 1, nullptr, true, R.tbase, &R.g));
-    if (R.w) GWO_TRY(insert_log(rb + R.off_w, rb + R.off_w + 1, rb + R.off_w + 2, R.w, 3, nullptr, false, 0, &R.g));
+// Inserts received records: every posted exchange but the `keep` newest (whose records may still be on the wire).
+gwo_status Handle::comm_insert_received(size_t keep) {
+    Comm &C = *comm;
+    while (C.recvq.size() > keep) {
+        const Comm::Recv R = C.recvq.front();
+        C.recvq.pop_front();
+        GWO_TRY(hipcheck(hipStreamWaitEvent(stream, C.ev_rrecv[R.slot], 0), "exchange wait"));
+        const int64_t *rb = (const int64_t *)C.rrecv[R.slot].ptr;
+        if (R.n) GWO_TRY(insert_log(rb, (const int64_t *)(rb + 2 * R.n), rb + R.n, R.n, 1, nullptr, true, R.tbase, &R.g));
+        if (R.w) GWO_TRY(insert_log(rb + R.off_w, rb + R.off_w + 1, rb + R.off_w + 2, R.w, 3, nullptr, false, 0, &R.g));
+        GWO_TRY(hipcheck(hipEventRecord(C.ev_read[R.slot], stream), "event"));
+        C.used_read[R.slot] = true;
+    }
     return GWO_OK;
 }
 
-// Keeps the last routed exchange's receives for the next routed batch (comm_defers).
-void Handle::comm_defer_received() {
-    comm->pend = comm->last;
-    comm->last.active = false;
+// Every routed batch's records inserted: the pending exchange posted (this waits for its counts), all receives read.
+gwo_status Handle::comm_flush_received() {
+    if (!comm) return GWO_OK;
+    if (comm->post.active) GWO_TRY(comm_post());
+    return comm_insert_received(0);
 }
 
+// The oldest watermark any routed batch not yet inserted was classified at.
 bool Handle::comm_pending_wm(int64_t *wm) const {
-    if (!comm || !comm->pend.active) return false;
-    *wm = comm->pend.g.wm;
-    return true;
+    if (!comm) return false;
+    bool any = false;
+    int64_t m = 0;
+    if (comm->post.active) {
+        m = comm->post.g.wm;
+        any = true;
+    }
+    for (const Comm::Recv &R : comm->recvq) {
+        m = any ? std::min(m, R.g.wm) : R.g.wm;
+        any = true;
+    }
+    if (any) *wm = m;
+    return any;
 }
 
 // AoS {key, ts, value} records -> the handle's column scratch (table, sliding and session layouts)
@@ -440,12 +534,57 @@ static gwo_status allreduce_min(Handle *h, int64_t v, int64_t *out) {
     return GWO_OK;
 }
 
+// Asynchronous agreement (gwo_comm_set_async_watermark): this call's all-reduce is queued with its result published to
+// host-mapped memory, and the min the previous call queued -- long complete -- is applied.  Every rank applies the
+// same agreed values, one call later than the synchronous mode (as if one channel's watermark arrived one step
+// later: a valid StatusWatermarkValve history, monotone because each rank's input is).  The end of input
+// (Long.MAX_VALUE) and a single real rank (virtual ranks: the min is its own) agree synchronously.
+static gwo_status allreduce_min_async(Handle *h, int64_t v, int64_t *applied) {
+    Comm &C = *h->comm;
+    int64_t *d = (int64_t *)C.counts.ptr + 6 * std::max(C.nranks, C.vranks) + 2;   // (past the synchronous word)
+    const int q = (int)(C.wm_seq & 1);
+    if (!C.hwm[q]) {
+        // [0] the published min, [1] its sequence word, [2] this call's input (the copy reads it after the call returns,
+        // so each block keeps its own staging word until the call two later)
+        GWO_TRY(h->hipcheck(hipHostMalloc((void **)&C.hwm[q], 32, hipHostMallocCoherent | hipHostMallocMapped), "wm"));
+        GWO_TRY(h->hipcheck(hipHostGetDevicePointer((void **)&C.hwm_dev[q], C.hwm[q], 0), "wm"));
+    }
+    if (C.wm_pending) {   // the previous call's min
+        volatile const unsigned long long *seqw = C.hwm[q ^ 1] + 1;
+        if (*seqw != C.wm_seq) C.wm_waits++;
+        GWO_TRY(h->spin_seq((const unsigned long long *)seqw, C.wm_seq, "watermark agreement"));
+        *applied = (int64_t)C.hwm[q ^ 1][0];
+    } else {
+        *applied = C.agreed_wm;
+    }
+    C.hwm[q][2] = (unsigned long long)v;
+    GWO_TRY(h->hipcheck(hipMemcpyAsync(d, C.hwm[q] + 2, 8, hipMemcpyHostToDevice, C.cs2), "wm"));
+    GWO_TRY(nccl_ok(h, ncclAllReduce(d, d, 1, ncclInt64, ncclMin, C.nc2, C.cs2), "allreduce wm"));
+    launch_publish_words((const unsigned long long *)d, 1, C.hwm_dev[q], ++C.wm_seq, C.cs2);
+    GWO_TRY(h->launch_ok("wm readback"));
+    C.wm_pending = true;
+    return GWO_OK;
+}
+
 gwo_status Handle::comm_min_watermark(int64_t wm_in, int64_t *out) {
     Comm &C = *comm;
     if (C.nranks == 1 && C.vranks <= 1) {   // nothing to agree on
         *out = C.agreed_wm = wm_in;
         return GWO_OK;
     }
+    if (C.async_wm && wm_in != (int64_t)0x7fffffffffffffffLL) {
+        int64_t applied = C.agreed_wm;
+        GWO_TRY(allreduce_min_async(this, wm_in, &applied));
+        if (C.nranks == 1) applied = wm_in;   // virtual ranks: the collective ran, the min over one rank is its input
+        *out = C.agreed_wm = std::max(C.agreed_wm, applied);
+        return GWO_OK;
+    }
+    if (C.wm_pending) {   // a queued asynchronous agreement completes first (RCCL orders the count communicator)
+        const int q = (int)(C.wm_seq & 1) ^ 1;
+        GWO_TRY(spin_seq(C.hwm[q] + 1, C.wm_seq, "watermark agreement"));
+        C.wm_pending = false;
+    }
+    C.wm_waits++;
     GWO_TRY(allreduce_min(this, wm_in, out));
     C.agreed_wm = *out;
     return GWO_OK;
@@ -502,9 +641,7 @@ extern "C" gwo_status gwo_comm_init(gwo_handle *hh, const uint8_t *id, int32_t n
     if (hipStreamCreateWithFlags(&C->cs, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithPriority(&C->cs2, hipStreamNonBlocking, prio_greatest) != hipSuccess ||
         hipEventCreateWithFlags(&C->ev_routed, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&C->ev_recv, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&C->ev_rrecv[0], hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&C->ev_rrecv[1], hipEventDisableTiming) != hipSuccess) {
+        hipEventCreateWithFlags(&C->ev_recv, hipEventDisableTiming) != hipSuccess || !comm_events(C)) {
         h->comm = C;   // comm_free releases what was created
         h->comm_free();
         return GWO_ERR_HIP;
@@ -521,7 +658,8 @@ extern "C" gwo_status gwo_comm_init(gwo_handle *hh, const uint8_t *id, int32_t n
     }
     // the ranks' watermarks may differ (subtasks restored from different checkpoints): agree on their min now, so
     // every rank's first routed batch encodes and decodes wire timestamps against the same base
-    gwo_status st = h->ensure_buf(C->counts, (size_t)6 * cranks * 8 + 16);   // (never reallocated later)
+    gwo_status st = h->ensure_buf(C->counts, (size_t)6 * cranks * 8 + 32);   // (never reallocated later)
+    if (const char *e = getenv("GWO_COMM_ASYNC_WM")) C->async_wm = atoi(e) != 0;
     if (st == GWO_OK) st = allreduce_min(h, h->wm, &C->agreed_wm);
     return st;
 }
@@ -564,4 +702,23 @@ extern "C" gwo_status gwo_partition_by_operator(const int64_t *key, const int64_
         if (p) (void)hipFree(p);
     (void)hipStreamDestroy(s);
     return st;
+}
+
+extern "C" gwo_status gwo_comm_set_async_watermark(gwo_handle *hh, int32_t enabled) {
+    Handle *h = reinterpret_cast<Handle *>(hh);
+    if (!h) return GWO_ERR_INVALID_ARGUMENT;
+    if (h->poisoned) return h->poison_status;
+    if (!h->comm) return h->fail(GWO_ERR_STATE, "no communicator: gwo_comm_init first");
+    h->comm->async_wm = enabled != 0;
+    return GWO_OK;
+}
+
+extern "C" gwo_status gwo_comm_stats(gwo_handle *hh, int64_t *routed_batches, int64_t *count_waits, int64_t *wm_waits) {
+    Handle *h = reinterpret_cast<Handle *>(hh);
+    if (!h || !routed_batches || !count_waits || !wm_waits) return GWO_ERR_INVALID_ARGUMENT;
+    if (!h->comm) return h->fail(GWO_ERR_STATE, "no communicator");
+    *routed_batches = h->comm->routed;
+    *count_waits = h->comm->count_waits;
+    *wm_waits = h->comm->wm_waits;
+    return GWO_OK;
 }

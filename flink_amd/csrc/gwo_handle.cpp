@@ -252,17 +252,9 @@ gwo_status Handle::submit(const int64_t *key, const int64_t *ts, const void *val
         if (!routed) return n ? insert_log(dk, dt, dv, n) : GWO_OK;   // one rank: nothing leaves this GPU
         if (n > 0) GWO_TRY(insert_log(dk, dt, dv, n, 1, &rt));
         else GWO_TRY(comm_after_route(dk, dt, dv, 0));
-        if (comm_defers()) {
-            // this batch's records are on the wire now; the previous batch's arrived while its K1 ran
-            GWO_TRY(comm_flush_received());
-            comm_defer_received();
-            return GWO_OK;
-        }
-        GWO_TRY(comm_flush_received());   // (deferral switched off by a configuration change: none pending)
-        const Received R = comm_received();
-        GWO_TRY(comm_wait_received());
-        if (R.n) GWO_TRY(insert_log(R.key, (const int64_t *)R.ts32, R.val, R.n, 1, nullptr, true, R.tbase));
-        return R.wide_n ? insert_log(R.wide, R.wide + 1, R.wide + 2, R.wide_n, 3) : GWO_OK;
+        // deferred: the previous batch's exchange was posted behind this batch's K1 (its counts had arrived), the one
+        // before it has landed and is inserted now; otherwise this batch's exchange completes inside its submit
+        return comm_defers() ? comm_insert_received(1) : comm_flush_received();
     }
     if (comm) {
         const int64_t *aos = nullptr, *loc = nullptr;

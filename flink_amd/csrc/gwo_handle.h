@@ -397,20 +397,15 @@ struct Handle {
     gwo_status log_route_only(const int64_t *k, const int64_t *t, const int64_t *v, int64_t n, const LogRoute &rt);
     gwo_status comm_mark_routed();
     gwo_status comm_after_route(const int64_t *k, const int64_t *t, const int64_t *v, int64_t n);
-    // deferred receives of the routed log path: inserted at the next routed batch or at log_flush
+    // K1's readback of a routed batch: re-route with exact capacities when a destination region overflowed
+    gwo_status comm_check_route(const int64_t *k, const int64_t *t, const int64_t *v, int64_t n, uint64_t maxn,
+                                uint64_t maxw);
+    gwo_status comm_post();   // posts the record exchange of the routed batch whose counts were published last
+    // deferred receives of the routed log path: inserted two routed batches later or at log_flush
     bool comm_defers() const;
-    void comm_defer_received();
+    gwo_status comm_insert_received(size_t keep);
     gwo_status comm_flush_received();
-    bool comm_pending_wm(int64_t *wm) const;   // the watermark the deferred records are classified at
-    // records received by the last exchange: 20-B ones as columns (keys, values, int32 ts - tbase) and 24-B ones
-    struct Received {
-        const int64_t *key = nullptr, *val = nullptr;
-        const int32_t *ts32 = nullptr;
-        int64_t n = 0, tbase = 0;
-        const int64_t *wide = nullptr;   // {key, ts, value} records
-        int64_t wide_n = 0;
-    };
-    Received comm_received() const;
+    bool comm_pending_wm(int64_t *wm) const;   // the oldest watermark a not yet inserted routed batch is classified at
 
     void prof_begin(int k, hipStream_t s = nullptr);
     void prof_end(int k, int64_t items, hipStream_t s = nullptr);

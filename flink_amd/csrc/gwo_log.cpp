@@ -607,6 +607,9 @@ gwo_status Handle::log_resolve_batch(LogJob &J, bool &refire) {
             } else {
                 late_dropped += hs.late;
             }
+            // routed K1: a destination region that overflowed is re-routed now (the columns are still the caller's)
+            if (J.rt.mode == 2 && comm)
+                GWO_TRY(comm_check_route(J.k, J.t, J.v, J.n, rbp[LOG_RB_RMAX], rbp[LOG_RB_RWMAX]));
             if (hs.accepted == 0) {
                 if (J.spec)
                     for (int w = 0; w < J.nunits; ++w) log_uncarve(J, w, 0);

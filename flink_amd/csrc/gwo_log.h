@@ -93,7 +93,9 @@ static constexpr int LOG_RB_GO = LOG_RB_CHUNKS + 1;
 static constexpr int LOG_RB_MAXREG = LOG_RB_GO + 1;      // largest region count (> cap: K1 dropped records)
 static constexpr int LOG_RB_NEXT = LOG_RB_MAXREG + 1;    // the first window after the launch's range holding accepted
                                                          // records (Long.MAX_VALUE: none) -- the next K1 range starts there
-static constexpr int LOG_RB_T0 = LOG_RB_NEXT + 1;        // device wall clock when workgroup 0 started (profiling)
+static constexpr int LOG_RB_RMAX = LOG_RB_NEXT + 1;      // routed K1: the largest narrow / wide destination count (above
+static constexpr int LOG_RB_RWMAX = LOG_RB_RMAX + 1;     //   the region capacity: records were dropped, the host re-routes)
+static constexpr int LOG_RB_T0 = LOG_RB_RWMAX + 1;       // device wall clock when workgroup 0 started (profiling)
 static constexpr int LOG_RB_T1 = LOG_RB_T0 + 1;          // device wall clock when the tail finished its work
 static constexpr int LOG_RB_SEQ = LOG_RB_T1 + 1;         // written last: the launch's sequence number
 static constexpr int LOG_RB_WORDS = LOG_RB_SEQ + 1;

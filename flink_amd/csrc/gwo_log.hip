@@ -209,10 +209,17 @@ __device__ __forceinline__ void k1_plan_tail(unsigned long long *cursor, BatchSt
             cq[q][x] = t < LOG_ND && q < a.nunits
                            ? atomicExch(&cursor[((size_t)(q * LOG_ND + t) * LOG_XG + x) * LOG_CUR_STRIDE], 0ull)
                            : 0ull;
+    __shared__ unsigned long long s_rmax[2];
+    if (t < 2) s_rmax[t] = 0;
+    __syncthreads();
     if (rt.mode == 1)   // routed records per destination; the cursors start the next routed K1 at zero
         for (int p = t; p < rt.nranks; p += LOG_K1_THREADS) {
-            rt.count[2 * p] = atomicExch(&rt.cursor[(size_t)p * LOG_CUR_STRIDE], 0ull);
-            rt.count[2 * p + 1] = atomicExch(&rt.cursor[(size_t)(LOG_RT_MAX + p) * LOG_CUR_STRIDE], 0ull);
+            const unsigned long long cn = atomicExch(&rt.cursor[(size_t)p * LOG_CUR_STRIDE], 0ull);
+            const unsigned long long cw = atomicExch(&rt.cursor[(size_t)(LOG_RT_MAX + p) * LOG_CUR_STRIDE], 0ull);
+            rt.count[2 * p] = cn;
+            rt.count[2 * p + 1] = cw;
+            atomicMax(&s_rmax[0], cn);   // the largest counts go to the readback: a region overflow is seen with the plan
+            atomicMax(&s_rmax[1], cw);
         }
     __shared__ unsigned long long s_k1[K1_SW];
     if (t < SW) {   // read-and-reset through the same device-scope atomics the workgroups used
@@ -303,6 +310,8 @@ __device__ __forceinline__ void k1_plan_tail(unsigned long long *cursor, BatchSt
         *a.go = go ? 1u : 0u;
         rb_put(&a.rb[LOG_RB_GO], go ? 1ull : 0ull);
         rb_put(&a.rb[LOG_RB_MAXREG], s_maxreg);
+        rb_put(&a.rb[LOG_RB_RMAX], s_rmax[0]);
+        rb_put(&a.rb[LOG_RB_RWMAX], s_rmax[1]);
     }
     if (t == 0 && a.t0) {
         rb_put(&a.rb[LOG_RB_T0], atomicAdd(a.t0, 0ull));

@@ -1358,6 +1358,30 @@ gwo_status gwo_sync(gwo_handle *hh) {
     return h->hipcheck(hipStreamSynchronize(h->stream), "sync");
 }
 
+gwo_status gwo_host_register(void *ptr, int64_t bytes) {
+    if (!ptr || bytes <= 0) return GWO_ERR_INVALID_ARGUMENT;
+    const hipError_t e = hipHostRegister(ptr, (size_t)bytes, hipHostRegisterPortable);
+    if (e == hipErrorHostMemoryAlreadyRegistered) {
+        (void)hipGetLastError();
+        return GWO_OK;
+    }
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        return GWO_ERR_HIP;
+    }
+    return GWO_OK;
+}
+
+gwo_status gwo_host_unregister(void *ptr) {
+    if (!ptr) return GWO_ERR_INVALID_ARGUMENT;
+    const hipError_t e = hipHostUnregister(ptr);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        return e == hipErrorHostMemoryNotRegistered ? GWO_ERR_INVALID_ARGUMENT : GWO_ERR_HIP;
+    }
+    return GWO_OK;
+}
+
 gwo_status gwo_get_stream(gwo_handle *hh, void **stream) {
     Handle *h = reinterpret_cast<Handle *>(hh);
     if (!h || !stream) return GWO_ERR_INVALID_ARGUMENT;

@@ -142,8 +142,15 @@ void gwo_config_init(gwo_config *cfg);
 gwo_status gwo_create(const gwo_config *cfg, gwo_handle **out);
 gwo_status gwo_destroy(gwo_handle *h);
 
-/* processElement for n records in arrival order; value may be NULL when every aggregate is COUNT. */
+/* processElement for n records in arrival order; value may be NULL when every aggregate is COUNT.  Columns are device
+ * pointers (read in place; the allocation must outlive the handle: its address range is cached) or host pointers
+ * (copied to HBM on the handle's stream -- pinned memory, see gwo_host_register, is copied by DMA directly). */
 gwo_status gwo_submit(gwo_handle *h, const int64_t *key, const int64_t *ts, const void *value, int64_t n);
+/* Pins (page-locks) host memory for the GPUs (hipHostRegister), so gwo_submit / gwo_drain move it by DMA without a
+ * pageable staging bounce: the Java operator registers its direct ByteBuffer columns once in open() (the mailbox
+ * batching into pinned columnar buffers) and unregisters them in close().  Process-wide, not per handle. */
+gwo_status gwo_host_register(void *ptr, int64_t bytes);
+gwo_status gwo_host_unregister(void *ptr);
 /* processWatermark: fire every window whose timers are <= wm, then adopt wm as current watermark. */
 gwo_status gwo_advance_watermark(gwo_handle *h, int64_t wm);
 /* processWatermark(Long.MAX_VALUE) -- a bounded source's end (StreamSource.java:122). */
@@ -312,6 +319,15 @@ gwo_status gwo_comm_unique_id(uint8_t id[GWO_COMM_ID_BYTES]);
  * gwo_advance_watermark are collective: gwo_submit routes records to their owner GPU
  * (partition + ncclSend/ncclRecv all-to-all); the watermark becomes the min over ranks. */
 gwo_status gwo_comm_init(gwo_handle *h, const uint8_t id[GWO_COMM_ID_BYTES], int32_t nranks, int32_t rank);
+/* Watermark agreement without a host wait: each gwo_advance_watermark queues its all-reduce (min over ranks) and applies
+ * the min the previous call queued -- every rank the same values, one call later than the default synchronous
+ * agreement (a valid StatusWatermarkValve history: one channel's watermark arriving one step later).  The end of input
+ * always agrees synchronously.  Off by default (outputs then match a single operator fed the same watermarks). */
+gwo_status gwo_comm_set_async_watermark(gwo_handle *h, int32_t enabled);
+/* Host round trips of the routed exchange (log layout): routed batches, waits for a batch's exchanged counts (a routed
+ * batch's record exchange is posted at the next routed batch, when its counts have arrived: only a flush -- a fire
+ * its records may fall into, a snapshot, gwo_sync -- waits), and synchronous watermark agreements. */
+gwo_status gwo_comm_stats(gwo_handle *h, int64_t *routed_batches, int64_t *count_waits, int64_t *wm_waits);
 
 /* Batch form of KeyGroupStreamPartitioner.selectChannel (KeyGroupStreamPartitioner.java:51-58): groups n
  * records by destination computeOperatorIndexForKeyGroup(assignToKeyGroup(key)) into per-destination runs

@@ -7,8 +7,8 @@
  * rows are emitted before the watermark is forwarded), HeapSnapshotStrategy.java:97-222 (keyed state written
  * per key group) and StateInitializationContext.getRawKeyedStateInputs (restore of the subtask's key groups).
  *
- * Records are batched into direct (pinned-able) columnar buffers; every watermark flushes the batch, advances
- * the GPU watermark, drains the fired rows and forwards the watermark.  Keys are Long, Integer or String
+ * Records are batched into direct columnar buffers pinned once in open() (gwo_host_register); every watermark
+ * flushes the batch, advances the GPU watermark, drains the fired rows and forwards the watermark.  Keys are Long, Integer or String
  * (String keys are interned into the handle's device dictionary, gwo.h gwo_submit_utf16).  Checkpoints write the
  * handle's rows (key, window, raw accumulator words, fire-timer flag) into the raw keyed state stream, one
  * section per key group, so rescaling hands every key group to its new owner.
@@ -57,6 +57,7 @@ public class GpuWindowOperator<IN, K> extends AbstractStreamOperator<GpuWindowRe
     // drain buffers, allocated once at open() (batch rows; the side output's grow on demand)
     private transient ByteBuffer outKeys, outStarts, outEnds, sideKeys, sideTs, sideValues;
     private transient ByteBuffer[] outResults;
+    private transient List<ByteBuffer> pinned;   // direct buffers registered with gwo_host_register in open()
     private transient long[] idScratch;
     private transient List<String> pendingStrings;
     private transient int n;
@@ -109,6 +110,21 @@ public class GpuWindowOperator<IN, K> extends AbstractStreamOperator<GpuWindowRe
         for (int a = 0; a < outResults.length; a++) {
             outResults[a] = direct(batch * 8L);
         }
+        // the mailbox batches into pinned columns: registered once, so every gwo_submit (and every drain) moves them
+        // by DMA (gwo.h gwo_host_register)
+        pinned = new ArrayList<>();
+        pin(keys);
+        pin(timestamps);
+        pin(values);
+        if (offsets != null) {
+            pin(offsets);
+        }
+        pin(outKeys);
+        pin(outStarts);
+        pin(outEnds);
+        for (ByteBuffer r : outResults) {
+            pin(r);
+        }
         idScratch = new long[batch];
         numLateRecordsDropped = metrics.counter("numLateRecordsDropped");
         resultDtypes = new int[spec.aggs.length];
@@ -117,9 +133,20 @@ public class GpuWindowOperator<IN, K> extends AbstractStreamOperator<GpuWindowRe
         }
     }
 
+    private void pin(ByteBuffer b) {
+        GwoNative.hostRegister(b);
+        pinned.add(b);
+    }
+
     @Override
     public void close() throws Exception {
         super.close();
+        if (pinned != null) {
+            for (ByteBuffer b : pinned) {
+                GwoNative.hostUnregister(b);
+            }
+            pinned = null;
+        }
         if (handle != 0) {
             GwoNative.destroy(handle);
             handle = 0;
@@ -174,7 +201,12 @@ public class GpuWindowOperator<IN, K> extends AbstractStreamOperator<GpuWindowRe
                 units += s.length();
             }
             if (chars == null || chars.capacity() < units * 2) {
+                if (chars != null) {
+                    GwoNative.hostUnregister(chars);
+                    pinned.remove(chars);
+                }
                 chars = direct(Math.max(units * 2L, 1L << 16));
+                pin(chars);
             }
             int at = 0;
             offsets.putLong(0, 0);
@@ -228,6 +260,9 @@ public class GpuWindowOperator<IN, K> extends AbstractStreamOperator<GpuWindowRe
                 sideKeys = direct(batch * 8L);
                 sideTs = direct(batch * 8L);
                 sideValues = direct(batch * 8L);
+                pin(sideKeys);
+                pin(sideTs);
+                pin(sideValues);
             }
             final int got = (int) GwoNative.drainSideOutput(handle, sideKeys, sideTs, sideValues, cap);
             final String[] names = spec.keyKind == GwoNative.KEY_STRING ? keyStrings(sideKeys, got) : null;

@@ -50,6 +50,12 @@ final class GwoNative {
 
     static native void destroy(long handle);
 
+    /** gwo_host_register: pins a direct buffer's memory (hipHostRegister) so its batches move to the GPU by DMA. */
+    static native void hostRegister(ByteBuffer buffer);
+
+    /** gwo_host_unregister: releases the pinning of hostRegister. */
+    static native void hostUnregister(ByteBuffer buffer);
+
     /** gwo_submit: n records; keys, timestamps, values as int64 (values: int64 or float64 bits). */
     static native void submit(long handle, ByteBuffer keys, ByteBuffer timestamps, ByteBuffer values, int n);
 

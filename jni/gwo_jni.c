@@ -105,6 +105,22 @@ JNIEXPORT void JNICALL JFN(destroy)(JNIEnv *env, jclass c, jlong h) {
     fail(env, NULL, gwo_destroy(H(h)));
 }
 
+/* gwo_host_register / gwo_host_unregister of a direct ByteBuffer's memory (the operator's columns, pinned once in
+ * open(): its batches then reach the GPU by DMA). */
+JNIEXPORT void JNICALL JFN(hostRegister)(JNIEnv *env, jclass c, jobject buf) {
+    (void)c;
+    void *p = sized(env, buf, 1, "direct buffer required");
+    if ((*env)->ExceptionCheck(env)) return;
+    fail(env, NULL, gwo_host_register(p, (int64_t)(*env)->GetDirectBufferCapacity(env, buf)));
+}
+
+JNIEXPORT void JNICALL JFN(hostUnregister)(JNIEnv *env, jclass c, jobject buf) {
+    (void)c;
+    void *p = sized(env, buf, 1, "direct buffer required");
+    if ((*env)->ExceptionCheck(env)) return;
+    fail(env, NULL, gwo_host_unregister(p));
+}
+
 JNIEXPORT void JNICALL JFN(submit)(JNIEnv *env, jclass c, jlong h, jobject k, jobject t, jobject v, jint n) {
     (void)c;
     if (n < 0) { throw_arg(env, "negative record count"); return; }

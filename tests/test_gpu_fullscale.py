@@ -3,7 +3,8 @@
 * One full C4 window (BASELINE.json configs[3]: 100M keys, maxParallelism 32768, tumbling 10 s
   sum/min/max over int64, 16.7M records per 1-s watermark step) through the LOG layout, compared row for
   row with the C restatement of WindowOperator (oracle/window_oracle.c, 16 threads sharded by key group;
-  pinned against the Python oracle in tests/test_oracle_c.py).
+  pinned against the Python oracle in tests/test_oracle_c.py); and the whole 60-s C4 stream (six windows
+  retire) against the C twin's output hash.
 * Key-group sharding on one GPU: N = 2, 4, 8 handles, each owning
   KeyGroupRangeAssignment.computeKeyGroupRangeForOperatorIndex(32768, N, i)
   (flink-runtime/.../state/KeyGroupRangeAssignment.java:88-101), fed by gwo_partition_by_operator (the
@@ -132,6 +133,66 @@ def test_c4_full_window_log_layout_vs_c_twin(F):
     assert np.count_nonzero(np.bincount(kg, minlength=maxp)) == maxp
     for c, name in enumerate(["key", "start", "end", "sum", "min", "max"]):
         assert torch.equal(got[c], want[c]), f"column {name} differs"
+
+
+def _gpu_row_checksum(cols):
+    """cbaseline.row_checksum on the device: wrapping sum over rows of an FNV-1a-style hash of the row's words."""
+    import torch
+    h = torch.full_like(cols[0], 1469598103934665603)
+    for c in cols:
+        h = (h ^ c) * 1099511628211   # int64 arithmetic wraps like the C twin's uint64
+    return int(h.sum().item()) % (1 << 64)
+
+
+def test_c4_whole_stream_six_windows_vs_c_twin(F):
+    """The whole C4 stream: 1e9 records over 60 s of event time in 60 watermark steps, so six 10-s windows fill,
+    fire and retire through the LOG layout (the chunk pool recycled five times) plus the end-of-input fire.  Every
+    step's rows (key, start, end, sum, min, max, count) are drained and hashed on the device; the sum of the row
+    hashes over the stream and the late count equal the C twin's (window_oracle.c emit(): the same hash).  The
+    row-for-row comparison of one full window is test_c4_full_window_log_layout_vs_c_twin."""
+    import torch
+    from flink_amd import _native as N
+    R, span, window, lag, maxp, nkeys = 1_000_000_000, 60_000, 10_000, 1_000, 32768, 100_000_000
+    per = R * 1000 // span
+    steps = span // 1000
+    n = per * steps
+    key, ts, val = _gen(N, 42, 0, R, nkeys, span, n)
+    bounds = [(i * per, (i + 1) * per) for i in range(steps)]
+    wms = _watermarks(ts, bounds, lag)
+    rec_per_window = R * window // span
+    exp_keys = int(nkeys * (1.0 - np.exp(-rec_per_window / nkeys)))
+    agg = F.MultiAggregate(F.SumAggregate(), F.MinAggregate(), F.MaxAggregate(), F.CountAggregate())
+    op = F.GpuWindowOperator(F.TumblingEventTimeWindows.of(window), agg, max_parallelism=maxp,
+                             expected_keys=exp_keys)
+    lib, h = N.lib(), op.handle
+    cs, rows, fires = 0, 0, 0
+    for (s, e), wm in zip(bounds, wms):
+        N.check(lib.gwo_submit(h, C.c_void_p(key.data_ptr() + 8 * s), C.c_void_p(ts.data_ptr() + 8 * s),
+                               C.c_void_p(val.data_ptr() + 8 * s), e - s), h, "submit")
+        N.check(lib.gwo_advance_watermark(h, wm), h, "watermark")
+        cols = _drain_device(N, h, 4)
+        if cols[0].numel():
+            fires += 1
+            rows += cols[0].numel()
+            cs = (cs + _gpu_row_checksum(cols)) % (1 << 64)
+        del cols
+    N.check(lib.gwo_end_input(h), h)
+    cols = _drain_device(N, h, 4)
+    rows += cols[0].numel()
+    cs = (cs + _gpu_row_checksum(cols)) % (1 << 64)
+    del cols
+    late = C.c_int64()
+    N.check(lib.gwo_late_dropped(h, C.byref(late)), h)
+    op.close()
+    kh, th, vh = key.cpu().numpy(), ts.cpu().numpy(), val.cpu().numpy()
+    del key, ts, val
+    torch.cuda.empty_cache()
+    batches = [(e, w) for (_, e), w in zip(bounds, wms)] + [(n, LONG_MAX)]
+    _, want_cs, want_late = cbaseline.run_tumbling(kh, th, vh, batches, window, threads=16, max_par=maxp, rows=False)
+    assert fires == 5                      # windows [0, 10 s) .. [40 s, 50 s) fire at watermark steps; the sixth at end
+    assert rows > 5 * 80_000_000
+    assert late.value == want_late
+    assert cs == want_cs
 
 
 @pytest.mark.parametrize("layout", ["log", "table"])

@@ -141,7 +141,7 @@ def test_c3_sliding_10m_keys_full_scale(F, layout):
     from flink_amd import _native as N
     R, span, nkeys = 200_000_000, 120_000, 10_000_000
     per = R * 1000 // span
-    steps = 62
+    steps = span // 1000   # the whole 120-s stream: windows fill, slide and retire for another minute
     n = per * steps
     key, ts, val = _gen(N, n, nkeys, span, 1000, total=R)
     th = ts.cpu().numpy()
@@ -152,7 +152,7 @@ def test_c3_sliding_10m_keys_full_scale(F, layout):
     batches = [((s + 1) * per, wms[s]) for s in range(steps)] + [(n, LONG_MAX)]
     op = F.GpuWindowOperator(F.SlidingEventTimeWindows.of(60_000, 1000), F.AverageAggregate(), max_parallelism=128,
                              state_layout=layout, expected_keys=nkeys if layout == "log" else 0)
-    keep = {59, 60, 61}   # the watermark steps that fire windows [-1 s, 59 s), [0, 60 s), [1 s, 61 s) ...
+    keep = {59, 60, 61, 119}   # watermark steps firing windows [-1 s, 59 s), [0, 60 s), [1 s, 61 s) and [59 s, 119 s)
     counts, sums, kept = _run_steps(N, op.handle, key, ts, val, batches, 1, keep)
     late_gpu = op.num_late_records_dropped
     op.close()

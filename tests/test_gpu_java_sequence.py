@@ -102,11 +102,17 @@ class JavaSequence:
             N.check(self.lib.gwo_result_dtype(h, a, C.byref(d)), h)
             self.dt.append(np.float64 if d.value == N.DTYPE_FLOAT64 else np.int64)
         self.ores = [np.zeros(batch, d) for d in self.dt]
+        # open(): every column and drain buffer is pinned once (GwoNative.hostRegister -> gwo_host_register)
+        self.pinned = [self.keys, self.ts, self.vals, self.ok, self.os_, self.oe] + self.ores
+        for b in self.pinned:
+            N.check(self.lib.gwo_host_register(_p(b), b.nbytes), None, "host register")
         self.n = 0
         self.late_reported = 0
         self.late_metric = 0
 
     def close(self):
+        for b in self.pinned:   # close(): unpinned, then the handle destroyed
+            self.N.check(self.lib.gwo_host_unregister(_p(b)), None, "host unregister")
         self.lib.gwo_destroy(self.h)
 
     # processElement
@@ -367,3 +373,16 @@ def test_java_snapshot_sections_rescale_2_to_3(N, case):
     a, agg = spec["o"]()
     ref, _ = _oracle_run(a, agg, spec.get("lateness", 0), k, t, v, b)
     assert sorted(out_before.rows() + out_after.rows()) == sorted((r.key, r.start, r.end, r.result) for r in ref.output)
+
+
+def test_host_register_contract(N):
+    """gwo_host_register pins host memory (idempotent), gwo_host_unregister releases it; unregistering memory that is
+    not registered, a null pointer or a non-positive size is GWO_ERR_INVALID_ARGUMENT."""
+    lib = N.lib()
+    a = np.zeros(1 << 16, np.int64)
+    assert lib.gwo_host_register(_p(a), a.nbytes) == 0
+    assert lib.gwo_host_register(_p(a), a.nbytes) == 0          # already registered: fine
+    assert lib.gwo_host_unregister(_p(a)) == 0
+    assert lib.gwo_host_unregister(_p(a)) == 1   # GWO_ERR_INVALID_ARGUMENT
+    assert lib.gwo_host_register(None, 64) == 1   # GWO_ERR_INVALID_ARGUMENT
+    assert lib.gwo_host_register(_p(a), 0) == 1   # GWO_ERR_INVALID_ARGUMENT

@@ -212,3 +212,42 @@ def test_virtual_ranks_deferred_receives_snapshot(F, monkeypatch, defer):
     assert sorted((a_, s, e, *r) for a_, s, e, r in rows + list(c.output)) == want
     assert late + c.num_late_records_dropped == want_late
     c.close()
+
+
+@pytest.mark.parametrize("async_wm", [0, 1])
+def test_virtual_ranks_routed_batches_without_host_waits(F, monkeypatch, async_wm):
+    """The routed exchange posts each batch's receives one batch behind, from counts the previous batch published to
+    host-mapped memory: a routed batch followed by a watermark that fires nothing never waits on the host for the
+    count exchange (gwo_comm_stats' count_waits stays 0), and with the asynchronous watermark agreement the watermark
+    all-reduce is not waited for either (wm_waits 0).  60-s windows over a 40-s stream: no window fires before the
+    end of input, which flushes the last receives; the output is the oracle's."""
+    from flink_amd import _native as N
+    lib = N.lib()
+    k, t, v, b = _stream(n=200_000, nkeys=20_000, every=5_000, lag=1000, seed=31)
+    t = (t * 2) // 3   # 40-s span
+    b = G.punctuated_watermarks(t, 5_000, 1000)
+    op = F.GpuWindowOperator(F.TumblingEventTimeWindows.of(60_000),
+                             F.MultiAggregate(F.SumAggregate(), F.MinAggregate(), F.CountAggregate()),
+                             state_layout="log", max_parallelism=32768)
+    _virtual(F, op, monkeypatch, 8)
+    N.check(lib.gwo_comm_set_async_watermark(op.handle, async_wm), op.handle, "async watermark")
+    prev = 0
+    for end, wm in b:
+        op.process_batch(k[prev:end], t[prev:end], v[prev:end])
+        op.process_watermark(wm)
+        prev = end
+    routed, cw, ww = C.c_int64(), C.c_int64(), C.c_int64()
+    N.check(lib.gwo_comm_stats(op.handle, C.byref(routed), C.byref(cw), C.byref(ww)), op.handle, "stats")
+    assert routed.value == len(b) and len(b) >= 30
+    assert cw.value == 0
+    if async_wm:
+        assert ww.value == 0
+    else:
+        assert ww.value > 0   # the synchronous agreement waits for each watermark's all-reduce
+    assert op.output == []
+    op.end_input()
+    (wk, ws, we, res), late = V.tumbling_lateness0(k, t, v, b + [(len(k), LONG_MAX)], 60_000, 0, [1, 2, 0])
+    want = sorted(zip(wk.tolist(), ws.tolist(), we.tolist(), *[r.tolist() for r in res]))
+    assert sorted((a, s, e, *r) for a, s, e, r in op.output) == want
+    assert op.num_late_records_dropped == late
+    op.close()
