@@ -61,6 +61,8 @@ def parse():
     p.add_argument("--pipeline", action="store_true",
                    help="pipelined submission (gwo_set_pipelined_submit): measured slower on C4, since pass 2 then "
                         "runs after the next batch's K1 and misses its batch buffer in the MALL")
+    p.add_argument("--sync-watermark", action="store_true",
+                   help="multi-GPU: agree on each watermark synchronously (default: gwo_comm_set_async_watermark)")
     p.add_argument("--comm-single", action="store_true",
                    help="attach a 1-rank RCCL communicator at N=1 (one rank: no record leaves the GPU)")
     p.add_argument("--comm-virtual", type=int, default=0,
@@ -221,6 +223,14 @@ def main():
             os.environ["GWO_COMM_VIRTUAL"] = str(a.comm_virtual)
         N.check(lib.gwo_comm_init(h, uid, 1, 0), h, "gwo_comm_init")
         os.environ.pop("GWO_COMM_VIRTUAL", None)
+    has_comm = world > 1 or a.comm_single
+    if has_comm and not a.sync_watermark:   # the watermark all-reduce is not waited for (applied one call later)
+        N.check(lib.gwo_comm_set_async_watermark(h, 1), h, "async watermark")
+
+    def comm_stats():
+        v = [C.c_int64() for _ in range(3)]
+        N.check(lib.gwo_comm_stats(h, *[C.byref(x) for x in v]), h, "gwo_comm_stats")
+        return [x.value for x in v]
 
     # the per-step arguments are built before timing: a step is the operator's three calls
     kp, tp, vp = key.data_ptr(), ts.data_ptr(), val.data_ptr()
@@ -243,6 +253,7 @@ def main():
     for i in range(a.warmup):
         step(i)
     N.check(lib.gwo_sync(h), h)
+    cs0 = comm_stats() if has_comm else None
     rows_before = rows_emitted()
     lib.gwo_reset_stats(h)
     # time K1 and the fire (the candidates for the dominant kernel); pass 2 is never dominant here
@@ -260,6 +271,17 @@ def main():
         dist.barrier()
     elapsed = t1 - t0
     lib.gwo_set_profiling(h, 0)
+    comm = None
+    if has_comm:   # host waits inside the timed steps (gwo_comm_stats), max over ranks
+        cs1 = comm_stats()
+        d = [b - a_ for a_, b in zip(cs0, cs1)]
+        if dist:
+            t = torch.tensor(d, dtype=torch.int64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            d = t.tolist()
+        comm = {"routed_batches": d[0], "count_waits": d[1], "watermark_waits": d[2],
+                "watermark_agreement": "sync" if a.sync_watermark else "async",
+                "virtual_ranks": a.comm_virtual if world == 1 else None}
 
     def kstat(k):
         la, ms, it = C.c_int64(), C.c_double(), C.c_int64()
@@ -360,6 +382,8 @@ def main():
             "cpu_baseline": cpu,
             "host_fed": host_fed,
         }
+        if comm:
+            out["comm"] = comm
         print(json.dumps(out), flush=True)
     if dist:
         dist.barrier()

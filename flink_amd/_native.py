@@ -105,6 +105,7 @@ SIGNATURES = [
     ("gwo_export_heap_state", C.c_int, [_P, C.POINTER(GwoHeapStateIds), _P, C.c_int64, _I64P, _P, _I64P]),
     ("gwo_import_heap_state", C.c_int, [_P, C.POINTER(GwoHeapStateIds), _P, C.c_int64, C.c_int64]),
     ("gwo_sync", C.c_int, [_P]),
+    ("gwo_wait_fires", C.c_int, [_P]),
     ("gwo_get_stream", C.c_int, [_P, C.POINTER(_P)]),
     ("gwo_last_error", C.c_char_p, [_P]),
     ("gwo_status_string", C.c_char_p, [C.c_int]),

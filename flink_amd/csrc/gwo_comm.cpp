@@ -12,6 +12,7 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <chrono>
 #include <deque>
 #include <vector>
 
@@ -51,8 +52,10 @@ struct Comm {
     int64_t agreed_wm = (int64_t)0x8000000000000000LL;
     // Routed exchanges of the log layout rotate over NS send/receive buffer slots.  Batch i's routed K1
     // fills send slot i % NS and its per-destination counts; the counts are exchanged on the count communicator right
-    // behind K1 and published to host-mapped memory, and batch i's record exchange is posted one batch later -- at
-    // batch i+1's gwo_submit, when the counts have long arrived -- so no routed batch waits on the host for them.
+    // behind K1 and published to host-mapped memory, and batch i's record exchange is posted one batch later: at
+    // batch i+1's gwo_submit right behind its K1 when the counts are there, else after that K1's readback, else at the
+    // next batch (the counts follow batch i's K1 on a high-priority stream) -- no routed batch waits for them; only a
+    // flush, or a slot coming round with its batch's counts still missing, would.
     // Its received records are inserted at batch i+2 (or at any earlier flush: a fire they may fall into, a snapshot,
     // gwo_sync, a state query).  Slot reuse is ordered on the device: a routed K1 waits for the exchange that last
     // sent from its slot, an exchange waits for the K1 that last read its receive slot.
@@ -70,14 +73,13 @@ struct Comm {
     ncclComm_t nc2 = nullptr;
     hipStream_t cs2 = nullptr;
     struct Post {                  // a routed batch whose record exchange is not posted yet
-        bool active = false;
         int slot = 0;
         unsigned long long seq = 0;
         uint64_t rcap = 0, wcap = 0;
         int64_t tbase = 0;
         WindowGeom g{};
     };
-    Post post;
+    std::deque<Post> posts;        // (oldest first; at most 2: the current batch's and the previous one's)
     struct Recv {
         int slot = 0;
         int64_t n = 0, w = 0;      // narrow / wide records received
@@ -269,6 +271,10 @@ gwo_status Handle::comm_route_args(int64_t n, LogRoute *rt, bool *on) {
     C.rcap = ((uint64_t)(mean + 6.0 * std::sqrt(mean) + 64.0) + 1) & ~1ull;   // even: regions stay 8-B aligned
     C.wcap = 256 + (uint64_t)n / 1024;
     C.tbase = log_rt_tbase(C.agreed_wm);   // the same on every rank (min over ranks)
+    // the batch NS ago used this slot: its exchange is posted by now (in the rare case that its counts were still
+    // missing at every earlier chance, this waits for them)
+    while (!C.posts.empty() && std::any_of(C.posts.begin(), C.posts.end(), [&](const Comm::Post &Q) { return Q.slot == slot; }))
+        GWO_TRY(comm_post());
     DevBuf &sb = C.rsend[slot];
     // the slot's last exchange (NS batches ago) sent from this buffer: K1 overwrites it only behind that (device-side)
     if (C.used_send[slot]) GWO_TRY(hipcheck(hipStreamWaitEvent(stream, C.ev_rrecv[slot], 0), "send slot"));
@@ -324,9 +330,8 @@ gwo_status Handle::comm_after_route(const int64_t *k, const int64_t *t, const in
     launch_publish_words(d_send, 4 * P, C.hcnt_dev[slot], ++C.cnt_seq, C.cs2);
     GWO_TRY(launch_ok("count readback"));
     C.routed++;
-    if (C.post.active) GWO_TRY(comm_post());   // batch i-1
-    Comm::Post &Q = C.post;
-    Q.active = true;
+    C.posts.emplace_back();
+    Comm::Post &Q = C.posts.back();
     Q.slot = slot;
     Q.seq = C.cnt_seq;
     Q.rcap = C.rcap;
@@ -335,6 +340,21 @@ gwo_status Handle::comm_after_route(const int64_t *k, const int64_t *t, const in
     Q.g = log_geom_now();
     C.used_send[slot] = true;
     C.rslot = (slot + 1) % Comm::NS;
+    // batch i-1's exchange now, behind this K1, if its counts are there (no wait); else after this batch's readback,
+    // or at the latest when its slot comes round again
+    return comm_post_older(false);
+}
+
+// Posts the record exchanges of the routed batches before the newest, oldest first: all of them (wait: missing counts
+// are waited for, counted in count_waits), or (!wait) as long as their counts have arrived.
+gwo_status Handle::comm_post_older(bool wait) {
+    Comm &C = *comm;
+    const int P = route_ranks(C);
+    while (C.posts.size() > 1) {
+        const Comm::Post &Q = C.posts.front();
+        if (!wait && *(volatile const unsigned long long *)(C.hcnt[Q.slot] + 4 * P) != Q.seq) break;
+        GWO_TRY(comm_post());
+    }
     return GWO_OK;
 }
 
@@ -345,8 +365,9 @@ gwo_status Handle::comm_after_route(const int64_t *k, const int64_t *t, const in
 gwo_status Handle::comm_check_route(const int64_t *k, const int64_t *t, const int64_t *v, int64_t n, uint64_t maxn,
                                     uint64_t maxw) {
     Comm &C = *comm;
-    Comm::Post &Q = C.post;
-    if (!Q.active || (maxn <= Q.rcap && maxw <= Q.wcap)) return GWO_OK;
+    if (C.posts.empty()) return GWO_OK;
+    Comm::Post &Q = C.posts.back();   // the batch being resolved (the newest routed one: no pipelining with a comm)
+    if (maxn <= Q.rcap && maxw <= Q.wcap) return GWO_OK;
     const int P = route_ranks(C);
     const uint64_t rcap = (std::max<uint64_t>(Q.rcap, maxn) + 1) & ~1ull, wcap = std::max<uint64_t>(Q.wcap, maxw);
     DevBuf &sbuf = C.rsend[Q.slot];
@@ -370,20 +391,33 @@ gwo_status Handle::comm_check_route(const int64_t *k, const int64_t *t, const in
     return GWO_OK;
 }
 
-// Posts the record exchange of the routed batch waiting in C.post: its counts from the host-mapped block (already
+// Posts the record exchange of the oldest routed batch not posted yet: its counts from the host-mapped block (already
 // there unless a flush forces the current batch's exchange), then per peer the narrow records as three arrays (keys,
 // values, int32 timestamps: 20 B a record) and the wide ones, on the record stream behind the batch's routed K1.
 gwo_status Handle::comm_post() {
     Comm &C = *comm;
-    Comm::Post Q = C.post;
-    C.post.active = false;
+    const Comm::Post Q = C.posts.front();
+    C.posts.pop_front();
     const int P = route_ranks(C), me = C.rank;
     const bool virt = C.vranks > 1;
     constexpr int NSLOT = Comm::NS;
     (void)NSLOT;
     volatile const unsigned long long *seqw = C.hcnt[Q.slot] + 4 * P;
-    if (*seqw != Q.seq) C.count_waits++;   // the counts are not there yet: this post waits for them
-    GWO_TRY(spin_seq((const unsigned long long *)seqw, Q.seq, "count exchange"));
+    if (*seqw != Q.seq) {   // the counts are not there yet: this post waits for them
+        C.count_waits++;
+        static const bool trace = getenv("GWO_COMM_TRACE") != nullptr;   // (diagnostics)
+        if (trace) {
+            const unsigned long long seen = *seqw;
+            const hipError_t q2 = hipStreamQuery(C.cs2), q1 = hipStreamQuery(C.cs), q0 = hipStreamQuery(stream);
+            const auto t0 = std::chrono::steady_clock::now();
+            GWO_TRY(spin_seq((const unsigned long long *)seqw, Q.seq, "count exchange", C.cs2));
+            const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+            fprintf(stderr, "[comm] post seq %llu (latest %llu) saw %llu: waited %.1f us; cs2 %s cs %s main %s\n", Q.seq,
+                    C.cnt_seq, seen, us, q2 == hipSuccess ? "idle" : "busy", q1 == hipSuccess ? "idle" : "busy",
+                    q0 == hipSuccess ? "idle" : "busy");
+        }
+    }
+    GWO_TRY(spin_seq((const unsigned long long *)seqw, Q.seq, "count exchange", C.cs2));
     unsigned long long hs[2 * LOG_RT_MAX], hr[2 * LOG_RT_MAX];
     memcpy(hs, C.hcnt[Q.slot], (size_t)2 * P * 8);
     memcpy(hr, C.hcnt[Q.slot] + 2 * P, (size_t)2 * P * 8);
@@ -481,7 +515,7 @@ gwo_status Handle::comm_insert_received(size_t keep) {
 // Every routed batch's records inserted: the pending exchange posted (this waits for its counts), all receives read.
 gwo_status Handle::comm_flush_received() {
     if (!comm) return GWO_OK;
-    if (comm->post.active) GWO_TRY(comm_post());
+    while (!comm->posts.empty()) GWO_TRY(comm_post());
     return comm_insert_received(0);
 }
 
@@ -490,8 +524,8 @@ bool Handle::comm_pending_wm(int64_t *wm) const {
     if (!comm) return false;
     bool any = false;
     int64_t m = 0;
-    if (comm->post.active) {
-        m = comm->post.g.wm;
+    for (const Comm::Post &Q : comm->posts) {
+        m = any ? std::min(m, Q.g.wm) : Q.g.wm;
         any = true;
     }
     for (const Comm::Recv &R : comm->recvq) {
@@ -552,7 +586,7 @@ static gwo_status allreduce_min_async(Handle *h, int64_t v, int64_t *applied) {
     if (C.wm_pending) {   // the previous call's min
         volatile const unsigned long long *seqw = C.hwm[q ^ 1] + 1;
         if (*seqw != C.wm_seq) C.wm_waits++;
-        GWO_TRY(h->spin_seq((const unsigned long long *)seqw, C.wm_seq, "watermark agreement"));
+        GWO_TRY(h->spin_seq((const unsigned long long *)seqw, C.wm_seq, "watermark agreement", C.cs2));
         *applied = (int64_t)C.hwm[q ^ 1][0];
     } else {
         *applied = C.agreed_wm;
@@ -581,7 +615,7 @@ gwo_status Handle::comm_min_watermark(int64_t wm_in, int64_t *out) {
     }
     if (C.wm_pending) {   // a queued asynchronous agreement completes first (RCCL orders the count communicator)
         const int q = (int)(C.wm_seq & 1) ^ 1;
-        GWO_TRY(spin_seq(C.hwm[q] + 1, C.wm_seq, "watermark agreement"));
+        GWO_TRY(spin_seq(C.hwm[q] + 1, C.wm_seq, "watermark agreement", C.cs2));
         C.wm_pending = false;
     }
     C.wm_waits++;
@@ -593,6 +627,30 @@ gwo_status Handle::comm_min_watermark(int64_t wm_in, int64_t *out) {
 }  // namespace gwo
 
 using namespace gwo;
+
+// RCCL connects peers lazily, at a communicator's first operation of a kind: one word to and from every peer on both
+// communicators now, so the first routed batch and watermark do not pay for the connection setup (measured: the
+// first asynchronous watermark agreements were still queued behind it when the next watermark came).
+static gwo_status comm_warm(Handle *h) {
+    Comm &C = *h->comm;
+    const int P = route_ranks(C), me = C.rank;
+    if (P <= 1) return GWO_OK;
+    uint64_t *d = (uint64_t *)C.counts.ptr;   // word 0 is sent, words 1 + p receive (scratch: 6 * P words)
+    for (int pass = 0; pass < 2; ++pass) {
+        ncclComm_t nc = pass ? C.nc : C.nc2;
+        hipStream_t s = pass ? C.cs : C.cs2;
+        GWO_TRY(nccl_ok(h, ncclGroupStart(), "group"));
+        for (int p = 0; p < P; ++p) {
+            if (p == me) continue;
+            const int peer = C.vranks > 1 ? me : p;
+            GWO_TRY(nccl_ok(h, ncclSend(d, 1, ncclUint64, peer, nc, s), "warm send"));
+            GWO_TRY(nccl_ok(h, ncclRecv(d + 1 + p, 1, ncclUint64, peer, nc, s), "warm recv"));
+        }
+        GWO_TRY(nccl_ok(h, ncclGroupEnd(), "group end"));
+        GWO_TRY(h->hipcheck(hipStreamSynchronize(s), "comm warm-up"));
+    }
+    return GWO_OK;
+}
 
 extern "C" gwo_status gwo_comm_unique_id(uint8_t *id) {
     if (!id) return GWO_ERR_INVALID_ARGUMENT;
@@ -661,6 +719,7 @@ extern "C" gwo_status gwo_comm_init(gwo_handle *hh, const uint8_t *id, int32_t n
     gwo_status st = h->ensure_buf(C->counts, (size_t)6 * cranks * 8 + 32);   // (never reallocated later)
     if (const char *e = getenv("GWO_COMM_ASYNC_WM")) C->async_wm = atoi(e) != 0;
     if (st == GWO_OK) st = allreduce_min(h, h->wm, &C->agreed_wm);
+    if (st == GWO_OK) st = comm_warm(h);
     return st;
 }
 

@@ -252,9 +252,12 @@ gwo_status Handle::submit(const int64_t *key, const int64_t *ts, const void *val
         if (!routed) return n ? insert_log(dk, dt, dv, n) : GWO_OK;   // one rank: nothing leaves this GPU
         if (n > 0) GWO_TRY(insert_log(dk, dt, dv, n, 1, &rt));
         else GWO_TRY(comm_after_route(dk, dt, dv, 0));
-        // deferred: the previous batch's exchange was posted behind this batch's K1 (its counts had arrived), the one
-        // before it has landed and is inserted now; otherwise this batch's exchange completes inside its submit
-        return comm_defers() ? comm_insert_received(1) : comm_flush_received();
+        // deferred: the previous batch's exchange is posted (behind this batch's K1 when its counts had arrived, else
+        // now if they have, else later -- never waiting), the exchanges posted before the newest have landed and are
+        // inserted now; otherwise this batch's exchange completes inside its submit
+        if (!comm_defers()) return comm_flush_received();
+        GWO_TRY(comm_post_older(false));
+        return comm_insert_received(1);
     }
     if (comm) {
         const int64_t *aos = nullptr, *loc = nullptr;

@@ -234,7 +234,8 @@ struct Handle {
     gwo_status dalloc(void **p, size_t bytes);
     gwo_status hipcheck(hipError_t e, const char *what);
     gwo_status spin_event(hipEvent_t ev, const char *what);
-    gwo_status spin_seq(const unsigned long long *word, unsigned long long seq, const char *what);
+    gwo_status spin_seq(const unsigned long long *word, unsigned long long seq, const char *what,
+                        hipStream_t producer = nullptr);   // producer: the stream that publishes the word (default: stream)
     bool known_device(const void *p, size_t bytes);
     std::vector<std::pair<uintptr_t, uintptr_t>> dev_ranges;   // device allocations seen by stage_inputs
     gwo_status ensure_buf(DevBuf &b, size_t bytes);
@@ -345,7 +346,7 @@ struct Handle {
     gwo_status log_carve(LogWindow &W, size_t bytes, char **out);
     void log_release(LogWindow &W);
     int log_choose_lp(uint64_t batch_records) const;
-    gwo_status log_split_exact(long long base, int nunits, uint64_t cap, const uint64_t *counts, int tmpx);
+    gwo_status log_split_exact(long long base, int nunits, uint64_t cap, int k1grid, const uint64_t *counts, int tmpx);
     gwo_status log_split_dev(const LogJob &J, const unsigned long long *rbp);
     gwo_status log_resolve_split();
     // ts32: `t` points at int32 timestamps - tbase (records received in the 20-B wire format)
@@ -400,7 +401,8 @@ struct Handle {
     // K1's readback of a routed batch: re-route with exact capacities when a destination region overflowed
     gwo_status comm_check_route(const int64_t *k, const int64_t *t, const int64_t *v, int64_t n, uint64_t maxn,
                                 uint64_t maxw);
-    gwo_status comm_post();   // posts the record exchange of the routed batch whose counts were published last
+    gwo_status comm_post();   // posts the record exchange of the oldest routed batch not posted yet
+    gwo_status comm_post_older(bool wait);   // posts the exchanges before the newest routed batch's (see gwo_comm.cpp)
     // deferred receives of the routed log path: inserted two routed batches later or at log_flush
     bool comm_defers() const;
     gwo_status comm_insert_received(size_t keep);

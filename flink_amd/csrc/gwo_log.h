@@ -15,6 +15,13 @@
 #define LOG_K1_GRID 512          // K1 workgroups: 2 per CU on MI355X's 256 CUs, all resident, each looping over
                                  // tiles with the next tile prefetched (measured: 0.223 ms vs 0.249 at 2048)
 #endif
+// K1's trash lines (after the region cursors in the same allocation): a write-phase lane with no record to write
+// stores to its workgroup's line instead of skipping the store, so every tile issues exactly LOG_K1_PER stores per
+// thread and the compiler's wait counting stays exact (a skippable store counts as none: the next tile's waits for
+// its prefetched values became waits for everything in flight)
+#define LOG_CURSOR_WORDS (LOG_NU * LOG_ND * LOG_XG * LOG_CUR_STRIDE)
+#define LOG_K1_TRASH_WG (2 * LOG_K1_PER)           // words per workgroup (one 16-B record per store of a tile)
+#define LOG_K1_TRASH_WORDS (LOG_K1_GRID * LOG_K1_TRASH_WG)
 #define LOG_TILE_PER 7            // pass-2 chunk: 512 threads x 7 records
 #define LOG_TILE_THREADS 512
 #define LOG_TILE (LOG_TILE_PER * LOG_TILE_THREADS)   // 3584 records: 56 KiB of 16-B records in LDS
@@ -27,12 +34,16 @@ static_assert(LOG_K1_TILE <= 65536, "K1 ranks within a tile are 16-bit");
 #define LOG_MAX_LP (LOG_DB + 10 < 18 ? LOG_DB + 10 : 18)   // <= 1024 partitions per coarse digit (pass-2 LDS)
 #define LOG_FIRE_THREADS 512
 #define LOG_CUR_STRIDE 16        // K1 bucket cursors: one per 128-B line (memory-side atomics serialise per line)
-#ifndef LOG_XG
-#define LOG_XG 1                 // K1 region groups per bucket: workgroup w appends to group w % LOG_XG.  With 8
-                                 // (workgroups w and w + 8 share an XCD) each group's runs merge in one L2: K1 alone
-                                 // ran 13 % faster in isolation, but end to end K1 + pass 2 measured 221 + 100 us (1
-                                 // group), 224 + 122 (4), 223 + 134 (8) per C4 batch -- so one group
-#endif
+// K1's batch buffer: one run per (bucket, workgroup) -- bucket b's records from workgroup w at
+// tmp + ((b * G + w) * cap) * W words (G = the launch's workgroups, log_k1_grid; cap = records per run, a multiple of
+// LOG_RUN_ALIGN so every run starts on a 128-B line).  A workgroup appends each tile's records of a bucket to its own
+// run (the cursor is the owning thread's register: no reservation round trip per tile), so a run's lines fill up in
+// the L2 of one XCD, written whole.  Behind the runs, the count table: [nb * G] uint32, run (b, w) at b * G + w.
+// (r03's layout -- one region per bucket, a device-scope atomic reservation per tile -- put that atomic's round
+// trip, queued behind the whole chip's traffic, on every tile's critical path, and merged partial lines of
+// neighbouring runs from different XCDs in HBM: 1.22x the algorithmic writes.)
+#define LOG_XG 1
+#define LOG_RUN_ALIGN 8
 #define FIRE_RPT 7                                   // records per thread in the fire's register prefetch
 #define FIRE_RCAP (FIRE_RPT * LOG_FIRE_THREADS)      // 3584: records per partition of the fire's fast path
 #define FIRE_OWN_LOG2 13
@@ -122,7 +133,9 @@ struct CollectArgs {
 // (device-scope atomics on the same address serialise at ~12 ns each on MI355X: 4 per-wave atomics per
 // workgroup on one word cost ~25 us at the end of a 512-workgroup launch); the tail folds the shards.
 #define LOG_SHARDS 16
-enum : int { K1S_MIN = 0, K1S_MAX, K1S_ACC, K1S_LATE, K1S_REFIRE, K1S_BADTS, K1S_BADKG, K1S_HOUT, K1S_BADR, K1S_NEXT, K1_SW };
+enum : int { K1S_MIN = 0, K1S_MAX, K1S_ACC, K1S_LATE, K1S_REFIRE, K1S_BADTS, K1S_BADKG, K1S_HOUT, K1S_BADR, K1S_NEXT,
+             K1S_MAXRUN,   // the largest (bucket, workgroup) run (> cap: records were dropped, the host re-runs K1)
+             K1_SW };
 static constexpr size_t LOG_DONE_WORDS = (LOG_SHARDS + 1) * LOG_CUR_STRIDE;
 
 // Multi-GPU keyBy routing fused into K1 (the log layout's first K1 over a batch): a record whose key group
@@ -167,6 +180,8 @@ static inline __host__ __device__ bool log_rt_fits(int64_t t, int64_t tbase) {
 static inline int64_t log_rt_tbase(int64_t wm) { return wm == (int64_t)0x8000000000000000LL ? 0 : wm; }
 
 namespace gwo {
+int log_k1_grid(int64_t n);                                    // K1 workgroups for n records
+size_t log_tmp_bytes(int nb, int grid, uint64_t cap, int w);   // K1's batch buffer: runs + count table
 // K1: classify + key-group check + late accounting + (window, coarse digit) grouping of a batch; its last
 // workgroup writes the readback block and the device plan of pass 2, and resets cursors and statistics.
 // key/ts/val columns with `stride` int64 words between records (1: SoA columns; 3: {key, ts, value} records)
@@ -180,7 +195,7 @@ void launch_log_part(const int64_t *key, const int64_t *ts, const int64_t *val, 
 // Pass 2: every coarse bucket -> its window's segment, grouped by partition.  `overflow` is a
 // host-visible flag (set to 1 when a partition exceeds its capacity).  go != NULL: a speculative launch
 // of `nchunks` (an upper bound) workgroups that exits unless *go (K1's verdict) is set.
-void launch_log_split(const int64_t *tmp, uint64_t cap, int has_val, const LogBucket *buckets, int nb,
+void launch_log_split(const int64_t *tmp, uint64_t cap, int k1grid, int has_val, const LogBucket *buckets, int nb,
                       const LogSegSet &segs, unsigned *overflow, uint32_t nchunks, const unsigned *go, hipStream_t s);
 int log_fire_cap_log2(int nwords);
 // Loads the fire and pass-2 code objects with empty launches (HIP loads a kernel's code on its first launch:

@@ -762,13 +762,14 @@ gwo_status Handle::combine_flush() {
 }
 
 // Spins on a host-mapped readback block's sequence word (written last by a kernel's final workgroup).  Now and
-// then the stream is queried, so that a failed launch cannot spin forever: an idle stream whose word never
-// arrived is an error.  Ends with an acquire fence: the block's other words are visible.
-gwo_status Handle::spin_seq(const unsigned long long *word, unsigned long long seq, const char *what) {
+// then the producing stream is queried, so that a failed launch cannot spin forever: an idle stream whose word
+// never arrived is an error.  Ends with an acquire fence: the block's other words are visible.
+gwo_status Handle::spin_seq(const unsigned long long *word, unsigned long long seq, const char *what,
+                            hipStream_t producer) {
     volatile const unsigned long long *w = word;
     for (unsigned it = 1; *w != seq; ++it) {
         if ((it & 1023) == 0) {
-            hipError_t e = hipStreamQuery(stream);
+            hipError_t e = hipStreamQuery(producer ? producer : stream);
             if (e != hipSuccess && e != hipErrorNotReady) return hipcheck(e, what);
             if (e == hipSuccess && *w != seq) return poison(GWO_ERR_HIP, "readback sequence word not visible after completion");
         }
@@ -1356,6 +1357,11 @@ gwo_status gwo_sync(gwo_handle *hh) {
     if (h->logst) GWO_TRY(h->log_resolve_split());
     GWO_TRY(h->finish_fire());
     return h->hipcheck(hipStreamSynchronize(h->stream), "sync");
+}
+
+gwo_status gwo_wait_fires(gwo_handle *hh) {
+    H_OR_FAIL;
+    return h->finish_fire();
 }
 
 gwo_status gwo_host_register(void *ptr, int64_t bytes) {

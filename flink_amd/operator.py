@@ -185,8 +185,9 @@ class GpuWindowOperator:
     # -- results -----------------------------------------------------------------------------
     def _collect(self):
         # processWatermark emits the fired rows before it returns (AbstractStreamOperator.java:566-571):
-        # wait for an asynchronous fire (log layout) to complete
-        N.check(self._lib.gwo_sync(self._h), self._h, "gwo_sync")
+        # wait for an asynchronous fire (log layout, sessions) to complete -- only the fires: batches and the
+        # multi-GPU exchange stay in flight
+        N.check(self._lib.gwo_wait_fires(self._h), self._h, "gwo_wait_fires")
         n = C.c_int64()
         N.check(self._lib.gwo_output_count(self._h, C.byref(n)), self._h)
         if n.value:

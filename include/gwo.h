@@ -240,6 +240,11 @@ gwo_status gwo_import_heap_state(gwo_handle *h, const gwo_heap_state_ids *ids, c
                                  int64_t watermark);
 
 gwo_status gwo_sync(gwo_handle *h);
+/* Waits for the fires queued so far only (the log layout and sessions fire asynchronously): afterwards
+ * gwo_output_count counts every row of the watermarks applied -- what WindowOperator emits before it forwards a
+ * watermark (AbstractStreamOperator.java:566-571).  Unlike gwo_sync it leaves submitted batches and the multi-GPU
+ * exchange in flight (a watermark already completed whatever a window it fired could hold). */
+gwo_status gwo_wait_fires(gwo_handle *h);
 gwo_status gwo_get_stream(gwo_handle *h, void **stream);
 const char *gwo_last_error(const gwo_handle *h);
 const char *gwo_status_string(gwo_status s);

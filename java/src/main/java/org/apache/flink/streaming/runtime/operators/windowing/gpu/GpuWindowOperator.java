@@ -228,11 +228,12 @@ public class GpuWindowOperator<IN, K> extends AbstractStreamOperator<GpuWindowRe
 
     // ---- results (TimestampedCollector.collect, WindowOperator.java:546-550) --------------------------------
     // Called after advanceWatermark and before the watermark is forwarded (AbstractStreamOperator.java:566-571):
-    // gwo_sync first completes a fire that runs asynchronously (sessions, log layout), then the rows are drained
-    // in chunks of `batch` rows through the buffers allocated at open() until none is left.
+    // gwo_wait_fires first completes a fire that runs asynchronously (sessions, log layout), then the rows are
+    // drained in chunks of `batch` rows through the buffers allocated at open() until none is left.  Submitted
+    // batches and the multi-GPU exchange stay in flight.
     @SuppressWarnings("unchecked")
     private void emitFired() {
-        GwoNative.sync(handle);
+        GwoNative.waitFires(handle);
         long rows;
         while ((rows = GwoNative.outputCount(handle)) > 0) {
             final int cap = (int) Math.min(rows, batch);

@@ -65,8 +65,11 @@ final class GwoNative {
 
     static native void advanceWatermark(long handle, long watermark);
 
-    /** gwo_sync: completes a fire still running (sessions, log layout) so outputCount sees all of its rows. */
+    /** gwo_sync: completes every submitted batch, exchange and fire (snapshots, close). */
     static native void sync(long handle);
+
+    /** gwo_wait_fires: completes a fire still running (sessions, log layout) so outputCount sees all of its rows. */
+    static native void waitFires(long handle);
 
     static native long outputCount(long handle);
 

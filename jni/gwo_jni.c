@@ -151,11 +151,17 @@ JNIEXPORT void JNICALL JFN(submitUtf16)(JNIEnv *env, jclass c, jlong h, jobject 
     fail(env, H(h), gwo_submit_utf16(H(h), pc, off, pt, pv, n));
 }
 
-/* gwo_sync: waits for a fire still running (sessions and the log layout fire asynchronously), so that
- * outputCount afterwards counts every row of the watermark just applied. */
+/* gwo_sync: every submitted batch, exchange and fire completed (snapshots, close). */
 JNIEXPORT void JNICALL JFN(sync)(JNIEnv *env, jclass c, jlong h) {
     (void)c;
     fail(env, H(h), gwo_sync(H(h)));
+}
+
+/* gwo_wait_fires: waits for a fire still running (sessions and the log layout fire asynchronously), so that
+ * outputCount afterwards counts every row of the watermark just applied; batches stay in flight. */
+JNIEXPORT void JNICALL JFN(waitFires)(JNIEnv *env, jclass c, jlong h) {
+    (void)c;
+    fail(env, H(h), gwo_wait_fires(H(h)));
 }
 
 JNIEXPORT void JNICALL JFN(advanceWatermark)(JNIEnv *env, jclass c, jlong h, jlong wm) {

@@ -6,7 +6,8 @@ FLAGS="$*"
 R=$(cd "$(dirname "$0")/.." && pwd)
 OUT=$R/exp/$NAME
 mkdir -p $OUT/obj
-for f in $R/flink_amd/csrc/*.hip; do
+SRC=${SRC:-$R/flink_amd/csrc}   # SRC=dir: kernels from another tree (e.g. a commit's sources, for A/B against it)
+for f in $SRC/*.hip; do
   b=$(basename $f .hip)
   EXTRA=""
   [ "$b" = gwo_log ] && EXTRA="-mllvm -amdgpu-atomic-optimizer-strategy=None"

@@ -8,7 +8,7 @@ its JNI shim (java/.../gpu/GpuWindowOperator.java, jni/gwo_jni.c):
   groups (getRuntimeContext().getMaxNumberOfParallelSubtasks(), StreamTaskStateInitializerImpl.java:290-306);
   restoreRows when restored (min watermark over the key-group sections it reads, one gwo_restore);
 * processElement: records appended to columns, gwo_submit every `batch` records;
-* processWatermark / endInput: flush, gwo_advance_watermark, emitFired -- gwo_sync (JNI `sync`), then
+* processWatermark / endInput: flush, gwo_advance_watermark, emitFired -- gwo_wait_fires (JNI `waitFires`), then
   gwo_output_count / gwo_drain in chunks of `batch` rows until none is left, the side output the same way,
   gwo_late_dropped -- then the watermark is forwarded (rows before the watermark, AbstractStreamOperator.java:
   566-571);
@@ -142,7 +142,7 @@ class JavaSequence:
 
     def emit_fired(self):
         N, lib, h = self.N, self.lib, self.h
-        N.check(lib.gwo_sync(h), h, "sync")
+        N.check(lib.gwo_wait_fires(h), h, "waitFires")
         n = C.c_int64()
         while True:
             N.check(lib.gwo_output_count(h, C.byref(n)), h)

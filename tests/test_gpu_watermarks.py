@@ -8,6 +8,7 @@ Expected outputs come from the oracle run on the same stream with the watermarks
 (running max), which is what the valve forwards.  Integer aggregates: bit-exact.
 """
 import ctypes as C
+import time
 
 import numpy as np
 import pytest
@@ -219,7 +220,8 @@ def test_virtual_ranks_routed_batches_without_host_waits(F, monkeypatch, async_w
     """The routed exchange posts each batch's receives one batch behind, from counts the previous batch published to
     host-mapped memory: a routed batch followed by a watermark that fires nothing never waits on the host for the
     count exchange (gwo_comm_stats' count_waits stays 0), and with the asynchronous watermark agreement the watermark
-    all-reduce is not waited for either (wm_waits 0).  60-s windows over a 40-s stream: no window fires before the
+    all-reduce is not waited for either (wm_waits 0).  The operator's calls are made directly (gwo_submit,
+    gwo_advance_watermark, gwo_wait_fires): gwo_sync would complete the exchange on purpose.  60-s windows over a 40-s stream: no window fires before the
     end of input, which flushes the last receives; the output is the oracle's."""
     from flink_amd import _native as N
     lib = N.lib()
@@ -232,10 +234,17 @@ def test_virtual_ranks_routed_batches_without_host_waits(F, monkeypatch, async_w
     _virtual(F, op, monkeypatch, 8)
     N.check(lib.gwo_comm_set_async_watermark(op.handle, async_wm), op.handle, "async watermark")
     prev = 0
-    for end, wm in b:
-        op.process_batch(k[prev:end], t[prev:end], v[prev:end])
-        op.process_watermark(wm)
+    h = op.handle
+    for end, wm in b:   # the operator's calls (process_batch, process_watermark) with the rows left in place
+        kk, tt, vv = (np.ascontiguousarray(x[prev:end]) for x in (k, t, v))
+        N.check(lib.gwo_submit(h, kk.ctypes.data, tt.ctypes.data, vv.ctypes.data, end - prev), h, "submit")
+        N.check(lib.gwo_advance_watermark(h, wm), h, "watermark")
+        N.check(lib.gwo_wait_fires(h), h, "wait fires")
+        n = C.c_int64()
+        N.check(lib.gwo_output_count(h, C.byref(n)), h)
+        assert n.value == 0
         prev = end
+        time.sleep(0.002)   # a source's batching cadence: the device is never behind, so any wait is the protocol's
     routed, cw, ww = C.c_int64(), C.c_int64(), C.c_int64()
     N.check(lib.gwo_comm_stats(op.handle, C.byref(routed), C.byref(cw), C.byref(ww)), op.handle, "stats")
     assert routed.value == len(b) and len(b) >= 30
@@ -244,7 +253,6 @@ def test_virtual_ranks_routed_batches_without_host_waits(F, monkeypatch, async_w
         assert ww.value == 0
     else:
         assert ww.value > 0   # the synchronous agreement waits for each watermark's all-reduce
-    assert op.output == []
     op.end_input()
     (wk, ws, we, res), late = V.tumbling_lateness0(k, t, v, b + [(len(k), LONG_MAX)], 60_000, 0, [1, 2, 0])
     want = sorted(zip(wk.tolist(), ws.tolist(), we.tolist(), *[r.tolist() for r in res]))

@@ -78,12 +78,12 @@ def test_jni_shim_compiles_against_the_jni_calls_it_makes():
 
 
 def test_operator_emits_after_sync_and_reads_max_parallelism_from_the_task():
-    """GpuWindowOperator: emitFired completes a running fire (gwo_sync) before counting rows and drains into buffers
+    """GpuWindowOperator: emitFired completes a running fire (gwo_wait_fires) before counting rows and drains into buffers
     allocated once; the number of key groups is the task's (getMaxNumberOfParallelSubtasks), not ExecutionConfig's;
     the value dtype comes from the aggregate descriptor."""
     op = open(os.path.join(PKG, "GpuWindowOperator.java")).read()
     body = op[op.index("private void emitFired()"):op.index("private String[] keyStrings(")]
-    assert body.index("GwoNative.sync(handle)") < body.index("GwoNative.outputCount(handle)")
+    assert body.index("GwoNative.waitFires(handle)") < body.index("GwoNative.outputCount(handle)")
     assert "direct(" not in body.replace("sideKeys = direct(", "").replace("sideTs = direct(", "") \
         .replace("sideValues = direct(", "")
     assert "getRuntimeContext().getMaxNumberOfParallelSubtasks()" in op
