@@ -578,8 +578,7 @@ static gwo_status allreduce_min_async(Handle *h, int64_t v, int64_t *applied) {
     int64_t *d = (int64_t *)C.counts.ptr + 6 * std::max(C.nranks, C.vranks) + 2;   // (past the synchronous word)
     const int q = (int)(C.wm_seq & 1);
     if (!C.hwm[q]) {
-        // [0] the published min, [1] its sequence word, [2] this call's input (the copy reads it after the call returns,
-        // so each block keeps its own staging word until the call two later)
+        // [0] the published min, [1] its sequence word
         GWO_TRY(h->hipcheck(hipHostMalloc((void **)&C.hwm[q], 32, hipHostMallocCoherent | hipHostMallocMapped), "wm"));
         GWO_TRY(h->hipcheck(hipHostGetDevicePointer((void **)&C.hwm_dev[q], C.hwm[q], 0), "wm"));
     }
@@ -591,8 +590,8 @@ static gwo_status allreduce_min_async(Handle *h, int64_t v, int64_t *applied) {
     } else {
         *applied = C.agreed_wm;
     }
-    C.hwm[q][2] = (unsigned long long)v;
-    GWO_TRY(h->hipcheck(hipMemcpyAsync(d, C.hwm[q] + 2, 8, hipMemcpyHostToDevice, C.cs2), "wm"));
+    launch_put_word((unsigned long long *)d, (unsigned long long)v, C.cs2);   // (no copy from host memory)
+    GWO_TRY(h->launch_ok("wm"));
     GWO_TRY(nccl_ok(h, ncclAllReduce(d, d, 1, ncclInt64, ncclMin, C.nc2, C.cs2), "allreduce wm"));
     launch_publish_words((const unsigned long long *)d, 1, C.hwm_dev[q], ++C.wm_seq, C.cs2);
     GWO_TRY(h->launch_ok("wm readback"));

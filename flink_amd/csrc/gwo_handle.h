@@ -346,7 +346,7 @@ struct Handle {
     gwo_status log_carve(LogWindow &W, size_t bytes, char **out);
     void log_release(LogWindow &W);
     int log_choose_lp(uint64_t batch_records) const;
-    gwo_status log_split_exact(long long base, int nunits, uint64_t cap, int k1grid, const uint64_t *counts, int tmpx);
+    gwo_status log_split_exact(long long base, int nunits, uint64_t cap, const uint64_t *counts, int tmpx);
     gwo_status log_split_dev(const LogJob &J, const unsigned long long *rbp);
     gwo_status log_resolve_split();
     // ts32: `t` points at int32 timestamps - tbase (records received in the 20-B wire format)

@@ -232,6 +232,7 @@ void launch_scan(const int64_t *key, const int64_t *ts, int64_t n, const WindowG
                  unsigned long long *side_count, long long side_cap, int side_enabled, unsigned long long *shards,
                  hipStream_t s, const ScanSpec *spec = nullptr);
 
+void launch_put_word(unsigned long long *dst, unsigned long long v, hipStream_t s);
 void launch_publish_words(const unsigned long long *src, int nw, unsigned long long *rb, unsigned long long seq,
                           hipStream_t s);
 

@@ -1541,6 +1541,16 @@ void launch_publish_words(const unsigned long long *src, int nw, unsigned long l
     hipLaunchKernelGGL(publish_words_kernel, dim3(1), dim3(64), 0, s, src, nw, rb, seq);
 }
 
+// One word into device memory, in stream order (a value travelling in the launch's arguments instead of a copy from
+// host memory).
+__global__ __launch_bounds__(64) void put_word_kernel(unsigned long long *dst, unsigned long long v) {
+    if (threadIdx.x == 0) *dst = v;
+}
+
+void launch_put_word(unsigned long long *dst, unsigned long long v, hipStream_t s) {
+    hipLaunchKernelGGL(put_word_kernel, dim3(1), dim3(64), 0, s, dst, v);
+}
+
 void launch_scan(const int64_t *key, const int64_t *ts, int64_t n, const WindowGeom &g, long long hist_base,
                  BatchStats *stats, int64_t *side_key, int64_t *side_ts, int64_t *side_val, const int64_t *val,
                  unsigned long long *side_count, long long side_cap, int side_enabled, unsigned long long *shards,

@@ -27,13 +27,6 @@ static uint64_t group_capacity(double mean) {
     return (uint64_t)std::ceil(mean + 6.0 * std::sqrt(mean) + 4.0);
 }
 
-// K1's run capacity (records per (bucket, workgroup) run) for n records: every record in one window, 256 digits x G
-// workgroups; a multiple of LOG_RUN_ALIGN (runs start on 128-B lines).
-static uint64_t run_capacity(double per_run) {
-    const uint64_t c = std::max<uint64_t>(group_capacity(per_run), LOG_RUN_ALIGN);
-    return (c + LOG_RUN_ALIGN - 1) / LOG_RUN_ALIGN * LOG_RUN_ALIGN;
-}
-
 gwo_status Handle::log_init() {
     logst = new LogState();
     LogState &L = *logst;
@@ -42,6 +35,7 @@ gwo_status Handle::log_init() {
     GWO_TRY(dalloc((void **)&L.d_bk, kPlanBytes * LOG_SLOTS));
     GWO_TRY(dalloc((void **)&L.d_plan, kPlanBytes));
     GWO_TRY(dalloc((void **)&L.d_overflow, 16));
+    GWO_TRY(dalloc((void **)&L.d_slow, (LOG_SLOW_CAP + 1) * 4));   // the fire's slow-path partition list + count
     GWO_TRY(hipcheck(hipMemsetAsync(L.d_overflow, 0, 16, stream), "overflow"));
     GWO_TRY(dalloc((void **)&L.d_go, LOG_SLOTS * sizeof(unsigned)));
     GWO_TRY(dalloc((void **)&L.d_t0, 8));
@@ -81,7 +75,7 @@ gwo_status Handle::log_init() {
     {   // pass 2's code object too: a speculative launch whose verdict word is 0 exits at once
         GWO_TRY(hipcheck(hipMemsetAsync(L.d_go, 0, LOG_SLOTS * sizeof(unsigned), stream), "go"));
         GWO_TRY(hipcheck(hipMemsetAsync(L.d_bk, 0, kPlanBytes, stream), "plan"));
-        launch_log_split(nullptr, 1, 1, needs_value, L.d_bk, 0, LogSegSet{}, L.d_split_flag, 1, L.d_go, stream);
+        launch_log_split(nullptr, 1, needs_value, L.d_bk, 0, LogSegSet{}, L.d_split_flag, 1, L.d_go, stream);
         GWO_TRY(launch_ok("warm-up"));
     }
     return log_reserve();
@@ -136,6 +130,7 @@ void Handle::log_free() {
     if (L.d_bk) (void)hipFree(L.d_bk);
     if (L.d_plan) (void)hipFree(L.d_plan);
     if (L.d_overflow) (void)hipFree(L.d_overflow);
+    if (L.d_slow) (void)hipFree(L.d_slow);
     if (L.d_go) (void)hipFree(L.d_go);
     if (L.d_done) (void)hipFree(L.d_done);
     if (L.d_t0) (void)hipFree(L.d_t0);
@@ -207,8 +202,7 @@ int Handle::log_choose_lp(uint64_t batch_records) const {
 // keys).  Fresh segments for windows [base, base + nunits) of batch buffer `tmpx` (bucket counts in
 // `counts`); re-runs with each bucket's partitions sized to its measured largest one until nothing
 // overflows.
-gwo_status Handle::log_split_exact(long long base, int nunits, uint64_t cap, int k1grid, const uint64_t *counts,
-                                   int tmpx) {
+gwo_status Handle::log_split_exact(long long base, int nunits, uint64_t cap, const uint64_t *counts, int tmpx) {
     LogState &L = *logst;
     const int W = needs_value ? 2 : 1;
     const int nb = nunits * LOG_ND;
@@ -266,8 +260,8 @@ gwo_status Handle::log_split_exact(long long base, int nunits, uint64_t cap, int
         L.h_split_flag[tmpx] = 0;
         GWO_TRY(hipcheck(hipMemcpyAsync(L.d_plan, L.h_buckets, (nb + 1) * sizeof(LogBucket), hipMemcpyHostToDevice, stream),
                          "split plan"));
-        launch_log_split((const int64_t *)L.tmp[tmpx].ptr, cap, k1grid, needs_value, L.d_plan, nb, set,
-                         L.d_split_flag + tmpx, chunks, nullptr, stream);
+        launch_log_split((const int64_t *)L.tmp[tmpx].ptr, cap, needs_value, L.d_plan, nb, set, L.d_split_flag + tmpx,
+                         chunks, nullptr, stream);
         GWO_TRY(launch_ok("log split"));
         GWO_TRY(hipcheck(hipStreamSynchronize(stream), "log split"));
         if (L.h_split_flag[tmpx] == 0) break;
@@ -306,7 +300,6 @@ gwo_status Handle::log_commit_spec(LogJob &J, const unsigned long long *rbp) {
     L.pend.nunits = J.nunits;
     L.pend.base = J.base;
     L.pend.cap = J.cap;
-    L.pend.k1grid = log_k1_grid(J.n);
     L.pend.counts.assign(rbp, rbp + J.nunits * LOG_ND);
     for (int w = 0; w < J.nunits; ++w) {
         if (!wcount[w]) continue;
@@ -338,8 +331,8 @@ gwo_status Handle::log_split_dev(const LogJob &J, const unsigned long long *rbp)
     }
     L.h_split_flag[J.slot] = 0;
     prof_begin(GWO_KERNEL_PARTITION);
-    launch_log_split((const int64_t *)L.tmp[J.slot].ptr, J.cap, log_k1_grid(J.n), needs_value, L.bk(J.slot),
-                     J.nunits * LOG_ND, set, L.d_split_flag + J.slot, (uint32_t)rbp[LOG_RB_CHUNKS], nullptr, stream);
+    launch_log_split((const int64_t *)L.tmp[J.slot].ptr, J.cap, needs_value, L.bk(J.slot), J.nunits * LOG_ND, set,
+                     L.d_split_flag + J.slot, (uint32_t)rbp[LOG_RB_CHUNKS], nullptr, stream);
     GWO_TRY(launch_ok("log split"));
     prof_end(GWO_KERNEL_PARTITION, (int64_t)total);
     // completion is implied by the next K1's readback (stream order); only a pipelined K1, queued before
@@ -352,7 +345,6 @@ gwo_status Handle::log_split_dev(const LogJob &J, const unsigned long long *rbp)
     L.pend.nunits = J.nunits;
     L.pend.base = J.base;
     L.pend.cap = J.cap;
-    L.pend.k1grid = log_k1_grid(J.n);
     L.pend.counts.assign(rbp, rbp + J.nunits * LOG_ND);
     for (int w = 0; w < J.nunits; ++w) {
         if (!wcount[w]) continue;
@@ -384,7 +376,7 @@ gwo_status Handle::log_resolve_split() {
         Wn.records -= c;
     }
     std::vector<uint64_t> counts = L.pend.counts;
-    return log_split_exact(L.pend.base, L.pend.nunits, L.pend.cap, L.pend.k1grid, counts.data(), L.pend.tmpx);
+    return log_split_exact(L.pend.base, L.pend.nunits, L.pend.cap, counts.data(), L.pend.tmpx);
 }
 
 // Upper bound of the segment records one window receives from a batch of n records: the device plan
@@ -467,11 +459,10 @@ gwo_status Handle::log_k1(LogJob &J, bool first_pass) {
         ca.cnt[w] = d.cnt;
     }
     DevBuf &tmp = L.tmp[J.slot];
-    const int k1grid = log_k1_grid(J.n);
-    if (tmp.bytes < log_tmp_bytes(J.nunits * LOG_ND, k1grid, J.cap, W)) {
+    if (tmp.bytes < (size_t)J.nunits * LOG_ND * LOG_XG * J.cap * W * 8) {
         GWO_TRY(log_resolve_split());   // ensure_buf may free: nothing may still read it
         // sized for LOG_NU windows, so a batch spanning more windows than the last one does not reallocate
-        GWO_TRY(ensure_buf(tmp, log_tmp_bytes(std::max(J.nunits, LOG_NU) * LOG_ND, k1grid, J.cap, W)));
+        GWO_TRY(ensure_buf(tmp, (size_t)std::max(J.nunits, LOG_NU) * LOG_ND * LOG_XG * J.cap * W * 8));
     }
     const bool side = first_pass && side_enabled();
     LogThr thr = log_thresholds(J);
@@ -503,7 +494,7 @@ gwo_status Handle::log_k1(LogJob &J, bool first_pass) {
         const uint64_t grid = ((uint64_t)J.n + LOG_TILE - 1) / LOG_TILE + (uint64_t)J.nunits * LOG_ND;
         L.h_split_flag[J.slot] = 0;
         prof_begin(GWO_KERNEL_PARTITION);
-        launch_log_split((const int64_t *)tmp.ptr, J.cap, k1grid, needs_value, L.bk(J.slot), J.nunits * LOG_ND, set,
+        launch_log_split((const int64_t *)tmp.ptr, J.cap, needs_value, L.bk(J.slot), J.nunits * LOG_ND, set,
                          L.d_split_flag + J.slot, (uint32_t)grid, L.d_go + J.slot, stream);
         GWO_TRY(launch_ok("log split"));
         prof_end(GWO_KERNEL_PARTITION, J.n);
@@ -654,8 +645,8 @@ gwo_status Handle::log_resolve_batch(LogJob &J, bool &refire) {
             }
         }
         const uint64_t maxc = rbp[LOG_RB_MAXREG];
-        if (maxc > J.cap) {   // a run overflowed its capacity (skewed keys): redo this range exactly
-            J.cap = (maxc + LOG_RUN_ALIGN - 1) / LOG_RUN_ALIGN * LOG_RUN_ALIGN;
+        if (maxc > J.cap) {   // a region overflowed its capacity (skewed keys): redo this range exactly
+            J.cap = maxc;
             GWO_TRY(log_k1(J, false));
             continue;
         }
@@ -716,7 +707,7 @@ gwo_status Handle::insert_log(const int64_t *k, const int64_t *t, const int64_t 
     if (slog) GWO_TRY(slog_reserve(n));
     J.base = hist_hint;
     J.nunits = (int)std::min<long long>(LOG_NU, std::max<long long>(1, L.span_hint));
-    J.cap = run_capacity((double)n / ((double)LOG_ND * log_k1_grid(n)));
+    J.cap = group_capacity((double)n / ((double)LOG_ND * LOG_XG));
     // speculative pass 2 (no host round trip between K1 and pass 2) unless late records go to the side output
     // (K1's first pass appends them; a re-run must not repeat that)
     J.spec = !side_enabled();
@@ -854,7 +845,7 @@ gwo_status Handle::fire_log(int64_t new_wm) {
         prof_begin(GWO_KERNEL_FIRE, fs);
         launch_log_fire((const LogSegDesc *)L.firedesc.ptr + at, (int)W.segs.size(), W.lp, needs_value, plan, rplan,
                         start, end, o, L.d_overflow, L.max_groups, async_fire ? 1 : 2, W.partial.rec ? 1 : 0, W.partial,
-                        fs);
+                        L.d_slow, L.d_slow + LOG_SLOW_CAP, fs);
         GWO_TRY(launch_ok("log fire"));
         prof_end(GWO_KERNEL_FIRE, (int64_t)W.records, fs);
         at += W.segs.size();
@@ -894,7 +885,7 @@ gwo_status Handle::finish_fire() {
             int64_t end = (int64_t)((uint64_t)start + (uint64_t)cfg.size);
             launch_log_fire((const LogSegDesc *)L.firedesc.ptr + at, (int)W.segs.size(), W.lp, needs_value, plan,
                             rplan, start, end, o, L.d_overflow, L.max_groups, 2, W.partial.rec ? 1 : 0, W.partial,
-                            stream);
+                            L.d_slow, L.d_slow + LOG_SLOW_CAP, stream);
             GWO_TRY(launch_ok("log fire"));
             at += W.segs.size();
         }
@@ -991,7 +982,7 @@ gwo_status Handle::log_fold_raw(const std::vector<long long> &units, const SnapC
         const int64_t start = unit_start(u);
         const int64_t end = (int64_t)((uint64_t)start + (uint64_t)log_usize());   // sliding: the pane
         launch_log_fire((const LogSegDesc *)L.firedesc.ptr + at, (int)W.segs.size(), W.lp, needs_value, plan, raw, start,
-                        end, o, L.d_overflow, L.max_groups, 2, 1, W.partial, stream);
+                        end, o, L.d_overflow, L.max_groups, 2, 1, W.partial, L.d_slow, L.d_slow + LOG_SLOW_CAP, stream);
         GWO_TRY(launch_ok("log fold"));
         at += W.segs.size();
     }

@@ -8,8 +8,8 @@
 #define LOG_SLOTS 3              // batch buffers: K1 in flight (pipelined), deferred pass 2, next K1
 #ifndef LOG_K1_PER
 #define LOG_K1_PER 16            // K1 tile: up to 256 threads x 16 records (64 KiB of 16-B records in LDS, two
-#define LOG_K1_THREADS 256       // workgroups per CU); a launch's tiles are sized so every workgroup loops over
-#endif                           // the same number of them (log_k1_tile)
+#endif                           // workgroups per CU); a launch's tiles are sized so every workgroup loops over
+#define LOG_K1_THREADS 256       // the same number of them (log_k1_tile)
 #define LOG_K1_TILE (LOG_K1_PER * LOG_K1_THREADS)
 #ifndef LOG_K1_GRID
 #define LOG_K1_GRID 512          // K1 workgroups: 2 per CU on MI355X's 256 CUs, all resident, each looping over
@@ -34,16 +34,14 @@ static_assert(LOG_K1_TILE <= 65536, "K1 ranks within a tile are 16-bit");
 #define LOG_MAX_LP (LOG_DB + 10 < 18 ? LOG_DB + 10 : 18)   // <= 1024 partitions per coarse digit (pass-2 LDS)
 #define LOG_FIRE_THREADS 512
 #define LOG_CUR_STRIDE 16        // K1 bucket cursors: one per 128-B line (memory-side atomics serialise per line)
-// K1's batch buffer: one run per (bucket, workgroup) -- bucket b's records from workgroup w at
-// tmp + ((b * G + w) * cap) * W words (G = the launch's workgroups, log_k1_grid; cap = records per run, a multiple of
-// LOG_RUN_ALIGN so every run starts on a 128-B line).  A workgroup appends each tile's records of a bucket to its own
-// run (the cursor is the owning thread's register: no reservation round trip per tile), so a run's lines fill up in
-// the L2 of one XCD, written whole.  Behind the runs, the count table: [nb * G] uint32, run (b, w) at b * G + w.
-// (r03's layout -- one region per bucket, a device-scope atomic reservation per tile -- put that atomic's round
-// trip, queued behind the whole chip's traffic, on every tile's critical path, and merged partial lines of
-// neighbouring runs from different XCDs in HBM: 1.22x the algorithmic writes.)
-#define LOG_XG 1
-#define LOG_RUN_ALIGN 8
+#ifndef LOG_XG
+#define LOG_XG 1                 // K1 region groups per bucket: workgroup w appends to group w % LOG_XG.  With 8
+                                 // (workgroups w and w + 8 share an XCD) each group's runs merge in one L2: K1 alone
+                                 // ran 13 % faster in isolation, but end to end K1 + pass 2 measured 221 + 100 us (1
+                                 // group), 224 + 122 (4), 223 + 134 (8) per C4 batch -- so one group.  (r04: one run per
+                                 // (bucket, workgroup), no reservation atomics, a count table read by pass 2 through a
+                                 // binary search: K1 -5 us, pass 2 +13 us, writes 1.22x -> 1.17x -- reverted.)
+#endif
 #define FIRE_RPT 7                                   // records per thread in the fire's register prefetch
 #define FIRE_RCAP (FIRE_RPT * LOG_FIRE_THREADS)      // 3584: records per partition of the fire's fast path
 #define FIRE_OWN_LOG2 13
@@ -52,6 +50,7 @@ static_assert(LOG_K1_TILE <= 65536, "K1 ranks within a tile are 16-bit");
 #ifndef LOG_PART_FILL
 #define LOG_PART_FILL 7          // a new window's partitions are sized for LOG_PART_FILL/8 of FIRE_RCAP records
 #endif
+#define LOG_SLOW_CAP (1 << LOG_MAX_LP)   // partitions of a window (the fire's slow-path list)
 #define LOG_MAX_SEGS 512         // segments (batches) per window that one fire folds (= LOG_FIRE_THREADS)
 
 // One segment = the records one batch appended to one window.  Partition p's records are
@@ -134,7 +133,6 @@ struct CollectArgs {
 // workgroup on one word cost ~25 us at the end of a 512-workgroup launch); the tail folds the shards.
 #define LOG_SHARDS 16
 enum : int { K1S_MIN = 0, K1S_MAX, K1S_ACC, K1S_LATE, K1S_REFIRE, K1S_BADTS, K1S_BADKG, K1S_HOUT, K1S_BADR, K1S_NEXT,
-             K1S_MAXRUN,   // the largest (bucket, workgroup) run (> cap: records were dropped, the host re-runs K1)
              K1_SW };
 static constexpr size_t LOG_DONE_WORDS = (LOG_SHARDS + 1) * LOG_CUR_STRIDE;
 
@@ -181,7 +179,6 @@ static inline int64_t log_rt_tbase(int64_t wm) { return wm == (int64_t)0x8000000
 
 namespace gwo {
 int log_k1_grid(int64_t n);                                    // K1 workgroups for n records
-size_t log_tmp_bytes(int nb, int grid, uint64_t cap, int w);   // K1's batch buffer: runs + count table
 // K1: classify + key-group check + late accounting + (window, coarse digit) grouping of a batch; its last
 // workgroup writes the readback block and the device plan of pass 2, and resets cursors and statistics.
 // key/ts/val columns with `stride` int64 words between records (1: SoA columns; 3: {key, ts, value} records)
@@ -195,7 +192,7 @@ void launch_log_part(const int64_t *key, const int64_t *ts, const int64_t *val, 
 // Pass 2: every coarse bucket -> its window's segment, grouped by partition.  `overflow` is a
 // host-visible flag (set to 1 when a partition exceeds its capacity).  go != NULL: a speculative launch
 // of `nchunks` (an upper bound) workgroups that exits unless *go (K1's verdict) is set.
-void launch_log_split(const int64_t *tmp, uint64_t cap, int k1grid, int has_val, const LogBucket *buckets, int nb,
+void launch_log_split(const int64_t *tmp, uint64_t cap, int has_val, const LogBucket *buckets, int nb,
                       const LogSegSet &segs, unsigned *overflow, uint32_t nchunks, const unsigned *go, hipStream_t s);
 int log_fire_cap_log2(int nwords);
 // Loads the fire and pass-2 code objects with empty launches (HIP loads a kernel's code on its first launch:
@@ -209,5 +206,6 @@ void ktrace_report();
 // partition takes the LDS hash-table path (a checkpoint fold with a raw-word result plan: up to 8 columns).
 void launch_log_fire(const LogSegDesc *segs, int nseg, int lp, int has_val, const AccPlan &plan,
                      const ResultPlan &rp, int64_t start, int64_t end, OutCols out, unsigned long long *overflow,
-                     int cus, int max_per_cu, int slow_only, const LogSegDesc &partial, hipStream_t s);
+                     int cus, int max_per_cu, int slow_only, const LogSegDesc &partial, uint32_t *slow_list,
+                     uint32_t *slow_cnt, hipStream_t s);   // slow_list: [2^lp] partitions + slow_cnt, device scratch
 }  // namespace gwo

@@ -193,9 +193,13 @@ __device__ __forceinline__ void k1_plan_tail(unsigned long long *cursor, BatchSt
     static_assert(SW <= K1_T0 && K1_T1 + LOG_SHARDS + 1 <= LOG_K1_THREADS, "statistics words");
     __shared__ unsigned long long s_sw[SW];
     __shared__ unsigned s_bad;
+    __shared__ unsigned long long s_maxreg;
     const int t = threadIdx.x;
     unsigned long long *sw = (unsigned long long *)st;
-    if (t == 0) s_bad = 0;
+    if (t == 0) {
+        s_bad = 0;
+        s_maxreg = 0;
+    }
     // the launch's bucket counts (cursors reset for the next K1): every exchange in flight before any is used
     unsigned long long cq[LOG_NU][LOG_XG];
 #pragma unroll
@@ -225,7 +229,7 @@ __device__ __forceinline__ void k1_plan_tail(unsigned long long *cursor, BatchSt
         const int f = t - K1_T0;
         const unsigned long long init = (f == K1S_MIN || f == K1S_NEXT) ? 0x7fffffffffffffffull
                                                                         : (f == K1S_MAX ? 0x8000000000000000ull : 0ull);
-        const int kind = (f == K1S_MIN || f == K1S_NEXT) ? 1 : ((f == K1S_MAX || f == K1S_MAXRUN) ? 2 : 0);
+        const int kind = (f == K1S_MIN || f == K1S_NEXT) ? 1 : (f == K1S_MAX ? 2 : 0);
         s_k1[f] = xchg_fold<LOG_SHARDS>(&a.shard[f], LOG_CUR_STRIDE, init, kind);
     } else if (t >= K1_T1 && t < K1_T1 + LOG_SHARDS + 1) {   // arrival counters start the next K1 at zero
         atomicExch(&a.done[(t - K1_T1) * LOG_CUR_STRIDE], 0ull);
@@ -249,7 +253,7 @@ __device__ __forceinline__ void k1_plan_tail(unsigned long long *cursor, BatchSt
     const BatchStats &S = *(const BatchStats *)s_sw;
     unsigned long long chunk_run = 0;
     unsigned bad = 0;
-    const unsigned long long maxrun = s_k1[K1S_MAXRUN];   // the largest (bucket, workgroup) run
+    unsigned long long maxreg = 0;
 #pragma unroll
     for (int q = 0; q < LOG_NU; ++q) {   // window q of the launch: bucket b = q * LOG_ND + t (digit t)
         if (q >= a.nunits) break;
@@ -263,6 +267,7 @@ __device__ __forceinline__ void k1_plan_tail(unsigned long long *cursor, BatchSt
         for (int x = 0; x < LOG_XG; ++x) {
             xoff[x] = (uint32_t)n_b;
             n_b += c[x];
+            maxreg = c[x] > maxreg ? c[x] : maxreg;
         }
         if (dig) rb_put(&a.rb[b], n_b);
         uint32_t pcap = 0, chunks = 0;
@@ -291,8 +296,9 @@ __device__ __forceinline__ void k1_plan_tail(unsigned long long *cursor, BatchSt
         }
         chunk_run += chk_tot;
     }
-    if (maxrun > a.cap) bad = 1;           // K1 dropped records past a run: the host re-runs K1
+    if (maxreg > a.cap) bad = 1;           // K1 dropped records past a region: the host re-runs K1
     if (bad) atomicOr(&s_bad, 1u);
+    if (maxreg) atomicMax(&s_maxreg, maxreg);
     __syncthreads();
     if (t == 0) {
         LogBucket E{};
@@ -303,7 +309,7 @@ __device__ __forceinline__ void k1_plan_tail(unsigned long long *cursor, BatchSt
                         S.min_idx >= base && S.min_idx < base + a.nunits && chunk_run < (1ull << 32);
         *a.go = go ? 1u : 0u;
         rb_put(&a.rb[LOG_RB_GO], go ? 1ull : 0ull);
-        rb_put(&a.rb[LOG_RB_MAXREG], maxrun);
+        rb_put(&a.rb[LOG_RB_MAXREG], s_maxreg);
         rb_put(&a.rb[LOG_RB_RMAX], s_rmax[0]);
         rb_put(&a.rb[LOG_RB_RWMAX], s_rmax[1]);
     }
@@ -317,9 +323,9 @@ __device__ __forceinline__ void k1_plan_tail(unsigned long long *cursor, BatchSt
 
 // ------------------------------------------------------------------------------------------------
 // K1 log_part: batch -> batch buffer, grouped by bucket b = (window - base) * LOG_ND + coarse digit.
-// Workgroup w appends bucket b's records to its run (b, w) of cap records (gwo_log.h); at the end it writes the
-// run's count to the count table and adds it to the bucket's total (cursor[b * LOG_CUR_STRIDE]); a count above
-// cap (skewed keys) dropped records, and the host re-runs K1 with cap = the largest run.
+// Bucket b owns LOG_XG regions of cap records; workgroup w appends to region group x = w % LOG_XG at
+// records [(b * LOG_XG + x) * cap, ...), whose cursor cursor[(b * LOG_XG + x) * LOG_CUR_STRIDE] ends as its
+// record count (also when it exceeds cap: those records are not written and the host reruns).
 // ------------------------------------------------------------------------------------------------
 // ROUTE: the multi-GPU instance (LogRoute): records of other GPUs are routed (rt.mode 1) or skipped (2).
 // TS32: `ts` holds int32 timestamps - th.tbase (records received in the 20-B wire format; S == 1).
@@ -360,11 +366,8 @@ __global__ __launch_bounds__(LOG_K1_THREADS) void log_part_kernel(
     const int nr = ROUTE ? rt.nranks : 0;
     const int per = (nb + LOG_K1_THREADS - 1) / LOG_K1_THREADS;   // counters owned per thread (<= 4)
     const int tid = threadIdx.x;
+    const int xg = blockIdx.x % LOG_XG;                           // region group (an XCD under round-robin placement)
     const uint32_t cap32 = cap < 0xffffffffull ? (uint32_t)cap : 0xffffffffu;
-    // this workgroup's runs: bucket b's at tmp + ((b * G + w) * cap) * W; thread tid * per + q's cursor in cur[q]
-    int64_t *const runs = tmp + (uint64_t)blockIdx.x * cap * W;
-    const uint64_t bstride = (uint64_t)gridDim.x * cap * W;   // words from one bucket's runs to the next's
-    uint32_t cur[4] = {0u, 0u, 0u, 0u};
     long long mn = 0x7fffffffffffffffLL, mx = (long long)0x8000000000000000LL;   // accepted windows (slow path)
     long long nx = 0x7fffffffffffffffLL;   // first accepted window after the launch's range (slow path)
     uint32_t wmask = 0;   // launch windows (bit jj) the inline path accepted records into
@@ -392,11 +395,13 @@ __global__ __launch_bounds__(LOG_K1_THREADS) void log_part_kernel(
     // write phase): the loop's waits are then counted the same on entry as on the back edge (the compiler takes the
     // smaller count where paths merge, and zero stores after the loads made each tile wait for all of its memory
     // operations -- the previous tile's store acknowledgements and the reservation atomics -- before the scatter)
+#ifndef GWO_K1_NO_TRASH
 #pragma unroll
     for (int j = 0; j < LOG_K1_TILE / LOG_K1_THREADS; ++j) {   // (distinct words: not merged into one store)
         if (HASV) *(ll2 *)(trash + 2 * j) = ll2{0, 0};
         else trash[2 * j] = 0;
     }
+#endif
     // the launch's window bounds as scalars (a run-time index into the argument, th.bound[nunits], is a scalar load
     // per record, and its lgkmcnt wait also waited for the record's LDS atomic)
     const int64_t tb0 = th.bound[0], tb1 = th.bound[1], tb2 = th.bound[2], tb3 = th.bound[3];
@@ -525,13 +530,15 @@ __global__ __launch_bounds__(LOG_K1_THREADS) void log_part_kernel(
         kt.stamp(1);
         lds_barrier();
         kt.stamp(2);
-        // each bucket's place in this workgroup's run: the owning thread's cursor (no device-wide reservation)
-        uint32_t at[4];
+        // reserve each bucket's run in this workgroup's region group, before the offsets scan, so that the
+        // atomics' round trip overlaps the scan and the LDS scatter (q < per is uniform: no per-lane branch, so the
+        // results are waited for only where they are used, after the next tile's loads are issued)
+        unsigned long long at[4];   // (no initial value: a merge with one would wait for the atomic at the branch)
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const int b = tid * per + q;
-            at[q] = cur[q];
-            cur[q] += (q < per && b < nb) ? s_cnt[b] : 0u;
+            if (q < per) at[q] = atomicAdd(&cursor[((size_t)b * LOG_XG + xg) * LOG_CUR_STRIDE],
+                                           (unsigned long long)(b < nb ? s_cnt[b] : 0u));
         }
         unsigned long long rat = 0;
         if (ROUTE && (rt.mode == 1 || rt.mode == 3) && tid < nr) {
@@ -583,14 +590,20 @@ __global__ __launch_bounds__(LOG_K1_THREADS) void log_part_kernel(
         }
         // next tile in flight during the writes: unconditional (past the end every lane re-reads record 0, one line),
         // so the write phase's waits count exactly these loads instead of waiting for all of them
+#ifndef GWO_K1_DELTA_FIRST
         load_tile(tile + tstride);
-        // s_cnt[b] := the tile's first record in the run - the bucket's tile offset, so the write phase finds a
-        // record's destination with one read (mod 2^32: q = s_cnt[b] + p; q >= cap: past the run, dropped)
+#endif
+        // s_cnt[b] := the run's first region record - the bucket's tile offset, so the write phase finds a record's
+        // destination with one read (mod 2^32: q = s_cnt[b] + p; at >= cap -> q >= cap, the run is dropped).  The
+        // atomics precede the loads just issued: their wait is vmcnt(loads), in order, not a wait for the loads.
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             int b = tid * per + q;
-            if (q < per && loc[q]) s_cnt[b] = (at[q] < cap32 ? at[q] : cap32) - lof[q];
+            if (q < per && loc[q]) s_cnt[b] = (at[q] < cap32 ? (uint32_t)at[q] : cap32) - lof[q];
         }
+#ifdef GWO_K1_DELTA_FIRST   // (A/B: r03's order)
+        load_tile(tile + tstride);
+#endif
         lds_barrier();
         kt.stamp(4);
         // write phase: straight-line code (a loop here made the compiler wait for every prefetched load first),
@@ -621,28 +634,21 @@ __global__ __launch_bounds__(LOG_K1_THREADS) void log_part_kernel(
 #else
                 const bool ok = pp[u] < total && bb[u] < (uint32_t)nb && q < cap32;
 #endif
-                int64_t *dst = ok ? runs + bb[u] * bstride + (uint64_t)q * W : trash;
+#ifdef GWO_K1_NO_TRASH   // (A/B: r03's predicated stores)
+                if (ok) {
+                    int64_t *dst = tmp + (((uint64_t)bb[u] * LOG_XG + xg) * cap + q) * W;
+                    if (HASV) *(ll2 *)dst = rr[u];
+                    else *dst = r1[u];
+                }
+#else
+                int64_t *dst = ok ? tmp + (((uint64_t)bb[u] * LOG_XG + xg) * cap + q) * W : trash;
                 if (HASV) *(ll2 *)dst = rr[u];
                 else *dst = r1[u];
+#endif
             }
         }
         lds_barrier();
         kt.stamp(5);
-    }
-    // the runs' counts: the count table (pass 2 finds a bucket's records through it) and the buckets' totals (the
-    // tail's plan); a route-only re-run wrote no run and leaves the first K1's table alone
-    unsigned long long maxrun = 0;
-    if (!(ROUTE && rt.mode == 3)) {
-        uint32_t *const tab = (uint32_t *)(tmp + (uint64_t)nb * gridDim.x * cap * W);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int b = tid * per + q;
-            if (q < per && b < nb) {
-                tab[(uint64_t)b * gridDim.x + blockIdx.x] = cur[q];
-                if (cur[q]) atomicAdd(&cursor[(size_t)b * LOG_XG * LOG_CUR_STRIDE], (unsigned long long)cur[q]);
-                maxrun = cur[q] > maxrun ? cur[q] : maxrun;
-            }
-        }
     }
     if (wmask) {
         const long long lo = base + __builtin_ctz(wmask), hi = base + 31 - __builtin_clz(wmask);
@@ -651,16 +657,15 @@ __global__ __launch_bounds__(LOG_K1_THREADS) void log_part_kernel(
     }
     // workgroup statistics -> shard blockIdx % LOG_SHARDS (zero words skipped)
     unsigned long long v[K1_SW] = {(unsigned long long)mn, (unsigned long long)mx, acc, late, refire, bad_ts, bad_kg,
-                                   out, bad_range, (unsigned long long)nx, maxrun};
+                                   out, bad_range, (unsigned long long)nx};
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
         const long long a = __shfl_xor((long long)v[K1S_MIN], o), b = __shfl_xor((long long)v[K1S_MAX], o);
         const long long c = __shfl_xor((long long)v[K1S_NEXT], o);
-        const unsigned long long d = __shfl_xor(v[K1S_MAXRUN], o);
         v[K1S_MIN] = a < (long long)v[K1S_MIN] ? (unsigned long long)a : v[K1S_MIN];
         v[K1S_MAX] = b > (long long)v[K1S_MAX] ? (unsigned long long)b : v[K1S_MAX];
         v[K1S_NEXT] = c < (long long)v[K1S_NEXT] ? (unsigned long long)c : v[K1S_NEXT];
-        v[K1S_MAXRUN] = d > v[K1S_MAXRUN] ? d : v[K1S_MAXRUN];
+
 #pragma unroll
         for (int f = K1S_ACC; f < K1S_NEXT; ++f) v[f] += __shfl_xor(v[f], o);
     }
@@ -675,7 +680,7 @@ __global__ __launch_bounds__(LOG_K1_THREADS) void log_part_kernel(
         for (int w = 1; w < LOG_K1_THREADS / 64; ++w) {
             const unsigned long long x = s_st[w][tid];
             if (tid == K1S_MIN || tid == K1S_NEXT) r = (long long)x < (long long)r ? x : r;
-            else if (tid == K1S_MAX || tid == K1S_MAXRUN) r = (long long)x > (long long)r ? x : r;
+            else if (tid == K1S_MAX) r = (long long)x > (long long)r ? x : r;
             else r += x;
         }
         unsigned long long *sh = ca.shard + (blockIdx.x % LOG_SHARDS) * LOG_CUR_STRIDE + tid;
@@ -683,8 +688,6 @@ __global__ __launch_bounds__(LOG_K1_THREADS) void log_part_kernel(
             if ((long long)r != 0x7fffffffffffffffLL) atomicMin((long long *)sh, (long long)r);
         } else if (tid == K1S_MAX) {
             if ((long long)r != (long long)0x8000000000000000LL) atomicMax((long long *)sh, (long long)r);
-        } else if (tid == K1S_MAXRUN) {
-            if (r) atomicMax((long long *)sh, (long long)r);
         } else if (r) {
             atomicAdd(sh, r);
         }
@@ -732,7 +735,7 @@ __global__ __launch_bounds__(LOG_K1_THREADS) void log_part_kernel(
 // ------------------------------------------------------------------------------------------------
 template <bool HASV>
 __global__ __launch_bounds__(LOG_TILE_THREADS) void log_split_kernel(const int64_t *__restrict__ tmp, uint64_t cap,
-                                                                     int k1grid, const LogBucket *__restrict__ bk, int nb,
+                                                                     const LogBucket *__restrict__ bk, int nb,
                                                                      const LogSegSet segs,
                                                                      unsigned *overflow, const unsigned *go) {
     constexpr int W = HASV ? 2 : 1;
@@ -742,9 +745,7 @@ __global__ __launch_bounds__(LOG_TILE_THREADS) void log_split_kernel(const int64
     __shared__ uint16_t s_bk[LOG_TILE];
     __shared__ uint32_t s_cnt[1024];
     __shared__ uint32_t s_off[1024];
-    __shared__ uint32_t s_pref[LOG_K1_GRID];   // the bucket's runs: first record of run w in the bucket
     __shared__ int s_c;
-    static_assert(LOG_K1_GRID <= LOG_TILE_THREADS && (LOG_K1_GRID & (LOG_K1_GRID - 1)) == 0, "one run per thread");
     const int tid = threadIdx.x;
     // this chunk's bucket: the largest c with bk[c].chunk0 <= blockIdx.x (one parallel load of the
     // nb chunk prefixes into LDS, then a binary search there)
@@ -769,37 +770,21 @@ __global__ __launch_bounds__(LOG_TILE_THREADS) void log_split_kernel(const int64
     if (chunk == 0)
         for (int f = tid; f < F; f += LOG_TILE_THREADS) S.off[d * F + f] = B.seg_base + (uint32_t)f * B.pcap;
     for (int f = tid; f < F; f += LOG_TILE_THREADS) s_cnt[f] = 0;
-    {   // the bucket = K1's runs (c, 0 .. G-1) back to back: their first records (the count table, behind the runs)
-        const uint32_t *tab = (const uint32_t *)(tmp + (uint64_t)nb * k1grid * cap * W) + (uint64_t)c * k1grid;
-        const uint32_t rc = tid < k1grid ? min(tab[tid], (uint32_t)cap) : 0u;
-        uint32_t tot;
-        const uint32_t ex = block_excl_scan_dpp<LOG_TILE_THREADS>(rc, &tot);
-        if (tid < LOG_K1_GRID) s_pref[tid] = tid < k1grid ? ex : 0xffffffffu;
-    }
     __syncthreads();
     const uint32_t begin = chunk * LOG_TILE;
     const uint32_t m = min((uint32_t)LOG_TILE, B.n - begin);
     int64_t kk[LOG_TILE_PER], vv[LOG_TILE_PER];
     uint32_t code[LOG_TILE_PER];
-    // record v of the bucket is record v - s_pref[w] of run w, the last run with s_pref[w] <= v (a branch-free
-    // binary search, every record's reads in flight together; an empty run shares its successor's first record and
-    // is passed over, being earlier)
-    uint32_t rv[LOG_TILE_PER], rw[LOG_TILE_PER];
+    // unconditional loads (a lane past the end re-reads the chunk's first record): no branch per load; record v
+    // of the bucket is record v - xoff[x] of region group x, the last group with xoff[x] <= v
 #pragma unroll
     for (int j = 0; j < LOG_TILE_PER; ++j) {
-        const uint32_t i = j * LOG_TILE_THREADS + tid;
-        rv[j] = begin + (i < m ? i : 0u);
-        rw[j] = 0;
-    }
+        uint32_t i = j * LOG_TILE_THREADS + tid;
+        const uint32_t v = begin + (i < m ? i : 0u);
+        int x = 0;
 #pragma unroll
-    for (int step = LOG_K1_GRID / 2; step > 0; step >>= 1)
-#pragma unroll
-        for (int j = 0; j < LOG_TILE_PER; ++j) rw[j] += s_pref[rw[j] + step] <= rv[j] ? (uint32_t)step : 0u;
-    // unconditional loads (a lane past the end re-reads the chunk's first record): no branch per load
-#pragma unroll
-    for (int j = 0; j < LOG_TILE_PER; ++j) {
-        const uint32_t v = rv[j], x = rw[j];
-        const int64_t *src = tmp + (((uint64_t)c * k1grid + x) * cap + (v - s_pref[x])) * W;
+        for (int y = 1; y < LOG_XG; ++y) x += v >= B.xoff[y];
+        const int64_t *src = tmp + (((uint64_t)c * LOG_XG + x) * cap + (v - B.xoff[x])) * W;
         if (HASV) {
             ll2 r2 = __builtin_nontemporal_load((const ll2 *)src);
             kk[j] = r2.x;
@@ -1126,7 +1111,8 @@ __global__ __launch_bounds__(LOG_FIRE_THREADS) __attribute__((amdgpu_waves_per_e
                                                                     AccPlan p, ResultPlan rp, int64_t start,
                                                                     int64_t end, OutCols o,
                                                                     unsigned long long *overflow, int slow_only,
-                                                                    LogSegDesc partial) {
+                                                                    LogSegDesc partial, uint32_t *plist,
+                                                                    uint32_t *pcount) {
     // Dynamic LDS (FIRE_LDS bytes).  Fast path:
     //   s_key [FIRE_RCAP] int64   record keys (record i = r * 512 + tid), then leader keys by row ordinal
     //   s_val [FIRE_RCAP] int64   values grouped by key (after the election; overlays s_own)
@@ -1153,8 +1139,15 @@ __global__ __launch_bounds__(LOG_FIRE_THREADS) __attribute__((amdgpu_waves_per_e
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int cap = 1 << cap_log2;
     FireCtx c{s_dyn, s_dyn + cap, s_side, &s_used, &s_fail, cap, (unsigned)(cap - (cap >> 3))};
-    uint32_t part = blockIdx.x;
-    if (part >= nparts) return;
+    // !PART: the watermark fire's fast path only -- a partition it cannot hold is appended to plist (count *pcount)
+    // and folded by the PART instance launched right behind it over that list (plist set: partitions plist[i]), so
+    // the fast instance carries none of the slow path's code or registers (its scalars had spilled to VGPR lanes:
+    // a v_readlane per use)
+    const bool listed = PART && plist != nullptr;
+    const uint32_t npi = listed ? *pcount : nparts;
+    uint32_t pi = blockIdx.x;
+    if (pi >= npi) return;
+    uint32_t part = listed ? plist[pi] : pi;
     KTrace kt;
     kt.start(__builtin_amdgcn_readfirstlane(threadIdx.x) < 64 && g_kt_on);   // wave 0, uniform (scalar registers)
     for (int s = tid; s < nseg; s += LOG_FIRE_THREADS) s_rp[s] = segs[s].rec;
@@ -1254,8 +1247,9 @@ __global__ __launch_bounds__(LOG_FIRE_THREADS) __attribute__((amdgpu_waves_per_e
     prefetch(!(PART && slow_only));
     while (true) {
         const uint32_t total = s_beg[nseg];
-        const uint32_t nxt = part + gridDim.x;
-        const bool more = nxt < nparts;
+        const uint32_t nxt_i = pi + gridDim.x;
+        const bool more = nxt_i < npi;
+        const uint32_t nxt = listed ? (more ? plist[nxt_i] : 0u) : nxt_i;
         // next partition's segment offsets: in flight while this one is folded (issued after the fast
         // path's first use of rk/rv, so waiting for the prefetch does not wait for them too)
         auto load_next = [&]() {
@@ -1398,9 +1392,14 @@ __global__ __launch_bounds__(LOG_FIRE_THREADS) __attribute__((amdgpu_waves_per_e
             }
         }
         if (total > (uint32_t)FIRE_RCAP) load_next();   // (the fast path loaded them in P0)
-        if (!fast) {
+        if constexpr (!PART) {
+            if (!fast && tid == 0) {   // for the slow instance
+                plist[atomicAdd(pcount, 1u)] = part;
+                atomicAdd(overflow + 1, 1ull);   // slow-path partitions (statistics)
+            }
+        } else if (!fast) {
             // slow path: hash-table rounds over disjoint ranges of hash bits 12..43, direct loads
-            if (tid == 0) atomicAdd(overflow + 1, 1ull);   // slow-path partitions (statistics)
+            if (tid == 0 && !listed) atomicAdd(overflow + 1, 1ull);   // slow-path partitions (statistics)
             __syncthreads();
             fire_clear(c, p);
             __syncthreads();
@@ -1567,6 +1566,7 @@ __global__ __launch_bounds__(LOG_FIRE_THREADS) __attribute__((amdgpu_waves_per_e
             kt.stamp(5);
         }
         if (!more) break;
+        pi = nxt_i;
         part = nxt;
     }
     if (kt.on && blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&g_kt[33], 1ull);
@@ -1612,24 +1612,20 @@ void launch_log_part(const int64_t *key, const int64_t *ts, const int64_t *val, 
 #undef GWO_K1
 }
 
-void launch_log_split(const int64_t *tmp, uint64_t cap, int k1grid, int has_val, const LogBucket *buckets, int nb,
+void launch_log_split(const int64_t *tmp, uint64_t cap, int has_val, const LogBucket *buckets, int nb,
                       const LogSegSet &segs, unsigned *overflow, uint32_t nchunks, const unsigned *go, hipStream_t s) {
     if (nchunks == 0) return;
     if (has_val)
-        hipLaunchKernelGGL(log_split_kernel<true>, dim3(nchunks), dim3(LOG_TILE_THREADS), 0, s, tmp, cap, k1grid, buckets,
-                           nb, segs, overflow, go);
+        hipLaunchKernelGGL(log_split_kernel<true>, dim3(nchunks), dim3(LOG_TILE_THREADS), 0, s, tmp, cap, buckets, nb,
+                           segs, overflow, go);
     else
-        hipLaunchKernelGGL(log_split_kernel<false>, dim3(nchunks), dim3(LOG_TILE_THREADS), 0, s, tmp, cap, k1grid,
-                           buckets, nb, segs, overflow, go);
+        hipLaunchKernelGGL(log_split_kernel<false>, dim3(nchunks), dim3(LOG_TILE_THREADS), 0, s, tmp, cap, buckets, nb,
+                           segs, overflow, go);
 }
 
 int log_k1_grid(int64_t n) {
     int64_t grid = (n + LOG_K1_TILE - 1) / LOG_K1_TILE;
     return (int)(grid < 1 ? 1 : (grid > LOG_K1_GRID ? LOG_K1_GRID : grid));
-}
-
-size_t log_tmp_bytes(int nb, int grid, uint64_t cap, int w) {
-    return (size_t)nb * grid * cap * w * 8 + (size_t)nb * grid * 4;
 }
 
 void warm_log_kernels(int nwords, int has_val, hipStream_t s) {
@@ -1641,12 +1637,17 @@ void warm_log_kernels(int nwords, int has_val, hipStream_t s) {
     if (lds < (size_t)FIRE_LDS) lds = FIRE_LDS;
 #define GWO_WARM_NW(NW)                                                                                            \
     case NW:                                                                                                       \
-        if (has_val)                                                                                               \
+        if (has_val) {                                                                                             \
             hipLaunchKernelGGL((log_fire_kernel<NW, false, true>), dim3(1), dim3(LOG_FIRE_THREADS), lds, s, nullptr, 0, 0u, cl, \
-                               has_val, p, rp, 0, 0, o, nullptr, 0, LogSegDesc{});                                 \
-        else                                                                                                       \
+                               has_val, p, rp, 0, 0, o, nullptr, 0, LogSegDesc{}, nullptr, nullptr);               \
+            hipLaunchKernelGGL((log_fire_kernel<NW, true, true>), dim3(1), dim3(LOG_FIRE_THREADS), lds, s, nullptr, 0, 0u, cl, \
+                               has_val, p, rp, 0, 0, o, nullptr, 0, LogSegDesc{}, nullptr, nullptr);               \
+        } else {                                                                                                   \
             hipLaunchKernelGGL((log_fire_kernel<NW, false, false>), dim3(1), dim3(LOG_FIRE_THREADS), lds, s, nullptr, 0, 0u, cl, \
-                               has_val, p, rp, 0, 0, o, nullptr, 0, LogSegDesc{});                                 \
+                               has_val, p, rp, 0, 0, o, nullptr, 0, LogSegDesc{}, nullptr, nullptr);               \
+            hipLaunchKernelGGL((log_fire_kernel<NW, true, false>), dim3(1), dim3(LOG_FIRE_THREADS), lds, s, nullptr, 0, 0u, cl, \
+                               has_val, p, rp, 0, 0, o, nullptr, 0, LogSegDesc{}, nullptr, nullptr);               \
+        }                                                                                                          \
         break;
     switch (nwords) {
         GWO_WARM_NW(1)
@@ -1671,7 +1672,8 @@ int log_fire_cap_log2(int nwords) {
 
 void launch_log_fire(const LogSegDesc *segs, int nseg, int lp, int has_val, const AccPlan &plan,
                      const ResultPlan &rp, int64_t start, int64_t end, OutCols out, unsigned long long *overflow,
-                     int cus, int max_per_cu, int slow_only, const LogSegDesc &partial, hipStream_t s) {
+                     int cus, int max_per_cu, int slow_only, const LogSegDesc &partial, uint32_t *slow_list,
+                     uint32_t *slow_cnt, hipStream_t s) {
     if (nseg < 0 || nseg > LOG_MAX_SEGS || (nseg == 0 && !partial.rec)) return;   // nothing to fold (defensive)
     static_assert(FIRE_OWN * 4 <= FIRE_RCAP * 12 && FIRE_OWN == (1 << FIRE_OWN_LOG2) && FIRE_RCAP <= 4096 &&
                       FIRE_OWN > FIRE_RCAP, "fire fast-path layout");
@@ -1682,21 +1684,27 @@ void launch_log_fire(const LogSegDesc *segs, int nseg, int lp, int has_val, cons
     // persistent grid: two 64-KiB-LDS workgroups per CU, or fewer to leave room for concurrent kernels
     const uint32_t groups = (uint32_t)cus * (uint32_t)(max_per_cu < 2 ? max_per_cu : 2);
     uint32_t grid = parts < groups ? parts : groups;
+    // the watermark fire: the fast instance lists the partitions it cannot hold, the slow instance folds that list
+    const bool listed = !(partial.rec || slow_only);
+    if (listed) (void)hipMemsetAsync(slow_cnt, 0, 4, s);
 #define GWO_FIRE_NW(NW)                                                                                          \
     case NW:                                                                                                     \
-        if (partial.rec || slow_only) {                                                                          \
-            if (has_val)                                                                                         \
-                hipLaunchKernelGGL((log_fire_kernel<NW, true, true>), dim3(grid), dim3(LOG_FIRE_THREADS), lds, s, segs, nseg, \
-                                   parts, cl, has_val, plan, rp, start, end, out, overflow, slow_only, partial); \
-            else                                                                                                 \
-                hipLaunchKernelGGL((log_fire_kernel<NW, true, false>), dim3(grid), dim3(LOG_FIRE_THREADS), lds, s, segs, nseg, \
-                                   parts, cl, has_val, plan, rp, start, end, out, overflow, slow_only, partial); \
-        } else if (has_val) {                                                                                    \
-            hipLaunchKernelGGL((log_fire_kernel<NW, false, true>), dim3(grid), dim3(LOG_FIRE_THREADS), lds, s, segs, nseg, \
-                               parts, cl, has_val, plan, rp, start, end, out, overflow, slow_only, partial);     \
+        if (has_val) {                                                                                           \
+            if (listed)                                                                                          \
+                hipLaunchKernelGGL((log_fire_kernel<NW, false, true>), dim3(grid), dim3(LOG_FIRE_THREADS), lds, s, segs, \
+                                   nseg, parts, cl, has_val, plan, rp, start, end, out, overflow, 0, partial, slow_list, \
+                                   slow_cnt);                                                                    \
+            hipLaunchKernelGGL((log_fire_kernel<NW, true, true>), dim3(grid), dim3(LOG_FIRE_THREADS), lds, s, segs, nseg, \
+                               parts, cl, has_val, plan, rp, start, end, out, overflow, listed ? 1 : slow_only, partial, \
+                               listed ? slow_list : nullptr, slow_cnt);                                          \
         } else {                                                                                                 \
-            hipLaunchKernelGGL((log_fire_kernel<NW, false, false>), dim3(grid), dim3(LOG_FIRE_THREADS), lds, s, segs, nseg, \
-                               parts, cl, has_val, plan, rp, start, end, out, overflow, slow_only, partial);     \
+            if (listed)                                                                                          \
+                hipLaunchKernelGGL((log_fire_kernel<NW, false, false>), dim3(grid), dim3(LOG_FIRE_THREADS), lds, s, \
+                                   segs, nseg, parts, cl, has_val, plan, rp, start, end, out, overflow, 0, partial, \
+                                   slow_list, slow_cnt);                                                         \
+            hipLaunchKernelGGL((log_fire_kernel<NW, true, false>), dim3(grid), dim3(LOG_FIRE_THREADS), lds, s, segs, \
+                               nseg, parts, cl, has_val, plan, rp, start, end, out, overflow, listed ? 1 : slow_only, \
+                               partial, listed ? slow_list : nullptr, slow_cnt);                                 \
         }                                                                                                        \
         break;
     switch (plan.nwords) {

@@ -31,7 +31,7 @@ struct LogJob {
     WindowGeom g{};              // geometry + watermark at gwo_submit time (classification input)
     long long base = 0;          // first window of the range
     int nunits = 1;
-    uint64_t cap = 0;            // records per (bucket, K1 workgroup) run of the batch buffer (gwo_log.h)
+    uint64_t cap = 0;            // records per (window, coarse digit, region group) region of the batch buffer
     int slot = 0;                // batch buffer / readback slot
     unsigned long long seq = 0;  // readback sequence number of the last K1 launch
     LogSegDesc desc[LOG_NU] = {}; // the range's new segments: counters/offsets carved at launch, records after
@@ -63,11 +63,11 @@ struct LogState {
         unsigned long long after_seq = 0;   // a K1 readback with a higher sequence number follows it
         bool has_event = false;
         uint64_t cap = 0;
-        int k1grid = 1;                     // K1's workgroups (runs per bucket)
         std::vector<uint64_t> counts;
     } pend;
     hipEvent_t ev_split = nullptr;               // after the deferred pass 2 (pipelined mode only)
     unsigned long long seen_seq = 0;             // highest K1 readback sequence number observed complete
+    uint32_t *d_slow = nullptr;                  // [LOG_SLOW_CAP] partitions the fire's fast instance left, then their count
     unsigned *h_split_flag = nullptr;            // pinned, device-written [LOG_SLOTS]: pass-2 overflow flags
     unsigned *d_split_flag = nullptr;            // device view of h_split_flag
     unsigned *d_go = nullptr;                    // [LOG_SLOTS] K1's verdict on the speculative pass 2

@@ -6,19 +6,28 @@ import sys
 from collections import defaultdict
 
 root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out"
-acc = defaultdict(lambda: defaultdict(float))
-cnt = defaultdict(lambda: defaultdict(set))
+vals = defaultdict(lambda: defaultdict(dict))   # kernel -> counter -> dispatch -> value
 for f in sorted(glob.glob(f"{root}/pmc_*/run_counter_collection.csv")):
     for r in csv.DictReader(open(f)):
         k = r["Kernel_Name"].split("(")[0][:48]
         c = r["Counter_Name"]
-        acc[k][c] += float(r["Counter_Value"])
-        cnt[k][c].add(r["Dispatch_Id"])
+        d = vals[k][c]
+        d[r["Dispatch_Id"]] = d.get(r["Dispatch_Id"], 0.0) + float(r["Counter_Value"])
+# per kernel and counter: the mean over the dispatches of at least a tenth of the largest (a launch over an empty or
+# tiny window -- the first fire of a run -- would otherwise halve a full fire's bytes)
+acc = defaultdict(lambda: defaultdict(float))
+cnt = defaultdict(lambda: defaultdict(set))
+for k in vals:
+    for c, d in vals[k].items():
+        top = max(d.values()) if d else 0.0
+        keep = [i for i, x in d.items() if x >= 0.1 * top]
+        acc[k][c] = sum(d[i] for i in keep)
+        cnt[k][c] = set(keep)
 for k in sorted(acc):
     print(k)
     for c in sorted(acc[k]):
         n = len(cnt[k][c])
-        print(f"    {c:28s} {acc[k][c] / n:16.1f}  (per dispatch, {n} dispatches)")
+        print(f"    {c:28s} {acc[k][c] / max(n, 1):16.1f}  (per dispatch, {n} dispatches of >= 1/10 of the largest)")
 
 
 def traffic_json(out_path, root="gpurun_out"):
@@ -35,6 +44,8 @@ def traffic_json(out_path, root="gpurun_out"):
         nf, nw = len(cnt[k]["FETCH_SIZE"]), len(cnt[k]["WRITE_SIZE"])
         fb, wb = f / nf * 1024 * 2, w / nw * 1024
         name = k.split("::")[-1].split("<")[0]
+        if name in res and res[name]["hbm_bytes_per_launch"] >= fb + wb:
+            continue   # (another instance of the kernel, e.g. the fire's near-empty slow-list instance)
         res[name] = {"hbm_bytes_per_launch": fb + wb, "read_bytes": fb, "write_bytes": wb,
                      "launches_measured": nf, "note": "rocprofv3 FETCH_SIZE x2 (gfx950) + WRITE_SIZE, KB->B"}
     json.dump(res, open(out_path, "w"), indent=1)
