@@ -1458,108 +1458,105 @@ __global__ __launch_bounds__(LOG_FIRE_THREADS) __attribute__((amdgpu_waves_per_e
         prefetch(more && !(PART && slow_only));
         kt.stamp(4);
         if (fast) {
-            // P5: one row per leader, in ordinal order.  Thread t takes ordinal t - sh (sh = rbase & 1),
-            // so lanes 2m and 2m+1 own a 16-B-aligned pair of global rows; after a DPP swap within the
-            // pair the even lane stores the pair's key/start/end and the odd lane its results, one 16-B
-            // store per column (8-B stores are issue-bound at about half the bandwidth).  A row whose
-            // partner is outside the partition's run is stored alone, 8 B per column.
+            // P5: one row per leader, in ordinal order.  Each lane takes two consecutive ordinals, so that its rows
+            // are a 16-B-aligned pair of global rows (lane t: ordinals 2t - sh, 2t + 1 - sh with sh = rbase & 1) and
+            // it stores each column of both with one 16-B store (8-B stores are issue-bound at about half the
+            // bandwidth; r03 paired lanes with DPP swaps instead, which cost a fifth of this phase's VALU).  A row
+            // whose partner is outside the partition's run is stored alone, 8 B per column.
             const uint32_t rows = s_tot >> 16;
             const unsigned long long rbase = s_rbase;
             const int sh = (int)(rbase & 1ull);
-            const bool odd = (tid & 1) != 0;
-            for (int base = 0; base < (int)rows + sh; base += LOG_FIRE_THREADS) {
-                const int q = base + tid - sh;
-                const bool valid = q >= 0 && q < (int)rows;
-                int64_t k = 0, res[4] = {0, 0, 0, 0};
-                {   // (reads unconditional, from row 0 for lanes without a row: no LDS read waits at a branch join)
-                    const uint32_t qc = valid ? (uint32_t)q : 0u;
-                    const uint32_t off = s_cnt[qc], nxt = s_cnt[qc + 1];
-                    k = s_key[qc];
-                    const uint32_t n = valid ? nxt - off : 0u;
-                    // the run's count, sum and min/max (of the values, or of their Double.compareTo order
-                    // keys for float64): its first 4 values read together, the rest (rare) in a loop; the plan's
-                    // words are read off them afterwards
-                    int64_t si = 0, mn = 0x7fffffffffffffffLL, mx = (int64_t)0x8000000000000000LL;
-                    double sf = 0.0;
-                    if (has_val) {
-                        int64_t v4[4];
+            // one row's key and results; reads unconditional (from row 0 for a lane without a row: no LDS read waits
+            // at a branch join)
+            auto fold_row = [&](int q, bool valid, int64_t &k, int64_t (&res)[4]) {
+                const uint32_t qc = valid ? (uint32_t)q : 0u;
+                const uint32_t off = s_cnt[qc], nxt = s_cnt[qc + 1];
+                k = s_key[qc];
+                const uint32_t n = valid ? nxt - off : 0u;
+                // the run's count, sum and min/max (of the values, or of their Double.compareTo order keys for
+                // float64): its first 4 values read together, the rest (rare) in a loop; the plan's words are read
+                // off them afterwards
+                int64_t si = 0, mn = 0x7fffffffffffffffLL, mx = (int64_t)0x8000000000000000LL;
+                double sf = 0.0;
+                if (has_val) {
+                    int64_t v4[4];
+#pragma unroll
+                    for (int t = 0; t < 4; ++t) {
+                        const uint32_t ix = off + t < (uint32_t)FIRE_RCAP ? off + t : 0u;
+                        v4[t] = s_val[ix];
+                    }
+                    if (p.value_is_f64) {
 #pragma unroll
                         for (int t = 0; t < 4; ++t) {
-                            const uint32_t ix = off + t < (uint32_t)FIRE_RCAP ? off + t : 0u;
-                            v4[t] = s_val[ix];
+                            const bool in = (uint32_t)t < n;
+                            const int64_t v = v4[t], ok = f64_order_key(v);
+                            sf += in ? __longlong_as_double(v) : 0.0;
+                            mn = (in && ok < mn) ? ok : mn;
+                            mx = (in && ok > mx) ? ok : mx;
                         }
-                        if (p.value_is_f64) {
+                        for (uint32_t t = 4; t < n; ++t) {
+                            const int64_t v = s_val[off + t], ok = f64_order_key(v);
+                            sf += __longlong_as_double(v);
+                            mn = ok < mn ? ok : mn;
+                            mx = ok > mx ? ok : mx;
+                        }
+                    } else {
 #pragma unroll
-                            for (int t = 0; t < 4; ++t) {
-                                const bool in = (uint32_t)t < n;
-                                const int64_t v = v4[t], ok = f64_order_key(v);
-                                sf += in ? __longlong_as_double(v) : 0.0;
-                                mn = (in && ok < mn) ? ok : mn;
-                                mx = (in && ok > mx) ? ok : mx;
-                            }
-                            for (uint32_t t = 4; t < n; ++t) {
-                                const int64_t v = s_val[off + t], ok = f64_order_key(v);
-                                sf += __longlong_as_double(v);
-                                mn = ok < mn ? ok : mn;
-                                mx = ok > mx ? ok : mx;
-                            }
-                        } else {
-#pragma unroll
-                            for (int t = 0; t < 4; ++t) {
-                                const bool in = (uint32_t)t < n;
-                                const int64_t v = v4[t];
-                                si = (int64_t)((uint64_t)si + (uint64_t)(in ? v : 0));
-                                mn = (in && v < mn) ? v : mn;
-                                mx = (in && v > mx) ? v : mx;
-                            }
-                            for (uint32_t t = 4; t < n; ++t) {
-                                const int64_t v = s_val[off + t];
-                                si = (int64_t)((uint64_t)si + (uint64_t)v);
-                                mn = v < mn ? v : mn;
-                                mx = v > mx ? v : mx;
-                            }
+                        for (int t = 0; t < 4; ++t) {
+                            const bool in = (uint32_t)t < n;
+                            const int64_t v = v4[t];
+                            si = (int64_t)((uint64_t)si + (uint64_t)(in ? v : 0));
+                            mn = (in && v < mn) ? v : mn;
+                            mx = (in && v > mx) ? v : mx;
+                        }
+                        for (uint32_t t = 4; t < n; ++t) {
+                            const int64_t v = s_val[off + t];
+                            si = (int64_t)((uint64_t)si + (uint64_t)v);
+                            mn = v < mn ? v : mn;
+                            mx = v > mx ? v : mx;
                         }
                     }
-                    int64_t acc[NW];
-#pragma unroll
-                    for (int w = 0; w < NW; ++w) {
-                        switch (p.op[w]) {
-                            case ACC_ADD_I64: acc[w] = p.src[w] == SRC_ONE ? (int64_t)n : si; break;
-                            case ACC_ADD_F64: acc[w] = __double_as_longlong(sf); break;
-                            case ACC_MIN_I64: acc[w] = p.src[w] == SRC_ONE ? 1 : mn; break;
-                            default: acc[w] = p.src[w] == SRC_ONE ? 1 : mx; break;
-                        }
-                    }
-                    row_results<NW>(rp, acc, res);
                 }
-                const bool pvalid = dpp_swap_pair(valid ? 1 : 0) != 0;
-                const int64_t kp = dpp_swap_pair64(k);
-                int64_t rpv[4];
+                int64_t acc[NW];
 #pragma unroll
-                for (int a = 0; a < 4; ++a) rpv[a] = dpp_swap_pair64(res[a]);
-                if (!valid) continue;
-                const unsigned long long pos = rbase + (unsigned long long)(long long)q;
-                const unsigned long long pb = pos & ~1ull;   // the pair's first row
+                for (int w = 0; w < NW; ++w) {
+                    switch (p.op[w]) {
+                        case ACC_ADD_I64: acc[w] = p.src[w] == SRC_ONE ? (int64_t)n : si; break;
+                        case ACC_ADD_F64: acc[w] = __double_as_longlong(sf); break;
+                        case ACC_MIN_I64: acc[w] = p.src[w] == SRC_ONE ? 1 : mn; break;
+                        default: acc[w] = p.src[w] == SRC_ONE ? 1 : mx; break;
+                    }
+                }
+                row_results<NW>(rp, acc, res);
+            };
+            for (int base = 0; base < (int)rows + sh; base += 2 * LOG_FIRE_THREADS) {
+                const int q0 = base + 2 * tid - sh, q1 = q0 + 1;
+                const bool v0 = q0 >= 0 && q0 < (int)rows, v1 = q1 < (int)rows;
+                if (!v0 && !v1) continue;
+                int64_t k0, k1, r0[4] = {0, 0, 0, 0}, r1[4] = {0, 0, 0, 0};
+                fold_row(q0, v0, k0, r0);
+                fold_row(q1, v1, k1, r1);
+                const unsigned long long pb = rbase + (unsigned long long)(long long)q0;   // even: the pair's first row
 #ifdef GWO_ABL_FIRE_NOSTORE   // ablation (timing experiments only): the emit without its global stores
                 if (pb != ~0ull) continue;
 #endif
-                if (pvalid && (long long)pb + 1 < o.cap) {
-                    if (!odd) {
-                        *(ll2 *)(o.key + pb) = ll2{k, kp};
-                        *(ll2 *)(o.start + pb) = ll2{start, start};
-                        *(ll2 *)(o.end + pb) = ll2{end, end};
-                    } else {
-#pragma unroll
-                        for (int a = 0; a < 4; ++a)
-                            if (a < rp.naggs) *(ll2 *)(o.res[a] + pb) = ll2{rpv[a], res[a]};
-                    }
-                } else if ((long long)pos < o.cap) {
-                    o.key[pos] = k;
-                    o.start[pos] = start;
-                    o.end[pos] = end;
+                if (v0 && v1 && (long long)pb + 1 < o.cap) {
+                    *(ll2 *)(o.key + pb) = ll2{k0, k1};
+                    *(ll2 *)(o.start + pb) = ll2{start, start};
+                    *(ll2 *)(o.end + pb) = ll2{end, end};
 #pragma unroll
                     for (int a = 0; a < 4; ++a)
-                        if (a < rp.naggs) o.res[a][pos] = res[a];
+                        if (a < rp.naggs) *(ll2 *)(o.res[a] + pb) = ll2{r0[a], r1[a]};
+                } else {   // a row alone (first or last of the partition's run)
+                    const unsigned long long pos = v0 ? pb : pb + 1;
+                    if ((long long)pos < o.cap) {
+                        o.key[pos] = v0 ? k0 : k1;
+                        o.start[pos] = start;
+                        o.end[pos] = end;
+#pragma unroll
+                        for (int a = 0; a < 4; ++a)
+                            if (a < rp.naggs) o.res[a][pos] = v0 ? r0[a] : r1[a];
+                    }
                 }
             }
             lds_barrier();   // the next partition overwrites s_key / s_cnt

@@ -14,6 +14,6 @@ for f in $SRC/*.hip; do
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unused-function $EXTRA $FLAGS -c $f -o $OUT/obj/$b.hip.o &
 done
 wait
-for f in $SRC/*.hip; do [ -s $OUT/obj/$(basename $f .hip).hip.o ] && [ $OUT/obj/$(basename $f .hip).hip.o -nt $f ] || { echo "compile failed: $f"; exit 1; }; done
+for f in $SRC/*.hip; do [ -s $OUT/obj/$(basename $f .hip).hip.o ] || { echo "compile failed: $f"; exit 1; }; done   # (obj/ starts empty)
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $OUT/libgwo.so $OUT/obj/*.hip.o $R/build/obj/*.cpp.o -L/opt/rocm/lib -lamdhip64 -lrccl -Wl,-rpath,/opt/rocm/lib
 echo built $OUT/libgwo.so
