@@ -1049,6 +1049,32 @@ __device__ __forceinline__ void emit_row(const ResultPlan &rp, const int64_t (&a
 }
 
 // Result columns of one row from NW accumulator words (ResultPlan: value, f64 order key, avg).
+// row_results on a plan held in scalars (the fire's emit: the plan loaded where it is used, see P5)
+template <int NW>
+__device__ __forceinline__ void row_results_s(int naggs, const int (&kind)[4], const int (&word)[4], int f64,
+                                              const int64_t (&acc)[NW], int64_t (&res)[4]) {
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+        if (a >= naggs) break;
+        const int wi = word[a];
+        int64_t x = acc[0], y = acc[0];
+#pragma unroll
+        for (int w = 1; w < NW; ++w) {
+            if (w == wi) x = acc[w];
+            if (w == wi + 1) y = acc[w];
+        }
+        switch (kind[a]) {
+            case 2:
+            case 3: res[a] = f64 ? f64_from_order_key(x) : x; break;
+            case 4: {
+                double s = f64 ? __longlong_as_double(x) : (double)x;
+                res[a] = __double_as_longlong(s / (double)y);
+                break;
+            }
+            default: res[a] = x; break;
+        }
+    }
+}
 template <int NW>
 __device__ __forceinline__ void row_results(const ResultPlan &rp, const int64_t (&acc)[NW], int64_t (&res)[4]) {
 #pragma unroll
@@ -1105,14 +1131,42 @@ __device__ __forceinline__ uint32_t slot_mix(int64_t k) {
 // HV: the records carry values (16-B records; keys only: 8 B) -- a compile-time choice, since a load into registers
 // chosen at run time between two widths merges the two definitions and waits for the load on the spot (the register
 // prefetch of the next partition had waited for each of its 7 loads in turn).
+// The fire's arguments, one struct: the kernel reads it through the kernarg segment pointer (offset 0), so the emit can
+// load the plan and the output columns where it uses them (see P5).
+struct FireArgs {
+    const LogSegDesc *segs;
+    int nseg;
+    uint32_t nparts;
+    int cap_log2;
+    int has_val;
+    AccPlan p;
+    ResultPlan rp;
+    int64_t start, end;
+    OutCols o;
+    unsigned long long *overflow;
+    int slow_only;
+    LogSegDesc partial;
+    uint32_t *plist;
+    uint32_t *pcount;
+};
+typedef __attribute__((address_space(4))) const FireArgs KFireArgs;   // in the (constant) kernarg segment
+
 template <int NW, bool PART, bool HV>
-__global__ __launch_bounds__(LOG_FIRE_THREADS) __attribute__((amdgpu_waves_per_eu(4, 4))) void log_fire_kernel(const LogSegDesc *__restrict__ segs, int nseg,
-                                                                    uint32_t nparts, int cap_log2, int has_val_arg,
-                                                                    AccPlan p, ResultPlan rp, int64_t start,
-                                                                    int64_t end, OutCols o,
-                                                                    unsigned long long *overflow, int slow_only,
-                                                                    LogSegDesc partial, uint32_t *plist,
-                                                                    uint32_t *pcount) {
+__global__ __launch_bounds__(LOG_FIRE_THREADS) __attribute__((amdgpu_waves_per_eu(4, 4))) void log_fire_kernel(FireArgs A) {
+    const LogSegDesc *__restrict__ segs = A.segs;
+    const int nseg = A.nseg;
+    const uint32_t nparts = A.nparts;
+    const int cap_log2 = A.cap_log2;
+    const int has_val_arg = A.has_val;
+    const AccPlan &p = A.p;
+    const ResultPlan &rp = A.rp;
+    const int64_t start = A.start, end = A.end;
+    const OutCols &o = A.o;
+    unsigned long long *const overflow = A.overflow;
+    const int slow_only = A.slow_only;
+    const LogSegDesc &partial = A.partial;
+    uint32_t *const plist = A.plist;
+    uint32_t *const pcount = A.pcount;
     // Dynamic LDS (FIRE_LDS bytes).  Fast path:
     //   s_key [FIRE_RCAP] int64   record keys (record i = r * 512 + tid), then leader keys by row ordinal
     //   s_val [FIRE_RCAP] int64   values grouped by key (after the election; overlays s_own)
@@ -1468,6 +1522,32 @@ __global__ __launch_bounds__(LOG_FIRE_THREADS) __attribute__((amdgpu_waves_per_e
             const int sh = (int)(rbase & 1ull);
             // one row's key and results; reads unconditional (from row 0 for a lane without a row: no LDS read waits
             // at a branch join)
+            // the plan and the output columns, loaded here (scalar loads from the kernarg segment, behind an opaque
+            // copy of its pointer, once per partition) instead of held in scalar registers across the persistent
+            // loop: they spilled to VGPR lanes, a v_readlane per use.  (The kernarg segment is constant memory, so no
+            // store is taken to alias them.)
+            KFireArgs *KA = (KFireArgs *)__builtin_amdgcn_kernarg_segment_ptr();
+            asm volatile("" : "+s"(KA));
+            int64_t *const okey = KA->o.key, *const ostart = KA->o.start, *const oend = KA->o.end;
+            int64_t *ores[4];
+#pragma unroll
+            for (int a = 0; a < 4; ++a) ores[a] = KA->o.res[a];
+            const long long ocap = KA->o.cap;
+            const int64_t wstart = KA->start, wend = KA->end;
+            int pop[NW], psrc[NW];
+#pragma unroll
+            for (int w = 0; w < NW; ++w) {
+                pop[w] = KA->p.op[w];
+                psrc[w] = KA->p.src[w];
+            }
+            const int vf64 = KA->p.value_is_f64;
+            const int naggs = KA->rp.naggs, rf64 = KA->rp.value_is_f64;
+            int rkind[4], rword[4];
+#pragma unroll
+            for (int a = 0; a < 4; ++a) {
+                rkind[a] = KA->rp.kind[a];
+                rword[a] = KA->rp.word[a];
+            }
             auto fold_row = [&](int q, bool valid, int64_t &k, int64_t (&res)[4]) {
                 const uint32_t qc = valid ? (uint32_t)q : 0u;
                 const uint32_t off = s_cnt[qc], nxt = s_cnt[qc + 1];
@@ -1485,7 +1565,7 @@ __global__ __launch_bounds__(LOG_FIRE_THREADS) __attribute__((amdgpu_waves_per_e
                         const uint32_t ix = off + t < (uint32_t)FIRE_RCAP ? off + t : 0u;
                         v4[t] = s_val[ix];
                     }
-                    if (p.value_is_f64) {
+                    if (vf64) {
 #pragma unroll
                         for (int t = 0; t < 4; ++t) {
                             const bool in = (uint32_t)t < n;
@@ -1520,14 +1600,14 @@ __global__ __launch_bounds__(LOG_FIRE_THREADS) __attribute__((amdgpu_waves_per_e
                 int64_t acc[NW];
 #pragma unroll
                 for (int w = 0; w < NW; ++w) {
-                    switch (p.op[w]) {
-                        case ACC_ADD_I64: acc[w] = p.src[w] == SRC_ONE ? (int64_t)n : si; break;
+                    switch (pop[w]) {
+                        case ACC_ADD_I64: acc[w] = psrc[w] == SRC_ONE ? (int64_t)n : si; break;
                         case ACC_ADD_F64: acc[w] = __double_as_longlong(sf); break;
-                        case ACC_MIN_I64: acc[w] = p.src[w] == SRC_ONE ? 1 : mn; break;
-                        default: acc[w] = p.src[w] == SRC_ONE ? 1 : mx; break;
+                        case ACC_MIN_I64: acc[w] = psrc[w] == SRC_ONE ? 1 : mn; break;
+                        default: acc[w] = psrc[w] == SRC_ONE ? 1 : mx; break;
                     }
                 }
-                row_results<NW>(rp, acc, res);
+                row_results_s<NW>(naggs, rkind, rword, rf64, acc, res);
             };
             for (int base = 0; base < (int)rows + sh; base += 2 * LOG_FIRE_THREADS) {
                 const int q0 = base + 2 * tid - sh, q1 = q0 + 1;
@@ -1540,22 +1620,22 @@ __global__ __launch_bounds__(LOG_FIRE_THREADS) __attribute__((amdgpu_waves_per_e
 #ifdef GWO_ABL_FIRE_NOSTORE   // ablation (timing experiments only): the emit without its global stores
                 if (pb != ~0ull) continue;
 #endif
-                if (v0 && v1 && (long long)pb + 1 < o.cap) {
-                    *(ll2 *)(o.key + pb) = ll2{k0, k1};
-                    *(ll2 *)(o.start + pb) = ll2{start, start};
-                    *(ll2 *)(o.end + pb) = ll2{end, end};
+                if (v0 && v1 && (long long)pb + 1 < ocap) {
+                    *(ll2 *)(okey + pb) = ll2{k0, k1};
+                    *(ll2 *)(ostart + pb) = ll2{wstart, wstart};
+                    *(ll2 *)(oend + pb) = ll2{wend, wend};
 #pragma unroll
                     for (int a = 0; a < 4; ++a)
-                        if (a < rp.naggs) *(ll2 *)(o.res[a] + pb) = ll2{r0[a], r1[a]};
+                        if (a < naggs) *(ll2 *)(ores[a] + pb) = ll2{r0[a], r1[a]};
                 } else {   // a row alone (first or last of the partition's run)
                     const unsigned long long pos = v0 ? pb : pb + 1;
-                    if ((long long)pos < o.cap) {
-                        o.key[pos] = v0 ? k0 : k1;
-                        o.start[pos] = start;
-                        o.end[pos] = end;
+                    if ((long long)pos < ocap) {
+                        okey[pos] = v0 ? k0 : k1;
+                        ostart[pos] = wstart;
+                        oend[pos] = wend;
 #pragma unroll
                         for (int a = 0; a < 4; ++a)
-                            if (a < rp.naggs) o.res[a][pos] = v0 ? r0[a] : r1[a];
+                            if (a < naggs) ores[a][pos] = v0 ? r0[a] : r1[a];
                     }
                 }
             }
@@ -1632,18 +1712,20 @@ void warm_log_kernels(int nwords, int has_val, hipStream_t s) {
     const int cl = log_fire_cap_log2(nwords);
     size_t lds = (size_t)(1 + nwords) * 8 << cl;
     if (lds < (size_t)FIRE_LDS) lds = FIRE_LDS;
+    FireArgs fa{};   // no partitions: every workgroup returns at once
+    fa.cap_log2 = cl;
+    fa.has_val = has_val;
+    fa.p = p;
+    fa.rp = rp;
+    fa.o = o;
 #define GWO_WARM_NW(NW)                                                                                            \
     case NW:                                                                                                       \
         if (has_val) {                                                                                             \
-            hipLaunchKernelGGL((log_fire_kernel<NW, false, true>), dim3(1), dim3(LOG_FIRE_THREADS), lds, s, nullptr, 0, 0u, cl, \
-                               has_val, p, rp, 0, 0, o, nullptr, 0, LogSegDesc{}, nullptr, nullptr);               \
-            hipLaunchKernelGGL((log_fire_kernel<NW, true, true>), dim3(1), dim3(LOG_FIRE_THREADS), lds, s, nullptr, 0, 0u, cl, \
-                               has_val, p, rp, 0, 0, o, nullptr, 0, LogSegDesc{}, nullptr, nullptr);               \
+            hipLaunchKernelGGL((log_fire_kernel<NW, false, true>), dim3(1), dim3(LOG_FIRE_THREADS), lds, s, fa);      \
+            hipLaunchKernelGGL((log_fire_kernel<NW, true, true>), dim3(1), dim3(LOG_FIRE_THREADS), lds, s, fa);       \
         } else {                                                                                                   \
-            hipLaunchKernelGGL((log_fire_kernel<NW, false, false>), dim3(1), dim3(LOG_FIRE_THREADS), lds, s, nullptr, 0, 0u, cl, \
-                               has_val, p, rp, 0, 0, o, nullptr, 0, LogSegDesc{}, nullptr, nullptr);               \
-            hipLaunchKernelGGL((log_fire_kernel<NW, true, false>), dim3(1), dim3(LOG_FIRE_THREADS), lds, s, nullptr, 0, 0u, cl, \
-                               has_val, p, rp, 0, 0, o, nullptr, 0, LogSegDesc{}, nullptr, nullptr);               \
+            hipLaunchKernelGGL((log_fire_kernel<NW, false, false>), dim3(1), dim3(LOG_FIRE_THREADS), lds, s, fa);     \
+            hipLaunchKernelGGL((log_fire_kernel<NW, true, false>), dim3(1), dim3(LOG_FIRE_THREADS), lds, s, fa);      \
         }                                                                                                          \
         break;
     switch (nwords) {
@@ -1684,24 +1766,35 @@ void launch_log_fire(const LogSegDesc *segs, int nseg, int lp, int has_val, cons
     // the watermark fire: the fast instance lists the partitions it cannot hold, the slow instance folds that list
     const bool listed = !(partial.rec || slow_only);
     if (listed) (void)hipMemsetAsync(slow_cnt, 0, 4, s);
+    FireArgs fa{};
+    fa.segs = segs;
+    fa.nseg = nseg;
+    fa.nparts = parts;
+    fa.cap_log2 = cl;
+    fa.has_val = has_val;
+    fa.p = plan;
+    fa.rp = rp;
+    fa.start = start;
+    fa.end = end;
+    fa.o = out;
+    fa.overflow = overflow;
+    fa.partial = partial;
+    fa.pcount = slow_cnt;
+    FireArgs fs = fa;            // the slow instance: over the fast instance's list, or every partition
+    fa.slow_only = 0;
+    fa.plist = slow_list;
+    fs.slow_only = listed ? 1 : slow_only;
+    fs.plist = listed ? slow_list : nullptr;
 #define GWO_FIRE_NW(NW)                                                                                          \
     case NW:                                                                                                     \
         if (has_val) {                                                                                           \
             if (listed)                                                                                          \
-                hipLaunchKernelGGL((log_fire_kernel<NW, false, true>), dim3(grid), dim3(LOG_FIRE_THREADS), lds, s, segs, \
-                                   nseg, parts, cl, has_val, plan, rp, start, end, out, overflow, 0, partial, slow_list, \
-                                   slow_cnt);                                                                    \
-            hipLaunchKernelGGL((log_fire_kernel<NW, true, true>), dim3(grid), dim3(LOG_FIRE_THREADS), lds, s, segs, nseg, \
-                               parts, cl, has_val, plan, rp, start, end, out, overflow, listed ? 1 : slow_only, partial, \
-                               listed ? slow_list : nullptr, slow_cnt);                                          \
+                hipLaunchKernelGGL((log_fire_kernel<NW, false, true>), dim3(grid), dim3(LOG_FIRE_THREADS), lds, s, fa); \
+            hipLaunchKernelGGL((log_fire_kernel<NW, true, true>), dim3(grid), dim3(LOG_FIRE_THREADS), lds, s, fs);   \
         } else {                                                                                                 \
             if (listed)                                                                                          \
-                hipLaunchKernelGGL((log_fire_kernel<NW, false, false>), dim3(grid), dim3(LOG_FIRE_THREADS), lds, s, \
-                                   segs, nseg, parts, cl, has_val, plan, rp, start, end, out, overflow, 0, partial, \
-                                   slow_list, slow_cnt);                                                         \
-            hipLaunchKernelGGL((log_fire_kernel<NW, true, false>), dim3(grid), dim3(LOG_FIRE_THREADS), lds, s, segs, \
-                               nseg, parts, cl, has_val, plan, rp, start, end, out, overflow, listed ? 1 : slow_only, \
-                               partial, listed ? slow_list : nullptr, slow_cnt);                                 \
+                hipLaunchKernelGGL((log_fire_kernel<NW, false, false>), dim3(grid), dim3(LOG_FIRE_THREADS), lds, s, fa); \
+            hipLaunchKernelGGL((log_fire_kernel<NW, true, false>), dim3(grid), dim3(LOG_FIRE_THREADS), lds, s, fs);  \
         }                                                                                                        \
         break;
     switch (plan.nwords) {
