@@ -1387,18 +1387,22 @@ __global__ __launch_bounds__(LOG_FIRE_THREADS) __attribute__((amdgpu_waves_per_e
             {
                 // P3: exclusive scan over record ids of (count | 1 << 16) at leaders -> each leader's
                 // first value offset (low half) and row ordinal (high half).
-                uint32_t xl[FIRE_RPT];   // exclusive prefix within the wave (one array live across the barriers)
+                // (records in thread-major order -- thread t's FIRE_RPT records, then thread t + 1's: a serial prefix
+                // per thread and one wave scan, instead of a wave scan per register slot)
+                uint32_t xl[FIRE_RPT];   // exclusive prefix within the thread (one array live across the barriers)
+                uint32_t run = 0;
 #pragma unroll
                 for (int r = 0; r < FIRE_RPT; ++r) {   // (an unconditional read: a read under a branch is waited at the join)
                     const uint32_t ow = s_own[sl[r]];   // followers: sl = a record index, a valid slot too
                     const uint32_t x = ((leader >> r) & 1u) ? ((ow >> 12) | 0x10000u) : 0u;
-                    const uint32_t incl = wave_incl_scan(x);
-                    xl[r] = incl - x;
-                    if (lane == 63) s_wsum[r * (LOG_FIRE_THREADS / 64) + wave] = incl;
+                    xl[r] = run;
+                    run += x;
                 }
+                const uint32_t incl = wave_incl_scan(run);
+                if (lane == 63) s_wsum[wave] = incl;
                 lds_barrier();
                 if (wave == 0) {
-                    constexpr int NS = FIRE_RPT * (LOG_FIRE_THREADS / 64);
+                    constexpr int NS = LOG_FIRE_THREADS / 64;
                     const uint32_t w = lane < NS ? s_wsum[lane] : 0u;
                     const uint32_t wi = wave_incl_scan(w);
                     if (lane < NS) s_wsum[lane] = wi - w;
@@ -1406,11 +1410,12 @@ __global__ __launch_bounds__(LOG_FIRE_THREADS) __attribute__((amdgpu_waves_per_e
                     if (lane == 0) s_tot = tot;
                 }
                 lds_barrier();
+                const uint32_t tbase = s_wsum[wave] + incl - run;   // this thread's first record's prefix
                 uint32_t lo[FIRE_RPT];   // leaders: value offset | row ordinal << 16
 #pragma unroll
                 for (int r = 0; r < FIRE_RPT; ++r) {
                     const uint32_t i = r * LOG_FIRE_THREADS + tid;
-                    const uint32_t pre = s_wsum[r * (LOG_FIRE_THREADS / 64) + wave] + xl[r];
+                    const uint32_t pre = tbase + xl[r];
                     lo[r] = pre;
                     if ((leader >> r) & 1u) s_cnt[i] = pre & 0xffffu;
                 }
