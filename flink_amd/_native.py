@@ -104,6 +104,9 @@ SIGNATURES = [
     ("gwo_restore", C.c_int, [_P, C.POINTER(GwoStateRows), C.c_int32, C.c_int64, C.c_int64]),
     ("gwo_export_heap_state", C.c_int, [_P, C.POINTER(GwoHeapStateIds), _P, C.c_int64, _I64P, _P, _I64P]),
     ("gwo_import_heap_state", C.c_int, [_P, C.POINTER(GwoHeapStateIds), _P, C.c_int64, C.c_int64]),
+    ("gwo_export_heap_state_begin", C.c_int, [_P, C.POINTER(GwoHeapStateIds), _I64P, _I64P, _I64P]),
+    ("gwo_export_heap_state_read", C.c_int, [_P, C.c_int64, _P, C.c_int64]),
+    ("gwo_export_heap_state_end", C.c_int, [_P]),
     ("gwo_sync", C.c_int, [_P]),
     ("gwo_wait_fires", C.c_int, [_P]),
     ("gwo_get_stream", C.c_int, [_P, C.POINTER(_P)]),

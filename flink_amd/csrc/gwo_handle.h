@@ -222,6 +222,8 @@ struct Handle {
     gwo_status export_heap_state(const gwo_heap_state_ids *ids, uint8_t *buf, int64_t cap, int64_t *len,
                                  int64_t *kg_offsets, int64_t *wm_out);
     gwo_status import_heap_state(const gwo_heap_state_ids *ids, const uint8_t *buf, int64_t len, int64_t new_wm);
+    std::vector<uint8_t> heap_img;   // gwo_export_heap_state_begin's image (host memory), until _end
+    bool heap_img_open = false;
 
     // String keys (gwo_strings.cpp)
     gwo_status intern_utf16(const uint16_t *chars, const int64_t *offsets, int64_t n, const int64_t **ids);

@@ -488,4 +488,40 @@ gwo_status gwo_import_heap_state(gwo_handle *hh, const gwo_heap_state_ids *ids, 
     return h->import_heap_state(ids, buf, len, watermark);
 }
 
+gwo_status gwo_export_heap_state_begin(gwo_handle *hh, const gwo_heap_state_ids *ids, int64_t *len, int64_t *kg_offsets,
+                                       int64_t *watermark) {
+    if (!hh || !len) return GWO_ERR_INVALID_ARGUMENT;
+    gwo::Handle *h = (gwo::Handle *)hh;
+    if (h->poisoned) return h->poison_status;
+    gwo::DeviceGuard g(h->cfg.device);
+    int64_t n = 0;
+    GWO_TRY(h->export_heap_state(ids, nullptr, 0, &n, nullptr, nullptr));
+    std::vector<uint8_t> img((size_t)std::max<int64_t>(n, 1));
+    GWO_TRY(h->export_heap_state(ids, img.data(), n, &n, kg_offsets, watermark));
+    img.resize((size_t)n);
+    h->heap_img.swap(img);
+    h->heap_img_open = true;
+    *len = n;
+    return GWO_OK;
+}
+
+gwo_status gwo_export_heap_state_read(gwo_handle *hh, int64_t offset, uint8_t *buf, int64_t len) {
+    if (!hh || len < 0 || offset < 0 || (len > 0 && !buf)) return GWO_ERR_INVALID_ARGUMENT;
+    gwo::Handle *h = (gwo::Handle *)hh;
+    if (!h->heap_img_open) return h->fail(GWO_ERR_STATE, "export_heap_state_read: no image (gwo_export_heap_state_begin)");
+    if (offset + len > (int64_t)h->heap_img.size())
+        return h->fail(GWO_ERR_INVALID_ARGUMENT, "export_heap_state_read: [%lld, %lld) past the image (%lld bytes)",
+                       (long long)offset, (long long)(offset + len), (long long)h->heap_img.size());
+    if (len) memcpy(buf, h->heap_img.data() + offset, (size_t)len);
+    return GWO_OK;
+}
+
+gwo_status gwo_export_heap_state_end(gwo_handle *hh) {
+    if (!hh) return GWO_ERR_INVALID_ARGUMENT;
+    gwo::Handle *h = (gwo::Handle *)hh;
+    std::vector<uint8_t>().swap(h->heap_img);
+    h->heap_img_open = false;
+    return GWO_OK;
+}
+
 }  // extern "C"

@@ -238,6 +238,14 @@ gwo_status gwo_export_heap_state(gwo_handle *h, const gwo_heap_state_ids *ids, u
                                  int64_t *kg_offsets, int64_t *watermark);
 gwo_status gwo_import_heap_state(gwo_handle *h, const gwo_heap_state_ids *ids, const uint8_t *buf, int64_t len,
                                  int64_t watermark);
+/* The same image, staged for a host that streams it key group by key group (the Java operator writes each group
+ * into its keyed state backend): _begin builds it in host memory the handle owns and returns its length, each key
+ * group's offset (kg_offsets: one per key group of the range) and the watermark; _read copies [offset, offset + len)
+ * of it; _end releases it (also implied by gwo_destroy).  The device state is not changed. */
+gwo_status gwo_export_heap_state_begin(gwo_handle *h, const gwo_heap_state_ids *ids, int64_t *len, int64_t *kg_offsets,
+                                       int64_t *watermark);
+gwo_status gwo_export_heap_state_read(gwo_handle *h, int64_t offset, uint8_t *buf, int64_t len);
+gwo_status gwo_export_heap_state_end(gwo_handle *h);
 
 gwo_status gwo_sync(gwo_handle *h);
 /* Waits for the fires queued so far only (the log layout and sessions fire asynchronously): afterwards

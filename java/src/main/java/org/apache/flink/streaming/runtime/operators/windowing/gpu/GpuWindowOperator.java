@@ -10,27 +10,44 @@
  * Records are batched into direct columnar buffers pinned once in open() (gwo_host_register); every watermark
  * flushes the batch, advances the GPU watermark, drains the fired rows and forwards the watermark.  Keys are Long, Integer or String
  * (String keys are interned into the handle's device dictionary, gwo.h gwo_submit_utf16).  Checkpoints write the
- * handle's rows (key, window, raw accumulator words, fire-timer flag) into the raw keyed state stream, one
- * section per key group, so rescaling hands every key group to its new owner.
+ * GPU state into WindowOperator's own managed keyed states ("window-contents", "merging-window-set", the
+ * "window-timers" timer service), key group by key group, so a savepoint moves between WindowOperator and this
+ * operator in both directions, and rescaling hands every key group to its new owner.
  */
 package org.apache.flink.streaming.runtime.operators.windowing.gpu;
 
+import org.apache.flink.api.common.state.AggregatingStateDescriptor;
+import org.apache.flink.api.common.state.ListStateDescriptor;
+import org.apache.flink.api.common.typeutils.TypeSerializer;
+import org.apache.flink.api.common.typeutils.base.array.LongPrimitiveArraySerializer;
 import org.apache.flink.api.java.functions.KeySelector;
+import org.apache.flink.api.java.tuple.Tuple2;
+import org.apache.flink.api.java.typeutils.runtime.TupleSerializer;
+import org.apache.flink.core.memory.DataInputDeserializer;
 import org.apache.flink.core.memory.DataInputView;
 import org.apache.flink.core.memory.DataInputViewStreamWrapper;
+import org.apache.flink.core.memory.DataOutputSerializer;
 import org.apache.flink.core.memory.DataOutputView;
-import org.apache.flink.core.memory.DataOutputViewStreamWrapper;
 import org.apache.flink.metrics.Counter;
 import org.apache.flink.runtime.state.KeyGroupRange;
+import org.apache.flink.runtime.state.KeyGroupRangeAssignment;
 import org.apache.flink.runtime.state.KeyGroupStatePartitionStreamProvider;
-import org.apache.flink.runtime.state.KeyedStateCheckpointOutputStream;
 import org.apache.flink.runtime.state.StateInitializationContext;
 import org.apache.flink.runtime.state.StateSnapshotContext;
+import org.apache.flink.runtime.state.VoidNamespace;
+import org.apache.flink.runtime.state.VoidNamespaceSerializer;
+import org.apache.flink.runtime.state.internal.InternalAppendingState;
+import org.apache.flink.runtime.state.internal.InternalListState;
 import org.apache.flink.streaming.api.operators.AbstractStreamOperator;
 import org.apache.flink.streaming.api.operators.BoundedOneInput;
+import org.apache.flink.streaming.api.operators.InternalTimer;
+import org.apache.flink.streaming.api.operators.InternalTimerService;
 import org.apache.flink.streaming.api.operators.OneInputStreamOperator;
+import org.apache.flink.streaming.api.operators.Triggerable;
 import org.apache.flink.streaming.api.watermark.Watermark;
+import org.apache.flink.streaming.api.windowing.windows.TimeWindow;
 import org.apache.flink.streaming.runtime.streamrecord.StreamRecord;
+import org.apache.flink.types.StringValue;
 import org.apache.flink.util.OutputTag;
 
 import java.io.InputStream;
@@ -38,10 +55,16 @@ import java.nio.ByteBuffer;
 import java.nio.ByteOrder;
 import java.nio.charset.StandardCharsets;
 import java.util.ArrayList;
+import java.util.HashSet;
+import java.util.LinkedHashMap;
 import java.util.List;
+import java.util.Map;
+import java.util.Set;
+import java.util.TreeMap;
+import java.util.TreeSet;
 
 public class GpuWindowOperator<IN, K> extends AbstractStreamOperator<GpuWindowResult<K>>
-        implements OneInputStreamOperator<IN, GpuWindowResult<K>>, BoundedOneInput {
+        implements OneInputStreamOperator<IN, GpuWindowResult<K>>, BoundedOneInput, Triggerable<K, TimeWindow> {
 
     private static final long serialVersionUID = 1L;
     private static final long LONG_MIN = Long.MIN_VALUE;
@@ -49,6 +72,7 @@ public class GpuWindowOperator<IN, K> extends AbstractStreamOperator<GpuWindowRe
     private final GpuWindowSpec spec;
     private final KeySelector<IN, K> keySelector;
     private final GpuAggregates.ValueExtractor<IN> valueOf;
+    private final GpuAggregates.Descriptor<IN> fn;   // window-contents' AggregateFunction (its long[] accumulator)
     private final OutputTag<GpuLateRecord<K>> lateTag;   // null: late records are counted and dropped
     private final int batch;
 
@@ -64,13 +88,18 @@ public class GpuWindowOperator<IN, K> extends AbstractStreamOperator<GpuWindowRe
     private transient long lateReported;
     private transient Counter numLateRecordsDropped;   // WindowOperator.java:141,221,424
     private transient int[] resultDtypes;
+    // WindowOperator's keyed states, holding a checkpoint's copy of the GPU state (see snapshotState)
+    private transient InternalAppendingState<K, TimeWindow, IN, long[], Object[]> windowState;
+    private transient InternalListState<K, VoidNamespace, Tuple2<TimeWindow, TimeWindow>> mergingSets;
+    private transient InternalTimerService<TimeWindow> timers;
+    private transient boolean mirrored;
 
-    public GpuWindowOperator(GpuWindowSpec spec, KeySelector<IN, K> keySelector,
-                             GpuAggregates.ValueExtractor<IN> valueOf, OutputTag<GpuLateRecord<K>> lateTag,
-                             int batch) {
+    public GpuWindowOperator(GpuWindowSpec spec, KeySelector<IN, K> keySelector, GpuAggregates.Descriptor<IN> fn,
+                             OutputTag<GpuLateRecord<K>> lateTag, int batch) {
         this.spec = spec;
         this.keySelector = keySelector;
-        this.valueOf = valueOf;
+        this.fn = fn;
+        this.valueOf = fn.value;
         this.lateTag = lateTag;
         this.batch = batch;
     }
@@ -88,8 +117,9 @@ public class GpuWindowOperator<IN, K> extends AbstractStreamOperator<GpuWindowRe
         handle = GwoNative.create(spec.assigner, spec.size, spec.slide, spec.offset, spec.gap, spec.allowedLateness,
                 spec.aggs, spec.valueDtype, spec.keyKind, maxParallelism, range.getStartKeyGroup(),
                 range.getEndKeyGroup(), spec.device, lateTag != null, spec.stateLayout, spec.expectedKeys);
-        if (context.isRestored()) {
-            restoreRows(context);
+        registerWindowStates();
+        if (context.isRestored() && !importMirror()) {
+            restoreRows(context);   // (a savepoint of an earlier version: raw keyed state rows)
         }
     }
 
@@ -156,6 +186,9 @@ public class GpuWindowOperator<IN, K> extends AbstractStreamOperator<GpuWindowRe
     // ---- OneInputStreamOperator ------------------------------------------------------------------------------
     @Override
     public void processElement(StreamRecord<IN> element) throws Exception {
+        if (mirrored) {
+            clearMirror();
+        }
         final IN v = element.getValue();
         final K key = keySelector.getKey(v);
         final int i = n;
@@ -178,6 +211,7 @@ public class GpuWindowOperator<IN, K> extends AbstractStreamOperator<GpuWindowRe
 
     @Override
     public void processWatermark(Watermark mark) throws Exception {
+        clearMirror();   // (before the timer service sees the watermark: the mirror's timers never fire)
         flush();   // the pending records precede the watermark
         GwoNative.advanceWatermark(handle, mark.getTimestamp());
         emitFired();
@@ -186,6 +220,7 @@ public class GpuWindowOperator<IN, K> extends AbstractStreamOperator<GpuWindowRe
 
     @Override
     public void endInput() throws Exception {
+        clearMirror();
         flush();
         GwoNative.advanceWatermark(handle, Long.MAX_VALUE);   // StreamSource.java:122
         emitFired();
@@ -294,55 +329,255 @@ public class GpuWindowOperator<IN, K> extends AbstractStreamOperator<GpuWindowRe
         return spec.keyKind == GwoNative.KEY_INT ? (Object) (int) k : (Object) k;
     }
 
-    // ---- checkpoints: rows per key group in the raw keyed state stream ---------------------------------------
+    // ---- checkpoints: the window state as WindowOperator's managed keyed state --------------------------------
+    // WindowOperator keeps its state in the keyed state backend (WindowOperator.java:224-271): "window-contents" (the
+    // AggregateFunction's accumulator per (key, TimeWindow)), "merging-window-set" (sessions: per key, window -> state
+    // window) and the "window-timers" timer service.  This operator registers the same states with the same
+    // serializers.  At a checkpoint it writes the GPU state into them, one key group at a time from the image
+    // gwo_export_heap_state_begin stages in native memory (the heap backend's section layout, parsed here), so the
+    // backend's snapshot -- taken right after snapshotState (StreamOperatorStateHandler.java:186-198) -- is a savepoint
+    // WindowOperator restores, and a WindowOperator savepoint restores here (initializeState reads the states back
+    // into one gwo_import_heap_state).  The mirror is cleared again at the next record, watermark or close: the GPU
+    // holds the live state, the backend only each checkpoint's copy.
+    private static final short SID_CONTENTS = 0, SID_MERGING = 1, SID_EVENT_TIMERS = 2, SID_PROCESSING_TIMERS = 3;
+
+    private int[] stateIds() {   // gwo_heap_state_ids: this operator's own numbering of the sections it parses
+        final boolean merging = spec.assigner == GwoNative.ASSIGNER_SESSION;
+        return new int[] {SID_CONTENTS, merging ? SID_MERGING : -1, SID_EVENT_TIMERS, SID_PROCESSING_TIMERS};
+    }
+
+    @SuppressWarnings("unchecked")
+    private void registerWindowStates() throws Exception {
+        final TimeWindow.Serializer ws = new TimeWindow.Serializer();
+        windowState = (InternalAppendingState<K, TimeWindow, IN, long[], Object[]>) getOrCreateKeyedState(ws,
+                new AggregatingStateDescriptor<>("window-contents", fn, LongPrimitiveArraySerializer.INSTANCE));
+        if (spec.assigner == GwoNative.ASSIGNER_SESSION) {   // WindowOperator.java:261-271
+            final TupleSerializer<Tuple2<TimeWindow, TimeWindow>> pairs = new TupleSerializer<>(
+                    (Class<Tuple2<TimeWindow, TimeWindow>>) (Class<?>) Tuple2.class, new TypeSerializer[] {ws, ws});
+            mergingSets = (InternalListState<K, VoidNamespace, Tuple2<TimeWindow, TimeWindow>>) getOrCreateKeyedState(
+                    VoidNamespaceSerializer.INSTANCE, new ListStateDescriptor<>("merging-window-set", pairs));
+        }
+        timers = getInternalTimerService("window-timers", ws, this);
+    }
+
+    // The mirror's timers never fire: the mirror is cleared before a watermark reaches the timer service.
+    @Override
+    public void onEventTime(InternalTimer<K, TimeWindow> timer) {}
+
+    @Override
+    public void onProcessingTime(InternalTimer<K, TimeWindow> timer) {}
+
     @Override
     public void snapshotState(StateSnapshotContext context) throws Exception {
         super.snapshotState(context);
         flush();   // prepareSnapshotPreBarrier semantics: the batch is part of the state
-        final long[] bound = GwoNative.snapshotRows(handle);
-        final int words = (int) bound[1];
-        final long capL = Math.max(bound[0], 1);
-        if (capL * Math.max(words, 1) > Integer.MAX_VALUE - 8) {
-            throw new IllegalStateException("GPU window state of " + bound[0] + " rows x " + words
-                    + " words exceeds one Java array; checkpoint it with more subtasks");
+        clearMirror();   // a previous checkpoint's, when no record came in between
+        final KeyGroupRange range = getKeyedStateBackend().getKeyGroupRange();
+        final int groups = range.getNumberOfKeyGroups();
+        final long[] offsets = new long[groups];
+        final long[] watermark = new long[1];
+        final long total = GwoNative.exportHeapStateBegin(handle, stateIds(), offsets, watermark);
+        try {
+            byte[] buf = new byte[1 << 16];
+            for (int g = 0; g < groups; g++) {   // key group by key group: one section in Java memory at a time
+                final long len = (g + 1 < groups ? offsets[g + 1] : total) - offsets[g];
+                if (len > Integer.MAX_VALUE - 8) {
+                    throw new IllegalStateException("key group " + (range.getStartKeyGroup() + g) + " holds " + len
+                            + " bytes of window state; checkpoint it with a larger maxParallelism");
+                }
+                if (buf.length < len) {
+                    buf = new byte[(int) Math.max(len, Math.min(2L * buf.length, Integer.MAX_VALUE - 8))];
+                }
+                GwoNative.exportHeapStateRead(handle, offsets[g], buf, (int) len);
+                mirrorKeyGroup(new DataInputDeserializer(buf, 0, (int) len), range.getStartKeyGroup() + g);
+            }
+        } finally {
+            GwoNative.exportHeapStateEnd(handle);
         }
-        final int cap = (int) capL;
-        final long[] k = new long[cap], s = new long[cap], e = new long[cap], w = new long[cap * Math.max(words, 1)];
-        final int[] kg = new int[cap], tm = new int[cap];
-        final long[] got = GwoNative.snapshot(handle, k, s, e, w, kg, tm, words, cap);
-        final int rows = (int) got[0];
-        final String[] names = spec.keyKind == GwoNative.KEY_STRING ? GwoNative.keyStrings(handle, k, rows) : null;
-        KeyedStateCheckpointOutputStream out = context.getRawKeyedOperatorStateOutput();
-        DataOutputView view = new DataOutputViewStreamWrapper(out);
-        int i = 0;
-        for (int group : out.getKeyGroupList()) {   // the rows arrive grouped by ascending key group
-            out.startNewKeyGroup(group);
-            int j = i;
-            while (j < rows && kg[j] == group) {
-                j++;
-            }
-            view.writeLong(got[1]);   // watermark
-            view.writeInt(words);
-            view.writeInt(j - i);
-            for (int r = i; r < j; r++) {
-                if (names != null) {
-                    byte[] utf = names[r].getBytes(StandardCharsets.UTF_16LE);
-                    view.writeInt(utf.length);
-                    view.write(utf);
+        mirrored = true;
+    }
+
+    // One key group's section (include/gwo.h, gwo_export_heap_state) into the backend's states.
+    private void mirrorKeyGroup(DataInputView in, int group) throws Exception {
+        if (in.readInt() != group) {
+            throw new IllegalStateException("heap-state image out of key-group order at " + group);
+        }
+        final int states = spec.assigner == GwoNative.ASSIGNER_SESSION ? 4 : 3;
+        for (int st = 0; st < states; st++) {
+            final short id = in.readShort();
+            final int n = in.readInt();
+            for (int e = 0; e < n; e++) {
+                if (id == SID_CONTENTS) {   // TimeWindow namespace, key, accumulator
+                    final TimeWindow w = readWindow(in);
+                    setCurrentKey(readKey(in));
+                    windowState.setCurrentNamespace(w);
+                    windowState.updateInternal(readAccumulator(in));
+                } else if (id == SID_MERGING) {   // VoidNamespace, key, (window, state window) pairs
+                    in.readByte();
+                    setCurrentKey(readKey(in));
+                    final int m = in.readInt();
+                    final List<Tuple2<TimeWindow, TimeWindow>> pairs = new ArrayList<>(m);
+                    for (int x = 0; x < m; x++) {
+                        pairs.add(new Tuple2<>(readWindow(in), readWindow(in)));
+                    }
+                    mergingSets.setCurrentNamespace(VoidNamespace.INSTANCE);
+                    mergingSets.update(pairs);
+                } else if (id == SID_EVENT_TIMERS) {   // timestamp (sign bit flipped), key, window
+                    final long ts = in.readLong() ^ Long.MIN_VALUE;
+                    setCurrentKey(readKey(in));
+                    timers.registerEventTimeTimer(readWindow(in), ts);
                 } else {
-                    view.writeLong(k[r]);
-                }
-                view.writeLong(s[r]);
-                view.writeLong(e[r]);
-                view.writeInt(tm[r]);
-                for (int x = 0; x < words; x++) {
-                    view.writeLong(w[r * words + x]);
+                    throw new IllegalStateException("processing-time timer in an event-time window operator");
                 }
             }
-            i = j;
         }
     }
 
+    // The backend's window states -> one gwo_import_heap_state (a WindowOperator savepoint, or this operator's).
+    // Every window with state has a timer (its fire timer, or with allowedLateness its cleanup timer), so the timers
+    // enumerate the (key, window) entries; sessions read their accumulator through the merging window set.
+    @SuppressWarnings("unchecked")
+    private boolean importMirror() throws Exception {
+        final Map<Integer, List<Object[]>> entries = new TreeMap<>();   // key group -> {key, window, accumulator}
+        final Map<Integer, List<Object[]>> timerList = new TreeMap<>(); // key group -> {timestamp, key, window}
+        final Set<Tuple2<Object, TimeWindow>> seen = new HashSet<>();
+        final int maxParallelism = getRuntimeContext().getMaxNumberOfParallelSubtasks();
+        timers.forEachEventTimeTimer((w, ts) -> {
+            final Object key = getCurrentKey();
+            final int group = KeyGroupRangeAssignment.assignToKeyGroup(key, maxParallelism);
+            timerList.computeIfAbsent(group, x -> new ArrayList<>()).add(new Object[] {ts, key, w});
+            if (!seen.add(new Tuple2<>(key, w))) {
+                return;
+            }
+            TimeWindow stateWindow = w;
+            if (mergingSets != null) {
+                mergingSets.setCurrentNamespace(VoidNamespace.INSTANCE);
+                final Iterable<Tuple2<TimeWindow, TimeWindow>> pairs = mergingSets.get();
+                if (pairs != null) {
+                    for (Tuple2<TimeWindow, TimeWindow> pr : pairs) {
+                        if (pr.f0.equals(w)) {
+                            stateWindow = pr.f1;
+                        }
+                    }
+                }
+            }
+            windowState.setCurrentNamespace(stateWindow);
+            final long[] acc = windowState.getInternal();
+            if (acc != null) {
+                entries.computeIfAbsent(group, x -> new ArrayList<>()).add(new Object[] {key, w, acc});
+            }
+        });
+        if (timerList.isEmpty()) {
+            return false;
+        }
+        final DataOutputSerializer out = new DataOutputSerializer(1 << 16);
+        final Set<Integer> groups = new TreeSet<>(entries.keySet());
+        groups.addAll(timerList.keySet());
+        for (int group : groups) {   // sections in the layout mirrorKeyGroup parses, each window its own state window
+            final List<Object[]> es = entries.getOrDefault(group, new ArrayList<>());
+            final List<Object[]> ts = timerList.getOrDefault(group, new ArrayList<>());
+            out.writeInt(group);
+            out.writeShort(SID_CONTENTS);
+            out.writeInt(es.size());
+            for (Object[] e : es) {
+                writeWindow(out, (TimeWindow) e[1]);
+                writeKey(out, e[0]);
+                final long[] acc = (long[]) e[2];
+                out.writeInt(acc.length);
+                for (long x : acc) {
+                    out.writeLong(x);
+                }
+            }
+            if (mergingSets != null) {
+                final Map<Object, List<TimeWindow>> byKey = new LinkedHashMap<>();
+                for (Object[] e : es) {
+                    byKey.computeIfAbsent(e[0], x -> new ArrayList<>()).add((TimeWindow) e[1]);
+                }
+                out.writeShort(SID_MERGING);
+                out.writeInt(byKey.size());
+                for (Map.Entry<Object, List<TimeWindow>> kv : byKey.entrySet()) {
+                    out.writeByte(0);
+                    writeKey(out, kv.getKey());
+                    out.writeInt(kv.getValue().size());
+                    for (TimeWindow w : kv.getValue()) {
+                        writeWindow(out, w);
+                        writeWindow(out, w);
+                    }
+                }
+            }
+            out.writeShort(SID_EVENT_TIMERS);
+            out.writeInt(ts.size());
+            for (Object[] t : ts) {
+                out.writeLong((Long) t[0] ^ Long.MIN_VALUE);
+                writeKey(out, t[1]);
+                writeWindow(out, (TimeWindow) t[2]);
+            }
+            out.writeShort(SID_PROCESSING_TIMERS);
+            out.writeInt(0);
+        }
+        // no watermark is part of WindowOperator's state: the restored operator starts at Long.MIN_VALUE like it
+        GwoNative.importHeapState(handle, stateIds(), out.getCopyOfBuffer(), Long.MIN_VALUE);
+        mirrored = true;   // the backend copy is dropped at the first record or watermark
+        return true;
+    }
+
+    // Drops the backend copy (the GPU holds the state): every window state, merging set and timer of the mirror.
+    private void clearMirror() throws Exception {
+        if (!mirrored) {
+            return;
+        }
+        final List<Object[]> all = new ArrayList<>();
+        timers.forEachEventTimeTimer((w, ts) -> all.add(new Object[] {getCurrentKey(), w, ts}));
+        for (Object[] t : all) {
+            setCurrentKey(t[0]);
+            final TimeWindow w = (TimeWindow) t[1];
+            timers.deleteEventTimeTimer(w, (Long) t[2]);
+            windowState.setCurrentNamespace(w);
+            windowState.clear();
+            if (mergingSets != null) {
+                mergingSets.setCurrentNamespace(VoidNamespace.INSTANCE);
+                mergingSets.clear();
+            }
+        }
+        mirrored = false;
+    }
+
+    private Object readKey(DataInputView in) throws Exception {
+        switch (spec.keyKind) {
+            case GwoNative.KEY_STRING: return StringValue.readString(in);
+            case GwoNative.KEY_INT: return in.readInt();
+            default: return in.readLong();
+        }
+    }
+
+    private void writeKey(DataOutputView out, Object key) throws Exception {
+        switch (spec.keyKind) {
+            case GwoNative.KEY_STRING: StringValue.writeString((String) key, out); break;
+            case GwoNative.KEY_INT: out.writeInt((Integer) key); break;
+            default: out.writeLong((Long) key); break;
+        }
+    }
+
+    private static TimeWindow readWindow(DataInputView in) throws Exception {
+        final long start = in.readLong();
+        return new TimeWindow(start, in.readLong());
+    }
+
+    private static void writeWindow(DataOutputView out, TimeWindow w) throws Exception {
+        out.writeLong(w.getStart());
+        out.writeLong(w.getEnd());
+    }
+
+    private static long[] readAccumulator(DataInputView in) throws Exception {   // LongPrimitiveArraySerializer
+        final long[] acc = new long[in.readInt()];
+        for (int i = 0; i < acc.length; i++) {
+            acc[i] = in.readLong();
+        }
+        return acc;
+    }
+
+    // Raw keyed state rows of a savepoint taken by an earlier version of this operator (before the managed mirror):
+    // per key group, watermark, words, count, then per row key, start, end, timer, words.
     private void restoreRows(StateInitializationContext context) throws Exception {
         List<Object> key = new ArrayList<>();
         List<long[]> rows = new ArrayList<>();   // start, end, timer, words...

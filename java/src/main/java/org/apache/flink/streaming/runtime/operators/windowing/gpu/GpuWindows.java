@@ -56,6 +56,6 @@ public final class GpuWindows {
         @SuppressWarnings({"unchecked", "rawtypes"})
         TypeInformation<GpuWindowResult<K>> outType = (TypeInformation) TypeInformation.of(GpuWindowResult.class);
         return keyed.transform("GpuWindowOperator", outType,
-                new GpuWindowOperator<>(spec, selector, fn.value, lateTag, 1 << 20));
+                new GpuWindowOperator<>(spec, selector, fn, lateTag, 1 << 20));
     }
 }

@@ -111,6 +111,17 @@ final class GwoNative {
      */
     static native byte[] exportHeapState(long handle, int[] ids, long[] keyGroupOffsets, long[] watermarkOut);
 
+    /**
+     * gwo_export_heap_state_begin: stages that image in native memory; returns its length (keyGroupOffsets and
+     * watermarkOut as for exportHeapState).  exportHeapStateRead copies [offset, offset + len) of it into dst;
+     * exportHeapStateEnd releases it.
+     */
+    static native long exportHeapStateBegin(long handle, int[] ids, long[] keyGroupOffsets, long[] watermarkOut);
+
+    static native void exportHeapStateRead(long handle, long offset, byte[] dst, int len);
+
+    static native void exportHeapStateEnd(long handle);
+
     /** gwo_import_heap_state: key-group sections of that layout; only the handle's KeyGroupRange is kept. */
     static native void importHeapState(long handle, int[] ids, byte[] data, long watermark);
 

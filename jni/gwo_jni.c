@@ -366,6 +366,43 @@ JNIEXPORT jbyteArray JNICALL JFN(exportHeapState)(JNIEnv *env, jclass c, jlong h
     return r;
 }
 
+/* Staged export (gwo_export_heap_state_begin/_read/_end): the operator streams the image key group by key group into
+ * its keyed state backend instead of holding it in one byte[]. */
+JNIEXPORT jlong JNICALL JFN(exportHeapStateBegin)(JNIEnv *env, jclass c, jlong h, jintArray ids, jlongArray kgOffsets,
+                                                 jlongArray watermarkOut) {
+    (void)c;
+    gwo_heap_state_ids sid;
+    gwo_config cfg;
+    if (!heap_ids(env, ids, &sid) || !array_ok(env, watermarkOut, 1, "watermark array")) return -1;
+    if (fail(env, H(h), gwo_get_config(H(h), &cfg))) return -1;
+    if (!array_ok(env, kgOffsets, (jlong)cfg.key_group_end - cfg.key_group_start + 1,
+                  "keyGroupOffsets smaller than the subtask's key-group count"))
+        return -1;
+    jlong *po = (*env)->GetLongArrayElements(env, kgOffsets, NULL);
+    if (!po) return -1;
+    int64_t len = 0, wm = 0;
+    const int bad = fail(env, H(h), gwo_export_heap_state_begin(H(h), &sid, &len, (int64_t *)po, &wm));
+    (*env)->ReleaseLongArrayElements(env, kgOffsets, po, bad ? JNI_ABORT : 0);
+    if (bad) return -1;
+    jlong w = wm;
+    (*env)->SetLongArrayRegion(env, watermarkOut, 0, 1, &w);
+    return (jlong)len;
+}
+
+JNIEXPORT void JNICALL JFN(exportHeapStateRead)(JNIEnv *env, jclass c, jlong h, jlong offset, jbyteArray dst, jint len) {
+    (void)c;
+    if (len < 0 || !array_ok(env, dst, len, "destination smaller than len")) return;
+    jbyte *p = (*env)->GetByteArrayElements(env, dst, NULL);
+    if (!p) return;
+    const int bad = fail(env, H(h), gwo_export_heap_state_read(H(h), offset, (uint8_t *)p, len));
+    (*env)->ReleaseByteArrayElements(env, dst, p, bad ? JNI_ABORT : 0);
+}
+
+JNIEXPORT void JNICALL JFN(exportHeapStateEnd)(JNIEnv *env, jclass c, jlong h) {
+    (void)c;
+    fail(env, H(h), gwo_export_heap_state_end(H(h)));
+}
+
 JNIEXPORT void JNICALL JFN(importHeapState)(JNIEnv *env, jclass c, jlong h, jintArray ids, jbyteArray data,
                                             jlong watermark) {
     (void)c;

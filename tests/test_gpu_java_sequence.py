@@ -6,14 +6,17 @@ its JNI shim (java/.../gpu/GpuWindowOperator.java, jni/gwo_jni.c):
 
 * initializeState: gwo_create with the subtask's KeyGroupRange and maxParallelism = the task's number of key
   groups (getRuntimeContext().getMaxNumberOfParallelSubtasks(), StreamTaskStateInitializerImpl.java:290-306);
-  restoreRows when restored (min watermark over the key-group sections it reads, one gwo_restore);
+  when restored, the managed-state import below;
 * processElement: records appended to columns, gwo_submit every `batch` records;
 * processWatermark / endInput: flush, gwo_advance_watermark, emitFired -- gwo_wait_fires (JNI `waitFires`), then
   gwo_output_count / gwo_drain in chunks of `batch` rows until none is left, the side output the same way,
   gwo_late_dropped -- then the watermark is forwarded (rows before the watermark, AbstractStreamOperator.java:
   566-571);
-* snapshotState: flush, gwo_snapshot_rows, gwo_snapshot, rows written per key group into the raw keyed state
-  stream (DataOutputView: big-endian watermark, words, count, then per row key, start, end, timer, words).
+* snapshotState: flush, gwo_export_heap_state_begin, per key group gwo_export_heap_state_read and the section
+  parsed into WindowOperator's managed keyed states ("window-contents", "merging-window-set", the "window-timers"
+  timer service), gwo_export_heap_state_end;
+* initializeState of a restored subtask: the backend's entries of its key groups (enumerated through the timers,
+  sessions through the merging window set) written as key-group sections into one gwo_import_heap_state.
 
 Sessions fire asynchronously (gwo_session.cpp fire_session): without the sync in emitFired the drain loop would
 miss rows and forward the watermark first (the round-2 advisor's finding); the session case covers it.
@@ -28,6 +31,7 @@ import pytest
 
 from oracle import flink_oracle as O
 from oracle import gen as G
+from oracle import heap_keyed_state as H
 
 pytestmark = pytest.mark.gpu
 
@@ -64,6 +68,16 @@ class Output:
         return [e[1] for e in self.events if e[0] == "r"]
 
 
+_OPEN = []   # JavaSequence objects not closed yet (a failing test's are closed by the fixture below)
+
+
+@pytest.fixture(autouse=True)
+def _close_sequences():
+    yield
+    while _OPEN:   # (their pinned numpy columns must not stay registered once Python frees them)
+        _OPEN.pop().close()
+
+
 class JavaSequence:
     """GpuWindowOperator.java, call for call (Long keys)."""
 
@@ -89,6 +103,8 @@ class JavaSequence:
         self.f64 = cfg.value_dtype == N.DTYPE_FLOAT64
         self.side_enabled = side_output
         self.range = key_group_range
+        self.max_par = max_par
+        self.merging = spec["assigner"] == N.ASSIGNER_SESSION
         if restore_sections is not None:
             self._restore(restore_sections)
         # open(): the columns and the drain buffers, allocated once
@@ -109,8 +125,11 @@ class JavaSequence:
         self.n = 0
         self.late_reported = 0
         self.late_metric = 0
+        _OPEN.append(self)
 
     def close(self):
+        if self in _OPEN:
+            _OPEN.remove(self)
         for b in self.pinned:   # close(): unpinned, then the handle destroyed
             self.N.check(self.lib.gwo_host_unregister(_p(b)), None, "host unregister")
         self.lib.gwo_destroy(self.h)
@@ -177,67 +196,68 @@ class JavaSequence:
         self.late_metric += late.value - self.late_reported
         self.late_reported = late.value
 
-    # snapshotState: {key group: bytes of its section}
+    # snapshotState: the GPU state into WindowOperator's managed keyed states, key group by key group
+    # (gwo_export_heap_state_begin, one gwo_export_heap_state_read per key group, gwo_export_heap_state_end; each
+    # section parsed into the backend).  Returns the backend's copy (a WindowState: what the heap backend snapshots).
     def snapshot_state(self, key_group_list):
         N, lib, h = self.N, self.lib, self.h
         self.flush()
-        rows_b, words = C.c_int64(), C.c_int32()
-        N.check(lib.gwo_snapshot_rows(h, C.byref(rows_b), C.byref(words)), h)
-        cap, nw = max(rows_b.value, 1), words.value
-        k, s, e = (np.zeros(cap, np.int64) for _ in range(3))
-        w = np.zeros(cap * max(nw, 1), np.int64)
-        kg, tm = np.zeros(cap, np.int32), np.zeros(cap, np.int32)
-        rows = N.GwoStateRows(_p(k), _p(s), _p(e), _p(w), _p(kg), _p(tm))
-        got, wm = C.c_int64(), C.c_int64()
-        N.check(lib.gwo_snapshot(h, C.byref(rows), cap, C.byref(got), C.byref(wm)), h, "snapshot")
-        m = got.value
-        sections, i = {}, 0
-        for group in key_group_list:
-            j = i
-            while j < m and kg[j] == group:
-                j += 1
-            buf = [struct.pack(">qii", wm.value, nw, j - i)]
-            for r in range(i, j):
-                buf.append(struct.pack(">qqqi", k[r], s[r], e[r], tm[r]))
-                buf.append(struct.pack(f">{nw}q", *w[r * nw:(r + 1) * nw]))
-            sections[group] = b"".join(buf)
-            i = j
-        assert i == m, "rows left over: the snapshot was not grouped by ascending key group"
-        return sections
+        groups = list(key_group_list)
+        ids = N.GwoHeapStateIds(0, 1 if self.merging else -1, 2, 3)
+        offs = np.zeros(len(groups), np.int64)
+        total, wm = C.c_int64(), C.c_int64()
+        N.check(lib.gwo_export_heap_state_begin(h, C.byref(ids), C.byref(total),
+                                                offs.ctypes.data_as(C.POINTER(C.c_int64)), C.byref(wm)), h, "begin")
+        backend = H.WindowState()
+        try:
+            for i, g in enumerate(groups):
+                end = int(offs[i + 1]) if i + 1 < len(groups) else total.value
+                n = end - int(offs[i])
+                buf = (C.c_uint8 * max(n, 1))()
+                N.check(lib.gwo_export_heap_state_read(h, int(offs[i]), buf, n), h, "read")
+                part = H.parse_export(bytes(buf)[:n], "long", self.merging, (g, g))
+                backend.contents.update(part.contents)
+                backend.merging.update(part.merging)
+                backend.timers |= part.timers
+        finally:
+            N.check(lib.gwo_export_heap_state_end(h), h, "end")
+        return backend
 
-    def _restore(self, sections):
-        keys, rows, wm, words = [], [], LONG_MAX, -1
-        for group in range(self.range[0], self.range[1] + 1):
-            b = sections.get(group)
-            if b is None:
-                continue
-            w_, words, m = struct.unpack_from(">qii", b, 0)
-            wm = min(wm, w_)
-            off = 16
-            for _ in range(m):
-                key, st, en, tmr = struct.unpack_from(">qqqi", b, off)
-                off += 28
-                ws = struct.unpack_from(f">{words}q", b, off)
-                off += 8 * words
-                keys.append(key)
-                rows.append((st, en, tmr) + ws)
-        if words < 0:
+    # initializeState of a restored subtask (importMirror): the backend's entries of this subtask's key groups,
+    # enumerated through the timers, sessions resolved through the merging window set, written as sections (each
+    # window its own state window) into one gwo_import_heap_state at Long.MIN_VALUE
+    def _restore(self, backend):
+        kg_of = lambda key: O.assign_to_key_group(O.long_hash_code(int(key)), self.max_par)
+        timers = {t for t in backend.timers if self.range[0] <= kg_of(t[1]) <= self.range[1]}
+        if not timers:
             return
-        m = len(rows)
-        k = np.array(keys or [0], np.int64)
-        s = np.array([r[0] for r in rows] or [0], np.int64)
-        e = np.array([r[1] for r in rows] or [0], np.int64)
-        tm = np.array([r[2] for r in rows] or [0], np.int32)
-        w = np.array([x for r in rows for x in r[3:]] or [0], np.int64)
-        st = self.N.GwoStateRows(_p(k), _p(s), _p(e), _p(w), None, _p(tm))
-        self.N.check(self.lib.gwo_restore(self.h, C.byref(st), words, m, wm), self.h, "restore")
+        s = H.WindowState()
+        s.timers = timers
+        for ts, key, w in sorted(timers):
+            if (key, w) in s.contents:
+                continue
+            sw = backend.merging.get(key, {}).get(w, w) if self.merging else w
+            acc = backend.contents.get((key, sw))
+            if acc is not None:
+                s.contents[(key, w)] = acc
+                if self.merging:
+                    s.merging.setdefault(key, {})[w] = w
+        buf = H.write_state(s, "long", kg_of, self.range)
+        ids = self.N.GwoHeapStateIds(0, 1 if self.merging else -1, 2, 3)
+        arr = (C.c_uint8 * max(len(buf), 1)).from_buffer_copy(buf + b"\0")
+        self.N.check(self.lib.gwo_import_heap_state(self.h, C.byref(ids), arr, len(buf), LONG_MIN), self.h, "import")
 
 
-def _oracle_run(assigner, agg, lateness, k, t, v, batches, side=False):
-    """The loop oracle over the stream; also returns, per watermark (by index), the rows its timers emitted."""
+def _oracle_run(assigner, agg, lateness, k, t, v, batches, side=False, restore_after=None):
+    """The loop oracle over the stream; also returns, per watermark (by index), the rows its timers emitted.
+    restore_after=i: a restore from a checkpoint after watermark i -- the keyed state and timers carry over, the
+    watermark starts again at Long.MIN_VALUE (WindowOperator keeps no watermark in its state: a restored subtask's
+    timer service starts at Long.MIN_VALUE, InternalTimerServiceImpl.java:78)."""
     op = O.WindowOperatorOracle(assigner, agg, lateness, side_output=side)
     prev, fired = 0, []
-    for end, wm in batches:
+    for bi, (end, wm) in enumerate(batches):
+        if restore_after is not None and bi == restore_after + 1:
+            op.wm = LONG_MIN
         for i in range(prev, end):
             op.process_element(int(k[i]), int(t[i]), v[i].item())
         before = len(op.output)
@@ -333,9 +353,9 @@ def test_java_call_sequence_matches_oracle(N, case):
 
 @pytest.mark.parametrize("case", ["tumbling_log", "tumbling_table_lateness", "sessions"])
 def test_java_snapshot_sections_rescale_2_to_3(N, case):
-    """Two subtasks (KeyGroupRange of operator i of 2) checkpoint into per-key-group raw keyed state sections; three
-    new subtasks each read the sections of ITS key groups (the raw keyed state inputs Flink hands a rescaled
-    subtask) and continue.  The union of all rows equals the uninterrupted single-operator oracle run."""
+    """Two subtasks (KeyGroupRange of operator i of 2) checkpoint into WindowOperator's managed keyed states; three
+    new subtasks each import the entries of ITS key groups (the managed keyed state Flink hands a rescaled subtask)
+    and continue.  The union of all rows equals the uninterrupted single-operator oracle run."""
     maxp = 128
     spec = _cases(N)[case]
     k, t, v, b = _stream(7 + len(case))
@@ -343,7 +363,7 @@ def test_java_snapshot_sections_rescale_2_to_3(N, case):
     half = len(b) // 2
     cut = b[half - 1][0]
     out_before, out_after = Output(), Output()
-    sections = {}
+    backend = H.WindowState()   # the keyed state backends' snapshots, by key (redistributed by key group)
     for p in range(2):
         r = O.compute_key_group_range_for_operator_index(maxp, 2, p)
         own = (kg >= r[0]) & (kg <= r[1])
@@ -354,13 +374,16 @@ def test_java_snapshot_sections_rescale_2_to_3(N, case):
                 seq.process_element(int(k[i]), int(t[i]), int(v[i]))
             seq.process_watermark(wm)
             prev = end
-        sections.update(seq.snapshot_state(range(r[0], r[1] + 1)))
+        part = seq.snapshot_state(range(r[0], r[1] + 1))
+        backend.contents.update(part.contents)
+        backend.merging.update(part.merging)
+        backend.timers |= part.timers
         seq.close()
     late = 0
     for p in range(3):
         r = O.compute_key_group_range_for_operator_index(maxp, 3, p)
         own = (kg >= r[0]) & (kg <= r[1])
-        seq = JavaSequence(N, spec, r, maxp, batch=700, out=out_after, restore_sections=sections)
+        seq = JavaSequence(N, spec, r, maxp, batch=700, out=out_after, restore_sections=backend)
         prev = cut
         for end, wm in b[half:]:
             for i in np.flatnonzero(own[prev:end]) + prev:
@@ -371,7 +394,7 @@ def test_java_snapshot_sections_rescale_2_to_3(N, case):
         late += seq.late_metric
         seq.close()
     a, agg = spec["o"]()
-    ref, _ = _oracle_run(a, agg, spec.get("lateness", 0), k, t, v, b)
+    ref, _ = _oracle_run(a, agg, spec.get("lateness", 0), k, t, v, b, restore_after=half - 1)
     assert sorted(out_before.rows() + out_after.rows()) == sorted((r.key, r.start, r.end, r.result) for r in ref.output)
 
 
@@ -386,3 +409,42 @@ def test_host_register_contract(N):
     assert lib.gwo_host_unregister(_p(a)) == 1   # GWO_ERR_INVALID_ARGUMENT
     assert lib.gwo_host_register(None, 64) == 1   # GWO_ERR_INVALID_ARGUMENT
     assert lib.gwo_host_register(_p(a), 0) == 1   # GWO_ERR_INVALID_ARGUMENT
+
+
+@pytest.mark.parametrize("case", ["tumbling_log", "sessions"])
+def test_staged_export_equals_export(N, case):
+    """gwo_export_heap_state_begin/_read/_end stage exactly gwo_export_heap_state's image (same bytes, key-group
+    offsets and watermark), reading past the image is GWO_ERR_INVALID_ARGUMENT, and _end releases it (a read after it
+    is GWO_ERR_STATE)."""
+    spec = _cases(N)[case]
+    k, t, v, b = _stream(5)
+    seq = JavaSequence(N, spec, (0, 127), 128, batch=1000, out=Output())
+    _drive(seq, _events(k, t, v, b[: len(b) // 2]))
+    seq.flush()
+    lib, h = seq.lib, seq.h
+    ids = N.GwoHeapStateIds(0, 1 if seq.merging else -1, 2, 3)
+    need, wm = C.c_int64(), C.c_int64()
+    o1 = np.zeros(128, np.int64)
+    N.check(lib.gwo_export_heap_state(h, C.byref(ids), None, 0, C.byref(need), None, None), h)
+    ref = (C.c_uint8 * max(need.value, 1))()
+    N.check(lib.gwo_export_heap_state(h, C.byref(ids), ref, need.value, C.byref(need), _p(o1), C.byref(wm)), h)
+    total, wm2 = C.c_int64(), C.c_int64()
+    o2 = np.zeros(128, np.int64)
+    N.check(lib.gwo_export_heap_state_begin(h, C.byref(ids), C.byref(total), o2.ctypes.data_as(C.POINTER(C.c_int64)),
+                                            C.byref(wm2)), h)
+    assert total.value == need.value > 0 and wm2.value == wm.value
+    assert (o1 == o2).all()
+    got = (C.c_uint8 * total.value)()
+    half = total.value // 2
+    N.check(lib.gwo_export_heap_state_read(h, 0, got, half), h)
+    tail = (C.c_uint8 * (total.value - half))()
+    N.check(lib.gwo_export_heap_state_read(h, half, tail, total.value - half), h)
+    staged = bytes(got)[:half] + bytes(tail)
+    # the same entries (a key group's entries may come in another order from another snapshot of the device state)
+    a_ = H.parse_export(staged, "long", seq.merging, (0, 127))
+    b_ = H.parse_export(bytes(ref)[: need.value], "long", seq.merging, (0, 127))
+    assert a_.contents == b_.contents and a_.merging == b_.merging and a_.timers == b_.timers and a_.contents
+    assert lib.gwo_export_heap_state_read(h, 1, got, total.value) == 1   # GWO_ERR_INVALID_ARGUMENT: past the image
+    N.check(lib.gwo_export_heap_state_end(h), h)
+    assert lib.gwo_export_heap_state_read(h, 0, got, 1) != 0   # released
+    seq.close()
