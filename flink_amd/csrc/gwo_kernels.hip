@@ -510,20 +510,69 @@ enum : int { CS_ACC = 0, CS_LATE, CS_REFIRE, CS_BADTS, CS_BADRANGE, CS_BADKG, CS
 
 // NWT: the accumulator words at compile time (1-4; 0: p.nwords at run time) -- loops over words unroll and the plan's
 // per-word fields become scalar constants instead of run-time indexed arrays (the kernel was VALU-bound on them)
+// The gather's arguments, one struct: read through the kernarg segment pointer (offset 0) where the slow path and the
+// tail use them, so that only the per-record fields stay in scalar registers across the tile loop (the ~600 B of
+// arguments had spilled from SGPRs into VGPR lanes: a v_readlane per use, most of the kernel's VALU).
+struct GatherArgs {
+    const int64_t *key, *ts, *val;
+    int64_t n;
+    WindowGeom g;
+    AccPlan p;
+    CombineArgs a;
+    BatchStats *st;
+    int64_t *side_key, *side_ts, *side_val;
+    unsigned long long *side_count;
+    long long side_cap;
+    int side_enabled;
+};
+typedef __attribute__((address_space(4))) const GatherArgs KGatherArgs;
+// The kernarg segment behind an opaque copy of its pointer: loads through it stay where they are written.
+__device__ __forceinline__ KGatherArgs *gather_args() {
+    KGatherArgs *ka = (KGatherArgs *)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(ka));
+    return ka;
+}
+__device__ __forceinline__ WindowGeom load_geom(__attribute__((address_space(4))) const WindowGeom *s) {
+    WindowGeom g;
+    g.unit = s->unit;
+    g.unit_off = s->unit_off;
+    g.unit_off_mod = s->unit_off_mod;
+    g.size = s->size;
+    g.slide = s->slide;
+    g.offset = s->offset;
+    g.lateness = s->lateness;
+    g.wm = s->wm;
+    g.inv_size = s->inv_size;
+    g.inv_slide = s->inv_slide;
+    g.inv_unit = s->inv_unit;
+    g.sliding = s->sliding;
+    g.key_kind = s->key_kind;
+    g.max_par = s->max_par;
+    g.kg_lo = s->kg_lo;
+    g.kg_hi = s->kg_hi;
+    g.refire_ok = s->refire_ok;
+    g.refire_only = s->refire_only;
+    return g;
+}
+
 template <int NWT>
-__global__ __launch_bounds__(CB_THREADS) void gather_kernel(const int64_t *__restrict__ key,
-                                                            const int64_t *__restrict__ ts,
-                                                            const int64_t *__restrict__ val, int64_t n, WindowGeom g,
-                                                            AccPlan p, CombineArgs a, BatchStats *st, int64_t *side_key,
-                                                            int64_t *side_ts, int64_t *side_val,
-                                                            unsigned long long *side_count, long long side_cap,
-                                                            int side_enabled) {
+__global__ __launch_bounds__(CB_THREADS) void gather_kernel(GatherArgs A) {
+    const int64_t *__restrict__ key = A.key;
+    const int64_t *__restrict__ ts = A.ts;
+    const int64_t *__restrict__ val = A.val;
+    const int64_t n = A.n;
+    const AccPlan &p = A.p;
+    const CombineArgs &a = A.a;
+    // the per-record fields of the geometry (the rest is read in the slow path)
+    const int32_t g_key_kind = A.g.key_kind, g_max_par = A.g.max_par, g_kg_lo = A.g.kg_lo, g_kg_hi = A.g.kg_hi;
+    const int32_t g_refire_only = A.g.refire_only;
+    unsigned long long *const dbg = A.a.dbg;
     extern __shared__ __attribute__((aligned(16))) int64_t s_dyn[];
     const int S = a.S, NW = NWT > 0 ? NWT : p.nwords, tid = threadIdx.x;
     // trace: per-workgroup slot of 8 words, plain stores (start, then phase ends), reduced on the host
 #define CB_STAMP(k)                                                        \
     do {                                                                   \
-        if (a.dbg && tid == 0) a.dbg[blockIdx.x * 8 + (k)] = wall_clock64(); \
+        if (dbg && tid == 0) dbg[blockIdx.x * 8 + (k)] = wall_clock64(); \
     } while (0)
     CB_STAMP(0);
     int64_t *s_key = s_dyn;                     // [CB_NU * S]
@@ -556,7 +605,7 @@ __global__ __launch_bounds__(CB_THREADS) void gather_kernel(const int64_t *__res
     };
     const int64_t tstride = (int64_t)gridDim.x * CB_TILE;
     if ((int64_t)blockIdx.x * CB_TILE < n) load_tile((int64_t)blockIdx.x * CB_TILE);
-    if (a.dbg) {   // trace: when the first tile's loads have all arrived
+    if (dbg) {   // trace: when the first tile's loads have all arrived
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         CB_STAMP(6);
     }
@@ -575,17 +624,17 @@ __global__ __launch_bounds__(CB_THREADS) void gather_kernel(const int64_t *__res
             const int64_t tv = tt[j];
             const int jj = (tv >= a.bound[1]) + (tv >= a.bound[2]) + (tv >= a.bound[3]);
             if (!(a.thr_ok && tv >= a.bound[0] && tv < a.bound[4] && ((a.cls >> (2 * jj)) & 3u) == 0 &&
-                  !g.refire_only)) {
+                  !g_refire_only)) {
                 slow |= 1u << j;
                 continue;
             }
             acc++;
             const int64_t k = kk[j];
             if (!a.full_range) {
-                const int32_t kg = key_group(k, g.key_kind, g.max_par);
-                if (kg < g.kg_lo || kg > g.kg_hi) {
+                const int32_t kg = key_group(k, g_key_kind, g_max_par);
+                if (kg < g_kg_lo || kg > g_kg_hi) {
                     bad_kg++;
-                    atomicExch((unsigned long long *)&st->bad_kg_key, (unsigned long long)k);
+                    atomicExch((unsigned long long *)&gather_args()->st->bad_kg_key, (unsigned long long)k);
                 }
             }
             const long long u = a.hint + jj;
@@ -606,6 +655,8 @@ __global__ __launch_bounds__(CB_THREADS) void gather_kernel(const int64_t *__res
             const int j = __builtin_ctz(slow);
             slow &= slow - 1;
             const int64_t i = tile + j * CB_THREADS + tid;
+            KGatherArgs *ka = gather_args();   // (the rare path reads its arguments here, not from registers)
+            const WindowGeom g = load_geom(&ka->g);
             long long u = 0;
             const int64_t tv = ts[i];
             const int c = classify(tv, g, u);
@@ -616,12 +667,12 @@ __global__ __launch_bounds__(CB_THREADS) void gather_kernel(const int64_t *__res
             } else if (c == REC_LATE) {
                 if (g.refire_only) continue;
                 late++;
-                if (side_enabled) {
-                    const unsigned long long pos = atomicAdd(side_count, 1ull);
-                    if ((long long)pos < side_cap) {
-                        side_key[pos] = key[i];
-                        side_ts[pos] = tv;
-                        side_val[pos] = val ? val[i] : 0;
+                if (ka->side_enabled) {
+                    const unsigned long long pos = atomicAdd(ka->side_count, 1ull);
+                    if ((long long)pos < ka->side_cap) {
+                        ka->side_key[pos] = key[i];
+                        ka->side_ts[pos] = tv;
+                        ka->side_val[pos] = val ? val[i] : 0;
                     }
                 }
             } else if (takes(c, g)) {
@@ -631,7 +682,7 @@ __global__ __launch_bounds__(CB_THREADS) void gather_kernel(const int64_t *__res
                 const int32_t kg = a.full_range ? g.kg_lo : key_group(k, g.key_kind, g.max_par);
                 if (kg < g.kg_lo || kg > g.kg_hi) {
                     bad_kg++;
-                    atomicExch((unsigned long long *)&st->bad_kg_key, (unsigned long long)k);
+                    atomicExch((unsigned long long *)&ka->st->bad_kg_key, (unsigned long long)k);
                 }
                 mn = u < mn ? u : mn;
                 mx = u > mx ? u : mx;
@@ -738,6 +789,7 @@ __global__ __launch_bounds__(CB_THREADS) void gather_kernel(const int64_t *__res
             }
     }
     CB_STAMP(2);
+    KGatherArgs *const kt = gather_args();   // the tail's arguments, loaded here
     if (run_n) atomicAdd(&s_hist[run_b], run_n);
     // per-workgroup statistics slot
     unsigned long long v[CS_HIST] = {acc, late, refire, bad_ts, bad_range, bad_kg, hout, 0, 0, 0, 0};
@@ -775,7 +827,7 @@ __global__ __launch_bounds__(CB_THREADS) void gather_kernel(const int64_t *__res
     __syncthreads();
     // this workgroup's statistics go into shard blockIdx % CB_SHARDS of the statistics words (device-scope
     // atomics, zero words skipped: ~G / CB_SHARDS operations per address)
-    unsigned long long *shard = a.blk + (size_t)(blockIdx.x % CB_SHARDS) * CS_WORDS;
+    unsigned long long *shard = kt->a.blk + (size_t)(blockIdx.x % CB_SHARDS) * CS_WORDS;
     if (tid < CS_HIST) {
         unsigned long long r = tid == CS_MIN ? 0x7fffffffffffffffull : 0ull;
         for (int w = 0; w < CB_THREADS / 64; ++w) {
@@ -797,15 +849,15 @@ __global__ __launch_bounds__(CB_THREADS) void gather_kernel(const int64_t *__res
     __shared__ int s_last;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (tid == 0) s_last = atomicAdd(a.done, 1ull) == (unsigned long long)(gridDim.x - 1);
+    if (tid == 0) s_last = atomicAdd(kt->a.done, 1ull) == (unsigned long long)(gridDim.x - 1);
     __syncthreads();
     CB_STAMP(4);
     // the dump (accumulators only of occupied slots; dump_used tells the merge which tables) reaches the merge
     // through the kernel boundary; the last workgroup's tail below overlaps its stores
     auto dump = [&]() {
-        if (tid == 0) a.dump_used[blockIdx.x] = used;
-        int64_t *dk = a.dump_key + (size_t)blockIdx.x * CB_NU * S;
-        int64_t *da = a.dump_acc + (size_t)blockIdx.x * CB_NU * S * NW;
+        if (tid == 0) kt->a.dump_used[blockIdx.x] = used;
+        int64_t *dk = kt->a.dump_key + (size_t)blockIdx.x * CB_NU * S;
+        int64_t *da = kt->a.dump_acc + (size_t)blockIdx.x * CB_NU * S * NW;
         for (int i = tid; i < CB_NU * S; i += CB_THREADS) {
             if (!((used >> (i >= S ? 1 : 0)) & 1u)) continue;
             const int64_t k = s_key[i];
@@ -823,7 +875,7 @@ __global__ __launch_bounds__(CB_THREADS) void gather_kernel(const int64_t *__res
         const unsigned long long init =
             tid == CS_MIN ? 0x7fffffffffffffffull : (tid == CS_MAX ? 0x8000000000000000ull : 0ull);
         // read and reset for the next batch
-        s_tot[tid] = xchg_fold<CB_SHARDS>(&a.blk[tid], CS_WORDS, init, tid == CS_MIN ? 1 : (tid == CS_MAX ? 2 : 0));
+        s_tot[tid] = xchg_fold<CB_SHARDS>(&kt->a.blk[tid], CS_WORDS, init, tid == CS_MIN ? 1 : (tid == CS_MAX ? 2 : 0));
     }
     // the readback block: BatchStats image, side-output count, occupancy of the hint tables, sequence word last
     __shared__ unsigned long long s_spec[4];   // listed records, side-output count, occupancy of the hint tables
@@ -833,48 +885,48 @@ __global__ __launch_bounds__(CB_THREADS) void gather_kernel(const int64_t *__res
                                        RBW(bad_range), RBW(bad_kg), RBW(hist_out),    RBW(min_idx),
                                        RBW(max_idx),  RBW(distinct), RBW(distinct) + 1, 0};
         const unsigned long long r = s_tot[tid];
-        rb_put(&a.rb[tid < CS_HIST ? word[tid] : RBW(hist) + tid - CS_HIST], r);
+        rb_put(&kt->a.rb[tid < CS_HIST ? word[tid] : RBW(hist) + tid - CS_HIST], r);
         if (tid == CS_BADKG)
-            rb_put(&a.rb[RBW(bad_kg_key)], r ? atomicAdd((unsigned long long *)&st->bad_kg_key, 0ull) : 0ull);
+            rb_put(&kt->a.rb[RBW(bad_kg_key)], r ? atomicAdd((unsigned long long *)&kt->st->bad_kg_key, 0ull) : 0ull);
     } else if (tid >= CB_THREADS - 4) {
         const int q = tid - (CB_THREADS - 4);   // 0: overflow, 1: side count, 2-3: occupancy
         if (q == 0) {
-            const unsigned long long ov = atomicExch(a.ovf_count, 0ull);   // read and reset for the next batch
-            rb_put(&a.rb[RBW(overflow)], ov);
+            const unsigned long long ov = atomicExch(kt->a.ovf_count, 0ull);   // read and reset for the next batch
+            rb_put(&kt->a.rb[RBW(overflow)], ov);
 #undef RBW
-            *a.done = 0;
+            *kt->a.done = 0;
             s_spec[0] = ov;
         } else if (q == 1) {
-            const unsigned long long sc = a.side_enabled ? atomicAdd(side_count, 0ull) : 0ull;
-            rb_put(&a.rb[CB_RB_SIDE], sc);
+            const unsigned long long sc = kt->a.side_enabled ? atomicAdd(kt->side_count, 0ull) : 0ull;
+            rb_put(&kt->a.rb[CB_RB_SIDE], sc);
             s_spec[1] = sc;
         } else {
-            unsigned long long *o = a.occ[q - 2];
+            unsigned long long *o = kt->a.occ[q - 2];
             unsigned long long tot = 0;
             if (o)
                 for (int sh = 0; sh < GWO_OCC_SHARDS; ++sh) tot += atomicAdd(o + sh * GWO_OCC_SHARD_STRIDE, 0ull);
-            rb_put(&a.rb[CB_RB_OCC + q - 2], tot);
+            rb_put(&kt->a.rb[CB_RB_OCC + q - 2], tot);
             s_spec[q] = tot;
         }
     }
     __syncthreads();
     CB_STAMP(5);
     if (tid == 0) {   // the speculative merge's verdict
-        bool go = a.go != nullptr && (!a.chain || *(volatile const uint32_t *)a.go != 0u) && s_tot[CS_ACC] > 0 && s_tot[CS_BADTS] == 0 && s_tot[CS_BADRANGE] == 0 &&
+        bool go = kt->a.go != nullptr && (!kt->a.chain || *(volatile const uint32_t *)kt->a.go != 0u) && s_tot[CS_ACC] > 0 && s_tot[CS_BADTS] == 0 && s_tot[CS_BADRANGE] == 0 &&
                   s_tot[CS_BADKG] == 0 && s_tot[CS_REFIRE] == 0 && s_tot[CS_HOUT] == 0 && s_spec[0] == 0 &&
-                  (!a.side_enabled || (long long)s_spec[1] <= a.side_cap) &&
-                  (long long)s_tot[CS_MIN] >= a.hint && (long long)s_tot[CS_MAX] <= a.hint + 1;
+                  (!kt->a.side_enabled || (long long)s_spec[1] <= kt->a.side_cap) &&
+                  (long long)s_tot[CS_MIN] >= kt->a.hint && (long long)s_tot[CS_MAX] <= kt->a.hint + 1;
         for (int r = 0; r < 2 && go; ++r) {
             const unsigned long long recs = s_tot[CS_HIST + r];
             if (!recs) continue;
             const unsigned long long inc = min(recs, s_tot[CS_D0 + r]);
-            go = a.occ[r] != nullptr && 10 * (s_spec[2 + r] + inc) <= 7 * a.cap[r];   // the host's kMaxLoad 0.7
+            go = kt->a.occ[r] != nullptr && 10 * (s_spec[2 + r] + inc) <= 7 * kt->a.cap[r];   // the host's kMaxLoad 0.7
         }
-        if (a.go) *a.go = go ? 1u : 0u;
-        rb_put(&a.rb[CB_RB_GO], go ? 1ull : 0ull);
+        if (kt->a.go) *kt->a.go = go ? 1u : 0u;
+        rb_put(&kt->a.rb[CB_RB_GO], go ? 1ull : 0ull);
     }
 #undef CB_STAMP
-    rb_publish(&a.rb[CB_RB_SEQ], a.seq);
+    rb_publish(&kt->a.rb[CB_RB_SEQ], kt->a.seq);
     dump();   // the last workgroup's own dump: after the readback, which waits for every store issued before it
 }
 
@@ -1641,9 +1693,9 @@ void launch_gather(const int64_t *key, const int64_t *ts, const int64_t *val, in
                    const AccPlan &p, const CombineArgs &a, int grid, BatchStats *st, int64_t *side_key, int64_t *side_ts,
                    int64_t *side_val, unsigned long long *side_count, long long side_cap, int side_enabled,
                    hipStream_t s) {
-#define GATHER(NWT)                                                                                            \
-    hipLaunchKernelGGL(gather_kernel<NWT>, dim3(grid), dim3(CB_THREADS), gather_lds_bytes(a.S, p.nwords), s, key, ts, \
-                       val, n, g, p, a, st, side_key, side_ts, side_val, side_count, side_cap, side_enabled)
+    GatherArgs A{key, ts, val, n, g, p, a, st, side_key, side_ts, side_val, side_count, side_cap, side_enabled};
+#define GATHER(NWT) \
+    hipLaunchKernelGGL(gather_kernel<NWT>, dim3(grid), dim3(CB_THREADS), gather_lds_bytes(a.S, p.nwords), s, A)
     switch (p.nwords) {
         case 1: GATHER(1); break;
         case 2: GATHER(2); break;
