@@ -220,6 +220,21 @@ struct SessErr {
     unsigned long long emitted;
     unsigned long long live_delta;     // sessions created - removed (two's complement)
     unsigned long long pool_full;      // a spill found no pool room (the host sizes the pool so it cannot)
+    unsigned long long long_slots;     // keys with more records in a batch than their bucket holds (SessLists)
+};
+
+// A batch's records grouped by key without a sort (gwo_session.hip): the slot pass appends each record's index to
+// its slot's bucket -- word 0 the count, words 1..SESS_BKT_N the indices, in atomic order -- and the slot to the
+// touched list on its first record; the process pass visits the touched slots, orders each bucket by index (arrival
+// order) and resets its count.  A slot with more records than its bucket holds is queued on `longs` and applied by
+// sess_long_kernel from the records' slots in index order.
+#define SESS_BKT 16
+#define SESS_BKT_N (SESS_BKT - 1)
+struct SessLists {
+    uint32_t *bkt;                     // [(cap + 1) * SESS_BKT], counts zero between batches
+    uint32_t *touched;                 // slots with records this batch
+    uint32_t *longs;                   // slots whose records overflowed their bucket
+    uint32_t *ctl;                     // [0] touched count, [1] long count, [2] workgroups done (sess_long_kernel)
 };
 
 // ---- host-side launchers (gwo_kernels.hip) -----------------------------------------------------

@@ -10,11 +10,16 @@
 namespace gwo {
 
 void launch_sess_slot(const int64_t *key, const int64_t *ts, int64_t n, const TableDesc &t, uint64_t cap, int stride,
-                      const SessGeom &g, uint32_t *rec_slot, SessErr *err, hipStream_t s);
+                      const SessGeom &g, uint32_t *rec_slot, SessErr *err, const SessLists *ls, hipStream_t s);
 void launch_sess_process(const int64_t *key, const int64_t *ts, const int64_t *val, int64_t n, const uint32_t *sslot,
                          const uint32_t *sidx, const TableDesc &t, uint64_t cap, int stride, const AccPlan &p,
                          const ResultPlan &rp, const SessGeom &g, OutCols o, SessErr *err, int64_t *sk, int64_t *st,
-                         int64_t *sv, unsigned long long *sc, long long scap, hipStream_t s);
+                         int64_t *sv, unsigned long long *sc, long long scap, const SessLists *ls, hipStream_t s);
+void launch_sess_long(const int64_t *key, const int64_t *ts, const int64_t *val, int64_t n, const uint32_t *rec_slot,
+                      const TableDesc &t, uint64_t cap, int stride, const AccPlan &p, const ResultPlan &rp,
+                      const SessGeom &g, OutCols o, SessErr *err, int64_t *sk, int64_t *st, int64_t *sv,
+                      unsigned long long *sc, long long scap, const SessLists &ls, unsigned long long *rb,
+                      unsigned long long seq, hipStream_t s);
 void launch_sess_fire(const TableDesc &t, uint64_t cap, int stride, const AccPlan &p, const ResultPlan &rp,
                       const SessGeom &g, OutCols o, SessErr *err, hipStream_t s);
 void launch_sess_compact(const TableDesc &src, uint64_t cap, const TableDesc &dst, int stride, hipStream_t s);
@@ -38,8 +43,14 @@ struct SessionState {
     SessErr *d_err_fire = nullptr;  // the watermark sweep's own block: its readback completes lazily (finish_fire)
     SessErr *h_err_fire = nullptr;  // pinned
     SessErr fire_prev{};
-    int sort_digits = 8;            // radix digit bits of the slot sort (GWO_SESS_DIGITS: 8 or 10)            // d_err_fire (also cumulative) as of the last read-back
+    int sort_digits = 8;            // radix digit bits of the slot sort (GWO_SESS_DIGITS: 8 or 10)
     DevBuf rec_slot, k1, v1, k2, v2, hist;
+    // records grouped by slot in buckets (SessLists) instead of the radix sort; GWO_SESS_LISTS=0/1 fixes the choice,
+    // otherwise the host switches to the sort while batches overflow many buckets (each such key costs a scan of the
+    // batch's slots in sess_long_kernel) and back once they stop
+    bool lists = true, lists_auto = true;
+    DevBuf bkt;                     // [(cap + 1) * SESS_BKT] bucket words (counts zero between batches)
+    uint32_t *ctl = nullptr;        // SessLists::ctl
     // spill pool of keys with more in-flight sessions than an entry holds (gwo_internal.h SessGeom)
     int64_t *pool = nullptr;
     uint64_t pool_cap = 0;          // session records
@@ -53,6 +64,8 @@ struct SessionState {
     bool rb_pending = false;
     uint64_t pend_n = 0;
 };
+
+static constexpr unsigned long long kSessLongMax = 32;   // sess_long_kernel runs 32 workgroups
 
 gwo_status Handle::sess_alloc(uint64_t cap, Table &t, int64_t **due) {
     SessionState &S = *sess;
@@ -79,6 +92,12 @@ gwo_status Handle::session_init() {
     SessionState &S = *sess;
     if (const char *e = getenv("GWO_SESSION_SLOTS")) S.smax = std::max(1, std::min(16, atoi(e)));
     if (const char *e = getenv("GWO_SESS_DIGITS")) S.sort_digits = atoi(e) == 10 ? 10 : 8;
+    if (const char *e = getenv("GWO_SESS_LISTS")) {
+        S.lists = atoi(e) != 0;
+        S.lists_auto = false;
+    }
+    GWO_TRY(dalloc((void **)&S.ctl, 16));
+    GWO_TRY(hipcheck(hipMemsetAsync(S.ctl, 0, 16, stream), "session lists"));
     S.stride = (2 + S.smax * (3 + plan.nwords) + 1) & ~1;
     // the pool's bump counter sits right behind the batch's SessErr block: one copy reads both back
     GWO_TRY(dalloc((void **)&S.d_err, sizeof(SessErr) + 8));
@@ -109,6 +128,8 @@ void Handle::session_free() {
     if (S.d_err_fire) (void)hipFree(S.d_err_fire);
     if (S.h_err_fire) (void)hipHostFree(S.h_err_fire);
     if (S.pool) (void)hipFree(S.pool);
+    if (S.ctl) (void)hipFree(S.ctl);
+    S.bkt.release();
     S.rec_slot.release();
     S.k1.release();
     S.v1.release();
@@ -248,32 +269,56 @@ gwo_status Handle::insert_session(const int64_t *k, const int64_t *t, const int6
     GWO_TRY(ensure_buf(S.rec_slot, n * 4));
     GWO_TRY(ensure_buf(S.k1, n * 4));
     GWO_TRY(ensure_buf(S.v1, n * 4));
-    GWO_TRY(ensure_buf(S.k2, n * 4));
-    GWO_TRY(ensure_buf(S.v2, n * 4));
-    int64_t nblocks = (n + 4095) / 4096;
-    const int64_t hist_words = (int64_t)1024 * std::max<int64_t>(nblocks, 64);   // room for the small-sort tiles
-    GWO_TRY(ensure_buf(S.hist, (size_t)hist_words * 4 + 16));
+    const bool lists = S.lists;
+    int64_t hist_words = 0;
+    if (lists) {
+        const size_t was = S.bkt.bytes;
+        GWO_TRY(ensure_buf(S.bkt, ((size_t)S.T.cap + 1) * SESS_BKT * 4));
+        if (S.bkt.bytes != was)   // a fresh bucket array: every count zero
+            GWO_TRY(hipcheck(hipMemsetAsync(S.bkt.ptr, 0, S.bkt.bytes, stream), "session buckets"));
+    } else {
+        GWO_TRY(ensure_buf(S.k2, n * 4));
+        GWO_TRY(ensure_buf(S.v2, n * 4));
+        int64_t nblocks = (n + 4095) / 4096;
+        hist_words = (int64_t)1024 * std::max<int64_t>(nblocks, 64);   // room for the small-sort tiles
+        GWO_TRY(ensure_buf(S.hist, (size_t)hist_words * 4 + 16));
+    }
     if (side_enabled() && side_cap - (long long)side_rows_committed < n)
         GWO_TRY(grow_side((long long)side_rows_committed + n));
     SessGeom g = sess_geom(*this, S.smax);
-    prof_begin(GWO_KERNEL_SESSION);
-    launch_sess_slot(k, t, n, desc(S.T), S.T.cap, S.stride, g, (uint32_t *)S.rec_slot.ptr, S.d_err, stream);
-    GWO_TRY(launch_ok("sess slot"));
-    int bits = 1;   // slots are 0..cap (cap: the side slot)
-    while (bits < 32 && (S.T.cap >> bits) > 0) bits++;
-    int which = radix_sort_pairs((const uint32_t *)S.rec_slot.ptr, nullptr, n, bits, (uint32_t *)S.k1.ptr,
-                                 (uint32_t *)S.v1.ptr, (uint32_t *)S.k2.ptr, (uint32_t *)S.v2.ptr,
-                                 (uint32_t *)S.hist.ptr, stream, S.sort_digits, hist_words);
-    GWO_TRY(launch_ok("radix sort"));
-    const uint32_t *ss = which ? (const uint32_t *)S.k2.ptr : (const uint32_t *)S.k1.ptr;
-    const uint32_t *si = which ? (const uint32_t *)S.v2.ptr : (const uint32_t *)S.v1.ptr;
+    // lists: the touched slots in k1, the overflowing ones in v1 (radix: the sort's buffers)
+    const SessLists ls{(uint32_t *)S.bkt.ptr, (uint32_t *)S.k1.ptr, (uint32_t *)S.v1.ptr, S.ctl};
     OutCols o = out_cols();
-    launch_sess_process(k, t, v, n, ss, si, desc(S.T), S.T.cap, S.stride, plan, rplan, g, o, S.d_err,
-                        (int64_t *)side_key.ptr, (int64_t *)side_ts.ptr, (int64_t *)side_val.ptr, d_side_count,
-                        side_enabled() ? side_cap : 0, stream);
-    GWO_TRY(launch_ok("sess process"));
-    prof_end(GWO_KERNEL_SESSION, n);
-    GWO_TRY(sess_publish_err());
+    int64_t *sk = (int64_t *)side_key.ptr, *sts = (int64_t *)side_ts.ptr, *sv = (int64_t *)side_val.ptr;
+    const long long scap = side_enabled() ? side_cap : 0;
+    prof_begin(GWO_KERNEL_SESSION);
+    launch_sess_slot(k, t, n, desc(S.T), S.T.cap, S.stride, g, (uint32_t *)S.rec_slot.ptr, S.d_err, lists ? &ls : nullptr,
+                     stream);
+    GWO_TRY(launch_ok("sess slot"));
+    if (lists) {
+        launch_sess_process(k, t, v, n, nullptr, nullptr, desc(S.T), S.T.cap, S.stride, plan, rplan, g, o, S.d_err, sk,
+                            sts, sv, d_side_count, scap, &ls, stream);
+        GWO_TRY(launch_ok("sess process"));
+        // the batch's statistics are published by the last kernel's last workgroup (no publish launch)
+        launch_sess_long(k, t, v, n, (const uint32_t *)S.rec_slot.ptr, desc(S.T), S.T.cap, S.stride, plan, rplan, g, o,
+                         S.d_err, sk, sts, sv, d_side_count, scap, ls, S.rb_dev, ++S.rb_seq, stream);
+        GWO_TRY(launch_ok("sess long"));
+        prof_end(GWO_KERNEL_SESSION, n);
+    } else {
+        int bits = 1;   // slots are 0..cap (cap: the side slot)
+        while (bits < 32 && (S.T.cap >> bits) > 0) bits++;
+        int which = radix_sort_pairs((const uint32_t *)S.rec_slot.ptr, nullptr, n, bits, (uint32_t *)S.k1.ptr,
+                                     (uint32_t *)S.v1.ptr, (uint32_t *)S.k2.ptr, (uint32_t *)S.v2.ptr,
+                                     (uint32_t *)S.hist.ptr, stream, S.sort_digits, hist_words);
+        GWO_TRY(launch_ok("radix sort"));
+        const uint32_t *ss = which ? (const uint32_t *)S.k2.ptr : (const uint32_t *)S.k1.ptr;
+        const uint32_t *si = which ? (const uint32_t *)S.v2.ptr : (const uint32_t *)S.v1.ptr;
+        launch_sess_process(k, t, v, n, ss, si, desc(S.T), S.T.cap, S.stride, plan, rplan, g, o, S.d_err, sk, sts, sv,
+                            d_side_count, scap, nullptr, stream);
+        GWO_TRY(launch_ok("sess process"));
+        prof_end(GWO_KERNEL_SESSION, n);
+        GWO_TRY(sess_publish_err());
+    }
     if (pipe_submit && cfg.allowed_lateness == 0 && !side_enabled()) {   // read at the watermark (sess_resolve)
         S.rb_pending = true;
         S.pend_n = (uint64_t)n;
@@ -304,6 +349,11 @@ gwo_status Handle::sess_apply_err() {
         return poison(GWO_ERR_MERGE_LATE, "The end timestamp of an event-time window cannot become earlier than the "
                                           "current watermark by merging.");
     if (e.pool_full) return poison(GWO_ERR_HIP, "session spill pool exhausted despite its reservation");
+    // bucket overflows: a few keys per batch are cheap (a workgroup each scans the batch's slots), many are not
+    if (S.lists_auto) {
+        if (S.lists && e.long_slots > kSessLongMax) S.lists = false;
+        else if (!S.lists && e.long_slots <= kSessLongMax / 4) S.lists = true;
+    }
     S.live += e.live_delta;
     out_rows += e.emitted;
     if (side_enabled()) {

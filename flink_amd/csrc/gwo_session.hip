@@ -14,9 +14,11 @@
 // intersecting windows).
 //
 // A batch is processed key-parallel but arrival-ordered within a key: records are grouped by
-// their key's table slot with a stable radix sort (gwo_sort.hip) and one lane walks each key's
-// records in order.  That keeps the reference's order-dependent cases exact (an on-time record
-// arriving after a late one can bridge sessions; allowedLateness > 0 re-fires).
+// their key's table slot -- in per-slot buckets filled by the slot pass (SessLists; three launches per
+// batch), or, when the host sees many keys overflow their buckets, with a stable radix sort
+// (gwo_sort.hip) -- and one lane walks each key's records in order.  That keeps the reference's
+// order-dependent cases exact (an on-time record arriving after a late one can bridge sessions;
+// allowedLateness > 0 re-fires).
 #include "gwo_device.h"
 
 namespace gwo {
@@ -25,10 +27,13 @@ __device__ __forceinline__ int64_t *entry_ptr(const TableDesc &t, uint32_t slot,
     return slot < cap ? t.base + (uint64_t)slot * stride : t.side;
 }
 
-// pass 1: slot of every record's key (claims entries for new keys)
+// pass 1: slot of every record's key (claims entries for new keys); with lists (SessLists) also the record's place in
+// its slot's bucket and, for a slot's first record of the batch, the slot's place in the touched list (one append
+// per wave)
+template <bool LISTS>
 __global__ __launch_bounds__(256) void sess_slot_kernel(const int64_t *__restrict__ key, const int64_t *__restrict__ ts,
                                                         int64_t n, TableDesc t, uint64_t cap, int stride, SessGeom g,
-                                                        uint32_t *__restrict__ rec_slot, SessErr *err) {
+                                                        uint32_t *__restrict__ rec_slot, SessErr *err, SessLists ls) {
     const int64_t step = (int64_t)gridDim.x * blockDim.x;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += step) {
         int64_t k = key[i];
@@ -41,7 +46,21 @@ __global__ __launch_bounds__(256) void sess_slot_kernel(const int64_t *__restric
         bool claimed;
         int64_t *a = find_or_insert(t, stride, k, claimed);
         count_claims(t.occ, claimed);
-        rec_slot[i] = k == GWO_EMPTY_KEY ? (uint32_t)cap : (uint32_t)((a - 1 - t.base) / stride);
+        const uint32_t slot = k == GWO_EMPTY_KEY ? (uint32_t)cap : (uint32_t)((a - 1 - t.base) / stride);
+        rec_slot[i] = slot;
+        if (LISTS) {
+            uint32_t *bk = ls.bkt + (uint64_t)slot * SESS_BKT;
+            const uint32_t r = atomicAdd(bk, 1u);
+            if (r < SESS_BKT_N) bk[1 + r] = (uint32_t)i;
+            const uint64_t first = __ballot(r == 0);
+            if (first) {
+                const int lane = threadIdx.x & 63, leader = __ffsll((unsigned long long)first) - 1;
+                uint32_t base = 0;
+                if (lane == leader) base = atomicAdd(&ls.ctl[0], (uint32_t)__popcll(first));
+                base = __shfl(base, leader);
+                if (r == 0) ls.touched[base + __popcll(first & ((1ull << lane) - 1))] = slot;
+            }
+        }
     }
 }
 
@@ -104,7 +123,170 @@ __device__ __forceinline__ int64_t *sess_grow(const SessGeom &g, const int64_t *
     return dst;
 }
 
-// pass 2: one lane per key, records in arrival order
+// One key's session list while a batch's records are applied to it (sess_key_*): the inline sessions copied into
+// this lane's LDS slice L (written back at the end), or its pool array.  A private array indexed at run time would
+// live in scratch memory.
+struct SessKey {
+    int64_t *e;
+    int64_t *L;
+    int64_t *S;
+    int64_t off;
+    int ns, scap;
+    bool spilled, dirty;
+    long long created;
+};
+
+__device__ __forceinline__ void sess_key_begin(SessKey &K, int64_t *e, int64_t *L, const SessGeom &g, int sw) {
+    K.e = e;
+    K.L = L;
+    K.S = L;
+    K.scap = g.smax;
+    K.off = 0;
+    K.spilled = e[1] < 0;
+    K.dirty = false;
+    K.created = 0;
+    if (K.spilled) {
+        K.off = e[2];
+        K.scap = (int)e[3];
+        K.ns = (int)e[4];
+        K.S = g.pool + (uint64_t)K.off * sw;
+    } else {
+        K.ns = (int)e[1];
+        for (int i = 0; i < K.ns * sw; ++i) L[i] = e[2 + i];
+    }
+}
+
+// Record i applied to its key's sessions: WindowOperator.processElement's merging branch.
+__device__ __forceinline__ void sess_key_record(SessKey &K, uint32_t i, const int64_t *__restrict__ key,
+                                                const int64_t *__restrict__ ts, const int64_t *__restrict__ val,
+                                                const AccPlan &p, const ResultPlan &rp, const SessGeom &g,
+                                                const OutCols &o, SessErr *err, int64_t *side_key, int64_t *side_ts,
+                                                int64_t *side_val, unsigned long long *side_count, long long side_cap,
+                                                int sw) {
+    const int64_t k = key[i], tsi = ts[i];
+    const int64_t v = val ? val[i] : 0;
+    if (tsi == GWO_LONG_MIN) return;  // the whole batch is rejected by the host
+    const int64_t ws = tsi, we = jadd(tsi, g.gap);
+    int64_t *S = K.S;
+    int ns = K.ns;
+    // in-flight sessions intersecting [ws, we) (TimeWindow.intersects is inclusive)
+    int64_t ms = ws, me = we;
+    int nm = 0, first = -1;
+    for (int s = 0; s < ns; ++s) {
+        const int64_t *X = S + s * sw;
+        if (X[0] <= we && X[1] >= ws) {
+            if (first < 0) first = s;
+            nm++;
+            ms = X[0] < ms ? X[0] : ms;
+            me = X[1] > me ? X[1] : me;
+        }
+    }
+    int actual;
+    bool fresh = false;
+    if (nm == 0) {
+        if (ns >= K.scap) {   // the list is full: spill (or grow) into a pool array twice its size
+            int64_t *nS = sess_grow(g, S, ns, sw, 2 * K.scap, K.off, K.scap);
+            if (!nS) {
+                atomicAdd(&err->pool_full, 1ull);
+                return;
+            }
+            S = K.S = nS;
+            K.spilled = true;
+        }
+        actual = ns++;
+        int64_t *X = S + actual * sw;
+        X[0] = ws;
+        X[1] = we;
+        X[2] = 0;
+        for (int w = 0; w < p.nwords; ++w) X[3 + w] = p.ident[w];
+        fresh = true;
+        K.created++;
+    } else if (nm == 1 && S[first * sw] == ms && S[first * sw + 1] == me) {
+        actual = first;  // new window inside an existing session: no merge callback
+    } else {
+        int64_t rmax = jsub(me, 1);
+        if (jadd(rmax, g.lateness) <= g.wm) {  // WindowOperator.java:318-323
+            atomicAdd(&err->merge_late, 1ull);
+            return;
+        }
+        // mergeNamespaces: fold every merged session into the first
+        int64_t acc[GWO_MAX_WORDS];
+        for (int w = 0; w < p.nwords; ++w) acc[w] = p.ident[w];
+        int keep = 0;
+        for (int s = 0; s < ns; ++s) {
+            const int64_t *X = S + s * sw;
+            bool m = X[0] <= we && X[1] >= ws;
+            if (m) {
+                for (int w = 0; w < p.nwords; ++w) acc[w] = combine(p.op[w], acc[w], X[3 + w]);
+            } else {
+                if (keep != s)
+                    for (int w = 0; w < sw; ++w) S[keep * sw + w] = X[w];
+                keep++;
+            }
+        }
+        K.created -= nm - 1;
+        ns = keep + 1;
+        actual = keep;
+        int64_t *X = S + actual * sw;
+        X[0] = ms;
+        X[1] = me;
+        X[2] = rmax > g.wm ? 1 : 0;  // EventTimeTrigger.onMerge: timer iff maxTs > watermark
+        for (int w = 0; w < p.nwords; ++w) X[3 + w] = acc[w];
+    }
+    K.dirty = true;
+    K.ns = ns;
+    int64_t *A = S + actual * sw;
+    const int64_t amax = jsub(A[1], 1);
+    if (cleanup_time(amax, g.lateness) <= g.wm) {  // isWindowLate -> retireWindow
+        if (fresh) {
+            K.ns--;
+            K.created--;
+        }
+        if (jadd(tsi, g.lateness) <= g.wm) {       // isElementLate
+            atomicAdd(&err->late, 1ull);
+            if (g.side_enabled) {
+                unsigned long long pos = atomicAdd(side_count, 1ull);
+                if ((long long)pos < side_cap) {
+                    side_key[pos] = k;
+                    side_ts[pos] = tsi;
+                    side_val[pos] = v;
+                }
+            }
+        }
+        return;
+    }
+    for (int w = 0; w < p.nwords; ++w) A[3 + w] = combine(p.op[w], A[3 + w], lift_word(p, w, v));
+    if (amax <= g.wm) {
+        emit_row(o, p, rp, k, A[0], A[1], A + 3);  // onElement FIRE
+        atomicAdd(&err->emitted, 1ull);
+    } else {
+        A[2] = 1;                                  // registerEventTimeTimer
+    }
+}
+
+__device__ __forceinline__ void sess_key_end(SessKey &K, uint32_t slot, uint64_t cap, const SessGeom &g, SessErr *err,
+                                             int sw) {
+    if (!K.dirty) return;
+    int64_t *e = K.e;
+    if (K.spilled) {
+        e[1] = -1;
+        e[2] = K.off;
+        e[3] = K.scap;
+        e[4] = K.ns;
+    } else {
+        e[1] = K.ns;
+        for (int i = 0; i < K.ns * sw; ++i) e[2 + i] = K.L[i];
+    }
+    g.due[slot < cap ? slot : cap] = sess_due(K.S, K.ns, sw, g.lateness);
+    if (K.created) atomicAdd(&err->live_delta, (unsigned long long)K.created);
+}
+
+#define SESS_REC_ARGS key, ts, val, p, rp, g, o, err, side_key, side_ts, side_val, side_count, side_cap, sw
+
+// pass 2: one lane per key, records in arrival order.  LISTS: the touched slots, each bucket ordered by selection
+// (a bucket holds at most SESS_BKT_N records: a slot with more is queued for sess_long_kernel); otherwise the
+// slot-sorted records (stable radix sort, gwo_sort.hip), a lane per run head.
+template <bool LISTS>
 __global__ __launch_bounds__(64) void sess_process_kernel(const int64_t *__restrict__ key, const int64_t *__restrict__ ts,
                                                           const int64_t *__restrict__ val, int64_t n,
                                                           const uint32_t *__restrict__ sorted_slot,
@@ -112,145 +294,113 @@ __global__ __launch_bounds__(64) void sess_process_kernel(const int64_t *__restr
                                                           uint64_t cap, int stride, AccPlan p, ResultPlan rp, SessGeom g,
                                                           OutCols o, SessErr *err, int64_t *side_key, int64_t *side_ts,
                                                           int64_t *side_val, unsigned long long *side_count,
-                                                          long long side_cap) {
+                                                          long long side_cap, SessLists ls) {
     extern __shared__ int64_t s_L[];   // [64][smax * sw]: each lane's copy of its key's inline sessions
     const int64_t step = (int64_t)gridDim.x * blockDim.x;
     const int sw = 3 + p.nwords;
-    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n; q += step) {
-        uint32_t slot = sorted_slot[q];
-        if (q > 0 && sorted_slot[q - 1] == slot) continue;  // not the head of this key's run
-        int64_t *e = entry_ptr(t, slot, stride, cap);
-        // the key's session list: the inline sessions copied into L (written back at the end), or its pool array
-        // in this lane's LDS slice (a private array indexed at run time would live in scratch memory)
-        int64_t *L = s_L + (size_t)threadIdx.x * g.smax * sw;
-        int64_t *S = L;
-        int ns, scap = g.smax;
-        int64_t off = 0;
-        bool spilled = e[1] < 0;
-        if (spilled) {
-            off = e[2];
-            scap = (int)e[3];
-            ns = (int)e[4];
-            S = g.pool + (uint64_t)off * sw;
-        } else {
-            ns = (int)e[1];
-            for (int i = 0; i < ns * sw; ++i) L[i] = e[2 + i];
-        }
-        long long created = 0;
-        bool dirty = false;
-        for (int64_t r = q; r < n && sorted_slot[r] == slot; ++r) {
-            const uint32_t i = sorted_idx[r];
-            const int64_t k = key[i], tsi = ts[i];
-            const int64_t v = val ? val[i] : 0;
-            if (tsi == GWO_LONG_MIN) continue;  // the whole batch is rejected by the host
-            const int64_t ws = tsi, we = jadd(tsi, g.gap);
-            // in-flight sessions intersecting [ws, we) (TimeWindow.intersects is inclusive)
-            int64_t ms = ws, me = we;
-            int nm = 0, first = -1;
-            for (int s = 0; s < ns; ++s) {
-                const int64_t *X = S + s * sw;
-                if (X[0] <= we && X[1] >= ws) {
-                    if (first < 0) first = s;
-                    nm++;
-                    ms = X[0] < ms ? X[0] : ms;
-                    me = X[1] > me ? X[1] : me;
-                }
-            }
-            int actual;
-            bool fresh = false;
-            if (nm == 0) {
-                if (ns >= scap) {   // the list is full: spill (or grow) into a pool array twice its size
-                    int64_t *nS = sess_grow(g, S, ns, sw, 2 * scap, off, scap);
-                    if (!nS) {
-                        atomicAdd(&err->pool_full, 1ull);
-                        continue;
-                    }
-                    S = nS;
-                    spilled = true;
-                }
-                actual = ns++;
-                int64_t *X = S + actual * sw;
-                X[0] = ws;
-                X[1] = we;
-                X[2] = 0;
-                for (int w = 0; w < p.nwords; ++w) X[3 + w] = p.ident[w];
-                fresh = true;
-                created++;
-            } else if (nm == 1 && S[first * sw] == ms && S[first * sw + 1] == me) {
-                actual = first;  // new window inside an existing session: no merge callback
-            } else {
-                int64_t rmax = jsub(me, 1);
-                if (jadd(rmax, g.lateness) <= g.wm) {  // WindowOperator.java:318-323
-                    atomicAdd(&err->merge_late, 1ull);
-                    continue;
-                }
-                // mergeNamespaces: fold every merged session into the first
-                int64_t acc[GWO_MAX_WORDS];
-                for (int w = 0; w < p.nwords; ++w) acc[w] = p.ident[w];
-                int keep = 0;
-                for (int s = 0; s < ns; ++s) {
-                    const int64_t *X = S + s * sw;
-                    bool m = X[0] <= we && X[1] >= ws;
-                    if (m) {
-                        for (int w = 0; w < p.nwords; ++w) acc[w] = combine(p.op[w], acc[w], X[3 + w]);
-                    } else {
-                        if (keep != s)
-                            for (int w = 0; w < sw; ++w) S[keep * sw + w] = X[w];
-                        keep++;
-                    }
-                }
-                created -= nm - 1;
-                ns = keep + 1;
-                actual = keep;
-                int64_t *X = S + actual * sw;
-                X[0] = ms;
-                X[1] = me;
-                X[2] = rmax > g.wm ? 1 : 0;  // EventTimeTrigger.onMerge: timer iff maxTs > watermark
-                for (int w = 0; w < p.nwords; ++w) X[3 + w] = acc[w];
-            }
-            dirty = true;
-            int64_t *A = S + actual * sw;
-            const int64_t amax = jsub(A[1], 1);
-            if (cleanup_time(amax, g.lateness) <= g.wm) {  // isWindowLate -> retireWindow
-                if (fresh) {
-                    ns--;
-                    created--;
-                }
-                if (jadd(tsi, g.lateness) <= g.wm) {       // isElementLate
-                    atomicAdd(&err->late, 1ull);
-                    if (g.side_enabled) {
-                        unsigned long long pos = atomicAdd(side_count, 1ull);
-                        if ((long long)pos < side_cap) {
-                            side_key[pos] = k;
-                            side_ts[pos] = tsi;
-                            side_val[pos] = v;
-                        }
-                    }
-                }
+    int64_t *L = s_L + (size_t)threadIdx.x * g.smax * sw;
+    const int64_t nq = LISTS ? (int64_t)ls.ctl[0] : n;
+    unsigned long long nlong = 0;
+    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < nq; q += step) {
+        SessKey K;
+        if (LISTS) {
+            const uint32_t slot = ls.touched[q];
+            uint32_t *bk = ls.bkt + (uint64_t)slot * SESS_BKT;
+            const uint4 b0 = ((const uint4 *)bk)[0], b1 = ((const uint4 *)bk)[1];
+            const uint4 b2 = ((const uint4 *)bk)[2], b3 = ((const uint4 *)bk)[3];
+            const uint32_t c = b0.x;
+            bk[0] = 0;   // the bucket is empty again for the next batch
+            if (c > SESS_BKT_N) {
+                ls.longs[atomicAdd(&ls.ctl[1], 1u)] = slot;
+                nlong++;
                 continue;
             }
-            for (int w = 0; w < p.nwords; ++w) A[3 + w] = combine(p.op[w], A[3 + w], lift_word(p, w, v));
-            if (amax <= g.wm) {
-                emit_row(o, p, rp, k, A[0], A[1], A + 3);  // onElement FIRE
-                atomicAdd(&err->emitted, 1ull);
-            } else {
-                A[2] = 1;                                  // registerEventTimeTimer
+            uint32_t r[SESS_BKT_N] = {b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w, b2.x,
+                                      b2.y, b2.z, b2.w, b3.x, b3.y, b3.z, b3.w};
+#pragma unroll
+            for (int x = 0; x < SESS_BKT_N; ++x) r[x] = x < (int)c ? r[x] : 0xffffffffu;
+            sess_key_begin(K, entry_ptr(t, slot, stride, cap), L, g, sw);
+            for (uint32_t j = 0; j < c; ++j) {   // smallest remaining index first: arrival order
+                uint32_t m = r[0];
+#pragma unroll
+                for (int x = 1; x < SESS_BKT_N; ++x) m = r[x] < m ? r[x] : m;
+#pragma unroll
+                for (int x = 0; x < SESS_BKT_N; ++x) r[x] = r[x] == m ? 0xffffffffu : r[x];
+                sess_key_record(K, m, SESS_REC_ARGS);
             }
-        }
-        if (dirty) {
-            if (spilled) {
-                e[1] = -1;
-                e[2] = off;
-                e[3] = scap;
-                e[4] = ns;
-            } else {
-                e[1] = ns;
-                for (int i = 0; i < ns * sw; ++i) e[2 + i] = L[i];
-            }
-            g.due[slot < cap ? slot : cap] = sess_due(S, ns, sw, g.lateness);
-            if (created) atomicAdd(&err->live_delta, (unsigned long long)created);
+            sess_key_end(K, slot, cap, g, err, sw);
+        } else {
+            const uint32_t slot = sorted_slot[q];
+            if (q > 0 && sorted_slot[q - 1] == slot) continue;  // not the head of this key's run
+            sess_key_begin(K, entry_ptr(t, slot, stride, cap), L, g, sw);
+            int64_t r = q;
+            for (; r < n && sorted_slot[r] == slot; ++r) sess_key_record(K, sorted_idx[r], SESS_REC_ARGS);
+            nlong += r - q > SESS_BKT_N;   // what the lists would have sent to sess_long_kernel (the host's choice)
+            sess_key_end(K, slot, cap, g, err, sw);
         }
     }
+    if (nlong) atomicAdd(&err->long_slots, nlong);
+}
+
+// pass 3 (lists only): the slots whose records overflowed their buckets, a workgroup each: the records' slots are
+// scanned in index order, a chunk at a time, and thread 0 applies the chunk's matches in order.  The batch's last
+// kernel: its last workgroup publishes the statistics block (and the pool's bump counter behind it) into the
+// host-mapped readback, sequence word last, and resets the list counters.
+#define SL_PER 8
+#define SL_CHUNK (256 * SL_PER)
+__global__ __launch_bounds__(256) void sess_long_kernel(const int64_t *__restrict__ key, const int64_t *__restrict__ ts,
+                                                        const int64_t *__restrict__ val, int64_t n,
+                                                        const uint32_t *__restrict__ rec_slot, TableDesc t,
+                                                        uint64_t cap, int stride, AccPlan p, ResultPlan rp, SessGeom g,
+                                                        OutCols o, SessErr *err, int64_t *side_key, int64_t *side_ts,
+                                                        int64_t *side_val, unsigned long long *side_count,
+                                                        long long side_cap, SessLists ls, unsigned long long *rb,
+                                                        unsigned long long seq) {
+    extern __shared__ int64_t s_L[];       // thread 0's copy of the key's inline sessions
+    __shared__ uint32_t s_idx[SL_CHUNK];   // a chunk's records of the key, in arrival order
+    const int sw = 3 + p.nwords;
+    const uint32_t nl = ls.ctl[1];
+    for (uint32_t j = blockIdx.x; j < nl; j += gridDim.x) {
+        const uint32_t slot = ls.longs[j];
+        SessKey K;
+        if (threadIdx.x == 0) sess_key_begin(K, entry_ptr(t, slot, stride, cap), s_L, g, sw);
+        for (int64_t c0 = 0; c0 < n; c0 += SL_CHUNK) {
+            const int64_t i0 = c0 + (int64_t)threadIdx.x * SL_PER;
+            uint32_t m = 0;
+            if (i0 + SL_PER <= n) {
+                const uint4 a = ((const uint4 *)(rec_slot + i0))[0], b = ((const uint4 *)(rec_slot + i0))[1];
+                m = (a.x == slot) | (a.y == slot) << 1 | (a.z == slot) << 2 | (a.w == slot) << 3 | (b.x == slot) << 4 |
+                    (b.y == slot) << 5 | (b.z == slot) << 6 | (b.w == slot) << 7;
+            } else {
+                for (int x = 0; x < SL_PER; ++x) m |= (i0 + x < n && rec_slot[i0 + x] == slot) ? 1u << x : 0u;
+            }
+            unsigned tot;
+            unsigned pos = block_exclusive_scan(__popc(m), &tot);
+            for (int x = 0; x < SL_PER; ++x)
+                if ((m >> x) & 1u) s_idx[pos++] = (uint32_t)(i0 + x);
+            __syncthreads();
+            if (threadIdx.x == 0)
+                for (unsigned r = 0; r < tot; ++r) sess_key_record(K, s_idx[r], SESS_REC_ARGS);
+            __syncthreads();
+        }
+        if (threadIdx.x == 0) sess_key_end(K, slot, cap, g, err, sw);
+    }
+    // statistics are device-scope atomics, read back here with read-modify-write atomics (coherent across XCDs)
+    // after every workgroup's stores and atomics completed (vmcnt) and its arrival was counted
+    __shared__ int s_last;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) s_last = atomicAdd(&ls.ctl[2], 1u) == gridDim.x - 1;
+    __syncthreads();
+    if (!s_last) return;
+    constexpr int NWD = (int)(sizeof(SessErr) / 8) + 1;
+    if (threadIdx.x < NWD) rb_put(&rb[threadIdx.x], atomicAdd((unsigned long long *)err + threadIdx.x, 0ull));
+    if (threadIdx.x == 0) {
+        ls.ctl[0] = 0;
+        ls.ctl[1] = 0;
+        ls.ctl[2] = 0;
+    }
+    rb_publish(&rb[NWD], seq);
 }
 
 // watermark: fire pending timers <= wm, clear sessions whose cleanup time <= wm
@@ -413,18 +563,36 @@ static inline int sgrid(int64_t n, int threads, int cap) {
 }
 
 void launch_sess_slot(const int64_t *key, const int64_t *ts, int64_t n, const TableDesc &t, uint64_t cap, int stride,
-                      const SessGeom &g, uint32_t *rec_slot, SessErr *err, hipStream_t s) {
-    hipLaunchKernelGGL(sess_slot_kernel, dim3(sgrid(n, 256, 8192)), dim3(256), 0, s, key, ts, n, t, cap, stride, g,
-                       rec_slot, err);
+                      const SessGeom &g, uint32_t *rec_slot, SessErr *err, const SessLists *ls, hipStream_t s) {
+    if (ls)
+        hipLaunchKernelGGL(sess_slot_kernel<true>, dim3(sgrid(n, 256, 8192)), dim3(256), 0, s, key, ts, n, t, cap,
+                           stride, g, rec_slot, err, *ls);
+    else
+        hipLaunchKernelGGL(sess_slot_kernel<false>, dim3(sgrid(n, 256, 8192)), dim3(256), 0, s, key, ts, n, t, cap,
+                           stride, g, rec_slot, err, SessLists{});
 }
 
 void launch_sess_process(const int64_t *key, const int64_t *ts, const int64_t *val, int64_t n, const uint32_t *sslot,
                          const uint32_t *sidx, const TableDesc &t, uint64_t cap, int stride, const AccPlan &p,
                          const ResultPlan &rp, const SessGeom &g, OutCols o, SessErr *err, int64_t *sk, int64_t *st,
-                         int64_t *sv, unsigned long long *sc, long long scap, hipStream_t s) {
+                         int64_t *sv, unsigned long long *sc, long long scap, const SessLists *ls, hipStream_t s) {
     const size_t lds = (size_t)64 * g.smax * (3 + p.nwords) * 8;
-    hipLaunchKernelGGL(sess_process_kernel, dim3(sgrid(n, 64, 65536)), dim3(64), lds, s, key, ts, val, n, sslot, sidx,
-                       t, cap, stride, p, rp, g, o, err, sk, st, sv, sc, scap);
+    if (ls)
+        hipLaunchKernelGGL(sess_process_kernel<true>, dim3(sgrid(n, 64, 65536)), dim3(64), lds, s, key, ts, val, n,
+                           sslot, sidx, t, cap, stride, p, rp, g, o, err, sk, st, sv, sc, scap, *ls);
+    else
+        hipLaunchKernelGGL(sess_process_kernel<false>, dim3(sgrid(n, 64, 65536)), dim3(64), lds, s, key, ts, val, n,
+                           sslot, sidx, t, cap, stride, p, rp, g, o, err, sk, st, sv, sc, scap, SessLists{});
+}
+
+void launch_sess_long(const int64_t *key, const int64_t *ts, const int64_t *val, int64_t n, const uint32_t *rec_slot,
+                      const TableDesc &t, uint64_t cap, int stride, const AccPlan &p, const ResultPlan &rp,
+                      const SessGeom &g, OutCols o, SessErr *err, int64_t *sk, int64_t *st, int64_t *sv,
+                      unsigned long long *sc, long long scap, const SessLists &ls, unsigned long long *rb,
+                      unsigned long long seq, hipStream_t s) {
+    const size_t lds = (size_t)g.smax * (3 + p.nwords) * 8;
+    hipLaunchKernelGGL(sess_long_kernel, dim3(32), dim3(256), lds, s, key, ts, val, n, rec_slot, t, cap, stride, p, rp,
+                       g, o, err, sk, st, sv, sc, scap, ls, rb, seq);
 }
 
 void launch_sess_fire(const TableDesc &t, uint64_t cap, int stride, const AccPlan &p, const ResultPlan &rp,

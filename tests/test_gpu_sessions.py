@@ -4,6 +4,10 @@ The reference's MergingWindowSet (flink-streaming-java/.../windowing/MergingWind
 number of in-flight windows per key; the GPU entry holds a few inline and spills the rest into a pool
 (gwo_session.hip).  These streams force spills, growth of spilled lists, merges across spilled sessions, re-fires
 with allowedLateness, a checkpoint of spilled keys and their restore -- all against the oracle, bit-exact.
+
+A batch's records are grouped by key in per-slot buckets of SESS_BKT_N records (gwo_internal.h SessLists); keys with
+more records in one batch go through sess_long_kernel, and while many do the host groups with the radix sort instead.
+GWO_SESS_LISTS=0/1 pins either grouping ("auto": the host's choice), read when an operator is created.
 """
 import numpy as np
 import pytest
@@ -72,8 +76,17 @@ def _hot_stream(rng, nsess, gap, extra_keys=50):
     return k[perm], t[perm], rng.integers(-50, 50, len(k)).astype(np.int64)
 
 
+def _mode(monkeypatch, mode):
+    if mode == "auto":
+        monkeypatch.delenv("GWO_SESS_LISTS", raising=False)
+    else:
+        monkeypatch.setenv("GWO_SESS_LISTS", mode)
+
+
+@pytest.mark.parametrize("mode", ["auto", "0"])
 @pytest.mark.parametrize("nsess", [17, 300])
-def test_hot_key_many_inflight_sessions_one_batch(F, nsess):
+def test_hot_key_many_inflight_sessions_one_batch(F, nsess, mode, monkeypatch):
+    _mode(monkeypatch, mode)
     rng = np.random.default_rng(nsess)
     k, t, v = _hot_stream(rng, nsess, 1_000)
     batches = [(len(k), -(1 << 63))]   # every session in flight at once
@@ -83,10 +96,12 @@ def test_hot_key_many_inflight_sessions_one_batch(F, nsess):
     assert sum(1 for r in got if r[0] == 7) == nsess
 
 
+@pytest.mark.parametrize("mode", ["auto", "0"])
 @pytest.mark.parametrize("lateness", [0, 2_500])
-def test_spilled_sessions_grow_merge_and_refire(F, lateness):
+def test_spilled_sessions_grow_merge_and_refire(F, lateness, mode, monkeypatch):
     """Sessions of a hot key accumulate over several batches (the spilled list doubles), then bridging records
     merge runs of spilled sessions, and late records re-fire emitted ones."""
+    _mode(monkeypatch, mode)
     rng = np.random.default_rng(3 + lateness)
     gap = 1_000
     parts = []
@@ -125,4 +140,29 @@ def test_spilled_sessions_checkpoint_and_restore(F):
                (n, int(t[-1]) - 5_000)]
     want, wl = _oracle(k, t, v, batches, 1_000, 0)
     got, gl = _gpu(F, k, t, v, batches, 1_000, 0, snapshot_at=0)   # key 7 holds ~30+ in-flight sessions here
+    assert got == want and gl == wl
+
+
+@pytest.mark.parametrize("mode", ["auto", "0", "1"])
+@pytest.mark.parametrize("lateness", [0, 3_000])
+def test_overflowing_buckets_switch_grouping(F, mode, lateness, monkeypatch):
+    """Batches where hundreds of keys bring more records than a bucket holds (the host switches to the sort after the
+    first), then thin batches (back to the buckets), with watermarks between them: every grouping bit-exact."""
+    _mode(monkeypatch, mode)
+    rng = np.random.default_rng(11 + lateness)
+    gap, ks, ts, batches, t0 = 1_000, [], [], [], 0
+    for b in range(7):
+        heavy = b < 3
+        nkeys, per = (200, 24) if heavy else (3_000, 1)
+        k = np.repeat(rng.integers(0, 5_000, nkeys), per).astype(np.int64)
+        t = t0 + rng.integers(0, 8_000, len(k)).astype(np.int64)
+        perm = rng.permutation(len(k))
+        ks.append(k[perm])
+        ts.append(t[perm])
+        t0 += 6_000
+        batches.append((sum(len(x) for x in ks), t0 - 4_000))
+    k, t = np.concatenate(ks), np.concatenate(ts)
+    v = rng.integers(-100, 100, len(k)).astype(np.int64)
+    want, wl = _oracle(k, t, v, batches, gap, lateness)
+    got, gl = _gpu(F, k, t, v, batches, gap, lateness)
     assert got == want and gl == wl
