@@ -224,17 +224,18 @@ struct SessErr {
 };
 
 // A batch's records grouped by key without a sort (gwo_session.hip): the slot pass appends each record's index to
-// its slot's bucket -- word 0 the count, words 1..SESS_BKT_N the indices, in atomic order -- and the slot to the
-// touched list on its first record; the process pass visits the touched slots, orders each bucket by index (arrival
-// order) and resets its count.  A slot with more records than its bucket holds is queued on `longs` and applied by
-// sess_long_kernel from the records' slots in index order.
+// its slot's bucket -- word 0 the count, words 1..SESS_BKT_N the indices, in atomic order -- and marks the slot's
+// first record (SESS_OWNER in its rec_slot word); the process pass's owner lanes order their buckets by index
+// (arrival order) and reset the counts.  A slot with more records than its bucket holds is queued on `longs` and
+// applied by sess_long_kernel from the records' slots in index order.
 #define SESS_BKT 16
 #define SESS_BKT_N (SESS_BKT - 1)
+#define SESS_OWNER 0x80000000u
 struct SessLists {
     uint32_t *bkt;                     // [(cap + 1) * SESS_BKT], counts zero between batches
-    uint32_t *touched;                 // slots with records this batch
     uint32_t *longs;                   // slots whose records overflowed their bucket
-    uint32_t *ctl;                     // [0] touched count, [1] long count, [2] workgroups done (sess_long_kernel)
+    uint32_t *ctl;                     // [1] long count, [2] workgroups done (sess_long_kernel), [3] workgroups
+                                       // done (sess_fire_kernel)
 };
 
 // ---- host-side launchers (gwo_kernels.hip) -----------------------------------------------------

@@ -19,9 +19,10 @@ void launch_sess_long(const int64_t *key, const int64_t *ts, const int64_t *val,
                       const TableDesc &t, uint64_t cap, int stride, const AccPlan &p, const ResultPlan &rp,
                       const SessGeom &g, OutCols o, SessErr *err, int64_t *sk, int64_t *st, int64_t *sv,
                       unsigned long long *sc, long long scap, const SessLists &ls, unsigned long long *rb,
-                      unsigned long long seq, hipStream_t s);
+                      unsigned long long seq, unsigned long long *reset_rows, hipStream_t s);
 void launch_sess_fire(const TableDesc &t, uint64_t cap, int stride, const AccPlan &p, const ResultPlan &rp,
-                      const SessGeom &g, OutCols o, SessErr *err, hipStream_t s);
+                      const SessGeom &g, OutCols o, SessErr *err, uint32_t *done, unsigned long long *rb,
+                      unsigned long long seq, hipStream_t s);
 void launch_sess_compact(const TableDesc &src, uint64_t cap, const TableDesc &dst, int stride, hipStream_t s);
 void launch_sess_pool_compact(const TableDesc &t, uint64_t cap, int stride, int sw, const int64_t *old_pool,
                               const SessGeom &g, hipStream_t s);
@@ -41,7 +42,10 @@ struct SessionState {
     SessErr err_prev{};             // d_err as of the last read-back
     SessErr e{};                    // the last read-back's change (bad_kg_key: the value itself)
     SessErr *d_err_fire = nullptr;  // the watermark sweep's own block: its readback completes lazily (finish_fire)
-    SessErr *h_err_fire = nullptr;  // pinned
+    SessErr *h_err_fire = nullptr;  // d_err_fire as of the sweep's readback
+    unsigned long long *rbf = nullptr, *rbf_dev = nullptr;   // host-mapped: the sweep's last workgroup publishes it
+    unsigned long long rbf_seq = 0;
+    bool reset_behind_fire = false; // a batch reset the row counter behind the pending sweep (its rows discarded)
     SessErr fire_prev{};
     int sort_digits = 8;            // radix digit bits of the slot sort (GWO_SESS_DIGITS: 8 or 10)
     DevBuf rec_slot, k1, v1, k2, v2, hist;
@@ -50,7 +54,7 @@ struct SessionState {
     // batch's slots in sess_long_kernel) and back once they stop
     bool lists = true, lists_auto = true;
     DevBuf bkt;                     // [(cap + 1) * SESS_BKT] bucket words (counts zero between batches)
-    uint32_t *ctl = nullptr;        // SessLists::ctl
+    uint32_t *ctl = nullptr;        // SessLists::ctl; word 3: sess_fire_kernel's workgroups done
     // spill pool of keys with more in-flight sessions than an entry holds (gwo_internal.h SessGeom)
     int64_t *pool = nullptr;
     uint64_t pool_cap = 0;          // session records
@@ -104,6 +108,10 @@ gwo_status Handle::session_init() {
     GWO_TRY(hipcheck(hipHostMalloc((void **)&S.h_err, sizeof(SessErr) + 8, hipHostMallocDefault), "pinned"));
     GWO_TRY(dalloc((void **)&S.d_err_fire, sizeof(SessErr)));
     GWO_TRY(hipcheck(hipHostMalloc((void **)&S.h_err_fire, sizeof(SessErr), hipHostMallocDefault), "pinned"));
+    GWO_TRY(hipcheck(hipHostMalloc((void **)&S.rbf, sizeof(SessErr) + 8, hipHostMallocCoherent | hipHostMallocMapped),
+                     "fire readback"));
+    memset(S.rbf, 0, sizeof(SessErr) + 8);
+    GWO_TRY(hipcheck(hipHostGetDevicePointer((void **)&S.rbf_dev, S.rbf, 0), "fire readback"));
     GWO_TRY(hipcheck(hipEventCreateWithFlags(&ev_fire, hipEventDisableTiming), "event"));
     GWO_TRY(hipcheck(hipHostMalloc((void **)&S.rb, sizeof(SessErr) + 16, hipHostMallocCoherent | hipHostMallocMapped),
                      "session readback"));
@@ -125,6 +133,7 @@ void Handle::session_free() {
     if (S.d_err) (void)hipFree(S.d_err);
     if (S.h_err) (void)hipHostFree(S.h_err);
     if (S.rb) (void)hipHostFree(S.rb);
+    if (S.rbf) (void)hipHostFree(S.rbf);
     if (S.d_err_fire) (void)hipFree(S.d_err_fire);
     if (S.h_err_fire) (void)hipHostFree(S.h_err_fire);
     if (S.pool) (void)hipFree(S.pool);
@@ -268,7 +277,6 @@ gwo_status Handle::insert_session(const int64_t *k, const int64_t *t, const int6
     if (cfg.allowed_lateness > 0) GWO_TRY(ensure_output((uint64_t)n));   // re-fires: at most one row per record
     GWO_TRY(ensure_buf(S.rec_slot, n * 4));
     GWO_TRY(ensure_buf(S.k1, n * 4));
-    GWO_TRY(ensure_buf(S.v1, n * 4));
     const bool lists = S.lists;
     int64_t hist_words = 0;
     if (lists) {
@@ -277,6 +285,7 @@ gwo_status Handle::insert_session(const int64_t *k, const int64_t *t, const int6
         if (S.bkt.bytes != was)   // a fresh bucket array: every count zero
             GWO_TRY(hipcheck(hipMemsetAsync(S.bkt.ptr, 0, S.bkt.bytes, stream), "session buckets"));
     } else {
+        GWO_TRY(ensure_buf(S.v1, n * 4));
         GWO_TRY(ensure_buf(S.k2, n * 4));
         GWO_TRY(ensure_buf(S.v2, n * 4));
         int64_t nblocks = (n + 4095) / 4096;
@@ -286,8 +295,8 @@ gwo_status Handle::insert_session(const int64_t *k, const int64_t *t, const int6
     if (side_enabled() && side_cap - (long long)side_rows_committed < n)
         GWO_TRY(grow_side((long long)side_rows_committed + n));
     SessGeom g = sess_geom(*this, S.smax);
-    // lists: the touched slots in k1, the overflowing ones in v1 (radix: the sort's buffers)
-    const SessLists ls{(uint32_t *)S.bkt.ptr, (uint32_t *)S.k1.ptr, (uint32_t *)S.v1.ptr, S.ctl};
+    // lists: the overflowing slots in k1 (radix: the sort's buffers)
+    const SessLists ls{(uint32_t *)S.bkt.ptr, (uint32_t *)S.k1.ptr, S.ctl};
     OutCols o = out_cols();
     int64_t *sk = (int64_t *)side_key.ptr, *sts = (int64_t *)side_ts.ptr, *sv = (int64_t *)side_val.ptr;
     const long long scap = side_enabled() ? side_cap : 0;
@@ -296,12 +305,21 @@ gwo_status Handle::insert_session(const int64_t *k, const int64_t *t, const int6
                      stream);
     GWO_TRY(launch_ok("sess slot"));
     if (lists) {
-        launch_sess_process(k, t, v, n, nullptr, nullptr, desc(S.T), S.T.cap, S.stride, plan, rplan, g, o, S.d_err, sk,
+        launch_sess_process(k, t, v, n, (const uint32_t *)S.rec_slot.ptr, nullptr, desc(S.T), S.T.cap, S.stride, plan, rplan, g, o, S.d_err, sk,
                             sts, sv, d_side_count, scap, &ls, stream);
         GWO_TRY(launch_ok("sess process"));
-        // the batch's statistics are published by the last kernel's last workgroup (no publish launch)
+        // the batch's statistics are published by the last kernel's last workgroup (no publish launch), which also
+        // resets the output's row counter after a discard: without allowedLateness a batch emits no rows, so the
+        // counter is free until the next sweep (whose memset this saves).  A sweep still running when the rows
+        // were discarded is ahead of it in the stream: its rows go too (session_finish_fire).
+        unsigned long long *reset_rows = nullptr;
+        if (out_count_dirty && cfg.allowed_lateness == 0 && (!fire_pending || discard_after_fire)) {
+            reset_rows = d_out_count;
+            out_count_dirty = false;
+            S.reset_behind_fire = fire_pending;
+        }
         launch_sess_long(k, t, v, n, (const uint32_t *)S.rec_slot.ptr, desc(S.T), S.T.cap, S.stride, plan, rplan, g, o,
-                         S.d_err, sk, sts, sv, d_side_count, scap, ls, S.rb_dev, ++S.rb_seq, stream);
+                         S.d_err, sk, sts, sv, d_side_count, scap, ls, S.rb_dev, ++S.rb_seq, reset_rows, stream);
         GWO_TRY(launch_ok("sess long"));
         prof_end(GWO_KERNEL_SESSION, n);
     } else {
@@ -380,13 +398,13 @@ gwo_status Handle::fire_session(int64_t new_wm) {
     GWO_TRY(ensure_output(live_bound));
     SessGeom g = sess_geom(*this, S.smax);
     g.wm = new_wm;
+    S.reset_behind_fire = false;
     prof_begin(GWO_KERNEL_FIRE);
-    launch_sess_fire(desc(S.T), S.T.cap, S.stride, plan, rplan, g, out_cols(), S.d_err_fire, stream);
+    launch_sess_fire(desc(S.T), S.T.cap, S.stride, plan, rplan, g, out_cols(), S.d_err_fire, S.ctl + 3, S.rbf_dev,
+                     ++S.rbf_seq, stream);
     GWO_TRY(launch_ok("sess fire"));
     prof_end(GWO_KERNEL_FIRE, (int64_t)S.T.cap);
-    GWO_TRY(hipcheck(hipMemcpyAsync(S.h_err_fire, S.d_err_fire, sizeof(SessErr), hipMemcpyDeviceToHost, stream),
-                     "fire err"));
-    GWO_TRY(hipcheck(hipEventRecord(ev_fire, stream), "event"));
+    GWO_TRY(hipcheck(hipEventRecord(ev_fire, stream), "event"));   // poll_fire's completion test
     fire_pending = true;
     return sess_resolve();
 }
@@ -394,14 +412,16 @@ gwo_status Handle::fire_session(int64_t new_wm) {
 gwo_status Handle::session_finish_fire() {
     SessionState &S = *sess;
     fire_pending = false;
-    GWO_TRY(spin_event(ev_fire, "session fire"));
+    constexpr int NW = (int)(sizeof(SessErr) / 8);
+    GWO_TRY(spin_seq(S.rbf + NW, S.rbf_seq, "session fire readback"));
+    memcpy(S.h_err_fire, S.rbf, sizeof(SessErr));
     const unsigned long long emitted = S.h_err_fire->emitted - S.fire_prev.emitted;
     S.live += S.h_err_fire->live_delta - S.fire_prev.live_delta;
     S.fire_prev = *S.h_err_fire;
     if (discard_after_fire) {   // gwo_discard_output was called while the sweep ran: its rows go too
         discard_after_fire = false;
         rows_gone += emitted;
-        out_count_dirty = true;
+        out_count_dirty = !S.reset_behind_fire;
     } else {
         out_rows += emitted;
     }

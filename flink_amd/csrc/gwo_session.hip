@@ -28,8 +28,8 @@ __device__ __forceinline__ int64_t *entry_ptr(const TableDesc &t, uint32_t slot,
 }
 
 // pass 1: slot of every record's key (claims entries for new keys); with lists (SessLists) also the record's place in
-// its slot's bucket and, for a slot's first record of the batch, the slot's place in the touched list (one append
-// per wave)
+// its slot's bucket, and the slot's first record of the batch marked as the one whose lane applies the bucket
+// (SESS_OWNER in rec_slot)
 template <bool LISTS>
 __global__ __launch_bounds__(256) void sess_slot_kernel(const int64_t *__restrict__ key, const int64_t *__restrict__ ts,
                                                         int64_t n, TableDesc t, uint64_t cap, int stride, SessGeom g,
@@ -47,19 +47,13 @@ __global__ __launch_bounds__(256) void sess_slot_kernel(const int64_t *__restric
         int64_t *a = find_or_insert(t, stride, k, claimed);
         count_claims(t.occ, claimed);
         const uint32_t slot = k == GWO_EMPTY_KEY ? (uint32_t)cap : (uint32_t)((a - 1 - t.base) / stride);
-        rec_slot[i] = slot;
         if (LISTS) {
             uint32_t *bk = ls.bkt + (uint64_t)slot * SESS_BKT;
             const uint32_t r = atomicAdd(bk, 1u);
             if (r < SESS_BKT_N) bk[1 + r] = (uint32_t)i;
-            const uint64_t first = __ballot(r == 0);
-            if (first) {
-                const int lane = threadIdx.x & 63, leader = __ffsll((unsigned long long)first) - 1;
-                uint32_t base = 0;
-                if (lane == leader) base = atomicAdd(&ls.ctl[0], (uint32_t)__popcll(first));
-                base = __shfl(base, leader);
-                if (r == 0) ls.touched[base + __popcll(first & ((1ull << lane) - 1))] = slot;
-            }
+            rec_slot[i] = slot | (r == 0 ? SESS_OWNER : 0u);
+        } else {
+            rec_slot[i] = slot;
         }
     }
 }
@@ -67,7 +61,7 @@ __global__ __launch_bounds__(256) void sess_slot_kernel(const int64_t *__restric
 // One output row at a reserved position (rows past the output capacity are counted, not written).
 __device__ __forceinline__ void emit_row_at(const OutCols &o, const AccPlan &p, const ResultPlan &rp,
                                             unsigned long long pos, int64_t key, int64_t start, int64_t end,
-                                            const int64_t *acc) {
+                                            const int64_t *acc, int ast = 1) {
     if ((long long)pos >= o.cap) return;
     o.key[pos] = key;
     o.start[pos] = start;
@@ -77,21 +71,16 @@ __device__ __forceinline__ void emit_row_at(const OutCols &o, const AccPlan &p, 
         int64_t r;
         switch (rp.kind[a]) {
             case 2:
-            case 3: r = rp.value_is_f64 ? f64_from_order_key(acc[w]) : acc[w]; break;
+            case 3: r = rp.value_is_f64 ? f64_from_order_key(acc[w * ast]) : acc[w * ast]; break;
             case 4: {
-                double s = rp.value_is_f64 ? __longlong_as_double(acc[w]) : (double)acc[w];
-                r = __double_as_longlong(s / (double)acc[w + 1]);
+                double s = rp.value_is_f64 ? __longlong_as_double(acc[w * ast]) : (double)acc[w * ast];
+                r = __double_as_longlong(s / (double)acc[(w + 1) * ast]);
                 break;
             }
-            default: r = acc[w]; break;
+            default: r = acc[w * ast]; break;
         }
         o.res[a][pos] = r;
     }
-}
-
-__device__ __forceinline__ void emit_row(const OutCols &o, const AccPlan &p, const ResultPlan &rp, int64_t key,
-                                         int64_t start, int64_t end, const int64_t *acc) {
-    emit_row_at(o, p, rp, atomicAdd(o.count, 1ull), key, start, end, acc);
 }
 
 #define SESS_MAXS 16
@@ -100,46 +89,51 @@ __device__ __forceinline__ void emit_row(const OutCols &o, const AccPlan &p, con
 // The earliest watermark at which an entry's sessions need the fire sweep: a pending event-time timer fires at
 // maxTimestamp = end - 1 (EventTimeTrigger.onEventTime), a session retires at cleanupTime(maxTimestamp)
 // (WindowOperator.java:528-540).  The sweep only visits slots whose value the watermark reached.
-__device__ __forceinline__ int64_t sess_due(const int64_t *S, int ns, int sw, int64_t lateness) {
+__device__ __forceinline__ int64_t sess_due(const int64_t *S, int ns, int sw, int64_t lateness, int sst = 1) {
     int64_t d = SESS_NONE;
     for (int s = 0; s < ns; ++s) {
-        const int64_t mx = jsub(S[s * sw + 1], 1);
-        const int64_t t = (S[s * sw + 2] & 1) ? mx : cleanup_time(mx, lateness);
+        const int64_t mx = jsub(S[(s * sw + 1) * sst], 1);
+        const int64_t t = (S[(s * sw + 2) * sst] & 1) ? mx : cleanup_time(mx, lateness);
         d = t < d ? t : d;
     }
     return d;
 }
 
-// Moves a key's session list into a fresh pool array of at least `want` sessions (doubling); returns the
-// array or nullptr when the pool is exhausted (the host sizes the pool so that cannot happen).
-__device__ __forceinline__ int64_t *sess_grow(const SessGeom &g, const int64_t *S, int ns, int sw, int want,
+// Moves a key's session list (element stride sst) into a fresh pool array of at least `want` sessions (doubling);
+// returns the array or nullptr when the pool is exhausted (the host sizes the pool so that cannot happen).
+__device__ __forceinline__ int64_t *sess_grow(const SessGeom &g, const int64_t *S, int sst, int ns, int sw, int want,
                                               int64_t &off, int &scap) {
     const unsigned long long o = atomicAdd(g.pool_top, (unsigned long long)want);
     if (o + (unsigned long long)want > g.pool_cap) return nullptr;
     int64_t *dst = g.pool + o * (unsigned long long)sw;
-    for (int i = 0; i < ns * sw; ++i) dst[i] = S[i];
+    for (int i = 0; i < ns * sw; ++i) dst[i] = S[i * sst];
     off = (int64_t)o;
     scap = want;
     return dst;
 }
 
 // One key's session list while a batch's records are applied to it (sess_key_*): the inline sessions copied into
-// this lane's LDS slice L (written back at the end), or its pool array.  A private array indexed at run time would
-// live in scratch memory.
+// LDS (written back at the end), or its pool array.  Word i of the list is S[i * sst]: a lane's LDS copy is
+// interleaved with its wave's other lanes (sst = 64: word i of lane l at L0[i * 64 + l]), so the lanes of a wave
+// touch consecutive words -- a slice per lane (a 256-B stride) put every lane's access on the same LDS bank.  A
+// private array indexed at run time would live in scratch memory.
 struct SessKey {
     int64_t *e;
-    int64_t *L;
-    int64_t *S;
+    int64_t *L;      // the LDS copy (word i at L[i * lst])
+    int64_t *S;      // the list being edited: L, or the key's pool array
     int64_t off;
     int ns, scap;
+    int lst, sst;    // element strides of L and of S
     bool spilled, dirty;
     long long created;
 };
 
-__device__ __forceinline__ void sess_key_begin(SessKey &K, int64_t *e, int64_t *L, const SessGeom &g, int sw) {
+__device__ __forceinline__ void sess_key_begin(SessKey &K, int64_t *e, int64_t *L, int lst, const SessGeom &g, int sw) {
     K.e = e;
     K.L = L;
+    K.lst = lst;
     K.S = L;
+    K.sst = lst;
     K.scap = g.smax;
     K.off = 0;
     K.spilled = e[1] < 0;
@@ -150,58 +144,96 @@ __device__ __forceinline__ void sess_key_begin(SessKey &K, int64_t *e, int64_t *
         K.scap = (int)e[3];
         K.ns = (int)e[4];
         K.S = g.pool + (uint64_t)K.off * sw;
+        K.sst = 1;
     } else {
         K.ns = (int)e[1];
-        for (int i = 0; i < K.ns * sw; ++i) L[i] = e[2 + i];
+        for (int i = 0; i < K.ns * sw; ++i) L[i * lst] = e[2 + i];
     }
 }
 
-// Record i applied to its key's sessions: WindowOperator.processElement's merging branch.
-__device__ __forceinline__ void sess_key_record(SessKey &K, uint32_t i, const int64_t *__restrict__ key,
-                                                const int64_t *__restrict__ ts, const int64_t *__restrict__ val,
-                                                const AccPlan &p, const ResultPlan &rp, const SessGeom &g,
-                                                const OutCols &o, SessErr *err, int64_t *side_key, int64_t *side_ts,
-                                                int64_t *side_val, unsigned long long *side_count, long long side_cap,
-                                                int sw) {
-    const int64_t k = key[i], tsi = ts[i];
-    const int64_t v = val ? val[i] : 0;
+// The same with every inline word loaded at once (smax sessions, used or not: one round trip instead of a chain of
+// dependent loads), the entry's key and session count in the same round trip.
+__device__ __forceinline__ void sess_key_begin_bulk(SessKey &K, int64_t *e, int64_t *L, int lst, const SessGeom &g,
+                                                    int sw) {
+    const int nwd = g.smax * sw;
+    const int64_t e1 = e[1], e2 = e[2], e3 = e[3], e4 = e[4];
+    for (int i0 = 0; i0 < nwd; i0 += 16) {   // e + 2 is 16-B aligned (even stride); words past nwd stay in the entry
+        longlong2 w[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+            w[j] = i0 + 2 * j < nwd ? ((const longlong2 *)(e + 2 + i0))[j] : make_longlong2(0, 0);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            if (i0 + 2 * j < nwd) L[(i0 + 2 * j) * lst] = w[j].x;
+            if (i0 + 2 * j + 1 < nwd) L[(i0 + 2 * j + 1) * lst] = w[j].y;
+        }
+    }
+    K.e = e;
+    K.L = L;
+    K.lst = lst;
+    K.S = L;
+    K.sst = lst;
+    K.scap = g.smax;
+    K.off = 0;
+    K.spilled = e1 < 0;
+    K.dirty = false;
+    K.created = 0;
+    K.ns = (int)e1;
+    if (K.spilled) {
+        K.off = e2;
+        K.scap = (int)e3;
+        K.ns = (int)e4;
+        K.S = g.pool + (uint64_t)K.off * sw;
+        K.sst = 1;
+    }
+}
+
+// Record (k, tsi, v) applied to its key's sessions: WindowOperator.processElement's merging branch.
+__device__ __forceinline__ void sess_key_record(SessKey &K, int64_t k, int64_t tsi, int64_t v, const AccPlan &p,
+                                                const ResultPlan &rp, const SessGeom &g, const OutCols &o,
+                                                SessErr *err, int64_t *side_key, int64_t *side_ts, int64_t *side_val,
+                                                unsigned long long *side_count, long long side_cap, int sw) {
     if (tsi == GWO_LONG_MIN) return;  // the whole batch is rejected by the host
     const int64_t ws = tsi, we = jadd(tsi, g.gap);
     int64_t *S = K.S;
+    int sst = K.sst;
+    int ssw = sw * sst;   // one session's step
     int ns = K.ns;
     // in-flight sessions intersecting [ws, we) (TimeWindow.intersects is inclusive)
     int64_t ms = ws, me = we;
     int nm = 0, first = -1;
     for (int s = 0; s < ns; ++s) {
-        const int64_t *X = S + s * sw;
-        if (X[0] <= we && X[1] >= ws) {
+        const int64_t x0 = S[s * ssw], x1 = S[s * ssw + sst];
+        if (x0 <= we && x1 >= ws) {
             if (first < 0) first = s;
             nm++;
-            ms = X[0] < ms ? X[0] : ms;
-            me = X[1] > me ? X[1] : me;
+            ms = x0 < ms ? x0 : ms;
+            me = x1 > me ? x1 : me;
         }
     }
     int actual;
     bool fresh = false;
     if (nm == 0) {
         if (ns >= K.scap) {   // the list is full: spill (or grow) into a pool array twice its size
-            int64_t *nS = sess_grow(g, S, ns, sw, 2 * K.scap, K.off, K.scap);
+            int64_t *nS = sess_grow(g, S, sst, ns, sw, 2 * K.scap, K.off, K.scap);
             if (!nS) {
                 atomicAdd(&err->pool_full, 1ull);
                 return;
             }
             S = K.S = nS;
+            sst = K.sst = 1;
+            ssw = sw;
             K.spilled = true;
         }
         actual = ns++;
-        int64_t *X = S + actual * sw;
+        int64_t *X = S + actual * sw * sst;
         X[0] = ws;
-        X[1] = we;
-        X[2] = 0;
-        for (int w = 0; w < p.nwords; ++w) X[3 + w] = p.ident[w];
+        X[sst] = we;
+        X[2 * sst] = 0;
+        for (int w = 0; w < p.nwords; ++w) X[(3 + w) * sst] = p.ident[w];
         fresh = true;
         K.created++;
-    } else if (nm == 1 && S[first * sw] == ms && S[first * sw + 1] == me) {
+    } else if (nm == 1 && S[first * ssw] == ms && S[first * ssw + sst] == me) {
         actual = first;  // new window inside an existing session: no merge callback
     } else {
         int64_t rmax = jsub(me, 1);
@@ -214,29 +246,29 @@ __device__ __forceinline__ void sess_key_record(SessKey &K, uint32_t i, const in
         for (int w = 0; w < p.nwords; ++w) acc[w] = p.ident[w];
         int keep = 0;
         for (int s = 0; s < ns; ++s) {
-            const int64_t *X = S + s * sw;
-            bool m = X[0] <= we && X[1] >= ws;
+            const int64_t *X = S + s * ssw;
+            bool m = X[0] <= we && X[sst] >= ws;
             if (m) {
-                for (int w = 0; w < p.nwords; ++w) acc[w] = combine(p.op[w], acc[w], X[3 + w]);
+                for (int w = 0; w < p.nwords; ++w) acc[w] = combine(p.op[w], acc[w], X[(3 + w) * sst]);
             } else {
                 if (keep != s)
-                    for (int w = 0; w < sw; ++w) S[keep * sw + w] = X[w];
+                    for (int w = 0; w < sw; ++w) S[keep * ssw + w * sst] = X[w * sst];
                 keep++;
             }
         }
         K.created -= nm - 1;
         ns = keep + 1;
         actual = keep;
-        int64_t *X = S + actual * sw;
+        int64_t *X = S + actual * ssw;
         X[0] = ms;
-        X[1] = me;
-        X[2] = rmax > g.wm ? 1 : 0;  // EventTimeTrigger.onMerge: timer iff maxTs > watermark
-        for (int w = 0; w < p.nwords; ++w) X[3 + w] = acc[w];
+        X[sst] = me;
+        X[2 * sst] = rmax > g.wm ? 1 : 0;  // EventTimeTrigger.onMerge: timer iff maxTs > watermark
+        for (int w = 0; w < p.nwords; ++w) X[(3 + w) * sst] = acc[w];
     }
     K.dirty = true;
     K.ns = ns;
-    int64_t *A = S + actual * sw;
-    const int64_t amax = jsub(A[1], 1);
+    int64_t *A = S + actual * ssw;
+    const int64_t amax = jsub(A[sst], 1);
     if (cleanup_time(amax, g.lateness) <= g.wm) {  // isWindowLate -> retireWindow
         if (fresh) {
             K.ns--;
@@ -255,18 +287,19 @@ __device__ __forceinline__ void sess_key_record(SessKey &K, uint32_t i, const in
         }
         return;
     }
-    for (int w = 0; w < p.nwords; ++w) A[3 + w] = combine(p.op[w], A[3 + w], lift_word(p, w, v));
+    for (int w = 0; w < p.nwords; ++w) A[(3 + w) * sst] = combine(p.op[w], A[(3 + w) * sst], lift_word(p, w, v));
     if (amax <= g.wm) {
-        emit_row(o, p, rp, k, A[0], A[1], A + 3);  // onElement FIRE
+        emit_row_at(o, p, rp, atomicAdd(o.count, 1ull), k, A[0], A[sst], A + 3 * sst, sst);  // onElement FIRE
         atomicAdd(&err->emitted, 1ull);
     } else {
-        A[2] = 1;                                  // registerEventTimeTimer
+        A[2 * sst] = 1;                            // registerEventTimeTimer
     }
 }
 
-__device__ __forceinline__ void sess_key_end(SessKey &K, uint32_t slot, uint64_t cap, const SessGeom &g, SessErr *err,
-                                             int sw) {
-    if (!K.dirty) return;
+// Writes the key's sessions back; returns the change in its number of sessions (summed per wave by the caller:
+// one device-scope add per key on one address serialised ~10K adds per batch).
+__device__ __forceinline__ long long sess_key_end(SessKey &K, uint32_t slot, uint64_t cap, const SessGeom &g, int sw) {
+    if (!K.dirty) return 0;
     int64_t *e = K.e;
     if (K.spilled) {
         e[1] = -1;
@@ -275,17 +308,19 @@ __device__ __forceinline__ void sess_key_end(SessKey &K, uint32_t slot, uint64_t
         e[4] = K.ns;
     } else {
         e[1] = K.ns;
-        for (int i = 0; i < K.ns * sw; ++i) e[2 + i] = K.L[i];
+        for (int i = 0; i < K.ns * sw; ++i) e[2 + i] = K.L[i * K.lst];
     }
-    g.due[slot < cap ? slot : cap] = sess_due(K.S, K.ns, sw, g.lateness);
-    if (K.created) atomicAdd(&err->live_delta, (unsigned long long)K.created);
+    g.due[slot < cap ? slot : cap] = sess_due(K.S, K.ns, sw, g.lateness, K.sst);
+    return K.created;
 }
 
-#define SESS_REC_ARGS key, ts, val, p, rp, g, o, err, side_key, side_ts, side_val, side_count, side_cap, sw
+#define SESS_REC_ARGS p, rp, g, o, err, side_key, side_ts, side_val, side_count, side_cap, sw
+#define SESS_REC(i) key[i], ts[i], val ? val[i] : 0
 
-// pass 2: one lane per key, records in arrival order.  LISTS: the touched slots, each bucket ordered by selection
-// (a bucket holds at most SESS_BKT_N records: a slot with more is queued for sess_long_kernel); otherwise the
-// slot-sorted records (stable radix sort, gwo_sort.hip), a lane per run head.
+// pass 2: one lane per key, records in arrival order.  LISTS: the lane of each slot's first record (the owner flag
+// in rec_slot) loads the bucket, the entry and every bucketed record's timestamp and value at once, then applies the
+// records smallest index first (a bucket holds at most SESS_BKT_N records: a slot with more is queued for
+// sess_long_kernel); otherwise the slot-sorted records (stable radix sort, gwo_sort.hip), a lane per run head.
 template <bool LISTS>
 __global__ __launch_bounds__(64) void sess_process_kernel(const int64_t *__restrict__ key, const int64_t *__restrict__ ts,
                                                           const int64_t *__restrict__ val, int64_t n,
@@ -295,19 +330,23 @@ __global__ __launch_bounds__(64) void sess_process_kernel(const int64_t *__restr
                                                           OutCols o, SessErr *err, int64_t *side_key, int64_t *side_ts,
                                                           int64_t *side_val, unsigned long long *side_count,
                                                           long long side_cap, SessLists ls) {
-    extern __shared__ int64_t s_L[];   // [64][smax * sw]: each lane's copy of its key's inline sessions
+    extern __shared__ int64_t s_L[];   // [smax * sw][64]: the lanes' copies of their keys' inline sessions, interleaved
     const int64_t step = (int64_t)gridDim.x * blockDim.x;
     const int sw = 3 + p.nwords;
-    int64_t *L = s_L + (size_t)threadIdx.x * g.smax * sw;
-    const int64_t nq = LISTS ? (int64_t)ls.ctl[0] : n;
+    int64_t *L = s_L + threadIdx.x;
     unsigned long long nlong = 0;
-    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < nq; q += step) {
+    long long created = 0;
+    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n; q += step) {
         SessKey K;
         if (LISTS) {
-            const uint32_t slot = ls.touched[q];
+            const uint32_t xs = sorted_slot[q];   // rec_slot: the lane of a slot's first record applies its bucket
+            if (!(xs & SESS_OWNER)) continue;
+            const uint32_t slot = xs & ~SESS_OWNER;
             uint32_t *bk = ls.bkt + (uint64_t)slot * SESS_BKT;
             const uint4 b0 = ((const uint4 *)bk)[0], b1 = ((const uint4 *)bk)[1];
             const uint4 b2 = ((const uint4 *)bk)[2], b3 = ((const uint4 *)bk)[3];
+            int64_t *e = entry_ptr(t, slot, stride, cap);
+            sess_key_begin_bulk(K, e, L, 64, g, sw);   // in flight with the bucket
             const uint32_t c = b0.x;
             bk[0] = 0;   // the bucket is empty again for the next batch
             if (c > SESS_BKT_N) {
@@ -317,29 +356,53 @@ __global__ __launch_bounds__(64) void sess_process_kernel(const int64_t *__restr
             }
             uint32_t r[SESS_BKT_N] = {b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w, b2.x,
                                       b2.y, b2.z, b2.w, b3.x, b3.y, b3.z, b3.w};
+            // every record's timestamp and value in one round trip (unused places load record r[0]'s again)
+            int64_t rt[SESS_BKT_N], rv[SESS_BKT_N];
 #pragma unroll
-            for (int x = 0; x < SESS_BKT_N; ++x) r[x] = x < (int)c ? r[x] : 0xffffffffu;
-            sess_key_begin(K, entry_ptr(t, slot, stride, cap), L, g, sw);
+            for (int x = 0; x < SESS_BKT_N; ++x) {
+                r[x] = x < (int)c ? r[x] : 0xffffffffu;
+                const uint32_t i = x < (int)c ? r[x] : b0.y;
+                rt[x] = ts[i];
+                rv[x] = val ? val[i] : 0;
+            }
+            const int64_t k = slot < cap ? e[0] : GWO_EMPTY_KEY;   // the side slot holds the empty-key marker's key
+#ifdef GWO_SP_NOREC
+            if (rt[0] + rv[0] + k != 12345) continue;
+#endif
+#ifdef GWO_SP_ONE
+            for (uint32_t j = 0; j < (c < 1 ? c : 1); ++j) {
+#else
             for (uint32_t j = 0; j < c; ++j) {   // smallest remaining index first: arrival order
+#endif
                 uint32_t m = r[0];
+                int64_t tm = rt[0], vm = rv[0];
 #pragma unroll
-                for (int x = 1; x < SESS_BKT_N; ++x) m = r[x] < m ? r[x] : m;
+                for (int x = 1; x < SESS_BKT_N; ++x) {
+                    const bool lt = r[x] < m;
+                    m = lt ? r[x] : m;
+                    tm = lt ? rt[x] : tm;
+                    vm = lt ? rv[x] : vm;
+                }
 #pragma unroll
                 for (int x = 0; x < SESS_BKT_N; ++x) r[x] = r[x] == m ? 0xffffffffu : r[x];
-                sess_key_record(K, m, SESS_REC_ARGS);
+                sess_key_record(K, k, tm, vm, SESS_REC_ARGS);
             }
-            sess_key_end(K, slot, cap, g, err, sw);
+            created += sess_key_end(K, slot, cap, g, sw);
         } else {
             const uint32_t slot = sorted_slot[q];
             if (q > 0 && sorted_slot[q - 1] == slot) continue;  // not the head of this key's run
-            sess_key_begin(K, entry_ptr(t, slot, stride, cap), L, g, sw);
+            sess_key_begin(K, entry_ptr(t, slot, stride, cap), L, 64, g, sw);
             int64_t r = q;
-            for (; r < n && sorted_slot[r] == slot; ++r) sess_key_record(K, sorted_idx[r], SESS_REC_ARGS);
+            for (; r < n && sorted_slot[r] == slot; ++r) {
+                const uint32_t i = sorted_idx[r];
+                sess_key_record(K, SESS_REC(i), SESS_REC_ARGS);
+            }
             nlong += r - q > SESS_BKT_N;   // what the lists would have sent to sess_long_kernel (the host's choice)
-            sess_key_end(K, slot, cap, g, err, sw);
+            created += sess_key_end(K, slot, cap, g, sw);
         }
     }
-    if (nlong) atomicAdd(&err->long_slots, nlong);
+    wave_atomic_add(&err->live_delta, (unsigned long long)created);
+    wave_atomic_add(&err->long_slots, nlong);
 }
 
 // pass 3 (lists only): the slots whose records overflowed their buckets, a workgroup each: the records' slots are
@@ -355,7 +418,7 @@ __global__ __launch_bounds__(256) void sess_long_kernel(const int64_t *__restric
                                                         OutCols o, SessErr *err, int64_t *side_key, int64_t *side_ts,
                                                         int64_t *side_val, unsigned long long *side_count,
                                                         long long side_cap, SessLists ls, unsigned long long *rb,
-                                                        unsigned long long seq) {
+                                                        unsigned long long seq, unsigned long long *reset_rows) {
     extern __shared__ int64_t s_L[];       // thread 0's copy of the key's inline sessions
     __shared__ uint32_t s_idx[SL_CHUNK];   // a chunk's records of the key, in arrival order
     const int sw = 3 + p.nwords;
@@ -363,16 +426,19 @@ __global__ __launch_bounds__(256) void sess_long_kernel(const int64_t *__restric
     for (uint32_t j = blockIdx.x; j < nl; j += gridDim.x) {
         const uint32_t slot = ls.longs[j];
         SessKey K;
-        if (threadIdx.x == 0) sess_key_begin(K, entry_ptr(t, slot, stride, cap), s_L, g, sw);
+        if (threadIdx.x == 0) sess_key_begin(K, entry_ptr(t, slot, stride, cap), s_L, 1, g, sw);
         for (int64_t c0 = 0; c0 < n; c0 += SL_CHUNK) {
             const int64_t i0 = c0 + (int64_t)threadIdx.x * SL_PER;
             uint32_t m = 0;
             if (i0 + SL_PER <= n) {
                 const uint4 a = ((const uint4 *)(rec_slot + i0))[0], b = ((const uint4 *)(rec_slot + i0))[1];
-                m = (a.x == slot) | (a.y == slot) << 1 | (a.z == slot) << 2 | (a.w == slot) << 3 | (b.x == slot) << 4 |
-                    (b.y == slot) << 5 | (b.z == slot) << 6 | (b.w == slot) << 7;
+                constexpr uint32_t S_ = ~SESS_OWNER;
+                m = ((a.x & S_) == slot) | ((a.y & S_) == slot) << 1 | ((a.z & S_) == slot) << 2 |
+                    ((a.w & S_) == slot) << 3 | ((b.x & S_) == slot) << 4 | ((b.y & S_) == slot) << 5 |
+                    ((b.z & S_) == slot) << 6 | ((b.w & S_) == slot) << 7;
             } else {
-                for (int x = 0; x < SL_PER; ++x) m |= (i0 + x < n && rec_slot[i0 + x] == slot) ? 1u << x : 0u;
+                for (int x = 0; x < SL_PER; ++x)
+                    m |= (i0 + x < n && (rec_slot[i0 + x] & ~SESS_OWNER) == slot) ? 1u << x : 0u;
             }
             unsigned tot;
             unsigned pos = block_exclusive_scan(__popc(m), &tot);
@@ -380,10 +446,16 @@ __global__ __launch_bounds__(256) void sess_long_kernel(const int64_t *__restric
                 if ((m >> x) & 1u) s_idx[pos++] = (uint32_t)(i0 + x);
             __syncthreads();
             if (threadIdx.x == 0)
-                for (unsigned r = 0; r < tot; ++r) sess_key_record(K, s_idx[r], SESS_REC_ARGS);
+                for (unsigned r = 0; r < tot; ++r) {
+                    const uint32_t i = s_idx[r];
+                    sess_key_record(K, SESS_REC(i), SESS_REC_ARGS);
+                }
             __syncthreads();
         }
-        if (threadIdx.x == 0) sess_key_end(K, slot, cap, g, err, sw);
+        if (threadIdx.x == 0) {
+            const long long c = sess_key_end(K, slot, cap, g, sw);
+            if (c) atomicAdd(&err->live_delta, (unsigned long long)c);
+        }
     }
     // statistics are device-scope atomics, read back here with read-modify-write atomics (coherent across XCDs)
     // after every workgroup's stores and atomics completed (vmcnt) and its arrival was counted
@@ -396,9 +468,9 @@ __global__ __launch_bounds__(256) void sess_long_kernel(const int64_t *__restric
     constexpr int NWD = (int)(sizeof(SessErr) / 8) + 1;
     if (threadIdx.x < NWD) rb_put(&rb[threadIdx.x], atomicAdd((unsigned long long *)err + threadIdx.x, 0ull));
     if (threadIdx.x == 0) {
-        ls.ctl[0] = 0;
         ls.ctl[1] = 0;
         ls.ctl[2] = 0;
+        if (reset_rows) *reset_rows = 0;   // the output's row counter after a discard (instead of a memset)
     }
     rb_publish(&rb[NWD], seq);
 }
@@ -407,8 +479,12 @@ __global__ __launch_bounds__(256) void sess_long_kernel(const int64_t *__restric
 // Persistent workgroups (about one per CU) sweep the slots in rounds of SF_SPT slots per thread; a round counts
 // its rows first and reserves them with ONE returning atomic per workgroup (block_reserve), then emits.  A
 // reservation per wave or per row serialised on the shared row counter: ~180 us per watermark at C5's ~5K
-// fired sessions, for a kernel that does a few microseconds of work.  Statistics: one add per workgroup.
+// fired sessions, for a kernel that does a few microseconds of work.  Statistics: one add per workgroup.  A round's
+// due slots are compacted into a workgroup list and a thread takes one each (C5: 19.1 -> 14.6 us per watermark);
+// more workgroups with fewer slots per thread measured slower (SF_SPT 2 / 1024 workgroups: 33 us, 1 / 2048: 54 us).
+#ifndef SF_SPT
 #define SF_SPT 8
+#endif
 __device__ __forceinline__ int64_t *sess_slot_entry(const TableDesc &t, uint64_t cap, int stride, uint64_t i,
                                                     int64_t &k) {
     if (i < cap) {
@@ -420,12 +496,102 @@ __device__ __forceinline__ int64_t *sess_slot_entry(const TableDesc &t, uint64_t
     return t.side[0] == 0 ? nullptr : t.side;
 }
 
+// One due slot of the sweep: its pending timers at maxTs <= wm emit rows at pos, pos + 1, ... (reserved by the caller;
+// pos is advanced past them for the thread's next due slot), its
+// sessions past their cleanup time retire (WindowOperator.java:430-473, 528-540), its due watermark is recomputed.
+// Returns the number of retired sessions.
+__device__ __forceinline__ long long sf_sweep_slot(int64_t *e, uint64_t i, int64_t k, const TableDesc &t, uint64_t cap,
+                                                   int sw, const AccPlan &p, const ResultPlan &rp, const SessGeom &g,
+                                                   const OutCols &o, unsigned long long &pos) {
+    const bool spilled = e[1] < 0;
+    const int ns = spilled ? (int)e[4] : (int)e[1];
+    int64_t *base = spilled ? g.pool + (uint64_t)e[2] * sw : e + 2;
+    long long removed = 0;
+    int keep = 0;
+    for (int s = 0; s < ns; ++s) {
+        int64_t *S = base + s * sw;
+        const int64_t mx = jsub(S[1], 1);
+        if ((S[2] & 1) && mx <= g.wm) {
+            emit_row_at(o, p, rp, pos++, k, S[0], S[1], S + 3);
+            S[2] &= ~1ll;
+        }
+        if (cleanup_time(mx, g.lateness) <= g.wm) {
+            removed++;
+            continue;
+        }
+        if (keep != s)
+            for (int w = 0; w < sw; ++w) base[keep * sw + w] = S[w];
+        keep++;
+    }
+    if (keep != ns) {
+        if (!spilled) e[1] = keep;
+        else if (keep == 0) e[1] = 0;   // every spilled session retired: the key is inline (and empty) again
+        else e[4] = keep;
+    }
+    g.due[i] = sess_due(base, keep, sw, g.lateness);
+    return removed;
+}
+
 __global__ __launch_bounds__(256) void sess_fire_kernel(TableDesc t, uint64_t cap, int stride, AccPlan p, ResultPlan rp,
-                                                        SessGeom g, OutCols o, SessErr *err) {
+                                                        SessGeom g, OutCols o, SessErr *err, uint32_t *done,
+                                                        unsigned long long *rb, unsigned long long seq) {
     const int sw = 3 + p.nwords;
     const uint64_t span = (uint64_t)gridDim.x * 256;   // slots one pass of the grid covers
     unsigned long long emitted = 0;
     long long removed_all = 0;
+#ifndef GWO_SF_ROUNDS   // (the r03 sweep, kept for A/B: a thread walks its due slots one after another)
+    // the round's due slots compacted into a workgroup list first, then a thread per due slot: its entry header and
+    // first session load in one round trip (a thread with several due slots no longer walks them one after another)
+    __shared__ uint32_t s_due[256 * SF_SPT];
+    for (uint64_t r0 = 0; r0 <= cap; r0 += span * SF_SPT) {
+        unsigned m = 0;
+#pragma unroll
+        for (int j = 0; j < SF_SPT; ++j) {
+            const uint64_t i = r0 + (uint64_t)j * span + (uint64_t)blockIdx.x * 256 + threadIdx.x;
+            const int64_t dv = g.due[i <= cap ? i : cap];
+            m |= (i <= cap && dv <= g.wm) ? 1u << j : 0u;
+        }
+        unsigned tot;
+        unsigned at = block_exclusive_scan(__popc(m), &tot);
+#pragma unroll
+        for (int j = 0; j < SF_SPT; ++j)
+            if ((m >> j) & 1u) s_due[at++] = (uint32_t)((uint64_t)j * span + (uint64_t)blockIdx.x * 256 + threadIdx.x);
+        __syncthreads();
+        for (unsigned b0 = 0; b0 < tot; b0 += 256) {   // workgroup-uniform
+            const uint64_t i = b0 + threadIdx.x < tot ? r0 + s_due[b0 + threadIdx.x] : cap + 1;
+            int64_t *e = nullptr;
+            int64_t k = GWO_EMPTY_KEY, h1 = 0, h2 = 0, h4 = 0, x1 = 0, x2 = 0;
+            if (i <= cap) {
+                int64_t *ee = i < cap ? t.base + i * (uint64_t)stride : t.side;
+                const int64_t h0 = ee[0];   // header and the first inline session's end and flags: one round trip
+                h1 = ee[1];
+                h2 = ee[2];
+                h4 = ee[4];
+                x1 = ee[3];
+                x2 = ee[4];
+                if (i < cap ? h0 != GWO_EMPTY_KEY : h0 != 0) e = ee;
+                k = i < cap ? h0 : GWO_EMPTY_KEY;
+            }
+            unsigned nrow = 0;
+            int ns = 0;
+            const int64_t *base = nullptr;
+            if (e) {
+                const bool spilled = h1 < 0;
+                ns = spilled ? (int)h4 : (int)h1;
+                base = spilled ? g.pool + (uint64_t)h2 * sw : e + 2;
+                for (int s = 0; s < ns; ++s) {   // rows: pending timers at maxTs <= wm (EventTimeTrigger.onEventTime)
+                    const int64_t end = (s || spilled) ? base[s * sw + 1] : x1;
+                    const int64_t fl = (s || spilled) ? base[s * sw + 2] : x2;
+                    nrow += (fl & 1) && jsub(end, 1) <= g.wm;
+                }
+            }
+            unsigned long long pos = block_reserve(nrow, o.count);
+            emitted += nrow;
+            if (e && ns) removed_all += sf_sweep_slot(e, i, k, t, cap, sw, p, rp, g, o, pos);
+        }
+        __syncthreads();   // s_due is rewritten by the next round
+    }
+#else
     // rounds are workgroup-uniform (block_reserve synchronises the workgroup)
     for (uint64_t r0 = 0; r0 <= cap; r0 += span * SF_SPT) {
         unsigned due_m = 0, nrow = 0;
@@ -459,33 +625,10 @@ __global__ __launch_bounds__(256) void sess_fire_kernel(TableDesc t, uint64_t ca
             const uint64_t i = r0 + (uint64_t)j * span + (uint64_t)blockIdx.x * 256 + threadIdx.x;
             int64_t k;
             int64_t *e = sess_slot_entry(t, cap, stride, i, k);
-            const bool spilled = e[1] < 0;
-            const int ns = spilled ? (int)e[4] : (int)e[1];
-            int64_t *base = spilled ? g.pool + (uint64_t)e[2] * sw : e + 2;
-            int keep = 0;
-            for (int s = 0; s < ns; ++s) {
-                int64_t *S = base + s * sw;
-                const int64_t mx = jsub(S[1], 1);
-                if ((S[2] & 1) && mx <= g.wm) {
-                    emit_row_at(o, p, rp, pos++, k, S[0], S[1], S + 3);
-                    S[2] &= ~1ll;
-                }
-                if (cleanup_time(mx, g.lateness) <= g.wm) {
-                    removed_all++;
-                    continue;
-                }
-                if (keep != s)
-                    for (int w = 0; w < sw; ++w) base[keep * sw + w] = S[w];
-                keep++;
-            }
-            if (keep != ns) {
-                if (!spilled) e[1] = keep;
-                else if (keep == 0) e[1] = 0;   // every spilled session retired: the key is inline (and empty) again
-                else e[4] = keep;
-            }
-            g.due[i] = sess_due(base, keep, sw, g.lateness);
+            removed_all += sf_sweep_slot(e, i, k, t, cap, sw, p, rp, g, o, pos);
         }
     }
+#endif
     // workgroup totals: one add each
     __shared__ unsigned long long s_e[4];
     __shared__ long long s_r[4];
@@ -506,6 +649,18 @@ __global__ __launch_bounds__(256) void sess_fire_kernel(TableDesc t, uint64_t ca
         if (e) atomicAdd(&err->emitted, e);
         if (r) atomicAdd(&err->live_delta, (unsigned long long)(-r));
     }
+    // the last workgroup publishes the sweep's statistics into the host-mapped readback, sequence word last (no
+    // copy behind the kernel): read with read-modify-write atomics after every workgroup's adds completed
+    __shared__ int s_last;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) s_last = atomicAdd(done, 1u) == gridDim.x - 1;
+    __syncthreads();
+    if (!s_last) return;
+    constexpr int NW = (int)(sizeof(SessErr) / 8);
+    if (threadIdx.x < NW) rb_put(&rb[threadIdx.x], atomicAdd((unsigned long long *)err + threadIdx.x, 0ull));
+    if (threadIdx.x == 0) *done = 0;
+    rb_publish(&rb[NW], seq);
 }
 
 // Every slot's due watermark from its entry (after a compaction or a restore wrote entries directly).
@@ -589,17 +744,21 @@ void launch_sess_long(const int64_t *key, const int64_t *ts, const int64_t *val,
                       const TableDesc &t, uint64_t cap, int stride, const AccPlan &p, const ResultPlan &rp,
                       const SessGeom &g, OutCols o, SessErr *err, int64_t *sk, int64_t *st, int64_t *sv,
                       unsigned long long *sc, long long scap, const SessLists &ls, unsigned long long *rb,
-                      unsigned long long seq, hipStream_t s) {
+                      unsigned long long seq, unsigned long long *reset_rows, hipStream_t s) {
     const size_t lds = (size_t)g.smax * (3 + p.nwords) * 8;
     hipLaunchKernelGGL(sess_long_kernel, dim3(32), dim3(256), lds, s, key, ts, val, n, rec_slot, t, cap, stride, p, rp,
-                       g, o, err, sk, st, sv, sc, scap, ls, rb, seq);
+                       g, o, err, sk, st, sv, sc, scap, ls, rb, seq, reset_rows);
 }
 
 void launch_sess_fire(const TableDesc &t, uint64_t cap, int stride, const AccPlan &p, const ResultPlan &rp,
-                      const SessGeom &g, OutCols o, SessErr *err, hipStream_t s) {
+                      const SessGeom &g, OutCols o, SessErr *err, uint32_t *done, unsigned long long *rb,
+                      unsigned long long seq, hipStream_t s) {
     // about one workgroup per CU (MI355X: 256), fewer for small tables
-    hipLaunchKernelGGL(sess_fire_kernel, dim3(sgrid((int64_t)cap + 1, 256 * SF_SPT, 256)), dim3(256), 0, s, t, cap,
-                       stride, p, rp, g, o, err);
+#ifndef SF_WG
+#define SF_WG 256
+#endif
+    hipLaunchKernelGGL(sess_fire_kernel, dim3(sgrid((int64_t)cap + 1, 256 * SF_SPT, SF_WG)), dim3(256), 0, s, t, cap,
+                       stride, p, rp, g, o, err, done, rb, seq);
 }
 
 void launch_sess_pool_compact(const TableDesc &t, uint64_t cap, int stride, int sw, const int64_t *old_pool,
