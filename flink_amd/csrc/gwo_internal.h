@@ -236,7 +236,13 @@ struct SessLists {
     uint32_t *longs;                   // slots whose records overflowed their bucket
     uint32_t *ctl;                     // [1] long count, [2] workgroups done (sess_long_kernel), [3] workgroups
                                        // done (sess_fire_kernel)
+    unsigned long long *shards;        // SESS_SHARDS x SESS_SHARD_STRIDE words: [0] live-session change (process
+                                       // kernel), [1] sweep rows, [2] sweep live change; folded by the last workgroups
 };
+// Per-wave statistics adds spread over line-separated shards: ~1200 device-scope adds per batch on ONE address
+// serialise where they meet (one per wave of the process kernel, measured as most of its time).
+#define SESS_SHARDS 64
+#define SESS_SHARD_STRIDE 16
 
 // ---- host-side launchers (gwo_kernels.hip) -----------------------------------------------------
 #include <hip/hip_runtime.h>

@@ -21,8 +21,8 @@ void launch_sess_long(const int64_t *key, const int64_t *ts, const int64_t *val,
                       unsigned long long *sc, long long scap, const SessLists &ls, unsigned long long *rb,
                       unsigned long long seq, unsigned long long *reset_rows, hipStream_t s);
 void launch_sess_fire(const TableDesc &t, uint64_t cap, int stride, const AccPlan &p, const ResultPlan &rp,
-                      const SessGeom &g, OutCols o, SessErr *err, uint32_t *done, unsigned long long *rb,
-                      unsigned long long seq, hipStream_t s);
+                      const SessGeom &g, OutCols o, SessErr *err, uint32_t *done, unsigned long long *shards,
+                      unsigned long long *rb, unsigned long long seq, hipStream_t s);
 void launch_sess_compact(const TableDesc &src, uint64_t cap, const TableDesc &dst, int stride, hipStream_t s);
 void launch_sess_pool_compact(const TableDesc &t, uint64_t cap, int stride, int sw, const int64_t *old_pool,
                               const SessGeom &g, hipStream_t s);
@@ -55,6 +55,7 @@ struct SessionState {
     bool lists = true, lists_auto = true;
     DevBuf bkt;                     // [(cap + 1) * SESS_BKT] bucket words (counts zero between batches)
     uint32_t *ctl = nullptr;        // SessLists::ctl; word 3: sess_fire_kernel's workgroups done
+    unsigned long long *shards = nullptr;   // SessLists::shards (zero between kernels)
     // spill pool of keys with more in-flight sessions than an entry holds (gwo_internal.h SessGeom)
     int64_t *pool = nullptr;
     uint64_t pool_cap = 0;          // session records
@@ -102,6 +103,8 @@ gwo_status Handle::session_init() {
     }
     GWO_TRY(dalloc((void **)&S.ctl, 16));
     GWO_TRY(hipcheck(hipMemsetAsync(S.ctl, 0, 16, stream), "session lists"));
+    GWO_TRY(dalloc((void **)&S.shards, SESS_SHARDS * SESS_SHARD_STRIDE * 8));
+    GWO_TRY(hipcheck(hipMemsetAsync(S.shards, 0, SESS_SHARDS * SESS_SHARD_STRIDE * 8, stream), "session shards"));
     S.stride = (2 + S.smax * (3 + plan.nwords) + 1) & ~1;
     // the pool's bump counter sits right behind the batch's SessErr block: one copy reads both back
     GWO_TRY(dalloc((void **)&S.d_err, sizeof(SessErr) + 8));
@@ -138,6 +141,7 @@ void Handle::session_free() {
     if (S.h_err_fire) (void)hipHostFree(S.h_err_fire);
     if (S.pool) (void)hipFree(S.pool);
     if (S.ctl) (void)hipFree(S.ctl);
+    if (S.shards) (void)hipFree(S.shards);
     S.bkt.release();
     S.rec_slot.release();
     S.k1.release();
@@ -296,7 +300,7 @@ gwo_status Handle::insert_session(const int64_t *k, const int64_t *t, const int6
         GWO_TRY(grow_side((long long)side_rows_committed + n));
     SessGeom g = sess_geom(*this, S.smax);
     // lists: the overflowing slots in k1 (radix: the sort's buffers)
-    const SessLists ls{(uint32_t *)S.bkt.ptr, (uint32_t *)S.k1.ptr, S.ctl};
+    const SessLists ls{(uint32_t *)S.bkt.ptr, (uint32_t *)S.k1.ptr, S.ctl, S.shards};
     OutCols o = out_cols();
     int64_t *sk = (int64_t *)side_key.ptr, *sts = (int64_t *)side_ts.ptr, *sv = (int64_t *)side_val.ptr;
     const long long scap = side_enabled() ? side_cap : 0;
@@ -400,8 +404,8 @@ gwo_status Handle::fire_session(int64_t new_wm) {
     g.wm = new_wm;
     S.reset_behind_fire = false;
     prof_begin(GWO_KERNEL_FIRE);
-    launch_sess_fire(desc(S.T), S.T.cap, S.stride, plan, rplan, g, out_cols(), S.d_err_fire, S.ctl + 3, S.rbf_dev,
-                     ++S.rbf_seq, stream);
+    launch_sess_fire(desc(S.T), S.T.cap, S.stride, plan, rplan, g, out_cols(), S.d_err_fire, S.ctl + 3, S.shards,
+                     S.rbf_dev, ++S.rbf_seq, stream);
     GWO_TRY(launch_ok("sess fire"));
     prof_end(GWO_KERNEL_FIRE, (int64_t)S.T.cap);
     GWO_TRY(hipcheck(hipEventRecord(ev_fire, stream), "event"));   // poll_fire's completion test

@@ -401,8 +401,24 @@ __global__ __launch_bounds__(64) void sess_process_kernel(const int64_t *__restr
             created += sess_key_end(K, slot, cap, g, sw);
         }
     }
-    wave_atomic_add(&err->live_delta, (unsigned long long)created);
+    wave_atomic_add(LISTS ? &ls.shards[(blockIdx.x % SESS_SHARDS) * SESS_SHARD_STRIDE] : &err->live_delta,
+                    (unsigned long long)created);
     wave_atomic_add(&err->long_slots, nlong);
+}
+
+// Folds (reads and resets) shard word w of every shard: called by every thread of the workgroup, the total
+// returned to all.
+__device__ __forceinline__ unsigned long long sess_fold_shards(unsigned long long *shards, int w) {
+    __shared__ unsigned long long s_fold;
+    if (threadIdx.x < 64) {
+        unsigned long long v = threadIdx.x < SESS_SHARDS ? atomicExch(&shards[threadIdx.x * SESS_SHARD_STRIDE + w], 0ull) : 0ull;
+        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+        if (threadIdx.x == 0) s_fold = v;
+    }
+    __syncthreads();
+    const unsigned long long r = s_fold;
+    __syncthreads();
+    return r;
 }
 
 // pass 3 (lists only): the slots whose records overflowed their buckets, a workgroup each: the records' slots are
@@ -466,7 +482,11 @@ __global__ __launch_bounds__(256) void sess_long_kernel(const int64_t *__restric
     __syncthreads();
     if (!s_last) return;
     constexpr int NWD = (int)(sizeof(SessErr) / 8) + 1;
-    if (threadIdx.x < NWD) rb_put(&rb[threadIdx.x], atomicAdd((unsigned long long *)err + threadIdx.x, 0ull));
+    const unsigned long long live = sess_fold_shards(ls.shards, 0);   // the process kernel's live-session change
+    if (threadIdx.x < NWD) {
+        const unsigned long long add = threadIdx.x == (int)(offsetof(SessErr, live_delta) / 8) ? live : 0ull;
+        rb_put(&rb[threadIdx.x], atomicAdd((unsigned long long *)err + threadIdx.x, add) + add);
+    }
     if (threadIdx.x == 0) {
         ls.ctl[1] = 0;
         ls.ctl[2] = 0;
@@ -534,7 +554,8 @@ __device__ __forceinline__ long long sf_sweep_slot(int64_t *e, uint64_t i, int64
 
 __global__ __launch_bounds__(256) void sess_fire_kernel(TableDesc t, uint64_t cap, int stride, AccPlan p, ResultPlan rp,
                                                         SessGeom g, OutCols o, SessErr *err, uint32_t *done,
-                                                        unsigned long long *rb, unsigned long long seq) {
+                                                        unsigned long long *shards, unsigned long long *rb,
+                                                        unsigned long long seq) {
     const int sw = 3 + p.nwords;
     const uint64_t span = (uint64_t)gridDim.x * 256;   // slots one pass of the grid covers
     unsigned long long emitted = 0;
@@ -646,8 +667,9 @@ __global__ __launch_bounds__(256) void sess_fire_kernel(TableDesc t, uint64_t ca
     if (threadIdx.x == 0) {
         const unsigned long long e = s_e[0] + s_e[1] + s_e[2] + s_e[3];
         const long long r = s_r[0] + s_r[1] + s_r[2] + s_r[3];
-        if (e) atomicAdd(&err->emitted, e);
-        if (r) atomicAdd(&err->live_delta, (unsigned long long)(-r));
+        unsigned long long *sh = shards + (blockIdx.x % SESS_SHARDS) * SESS_SHARD_STRIDE;
+        if (e) atomicAdd(sh + 1, e);
+        if (r) atomicAdd(sh + 2, (unsigned long long)(-r));
     }
     // the last workgroup publishes the sweep's statistics into the host-mapped readback, sequence word last (no
     // copy behind the kernel): read with read-modify-write atomics after every workgroup's adds completed
@@ -658,7 +680,14 @@ __global__ __launch_bounds__(256) void sess_fire_kernel(TableDesc t, uint64_t ca
     __syncthreads();
     if (!s_last) return;
     constexpr int NW = (int)(sizeof(SessErr) / 8);
-    if (threadIdx.x < NW) rb_put(&rb[threadIdx.x], atomicAdd((unsigned long long *)err + threadIdx.x, 0ull));
+    const unsigned long long em = sess_fold_shards(shards, 1), lv = sess_fold_shards(shards, 2);
+    if (threadIdx.x < NW) {
+        const int w = threadIdx.x;
+        const unsigned long long add = w == (int)(offsetof(SessErr, emitted) / 8)      ? em
+                                       : w == (int)(offsetof(SessErr, live_delta) / 8) ? lv
+                                                                                       : 0ull;
+        rb_put(&rb[w], atomicAdd((unsigned long long *)err + w, add) + add);
+    }
     if (threadIdx.x == 0) *done = 0;
     rb_publish(&rb[NW], seq);
 }
@@ -751,14 +780,14 @@ void launch_sess_long(const int64_t *key, const int64_t *ts, const int64_t *val,
 }
 
 void launch_sess_fire(const TableDesc &t, uint64_t cap, int stride, const AccPlan &p, const ResultPlan &rp,
-                      const SessGeom &g, OutCols o, SessErr *err, uint32_t *done, unsigned long long *rb,
-                      unsigned long long seq, hipStream_t s) {
+                      const SessGeom &g, OutCols o, SessErr *err, uint32_t *done, unsigned long long *shards,
+                      unsigned long long *rb, unsigned long long seq, hipStream_t s) {
     // about one workgroup per CU (MI355X: 256), fewer for small tables
 #ifndef SF_WG
 #define SF_WG 256
 #endif
     hipLaunchKernelGGL(sess_fire_kernel, dim3(sgrid((int64_t)cap + 1, 256 * SF_SPT, SF_WG)), dim3(256), 0, s, t, cap,
-                       stride, p, rp, g, o, err, done, rb, seq);
+                       stride, p, rp, g, o, err, done, shards, rb, seq);
 }
 
 void launch_sess_pool_compact(const TableDesc &t, uint64_t cap, int stride, int sw, const int64_t *old_pool,
