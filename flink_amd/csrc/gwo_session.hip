@@ -354,40 +354,49 @@ __global__ __launch_bounds__(64) void sess_process_kernel(const int64_t *__restr
                 nlong++;
                 continue;
             }
-            uint32_t r[SESS_BKT_N] = {b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w, b2.x,
-                                      b2.y, b2.z, b2.w, b3.x, b3.y, b3.z, b3.w};
-            // every record's timestamp and value in one round trip (unused places load record r[0]'s again)
-            int64_t rt[SESS_BKT_N], rv[SESS_BKT_N];
+            // the bucket's indices sorted (arrival order) by a bitonic network over 16 registers, then every record's
+            // timestamp and value gathered in that order into this lane's LDS column (one round trip; the record loop
+            // reads them by position -- a selection per record over 15 registers with its payload measured 9 us of
+            // the kernel's 24)
+            uint32_t r[16] = {b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w, b2.x, b2.y, b2.z, b2.w, b3.x, b3.y, b3.z, b3.w,
+                              0xffffffffu};
+#pragma unroll
+            for (int x = 0; x < SESS_BKT_N; ++x) r[x] = x < (int)c ? r[x] : 0xffffffffu;
+#pragma unroll
+            for (int kk = 2; kk <= 16; kk <<= 1)
+#pragma unroll
+                for (int jj = kk >> 1; jj > 0; jj >>= 1)
+#pragma unroll
+                    for (int x = 0; x < 16; ++x) {
+                        const int y = x ^ jj;
+                        if (y > x) {
+                            const uint32_t lo = min(r[x], r[y]), hi = max(r[x], r[y]);
+                            r[x] = (x & kk) == 0 ? lo : hi;
+                            r[y] = (x & kk) == 0 ? hi : lo;
+                        }
+                    }
+            int64_t *R = L + (size_t)g.smax * sw * 64;   // [2 * SESS_BKT_N][64]: (ts, value) of the sorted records
+            int64_t rt[SESS_BKT_N], rv[SESS_BKT_N];   // every load issued before the first is used
 #pragma unroll
             for (int x = 0; x < SESS_BKT_N; ++x) {
-                r[x] = x < (int)c ? r[x] : 0xffffffffu;
-                const uint32_t i = x < (int)c ? r[x] : b0.y;
+                const uint32_t i = x < (int)c ? r[x] : r[0];
                 rt[x] = ts[i];
                 rv[x] = val ? val[i] : 0;
             }
-            const int64_t k = slot < cap ? e[0] : GWO_EMPTY_KEY;   // the side slot holds the empty-key marker's key
-#ifdef GWO_SP_NOREC
-            if (rt[0] + rv[0] + k != 12345) continue;
-#endif
-#ifdef GWO_SP_ONE
-            for (uint32_t j = 0; j < (c < 1 ? c : 1); ++j) {
-#else
-            for (uint32_t j = 0; j < c; ++j) {   // smallest remaining index first: arrival order
-#endif
-                uint32_t m = r[0];
-                int64_t tm = rt[0], vm = rv[0];
 #pragma unroll
-                for (int x = 1; x < SESS_BKT_N; ++x) {
-                    const bool lt = r[x] < m;
-                    m = lt ? r[x] : m;
-                    tm = lt ? rt[x] : tm;
-                    vm = lt ? rv[x] : vm;
+            for (int x = 0; x < SESS_BKT_N; ++x) {
+                if (x < (int)c) {
+                    R[(2 * x) * 64] = rt[x];
+                    R[(2 * x + 1) * 64] = rv[x];
                 }
-#pragma unroll
-                for (int x = 0; x < SESS_BKT_N; ++x) r[x] = r[x] == m ? 0xffffffffu : r[x];
-                sess_key_record(K, k, tm, vm, SESS_REC_ARGS);
             }
+            const int64_t k = slot < cap ? e[0] : GWO_EMPTY_KEY;   // the side slot holds the empty-key marker's key
+            for (uint32_t j = 0; j < c; ++j) sess_key_record(K, k, R[(2 * j) * 64], R[(2 * j + 1) * 64], SESS_REC_ARGS);
+#ifdef GWO_SP_NOEND
+            created += K.created + K.ns;
+#else
             created += sess_key_end(K, slot, cap, g, sw);
+#endif
         } else {
             const uint32_t slot = sorted_slot[q];
             if (q > 0 && sorted_slot[q - 1] == slot) continue;  // not the head of this key's run
@@ -760,7 +769,7 @@ void launch_sess_process(const int64_t *key, const int64_t *ts, const int64_t *v
                          const uint32_t *sidx, const TableDesc &t, uint64_t cap, int stride, const AccPlan &p,
                          const ResultPlan &rp, const SessGeom &g, OutCols o, SessErr *err, int64_t *sk, int64_t *st,
                          int64_t *sv, unsigned long long *sc, long long scap, const SessLists *ls, hipStream_t s) {
-    const size_t lds = (size_t)64 * g.smax * (3 + p.nwords) * 8;
+    const size_t lds = (size_t)64 * (g.smax * (3 + p.nwords) + (ls ? 2 * SESS_BKT_N : 0)) * 8;
     if (ls)
         hipLaunchKernelGGL(sess_process_kernel<true>, dim3(sgrid(n, 64, 65536)), dim3(64), lds, s, key, ts, val, n,
                            sslot, sidx, t, cap, stride, p, rp, g, o, err, sk, st, sv, sc, scap, *ls);
