@@ -200,12 +200,16 @@ __device__ __forceinline__ void sess_key_record(SessKey &K, int64_t k, int64_t t
     int ssw = sw * sst;   // one session's step
     int ns = K.ns;
     // in-flight sessions intersecting [ws, we) (TimeWindow.intersects is inclusive)
-    int64_t ms = ws, me = we;
+    int64_t ms = ws, me = we, f0 = 0, f1 = 0;   // (f0, f1): the first intersecting session
     int nm = 0, first = -1;
     for (int s = 0; s < ns; ++s) {
         const int64_t x0 = S[s * ssw], x1 = S[s * ssw + sst];
         if (x0 <= we && x1 >= ws) {
-            if (first < 0) first = s;
+            if (first < 0) {
+                first = s;
+                f0 = x0;
+                f1 = x1;
+            }
             nm++;
             ms = x0 < ms ? x0 : ms;
             me = x1 > me ? x1 : me;
@@ -233,7 +237,7 @@ __device__ __forceinline__ void sess_key_record(SessKey &K, int64_t k, int64_t t
         for (int w = 0; w < p.nwords; ++w) X[(3 + w) * sst] = p.ident[w];
         fresh = true;
         K.created++;
-    } else if (nm == 1 && S[first * ssw] == ms && S[first * ssw + sst] == me) {
+    } else if (nm == 1 && f0 == ms && f1 == me) {
         actual = first;  // new window inside an existing session: no merge callback
     } else {
         int64_t rmax = jsub(me, 1);
@@ -268,7 +272,7 @@ __device__ __forceinline__ void sess_key_record(SessKey &K, int64_t k, int64_t t
     K.dirty = true;
     K.ns = ns;
     int64_t *A = S + actual * ssw;
-    const int64_t amax = jsub(A[sst], 1);
+    const int64_t amax = jsub(me, 1);   // the session's end: [ws, we) new, the one it lies in, or the merged one
     if (cleanup_time(amax, g.lateness) <= g.wm) {  // isWindowLate -> retireWindow
         if (fresh) {
             K.ns--;
