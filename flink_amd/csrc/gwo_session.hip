@@ -788,7 +788,10 @@ void launch_sess_long(const int64_t *key, const int64_t *ts, const int64_t *val,
                       unsigned long long *sc, long long scap, const SessLists &ls, unsigned long long *rb,
                       unsigned long long seq, unsigned long long *reset_rows, hipStream_t s) {
     const size_t lds = (size_t)g.smax * (3 + p.nwords) * 8;
-    hipLaunchKernelGGL(sess_long_kernel, dim3(32), dim3(256), lds, s, key, ts, val, n, rec_slot, t, cap, stride, p, rp,
+#ifndef SESS_LONG_WG
+#define SESS_LONG_WG 32
+#endif
+    hipLaunchKernelGGL(sess_long_kernel, dim3(SESS_LONG_WG), dim3(256), lds, s, key, ts, val, n, rec_slot, t, cap, stride, p, rp,
                        g, o, err, sk, st, sv, sc, scap, ls, rb, seq, reset_rows);
 }
 
