@@ -472,6 +472,12 @@ gwo_status Handle::log_k1(LogJob &J, bool first_pass) {
     // plan) -- no stream markers around it
     J.timed = profiling && ((prof_mask >> GWO_KERNEL_INSERT) & 1u) && L.clock_khz > 0;
     ca.t0 = J.timed ? L.d_t0 : nullptr;
+    // sliding window steps run synchronously (no sweep in flight): after a discard the row counter is reset by this
+    // K1's tail, ahead of the next step, instead of by a memset right before it
+    if (slog && out_count_dirty && !fire_pending && !out_stale) {
+        ca.reset_rows = d_out_count;
+        out_count_dirty = false;
+    }
     launch_log_part(J.k, J.t, J.v, J.n, J.stride, J.g, J.base, J.nunits, needs_value, L.d_cursor, J.cap,
                     (int64_t *)tmp.ptr, d_stats, (int64_t *)side_key.ptr, (int64_t *)side_ts.ptr,
                     (int64_t *)side_val.ptr, d_side_count, side ? side_cap : 0, side, ca, thr, J.rt, stream);

@@ -126,6 +126,8 @@ struct CollectArgs {
                                  // count of finished shards at done[LOG_SHARDS * LOG_CUR_STRIDE] (the last plans)
     unsigned long long *shard;   // [LOG_SHARDS * LOG_CUR_STRIDE] K1 statistics shards (K1_SW words each, one line)
     unsigned long long *t0;      // device wall clock at workgroup 0's start (K1 timing without stream markers)
+    unsigned long long *reset_rows;   // non-null: the output's row counter, zeroed by the tail (sliding window steps:
+                                      // after a discard, instead of a memset ahead of the next step)
 };
 
 // K1's statistics: every workgroup reduces its counters in LDS and folds them into shard blockIdx % LOG_SHARDS

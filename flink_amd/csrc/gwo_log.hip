@@ -714,6 +714,7 @@ __global__ __launch_bounds__(LOG_K1_THREADS) void log_part_kernel(
     }
     __syncthreads();
     if (s_last) {
+        if (ca.reset_rows && tid == 0) *ca.reset_rows = 0;
         if (ROUTE && rt.mode == 3) {   // route-only re-run: counts out, cursors and arrival counters reset; no plan
             for (int p = tid; p < rt.nranks; p += LOG_K1_THREADS) {
                 rt.count[2 * p] = atomicExch(&rt.cursor[(size_t)p * LOG_CUR_STRIDE], 0ull);
