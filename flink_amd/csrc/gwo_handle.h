@@ -385,7 +385,8 @@ struct Handle {
     gwo_status slog_late_pass(const LogJob &J0);
     void slog_release_before(long long first_pane);
     gwo_status fire_slog(int64_t new_wm);
-    gwo_status slog_step(int64_t start, int64_t end, uint64_t bound, size_t s0, size_t s1, bool emit, bool fresh);
+    gwo_status slog_step(int64_t start, int64_t end, uint64_t bound, size_t s0, size_t s1, bool emit, bool fresh,
+                         bool *redo);
     // comm (gwo_comm.cpp)
     void comm_free();
     gwo_status comm_exchange(const int64_t *k, const int64_t *t, const int64_t *v, int64_t n, const int64_t **aos,

@@ -218,9 +218,14 @@ void Handle::slog_release_before(long long first_pane) {
 }
 
 // One launch of a window step over segments h_segs[s0, s1): R' = R + those segments (rows only when `emit`).
-gwo_status Handle::slog_step(int64_t start, int64_t end, uint64_t bound, size_t s0, size_t s1, bool emit, bool fresh) {
+// redo: set when the step ran speculatively behind a pass 2 that overflowed (its rows are rewound; the caller
+// redoes the split exactly and the step).
+gwo_status Handle::slog_step(int64_t start, int64_t end, uint64_t bound, size_t s0, size_t s1, bool emit, bool fresh,
+                             bool *redo) {
     SlideState &S = *slide;
     SlogState &G = *slog;
+    LogState &L = *logst;
+    *redo = false;
     const int NW = plan.nwords, RW = 1 + NW;
         // R' geometry: the partitions split when the largest one nears the LDS table
         const int in = G.cur, outb = 1 - G.cur;
@@ -270,6 +275,16 @@ gwo_status Handle::slog_step(int64_t start, int64_t end, uint64_t bound, size_t 
             GWO_TRY(spin_seq(G.rb + SLS_WORDS, G.rb_seq, "slog window step"));
             uint64_t st[SLS_WORDS] = {};
             for (int w = 0; w < SLS_WORDS; ++w) st[w] = G.rb[w];
+            if (L.pend.active) {   // queued behind a pass 2 not checked yet (fire_slog): it completed before this step
+                if (L.h_split_flag[L.pend.tmpx] != 0) {   // it overflowed: this step read an incomplete segment
+                    *h_scalar = rows0;
+                    GWO_TRY(hipcheck(hipMemcpyAsync(d_out_count, h_scalar, 8, hipMemcpyHostToDevice, stream),
+                                     "row rewind"));
+                    *redo = true;
+                    return GWO_OK;
+                }
+                L.pend.active = false;   // (log_resolve_split's no-overflow outcome)
+            }
             if (st[SLS_NEG] && !mode) return poison(GWO_ERR_HIP, "sliding log: a key's window count became negative");
             if (st[SLS_LDS]) return poison(GWO_ERR_CAPACITY, "sliding log: a partition overflowed its LDS table");
             if (st[SLS_ROVF]) {   // a partition of R' outgrew its region: larger regions, same step again
@@ -317,7 +332,9 @@ gwo_status Handle::fire_slog(int64_t new_wm) {
     SlogState &G = *slog;
     LogState &L = *logst;
     GWO_TRY(log_flush());
-    GWO_TRY(log_resolve_split());   // every pane's last segment is complete
+    // a pass 2 still unchecked is not waited for: the first window step is queued right behind it and checks its
+    // overflow flag with the step's own readback (an overflow -- rare -- rewinds the step's rows, redoes the split
+    // exactly and then the step); r03 waited here for pass 2, ~30 us of idle GPU per C3 step
     const __int128 j_new = first_unfired_window(new_wm);
     if (!S.j_set) {
         S.J = j_new;
@@ -371,6 +388,8 @@ gwo_status Handle::fire_slog(int64_t new_wm) {
                 leaving.push_back(jt->first);
             }
         }
+        const auto pending_was = G.pending;
+        const uint64_t pending_records_was = G.pending_records;
         G.pending.clear();
         G.pending_records = 0;
         // more segments than one step takes (a rebuild over a whole window, many small batches per pane): chunks
@@ -390,10 +409,18 @@ gwo_status Handle::fire_slog(int64_t new_wm) {
             continue;
         }
         const size_t nchunks = std::max<size_t>(1, (G.h_segs.size() + SLOG_MAX_SEGS - 1) / SLOG_MAX_SEGS);
-        for (size_t ch = 0; ch < nchunks; ++ch) {
+        bool redo = false;
+        for (size_t ch = 0; ch < nchunks && !redo; ++ch) {
             const bool last = ch + 1 == nchunks;
             const size_t s0 = ch * SLOG_MAX_SEGS, s1 = std::min(G.h_segs.size(), s0 + SLOG_MAX_SEGS);
-            GWO_TRY(slog_step(start, end, bound, s0, s1, last, ch == 0 && G.rebuild));
+            GWO_TRY(slog_step(start, end, bound, s0, s1, last, ch == 0 && G.rebuild, &redo));
+        }
+        if (redo) {   // (only the first chunk can be speculative: R is untouched, the window is built again)
+            if (debug) fprintf(stderr, "[gwo] slog: the pass 2 ahead of window %lld overflowed: step redone\n", (long long)start);
+            G.pending = pending_was;
+            G.pending_records = pending_records_was;
+            GWO_TRY(log_resolve_split());
+            continue;
         }
         G.rebuild = G.live == 0;
         for (long long u : leaving) {

@@ -258,3 +258,22 @@ def test_sliding_log_many_small_batches_and_restore_rebuild(F):
     assert sorted((x, s, e, *r) for x, s, e, r in rows + list(c.output)) == want
     assert late_a + c.num_late_records_dropped == late
     c.close()
+
+
+def test_sliding_log_hot_key_pass2_overflow_redo(F):
+    """One key holds half of every batch: its partition outgrows pass 2's speculative capacity, so the window step
+    queued behind that pass 2 (fire_slog no longer waits for it) reads an incomplete segment -- its rows are
+    rewound, the split redone exactly and the step run again.  Same rows as the oracle."""
+    k, t, v, b = _stream(400_000, 100_000, 20_000, 500, 900, 41, span=20_000)
+    k = k.copy()
+    k[::2] = 77   # the hot key
+    # a large key-count hint: pass 2 splits every coarse bucket into many partitions (a partition's capacity is a
+    # share of its bucket, which the hot key's records exceed)
+    op = F.GpuWindowOperator(F.SlidingEventTimeWindows.of(3_000, 1_000),
+                             F.MultiAggregate(F.SumAggregate(), F.CountAggregate()), state_layout="log",
+                             expected_keys=4_000_000)
+    _run(op, k, t, v, b)
+    (wk, ws, we, res), late = V.sliding_lateness0(k, t, v, _final(b), 3_000, 1_000, 0, [1, 0])
+    assert _got(op) == _want(wk, ws, we, res)
+    assert op.num_late_records_dropped == late
+    op.close()
