@@ -372,9 +372,17 @@ gwo_status Handle::poll_fire() {
 gwo_status Handle::state_size(int64_t *entries) {
     GWO_TRY(flush_pending());
     if (cfg.assigner == GWO_ASSIGNER_SESSION) return session_state_size(entries);
-    if (logst) return log_state_size(entries);
+    int64_t s = 0;   // sliding windows restored from a per-window savepoint: their entries
+    if (slide) {
+        for (auto &kv : slide->rwin) s += (int64_t)(kv.second.n_pend + kv.second.n_done);
+        if (slog) s += (int64_t)slog_rwin_count();
+    }
+    if (logst) {
+        GWO_TRY(log_state_size(entries));
+        *entries += s;
+        return GWO_OK;
+    }
     GWO_TRY(read_occupancy());
-    int64_t s = 0;
     for (auto &kv : tables) s += (int64_t)kv.second.occ;
     *entries = s;
     return GWO_OK;

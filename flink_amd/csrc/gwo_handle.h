@@ -31,6 +31,13 @@ struct RestoreRows {
     std::vector<char> mine;                        // row's key group lies in this subtask's KeyGroupRange
 };
 
+// Restored sliding-window entries read back for an export (gwo_slide.cpp slide_restored_rows).
+struct WindowRows {
+    std::vector<int64_t> key, words;               // words: plan.nwords per row
+    std::vector<long long> j;                      // window index (start = j * slide + floorMod(offset, slide))
+    std::vector<char> pending;                     // fire timer pending (else fired, waiting for its cleanup)
+};
+
 const char *status_str(gwo_status s);
 bool is_device_ptr(const void *p);   // NULL counts as device (nothing to stage)
 
@@ -86,6 +93,7 @@ struct LogWindow;
 struct LogJob;
 struct StrDict;        // gwo_strings.cpp
 struct SlogState;      // gwo_slog.cpp
+struct RestoredWindow; // gwo_slide.h
 
 struct Handle {
     static constexpr double kMaxLoad = 0.7;   // grow above this load factor
@@ -326,6 +334,13 @@ struct Handle {
     __int128 first_unfired_window(int64_t at_wm) const;
     gwo_status slide_refire_rows(const int64_t *k, const int64_t *t, const int64_t *v, int64_t n, const WindowGeom &g,
                                  uint64_t records);
+    // sliding windows restored from a per-window savepoint (gwo_import_heap_state; gwo_slide.cpp)
+    gwo_status slide_restore_windows(const RestoreRows &R, int64_t new_wm);
+    gwo_status rwin_fold(RestoredWindow &r, Table &dst, int sign, int live_word, unsigned long long *live);
+    void rwin_release_before(long long j);
+    bool slide_has_restored() const;
+    gwo_status slide_restored_rows(WindowRows &out);
+    gwo_status restore_impl(const gwo_state_rows *rows, int32_t n_words, int64_t n, int64_t new_wm, bool per_window);
     // sessions (gwo_session.cpp)
     gwo_status sess_alloc(uint64_t cap, Table &t, int64_t **due);
     gwo_status sess_rebuild_due();
@@ -387,6 +402,11 @@ struct Handle {
     gwo_status fire_slog(int64_t new_wm);
     gwo_status slog_step(int64_t start, int64_t end, uint64_t bound, size_t s0, size_t s1, bool emit, bool fresh,
                          bool *redo);
+    gwo_status slog_rwin_add(long long j, const std::vector<int64_t> &key, const std::vector<int64_t> &words,
+                             const std::vector<int64_t> &rows);
+    void slog_rwin_release_before(long long j);
+    size_t slog_rwin_count() const;
+    gwo_status slog_rwin_rows(WindowRows &out);
     // comm (gwo_comm.cpp)
     void comm_free();
     gwo_status comm_exchange(const int64_t *k, const int64_t *t, const int64_t *v, int64_t n, const int64_t **aos,

@@ -174,15 +174,21 @@ gwo_status Handle::export_heap_state(const gwo_heap_state_ids *ids, uint8_t *buf
     gwo_state_rows rows{key.data(), start.data(), end.data(), words.data(), kg.data(), timer.data()};
     int64_t n = 0;
     GWO_TRY(snapshot(&rows, (int64_t)m, &n));
+    // sliding windows restored from a per-window savepoint and not retired yet: rows n.. of `key`
+    WindowRows RWn;
+    if (cfg.assigner == GWO_ASSIGNER_SLIDING) GWO_TRY(slide_restored_rows(RWn));
+    const int64_t nr = (int64_t)RWn.key.size();
+    key.resize((size_t)n);
+    key.insert(key.end(), RWn.key.begin(), RWn.key.end());
     // String keys: the Strings of the ids (StringValue.writeString writes their UTF-16 units)
     std::vector<int64_t> soff;
     std::vector<uint16_t> sch;
-    if (cfg.key_kind == GWO_KEY_STRING && n > 0) {
-        soff.resize(n + 1);
+    if (cfg.key_kind == GWO_KEY_STRING && n + nr > 0) {
+        soff.resize(n + nr + 1);
         int64_t need = 0;
-        GWO_TRY(key_strings(key.data(), n, soff.data(), nullptr, 0, &need));
+        GWO_TRY(key_strings(key.data(), n + nr, soff.data(), nullptr, 0, &need));
         sch.resize(std::max<int64_t>(need, 1));
-        GWO_TRY(key_strings(key.data(), n, soff.data(), sch.data(), (int64_t)sch.size(), &need));
+        GWO_TRY(key_strings(key.data(), n + nr, soff.data(), sch.data(), (int64_t)sch.size(), &need));
     }
     // (key, window) entries: rows as they are, or -- sliding -- each pane's windows that still hold state
     std::vector<WinEntry> es;
@@ -214,6 +220,29 @@ gwo_status Handle::export_heap_state(const gwo_heap_state_ids *ids, uint8_t *buf
                     WinEntry &e = es[it->second];
                     for (int w = 0; w < NW; ++w) e.words[w] = combine_h(plan.op[w], e.words[w], words[i * NW + w]);
                 }
+            }
+        }
+        // restored entries: a window with new records of the key has its timer again; one that only holds restored
+        // entries keeps the timer state it was restored with (pending, or fired and waiting for the cleanup)
+        for (int64_t r = 0; r < nr; ++r) {
+            const __int128 j = RWn.j[r];
+            auto it = at.find({RWn.key[r], j});
+            const int64_t *rw = RWn.words.data() + (size_t)r * NW;
+            if (it == at.end()) {
+                WinEntry e;
+                e.key = RWn.key[r];
+                e.kg = key_group(e.key, cfg.key_kind, cfg.max_parallelism);
+                e.start = win_start(j);
+                e.end = (int64_t)((uint64_t)e.start + (uint64_t)cfg.size);
+                e.words.assign(rw, rw + NW);
+                e.pending = RWn.pending[r] != 0;
+                at[{e.key, j}] = es.size();
+                es.push_back(std::move(e));
+                row_of.push_back(n + r);
+            } else {
+                WinEntry &e = es[it->second];
+                for (int w = 0; w < NW; ++w) e.words[w] = combine_h(plan.op[w], e.words[w], rw[w]);
+                e.pending = e.pending || RWn.pending[r] != 0;
             }
         }
         std::vector<size_t> ord(es.size());
@@ -331,10 +360,9 @@ gwo_status Handle::export_heap_state(const gwo_heap_state_ids *ids, uint8_t *buf
 
 gwo_status Handle::import_heap_state(const gwo_heap_state_ids *ids, const uint8_t *buf, int64_t len, int64_t new_wm) {
     if (!ids || (!buf && len > 0)) return fail(GWO_ERR_INVALID_ARGUMENT, "import_heap_state: ids and buf are required");
-    if (cfg.assigner == GWO_ASSIGNER_SLIDING)
-        return fail(GWO_ERR_UNSUPPORTED, "import_heap_state: sliding windows keep panes; a per-window savepoint "
-                                         "cannot be split into panes");
     const bool merging = cfg.assigner == GWO_ASSIGNER_SESSION;
+    if (merging && ids->merging_window_set < 0)
+        return fail(GWO_ERR_INVALID_ARGUMENT, "import_heap_state: session windows need the merging-window-set id");
     Rd r{buf, len};
     struct Entry {
         std::string skey;   // String keys: UTF-16 units as bytes
@@ -363,12 +391,31 @@ gwo_status Handle::import_heap_state(const gwo_heap_state_ids *ids, const uint8_
         }
         if (cfg.key_kind != GWO_KEY_STRING) sk.assign((const char *)&k, 8);
     };
+    // A key group's section holds every registered state once (HeapSnapshotStrategy.java:175-193 iterates the
+    // backend's state tables): WindowOperator's three (four with a merging assigner) in the writer's id order.
+    // Any other id is a keyed state this operator does not keep -- a custom trigger's (e.g. the reference's
+    // session-with-stateful-trigger savepoint) or the user's -- whose entries it cannot even skip: UNSUPPORTED.
+    const int nstates = merging ? 4 : 3;
     while (r.at < r.n && !r.bad) {
         const int32_t g = r.i32();
         const bool mine = g >= cfg.key_group_start && g <= cfg.key_group_end;
-        const int nstates = merging ? 4 : 3;
+        unsigned seen = 0;
         for (int s = 0; s < nstates && !r.bad; ++s) {
             const int16_t id = r.i16();
+            if (r.bad) break;
+            const int bit = id == ids->window_contents ? 0 : id == ids->event_timers ? 1
+                          : id == ids->processing_timers ? 2 : (merging && id == ids->merging_window_set) ? 3 : -1;
+            if (bit < 0)
+                return fail(GWO_ERR_UNSUPPORTED, "import_heap_state: key group %d holds state id %d, which is none of "
+                                                 "the window operator's states (window-contents %d, event timers %d, "
+                                                 "processing timers %d%s): a custom trigger's or another keyed state, "
+                                                 "which this operator does not run", (int)g, (int)id,
+                            (int)ids->window_contents, (int)ids->event_timers, (int)ids->processing_timers,
+                            merging ? ", merging-window-set" : "");
+            if (seen >> bit & 1u)
+                return fail(GWO_ERR_INVALID_ARGUMENT, "import_heap_state: key group %d holds state id %d twice", (int)g,
+                            (int)id);
+            seen |= 1u << bit;
             const int32_t cnt = r.i32();
             if (cnt < 0) r.bad = true;
             for (int32_t e = 0; e < cnt && !r.bad; ++e) {
@@ -402,11 +449,9 @@ gwo_status Handle::import_heap_state(const gwo_heap_state_ids *ids, const uint8_
                     get_key(sk, k);
                     const int64_t ws = r.i64(), we = r.i64();
                     if (mine) timers[std::make_tuple(sk, ws, we, ts)] = 1;
-                } else if (id == ids->processing_timers) {
+                } else {   // (id == ids->processing_timers)
                     return fail(GWO_ERR_UNSUPPORTED, "import_heap_state: processing-time timers in an event-time "
                                                      "window operator's state");
-                } else {
-                    return fail(GWO_ERR_INVALID_ARGUMENT, "import_heap_state: unknown state id %d", (int)id);
                 }
             }
         }
@@ -463,7 +508,8 @@ gwo_status Handle::import_heap_state(const gwo_heap_state_ids *ids, const uint8_
         static int32_t zt = 0;
         rows = gwo_state_rows{z, z, z, z, nullptr, &zt};
     }
-    return restore(&rows, plan.nwords, R.n, new_wm);
+    // sliding: the rows are windows (one accumulator per (key, window)), restored per window
+    return restore_impl(&rows, plan.nwords, R.n, new_wm, cfg.assigner == GWO_ASSIGNER_SLIDING);
 }
 
 }  // namespace gwo
@@ -494,6 +540,8 @@ gwo_status gwo_export_heap_state_begin(gwo_handle *hh, const gwo_heap_state_ids 
     gwo::Handle *h = (gwo::Handle *)hh;
     if (h->poisoned) return h->poison_status;
     gwo::DeviceGuard g(h->cfg.device);
+    std::vector<uint8_t>().swap(h->heap_img);   // a failed _begin leaves no stale image readable
+    h->heap_img_open = false;
     int64_t n = 0;
     GWO_TRY(h->export_heap_state(ids, nullptr, 0, &n, nullptr, nullptr));
     std::vector<uint8_t> img((size_t)std::max<int64_t>(n, 1));
@@ -509,7 +557,7 @@ gwo_status gwo_export_heap_state_read(gwo_handle *hh, int64_t offset, uint8_t *b
     if (!hh || len < 0 || offset < 0 || (len > 0 && !buf)) return GWO_ERR_INVALID_ARGUMENT;
     gwo::Handle *h = (gwo::Handle *)hh;
     if (!h->heap_img_open) return h->fail(GWO_ERR_STATE, "export_heap_state_read: no image (gwo_export_heap_state_begin)");
-    if (offset + len > (int64_t)h->heap_img.size())
+    if (offset > (int64_t)h->heap_img.size() || len > (int64_t)h->heap_img.size() - offset)
         return h->fail(GWO_ERR_INVALID_ARGUMENT, "export_heap_state_read: [%lld, %lld) past the image (%lld bytes)",
                        (long long)offset, (long long)(offset + len), (long long)h->heap_img.size());
     if (len) memcpy(buf, h->heap_img.data() + offset, (size_t)len);

@@ -286,7 +286,8 @@ void launch_merge(const int64_t *key, const int64_t *ts, const int64_t *val, con
 void launch_slide_refire_slots(const int64_t *key, const int64_t *r_idx, const long long *r_u, int64_t m,
                                const AccPlan &p, const WindowGeom &g, unsigned long long *keytab, uint64_t kmask,
                                long long j0, uint32_t nj, const TableDesc *pdir, long long pane_base,
-                               long long pane_len, uint32_t *r_slot, int64_t *before, hipStream_t s);
+                               long long pane_len, const TableDesc *wdir, uint32_t *r_slot, int64_t *before,
+                               hipStream_t s);
 // gwo_sort.hip: stable LSD radix sort of (uint32 key, uint32 payload; vals NULL = index); returns 0 when the
 // result is in (k1, v1), 1 when in (k2, v2).  hist holds hist_cap words (at least 256 * ceil(n / 4096); more lets a
 // small sort use smaller tiles)
@@ -301,9 +302,13 @@ void launch_fire(const TableDesc &t, uint64_t cap, const AccPlan &plan, const Re
                  int64_t end, OutCols out, int reset, int live_word, hipStream_t s);
 
 // dst += sign * src for every occupied entry of src (sign -1 only for all-ACC_ADD_I64 plans);
-// live_word/live maintain dst's count of entries with a positive count word.
+// live_word/live maintain dst's count of entries with a positive count word.  existing != 0: only the keys dst
+// already holds (live, with live_word >= 0) are combined.
 void launch_fold(const TableDesc &src, uint64_t src_cap, const TableDesc &dst, const AccPlan &plan, int sign,
-                 int live_word, unsigned long long *live, hipStream_t s);
+                 int live_word, unsigned long long *live, hipStream_t s, int existing = 0);
+// rows (key[i], words[i * nwords ...]) combined into table t
+void launch_rows_insert(const int64_t *key, const int64_t *words, int64_t n, const TableDesc &t, const AccPlan &p,
+                        hipStream_t s);
 
 // rehash keeping only entries whose live_word is > 0 (live_word < 0: every occupied entry)
 void launch_rehash_live(const TableDesc &src, uint64_t src_cap, const TableDesc &dst, const AccPlan &plan,

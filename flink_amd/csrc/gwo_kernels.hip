@@ -1166,10 +1166,25 @@ __global__ __launch_bounds__(256) void rehash_kernel(TableDesc src, uint64_t cap
     }
 }
 
+__device__ __forceinline__ const int64_t *table_find(const TableDesc &t, int stride, int64_t key) {
+    if (!t.base) return nullptr;
+    if (key == GWO_EMPTY_KEY) return t.side[0] != 0 ? t.side + 1 : nullptr;
+    uint64_t slot = slot_hash(key) & t.mask;
+    while (true) {
+        const int64_t *e = t.base + slot * (uint64_t)stride;
+        if (e[0] == key) return e + 1;
+        if (e[0] == GWO_EMPTY_KEY) return nullptr;
+        slot = (slot + 1) & t.mask;
+    }
+}
+
 // Pane fold: dst (+/-)= src entry-wise.  Sliding windows: add an entering pane to / subtract a
 // leaving pane from the running window total, or combine a window's panes (recompute strategy).
+// existing != 0: only keys dst already holds (with live_word >= 0: holds live) take src's words -- a restored
+// window's entries whose fire timer already fired join the window's next emission only for keys that have new
+// records in it (WindowOperator re-registers the timer per (key, window) on a new element).
 __global__ __launch_bounds__(256) void fold_kernel(TableDesc src, uint64_t cap, TableDesc dst, AccPlan p, int sign,
-                                                   int live_word, unsigned long long *live) {
+                                                   int live_word, unsigned long long *live, int existing) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     long long dlive = 0;   // live entries this lane added (+) or retired (-): one add per wave at the end
     const uint64_t lane = threadIdx.x & 63, lim = (cap + 1 + 63) & ~63ull;   // whole waves iterate together
@@ -1186,9 +1201,16 @@ __global__ __launch_bounds__(256) void fold_kernel(TableDesc src, uint64_t cap, 
             e = src.side;
             k = GWO_EMPTY_KEY;
         }
-        bool claimed;
-        int64_t *a = find_or_insert(dst, p.stride, k, claimed);
-        count_claims(dst.occ, claimed);
+        int64_t *a;
+        if (existing) {
+            a = (int64_t *)table_find(dst, p.stride, k);
+            if (!a || (live_word >= 0 && __hip_atomic_load(a + live_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <= 0))
+                continue;
+        } else {
+            bool claimed;
+            a = find_or_insert(dst, p.stride, k, claimed);
+            count_claims(dst.occ, claimed);
+        }
         for (int w = 0; w < p.nwords; ++w) {
             int64_t x = e[1 + w];
             if (sign < 0) x = (int64_t)(0ull - (uint64_t)x);   // ACC_ADD_I64 only: wrap-around inverse
@@ -1368,22 +1390,11 @@ __global__ __launch_bounds__(RF_THREADS) void refire_write_kernel(const int64_t 
 // from a scratch table of the batch's re-fire keys (slot words hold key ^ 2^63, 0 = free; the empty-key
 // marker itself takes slot cap).  `before` = the window's state before the batch: its panes' entries
 // for the key, combined (the panes are the pane directory [pane_base, pane_base + pane_len)).
-__device__ __forceinline__ const int64_t *table_find(const TableDesc &t, int stride, int64_t key) {
-    if (!t.base) return nullptr;
-    if (key == GWO_EMPTY_KEY) return t.side[0] != 0 ? t.side + 1 : nullptr;
-    uint64_t slot = slot_hash(key) & t.mask;
-    while (true) {
-        const int64_t *e = t.base + slot * (uint64_t)stride;
-        if (e[0] == key) return e + 1;
-        if (e[0] == GWO_EMPTY_KEY) return nullptr;
-        slot = (slot + 1) & t.mask;
-    }
-}
 
 __global__ __launch_bounds__(RF_THREADS) void slide_refire_slot_kernel(
     const int64_t *__restrict__ key, const int64_t *r_idx, const long long *r_u, int64_t m, AccPlan p, WindowGeom g,
     unsigned long long *keytab, uint64_t kmask, long long j0, uint32_t nj, const TableDesc *__restrict__ pdir,
-    long long pane_base, long long pane_len, uint32_t *r_slot, int64_t *before) {
+    long long pane_base, long long pane_len, const TableDesc *__restrict__ wdir, uint32_t *r_slot, int64_t *before) {
     const int64_t om = jsub(g.offset, fdiv_floor(g.offset, g.slide, g.inv_slide) * g.slide);
     const long long panes = g.size / g.unit;
     for (int64_t j = (int64_t)blockIdx.x * RF_THREADS + threadIdx.x; j < m; j += (int64_t)gridDim.x * RF_THREADS) {
@@ -1411,6 +1422,12 @@ __global__ __launch_bounds__(RF_THREADS) void slide_refire_slot_kernel(
             if (e)
                 for (int x = 0; x < p.nwords; ++x) acc[x] = combine(p.op[x], acc[x], e[x]);
         }
+        if (wdir)   // the window's entries restored from a per-window savepoint (pending and fired ones)
+            for (int h = 0; h < 2; ++h) {
+                const int64_t *e = table_find(wdir[2 * (w - j0) + h], p.stride, k);
+                if (e)
+                    for (int x = 0; x < p.nwords; ++x) acc[x] = combine(p.op[x], acc[x], e[x]);
+            }
         for (int x = 0; x < p.nwords; ++x) before[j * GWO_MAX_WORDS + x] = acc[x];
     }
 }
@@ -1573,10 +1590,11 @@ void launch_refire_emit(const int64_t *key, const int64_t *val, const int64_t *r
 void launch_slide_refire_slots(const int64_t *key, const int64_t *r_idx, const long long *r_u, int64_t m,
                                const AccPlan &p, const WindowGeom &g, unsigned long long *keytab, uint64_t kmask,
                                long long j0, uint32_t nj, const TableDesc *pdir, long long pane_base,
-                               long long pane_len, uint32_t *r_slot, int64_t *before, hipStream_t s) {
+                               long long pane_len, const TableDesc *wdir, uint32_t *r_slot, int64_t *before,
+                               hipStream_t s) {
     int blocks = (int)std::min<int64_t>(1024, (m + RF_THREADS - 1) / RF_THREADS);
     hipLaunchKernelGGL(slide_refire_slot_kernel, dim3(std::max(blocks, 1)), dim3(RF_THREADS), 0, s, key, r_idx, r_u, m,
-                       p, g, keytab, kmask, j0, nj, pdir, pane_base, pane_len, r_slot, before);
+                       p, g, keytab, kmask, j0, nj, pdir, pane_base, pane_len, wdir, r_slot, before);
 }
 
 // Copies nw device words into a host-mapped readback block, sequence word last (the host spins on it instead of a
@@ -1655,9 +1673,27 @@ void launch_rehash_live(const TableDesc &src, uint64_t src_cap, const TableDesc 
 }
 
 void launch_fold(const TableDesc &src, uint64_t src_cap, const TableDesc &dst, const AccPlan &plan, int sign,
-                 int live_word, unsigned long long *live, hipStream_t s) {
+                 int live_word, unsigned long long *live, hipStream_t s, int existing) {
     int grid = grid_for((int64_t)src_cap + 1, 1, 8192);
-    hipLaunchKernelGGL(fold_kernel, dim3(grid), dim3(256), 0, s, src, src_cap, dst, plan, sign, live_word, live);
+    hipLaunchKernelGGL(fold_kernel, dim3(grid), dim3(256), 0, s, src, src_cap, dst, plan, sign, live_word, live,
+                       existing);
+}
+
+// Rows (key, nwords raw words; row-major) combined into one table: a restored sliding window's entries.
+__global__ __launch_bounds__(256) void rows_insert_kernel(const int64_t *key, const int64_t *words, int64_t n,
+                                                          TableDesc t, AccPlan p) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        bool claimed;
+        int64_t *a = find_or_insert(t, p.stride, key[i], claimed);
+        count_claims(t.occ, claimed);
+        for (int w = 0; w < p.nwords; ++w) atomic_combine(a + w, p.op[w], words[i * p.nwords + w]);
+    }
+}
+
+void launch_rows_insert(const int64_t *key, const int64_t *words, int64_t n, const TableDesc &t, const AccPlan &p,
+                        hipStream_t s) {
+    hipLaunchKernelGGL(rows_insert_kernel, dim3(grid_for(n, 1, 4096)), dim3(256), 0, s, key, words, n, t, p);
 }
 
 void launch_key_groups(const int64_t *keys, int64_t n, int key_kind, int max_par, int par, int32_t *kg,

@@ -1331,6 +1331,9 @@ gwo_status gwo_snapshot_rows(gwo_handle *hh, int64_t *n_rows, int32_t *n_words) 
     H_OR_FAIL;
     if (!n_rows || !n_words) return GWO_ERR_INVALID_ARGUMENT;
     *n_words = h->plan.nwords;
+    if (h->slide_has_restored())
+        return h->fail(GWO_ERR_UNSUPPORTED, "snapshot: sliding windows restored from a per-window savepoint are "
+                                            "checkpointed in the heap layout (gwo_export_heap_state) until they retire");
     return h->snapshot_rows(n_rows);
 }
 
@@ -1340,6 +1343,9 @@ gwo_status gwo_snapshot(gwo_handle *hh, const gwo_state_rows *rows, int64_t cap,
         (cap > 0 && (!rows->key || !rows->window_start || !rows->window_end || !rows->words)))
         return GWO_ERR_INVALID_ARGUMENT;
     *watermark = h->wm;
+    if (h->slide_has_restored())
+        return h->fail(GWO_ERR_UNSUPPORTED, "snapshot: sliding windows restored from a per-window savepoint are "
+                                            "checkpointed in the heap layout (gwo_export_heap_state) until they retire");
     return h->snapshot(rows, cap, n_out);
 }
 

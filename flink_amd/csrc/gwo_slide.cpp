@@ -199,8 +199,10 @@ gwo_status Handle::fire_sliding(int64_t new_wm) {
     }
     OutCols o = out_cols();
     while (S.J < j_new) {
-        // ---- skip windows that hold no data ----
+        // ---- skip windows that hold no data (restored entries with a pending fire timer count as data) ----
         long long lo = win_first_pane(S.J), hi = win_last_pane(S.J);
+        auto rw = S.rwin.find((long long)S.J);
+        const bool rpend = rw != S.rwin.end() && rw->second.n_pend > 0;
         bool empty;
         if (S.ring) {
             GWO_TRY(hipcheck(hipMemcpyAsync(&S.h_live, S.d_live, 8, hipMemcpyDeviceToHost, stream), "live"));
@@ -210,10 +212,15 @@ gwo_status Handle::fire_sliding(int64_t new_wm) {
             auto it = tables.lower_bound(lo);
             empty = it == tables.end() || it->first > hi;
         }
-        if (empty) {
+        if (empty && !rpend) {
             __int128 target = j_new;
             auto it = tables.lower_bound(lo);
             if (it != tables.end()) target = std::min(j_new, std::max(S.J + 1, first_window_of_pane(it->first)));
+            for (auto nx = S.rwin.upper_bound((long long)S.J); nx != S.rwin.end(); ++nx)
+                if (nx->second.n_pend) {
+                    target = std::min(target, (__int128)nx->first);
+                    break;
+                }
             // panes before the target window are in no unfired (or uncleaned) window any more
             GWO_TRY(release_panes_before(std::min(win_first_pane(target), keep_from)));
             S.J = target;
@@ -224,6 +231,12 @@ gwo_status Handle::fire_sliding(int64_t new_wm) {
         const int64_t end = (int64_t)((uint64_t)start + (uint64_t)cfg.size);
         // ---- emit window J ----
         if (S.ring) {
+            if (rw != S.rwin.end()) {   // restored entries join J's rows: T += them for the emission, -= after it
+                GWO_TRY(ensure_ring(rw->second.n_pend));
+                GWO_TRY(rwin_fold(rw->second, aux_tables[S.t_idx], +1, S.count_word, S.d_live));
+                GWO_TRY(hipcheck(hipMemcpyAsync(&S.h_live, S.d_live, 8, hipMemcpyDeviceToHost, stream), "live"));
+                GWO_TRY(hipcheck(hipStreamSynchronize(stream), "live sync"));
+            }
             Table &T = aux_tables[S.t_idx];
             GWO_TRY(ensure_output(S.h_live));
             o = out_cols();
@@ -231,8 +244,9 @@ gwo_status Handle::fire_sliding(int64_t new_wm) {
             launch_fire(desc(T), T.cap, plan, rplan, start, end, o, 0, S.count_word, stream);
             prof_end(GWO_KERNEL_FIRE, (int64_t)T.cap);
             out_rows += S.h_live;
+            if (rw != S.rwin.end()) GWO_TRY(rwin_fold(rw->second, T, -1, S.count_word, S.d_live));
         } else {
-            uint64_t total = 0;
+            uint64_t total = rw != S.rwin.end() ? rw->second.n_pend : 0;
             GWO_TRY(read_occupancy());
             for (auto it = tables.lower_bound(lo); it != tables.end() && it->first <= hi; ++it) total += it->second.occ;
             Table W;
@@ -242,6 +256,7 @@ gwo_status Handle::fire_sliding(int64_t new_wm) {
             prof_begin(GWO_KERNEL_SLIDE);
             for (auto it = tables.lower_bound(lo); it != tables.end() && it->first <= hi; ++it)
                 launch_fold(desc(it->second), it->second.cap, desc(W), plan, +1, -1, nullptr, stream);
+            if (rw != S.rwin.end()) GWO_TRY(rwin_fold(rw->second, W, +1, -1, nullptr));   // after the panes
             prof_end(GWO_KERNEL_SLIDE, (int64_t)total);
             uint64_t rows = 0;
             GWO_TRY(ctr_read(W.counter, &rows));
@@ -275,7 +290,150 @@ gwo_status Handle::fire_sliding(int64_t new_wm) {
         S.J += 1;
     }
     // windows whose cleanup time this watermark passed (no fire needed) free their panes too
+    rwin_release_before((long long)std::min(S.J, first_uncleaned_window(new_wm)));
     return release_panes_before(std::min(win_first_pane(S.J), keep_from));
+}
+
+// ---- sliding windows restored from a per-window savepoint (gwo_import_heap_state) ------------------------------
+// Restored entries of window j: pend (fire timer pending) inserted into the window's rows, done (already fired,
+// waiting for the cleanup) only into keys the window holds from new records; sign -1 takes them out again.
+gwo_status Handle::rwin_fold(RestoredWindow &r, Table &dst, int sign, int live_word, unsigned long long *live) {
+    if (r.pend.base) launch_fold(desc(r.pend), r.pend.cap, desc(dst), plan, sign, live_word, live, stream, 0);
+    if (r.done.base) launch_fold(desc(r.done), r.done.cap, desc(dst), plan, sign, live_word, live, stream, 1);
+    GWO_TRY(launch_ok("restored window fold"));
+    if (sign > 0) dst.occ += r.n_pend;   // an upper bound until the next read
+    return GWO_OK;
+}
+
+void Handle::rwin_release_before(long long j) {
+    if (!slide) return;
+    for (auto it = slide->rwin.begin(); it != slide->rwin.end() && it->first < j;) {
+        for (Table *t : {&it->second.pend, &it->second.done})
+            if (t->base) {   // back to the pool clean: a no-output sweep resets every entry
+                OutCols none = out_cols();
+                none.cap = 0;
+                (void)hipMemsetAsync(d_scratch_count, 0, 8, stream);
+                none.count = d_scratch_count;
+                launch_fire(desc(*t), t->cap, plan, rplan, 0, 0, none, 1, -1, stream);
+                release_table(*t);
+            }
+        it = slide->rwin.erase(it);
+    }
+    if (slog) slog_rwin_release_before(j);
+}
+
+bool Handle::slide_has_restored() const {
+    return slide && (!slide->rwin.empty() || (slog && slog_rwin_count() > 0));
+}
+
+// Rows (key, window start, raw words, fire timer pending) of a per-window savepoint: validated, then kept per
+// window (RestoredWindow / the sliding log's partial segments).  New records after the restore go to panes as
+// always; a window's rows combine both when it fires.
+gwo_status Handle::slide_restore_windows(const RestoreRows &R, int64_t new_wm) {
+    SlideState &S = *slide;
+    const int NW = plan.nwords;
+    std::map<long long, std::vector<int64_t>> pend, done;   // window -> row indices
+    for (int64_t i = 0; i < R.n; ++i) {
+        if (!R.mine[i]) continue;
+        const __int128 a = (__int128)R.start[i] - S.om;
+        const __int128 j = fdiv128(a, cfg.slide);
+        if (win_start(j) != R.start[i] || (int64_t)((uint64_t)R.start[i] + (uint64_t)cfg.size) != R.end[i])
+            return fail(GWO_ERR_INVALID_ARGUMENT, "import: [%lld, %lld) is not a window of this sliding assigner",
+                        (long long)R.start[i], (long long)R.end[i]);
+        const int64_t max_ts = (int64_t)((uint64_t)R.end[i] - 1);
+        const bool pending = R.timer.empty() ? max_ts > new_wm : R.timer[i] != 0;
+        if (pending && max_ts <= new_wm)
+            return fail(GWO_ERR_UNSUPPORTED, "import: window [%lld, %lld) has a pending fire timer at or below the "
+                                             "restore watermark %lld (restore at the checkpoint's watermark or "
+                                             "Long.MIN_VALUE)", (long long)R.start[i], (long long)R.end[i],
+                        (long long)new_wm);
+        if (!pending && cleanup_time_host(max_ts) <= new_wm) continue;   // its state is gone at this watermark
+        if (!pending && slog)
+            return fail(GWO_ERR_UNSUPPORTED, "import: window [%lld, %lld) already fired; the sliding log keeps no "
+                                             "fired windows (allowedLateness 0)", (long long)R.start[i],
+                        (long long)R.end[i]);
+        (pending ? pend : done)[(long long)j].push_back(i);
+    }
+    // the count word marks a key present in a window (ring strategies): a restored entry holds >= 1 record
+    std::vector<int64_t> words(R.words);
+    if (S.count_word >= 0) {
+        bool hidden = true;   // slide_init's own count word (no COUNT / AVG aggregate supplies one)
+        for (int a = 0; a < rplan.naggs; ++a) {
+            if (rplan.kind[a] == GWO_AGG_COUNT && rplan.word[a] == S.count_word) hidden = false;
+            if (rplan.kind[a] == GWO_AGG_AVG && rplan.word[a] + 1 == S.count_word) hidden = false;
+        }
+        for (auto *m : {&pend, &done})
+            for (auto &kv : *m)
+                for (int64_t i : kv.second) {
+                    int64_t &c = words[(size_t)i * NW + S.count_word];
+                    if (hidden) c = 1;
+                    else if (c <= 0)
+                        return fail(GWO_ERR_INVALID_ARGUMENT, "import: a window accumulator of key %lld counts %lld "
+                                                              "records", (long long)R.key[i], (long long)c);
+                }
+    }
+    // validated: from here on the handle holds the restored state
+    wm = in_wm = new_wm;
+    if (slog) {
+        GWO_TRY(slog_anchor());
+        for (auto &kv : pend) GWO_TRY(slog_rwin_add(kv.first, R.key, words, kv.second));
+        return GWO_OK;
+    }
+    GWO_TRY(slide_restore_anchor());
+    std::vector<int64_t> hk, hw;
+    DevBuf dk, dw;
+    for (int kind = 0; kind < 2; ++kind)
+        for (auto &kv : kind ? done : pend) {
+            const std::vector<int64_t> &ix = kv.second;
+            hk.clear();
+            hw.clear();
+            for (int64_t i : ix) {
+                hk.push_back(R.key[i]);
+                hw.insert(hw.end(), words.begin() + (size_t)i * NW, words.begin() + (size_t)(i + 1) * NW);
+            }
+            RestoredWindow &rw = S.rwin[kv.first];
+            Table &t = kind ? rw.done : rw.pend;
+            uint64_t cap = kMinCap;
+            while ((double)ix.size() > kInitLoad * (double)cap) cap <<= 1;
+            GWO_TRY(alloc_table(cap, t));
+            (kind ? rw.n_done : rw.n_pend) = ix.size();
+            GWO_TRY(ensure_buf(dk, hk.size() * 8));
+            GWO_TRY(ensure_buf(dw, hw.size() * 8));
+            GWO_TRY(hipcheck(hipMemcpyAsync(dk.ptr, hk.data(), hk.size() * 8, hipMemcpyHostToDevice, stream), "rows"));
+            GWO_TRY(hipcheck(hipMemcpyAsync(dw.ptr, hw.data(), hw.size() * 8, hipMemcpyHostToDevice, stream), "rows"));
+            launch_rows_insert((const int64_t *)dk.ptr, (const int64_t *)dw.ptr, (int64_t)ix.size(), desc(t), plan,
+                               stream);
+            GWO_TRY(launch_ok("restore window"));
+            GWO_TRY(hipcheck(hipStreamSynchronize(stream), "restore window"));   // (dk, dw are reused)
+        }
+    dk.release();
+    dw.release();
+    return GWO_OK;
+}
+
+// The restored entries still held (table layout and sliding log): key, window index, raw words, fire timer pending.
+gwo_status Handle::slide_restored_rows(WindowRows &out) {
+    if (!slide) return GWO_OK;
+    if (slog) return slog_rwin_rows(out);
+    const int NW = plan.nwords;
+    std::vector<int64_t> img;
+    for (auto &kv : slide->rwin)
+        for (int kind = 0; kind < 2; ++kind) {
+            const Table &t = kind ? kv.second.done : kv.second.pend;
+            if (!t.base) continue;
+            img.resize((size_t)(t.cap + 1) * plan.stride);
+            GWO_TRY(hipcheck(hipMemcpy(img.data(), t.base, img.size() * 8, hipMemcpyDeviceToHost), "restored window"));
+            for (uint64_t e = 0; e <= t.cap; ++e) {
+                const int64_t *x = img.data() + e * plan.stride;
+                const bool side = e == t.cap;
+                if (side ? x[0] == 0 : x[0] == (int64_t)0x8000000000000000LL) continue;
+                out.key.push_back(side ? (int64_t)0x8000000000000000LL : x[0]);
+                out.j.push_back(kv.first);
+                out.pending.push_back(kind == 0);
+                out.words.insert(out.words.end(), x + 1, x + 1 + NW);
+            }
+        }
+    return GWO_OK;
 }
 
 // Reset and return to the pool every pane table with index < first.
@@ -327,11 +485,20 @@ gwo_status Handle::slide_refire_rows(const int64_t *k, const int64_t *t, const i
     std::vector<TableDesc> pdir((size_t)pane_len, TableDesc{});
     for (auto it = tables.lower_bound(pane_base); it != tables.end() && it->first <= pane_hi; ++it)
         pdir[(size_t)(it->first - pane_base)] = desc(it->second);
+    // restored windows' entries (pending, fired) of the fired, uncleaned windows [j_clean, j_fire)
+    std::vector<TableDesc> wdir;
+    for (auto it = S.rwin.lower_bound((long long)j_clean); it != S.rwin.end() && it->first < (long long)j_fire; ++it) {
+        if (wdir.empty()) wdir.assign((size_t)nj * 2, TableDesc{});
+        const size_t d = (size_t)(it->first - (long long)j_clean);
+        if (it->second.pend.base) wdir[2 * d] = desc(it->second.pend);
+        if (it->second.done.base) wdir[2 * d + 1] = desc(it->second.done);
+    }
     const uint64_t rs_blocks = (mmax + 4095) / 4096;
     auto up = [](size_t x) { return (x + 255) & ~(size_t)255; };
-    // carve: blk[256] u32 | pdir | r_idx[m] | r_u[m] | before[m][MAX_WORDS] | r_slot, k1, v1, k2, v2 [m] u32 |
+    // carve: blk[256] u32 | pdir | wdir | r_idx[m] | r_u[m] | before[m][MAX_WORDS] | r_slot, k1, v1, k2, v2 [m] u32 |
     //        hist | keytab[kcap] u64
-    const size_t o_blk = 0, o_pdir = 1024, o_idx = up(o_pdir + (size_t)pane_len * sizeof(TableDesc));
+    const size_t o_blk = 0, o_pdir = 1024, o_wdir = up(o_pdir + (size_t)pane_len * sizeof(TableDesc));
+    const size_t o_idx = up(o_wdir + wdir.size() * sizeof(TableDesc));
     const size_t o_u = o_idx + mmax * 8, o_before = o_u + mmax * 8, o_slot = o_before + mmax * GWO_MAX_WORDS * 8;
     const size_t o_k1 = o_slot + mmax * 4, o_v1 = o_k1 + mmax * 4, o_k2 = o_v1 + mmax * 4, o_v2 = o_k2 + mmax * 4;
     const size_t o_hist = up(o_v2 + mmax * 4), o_keys = up(o_hist + 256 * 4 * rs_blocks), total = o_keys + kcap * 8;
@@ -339,6 +506,9 @@ gwo_status Handle::slide_refire_rows(const int64_t *k, const int64_t *t, const i
     char *b = (char *)refire_buf.ptr;
     GWO_TRY(hipcheck(hipMemcpyAsync(b + o_pdir, pdir.data(), (size_t)pane_len * sizeof(TableDesc),
                                     hipMemcpyHostToDevice, stream), "refire panes"));
+    if (!wdir.empty())
+        GWO_TRY(hipcheck(hipMemcpyAsync(b + o_wdir, wdir.data(), wdir.size() * sizeof(TableDesc), hipMemcpyHostToDevice,
+                                        stream), "refire windows"));
     GWO_TRY(hipcheck(hipMemsetAsync(b + o_keys, 0, kcap * 8, stream), "refire keys"));
     launch_refire_collect(t, n, g, 0, 0, (uint32_t *)(b + o_blk), (int64_t *)(b + o_idx), (long long *)(b + o_u),
                           stream);
@@ -351,7 +521,8 @@ gwo_status Handle::slide_refire_rows(const int64_t *k, const int64_t *t, const i
     if (m == 0 || m > mmax) return poison(GWO_ERR_HIP, "allowedLateness re-fire: pair count disagrees with the scan");
     launch_slide_refire_slots(k, (const int64_t *)(b + o_idx), (const long long *)(b + o_u), (int64_t)m, plan, g,
                               (unsigned long long *)(b + o_keys), kcap - 1, (long long)j_clean, nj,
-                              (const TableDesc *)(b + o_pdir), pane_base, pane_len, (uint32_t *)(b + o_slot),
+                              (const TableDesc *)(b + o_pdir), pane_base, pane_len,
+                              wdir.empty() ? nullptr : (const TableDesc *)(b + o_wdir), (uint32_t *)(b + o_slot),
                               (int64_t *)(b + o_before), stream);
     GWO_TRY(launch_ok("refire slots"));
     const int which = radix_sort_pairs((const uint32_t *)(b + o_slot), nullptr, (int64_t)m, bits,

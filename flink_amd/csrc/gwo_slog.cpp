@@ -47,6 +47,9 @@ struct SlogState {
     std::vector<SlogSeg> h_segs;
     int groups = 0;                // CUs
     bool reserved = false;
+    // windows restored from a per-window savepoint (gwo_import_heap_state): window index -> its entries as a
+    // partial-accumulator segment (key + raw words), added to R at the window's step and subtracted at the next
+    std::map<long long, LogWindow> rwins;
 };
 
 static uint64_t slog_capacity(double mean) { return (uint64_t)std::ceil(mean + 6.0 * std::sqrt(mean) + 16.0); }
@@ -129,6 +132,7 @@ gwo_status Handle::slog_init() {
 void Handle::slog_free() {
     if (!slog) return;
     SlogState &G = *slog;
+    for (auto &kv : G.rwins) log_release(kv.second);
     for (int i = 0; i < 2; ++i) {
         G.ring[i].release();
         G.bkt[i].release();
@@ -175,6 +179,73 @@ gwo_status Handle::slog_anchor() {
     slog->rebuild = true;
     slog->pending.clear();
     slog->pending_records = 0;
+    return GWO_OK;
+}
+
+// Restored window j's pending entries (rows of key / words, words already carrying a positive count word) as a
+// partial segment partitioned like R (top lp bits of digit_hash; lp never shrinks, so it is never finer than R's).
+gwo_status Handle::slog_rwin_add(long long j, const std::vector<int64_t> &key, const std::vector<int64_t> &words,
+                                 const std::vector<int64_t> &rows) {
+    SlogState &G = *slog;
+    const int NW = plan.nwords, RW = 1 + NW;
+    LogWindow &W = G.rwins[j];
+    W.lp = G.lp;
+    const uint32_t F = 1u << W.lp;
+    std::vector<uint32_t> cnt(F, 0), off(F, 0);
+    for (int64_t i : rows) cnt[digit_hash(key[i]) >> (32 - W.lp)]++;
+    uint32_t run = 0;
+    for (uint32_t p = 0; p < F; ++p) {
+        off[p] = run;
+        run += cnt[p];
+    }
+    std::vector<uint32_t> fill(off);
+    std::vector<int64_t> rec((size_t)rows.size() * RW);
+    for (int64_t i : rows) {
+        int64_t *r = rec.data() + (size_t)fill[digit_hash(key[i]) >> (32 - W.lp)]++ * RW;
+        r[0] = key[i];
+        for (int w = 0; w < NW; ++w) r[1 + w] = words[(size_t)i * NW + w];
+    }
+    char *p_rec = nullptr, *p_off = nullptr, *p_cnt = nullptr;
+    GWO_TRY(log_carve(W, rec.size() * 8, &p_rec));
+    GWO_TRY(log_carve(W, (size_t)F * 4, &p_off));
+    GWO_TRY(log_carve(W, (size_t)F * 4, &p_cnt));
+    GWO_TRY(hipcheck(hipMemcpy(p_rec, rec.data(), rec.size() * 8, hipMemcpyHostToDevice), "restore records"));
+    GWO_TRY(hipcheck(hipMemcpy(p_off, off.data(), (size_t)F * 4, hipMemcpyHostToDevice), "restore offsets"));
+    GWO_TRY(hipcheck(hipMemcpy(p_cnt, cnt.data(), (size_t)F * 4, hipMemcpyHostToDevice), "restore counts"));
+    W.partial = LogSegDesc{(int64_t *)p_rec, (uint32_t *)p_off, (uint32_t *)p_cnt, W.lp, 0};
+    W.partial_rows = rows.size();
+    return GWO_OK;
+}
+
+void Handle::slog_rwin_release_before(long long j) {
+    SlogState &G = *slog;
+    for (auto it = G.rwins.begin(); it != G.rwins.end() && it->first < j;) {
+        log_release(it->second);
+        it = G.rwins.erase(it);
+    }
+}
+
+size_t Handle::slog_rwin_count() const {
+    size_t n = 0;
+    for (auto &kv : slog->rwins) n += kv.second.partial_rows;
+    return n;
+}
+
+gwo_status Handle::slog_rwin_rows(WindowRows &out) {
+    const int NW = plan.nwords, RW = 1 + NW;
+    std::vector<int64_t> rec;
+    for (auto &kv : slog->rwins) {
+        const LogWindow &W = kv.second;
+        rec.resize((size_t)W.partial_rows * RW);
+        if (rec.empty()) continue;
+        GWO_TRY(hipcheck(hipMemcpy(rec.data(), W.partial.rec, rec.size() * 8, hipMemcpyDeviceToHost), "restored window"));
+        for (uint64_t r = 0; r < W.partial_rows; ++r) {
+            out.key.push_back(rec[r * RW]);
+            out.j.push_back(kv.first);
+            out.pending.push_back(1);
+            out.words.insert(out.words.end(), rec.begin() + r * RW + 1, rec.begin() + (r + 1) * RW);
+        }
+    }
     return GWO_OK;
 }
 
@@ -353,25 +424,33 @@ gwo_status Handle::fire_slog(int64_t new_wm) {
                 G.h_segs.push_back(SlogSeg{W.partial.rec, W.partial.off, W.partial.cnt, W.partial.lp, sign, 1, 0});
             if (sign > 0) plus_records += W.records + W.partial_rows;
         };
+        auto add_restored = [&](__int128 j, int sign) {   // a restored window's entries: in R for its own step only
+            auto r = G.rwins.find((long long)j);
+            if (r != G.rwins.end() && r->second.partial.rec) add_pane(r->second, sign);
+        };
         if (G.rebuild) {
-            // R holds nothing of window J - 1: skip to the first window holding a pane with records and sum its panes
+            // R holds nothing of window J - 1: skip to the first window holding a pane with records (or restored
+            // entries) and sum its panes
             slog_release_before(lo);
+            slog_rwin_release_before((long long)S.J);
             auto it = L.wins.begin();
             while (it != L.wins.end() && it->second.segs.empty() && !it->second.partial.rec) {
                 log_release(it->second);   // offsets carved for a K1 range that got no records
                 it = L.wins.erase(it);
             }
-            if (it == L.wins.end()) {
+            if (it == L.wins.end() && G.rwins.empty()) {
                 S.J = j_new;
                 break;
             }
-            const __int128 ja = std::max(S.J, first_window_of_pane(it->first));
+            __int128 ja = it == L.wins.end() ? j_new : std::max(S.J, first_window_of_pane(it->first));
+            if (!G.rwins.empty()) ja = std::min(ja, (__int128)G.rwins.begin()->first);
             if (ja >= j_new) break;
             S.J = ja;
             lo = win_first_pane(S.J);
             hi = win_last_pane(S.J);
             slog_release_before(lo);
             for (auto jt = L.wins.lower_bound(lo); jt != L.wins.end() && jt->first <= hi; ++jt) add_pane(jt->second, +1);
+            add_restored(S.J, +1);
             G.live = 0;
         } else {
             const long long plo = win_first_pane(S.J - 1), phi = win_last_pane(S.J - 1);
@@ -387,6 +466,8 @@ gwo_status Handle::fire_slog(int64_t new_wm) {
                 add_pane(jt->second, -1);
                 leaving.push_back(jt->first);
             }
+            add_restored(S.J, +1);
+            add_restored(S.J - 1, -1);
         }
         const auto pending_was = G.pending;
         const uint64_t pending_records_was = G.pending_records;
@@ -427,6 +508,7 @@ gwo_status Handle::fire_slog(int64_t new_wm) {
             log_release(L.wins[u]);
             L.wins.erase(u);
         }
+        slog_rwin_release_before((long long)S.J);   // R holds window J's restored entries until the next step
         S.J += 1;
     }
     return GWO_OK;

@@ -14,7 +14,8 @@
 #include "gwo_internal.h"
 
 #define SLOG_THREADS 256         // a small workgroup: ~5 per CU keep that many partitions' HBM round trips in flight
-#define SLOG_MAX_SEGS 64          // signed inputs of one window step (pane segments, restored partials)
+#define SLOG_MAX_SEGS 63          // signed inputs of one window step (pane segments, restored partials): wave 0
+                                  // scans R_p and the segments, one lane each
 #define SLOG_SHARDS 16            // statistics shards (one 128-B line each)
 #define SLOG_STAT_STRIDE 16
 

@@ -139,11 +139,17 @@ gwo_status Handle::snapshot(const gwo_state_rows *rows, int64_t cap, int64_t *n_
 // ---- restore -----------------------------------------------------------------------------------------------
 // Host copies of the rows (checkpoints are read from storage into host memory; device rows work too).
 gwo_status Handle::restore(const gwo_state_rows *rows, int32_t n_words, int64_t n, int64_t new_wm) {
+    return restore_impl(rows, n_words, n, new_wm, false);
+}
+
+// per_window: sliding rows are windows (a per-window savepoint, gwo_import_heap_state), not panes.
+gwo_status Handle::restore_impl(const gwo_state_rows *rows, int32_t n_words, int64_t n, int64_t new_wm,
+                                bool per_window) {
     if (n_words != plan.nwords)
         return fail(GWO_ERR_INVALID_ARGUMENT, "restore: rows carry %d accumulator words, this operator's aggregates use %d",
                     n_words, plan.nwords);
     const bool fresh = wm == (int64_t)0x8000000000000000LL && tables.empty() && (!sess || session_live() == 0) &&
-                       (!logst || log_window_count() == 0);
+                       (!logst || log_window_count() == 0) && !slide_has_restored();
     if (!fresh) return fail(GWO_ERR_STATE, "restore: the handle already holds state");
     RestoreRows R;
     R.n = n;
@@ -174,6 +180,7 @@ gwo_status Handle::restore(const gwo_state_rows *rows, int32_t n_words, int64_t 
         R.mine[i] = kg >= cfg.key_group_start && kg <= cfg.key_group_end;
     }
     if (sess) return session_restore_rows(R, new_wm);
+    if (slide && per_window) return slide_restore_windows(R, new_wm);
     if (logst) return log_restore_rows(R, new_wm);
     return table_restore_rows(R, new_wm);
 }

@@ -8,8 +8,14 @@
   heap backend at the same point -- the oracle's window contents, merging-window-set and event timers --
   for tumbling (both layouts), sliding (windows built from panes) and sessions, with allowedLateness > 0.
 * Import: the oracle's state written in the heap layout and imported into a fresh operator continues exactly
-  like the oracle; a 2 -> 3 rescale through exported key groups equals one operator.
-* Rejections: sliding import, a purging trigger's session, a foreign accumulator, truncated bytes.
+  like the oracle -- sliding windows too (one accumulator per (key, window), WindowOperator.java:385-413, kept per
+  window and combined into the window's rows at its fire) on every sliding layout: table panes with the ring and the
+  recompute strategy, allowedLateness 0 and > 0, and the sliding log; a 2 -> 3 rescale through exported key groups
+  equals one operator.
+* The reference's sliding snapshot point (WindowOperatorTest.java:111-184, snapshot at :150-157) replayed through
+  the heap layout, imported at Long.MIN_VALUE as a restored WindowOperator's timer service starts.
+* Rejections: a purging trigger's session, the reference's session-with-stateful-trigger savepoint (a keyed state
+  the operator does not run), a foreign accumulator, truncated bytes, a row that is no sliding window.
 Integer aggregates: bit-exact.
 """
 import os
@@ -23,7 +29,7 @@ from oracle import heap_keyed_state as H
 
 pytestmark = pytest.mark.gpu
 
-LONG_MAX = (1 << 63) - 1
+LONG_MIN, LONG_MAX = -(1 << 63), (1 << 63) - 1
 GOLD = os.path.join(os.path.dirname(__file__), "golden", "heap_state")
 
 
@@ -87,28 +93,40 @@ def _streams(kind, seed):
     return k, t, v, G.punctuated_watermarks(t, 700, 1_200)
 
 
+_SL = (lambda F: F.SlidingEventTimeWindows.of(6_000, 2_000), lambda: O.SlidingEventTimeWindows(6_000, 2_000))
 CASES = {
     "tumbling_table": (lambda F: F.TumblingEventTimeWindows.of(5_000), lambda: O.TumblingEventTimeWindows(5_000),
                        "table", 2_000),
     "tumbling_log": (lambda F: F.TumblingEventTimeWindows.of(5_000), lambda: O.TumblingEventTimeWindows(5_000),
                      "log", 0),
-    "sliding": (lambda F: F.SlidingEventTimeWindows.of(6_000, 2_000), lambda: O.SlidingEventTimeWindows(6_000, 2_000),
-                "auto", 1_500),
+    "sliding": (*_SL, "auto", 1_500),                      # table panes, recompute (MIN), re-fires
+    "sliding_ring": (*_SL, "table", 1_500, "ring"),        # table panes, running total (int64 sums), re-fires
+    "sliding_ring_l0": (*_SL, "table", 0, "ring"),
+    "sliding_recompute_l0": (*_SL, "table", 0),
+    "sliding_log": (*_SL, "log", 0, "ring"),                # logged panes, partitioned running total
     "session": (lambda F: F.EventTimeSessionWindows.withGap(3_000), lambda: O.EventTimeSessionWindows(3_000),
                 "auto", 2_000),
 }
 
 
-def _aggs(F):
+def _aggs(F, kind="mixed"):
+    if kind == "ring":
+        return (F.MultiAggregate(F.SumAggregate(), F.CountAggregate(), F.AverageAggregate()),
+                O.MultiAgg([O.SumLongAgg(), O.CountAgg(), O.AvgAgg()]))
     return (F.MultiAggregate(F.SumAggregate(), F.MinAggregate(), F.AverageAggregate()),
             O.MultiAgg([O.SumLongAgg(), O.MinAgg(), O.AvgAgg()]))
 
 
+def _case(case):
+    c = CASES[case]
+    return c[0], c[1], c[2], c[3], (c[4] if len(c) > 4 else "mixed")
+
+
 @pytest.mark.parametrize("case", sorted(CASES))
 def test_export_matches_reference_state(F, case):
-    ga, oa, layout, lateness = CASES[case]
+    ga, oa, layout, lateness, ak = _case(case)
     k, t, v, b = _streams("session" if case == "session" else "win", 7)
-    agg, oagg = _aggs(F)
+    agg, oagg = _aggs(F, ak)
     maxp = 64
     op = F.GpuWindowOperator(ga(F), agg, allowed_lateness=lateness, state_layout=layout, max_parallelism=maxp)
     ref = O.WindowOperatorOracle(oa(), oagg, lateness, max_parallelism=maxp)
@@ -135,14 +153,21 @@ def test_export_matches_reference_state(F, case):
     op.close()
 
 
-@pytest.mark.parametrize("case", ["tumbling_table", "tumbling_log", "session"])
+@pytest.mark.parametrize("case", ["tumbling_table", "tumbling_log", "session", "sliding", "sliding_ring",
+                                  "sliding_ring_l0", "sliding_recompute_l0", "sliding_log"])
 @pytest.mark.parametrize("key_kind", ["long", "string"])
-def test_import_continues_like_reference(F, case, key_kind):
-    ga, oa, layout, lateness = CASES[case]
+@pytest.mark.parametrize("restore_at", ["checkpoint", "long_min"])
+def test_import_continues_like_reference(F, case, key_kind, restore_at):
+    """restore_at long_min: the watermark a restored WindowOperator's timer service starts at (InternalTimerServiceImpl
+    .java:78) -- records of windows that already fired before the checkpoint are on time again until the next
+    watermark, as in the reference."""
+    if key_kind == "string" and case == "sliding_log":
+        pytest.skip("the log layouts take Long/Integer keys")
+    ga, oa, layout, lateness, ak = _case(case)
     k, t, v, b = _streams("session" if case == "session" else "win", 13)
     kv = (lambda x: f"k{int(x)}") if key_kind == "string" else int
     kh = O.string_hash_code if key_kind == "string" else O.long_hash_code
-    agg, oagg = _aggs(F)
+    agg, oagg = _aggs(F, ak)
     maxp = 32
     ref = O.WindowOperatorOracle(oa(), oagg, lateness, max_parallelism=maxp, key_hash=kh)
     cut = len(b) // 2
@@ -156,6 +181,8 @@ def test_import_continues_like_reference(F, case, key_kind):
     buf = H.write_state(H.state_of_oracle(ref), key_kind, lambda x: O.assign_to_key_group(kh(x), maxp), (0, maxp - 1))
     op = F.GpuWindowOperator(ga(F), agg, allowed_lateness=lateness, state_layout=layout, max_parallelism=maxp,
                              key_kind=key_kind)
+    if restore_at == "long_min":
+        ref.wm = LONG_MIN
     op.import_heap_state(buf, ref.wm)
     p0 = prev
     for end, wm in b[cut:]:
@@ -169,8 +196,46 @@ def test_import_continues_like_reference(F, case, key_kind):
     op.end_input()
     ref.end_input()
     want = sorted((r.key, r.start, r.end, r.result) for r in ref.output[before:])
-    assert sorted(op.output) == want
+    got = sorted(op.output)
+    assert len(want) > 0
+    assert got == want
     assert op.num_late_records_dropped == ref.num_late_records_dropped - late_before
+    op.close()
+
+
+@pytest.mark.parametrize("layout", ["table", "log"])
+@pytest.mark.parametrize("restore_at", ["checkpoint", "long_min"])
+def test_reference_sliding_snapshot_point_through_heap_layout(F, golden, layout, restore_at):
+    """WindowOperatorTest.testSlidingEventTimeWindowsApply's snapshot (WindowOperatorTest.java:150-157, after
+    processWatermark(2999)): the reference operator's heap state at that point (the oracle's, per (key, window)), in
+    the heap layout, imported into a fresh GPU operator; the rest of the stream then gives the test's expected output."""
+    s = next(x for x in golden["operator_streams"] if x["name"] == "sliding_3s_1s")
+    a = s["assigner"]
+    cut = s["snapshot_after"] + 1
+    ref = O.WindowOperatorOracle(O.SlidingEventTimeWindows(a["size"], a["slide"], a["offset"]), O.SumLongAgg(), 0)
+    for ev in s["events"][:cut]:
+        if ev[0] == "e":
+            ref.process_element(ev[1], ev[2], ev[3])
+        else:
+            ref.process_watermark(ev[1])
+    before = [(r.key, r.start, r.end, r.result) for r in ref.output]
+    state = H.state_of_oracle(ref)
+    assert len(state.contents) > 0
+    buf = H.write_state(state, "long", lambda x: O.assign_to_key_group(O.long_hash_code(x), 128), (0, 127))
+    op = F.GpuWindowOperator(F.SlidingEventTimeWindows.of(a["size"], a["slide"], a["offset"]), F.SumAggregate(),
+                             state_layout=layout)
+    op.import_heap_state(buf, LONG_MIN if restore_at == "long_min" else ref.wm)
+    assert op.state_size() >= len(state.contents)
+    # the restored operator exports what it imported (windows still waiting for their fire timers)
+    back = H.parse_export(op.export_heap_state()[0], "long", False, (0, 127))
+    assert back.contents == state.contents and back.timers == state.timers
+    for ev in s["events"][cut:]:
+        if ev[0] == "e":
+            op.process_element(ev[1], ev[2], ev[3])
+        else:
+            op.process_watermark(ev[1])
+    op.end_input()
+    assert sorted(before + list(op.output)) == sorted(map(tuple, s["expected"]))
     op.close()
 
 
@@ -227,11 +292,41 @@ def test_rescale_through_heap_layout(F):
 
 def test_import_rejections(F):
     from flink_amd import _native as N
-    sl = F.GpuWindowOperator(F.SlidingEventTimeWindows.of(3_000, 1_000), F.SumAggregate())
-    with pytest.raises(N.GwoError) as e:
-        sl.import_heap_state(H.write_state(H.WindowState(), "long", lambda k: 0, (0, 127)), 0)
-    assert e.value.status == N.GWO_ERR_UNSUPPORTED
+    mk = lambda: F.GpuWindowOperator(F.SlidingEventTimeWindows.of(3_000, 1_000), F.SumAggregate(), max_parallelism=1)
+    sl = mk()
+    sl.import_heap_state(H.write_state(H.WindowState(), "long", lambda k: 0, (0, 0)), 0)   # empty: fine
     sl.close()
+    s = H.WindowState()
+    s.contents[(5, (500, 3500))] = (4, 0)      # not a window of size 3000 / slide 1000
+    s.timers.add((3499, 5, (500, 3500)))
+    sl = mk()
+    with pytest.raises(N.GwoError) as e:
+        sl.import_heap_state(H.write_state(s, "long", lambda k: 0, (0, 0)), 0)
+    assert e.value.status == N.GWO_ERR_INVALID_ARGUMENT
+    s = H.WindowState()
+    s.contents[(5, (0, 3000))] = (4, 0)
+    s.timers.add((2999, 5, (0, 3000)))          # a pending fire timer the restore watermark already passed
+    with pytest.raises(N.GwoError) as e:
+        sl.import_heap_state(H.write_state(s, "long", lambda k: 0, (0, 0)), 5000)
+    assert e.value.status == N.GWO_ERR_UNSUPPORTED
+    sl.import_heap_state(H.write_state(s, "long", lambda k: 0, (0, 0)), 1000)   # the rejections left it fresh
+    with pytest.raises(N.GwoError) as e:        # per-window state has no pane rows: checkpoints go the heap layout
+        sl.snapshot_state()
+    assert e.value.status == N.GWO_ERR_UNSUPPORTED
+    sl.process_watermark(2999)
+    assert sl.output == [(5, 0, 3000, 4)]
+    sl.close()
+    # the reference's session-with-stateful-trigger savepoint: its key groups hold the trigger's "count" state
+    with open(os.path.join(GOLD, "win-op-migration-test-session-with-stateful-trigger-flink1.11-snapshot"), "rb") as f:
+        h = H.read_operator_subtask_state(f.read())["managed_keyed"][0]
+    names = [m[0] for m in H.state_meta(h.data, h.offsets[0])]
+    ids = tuple(names.index(x) for x in (H.WINDOW_CONTENTS, H.MERGING_WINDOW_SET, H.EVENT_TIMERS, H.PROCESSING_TIMERS))
+    se = F.GpuWindowOperator(F.EventTimeSessionWindows.withGap(3_000), F.SumAggregate(), key_kind="string",
+                             max_parallelism=1)
+    with pytest.raises(N.GwoError) as e:
+        se.import_heap_state(h.data[h.offsets[0]:], 0, ids=ids)
+    assert e.value.status == N.GWO_ERR_UNSUPPORTED and "trigger" in str(e.value)
+    se.close()
     # a purging trigger's session: tracked in the merging-window-set without contents
     s = H.WindowState()
     s.merging["key2"] = {(0, 6500): (0, 3000)}
