@@ -59,6 +59,11 @@ class GwoStateRows(C.Structure):
                 ("key_group", C.c_void_p), ("timer", C.c_void_p)]
 
 
+class GwoCommWaits(C.Structure):
+    _fields_ = [(n, C.c_int64) for n in ("routed_batches", "count_waits", "wm_waits", "flow_count_waits",
+                                         "flow_wm_waits", "count_wait_ns", "wm_wait_ns")]
+
+
 class GwoHeapStateIds(C.Structure):
     _fields_ = [("window_contents", C.c_int16), ("merging_window_set", C.c_int16), ("event_timers", C.c_int16),
                 ("processing_timers", C.c_int16)]
@@ -124,6 +129,7 @@ SIGNATURES = [
     ("gwo_comm_init", C.c_int, [_P, C.POINTER(C.c_uint8), C.c_int32, C.c_int32]),
     ("gwo_comm_set_async_watermark", C.c_int, [_P, C.c_int32]),
     ("gwo_comm_stats", C.c_int, [_P, _I64P, _I64P, _I64P]),
+    ("gwo_comm_wait_stats", C.c_int, [_P, _P]),
     ("gwo_partition_by_operator", C.c_int, [_P, _P, _P, C.c_int64, C.c_int32, C.c_int32, C.c_int32, _P, C.c_int64,
                                             _P, C.c_int32]),
     ("gwo_generate", C.c_int, [C.POINTER(GwoGenSpec), C.c_int64, _P, _P, _P, _P, C.c_int32]),

@@ -64,6 +64,7 @@ struct Comm {
     hipEvent_t ev_rrecv[NS] = {};                  // the slot's record exchange finished (cs)
     hipEvent_t ev_rout[NS] = {};                   // the slot's routed K1 (and re-route) finished (main stream)
     hipEvent_t ev_read[NS] = {};                   // the slot's received records were read (main stream)
+    hipEvent_t ev_cnt[NS] = {};                    // the slot's count exchange was published (count stream)
     bool used_send[NS] = {}, used_read[NS] = {};
     unsigned long long *hcnt[NS] = {}, *hcnt_dev[NS] = {};   // host-mapped: 4P count words + sequence word
     unsigned long long cnt_seq = 0;
@@ -91,18 +92,29 @@ struct Comm {
     // host round trips of the routed exchange: batches routed, waits for a batch's counts (only a flush waits: a fire
     // its records may fall into, a snapshot, gwo_sync), synchronous watermark agreements
     int64_t routed = 0, count_waits = 0, wm_waits = 0;
+    // waits while the device was still running the newest routed batches (the host ran ahead by more than the slot
+    // ring holds: flow control, not a protocol round trip) -- kept apart from count_waits / wm_waits
+    int64_t bp_count_waits = 0, bp_wm_waits = 0;
+    int64_t count_wait_ns = 0, wm_wait_ns = 0;   // host time spent in those waits (all of them)
+    int wm_after_slot = -1;        // the count exchange the queued asynchronous agreement follows on the count stream
     // asynchronous watermark agreement (gwo_comm_set_async_watermark): two host-mapped result blocks, alternating
     bool async_wm = false, wm_pending = false;
     unsigned long long *hwm[2] = {}, *hwm_dev[2] = {};
     unsigned long long wm_seq = 0;
     bool defer = true;             // GWO_COMM_DEFER=0: insert every batch's received records inside its gwo_submit
+    int hold = 0;                  // GWO_COMM_HOLD_COUNTS (diagnostics, counts_arrived)
 };
 
 static int route_ranks(const Comm &C) { return C.vranks > 1 ? C.vranks : C.nranks; }
 
+// A wait is flow control, not a round trip of the protocol, when the device has not even run what the awaited result
+// is queued behind: a batch's counts behind its routed K1, a watermark agreement behind the previous batch's count
+// exchange.  (The host then runs ahead of the device by more than the slot ring holds.)
+static bool not_done(hipEvent_t e) { return hipEventQuery(e) == hipErrorNotReady; }
+
 static bool comm_events(Comm *C) {
     for (int q = 0; q < Comm::NS; ++q)
-        for (hipEvent_t *e : {&C->ev_rrecv[q], &C->ev_rout[q], &C->ev_read[q]})
+        for (hipEvent_t *e : {&C->ev_rrecv[q], &C->ev_rout[q], &C->ev_read[q], &C->ev_cnt[q]})
             if (hipEventCreateWithFlags(e, hipEventDisableTiming) != hipSuccess) return false;
     return true;
 }
@@ -120,7 +132,7 @@ void Handle::comm_free() {
         comm->rsend[q].release();
         comm->rrecv[q].release();
         comm->rcnt[q].release();
-        for (hipEvent_t e : {comm->ev_rrecv[q], comm->ev_rout[q], comm->ev_read[q]})
+        for (hipEvent_t e : {comm->ev_rrecv[q], comm->ev_rout[q], comm->ev_read[q], comm->ev_cnt[q]})
             if (e) (void)hipEventDestroy(e);
         if (comm->hcnt[q]) (void)hipHostFree(comm->hcnt[q]);
     }
@@ -329,6 +341,7 @@ gwo_status Handle::comm_after_route(const int64_t *k, const int64_t *t, const in
     GWO_TRY(nccl_ok(this, ncclGroupEnd(), "group end"));
     launch_publish_words(d_send, 4 * P, C.hcnt_dev[slot], ++C.cnt_seq, C.cs2);
     GWO_TRY(launch_ok("count readback"));
+    GWO_TRY(hipcheck(hipEventRecord(C.ev_cnt[slot], C.cs2), "event"));
     C.routed++;
     C.posts.emplace_back();
     Comm::Post &Q = C.posts.back();
@@ -341,18 +354,30 @@ gwo_status Handle::comm_after_route(const int64_t *k, const int64_t *t, const in
     C.used_send[slot] = true;
     C.rslot = (slot + 1) % Comm::NS;
     // batch i-1's exchange now, behind this K1, if its counts are there (no wait); else after this batch's readback,
-    // or at the latest when its slot comes round again
-    return comm_post_older(false);
+    // or at the latest when its slot comes round again.  (Inside this batch's insert: no received records may be
+    // inserted here, so a post whose receive slot still holds some waits for gwo_submit's own call.)
+    return comm_post_older(false, false);
+}
+
+// Counts of a routed batch are on the host (GWO_COMM_HOLD_COUNTS=n, diagnostics: every 4th batch's counts count as
+// missing until n more batches were routed -- the late-count interleavings of a loaded node, on one GPU).
+static bool counts_arrived(const Comm &C, const Comm::Post &Q, int P) {
+    if (C.hold > 0 && Q.seq % 4 == 1 && C.cnt_seq < Q.seq + (unsigned long long)C.hold) return false;
+    return *(volatile const unsigned long long *)(C.hcnt[Q.slot] + 4 * P) == Q.seq;
 }
 
 // Posts the record exchanges of the routed batches before the newest, oldest first: all of them (wait: missing counts
-// are waited for, counted in count_waits), or (!wait) as long as their counts have arrived.
-gwo_status Handle::comm_post_older(bool wait) {
+// are waited for, counted in count_waits), or (!wait) as long as their counts have arrived.  may_insert: the caller is
+// between batches, so received records still in a post's receive slot may be inserted first (comm_post); else such a
+// post stops the loop.
+gwo_status Handle::comm_post_older(bool wait, bool may_insert) {
     Comm &C = *comm;
     const int P = route_ranks(C);
     while (C.posts.size() > 1) {
         const Comm::Post &Q = C.posts.front();
-        if (!wait && *(volatile const unsigned long long *)(C.hcnt[Q.slot] + 4 * P) != Q.seq) break;
+        if (!wait && !counts_arrived(C, Q, P)) break;
+        if (!may_insert && std::any_of(C.recvq.begin(), C.recvq.end(), [&](const Comm::Recv &R) { return R.slot == Q.slot; }))
+            break;
         GWO_TRY(comm_post());
     }
     return GWO_OK;
@@ -404,7 +429,8 @@ gwo_status Handle::comm_post() {
     (void)NSLOT;
     volatile const unsigned long long *seqw = C.hcnt[Q.slot] + 4 * P;
     if (*seqw != Q.seq) {   // the counts are not there yet: this post waits for them
-        C.count_waits++;
+        if (not_done(C.ev_rout[Q.slot])) C.bp_count_waits++;
+        else C.count_waits++;
         static const bool trace = getenv("GWO_COMM_TRACE") != nullptr;   // (diagnostics)
         if (trace) {
             const unsigned long long seen = *seqw;
@@ -417,7 +443,13 @@ gwo_status Handle::comm_post() {
                     q0 == hipSuccess ? "idle" : "busy");
         }
     }
-    GWO_TRY(spin_seq((const unsigned long long *)seqw, Q.seq, "count exchange", C.cs2));
+    {
+        const auto t0 = std::chrono::steady_clock::now();
+        const bool missing = *seqw != Q.seq;
+        GWO_TRY(spin_seq((const unsigned long long *)seqw, Q.seq, "count exchange", C.cs2));
+        if (missing)
+            C.count_wait_ns += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
+    }
     unsigned long long hs[2 * LOG_RT_MAX], hr[2 * LOG_RT_MAX];
     memcpy(hs, C.hcnt[Q.slot], (size_t)2 * P * 8);
     memcpy(hr, C.hcnt[Q.slot] + 2 * P, (size_t)2 * P * 8);
@@ -438,6 +470,15 @@ gwo_status Handle::comm_post() {
     R.off_w = 2 * RN + ts_words;
     R.tbase = Q.tbase;
     R.g = Q.g;
+    // Received records still waiting in this receive slot (an older batch's, kept back while a later batch's counts
+    // were late) are inserted first, oldest first, so ev_read below covers them: otherwise this exchange would
+    // overwrite them (or the growth path free their buffer) before their K1 read them.  (Callers inside a batch's
+    // insert never get here with such records: comm_post_older(.., false) leaves the post for later.)
+    for (size_t i = C.recvq.size(); i-- > 0;)
+        if (C.recvq[i].slot == Q.slot) {
+            GWO_TRY(comm_insert_received(C.recvq.size() - (i + 1)));
+            break;
+        }
     // the exchange follows the batch's routed K1 and the K1 that last read this receive slot (device-side order)
     GWO_TRY(hipcheck(hipStreamWaitEvent(C.cs, C.ev_rout[Q.slot], 0), "event wait"));
     if (C.used_read[Q.slot]) GWO_TRY(hipcheck(hipStreamWaitEvent(C.cs, C.ev_read[Q.slot], 0), "event wait"));
@@ -584,12 +625,19 @@ static gwo_status allreduce_min_async(Handle *h, int64_t v, int64_t *applied) {
     }
     if (C.wm_pending) {   // the previous call's min
         volatile const unsigned long long *seqw = C.hwm[q ^ 1] + 1;
-        if (*seqw != C.wm_seq) C.wm_waits++;
-        GWO_TRY(h->spin_seq((const unsigned long long *)seqw, C.wm_seq, "watermark agreement", C.cs2));
+        if (*seqw != C.wm_seq) {   // (queued behind the previous batch's count exchange, itself behind its K1)
+            // (the agreement was queued right behind the then newest routed batch's count exchange)
+            if (C.wm_after_slot >= 0 && not_done(C.ev_cnt[C.wm_after_slot])) C.bp_wm_waits++;
+            else C.wm_waits++;
+            const auto t0 = std::chrono::steady_clock::now();
+            GWO_TRY(h->spin_seq((const unsigned long long *)seqw, C.wm_seq, "watermark agreement", C.cs2));
+            C.wm_wait_ns += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
+        }
         *applied = (int64_t)C.hwm[q ^ 1][0];
     } else {
         *applied = C.agreed_wm;
     }
+    C.wm_after_slot = C.routed > 0 ? (C.rslot + Comm::NS - 1) % Comm::NS : -1;
     launch_put_word((unsigned long long *)d, (unsigned long long)v, C.cs2);   // (no copy from host memory)
     GWO_TRY(h->launch_ok("wm"));
     GWO_TRY(nccl_ok(h, ncclAllReduce(d, d, 1, ncclInt64, ncclMin, C.nc2, C.cs2), "allreduce wm"));
@@ -618,7 +666,9 @@ gwo_status Handle::comm_min_watermark(int64_t wm_in, int64_t *out) {
         C.wm_pending = false;
     }
     C.wm_waits++;
+    const auto t0 = std::chrono::steady_clock::now();
     GWO_TRY(allreduce_min(this, wm_in, out));
+    C.wm_wait_ns += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
     C.agreed_wm = *out;
     return GWO_OK;
 }
@@ -690,6 +740,7 @@ extern "C" gwo_status gwo_comm_init(gwo_handle *hh, const uint8_t *id, int32_t n
         return GWO_ERR_OUT_OF_MEMORY;
     }
     if (const char *e = getenv("GWO_COMM_DEFER")) C->defer = atoi(e) != 0;
+    if (const char *e = getenv("GWO_COMM_HOLD_COUNTS")) C->hold = atoi(e);
     // The count stream gets the greatest priority: HIP multiplexes streams onto a few hardware queues (4 per process
     // on this pool), and a default-priority count stream shared the record stream's queue (measured in the kernel
     // trace), so the watermark all-reduce waited behind the previous batch's records on the wire.
@@ -778,5 +829,20 @@ extern "C" gwo_status gwo_comm_stats(gwo_handle *hh, int64_t *routed_batches, in
     *routed_batches = h->comm->routed;
     *count_waits = h->comm->count_waits;
     *wm_waits = h->comm->wm_waits;
+    return GWO_OK;
+}
+
+extern "C" gwo_status gwo_comm_wait_stats(gwo_handle *hh, gwo_comm_waits *out) {
+    Handle *h = reinterpret_cast<Handle *>(hh);
+    if (!h || !out) return GWO_ERR_INVALID_ARGUMENT;
+    if (!h->comm) return h->fail(GWO_ERR_STATE, "no communicator");
+    const Comm &C = *h->comm;
+    out->routed_batches = C.routed;
+    out->count_waits = C.count_waits;
+    out->wm_waits = C.wm_waits;
+    out->flow_count_waits = C.bp_count_waits;
+    out->flow_wm_waits = C.bp_wm_waits;
+    out->count_wait_ns = C.count_wait_ns;
+    out->wm_wait_ns = C.wm_wait_ns;
     return GWO_OK;
 }

@@ -202,6 +202,7 @@ Handle::~Handle() {
     slide_free();
     dict_free();
     for (auto &kv : tables) (void)hipFree(kv.second.base);
+    for (auto &kv : rdone) (void)hipFree(kv.second.base);
     for (auto &t : aux_tables) (void)hipFree(t.base);
     trim_pool();
     if (d_stats) (void)hipFree(d_stats);
@@ -256,7 +257,7 @@ gwo_status Handle::submit(const int64_t *key, const int64_t *ts, const void *val
         // now if they have, else later -- never waiting), the exchanges posted before the newest have landed and are
         // inserted now; otherwise this batch's exchange completes inside its submit
         if (!comm_defers()) return comm_flush_received();
-        GWO_TRY(comm_post_older(false));
+        GWO_TRY(comm_post_older(false, true));
         return comm_insert_received(1);
     }
     if (comm) {
@@ -384,6 +385,7 @@ gwo_status Handle::state_size(int64_t *entries) {
     }
     GWO_TRY(read_occupancy());
     for (auto &kv : tables) s += (int64_t)kv.second.occ;
+    for (auto &kv : rdone) s += (int64_t)kv.second.occ;
     *entries = s;
     return GWO_OK;
 }

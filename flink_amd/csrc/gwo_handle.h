@@ -113,6 +113,11 @@ struct Handle {
     int64_t in_wm = (int64_t)0x8000000000000000LL;
 
     std::map<long long, Table> tables;         // window / pane index -> table
+    // tumbling windows restored with entries already emitted (kept for allowedLateness) at a watermark below their
+    // maxTimestamp (a restored timer service starts at Long.MIN_VALUE): a key with new records in the window before
+    // the watermark passes maxTimestamp re-registers its fire timer (WindowOperator.java:393-410) and fires with both
+    // (fire_tumbling); the others stay emitted
+    std::map<long long, Table> rdone;
     std::vector<Table> aux_tables;             // engine-private tables (sliding ring totals)
     std::multimap<uint64_t, int64_t *> pool;   // clean tables by capacity
 
@@ -425,7 +430,7 @@ struct Handle {
     gwo_status comm_check_route(const int64_t *k, const int64_t *t, const int64_t *v, int64_t n, uint64_t maxn,
                                 uint64_t maxw);
     gwo_status comm_post();   // posts the record exchange of the oldest routed batch not posted yet
-    gwo_status comm_post_older(bool wait);   // posts the exchanges before the newest routed batch's (see gwo_comm.cpp)
+    gwo_status comm_post_older(bool wait, bool may_insert);   // posts the exchanges before the newest routed batch's
     // deferred receives of the routed log path: inserted two routed batches later or at log_flush
     bool comm_defers() const;
     gwo_status comm_insert_received(size_t keep);

@@ -258,7 +258,21 @@ gwo_status Handle::export_heap_state(const gwo_heap_state_ids *ids, uint8_t *buf
         row_of.swap(r2);
     } else {
         es.reserve(n);
+        // a tumbling window restored with emitted entries (rdone) holds a key twice once the key got new records:
+        // one heap entry, its accumulator the combination, its fire timer pending
+        std::map<std::pair<int64_t, int64_t>, size_t> seen;
+        const bool dedup = !rdone.empty();
         for (int64_t i = 0; i < n; ++i) {
+            if (dedup) {
+                auto it = seen.find({key[i], start[i]});
+                if (it != seen.end()) {
+                    WinEntry &e = es[it->second];
+                    for (int w = 0; w < NW; ++w) e.words[w] = combine_h(plan.op[w], e.words[w], words[i * NW + w]);
+                    e.pending = e.pending || timer[i] != 0;
+                    continue;
+                }
+                seen[{key[i], start[i]}] = es.size();
+            }
             WinEntry e;
             e.kg = kg[i];
             e.key = key[i];

@@ -302,8 +302,8 @@ void launch_fire(const TableDesc &t, uint64_t cap, const AccPlan &plan, const Re
                  int64_t end, OutCols out, int reset, int live_word, hipStream_t s);
 
 // dst += sign * src for every occupied entry of src (sign -1 only for all-ACC_ADD_I64 plans);
-// live_word/live maintain dst's count of entries with a positive count word.  existing != 0: only the keys dst
-// already holds (live, with live_word >= 0) are combined.
+// live_word/live maintain dst's count of entries with a positive count word.  existing 1: only the keys dst already
+// holds (live, with live_word >= 0) are combined; 2: only the keys it does not hold.
 void launch_fold(const TableDesc &src, uint64_t src_cap, const TableDesc &dst, const AccPlan &plan, int sign,
                  int live_word, unsigned long long *live, hipStream_t s, int existing = 0);
 // rows (key[i], words[i * nwords ...]) combined into table t

@@ -1180,9 +1180,10 @@ __device__ __forceinline__ const int64_t *table_find(const TableDesc &t, int str
 
 // Pane fold: dst (+/-)= src entry-wise.  Sliding windows: add an entering pane to / subtract a
 // leaving pane from the running window total, or combine a window's panes (recompute strategy).
-// existing != 0: only keys dst already holds (with live_word >= 0: holds live) take src's words -- a restored
+// existing == 1: only keys dst already holds (with live_word >= 0: holds live) take src's words -- a restored
 // window's entries whose fire timer already fired join the window's next emission only for keys that have new
-// records in it (WindowOperator re-registers the timer per (key, window) on a new element).
+// records in it (WindowOperator re-registers the timer per (key, window) on a new element); existing == 2: only
+// keys dst does not hold yet (the rest of those entries, after the emission).
 __global__ __launch_bounds__(256) void fold_kernel(TableDesc src, uint64_t cap, TableDesc dst, AccPlan p, int sign,
                                                    int live_word, unsigned long long *live, int existing) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
@@ -1202,7 +1203,7 @@ __global__ __launch_bounds__(256) void fold_kernel(TableDesc src, uint64_t cap, 
             k = GWO_EMPTY_KEY;
         }
         int64_t *a;
-        if (existing) {
+        if (existing == 1) {
             a = (int64_t *)table_find(dst, p.stride, k);
             if (!a || (live_word >= 0 && __hip_atomic_load(a + live_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <= 0))
                 continue;
@@ -1210,6 +1211,7 @@ __global__ __launch_bounds__(256) void fold_kernel(TableDesc src, uint64_t cap, 
             bool claimed;
             a = find_or_insert(dst, p.stride, k, claimed);
             count_claims(dst.occ, claimed);
+            if (existing == 2 && !claimed) continue;
         }
         for (int w = 0; w < p.nwords; ++w) {
             int64_t x = e[1 + w];

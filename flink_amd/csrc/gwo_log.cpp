@@ -779,7 +779,8 @@ gwo_status Handle::fire_log(int64_t new_wm) {
     if (log_pending_may_fire(new_wm)) GWO_TRY(log_flush());
     std::vector<long long> fire;
     due(fire);
-    if (cfg.allowed_lateness == 0 && !tables.empty()) GWO_TRY(fire_tumbling(new_wm));   // restored fired windows
+    if (cfg.allowed_lateness == 0 && (!tables.empty() || !rdone.empty()))
+        GWO_TRY(fire_tumbling(new_wm));   // restored fired windows
     if (cfg.allowed_lateness > 0) {
         // a fired window stays until its cleanup time and takes late records: it moves to a hash table,
         // which the table path fires, re-fires and cleans up (fire_tumbling, refire_rows)
@@ -936,9 +937,10 @@ gwo_status Handle::log_state_size(int64_t *entries) {
     GWO_TRY(log_flush());
     uint64_t s = 0;
     for (auto &kv : logst->wins) s += kv.second.records + kv.second.partial_rows;
-    if (!tables.empty()) {   // fired windows kept for allowedLateness
+    if (!tables.empty() || !rdone.empty()) {   // fired windows kept for allowedLateness
         GWO_TRY(read_occupancy());
         for (auto &kv : tables) s += kv.second.occ;
+        for (auto &kv : rdone) s += kv.second.occ;
     }
     *entries = (int64_t)s;
     return GWO_OK;
@@ -1068,11 +1070,10 @@ gwo_status Handle::log_restore_rows(const RestoreRows &R, int64_t new_wm) {
             kinds[u] |= 1;
         }
     }
-    for (auto &kv : kinds)
-        if (kv.second == 3)
+    for (auto &kv : kinds)   // emitted rows beside pending ones: only above the watermark (table_restore_rows: rdone)
+        if (kv.second == 3 && (int64_t)((uint64_t)unit_start(kv.first) + (uint64_t)cfg.size - 1) <= new_wm)
             return fail(GWO_ERR_UNSUPPORTED, "restore: window %lld has rows already emitted and rows still pending "
-                                             "(checkpoints taken at different watermarks)",
-                        (long long)unit_start(kv.first));
+                                             "at a watermark past its end", (long long)unit_start(kv.first));
     if (!fired.empty()) {
         RestoreRows T;
         T.n = (int64_t)fired.size();

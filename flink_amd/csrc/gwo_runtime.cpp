@@ -227,12 +227,14 @@ gwo_status Handle::reset_side(const Table &t) {
 gwo_status Handle::read_occupancy() {
     int hi = 0;
     for (auto &kv : tables) hi = std::max(hi, kv.second.counter + 1);
+    for (auto &kv : rdone) hi = std::max(hi, kv.second.counter + 1);
     for (auto &kv : aux_tables) hi = std::max(hi, kv.counter + 1);
     if (hi == 0) return hipcheck(hipStreamSynchronize(stream), "occ sync");   // callers rely on the sync
     GWO_TRY(hipcheck(hipMemcpyAsync(h_counters, d_counters, (size_t)hi * GWO_OCC_WORDS * 8, hipMemcpyDeviceToHost, stream),
                      "occ"));
     GWO_TRY(hipcheck(hipStreamSynchronize(stream), "occ sync"));
     for (auto &kv : tables) kv.second.occ = ctr_host(kv.second.counter);
+    for (auto &kv : rdone) kv.second.occ = ctr_host(kv.second.counter);
     for (auto &t : aux_tables) t.occ = ctr_host(t.counter);
     return GWO_OK;
 }
@@ -1065,6 +1067,17 @@ gwo_status Handle::settle_out() {
 }
 
 gwo_status Handle::fire_tumbling(int64_t new_wm) {
+    // restored emitted entries (rdone) of a window that got no new records by its maxTs: the window stays emitted as
+    // restored (re-fires, cleanup)
+    for (auto it = rdone.begin(); it != rdone.end();) {
+        const int64_t max_ts = (int64_t)((uint64_t)unit_start(it->first) + (uint64_t)cfg.size - 1);
+        if (max_ts <= new_wm && !tables.count(it->first)) {
+            tables.emplace(it->first, it->second);   // (fired)
+            it = rdone.erase(it);
+        } else {
+            ++it;
+        }
+    }
     // timers in timestamp order; each window has its maxTs (fire) and cleanup timers
     std::vector<long long> emit, clear;
     for (auto &kv : tables) {
@@ -1081,9 +1094,13 @@ gwo_status Handle::fire_tumbling(int64_t new_wm) {
     // the table layout alone (not the log layout's fired-window tables, whose fire counts rows right after):
     // no occupancy read -- output room for every slot of the emitted tables, the row count read back behind the
     // fire kernels (settle_out)
-    const bool lazy = !logst;
+    bool any_rdone = false;
+    for (long long u : emit) any_rdone |= rdone.count(u) != 0;
+    const bool lazy = !logst && !any_rdone;
     GWO_TRY(settle_out());
     if (!lazy) GWO_TRY(read_occupancy());
+    for (long long u : emit)   // room for the restored emitted entries that join the window after its emission
+        if (rdone.count(u)) GWO_TRY(ensure_table(u, rdone[u].occ));
     uint64_t extra = 0;
     for (long long u : emit) extra += lazy ? tables[u].cap : tables[u].occ;
     GWO_TRY(ensure_output(extra));
@@ -1094,12 +1111,27 @@ gwo_status Handle::fire_tumbling(int64_t new_wm) {
         bool also_clear = std::find(clear.begin(), clear.end(), u) != clear.end();
         int64_t start = unit_start(u);
         int64_t end = (int64_t)((uint64_t)start + (uint64_t)cfg.size);
+        auto rd = rdone.find(u);
+        // keys with new records since the restore fire with their restored emitted entries too (existing keys only)
+        if (rd != rdone.end()) launch_fold(desc(rd->second), rd->second.cap, desc(t), plan, +1, -1, nullptr, stream, 1);
         prof_begin(GWO_KERNEL_FIRE);
         launch_fire(desc(t), t.cap, plan, rplan, start, end, o, also_clear ? 1 : 0, -1, stream);
         GWO_TRY(launch_ok("fire"));
         prof_end(GWO_KERNEL_FIRE, (int64_t)t.cap);
         if (!lazy) out_rows += t.occ;
         t.fired = true;
+        if (rd != rdone.end()) {   // the other restored entries join the (now emitted) window: re-fires, cleanup
+            if (!also_clear) launch_fold(desc(rd->second), rd->second.cap, desc(t), plan, +1, -1, nullptr, stream, 2);
+            OutCols none = o;
+            none.cap = 0;
+            GWO_TRY(hipcheck(hipMemsetAsync(d_scratch_count, 0, 8, stream), "z"));
+            none.count = d_scratch_count;
+            launch_fire(desc(rd->second), rd->second.cap, plan, rplan, 0, 0, none, 1, -1, stream);   // (reset)
+            GWO_TRY(launch_ok("restored entries"));
+            release_table(rd->second);
+            rdone.erase(rd);
+            t.dirty = true;
+        }
     }
     if (lazy && !emit.empty()) {
         if (!h_out_cnt) {

@@ -51,6 +51,7 @@ gwo_status Handle::snapshot_rows(int64_t *n_rows) {
     GWO_TRY(read_occupancy());
     int64_t r = 0;
     for (auto &kv : tables) r += (int64_t)kv.second.occ;
+    for (auto &kv : rdone) r += (int64_t)kv.second.occ;
     *n_rows = r;
     return GWO_OK;
 }
@@ -89,6 +90,11 @@ gwo_status Handle::snapshot(const gwo_state_rows *rows, int64_t cap, int64_t *n_
             const int32_t timer = (cfg.assigner == GWO_ASSIGNER_TUMBLING && kv.second.fired) ? 0 : 1;
             launch_snap_table(desc(kv.second), kv.second.cap, plan, start, (int64_t)((uint64_t)start + (uint64_t)span),
                               timer, c, stream);
+        }
+        for (auto &kv : rdone) {   // emitted entries (a key with new records also has a pending row from `tables`)
+            const int64_t start = unit_start(kv.first);
+            launch_snap_table(desc(kv.second), kv.second.cap, plan, start, (int64_t)((uint64_t)start + (uint64_t)cfg.size),
+                              0, c, stream);
         }
         GWO_TRY(launch_ok("snapshot"));
     }
@@ -148,7 +154,8 @@ gwo_status Handle::restore_impl(const gwo_state_rows *rows, int32_t n_words, int
     if (n_words != plan.nwords)
         return fail(GWO_ERR_INVALID_ARGUMENT, "restore: rows carry %d accumulator words, this operator's aggregates use %d",
                     n_words, plan.nwords);
-    const bool fresh = wm == (int64_t)0x8000000000000000LL && tables.empty() && (!sess || session_live() == 0) &&
+    const bool fresh = wm == (int64_t)0x8000000000000000LL && tables.empty() && rdone.empty() &&
+                       (!sess || session_live() == 0) &&
                        (!logst || log_window_count() == 0) && !slide_has_restored();
     if (!fresh) return fail(GWO_ERR_STATE, "restore: the handle already holds state");
     RestoreRows R;
@@ -185,13 +192,22 @@ gwo_status Handle::restore_impl(const gwo_state_rows *rows, int32_t n_words, int
     return table_restore_rows(R, new_wm);
 }
 
-// Table layout (tumbling, sliding panes): rows grouped into per-window (per-pane) hash tables.  Every check
-// happens before the handle changes: rows must be window (pane) starts, and a tumbling window's rows must agree
-// on its fire timer (pending or already emitted) -- rows of one window from subtasks checkpointed at different
-// watermarks can disagree, which the per-window table cannot represent: GWO_ERR_UNSUPPORTED.
+// Table layout (tumbling, sliding panes): rows grouped into per-window (per-pane) hash tables; every check
+// happens before the handle changes (rows must be window (pane) starts).  A tumbling row's timer flag says whether its
+// fire timer is pending or the window already emitted it (kept for allowedLateness):
+//   * pending rows -> the window's table, which fires at maxTimestamp;
+//   * emitted rows of a window the restore watermark passed -> the window's table, marked fired (re-fires, cleanup);
+//   * emitted rows of a window whose maxTimestamp lies above the restore watermark (a restored WindowOperator's timer
+//     service starts at Long.MIN_VALUE; or subtasks checkpointed at different watermarks, rescaled into one) -> rdone:
+//     such an entry stays emitted unless its key gets new records before the watermark passes maxTimestamp, which
+//     re-registers that (key, window) timer (WindowOperator.java:393-410), so the key fires with both (fire_tumbling);
+//     so do emitted rows of a window that also has pending rows (subtasks checkpointed at different watermarks).
 gwo_status Handle::table_restore_rows(const RestoreRows &R, int64_t new_wm) {
-    std::map<long long, uint64_t> per_unit;
+    std::map<long long, uint64_t> per_unit, per_done;
     std::map<long long, int> timers;   // bit 0: a row with a pending timer, bit 1: a row already emitted
+    std::vector<char> to_done(R.n, 0);
+    std::vector<long long> unit_of(R.n, 0);
+    const bool tumbling = cfg.assigner == GWO_ASSIGNER_TUMBLING;
     for (int64_t i = 0; i < R.n; ++i) {
         if (!R.mine[i]) continue;
         const __int128 a = (__int128)R.start[i] - (__int128)geom.unit_off_mod;
@@ -200,43 +216,75 @@ gwo_status Handle::table_restore_rows(const RestoreRows &R, int64_t new_wm) {
         const long long u = (long long)q;
         if (unit_start(u) != R.start[i])
             return fail(GWO_ERR_INVALID_ARGUMENT, "restore: %lld is not a window start", (long long)R.start[i]);
-        per_unit[u]++;
         if (!R.timer.empty()) timers[u] |= R.timer[i] ? 1 : 2;
+        unit_of[i] = u;
     }
-    if (!per_unit.empty() && per_unit.rbegin()->first - per_unit.begin()->first >= (1LL << 20))
-        return fail(GWO_ERR_UNSUPPORTED, "restore: windows span more than 2^20 units");
-    if (cfg.assigner == GWO_ASSIGNER_TUMBLING)
-        for (auto &kv : timers)
-            if (kv.second == 3)
-                return fail(GWO_ERR_UNSUPPORTED, "restore: window %lld has rows already emitted and rows still pending "
-                                                 "(checkpoints taken at different watermarks)",
-                            (long long)unit_start(kv.first));
+    for (int64_t i = 0; i < R.n; ++i) {
+        if (!R.mine[i]) continue;
+        const long long u = unit_of[i];
+        const int64_t max_ts = (int64_t)((uint64_t)R.start[i] + (uint64_t)cfg.size - 1);
+        if (tumbling && !R.timer.empty() && R.timer[i] == 0 && (max_ts > new_wm || timers[u] == 3)) {
+            if (logst && cfg.allowed_lateness == 0)   // (a window fires and clears at once: no such state exists)
+                return fail(GWO_ERR_UNSUPPORTED, "restore: window %lld holds entries already emitted (above the "
+                                                 "restore watermark or beside pending ones) with allowedLateness 0",
+                            (long long)unit_start(u));
+            to_done[i] = 1;
+            per_done[u]++;
+        } else {
+            per_unit[u]++;
+        }
+    }
+    long long lo = 0, hi = -1;
+    for (auto *m : {&per_unit, &per_done})
+        if (!m->empty()) {
+            lo = hi < lo ? m->begin()->first : std::min(lo, m->begin()->first);
+            hi = std::max(hi, m->rbegin()->first);
+        }
+    if (hi >= lo && hi - lo >= (1LL << 20)) return fail(GWO_ERR_UNSUPPORTED, "restore: windows span more than 2^20 units");
     wm = in_wm = new_wm;   // validated: from here on the handle holds the restored state
-    if (per_unit.empty()) return slide ? slide_restore_anchor() : GWO_OK;
+    if (hi < lo) return slide ? slide_restore_anchor() : GWO_OK;
     for (auto &kv : per_unit) {
         GWO_TRY(ensure_table(kv.first, kv.second));   // marks windows whose end the watermark passed as fired
         auto t = timers.find(kv.first);
-        if (cfg.assigner == GWO_ASSIGNER_TUMBLING && t != timers.end()) tables[kv.first].fired = t->second == 2;
+        if (tumbling && t != timers.end()) tables[kv.first].fired = t->second == 2;
     }
-    const long long lo = per_unit.begin()->first, hi = per_unit.rbegin()->first;
+    for (auto &kv : per_done) {
+        Table t;
+        uint64_t cap = kMinCap;
+        while ((double)kv.second > kInitLoad * (double)cap) cap <<= 1;
+        GWO_TRY(alloc_table(cap, t));
+        t.fired = true;
+        rdone.emplace(kv.first, t);
+    }
     const int dir_len = (int)(hi - lo + 1);
-    h_dir.assign(dir_len, TableDesc{});
-    for (auto &kv : tables) h_dir[kv.first - lo] = desc(kv.second);
-    GWO_TRY(ensure_buf(dir_buf, dir_len * sizeof(TableDesc)));
-    GWO_TRY(hipcheck(hipMemcpyAsync(dir_buf.ptr, h_dir.data(), dir_len * sizeof(TableDesc), hipMemcpyHostToDevice, stream),
-                     "restore dir"));
     DevBuf bk, bs, bw;
-    GWO_TRY(ensure_buf(bk, (size_t)R.n * 8));
-    GWO_TRY(ensure_buf(bs, (size_t)R.n * 8));
-    GWO_TRY(ensure_buf(bw, (size_t)R.n * R.nw * 8));
-    GWO_TRY(hipcheck(hipMemcpyAsync(bk.ptr, R.key.data(), (size_t)R.n * 8, hipMemcpyHostToDevice, stream), "restore keys"));
-    GWO_TRY(hipcheck(hipMemcpyAsync(bs.ptr, R.start.data(), (size_t)R.n * 8, hipMemcpyHostToDevice, stream), "restore starts"));
-    GWO_TRY(hipcheck(hipMemcpyAsync(bw.ptr, R.words.data(), (size_t)R.n * R.nw * 8, hipMemcpyHostToDevice, stream),
-                     "restore words"));
-    launch_restore((const int64_t *)bk.ptr, (const int64_t *)bs.ptr, (const int64_t *)bw.ptr, R.n, plan, geom_now(),
-                   (const TableDesc *)dir_buf.ptr, lo, dir_len, stream);
-    gwo_status st = launch_ok("restore");
-    if (st == GWO_OK) st = hipcheck(hipStreamSynchronize(stream), "restore sync");
+    gwo_status st = GWO_OK;
+    for (int pass = 0; pass < 2 && st == GWO_OK; ++pass) {   // pending / fired rows, then rows for rdone
+        std::map<long long, Table> &dst = pass ? rdone : tables;
+        std::vector<int64_t> k, s, w;
+        for (int64_t i = 0; i < R.n; ++i)
+            if (R.mine[i] && to_done[i] == pass) {
+                k.push_back(R.key[i]);
+                s.push_back(R.start[i]);
+                w.insert(w.end(), R.words.begin() + (size_t)i * R.nw, R.words.begin() + (size_t)(i + 1) * R.nw);
+            }
+        if (k.empty()) continue;
+        h_dir.assign(dir_len, TableDesc{});
+        for (auto &kv : dst) h_dir[kv.first - lo] = desc(kv.second);
+        GWO_TRY(ensure_buf(dir_buf, dir_len * sizeof(TableDesc)));
+        GWO_TRY(hipcheck(hipMemcpyAsync(dir_buf.ptr, h_dir.data(), dir_len * sizeof(TableDesc), hipMemcpyHostToDevice,
+                                        stream), "restore dir"));
+        GWO_TRY(ensure_buf(bk, k.size() * 8));
+        GWO_TRY(ensure_buf(bs, s.size() * 8));
+        GWO_TRY(ensure_buf(bw, w.size() * 8));
+        GWO_TRY(hipcheck(hipMemcpyAsync(bk.ptr, k.data(), k.size() * 8, hipMemcpyHostToDevice, stream), "restore keys"));
+        GWO_TRY(hipcheck(hipMemcpyAsync(bs.ptr, s.data(), s.size() * 8, hipMemcpyHostToDevice, stream), "restore starts"));
+        GWO_TRY(hipcheck(hipMemcpyAsync(bw.ptr, w.data(), w.size() * 8, hipMemcpyHostToDevice, stream), "restore words"));
+        launch_restore((const int64_t *)bk.ptr, (const int64_t *)bs.ptr, (const int64_t *)bw.ptr, (int64_t)k.size(), plan,
+                       geom_now(), (const TableDesc *)dir_buf.ptr, lo, dir_len, stream);
+        st = launch_ok("restore");
+        if (st == GWO_OK) st = hipcheck(hipStreamSynchronize(stream), "restore sync");   // (host columns are reused)
+    }
     bk.release();
     bs.release();
     bw.release();

@@ -339,8 +339,18 @@ gwo_status gwo_comm_init(gwo_handle *h, const uint8_t id[GWO_COMM_ID_BYTES], int
 gwo_status gwo_comm_set_async_watermark(gwo_handle *h, int32_t enabled);
 /* Host round trips of the routed exchange (log layout): routed batches, waits for a batch's exchanged counts (a routed
  * batch's record exchange is posted at the next routed batch, when its counts have arrived: only a flush -- a fire
- * its records may fall into, a snapshot, gwo_sync -- waits), and synchronous watermark agreements. */
+ * its records may fall into, a snapshot, gwo_sync -- waits), and watermark agreements waited for (every synchronous
+ * one; asynchronous: the previous call's all-reduce not yet published).  Waits that happen while the device is still
+ * running the newest routed batches' K1 are flow control -- the host ran ahead of the device by more than the 3
+ * send/receive slots hold -- and are counted apart by gwo_comm_backpressure, not here. */
 gwo_status gwo_comm_stats(gwo_handle *h, int64_t *routed_batches, int64_t *count_waits, int64_t *wm_waits);
+/* The same counters, the flow-control waits counted apart, and the host time spent waiting (every wait, ns). */
+typedef struct {
+    int64_t routed_batches, count_waits, wm_waits;
+    int64_t flow_count_waits, flow_wm_waits;   /* the awaited result was still queued behind unfinished device work */
+    int64_t count_wait_ns, wm_wait_ns;
+} gwo_comm_waits;
+gwo_status gwo_comm_wait_stats(gwo_handle *h, gwo_comm_waits *out);
 
 /* Batch form of KeyGroupStreamPartitioner.selectChannel (KeyGroupStreamPartitioner.java:51-58): groups n
  * records by destination computeOperatorIndexForKeyGroup(assignToKeyGroup(key)) into per-destination runs

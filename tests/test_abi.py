@@ -38,7 +38,8 @@ def test_struct_layout_matches_header(tmp_path):
     import subprocess
     from flink_amd import _native as N
     structs = {"gwo_config": N.GwoConfig, "gwo_out": N.GwoOut, "gwo_side_out": N.GwoSideOut,
-               "gwo_gen_spec": N.GwoGenSpec, "gwo_heap_state_ids": N.GwoHeapStateIds}
+               "gwo_gen_spec": N.GwoGenSpec, "gwo_heap_state_ids": N.GwoHeapStateIds,
+               "gwo_comm_waits": N.GwoCommWaits}
     lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "gwo.h"', "int main(void){"]
     for cname, py in structs.items():
         lines.append(f'printf("{cname} __sizeof__ %zu\\n", sizeof({cname}));')

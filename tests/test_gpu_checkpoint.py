@@ -243,10 +243,11 @@ def test_rescale_two_to_three_with_unequal_watermarks(F, layout):
     assert sorted(rows + more) == want
 
 
-def test_restore_rejects_ambiguous_or_mismatched_checkpoints(F):
+def test_restore_mixed_timers_and_rejects_mismatched_checkpoints(F):
     """A tumbling window emitted by one subtask but still pending in another (allowedLateness > 0, unequal
-    watermarks) cannot be restored into one table; nor can rows with another aggregate layout (n_words).  A
-    rejected restore leaves the handle fresh: a valid restore afterwards succeeds."""
+    watermarks) restores per key as the reference's timers are per (key, window): the pending key fires at the
+    window's maxTimestamp, the emitted keys only re-fire on late records.  Rows with another aggregate layout
+    (n_words) are rejected, and a rejected restore leaves the handle fresh: a valid restore afterwards succeeds."""
     from flink_amd import _native as N
     mk = lambda rng_=None, agg=None: F.GpuWindowOperator(F.TumblingEventTimeWindows.of(1_000), agg or F.SumAggregate(),
                                                          allowed_lateness=5_000, state_layout="table",
@@ -263,10 +264,16 @@ def test_restore_rejects_ambiguous_or_mismatched_checkpoints(F):
     s2 = b.snapshot_state()
     assert (s2["timer"] == 1).all()
     b.close()
+    m = mk()
+    m.restore_state([s1, s2])    # at the minimum watermark, 500
+    assert m.current_watermark == 500 and m.state_size() == 3
+    m.process_watermark(999)
+    assert m.output == [(3, 0, 1000, 1)]             # only the pending key's timer fires
+    m.process_batch(np.array([1]), np.array([150]), np.array([5]))   # late but allowed: re-fires with the sum
+    m.process_watermark(1_000)
+    assert m.output == [(3, 0, 1000, 1), (1, 0, 1000, 6)]
+    m.close()
     c = mk()
-    with pytest.raises(N.GwoError) as e:
-        c.restore_state([s1, s2])
-    assert e.value.status == N.GWO_ERR_UNSUPPORTED
     bad = dict(s1, words=np.zeros((len(s1["key"]), 2), np.int64))
     with pytest.raises(N.GwoError) as e:
         c.restore_state(bad)
