@@ -334,10 +334,23 @@ def main():
     peak = 8000.0
     traffic = None
     tfile = os.path.join(ROOT, "profiles", "traffic.json")
-    if os.path.exists(tfile):
-        t = json.load(open(tfile)).get(dname)
-        if t:
-            traffic = t["hbm_bytes_per_launch"]
+    tj = json.load(open(tfile)) if os.path.exists(tfile) else {}
+    t = tj.get(dname)
+    if t:
+        traffic = t["hbm_bytes_per_launch"]
+    # path-level measured bytes: every kernel of the timed region's PMC bytes per launch x its launches
+    # in the timed region (K1 and its pass 2 once per batch, the fire once per window), over the elapsed time
+    pmc_path = None
+    if a.layout != "table" and all(k in tj for k in ("log_part_kernel", "log_split_kernel", "log_fire_kernel")):
+        k1n, fires = stats["insert"][0], stats["fire"][0]
+        parts = {"log_part_kernel": (tj["log_part_kernel"]["hbm_bytes_per_launch"], k1n),
+                 "log_split_kernel": (tj["log_split_kernel"]["hbm_bytes_per_launch"], k1n),
+                 "log_fire_kernel": (tj["log_fire_kernel"]["hbm_bytes_per_launch"], fires)}
+        pb = sum(b * n for b, n in parts.values())
+        pmc_path = {"bytes_per_step": pb / a.steps, "achieved": pb / elapsed / 1e9, "unit": "GB/s",
+                    "frac": pb / elapsed / 1e9 / 8000.0,
+                    "per_kernel": {k: {"bytes_per_launch": b, "launches": n} for k, (b, n) in parts.items()},
+                    "measured_at": tj.get("_meta", {"head": "unstamped"})}
 
     op.close()
     del key, ts, val
@@ -373,11 +386,13 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": peak, "unit": "GB/s",
                          "frac": achieved / peak, "traffic": traffic, "kernel": dname,
                          "alg_bytes_per_launch": dbytes / max(dl, 1), "avg_launch_ms": avg_ms,
-                         "launches": dl, "traffic_source": "profiles/traffic.json (rocprofv3 PMC)" if traffic else None},
+                         "launches": dl, "traffic_source": "profiles/traffic.json (rocprofv3 PMC)" if traffic else None,
+                         "traffic_measured_at": tj.get("_meta", {}).get("head", "unstamped") if traffic else None},
             "roofline_path": {"alg_bytes_per_step": path_bytes / a.steps,
                               "achieved": path_bytes / elapsed / 1e9, "unit": "GB/s",
                               "frac": path_bytes / elapsed / 1e9 / peak,
                               "distinct_entries_per_step": u_tot / a.steps, "fired_rows_per_step": rows / a.steps},
+            "roofline_pmc_path": pmc_path,
             "kernels_ms": {k: {"launches": v[0], "total_ms": v[1]} for k, v in stats.items() if v[0]},
             "cpu_baseline": cpu,
             "host_fed": host_fed,

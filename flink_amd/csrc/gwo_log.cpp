@@ -665,7 +665,8 @@ gwo_status Handle::log_resolve_batch(LogJob &J, bool &refire) {
         GWO_TRY(log_k1(J, false));
     }
     hist_hint = lo;
-    L.span_hint = hi - lo + 2;
+    static const int span_margin = getenv("GWO_LOG_SPAN_MARGIN") ? atoi(getenv("GWO_LOG_SPAN_MARGIN")) : 1;
+    L.span_hint = hi - lo + 1 + span_margin;
     return GWO_OK;
 }
 

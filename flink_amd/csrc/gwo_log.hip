@@ -41,18 +41,18 @@ __device__ unsigned long long g_kt[64];   // [0, 16): K1 phases, [16, 32): fire 
 struct KTrace {
     bool on;
     uint64_t t;
-    uint64_t acc[8];
+    uint64_t acc[10];
     __device__ __forceinline__ void start(bool en) {
         on = en;
         t = on ? __builtin_amdgcn_s_memtime() : 0;
 #pragma unroll
-        for (int i = 0; i < 8; ++i) acc[i] = 0;
+        for (int i = 0; i < 10; ++i) acc[i] = 0;
     }
     __device__ __forceinline__ void stamp(int ph) {
         if (on) {
             const uint64_t n = __builtin_amdgcn_s_memtime();
 #pragma unroll
-            for (int i = 0; i < 8; ++i)
+            for (int i = 0; i < 10; ++i)
                 if (i == ph) acc[i] += n - t;
             t = n;
         }
@@ -60,7 +60,7 @@ struct KTrace {
     __device__ __forceinline__ void flush(int base) {
         if (on && (threadIdx.x & 63) == 0)
 #pragma unroll
-            for (int i = 0; i < 8; ++i)
+            for (int i = 0; i < 10; ++i)
                 if (acc[i]) atomicAdd(&g_kt[base + i], acc[i]);
     }
 };
@@ -329,8 +329,11 @@ __device__ __forceinline__ void k1_plan_tail(unsigned long long *cursor, BatchSt
 // ------------------------------------------------------------------------------------------------
 // ROUTE: the multi-GPU instance (LogRoute): records of other GPUs are routed (rt.mode 1) or skipped (2).
 // TS32: `ts` holds int32 timestamps - th.tbase (records received in the 20-B wire format; S == 1).
-template <bool HASV, int S, bool ROUTE, bool TS32>   // S: record stride in int64 words (1: SoA columns, 3: {key, ts, value}; 0: runtime)
-__global__ __launch_bounds__(LOG_K1_THREADS) void log_part_kernel(
+// V2 (S == 1, 16-B aligned columns, even tile length): each lane loads two adjacent records per column with one
+// 16-B load (8 B for int32 timestamps) -- record j of a thread is tile + (j / 2) * 2 * LOG_K1_THREADS + 2 * tid + j % 2.
+// A pair straddling the end of the batch reads 8 B past it, inside the 16-B aligned granule of its first record.
+template <bool HASV, int S, bool ROUTE, bool TS32, bool V2>   // S: record stride in int64 words (1: SoA columns, 3: {key, ts, value}; 0: runtime)
+__global__ __launch_bounds__(LOG_K1_THREADS, ROUTE ? 1 : 2) void log_part_kernel(
     const int64_t *__restrict__ key, const int64_t *__restrict__ ts, const int64_t *__restrict__ val, int64_t n,
     int64_t stride, WindowGeom g, long long base, int nunits, unsigned long long *__restrict__ cursor, uint64_t cap,
     int64_t *__restrict__ tmp, BatchStats *st, int64_t *side_key, int64_t *side_ts, int64_t *side_val,
@@ -373,18 +376,52 @@ __global__ __launch_bounds__(LOG_K1_THREADS) void log_part_kernel(
     uint32_t wmask = 0;   // launch windows (bit jj) the inline path accepted records into
     unsigned acc = 0, late = 0, refire = 0, bad_ts = 0, out = 0, bad_kg = 0, bad_range = 0;   // per thread: < 2^32
     int64_t kk[LOG_K1_PER], vv[LOG_K1_PER], tt[LOG_K1_PER];
+    static_assert(!V2 || (S == 1 && LOG_K1_PER % 2 == 0), "V2: SoA columns, pairs of records");
+    // record j's position in the tile
+    auto rec_pos = [&](int j) -> int {
+        return V2 ? (j >> 1) * 2 * LOG_K1_THREADS + 2 * tid + (j & 1) : j * LOG_K1_THREADS + tid;
+    };
     // unconditional loads of a tile (lanes past the end re-read the tile's first record and are
     // discarded); the next tile's loads are issued before this tile's write phase
     auto load_tile = [&](int64_t tile) {
+        if (V2) {
 #pragma unroll
-        for (int j = 0; j < LOG_K1_PER; ++j) {
-            int64_t i = tile + j * LOG_K1_THREADS + tid;
-            i = (i < n && j * LOG_K1_THREADS + tid < tlen) ? i : (tile < n ? tile : 0);
-            const int64_t o = S ? i * S : i * stride;
-            tt[j] = TS32 ? th.tbase + (int64_t)__builtin_nontemporal_load((const int32_t *)ts + o)
-                         : __builtin_nontemporal_load(ts + o);
-            kk[j] = __builtin_nontemporal_load(key + o);
-            vv[j] = HASV ? __builtin_nontemporal_load(val + o) : 0;
+            for (int j2 = 0; j2 < LOG_K1_PER / 2; ++j2) {
+                const int p = j2 * 2 * LOG_K1_THREADS + 2 * tid;
+                int64_t i = tile + p;
+                i = (i < n && p < tlen) ? i : (tile < n ? tile : 0);   // (tile, n: even offsets of aligned columns)
+                if (TS32) {
+                    typedef int int2v __attribute__((ext_vector_type(2)));
+                    const int2v t2 = __builtin_nontemporal_load((const int2v *)((const int32_t *)ts + i));
+                    tt[2 * j2] = th.tbase + (int64_t)t2.x;
+                    tt[2 * j2 + 1] = th.tbase + (int64_t)t2.y;
+                } else {
+                    const ll2 t2 = __builtin_nontemporal_load((const ll2 *)(ts + i));
+                    tt[2 * j2] = t2.x;
+                    tt[2 * j2 + 1] = t2.y;
+                }
+                const ll2 k2 = __builtin_nontemporal_load((const ll2 *)(key + i));
+                kk[2 * j2] = k2.x;
+                kk[2 * j2 + 1] = k2.y;
+                if (HASV) {
+                    const ll2 v2 = __builtin_nontemporal_load((const ll2 *)(val + i));
+                    vv[2 * j2] = v2.x;
+                    vv[2 * j2 + 1] = v2.y;
+                } else {
+                    vv[2 * j2] = vv[2 * j2 + 1] = 0;
+                }
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < LOG_K1_PER; ++j) {
+                int64_t i = tile + j * LOG_K1_THREADS + tid;
+                i = (i < n && j * LOG_K1_THREADS + tid < tlen) ? i : (tile < n ? tile : 0);
+                const int64_t o = S ? i * S : i * stride;
+                tt[j] = TS32 ? th.tbase + (int64_t)__builtin_nontemporal_load((const int32_t *)ts + o)
+                             : __builtin_nontemporal_load(ts + o);
+                kk[j] = __builtin_nontemporal_load(key + o);
+                vv[j] = HASV ? __builtin_nontemporal_load(val + o) : 0;
+            }
         }
     };
     const int64_t tstride = (int64_t)gridDim.x * tlen;
@@ -420,8 +457,8 @@ __global__ __launch_bounds__(LOG_K1_THREADS) void log_part_kernel(
         uint32_t slow = 0;   // bit j: record j is classified out of line (below)
 #pragma unroll
         for (int j = 0; j < LOG_K1_PER; ++j) {
-            const int64_t i = tile + j * LOG_K1_THREADS + tid;
-            const bool in = i < n && j * LOG_K1_THREADS + tid < tlen;
+            const int64_t i = tile + rec_pos(j);
+            const bool in = i < n && rec_pos(j) < tlen;
             uint32_t ci = (uint32_t)nb;   // counter this record increments (nb: the spare)
             uint32_t cb = 0xffffu;        // its code's upper half (0xffff: none)
             bool local = in;
@@ -477,7 +514,7 @@ __global__ __launch_bounds__(LOG_K1_THREADS) void log_part_kernel(
         while (slow) {
             const int j = __builtin_ctz(slow);
             slow &= slow - 1;
-            const int64_t i = tile + j * LOG_K1_THREADS + tid;
+            const int64_t i = tile + rec_pos(j);
             const int64_t o = S ? i * S : i * stride;
             const int64_t t = TS32 ? th.tbase + (int64_t)((const int32_t *)ts)[o] : ts[o], k = key[o];
             long long u = 0;
@@ -537,8 +574,15 @@ __global__ __launch_bounds__(LOG_K1_THREADS) void log_part_kernel(
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const int b = tid * per + q;
+#ifdef GWO_ABL_K1_NORET   // ablation (timing only: records land at made-up offsets): reservations not waited for
+            if (q < per) {
+                atomicAdd(&cursor[((size_t)b * LOG_XG + xg) * LOG_CUR_STRIDE], (unsigned long long)(b < nb ? s_cnt[b] : 0u));
+                at[q] = ((unsigned long long)(tile / tlen) * 40ull) % (cap > 128 ? cap - 128 : 1);
+            }
+#else
             if (q < per) at[q] = atomicAdd(&cursor[((size_t)b * LOG_XG + xg) * LOG_CUR_STRIDE],
                                            (unsigned long long)(b < nb ? s_cnt[b] : 0u));
+#endif
         }
         unsigned long long rat = 0;
         if (ROUTE && (rt.mode == 1 || rt.mode == 3) && tid < nr) {
@@ -590,9 +634,11 @@ __global__ __launch_bounds__(LOG_K1_THREADS) void log_part_kernel(
         }
         // next tile in flight during the writes: unconditional (past the end every lane re-reads record 0, one line),
         // so the write phase's waits count exactly these loads instead of waiting for all of them
+        kt.stamp(4);   // (scatter)
 #ifndef GWO_K1_DELTA_FIRST
         load_tile(tile + tstride);
 #endif
+        kt.stamp(7);   // (next tile's loads issued)
         // s_cnt[b] := the run's first region record - the bucket's tile offset, so the write phase finds a record's
         // destination with one read (mod 2^32: q = s_cnt[b] + p; at >= cap -> q >= cap, the run is dropped).  The
         // atomics precede the loads just issued: their wait is vmcnt(loads), in order, not a wait for the loads.
@@ -604,8 +650,9 @@ __global__ __launch_bounds__(LOG_K1_THREADS) void log_part_kernel(
 #ifdef GWO_K1_DELTA_FIRST   // (A/B: r03's order)
         load_tile(tile + tstride);
 #endif
+        kt.stamp(8);   // (the reservations' results in s_cnt)
         lds_barrier();
-        kt.stamp(4);
+        kt.stamp(9);
         // write phase: straight-line code (a loop here made the compiler wait for every prefetched load first),
         // 4 records per thread per group with their LDS reads in flight together
 #pragma unroll
@@ -1659,6 +1706,12 @@ __global__ __launch_bounds__(LOG_FIRE_THREADS) __attribute__((amdgpu_waves_per_e
 // ------------------------------------------------------------------------------------------------
 // launchers
 // ------------------------------------------------------------------------------------------------
+// GWO_K1_V2=0: K1 loads one record per lane per column (A/B of the 16-B pair loads)
+static bool getenv_k1_v2() {
+    static const int on = getenv("GWO_K1_V2") ? atoi(getenv("GWO_K1_V2")) : 1;
+    return on != 0;
+}
+
 void launch_log_part(const int64_t *key, const int64_t *ts, const int64_t *val, int64_t n, int64_t stride,
                      const WindowGeom &g,
                      long long base, int nunits, int has_val, unsigned long long *cursor, uint64_t cap,
@@ -1673,25 +1726,35 @@ void launch_log_part(const int64_t *key, const int64_t *ts, const int64_t *val, 
     tl = tl < 1 ? 1 : (tl > LOG_K1_TILE ? LOG_K1_TILE : tl);
     const bool route = rt.mode != 0 && stride == 1;
     const size_t dyn = ((size_t)2 * nunits * LOG_ND + 1 + (route ? LOG_RT_MAX : 0)) * sizeof(uint32_t);
-#define GWO_K1(HV, S, R, T32)                                                                                  \
-    hipLaunchKernelGGL((log_part_kernel<HV, S, R, T32>), dim3((int)grid), dim3(LOG_K1_THREADS), dyn, s, key, ts, val, \
-                       n, stride, g, base, nunits, cursor, cap, tmp, st, side_key, side_ts, side_val, side_count, \
+    // 16-B loads of record pairs: SoA columns aligned to 16 B (8 B for int32 timestamps), tiles of an even length
+    const bool v2 = stride == 1 && ((uintptr_t)key & 15) == 0 && (!has_val || ((uintptr_t)val & 15) == 0) &&
+                    ((uintptr_t)ts & (thr.ts32 ? 7 : 15)) == 0 && getenv_k1_v2();
+    if (v2) tl = (tl + 1) & ~(int64_t)1;
+#define GWO_K1(HV, S, R, T32, VV)                                                                              \
+    hipLaunchKernelGGL((log_part_kernel<HV, S, R, T32, VV>), dim3((int)grid), dim3(LOG_K1_THREADS), dyn, s, key, ts, \
+                       val, n, stride, g, base, nunits, cursor, cap, tmp, st, side_key, side_ts, side_val, side_count, \
                        side_cap, side_enabled, ca, thr, rt, (int)tl)
+#define GWO_K1S(HV, R, T32)                  \
+    do {                                     \
+        if (v2) GWO_K1(HV, 1, R, T32, true); \
+        else GWO_K1(HV, 1, R, T32, false);   \
+    } while (0)
     if (route) {   // routing: the first K1 over a batch's own columns (and its route-only re-run)
-        if (has_val) GWO_K1(true, 1, true, false);
-        else GWO_K1(false, 1, true, false);
+        if (has_val) GWO_K1S(true, true, false);
+        else GWO_K1S(false, true, false);
     } else if (thr.ts32) {               // received 20-B wire records (SoA columns, int32 timestamps)
-        if (has_val) GWO_K1(true, 1, false, true);
-        else GWO_K1(false, 1, false, true);
+        if (has_val) GWO_K1S(true, false, true);
+        else GWO_K1S(false, false, true);
     } else if (has_val) {
-        if (stride == 1) GWO_K1(true, 1, false, false);
-        else if (stride == 3) GWO_K1(true, 3, false, false);
-        else GWO_K1(true, 0, false, false);
+        if (stride == 1) GWO_K1S(true, false, false);
+        else if (stride == 3) GWO_K1(true, 3, false, false, false);
+        else GWO_K1(true, 0, false, false, false);
     } else {
-        if (stride == 1) GWO_K1(false, 1, false, false);
-        else if (stride == 3) GWO_K1(false, 3, false, false);
-        else GWO_K1(false, 0, false, false);
+        if (stride == 1) GWO_K1S(false, false, false);
+        else if (stride == 3) GWO_K1(false, 3, false, false, false);
+        else GWO_K1(false, 0, false, false, false);
     }
+#undef GWO_K1S
 #undef GWO_K1
 }
 
@@ -1826,8 +1889,9 @@ void ktrace_report() {
     if (hipMemcpyFromSymbol(v, HIP_SYMBOL(g_kt), sizeof(v)) != hipSuccess) return;
     const double k1 = v[32] ? (double)v[32] : 1.0, fi = v[33] ? (double)v[33] : 1.0;
     fprintf(stderr, "[ktrace] K1 launches %llu, per launch per workgroup (Mcycles, summed over workgroups):\n", v[32]);
-    const char *kn[7] = {"zero+loop", "classify", "slow+barrier", "reserve+offsets", "scatter+prefetch", "write", "stats"};
-    for (int i = 0; i < 7; ++i) fprintf(stderr, "  K1 %-18s %10.3f\n", kn[i], v[i] / k1 / 1e6);
+    const char *kn[10] = {"zero+loop", "classify", "slow+barrier", "reserve+offsets", "scatter", "write", "stats",
+                          "load issue", "reserved delta", "barrier"};
+    for (int i = 0; i < 10; ++i) fprintf(stderr, "  K1 %-18s %10.3f\n", kn[i], v[i] / k1 / 1e6);
     const char *fn[6] = {"P0 keys/table", "P1 claim", "P1 barrier", "P3-P4b", "publish+prefetch", "P5 emit"};
     fprintf(stderr, "[ktrace] fires %llu, per fire (Mcycles, summed over workgroups):\n", v[33]);
     for (int i = 0; i < 6; ++i) fprintf(stderr, "  fire %-18s %10.3f\n", fn[i], v[16 + i] / fi / 1e6);

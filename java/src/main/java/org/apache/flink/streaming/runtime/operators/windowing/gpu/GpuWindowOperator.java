@@ -29,6 +29,7 @@ import org.apache.flink.core.memory.DataInputViewStreamWrapper;
 import org.apache.flink.core.memory.DataOutputSerializer;
 import org.apache.flink.core.memory.DataOutputView;
 import org.apache.flink.metrics.Counter;
+import org.apache.flink.runtime.state.AbstractKeyedStateBackend;
 import org.apache.flink.runtime.state.KeyGroupRange;
 import org.apache.flink.runtime.state.KeyGroupRangeAssignment;
 import org.apache.flink.runtime.state.KeyGroupStatePartitionStreamProvider;
@@ -114,12 +115,23 @@ public class GpuWindowOperator<IN, K> extends AbstractStreamOperator<GpuWindowRe
         // (StreamTaskStateInitializerImpl.java:290-306), which is what getMaxNumberOfParallelSubtasks returns --
         // per-operator setMaxParallelism and KeyGroupRangeAssignment.computeDefaultMaxParallelism included
         final int maxParallelism = getRuntimeContext().getMaxNumberOfParallelSubtasks();
+        // The checkpoint mirror (snapshotState) registers its window timers while the operator snapshots; a backend
+        // that snapshots timers synchronously into raw keyed state (RocksDB with the HEAP timer service) writes them
+        // BEFORE operator.snapshotState runs (InternalTimeServiceManager.java:160-170, StreamOperatorStateHandler
+        // .java:183-186), so its checkpoint would hold the previous mirror's timers: refuse it up front
+        if (getKeyedStateBackend() instanceof AbstractKeyedStateBackend
+                && ((AbstractKeyedStateBackend<?>) getKeyedStateBackend()).requiresLegacySynchronousTimerSnapshots()) {
+            throw new UnsupportedOperationException("GpuWindowOperator checkpoints its windows through the keyed state "
+                    + "backend's timer service; this backend snapshots timers synchronously before the operator (RocksDB "
+                    + "with state.backend.rocksdb.timer-service.factory=HEAP): use the ROCKSDB timer service or a heap "
+                    + "state backend");
+        }
         handle = GwoNative.create(spec.assigner, spec.size, spec.slide, spec.offset, spec.gap, spec.allowedLateness,
                 spec.aggs, spec.valueDtype, spec.keyKind, maxParallelism, range.getStartKeyGroup(),
                 range.getEndKeyGroup(), spec.device, lateTag != null, spec.stateLayout, spec.expectedKeys);
         registerWindowStates();
         if (context.isRestored() && !importMirror()) {
-            restoreRows(context);   // (a savepoint of an earlier version: raw keyed state rows)
+            restoreRows(context);   // (a savepoint of an earlier version: raw keyed state rows only, no timers)
         }
     }
 
@@ -170,25 +182,32 @@ public class GpuWindowOperator<IN, K> extends AbstractStreamOperator<GpuWindowRe
 
     @Override
     public void close() throws Exception {
-        super.close();
-        if (pinned != null) {
-            for (ByteBuffer b : pinned) {
-                GwoNative.hostUnregister(b);
+        try {
+            super.close();
+        } finally {
+            try {
+                if (pinned != null) {
+                    for (ByteBuffer b : pinned) {
+                        try {   // (a buffer that shared a page with one pinned earlier was never registered itself)
+                            GwoNative.hostUnregister(b);
+                        } catch (IllegalArgumentException notRegistered) {
+                            // nothing to release
+                        }
+                    }
+                    pinned = null;
+                }
+            } finally {
+                if (handle != 0) {   // the device state is released whatever happened before
+                    GwoNative.destroy(handle);
+                    handle = 0;
+                }
             }
-            pinned = null;
-        }
-        if (handle != 0) {
-            GwoNative.destroy(handle);
-            handle = 0;
         }
     }
 
     // ---- OneInputStreamOperator ------------------------------------------------------------------------------
     @Override
     public void processElement(StreamRecord<IN> element) throws Exception {
-        if (mirrored) {
-            clearMirror();
-        }
         final IN v = element.getValue();
         final K key = keySelector.getKey(v);
         final int i = n;
@@ -211,16 +230,17 @@ public class GpuWindowOperator<IN, K> extends AbstractStreamOperator<GpuWindowRe
 
     @Override
     public void processWatermark(Watermark mark) throws Exception {
-        clearMirror();   // (before the timer service sees the watermark: the mirror's timers never fire)
         flush();   // the pending records precede the watermark
         GwoNative.advanceWatermark(handle, mark.getTimestamp());
         emitFired();
-        super.processWatermark(mark);
+        // forwarded without advancing the "window-timers" service (AbstractStreamOperator.processWatermark would): it
+        // holds only the last checkpoint's mirror, whose timers must stay until the next checkpoint replaces them --
+        // they are how clearMirror finds the mirrored entries, so no record or watermark pays for clearing them
+        output.emitWatermark(mark);
     }
 
     @Override
     public void endInput() throws Exception {
-        clearMirror();
         flush();
         GwoNative.advanceWatermark(handle, Long.MAX_VALUE);   // StreamSource.java:122
         emitFired();
@@ -371,7 +391,9 @@ public class GpuWindowOperator<IN, K> extends AbstractStreamOperator<GpuWindowRe
     public void snapshotState(StateSnapshotContext context) throws Exception {
         super.snapshotState(context);
         flush();   // prepareSnapshotPreBarrier semantics: the batch is part of the state
-        clearMirror();   // a previous checkpoint's, when no record came in between
+        // the previous checkpoint's mirror is dropped here, not at the next record: a checkpoint copies O(state) into
+        // the backend anyway, the record and watermark path never touches the mirror
+        clearMirror();
         final KeyGroupRange range = getKeyedStateBackend().getKeyGroupRange();
         final int groups = range.getNumberOfKeyGroups();
         final long[] offsets = new long[groups];
@@ -521,7 +543,10 @@ public class GpuWindowOperator<IN, K> extends AbstractStreamOperator<GpuWindowRe
         return true;
     }
 
-    // Drops the backend copy (the GPU holds the state): every window state, merging set and timer of the mirror.
+    // Drops the backend copy (the GPU holds the state): every window state, merging set and timer of the mirror,
+    // enumerated through the mirror's timers (every mirrored window has one; they never fire, see processWatermark).
+    // Sessions: a window's accumulator lives at its state window (a restored WindowOperator savepoint's merged sessions
+    // map windows to other state windows), resolved through the merging set before that is cleared.
     private void clearMirror() throws Exception {
         if (!mirrored) {
             return;
@@ -535,6 +560,14 @@ public class GpuWindowOperator<IN, K> extends AbstractStreamOperator<GpuWindowRe
             windowState.setCurrentNamespace(w);
             windowState.clear();
             if (mergingSets != null) {
+                mergingSets.setCurrentNamespace(VoidNamespace.INSTANCE);
+                final Iterable<Tuple2<TimeWindow, TimeWindow>> pairs = mergingSets.get();
+                if (pairs != null) {
+                    for (Tuple2<TimeWindow, TimeWindow> pr : pairs) {
+                        windowState.setCurrentNamespace(pr.f1);
+                        windowState.clear();
+                    }
+                }
                 mergingSets.setCurrentNamespace(VoidNamespace.INSTANCE);
                 mergingSets.clear();
             }

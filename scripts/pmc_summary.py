@@ -48,6 +48,13 @@ def traffic_json(out_path, root="gpurun_out"):
             continue   # (another instance of the kernel, e.g. the fire's near-empty slow-list instance)
         res[name] = {"hbm_bytes_per_launch": fb + wb, "read_bytes": fb, "write_bytes": wb,
                      "launches_measured": nf, "note": "rocprofv3 FETCH_SIZE x2 (gfx950) + WRITE_SIZE, KB->B"}
+    import datetime
+    import os
+    # the source tree the counters were taken on (TRAFFIC_HEAD: the git HEAD the gpurun command was sent from; the GPU
+    # box has no .git), so a stale file shows in the bench line
+    res["_meta"] = {"head": os.environ.get("TRAFFIC_HEAD", "unknown"),
+                    "date": datetime.datetime.utcnow().strftime("%Y-%m-%d %H:%M UTC"),
+                    "command": os.environ.get("TRAFFIC_CMD", "")}
     json.dump(res, open(out_path, "w"), indent=1)
     print("wrote", out_path)
 
