@@ -61,7 +61,7 @@ class GwoStateRows(C.Structure):
 
 class GwoCommWaits(C.Structure):
     _fields_ = [(n, C.c_int64) for n in ("routed_batches", "count_waits", "wm_waits", "flow_count_waits",
-                                         "flow_wm_waits", "count_wait_ns", "wm_wait_ns")]
+                                         "flow_wm_waits", "count_wait_ns", "wm_wait_ns", "flow_wait_ns")]
 
 
 class GwoHeapStateIds(C.Structure):

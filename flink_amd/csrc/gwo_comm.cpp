@@ -95,7 +95,8 @@ struct Comm {
     // waits while the device was still running the newest routed batches (the host ran ahead by more than the slot
     // ring holds: flow control, not a protocol round trip) -- kept apart from count_waits / wm_waits
     int64_t bp_count_waits = 0, bp_wm_waits = 0;
-    int64_t count_wait_ns = 0, wm_wait_ns = 0;   // host time spent in those waits (all of them)
+    int64_t count_wait_ns = 0, wm_wait_ns = 0;   // host time spent in those waits
+    int64_t flow_wait_ns = 0;                     // host time spent in flow-control waits
     int wm_after_slot = -1;        // the count exchange the queued asynchronous agreement follows on the count stream
     // asynchronous watermark agreement (gwo_comm_set_async_watermark): two host-mapped result blocks, alternating
     bool async_wm = false, wm_pending = false;
@@ -429,26 +430,20 @@ gwo_status Handle::comm_post() {
     (void)NSLOT;
     volatile const unsigned long long *seqw = C.hcnt[Q.slot] + 4 * P;
     if (*seqw != Q.seq) {   // the counts are not there yet: this post waits for them
-        if (not_done(C.ev_rout[Q.slot])) C.bp_count_waits++;
-        else C.count_waits++;
+        const bool flow = not_done(C.ev_rout[Q.slot]);   // (their K1 has not even finished: flow control)
+        (flow ? C.bp_count_waits : C.count_waits)++;
         static const bool trace = getenv("GWO_COMM_TRACE") != nullptr;   // (diagnostics)
-        if (trace) {
-            const unsigned long long seen = *seqw;
-            const hipError_t q2 = hipStreamQuery(C.cs2), q1 = hipStreamQuery(C.cs), q0 = hipStreamQuery(stream);
-            const auto t0 = std::chrono::steady_clock::now();
-            GWO_TRY(spin_seq((const unsigned long long *)seqw, Q.seq, "count exchange", C.cs2));
-            const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
-            fprintf(stderr, "[comm] post seq %llu (latest %llu) saw %llu: waited %.1f us; cs2 %s cs %s main %s\n", Q.seq,
-                    C.cnt_seq, seen, us, q2 == hipSuccess ? "idle" : "busy", q1 == hipSuccess ? "idle" : "busy",
-                    q0 == hipSuccess ? "idle" : "busy");
-        }
-    }
-    {
+        const hipError_t q2 = trace ? hipStreamQuery(C.cs2) : hipSuccess, q1 = trace ? hipStreamQuery(C.cs) : hipSuccess,
+                         q0 = trace ? hipStreamQuery(stream) : hipSuccess;
+        const unsigned long long seen = *seqw;
         const auto t0 = std::chrono::steady_clock::now();
-        const bool missing = *seqw != Q.seq;
         GWO_TRY(spin_seq((const unsigned long long *)seqw, Q.seq, "count exchange", C.cs2));
-        if (missing)
-            C.count_wait_ns += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
+        const int64_t ns = std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
+        (flow ? C.flow_wait_ns : C.count_wait_ns) += ns;
+        if (trace)
+            fprintf(stderr, "[comm] post seq %llu (latest %llu) saw %llu: waited %.1f us; cs2 %s cs %s main %s\n", Q.seq,
+                    C.cnt_seq, seen, ns / 1e3, q2 == hipSuccess ? "idle" : "busy", q1 == hipSuccess ? "idle" : "busy",
+                    q0 == hipSuccess ? "idle" : "busy");
     }
     unsigned long long hs[2 * LOG_RT_MAX], hr[2 * LOG_RT_MAX];
     memcpy(hs, C.hcnt[Q.slot], (size_t)2 * P * 8);
@@ -627,11 +622,12 @@ static gwo_status allreduce_min_async(Handle *h, int64_t v, int64_t *applied) {
         volatile const unsigned long long *seqw = C.hwm[q ^ 1] + 1;
         if (*seqw != C.wm_seq) {   // (queued behind the previous batch's count exchange, itself behind its K1)
             // (the agreement was queued right behind the then newest routed batch's count exchange)
-            if (C.wm_after_slot >= 0 && not_done(C.ev_cnt[C.wm_after_slot])) C.bp_wm_waits++;
-            else C.wm_waits++;
+            const bool flow = C.wm_after_slot >= 0 && not_done(C.ev_cnt[C.wm_after_slot]);
+            (flow ? C.bp_wm_waits : C.wm_waits)++;
             const auto t0 = std::chrono::steady_clock::now();
             GWO_TRY(h->spin_seq((const unsigned long long *)seqw, C.wm_seq, "watermark agreement", C.cs2));
-            C.wm_wait_ns += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
+            (flow ? C.flow_wait_ns : C.wm_wait_ns) +=
+                std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
         }
         *applied = (int64_t)C.hwm[q ^ 1][0];
     } else {
@@ -844,5 +840,6 @@ extern "C" gwo_status gwo_comm_wait_stats(gwo_handle *hh, gwo_comm_waits *out) {
     out->flow_wm_waits = C.bp_wm_waits;
     out->count_wait_ns = C.count_wait_ns;
     out->wm_wait_ns = C.wm_wait_ns;
+    out->flow_wait_ns = C.flow_wait_ns;
     return GWO_OK;
 }

@@ -344,11 +344,12 @@ gwo_status gwo_comm_set_async_watermark(gwo_handle *h, int32_t enabled);
  * running the newest routed batches' K1 are flow control -- the host ran ahead of the device by more than the 3
  * send/receive slots hold -- and are counted apart by gwo_comm_backpressure, not here. */
 gwo_status gwo_comm_stats(gwo_handle *h, int64_t *routed_batches, int64_t *count_waits, int64_t *wm_waits);
-/* The same counters, the flow-control waits counted apart, and the host time spent waiting (every wait, ns). */
+/* The same counters, the flow-control waits counted apart, and the host time spent waiting (ns). */
 typedef struct {
     int64_t routed_batches, count_waits, wm_waits;
     int64_t flow_count_waits, flow_wm_waits;   /* the awaited result was still queued behind unfinished device work */
-    int64_t count_wait_ns, wm_wait_ns;
+    int64_t count_wait_ns, wm_wait_ns;         /* time in count_waits / wm_waits */
+    int64_t flow_wait_ns;                      /* time in the flow-control waits */
 } gwo_comm_waits;
 gwo_status gwo_comm_wait_stats(gwo_handle *h, gwo_comm_waits *out);
 

@@ -262,11 +262,15 @@ def test_virtual_ranks_routed_batches_without_host_waits(F, monkeypatch, async_w
     w = N.GwoCommWaits()
     N.check(lib.gwo_comm_wait_stats(h, C.byref(w)), h, "wait stats")
     print(f"routed {w.routed_batches}: count waits {w.count_waits} ({w.count_wait_ns / 1e3:.1f} us), watermark waits "
-          f"{w.wm_waits} ({w.wm_wait_ns / 1e3:.1f} us); flow control {w.flow_count_waits} count, {w.flow_wm_waits} wm")
+          f"{w.wm_waits} ({w.wm_wait_ns / 1e3:.1f} us); flow control {w.flow_count_waits} count, {w.flow_wm_waits} wm "
+          f"({w.flow_wait_ns / 1e3:.1f} us)")
     assert w.routed_batches == len(b) and len(b) >= 30
-    assert w.count_waits <= len(b) // 8, f"count waits with their K1 finished: {w.count_waits}"
-    assert w.count_wait_ns < 5_000 * len(b), f"{w.count_wait_ns / 1e3:.1f} us waiting for counts"
-    if async_wm:
+    if not hold:   # (held counts force posts at slot reuse: there the interleaving is the point, not the waiting)
+        assert w.count_waits <= len(b) // 8, f"count waits with their K1 finished: {w.count_waits}"
+        assert w.count_wait_ns < 5_000 * len(b), f"{w.count_wait_ns / 1e3:.1f} us waiting for counts"
+    if hold:
+        pass
+    elif async_wm:
         assert w.wm_waits <= len(b) // 8, f"asynchronous watermark agreements waited for: {w.wm_waits}"
         assert w.wm_wait_ns < 5_000 * len(b), f"{w.wm_wait_ns / 1e3:.1f} us waiting for agreements"
     else:
