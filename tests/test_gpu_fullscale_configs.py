@@ -233,3 +233,55 @@ def test_c2_ysb_campaign_count_1m_batches(F, pipelined):
     ends = want[2].cpu().numpy()
     step_of = np.searchsorted(np.maximum.accumulate(wm), ends - 1, side="left")
     assert counts == np.bincount(step_of, minlength=nb).tolist()
+
+
+@pytest.mark.parametrize("layout", ["table", "log"])
+def test_c3_sliding_export_import_continue(F, layout):
+    """C3's shape (sliding 60 s / 1 s AverageAggregate, a watermark every second, lag 1 s) through a checkpoint in the
+    heap backend's layout: an operator runs 62 s of a 120-s stream, its state is exported (one accumulator per
+    (key, window): WindowOperator's window-contents and timers), a fresh operator imports it at the checkpoint's
+    watermark and runs the rest.  Every step's rows -- before and after the restore -- equal the uninterrupted C
+    twin's (count and checksum per step, row for row on the steps that fire the first restored windows).  100K keys
+    (the export holds ~60 entries per key: 6M window entries, the heap backend's own size for this state)."""
+    import torch
+    from flink_amd import _native as N
+    R, span, nkeys = 12_000_000, 120_000, 100_000
+    per = R * 1000 // span
+    steps = span // 1000
+    n = per * steps
+    key, ts, val = _gen(N, n, nkeys, span, 1000, total=R, seed=7)
+    th = ts.cpu().numpy()
+    wms, mx = [], -(1 << 63)
+    for s in range(steps):
+        mx = max(mx, int(th[s * per:(s + 1) * per].max()))
+        wms.append(mx - 1000 - 1)
+    batches = [((s + 1) * per, wms[s]) for s in range(steps)] + [(n, LONG_MAX)]
+    cut = 62
+    mk = lambda: F.GpuWindowOperator(F.SlidingEventTimeWindows.of(60_000, 1000), F.AverageAggregate(),
+                                     max_parallelism=128, state_layout=layout,
+                                     expected_keys=nkeys if layout == "log" else 0)
+    a = mk()
+    keep_a, keep_b = {59, 60, 61}, {62, 63, 119}
+    c1, s1, k1 = _run_steps(N, a.handle, key, ts, val, batches[:cut], 1, keep_a)
+    blob, _, wm = a.export_heap_state()
+    late_a = a.num_late_records_dropped
+    a.close()
+    assert wm == batches[cut - 1][1]
+    b = mk()
+    b.import_heap_state(blob, wm)
+    assert b.state_size() > 50 * nkeys   # every key in (nearly) every open window
+    del blob
+    rest = [(e - batches[cut - 1][0], w) for e, w in batches[cut:]]
+    off = batches[cut - 1][0]
+    c2, s2, k2 = _run_steps(N, b.handle, key[off:], ts[off:], val[off:], rest, 1, {x - cut for x in keep_b})
+    late_b = b.num_late_records_dropped
+    b.close()
+    kh, vh = key.cpu().numpy(), val.cpu().numpy()
+    del key, ts, val
+    torch.cuda.empty_cache()
+    rows, srows, scs, late = cbaseline.run_sliding(kh, th, vh, batches, 60_000, 1000, 0, 0, ["avg"], THREADS, 128,
+                                                   keep_steps=keep_a | keep_b)
+    assert late_a + late_b == late
+    kept = dict(k1)
+    kept.update({x + cut: cols for x, cols in k2.items()})
+    _compare(c1 + c2, s1 + s2, kept, srows, scs, rows, 1)
