@@ -252,7 +252,7 @@ struct Handle {
     gwo_status spin_seq(const unsigned long long *word, unsigned long long seq, const char *what,
                         hipStream_t producer = nullptr);   // producer: the stream that publishes the word (default: stream)
     bool known_device(const void *p, size_t bytes);
-    std::vector<std::pair<uintptr_t, uintptr_t>> dev_ranges;   // device allocations seen by stage_inputs
+    std::vector<std::pair<uintptr_t, uintptr_t>> dev_ranges;   // device allocations seen by this stage_inputs call
     gwo_status ensure_buf(DevBuf &b, size_t bytes);
     int take_counter();
     // occupancy counter c: GWO_OCC_WORDS device words (sharded, see gwo_device.h occ_add)

@@ -320,9 +320,10 @@ bool is_device_ptr(const void *p) {
     return attr.type == hipMemoryTypeDevice || attr.type == hipMemoryTypeManaged;
 }
 
-// Columns inside a device allocation seen before need no pointer query: a batch's columns are usually slices of
-// the same few buffers (hipPointerGetAttributes is a runtime call per column per batch).  A freed range can only be
-// reused by another device or pinned allocation, both of which the kernels read directly.
+// Columns inside a device allocation seen earlier in the same call need no pointer query: a batch's columns are
+// usually slices of one buffer (hipPointerGetAttributes is a runtime call per column).  The ranges are forgotten at
+// every call (stage_inputs), so a range the caller freed between calls -- whose addresses a later host allocation
+// may take -- is never trusted.
 bool Handle::known_device(const void *p, size_t bytes) {
     const uintptr_t a = (uintptr_t)p;
     for (const auto &r : dev_ranges)
@@ -343,6 +344,7 @@ gwo_status Handle::stage_inputs(const int64_t *key, const int64_t *ts, const voi
                                 const int64_t **dt, const int64_t **dv) {
     const void *src[3] = {key, ts, val};
     DevBuf *bufs[3] = {&stage_key, &stage_ts, &stage_val};
+    dev_ranges.clear();   // (known_device: only this call's columns are trusted)
     const int64_t **dst[3] = {dk, dt, dv};
     for (int c = 0; c < 3; ++c) {
         if (!src[c]) {

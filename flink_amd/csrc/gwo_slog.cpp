@@ -78,8 +78,7 @@ gwo_status Handle::slog_init() {
     SlogState &G = *slog;
     // a table of <= 32 KiB (1024 slots for avg's two words; the sweep's slots per thread: 2..8) so about five
     // workgroups share a CU and overlap their partitions' HBM round trips
-    int c = 11;
-    while (c > 9 && slog_lds_bytes(c, plan.nwords) > 32 * 1024) c--;
+    const int c = slog_table_log2(plan.nwords);   // (the kernel instance for nwords is built for this size)
     G.cap_log2 = c;
     // R partitions: ~0.6 of the LDS table per partition at the caller's distinct-key hint (or the first batch)
     const double per = 0.6 * (double)(1 << c);
@@ -329,7 +328,10 @@ gwo_status Handle::slog_step(int64_t start, int64_t end, uint64_t bound, size_t 
         a.stat = G.d_stat;
         static int trace = getenv("GWO_SLOG_TRACE") ? atoi(getenv("GWO_SLOG_TRACE")) : 0;
         static unsigned long long *d_dbg = nullptr;
-        if (trace && !d_dbg) (void)hipMalloc((void **)&d_dbg, 32 * 8 * 8);
+        if (trace && !d_dbg) {
+            (void)hipMalloc((void **)&d_dbg, (SLOG_DBG_PHASES + 2 * SLOG_DBG_BLOCKS) * 8);
+            (void)hipMemset(d_dbg, 0, (SLOG_DBG_PHASES + 2 * SLOG_DBG_BLOCKS) * 8);
+        }
         a.dbg = trace ? d_dbg : nullptr;
         static int mode = getenv("GWO_SLOG_MODE") ? atoi(getenv("GWO_SLOG_MODE")) : 0;
         a.mode = mode;
@@ -375,14 +377,38 @@ gwo_status Handle::slog_step(int64_t start, int64_t end, uint64_t bound, size_t 
             G.live = st[SLS_LIVE];
             G.maxp = st[SLS_MAXP];
             if (trace && (S.J % 16) == 0) {   // phase times of workgroup 0 (device wall clock, 100 MHz)
-                unsigned long long h[32 * 8];
-                (void)hipMemcpy(h, d_dbg, sizeof h, hipMemcpyDeviceToHost);
+                static std::vector<unsigned long long> hv(SLOG_DBG_PHASES + 2 * SLOG_DBG_BLOCKS);
+                (void)hipMemcpy(hv.data(), d_dbg, hv.size() * 8, hipMemcpyDeviceToHost);
+                const unsigned long long *h = hv.data();
+                {   // workgroup start/end spread (ticks of 10 ns from the first start)
+                    std::vector<long long> st, en;
+                    for (int b = 0; b < SLOG_DBG_BLOCKS; ++b)
+                        if (h[SLOG_DBG_PHASES + 2 * b] && h[SLOG_DBG_PHASES + 2 * b + 1]) {
+                            st.push_back((long long)h[SLOG_DBG_PHASES + 2 * b]);
+                            en.push_back((long long)h[SLOG_DBG_PHASES + 2 * b + 1]);
+                        }
+                    if (!st.empty()) {
+                        const long long t0 = *std::min_element(st.begin(), st.end());
+                        for (auto &x : st) x -= t0;
+                        for (auto &x : en) x -= t0;
+                        std::sort(st.begin(), st.end());
+                        std::sort(en.begin(), en.end());
+                        const size_t n = st.size();
+                        fprintf(stderr, "[slog] window %lld workgroups %zu start p50/p90/max %lld/%lld/%lld end min/p10/p50/p90/max "
+                                        "%lld/%lld/%lld/%lld/%lld\n", (long long)start, n, st[n / 2], st[n * 9 / 10], st[n - 1],
+                                en[0], en[n / 10], en[n / 2], en[n * 9 / 10], en[n - 1]);
+                    }
+                    (void)hipMemset(d_dbg, 0, hv.size() * 8);
+                }
                 fprintf(stderr, "[slog] window %lld slow=%llu maxp=%llu:", (long long)start, (unsigned long long)st[SLS_SLOW],
                         (unsigned long long)st[SLS_MAXP]);
-                for (int q = 0; q < 16; ++q)
-                    fprintf(stderr, " [%lld %lld %lld %lld %lld]", (long long)(h[q * 8 + 1] - h[q * 8]),
-                            (long long)(h[q * 8 + 2] - h[q * 8 + 1]), (long long)(h[q * 8 + 3] - h[q * 8 + 2]),
-                            (long long)(h[q * 8 + 4] - h[q * 8 + 3]), (long long)(h[q * 8 + 5] - h[q * 8 + 4]));
+                // per partition: ranges, placement, fold (to the barrier after it), sweep loop 1, pass A, pass B, tail
+                for (int q = 0; q < 16; ++q) {
+                    const unsigned long long *x = h + q * 8;
+                    fprintf(stderr, " [%lld %lld %lld %lld %lld %lld %lld]", (long long)(x[1] - x[0]), (long long)(x[2] - x[1]),
+                            (long long)(x[3] - x[2]), (long long)(x[6] - x[3]), (long long)(x[7] - x[6]),
+                            (long long)(x[4] - x[7]), (long long)(x[5] - x[4]));
+                }
                 fprintf(stderr, "\n");
             }
             break;

@@ -13,7 +13,9 @@
 
 #include "gwo_internal.h"
 
+#ifndef SLOG_THREADS
 #define SLOG_THREADS 256         // a small workgroup: ~5 per CU keep that many partitions' HBM round trips in flight
+#endif
 #define SLOG_MAX_SEGS 63          // signed inputs of one window step (pane segments, restored partials): wave 0
                                   // scans R_p and the segments, one lane each
 #define SLOG_SHARDS 16            // statistics shards (one 128-B line each)
@@ -64,14 +66,31 @@ struct SlogArgs {
     ResultPlan rp;
     OutCols o;
     unsigned long long *stat;     // [SLOG_SHARDS * SLOG_STAT_STRIDE]
-    unsigned long long *dbg;      // optional phase timestamps of workgroup 0 (GWO_SLOG_TRACE)
-    int32_t mode;                 // diagnostics only (GWO_SLOG_MODE): 1 no probe, 2 no word atomics
+    unsigned long long *dbg;      // optional (GWO_SLOG_TRACE): phase timestamps of workgroup 0, then each workgroup's
+                                  // start and end
+#define SLOG_DBG_PHASES 256       // 32 partitions x 8 phase stamps
+#define SLOG_DBG_BLOCKS 4096
+    int32_t mode;                 // diagnostics only (GWO_SLOG_MODE, results invalid): 4 no row reservation,
+                                  // 8 no R' stores, 16 no row stores
     int32_t emit;                 // 0: an intermediate step of a chunked window step (R' only, no rows)
 };
+
+#ifndef GWO_SLOG_TABLE_KB
+#define GWO_SLOG_TABLE_KB 32
+#endif
+// log2 of the window step's LDS table slots for nwords accumulator words: the largest of 2^9..2^11 whose table fits
+// GWO_SLOG_TABLE_KB KiB (32: about five workgroups share a CU and overlap their partitions' HBM round trips)
+constexpr int slog_cap_log2_for(int nwords) {
+    int c = 11;
+    while (c > 9 && ((long long)1 << c) * (long long)(1 + nwords) * 8 > GWO_SLOG_TABLE_KB * 1024) c--;
+    return c;
+}
 
 namespace gwo {
 // Dynamic LDS bytes of the fire kernel for a table of 2^cap_log2 slots.
 size_t slog_lds_bytes(int cap_log2, int nwords);
+// log2 of the table slots the kernel instance for nwords is built for (slog_cap_log2_for, in the kernels' unit)
+int slog_table_log2(int nwords);
 // One window step over every partition of a.in (persistent grid: every workgroup resident on the `cus` CUs).
 void launch_slog_fire(const SlogArgs &a, int cus, hipStream_t s);
 void launch_slog_stat_publish(unsigned long long *stat, unsigned long long *rb, unsigned long long seq, hipStream_t s);

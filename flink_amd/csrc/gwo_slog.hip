@@ -32,6 +32,7 @@ typedef __attribute__((address_space(1))) const uint32_t g_u32;
 typedef __attribute__((address_space(1))) const uint8_t g_u8;
 
 size_t slog_lds_bytes(int cap_log2, int nwords) { return ((size_t)1 << cap_log2) * (size_t)(1 + nwords) * 8; }
+int slog_table_log2(int nwords) { return slog_cap_log2_for(nwords); }
 
 // Bucket of a key: a multiplicative hash of both halves, independent of the partition bits (digit_hash) and of lp,
 // so a partition split keeps every key's bucket.
@@ -45,8 +46,14 @@ __device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v)
     return v;
 }
 
+// LDS position of table slot s (bucket s >> 3, slot s & 7 of it): the slot index within the bucket is XORed with bits
+// 2-4 of the bucket.  A bucket is 64 B, so without it slot i of every bucket falls on one of only 4 bank pairs and
+// a wave searching 64 random buckets reads 16-way conflicted; with it slot i spreads over all 32 (and the sweep's
+// thread-contiguous slots, 8-way conflicted at a 32-B lane stride, spread too).  A bucket's slots stay in its 64 B.
+__device__ __forceinline__ int slot_lds(int s) { return s ^ ((s >> 5) & 7); }
+
 __device__ __forceinline__ int64_t lds_key(const int64_t *s_key, int slot) {
-    return __hip_atomic_load(&s_key[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    return __hip_atomic_load(&s_key[slot_lds(slot)], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
 // Find or claim key k's slot.  The search reads whole buckets (8 LDS reads, one round trip) from the key's home
@@ -77,7 +84,7 @@ __device__ __forceinline__ int slog_find(int64_t *s_key, uint8_t *s_ovf, int NB,
             b = (b + 1) & (NB - 1);
         }
         if (ff < 0) return -2;
-        const unsigned long long prev = atomicCAS((unsigned long long *)&s_key[ff], (unsigned long long)GWO_EMPTY_KEY,
+        const unsigned long long prev = atomicCAS((unsigned long long *)&s_key[slot_lds(ff)], (unsigned long long)GWO_EMPTY_KEY,
                                                   (unsigned long long)k);
         if ((int64_t)prev == GWO_EMPTY_KEY) {
             claims++;
@@ -129,6 +136,7 @@ __global__ __launch_bounds__(SLOG_THREADS) __attribute__((amdgpu_waves_per_eu(4,
     }
     __syncthreads();
 
+    if (a.dbg && tid == 0 && blockIdx.x < SLOG_DBG_BLOCKS) a.dbg[SLOG_DBG_PHASES + 2 * blockIdx.x] = wall_clock64();
     int pn = 0;
     auto stamp = [&](int ph) {
         if (a.dbg && blockIdx.x == 0 && tid == 0 && pn < 32) a.dbg[pn * 8 + ph] = wall_clock64();
@@ -240,7 +248,7 @@ __global__ __launch_bounds__(SLOG_THREADS) __attribute__((amdgpu_waves_per_eu(4,
                             continue;
                         }
                         const uint32_t b = s_map[i];
-                        const int slot = (int)(b * 8 + (i - s_pre[b]));
+                        const int slot = slot_lds((int)(b * 8 + (i - s_pre[b])));
                         s_key[slot] = ek[j];
 #pragma unroll
                         for (int w = 0; w < NW; ++w) s_w[w * T + slot] = ew[j][w];
@@ -298,7 +306,7 @@ __global__ __launch_bounds__(SLOG_THREADS) __attribute__((amdgpu_waves_per_eu(4,
                         s_fail = 1;
                         continue;
                     }
-                    int64_t *dst = slot >= 0 ? s_w + slot : s_side + 1;
+                    int64_t *dst = slot >= 0 ? s_w + slot_lds(slot) : s_side + 1;
                     const int ds = slot >= 0 ? T : 1;
                     if (slot < 0) s_side[0] = 1;
                     const bool raw = (m >> 12) & 1, neg = (m >> 14) & 1;
@@ -310,12 +318,12 @@ __global__ __launch_bounds__(SLOG_THREADS) __attribute__((amdgpu_waves_per_eu(4,
                     }
                 }
             }
-            stamp(3);
             const unsigned long long cw = wave_sum_u64(claims);
             if (lane == 0 && cw) atomicAdd(&s_used, (unsigned)cw);
             __syncthreads();
             const bool failed = s_fail != 0 || s_used > limit;
             __syncthreads();
+            stamp(3);
             if (failed) {   // more keys in range than the table holds: reset, halve the range
                 for (int i = tid; i < T; i += SLOG_THREADS) s_key[i] = GWO_EMPTY_KEY;
                 for (int i = tid; i < T * NW; i += SLOG_THREADS) s_w[i] = 0;
@@ -339,7 +347,7 @@ __global__ __launch_bounds__(SLOG_THREADS) __attribute__((amdgpu_waves_per_eu(4,
             const int b_t = (tid * SPT) >> 3;   // this thread's bucket
             uint32_t cnt0 = 0, cnt1 = 0, code = 0;   // code bit 2i: slot i live, bit 2i+1: its output half
             for (int i = 0; i < SPT; ++i) {
-                const int s = tid * SPT + i;
+                const int s = slot_lds(tid * SPT + i);
                 const int64_t k = s_key[s];
                 if (k == GWO_EMPTY_KEY) continue;
                 const int64_t c = s_w[a.count_word * T + s];
@@ -381,6 +389,7 @@ __global__ __launch_bounds__(SLOG_THREADS) __attribute__((amdgpu_waves_per_eu(4,
             }
             if (lane == 63) s_wsum[wave] = incl;
             __syncthreads();   // (also: every s_ovo flag is set)
+            stamp(6);
             uint32_t pre = 0, tot = 0;
 #pragma unroll
             for (int w = 0; w < SLOG_THREADS / 64; ++w) {
@@ -390,7 +399,9 @@ __global__ __launch_bounds__(SLOG_THREADS) __attribute__((amdgpu_waves_per_eu(4,
             }
             const uint32_t ex = pre + incl - v;   // this thread's first positions (low: half 0, high: half 1)
             const uint32_t tot0 = tot & 0xffffu, tot1 = tot >> 16;
-            if (tid == 0) s_rowbase = (a.emit && tot0 + tot1) ? atomicAdd(a.o.count, (unsigned long long)(tot0 + tot1)) : 0ull;
+            if (tid == 0)
+                s_rowbase = (a.mode & 4) ? (unsigned long long)p * 700ull   // (diagnostic: no reservation)
+                            : (a.emit && tot0 + tot1) ? atomicAdd(a.o.count, (unsigned long long)(tot0 + tot1)) : 0ull;
             const uint32_t qb0 = s_qn[0], qb1 = s_qn[1];
             const uint32_t qout0 = split ? 2 * p : p;
             // R''s bucket bytes: the first thread of each bucket sums the bucket's threads (consecutive lanes)
@@ -408,7 +419,7 @@ __global__ __launch_bounds__(SLOG_THREADS) __attribute__((amdgpu_waves_per_eu(4,
                 uint32_t at0 = ex & 0xffffu, at1 = ex >> 16;
                 auto put = [&](int64_t k, const int64_t *wp, int ws, uint32_t half) {
                     const uint32_t qpos = (half ? qb1 + at1++ : qb0 + at0++);
-                    if (qpos >= a.out.rcap) return;
+                    if (qpos >= a.out.rcap || (a.mode & 8)) return;
                     int64_t *col = a.out.rec + (uint64_t)(qout0 + half) * a.out.rcap * RW;   // SoA columns
                     col[qpos] = k;
 #pragma unroll
@@ -417,11 +428,12 @@ __global__ __launch_bounds__(SLOG_THREADS) __attribute__((amdgpu_waves_per_eu(4,
                 if (side_live) put(GWO_EMPTY_KEY, s_side + 1, 1, side_half);
                 for (int i = 0; i < SPT; ++i) {
                     if (!((code >> (2 * i)) & 1u)) continue;
-                    const int sl = tid * SPT + i;
+                    const int sl = slot_lds(tid * SPT + i);
                     put(s_key[sl], s_w + sl, T, (code >> (2 * i + 1)) & 1u);
                 }
             }
             __syncthreads();   // s_rowbase is published; every read of s_qn and s_ovo is done
+            stamp(7);
             // pass B: rows (the partition's run: half-0 keys first), slots reset for the next fold
             {
                 const unsigned long long rowbase = s_rowbase;
@@ -429,7 +441,7 @@ __global__ __launch_bounds__(SLOG_THREADS) __attribute__((amdgpu_waves_per_eu(4,
                 auto row = [&](int64_t k, const int64_t *wp, int ws, uint32_t half) {
                     const uint32_t ord = half ? tot0 + at1++ : at0++;
                     const unsigned long long r = rowbase + ord;
-                    if (!a.emit || (long long)r >= a.o.cap) return;
+                    if (!a.emit || (long long)r >= a.o.cap || (a.mode & 16)) return;
                     int64_t acc[NW];
 #pragma unroll
                     for (int w = 0; w < NW; ++w) acc[w] = wp[w * ws];
@@ -452,7 +464,7 @@ __global__ __launch_bounds__(SLOG_THREADS) __attribute__((amdgpu_waves_per_eu(4,
                 if (side_live) row(GWO_EMPTY_KEY, s_side + 1, 1, side_half);
                 for (int i = 0; i < SPT; ++i) {
                     if (!((code >> (2 * i)) & 1u)) continue;
-                    const int sl = tid * SPT + i;
+                    const int sl = slot_lds(tid * SPT + i);
                     row(s_key[sl], s_w + sl, T, (code >> (2 * i + 1)) & 1u);
                     s_key[sl] = GWO_EMPTY_KEY;
 #pragma unroll
@@ -489,6 +501,7 @@ __global__ __launch_bounds__(SLOG_THREADS) __attribute__((amdgpu_waves_per_eu(4,
         __syncthreads();   // s_beg / s_qn / s_rn are rewritten for the next partition
         stamp(5);
     }
+    if (a.dbg && tid == 0 && blockIdx.x < SLOG_DBG_BLOCKS) a.dbg[SLOG_DBG_PHASES + 2 * blockIdx.x + 1] = wall_clock64();
     // statistics -> shard blockIdx % SLOG_SHARDS
     const unsigned long long nl = wave_sum_u64(st_neg);
     if (lane == 0 && nl) atomicAdd(&a.stat[(blockIdx.x % SLOG_SHARDS) * SLOG_STAT_STRIDE + SLS_NEG], nl);

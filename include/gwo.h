@@ -223,7 +223,13 @@ gwo_status gwo_restore(gwo_handle *h, const gwo_state_rows *rows, int32_t n_word
  * The accumulator is GpuAggregates.Descriptor's long[] (LongPrimitiveArraySerializer: int32 length, int64 words; two
  * words per aggregate: COUNT {n, 0}, SUM {sum, 0}, MIN/MAX {value, 0} -- float64 {double bits, 1} --, AVG {sum, count}),
  * so a savepoint of the reference WindowOperator running that same AggregateFunction restores here and vice versa.
- * Sliding windows export one entry per (key, window) from their panes; their import is GWO_ERR_UNSUPPORTED.
+ * Sliding windows export one entry per (key, window) from their panes.  Their import restores each (key, window)
+ * entry as its own restored window -- pending windows fire as the watermark passes them (the ring and recompute
+ * tables and the log layout's running total alike), emitted ones re-fire their late records while allowedLateness
+ * keeps them; a pending window the import watermark already passed, an emitted window on the log layout, or a
+ * gwo_snapshot / gwo_snapshot_rows of a handle that still holds restored sliding windows is GWO_ERR_UNSUPPORTED
+ * (export works).  A state id outside `ids` (a stateful trigger's or user keyed state) is GWO_ERR_UNSUPPORTED with
+ * the id named in the message.
  * gwo_export_heap_state with buf == NULL sets *len to the bytes needed; kg_offsets (may be NULL) receives each key
  * group's offset in buf (KeyGroupRangeOffsets).  gwo_import_heap_state reads a concatenation of key-group sections
  * (several old subtasks' for a rescale), keeps ITS key groups and restores them as gwo_restore does (fresh handle;

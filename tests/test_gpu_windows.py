@@ -1099,3 +1099,29 @@ def test_snapshot_restore_sliding_panes(F, ring):
     _run_batches(c, k[prev:], t[prev:], v[prev:], [(e - prev, w) for e, w in b[half:]])
     assert sorted(rows + list(c.output)) == sorted((r.key, r.start, r.end, r.result) for r in ref.output)
     c.close()
+
+
+def test_device_and_host_batches_alternate_after_free(F):
+    """Batches alternate between device columns (freed after their call) and host columns: each call learns its
+    own device ranges (Handle::known_device), so host columns -- possibly at addresses a freed device buffer had --
+    are always staged, and every row equals the oracle's."""
+    import torch
+    k, t, v, b = _c1(n=200_000, nkeys=2_000, every=20_000)
+    op = F.GpuWindowOperator(F.TumblingEventTimeWindows.of(5000), F.SumAggregate())
+    prev = 0
+    for i, (end, wm) in enumerate(b):
+        if i % 2 == 0:
+            dk, dt, dv = (torch.from_numpy(np.ascontiguousarray(x[prev:end])).cuda() for x in (k, t, v))
+            op.process_device_batch(dk.data_ptr(), dt.data_ptr(), dv.data_ptr(), end - prev)
+            torch.cuda.synchronize()
+            del dk, dt, dv
+            torch.cuda.empty_cache()
+        else:
+            op.process_batch(k[prev:end].copy(), t[prev:end].copy(), v[prev:end].copy())
+        op.process_watermark(wm)
+        prev = end
+    op.end_input()
+    (wk, ws, we, res), late = V.tumbling_lateness0(k, t, v, _final(b), 5000, 0, [1])
+    assert _rows(op) == _want(wk, ws, we, res)
+    assert op.num_late_records_dropped == late
+    op.close()
