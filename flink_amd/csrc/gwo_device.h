@@ -227,6 +227,23 @@ __device__ __forceinline__ unsigned long long block_reserve(unsigned v, unsigned
 // __syncthreads() lowers to a workgroup release + acquire fence, which on gfx950 waits vmcnt(0) whenever a global
 // store or atomic may be pending: every load, store and atomic in flight (a prefetch, a row reservation, a tile's
 // output) drained at each barrier.  Use only where the barrier orders LDS accesses, never global memory.
+// Arrival of this workgroup at the end of its grid, from thread 0 once every statistic of the workgroup has completed
+// (vmcnt): true for the last workgroup.  Arrivals are counted per shard (blockIdx % ARR_SHARDS, a 128-B line each) and
+// the last of a shard counts the shard, so an address takes about gridDim / 16 + 16 adds instead of gridDim
+// (device-scope atomics on one address serialise at ~12 ns each: ~3 us for the last of 256 workgroups).  ctr:
+// ARR_WORDS words, zero at launch and left zero (each counter is reset by its last arriver).
+// (ARR_SHARDS, ARR_WORDS: gwo_internal.h)
+__device__ __forceinline__ bool grid_arrive_last(unsigned long long *ctr) {
+    const unsigned q = blockIdx.x % ARR_SHARDS;
+    const unsigned members = (gridDim.x - q + ARR_SHARDS - 1) / ARR_SHARDS;
+    const unsigned nsh = gridDim.x < ARR_SHARDS ? gridDim.x : ARR_SHARDS;
+    if (atomicAdd(&ctr[q * 16], 1ull) != members - 1) return false;
+    atomicExch(&ctr[q * 16], 0ull);   // every member of the shard has arrived: free for the next launch
+    if (atomicAdd(&ctr[ARR_SHARDS * 16], 1ull) != nsh - 1) return false;
+    atomicExch(&ctr[ARR_SHARDS * 16], 0ull);
+    return true;
+}
+
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 __device__ __forceinline__ unsigned block_exclusive_scan(unsigned v, unsigned *total) {

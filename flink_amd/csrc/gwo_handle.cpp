@@ -215,7 +215,7 @@ Handle::~Handle() {
     if (h_ident_side) (void)hipHostFree(h_ident_side);
     dir_buf.release();
     refire_buf.release();
-    for (DevBuf *b : {&cb_dump_key, &cb_dump_acc, &cb_ovf, &cb_blk, &cb_ctr, &cb_dir, &cb_spec_dir, &sp_dir, &sp_go, &cb_dbg})
+    for (DevBuf *b : {&cb_dump_key, &cb_dump_acc, &cb_ovf, &cb_blk, &cb_ctr, &cb_dir, &cb_arr, &cb_spec_dir, &sp_dir, &sp_go, &cb_dbg})
         b->release();
     if (cb_rb) (void)hipHostFree(cb_rb);
     if (cb_ev) (void)hipEventDestroy(cb_ev);

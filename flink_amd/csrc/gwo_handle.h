@@ -171,7 +171,7 @@ struct Handle {
     int cb_cus = 0;
     uint64_t recent_cap = 0;                           // capacity of the last retired window/pane table
     int cb_max_wg = 0;                                 // gather workgroups at most (GWO_CB_WG; default 4 per CU)
-    DevBuf cb_dump_key, cb_dump_acc, cb_ovf, cb_blk, cb_ctr, cb_dir;   // combine path scratch (insert_combined)
+    DevBuf cb_dump_key, cb_dump_acc, cb_ovf, cb_blk, cb_ctr, cb_dir, cb_arr;   // combine path scratch (insert_combined)
     unsigned long long *cb_rb = nullptr, *cb_rb_dev = nullptr;        // host-mapped readback blocks (2 slots)
     unsigned long long cb_seq = 0;
     hipEvent_t cb_ev = nullptr;

@@ -17,6 +17,8 @@
 #define GWO_OCC_SHARDS 8          // occupancy counter shards (gwo_device.h occ_add)
 #define GWO_OCC_SHARD_STRIDE 8    // words between shards: one 64-B line each
 #define GWO_OCC_WORDS (GWO_OCC_SHARDS * GWO_OCC_SHARD_STRIDE)
+#define ARR_SHARDS 16             // grid_arrive_last (gwo_device.h): arrival counter shards, a 128-B line each
+#define ARR_WORDS ((ARR_SHARDS + 1) * 16)
 // scan_kernel statistics shards: SCAN_SHARDS x SCAN_SW words (min, max, 6 counters, the histogram), then
 // SCAN_SHARDS + 1 arrival counters 16 words apart; min/max preset, every scan leaves them reset
 #define SCAN_SHARDS 16
@@ -120,7 +122,7 @@ struct CombineArgs {
     unsigned long long *ovf_count;     // reset by the gather's last workgroup
     unsigned long long ovf_cap;
     unsigned long long *blk;           // statistics shards (gather_stat_words(); min/max words preset)
-    unsigned long long *done;          // workgroups finished (reset by the last one)
+    unsigned long long *done;          // arrival counters of the gather's workgroups (ARR_WORDS, left zero)
     int32_t S;                         // LDS slots per unit (power of two)
     int32_t sbits;                     // log2(S)
     long long hint;                    // units hint, hint + 1 fold in LDS; the histogram starts at hint

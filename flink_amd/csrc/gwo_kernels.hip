@@ -849,7 +849,7 @@ __global__ __launch_bounds__(CB_THREADS) void gather_kernel(GatherArgs A) {
     __shared__ int s_last;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (tid == 0) s_last = atomicAdd(kt->a.done, 1ull) == (unsigned long long)(gridDim.x - 1);
+    if (tid == 0) s_last = grid_arrive_last(kt->a.done);
     __syncthreads();
     CB_STAMP(4);
     // the dump (accumulators only of occupied slots; dump_used tells the merge which tables) reaches the merge
@@ -894,7 +894,6 @@ __global__ __launch_bounds__(CB_THREADS) void gather_kernel(GatherArgs A) {
             const unsigned long long ov = atomicExch(kt->a.ovf_count, 0ull);   // read and reset for the next batch
             rb_put(&kt->a.rb[RBW(overflow)], ov);
 #undef RBW
-            *kt->a.done = 0;
             s_spec[0] = ov;
         } else if (q == 1) {
             const unsigned long long sc = kt->a.side_enabled ? atomicAdd(kt->side_count, 0ull) : 0ull;

@@ -1234,6 +1234,7 @@ __global__ __launch_bounds__(LOG_FIRE_THREADS) __attribute__((amdgpu_waves_per_e
     __shared__ uint32_t s_beg[LOG_MAX_SEGS + 1];   // flattened record space of a partition: segment s
     __shared__ uint32_t s_src[LOG_MAX_SEGS];       //   covers [s_beg[s], s_beg[s+1]) from record s_src[s]
     __shared__ const int64_t *s_rp[LOG_MAX_SEGS];
+    __shared__ uint16_t s_cseg[FIRE_RCAP / 64];    // segment of record 64 c (chunks starting below the total)
     __shared__ uint32_t s_wsum[FIRE_RPT * (LOG_FIRE_THREADS / 64)];   // per-(r, wave) sums -> prefixes
     __shared__ uint32_t s_tot, s_rows;
     __shared__ uint32_t s_pw[LOG_FIRE_THREADS / 64 + 1];
@@ -1280,8 +1281,12 @@ __global__ __launch_bounds__(LOG_FIRE_THREADS) __attribute__((amdgpu_waves_per_e
         }
         lds_barrier();
         if (tid < nseg) {
-            s_beg[tid] = s_pw[wave] + incl_c - cnt;
+            const uint32_t b = s_pw[wave] + incl_c - cnt;
+            s_beg[tid] = b;
             s_src[tid] = off;
+            // the chunks of 64 records that start inside this segment (the fast path's records only)
+            const uint32_t e = b + cnt < (uint32_t)FIRE_RCAP ? b + cnt : (uint32_t)FIRE_RCAP;
+            for (uint32_t ch = (b + 63) >> 6; (ch << 6) < e; ++ch) s_cseg[ch] = (uint16_t)tid;
         }
         if (tid == 0) s_beg[nseg] = s_pw[LOG_FIRE_THREADS / 64];
         lds_barrier();
@@ -1297,13 +1302,17 @@ __global__ __launch_bounds__(LOG_FIRE_THREADS) __attribute__((amdgpu_waves_per_e
         const bool fits = on && total <= (uint32_t)FIRE_RCAP;
         const int64_t *addr[FIRE_RPT];
         int segr[FIRE_RPT];
-        if (nseg <= 32) {   // segment of record i = number of segment starts <= i (broadcast LDS reads)
+        if (fits) {   // segment of record i: its 64-record chunk's first record's segment, then the (few) starts
+                      // between (record i's chunk is a wave's run: one broadcast read)
 #pragma unroll
-            for (int r = 0; r < FIRE_RPT; ++r) segr[r] = 0;
-            for (int sg = 1; sg < nseg; ++sg) {
-                const uint32_t bs = s_beg[sg];
-#pragma unroll
-                for (int r = 0; r < FIRE_RPT; ++r) segr[r] += (uint32_t)(tid + r * LOG_FIRE_THREADS) >= bs;
+            for (int r = 0; r < FIRE_RPT; ++r) {
+                const uint32_t i = tid + r * LOG_FIRE_THREADS;
+                int seg = 0;
+                if (i < total) {
+                    seg = s_cseg[i >> 6];
+                    while (i >= s_beg[seg + 1]) seg++;
+                }
+                segr[r] = seg;
             }
         } else {
             int seg = 0;

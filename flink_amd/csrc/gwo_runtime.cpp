@@ -468,7 +468,11 @@ gwo_status Handle::insert_combined(const int64_t *k, const int64_t *t, const int
     a.ovf_count = (unsigned long long *)cb_ctr.ptr;
     a.ovf_cap = (unsigned long long)n;
     a.blk = (unsigned long long *)cb_blk.ptr;
-    a.done = (unsigned long long *)cb_ctr.ptr + 1;
+    if (!cb_arr.ptr) {
+        GWO_TRY(ensure_buf(cb_arr, ARR_WORDS * 8));
+        GWO_TRY(hipcheck(hipMemsetAsync(cb_arr.ptr, 0, ARR_WORDS * 8, stream), "arrival counters"));
+    }
+    a.done = (unsigned long long *)cb_arr.ptr;
     if (!cb_rb) {
         GWO_TRY(hipcheck(hipHostMalloc((void **)&cb_rb, 2 * CB_RB_WORDS * 8, hipHostMallocCoherent | hipHostMallocMapped),
                          "combine readback"));

@@ -21,7 +21,7 @@ void launch_sess_long(const int64_t *key, const int64_t *ts, const int64_t *val,
                       unsigned long long *sc, long long scap, const SessLists &ls, unsigned long long *rb,
                       unsigned long long seq, unsigned long long *reset_rows, hipStream_t s);
 void launch_sess_fire(const TableDesc &t, uint64_t cap, int stride, const AccPlan &p, const ResultPlan &rp,
-                      const SessGeom &g, OutCols o, SessErr *err, uint32_t *done, unsigned long long *shards,
+                      const SessGeom &g, OutCols o, SessErr *err, unsigned long long *arr, unsigned long long *shards,
                       unsigned long long *rb, unsigned long long seq, hipStream_t s);
 void launch_sess_compact(const TableDesc &src, uint64_t cap, const TableDesc &dst, int stride, hipStream_t s);
 void launch_sess_pool_compact(const TableDesc &t, uint64_t cap, int stride, int sw, const int64_t *old_pool,
@@ -54,7 +54,8 @@ struct SessionState {
     // batch's slots in sess_long_kernel) and back once they stop
     bool lists = true, lists_auto = true;
     DevBuf bkt;                     // [(cap + 1) * SESS_BKT] bucket words (counts zero between batches)
-    uint32_t *ctl = nullptr;        // SessLists::ctl; word 3: sess_fire_kernel's workgroups done
+    uint32_t *ctl = nullptr;        // SessLists::ctl
+    unsigned long long *arr = nullptr;   // sess_fire_kernel's arrival counters (ARR_WORDS)
     unsigned long long *shards = nullptr;   // SessLists::shards (zero between kernels)
     // spill pool of keys with more in-flight sessions than an entry holds (gwo_internal.h SessGeom)
     int64_t *pool = nullptr;
@@ -103,6 +104,8 @@ gwo_status Handle::session_init() {
     }
     GWO_TRY(dalloc((void **)&S.ctl, 16));
     GWO_TRY(hipcheck(hipMemsetAsync(S.ctl, 0, 16, stream), "session lists"));
+    GWO_TRY(dalloc((void **)&S.arr, ARR_WORDS * 8));
+    GWO_TRY(hipcheck(hipMemsetAsync(S.arr, 0, ARR_WORDS * 8, stream), "fire arrivals"));
     GWO_TRY(dalloc((void **)&S.shards, SESS_SHARDS * SESS_SHARD_STRIDE * 8));
     GWO_TRY(hipcheck(hipMemsetAsync(S.shards, 0, SESS_SHARDS * SESS_SHARD_STRIDE * 8, stream), "session shards"));
     S.stride = (2 + S.smax * (3 + plan.nwords) + 1) & ~1;
@@ -141,6 +144,7 @@ void Handle::session_free() {
     if (S.h_err_fire) (void)hipHostFree(S.h_err_fire);
     if (S.pool) (void)hipFree(S.pool);
     if (S.ctl) (void)hipFree(S.ctl);
+    if (S.arr) (void)hipFree(S.arr);
     if (S.shards) (void)hipFree(S.shards);
     S.bkt.release();
     S.rec_slot.release();
@@ -404,7 +408,7 @@ gwo_status Handle::fire_session(int64_t new_wm) {
     g.wm = new_wm;
     S.reset_behind_fire = false;
     prof_begin(GWO_KERNEL_FIRE);
-    launch_sess_fire(desc(S.T), S.T.cap, S.stride, plan, rplan, g, out_cols(), S.d_err_fire, S.ctl + 3, S.shards,
+    launch_sess_fire(desc(S.T), S.T.cap, S.stride, plan, rplan, g, out_cols(), S.d_err_fire, S.arr, S.shards,
                      S.rbf_dev, ++S.rbf_seq, stream);
     GWO_TRY(launch_ok("sess fire"));
     prof_end(GWO_KERNEL_FIRE, (int64_t)S.T.cap);

@@ -566,7 +566,7 @@ __device__ __forceinline__ long long sf_sweep_slot(int64_t *e, uint64_t i, int64
 }
 
 __global__ __launch_bounds__(256) void sess_fire_kernel(TableDesc t, uint64_t cap, int stride, AccPlan p, ResultPlan rp,
-                                                        SessGeom g, OutCols o, SessErr *err, uint32_t *done,
+                                                        SessGeom g, OutCols o, SessErr *err, unsigned long long *arr,
                                                         unsigned long long *shards, unsigned long long *rb,
                                                         unsigned long long seq) {
     const int sw = 3 + p.nwords;
@@ -689,7 +689,7 @@ __global__ __launch_bounds__(256) void sess_fire_kernel(TableDesc t, uint64_t ca
     __shared__ int s_last;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (threadIdx.x == 0) s_last = atomicAdd(done, 1u) == gridDim.x - 1;
+    if (threadIdx.x == 0) s_last = grid_arrive_last(arr);
     __syncthreads();
     if (!s_last) return;
     constexpr int NW = (int)(sizeof(SessErr) / 8);
@@ -701,7 +701,6 @@ __global__ __launch_bounds__(256) void sess_fire_kernel(TableDesc t, uint64_t ca
                                                                                        : 0ull;
         rb_put(&rb[w], atomicAdd((unsigned long long *)err + w, add) + add);
     }
-    if (threadIdx.x == 0) *done = 0;
     rb_publish(&rb[NW], seq);
 }
 
@@ -796,14 +795,14 @@ void launch_sess_long(const int64_t *key, const int64_t *ts, const int64_t *val,
 }
 
 void launch_sess_fire(const TableDesc &t, uint64_t cap, int stride, const AccPlan &p, const ResultPlan &rp,
-                      const SessGeom &g, OutCols o, SessErr *err, uint32_t *done, unsigned long long *shards,
+                      const SessGeom &g, OutCols o, SessErr *err, unsigned long long *arr, unsigned long long *shards,
                       unsigned long long *rb, unsigned long long seq, hipStream_t s) {
     // about one workgroup per CU (MI355X: 256), fewer for small tables
 #ifndef SF_WG
 #define SF_WG 256
 #endif
     hipLaunchKernelGGL(sess_fire_kernel, dim3(sgrid((int64_t)cap + 1, 256 * SF_SPT, SF_WG)), dim3(256), 0, s, t, cap,
-                       stride, p, rp, g, o, err, done, shards, rb, seq);
+                       stride, p, rp, g, o, err, arr, shards, rb, seq);
 }
 
 void launch_sess_pool_compact(const TableDesc &t, uint64_t cap, int stride, int sw, const int64_t *old_pool,
