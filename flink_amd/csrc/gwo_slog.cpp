@@ -308,15 +308,14 @@ gwo_status Handle::slog_step(int64_t start, int64_t end, uint64_t bound, size_t 
         rcap = G.ring[outb].bytes / (Pout * RW * 8);   // use all of it
         GWO_TRY(ensure_buf(G.bkt[outb], (size_t)Pout * (((size_t)1 << G.cap_log2) / 8)));
         if (emit) GWO_TRY(ensure_output(bound));
-        GWO_TRY(hipcheck(hipMemcpyAsync(G.segdesc.ptr, G.h_segs.data() + s0, (s1 - s0) * sizeof(SlogSeg),
-                                        hipMemcpyHostToDevice, stream), "slog segments"));
         if (fresh)   // R is empty: every partition of the input reads zero entries
             GWO_TRY(hipcheck(hipMemsetAsync(G.cnt[in], 0, ((size_t)1 << lp_in) * 4, stream), "ring reset"));
         SlogArgs a{};
         a.in = SlogRing{(int64_t *)G.ring[in].ptr, G.cnt[in], (uint8_t *)G.bkt[in].ptr, G.rcap[in], lp_in, 0};
         a.out = SlogRing{(int64_t *)G.ring[outb].ptr, G.cnt[outb], (uint8_t *)G.bkt[outb].ptr, rcap, lp_out, 0};
-        a.segs = (const SlogSeg *)G.segdesc.ptr;
+        a.segs = nullptr;
         a.nseg = (int)(s1 - s0);
+        for (size_t i = s0; i < s1; ++i) a.seg[i - s0] = G.h_segs[i];
         a.emit = emit ? 1 : 0;
         a.has_val = needs_value ? 1 : 0;
         a.count_word = S.count_word;

@@ -73,7 +73,11 @@ struct SlogArgs {
     int32_t mode;                 // diagnostics only (GWO_SLOG_MODE, results invalid): 4 no row reservation,
                                   // 8 no R' stores, 16 no row stores
     int32_t emit;                 // 0: an intermediate step of a chunked window step (R' only, no rows)
+    // the step's segment descriptors travel in the kernel arguments (read through the kernarg segment pointer): no
+    // copy from pageable host memory ahead of every window step
+    SlogSeg seg[SLOG_MAX_SEGS];
 };
+static_assert(sizeof(SlogArgs) <= 4096, "kernel arguments are limited to 4 KiB");
 
 #ifndef GWO_SLOG_TABLE_KB
 #define GWO_SLOG_TABLE_KB 32

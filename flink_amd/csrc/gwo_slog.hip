@@ -155,7 +155,18 @@ __global__ __launch_bounds__(SLOG_THREADS) __attribute__((amdgpu_waves_per_eu(4,
                 s_ptr[0] = a.in.rec + (uint64_t)p * a.in.rcap * RW;
                 s_meta[0] = 1 | (NW << 8) | (1 << 12) | (1 << 15);   // SoA columns of rcap words
             } else if (r <= a.nseg) {
-                const SlogSeg sg = a.segs[r - 1];
+                // the descriptor from the kernarg segment (a run-time index into the by-value argument would copy
+                // it into scratch memory)
+                typedef __attribute__((address_space(4))) const SlogArgs KSlogArgs;
+                KSlogArgs *ka = (KSlogArgs *)__builtin_amdgcn_kernarg_segment_ptr();
+                asm volatile("" : "+s"(ka));
+                SlogSeg sg;
+                sg.rec = ka->seg[r - 1].rec;
+                sg.off = ka->seg[r - 1].off;
+                sg.cnt = ka->seg[r - 1].cnt;
+                sg.lp = ka->seg[r - 1].lp;
+                sg.sign = ka->seg[r - 1].sign;
+                sg.fmt = ka->seg[r - 1].fmt;
                 const int d = lp_in - sg.lp;   // >= 0 (the host never gives a finer segment)
                 const uint32_t q = p >> d;
                 c = ((g_u32 *)sg.cnt)[q];
