@@ -25,7 +25,10 @@
 
 namespace gwo {
 
-constexpr int SLOG_J = 4;     // records per thread per pass (the loads of a pass are all in flight together)
+#ifndef GWO_SLOG_J
+#define GWO_SLOG_J 4
+#endif
+constexpr int SLOG_J = GWO_SLOG_J;   // records per thread per pass (the loads of a pass are all in flight together)
 
 typedef __attribute__((address_space(1))) const int64_t g_i64;
 typedef __attribute__((address_space(1))) const uint32_t g_u32;
@@ -95,8 +98,11 @@ __device__ __forceinline__ int slog_find(int64_t *s_key, uint8_t *s_ovf, int NB,
     return -2;
 }
 
+#ifndef GWO_SLOG_WPE
+#define GWO_SLOG_WPE 4   // waves per SIMD the registers are sized for (4: 128 VGPRs, 4 workgroups per CU)
+#endif
 template <int NW>
-__global__ __launch_bounds__(SLOG_THREADS) __attribute__((amdgpu_waves_per_eu(4, 4))) void slog_fire_kernel(SlogArgs a) {
+__global__ __launch_bounds__(SLOG_THREADS) __attribute__((amdgpu_waves_per_eu(GWO_SLOG_WPE, GWO_SLOG_WPE))) void slog_fire_kernel(SlogArgs a) {
     extern __shared__ __attribute__((aligned(16))) int64_t s_dyn[];
     const int T = 1 << a.cap_log2, NB = T >> 3, nbits = a.cap_log2 - 3, SPT = T / SLOG_THREADS;
     int64_t *const s_key = s_dyn;       // [T]
