@@ -32,6 +32,7 @@ struct SlogState {
     bool split_next = false;       // the next window step writes R' at lp + 1
     DevBuf ring[2];                // R (in) and R' (out) alternate
     DevBuf bkt[2];                 // their bucket bytes ([2^lp][nb])
+    DevBuf slot[2];                // their entries' table slots ([2^lp][rcap] uint16: the window step places by them)
     uint32_t *cnt[2] = {nullptr, nullptr};   // [2^LOG_MAX_LP] entries per partition
     uint64_t rcap[2] = {0, 0};
     int rlp[2] = {0, 0};
@@ -135,6 +136,7 @@ void Handle::slog_free() {
     for (int i = 0; i < 2; ++i) {
         G.ring[i].release();
         G.bkt[i].release();
+        G.slot[i].release();
         if (G.cnt[i]) (void)hipFree(G.cnt[i]);
     }
     G.segdesc.release();
@@ -307,12 +309,15 @@ gwo_status Handle::slog_step(int64_t start, int64_t end, uint64_t bound, size_t 
             GWO_TRY(ensure_buf(G.ring[outb], (size_t)((double)(Pout * rcap * RW * 8) * 1.5)));
         rcap = G.ring[outb].bytes / (Pout * RW * 8);   // use all of it
         GWO_TRY(ensure_buf(G.bkt[outb], (size_t)Pout * (((size_t)1 << G.cap_log2) / 8)));
+        GWO_TRY(ensure_buf(G.slot[outb], (size_t)Pout * rcap * 2));
         if (emit) GWO_TRY(ensure_output(bound));
         if (fresh)   // R is empty: every partition of the input reads zero entries
             GWO_TRY(hipcheck(hipMemsetAsync(G.cnt[in], 0, ((size_t)1 << lp_in) * 4, stream), "ring reset"));
         SlogArgs a{};
-        a.in = SlogRing{(int64_t *)G.ring[in].ptr, G.cnt[in], (uint8_t *)G.bkt[in].ptr, G.rcap[in], lp_in, 0};
-        a.out = SlogRing{(int64_t *)G.ring[outb].ptr, G.cnt[outb], (uint8_t *)G.bkt[outb].ptr, rcap, lp_out, 0};
+        a.in = SlogRing{(int64_t *)G.ring[in].ptr, G.cnt[in], (uint8_t *)G.bkt[in].ptr, G.rcap[in], lp_in, 0,
+                        (uint16_t *)G.slot[in].ptr};
+        a.out = SlogRing{(int64_t *)G.ring[outb].ptr, G.cnt[outb], (uint8_t *)G.bkt[outb].ptr, rcap, lp_out, 0,
+                         (uint16_t *)G.slot[outb].ptr};
         a.segs = nullptr;
         a.nseg = (int)(s1 - s0);
         for (size_t i = s0; i < s1; ++i) a.seg[i - s0] = G.h_segs[i];
@@ -363,7 +368,9 @@ gwo_status Handle::slog_step(int64_t start, int64_t end, uint64_t bound, size_t 
                 if (attempt >= 4) return poison(GWO_ERR_CAPACITY, "sliding log: running-total partition overflow");
                 rcap = std::max<uint64_t>(rcap * 2, st[SLS_MAXP] + st[SLS_MAXP] / 4 + 64);
                 GWO_TRY(ensure_buf(G.ring[outb], Pout * rcap * RW * 8));
+                GWO_TRY(ensure_buf(G.slot[outb], (size_t)Pout * rcap * 2));
                 a.out.rec = (int64_t *)G.ring[outb].ptr;
+                a.out.slot = (uint16_t *)G.slot[outb].ptr;
                 a.out.rcap = rcap;
                 *h_scalar = rows0;
                 GWO_TRY(hipcheck(hipMemcpyAsync(d_out_count, h_scalar, 8, hipMemcpyHostToDevice, stream), "row rewind"));

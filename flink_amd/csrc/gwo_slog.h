@@ -46,6 +46,7 @@ struct SlogRing {
     uint64_t rcap;
     int32_t lp;
     int32_t pad;
+    uint16_t *slot;               // GWO_SLOG_SLOTS: slot[q * rcap + i] = entry i's table slot (0xffff: the side entry)
 };
 #define SLOG_UNSTRUCT 0x80000000u
 #define SLOG_MAX_NB 256           // buckets of the LDS table at most (2048 slots)

@@ -98,6 +98,9 @@ __device__ __forceinline__ int slog_find(int64_t *s_key, uint8_t *s_ovf, int NB,
     return -2;
 }
 
+#ifndef GWO_SLOG_SLOTS
+#define GWO_SLOG_SLOTS 1   // R' carries each entry's table slot: the next step places R_p without the bucket bytes
+#endif
 #ifndef GWO_SLOG_WPE
 #define GWO_SLOG_WPE 4   // waves per SIMD the registers are sized for (4: 128 VGPRs, 4 workgroups per CU)
 #endif
@@ -115,8 +118,10 @@ __global__ __launch_bounds__(SLOG_THREADS) __attribute__((amdgpu_waves_per_eu(GW
     __shared__ uint32_t s_beg[SLOG_MAX_SEGS + 2], s_src[SLOG_MAX_SEGS + 1];
     __shared__ int32_t s_meta[SLOG_MAX_SEGS + 1];   // stride | words-to-load << 8 | raw << 12 | filter << 13 | neg << 14
     __shared__ uint8_t s_ovf[SLOG_MAX_NB];          // the fold's overflow flags (R's, and those its inserts set)
+#if !GWO_SLOG_SLOTS
     __shared__ uint8_t s_map[SLOG_MAX_NB * 9];      // R_p entry -> its bucket (a bucket holds <= 8 + the side entry)
     __shared__ uint16_t s_pre[SLOG_MAX_NB];         // first R_p entry of each bucket
+#endif
     __shared__ uint8_t s_ovo[2][SLOG_MAX_NB];       // R''s, recomputed from the keys' displacement by the sweep
     __shared__ unsigned s_wsum[SLOG_THREADS / 64];
     __shared__ unsigned s_qn[2];          // R' entries written so far for the partition's (one or two) outputs
@@ -135,6 +140,7 @@ __global__ __launch_bounds__(SLOG_THREADS) __attribute__((amdgpu_waves_per_eu(GW
     if (tid < SLOG_MAX_NB) {
         s_ovo[0][tid] = 0;
         s_ovo[1][tid] = 0;
+        s_ovf[tid] = 0;
     }
     if (tid == 0) {
         s_used = 0;
@@ -213,6 +219,56 @@ __global__ __launch_bounds__(SLOG_THREADS) __attribute__((amdgpu_waves_per_eu(GW
                 return !ranged || (sub >= lo && sub < hi);
             };
             unsigned claims = 0;
+#if GWO_SLOG_SLOTS
+            // ---- R_p placed (structured): every entry at the table slot it had (R''s slot column), thread t loads
+            // entries t, t + 256, ... (coalesced SoA columns); the overflow flags are rebuilt from the entries' own
+            // displacement (every bucket from a key's home to its slot's bucket was full when it was claimed) --
+            // one round trip, no bucket bytes, scan or map ----
+            {
+                const uint32_t rcount = structured ? (s_rn & ~SLOG_UNSTRUCT) : 0u;
+                const int64_t *col = a.in.rec + (uint64_t)p * a.in.rcap * RW;   // keys[rcap], then each word's column
+                const uint16_t *scol = a.in.slot + (uint64_t)p * a.in.rcap;
+                unsigned placed = 0;
+                for (uint32_t base = 0; base < rcount; base += SLOG_THREADS * 4) {
+                    int64_t ek[4], ew[4][NW];
+                    uint32_t es[4];
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const uint32_t i = base + j * SLOG_THREADS + tid;
+                        ek[j] = 0;
+                        es[j] = 0xffffu;
+#pragma unroll
+                        for (int w = 0; w < NW; ++w) ew[j][w] = 0;
+                        if (i >= rcount) continue;
+                        ek[j] = __builtin_nontemporal_load((g_i64 *)col + i);
+                        es[j] = scol[i];
+#pragma unroll
+                        for (int w = 0; w < NW; ++w)
+                            ew[j][w] = __builtin_nontemporal_load((g_i64 *)col + (uint64_t)(1 + w) * a.in.rcap + i);
+                    }
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const uint32_t i = base + j * SLOG_THREADS + tid;
+                        if (i >= rcount || !in_range(ek[j])) continue;
+                        if (ek[j] == GWO_EMPTY_KEY) {   // Long.MIN_VALUE: the side slot
+                            s_side[0] = 1;
+#pragma unroll
+                            for (int w = 0; w < NW; ++w) s_side[1 + w] = ew[j][w];
+                            continue;
+                        }
+                        const int sl = (int)(es[j] & (uint32_t)(T - 1));
+                        const int slot = slot_lds(sl);
+                        s_key[slot] = ek[j];
+#pragma unroll
+                        for (int w = 0; w < NW; ++w) s_w[w * T + slot] = ew[j][w];
+                        const int bs = sl >> 3;
+                        for (int bb = (int)slog_bucket(ek[j], nbits); bb != bs; bb = (bb + 1) & (NB - 1)) s_ovf[bb] = 1;
+                        placed++;
+                    }
+                }
+                claims += placed;
+            }
+#else
             // ---- R_p placed into its buckets (structured): the bucket bytes give each entry's bucket (an LDS map
             // entry -> bucket), then thread t loads entries t, t + 256, ... -- coalesced SoA columns ----
             {
@@ -274,6 +330,7 @@ __global__ __launch_bounds__(SLOG_THREADS) __attribute__((amdgpu_waves_per_eu(GW
                 }
                 claims += placed;
             }
+#endif
             __syncthreads();
             stamp(2);
             // ---- fold: the segments' records (and R_p when unstructured), SLOG_J per thread, loads in flight ----
@@ -345,6 +402,7 @@ __global__ __launch_bounds__(SLOG_THREADS) __attribute__((amdgpu_waves_per_eu(GW
                 for (int i = tid; i < T; i += SLOG_THREADS) s_key[i] = GWO_EMPTY_KEY;
                 for (int i = tid; i < T * NW; i += SLOG_THREADS) s_w[i] = 0;
                 if (tid <= GWO_MAX_WORDS) s_side[tid] = 0;
+                if (GWO_SLOG_SLOTS && tid < NB) s_ovf[tid] = 0;
                 if (tid == 0) {
                     s_used = 0;
                     s_fail = 0;
@@ -422,7 +480,7 @@ __global__ __launch_bounds__(SLOG_THREADS) __attribute__((amdgpu_waves_per_eu(GW
             const uint32_t qb0 = s_qn[0], qb1 = s_qn[1];
             const uint32_t qout0 = split ? 2 * p : p;
             // R''s bucket bytes: the first thread of each bucket sums the bucket's threads (consecutive lanes)
-            if (out_struct) {
+            if (out_struct && !GWO_SLOG_SLOTS) {
                 uint32_t bc = v;
                 for (int o = 1; o < 8 / SPT; o <<= 1) bc += __shfl_xor(bc, o);
                 if (((tid * SPT) & 7) == 0) {
@@ -434,19 +492,20 @@ __global__ __launch_bounds__(SLOG_THREADS) __attribute__((amdgpu_waves_per_eu(GW
             // pass A: R' (needs no row base), while thread 0's row reservation is in flight
             {
                 uint32_t at0 = ex & 0xffffu, at1 = ex >> 16;
-                auto put = [&](int64_t k, const int64_t *wp, int ws, uint32_t half) {
+                auto put = [&](int64_t k, const int64_t *wp, int ws, uint32_t half, uint32_t lslot) {
                     const uint32_t qpos = (half ? qb1 + at1++ : qb0 + at0++);
                     if (qpos >= a.out.rcap || (a.mode & 8)) return;
                     int64_t *col = a.out.rec + (uint64_t)(qout0 + half) * a.out.rcap * RW;   // SoA columns
                     col[qpos] = k;
+                    if (GWO_SLOG_SLOTS) a.out.slot[(uint64_t)(qout0 + half) * a.out.rcap + qpos] = (uint16_t)lslot;
 #pragma unroll
                     for (int w = 0; w < NW; ++w) col[(uint64_t)(1 + w) * a.out.rcap + qpos] = wp[w * ws];
                 };
-                if (side_live) put(GWO_EMPTY_KEY, s_side + 1, 1, side_half);
+                if (side_live) put(GWO_EMPTY_KEY, s_side + 1, 1, side_half, 0xffffu);
                 for (int i = 0; i < SPT; ++i) {
                     if (!((code >> (2 * i)) & 1u)) continue;
                     const int sl = slot_lds(tid * SPT + i);
-                    put(s_key[sl], s_w + sl, T, (code >> (2 * i + 1)) & 1u);
+                    put(s_key[sl], s_w + sl, T, (code >> (2 * i + 1)) & 1u, (uint32_t)(tid * SPT + i));
                 }
             }
             __syncthreads();   // s_rowbase is published; every read of s_qn and s_ovo is done
@@ -498,6 +557,7 @@ __global__ __launch_bounds__(SLOG_THREADS) __attribute__((amdgpu_waves_per_eu(GW
             if (tid < NB) {
                 s_ovo[0][tid] = 0;
                 s_ovo[1][tid] = 0;
+                if (GWO_SLOG_SLOTS) s_ovf[tid] = 0;
             }
             stamp(4);
             __syncthreads();
