@@ -85,21 +85,10 @@ static_assert(sizeof(SlogArgs) <= 4096, "kernel arguments are limited to 4 KiB")
 #endif
 // log2 of the window step's LDS table slots for nwords accumulator words: the largest of 2^9..2^11 whose table fits
 // GWO_SLOG_TABLE_KB KiB (32: about five workgroups share a CU and overlap their partitions' HBM round trips)
-#ifndef GWO_SLOG_BIG
-#define GWO_SLOG_BIG 1
-#endif
-// GWO_SLOG_BIG: a table of 2048 slots up to 64 KiB (1 to 3 words) instead of a smaller one, run by 512-thread
-// workgroups, 2 per CU when it exceeds GWO_SLOG_TABLE_KB (the same 16 waves per CU, half the partitions)
 constexpr int slog_cap_log2_for(int nwords) {
-    if (GWO_SLOG_BIG && 2048LL * (1 + nwords) * 8 <= 64 * 1024) return 11;
     int c = 11;
     while (c > 9 && ((long long)1 << c) * (long long)(1 + nwords) * 8 > GWO_SLOG_TABLE_KB * 1024) c--;
     return c;
-}
-
-// threads of the window step's workgroup for nwords words: 512 for a table above GWO_SLOG_TABLE_KB, else SLOG_THREADS
-constexpr int slog_threads_for(int nwords) {
-    return ((1LL << slog_cap_log2_for(nwords)) * (1 + nwords) * 8 > GWO_SLOG_TABLE_KB * 1024) ? 512 : SLOG_THREADS;
 }
 
 namespace gwo {

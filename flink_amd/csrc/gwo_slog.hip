@@ -105,10 +105,9 @@ __device__ __forceinline__ int slog_find(int64_t *s_key, uint8_t *s_ovf, int NB,
 #define GWO_SLOG_WPE 4   // waves per SIMD the registers are sized for (4: 128 VGPRs, 4 workgroups per CU)
 #endif
 template <int NW>
-__global__ __launch_bounds__(slog_threads_for(NW)) __attribute__((amdgpu_waves_per_eu(GWO_SLOG_WPE, GWO_SLOG_WPE))) void slog_fire_kernel(SlogArgs a) {
-    constexpr int TH = slog_threads_for(NW);
+__global__ __launch_bounds__(SLOG_THREADS) __attribute__((amdgpu_waves_per_eu(GWO_SLOG_WPE, GWO_SLOG_WPE))) void slog_fire_kernel(SlogArgs a) {
     extern __shared__ __attribute__((aligned(16))) int64_t s_dyn[];
-    const int T = 1 << a.cap_log2, NB = T >> 3, nbits = a.cap_log2 - 3, SPT = T / TH;
+    const int T = 1 << a.cap_log2, NB = T >> 3, nbits = a.cap_log2 - 3, SPT = T / SLOG_THREADS;
     int64_t *const s_key = s_dyn;       // [T]
     int64_t *const s_w = s_dyn + T;     // [NW][T]
     __shared__ int64_t s_side[1 + GWO_MAX_WORDS];   // key == Long.MIN_VALUE: [present, words]
@@ -124,7 +123,7 @@ __global__ __launch_bounds__(slog_threads_for(NW)) __attribute__((amdgpu_waves_p
     __shared__ uint16_t s_pre[SLOG_MAX_NB];         // first R_p entry of each bucket
 #endif
     __shared__ uint8_t s_ovo[2][SLOG_MAX_NB];       // R''s, recomputed from the keys' displacement by the sweep
-    __shared__ unsigned s_wsum[TH / 64];
+    __shared__ unsigned s_wsum[SLOG_THREADS / 64];
     __shared__ unsigned s_qn[2];          // R' entries written so far for the partition's (one or two) outputs
     __shared__ unsigned long long s_rowbase;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -135,8 +134,8 @@ __global__ __launch_bounds__(slog_threads_for(NW)) __attribute__((amdgpu_waves_p
     const int side_bucket = (int)slog_bucket(GWO_EMPTY_KEY, nbits);
     unsigned long long st_live = 0, st_maxp = 0, st_rovf = 0, st_neg = 0, st_lds = 0, st_slow = 0;
 
-    for (int i = tid; i < T; i += TH) s_key[i] = GWO_EMPTY_KEY;
-    for (int i = tid; i < T * NW; i += TH) s_w[i] = 0;
+    for (int i = tid; i < T; i += SLOG_THREADS) s_key[i] = GWO_EMPTY_KEY;
+    for (int i = tid; i < T * NW; i += SLOG_THREADS) s_w[i] = 0;
     if (tid <= GWO_MAX_WORDS) s_side[tid] = 0;
     if (tid < SLOG_MAX_NB) {
         s_ovo[0][tid] = 0;
@@ -230,12 +229,12 @@ __global__ __launch_bounds__(slog_threads_for(NW)) __attribute__((amdgpu_waves_p
                 const int64_t *col = a.in.rec + (uint64_t)p * a.in.rcap * RW;   // keys[rcap], then each word's column
                 const uint16_t *scol = a.in.slot + (uint64_t)p * a.in.rcap;
                 unsigned placed = 0;
-                for (uint32_t base = 0; base < rcount; base += TH * 4) {
+                for (uint32_t base = 0; base < rcount; base += SLOG_THREADS * 4) {
                     int64_t ek[4], ew[4][NW];
                     uint32_t es[4];
 #pragma unroll
                     for (int j = 0; j < 4; ++j) {
-                        const uint32_t i = base + j * TH + tid;
+                        const uint32_t i = base + j * SLOG_THREADS + tid;
                         ek[j] = 0;
                         es[j] = 0xffffu;
 #pragma unroll
@@ -249,7 +248,7 @@ __global__ __launch_bounds__(slog_threads_for(NW)) __attribute__((amdgpu_waves_p
                     }
 #pragma unroll
                     for (int j = 0; j < 4; ++j) {
-                        const uint32_t i = base + j * TH + tid;
+                        const uint32_t i = base + j * SLOG_THREADS + tid;
                         if (i >= rcount || !in_range(ek[j])) continue;
                         if (ek[j] == GWO_EMPTY_KEY) {   // Long.MIN_VALUE: the side slot
                             s_side[0] = 1;
@@ -297,11 +296,11 @@ __global__ __launch_bounds__(slog_threads_for(NW)) __attribute__((amdgpu_waves_p
                 __syncthreads();
                 const int64_t *col = a.in.rec + (uint64_t)p * a.in.rcap * RW;   // keys[rcap], then each word's column
                 unsigned placed = 0;
-                for (uint32_t base = 0; base < rcount; base += TH * 4) {
+                for (uint32_t base = 0; base < rcount; base += SLOG_THREADS * 4) {
                     int64_t ek[4], ew[4][NW];
 #pragma unroll
                     for (int j = 0; j < 4; ++j) {
-                        const uint32_t i = base + j * TH + tid;
+                        const uint32_t i = base + j * SLOG_THREADS + tid;
                         ek[j] = 0;
 #pragma unroll
                         for (int w = 0; w < NW; ++w) ew[j][w] = 0;
@@ -313,7 +312,7 @@ __global__ __launch_bounds__(slog_threads_for(NW)) __attribute__((amdgpu_waves_p
                     }
 #pragma unroll
                     for (int j = 0; j < 4; ++j) {
-                        const uint32_t i = base + j * TH + tid;
+                        const uint32_t i = base + j * SLOG_THREADS + tid;
                         if (i >= rcount || !in_range(ek[j])) continue;
                         if (ek[j] == GWO_EMPTY_KEY) {   // Long.MIN_VALUE: the side slot
                             s_side[0] = 1;
@@ -335,7 +334,7 @@ __global__ __launch_bounds__(slog_threads_for(NW)) __attribute__((amdgpu_waves_p
             __syncthreads();
             stamp(2);
             // ---- fold: the segments' records (and R_p when unstructured), SLOG_J per thread, loads in flight ----
-            for (uint32_t base = 0; base < total; base += TH * SLOG_J) {
+            for (uint32_t base = 0; base < total; base += SLOG_THREADS * SLOG_J) {
                 int64_t rk[SLOG_J], rw[SLOG_J][NW];
                 int rr[SLOG_J];
                 // every record's range and address first (LDS only), then every load: global (not flat) loads,
@@ -344,7 +343,7 @@ __global__ __launch_bounds__(slog_threads_for(NW)) __attribute__((amdgpu_waves_p
                 int nlj[SLOG_J];
 #pragma unroll
                 for (int j = 0; j < SLOG_J; ++j) {
-                    const uint32_t i = base + j * TH + tid;
+                    const uint32_t i = base + j * SLOG_THREADS + tid;
                     rr[j] = -1;
                     ea[j] = s_ptr[0];
                     nlj[j] = 0;
@@ -400,8 +399,8 @@ __global__ __launch_bounds__(slog_threads_for(NW)) __attribute__((amdgpu_waves_p
             __syncthreads();
             stamp(3);
             if (failed) {   // more keys in range than the table holds: reset, halve the range
-                for (int i = tid; i < T; i += TH) s_key[i] = GWO_EMPTY_KEY;
-                for (int i = tid; i < T * NW; i += TH) s_w[i] = 0;
+                for (int i = tid; i < T; i += SLOG_THREADS) s_key[i] = GWO_EMPTY_KEY;
+                for (int i = tid; i < T * NW; i += SLOG_THREADS) s_w[i] = 0;
                 if (tid <= GWO_MAX_WORDS) s_side[tid] = 0;
                 if (GWO_SLOG_SLOTS && tid < NB) s_ovf[tid] = 0;
                 if (tid == 0) {
@@ -468,7 +467,7 @@ __global__ __launch_bounds__(slog_threads_for(NW)) __attribute__((amdgpu_waves_p
             stamp(6);
             uint32_t pre = 0, tot = 0;
 #pragma unroll
-            for (int w = 0; w < TH / 64; ++w) {
+            for (int w = 0; w < SLOG_THREADS / 64; ++w) {
                 const uint32_t x = s_wsum[w];
                 pre += w < wave ? x : 0u;
                 tot += x;
@@ -624,13 +623,13 @@ void launch_slog_fire(const SlogArgs &a, int cus, hipStream_t s) {
     case NW: {                                                                                          \
         static int occ[16] = {};                                                                        \
         int &per_cu = occ[a.cap_log2 & 15];                                                             \
-        if (!per_cu && hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, slog_fire_kernel<NW>, slog_threads_for(NW), \
+        if (!per_cu && hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, slog_fire_kernel<NW>, SLOG_THREADS, \
                                                                     lds) != hipSuccess)                \
             per_cu = 1;                                                                                 \
         if (per_cu < 1) per_cu = 1;                                                                     \
         const uint32_t groups = (uint32_t)cus * (uint32_t)per_cu;                                       \
         const int grid = (int)(P < groups ? P : groups);                                                \
-        hipLaunchKernelGGL(slog_fire_kernel<NW>, dim3(grid), dim3(slog_threads_for(NW)), lds, s, a);             \
+        hipLaunchKernelGGL(slog_fire_kernel<NW>, dim3(grid), dim3(SLOG_THREADS), lds, s, a);             \
         break;                                                                                          \
     }
     switch (a.p.nwords) {
