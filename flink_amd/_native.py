@@ -85,6 +85,7 @@ SIGNATURES = [
     ("gwo_create", C.c_int, [C.POINTER(GwoConfig), C.POINTER(_P)]),
     ("gwo_destroy", C.c_int, [_P]),
     ("gwo_submit", C.c_int, [_P, _P, _P, _P, C.c_int64]),
+    ("gwo_wait_stream", C.c_int, [_P, _P]),
     ("gwo_host_register", C.c_int, [_P, C.c_int64]),
     ("gwo_host_unregister", C.c_int, [_P]),
     ("gwo_submit_utf16", C.c_int, [_P, _P, _P, _P, _P, C.c_int64]),

@@ -780,7 +780,8 @@ extern "C" gwo_status gwo_partition_by_operator(const int64_t *key, const int64_
         return GWO_ERR_INVALID_ARGUMENT;
     DeviceGuard guard_(device);
     hipStream_t s;
-    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return GWO_ERR_HIP;
+    // a blocking stream: ordered behind the null stream's work (a producer there needs no host sync, gwo.h)
+    if (hipStreamCreate(&s) != hipSuccess) return GWO_ERR_HIP;
     const size_t nb = (size_t)n * 8 + 8, ob = (size_t)parallelism * cap * 24 + 24;
     void *dk = nullptr, *dt = nullptr, *dv = nullptr, *dout = nullptr, *dcur = nullptr, *dcnt = nullptr;
     gwo_status st = GWO_OK;

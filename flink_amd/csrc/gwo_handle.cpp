@@ -238,6 +238,7 @@ Handle::~Handle() {
     if (ev_main) (void)hipEventDestroy(ev_main);
     if (ev_fire) (void)hipEventDestroy(ev_fire);
     if (ev_out) (void)hipEventDestroy(ev_out);
+    if (ev_input) (void)hipEventDestroy(ev_input);
     if (h_out_cnt) (void)hipHostFree(h_out_cnt);
 }
 

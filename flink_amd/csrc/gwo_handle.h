@@ -153,6 +153,7 @@ struct Handle {
     bool out_stale = false, discard_stale = false;
     unsigned long long *h_out_cnt = nullptr;   // pinned
     hipEvent_t ev_out = nullptr;
+    hipEvent_t ev_input = nullptr;             // gwo_wait_stream: the producer stream's work so far
     unsigned long long zero_u64 = 0;
     unsigned long long *h_scalar = nullptr;    // pinned scalar staging
     int64_t *h_ident_side = nullptr;           // pinned [0, identity words...] side-slot image

@@ -245,6 +245,7 @@ gwo_status Handle::log_split_exact(long long base, int nunits, uint64_t cap, con
                 GWO_TRY(log_carve(Wn, ((size_t)1 << lp) * 4, &p));
                 d.cnt = (uint32_t *)p;
                 d.lp = lp;
+                d.nrec = (uint32_t)seg;
                 GWO_TRY(hipcheck(hipMemsetAsync(d.cnt, 0, ((size_t)1 << lp) * 4, stream), "segment counts"));
             } else {
                 for (int dgt = 0; dgt < LOG_ND; ++dgt) {
@@ -304,6 +305,7 @@ gwo_status Handle::log_commit_spec(LogJob &J, const unsigned long long *rbp) {
     for (int w = 0; w < J.nunits; ++w) {
         if (!wcount[w]) continue;
         LogWindow &Wn = L.wins[J.base + w];
+        J.desc[w].nrec = (uint32_t)std::min<uint64_t>(rbp[LOG_RB_SEG + w], J.seg_cap[w]);   // the device plan's size
         Wn.segs.push_back(J.desc[w]);
         Wn.records += wcount[w];
     }
@@ -327,6 +329,7 @@ gwo_status Handle::log_split_dev(const LogJob &J, const unsigned long long *rbp)
         char *p = nullptr;
         GWO_TRY(log_carve(L.wins[J.base + w], seg * W * 8, &p));
         set.s[w].rec = (int64_t *)p;
+        set.s[w].nrec = (uint32_t)seg;
         total += wcount[w];
     }
     L.h_split_flag[J.slot] = 0;
@@ -1118,7 +1121,7 @@ gwo_status Handle::log_restore_rows(const RestoreRows &R, int64_t new_wm) {
         GWO_TRY(hipcheck(hipMemcpy(p_rec, rec.data(), rec.size() * 8, hipMemcpyHostToDevice), "restore records"));
         GWO_TRY(hipcheck(hipMemcpy(p_off, off.data(), (size_t)F * 4, hipMemcpyHostToDevice), "restore offsets"));
         GWO_TRY(hipcheck(hipMemcpy(p_cnt, cnt.data(), (size_t)F * 4, hipMemcpyHostToDevice), "restore counts"));
-        W.partial = LogSegDesc{(int64_t *)p_rec, (uint32_t *)p_off, (uint32_t *)p_cnt, W.lp, 0};
+        W.partial = LogSegDesc{(int64_t *)p_rec, (uint32_t *)p_off, (uint32_t *)p_cnt, W.lp, (uint32_t)ix.size()};
         W.partial_rows = ix.size();
     }
     return slog ? slog_anchor() : GWO_OK;

@@ -60,7 +60,7 @@ struct LogSegDesc {
     uint32_t *off;               // 2^lp start offsets (in records)
     uint32_t *cnt;               // 2^lp record counts (atomic cursors while pass 2 runs)
     int32_t lp;
-    int32_t pad;
+    uint32_t nrec;               // records carved for the segment (every partition's run lies inside them)
 };
 
 // Pass-2 work description of one coarse bucket b (window w of the launch, coarse digit d).  The bucket's

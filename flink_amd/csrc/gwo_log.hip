@@ -861,7 +861,9 @@ __global__ __launch_bounds__(LOG_TILE_THREADS) void log_split_kernel(const int64
         int f = tid * per + q;
         if (q < per && f < F && loc[q]) {
             uint32_t at = atomicAdd(&S.cnt[d * F + f], loc[q]);
-            if (at + loc[q] > B.pcap) *(volatile unsigned *)overflow = 1u;   // host-visible flag, plain store
+            // host-mapped flag: a system-scope store (write-through, no cache between it and the host), issued before
+            // the kernel ends -- the host reads it after a later readback in stream order (log_resolve_split)
+            if (at + loc[q] > B.pcap) __hip_atomic_store(overflow, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             s_cnt[f] = at;
         }
     }

@@ -1432,6 +1432,16 @@ gwo_status gwo_host_unregister(void *ptr) {
     return GWO_OK;
 }
 
+// Device input produced on another stream: the handle's stream waits (on the device) for the work queued there so
+// far.  Without it a producer on a different stream races K1, whose stream is non-blocking (gwo.h "Buffers").
+gwo_status gwo_wait_stream(gwo_handle *hh, void *producer) {
+    H_OR_FAIL;
+    if ((hipStream_t)producer == h->stream) return GWO_OK;
+    if (!h->ev_input) GWO_TRY(h->hipcheck(hipEventCreateWithFlags(&h->ev_input, hipEventDisableTiming), "event"));
+    GWO_TRY(h->hipcheck(hipEventRecord(h->ev_input, (hipStream_t)producer), "wait_stream record"));
+    return h->hipcheck(hipStreamWaitEvent(h->stream, h->ev_input, 0), "wait_stream");
+}
+
 gwo_status gwo_get_stream(gwo_handle *hh, void **stream) {
     Handle *h = reinterpret_cast<Handle *>(hh);
     if (!h || !stream) return GWO_ERR_INVALID_ARGUMENT;
@@ -1490,7 +1500,8 @@ static gwo_status stateless_run(int32_t device, size_t n, const void *in, size_t
                                 void (*body)(const int64_t *, void **, hipStream_t, void *), void *ctx) {
     DeviceGuard guard_(device);
     hipStream_t s;
-    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return GWO_ERR_HIP;
+    // a blocking stream: ordered behind the null stream's work (a producer there needs no host sync, gwo.h)
+    if (hipStreamCreate(&s) != hipSuccess) return GWO_ERR_HIP;
     gwo_status st = GWO_OK;
     const int64_t *din = (const int64_t *)in;
     void *tmp_in = nullptr;
@@ -1552,7 +1563,8 @@ gwo_status gwo_assign_key_groups_utf16(const uint16_t *chars, const int64_t *off
     if (n == 0) return GWO_OK;
     DeviceGuard guard_(device);
     hipStream_t s;
-    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return GWO_ERR_HIP;
+    // a blocking stream: ordered behind the null stream's work (a producer there needs no host sync, gwo.h)
+    if (hipStreamCreate(&s) != hipSuccess) return GWO_ERR_HIP;
     gwo_status st = GWO_OK;
     std::vector<void *> owned;
     auto dev_alloc = [&](size_t bytes) -> void * {

@@ -213,7 +213,7 @@ gwo_status Handle::slog_rwin_add(long long j, const std::vector<int64_t> &key, c
     GWO_TRY(hipcheck(hipMemcpy(p_rec, rec.data(), rec.size() * 8, hipMemcpyHostToDevice), "restore records"));
     GWO_TRY(hipcheck(hipMemcpy(p_off, off.data(), (size_t)F * 4, hipMemcpyHostToDevice), "restore offsets"));
     GWO_TRY(hipcheck(hipMemcpy(p_cnt, cnt.data(), (size_t)F * 4, hipMemcpyHostToDevice), "restore counts"));
-    W.partial = LogSegDesc{(int64_t *)p_rec, (uint32_t *)p_off, (uint32_t *)p_cnt, W.lp, 0};
+    W.partial = LogSegDesc{(int64_t *)p_rec, (uint32_t *)p_off, (uint32_t *)p_cnt, W.lp, (uint32_t)rows.size()};
     W.partial_rows = rows.size();
     return GWO_OK;
 }
@@ -339,9 +339,24 @@ gwo_status Handle::slog_step(int64_t start, int64_t end, uint64_t bound, size_t 
         a.dbg = trace ? d_dbg : nullptr;
         static int mode = getenv("GWO_SLOG_MODE") ? atoi(getenv("GWO_SLOG_MODE")) : 0;
         a.mode = mode;
+#if GWO_SLOG_CHECK
+        static unsigned long long *h_viol = nullptr, *d_viol = nullptr;
+        if (!h_viol) {
+            GWO_TRY(hipcheck(hipHostMalloc((void **)&h_viol, 8 * 8, hipHostMallocCoherent | hipHostMallocMapped), "check"));
+            memset(h_viol, 0, 8 * 8);
+            GWO_TRY(hipcheck(hipHostGetDevicePointer((void **)&d_viol, h_viol, 0), "check"));
+        }
+        a.chk.viol = d_viol;
+#endif
         const uint64_t rows0 = out_rows;
         for (int attempt = 0;; ++attempt) {
             a.o = out_cols();
+#if GWO_SLOG_CHECK
+            a.chk.in_rec = G.ring[in].bytes / 8;
+            a.chk.in_slot = G.slot[in].bytes / 2;
+            a.chk.out_rec = G.ring[outb].bytes / 8;
+            a.chk.out_slot = G.slot[outb].bytes / 2;
+#endif
             // (the statistics shards are zero: reset at creation and by every step's publish)
             prof_begin(GWO_KERNEL_FIRE);
             launch_slog_fire(a, G.groups, stream);
@@ -352,6 +367,16 @@ gwo_status Handle::slog_step(int64_t start, int64_t end, uint64_t bound, size_t 
             GWO_TRY(spin_seq(G.rb + SLS_WORDS, G.rb_seq, "slog window step"));
             uint64_t st[SLS_WORDS] = {};
             for (int w = 0; w < SLS_WORDS; ++w) st[w] = G.rb[w];
+#if GWO_SLOG_CHECK
+            if (h_viol[0]) {
+                fprintf(stderr, "[slog-check] window %lld attempt %d: %llu violations; first: what=%llu partition=%llu "
+                                "index=%llu bound=%llu width=%llu lp %llu->%llu (in rcap %llu, out rcap %llu, segs %d, fresh %d)\n",
+                        (long long)start, attempt, h_viol[0], h_viol[1], h_viol[2], h_viol[3], h_viol[4], h_viol[5],
+                        h_viol[6], h_viol[7], (unsigned long long)a.in.rcap, (unsigned long long)a.out.rcap, a.nseg,
+                        (int)fresh);
+                memset(h_viol, 0, 8 * 8);
+            }
+#endif
             if (L.pend.active) {   // queued behind a pass 2 not checked yet (fire_slog): it completed before this step
                 if (L.h_split_flag[L.pend.tmpx] != 0) {   // it overflowed: this step read an incomplete segment
                     *h_scalar = rows0;
@@ -420,6 +445,10 @@ gwo_status Handle::slog_step(int64_t start, int64_t end, uint64_t bound, size_t 
             break;
         }
         if (emit) out_rows = rows0 + G.live;
+        if ((long long)out_rows > out.cap)   // never hand out rows past the output columns (a drain would read them)
+            return poison(GWO_ERR_HIP, ("sliding log: " + std::to_string(out_rows) + " rows exceed the output capacity " +
+                                        std::to_string(out.cap) + " (window step bound " + std::to_string(bound) + ")")
+                                           .c_str());
         G.cur = outb;
         G.rcap[outb] = rcap;
         G.rlp[outb] = lp_out;
@@ -451,9 +480,9 @@ gwo_status Handle::fire_slog(int64_t new_wm) {
         uint64_t plus_records = 0;
         std::vector<long long> leaving;
         auto add_pane = [&](LogWindow &W, int sign) {
-            for (auto &d : W.segs) G.h_segs.push_back(SlogSeg{d.rec, d.off, d.cnt, d.lp, sign, 0, 0});
+            for (auto &d : W.segs) G.h_segs.push_back(SlogSeg{d.rec, d.off, d.cnt, d.lp, sign, 0, d.nrec});
             if (W.partial.rec)
-                G.h_segs.push_back(SlogSeg{W.partial.rec, W.partial.off, W.partial.cnt, W.partial.lp, sign, 1, 0});
+                G.h_segs.push_back(SlogSeg{W.partial.rec, W.partial.off, W.partial.cnt, W.partial.lp, sign, 1, W.partial.nrec});
             if (sign > 0) plus_records += W.records + W.partial_rows;
         };
         auto add_restored = [&](__int128 j, int sign) {   // a restored window's entries: in R for its own step only
@@ -491,7 +520,7 @@ gwo_status Handle::fire_slog(int64_t new_wm) {
                 auto jt = L.wins.find(pe.first);
                 if (jt == L.wins.end() || pe.second >= jt->second.segs.size()) continue;
                 const LogSegDesc &d = jt->second.segs[pe.second];
-                G.h_segs.push_back(SlogSeg{d.rec, d.off, d.cnt, d.lp, +1, 0, 0});
+                G.h_segs.push_back(SlogSeg{d.rec, d.off, d.cnt, d.lp, +1, 0, d.nrec});
             }
             plus_records += G.pending_records;
             for (auto jt = L.wins.lower_bound(plo); jt != L.wins.end() && jt->first < lo; ++jt) {

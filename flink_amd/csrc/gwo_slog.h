@@ -30,7 +30,9 @@ struct SlogSeg {
     int32_t lp;
     int32_t sign;                 // +1: the pane enters the window, -1: it leaves
     int32_t fmt;                  // 0: value records (has_val: key, value; else key), 1: key + nwords raw words
-    int32_t pad;
+    uint32_t nrec;                // records carved for the segment (0: unknown): a partition's run is clamped to it,
+                                  // so a step queued speculatively behind a pass 2 whose partition overflowed (its
+                                  // count is then the uncapped cursor; the step is redone) never reads past the carve
 };
 
 // The running total: partition q holds cnt[q] entries in the region rec[q * rcap * (1 + nwords)] as SoA columns
@@ -55,6 +57,20 @@ struct SlogRing {
 // count (an inconsistent leave), LDS table overflow, partitions that took the range rounds.
 enum : int { SLS_LIVE = 0, SLS_MAXP, SLS_ROVF, SLS_NEG, SLS_LDS, SLS_SLOW, SLS_WORDS };
 
+#ifndef GWO_SLOG_CHECK
+#define GWO_SLOG_CHECK 0          // 1: a diagnostic build -- every HBM access of the window step is checked against
+                                  // the host's allocation sizes; a violation is recorded (and skipped), not made
+#endif
+#if GWO_SLOG_CHECK
+// Allocation sizes (int64 / uint16 elements) and the first violation: viol[0] = count, viol[1..7] = what, partition,
+// index, bound, round width, in lp, out lp.
+struct SlogCheck {
+    uint64_t in_rec, in_slot, out_rec, out_slot;
+    unsigned long long *viol;
+};
+enum : int { SLC_IN_REC = 1, SLC_IN_SLOT, SLC_SLOT_RANGE, SLC_SEG_CNT, SLC_SEG_REC, SLC_OUT_REC, SLC_OUT_SLOT, SLC_PART };
+#endif
+
 struct SlogArgs {
     SlogRing in, out;             // out.lp == in.lp (same partitions) or in.lp + 1 (each partition splits in two)
     const SlogSeg *segs;
@@ -77,18 +93,29 @@ struct SlogArgs {
     // the step's segment descriptors travel in the kernel arguments (read through the kernarg segment pointer): no
     // copy from pageable host memory ahead of every window step
     SlogSeg seg[SLOG_MAX_SEGS];
+#if GWO_SLOG_CHECK
+    SlogCheck chk;
+#endif
 };
 static_assert(sizeof(SlogArgs) <= 4096, "kernel arguments are limited to 4 KiB");
 
 #ifndef GWO_SLOG_TABLE_KB
 #define GWO_SLOG_TABLE_KB 32
 #endif
+#ifndef GWO_SLOG_BIG
+#define GWO_SLOG_BIG 0            // 1: 2048-slot tables up to 64 KiB run by 512-thread workgroups (r05 experiment, off)
+#endif
 // log2 of the window step's LDS table slots for nwords accumulator words: the largest of 2^9..2^11 whose table fits
 // GWO_SLOG_TABLE_KB KiB (32: about five workgroups share a CU and overlap their partitions' HBM round trips)
 constexpr int slog_cap_log2_for(int nwords) {
+    if (GWO_SLOG_BIG && 2048LL * (1 + nwords) * 8 <= 64 * 1024) return 11;
     int c = 11;
     while (c > 9 && ((long long)1 << c) * (long long)(1 + nwords) * 8 > GWO_SLOG_TABLE_KB * 1024) c--;
     return c;
+}
+// threads of the window step's workgroup: 512 for a table above GWO_SLOG_TABLE_KB (GWO_SLOG_BIG), else SLOG_THREADS
+constexpr int slog_threads_for(int nwords) {
+    return ((1LL << slog_cap_log2_for(nwords)) * (1 + nwords) * 8 > GWO_SLOG_TABLE_KB * 1024) ? 512 : SLOG_THREADS;
 }
 
 namespace gwo {

@@ -98,6 +98,26 @@ __device__ __forceinline__ int slog_find(int64_t *s_key, uint8_t *s_ovf, int NB,
     return -2;
 }
 
+#if GWO_SLOG_CHECK
+// The diagnostic build's violation record (gwo_slog.h SlogCheck): the first one's details, every one counted.
+__device__ __noinline__ void slog_violation(unsigned long long *v, int what, uint64_t p, uint64_t idx, uint64_t bound,
+                                            uint64_t width, int lp_in, int lp_out) {
+    if (atomicAdd(&v[0], 1ull) == 0ull) {
+        v[1] = (unsigned long long)what;
+        v[2] = p;
+        v[3] = idx;
+        v[4] = bound;
+        v[5] = width;
+        v[6] = (unsigned long long)lp_in;
+        v[7] = (unsigned long long)lp_out;
+    }
+}
+#define SLOG_CHK(ok, what, idx, bound) \
+    (((ok)) ? true : (slog_violation(a.chk.viol, (what), p, (uint64_t)(idx), (uint64_t)(bound), width, lp_in, a.out.lp), false))
+#else
+#define SLOG_CHK(ok, what, idx, bound) true
+#endif
+
 #ifndef GWO_SLOG_SLOTS
 #define GWO_SLOG_SLOTS 1   // R' carries each entry's table slot: the next step places R_p without the bucket bytes
 #endif
@@ -105,9 +125,10 @@ __device__ __forceinline__ int slog_find(int64_t *s_key, uint8_t *s_ovf, int NB,
 #define GWO_SLOG_WPE 4   // waves per SIMD the registers are sized for (4: 128 VGPRs, 4 workgroups per CU)
 #endif
 template <int NW>
-__global__ __launch_bounds__(SLOG_THREADS) __attribute__((amdgpu_waves_per_eu(GWO_SLOG_WPE, GWO_SLOG_WPE))) void slog_fire_kernel(SlogArgs a) {
+__global__ __launch_bounds__(slog_threads_for(NW)) __attribute__((amdgpu_waves_per_eu(GWO_SLOG_WPE, GWO_SLOG_WPE))) void slog_fire_kernel(SlogArgs a) {
+    constexpr int TH = slog_threads_for(NW);   // SLOG_THREADS, or 512 with GWO_SLOG_BIG's larger tables
     extern __shared__ __attribute__((aligned(16))) int64_t s_dyn[];
-    const int T = 1 << a.cap_log2, NB = T >> 3, nbits = a.cap_log2 - 3, SPT = T / SLOG_THREADS;
+    const int T = 1 << a.cap_log2, NB = T >> 3, nbits = a.cap_log2 - 3, SPT = T / TH;
     int64_t *const s_key = s_dyn;       // [T]
     int64_t *const s_w = s_dyn + T;     // [NW][T]
     __shared__ int64_t s_side[1 + GWO_MAX_WORDS];   // key == Long.MIN_VALUE: [present, words]
@@ -123,7 +144,7 @@ __global__ __launch_bounds__(SLOG_THREADS) __attribute__((amdgpu_waves_per_eu(GW
     __shared__ uint16_t s_pre[SLOG_MAX_NB];         // first R_p entry of each bucket
 #endif
     __shared__ uint8_t s_ovo[2][SLOG_MAX_NB];       // R''s, recomputed from the keys' displacement by the sweep
-    __shared__ unsigned s_wsum[SLOG_THREADS / 64];
+    __shared__ unsigned s_wsum[TH / 64];
     __shared__ unsigned s_qn[2];          // R' entries written so far for the partition's (one or two) outputs
     __shared__ unsigned long long s_rowbase;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -134,8 +155,8 @@ __global__ __launch_bounds__(SLOG_THREADS) __attribute__((amdgpu_waves_per_eu(GW
     const int side_bucket = (int)slog_bucket(GWO_EMPTY_KEY, nbits);
     unsigned long long st_live = 0, st_maxp = 0, st_rovf = 0, st_neg = 0, st_lds = 0, st_slow = 0;
 
-    for (int i = tid; i < T; i += SLOG_THREADS) s_key[i] = GWO_EMPTY_KEY;
-    for (int i = tid; i < T * NW; i += SLOG_THREADS) s_w[i] = 0;
+    for (int i = tid; i < T; i += TH) s_key[i] = GWO_EMPTY_KEY;
+    for (int i = tid; i < T * NW; i += TH) s_w[i] = 0;
     if (tid <= GWO_MAX_WORDS) s_side[tid] = 0;
     if (tid < SLOG_MAX_NB) {
         s_ovo[0][tid] = 0;
@@ -161,7 +182,20 @@ __global__ __launch_bounds__(SLOG_THREADS) __attribute__((amdgpu_waves_per_eu(GW
             uint32_t c = 0, src = 0;
             const int r = lane;
             if (r == 0) {
-                const uint32_t rn = ((g_u32 *)a.in.cnt)[p];
+                uint32_t rn = ((g_u32 *)a.in.cnt)[p];
+#if GWO_SLOG_CHECK
+                {   // R_p's region and slot column inside their allocations (else: recorded, R_p read as empty)
+                    uint64_t width = 0;
+                    const uint32_t n = rn & ~SLOG_UNSTRUCT;
+                    bool ok = SLOG_CHK(n <= a.in.rcap, SLC_IN_REC, n, a.in.rcap);
+                    if (ok && n) ok = SLOG_CHK((uint64_t)(p + 1) * a.in.rcap * RW <= a.chk.in_rec, SLC_IN_REC,
+                                               (uint64_t)(p + 1) * a.in.rcap * RW, a.chk.in_rec);
+                    if (ok && n && !(rn & SLOG_UNSTRUCT))
+                        ok = SLOG_CHK((uint64_t)(p + 1) * a.in.rcap <= a.chk.in_slot, SLC_IN_SLOT,
+                                      (uint64_t)(p + 1) * a.in.rcap, a.chk.in_slot);
+                    if (!ok) rn = 0;
+                }
+#endif
                 s_rn = rn;
                 c = (rn & SLOG_UNSTRUCT) ? (rn & ~SLOG_UNSTRUCT) : 0u;
                 s_ptr[0] = a.in.rec + (uint64_t)p * a.in.rcap * RW;
@@ -179,10 +213,21 @@ __global__ __launch_bounds__(SLOG_THREADS) __attribute__((amdgpu_waves_per_eu(GW
                 sg.lp = ka->seg[r - 1].lp;
                 sg.sign = ka->seg[r - 1].sign;
                 sg.fmt = ka->seg[r - 1].fmt;
+                sg.nrec = ka->seg[r - 1].nrec;
                 const int d = lp_in - sg.lp;   // >= 0 (the host never gives a finer segment)
                 const uint32_t q = p >> d;
                 c = ((g_u32 *)sg.cnt)[q];
                 src = ((g_u32 *)sg.off)[q];
+                // a partition's run never reaches past the segment's carve: only a step queued behind a pass 2 whose
+                // partition overflowed sees a larger count (its uncapped cursor) -- that step is redone (slog_step)
+                if (sg.nrec) {
+                    const uint32_t room = src < sg.nrec ? sg.nrec - src : 0u;
+#if GWO_SLOG_CHECK
+                    uint64_t width = 0;
+                    if (c > room) (void)SLOG_CHK(false, SLC_SEG_CNT, (uint64_t)src + c, sg.nrec);
+#endif
+                    c = c < room ? c : room;
+                }
                 s_ptr[r] = sg.rec;
                 const int stride = sg.fmt ? RW : (a.has_val ? 2 : 1);
                 const int nl = sg.fmt ? NW : (a.has_val ? 1 : 0);
@@ -229,12 +274,12 @@ __global__ __launch_bounds__(SLOG_THREADS) __attribute__((amdgpu_waves_per_eu(GW
                 const int64_t *col = a.in.rec + (uint64_t)p * a.in.rcap * RW;   // keys[rcap], then each word's column
                 const uint16_t *scol = a.in.slot + (uint64_t)p * a.in.rcap;
                 unsigned placed = 0;
-                for (uint32_t base = 0; base < rcount; base += SLOG_THREADS * 4) {
+                for (uint32_t base = 0; base < rcount; base += TH * 4) {
                     int64_t ek[4], ew[4][NW];
                     uint32_t es[4];
 #pragma unroll
                     for (int j = 0; j < 4; ++j) {
-                        const uint32_t i = base + j * SLOG_THREADS + tid;
+                        const uint32_t i = base + j * TH + tid;
                         ek[j] = 0;
                         es[j] = 0xffffu;
 #pragma unroll
@@ -248,7 +293,7 @@ __global__ __launch_bounds__(SLOG_THREADS) __attribute__((amdgpu_waves_per_eu(GW
                     }
 #pragma unroll
                     for (int j = 0; j < 4; ++j) {
-                        const uint32_t i = base + j * SLOG_THREADS + tid;
+                        const uint32_t i = base + j * TH + tid;
                         if (i >= rcount || !in_range(ek[j])) continue;
                         if (ek[j] == GWO_EMPTY_KEY) {   // Long.MIN_VALUE: the side slot
                             s_side[0] = 1;
@@ -256,8 +301,17 @@ __global__ __launch_bounds__(SLOG_THREADS) __attribute__((amdgpu_waves_per_eu(GW
                             for (int w = 0; w < NW; ++w) s_side[1 + w] = ew[j][w];
                             continue;
                         }
+                        if (!SLOG_CHK(es[j] < (uint32_t)T, SLC_SLOT_RANGE, es[j], T)) continue;
                         const int sl = (int)(es[j] & (uint32_t)(T - 1));
                         const int slot = slot_lds(sl);
+#if GWO_SLOG_CHECK
+                        {   // two entries of R_p at one slot: the slot column is inconsistent
+                            const unsigned long long prev = atomicCAS((unsigned long long *)&s_key[slot],
+                                                                      (unsigned long long)GWO_EMPTY_KEY, (unsigned long long)ek[j]);
+                            if (!SLOG_CHK((int64_t)prev == GWO_EMPTY_KEY, SLC_SLOT_RANGE, ((uint64_t)sl << 32) | i, 0xdead))
+                                continue;
+                        }
+#endif
                         s_key[slot] = ek[j];
 #pragma unroll
                         for (int w = 0; w < NW; ++w) s_w[w * T + slot] = ew[j][w];
@@ -296,11 +350,11 @@ __global__ __launch_bounds__(SLOG_THREADS) __attribute__((amdgpu_waves_per_eu(GW
                 __syncthreads();
                 const int64_t *col = a.in.rec + (uint64_t)p * a.in.rcap * RW;   // keys[rcap], then each word's column
                 unsigned placed = 0;
-                for (uint32_t base = 0; base < rcount; base += SLOG_THREADS * 4) {
+                for (uint32_t base = 0; base < rcount; base += TH * 4) {
                     int64_t ek[4], ew[4][NW];
 #pragma unroll
                     for (int j = 0; j < 4; ++j) {
-                        const uint32_t i = base + j * SLOG_THREADS + tid;
+                        const uint32_t i = base + j * TH + tid;
                         ek[j] = 0;
 #pragma unroll
                         for (int w = 0; w < NW; ++w) ew[j][w] = 0;
@@ -312,7 +366,7 @@ __global__ __launch_bounds__(SLOG_THREADS) __attribute__((amdgpu_waves_per_eu(GW
                     }
 #pragma unroll
                     for (int j = 0; j < 4; ++j) {
-                        const uint32_t i = base + j * SLOG_THREADS + tid;
+                        const uint32_t i = base + j * TH + tid;
                         if (i >= rcount || !in_range(ek[j])) continue;
                         if (ek[j] == GWO_EMPTY_KEY) {   // Long.MIN_VALUE: the side slot
                             s_side[0] = 1;
@@ -334,7 +388,7 @@ __global__ __launch_bounds__(SLOG_THREADS) __attribute__((amdgpu_waves_per_eu(GW
             __syncthreads();
             stamp(2);
             // ---- fold: the segments' records (and R_p when unstructured), SLOG_J per thread, loads in flight ----
-            for (uint32_t base = 0; base < total; base += SLOG_THREADS * SLOG_J) {
+            for (uint32_t base = 0; base < total; base += TH * SLOG_J) {
                 int64_t rk[SLOG_J], rw[SLOG_J][NW];
                 int rr[SLOG_J];
                 // every record's range and address first (LDS only), then every load: global (not flat) loads,
@@ -343,7 +397,7 @@ __global__ __launch_bounds__(SLOG_THREADS) __attribute__((amdgpu_waves_per_eu(GW
                 int nlj[SLOG_J];
 #pragma unroll
                 for (int j = 0; j < SLOG_J; ++j) {
-                    const uint32_t i = base + j * SLOG_THREADS + tid;
+                    const uint32_t i = base + j * TH + tid;
                     rr[j] = -1;
                     ea[j] = s_ptr[0];
                     nlj[j] = 0;
@@ -399,8 +453,8 @@ __global__ __launch_bounds__(SLOG_THREADS) __attribute__((amdgpu_waves_per_eu(GW
             __syncthreads();
             stamp(3);
             if (failed) {   // more keys in range than the table holds: reset, halve the range
-                for (int i = tid; i < T; i += SLOG_THREADS) s_key[i] = GWO_EMPTY_KEY;
-                for (int i = tid; i < T * NW; i += SLOG_THREADS) s_w[i] = 0;
+                for (int i = tid; i < T; i += TH) s_key[i] = GWO_EMPTY_KEY;
+                for (int i = tid; i < T * NW; i += TH) s_w[i] = 0;
                 if (tid <= GWO_MAX_WORDS) s_side[tid] = 0;
                 if (GWO_SLOG_SLOTS && tid < NB) s_ovf[tid] = 0;
                 if (tid == 0) {
@@ -467,7 +521,7 @@ __global__ __launch_bounds__(SLOG_THREADS) __attribute__((amdgpu_waves_per_eu(GW
             stamp(6);
             uint32_t pre = 0, tot = 0;
 #pragma unroll
-            for (int w = 0; w < SLOG_THREADS / 64; ++w) {
+            for (int w = 0; w < TH / 64; ++w) {
                 const uint32_t x = s_wsum[w];
                 pre += w < wave ? x : 0u;
                 tot += x;
@@ -495,6 +549,13 @@ __global__ __launch_bounds__(SLOG_THREADS) __attribute__((amdgpu_waves_per_eu(GW
                 auto put = [&](int64_t k, const int64_t *wp, int ws, uint32_t half, uint32_t lslot) {
                     const uint32_t qpos = (half ? qb1 + at1++ : qb0 + at0++);
                     if (qpos >= a.out.rcap || (a.mode & 8)) return;
+#if GWO_SLOG_CHECK
+                    if (!SLOG_CHK((qout0 + half) < (1u << a.out.lp), SLC_PART, qout0 + half, 1u << a.out.lp)) return;
+                    if (!SLOG_CHK((uint64_t)(qout0 + half + 1) * a.out.rcap * RW <= a.chk.out_rec, SLC_OUT_REC,
+                                  (uint64_t)(qout0 + half + 1) * a.out.rcap * RW, a.chk.out_rec)) return;
+                    if (!SLOG_CHK((uint64_t)(qout0 + half + 1) * a.out.rcap <= a.chk.out_slot, SLC_OUT_SLOT,
+                                  (uint64_t)(qout0 + half + 1) * a.out.rcap, a.chk.out_slot)) return;
+#endif
                     int64_t *col = a.out.rec + (uint64_t)(qout0 + half) * a.out.rcap * RW;   // SoA columns
                     col[qpos] = k;
                     if (GWO_SLOG_SLOTS) a.out.slot[(uint64_t)(qout0 + half) * a.out.rcap + qpos] = (uint16_t)lslot;
@@ -623,13 +684,13 @@ void launch_slog_fire(const SlogArgs &a, int cus, hipStream_t s) {
     case NW: {                                                                                          \
         static int occ[16] = {};                                                                        \
         int &per_cu = occ[a.cap_log2 & 15];                                                             \
-        if (!per_cu && hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, slog_fire_kernel<NW>, SLOG_THREADS, \
+        if (!per_cu && hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, slog_fire_kernel<NW>, slog_threads_for(NW), \
                                                                     lds) != hipSuccess)                \
             per_cu = 1;                                                                                 \
         if (per_cu < 1) per_cu = 1;                                                                     \
         const uint32_t groups = (uint32_t)cus * (uint32_t)per_cu;                                       \
         const int grid = (int)(P < groups ? P : groups);                                                \
-        hipLaunchKernelGGL(slog_fire_kernel<NW>, dim3(grid), dim3(SLOG_THREADS), lds, s, a);             \
+        hipLaunchKernelGGL(slog_fire_kernel<NW>, dim3(grid), dim3(slog_threads_for(NW)), lds, s, a);     \
         break;                                                                                          \
     }
     switch (a.p.nwords) {

@@ -25,6 +25,16 @@ def _ptr(a):
     return a.ctypes.data_as(C.c_void_p) if a is not None else None
 
 
+def _torch_current_stream(device: int = 0):
+    """torch's current stream on `device` as a raw hipStream_t (0 = the null stream), or None when torch has not
+    initialised the GPU (then nothing of torch's can still be producing device columns)."""
+    import sys
+    torch = sys.modules.get("torch")
+    if torch is None or not torch.cuda.is_initialized():
+        return None
+    return int(torch.cuda.current_stream(device).cuda_stream)
+
+
 class GpuWindowOperator:
     """One subtask of ``keyBy(...).window(assigner).aggregate(fn)`` on one MI355X."""
 
@@ -75,6 +85,7 @@ class GpuWindowOperator:
         self.aggregate = aggregate
         self.value_dtype = np.float64 if vdt == N.DTYPE_FLOAT64 else np.int64
         self.batch_size = batch_size
+        self._borrowed = None   # device columns of the last process_device_batch (gwo.h: borrowed until the next call)
         self._pk, self._pt, self._pv = [], [], []
         self.output: list[tuple] = []
         self.side_output: list[tuple] = []
@@ -92,6 +103,7 @@ class GpuWindowOperator:
         if self._h:
             self._lib.gwo_destroy(self._h)
             self._h = None
+        self._borrowed = None
 
     dispose = close
 
@@ -123,11 +135,25 @@ class GpuWindowOperator:
         v = None if values is None else np.ascontiguousarray(values, dtype=self.value_dtype)
         self._submit(k, t, v)
 
-    def process_device_batch(self, key_ptr: int, ts_ptr: int, val_ptr, n: int):
-        """Columnar batch already resident in HBM (device pointers)."""
+    def process_device_batch(self, key_ptr: int, ts_ptr: int, val_ptr, n: int, producer_stream="current",
+                             keep=None):
+        """Columnar batch already resident in HBM (device pointers).
+
+        The columns may still be in flight on the stream that produced them: ``producer_stream`` (a raw
+        hipStream_t as int, 0 = the null stream; default "current" = torch's current stream of this device when
+        torch has initialised the GPU) is named to gwo_wait_stream, so the handle's stream waits for it on the
+        device (gwo.h "Device-input readiness").  ``None``: the caller guarantees the columns are complete.
+        ``keep`` (e.g. the tensors owning the columns) is held until the next call on this operator returns --
+        the borrow gwo.h states for device input."""
         self.flush()
+        if producer_stream == "current":
+            producer_stream = _torch_current_stream(self.cfg.device)
+        if producer_stream is not None:
+            N.check(self._lib.gwo_wait_stream(self._h, C.c_void_p(producer_stream or None)), self._h,
+                    "gwo_wait_stream")
         st = self._lib.gwo_submit(self._h, C.c_void_p(key_ptr), C.c_void_p(ts_ptr),
                                   C.c_void_p(val_ptr) if val_ptr else None, n)
+        self._borrowed = keep   # the previous batch's columns are released only now (this call has returned)
         N.check(st, self._h, "gwo_submit")
 
     def _submit(self, k, t, v):

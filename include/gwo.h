@@ -40,8 +40,18 @@
  * concurrently from different threads.
  *
  * Buffers: input columns may be host or device pointers (detected per call).  Device input is
- * borrowed until the next call on the handle returns; host input is copied before gwo_submit
- * returns.  Output columns given to gwo_drain may be host or device pointers.
+ * borrowed until the next call on the handle returns (the caller must neither free nor overwrite it
+ * before then); host input is copied before gwo_submit returns.  Output columns given to gwo_drain
+ * may be host or device pointers.
+ *
+ * Device-input readiness: the handle runs on its own non-blocking stream (or gwo_config.stream), which is
+ * NOT ordered after work the caller queued on other streams.  Device columns must therefore be complete
+ * as seen from the handle's stream when gwo_submit / gwo_submit_utf16 / gwo_intern_utf16 / gwo_restore
+ * is called: the caller either synchronises its producer first, produces on the handle's stream
+ * (gwo_config.stream, gwo_get_stream), or calls gwo_wait_stream(h, producer_stream) before the call --
+ * the handle's stream then waits on the device for everything queued on the producer so far, with no
+ * host wait.  The stateless helpers (gwo_assign_key_groups*, gwo_window_starts,
+ * gwo_partition_by_operator) run on a blocking stream, ordered behind the device's null stream.
  */
 #ifndef GWO_H
 #define GWO_H
@@ -143,9 +153,15 @@ gwo_status gwo_create(const gwo_config *cfg, gwo_handle **out);
 gwo_status gwo_destroy(gwo_handle *h);
 
 /* processElement for n records in arrival order; value may be NULL when every aggregate is COUNT.  Columns are device
- * pointers (read in place; the allocation must outlive the handle: its address range is cached) or host pointers
- * (copied to HBM on the handle's stream -- pinned memory, see gwo_host_register, is copied by DMA directly). */
+ * pointers (read in place; complete as seen from the handle's stream and borrowed until the next call on the handle
+ * returns -- see "Device-input readiness" above) or host pointers (copied to HBM on the handle's stream -- pinned
+ * memory, see gwo_host_register, is copied by DMA directly). */
 gwo_status gwo_submit(gwo_handle *h, const int64_t *key, const int64_t *ts, const void *value, int64_t n);
+/* Orders the handle's stream after the work queued so far on `producer` (a hipStream_t; NULL = the device's null
+ * stream): device columns written there are complete before any later call of this handle reads them.  One
+ * hipEventRecord + hipStreamWaitEvent, no host wait.  The caller names its producer before each gwo_submit of
+ * device columns it produced on another stream (the one-shot form keeps the ordering explicit per batch). */
+gwo_status gwo_wait_stream(gwo_handle *h, void *producer);
 /* Pins (page-locks) host memory for the GPUs (hipHostRegister), so gwo_submit / gwo_drain move it by DMA without a
  * pageable staging bounce: the Java operator registers its direct ByteBuffer columns once in open() (the mailbox
  * batching into pinned columnar buffers) and unregisters them in close().  Process-wide, not per handle. */

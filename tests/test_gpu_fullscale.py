@@ -228,9 +228,13 @@ def test_sharded_union_single_gpu(F, nshards, layout):
         for i, op in enumerate(ops):
             c = int(counts[i])
             if c:
-                kk, tt, vv = (reg[i, :c, j].contiguous() for j in range(3))
-                op.process_device_batch(kk.data_ptr(), tt.data_ptr(), vv.data_ptr(), c)
-                torch.cuda.synchronize()   # the batch's device columns are borrowed until the call returns
+                # the columns are produced on torch's stream and may still be in flight: process_device_batch names
+                # that stream to gwo_wait_stream (gwo.h "Device-input readiness") and keeps the tensors alive until
+                # the operator's next call returns (the borrow).  r05 failed here once (4 rows short, late counts
+                # equal) when K1 on the handle's non-blocking stream could read the columns before the copies --
+                # test_device_input_waits_for_producer_stream shows that race deterministically.
+                cols = [reg[i, :c, j].contiguous() for j in range(3)]
+                op.process_device_batch(*(x.data_ptr() for x in cols), c, keep=cols)
         for op in ops:
             N.check(lib.gwo_advance_watermark(op.handle, wm), op.handle)
     parts, late = [], 0
