@@ -208,6 +208,9 @@ public class GpuWindowOperator<IN, K> extends AbstractStreamOperator<GpuWindowRe
     // ---- OneInputStreamOperator ------------------------------------------------------------------------------
     @Override
     public void processElement(StreamRecord<IN> element) throws Exception {
+        if (mirrored) {   // the last checkpoint's (or restore's) copy in the keyed backend: dropped before any record
+            clearMirror();
+        }
         final IN v = element.getValue();
         final K key = keySelector.getKey(v);
         final int i = n;
@@ -230,17 +233,22 @@ public class GpuWindowOperator<IN, K> extends AbstractStreamOperator<GpuWindowRe
 
     @Override
     public void processWatermark(Watermark mark) throws Exception {
+        if (mirrored) {
+            clearMirror();
+        }
         flush();   // the pending records precede the watermark
         GwoNative.advanceWatermark(handle, mark.getTimestamp());
         emitFired();
-        // forwarded without advancing the "window-timers" service (AbstractStreamOperator.processWatermark would): it
-        // holds only the last checkpoint's mirror, whose timers must stay until the next checkpoint replaces them --
-        // they are how clearMirror finds the mirrored entries, so no record or watermark pays for clearing them
+        // forwarded without advancing the "window-timers" service (AbstractStreamOperator.processWatermark would): the
+        // service only ever holds a checkpoint's mirror, which is gone before any watermark gets here (clearMirror)
         output.emitWatermark(mark);
     }
 
     @Override
     public void endInput() throws Exception {
+        if (mirrored) {
+            clearMirror();
+        }
         flush();
         GwoNative.advanceWatermark(handle, Long.MAX_VALUE);   // StreamSource.java:122
         emitFired();
@@ -357,8 +365,12 @@ public class GpuWindowOperator<IN, K> extends AbstractStreamOperator<GpuWindowRe
     // gwo_export_heap_state_begin stages in native memory (the heap backend's section layout, parsed here), so the
     // backend's snapshot -- taken right after snapshotState (StreamOperatorStateHandler.java:186-198) -- is a savepoint
     // WindowOperator restores, and a WindowOperator savepoint restores here (initializeState reads the states back
-    // into one gwo_import_heap_state).  The mirror is cleared again at the next record, watermark or close: the GPU
-    // holds the live state, the backend only each checkpoint's copy.
+    // into one gwo_import_heap_state).  The mirror lives only from the operator's snapshot to the first of: the next
+    // record, watermark or end of input, notifyCheckpointComplete / notifyCheckpointAborted (or the backend's disposal
+    // with the operator).  The keyed backend's snapshot is taken synchronously right after snapshotState
+    // (StreamOperatorStateHandler.java:183-198: copy-on-write state maps and a copy of the timer queue on the heap
+    // backend, a native snapshot on RocksDB), so clearing the states afterwards does not touch the checkpoint.
+    // Between checkpoints the backend holds no window entries: the GPU is the only copy of the state.
     private static final short SID_CONTENTS = 0, SID_MERGING = 1, SID_EVENT_TIMERS = 2, SID_PROCESSING_TIMERS = 3;
 
     private int[] stateIds() {   // gwo_heap_state_ids: this operator's own numbering of the sections it parses
@@ -380,7 +392,8 @@ public class GpuWindowOperator<IN, K> extends AbstractStreamOperator<GpuWindowRe
         timers = getInternalTimerService("window-timers", ws, this);
     }
 
-    // The mirror's timers never fire: the mirror is cleared before a watermark reaches the timer service.
+    // The mirror's timers never fire: the mirror is cleared before any watermark, and the watermark never advances the
+    // timer service (processWatermark).
     @Override
     public void onEventTime(InternalTimer<K, TimeWindow> timer) {}
 
@@ -391,8 +404,7 @@ public class GpuWindowOperator<IN, K> extends AbstractStreamOperator<GpuWindowRe
     public void snapshotState(StateSnapshotContext context) throws Exception {
         super.snapshotState(context);
         flush();   // prepareSnapshotPreBarrier semantics: the batch is part of the state
-        // the previous checkpoint's mirror is dropped here, not at the next record: a checkpoint copies O(state) into
-        // the backend anyway, the record and watermark path never touches the mirror
+        // a mirror still in the backend (two checkpoints with no record or watermark between them) is replaced
         clearMirror();
         final KeyGroupRange range = getKeyedStateBackend().getKeyGroupRange();
         final int groups = range.getNumberOfKeyGroups();
@@ -539,8 +551,20 @@ public class GpuWindowOperator<IN, K> extends AbstractStreamOperator<GpuWindowRe
         }
         // no watermark is part of WindowOperator's state: the restored operator starts at Long.MIN_VALUE like it
         GwoNative.importHeapState(handle, stateIds(), out.getCopyOfBuffer(), Long.MIN_VALUE);
-        mirrored = true;   // the backend copy is dropped at the first record or watermark
+        mirrored = true;   // the restored copy is dropped at the first record, watermark or checkpoint notification
         return true;
+    }
+
+    @Override
+    public void notifyCheckpointComplete(long checkpointId) throws Exception {
+        super.notifyCheckpointComplete(checkpointId);
+        clearMirror();   // (the checkpoint holds its own copy since the synchronous snapshot)
+    }
+
+    @Override
+    public void notifyCheckpointAborted(long checkpointId) throws Exception {
+        super.notifyCheckpointAborted(checkpointId);
+        clearMirror();
     }
 
     // Drops the backend copy (the GPU holds the state): every window state, merging set and timer of the mirror,

@@ -6,7 +6,7 @@ before the producer has written them.  That is how `test_sharded_union_single_gp
 5 (the test built its columns with `.contiguous()` on torch's stream and submitted at once).  Here the producer is
 held back by a delay kernel so the race is deterministic:
 
-* unordered: the handle processes what the columns held BEFORE the producer's copy (batch A), not batch B;
+* unordered (log layout): the handle processes what the columns held BEFORE the producer's copy (batch A);
 * ordered (gwo_wait_stream, what `GpuWindowOperator.process_device_batch` does by default): exactly batch B,
   row for row against the C restatement of WindowOperator (oracle/window_oracle.c).
 
@@ -99,9 +99,11 @@ def test_device_input_waits_for_producer_stream(F, layout):
     assert got.shape == want_b.shape
     assert (_order(got) == want_b[np.lexsort((want_b[:, 0], want_b[:, 1]))]).all()
 
-    # unordered (the r05 test's pattern): K1 runs while the producer still sleeps and reads batch A -- the
-    # mechanism of the round-5 row loss, shown deterministically
-    got_u, delay_u = _run(F, layout, a_host, b_host, ordered=False)
-    if delay_u > 20.0:
-        assert got_u.shape == want_a.shape
-        assert (_order(got_u) == _order(want_a)).all()
+    # unordered (the r05 test's pattern), on the log layout -- the layout that lost rows in round 5: K1 runs while the
+    # producer still sleeps and reads batch A, exactly A's rows come out.  The mechanism of the round-5 row loss, shown
+    # deterministically.  (A fresh table-layout handle allocates its first window tables before its first kernel;
+    # hipMalloc synchronises the device, which happens to order it after the producer here -- not a guarantee.)
+    if layout == "log":
+        got_u, delay_u = _run(F, layout, a_host, b_host, ordered=False)
+        if delay_u > 20.0:
+            assert got_u.shape == want_a.shape and (_order(got_u) == _order(want_a)).all()

@@ -16,7 +16,11 @@ its JNI shim (java/.../gpu/GpuWindowOperator.java, jni/gwo_jni.c):
   parsed into WindowOperator's managed keyed states ("window-contents", "merging-window-set", the "window-timers"
   timer service), gwo_export_heap_state_end;
 * initializeState of a restored subtask: the backend's entries of its key groups (enumerated through the timers,
-  sessions through the merging window set) written as key-group sections into one gwo_import_heap_state.
+  sessions through the merging window set) written as key-group sections into one gwo_import_heap_state;
+* the mirror's lifetime (clearMirror): the backend's copy -- a checkpoint's, or a restore's -- is dropped at the
+  first record, watermark or end of input after it, or at notifyCheckpointComplete / notifyCheckpointAborted.
+  `JavaSequence.backend` models the keyed backend's live window states, so the tests assert that between
+  checkpoints it holds no window entry (the GPU is the only copy).
 
 Sessions fire asynchronously (gwo_session.cpp fire_session): without the sync in emitFired the drain loop would
 miss rows and forward the watermark first (the round-2 advisor's finding); the session case covers it.
@@ -105,6 +109,8 @@ class JavaSequence:
         self.range = key_group_range
         self.max_par = max_par
         self.merging = spec["assigner"] == N.ASSIGNER_SESSION
+        self.backend = H.WindowState()   # the keyed backend's live "window-contents" / "merging-window-set" / timers
+        self.mirrored = False
         if restore_sections is not None:
             self._restore(restore_sections)
         # open(): the columns and the drain buffers, allocated once
@@ -134,8 +140,24 @@ class JavaSequence:
             self.N.check(self.lib.gwo_host_unregister(_p(b)), None, "host unregister")
         self.lib.gwo_destroy(self.h)
 
+    def mirror_entries(self):
+        """Window entries + timers + merging sets the keyed backend holds now."""
+        return len(self.backend.contents) + len(self.backend.timers) + len(self.backend.merging)
+
+    def clear_mirror(self):   # clearMirror: every mirrored state and timer removed from the backend
+        if self.mirrored:
+            self.backend = H.WindowState()
+            self.mirrored = False
+
+    def notify_checkpoint_complete(self, checkpoint_id):
+        self.clear_mirror()
+
+    notify_checkpoint_aborted = notify_checkpoint_complete
+
     # processElement
     def process_element(self, key, ts, value):
+        if self.mirrored:
+            self.clear_mirror()
         i = self.n
         self.keys[i], self.ts[i], self.vals[i] = key, ts, value
         self.n += 1
@@ -149,12 +171,16 @@ class JavaSequence:
         self.n = 0
 
     def process_watermark(self, wm):
+        if self.mirrored:
+            self.clear_mirror()
         self.flush()
         self.N.check(self.lib.gwo_advance_watermark(self.h, wm), self.h, "advanceWatermark")
         self.emit_fired()
         self.out.watermark(wm)
 
     def end_input(self):
+        if self.mirrored:
+            self.clear_mirror()
         self.flush()
         self.N.check(self.lib.gwo_advance_watermark(self.h, LONG_MAX), self.h, "advanceWatermark")
         self.emit_fired()
@@ -202,6 +228,7 @@ class JavaSequence:
     def snapshot_state(self, key_group_list):
         N, lib, h = self.N, self.lib, self.h
         self.flush()
+        self.clear_mirror()   # a mirror still held (no record or watermark since the last checkpoint) is replaced
         groups = list(key_group_list)
         ids = N.GwoHeapStateIds(0, 1 if self.merging else -1, 2, 3)
         offs = np.zeros(len(groups), np.int64)
@@ -221,7 +248,13 @@ class JavaSequence:
                 backend.timers |= part.timers
         finally:
             N.check(lib.gwo_export_heap_state_end(h), h, "end")
-        return backend
+        self.backend, self.mirrored = backend, True
+        # the checkpoint: the backend's synchronous snapshot (copy-on-write maps, a copy of the timer queue)
+        snap = H.WindowState()
+        snap.contents.update(backend.contents)
+        snap.merging.update({k: dict(m) for k, m in backend.merging.items()})
+        snap.timers |= backend.timers
+        return snap
 
     # initializeState of a restored subtask (importMirror): the backend's entries of this subtask's key groups,
     # enumerated through the timers, sessions resolved through the merging window set, written as sections (each
@@ -246,6 +279,8 @@ class JavaSequence:
         ids = self.N.GwoHeapStateIds(0, 1 if self.merging else -1, 2, 3)
         arr = (C.c_uint8 * max(len(buf), 1)).from_buffer_copy(buf + b"\0")
         self.N.check(self.lib.gwo_import_heap_state(self.h, C.byref(ids), arr, len(buf), LONG_MIN), self.h, "import")
+        # the restored keyed states stay in the backend until the first record / watermark (importMirror: mirrored)
+        self.backend, self.mirrored = s, True
 
 
 def _oracle_run(assigner, agg, lateness, k, t, v, batches, side=False, restore_after=None):
@@ -271,6 +306,16 @@ def _oracle_run(assigner, agg, lateness, k, t, v, batches, side=False, restore_a
 def _events(k, t, v, batches):
     prev = 0
     for end, wm in batches:
+        for i in range(prev, end):
+            yield ("e", int(k[i]), int(t[i]), v[i].item())
+        yield ("w", wm)
+        prev = end
+
+
+def _events_from(k, t, v, batches, first):
+    """The events of batches[first:] (records after batches[first - 1]'s end, then each watermark)."""
+    prev = batches[first - 1][0] if first else 0
+    for end, wm in batches[first:]:
         for i in range(prev, end):
             yield ("e", int(k[i]), int(t[i]), v[i].item())
         yield ("w", wm)
@@ -334,7 +379,14 @@ def test_java_call_sequence_matches_oracle(N, case):
     k, t, v, b = _stream(hash(case) % 1000)
     out = Output()
     seq = JavaSequence(N, spec, (0, 127), 128, batch=1000, out=out, side_output=spec.get("side", False))
-    _drive(seq, _events(k, t, v, b))
+    half = len(b) // 2
+    _drive(seq, _events(k, t, v, b[:half]))
+    # a checkpoint mid-stream: the mirror exists only until the next record or watermark, and exporting does not
+    # change the GPU state (the rows below still equal the uninterrupted oracle run)
+    snap = seq.snapshot_state(range(0, 128))
+    assert seq.mirror_entries() == len(snap.contents) + len(snap.timers) + len(snap.merging) > 0
+    _drive(seq, _events_from(k, t, v, b, half))
+    assert seq.mirror_entries() == 0   # between checkpoints the backend holds no window entry
     seq.end_input()
     a, agg = spec["o"]()
     ref, fired = _oracle_run(a, agg, spec.get("lateness", 0), k, t, v, b, side=spec.get("side", False))
@@ -375,6 +427,9 @@ def test_java_snapshot_sections_rescale_2_to_3(N, case):
             seq.process_watermark(wm)
             prev = end
         part = seq.snapshot_state(range(r[0], r[1] + 1))
+        assert seq.mirror_entries() > 0
+        seq.notify_checkpoint_complete(1)
+        assert seq.mirror_entries() == 0   # dropped once the checkpoint is complete
         backend.contents.update(part.contents)
         backend.merging.update(part.merging)
         backend.timers |= part.timers
@@ -384,12 +439,15 @@ def test_java_snapshot_sections_rescale_2_to_3(N, case):
         r = O.compute_key_group_range_for_operator_index(maxp, 3, p)
         own = (kg >= r[0]) & (kg <= r[1])
         seq = JavaSequence(N, spec, r, maxp, batch=700, out=out_after, restore_sections=backend)
+        restored = seq.mirror_entries()
         prev = cut
         for end, wm in b[half:]:
             for i in np.flatnonzero(own[prev:end]) + prev:
                 seq.process_element(int(k[i]), int(t[i]), int(v[i]))
             seq.process_watermark(wm)
+            assert seq.mirror_entries() == 0   # the restored copy is gone after the first record / watermark
             prev = end
+        assert restored > 0
         seq.end_input()
         late += seq.late_metric
         seq.close()
