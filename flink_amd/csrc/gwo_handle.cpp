@@ -384,9 +384,18 @@ gwo_status Handle::state_size(int64_t *entries) {
         *entries += s;
         return GWO_OK;
     }
+    if (!rdone.empty()) {   // restored emitted entries: a key with new records is one entry, not two (snapshot merges)
+        int64_t bound = 0, got = 0;
+        GWO_TRY(snapshot_rows(&bound));
+        const size_t m = (size_t)std::max<int64_t>(bound, 1);
+        std::vector<int64_t> k(m), st(m), en(m), w(m * (size_t)std::max(plan.nwords, 1));
+        gwo_state_rows rows{k.data(), st.data(), en.data(), w.data(), nullptr, nullptr};
+        GWO_TRY(snapshot(&rows, (int64_t)m, &got));
+        *entries = s + got;
+        return GWO_OK;
+    }
     GWO_TRY(read_occupancy());
     for (auto &kv : tables) s += (int64_t)kv.second.occ;
-    for (auto &kv : rdone) s += (int64_t)kv.second.occ;
     *entries = s;
     return GWO_OK;
 }

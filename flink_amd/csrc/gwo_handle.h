@@ -40,6 +40,7 @@ struct WindowRows {
 
 const char *status_str(gwo_status s);
 bool is_device_ptr(const void *p);   // NULL counts as device (nothing to stage)
+int64_t combine_h(int op, int64_t a, int64_t b);   // one accumulator word of a plan op folded on the host (gwo_heapstate.cpp)
 
 struct DeviceGuard {
     int prev = -1;

@@ -94,6 +94,7 @@ int64_t f64_order_key_h(int64_t bits) {   // Double.compareTo total order (the p
     return bits >= 0 ? bits : (bits ^ 0x7fffffffffffffffLL);
 }
 int64_t f64_from_order_key_h(int64_t k) { return k >= 0 ? k : (k ^ 0x7fffffffffffffffLL); }
+}  // namespace
 
 int64_t combine_h(int op, int64_t a, int64_t b) {
     switch (op) {
@@ -111,8 +112,6 @@ int64_t combine_h(int op, int64_t a, int64_t b) {
         default: return b > a ? b : a;
     }
 }
-
-}  // namespace
 
 // accumulator words (the plan) -> GpuAggregates long[] (2 per aggregate), GpuAggregates.java createAccumulator/add
 static void words_to_java(const ResultPlan &rp, const int64_t *w, int64_t *out) {

@@ -100,7 +100,7 @@ gwo_status Handle::snapshot(const gwo_state_rows *rows, int64_t cap, int64_t *n_
     }
     GWO_TRY(hipcheck(hipMemcpyAsync(h_scalar, d_scratch_count, 8, hipMemcpyDeviceToHost, stream), "snapshot count"));
     GWO_TRY(hipcheck(hipStreamSynchronize(stream), "snapshot count"));
-    const int64_t n = (int64_t)*h_scalar;
+    int64_t n = (int64_t)*h_scalar;
     *n_out = n;
     if (n > (int64_t)m) return poison(GWO_ERR_HIP, "snapshot: more rows than the state holds");
     if (n > cap) return fail(GWO_ERR_CAPACITY, "snapshot: %lld rows, buffer holds %lld", (long long)n, (long long)cap);
@@ -126,6 +126,52 @@ gwo_status Handle::snapshot(const gwo_state_rows *rows, int64_t cap, int64_t *n_
     launch_snap_gather(c, perm, skg, n, NW, (int64_t *)ok.ptr, (int64_t *)os.ptr, (int64_t *)oe.ptr, (int64_t *)ow.ptr,
                        (int32_t *)okg.ptr, (int32_t *)ot.ptr, stream);
     GWO_TRY(launch_ok("snapshot gather"));
+    if (!rdone.empty() && !sess) {
+        // a tumbling window restored with emitted entries (rdone) holds a key twice once the key got new records: a
+        // pending row (tables) and an emitted one (rdone).  The heap backend keeps one entry per (key, window)
+        // (CopyOnWriteStateMapSnapshot.java:127-129) whose fire timer is pending -- the rows are merged here as
+        // gwo_export_heap_state merges them (rare path: host copies, the device buffers are rewritten)
+        std::vector<int64_t> hk(n), hs(n), he(n), hw((size_t)n * NW);
+        std::vector<int32_t> hg(n), ht(n);
+        GWO_TRY(hipcheck(hipMemcpyAsync(hk.data(), ok.ptr, (size_t)n * 8, hipMemcpyDeviceToHost, stream), "dedup"));
+        GWO_TRY(hipcheck(hipMemcpyAsync(hs.data(), os.ptr, (size_t)n * 8, hipMemcpyDeviceToHost, stream), "dedup"));
+        GWO_TRY(hipcheck(hipMemcpyAsync(he.data(), oe.ptr, (size_t)n * 8, hipMemcpyDeviceToHost, stream), "dedup"));
+        GWO_TRY(hipcheck(hipMemcpyAsync(hw.data(), ow.ptr, (size_t)n * NW * 8, hipMemcpyDeviceToHost, stream), "dedup"));
+        GWO_TRY(hipcheck(hipMemcpyAsync(hg.data(), okg.ptr, (size_t)n * 4, hipMemcpyDeviceToHost, stream), "dedup"));
+        GWO_TRY(hipcheck(hipMemcpyAsync(ht.data(), ot.ptr, (size_t)n * 4, hipMemcpyDeviceToHost, stream), "dedup"));
+        GWO_TRY(hipcheck(hipStreamSynchronize(stream), "dedup"));
+        std::map<std::pair<int64_t, int64_t>, int64_t> at;
+        int64_t m2 = 0;
+        for (int64_t i = 0; i < n; ++i) {
+            auto it = at.find({hk[i], hs[i]});
+            if (it != at.end()) {   // same key group as the row it joins: the key-group order stays
+                const int64_t j = it->second;
+                for (int w = 0; w < NW; ++w)
+                    hw[(size_t)j * NW + w] = combine_h(plan.op[w], hw[(size_t)j * NW + w], hw[(size_t)i * NW + w]);
+                ht[j] = ht[j] || ht[i];
+                continue;
+            }
+            at[{hk[i], hs[i]}] = m2;
+            hk[m2] = hk[i];
+            hs[m2] = hs[i];
+            he[m2] = he[i];
+            hg[m2] = hg[i];
+            ht[m2] = ht[i];
+            for (int w = 0; w < NW; ++w) hw[(size_t)m2 * NW + w] = hw[(size_t)i * NW + w];
+            m2++;
+        }
+        if (m2 < n) {
+            n = m2;
+            *n_out = n;
+            GWO_TRY(hipcheck(hipMemcpyAsync(ok.ptr, hk.data(), (size_t)n * 8, hipMemcpyHostToDevice, stream), "dedup"));
+            GWO_TRY(hipcheck(hipMemcpyAsync(os.ptr, hs.data(), (size_t)n * 8, hipMemcpyHostToDevice, stream), "dedup"));
+            GWO_TRY(hipcheck(hipMemcpyAsync(oe.ptr, he.data(), (size_t)n * 8, hipMemcpyHostToDevice, stream), "dedup"));
+            GWO_TRY(hipcheck(hipMemcpyAsync(ow.ptr, hw.data(), (size_t)n * NW * 8, hipMemcpyHostToDevice, stream), "dedup"));
+            GWO_TRY(hipcheck(hipMemcpyAsync(okg.ptr, hg.data(), (size_t)n * 4, hipMemcpyHostToDevice, stream), "dedup"));
+            GWO_TRY(hipcheck(hipMemcpyAsync(ot.ptr, ht.data(), (size_t)n * 4, hipMemcpyHostToDevice, stream), "dedup"));
+            GWO_TRY(hipcheck(hipStreamSynchronize(stream), "dedup"));
+        }
+    }
     struct {
         void *dst;
         DevBuf *src;

@@ -301,3 +301,42 @@ def test_sliding_rescale_straddling_watermarks_rejected(F):
     with pytest.raises(N.GwoError):
         c.restore_state([sa, sb])
     c.close()
+
+
+def test_restored_emitted_key_with_new_records_is_one_entry(F):
+    """A tumbling window restored with emitted entries (allowedLateness > 0, restored below maxTimestamp) whose key
+    then gets a new record holds that key in two device tables (the pending new records, the restored emitted entry).
+    The reference keeps ONE heap entry per (key, window) (CopyOnWriteStateMapSnapshot.java:127-129) -- its accumulator
+    the combination, its fire timer pending again (WindowOperator.java:393-410) -- so the snapshot rows, the state size
+    and the heap export all show one entry, and a restore of that snapshot fires the combined row."""
+    mk = lambda: F.GpuWindowOperator(F.TumblingEventTimeWindows.of(1_000),
+                                     F.MultiAggregate(F.SumAggregate(), F.MaxAggregate()), allowed_lateness=5_000,
+                                     state_layout="table")
+    a = mk()
+    a.process_batch(np.array([1, 2]), np.array([100, 200]), np.array([1, 4]))
+    a.process_watermark(999)    # [0, 1000) emitted (1: 1, 2: 4), kept for late re-fires
+    s1 = a.snapshot_state()
+    a.close()
+    b = mk()
+    b.process_batch(np.array([3]), np.array([300]), np.array([7]))
+    b.process_watermark(500)    # the same window, pending in this subtask
+    s2 = b.snapshot_state()
+    b.close()
+    m = mk()
+    m.restore_state([s1, s2])   # watermark 500: keys 1, 2 emitted, key 3 pending
+    m.process_batch(np.array([1]), np.array([150]), np.array([5]))   # key 1 again before maxTimestamp
+    assert m.state_size() == 3
+    snap = m.snapshot_state()
+    rows = sorted(zip(snap["key"].tolist(), snap["window_start"].tolist(), snap["timer"].tolist()))
+    assert rows == [(1, 0, 1), (2, 0, 0), (3, 0, 1)]
+    w1 = snap["words"][snap["key"].tolist().index(1)]
+    assert 6 in w1.tolist() and 5 in w1.tolist()     # sum 1 + 5, max(1, 5): the two entries combined
+    # the merged snapshot restores to the same behaviour: key 1 fires with the combined accumulator
+    r = mk()
+    r.restore_state(snap)
+    r.process_watermark(999)
+    assert sorted(r.output) == [(1, 0, 1000, (6, 5)), (3, 0, 1000, (7, 7))]
+    m.process_watermark(999)
+    assert sorted(m.output) == [(1, 0, 1000, (6, 5)), (3, 0, 1000, (7, 7))]
+    m.close()
+    r.close()

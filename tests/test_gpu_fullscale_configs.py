@@ -8,9 +8,9 @@ order-independent checksum over every row's words (key, start, end, result bits)
 steps that hold the complete windows.  Integer results bit-exact; the C3 average is the double
 (double)sum / count on both sides, compared bit for bit.
 
-* C3: sliding 60 s / 1 s AverageAggregate over 10M keys, the stream of 200M records over 120 s cut after 62 s of
-  event time (103M records, windows [0, 60 s) and [1 s, 61 s) complete), watermark every second (lag 1 s), then
-  endInput: 10M-key pane tables, rehashes, ring fires of ~10M rows per step.
+* C3: sliding 60 s / 1 s AverageAggregate over 10M keys, the whole stream of 200M records over 120 s, watermark
+  every second (lag 1 s), then endInput: windows fill, slide and retire for another minute -- 10M-key pane tables,
+  rehashes, window steps of ~10M rows each.
 * C5: event-time sessions (30 s gap) over 100K keys and 10M records in bursts, arrival order ts + U[0, 5 s),
   watermark maxTs - 5 s - 1 every 10 s of event time; and the late variant (0.1 % of the events delayed a further
   [5 s, 15 s) + 30 s, so many of them are dropped and counted).
