@@ -12,6 +12,15 @@ Inputs are synthetic and resident in HBM before timing (C5's stream is built on 
 and uploaded once).  A step = gwo_submit(batch) + gwo_advance_watermark + discarding the rows.
 Prints one JSON line per configuration (same fields as bench.py; `roofline_path` uses SURVEY.md
 §8d's B_alg with the configuration's I/S/O).  Usage: python bench_configs.py [c1 c2 c3 c5]
+  [--kernel-stats CSV] [--traffic JSON]
+
+`roofline` is the dominant kernel's (the one with the most time in a rocprofv3 kernel trace of the same
+configuration): its algorithmic bytes per launch (DOMINANT below: the bytes the reference's per-record work
+must move, per launch) over its average launch time from `--kernel-stats` (the rocprofv3 `--stats` CSV of
+`BENCH_PROF=0 python bench_configs.py cX`), against the 8 TB/s HBM peak; `traffic` and `roofline_pmc_path`
+come from `--traffic` (profiles/traffic_cfg.json: rocprofv3 FETCH_SIZE x 2 + WRITE_SIZE per launch and
+configuration, scripts/pmc_summary.py, stamped with the source tree it was measured on).  Without the files
+those fields are null.
 """
 import ctypes as C
 import json
@@ -25,6 +34,37 @@ sys.path.insert(0, ROOT)
 import numpy as np  # noqa: E402
 
 KERNELS = ("scan", "insert", "fire", "partition", "exchange", "slide", "session")
+
+# Dominant kernel per configuration (rocprofv3 kernel traces, profiles/r05_final_cfg_c*_kernel_stats.csv and r06) and
+# its algorithmic bytes per launch (SURVEY.md §8d units):
+#   c1 scan_kernel: one batch's key + timestamp columns, 16 B per record (classification, key groups, statistics)
+#   c2 gather_kernel: one batch's key + timestamp columns (COUNT reads no value), 16 B per record
+#   c3 slog_fire_kernel: one window step -- the running total R read and R' written (key, 2 words, table slot: 26 B
+#      per live key), the entering and the leaving pane's 16-B records, and one 32-B row (key, start, end, avg) per key
+#   c5 sess_process_kernel: one batch's records (24 B) and one read + one write of each touched key's entry (the
+#      table entry's header and inline session: 2 x 32 B per distinct key of the batch)
+DOMINANT = {"c1": "scan_kernel", "c2": "gather_kernel", "c3": "slog_fire_kernel", "c5": "sess_process_kernel"}
+
+
+def kernel_avg_ns(csv_path, name):
+    """(calls, average ns) of the kernel `name` (the function name, template arguments aside) in a rocprofv3 --stats
+    CSV; the instance with the most total time when several match."""
+    import csv
+    best = None
+    for r in csv.DictReader(open(csv_path)):
+        fn = r["Name"].split("(")[0].split("<")[0].split("::")[-1].replace("void ", "").strip()
+        if fn == name and (best is None or float(r["TotalDurationNs"]) > float(best["TotalDurationNs"])):
+            best = r
+    return (int(best["Calls"]), float(best["AverageNs"])) if best else (0, None)
+
+
+def kernel_calls(csv_path):
+    import csv
+    out = {}
+    for r in csv.DictReader(open(csv_path)):
+        fn = r["Name"].split("(")[0].split("<")[0].split("::")[-1].replace("void ", "").strip()
+        out[fn] = out.get(fn, 0) + int(r["Calls"])
+    return out
 
 
 def gen_device(N, lib, dev, torch, n, nkeys, span, disorder, key_mode=0, seed=42):
@@ -58,7 +98,7 @@ def session_stream(num_keys, n, gap=30_000, lag=5_000, seed=42, mean_inner=5_000
     return keys[order], ts[order], vals[order]
 
 
-def run(cfg):
+def run(cfg, kernel_stats=None, traffic=None):
     import torch
     import flink_amd as F
     from flink_amd import _native as N
@@ -156,27 +196,78 @@ def run(cfg):
             return la.value, ms.value
 
         stats = {name: kstat(i) for i, name in enumerate(KERNELS)}
-        rows = emitted() - rows0
+        rows_all = emitted()
+        rows = rows_all - rows0
         op.close()
-        return elapsed, rows, stats
+        return elapsed, rows, stats, rows_all
 
-    elapsed, nrows, _ = drive(False)
-    prof_elapsed, _, stats = drive(True) if os.environ.get("BENCH_PROF", "1") != "0" else (None, None, {})
+    elapsed, nrows, _, nrows_all = drive(False)
+    prof_elapsed, _, stats, _ = drive(True) if os.environ.get("BENCH_PROF", "1") != "0" else (None, None, {}, None)
     rows = [nrows]
     recs = bounds[-1][1] - bounds[warm][0]
     path_bytes = recs * I_B + rows[0] * (S_B + O_B)   # U*2S omitted: not measured here (lower bound)
+    steps_all = len(bounds)
+
+    # ---- the dominant kernel's roofline (DOMINANT): algorithmic bytes per launch over the traced average ----
+    # (averaged over every step of the drive, warm-up included, as the trace's launch average is: one launch per step)
+    dname = DOMINANT[cfg]
+    per_batch = [e - s for s, e in bounds]
+    if cfg in ("c1", "c2"):
+        alg = 16.0 * sum(per_batch) / len(per_batch)
+        unit = "one batch: 16 B (key, timestamp) per record"
+    elif cfg == "c3":
+        live = nrows_all / steps_all   # keys per window step (each emits one row)
+        pane = sum(per_batch) / len(per_batch)   # records per pane (a pane = one step's batch)
+        alg = live * 26 * 2 + 2 * pane * 16 + live * 32
+        unit = "one window step: R in + R' out (26 B per live key), entering + leaving pane (16 B per record), rows 32 B"
+    else:
+        kc = key.cpu().numpy()
+        u = [len(np.unique(kc[s:e])) for s, e in bounds]
+        alg = (24.0 * sum(per_batch) + 64.0 * sum(u)) / len(per_batch)
+        unit = "one batch: 24 B per record + 2 x 32 B per distinct key (entry read and written)"
+    roof = {"bound": "hbm", "kernel": dname, "alg_bytes_per_launch": alg, "alg_unit": unit, "peak": 8000.0,
+            "unit": "GB/s", "avg_launch_ms": None, "achieved": None, "frac": None, "traffic": None,
+            "kernel_stats": kernel_stats, "traffic_source": traffic}
+    if kernel_stats and os.path.exists(kernel_stats):
+        calls, avg = kernel_avg_ns(kernel_stats, dname)
+        if avg:
+            roof.update(avg_launch_ms=avg / 1e6, achieved=alg / avg, frac=alg / avg / 8000.0, launches_traced=calls)
+    pmc_path = None
+    if traffic and os.path.exists(traffic):
+        tj = json.load(open(traffic)).get(cfg, {})
+        if dname in tj:
+            roof["traffic"] = tj[dname]["hbm_bytes_per_launch"]
+        if kernel_stats and os.path.exists(kernel_stats) and tj:
+            # measured bytes of the whole path: every traced kernel's PMC bytes per launch x its launches (the trace
+            # covers the warm-up and timed steps of one drive), per step, over the timed run's time per step
+            calls = kernel_calls(kernel_stats)
+            pb = sum(v["hbm_bytes_per_launch"] * calls.get(k, 0) for k, v in tj.items() if not k.startswith("_"))
+            per_step = pb / steps_all
+            ms = elapsed / (len(bounds) - warm)
+            pmc_path = {"bytes_per_step": per_step, "achieved": per_step / ms / 1e9, "unit": "GB/s",
+                        "frac": per_step / ms / 1e9 / 8000.0, "measured_at": json.load(open(traffic)).get("_meta")}
     return {"metric": "records/sec per node, keyed window agg @1/2/4/8 GPU; % of HBM peak",
             "value": recs / elapsed, "unit": "records/s", "n_gpus": 1, "steps": len(bounds) - warm, "warmup": warm,
             "ms_per_step": elapsed / (len(bounds) - warm) * 1e3, "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "int64", "data": "synthetic, resident in HBM before timing",
             "config": {"workload": workload, "records": n, "records_per_step": every, "pipelined_submit": pipe},
+            "roofline": roof,
             "roofline_path": {"alg_bytes_lower_bound": path_bytes, "achieved": path_bytes / elapsed / 1e9,
                               "unit": "GB/s", "frac": path_bytes / elapsed / 1e9 / 8000.0},
+            "roofline_pmc_path": pmc_path,
             "fired_rows": rows[0],
             "ms_per_step_profiled": None if prof_elapsed is None else prof_elapsed / (len(bounds) - warm) * 1e3,
             "kernels_ms": {k: {"launches": v[0], "total_ms": v[1]} for k, v in stats.items() if v[0]}}
 
 
 if __name__ == "__main__":
-    for c in (sys.argv[1:] or ["c1", "c2", "c3", "c5"]):
-        print(json.dumps(run(c)), flush=True)
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("configs", nargs="*", default=["c1", "c2", "c3", "c5"])
+    ap.add_argument("--kernel-stats", default=None, help="rocprofv3 --stats CSV of this configuration ({cfg} is "
+                                                          "replaced by the configuration name)")
+    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_cfg.json"))
+    a = ap.parse_args()
+    for c in a.configs:
+        ks = a.kernel_stats.replace("{cfg}", c) if a.kernel_stats else None
+        print(json.dumps(run(c, ks, a.traffic)), flush=True)
