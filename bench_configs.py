@@ -241,7 +241,9 @@ def run(cfg, kernel_stats=None, traffic=None):
             # measured bytes of the whole path: every traced kernel's PMC bytes per launch x its launches (the trace
             # covers the warm-up and timed steps of one drive), per step, over the timed run's time per step
             calls = kernel_calls(kernel_stats)
-            pb = sum(v["hbm_bytes_per_launch"] * calls.get(k, 0) for k, v in tj.items() if not k.startswith("_"))
+            # (generate_kernel: the synthetic source, run once before timing -- not part of the path)
+            pb = sum(v["hbm_bytes_per_launch"] * calls.get(k, 0) for k, v in tj.items()
+                     if not k.startswith("_") and k != "generate_kernel")
             per_step = pb / steps_all
             ms = elapsed / (len(bounds) - warm)
             pmc_path = {"bytes_per_step": per_step, "achieved": per_step / ms / 1e9, "unit": "GB/s",

@@ -9,7 +9,9 @@
 #ifndef LOG_K1_PER
 #define LOG_K1_PER 16            // K1 tile: up to 256 threads x 16 records (64 KiB of 16-B records in LDS, two
 #endif                           // workgroups per CU); a launch's tiles are sized so every workgroup loops over
+#ifndef LOG_K1_THREADS
 #define LOG_K1_THREADS 256       // the same number of them (log_k1_tile)
+#endif
 #define LOG_K1_TILE (LOG_K1_PER * LOG_K1_THREADS)
 #ifndef LOG_K1_GRID
 #define LOG_K1_GRID 512          // K1 workgroups: 2 per CU on MI355X's 256 CUs, all resident, each looping over

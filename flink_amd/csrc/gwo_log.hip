@@ -159,10 +159,11 @@ __device__ __forceinline__ uint32_t tile_offsets(const uint32_t *s_cnt, uint32_t
     return total;
 }
 
-// Inclusive prefix of a 64-bit value over a 256-thread workgroup (wave shuffles + one LDS round);
+// Inclusive prefix of a 64-bit value over a K1 workgroup (LOG_K1_THREADS; wave shuffles + one LDS round);
 // ends synchronised.  *total = the workgroup sum.
-__device__ __forceinline__ unsigned long long block256_incl_scan64(unsigned long long v, unsigned long long *total) {
-    __shared__ unsigned long long s_w[4];
+__device__ __forceinline__ unsigned long long block_k1_incl_scan64(unsigned long long v, unsigned long long *total) {
+    constexpr int NWV = LOG_K1_THREADS / 64;
+    __shared__ unsigned long long s_w[NWV];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
@@ -171,14 +172,18 @@ __device__ __forceinline__ unsigned long long block256_incl_scan64(unsigned long
     }
     if (lane == 63) s_w[wid] = v;
     __syncthreads();
-    unsigned long long pre = 0;
-    for (int w = 0; w < wid; ++w) pre += s_w[w];
-    *total = s_w[0] + s_w[1] + s_w[2] + s_w[3];
+    unsigned long long pre = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < NWV; ++w) {
+        pre += w < wid ? s_w[w] : 0ull;
+        tot += s_w[w];
+    }
+    *total = tot;
     __syncthreads();
     return v + pre;
 }
 
-// K1's tail, run by its last workgroup (256 threads; formerly a separate collect kernel): moves the bucket
+// K1's tail, run by its last workgroup (LOG_K1_THREADS threads; formerly a separate collect kernel): moves the bucket
 // counts and batch statistics into the host-visible readback block (resetting cursors and statistics for the
 // next K1), and plans pass 2 on the device -- per bucket the partition capacity (mean + 6 sigma + 4 of a
 // Binomial(n_b, 1/F) partition, the host's group_capacity), the bucket's first record in its window's
@@ -280,8 +285,8 @@ __device__ __forceinline__ void k1_plan_tail(unsigned long long *cursor, BatchSt
             chunks = (uint32_t)((n_b + LOG_TILE - 1) / LOG_TILE);
         }
         unsigned long long seg_tot, chk_tot;
-        const unsigned long long seg_incl = block256_incl_scan64(seg, &seg_tot);
-        const unsigned long long chk_incl = block256_incl_scan64(chunks, &chk_tot);
+        const unsigned long long seg_incl = block_k1_incl_scan64(seg, &seg_tot);
+        const unsigned long long chk_incl = block_k1_incl_scan64(chunks, &chk_tot);
         LogBucket B;
         B.n = (uint32_t)n_b;
 #pragma unroll
@@ -332,8 +337,13 @@ __device__ __forceinline__ void k1_plan_tail(unsigned long long *cursor, BatchSt
 // V2 (S == 1, 16-B aligned columns, even tile length): each lane loads two adjacent records per column with one
 // 16-B load (8 B for int32 timestamps) -- record j of a thread is tile + (j / 2) * 2 * LOG_K1_THREADS + 2 * tid + j % 2.
 // A pair straddling the end of the batch reads 8 B past it, inside the 16-B aligned granule of its first record.
+#ifdef LOG_K1_WPE   // waves per SIMD the non-routed instances' registers are sized for (A/B of the workgroup shape)
+#define K1_WPE_ATTR(R) __attribute__((amdgpu_num_vgpr(512 / LOG_K1_WPE)))   // (every instance: A/B only)
+#else
+#define K1_WPE_ATTR(R)
+#endif
 template <bool HASV, int S, bool ROUTE, bool TS32, bool V2>   // S: record stride in int64 words (1: SoA columns, 3: {key, ts, value}; 0: runtime)
-__global__ __launch_bounds__(LOG_K1_THREADS, ROUTE ? 1 : 2) void log_part_kernel(
+__global__ __launch_bounds__(LOG_K1_THREADS, ROUTE ? 1 : 2) K1_WPE_ATTR(ROUTE) void log_part_kernel(
     const int64_t *__restrict__ key, const int64_t *__restrict__ ts, const int64_t *__restrict__ val, int64_t n,
     int64_t stride, WindowGeom g, long long base, int nunits, unsigned long long *__restrict__ cursor, uint64_t cap,
     int64_t *__restrict__ tmp, BatchStats *st, int64_t *side_key, int64_t *side_ts, int64_t *side_val,
