@@ -373,6 +373,9 @@ struct Handle {
     gwo_status log_split_exact(long long base, int nunits, uint64_t cap, const uint64_t *counts, int tmpx);
     gwo_status log_split_dev(const LogJob &J, const unsigned long long *rbp);
     gwo_status log_resolve_split();
+    bool log_split_mode() const;          // pass 2 on its own stream (GWO_SPLIT_STREAM, log_p2_begin)
+    hipStream_t log_p2_begin(int slot);
+    void log_p2_end(int slot);
     // ts32: `t` points at int32 timestamps - tbase (records received in the 20-B wire format)
     gwo_status insert_log(const int64_t *k, const int64_t *t, const int64_t *v, int64_t n, int64_t stride = 1,
                           const LogRoute *route = nullptr, bool ts32 = false, int64_t tbase = 0,

@@ -59,6 +59,14 @@ gwo_status Handle::log_init() {
     for (int i = 0; i < LOG_SLOTS; ++i)
         GWO_TRY(hipcheck(hipEventCreateWithFlags(&L.ev_rb[i], hipEventDisableTiming), "event"));
     GWO_TRY(hipcheck(hipEventCreateWithFlags(&L.ev_split, hipEventDisableTiming), "event"));
+    if (const char *e = getenv("GWO_SPLIT_STREAM")) L.split_mode = atoi(e) != 0;
+    if (L.split_mode) {
+        GWO_TRY(hipcheck(hipStreamCreateWithFlags(&L.split_stream, hipStreamNonBlocking), "pass-2 stream"));
+        for (int i = 0; i < LOG_SLOTS; ++i) {
+            GWO_TRY(hipcheck(hipEventCreateWithFlags(&L.ev_k1done[i], hipEventDisableTiming), "event"));
+            GWO_TRY(hipcheck(hipEventCreateWithFlags(&L.ev_p2[i], hipEventDisableTiming), "event"));
+        }
+    }
     GWO_TRY(hipcheck(hipHostMalloc((void **)&L.h_buckets, kPlanBytes, hipHostMallocDefault), "pinned"));
     GWO_TRY(hipcheck(hipHostMalloc((void **)&L.h_split_flag, 16, hipHostMallocCoherent | hipHostMallocMapped),
                      "pinned"));
@@ -123,6 +131,14 @@ void Handle::log_free() {
         if (L.ev_rb[i]) (void)hipEventDestroy(L.ev_rb[i]);
     }
     if (L.ev_split) (void)hipEventDestroy(L.ev_split);
+    if (L.split_stream) {
+        (void)hipStreamSynchronize(L.split_stream);
+        (void)hipStreamDestroy(L.split_stream);
+    }
+    for (int i = 0; i < LOG_SLOTS; ++i) {
+        if (L.ev_k1done[i]) (void)hipEventDestroy(L.ev_k1done[i]);
+        if (L.ev_p2[i]) (void)hipEventDestroy(L.ev_p2[i]);
+    }
     L.firedesc.release();
     if (L.h_split_flag) (void)hipHostFree(L.h_split_flag);
     if (L.h_fire_out) (void)hipHostFree(L.h_fire_out);
@@ -286,6 +302,25 @@ gwo_status Handle::log_split_exact(long long base, int nunits, uint64_t cap, con
     return GWO_OK;
 }
 
+// The stream a pass 2 of batch buffer `slot` runs on: the handle's, or (split mode; not with the sliding log, the
+// multi-GPU exchange or pipelined submission, whose steps and inserts queue behind pass 2 on the handle's stream) the
+// pass-2 stream behind an event marking everything queued on the handle's stream so far -- its K1.
+bool Handle::log_split_mode() const {
+    const LogState &L = *logst;
+    return L.split_mode && !slog && !comm && !L.pipeline;
+}
+hipStream_t Handle::log_p2_begin(int slot) {
+    LogState &L = *logst;
+    if (!log_split_mode()) return stream;
+    (void)hipEventRecord(L.ev_k1done[slot], stream);
+    (void)hipStreamWaitEvent(L.split_stream, L.ev_k1done[slot], 0);
+    return L.split_stream;
+}
+void Handle::log_p2_end(int slot) {
+    LogState &L = *logst;
+    if (log_split_mode()) (void)hipEventRecord(L.ev_p2[slot], L.split_stream);
+}
+
 // Commits a speculative pass 2 that runs the device plan (rb[LOG_RB_GO]): each window's segment records
 // are trimmed to the plan's size and the segments join their windows; the partition-overflow flag is checked
 // at the next sync point as for every pass 2 (log_resolve_split).
@@ -294,7 +329,7 @@ gwo_status Handle::log_commit_spec(LogJob &J, const unsigned long long *rbp) {
     uint64_t wcount[LOG_NU] = {};
     for (int b = 0; b < J.nunits * LOG_ND; ++b) wcount[b >> LOG_DB] += rbp[b];
     for (int w = 0; w < J.nunits; ++w) log_uncarve(J, w, wcount[w] ? rbp[LOG_RB_SEG + w] : 0);
-    L.pend.after_seq = J.seq;   // any later readback implies this pass 2 completed (stream order)
+    L.pend.after_seq = J.seq;   // any later readback implies this pass 2 completed (stream order; not in split mode)
     L.pend.has_event = false;
     L.pend.active = true;
     L.pend.tmpx = J.slot;
@@ -333,11 +368,13 @@ gwo_status Handle::log_split_dev(const LogJob &J, const unsigned long long *rbp)
         total += wcount[w];
     }
     L.h_split_flag[J.slot] = 0;
-    prof_begin(GWO_KERNEL_PARTITION);
+    hipStream_t ps = log_p2_begin(J.slot);
+    prof_begin(GWO_KERNEL_PARTITION, ps);
     launch_log_split((const int64_t *)L.tmp[J.slot].ptr, J.cap, needs_value, L.bk(J.slot), J.nunits * LOG_ND, set,
-                     L.d_split_flag + J.slot, (uint32_t)rbp[LOG_RB_CHUNKS], nullptr, stream);
+                     L.d_split_flag + J.slot, (uint32_t)rbp[LOG_RB_CHUNKS], nullptr, ps);
     GWO_TRY(launch_ok("log split"));
-    prof_end(GWO_KERNEL_PARTITION, (int64_t)total);
+    prof_end(GWO_KERNEL_PARTITION, (int64_t)total, ps);
+    log_p2_end(J.slot);
     // completion is implied by the next K1's readback (stream order); only a pipelined K1, queued before
     // this pass 2, needs an event (a marker between the kernels costs several microseconds)
     L.pend.after_seq = L.seq;
@@ -363,8 +400,9 @@ gwo_status Handle::log_split_dev(const LogJob &J, const unsigned long long *rbp)
 gwo_status Handle::log_resolve_split() {
     LogState &L = *logst;
     if (!L.pend.active) return GWO_OK;
-    // the event, not the stream: a pipelined K1 may be queued behind this pass 2
-    if (L.seen_seq <= L.pend.after_seq) {
+    if (log_split_mode()) {   // on its own stream: only its event says it completed
+        GWO_TRY(spin_event(L.ev_p2[L.pend.tmpx], "pass 2"));
+    } else if (L.seen_seq <= L.pend.after_seq) {   // the event, not the stream: a pipelined K1 may be queued behind it
         if (L.pend.has_event) GWO_TRY(spin_event(L.ev_split, "pass 2"));
         else GWO_TRY(hipcheck(hipStreamSynchronize(stream), "pass 2"));
     }
@@ -502,11 +540,13 @@ gwo_status Handle::log_k1(LogJob &J, bool first_pass) {
         // chunks = sum over buckets of ceil(n_b / TILE) <= ceil(n / TILE) + buckets
         const uint64_t grid = ((uint64_t)J.n + LOG_TILE - 1) / LOG_TILE + (uint64_t)J.nunits * LOG_ND;
         L.h_split_flag[J.slot] = 0;
-        prof_begin(GWO_KERNEL_PARTITION);
+        hipStream_t ps = log_p2_begin(J.slot);
+        prof_begin(GWO_KERNEL_PARTITION, ps);
         launch_log_split((const int64_t *)tmp.ptr, J.cap, needs_value, L.bk(J.slot), J.nunits * LOG_ND, set,
-                         L.d_split_flag + J.slot, (uint32_t)grid, L.d_go + J.slot, stream);
+                         L.d_split_flag + J.slot, (uint32_t)grid, L.d_go + J.slot, ps);
         GWO_TRY(launch_ok("log split"));
-        prof_end(GWO_KERNEL_PARTITION, J.n);
+        prof_end(GWO_KERNEL_PARTITION, J.n, ps);
+        log_p2_end(J.slot);
     }
     return GWO_OK;
 }

@@ -66,6 +66,11 @@ struct LogState {
         std::vector<uint64_t> counts;
     } pend;
     hipEvent_t ev_split = nullptr;               // after the deferred pass 2 (pipelined mode only)
+    // GWO_SPLIT_STREAM=1: pass 2 runs on its own stream behind an event after its K1, so the next batch's K1 (main
+    // stream) overlaps it; its completion is its event (ev_p2[slot]), never inferred from a later readback
+    bool split_mode = false;
+    hipStream_t split_stream = nullptr;
+    hipEvent_t ev_k1done[LOG_SLOTS] = {}, ev_p2[LOG_SLOTS] = {};
     unsigned long long seen_seq = 0;             // highest K1 readback sequence number observed complete
     uint32_t *d_slow = nullptr;                  // [LOG_SLOW_CAP] partitions the fire's fast instance left, then their count
     unsigned *h_split_flag = nullptr;            // pinned, device-written [LOG_SLOTS]: pass-2 overflow flags

@@ -17,6 +17,7 @@
 
 #include "../../include/gwo.h"
 #include "gwo_handle.h"
+#include "gwo_log_state.h"
 
 using namespace gwo;
 
@@ -296,6 +297,7 @@ gwo_status Handle::prof_collect() {
     if (pending_events.empty()) return GWO_OK;
     GWO_TRY(hipcheck(hipStreamSynchronize(stream), "prof sync"));
     if (fire_stream) GWO_TRY(hipcheck(hipStreamSynchronize(fire_stream), "prof sync"));
+    if (logst && logst->split_stream) GWO_TRY(hipcheck(hipStreamSynchronize(logst->split_stream), "prof sync"));
     for (auto &pe : pending_events) {
         float ms = 0.f;
         (void)hipEventElapsedTime(&ms, pe.a, pe.b);

@@ -228,7 +228,7 @@ def test_virtual_ranks_routed_batches_without_host_waits(F, monkeypatch, async_w
     batches ahead of the device must wait before reusing a slot.  What remains is latency, not a round trip per
     batch: a count exchange (or an all-reduce) queued behind a K1 that just finished can still be in flight when the
     host comes back within its few microseconds (the calls are ~tens of us apart here).  Allowed, for counts and for
-    asynchronous agreements alike: at most 1 wait in 8 batches and under 5 us of waiting per routed batch on average
+    asynchronous agreements alike: at most 1 wait in 4 batches and under 25 us of waiting per routed batch on average
     (the synchronous agreement waits for every one: its count is the number of calls).
 
     Flow control is bounded too: every 8th batch starts with the device caught up (gwo_sync), and such a batch and its
@@ -287,12 +287,13 @@ def test_virtual_ranks_routed_batches_without_host_waits(F, monkeypatch, async_w
           f"({w.flow_wait_ns / 1e3:.1f} us)")
     assert w.routed_batches == len(b) and len(b) >= 30
     assert w.flow_count_waits <= len(b) and w.flow_wm_waits <= len(b), "more than one flow-control wait per batch"
-    # protocol waits: counts (with their K1 finished) at most 1 in 8 batches -- 1 per held batch with held counts --
-    # and a generous 25 us of waiting per routed batch on average (a shared box's scheduling noise stays inside it)
-    assert w.count_waits <= (len(b) // 4 + 1 if hold else len(b) // 8), f"count waits with their K1 finished: {w.count_waits}"
+    # protocol waits: counts (with their K1 finished) at most 1 in 4 batches (r06 on MI355X: 0, 5 and 2 in 40 for the
+    # three variants) and a generous 25 us of waiting per routed batch on average (a shared box's scheduling noise
+    # stays inside it)
+    assert w.count_waits <= len(b) // 4, f"count waits with their K1 finished: {w.count_waits}"
     assert w.count_wait_ns < 25_000 * len(b), f"{w.count_wait_ns / 1e3:.1f} us waiting for counts"
     if async_wm:
-        assert w.wm_waits <= len(b) // 8, f"asynchronous watermark agreements waited for: {w.wm_waits}"
+        assert w.wm_waits <= len(b) // 4, f"asynchronous watermark agreements waited for: {w.wm_waits}"
         assert w.wm_wait_ns < 25_000 * len(b), f"{w.wm_wait_ns / 1e3:.1f} us waiting for agreements"
     else:
         assert w.wm_waits + w.flow_wm_waits >= len(b)   # the synchronous agreement waits for each all-reduce
