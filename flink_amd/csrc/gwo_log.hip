@@ -22,6 +22,7 @@
 //
 // Every HBM byte moves as a coalesced stream or as a run of consecutive 16-B records; the only
 // random accesses are LDS.
+#include "../../include/gwo.h"
 #include "gwo_device.h"
 #include "gwo_log.h"
 
@@ -1208,8 +1209,37 @@ struct FireArgs {
     LogSegDesc partial;
     uint32_t *plist;
     uint32_t *pcount;
+    // direct != 0 (int64 values, COUNT/SUM/MIN/MAX results only: no AVG, no float64): each result column is one of the
+    // run's count, sum, min, max or the constant 1, chosen per aggregate by sel (4 bits each: 0 n, 1 sum, 2 min, 3 max,
+    // 4 one) -- the emit selects without the plan's per-word and per-kind dispatch (fire_direct_sel)
+    int32_t direct;
+    uint32_t sel;
 };
 typedef __attribute__((address_space(4))) const FireArgs KFireArgs;   // in the (constant) kernarg segment
+
+// FireArgs.direct / .sel for a plan: every aggregate's result column is one accumulator word as it is (int64 values,
+// kinds COUNT, SUM, MIN, MAX) and each such word is the run's count, sum, min, max or the constant 1.
+static void fire_direct_sel(const AccPlan &p, const ResultPlan &rp, int32_t *direct, uint32_t *sel) {
+    *direct = 0;
+    *sel = 0;
+    if (p.value_is_f64 || rp.value_is_f64) return;
+    uint32_t s = 0;
+    for (int a = 0; a < rp.naggs; ++a) {
+        if (rp.kind[a] == GWO_AGG_AVG) return;
+        const int w = rp.word[a];
+        if (w < 0 || w >= p.nwords) return;
+        uint32_t c;
+        if (p.src[w] == SRC_ONE) c = p.op[w] == ACC_ADD_I64 ? 0u : 4u;
+        else if (p.src[w] != SRC_VALUE) return;
+        else if (p.op[w] == ACC_ADD_I64) c = 1u;
+        else if (p.op[w] == ACC_MIN_I64) c = 2u;
+        else if (p.op[w] == ACC_MAX_I64) c = 3u;
+        else return;
+        s |= c << (4 * a);
+    }
+    *direct = 1;
+    *sel = s;
+}
 
 template <int NW, bool PART, bool HV>
 __global__ __launch_bounds__(LOG_FIRE_THREADS) __attribute__((amdgpu_waves_per_eu(4, 4))) void log_fire_kernel(FireArgs A) {
@@ -1683,13 +1713,55 @@ __global__ __launch_bounds__(LOG_FIRE_THREADS) __attribute__((amdgpu_waves_per_e
                 }
                 row_results_s<NW>(naggs, rkind, rword, rf64, acc, res);
             };
+            // the direct plan (int64 COUNT/SUM/MIN/MAX: FireArgs.direct): the run's count, sum, min and max, then a
+            // branch-free select per result column -- no per-word or per-kind dispatch per row
+            const bool direct = KA->direct != 0;
+            const uint32_t dsel = KA->sel;
+            auto fold_row_direct = [&](int q, bool valid, int64_t &k, int64_t (&res)[4]) {
+                const uint32_t qc = valid ? (uint32_t)q : 0u;
+                const uint32_t off = s_cnt[qc], nxt = s_cnt[qc + 1];
+                k = s_key[qc];
+                const uint32_t n = valid ? nxt - off : 0u;
+                int64_t si = 0, mn = 0x7fffffffffffffffLL, mx = (int64_t)0x8000000000000000LL;
+                if (has_val) {
+                    // the run's first 4 values, unclamped (adjacent reads pair into ds_read2_b64): off <= FIRE_RCAP, and
+                    // s_val[FIRE_RCAP ..] is the s_own / s_cnt area, inside the allocation (values past n are unused)
+                    int64_t v4[4];
+#pragma unroll
+                    for (int t = 0; t < 4; ++t) v4[t] = s_val[off + t];
+#pragma unroll
+                    for (int t = 0; t < 4; ++t) {
+                        const bool in = (uint32_t)t < n;
+                        const int64_t v = v4[t];
+                        si = (int64_t)((uint64_t)si + (uint64_t)(in ? v : 0));
+                        mn = (in && v < mn) ? v : mn;
+                        mx = (in && v > mx) ? v : mx;
+                    }
+                    for (uint32_t t = 4; t < n; ++t) {
+                        const int64_t v = s_val[off + t];
+                        si = (int64_t)((uint64_t)si + (uint64_t)v);
+                        mn = v < mn ? v : mn;
+                        mx = v > mx ? v : mx;
+                    }
+                }
+#pragma unroll
+                for (int a = 0; a < 4; ++a) {
+                    const uint32_t c = (dsel >> (4 * a)) & 15u;   // wave-uniform
+                    res[a] = c == 0u ? (int64_t)n : c == 1u ? si : c == 2u ? mn : c == 3u ? mx : (int64_t)1;
+                }
+            };
             for (int base = 0; base < (int)rows + sh; base += 2 * LOG_FIRE_THREADS) {
                 const int q0 = base + 2 * tid - sh, q1 = q0 + 1;
                 const bool v0 = q0 >= 0 && q0 < (int)rows, v1 = q1 < (int)rows;
                 if (!v0 && !v1) continue;
                 int64_t k0, k1, r0[4] = {0, 0, 0, 0}, r1[4] = {0, 0, 0, 0};
-                fold_row(q0, v0, k0, r0);
-                fold_row(q1, v1, k1, r1);
+                if (direct) {
+                    fold_row_direct(q0, v0, k0, r0);
+                    fold_row_direct(q1, v1, k1, r1);
+                } else {
+                    fold_row(q0, v0, k0, r0);
+                    fold_row(q1, v1, k1, r1);
+                }
                 const unsigned long long pb = rbase + (unsigned long long)(long long)q0;   // even: the pair's first row
 #ifdef GWO_ABL_FIRE_NOSTORE   // ablation (timing experiments only): the emit without its global stores
                 if (pb != ~0ull) continue;
@@ -1870,6 +1942,8 @@ void launch_log_fire(const LogSegDesc *segs, int nseg, int lp, int has_val, cons
     fa.overflow = overflow;
     fa.partial = partial;
     fa.pcount = slow_cnt;
+    static const bool direct_on = getenv("GWO_FIRE_DIRECT") == nullptr || atoi(getenv("GWO_FIRE_DIRECT")) != 0;
+    if (direct_on) fire_direct_sel(plan, rp, &fa.direct, &fa.sel);
     FireArgs fs = fa;            // the slow instance: over the fast instance's list, or every partition
     fa.slow_only = 0;
     fa.plist = slow_list;
