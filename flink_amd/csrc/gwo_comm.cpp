@@ -793,16 +793,16 @@ extern "C" gwo_status gwo_partition_by_operator(const int64_t *key, const int64_
         (void)hipMemsetAsync(dcur, 0, route_cursor_bytes(), s);
         (void)hipMemsetAsync(dv, 0, nb, s);
         if (n > 0) {
-            (void)hipMemcpyAsync(dk, key, n * 8, hipMemcpyDefault, s);
-            (void)hipMemcpyAsync(dt, ts, n * 8, hipMemcpyDefault, s);
-            if (value) (void)hipMemcpyAsync(dv, value, n * 8, hipMemcpyDefault, s);
+            if (copy_in(dk, key, n * 8, s) != hipSuccess || copy_in(dt, ts, n * 8, s) != hipSuccess ||
+                (value && copy_in(dv, value, n * 8, s) != hipSuccess))
+                st = GWO_ERR_HIP;
             launch_route((const int64_t *)dk, (const int64_t *)dt, (const int64_t *)dv, n, key_kind, max_parallelism,
                          parallelism, (unsigned long long *)dcur, (uint64_t)cap, (int64_t *)dout, s);
         }
         launch_route_collect((unsigned long long *)dcur, parallelism, (unsigned long long *)dcnt, s);
-        (void)hipMemcpyAsync(out, dout, (size_t)parallelism * cap * 24, hipMemcpyDefault, s);
-        (void)hipMemcpyAsync(counts, dcnt, (size_t)parallelism * 8, hipMemcpyDefault, s);
-        if (hipStreamSynchronize(s) != hipSuccess) st = GWO_ERR_HIP;
+        if (copy_out(out, dout, (size_t)parallelism * cap * 24, s) != hipSuccess ||
+            copy_out(counts, dcnt, (size_t)parallelism * 8, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess)
+            st = GWO_ERR_HIP;
     }
     for (void *p : {dk, dt, dv, dout, dcur, dcnt})
         if (p) (void)hipFree(p);

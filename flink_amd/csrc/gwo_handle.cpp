@@ -325,7 +325,7 @@ gwo_status Handle::drain(const gwo_out *cols, int64_t cap, int64_t *n_out) {
     int ncols = 3 + rplan.naggs;
     for (int c = 0; c < ncols; ++c) {
         if (!dst[c]) continue;
-        GWO_TRY(hipcheck(hipMemcpyAsync(dst[c], src[c], take * 8, hipMemcpyDefault, stream), "drain copy"));
+        GWO_TRY(hipcheck(copy_out(dst[c], src[c], take * 8, stream), "drain copy"));
     }
     uint64_t rest = out_rows - take;
     for (uint64_t off = 0; off < rest; off += take) {
@@ -348,7 +348,7 @@ gwo_status Handle::drain_side(const gwo_side_out *cols, int64_t cap, int64_t *n_
     DevBuf *src[3] = {&side_key, &side_ts, &side_val};
     void *dst[3] = {cols->key, cols->ts, cols->value};
     for (int c = 0; c < 3; ++c)
-        if (dst[c]) GWO_TRY(hipcheck(hipMemcpyAsync(dst[c], src[c]->ptr, take * 8, hipMemcpyDefault, stream), "side copy"));
+        if (dst[c]) GWO_TRY(hipcheck(copy_out(dst[c], src[c]->ptr, take * 8, stream), "side copy"));
     uint64_t rest = side_rows_committed - take;
     for (uint64_t off = 0; off < rest; off += take) {
         uint64_t len = std::min<uint64_t>(take, rest - off);

@@ -40,6 +40,14 @@ struct WindowRows {
 
 const char *status_str(gwo_status s);
 bool is_device_ptr(const void *p);   // NULL counts as device (nothing to stage)
+
+// Copies to and from caller memory (gwo_xfer.cpp): pageable host memory goes through the library's pinned bounce
+// buffer, never through HIP's pageable copy path; pinned host and device memory are copied directly.
+enum MemKind { MEM_DEVICE, MEM_PINNED, MEM_PAGEABLE };
+MemKind mem_kind(const void *p);   // NULL counts as device
+hipError_t copy_out(void *dst, const void *dev_src, size_t bytes, hipStream_t s);   // complete on return
+hipError_t copy_in(void *dev_dst, const void *src, size_t bytes, hipStream_t s);   // pageable src reusable on return
+hipError_t fetch_host(void *host_dst, const void *src, size_t bytes, hipStream_t s);   // src device or host
 int64_t combine_h(int op, int64_t a, int64_t b);   // one accumulator word of a plan op folded on the host (gwo_heapstate.cpp)
 
 struct DeviceGuard {

@@ -512,7 +512,7 @@ gwo_status Handle::import_heap_state(const gwo_heap_state_ids *ids, const uint8_
         if (ch.empty()) ch.push_back(0);
         const int64_t *idp = nullptr;
         GWO_TRY(intern_utf16(ch.data(), off.data(), R.n, &idp));
-        GWO_TRY(hipcheck(hipMemcpy(R.key.data(), idp, (size_t)R.n * 8, hipMemcpyDefault), "interned ids"));
+        GWO_TRY(hipcheck(copy_out(R.key.data(), idp, (size_t)R.n * 8, stream), "interned ids"));
     }
     std::vector<int32_t> kgs(R.n);
     gwo_state_rows rows{R.key.data(), R.start.data(), R.end.data(), R.words.data(), nullptr, R.timer.data()};

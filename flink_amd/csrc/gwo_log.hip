@@ -1744,14 +1744,12 @@ __global__ __launch_bounds__(LOG_FIRE_THREADS) __attribute__((amdgpu_waves_per_e
                         mx = v > mx ? v : mx;
                     }
                 }
-                // the selection with masks (wave-uniform 64-bit masks of the aggregate's selector): no branches per row
+                // the selector is wave-uniform: these branches do not diverge (a mask-and-or selection measured 3 %
+                // slower per fire, profiles/r06_experiments.txt)
 #pragma unroll
                 for (int a = 0; a < 4; ++a) {
-                    const uint32_t c = (dsel >> (4 * a)) & 15u;   // wave-uniform
-                    const uint64_t m0 = c == 0u ? ~0ull : 0ull, m1 = c == 1u ? ~0ull : 0ull, m2 = c == 2u ? ~0ull : 0ull,
-                                   m3 = c == 3u ? ~0ull : 0ull;
-                    res[a] = (int64_t)(((uint64_t)n & m0) | ((uint64_t)si & m1) | ((uint64_t)mn & m2) | ((uint64_t)mx & m3) |
-                                       (c == 4u ? 1ull : 0ull));
+                    const uint32_t c = (dsel >> (4 * a)) & 15u;
+                    res[a] = c == 0u ? (int64_t)n : c == 1u ? si : c == 2u ? mn : c == 3u ? mx : (int64_t)1;
                 }
             };
             for (int base = 0; base < (int)rows + sh; base += 2 * LOG_FIRE_THREADS) {

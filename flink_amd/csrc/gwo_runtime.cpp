@@ -357,7 +357,7 @@ gwo_status Handle::stage_inputs(const int64_t *key, const int64_t *ts, const voi
             *dst[c] = (const int64_t *)src[c];
         } else {
             GWO_TRY(ensure_buf(*bufs[c], (size_t)n * 8));
-            GWO_TRY(hipcheck(hipMemcpyAsync(bufs[c]->ptr, src[c], (size_t)n * 8, hipMemcpyHostToDevice, stream), "stage"));
+            GWO_TRY(hipcheck(copy_in(bufs[c]->ptr, src[c], (size_t)n * 8, stream), "stage"));
             *dst[c] = (const int64_t *)bufs[c]->ptr;
         }
     }
@@ -1247,7 +1247,7 @@ gwo_status gwo_intern_utf16(gwo_handle *hh, const uint16_t *chars, const int64_t
     if (n == 0) return GWO_OK;
     const int64_t *ids = nullptr;
     GWO_TRY(h->intern_utf16(chars, offsets, n, &ids));
-    return h->hipcheck(hipMemcpy(ids_out, ids, (size_t)n * 8, hipMemcpyDefault), "intern ids");
+    return h->hipcheck(copy_out(ids_out, ids, (size_t)n * 8, h->stream), "intern ids");
 }
 
 gwo_status gwo_key_strings(gwo_handle *hh, const int64_t *ids, int64_t n, int64_t *offsets_out, uint16_t *chars_out,
@@ -1511,7 +1511,7 @@ static gwo_status stateless_run(int32_t device, size_t n, const void *in, size_t
     void *douts[2] = {nullptr, nullptr};
     if (!is_device_ptr(in)) {
         if (hipMalloc(&tmp_in, n * 8 + 8) != hipSuccess) st = GWO_ERR_OUT_OF_MEMORY;
-        else (void)hipMemcpyAsync(tmp_in, in, n * 8, hipMemcpyHostToDevice, s);
+        else if (copy_in(tmp_in, in, n * 8, s) != hipSuccess) st = GWO_ERR_HIP;
         din = (const int64_t *)tmp_in;
     }
     for (int i = 0; i < nouts && st == GWO_OK; ++i) {
@@ -1526,7 +1526,7 @@ static gwo_status stateless_run(int32_t device, size_t n, const void *in, size_t
     if (st == GWO_OK) {
         body(din, douts, s, ctx);
         for (int i = 0; i < nouts; ++i)
-            if (tmp_out[i]) (void)hipMemcpyAsync(outs[i], tmp_out[i], n * out_words, hipMemcpyDeviceToHost, s);
+            if (tmp_out[i] && copy_out(outs[i], tmp_out[i], n * out_words, s) != hipSuccess) st = GWO_ERR_HIP;
         if (hipStreamSynchronize(s) != hipSuccess) st = GWO_ERR_HIP;
     }
     if (tmp_in) (void)hipFree(tmp_in);
@@ -1586,14 +1586,14 @@ gwo_status gwo_assign_key_groups_utf16(const uint16_t *chars, const int64_t *off
     } else {
         nchars = offsets[n];
         int64_t *p = (int64_t *)dev_alloc((size_t)(n + 1) * 8);
-        if (p) (void)hipMemcpyAsync(p, offsets, (size_t)(n + 1) * 8, hipMemcpyHostToDevice, s);
+        if (p && copy_in(p, offsets, (size_t)(n + 1) * 8, s) != hipSuccess) st = GWO_ERR_HIP;
         d_off = p;
     }
     if (st == GWO_OK && (nchars < 0 || (nchars > 0 && !chars))) st = GWO_ERR_INVALID_ARGUMENT;
     const uint16_t *d_chars = chars;
     if (st == GWO_OK && nchars > 0 && !is_device_ptr(chars)) {
         uint16_t *p = (uint16_t *)dev_alloc((size_t)nchars * 2);
-        if (p) (void)hipMemcpyAsync(p, chars, (size_t)nchars * 2, hipMemcpyHostToDevice, s);
+        if (p && copy_in(p, chars, (size_t)nchars * 2, s) != hipSuccess) st = GWO_ERR_HIP;
         d_chars = p;
     }
     int32_t *outs[3] = {hash_out, kg_out, op_out}, *douts[3] = {nullptr, nullptr, nullptr};
@@ -1605,8 +1605,8 @@ gwo_status gwo_assign_key_groups_utf16(const uint16_t *chars, const int64_t *off
         launch_key_groups_utf16(d_chars, d_off, n, max_parallelism, parallelism, douts[0], douts[1], douts[2], s);
         if (hipGetLastError() != hipSuccess) st = GWO_ERR_HIP;
         for (int i = 0; i < 3 && st == GWO_OK; ++i)
-            if (outs[i] && douts[i] != outs[i])
-                (void)hipMemcpyAsync(outs[i], douts[i], (size_t)n * 4, hipMemcpyDeviceToHost, s);
+            if (outs[i] && douts[i] != outs[i] && copy_out(outs[i], douts[i], (size_t)n * 4, s) != hipSuccess)
+                st = GWO_ERR_HIP;
     }
     if (hipStreamSynchronize(s) != hipSuccess && st == GWO_OK) st = GWO_ERR_HIP;
     for (void *p : owned) (void)hipFree(p);

@@ -133,12 +133,12 @@ gwo_status Handle::snapshot(const gwo_state_rows *rows, int64_t cap, int64_t *n_
         // gwo_export_heap_state merges them (rare path: host copies, the device buffers are rewritten)
         std::vector<int64_t> hk(n), hs(n), he(n), hw((size_t)n * NW);
         std::vector<int32_t> hg(n), ht(n);
-        GWO_TRY(hipcheck(hipMemcpyAsync(hk.data(), ok.ptr, (size_t)n * 8, hipMemcpyDeviceToHost, stream), "dedup"));
-        GWO_TRY(hipcheck(hipMemcpyAsync(hs.data(), os.ptr, (size_t)n * 8, hipMemcpyDeviceToHost, stream), "dedup"));
-        GWO_TRY(hipcheck(hipMemcpyAsync(he.data(), oe.ptr, (size_t)n * 8, hipMemcpyDeviceToHost, stream), "dedup"));
-        GWO_TRY(hipcheck(hipMemcpyAsync(hw.data(), ow.ptr, (size_t)n * NW * 8, hipMemcpyDeviceToHost, stream), "dedup"));
-        GWO_TRY(hipcheck(hipMemcpyAsync(hg.data(), okg.ptr, (size_t)n * 4, hipMemcpyDeviceToHost, stream), "dedup"));
-        GWO_TRY(hipcheck(hipMemcpyAsync(ht.data(), ot.ptr, (size_t)n * 4, hipMemcpyDeviceToHost, stream), "dedup"));
+        GWO_TRY(hipcheck(copy_out(hk.data(), ok.ptr, (size_t)n * 8, stream), "dedup"));
+        GWO_TRY(hipcheck(copy_out(hs.data(), os.ptr, (size_t)n * 8, stream), "dedup"));
+        GWO_TRY(hipcheck(copy_out(he.data(), oe.ptr, (size_t)n * 8, stream), "dedup"));
+        GWO_TRY(hipcheck(copy_out(hw.data(), ow.ptr, (size_t)n * NW * 8, stream), "dedup"));
+        GWO_TRY(hipcheck(copy_out(hg.data(), okg.ptr, (size_t)n * 4, stream), "dedup"));
+        GWO_TRY(hipcheck(copy_out(ht.data(), ot.ptr, (size_t)n * 4, stream), "dedup"));
         GWO_TRY(hipcheck(hipStreamSynchronize(stream), "dedup"));
         std::map<std::pair<int64_t, int64_t>, int64_t> at;
         int64_t m2 = 0;
@@ -163,12 +163,12 @@ gwo_status Handle::snapshot(const gwo_state_rows *rows, int64_t cap, int64_t *n_
         if (m2 < n) {
             n = m2;
             *n_out = n;
-            GWO_TRY(hipcheck(hipMemcpyAsync(ok.ptr, hk.data(), (size_t)n * 8, hipMemcpyHostToDevice, stream), "dedup"));
-            GWO_TRY(hipcheck(hipMemcpyAsync(os.ptr, hs.data(), (size_t)n * 8, hipMemcpyHostToDevice, stream), "dedup"));
-            GWO_TRY(hipcheck(hipMemcpyAsync(oe.ptr, he.data(), (size_t)n * 8, hipMemcpyHostToDevice, stream), "dedup"));
-            GWO_TRY(hipcheck(hipMemcpyAsync(ow.ptr, hw.data(), (size_t)n * NW * 8, hipMemcpyHostToDevice, stream), "dedup"));
-            GWO_TRY(hipcheck(hipMemcpyAsync(okg.ptr, hg.data(), (size_t)n * 4, hipMemcpyHostToDevice, stream), "dedup"));
-            GWO_TRY(hipcheck(hipMemcpyAsync(ot.ptr, ht.data(), (size_t)n * 4, hipMemcpyHostToDevice, stream), "dedup"));
+            GWO_TRY(hipcheck(copy_in(ok.ptr, hk.data(), (size_t)n * 8, stream), "dedup"));
+            GWO_TRY(hipcheck(copy_in(os.ptr, hs.data(), (size_t)n * 8, stream), "dedup"));
+            GWO_TRY(hipcheck(copy_in(oe.ptr, he.data(), (size_t)n * 8, stream), "dedup"));
+            GWO_TRY(hipcheck(copy_in(ow.ptr, hw.data(), (size_t)n * NW * 8, stream), "dedup"));
+            GWO_TRY(hipcheck(copy_in(okg.ptr, hg.data(), (size_t)n * 4, stream), "dedup"));
+            GWO_TRY(hipcheck(copy_in(ot.ptr, ht.data(), (size_t)n * 4, stream), "dedup"));
             GWO_TRY(hipcheck(hipStreamSynchronize(stream), "dedup"));
         }
     }
@@ -182,7 +182,7 @@ gwo_status Handle::snapshot(const gwo_state_rows *rows, int64_t cap, int64_t *n_
     gwo_status st = GWO_OK;
     for (auto &x : cp)
         if (x.dst && st == GWO_OK)
-            st = hipcheck(hipMemcpyAsync(x.dst, x.src->ptr, x.bytes, hipMemcpyDefault, stream), "snapshot copy");
+            st = hipcheck(copy_out(x.dst, x.src->ptr, x.bytes, stream), "snapshot copy");
     if (st == GWO_OK) st = hipcheck(hipStreamSynchronize(stream), "snapshot sync");
     for (DevBuf *d : {&kg, &k1, &v1, &k2, &v2, &hist, &ok, &os, &oe, &ow, &okg, &ot}) d->release();
     return st;
@@ -220,10 +220,10 @@ gwo_status Handle::restore_impl(const gwo_state_rows *rows, int32_t n_words, int
                   {R.start.data(), rows->window_start, (size_t)n * 8},
                   {R.end.data(), rows->window_end, (size_t)n * 8},
                   {R.words.data(), rows->words, (size_t)n * n_words * 8}};
-        for (auto &x : cp) GWO_TRY(hipcheck(hipMemcpy(x.dst, x.src, x.bytes, hipMemcpyDefault), "restore rows"));
+        for (auto &x : cp) GWO_TRY(hipcheck(fetch_host(x.dst, x.src, x.bytes, stream), "restore rows"));
         if (rows->timer) {
             R.timer.resize(n);
-            GWO_TRY(hipcheck(hipMemcpy(R.timer.data(), rows->timer, (size_t)n * 4, hipMemcpyDefault), "restore timers"));
+            GWO_TRY(hipcheck(fetch_host(R.timer.data(), rows->timer, (size_t)n * 4, stream), "restore timers"));
         }
     }
     // only this subtask's key groups (a rescaled job restores the union of the old subtasks' rows)
@@ -323,9 +323,9 @@ gwo_status Handle::table_restore_rows(const RestoreRows &R, int64_t new_wm) {
         GWO_TRY(ensure_buf(bk, k.size() * 8));
         GWO_TRY(ensure_buf(bs, s.size() * 8));
         GWO_TRY(ensure_buf(bw, w.size() * 8));
-        GWO_TRY(hipcheck(hipMemcpyAsync(bk.ptr, k.data(), k.size() * 8, hipMemcpyHostToDevice, stream), "restore keys"));
-        GWO_TRY(hipcheck(hipMemcpyAsync(bs.ptr, s.data(), s.size() * 8, hipMemcpyHostToDevice, stream), "restore starts"));
-        GWO_TRY(hipcheck(hipMemcpyAsync(bw.ptr, w.data(), w.size() * 8, hipMemcpyHostToDevice, stream), "restore words"));
+        GWO_TRY(hipcheck(copy_in(bk.ptr, k.data(), k.size() * 8, stream), "restore keys"));
+        GWO_TRY(hipcheck(copy_in(bs.ptr, s.data(), s.size() * 8, stream), "restore starts"));
+        GWO_TRY(hipcheck(copy_in(bw.ptr, w.data(), w.size() * 8, stream), "restore words"));
         launch_restore((const int64_t *)bk.ptr, (const int64_t *)bs.ptr, (const int64_t *)bw.ptr, (int64_t)k.size(), plan,
                        geom_now(), (const TableDesc *)dir_buf.ptr, lo, dir_len, stream);
         st = launch_ok("restore");

@@ -69,9 +69,7 @@ gwo_status Handle::intern_utf16(const uint16_t *chars, const int64_t *offsets, i
     std::vector<int64_t> off_copy;
     if (is_device_ptr(offsets)) {
         off_copy.resize((size_t)n + 1);
-        GWO_TRY(hipcheck(hipMemcpyAsync(off_copy.data(), offsets, (size_t)(n + 1) * 8, hipMemcpyDeviceToHost, stream),
-                         "offsets"));
-        GWO_TRY(hipcheck(hipStreamSynchronize(stream), "offsets"));
+        GWO_TRY(hipcheck(copy_out(off_copy.data(), offsets, (size_t)(n + 1) * 8, stream), "offsets"));
         h_off = off_copy.data();
     }
     if (h_off[0] < 0) return fail(GWO_ERR_INVALID_ARGUMENT, "String key offsets must be non-negative and non-decreasing");
@@ -82,15 +80,14 @@ gwo_status Handle::intern_utf16(const uint16_t *chars, const int64_t *offsets, i
     first_last[1] = h_off[n];
     if (!is_device_ptr(offsets)) {
         GWO_TRY(ensure_buf(D.offsets, (size_t)(n + 1) * 8));
-        GWO_TRY(hipcheck(hipMemcpyAsync(D.offsets.ptr, offsets, (size_t)(n + 1) * 8, hipMemcpyHostToDevice, stream),
-                         "stage offsets"));
+        GWO_TRY(hipcheck(copy_in(D.offsets.ptr, offsets, (size_t)(n + 1) * 8, stream), "stage offsets"));
         d_off = (const int64_t *)D.offsets.ptr;
     }
     const uint64_t units = (uint64_t)first_last[1];
     const uint16_t *d_chars = chars;
     if (units > 0 && !is_device_ptr(chars)) {
         GWO_TRY(ensure_buf(D.chars, units * 2));
-        GWO_TRY(hipcheck(hipMemcpyAsync(D.chars.ptr, chars, units * 2, hipMemcpyHostToDevice, stream), "stage chars"));
+        GWO_TRY(hipcheck(copy_in(D.chars.ptr, chars, units * 2, stream), "stage chars"));
         d_chars = (const uint16_t *)D.chars.ptr;
     }
     // capacity: slots at load <= 1/2, arena and id index for every String of the batch being new
@@ -139,14 +136,13 @@ gwo_status Handle::intern_utf16(const uint16_t *chars, const int64_t *offsets, i
         D.h_off.resize(c[0]);
         D.h_len.resize(c[0]);
         D.h_arena.resize(c[1]);
-        GWO_TRY(hipcheck(hipMemcpyAsync(D.h_off.data() + old_count, (int64_t *)D.idx_off.ptr + old_count,
-                                        (c[0] - old_count) * 8, hipMemcpyDeviceToHost, stream), "dict mirror"));
-        GWO_TRY(hipcheck(hipMemcpyAsync(D.h_len.data() + old_count, (int64_t *)D.idx_len.ptr + old_count,
-                                        (c[0] - old_count) * 8, hipMemcpyDeviceToHost, stream), "dict mirror"));
+        GWO_TRY(hipcheck(copy_out(D.h_off.data() + old_count, (int64_t *)D.idx_off.ptr + old_count,
+                                  (c[0] - old_count) * 8, stream), "dict mirror"));
+        GWO_TRY(hipcheck(copy_out(D.h_len.data() + old_count, (int64_t *)D.idx_len.ptr + old_count,
+                                  (c[0] - old_count) * 8, stream), "dict mirror"));
         if (c[1] > old_used)
-            GWO_TRY(hipcheck(hipMemcpyAsync(D.h_arena.data() + old_used, (uint16_t *)D.arena.ptr + old_used,
-                                            (c[1] - old_used) * 2, hipMemcpyDeviceToHost, stream), "dict mirror"));
-        GWO_TRY(hipcheck(hipStreamSynchronize(stream), "dict mirror"));
+            GWO_TRY(hipcheck(copy_out(D.h_arena.data() + old_used, (uint16_t *)D.arena.ptr + old_used,
+                                      (c[1] - old_used) * 2, stream), "dict mirror"));
         D.count = c[0];
         D.arena_used = c[1];
     }
@@ -162,7 +158,7 @@ gwo_status Handle::key_strings(const int64_t *ids, int64_t n, int64_t *offsets_o
     const int64_t *src = ids;
     if (n > 0 && is_device_ptr(ids)) {
         hid.resize(n);
-        GWO_TRY(hipcheck(hipMemcpy(hid.data(), ids, (size_t)n * 8, hipMemcpyDeviceToHost), "ids"));
+        GWO_TRY(hipcheck(copy_out(hid.data(), ids, (size_t)n * 8, stream), "ids"));   // (ordered behind this handle's fires)
         src = hid.data();
     }
     const uint64_t count = dict ? dict->count : 0;
