@@ -1549,7 +1549,11 @@ __global__ __launch_bounds__(LOG_FIRE_THREADS) __attribute__((amdgpu_waves_per_e
                 kt.stamp(3);
             }
         }
-        if (total > (uint32_t)FIRE_RCAP) load_next();   // (the fast path loaded them in P0)
+        // (the fast path loaded them in P0).  Every partition the fast path did not take -- also a small one in a
+        // slow-only fold (a restored window's fire, a checkpoint's or a lateness migration's fold): keyed on the
+        // total instead, a workgroup's second small partition republished its first one's ranges (rows of one
+        // partition twice, another's lost, once a window had more partitions than the grid's 2 per CU)
+        if (!fast) load_next();
         if constexpr (!PART) {
             if (!fast && tid == 0) {   // for the slow instance
                 plist[atomicAdd(pcount, 1u)] = part;

@@ -132,3 +132,44 @@ def test_log_lateness_checkpoint_continues_exactly(F, restore_layout):
     assert sorted(rows + list(c.output)) == want
     assert late + c.num_late_records_dropped == wl
     c.close()
+
+
+def test_migration_and_refires_of_a_window_with_more_partitions_than_the_grid(F):
+    """A window of 1.5M records: more log partitions than the fold's persistent grid (2 workgroups per CU), so each
+    workgroup folds several partitions in turn.  Its fire with allowedLateness > 0 migrates it to a hash table through
+    the slow-only fold (gwo_log.cpp log_migrate); late records then re-fire rows from that table.  Checked row for row
+    against the C restatement of WindowOperator (oracle/window_oracle.c; WindowOperator.java:393-406 re-fires)."""
+    import ctypes as C
+    from flink_amd import _native as N
+    from oracle import cbaseline
+    if not cbaseline.available():
+        import os
+        import subprocess
+        subprocess.run(["make", "-C", os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                                   "oracle")], check=True, capture_output=True)
+    rng = np.random.default_rng(11)
+    n1, n2, size, lateness = 1_500_000, 200_000, 10_000, 5_000
+    k = rng.integers(0, 1_000_000, n1 + n2).astype(np.int64)
+    t = np.concatenate([rng.integers(0, size, n1), rng.integers(0, size, n2)]).astype(np.int64)
+    v = rng.integers(-10**6, 10**6, n1 + n2).astype(np.int64)
+    batches = [(n1, size), (n1 + n2, size + 2_000)]
+    rows, _, late = cbaseline.run_tumbling(k, t, v, batches, size, lateness=lateness, threads=8, max_par=128)
+    want = rows[:, :6]
+    op = _mk(F, size, lateness, "log")
+    lib = N.lib()
+    got = []
+    prev = 0
+    for end, wm in batches + [(n1 + n2, LONG_MAX)]:
+        if end > prev:
+            op.process_batch(k[prev:end], t[prev:end], v[prev:end])
+        prev = end
+        N.check(lib.gwo_advance_watermark(op.handle, wm), op.handle, "gwo_advance_watermark")
+        N.check(lib.gwo_wait_fires(op.handle), op.handle, "gwo_wait_fires")
+        key, start, end_, res = op.drain_arrays()
+        got.append(np.stack([key, start, end_, *res], axis=1))
+    assert op.num_late_records_dropped == late
+    op.close()
+    got = np.concatenate(got)
+    order = lambda a: a[np.lexsort(a.T[::-1])]
+    assert got.shape == want.shape
+    assert (order(got) == order(want)).all()
