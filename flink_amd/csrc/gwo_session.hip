@@ -366,23 +366,35 @@ __global__ __launch_bounds__(64) void sess_process_kernel(const int64_t *__restr
                               0xffffffffu};
 #pragma unroll
             for (int x = 0; x < SESS_BKT_N; ++x) r[x] = x < (int)c ? r[x] : 0xffffffffu;
+            // the network and the gathers sized to the largest bucket among the wave's owner lanes (wave-uniform:
+            // C5's buckets hold 1-3 records mostly, and a 16-wide network and 30 gathers per lane were most of the
+            // lane's instructions)
+            const int P = __ballot(c > 8u) ? 16 : __ballot(c > 4u) ? 8 : __ballot(c > 2u) ? 4 : __ballot(c > 1u) ? 2 : 1;
+            auto bitonic = [&](auto NP) {
+                constexpr int N_ = decltype(NP)::value;
 #pragma unroll
-            for (int kk = 2; kk <= 16; kk <<= 1)
+                for (int kk = 2; kk <= N_; kk <<= 1)
 #pragma unroll
-                for (int jj = kk >> 1; jj > 0; jj >>= 1)
+                    for (int jj = kk >> 1; jj > 0; jj >>= 1)
 #pragma unroll
-                    for (int x = 0; x < 16; ++x) {
-                        const int y = x ^ jj;
-                        if (y > x) {
-                            const uint32_t lo = min(r[x], r[y]), hi = max(r[x], r[y]);
-                            r[x] = (x & kk) == 0 ? lo : hi;
-                            r[y] = (x & kk) == 0 ? hi : lo;
+                        for (int x = 0; x < N_; ++x) {
+                            const int y = x ^ jj;
+                            if (y > x) {
+                                const uint32_t lo = min(r[x], r[y]), hi = max(r[x], r[y]);
+                                r[x] = (x & kk) == 0 ? lo : hi;
+                                r[y] = (x & kk) == 0 ? hi : lo;
+                            }
                         }
-                    }
+            };
+            if (P == 16) bitonic(std::integral_constant<int, 16>{});
+            else if (P == 8) bitonic(std::integral_constant<int, 8>{});
+            else if (P == 4) bitonic(std::integral_constant<int, 4>{});
+            else if (P == 2) bitonic(std::integral_constant<int, 2>{});
             int64_t *R = L + (size_t)g.smax * sw * 64;   // [2 * SESS_BKT_N][64]: (ts, value) of the sorted records
             int64_t rt[SESS_BKT_N], rv[SESS_BKT_N];   // every load issued before the first is used
 #pragma unroll
             for (int x = 0; x < SESS_BKT_N; ++x) {
+                if (x >= P) break;   // (wave-uniform)
                 const uint32_t i = x < (int)c ? r[x] : r[0];
                 rt[x] = ts[i];
                 rv[x] = val ? val[i] : 0;
@@ -452,6 +464,9 @@ __global__ __launch_bounds__(256) void sess_long_kernel(const int64_t *__restric
     __shared__ uint32_t s_idx[SL_CHUNK];   // a chunk's records of the key, in arrival order
     const int sw = 3 + p.nwords;
     const uint32_t nl = ls.ctl[1];
+    // no slot overflowed its bucket (C5: every batch): workgroup 0 alone publishes, with no arrival count
+    const bool none = nl == 0;
+    if (none && blockIdx.x != 0) return;
     for (uint32_t j = blockIdx.x; j < nl; j += gridDim.x) {
         const uint32_t slot = ls.longs[j];
         SessKey K;
@@ -489,11 +504,13 @@ __global__ __launch_bounds__(256) void sess_long_kernel(const int64_t *__restric
     // statistics are device-scope atomics, read back here with read-modify-write atomics (coherent across XCDs)
     // after every workgroup's stores and atomics completed (vmcnt) and its arrival was counted
     __shared__ int s_last;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) s_last = atomicAdd(&ls.ctl[2], 1u) == gridDim.x - 1;
-    __syncthreads();
-    if (!s_last) return;
+    if (!none) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (threadIdx.x == 0) s_last = atomicAdd(&ls.ctl[2], 1u) == gridDim.x - 1;
+        __syncthreads();
+        if (!s_last) return;
+    }
     constexpr int NWD = (int)(sizeof(SessErr) / 8) + 1;
     const unsigned long long live = sess_fold_shards(ls.shards, 0);   // the process kernel's live-session change
     if (threadIdx.x < NWD) {

@@ -1,12 +1,16 @@
-# A/B of library variants on bench_configs.py configurations: CONFIGS (default c2), VARIANTS (base = flink_amd/libgwo.so).
+# A/B of library variants on one bench_configs.py configuration within one GPU call: LIBS="path1 path2" (empty
+# string entry = the product library), CFG (default c5), REPS rounds; each run under its own limit.
 set -o pipefail
 R=$GRAFT_REPO_ROOT
 cd $R
-mkdir -p gpurun_out/cfgab
-for c in ${CONFIGS:-c2}; do
-  for v in ${VARIANTS:-base}; do
-    if [ "$v" = base ]; then L=""; else L=$R/exp/$v/libgwo.so; fi
-    GWO_LIB_PATH=$L timeout -k 10 300 python3 -u bench_configs.py $c > gpurun_out/cfgab/${c}_$v.log 2>&1 || { echo "FAIL $c $v"; tail -20 gpurun_out/cfgab/${c}_$v.log; exit 1; }
-    tail -n 1 gpurun_out/cfgab/${c}_$v.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('$c $v', 'G rec/s %.2f' % (d['value']/1e9), 'ms/step %.4f' % d['ms_per_step'], {k: round(x['total_ms']/max(x['launches'],1)*1e3,1) for k,x in d['kernels_ms'].items()})"
+O=gpurun_out/cfgab
+mkdir -p $O
+for rep in $(seq 1 ${REPS:-2}); do
+  for L in ${LIBS:-product}; do
+    tag=$(echo "$L" | tr '/' '_')
+    lp=$L; [ "$L" = product ] && lp=
+    BENCH_PROF=${BENCH_PROF:-0} GWO_LIB_PATH=$lp timeout -k 10 240 python3 -u bench_configs.py ${CFG:-c5} \
+        > $O/$tag.$rep.log 2>&1 || { echo "FAIL $L"; tail -20 $O/$tag.$rep.log; exit 1; }
+    tail -n 1 $O/$tag.$rep.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('$L', 'ms/step %.4f' % d['ms_per_step'], 'G rec/s %.3f' % (d['value']/1e9))"
   done
 done
