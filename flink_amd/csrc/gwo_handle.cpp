@@ -192,6 +192,7 @@ Handle::~Handle() {
     DeviceGuard g(cfg.device);
     if (stream) (void)hipStreamSynchronize(stream);
     if (fire_stream) (void)hipStreamSynchronize(fire_stream);
+    if (cb_side) (void)hipStreamSynchronize(cb_side);
     if (ktrace) ktrace_report();
     (void)prof_collect();
     for (hipEvent_t e : event_pool) (void)hipEventDestroy(e);
@@ -219,6 +220,10 @@ Handle::~Handle() {
         b->release();
     if (cb_rb) (void)hipHostFree(cb_rb);
     if (cb_ev) (void)hipEventDestroy(cb_ev);
+    for (hipEvent_t e : {cb_ev_main, cb_ev_gather, cb_ev_merge[0], cb_ev_merge[1]})
+        if (e) (void)hipEventDestroy(e);
+    if (cb_side) (void)hipStreamDestroy(cb_side);
+    cb_go.release();
     if (sp_rb) (void)hipHostFree(sp_rb);
     if (sp_ev) (void)hipEventDestroy(sp_ev);
     stage_key.release();

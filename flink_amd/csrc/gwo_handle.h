@@ -189,6 +189,16 @@ struct Handle {
     long long cb_dir_base = 0;
     int use_combine_spec = 1;                                          // GWO_COMBINE_SPEC=0: no speculative merge
     DevBuf cb_spec_dir;                                                // the speculative merge's directory
+    // overlapped pipelining (GWO_CB_OVERLAP=1; off by default: measured slower, profiles/r06_experiments.txt): a
+    // pipelined batch's gather runs on cb_side beside the previous batch's merge, which stays on the handle's
+    // stream -- so everything later on the handle's stream is ordered behind every merge with no join.  cb_side
+    // waits for the handle's stream when a chain starts or this call queued work there (a new table), and for the
+    // merge that last read the dump slot it writes.
+    bool cb_overlap = false;
+    hipStream_t cb_side = nullptr;
+    hipEvent_t cb_ev_main = nullptr, cb_ev_gather = nullptr, cb_ev_merge[2] = {nullptr, nullptr};
+    bool cb_merge_rec[2] = {false, false};
+    DevBuf cb_go;                                                      // [2] per-slot verdicts, [2..9] per-slot incs
     DevBuf cb_dbg;                                                     // GWO_CB_TRACE phase times
     std::vector<TableDesc> cb_spec_host;
     long long cb_spec_base = 0;
@@ -305,6 +315,7 @@ struct Handle {
         unsigned long long seq = 0;
         long long hint = 0;   // units hint, hint + 1: the speculative merge's tables
         int64_t wm = 0;       // the watermark the batch was classified at
+        bool side = false;    // its gather ran on cb_side
     } cb_pend;
     bool pipe_submit = false;   // gwo_set_pipelined_submit
     bool cb_redo = false;       // redoing a batch the pipelined verdict turned down: no pipelining
@@ -359,6 +370,7 @@ struct Handle {
     // sessions (gwo_session.cpp)
     gwo_status sess_alloc(uint64_t cap, Table &t, int64_t **due);
     gwo_status sess_rebuild_due();
+    gwo_status sess_join_sweep();
     gwo_status sess_read_err();
     gwo_status sess_ensure(uint64_t incoming);
     gwo_status sess_ensure_pool(uint64_t n);

@@ -144,6 +144,14 @@ struct CombineArgs {
     // pipelined submission: *go still holds the previous batch's verdict, which the host has not read yet; a no
     // there is a no here too (the host redoes both batches in order)
     int32_t chain;
+    // pipelined submission: the previous batch's verdict word (chain) -- each batch has its own word, so that a merge
+    // queued behind its gather reads its own batch's verdict
+    const uint32_t *go_prev;
+    // overlapped pipelining (the gather on a side stream beside the previous batch's merge): the previous batch's
+    // {hint, keys of unit hint, keys of unit hint + 1} (upper bounds of the entries its merge may still be claiming),
+    // added to the occupancy this verdict reads; this batch's own go to inc_out for the next (NULL: not overlapped)
+    const unsigned long long *inc_prev;
+    unsigned long long *inc_out;
     uint64_t cap[2];                   // capacities of the hint tables
     long long side_cap;
     unsigned long long *dbg;           // GWO_CB_TRACE: phase times on the device wall clock (NULL: off)

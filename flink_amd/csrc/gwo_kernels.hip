@@ -911,15 +911,28 @@ __global__ __launch_bounds__(CB_THREADS) void gather_kernel(GatherArgs A) {
     __syncthreads();
     CB_STAMP(5);
     if (tid == 0) {   // the speculative merge's verdict
-        bool go = kt->a.go != nullptr && (!kt->a.chain || *(volatile const uint32_t *)kt->a.go != 0u) && s_tot[CS_ACC] > 0 && s_tot[CS_BADTS] == 0 && s_tot[CS_BADRANGE] == 0 &&
+        bool go = kt->a.go != nullptr && (!kt->a.chain || *(volatile const uint32_t *)kt->a.go_prev != 0u) && s_tot[CS_ACC] > 0 && s_tot[CS_BADTS] == 0 && s_tot[CS_BADRANGE] == 0 &&
                   s_tot[CS_BADKG] == 0 && s_tot[CS_REFIRE] == 0 && s_tot[CS_HOUT] == 0 && s_spec[0] == 0 &&
                   (!kt->a.side_enabled || (long long)s_spec[1] <= kt->a.side_cap) &&
                   (long long)s_tot[CS_MIN] >= kt->a.hint && (long long)s_tot[CS_MAX] <= kt->a.hint + 1;
+        const unsigned long long *ip = kt->a.inc_prev;
+        unsigned long long incs[2];
+        for (int r = 0; r < 2; ++r) incs[r] = min(s_tot[CS_HIST + r], s_tot[CS_D0 + r]);
         for (int r = 0; r < 2 && go; ++r) {
-            const unsigned long long recs = s_tot[CS_HIST + r];
-            if (!recs) continue;
-            const unsigned long long inc = min(recs, s_tot[CS_D0 + r]);
-            go = kt->a.occ[r] != nullptr && 10 * (s_spec[2 + r] + inc) <= 7 * kt->a.cap[r];   // the host's kMaxLoad 0.7
+            if (!s_tot[CS_HIST + r]) continue;
+            // overlapped: the previous batch's merge may still be claiming its keys of this table (at most its
+            // distinct keys there); the bound is looser, so the limit is 0.9 -- a table never fills (a full one
+            // would leave find_or_insert probing forever)
+            unsigned long long extra = 0;
+            const long long u = kt->a.hint + r;
+            if (ip) extra = (long long)ip[0] == u ? ip[1] : ((long long)ip[0] + 1 == u ? ip[2] : 0ull);
+            go = kt->a.occ[r] != nullptr &&
+                 10 * (s_spec[2 + r] + incs[r] + extra) <= (ip ? 9ull : 7ull) * kt->a.cap[r];   // the host's kMaxLoad 0.7
+        }
+        if (kt->a.inc_out) {
+            kt->a.inc_out[0] = (unsigned long long)kt->a.hint;
+            kt->a.inc_out[1] = incs[0];
+            kt->a.inc_out[2] = incs[1];
         }
         if (kt->a.go) *kt->a.go = go ? 1u : 0u;
         rb_put(&kt->a.rb[CB_RB_GO], go ? 1ull : 0ull);

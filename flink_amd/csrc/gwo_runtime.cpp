@@ -297,6 +297,7 @@ gwo_status Handle::prof_collect() {
     if (pending_events.empty()) return GWO_OK;
     GWO_TRY(hipcheck(hipStreamSynchronize(stream), "prof sync"));
     if (fire_stream) GWO_TRY(hipcheck(hipStreamSynchronize(fire_stream), "prof sync"));
+    if (cb_side) GWO_TRY(hipcheck(hipStreamSynchronize(cb_side), "prof sync"));
     if (logst && logst->split_stream) GWO_TRY(hipcheck(hipStreamSynchronize(logst->split_stream), "prof sync"));
     for (auto &pe : pending_events) {
         float ms = 0.f;
@@ -443,12 +444,23 @@ gwo_status Handle::insert_combined(const int64_t *k, const int64_t *t, const int
     if (!cb_max_wg) {
         cb_max_wg = 4 * cb_cus;
         if (const char *e = getenv("GWO_CB_WG")) cb_max_wg = std::max(1, atoi(e));
+        if (const char *e = getenv("GWO_CB_OVERLAP")) cb_overlap = atoi(e) != 0;
     }
     const int G = (int)std::max<int64_t>(1, std::min<int64_t>((n + tile - 1) / tile, (int64_t)cb_max_wg));
     int S = 2048;   // (4096-slot tables where one workgroup per CU leaves the LDS: no faster, the merge slower)
     while (S > 256 && gather_lds_bytes(S, NW) > 65536 + 512) S >>= 1;   // (tables + 64 spare words)
-    GWO_TRY(ensure_buf(cb_dump_key, (size_t)G * 2 * S * 8 + (size_t)G * 4));
-    GWO_TRY(ensure_buf(cb_dump_acc, (size_t)G * 2 * S * NW * 8));
+    // pipelined: a dump region per readback slot (the previous batch's merge may still read the other one)
+    const bool pipe = combine_pipe_ok(k, t, v);
+    const bool overlap = pipe && cb_overlap && use_combine_spec;
+    const size_t key_region = ((size_t)G * 2 * S * 8 + (size_t)G * 4 + 255) & ~(size_t)255;
+    const size_t acc_region = ((size_t)G * 2 * S * NW * 8 + 255) & ~(size_t)255;
+    if (overlap && cb_side && (cb_dump_key.bytes < 2 * key_region || cb_dump_acc.bytes < 2 * acc_region)) {
+        // (a reallocation frees the regions in-flight work may read)
+        GWO_TRY(hipcheck(hipStreamSynchronize(cb_side), "gather sync"));
+        GWO_TRY(hipcheck(hipStreamSynchronize(stream), "merge sync"));
+    }
+    GWO_TRY(ensure_buf(cb_dump_key, 2 * key_region));
+    GWO_TRY(ensure_buf(cb_dump_acc, 2 * acc_region));
     GWO_TRY(ensure_buf(cb_ovf, (size_t)n * 4));
     if (!cb_ctr.ptr) {   // counters and statistics shards start reset; every gather leaves them reset
         GWO_TRY(ensure_buf(cb_ctr, 32));   // listed-record count, finished workgroups, speculation verdict
@@ -462,9 +474,14 @@ gwo_status Handle::insert_combined(const int64_t *k, const int64_t *t, const int
         GWO_TRY(ensure_buf(cb_blk, (size_t)words * 8));
         GWO_TRY(hipcheck(hipMemcpy(cb_blk.ptr, init.data(), (size_t)words * 8, hipMemcpyHostToDevice), "shards"));
     }
+    if (!cb_go.ptr) {   // per-slot verdicts [0..1] and per-slot {hint, incs} [2..9]
+        GWO_TRY(ensure_buf(cb_go, 16 * 8));
+        GWO_TRY(hipcheck(hipMemsetAsync(cb_go.ptr, 0, 16 * 8, stream), "verdicts"));
+    }
+    const int slot = cb_pend.active ? (cb_pend.slot ^ 1) : 0;
     CombineArgs a{};
-    a.dump_key = (int64_t *)cb_dump_key.ptr;
-    a.dump_acc = (int64_t *)cb_dump_acc.ptr;
+    a.dump_key = (int64_t *)((char *)cb_dump_key.ptr + (size_t)slot * key_region);
+    a.dump_acc = (int64_t *)((char *)cb_dump_acc.ptr + (size_t)slot * acc_region);
     a.dump_used = (uint32_t *)(a.dump_key + (size_t)G * 2 * S);
     a.ovf = (uint32_t *)cb_ovf.ptr;
     a.ovf_count = (unsigned long long *)cb_ctr.ptr;
@@ -483,8 +500,6 @@ gwo_status Handle::insert_combined(const int64_t *k, const int64_t *t, const int
         GWO_TRY(hipcheck(hipEventCreateWithFlags(&cb_ev, hipEventDisableTiming), "event"));
     }
     // pipelined: the previous batch's readback slot is still unread, so this batch takes the other one
-    const bool pipe = combine_pipe_ok(k, t, v);
-    const int slot = cb_pend.active ? (cb_pend.slot ^ 1) : 0;
     unsigned long long *const rb = cb_rb + (size_t)slot * CB_RB_WORDS;
     a.rb = cb_rb_dev + (size_t)slot * CB_RB_WORDS;
     a.seq = ++cb_seq;
@@ -492,12 +507,15 @@ gwo_status Handle::insert_combined(const int64_t *k, const int64_t *t, const int
     a.side_enabled = side_enabled();
     // tumbling: the next window's table exists before its first records arrive (sized like the last retired one),
     // so the batch that crosses into it keeps the speculative merge (and a pipelined batch needs no redo)
+    bool main_work = false;   // work queued on the handle's stream by this call that the gather must follow
     if (cfg.assigner == GWO_ASSIGNER_TUMBLING && use_combine_spec && !slide && tables.count(hist_hint) &&
         !tables.count(hist_hint + 1)) {
         const __int128 end1 = (__int128)(hist_hint + 2) * cfg.size + geom.unit_off_mod;   // window hint + 1's end
         if (end1 - 1 > (__int128)wm && end1 <= (__int128)(int64_t)0x7fffffffffffffffLL &&
-            end1 - cfg.size >= (__int128)(int64_t)0x8000000000000000LL)
+            end1 - cfg.size >= (__int128)(int64_t)0x8000000000000000LL) {
             GWO_TRY(ensure_table(hist_hint + 1, 0));
+            main_work = true;
+        }
     }
     Table *hint_tab[2] = {nullptr, nullptr};
     for (int j = 0; j < 2; ++j) {
@@ -545,6 +563,15 @@ gwo_status Handle::insert_combined(const int64_t *k, const int64_t *t, const int
             cb_spec_base = hist_hint;
         }
         a.go = (uint32_t *)((unsigned long long *)cb_ctr.ptr + 2);
+        a.go_prev = a.go;
+        if (pipe) {   // a verdict word per slot: the merge behind this gather reads this batch's
+            a.go = (uint32_t *)((unsigned long long *)cb_go.ptr + slot);
+            a.go_prev = (const uint32_t *)((unsigned long long *)cb_go.ptr + (slot ^ 1));
+        }
+        if (overlap) {
+            a.inc_out = (unsigned long long *)cb_go.ptr + 2 + 4 * slot;
+            if (cb_pend.active) a.inc_prev = (const unsigned long long *)cb_go.ptr + 2 + 4 * (slot ^ 1);
+        }
     }
     static const int cb_trace = getenv("GWO_CB_TRACE") ? atoi(getenv("GWO_CB_TRACE")) : 0;
     std::vector<unsigned long long> h_dbg;
@@ -553,12 +580,32 @@ gwo_status Handle::insert_combined(const int64_t *k, const int64_t *t, const int
         GWO_TRY(hipcheck(hipMemset(cb_dbg.ptr, 0, (size_t)G * 64), "trace"));
         a.dbg = (unsigned long long *)cb_dbg.ptr;
     }
-    prof_begin(GWO_KERNEL_SCAN);
+    hipStream_t gs = stream;
+    if (overlap) {
+        if (!cb_side) {
+            GWO_TRY(hipcheck(hipStreamCreateWithFlags(&cb_side, hipStreamNonBlocking), "gather stream"));
+            for (hipEvent_t *e : {&cb_ev_main, &cb_ev_gather, &cb_ev_merge[0], &cb_ev_merge[1]})
+                GWO_TRY(hipcheck(hipEventCreateWithFlags(e, hipEventDisableTiming), "event"));
+            // a producer stream named to gwo_wait_stream before this point is covered by the join below
+        }
+        if (!cb_pend.active || main_work) {   // a chain starts (or a table was made): behind the handle's stream
+            GWO_TRY(hipcheck(hipEventRecord(cb_ev_main, stream), "event"));
+            GWO_TRY(hipcheck(hipStreamWaitEvent(cb_side, cb_ev_main, 0), "event wait"));
+        }
+        if (cb_merge_rec[slot])   // the merge that read this dump slot and verdict word
+            GWO_TRY(hipcheck(hipStreamWaitEvent(cb_side, cb_ev_merge[slot], 0), "event wait"));
+        gs = cb_side;
+    }
+    prof_begin(GWO_KERNEL_SCAN, gs);
     launch_gather(k, t, v, n, g, plan, a, G, d_stats, (int64_t *)side_key.ptr, (int64_t *)side_ts.ptr,
-                  (int64_t *)side_val.ptr, d_side_count, side_enabled() ? side_cap : 0, side_enabled(), stream);
+                  (int64_t *)side_val.ptr, d_side_count, side_enabled() ? side_cap : 0, side_enabled(), gs);
     GWO_TRY(launch_ok("gather"));
-    prof_end(GWO_KERNEL_SCAN, n);
+    prof_end(GWO_KERNEL_SCAN, n, gs);
     if (spec) {
+        if (overlap) {   // the merge follows its gather (and, on the handle's stream, every earlier merge)
+            GWO_TRY(hipcheck(hipEventRecord(cb_ev_gather, gs), "event"));
+            GWO_TRY(hipcheck(hipStreamWaitEvent(stream, cb_ev_gather, 0), "event wait"));
+        }
         RingDesc none{};
         none.lo = 1;
         none.hi = 0;
@@ -566,6 +613,10 @@ gwo_status Handle::insert_combined(const int64_t *k, const int64_t *t, const int
         launch_merge(k, t, v, g, plan, a, G, 0, (const TableDesc *)cb_spec_dir.ptr, hist_hint, 2, none, a.go, stream);
         GWO_TRY(launch_ok("merge"));
         prof_end(GWO_KERNEL_INSERT, n);
+        if (overlap) {
+            GWO_TRY(hipcheck(hipEventRecord(cb_ev_merge[slot], stream), "event"));
+            cb_merge_rec[slot] = true;
+        }
     }
     if (pipe) {
         CbPend Q;
@@ -578,6 +629,7 @@ gwo_status Handle::insert_combined(const int64_t *k, const int64_t *t, const int
         Q.seq = a.seq;
         Q.hint = hist_hint;
         Q.wm = g.wm;
+        Q.side = overlap;
         *done = true;
         if (!cb_pend.active) {   // nothing to complete: return with this batch in flight
             cb_pend = Q;
@@ -591,7 +643,7 @@ gwo_status Handle::insert_combined(const int64_t *k, const int64_t *t, const int
         }
         // the previous batch's verdict was no, so this one's is too (chained) and neither merge ran: once this
         // gather is done, both go through the regular path, in order
-        GWO_TRY(spin_seq(rb + CB_RB_SEQ, Q.seq, "gather"));
+        GWO_TRY(spin_seq(rb + CB_RB_SEQ, Q.seq, "gather", gs));
         const CbPend P = cb_pend;   // (a turned-down batch stays in cb_pend)
         cb_pend.active = false;
         cb_redo = true;
@@ -734,7 +786,7 @@ bool Handle::combine_pipe_ok(const int64_t *k, const int64_t *t, const int64_t *
 gwo_status Handle::combine_resolve_pending(bool *go) {
     const CbPend &P = cb_pend;
     const unsigned long long *rb = cb_rb + (size_t)P.slot * CB_RB_WORDS;
-    GWO_TRY(spin_seq(rb + CB_RB_SEQ, P.seq, "gather"));
+    GWO_TRY(spin_seq(rb + CB_RB_SEQ, P.seq, "gather", P.side ? cb_side : nullptr));
     *go = rb[CB_RB_GO] != 0;
     if (!*go) return GWO_OK;
     memcpy(h_stats, rb, sizeof(BatchStats));
@@ -1441,6 +1493,8 @@ gwo_status gwo_wait_stream(gwo_handle *hh, void *producer) {
     if ((hipStream_t)producer == h->stream) return GWO_OK;
     if (!h->ev_input) GWO_TRY(h->hipcheck(hipEventCreateWithFlags(&h->ev_input, hipEventDisableTiming), "event"));
     GWO_TRY(h->hipcheck(hipEventRecord(h->ev_input, (hipStream_t)producer), "wait_stream record"));
+    if (h->cb_side)   // the pipelined combine path's gathers run there (gwo_set_pipelined_submit)
+        GWO_TRY(h->hipcheck(hipStreamWaitEvent(h->cb_side, h->ev_input, 0), "wait_stream"));
     return h->hipcheck(hipStreamWaitEvent(h->stream, h->ev_input, 0), "wait_stream");
 }
 

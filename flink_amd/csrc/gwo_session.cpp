@@ -69,6 +69,14 @@ struct SessionState {
     // published but not read yet -- read at the watermark right after its sweep is queued, or at any other call
     bool rb_pending = false;
     uint64_t pend_n = 0;
+    // the watermark sweep on the handle's fire_stream (pipelined submission, allowedLateness 0, no side output;
+    // GWO_SESS_SIDE_SWEEP=1 only: measured slower, profiles/r06_experiments.txt): the next batch's slot pass -- it
+    // claims entries and fills buckets, neither of which the sweep reads or writes (a slot's due watermark is SESS_NONE until its key has
+    // sessions) -- overlaps it, and the stream joins the sweep (ev_fire) before anything that reads or writes
+    // sessions, entries' contents or the pool (sess_join_sweep)
+    bool side_sweep = false;
+    bool sweep_on_side = false;     // a sweep queued on fire_stream that the handle's stream has not joined yet
+    hipStream_t sweep_stream = nullptr;   // the stream of the last sweep (its readback spin polls it)
 };
 
 static constexpr unsigned long long kSessLongMax = 32;   // sess_long_kernel runs 32 workgroups
@@ -98,6 +106,7 @@ gwo_status Handle::session_init() {
     SessionState &S = *sess;
     if (const char *e = getenv("GWO_SESSION_SLOTS")) S.smax = std::max(1, std::min(16, atoi(e)));
     if (const char *e = getenv("GWO_SESS_DIGITS")) S.sort_digits = atoi(e) == 10 ? 10 : 8;
+    if (const char *e = getenv("GWO_SESS_SIDE_SWEEP")) S.side_sweep = atoi(e) != 0;
     if (const char *e = getenv("GWO_SESS_LISTS")) {
         S.lists = atoi(e) != 0;
         S.lists_auto = false;
@@ -119,6 +128,8 @@ gwo_status Handle::session_init() {
     memset(S.rbf, 0, sizeof(SessErr) + 8);
     GWO_TRY(hipcheck(hipHostGetDevicePointer((void **)&S.rbf_dev, S.rbf, 0), "fire readback"));
     GWO_TRY(hipcheck(hipEventCreateWithFlags(&ev_fire, hipEventDisableTiming), "event"));
+    if (!fire_stream) GWO_TRY(hipcheck(hipStreamCreateWithFlags(&fire_stream, hipStreamNonBlocking), "fire stream"));
+    if (!ev_main) GWO_TRY(hipcheck(hipEventCreateWithFlags(&ev_main, hipEventDisableTiming), "event"));
     GWO_TRY(hipcheck(hipHostMalloc((void **)&S.rb, sizeof(SessErr) + 16, hipHostMallocCoherent | hipHostMallocMapped),
                      "session readback"));
     memset(S.rb, 0, sizeof(SessErr) + 16);
@@ -211,6 +222,7 @@ gwo_status Handle::sess_ensure_pool(uint64_t n) {
     SessionState &S = *sess;
     const uint64_t need = 4 * (S.live + n);
     if (S.pool_cap - S.pool_top >= need) return GWO_OK;
+    GWO_TRY(sess_join_sweep());   // the sweep reads and writes the spilled lists
     const uint64_t ncap = std::max<uint64_t>(6 * (S.live + n), 1 << 16);
     const int sw = 3 + plan.nwords;
     int64_t *np = nullptr;
@@ -231,6 +243,15 @@ gwo_status Handle::sess_ensure_pool(uint64_t n) {
     return GWO_OK;
 }
 
+// The handle's stream waits (on the device) for a sweep queued on fire_stream: before any launch that reads or writes
+// sessions, entry contents, due watermarks or the pool.
+gwo_status Handle::sess_join_sweep() {
+    SessionState &S = *sess;
+    if (!S.sweep_on_side) return GWO_OK;
+    S.sweep_on_side = false;
+    return hipcheck(hipStreamWaitEvent(stream, ev_fire, 0), "sweep join");
+}
+
 // Grow the per-key table (dropping keys without sessions) so `incoming` new keys fit.
 gwo_status Handle::sess_ensure(uint64_t incoming) {
     SessionState &S = *sess;
@@ -242,6 +263,7 @@ gwo_status Handle::sess_ensure(uint64_t incoming) {
     GWO_TRY(read_occupancy_one(S.T));
     S.occ_pending = incoming;
     if ((double)(S.T.occ + incoming) <= kMaxLoad * (double)S.T.cap) return GWO_OK;
+    GWO_TRY(sess_join_sweep());   // the compaction reads every entry
     uint64_t need = std::min<uint64_t>(S.T.occ, S.live) + incoming;
     uint64_t cap = kMinCap;
     while ((double)need > kInitLoad * (double)cap) cap <<= 1;
@@ -263,6 +285,7 @@ gwo_status Handle::sess_ensure(uint64_t incoming) {
 // Every slot's due watermark recomputed from the entries (after entries were written outside the hot path).
 gwo_status Handle::sess_rebuild_due() {
     SessionState &S = *sess;
+    GWO_TRY(sess_join_sweep());
     launch_sess_due(desc(S.T), S.T.cap, S.stride, 3 + plan.nwords, sess_geom(*this, S.smax), stream);
     return launch_ok("session due");
 }
@@ -312,6 +335,7 @@ gwo_status Handle::insert_session(const int64_t *k, const int64_t *t, const int6
     launch_sess_slot(k, t, n, desc(S.T), S.T.cap, S.stride, g, (uint32_t *)S.rec_slot.ptr, S.d_err, lists ? &ls : nullptr,
                      stream);
     GWO_TRY(launch_ok("sess slot"));
+    GWO_TRY(sess_join_sweep());   // the slot pass overlapped the sweep; the rest of the batch follows it
     if (lists) {
         launch_sess_process(k, t, v, n, (const uint32_t *)S.rec_slot.ptr, nullptr, desc(S.T), S.T.cap, S.stride, plan, rplan, g, o, S.d_err, sk,
                             sts, sv, d_side_count, scap, &ls, stream);
@@ -407,12 +431,21 @@ gwo_status Handle::fire_session(int64_t new_wm) {
     SessGeom g = sess_geom(*this, S.smax);
     g.wm = new_wm;
     S.reset_behind_fire = false;
-    prof_begin(GWO_KERNEL_FIRE);
+    const bool side = S.side_sweep && S.lists && pipe_submit && cfg.allowed_lateness == 0 && !side_enabled();
+    hipStream_t fs = stream;
+    if (side) {   // behind everything queued so far (the batch's kernels, the output reservation)
+        GWO_TRY(hipcheck(hipEventRecord(ev_main, stream), "event"));
+        GWO_TRY(hipcheck(hipStreamWaitEvent(fire_stream, ev_main, 0), "event wait"));
+        fs = fire_stream;
+    }
+    prof_begin(GWO_KERNEL_FIRE, fs);
     launch_sess_fire(desc(S.T), S.T.cap, S.stride, plan, rplan, g, out_cols(), S.d_err_fire, S.arr, S.shards,
-                     S.rbf_dev, ++S.rbf_seq, stream);
+                     S.rbf_dev, ++S.rbf_seq, fs);
     GWO_TRY(launch_ok("sess fire"));
-    prof_end(GWO_KERNEL_FIRE, (int64_t)S.T.cap);
-    GWO_TRY(hipcheck(hipEventRecord(ev_fire, stream), "event"));   // poll_fire's completion test
+    prof_end(GWO_KERNEL_FIRE, (int64_t)S.T.cap, fs);
+    GWO_TRY(hipcheck(hipEventRecord(ev_fire, fs), "event"));   // poll_fire's completion test (and the join)
+    S.sweep_on_side = side;
+    S.sweep_stream = fs;
     fire_pending = true;
     return sess_resolve();
 }
@@ -421,7 +454,8 @@ gwo_status Handle::session_finish_fire() {
     SessionState &S = *sess;
     fire_pending = false;
     constexpr int NW = (int)(sizeof(SessErr) / 8);
-    GWO_TRY(spin_seq(S.rbf + NW, S.rbf_seq, "session fire readback"));
+    GWO_TRY(spin_seq(S.rbf + NW, S.rbf_seq, "session fire readback", S.sweep_stream));
+    GWO_TRY(sess_join_sweep());   // (complete: the join only keeps the stream's order explicit)
     memcpy(S.h_err_fire, S.rbf, sizeof(SessErr));
     const unsigned long long emitted = S.h_err_fire->emitted - S.fire_prev.emitted;
     S.live += S.h_err_fire->live_delta - S.fire_prev.live_delta;
