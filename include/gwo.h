@@ -309,10 +309,10 @@ gwo_status gwo_key_strings(gwo_handle *h, const int64_t *ids, int64_t n, int64_t
  * What moves is error reporting: a batch's GWO_ERR_NO_TIMESTAMP / GWO_ERR_KEY_GROUP is returned by the
  * next call on the handle (the batch is still rejected before any window state changes, and the handle
  * stays failed).  Device columns stay borrowed until that next call returns.
- * Readiness when pipelined: the combine path's gather runs on a second stream of the handle, beside the previous
- * batch's merge, so a pipelined batch's device columns must be complete before the call or named with
- * gwo_wait_stream (which orders both of the handle's streams); producing them on the handle's stream itself is
- * not enough here. */
+ * Readiness when pipelined: the combine path's gather may run on a second stream of the handle, beside the
+ * previous batch's merge (GWO_CB_OVERLAP=1; off by default), so a pipelined batch's device columns must be complete
+ * before the call or named with gwo_wait_stream (which orders both of the handle's streams); producing them on the
+ * handle's stream itself is not enough there. */
 gwo_status gwo_set_pipelined_submit(gwo_handle *h, int32_t enabled);
 
 /* Per-kernel HIP-event timing, for bench.py's roofline (off by default). */
