@@ -193,6 +193,31 @@ def test_c5_sessions_100k_keys_10m_records(F, variant):
     _compare(counts, sums, kept, srows, scs, rows, 4)
 
 
+def test_sessions_600k_keys_multi_round_sweep(F):
+    """A session table of 2^21 slots (600K keys): the watermark sweep's persistent grid (256 workgroups x 256 threads
+    x 8 slots = 2^19 slots per round) takes four rounds per watermark, each with its own due-slot compaction and row
+    reservation -- C5's 100K keys fit one round.  Rows per watermark and the final rows against the C restatement
+    (MergingWindowSet.java:156-225, WindowOperator.java:430-473)."""
+    import torch
+    from flink_amd import _native as N
+    from oracle import gen as G
+    k, t, v, _ = G.session_stream(600_000, 6_000_000, gap=30_000, lag=5_000, seed=7)
+    batches = _event_watermarks(t, 10_000, 5_000) + [(len(k), LONG_MAX)]
+    key, ts, val = (torch.from_numpy(np.ascontiguousarray(x)).cuda() for x in (k, t, v))
+    agg = F.MultiAggregate(F.SumAggregate(), F.CountAggregate(), F.MinAggregate(), F.MaxAggregate())
+    op = F.GpuWindowOperator(F.EventTimeSessionWindows.withGap(30_000), agg, max_parallelism=128,
+                             expected_keys=600_000)
+    nb = len(batches)
+    counts, sums, kept = _run_steps(N, op.handle, key, ts, val, batches, 4, set(range(nb)))
+    late_gpu = op.num_late_records_dropped
+    op.close()
+    rows, srows, scs, late = cbaseline.run_sessions(k, t, v, batches, 30_000, 0, ["sum", "count", "min", "max"],
+                                                    THREADS, 128, keep_steps=range(nb + 1))
+    assert late_gpu == late
+    assert int(rows[:, 4].sum()) == len(k) - late
+    _compare(counts, sums, kept, srows, scs, rows, 4)
+
+
 @pytest.mark.parametrize("pipelined", [False, True])
 def test_c2_ysb_campaign_count_1m_batches(F, pipelined):
     """pipelined: gwo_set_pipelined_submit -- each batch's gather and speculative merge queue before the previous
