@@ -344,7 +344,10 @@ __device__ __forceinline__ void k1_plan_tail(unsigned long long *cursor, BatchSt
 #define K1_WPE_ATTR(R)
 #endif
 template <bool HASV, int S, bool ROUTE, bool TS32, bool V2>   // S: record stride in int64 words (1: SoA columns, 3: {key, ts, value}; 0: runtime)
-__global__ __launch_bounds__(LOG_K1_THREADS, ROUTE ? 1 : 2) K1_WPE_ATTR(ROUTE) void log_part_kernel(
+#ifndef GWO_K1_ROUTE_WG
+#define GWO_K1_ROUTE_WG 1   // routed instances: workgroups per CU the register budget is set for (2: spills, A/B)
+#endif
+__global__ __launch_bounds__(LOG_K1_THREADS, ROUTE ? GWO_K1_ROUTE_WG : 2) K1_WPE_ATTR(ROUTE) void log_part_kernel(
     const int64_t *__restrict__ key, const int64_t *__restrict__ ts, const int64_t *__restrict__ val, int64_t n,
     int64_t stride, WindowGeom g, long long base, int nunits, unsigned long long *__restrict__ cursor, uint64_t cap,
     int64_t *__restrict__ tmp, BatchStats *st, int64_t *side_key, int64_t *side_ts, int64_t *side_val,
