@@ -345,7 +345,8 @@ __device__ __forceinline__ void k1_plan_tail(unsigned long long *cursor, BatchSt
 #endif
 template <bool HASV, int S, bool ROUTE, bool TS32, bool V2>   // S: record stride in int64 words (1: SoA columns, 3: {key, ts, value}; 0: runtime)
 #ifndef GWO_K1_ROUTE_WG
-#define GWO_K1_ROUTE_WG 1   // routed instances: workgroups per CU the register budget is set for (2: spills, A/B)
+#define GWO_K1_ROUTE_WG 2   // routed instances: 2 workgroups per CU, with 52-140 B of spills per lane (1: no spills,
+                            // one per CU -- routed K1 7-15 % slower, profiles/r06_experiments.txt)
 #endif
 __global__ __launch_bounds__(LOG_K1_THREADS, ROUTE ? GWO_K1_ROUTE_WG : 2) K1_WPE_ATTR(ROUTE) void log_part_kernel(
     const int64_t *__restrict__ key, const int64_t *__restrict__ ts, const int64_t *__restrict__ val, int64_t n,
