@@ -46,6 +46,10 @@ static_assert(LOG_K1_TILE <= 65536, "K1 ranks within a tile are 16-bit");
 #endif
 #define FIRE_RPT 7                                   // records per thread in the fire's register prefetch
 #define FIRE_RCAP (FIRE_RPT * LOG_FIRE_THREADS)      // 3584: records per partition of the fire's fast path
+#ifndef FIRE_EMIT_V
+#define FIRE_EMIT_V 4                                // values per row the direct emit reads unconditionally
+#endif
+static_assert(FIRE_EMIT_V <= 8, "the direct emit's unclamped reads stay inside the fire's LDS");
 #define FIRE_OWN_LOG2 13
 #define FIRE_OWN (1 << FIRE_OWN_LOG2)                // election table slots of the fire's fast path
 #define FIRE_LDS (FIRE_RCAP * 8 * 2 + (FIRE_RCAP + 4) * 4)   // fast-path dynamic LDS: keys, values, counts (70 KiB)

@@ -1732,20 +1732,21 @@ __global__ __launch_bounds__(LOG_FIRE_THREADS) __attribute__((amdgpu_waves_per_e
                 const uint32_t n = valid ? nxt - off : 0u;
                 int64_t si = 0, mn = 0x7fffffffffffffffLL, mx = (int64_t)0x8000000000000000LL;
                 if (has_val) {
-                    // the run's first 4 values, unclamped (adjacent reads pair into ds_read2_b64): off <= FIRE_RCAP, and
-                    // s_val[FIRE_RCAP ..] is the s_own / s_cnt area, inside the allocation (values past n are unused)
-                    int64_t v4[4];
+                    // the run's first FIRE_EMIT_V values, unclamped (adjacent reads pair into ds_read2_b64): off <=
+                    // FIRE_RCAP, and s_val[FIRE_RCAP ..] is the s_own / s_cnt area, inside the allocation (values past
+                    // n are unused); the rest in a loop, which a wave runs as long as its longest run
+                    int64_t v4[FIRE_EMIT_V];
 #pragma unroll
-                    for (int t = 0; t < 4; ++t) v4[t] = s_val[off + t];
+                    for (int t = 0; t < FIRE_EMIT_V; ++t) v4[t] = s_val[off + t];
 #pragma unroll
-                    for (int t = 0; t < 4; ++t) {
+                    for (int t = 0; t < FIRE_EMIT_V; ++t) {
                         const bool in = (uint32_t)t < n;
                         const int64_t v = v4[t];
                         si = (int64_t)((uint64_t)si + (uint64_t)(in ? v : 0));
                         mn = (in && v < mn) ? v : mn;
                         mx = (in && v > mx) ? v : mx;
                     }
-                    for (uint32_t t = 4; t < n; ++t) {
+                    for (uint32_t t = FIRE_EMIT_V; t < n; ++t) {
                         const int64_t v = s_val[off + t];
                         si = (int64_t)((uint64_t)si + (uint64_t)v);
                         mn = v < mn ? v : mn;
