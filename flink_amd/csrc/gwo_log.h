@@ -46,6 +46,9 @@ static_assert(LOG_K1_TILE <= 65536, "K1 ranks within a tile are 16-bit");
 #endif
 #define FIRE_RPT 7                                   // records per thread in the fire's register prefetch
 #define FIRE_RCAP (FIRE_RPT * LOG_FIRE_THREADS)      // 3584: records per partition of the fire's fast path
+#ifndef FIRE_P3_BCAST
+#define FIRE_P3_BCAST 1                              // P3: followers' unused election-table read at word 0
+#endif
 #ifndef FIRE_EMIT_V
 #define FIRE_EMIT_V 4                                // values per row the direct emit reads unconditionally
 #endif

@@ -1496,7 +1496,11 @@ __global__ __launch_bounds__(LOG_FIRE_THREADS) __attribute__((amdgpu_waves_per_e
                 uint32_t run = 0;
 #pragma unroll
                 for (int r = 0; r < FIRE_RPT; ++r) {   // (an unconditional read: a read under a branch is waited at the join)
+#if FIRE_P3_BCAST   // followers read word 0 (their value is unused): one broadcast address instead of scattered ones
+                    const uint32_t ow = s_own[((leader >> r) & 1u) ? sl[r] : 0u];
+#else
                     const uint32_t ow = s_own[sl[r]];   // followers: sl = a record index, a valid slot too
+#endif
                     const uint32_t x = ((leader >> r) & 1u) ? ((ow >> 12) | 0x10000u) : 0u;
                     xl[r] = run;
                     run += x;
