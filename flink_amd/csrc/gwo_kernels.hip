@@ -468,6 +468,9 @@ __global__ __launch_bounds__(256) void insert_preagg_kernel(const int64_t *__res
 #ifndef CB_MERGE_RUN
 #define CB_MERGE_RUN 8
 #endif
+#ifndef CB_MERGE_EAGER
+#define CB_MERGE_EAGER 1
+#endif
 #define CB_SHARDS 16      // statistics shards (gather)
 #define CB_HOT 8          // lanes of one (unit, key) in a wave that take the wave pre-reduction
 
@@ -983,14 +986,19 @@ __global__ __launch_bounds__(256) void merge_kernel(const int64_t *__restrict__ 
             if (u >= ring.lo && u <= ring.hi) apply_ring(ring, p, run_k, run);
         };
         // the first CB_MW accumulator words of every entry load before any is folded (one round trip, not one
-        // per entry); further words, if any, load in the fold
+        // per entry); further words, if any, load in the fold.  CB_MERGE_EAGER: issued with the keys, not behind
+        // them (an empty slot's words are never written: read and ignored -- inside the dump allocation)
         constexpr int CB_MW = 2;
         int64_t av[CB_MERGE_RUN][CB_MW];
 #pragma unroll
         for (int j = 0; j < CB_MERGE_RUN; ++j)
 #pragma unroll
             for (int w = 0; w < CB_MW; ++w)
+#if CB_MERGE_EAGER
+                av[j][w] = live && w0 + j < G && w < NW ? a.dump_acc[((size_t)(w0 + j) * slots + slot) * NW + w] : 0;
+#else
                 av[j][w] = k[j] != GWO_EMPTY_KEY && w < NW ? a.dump_acc[((size_t)(w0 + j) * slots + slot) * NW + w] : 0;
+#endif
 #pragma unroll
         for (int j = 0; j < CB_MERGE_RUN; ++j) {
             if (k[j] == GWO_EMPTY_KEY) continue;
