@@ -29,7 +29,10 @@ void launch_sess_pool_compact(const TableDesc &t, uint64_t cap, int stride, int 
 void launch_sess_due(const TableDesc &t, uint64_t cap, int stride, int sw, const SessGeom &g, hipStream_t s);
 
 struct SessionState {
-    int smax = 8;
+    // in-flight sessions held inline per key entry (GWO_SESSION_SLOTS); a key with more spills into the pool.  C5 at
+    // 8 / 4 / 2 slots: 0.0548-0.0559 / 0.0527-0.0531 / 0.0517-0.0524 ms/step (profiles/r06_experiments.txt) -- a
+    // batch loads and writes back every inline slot of a touched key, and C5's keys hold 1-2 sessions at a time
+    int smax = 2;
     int stride = 0;
     Table T;
     int64_t *due = nullptr;         // [T.cap + 1] due watermark per slot (SessGeom::due)
