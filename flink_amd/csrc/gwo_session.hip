@@ -189,11 +189,15 @@ __device__ __forceinline__ void sess_key_begin_bulk(SessKey &K, int64_t *e, int6
 }
 
 // Record (k, tsi, v) applied to its key's sessions: WindowOperator.processElement's merging branch.
+// NWT: the plan's accumulator words at compile time (1-4; 0: p.nwords at run time) -- the word loops unroll.
+template <int NWT = 0>
 __device__ __forceinline__ void sess_key_record(SessKey &K, int64_t k, int64_t tsi, int64_t v, const AccPlan &p,
                                                 const ResultPlan &rp, const SessGeom &g, const OutCols &o,
                                                 SessErr *err, int64_t *side_key, int64_t *side_ts, int64_t *side_val,
                                                 unsigned long long *side_count, long long side_cap, int sw) {
     if (tsi == GWO_LONG_MIN) return;  // the whole batch is rejected by the host
+    const int NWP = NWT > 0 ? NWT : p.nwords;
+    if (NWT > 0) sw = 3 + NWT;
     const int64_t ws = tsi, we = jadd(tsi, g.gap);
     int64_t *S = K.S;
     int sst = K.sst;
@@ -234,7 +238,7 @@ __device__ __forceinline__ void sess_key_record(SessKey &K, int64_t k, int64_t t
         X[0] = ws;
         X[sst] = we;
         X[2 * sst] = 0;
-        for (int w = 0; w < p.nwords; ++w) X[(3 + w) * sst] = p.ident[w];
+        for (int w = 0; w < NWP; ++w) X[(3 + w) * sst] = p.ident[w];
         fresh = true;
         K.created++;
     } else if (nm == 1 && f0 == ms && f1 == me) {
@@ -247,13 +251,13 @@ __device__ __forceinline__ void sess_key_record(SessKey &K, int64_t k, int64_t t
         }
         // mergeNamespaces: fold every merged session into the first
         int64_t acc[GWO_MAX_WORDS];
-        for (int w = 0; w < p.nwords; ++w) acc[w] = p.ident[w];
+        for (int w = 0; w < NWP; ++w) acc[w] = p.ident[w];
         int keep = 0;
         for (int s = 0; s < ns; ++s) {
             const int64_t *X = S + s * ssw;
             bool m = X[0] <= we && X[sst] >= ws;
             if (m) {
-                for (int w = 0; w < p.nwords; ++w) acc[w] = combine(p.op[w], acc[w], X[(3 + w) * sst]);
+                for (int w = 0; w < NWP; ++w) acc[w] = combine(p.op[w], acc[w], X[(3 + w) * sst]);
             } else {
                 if (keep != s)
                     for (int w = 0; w < sw; ++w) S[keep * ssw + w * sst] = X[w * sst];
@@ -267,7 +271,7 @@ __device__ __forceinline__ void sess_key_record(SessKey &K, int64_t k, int64_t t
         X[0] = ms;
         X[sst] = me;
         X[2 * sst] = rmax > g.wm ? 1 : 0;  // EventTimeTrigger.onMerge: timer iff maxTs > watermark
-        for (int w = 0; w < p.nwords; ++w) X[(3 + w) * sst] = acc[w];
+        for (int w = 0; w < NWP; ++w) X[(3 + w) * sst] = acc[w];
     }
     K.dirty = true;
     K.ns = ns;
@@ -291,7 +295,7 @@ __device__ __forceinline__ void sess_key_record(SessKey &K, int64_t k, int64_t t
         }
         return;
     }
-    for (int w = 0; w < p.nwords; ++w) A[(3 + w) * sst] = combine(p.op[w], A[(3 + w) * sst], lift_word(p, w, v));
+    for (int w = 0; w < NWP; ++w) A[(3 + w) * sst] = combine(p.op[w], A[(3 + w) * sst], lift_word(p, w, v));
     if (amax <= g.wm) {
         emit_row_at(o, p, rp, atomicAdd(o.count, 1ull), k, A[0], A[sst], A + 3 * sst, sst);  // onElement FIRE
         atomicAdd(&err->emitted, 1ull);
@@ -325,7 +329,7 @@ __device__ __forceinline__ long long sess_key_end(SessKey &K, uint32_t slot, uin
 // in rec_slot) loads the bucket, the entry and every bucketed record's timestamp and value at once, then applies the
 // records smallest index first (a bucket holds at most SESS_BKT_N records: a slot with more is queued for
 // sess_long_kernel); otherwise the slot-sorted records (stable radix sort, gwo_sort.hip), a lane per run head.
-template <bool LISTS>
+template <bool LISTS, int NWT = 0>
 __global__ __launch_bounds__(64) void sess_process_kernel(const int64_t *__restrict__ key, const int64_t *__restrict__ ts,
                                                           const int64_t *__restrict__ val, int64_t n,
                                                           const uint32_t *__restrict__ sorted_slot,
@@ -336,7 +340,7 @@ __global__ __launch_bounds__(64) void sess_process_kernel(const int64_t *__restr
                                                           long long side_cap, SessLists ls) {
     extern __shared__ int64_t s_L[];   // [smax * sw][64]: the lanes' copies of their keys' inline sessions, interleaved
     const int64_t step = (int64_t)gridDim.x * blockDim.x;
-    const int sw = 3 + p.nwords;
+    const int sw = 3 + (NWT > 0 ? NWT : p.nwords);
     int64_t *L = s_L + threadIdx.x;
     unsigned long long nlong = 0;
     long long created = 0;
@@ -407,7 +411,7 @@ __global__ __launch_bounds__(64) void sess_process_kernel(const int64_t *__restr
                 }
             }
             const int64_t k = slot < cap ? e[0] : GWO_EMPTY_KEY;   // the side slot holds the empty-key marker's key
-            for (uint32_t j = 0; j < c; ++j) sess_key_record(K, k, R[(2 * j) * 64], R[(2 * j + 1) * 64], SESS_REC_ARGS);
+            for (uint32_t j = 0; j < c; ++j) sess_key_record<NWT>(K, k, R[(2 * j) * 64], R[(2 * j + 1) * 64], SESS_REC_ARGS);
 #ifdef GWO_SP_NOEND
             created += K.created + K.ns;
 #else
@@ -790,12 +794,21 @@ void launch_sess_process(const int64_t *key, const int64_t *ts, const int64_t *v
                          const ResultPlan &rp, const SessGeom &g, OutCols o, SessErr *err, int64_t *sk, int64_t *st,
                          int64_t *sv, unsigned long long *sc, long long scap, const SessLists *ls, hipStream_t s) {
     const size_t lds = (size_t)64 * (g.smax * (3 + p.nwords) + (ls ? 2 * SESS_BKT_N : 0)) * 8;
-    if (ls)
-        hipLaunchKernelGGL(sess_process_kernel<true>, dim3(sgrid(n, 64, 65536)), dim3(64), lds, s, key, ts, val, n,
-                           sslot, sidx, t, cap, stride, p, rp, g, o, err, sk, st, sv, sc, scap, *ls);
-    else
+#define GWO_SESS_PROC(NWT)                                                                                    \
+    hipLaunchKernelGGL((sess_process_kernel<true, NWT>), dim3(sgrid(n, 64, 65536)), dim3(64), lds, s, key, ts, val, n, \
+                       sslot, sidx, t, cap, stride, p, rp, g, o, err, sk, st, sv, sc, scap, *ls)
+    if (ls) {   // (the plan's word count at compile time for 1-4 words)
+        switch (p.nwords) {
+            case 1: GWO_SESS_PROC(1); break;
+            case 2: GWO_SESS_PROC(2); break;
+            case 3: GWO_SESS_PROC(3); break;
+            case 4: GWO_SESS_PROC(4); break;
+            default: GWO_SESS_PROC(0); break;
+        }
+    } else
         hipLaunchKernelGGL(sess_process_kernel<false>, dim3(sgrid(n, 64, 65536)), dim3(64), lds, s, key, ts, val, n,
                            sslot, sidx, t, cap, stride, p, rp, g, o, err, sk, st, sv, sc, scap, SessLists{});
+#undef GWO_SESS_PROC
 }
 
 void launch_sess_long(const int64_t *key, const int64_t *ts, const int64_t *val, int64_t n, const uint32_t *rec_slot,
