@@ -329,8 +329,11 @@ __device__ __forceinline__ long long sess_key_end(SessKey &K, uint32_t slot, uin
 // in rec_slot) loads the bucket, the entry and every bucketed record's timestamp and value at once, then applies the
 // records smallest index first (a bucket holds at most SESS_BKT_N records: a slot with more is queued for
 // sess_long_kernel); otherwise the slot-sorted records (stable radix sort, gwo_sort.hip), a lane per run head.
+#ifndef SESS_PROC_WAVES
+#define SESS_PROC_WAVES 1   // waves per process workgroup (each wave its own LDS columns)
+#endif
 template <bool LISTS, int NWT = 0>
-__global__ __launch_bounds__(64) void sess_process_kernel(const int64_t *__restrict__ key, const int64_t *__restrict__ ts,
+__global__ __launch_bounds__(64 * SESS_PROC_WAVES) void sess_process_kernel(const int64_t *__restrict__ key, const int64_t *__restrict__ ts,
                                                           const int64_t *__restrict__ val, int64_t n,
                                                           const uint32_t *__restrict__ sorted_slot,
                                                           const uint32_t *__restrict__ sorted_idx, TableDesc t,
@@ -341,7 +344,9 @@ __global__ __launch_bounds__(64) void sess_process_kernel(const int64_t *__restr
     extern __shared__ int64_t s_L[];   // [smax * sw][64]: the lanes' copies of their keys' inline sessions, interleaved
     const int64_t step = (int64_t)gridDim.x * blockDim.x;
     const int sw = 3 + (NWT > 0 ? NWT : p.nwords);
-    int64_t *L = s_L + threadIdx.x;
+    // this wave's LDS columns: [smax * sw + 2 * SESS_BKT_N][64] words per wave
+    int64_t *L = s_L + (size_t)(threadIdx.x >> 6) * ((size_t)g.smax * sw + (LISTS ? 2 * SESS_BKT_N : 0)) * 64 +
+                 (threadIdx.x & 63);
     unsigned long long nlong = 0;
     long long created = 0;
     for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n; q += step) {
@@ -793,9 +798,11 @@ void launch_sess_process(const int64_t *key, const int64_t *ts, const int64_t *v
                          const uint32_t *sidx, const TableDesc &t, uint64_t cap, int stride, const AccPlan &p,
                          const ResultPlan &rp, const SessGeom &g, OutCols o, SessErr *err, int64_t *sk, int64_t *st,
                          int64_t *sv, unsigned long long *sc, long long scap, const SessLists *ls, hipStream_t s) {
-    const size_t lds = (size_t)64 * (g.smax * (3 + p.nwords) + (ls ? 2 * SESS_BKT_N : 0)) * 8;
+    const size_t lds = (size_t)SESS_PROC_WAVES * 64 * (g.smax * (3 + p.nwords) + (ls ? 2 * SESS_BKT_N : 0)) * 8;
+    constexpr int PT = 64 * SESS_PROC_WAVES;
 #define GWO_SESS_PROC(NWT)                                                                                    \
-    hipLaunchKernelGGL((sess_process_kernel<true, NWT>), dim3(sgrid(n, 64, 65536)), dim3(64), lds, s, key, ts, val, n, \
+    hipLaunchKernelGGL((sess_process_kernel<true, NWT>), dim3(sgrid(n, PT, 65536 / SESS_PROC_WAVES)), dim3(PT), lds, s,  \
+                       key, ts, val, n, \
                        sslot, sidx, t, cap, stride, p, rp, g, o, err, sk, st, sv, sc, scap, *ls)
     if (ls) {   // (the plan's word count at compile time for 1-4 words)
         switch (p.nwords) {
@@ -806,7 +813,7 @@ void launch_sess_process(const int64_t *key, const int64_t *ts, const int64_t *v
             default: GWO_SESS_PROC(0); break;
         }
     } else
-        hipLaunchKernelGGL(sess_process_kernel<false>, dim3(sgrid(n, 64, 65536)), dim3(64), lds, s, key, ts, val, n,
+        hipLaunchKernelGGL(sess_process_kernel<false>, dim3(sgrid(n, PT, 65536 / SESS_PROC_WAVES)), dim3(PT), lds, s, key, ts, val, n,
                            sslot, sidx, t, cap, stride, p, rp, g, o, err, sk, st, sv, sc, scap, SessLists{});
 #undef GWO_SESS_PROC
 }
