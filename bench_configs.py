@@ -155,6 +155,7 @@ def run(cfg, kernel_stats=None, traffic=None):
     # pipelined submission on the combine path (C2) and sessions (C5); C1's 10K-record batches measured slower with it
     # (36.4 vs 33.7 us/step: the adaptive pre-aggregation probe batches get redone)
     pipe = os.environ.get("BENCH_PIPE", "1" if cfg in ("c2", "c5") else "0") != "0"
+    host_timing = os.environ.get("BENCH_HOST_TIMING", "0") != "0"
 
     def drive(prof):
         """One operator over the whole stream: `warm` untimed steps, then the rest timed.  prof: per-kernel HIP
@@ -184,8 +185,24 @@ def run(cfg, kernel_stats=None, traffic=None):
         lib.gwo_set_profiling(h, 1 if prof else 0)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        for i in range(warm, len(bounds)):
-            step(i)
+        if host_timing and not prof:   # BENCH_HOST_TIMING=1: each call's host time (diagnostics, stderr)
+            ns = np.zeros((len(bounds) - warm, 3), dtype=np.int64)
+            pc = time.perf_counter_ns
+            for r, i in enumerate(range(warm, len(bounds))):
+                a = args[i]
+                c0 = pc()
+                submit(h, a[0], a[1], a[2], a[3])
+                c1 = pc()
+                advance(h, a[4])
+                c2 = pc()
+                discard(h)
+                ns[r] = (c1 - c0, c2 - c1, pc() - c2)
+            med = np.median(ns, axis=0) / 1e3
+            print(f"host us per call (median) submit {med[0]:.2f} advance {med[1]:.2f} discard {med[2]:.2f}; "
+                  f"mean {ns.mean(axis=0) / 1e3}", file=sys.stderr)
+        else:
+            for i in range(warm, len(bounds)):
+                step(i)
         N.check(lib.gwo_sync(h), h)
         torch.cuda.synchronize()
         elapsed = time.perf_counter() - t0

@@ -371,8 +371,9 @@ gwo_status Handle::drain_side(const gwo_side_out *cols, int64_t cap, int64_t *n_
 gwo_status Handle::poll_fire() {
     GWO_TRY(settle_out());
     if (!fire_pending) return GWO_OK;
-    hipError_t e = hipEventQuery(ev_fire);
-    if (e == hipErrorNotReady) return GWO_OK;
+    const int sp = sess ? sess_fire_poll() : -1;
+    if (sp == 0) return GWO_OK;
+    if (sp < 0 && hipEventQuery(ev_fire) == hipErrorNotReady) return GWO_OK;
     return finish_fire();
 }
 

@@ -324,7 +324,7 @@ struct Handle {
     gwo_status combine_flush();   // resolve the pending pipelined batch (no-op without one)
     gwo_status flush_pending();   // every pipelined batch (combine path, sessions) resolved
     gwo_status sess_publish_err();
-    gwo_status sess_collect_err();
+    gwo_status sess_collect_err(bool lists_batch = false);
     gwo_status sess_apply_err();
     gwo_status sess_resolve();
     gwo_status insert_speculative(const int64_t *k, const int64_t *t, const int64_t *v, int64_t n, bool *done);
@@ -371,6 +371,7 @@ struct Handle {
     gwo_status sess_alloc(uint64_t cap, Table &t, int64_t **due);
     gwo_status sess_rebuild_due();
     gwo_status sess_join_sweep();
+    int sess_fire_poll();   // a session sweep's completion: 1 published, 0 running, -1 test ev_fire instead
     gwo_status sess_read_err();
     gwo_status sess_ensure(uint64_t incoming);
     gwo_status sess_ensure_pool(uint64_t n);

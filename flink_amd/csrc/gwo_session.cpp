@@ -1,5 +1,7 @@
 // gwo_session.cpp -- host side of EventTimeSessionWindows (kernels: gwo_session.hip, gwo_sort.hip).
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
 #include <cstdlib>
 #include <unordered_map>
 
@@ -8,6 +10,20 @@
 #include "gwo_handle.h"
 
 namespace gwo {
+
+// point i of the host profile: the time since the previous point (point 0 / 8 start a call's chain)
+#define SESS_HP(S, i)                                                                                              \
+    do {                                                                                                           \
+        if ((S).hprof) {                                                                                           \
+            const long long now_ = std::chrono::duration_cast<std::chrono::nanoseconds>(                          \
+                                       std::chrono::steady_clock::now().time_since_epoch()).count();              \
+            if ((i) != 0 && (i) != 8) {                                                                            \
+                (S).hp_sum[i] += now_ - (S).hp_last;                                                               \
+                (S).hp_cnt[i]++;                                                                                   \
+            }                                                                                                      \
+            (S).hp_last = now_;                                                                                    \
+        }                                                                                                          \
+    } while (0)
 
 void launch_sess_slot(const int64_t *key, const int64_t *ts, int64_t n, const TableDesc &t, uint64_t cap, int stride,
                       const SessGeom &g, uint32_t *rec_slot, SessErr *err, const SessLists *ls, hipStream_t s);
@@ -72,17 +88,27 @@ struct SessionState {
     // published but not read yet -- read at the watermark right after its sweep is queued, or at any other call
     bool rb_pending = false;
     uint64_t pend_n = 0;
+    bool pend_lists = false;        // the pending batch went through the lists path (its release word, fire_session)
+    uint64_t n_after_pend = 0;      // records of the batch being submitted behind the pending one (sess_collect_err)
     // the watermark sweep on the handle's fire_stream (pipelined submission, allowedLateness 0, no side output;
     // GWO_SESS_SIDE_SWEEP=1 only: measured slower, profiles/r06_experiments.txt): the next batch's slot pass -- it
     // claims entries and fills buckets, neither of which the sweep reads or writes (a slot's due watermark is SESS_NONE until its key has
     // sessions) -- overlaps it, and the stream joins the sweep (ev_fire) before anything that reads or writes
     // sessions, entries' contents or the pool (sess_join_sweep)
     bool side_sweep = false;
+    bool wm_resolve = false;        // GWO_SESS_WM_RESOLVE=1: the watermark reads a pipelined batch's readback
+    // GWO_SESS_HOST_PROF=1: host time between points of insert_session / fire_session (diagnostics, stderr at close)
+    bool hprof = false;
+    long long hp_last = 0, hp_sum[16] = {}, hp_cnt[16] = {};
+    bool fire_event = false;        // the last sweep recorded ev_fire (side sweep, or GWO_SESS_FIRE_EVENT=1)
+    bool fire_event_always = false;
+    bool early_slot = true;         // GWO_SESS_EARLY_SLOT=0: a batch reads the previous readback before its slot pass
     bool sweep_on_side = false;     // a sweep queued on fire_stream that the handle's stream has not joined yet
     hipStream_t sweep_stream = nullptr;   // the stream of the last sweep (its readback spin polls it)
 };
 
 static constexpr unsigned long long kSessLongMax = 32;   // sess_long_kernel runs 32 workgroups
+static constexpr double kSafeLoad = 0.9;   // sess_ensure: the load a slot pass may reach on a bound (one batch)
 
 gwo_status Handle::sess_alloc(uint64_t cap, Table &t, int64_t **due) {
     SessionState &S = *sess;
@@ -110,6 +136,10 @@ gwo_status Handle::session_init() {
     if (const char *e = getenv("GWO_SESSION_SLOTS")) S.smax = std::max(1, std::min(16, atoi(e)));
     if (const char *e = getenv("GWO_SESS_DIGITS")) S.sort_digits = atoi(e) == 10 ? 10 : 8;
     if (const char *e = getenv("GWO_SESS_SIDE_SWEEP")) S.side_sweep = atoi(e) != 0;
+    if (const char *e = getenv("GWO_SESS_WM_RESOLVE")) S.wm_resolve = atoi(e) != 0;
+    if (const char *e = getenv("GWO_SESS_EARLY_SLOT")) S.early_slot = atoi(e) != 0;
+    if (const char *e = getenv("GWO_SESS_FIRE_EVENT")) S.fire_event_always = atoi(e) != 0;
+    if (const char *e = getenv("GWO_SESS_HOST_PROF")) S.hprof = atoi(e) != 0;
     if (const char *e = getenv("GWO_SESS_LISTS")) {
         S.lists = atoi(e) != 0;
         S.lists_auto = false;
@@ -133,9 +163,10 @@ gwo_status Handle::session_init() {
     GWO_TRY(hipcheck(hipEventCreateWithFlags(&ev_fire, hipEventDisableTiming), "event"));
     if (!fire_stream) GWO_TRY(hipcheck(hipStreamCreateWithFlags(&fire_stream, hipStreamNonBlocking), "fire stream"));
     if (!ev_main) GWO_TRY(hipcheck(hipEventCreateWithFlags(&ev_main, hipEventDisableTiming), "event"));
-    GWO_TRY(hipcheck(hipHostMalloc((void **)&S.rb, sizeof(SessErr) + 16, hipHostMallocCoherent | hipHostMallocMapped),
+    // [SessErr words, pool top, sequence word, input-release word, table occupancy (the last two: sess_long_kernel)]
+    GWO_TRY(hipcheck(hipHostMalloc((void **)&S.rb, sizeof(SessErr) + 32, hipHostMallocCoherent | hipHostMallocMapped),
                      "session readback"));
-    memset(S.rb, 0, sizeof(SessErr) + 16);
+    memset(S.rb, 0, sizeof(SessErr) + 32);
     GWO_TRY(hipcheck(hipHostGetDevicePointer((void **)&S.rb_dev, S.rb, 0), "session readback"));
     S.d_pool_top = (unsigned long long *)((char *)S.d_err + sizeof(SessErr));
     GWO_TRY(hipcheck(hipMemsetAsync(S.d_err, 0, sizeof(SessErr) + 8, stream), "err"));
@@ -149,6 +180,12 @@ gwo_status Handle::session_init() {
 void Handle::session_free() {
     if (!sess) return;
     SessionState &S = *sess;
+    if (S.hprof) {
+        fprintf(stderr, "session host us:");
+        for (int i = 0; i < 16; ++i)
+            if (S.hp_cnt[i]) fprintf(stderr, " [%d] %.2f", i, S.hp_sum[i] / 1e3 / S.hp_cnt[i]);
+        fprintf(stderr, "\n");
+    }
     if (S.T.base) (void)hipFree(S.T.base);
     if (S.d_err) (void)hipFree(S.d_err);
     if (S.h_err) (void)hipHostFree(S.h_err);
@@ -203,10 +240,14 @@ gwo_status Handle::sess_read_err() {
     return sess_collect_err();
 }
 
-gwo_status Handle::sess_collect_err() {
+gwo_status Handle::sess_collect_err(bool lists_batch) {
     SessionState &S = *sess;
     constexpr int NWD = (int)(sizeof(SessErr) / 8) + 1;
     GWO_TRY(spin_seq(S.rb + NWD, S.rb_seq, "session readback"));
+    if (lists_batch) {   // the lists path's readback carries the table's exact occupancy after the batch
+        S.T.occ = S.rb[NWD + 2];
+        S.occ_pending = S.n_after_pend;   // records submitted behind the batch (a pipelined next batch)
+    }
     memcpy(S.h_err, S.rb, sizeof(SessErr) + 8);
     S.pool_top = *(const unsigned long long *)((const char *)S.h_err + sizeof(SessErr));
     constexpr int W = (int)(sizeof(SessErr) / 8);
@@ -263,9 +304,20 @@ gwo_status Handle::sess_ensure(uint64_t incoming) {
         S.occ_pending += incoming;
         return GWO_OK;
     }
+    // A pipelined batch is unread (its readback brings the exact occupancy, without a stream synchronisation): if the
+    // table is within the growth threshold but for that batch's claims, the slot pass goes ahead on a safety bound
+    // (every record a new key: the probes still find room below kSafeLoad) and the readback decides any growth at
+    // the next batch.  C5 read the counter back (a stream synchronisation behind the sweep) every ~4 batches.
+    const uint64_t but_pending = S.occ_pending > S.pend_n ? S.occ_pending - S.pend_n : 0;
+    if (S.rb_pending && S.pend_lists && (double)(S.T.occ + but_pending + incoming) <= kMaxLoad * (double)S.T.cap &&
+        (double)(S.T.occ + S.occ_pending + incoming) <= kSafeLoad * (double)S.T.cap) {
+        S.occ_pending += incoming;
+        return GWO_OK;
+    }
     GWO_TRY(read_occupancy_one(S.T));
     S.occ_pending = incoming;
     if ((double)(S.T.occ + incoming) <= kMaxLoad * (double)S.T.cap) return GWO_OK;
+    GWO_TRY(sess_resolve());      // (the live-session count below: exact, not one pipelined batch behind)
     GWO_TRY(sess_join_sweep());   // the compaction reads every entry
     uint64_t need = std::min<uint64_t>(S.T.occ, S.live) + incoming;
     uint64_t cap = kMinCap;
@@ -299,19 +351,26 @@ gwo_status Handle::read_occupancy_one(Table &t) {
 
 gwo_status Handle::insert_session(const int64_t *k, const int64_t *t, const int64_t *v, int64_t n) {
     SessionState &S = *sess;
+    SESS_HP(S, 0);
     // The last watermark's sweep is left running: the batch's kernels queue right behind it (no idle gap while the
     // host waits for it), and its rows and live-session change are applied at the next output access or watermark
     // (sizing below only needs upper bounds, which the unretired sessions give).  With allowedLateness > 0 the batch
     // emits re-fire rows behind the sweep's, so the sweep's rows are published first.
     if (cfg.allowed_lateness > 0) GWO_TRY(finish_fire());
-    GWO_TRY(sess_resolve());   // a pipelined batch's readback (sizing below reads the live-session count)
+    // A pipelined batch's readback (the previous batch: live-session count, pool top, errors) is read after this
+    // batch's slot pass is queued (early): the slot pass only claims entries (sized by the occupancy bound, which
+    // needs no readback) and fills buckets, so it covers the host's wait and the rest of its planning -- read before
+    // it, the next batch's launches trailed the watermark's sweep by ~5.5 us of idle GPU per C5 step.  A batch that
+    // failed still fails the handle before this batch's sessions change (its slot pass only claimed entries).
+    const bool early = S.rb_pending && S.early_slot;
+    if (!early) GWO_TRY(sess_resolve());
     if (n > 0xffffffffll) return fail(GWO_ERR_INVALID_ARGUMENT, "session batches are limited to 2^32 records");
     GWO_TRY(sess_ensure((uint64_t)n));
-    GWO_TRY(sess_ensure_pool((uint64_t)n));
+    if (!early) GWO_TRY(sess_ensure_pool((uint64_t)n));
     if (cfg.allowed_lateness > 0) GWO_TRY(ensure_output((uint64_t)n));   // re-fires: at most one row per record
     GWO_TRY(ensure_buf(S.rec_slot, n * 4));
     GWO_TRY(ensure_buf(S.k1, n * 4));
-    const bool lists = S.lists;
+    const bool lists = S.lists;   // (this batch's grouping: a readback read below may switch the next batch's)
     int64_t hist_words = 0;
     if (lists) {
         const size_t was = S.bkt.bytes;
@@ -334,10 +393,20 @@ gwo_status Handle::insert_session(const int64_t *k, const int64_t *t, const int6
     OutCols o = out_cols();
     int64_t *sk = (int64_t *)side_key.ptr, *sts = (int64_t *)side_ts.ptr, *sv = (int64_t *)side_val.ptr;
     const long long scap = side_enabled() ? side_cap : 0;
+    SESS_HP(S, 1);
     prof_begin(GWO_KERNEL_SESSION);
     launch_sess_slot(k, t, n, desc(S.T), S.T.cap, S.stride, g, (uint32_t *)S.rec_slot.ptr, S.d_err, lists ? &ls : nullptr,
                      stream);
     GWO_TRY(launch_ok("sess slot"));
+    SESS_HP(S, 2);
+    if (early) {
+        S.n_after_pend = (uint64_t)n;   // (counted in occ_pending by sess_ensure above)
+        const gwo_status st = sess_resolve();
+        S.n_after_pend = 0;
+        GWO_TRY(st);
+        GWO_TRY(sess_ensure_pool((uint64_t)n));
+    }
+    SESS_HP(S, 3);
     GWO_TRY(sess_join_sweep());   // the slot pass overlapped the sweep; the rest of the batch follows it
     if (lists) {
         launch_sess_process(k, t, v, n, (const uint32_t *)S.rec_slot.ptr, nullptr, desc(S.T), S.T.cap, S.stride, plan, rplan, g, o, S.d_err, sk,
@@ -356,6 +425,7 @@ gwo_status Handle::insert_session(const int64_t *k, const int64_t *t, const int6
         launch_sess_long(k, t, v, n, (const uint32_t *)S.rec_slot.ptr, desc(S.T), S.T.cap, S.stride, plan, rplan, g, o,
                          S.d_err, sk, sts, sv, d_side_count, scap, ls, S.rb_dev, ++S.rb_seq, reset_rows, stream);
         GWO_TRY(launch_ok("sess long"));
+        SESS_HP(S, 4);
         prof_end(GWO_KERNEL_SESSION, n);
     } else {
         int bits = 1;   // slots are 0..cap (cap: the side slot)
@@ -372,12 +442,13 @@ gwo_status Handle::insert_session(const int64_t *k, const int64_t *t, const int6
         prof_end(GWO_KERNEL_SESSION, n);
         GWO_TRY(sess_publish_err());
     }
-    if (pipe_submit && cfg.allowed_lateness == 0 && !side_enabled()) {   // read at the watermark (sess_resolve)
+    if (pipe_submit && cfg.allowed_lateness == 0 && !side_enabled()) {   // read by the next call (sess_resolve)
         S.rb_pending = true;
         S.pend_n = (uint64_t)n;
+        S.pend_lists = lists;
         return GWO_OK;
     }
-    GWO_TRY(sess_collect_err());
+    GWO_TRY(sess_collect_err(lists));
     return sess_apply_err();
 }
 
@@ -385,7 +456,7 @@ gwo_status Handle::insert_session(const int64_t *k, const int64_t *t, const int6
 gwo_status Handle::sess_resolve() {
     if (!sess || !sess->rb_pending) return GWO_OK;
     sess->rb_pending = false;
-    GWO_TRY(sess_collect_err());
+    GWO_TRY(sess_collect_err(sess->pend_lists));
     return sess_apply_err();
 }
 
@@ -425,7 +496,9 @@ gwo_status Handle::sess_apply_err() {
 // change are applied by finish_fire, at the next batch or output access (by then it has usually completed).
 gwo_status Handle::fire_session(int64_t new_wm) {
     SessionState &S = *sess;
+    SESS_HP(S, 8);
     GWO_TRY(finish_fire());
+    SESS_HP(S, 9);
     // a pipelined batch still unread adds at most one live session per record: the sweep is sized for that and
     // queued right behind the batch, then the batch's readback is read
     const uint64_t live_bound = S.live + (S.rb_pending ? S.pend_n : 0);
@@ -446,11 +519,34 @@ gwo_status Handle::fire_session(int64_t new_wm) {
                      S.rbf_dev, ++S.rbf_seq, fs);
     GWO_TRY(launch_ok("sess fire"));
     prof_end(GWO_KERNEL_FIRE, (int64_t)S.T.cap, fs);
-    GWO_TRY(hipcheck(hipEventRecord(ev_fire, fs), "event"));   // poll_fire's completion test (and the join)
+    SESS_HP(S, 10);
+    // the side sweep's join (and poll_fire's completion test) is an event; otherwise the sweep's readback sequence
+    // word is the test: an event recorded behind every sweep held the next batch's first kernel ~5.5 us behind the
+    // sweep's end (C5; GWO_SESS_FIRE_EVENT=1 restores it, profiles/r06_experiments.txt)
+    S.fire_event = side || S.fire_event_always;
+    if (S.fire_event) GWO_TRY(hipcheck(hipEventRecord(ev_fire, fs), "event"));
     S.sweep_on_side = side;
     S.sweep_stream = fs;
     fire_pending = true;
-    return sess_resolve();
+    // A pipelined batch's readback is left to the next call that needs it (the next batch's sizing, gwo_sync, the
+    // statistics and checkpoint calls): read here, it held the host until the batch's last kernel ended, and the
+    // next batch's launches then trailed the sweep by ~5.5 us of idle GPU per C5 step (GWO_SESS_WM_RESOLVE=1
+    // restores the read; profiles/r06_experiments.txt).
+    if (S.wm_resolve || !S.rb_pending) return sess_resolve();
+    // the batch's device columns are released before this call returns (gwo.h: borrowed until the next call): the
+    // lists path's long kernel publishes a release word as it starts (no long slot: nothing reads them any more),
+    // the sort path's readback is its release
+    constexpr int NWD = (int)(sizeof(SessErr) / 8) + 1;
+    const gwo_status st = spin_seq(S.rb + (S.pend_lists ? NWD + 1 : NWD), S.rb_seq, "session input release");
+    SESS_HP(S, 11);
+    return st;
+}
+
+int Handle::sess_fire_poll() {
+    SessionState &S = *sess;
+    if (S.fire_event) return -1;
+    constexpr int NW = (int)(sizeof(SessErr) / 8);
+    return *(volatile const unsigned long long *)(S.rbf + NW) == S.rbf_seq ? 1 : 0;
 }
 
 gwo_status Handle::session_finish_fire() {

@@ -476,6 +476,10 @@ __global__ __launch_bounds__(256) void sess_long_kernel(const int64_t *__restric
     // no slot overflowed its bucket (C5: every batch): workgroup 0 alone publishes, with no arrival count
     const bool none = nl == 0;
     if (none && blockIdx.x != 0) return;
+    constexpr int NWD = (int)(sizeof(SessErr) / 8) + 1;
+    // the batch's input columns are no longer read (the slot and process kernels are done, no slot is long): the
+    // release word, which a pipelined watermark waits for instead of the whole readback (gwo_session.cpp fire_session)
+    if (none && threadIdx.x == 0) rb_put(&rb[NWD + 1], seq);
     for (uint32_t j = blockIdx.x; j < nl; j += gridDim.x) {
         const uint32_t slot = ls.longs[j];
         SessKey K;
@@ -520,11 +524,21 @@ __global__ __launch_bounds__(256) void sess_long_kernel(const int64_t *__restric
         __syncthreads();
         if (!s_last) return;
     }
-    constexpr int NWD = (int)(sizeof(SessErr) / 8) + 1;
     const unsigned long long live = sess_fold_shards(ls.shards, 0);   // the process kernel's live-session change
     if (threadIdx.x < NWD) {
         const unsigned long long add = threadIdx.x == (int)(offsetof(SessErr, live_delta) / 8) ? live : 0ull;
         rb_put(&rb[threadIdx.x], atomicAdd((unsigned long long *)err + threadIdx.x, add) + add);
+    }
+    if (!none && threadIdx.x == NWD) rb_put(&rb[NWD + 1], seq);   // (every long slot's records applied)
+    if (threadIdx.x >= 64 && threadIdx.x < 128) {   // the table's occupancy (claimed entries) after this batch: the
+        // host sizes the next batches on it without reading the counter back itself (a stream synchronisation)
+        const int q = threadIdx.x - 64;
+        unsigned long long c = q < GWO_OCC_SHARDS
+                                   ? __hip_atomic_load(&t.occ[q * GWO_OCC_SHARD_STRIDE], __ATOMIC_RELAXED,
+                                                       __HIP_MEMORY_SCOPE_AGENT)
+                                   : 0ull;
+        for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
+        if (q == 0) rb_put(&rb[NWD + 2], c);
     }
     if (threadIdx.x == 0) {
         ls.ctl[1] = 0;

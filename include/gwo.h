@@ -303,9 +303,11 @@ gwo_status gwo_key_strings(gwo_handle *h, const int64_t *ids, int64_t n, int64_t
  * allowedLateness 0 -- other batches are resolved inside gwo_submit as usual).  gwo_submit queues the batch's
  * kernels (log: K1; combine: the gather and its speculative merge; sessions: sort and merge) and returns after
  * completing the PREVIOUS batch (its classification checks and pass 2, or its readback; sessions: the batch's
- * readback is read at the next watermark, after that watermark's sweep is queued), so the host's wait and planning
- * overlap running kernels.  Observable results are unchanged: gwo_advance_watermark,
- * gwo_sync, gwo_late_dropped, gwo_state_size and the side-output calls complete the pending batch first.
+ * readback is read by the next gwo_submit once that batch's slot pass is queued, or by the next call that needs it;
+ * a watermark's sweep queues behind the pending batch without reading it), so the host's wait and planning overlap
+ * running kernels.  Observable results are unchanged: gwo_sync, gwo_late_dropped, gwo_state_size, the checkpoint
+ * calls and the side-output calls complete the pending batch first (and gwo_advance_watermark, except on sessions,
+ * where the sweep's own rows do not depend on it).
  * What moves is error reporting: a batch's GWO_ERR_NO_TIMESTAMP / GWO_ERR_KEY_GROUP is returned by the
  * next call on the handle (the batch is still rejected before any window state changes, and the handle
  * stays failed).  Device columns stay borrowed until that next call returns.
