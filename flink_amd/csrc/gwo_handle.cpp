@@ -1,5 +1,6 @@
 // gwo_handle.cpp -- handle lifecycle, batch submit, watermark dispatch and output draining.
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <numeric>
@@ -120,6 +121,7 @@ gwo_status Handle::init(const gwo_config &c) {
     if (geom.unit > 0) geom.inv_unit = 1.0 / (double)geom.unit;
     debug = getenv("GWO_DEBUG") != nullptr;
     ktrace = getenv("GWO_KTRACE") != nullptr;
+    hprof = getenv("GWO_HOST_PROF") != nullptr && atoi(getenv("GWO_HOST_PROF")) != 0;
     if (ktrace) ktrace_enable(1);
     if (const char *e = getenv("GWO_ASYNC_FIRE")) async_fire = atoi(e) != 0;
     const char *pa = getenv("GWO_PREAGG");
@@ -194,6 +196,12 @@ Handle::~Handle() {
     if (fire_stream) (void)hipStreamSynchronize(fire_stream);
     if (cb_side) (void)hipStreamSynchronize(cb_side);
     if (ktrace) ktrace_report();
+    if (hprof) {
+        fprintf(stderr, "host us per point:");
+        for (int i = 0; i < 32; ++i)
+            if (hp_cnt[i]) fprintf(stderr, " [%d] %.2f", i, hp_sum[i] / 1e3 / hp_cnt[i]);
+        fprintf(stderr, "\n");
+    }
     (void)prof_collect();
     for (hipEvent_t e : event_pool) (void)hipEventDestroy(e);
     comm_free();
@@ -250,7 +258,9 @@ Handle::~Handle() {
 gwo_status Handle::submit(const int64_t *key, const int64_t *ts, const void *val, int64_t n) {
     const int64_t *dk = nullptr, *dt = nullptr, *dv = nullptr;
     if (!comm && n == 0) return GWO_OK;
+    hp(12, true);
     if (n > 0) GWO_TRY(stage_inputs(key, ts, needs_value ? val : nullptr, n, &dk, &dt, &dv));
+    hp(13);
     if (comm && logst) {
         // log layout: K1 routes other GPUs' records while it partitions this one's (comm_route_args)
         LogRoute rt{};

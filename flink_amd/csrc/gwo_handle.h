@@ -2,6 +2,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <chrono>
+
 #include <map>
 #include <string>
 #include <vector>
@@ -222,6 +224,21 @@ struct Handle {
 
     // profiling
     bool profiling = false;
+    // GWO_HOST_PROF=1: mean host time between numbered points of the submit / watermark paths (diagnostics, printed
+    // to stderr when the handle is destroyed).  Point p records the time since the previous point; the points that
+    // start a call's chain (hp_start) record nothing.
+    bool hprof = false;
+    long long hp_last = 0, hp_sum[32] = {}, hp_cnt[32] = {};
+    void hp(int p, bool start = false) {
+        if (!hprof) return;
+        const long long now =
+            std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch()).count();
+        if (!start) {
+            hp_sum[p] += now - hp_last;
+            hp_cnt[p]++;
+        }
+        hp_last = now;
+    }
     uint32_t prof_mask = ~0u;                  // kernels timed while profiling (bit = gwo_kernel_id)
     bool debug = false;                        // GWO_DEBUG=1: trace batches to stderr
     bool ktrace = false;                       // GWO_KTRACE: per-phase K1 / fire cycle sums at destruction

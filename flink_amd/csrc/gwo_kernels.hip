@@ -884,7 +884,9 @@ __global__ __launch_bounds__(CB_THREADS) void gather_kernel(GatherArgs A) {
     __shared__ unsigned long long s_spec[4];   // listed records, side-output count, occupancy of the hint tables
     if (tid < CS_WORDS && (tid < CS_HIST ? tid <= CS_D1 : true)) {
 #define RBW(f) (int)(offsetof(BatchStats, f) / 8)
-        constexpr int word[CS_HIST] = {RBW(accepted), RBW(late),    RBW(refire),      RBW(bad_ts),
+        // (static: a constant table in global memory; a local array indexed by tid was 20 B of scratch per lane,
+        // and a kernel with scratch waits ~6 us at dispatch behind the previous kernel)
+        static constexpr int word[CS_HIST] = {RBW(accepted), RBW(late),    RBW(refire),      RBW(bad_ts),
                                        RBW(bad_range), RBW(bad_kg), RBW(hist_out),    RBW(min_idx),
                                        RBW(max_idx),  RBW(distinct), RBW(distinct) + 1, 0};
         const unsigned long long r = s_tot[tid];

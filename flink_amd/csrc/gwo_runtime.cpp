@@ -596,6 +596,7 @@ gwo_status Handle::insert_combined(const int64_t *k, const int64_t *t, const int
             GWO_TRY(hipcheck(hipStreamWaitEvent(cb_side, cb_ev_merge[slot], 0), "event wait"));
         gs = cb_side;
     }
+    hp(16);
     prof_begin(GWO_KERNEL_SCAN, gs);
     launch_gather(k, t, v, n, g, plan, a, G, d_stats, (int64_t *)side_key.ptr, (int64_t *)side_ts.ptr,
                   (int64_t *)side_val.ptr, d_side_count, side_enabled() ? side_cap : 0, side_enabled(), gs);
@@ -613,6 +614,7 @@ gwo_status Handle::insert_combined(const int64_t *k, const int64_t *t, const int
         launch_merge(k, t, v, g, plan, a, G, 0, (const TableDesc *)cb_spec_dir.ptr, hist_hint, 2, none, a.go, stream);
         GWO_TRY(launch_ok("merge"));
         prof_end(GWO_KERNEL_INSERT, n);
+        hp(17);
         if (overlap) {
             GWO_TRY(hipcheck(hipEventRecord(cb_ev_merge[slot], stream), "event"));
             cb_merge_rec[slot] = true;
@@ -637,6 +639,7 @@ gwo_status Handle::insert_combined(const int64_t *k, const int64_t *t, const int
         }
         bool go = false;
         GWO_TRY(combine_resolve_pending(&go));   // the previous batch (usually finished by now)
+        hp(18);
         if (go) {
             cb_pend = Q;
             return GWO_OK;
@@ -895,6 +898,7 @@ gwo_status Handle::insert_speculative(const int64_t *k, const int64_t *t, const 
     sp.check_kg = !(cfg.key_group_start == 0 && cfg.key_group_end == cfg.max_parallelism - 1);
     // (no init_stats: the scan's last workgroup writes every statistic the verdict reads; the regular path resets
     // the rest before it runs)
+    hp(20);
     prof_begin(GWO_KERNEL_SCAN);
     launch_scan(k, t, n, g, hist_hint, d_stats, (int64_t *)side_key.ptr, (int64_t *)side_ts.ptr, (int64_t *)side_val.ptr,
                 v, d_side_count, side_enabled() ? side_cap : 0, side_enabled(), d_scan_sh, stream, &sp);
@@ -905,7 +909,9 @@ gwo_status Handle::insert_speculative(const int64_t *k, const int64_t *t, const 
                   sp.go);
     GWO_TRY(launch_ok("insert"));
     prof_end(GWO_KERNEL_INSERT, n);
+    hp(21);
     GWO_TRY(spin_seq(sp_rb + CB_RB_SEQ, sp.seq, "scan"));
+    hp(22);
 #define RBW(f) (int)(offsetof(BatchStats, f) / 8)
     const unsigned long long accepted = sp_rb[RBW(accepted)], late = sp_rb[RBW(late)];
     const long long lo = (long long)sp_rb[RBW(min_idx)];

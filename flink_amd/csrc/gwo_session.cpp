@@ -11,19 +11,6 @@
 
 namespace gwo {
 
-// point i of the host profile: the time since the previous point (point 0 / 8 start a call's chain)
-#define SESS_HP(S, i)                                                                                              \
-    do {                                                                                                           \
-        if ((S).hprof) {                                                                                           \
-            const long long now_ = std::chrono::duration_cast<std::chrono::nanoseconds>(                          \
-                                       std::chrono::steady_clock::now().time_since_epoch()).count();              \
-            if ((i) != 0 && (i) != 8) {                                                                            \
-                (S).hp_sum[i] += now_ - (S).hp_last;                                                               \
-                (S).hp_cnt[i]++;                                                                                   \
-            }                                                                                                      \
-            (S).hp_last = now_;                                                                                    \
-        }                                                                                                          \
-    } while (0)
 
 void launch_sess_slot(const int64_t *key, const int64_t *ts, int64_t n, const TableDesc &t, uint64_t cap, int stride,
                       const SessGeom &g, uint32_t *rec_slot, SessErr *err, const SessLists *ls, hipStream_t s);
@@ -97,9 +84,6 @@ struct SessionState {
     // sessions, entries' contents or the pool (sess_join_sweep)
     bool side_sweep = false;
     bool wm_resolve = false;        // GWO_SESS_WM_RESOLVE=1: the watermark reads a pipelined batch's readback
-    // GWO_SESS_HOST_PROF=1: host time between points of insert_session / fire_session (diagnostics, stderr at close)
-    bool hprof = false;
-    long long hp_last = 0, hp_sum[16] = {}, hp_cnt[16] = {};
     bool fire_event = false;        // the last sweep recorded ev_fire (side sweep, or GWO_SESS_FIRE_EVENT=1)
     bool fire_event_always = false;
     bool early_slot = true;         // GWO_SESS_EARLY_SLOT=0: a batch reads the previous readback before its slot pass
@@ -139,7 +123,6 @@ gwo_status Handle::session_init() {
     if (const char *e = getenv("GWO_SESS_WM_RESOLVE")) S.wm_resolve = atoi(e) != 0;
     if (const char *e = getenv("GWO_SESS_EARLY_SLOT")) S.early_slot = atoi(e) != 0;
     if (const char *e = getenv("GWO_SESS_FIRE_EVENT")) S.fire_event_always = atoi(e) != 0;
-    if (const char *e = getenv("GWO_SESS_HOST_PROF")) S.hprof = atoi(e) != 0;
     if (const char *e = getenv("GWO_SESS_LISTS")) {
         S.lists = atoi(e) != 0;
         S.lists_auto = false;
@@ -180,12 +163,6 @@ gwo_status Handle::session_init() {
 void Handle::session_free() {
     if (!sess) return;
     SessionState &S = *sess;
-    if (S.hprof) {
-        fprintf(stderr, "session host us:");
-        for (int i = 0; i < 16; ++i)
-            if (S.hp_cnt[i]) fprintf(stderr, " [%d] %.2f", i, S.hp_sum[i] / 1e3 / S.hp_cnt[i]);
-        fprintf(stderr, "\n");
-    }
     if (S.T.base) (void)hipFree(S.T.base);
     if (S.d_err) (void)hipFree(S.d_err);
     if (S.h_err) (void)hipHostFree(S.h_err);
@@ -351,7 +328,7 @@ gwo_status Handle::read_occupancy_one(Table &t) {
 
 gwo_status Handle::insert_session(const int64_t *k, const int64_t *t, const int64_t *v, int64_t n) {
     SessionState &S = *sess;
-    SESS_HP(S, 0);
+    hp(0);
     // The last watermark's sweep is left running: the batch's kernels queue right behind it (no idle gap while the
     // host waits for it), and its rows and live-session change are applied at the next output access or watermark
     // (sizing below only needs upper bounds, which the unretired sessions give).  With allowedLateness > 0 the batch
@@ -393,12 +370,12 @@ gwo_status Handle::insert_session(const int64_t *k, const int64_t *t, const int6
     OutCols o = out_cols();
     int64_t *sk = (int64_t *)side_key.ptr, *sts = (int64_t *)side_ts.ptr, *sv = (int64_t *)side_val.ptr;
     const long long scap = side_enabled() ? side_cap : 0;
-    SESS_HP(S, 1);
+    hp(1);
     prof_begin(GWO_KERNEL_SESSION);
     launch_sess_slot(k, t, n, desc(S.T), S.T.cap, S.stride, g, (uint32_t *)S.rec_slot.ptr, S.d_err, lists ? &ls : nullptr,
                      stream);
     GWO_TRY(launch_ok("sess slot"));
-    SESS_HP(S, 2);
+    hp(2);
     if (early) {
         S.n_after_pend = (uint64_t)n;   // (counted in occ_pending by sess_ensure above)
         const gwo_status st = sess_resolve();
@@ -406,7 +383,7 @@ gwo_status Handle::insert_session(const int64_t *k, const int64_t *t, const int6
         GWO_TRY(st);
         GWO_TRY(sess_ensure_pool((uint64_t)n));
     }
-    SESS_HP(S, 3);
+    hp(3);
     GWO_TRY(sess_join_sweep());   // the slot pass overlapped the sweep; the rest of the batch follows it
     if (lists) {
         launch_sess_process(k, t, v, n, (const uint32_t *)S.rec_slot.ptr, nullptr, desc(S.T), S.T.cap, S.stride, plan, rplan, g, o, S.d_err, sk,
@@ -425,7 +402,7 @@ gwo_status Handle::insert_session(const int64_t *k, const int64_t *t, const int6
         launch_sess_long(k, t, v, n, (const uint32_t *)S.rec_slot.ptr, desc(S.T), S.T.cap, S.stride, plan, rplan, g, o,
                          S.d_err, sk, sts, sv, d_side_count, scap, ls, S.rb_dev, ++S.rb_seq, reset_rows, stream);
         GWO_TRY(launch_ok("sess long"));
-        SESS_HP(S, 4);
+        hp(4);
         prof_end(GWO_KERNEL_SESSION, n);
     } else {
         int bits = 1;   // slots are 0..cap (cap: the side slot)
@@ -496,9 +473,9 @@ gwo_status Handle::sess_apply_err() {
 // change are applied by finish_fire, at the next batch or output access (by then it has usually completed).
 gwo_status Handle::fire_session(int64_t new_wm) {
     SessionState &S = *sess;
-    SESS_HP(S, 8);
+    hp(8, true);
     GWO_TRY(finish_fire());
-    SESS_HP(S, 9);
+    hp(9);
     // a pipelined batch still unread adds at most one live session per record: the sweep is sized for that and
     // queued right behind the batch, then the batch's readback is read
     const uint64_t live_bound = S.live + (S.rb_pending ? S.pend_n : 0);
@@ -519,7 +496,7 @@ gwo_status Handle::fire_session(int64_t new_wm) {
                      S.rbf_dev, ++S.rbf_seq, fs);
     GWO_TRY(launch_ok("sess fire"));
     prof_end(GWO_KERNEL_FIRE, (int64_t)S.T.cap, fs);
-    SESS_HP(S, 10);
+    hp(10);
     // the side sweep's join (and poll_fire's completion test) is an event; otherwise the sweep's readback sequence
     // word is the test: an event recorded behind every sweep held the next batch's first kernel ~5.5 us behind the
     // sweep's end (C5; GWO_SESS_FIRE_EVENT=1 restores it, profiles/r06_experiments.txt)
@@ -538,7 +515,7 @@ gwo_status Handle::fire_session(int64_t new_wm) {
     // the sort path's readback is its release
     constexpr int NWD = (int)(sizeof(SessErr) / 8) + 1;
     const gwo_status st = spin_seq(S.rb + (S.pend_lists ? NWD + 1 : NWD), S.rb_seq, "session input release");
-    SESS_HP(S, 11);
+    hp(11);
     return st;
 }
 
