@@ -570,15 +570,19 @@ void Handle::log_uncarve(const LogJob &J, int w, uint64_t keep) {
 gwo_status Handle::log_wait_readback(int slot, unsigned long long seq) {
     LogState &L = *logst;
     volatile unsigned long long *w = L.rb(slot) + LOG_RB_SEQ;
-    for (unsigned it = 1;; ++it) {
-        if (*w == seq) break;
-        if ((it & 1023) == 0) {
-            hipError_t e = L.rb_event[slot] ? hipEventQuery(L.ev_rb[slot]) : hipStreamQuery(stream);
-            if (e != hipSuccess && e != hipErrorNotReady) return hipcheck(e, "log partition");
-            if (e == hipSuccess && *w != seq)   // completed, yet the word never arrived: fail loudly
-                return poison(GWO_ERR_HIP, "log partition: readback sequence word not visible after completion");
+    if (!L.rb_event[slot]) {   // the stream is queried only after a while (spin_seq: a query is a stream marker)
+        GWO_TRY(spin_seq((const unsigned long long *)w, seq, "log partition"));
+    } else {
+        for (unsigned it = 1;; ++it) {
+            if (*w == seq) break;
+            if ((it & 1023) == 0) {
+                hipError_t e = hipEventQuery(L.ev_rb[slot]);
+                if (e != hipSuccess && e != hipErrorNotReady) return hipcheck(e, "log partition");
+                if (e == hipSuccess && *w != seq)   // completed, yet the word never arrived: fail loudly
+                    return poison(GWO_ERR_HIP, "log partition: readback sequence word not visible after completion");
+            }
+            __builtin_ia32_pause();
         }
-        __builtin_ia32_pause();
     }
     __atomic_thread_fence(__ATOMIC_ACQUIRE);
     L.seen_seq = std::max(L.seen_seq, seq);

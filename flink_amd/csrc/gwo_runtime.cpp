@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -826,17 +827,31 @@ gwo_status Handle::combine_flush() {
     return s;
 }
 
-// Spins on a host-mapped readback block's sequence word (written last by a kernel's final workgroup).  Now and
-// then the producing stream is queried, so that a failed launch cannot spin forever: an idle stream whose word
-// never arrived is an error.  Ends with an acquire fence: the block's other words are visible.
+// Spins on a host-mapped readback block's sequence word (written last by a kernel's final workgroup).  After
+// GWO_SPIN_QUERY_US (default 500 us) of spinning, and as often again, the producing stream is queried, so that a
+// failed launch cannot spin forever: an idle stream whose word never arrived is an error.  (A query every 1024
+// pauses -- ~30 us -- put a marker into the stream behind the queued kernels: the next batch's first kernel then
+// started ~6 us after the one before it, C2's gather; profiles/r06_experiments.txt.)  Ends with an acquire fence:
+// the block's other words are visible.
 gwo_status Handle::spin_seq(const unsigned long long *word, unsigned long long seq, const char *what,
                             hipStream_t producer) {
     volatile const unsigned long long *w = word;
+    if (*w == seq) {
+        __atomic_thread_fence(__ATOMIC_ACQUIRE);
+        return GWO_OK;
+    }
+    static const long long query_ns = 1000ll * (getenv("GWO_SPIN_QUERY_US") ? atoll(getenv("GWO_SPIN_QUERY_US")) : 500);
+    auto now_ns = [] {
+        return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
+            .count();
+    };
+    long long next = now_ns() + query_ns;
     for (unsigned it = 1; *w != seq; ++it) {
-        if ((it & 1023) == 0) {
+        if ((it & 255) == 0 && now_ns() >= next) {
             hipError_t e = hipStreamQuery(producer ? producer : stream);
             if (e != hipSuccess && e != hipErrorNotReady) return hipcheck(e, what);
             if (e == hipSuccess && *w != seq) return poison(GWO_ERR_HIP, "readback sequence word not visible after completion");
+            next = now_ns() + query_ns;
         }
         __builtin_ia32_pause();
     }
