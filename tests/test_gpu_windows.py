@@ -564,6 +564,49 @@ def test_sessions_pipelined_submit_matches_oracle(F, split):
     op.close()
 
 
+def test_sessions_pipelined_columns_released_at_the_watermark_with_table_growth(F):
+    """Pipelined sessions with every batch staged in ONE device buffer that is overwritten with garbage as soon as
+    gwo_advance_watermark returns: the watermark waits for the batch's input-release word instead of its readback, and
+    the next gwo_submit reads that readback after queueing its slot pass (gwo_session.cpp fire_session, insert_session).
+    New keys keep arriving into a table sized for 64, so it grows several times with a batch pending: sizing runs on
+    the readback's exact occupancy and, for the unread batch, the 0.9 safety bound (sess_ensure)."""
+    import ctypes as C
+    import torch
+    from flink_amd import _native as N
+    lib = N.lib()
+    rng = np.random.default_rng(29)
+    n = 40_000
+    k = (np.arange(n) * 6_000 // n + rng.integers(0, 80, n)).astype(np.int64)   # the key range widens over time
+    t = np.sort(rng.integers(0, 400_000, n)) + rng.integers(0, 6_000, n)
+    v = rng.integers(0, 100, n)
+    b = G.punctuated_watermarks(t, 700, 1_000)
+    ref = _session_oracle(k, t, v, b, 2_000, 0)
+    op = F.GpuWindowOperator(F.EventTimeSessionWindows.withGap(2_000), F.SumAggregate(), expected_keys=64)
+    h = op.handle
+    N.check(lib.gwo_set_pipelined_submit(h, 1), h)
+    cap = max(e - s for (e, _), s in zip(b, [0] + [e for e, _ in b[:-1]]))
+    dk, dt, dv = (torch.empty(cap, dtype=torch.int64, device="cuda") for _ in range(3))
+    prev = 0
+    for end, wm in b:
+        m = end - prev
+        if m:
+            for d, x in ((dk, k), (dt, t), (dv, v)):
+                d[:m].copy_(torch.from_numpy(np.ascontiguousarray(x[prev:end], dtype=np.int64)))
+            torch.cuda.synchronize()   # complete before the call (gwo.h device-input readiness)
+            N.check(lib.gwo_submit(h, C.c_void_p(dk.data_ptr()), C.c_void_p(dt.data_ptr()), C.c_void_p(dv.data_ptr()),
+                                   int(m)), h)
+        N.check(lib.gwo_advance_watermark(h, wm), h)
+        for d in (dk, dt, dv):   # released: the batch's kernels no longer read these columns
+            d.fill_(LONG_MIN)
+        torch.cuda.synchronize()
+        prev = end
+    N.check(lib.gwo_end_input(h), h)
+    op._collect()
+    assert sorted(op.output) == sorted((r.key, r.start, r.end, r.result) for r in ref.output)
+    assert op.num_late_records_dropped == ref.num_late_records_dropped
+    op.close()
+
+
 def test_fast_division_full_int64_range(F):
     """window_start_f/fdiv_floor (double reciprocal + exact corrections) against Java semantics over
     the whole int64 range, including the extremes and sizes from 1 to Long.MAX_VALUE."""
