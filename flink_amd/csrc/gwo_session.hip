@@ -440,19 +440,21 @@ __global__ __launch_bounds__(64 * SESS_PROC_WAVES) void sess_process_kernel(cons
     wave_atomic_add(&err->long_slots, nlong);
 }
 
-// Folds (reads and resets) shard word w of every shard: called by every thread of the workgroup, the total
-// returned to all.
-__device__ __forceinline__ unsigned long long sess_fold_shards(unsigned long long *shards, int w) {
-    __shared__ unsigned long long s_fold;
-    if (threadIdx.x < 64) {
-        unsigned long long v = threadIdx.x < SESS_SHARDS ? atomicExch(&shards[threadIdx.x * SESS_SHARD_STRIDE + w], 0ull) : 0ull;
+// Folds (reads and resets) shard words wa (threads 0-63) and wb (threads 64-127) of every shard in one round of
+// exchanges (256-thread workgroups; both totals returned to all threads).
+__device__ __forceinline__ void sess_fold_shards2(unsigned long long *shards, int wa, int wb, unsigned long long &ra,
+                                                  unsigned long long &rb) {
+    __shared__ unsigned long long s_fold2[2];
+    if (threadIdx.x < 128) {
+        const int h = threadIdx.x >> 6, q = threadIdx.x & 63;
+        unsigned long long v = q < SESS_SHARDS ? atomicExch(&shards[q * SESS_SHARD_STRIDE + (h ? wb : wa)], 0ull) : 0ull;
         for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-        if (threadIdx.x == 0) s_fold = v;
+        if (q == 0) s_fold2[h] = v;
     }
     __syncthreads();
-    const unsigned long long r = s_fold;
+    ra = s_fold2[0];
+    rb = s_fold2[1];
     __syncthreads();
-    return r;
 }
 
 // pass 3 (lists only): the slots whose records overflowed their buckets, a workgroup each: the records' slots are
@@ -524,15 +526,19 @@ __global__ __launch_bounds__(256) void sess_long_kernel(const int64_t *__restric
         __syncthreads();
         if (!s_last) return;
     }
-    const unsigned long long live = sess_fold_shards(ls.shards, 0);   // the process kernel's live-session change
-    if (threadIdx.x < NWD) {
-        const unsigned long long add = threadIdx.x == (int)(offsetof(SessErr, live_delta) / 8) ? live : 0ull;
-        rb_put(&rb[threadIdx.x], atomicAdd((unsigned long long *)err + threadIdx.x, add) + add);
-    }
-    if (!none && threadIdx.x == NWD) rb_put(&rb[NWD + 1], seq);   // (every long slot's records applied)
-    if (threadIdx.x >= 64 && threadIdx.x < 128) {   // the table's occupancy (claimed entries) after this batch: the
-        // host sizes the next batches on it without reading the counter back itself (a stream synchronisation)
-        const int q = threadIdx.x - 64;
+    // one round of device-scope atomics: the process kernel's live-session change folded from its shards (wave 0),
+    // the statistics words read (wave 1) and the table's occupancy summed from its counter shards (wave 2: the host
+    // sizes the next batches on it without reading the counter back, a stream synchronisation); the fold goes back
+    // into the statistics block without a return (rb_publish's wait covers it)
+    __shared__ unsigned long long s_live, s_w[NWD];
+    const int wv = threadIdx.x >> 6, q = threadIdx.x & 63;
+    if (wv == 0) {
+        unsigned long long v = q < SESS_SHARDS ? atomicExch(&ls.shards[q * SESS_SHARD_STRIDE], 0ull) : 0ull;
+        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+        if (q == 0) s_live = v;
+    } else if (wv == 1) {
+        if (q < NWD) s_w[q] = atomicAdd((unsigned long long *)err + q, 0ull);
+    } else if (wv == 2) {
         unsigned long long c = q < GWO_OCC_SHARDS
                                    ? __hip_atomic_load(&t.occ[q * GWO_OCC_SHARD_STRIDE], __ATOMIC_RELAXED,
                                                        __HIP_MEMORY_SCOPE_AGENT)
@@ -540,6 +546,13 @@ __global__ __launch_bounds__(256) void sess_long_kernel(const int64_t *__restric
         for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
         if (q == 0) rb_put(&rb[NWD + 2], c);
     }
+    __syncthreads();
+    if (threadIdx.x < NWD) {
+        const unsigned long long add = threadIdx.x == (int)(offsetof(SessErr, live_delta) / 8) ? s_live : 0ull;
+        if (add) atomicAdd((unsigned long long *)err + threadIdx.x, add);
+        rb_put(&rb[threadIdx.x], s_w[threadIdx.x] + add);
+    }
+    if (!none && threadIdx.x == NWD) rb_put(&rb[NWD + 1], seq);   // (every long slot's records applied)
     if (threadIdx.x == 0) {
         ls.ctl[1] = 0;
         ls.ctl[2] = 0;
@@ -733,7 +746,8 @@ __global__ __launch_bounds__(256) void sess_fire_kernel(TableDesc t, uint64_t ca
     __syncthreads();
     if (!s_last) return;
     constexpr int NW = (int)(sizeof(SessErr) / 8);
-    const unsigned long long em = sess_fold_shards(shards, 1), lv = sess_fold_shards(shards, 2);
+    unsigned long long em, lv;   // (one round of exchanges for both words: the sweep's last round trips)
+    sess_fold_shards2(shards, 1, 2, em, lv);
     if (threadIdx.x < NW) {
         const int w = threadIdx.x;
         const unsigned long long add = w == (int)(offsetof(SessErr, emitted) / 8)      ? em
