@@ -882,6 +882,8 @@ __global__ __launch_bounds__(CB_THREADS) void gather_kernel(GatherArgs A) {
     }
     // the readback block: BatchStats image, side-output count, occupancy of the hint tables, sequence word last
     __shared__ unsigned long long s_spec[4];   // listed records, side-output count, occupancy of the hint tables
+    __shared__ uint32_t s_goprev;   // the previous batch's verdict (pipelined chain), read in this same round
+    if (tid == CB_THREADS - 5) s_goprev = kt->a.chain ? *(volatile const uint32_t *)kt->a.go_prev : 1u;
     if (tid < CS_WORDS && (tid < CS_HIST ? tid <= CS_D1 : true)) {
 #define RBW(f) (int)(offsetof(BatchStats, f) / 8)
         // (static: a constant table in global memory; a local array indexed by tid was 20 B of scratch per lane,
@@ -916,7 +918,7 @@ __global__ __launch_bounds__(CB_THREADS) void gather_kernel(GatherArgs A) {
     __syncthreads();
     CB_STAMP(5);
     if (tid == 0) {   // the speculative merge's verdict
-        bool go = kt->a.go != nullptr && (!kt->a.chain || *(volatile const uint32_t *)kt->a.go_prev != 0u) && s_tot[CS_ACC] > 0 && s_tot[CS_BADTS] == 0 && s_tot[CS_BADRANGE] == 0 &&
+        bool go = kt->a.go != nullptr && s_goprev != 0u && s_tot[CS_ACC] > 0 && s_tot[CS_BADTS] == 0 && s_tot[CS_BADRANGE] == 0 &&
                   s_tot[CS_BADKG] == 0 && s_tot[CS_REFIRE] == 0 && s_tot[CS_HOUT] == 0 && s_spec[0] == 0 &&
                   (!kt->a.side_enabled || (long long)s_spec[1] <= kt->a.side_cap) &&
                   (long long)s_tot[CS_MIN] >= kt->a.hint && (long long)s_tot[CS_MAX] <= kt->a.hint + 1;
